@@ -1,0 +1,233 @@
+/*
+ * deftri.h — C-ABI of the MI355X-native deformable-triangulation LM solver.
+ *
+ * This is the drop-in boundary for the hot path of
+ * luicalrob/Triangulation-in-Deformable-Scenes: the g2o Levenberg–Marquardt
+ * solve inside `arapOptimization` (Modules/Optimization/g2oBundleAdjustment.cc:608-1008
+ * at the surveyed revision; the LM call is `optimizer.optimize(nOptIterations)`
+ * at g2oBundleAdjustment.cc:962).  The reference's C++ entry points
+ * (Modules/Optimization/g2oBundleAdjustment.h:36-75) are kept by the C++ adapter
+ * (csrc/adapter.cpp, deftri_adapter.h) and by the Python mirror (deftri/optimization.py);
+ * both sit on top of this plain C interface.
+ *
+ * Conventions
+ *  - every function returns int: 0 = OK, < 0 = error (see DEFTRI_E_*); the message
+ *    of the last error on a context is available from deftri_last_error().
+ *  - host arrays are owned by the caller and only read (or written, for outputs)
+ *    during the call; device buffers are owned by the context.
+ *  - one context per host thread; contexts are independent.
+ *  - no C++ exceptions cross this boundary.
+ *
+ * Problem layout ("graph descriptor"): the flattened g2o graph that
+ * arapOptimization builds (g2oBundleAdjustment.cc:640-953) — see DESIGN.md §2.
+ *   vertices : points (3 dof, VertexSBAPointXYZ, g2oTypes.h:39-56),
+ *              per KF-pair one SE3 T_g (g2o::VertexSE3Expmap, 6 dof, T <- exp(d)*T)
+ *              and per KF-pair two depth scales (VertexDepthScale, g2oTypes.h:78-94)
+ *   edges    : reprojection  EdgeSE3ProjectXYZPerKeyFrameOnlyPoints (g2oTypes.h:267-298),
+ *              depth         EdgeDepthCorrection (g2oTypes.h:390-421),
+ *              ARAP          EdgeARAP (g2oTypes.h:300-349).
+ */
+#ifndef DEFTRI_H
+#define DEFTRI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DEFTRI_ABI_VERSION 1
+
+/* error codes */
+#define DEFTRI_OK             0
+#define DEFTRI_E_ARG         -1   /* invalid argument / inconsistent descriptor */
+#define DEFTRI_E_HIP         -2   /* HIP runtime error (allocation, launch) */
+#define DEFTRI_E_NOPROBLEM   -3   /* solve/download before upload */
+#define DEFTRI_E_NUMERIC     -4   /* non-finite state */
+#define DEFTRI_E_NODEVICE    -5   /* no usable gfx950 device */
+#define DEFTRI_E_GRAPH       -6   /* graph construction failed (e.g. < 3 mesh points) */
+
+/* solver status written into deftri_report.status (g2o SparseOptimizer::optimize semantics) */
+#define DEFTRI_STATUS_OK         0  /* ran all requested iterations */
+#define DEFTRI_STATUS_TERMINATE  1  /* g2o "Terminate": 10 failed trials, rho == 0 or lambda not finite */
+
+typedef struct deftri_ctx deftri_ctx;
+
+/* Flattened non-rigid BA / ARAP problem (all indices are 0-based). */
+typedef struct deftri_problem_desc {
+    int32_t n_points;   /* P   point vertices, 3 dof each                                  */
+    int32_t n_pairs;    /* Q   KF pairs: one SE3 T_g vertex each                            */
+    int32_t n_scales;   /* S   depth-scale vertices (reference: 2 per pair)                 */
+    int32_t n_cams;     /* C   fixed camera poses / calibrations used by the edges          */
+    int32_t n_rep;      /* R   reprojection edges                                           */
+    int32_t n_depth;    /* D   depth edges                                                  */
+    int32_t n_arap;     /* E   ARAP edges (directed, as the reference inserts them)         */
+    int32_t n_rot;      /* rows of the per-mesh-vertex rotation table R_i                   */
+
+    /* initial state */
+    const double *points;     /* [P*3]  VertexSBAPointXYZ estimates                         */
+    const double *tg;         /* [Q*7]  SE3Quat per pair: qx qy qz qw tx ty tz              */
+    const double *scales;     /* [S]    VertexDepthScale estimates                           */
+
+    /* cameras (fixed): Kannala–Brandt8 params and pose T_cw (g2o::SE3Quat of the KF pose)   */
+    const float  *cam_kb8;    /* [C*8]  fx fy cx cy k0 k1 k2 k3 (KannalaBrandt8.cc:22-29)   */
+    const double *cam_pose;   /* [C*7]  qx qy qz qw tx ty tz                                */
+
+    /* reprojection edges: e = obs - KB8(T_cw * p), info = invSigma2(octave)*repW * I2,
+       Huber(delta) — g2oBundleAdjustment.cc:765-812                                          */
+    const int32_t *rep_point; /* [R] */
+    const int32_t *rep_cam;   /* [R] */
+    const double  *rep_obs;   /* [R*2] */
+    const double  *rep_info;  /* [R]  scalar multiple of I2 */
+    double huber_delta;       /* robust kernel delta (reference: (float)sqrt(100.991)); <= 0 disables */
+
+    /* depth edges: e = (d/s - (T_cw p)_z)^2 (x500 if s <= 0), info = 1/sigma^2
+       — g2oTypes.h:403-417, g2oBundleAdjustment.cc:816-856                                   */
+    const int32_t *dep_point; /* [D] */
+    const int32_t *dep_scale; /* [D] */
+    const int32_t *dep_cam;   /* [D] */
+    const double  *dep_meas;  /* [D] */
+    const double  *dep_info;  /* [D] */
+
+    /* ARAP edges (g2oTypes.h:311-342): vertices (p1_i, p2_i, p1_j, p2_j, T_g[pair]),
+       R_i = rot[arap_rot[2e]], R_j = rot[arap_rot[2e+1]], w_ij = arap_w[e],
+       area = pair_area[pair], info = pair_info[pair] (= arapW * T^2, :946)                 */
+    const int32_t *arap_pts;  /* [E*4] */
+    const int32_t *arap_pair; /* [E]   */
+    const int32_t *arap_rot;  /* [E*2] */
+    const double  *arap_w;    /* [E]   */
+    const double  *rot;       /* [n_rot*9] row-major 3x3 */
+    const double  *pair_area; /* [Q] */
+    const double  *pair_info; /* [Q] */
+
+    /* optional: 2-D ordering coordinates per point (the mesh plane).  NULL = use points x,y.
+       Only affects the fill-reducing ordering of the sparse LDL^T, never the result's meaning. */
+    const double *order_xy;   /* [P*2] or NULL */
+} deftri_problem_desc;
+
+typedef struct deftri_lm_params {
+    int32_t n_iterations;   /* g2o optimize(n) */
+    int32_t max_trials;     /* g2o _maxTrialsAfterFailure (default 10) */
+    double  tau;            /* lambda init = tau * max diag(H) (default 1e-5) */
+    double  user_lambda;    /* > 0: use as initial lambda (g2o _userLambdaInit) */
+    int32_t analytic_jacobians; /* 1 = analytic ARAP/depth Jacobians (GPU default); 0 = g2o numeric central differences (delta 1e-9) */
+    int32_t verbose;
+} deftri_lm_params;
+
+#define DEFTRI_MAX_REPORT_ITERS 1024
+
+typedef struct deftri_report {
+    int32_t status;                  /* DEFTRI_STATUS_* */
+    int32_t iterations;              /* completed optimize() iterations */
+    int32_t trials_total;            /* LM trials (accepted + rejected) */
+    int32_t trials_rejected;
+    double  chi2_initial;            /* activeRobustChi2 before the first iteration */
+    double  chi2_final;
+    double  lambda_final;
+    double  chi2_iter[DEFTRI_MAX_REPORT_ITERS];   /* accepted chi2 after each iteration */
+    int32_t trials_iter[DEFTRI_MAX_REPORT_ITERS]; /* trials used by each iteration */
+    /* timing (ms, device-timed with HIP events) */
+    double  ms_total;
+    double  ms_linearize;            /* residuals + Jacobians + H/b assembly */
+    double  ms_factor;               /* multifrontal LDL^T numeric factorization */
+    double  ms_solve;                /* forward/backward substitution */
+    double  ms_update;               /* oplus + chi2 re-evaluation */
+    /* sizes of the sparse factorization */
+    int64_t n_unknowns;
+    int64_t nnz_factor;              /* entries of L (incl. dense fronts' boundary rows) */
+    double  factor_flops;            /* per factorization */
+    int32_t n_fronts;
+    int32_t n_levels;
+} deftri_report;
+
+/* ---- context ---------------------------------------------------------------------- */
+/* device >= 0: HIP device ordinal.  device < 0: host-only context (graph construction and
+   symbolic analysis only; every device entry point then returns DEFTRI_E_NODEVICE). */
+int deftri_ctx_create(int32_t device, deftri_ctx **out);
+int deftri_ctx_destroy(deftri_ctx *ctx);
+const char *deftri_last_error(const deftri_ctx *ctx);
+int deftri_abi_version(void);
+
+/* ---- flat-graph API ---------------------------------------------------------------- */
+/* Validate, order (nested dissection), analyse (multifrontal symbolic) and copy to HBM. */
+int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc);
+/* Run g2o-semantics Levenberg–Marquardt on the device. */
+int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *params, deftri_report *report);
+/* Copy the current state back: points [P*3], scales [S], tg [Q*7] (any may be NULL). */
+int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg);
+/* Reset the device state to the uploaded initial values (no re-analysis). */
+int deftri_reset_state(deftri_ctx *ctx);
+
+/* ---- diagnostics (parity tests) ----------------------------------------------------- */
+/* activeRobustChi2 at the current device state. */
+int deftri_eval_chi2(deftri_ctx *ctx, double *chi2);
+/* Linearize at the current state and return b (gradient side, g2o sign: b = -J^T W e)
+   in the vertex order [T_g(6) per pair][scales][points(3)], and the diagonal of H. */
+int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n);
+/* y = H x for the current linearization (same vertex order). */
+int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n);
+/* Solve (H + lambda I) x = rhs with the device LDL^T. */
+int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n);
+/* Number of unknowns of the uploaded problem. */
+int64_t deftri_num_unknowns(const deftri_ctx *ctx);
+
+/* Validate + analyse (ordering, multifrontal plan) without touching a device. */
+int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc);
+/* Plan statistics of the analysed problem: n_unknowns, nnz_factor, factor_flops, n_fronts,
+   n_levels (other report fields zero). */
+int deftri_plan_stats(const deftri_ctx *ctx, deftri_report *report);
+/* TEST ONLY: execute the analysed multifrontal plan with host loops on a dense, row-major
+   n x n H (vertex order as above) to check the symbolic analysis without a GPU.  Not used by
+   any solve path. */
+int deftri_debug_plan_solve(deftri_ctx *ctx, const double *H, double lambda, const double *rhs,
+                            double *x, int64_t n);
+/* sizeof() of the ABI structs (deftri_problem_desc, deftri_lm_params, deftri_report,
+   deftri_keyframe, deftri_map) for binding checks. */
+int64_t deftri_sizeof(int32_t which);
+
+/* ---- map-level API (Modules/Optimization/g2oBundleAdjustment.h:56-60) ---------------- */
+/* A keyframe as the solver reads/writes it (Modules/Map/KeyFrame.h): slots i = 0..n_slots-1
+   hold an optional MapPoint (point_id < 0 = null), its keypoint, octave and simulated depth. */
+typedef struct deftri_keyframe {
+    int64_t id;                 /* KeyFrame id */
+    double  pose[7];            /* T_cw as qx qy qz qw tx ty tz (from Sophus::SE3f) */
+    float   kb8[8];             /* calibration */
+    int32_t n_scales;           /* octave table size */
+    const float *inv_sigma2;    /* [n_scales] Frame::vInvSigma2_ (Frame.cc:61-75) */
+    double  depth_scale;        /* estimatedDepthScale_ (in/out) */
+    int32_t n_slots;
+    int64_t *point_id;          /* [n_slots] MapPoint id, < 0 = null slot                  */
+    float   *point_pos;         /* [n_slots*3] MapPoint world position (in/out, fp32 as the reference) */
+    const int32_t *obs_index;   /* [n_slots] Map::isMapPointInKeyFrame(point, kf) (< 0 = none) */
+    const float *kp_uv;         /* [n_obs*2] keypoints by observation index */
+    const int32_t *kp_octave;   /* [n_obs] */
+    const float *depth;         /* [n_obs] simulated depth per observation index (KeyFrame.cc:123-125) */
+    int32_t n_obs;
+} deftri_keyframe;
+
+typedef struct deftri_map {
+    int32_t n_keyframes;
+    deftri_keyframe *keyframes;   /* in the reference's unordered_map iteration order */
+    double global_t[7];           /* Map::getGlobalKeyFramesTransformation(kf1,kf2) in; written back (out) */
+} deftri_map;
+
+/* arapOptimization(Map*, rep, global, arap, alpha, beta, depthError, nIt, optimizationUpdate)
+   (g2oBundleAdjustment.cc:608).  Builds the graph on the host (Delaunay mesh, cotangent
+   weights, per-vertex R_i, reference indexing), solves on the device, writes back
+   positions (fp32), depth scales and the global transformation.  optimization_update may be
+   NULL; when given it receives sum ||p_old - p_new|| (:974-990). */
+int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight,
+                             double global_weight, double arap_weight, double alpha,
+                             double beta, float depth_error, int32_t n_iterations,
+                             double *optimization_update, deftri_report *report);
+
+/* Build the flattened graph only (no solve): the arrays are owned by the context and stay
+   valid until the next call on it.  Used by the parity tests to compare indexing. */
+int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,
+                            double arap_weight, float depth_error,
+                            const deftri_problem_desc **desc_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEFTRI_H */

@@ -1,0 +1,93 @@
+"""oracle.py — TEST INFRASTRUCTURE ONLY: ctypes binding of oracle/liboracle.so (the CPU
+restatement of the reference LM path, deftri_oracle.c).  Imported only by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg."""
+import ctypes as C
+import os
+import pathlib
+import subprocess
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        so = HERE / "liboracle.so"
+        if not so.exists():
+            build()
+        _lib = C.CDLL(str(so))
+    return _lib
+
+
+def _abi():
+    from deftri import _abi as A
+    return A
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(C.POINTER(t))
+
+
+def chi2(prob, points=None, scales=None, tg=None):
+    d = prob.to_desc()
+    out = C.c_double()
+    lib().oracle_chi2(C.byref(d), _p(points, C.c_double), _p(scales, C.c_double), _p(tg, C.c_double),
+                      C.byref(out))
+    return out.value
+
+
+def edge_errors(prob):
+    d = prob.to_desc()
+    rep = np.zeros((len(prob.rep_point), 2)); dep = np.zeros(len(prob.dep_point))
+    arap = np.zeros(len(prob.arap_pair))
+    lib().oracle_edge_errors(C.byref(d), _p(rep, C.c_double), _p(dep, C.c_double), _p(arap, C.c_double))
+    return rep, dep, arap
+
+
+def arap_jacobians(prob, analytic=True):
+    d = prob.to_desc()
+    J = np.zeros((len(prob.arap_pair), 18))
+    lib().oracle_arap_jacobians(C.byref(d), C.c_int(1 if analytic else 0), _p(J, C.c_double))
+    return J
+
+
+def linearize(prob, analytic=True, dense=False, x=None):
+    d = prob.to_desc()
+    n = prob.n_unknowns
+    b = np.zeros(n)
+    H = np.zeros((n, n)) if dense else None
+    y = np.zeros(n) if x is not None else None
+    xx = None if x is None else np.ascontiguousarray(x, dtype=np.float64)
+    lib().oracle_linearize(C.byref(d), C.c_int(1 if analytic else 0), _p(b, C.c_double),
+                           _p(H, C.c_double), _p(xx, C.c_double), _p(y, C.c_double))
+    return b, H, y
+
+
+def damped_solve(prob, lam, rhs, analytic=True):
+    d = prob.to_desc()
+    x = np.zeros(prob.n_unknowns)
+    r = np.ascontiguousarray(rhs, dtype=np.float64)
+    rc = lib().oracle_damped_solve(C.byref(d), C.c_int(1 if analytic else 0), C.c_double(lam),
+                                   _p(r, C.c_double), _p(x, C.c_double))
+    if rc != 0:
+        raise ArithmeticError("oracle LDL^T: zero pivot")
+    return x
+
+
+def solve_lm(prob, n_iterations=10, analytic=False, tau=1e-5, max_trials=10, verbose=False):
+    A = _abi()
+    d = prob.to_desc()
+    prm = A.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=0.0,
+                     analytic_jacobians=1 if analytic else 0, verbose=1 if verbose else 0)
+    rep = A.Report()
+    pts = np.zeros((prob.n_points, 3)); sc = np.zeros(prob.n_scales); tg = np.zeros((prob.n_pairs, 7))
+    lib().oracle_solve_lm(C.byref(d), C.byref(prm), _p(pts, C.c_double), _p(sc, C.c_double),
+                          _p(tg, C.c_double), C.byref(rep))
+    return {"points": pts, "scales": sc, "tg": tg, "report": rep.as_dict()}

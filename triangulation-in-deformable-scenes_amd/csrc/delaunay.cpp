@@ -1,0 +1,323 @@
+// delaunay.cpp — 2-D Delaunay triangulation (replaces the reference's qhull "d Qbb Qt" call in
+// ComputeDelaunayTriangulation3D, Modules/Utils/Geometry.cc:317-368).
+//
+// Algorithm: radial sweep-hull with incremental Lawson legalization (points sorted by distance
+// from the seed triangle's circumcentre; each new point lies outside the current hull, is joined to
+// every visible hull edge, and the new edges are flipped until locally Delaunay).  Predicates
+// orient2d / incircle use a floating-point filter and fall back to exact expansion arithmetic
+// (two-sum / FMA two-product), so the output is THE Delaunay triangulation for points in general
+// position — which is what qhull's lower hull of the lifted points is.  O(n log n).
+#include "delaunay.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+namespace deftri {
+
+namespace {
+
+// ---------------- exact arithmetic (expansions, increasing magnitude, non-overlapping) -------
+inline void two_sum(double a, double b, double &s, double &e) {
+    s = a + b;
+    double bv = s - a, av = s - bv;
+    e = (a - av) + (b - bv);
+}
+inline void two_prod(double a, double b, double &p, double &e) {
+    p = a * b;
+    e = std::fma(a, b, -p);
+}
+using Exp = std::vector<double>;
+void grow(Exp &e, double b) {
+    Exp out;
+    out.reserve(e.size() + 1);
+    double q = b;
+    for (double x : e) {
+        double s, h;
+        two_sum(q, x, s, h);
+        if (h != 0.0) out.push_back(h);
+        q = s;
+    }
+    if (q != 0.0 || out.empty()) out.push_back(q);
+    e.swap(out);
+}
+Exp add(const Exp &a, const Exp &b) {
+    Exp r = a;
+    for (double x : b) grow(r, x);
+    return r;
+}
+Exp neg(Exp a) { for (double &x : a) x = -x; return a; }
+Exp scale(const Exp &e, double b) {
+    Exp r;
+    for (double x : e) {
+        double p, q;
+        two_prod(x, b, p, q);
+        grow(r, q);
+        grow(r, p);
+    }
+    return r;
+}
+Exp mul(const Exp &a, const Exp &b) {
+    Exp r;
+    for (double x : b) r = add(r, scale(a, x));
+    return r;
+}
+Exp diff(double a, double b) {
+    double s, e;
+    two_sum(a, -b, s, e);
+    Exp r;
+    if (e != 0.0) r.push_back(e);
+    r.push_back(s);
+    return r;
+}
+int sign(const Exp &e) {
+    for (size_t i = e.size(); i-- > 0;)
+        if (e[i] != 0.0) return e[i] > 0 ? 1 : -1;
+    return 0;
+}
+
+int orient_exact(const double *a, const double *b, const double *c) {
+    Exp acx = diff(a[0], c[0]), bcx = diff(b[0], c[0]), acy = diff(a[1], c[1]), bcy = diff(b[1], c[1]);
+    return sign(add(mul(acx, bcy), neg(mul(acy, bcx))));
+}
+
+int incircle_exact(const double *a, const double *b, const double *c, const double *d) {
+    Exp adx = diff(a[0], d[0]), ady = diff(a[1], d[1]);
+    Exp bdx = diff(b[0], d[0]), bdy = diff(b[1], d[1]);
+    Exp cdx = diff(c[0], d[0]), cdy = diff(c[1], d[1]);
+    Exp alift = add(mul(adx, adx), mul(ady, ady));
+    Exp blift = add(mul(bdx, bdx), mul(bdy, bdy));
+    Exp clift = add(mul(cdx, cdx), mul(cdy, cdy));
+    Exp bc = add(mul(bdx, cdy), neg(mul(bdy, cdx)));
+    Exp ca = add(mul(cdx, ady), neg(mul(cdy, adx)));
+    Exp ab = add(mul(adx, bdy), neg(mul(ady, bdx)));
+    return sign(add(add(mul(alift, bc), mul(blift, ca)), mul(clift, ab)));
+}
+
+// > 0 : a, b, c counter-clockwise
+int orient2d(const double *a, const double *b, const double *c) {
+    double detl = (a[0] - c[0]) * (b[1] - c[1]);
+    double detr = (a[1] - c[1]) * (b[0] - c[0]);
+    double det = detl - detr;
+    double bound = 3.3306690738754716e-16 * (std::fabs(detl) + std::fabs(detr));
+    if (det > bound) return 1;
+    if (-det > bound) return -1;
+    return orient_exact(a, b, c);
+}
+
+// > 0 : d inside the circumcircle of counter-clockwise (a, b, c)
+int incircle(const double *a, const double *b, const double *c, const double *d) {
+    double adx = a[0] - d[0], ady = a[1] - d[1], bdx = b[0] - d[0], bdy = b[1] - d[1];
+    double cdx = c[0] - d[0], cdy = c[1] - d[1];
+    double bdxcdy = bdx * cdy, cdxbdy = cdx * bdy, cdxady = cdx * ady, adxcdy = adx * cdy;
+    double adxbdy = adx * bdy, bdxady = bdx * ady;
+    double alift = adx * adx + ady * ady, blift = bdx * bdx + bdy * bdy, clift = cdx * cdx + cdy * cdy;
+    double det = alift * (bdxcdy - cdxbdy) + blift * (cdxady - adxcdy) + clift * (adxbdy - bdxady);
+    double perm = (std::fabs(bdxcdy) + std::fabs(cdxbdy)) * alift + (std::fabs(cdxady) + std::fabs(adxcdy)) * blift +
+                  (std::fabs(adxbdy) + std::fabs(bdxady)) * clift;
+    double bound = 1.2e-15 * perm;
+    if (det > bound) return 1;
+    if (-det > bound) return -1;
+    return incircle_exact(a, b, c, d);
+}
+
+struct Sweep {
+    const double *xy;
+    int n;
+    std::vector<int> tri, half;
+    std::vector<int> hprev, hnext, htri, hhash;
+    int hsize = 0, hstart = 0;
+    double cx = 0, cy = 0;
+    std::vector<int> stack;
+
+    const double *P(int i) const { return xy + 2 * (size_t)i; }
+
+    int key(double x, double y) const {
+        double dx = x - cx, dy = y - cy;
+        double p = dx / (std::fabs(dx) + std::fabs(dy));
+        double a = (dy > 0 ? 3 - p : 1 + p) / 4;        // pseudo-angle in [0, 1]
+        int k = (int)std::floor(a * hsize);
+        return ((k % hsize) + hsize) % hsize;
+    }
+    void link(int a, int b) {
+        half[a] = b;
+        if (b != -1) half[b] = a;
+    }
+    int add_tri(int i0, int i1, int i2, int a, int b, int c) {
+        int t = (int)tri.size();
+        tri.push_back(i0); tri.push_back(i1); tri.push_back(i2);
+        half.push_back(-1); half.push_back(-1); half.push_back(-1);
+        link(t, a); link(t + 1, b); link(t + 2, c);
+        return t;
+    }
+    int legalize(int a) {
+        size_t i = 0;
+        int ar = 0;
+        stack.clear();
+        while (true) {
+            int b = half[a];
+            int a0 = a - a % 3;
+            ar = a0 + (a + 2) % 3;
+            if (b == -1) {
+                if (stack.empty()) break;
+                a = stack.back(); stack.pop_back();
+                continue;
+            }
+            int b0 = b - b % 3;
+            int al = a0 + (a + 1) % 3;
+            int bl = b0 + (b + 2) % 3;
+            int p0 = tri[ar], pr = tri[a], pl = tri[al], p1 = tri[bl];
+            bool illegal = incircle(P(pr), P(pl), P(p0), P(p1)) > 0;
+            if (illegal) {
+                tri[a] = p1;
+                tri[b] = p0;
+                int hbl = half[bl];
+                if (hbl == -1) {
+                    int e = hstart;
+                    do {
+                        if (htri[e] == bl) { htri[e] = a; break; }
+                        e = hprev[e];
+                    } while (e != hstart);
+                }
+                link(a, hbl);
+                link(b, half[ar]);
+                link(ar, bl);
+                int br = b0 + (b + 1) % 3;
+                stack.push_back(br);
+            } else {
+                if (stack.empty()) break;
+                a = stack.back(); stack.pop_back();
+            }
+            (void)i;
+        }
+        return ar;
+    }
+
+    bool run(int &skipped) {
+        skipped = 0;
+        double minx = 1e300, miny = 1e300, maxx = -1e300, maxy = -1e300;
+        for (int i = 0; i < n; i++) {
+            minx = std::min(minx, P(i)[0]); maxx = std::max(maxx, P(i)[0]);
+            miny = std::min(miny, P(i)[1]); maxy = std::max(maxy, P(i)[1]);
+        }
+        double mx = (minx + maxx) / 2, my = (miny + maxy) / 2;
+        auto d2 = [&](int i, double x, double y) { double dx = P(i)[0] - x, dy = P(i)[1] - y; return dx * dx + dy * dy; };
+        int i0 = 0;
+        double best = 1e300;
+        for (int i = 0; i < n; i++) { double v = d2(i, mx, my); if (v < best) { best = v; i0 = i; } }
+        int i1 = -1;
+        best = 1e300;
+        for (int i = 0; i < n; i++) {
+            if (i == i0) continue;
+            double v = d2(i, P(i0)[0], P(i0)[1]);
+            if (v < best && v > 0) { best = v; i1 = i; }
+        }
+        if (i1 < 0) return false;
+        auto circumr2 = [&](int a, int b, int c, double &ox, double &oy) {
+            double dx = P(b)[0] - P(a)[0], dy = P(b)[1] - P(a)[1];
+            double ex = P(c)[0] - P(a)[0], ey = P(c)[1] - P(a)[1];
+            double bl = dx * dx + dy * dy, cl = ex * ex + ey * ey;
+            double dd = 0.5 / (dx * ey - dy * ex);
+            double x = (ey * bl - dy * cl) * dd, y = (dx * cl - ex * bl) * dd;
+            ox = P(a)[0] + x; oy = P(a)[1] + y;
+            return x * x + y * y;
+        };
+        int i2 = -1;
+        double minr = 1e300, ox, oy;
+        for (int i = 0; i < n; i++) {
+            if (i == i0 || i == i1) continue;
+            if (orient2d(P(i0), P(i1), P(i)) == 0) continue;
+            double r = circumr2(i0, i1, i, ox, oy);
+            if (std::isfinite(r) && r < minr) { minr = r; i2 = i; }
+        }
+        if (i2 < 0) return false;                        // all collinear
+        if (orient2d(P(i0), P(i1), P(i2)) < 0) std::swap(i1, i2);
+        circumr2(i0, i1, i2, cx, cy);
+        std::vector<double> dist(n);
+        for (int i = 0; i < n; i++) dist[i] = d2(i, cx, cy);
+        std::vector<int> ids(n);
+        std::iota(ids.begin(), ids.end(), 0);
+        std::sort(ids.begin(), ids.end(), [&](int a, int b) { return dist[a] < dist[b] || (dist[a] == dist[b] && a < b); });
+        hsize = std::max(1, (int)std::ceil(std::sqrt((double)n)));
+        hprev.assign(n, -1); hnext.assign(n, -1); htri.assign(n, -1); hhash.assign(hsize, -1);
+        hstart = i0;
+        hnext[i0] = i1; hprev[i2] = i1;
+        hnext[i1] = i2; hprev[i0] = i2;
+        hnext[i2] = i0; hprev[i1] = i0;
+        htri[i0] = 0; htri[i1] = 1; htri[i2] = 2;
+        hhash[key(P(i0)[0], P(i0)[1])] = i0;
+        hhash[key(P(i1)[0], P(i1)[1])] = i1;
+        hhash[key(P(i2)[0], P(i2)[1])] = i2;
+        tri.reserve(6 * (size_t)n); half.reserve(6 * (size_t)n);
+        add_tri(i0, i1, i2, -1, -1, -1);
+        double px = 0, py = 0;
+        for (int k = 0; k < n; k++) {
+            int i = ids[k];
+            double x = P(i)[0], y = P(i)[1];
+            if (k > 0 && x == px && y == py) { skipped++; continue; }      // exact duplicate
+            px = x; py = y;
+            if (i == i0 || i == i1 || i == i2) continue;
+            int start = 0, kk = key(x, y);
+            for (int j = 0; j < hsize; j++) {
+                start = hhash[(kk + j) % hsize];
+                if (start != -1 && start != hnext[start]) break;
+            }
+            start = hprev[start];
+            int e = start, q;
+            while (q = hnext[e], orient2d(P(e), P(q), P(i)) >= 0) {
+                e = q;
+                if (e == start) { e = -1; break; }
+            }
+            if (e == -1) { skipped++; continue; }
+            int t = add_tri(e, i, hnext[e], -1, -1, htri[e]);
+            htri[i] = legalize(t + 2);
+            htri[e] = t;
+            int nn = hnext[e];
+            while (q = hnext[nn], orient2d(P(nn), P(q), P(i)) < 0) {
+                t = add_tri(nn, i, q, htri[i], -1, htri[nn]);
+                htri[i] = legalize(t + 2);
+                hnext[nn] = nn;
+                nn = q;
+            }
+            if (e == start) {
+                while (q = hprev[e], orient2d(P(q), P(e), P(i)) < 0) {
+                    t = add_tri(q, i, e, -1, htri[e], htri[q]);
+                    legalize(t + 2);
+                    htri[q] = t;
+                    hnext[e] = e;
+                    e = q;
+                }
+            }
+            hstart = hprev[i] = e;
+            hnext[e] = hprev[nn] = i;
+            hnext[i] = nn;
+            hhash[key(x, y)] = i;
+            hhash[key(P(e)[0], P(e)[1])] = e;
+        }
+        // hull size
+        return true;
+    }
+};
+
+}  // namespace
+
+bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_size, int &skipped) {
+    tris.clear();
+    hull_size = 0;
+    skipped = 0;
+    if (n < 3) return false;
+    Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}};
+    if (!s.run(skipped)) return false;
+    tris.assign(s.tri.begin(), s.tri.end());
+    int h = 0, e = s.hstart;
+    do { h++; e = s.hnext[e]; } while (e != s.hstart && h <= n);
+    hull_size = h;
+    return true;
+}
+
+int orient2d_sign(const double *a, const double *b, const double *c) { return orient2d(a, b, c); }
+int incircle_sign(const double *a, const double *b, const double *c, const double *d) { return incircle(a, b, c, d); }
+
+}  // namespace deftri

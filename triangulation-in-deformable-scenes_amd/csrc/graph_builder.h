@@ -1,0 +1,37 @@
+// graph_builder.h — the graph construction of the reference's arapOptimization
+// (Modules/Optimization/g2oBundleAdjustment.cc:640-953) over the deftri_map view.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/deftri.h"
+
+namespace deftri {
+
+struct GraphResult {
+    deftri_problem_desc desc{};
+    // owned arrays behind desc
+    std::vector<double> points, tg, scales, cam_pose, rep_obs, rep_info, dep_meas, dep_info, arap_w, rot, pair_area,
+        pair_info, order_xy;
+    std::vector<float> cam_kb8;
+    std::vector<int32_t> rep_point, rep_cam, dep_point, dep_scale, dep_cam, arap_pts, arap_pair, arap_rot;
+    // writeback metadata
+    std::vector<int64_t> point_mpid;          // point index -> MapPoint id
+    std::vector<float> point_orig;            // fp32 original positions
+    std::vector<int32_t> kf_scale;            // keyframe (map order) -> last scale vertex (-1: none)
+    std::vector<int32_t> pair_kf1, pair_kf2;  // per pair: keyframe indices (map order)
+    std::vector<int32_t> pair_T;              // facets.count() per pair
+    std::vector<int32_t> pair_hull;           // convex hull size per pair
+};
+
+bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
+                      GraphResult &g, std::string &err);
+
+void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<double> &points,
+                    const std::vector<double> &scales, const std::vector<double> &tg, double *optimization_update);
+
+// 3x3 helpers exported for tests
+void procrustes_rotation(const double S[9], double R[9]);
+
+}  // namespace deftri

@@ -1,0 +1,90 @@
+// kernels.h — device-side problem / plan views and kernel launchers (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace deftri {
+
+// problem arrays resident in HBM (layout = deftri_problem_desc, SoA)
+struct DevProblem {
+    int32_t P = 0, Q = 0, S = 0, C = 0, R = 0, D = 0, E = 0, NR = 0;
+    // state
+    double *points = nullptr, *scales = nullptr, *tg = nullptr;
+    double *points_bak = nullptr, *scales_bak = nullptr, *tg_bak = nullptr;
+    // cameras
+    float *cam_kb8 = nullptr;
+    double *cam_pose = nullptr, *cam_R = nullptr;
+    // edges
+    int32_t *rep_point = nullptr, *rep_cam = nullptr;
+    double *rep_obs = nullptr, *rep_info = nullptr;
+    double huber_delta = 0;
+    int32_t *dep_point = nullptr, *dep_scale = nullptr, *dep_cam = nullptr;
+    double *dep_meas = nullptr, *dep_info = nullptr;
+    int32_t *arap_pts = nullptr, *arap_pair = nullptr, *arap_rot = nullptr;
+    double *arap_w = nullptr, *rot = nullptr, *pair_area = nullptr, *pair_info = nullptr;
+    // linearization
+    double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr, *chi_rep = nullptr;
+    double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr, *chi_dep = nullptr;
+    double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr, *chi_arap = nullptr;
+};
+
+struct FrontDev {
+    const int32_t *m, *s, *parent, *nchild, *child0, *child1;
+    const int64_t *arena_off, *vec_off, *rows_off, *bmap_off;
+    const int32_t *rows, *bmap;
+};
+
+struct LevelDev {
+    int64_t ea_off[2]; int32_t nea[2];
+    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0; };
+    std::vector<Step> steps;
+    int64_t fwd_off; int32_t nfwd;
+    int64_t gemv_off; int32_t ngemv;
+    int64_t bgemv_off; int32_t nbgemv;
+};
+
+struct DevPlan {
+    int64_t nv = 0, ndof = 0;
+    int64_t *voff = nullptr;
+    int32_t *vdim = nullptr;
+    // H blocks
+    int64_t nblocks = 0, hval_size = 0;
+    double *hval = nullptr;
+    int64_t *blk_val_off = nullptr, *blk_arena = nullptr;
+    int32_t *blk_rows = nullptr, *blk_cols = nullptr, *blk_ld = nullptr, *blk_diag = nullptr;
+    int64_t *blk_row_dof = nullptr, *blk_col_dof = nullptr;     // diagnostics (H x)
+    int64_t nhchunks = 0;
+    uint64_t *hcontrib = nullptr;
+    int64_t *hchunk_begin = nullptr, *hblk_chunk_begin = nullptr;
+    int32_t *hchunk_len = nullptr;
+    double *hpart = nullptr;
+    int64_t nbchunks = 0;
+    uint64_t *bcontrib = nullptr;
+    int64_t *bchunk_begin = nullptr, *bv_chunk_begin = nullptr;
+    int32_t *bchunk_len = nullptr;
+    double *bpart = nullptr;
+    double *b = nullptr;
+    // factor
+    int64_t arena_size = 0, vec_size = 0;
+    double *arena = nullptr, *vec = nullptr;
+    FrontDev fd{};
+    int32_t *tasks = nullptr;
+    std::vector<LevelDev> levels;
+    int *flag = nullptr;
+};
+
+void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
+void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);
+void launch_factor(const DevPlan &L, hipStream_t st);
+void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st);
+void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st);
+void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
+                double *out, hipStream_t st);
+void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st);
+void launch_hmul(const DevPlan &L, const int64_t *brow_dof, const int64_t *bcol_dof, const double *x, double *y,
+                 int64_t n, hipStream_t st);
+
+}  // namespace deftri

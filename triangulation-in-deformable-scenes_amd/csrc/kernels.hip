@@ -1,0 +1,853 @@
+// kernels.hip — gfx950 kernels of the deformable-triangulation LM hot path.
+//
+// Stage                    replaces (reference / g2o)                                   kernel(s)
+// ----------------------   -----------------------------------------------------------  -------------------------
+// residuals + Jacobians    computeActiveErrors + linearizeOplus of the three edge types  k_lin_rep/k_lin_dep/k_lin_arap
+//                          (g2oTypes.h:267-298, 300-349, 390-421; g2oTypes.cc:270-283)
+// H, b assembly            BlockSolver::buildSystem / constructQuadraticForm             k_hchunk/k_hfinal, k_bchunk/k_bfinal
+// H + lambda I             BlockSolver::setLambda                                        k_scatter
+// LDL^T                    LinearSolverEigen (SimplicialLDLT) factorization              k_ea, k_diag, k_trsm, k_update
+// solve                    SimplicialLDLT::solve                                         k_fwd, k_fwd_gemv, k_bwd_gemv, k_bwd
+// x <- x (+) dx            OptimizableGraph::update (vertex oplusImpl)                   k_update_state
+// chi2 / scale reductions  activeRobustChi2, OptimizationAlgorithmLevenberg::computeScale k_sum_partial/k_sum_final, ...
+//
+// All reductions are deterministic (fixed-order per-chunk partials, then an ordered final pass):
+// no floating-point atomics anywhere on the path.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_math.h"
+#include "kernels.h"
+
+namespace deftri {
+namespace dev {
+
+#define TID (blockIdx.x * blockDim.x + threadIdx.x)
+
+// ------------------------------------------------------------------------------------------
+// edge errors / Jacobians
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void huber_rho(double delta, double e2, double &rho0, double &rho1) {
+    if (delta <= 0) { rho0 = e2; rho1 = 1.0; return; }
+    double dsqr = delta * delta;
+    if (e2 <= dsqr) { rho0 = e2; rho1 = 1.0; }
+    else { double se = sqrt(e2); rho0 = 2 * se * delta - dsqr; rho1 = delta / se; }
+}
+
+__global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
+                          const double *__restrict__ obs, const double *__restrict__ info, double hdelta,
+                          const double *__restrict__ points, const double *__restrict__ cam_pose,
+                          const double *__restrict__ cam_R, const float *__restrict__ kb8,
+                          double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
+                          double *__restrict__ chi, int want_jac) {
+    int e = TID;
+    if (e >= R) return;
+    int c = rc[e];
+    const double *pp = points + 3 * (int64_t)rp[e];
+    double p[3] = {pp[0], pp[1], pp[2]}, pc[3];
+    SE3 T = se3_load(cam_pose + 7 * c);
+    se3_map(T, p, pc);
+    float pf[3] = {(float)pc[0], (float)pc[1], (float)pc[2]}, uv[2];
+    kb8_project(kb8 + 8 * c, pf, uv);
+    double e0 = obs[2 * e] - (double)uv[0], e1 = obs[2 * e + 1] - (double)uv[1];
+    double om = info[e];
+    double c2 = e0 * (om * e0) + e1 * (om * e1);
+    double rho0, rho1;
+    huber_rho(hdelta, c2, rho0, rho1);
+    chi[e] = rho0;
+    if (!want_jac) return;
+    float jf[6];
+    kb8_project_jac(kb8 + 8 * c, pf, jf);
+    const double *Rm = cam_R + 9 * c;
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            J[6 * (int64_t)e + 3 * r + k] = -(double)jf[3 * r] * Rm[k] - (double)jf[3 * r + 1] * Rm[3 + k] -
+                                           (double)jf[3 * r + 2] * Rm[6 + k];
+    W[e] = rho1 * om;
+    E[2 * (int64_t)e] = e0;
+    E[2 * (int64_t)e + 1] = e1;
+}
+
+__device__ __forceinline__ double depth_err(const SE3 &T, const double p[3], double meas, double s) {
+    double pc[3];
+    se3_map(T, p, pc);
+    double x = meas / s - pc[2];
+    double error = x * x;                         // pow(x, 2)
+    if (s <= 0.0) error = error * 500;
+    return error;
+}
+
+__global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
+                          const int32_t *__restrict__ dcam, const double *__restrict__ meas,
+                          const double *__restrict__ info, const double *__restrict__ points,
+                          const double *__restrict__ scales, const double *__restrict__ cam_pose,
+                          const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
+                          double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+    int e = TID;
+    if (e >= D) return;
+    int c = dcam[e];
+    const double *pp = points + 3 * (int64_t)dpt[e];
+    double p[3] = {pp[0], pp[1], pp[2]};
+    double s = scales[dsc[e]], mv = meas[e];
+    SE3 T = se3_load(cam_pose + 7 * c);
+    double err = depth_err(T, p, mv, s);
+    double om = info[e];
+    chi[e] = err * (om * err);
+    if (!want_jac) return;
+    double Jv[4];
+    if (analytic) {
+        double pc[3];
+        se3_map(T, p, pc);
+        double r = mv / s - pc[2];
+        double f = (s <= 0.0) ? 500.0 : 1.0;
+        const double *Rm = cam_R + 9 * c;
+        for (int k = 0; k < 3; k++) Jv[k] = f * 2.0 * r * (-Rm[6 + k]);
+        Jv[3] = f * 2.0 * r * (-mv / (s * s));
+    } else {                                       // g2o BaseBinaryEdge numeric, delta 1e-9
+        const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+        for (int k = 0; k < 3; k++) {
+            double bak = p[k];
+            p[k] = bak + delta; double ep = depth_err(T, p, mv, s);
+            p[k] = bak - delta; double em = depth_err(T, p, mv, s);
+            p[k] = bak;
+            Jv[k] = scalar * (ep - em);
+        }
+        Jv[3] = scalar * (depth_err(T, p, mv, s + delta) - depth_err(T, p, mv, s - delta));
+    }
+    for (int k = 0; k < 4; k++) J[4 * (int64_t)e + k] = Jv[k];
+    W[e] = om;
+    E[e] = err;
+}
+
+__device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
+                                           const double *v2j, const SE3 &T, const double *Ri,
+                                           const double *Rj, double w, double area) {
+    double Rg[9];
+    quat_to_mat(T.r, Rg);
+    double dg[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
+        double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
+        dg[k] = ((a - T.t[k]) - v1i[k]) + ((b - T.t[k]) - v1j[k]);
+    }
+    double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
+    double d1i[3], d2i[3], d1j[3], d2j[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        d1i[k] = v1i[k] - v1j[k]; d2i[k] = v2i[k] - v2j[k];
+        d1j[k] = v1j[k] - v1i[k]; d2j[k] = v2j[k] - v2i[k];
+    }
+    double fn = 0, gn = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        double f = (d2i[k] - (Ri[3 * k] * d1i[0] + Ri[3 * k + 1] * d1i[1] + Ri[3 * k + 2] * d1i[2])) / area;
+        double g = (d2j[k] - (Rj[3 * k] * d1j[0] + Rj[3 * k + 1] * d1j[1] + Rj[3 * k + 2] * d1j[2])) / area;
+        fn += f * f; gn += g * g;
+    }
+    return (w * (fn + gn) + eg) - 0.0;
+}
+
+__global__ void k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+                           const int32_t *__restrict__ arot, const double *__restrict__ aw,
+                           const double *__restrict__ rot, const double *__restrict__ parea,
+                           const double *__restrict__ pinfo, const double *__restrict__ points,
+                           const double *__restrict__ tg, double *__restrict__ J, double *__restrict__ W,
+                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+    int e = TID;
+    if (e >= E_) return;
+    const int32_t *v = apts + 4 * (int64_t)e;
+    double P[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const double *pp = points + 3 * (int64_t)v[k];
+        P[k][0] = pp[0]; P[k][1] = pp[1]; P[k][2] = pp[2];
+    }
+    int q = apair[e];
+    SE3 T = se3_load(tg + 7 * q);
+    const double *Ri = rot + 9 * (int64_t)arot[2 * (int64_t)e];
+    const double *Rj = rot + 9 * (int64_t)arot[2 * (int64_t)e + 1];
+    double w = aw[e], area = parea[q], om = pinfo[q];
+    double err = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
+    chi[e] = err * (om * err);
+    if (!want_jac) return;
+    double Jv[18];
+    if (analytic) {
+        double Rg[9];
+        quat_to_mat(T.r, Rg);
+        double d1[3], d2[3], a[3], c[3], g[3], u[3], s2[3];
+        for (int k = 0; k < 3; k++) { d1[k] = P[0][k] - P[2][k]; d2[k] = P[1][k] - P[3][k]; s2[k] = P[1][k] + P[3][k]; }
+        for (int k = 0; k < 3; k++) {
+            a[k] = d2[k] - (Ri[3 * k] * d1[0] + Ri[3 * k + 1] * d1[1] + Ri[3 * k + 2] * d1[2]);
+            c[k] = d2[k] - (Rj[3 * k] * d1[0] + Rj[3 * k + 1] * d1[1] + Rj[3 * k + 2] * d1[2]);
+            double rs = Rg[3 * k] * s2[0] + Rg[3 * k + 1] * s2[1] + Rg[3 * k + 2] * s2[2];
+            u[k] = rs - 2 * T.t[k];
+            g[k] = u[k] - (P[0][k] + P[2][k]);
+        }
+        double co = 2.0 * w / (area * area);
+        double qv[3], rv[3], rg[3];
+        for (int k = 0; k < 3; k++) {
+            qv[k] = co * (a[k] + c[k]);
+            rv[k] = co * ((Ri[k] * a[0] + Ri[3 + k] * a[1] + Ri[6 + k] * a[2]) +
+                          (Rj[k] * c[0] + Rj[3 + k] * c[1] + Rj[6 + k] * c[2]));
+            rg[k] = 2.0 * (Rg[k] * g[0] + Rg[3 + k] * g[1] + Rg[6 + k] * g[2]);
+        }
+        for (int k = 0; k < 3; k++) {
+            Jv[0 + k] = -rv[k] - 2.0 * g[k];
+            Jv[3 + k] = qv[k] + rg[k];
+            Jv[6 + k] = rv[k] - 2.0 * g[k];
+            Jv[9 + k] = -qv[k] + rg[k];
+        }
+        Jv[12] = 2.0 * (u[1] * g[2] - u[2] * g[1]);
+        Jv[13] = 2.0 * (u[2] * g[0] - u[0] * g[2]);
+        Jv[14] = 2.0 * (u[0] * g[1] - u[1] * g[0]);
+        Jv[15] = -4.0 * g[0]; Jv[16] = -4.0 * g[1]; Jv[17] = -4.0 * g[2];
+    } else {                                       // g2o BaseMultiEdge numeric, delta 1e-9
+        const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+        for (int vi = 0; vi < 4; vi++)
+            for (int dd = 0; dd < 3; dd++) {
+                double bak = P[vi][dd];
+                P[vi][dd] = bak + delta;
+                double ep = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
+                P[vi][dd] = bak - delta;
+                double em = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
+                P[vi][dd] = bak;
+                Jv[3 * vi + dd] = scalar * (ep - em);
+            }
+        for (int dd = 0; dd < 6; dd++) {
+            double uu[6] = {0, 0, 0, 0, 0, 0};
+            uu[dd] = delta;
+            SE3 Ep = se3_exp(uu);
+            SE3 Tp = se3_mul(Ep, T);
+            uu[dd] = -delta;
+            SE3 Em = se3_exp(uu);
+            SE3 Tm = se3_mul(Em, T);
+            double ep = arap_err(P[0], P[1], P[2], P[3], Tp, Ri, Rj, w, area);
+            double em = arap_err(P[0], P[1], P[2], P[3], Tm, Ri, Rj, w, area);
+            Jv[12 + dd] = scalar * (ep - em);
+        }
+    }
+    for (int k = 0; k < 18; k++) J[18 * (int64_t)e + k] = Jv[k];
+    W[e] = om;
+    E[e] = err;
+}
+
+// ------------------------------------------------------------------------------------------
+// deterministic H / b assembly
+// ------------------------------------------------------------------------------------------
+struct EdgeJ {
+    const double *Jrep, *Wrep, *Erep, *Jdep, *Wdep, *Edep, *Jarap, *Warap, *Earap;
+};
+
+// Jacobian slice of vertex `role` of edge (kind, e): pointer, vertex dim, residual dim, row stride
+__device__ __forceinline__ void jac_slice(const EdgeJ &ej, int kind, int64_t e, int role, const double *&ptr,
+                                          int &dim, int &m, int &stride, double &w, const double *&err) {
+    if (kind == 0) { ptr = ej.Jrep + 6 * e; dim = 3; m = 2; stride = 3; w = ej.Wrep[e]; err = ej.Erep + 2 * e; }
+    else if (kind == 1) {
+        ptr = ej.Jdep + 4 * e + (role == 0 ? 0 : 3); dim = (role == 0) ? 3 : 1; m = 1; stride = 0;
+        w = ej.Wdep[e]; err = ej.Edep + e;
+    } else {
+        ptr = ej.Jarap + 18 * e + (role < 4 ? 3 * role : 12); dim = (role < 4) ? 3 : 6; m = 1; stride = 0;
+        w = ej.Warap[e]; err = ej.Earap + e;
+    }
+}
+
+__global__ void k_hchunk(int64_t nchunks, const uint64_t *__restrict__ contrib, const int64_t *__restrict__ cbeg,
+                         const int32_t *__restrict__ clen, EdgeJ ej, double *__restrict__ part) {
+    int64_t c = TID;
+    if (c >= nchunks) return;
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) acc[k] = 0.0;
+    int rows = 0, cols = 0;
+    int64_t b0 = cbeg[c];
+    int n = clen[c];
+    for (int t = 0; t < n; t++) {
+        uint64_t rec = contrib[b0 + t];
+        int64_t e = (int64_t)(rec & 0xFFFFFFFFFFull);
+        int kind = (int)((rec >> 40) & 0xF), rcol = (int)((rec >> 44) & 0xF), rrow = (int)((rec >> 48) & 0xF);
+        const double *Jc, *Jr, *er;
+        int dc, dr, m, st;
+        double w;
+        jac_slice(ej, kind, e, rcol, Jc, dc, m, st, w, er);
+        jac_slice(ej, kind, e, rrow, Jr, dr, m, st, w, er);
+        rows = dr; cols = dc;
+        for (int r = 0; r < m; r++) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                if (i >= dr) break;
+                double a = Jr[r * st + i] * w;
+#pragma unroll
+                for (int j = 0; j < 6; j++) {
+                    if (j >= dc) break;
+                    acc[i * 6 + j] += a * Jc[r * st + j];
+                }
+            }
+        }
+    }
+    double *o = part + 36 * c;
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 6; j++)
+            if (i < rows && j < cols) o[i * cols + j] = acc[i * 6 + j];
+}
+
+__global__ void k_hfinal(int64_t nblocks, const int64_t *__restrict__ blk_chunk_begin,
+                         const int64_t *__restrict__ val_off, const int32_t *__restrict__ brows,
+                         const int32_t *__restrict__ bcols, const double *__restrict__ part,
+                         double *__restrict__ hval) {
+    int64_t b = TID;
+    if (b >= nblocks) return;
+    int n = brows[b] * bcols[b];
+    double *o = hval + val_off[b];
+    for (int k = 0; k < n; k++) o[k] = 0.0;
+    for (int64_t c = blk_chunk_begin[b]; c < blk_chunk_begin[b + 1]; c++)
+        for (int k = 0; k < n; k++) o[k] += part[36 * c + k];
+}
+
+__global__ void k_bchunk(int64_t nchunks, const uint64_t *__restrict__ contrib, const int64_t *__restrict__ cbeg,
+                         const int32_t *__restrict__ clen, EdgeJ ej, double *__restrict__ part) {
+    int64_t c = TID;
+    if (c >= nchunks) return;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    int64_t b0 = cbeg[c];
+    int n = clen[c];
+    for (int t = 0; t < n; t++) {
+        uint64_t rec = contrib[b0 + t];
+        int64_t e = (int64_t)(rec & 0xFFFFFFFFFFull);
+        int kind = (int)((rec >> 40) & 0xF), role = (int)((rec >> 44) & 0xF);
+        const double *Jv, *er;
+        int dim, m, st;
+        double w;
+        jac_slice(ej, kind, e, role, Jv, dim, m, st, w, er);
+        for (int r = 0; r < m; r++) {
+            double we = w * er[r];
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+                if (i < dim) acc[i] -= Jv[r * st + i] * we;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) part[6 * c + i] = acc[i];
+}
+
+__global__ void k_bfinal(int64_t nv, const int64_t *__restrict__ v_chunk_begin, const int64_t *__restrict__ voff,
+                         const int32_t *__restrict__ vdim, const double *__restrict__ part, double *__restrict__ b) {
+    int64_t v = TID;
+    if (v >= nv) return;
+    int dim = vdim[v];
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t c = v_chunk_begin[v]; c < v_chunk_begin[v + 1]; c++)
+        for (int i = 0; i < 6; i++) acc[i] += part[6 * c + i];
+    for (int i = 0; i < dim; i++) b[voff[v] + i] = acc[i];
+}
+
+// H (+ lambda I) -> fronts
+__global__ void k_scatter(int64_t nblocks, const int64_t *__restrict__ val_off, const int32_t *__restrict__ brows,
+                          const int32_t *__restrict__ bcols, const int64_t *__restrict__ barena,
+                          const int32_t *__restrict__ bld, const int32_t *__restrict__ bdiag,
+                          const double *__restrict__ hval, double lambda, double *__restrict__ arena) {
+    int64_t b = TID;
+    if (b >= nblocks) return;
+    int R = brows[b], Cc = bcols[b], ld = bld[b];
+    const double *h = hval + val_off[b];
+    double *a = arena + barena[b];
+    bool dg = bdiag[b] != 0;
+    for (int i = 0; i < R; i++)
+        for (int j = 0; j < Cc; j++) a[(int64_t)j * ld + i] = h[i * Cc + j] + ((dg && i == j) ? lambda : 0.0);
+}
+
+// ------------------------------------------------------------------------------------------
+// multifrontal LDL^T
+// ------------------------------------------------------------------------------------------
+__global__ void k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd, double *__restrict__ arena) {
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int c = tasks[3 * t], j0 = tasks[3 * t + 1];
+    int p = fd.parent[c];
+    int mc = fd.m[c], sc = fd.s[c], mp = fd.m[p];
+    int u = mc - sc;
+    const int32_t *bm = fd.bmap + fd.bmap_off[c];
+    const double *Fc = arena + fd.arena_off[c];
+    double *Fp = arena + fd.arena_off[p];
+    int j1 = min(j0 + 16, u);
+    for (int j = j0; j < j1; j++) {
+        int64_t pj = (int64_t)bm[j] * mp;
+        const double *src = Fc + (int64_t)(sc + j) * mc + sc;
+        for (int i = j + threadIdx.x; i < u; i += blockDim.x) Fp[pj + bm[i]] += src[i];
+    }
+}
+
+// LDL^T of the kb x kb diagonal block of panel k0 (lower triangle, unit L, D on the diagonal)
+__global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                              double *__restrict__ arena, int *__restrict__ flag) {
+    __shared__ double A[64][65];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], k0 = tasks[3 * t + 1];
+    int m = fd.m[f], s = fd.s[f];
+    int kb = min(64, s - k0);
+    double *F = arena + fd.arena_off[f];
+    for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
+        int j = idx / kb, i = idx % kb;
+        if (i >= j) A[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
+    }
+    __syncthreads();
+    for (int j = 0; j < kb; j++) {
+        double d = A[j][j];
+        if (threadIdx.x == 0 && d == 0.0) atomicOr(flag, 1);
+        for (int i = j + 1 + threadIdx.x; i < kb; i += blockDim.x) A[i][j] = A[i][j] / d;
+        __syncthreads();
+        int w = kb - 1 - j;
+        for (int idx = threadIdx.x; idx < w * w; idx += blockDim.x) {
+            int ii = idx / w, cc = idx % w;
+            if (ii >= cc) {
+                int i = j + 1 + ii, c2 = j + 1 + cc;
+                A[i][c2] -= A[i][j] * d * A[c2][j];
+            }
+        }
+        __syncthreads();
+    }
+    for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
+        int j = idx / kb, i = idx % kb;
+        if (i >= j) F[(int64_t)(k0 + j) * m + k0 + i] = A[i][j];
+    }
+}
+
+// rows r0..r0+63 below the panel: L_i = F_i L11^{-T} D^{-1}
+__global__ void __launch_bounds__(64) k_trsm(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                             double *__restrict__ arena) {
+    __shared__ double L[64][65];
+    __shared__ double X[64][65];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
+    int m = fd.m[f], s = fd.s[f];
+    int kb = min(64, s - k0);
+    double *F = arena + fd.arena_off[f];
+    int lane = threadIdx.x;
+    for (int j = 0; j < kb; j++) {
+        if (lane >= j && lane < kb) L[lane][j] = F[(int64_t)(k0 + j) * m + k0 + lane];
+    }
+    int i = r0 + lane;
+    bool act = i < m;
+    for (int j = 0; j < kb; j++) X[lane][j] = act ? F[(int64_t)(k0 + j) * m + i] : 0.0;
+    __syncthreads();
+    if (act) {
+        for (int j = 0; j < kb; j++) {
+            double z = X[lane][j];
+            for (int c = 0; c < j; c++) z -= L[j][c] * X[lane][c];
+            X[lane][j] = z;
+        }
+        for (int j = 0; j < kb; j++) F[(int64_t)(k0 + j) * m + i] = X[lane][j] / L[j][j];
+    }
+}
+
+// trailing update of tile (ti, tj): C -= L_i D L_j^T over the panel
+__global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int k0,
+                                                const FrontDev fd, double *__restrict__ arena) {
+    __shared__ double As[64][64];
+    __shared__ double Bs[64][64];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], ti = tasks[3 * t + 1], tj = tasks[3 * t + 2];
+    int m = fd.m[f], s = fd.s[f];
+    int kb = min(64, s - k0);
+    double *F = arena + fd.arena_off[f];
+    for (int idx = threadIdx.x; idx < 64 * kb; idx += blockDim.x) {
+        int c = idx / 64, r = idx % 64;
+        int64_t col = (int64_t)(k0 + c) * m;
+        double dcc = F[col + k0 + c];
+        As[c][r] = (ti + r < m) ? F[col + ti + r] : 0.0;
+        Bs[c][r] = (tj + r < m) ? F[col + tj + r] * dcc : 0.0;
+    }
+    __syncthreads();
+    int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
+    for (int c = 0; c < kb; c++) {
+        double av[4], bv[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) av[a] = As[c][ty * 4 + a];
+#pragma unroll
+        for (int b = 0; b < 4; b++) bv[b] = Bs[c][tx * 4 + b];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] += av[a] * bv[b];
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        int col = tj + tx * 4 + b;
+        if (col >= m) continue;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            int row = ti + ty * 4 + a;
+            if (row < m) F[(int64_t)col * m + row] -= acc[a][b];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// substitution
+// ------------------------------------------------------------------------------------------
+// forward: gather rhs + children's update vectors, solve the own unit-lower triangle
+__global__ void __launch_bounds__(256) k_fwd(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                             const double *__restrict__ arena, const double *__restrict__ rhs,
+                                             double *__restrict__ vec) {
+    __shared__ double Lp[64][65];
+    __shared__ double ts[64];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t];
+    int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    const int32_t *rows = fd.rows + fd.rows_off[f];
+    double *v = vec + fd.vec_off[f];
+    for (int r = threadIdx.x; r < m; r += blockDim.x) v[r] = (r < s) ? rhs[rows[r]] : 0.0;
+    __syncthreads();
+    for (int slot = 0; slot < fd.nchild[f]; slot++) {
+        int c = (slot == 0) ? fd.child0[f] : fd.child1[f];
+        int uc = fd.m[c] - fd.s[c];
+        const double *vc = vec + fd.vec_off[c] + fd.s[c];
+        const int32_t *bm = fd.bmap + fd.bmap_off[c];
+        for (int i = threadIdx.x; i < uc; i += blockDim.x) v[bm[i]] += vc[i];
+        __syncthreads();
+    }
+    for (int k0 = 0; k0 < s; k0 += 64) {
+        int kb = min(64, s - k0);
+        for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
+            int j = idx / kb, i = idx % kb;
+            if (i > j) Lp[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
+        }
+        if (threadIdx.x < kb) ts[threadIdx.x] = v[k0 + threadIdx.x];
+        __syncthreads();
+        if (threadIdx.x < 64) {                     // wave 0: triangle
+            int lane = threadIdx.x;
+            double x = lane < kb ? ts[lane] : 0.0;
+            for (int j = 0; j < kb; j++) {
+                double yj = __shfl(x, j);
+                if (lane > j && lane < kb) x -= Lp[lane][j] * yj;
+            }
+            if (lane < kb) ts[lane] = x;
+        }
+        __syncthreads();
+        if (threadIdx.x < kb) v[k0 + threadIdx.x] = ts[threadIdx.x];
+        for (int i = k0 + kb + threadIdx.x; i < s; i += blockDim.x) {
+            double acc = 0.0;
+            for (int j = 0; j < kb; j++) acc += F[(int64_t)(k0 + j) * m + i] * ts[j];
+            v[i] -= acc;
+        }
+        __syncthreads();
+    }
+}
+
+// boundary rows: t_B -= L21 y
+__global__ void __launch_bounds__(256) k_fwd_gemv(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                  const double *__restrict__ arena, double *__restrict__ vec) {
+    __shared__ double red[4][64];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], r0 = tasks[3 * t + 1];
+    int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    double *v = vec + fd.vec_off[f];
+    int lane = threadIdx.x % 64, part = threadIdx.x / 64;
+    int i = r0 + lane;
+    double acc = 0.0;
+    if (i < m)
+        for (int c = part; c < s; c += 4) acc += F[(int64_t)c * m + i] * v[c];
+    red[part][lane] = acc;
+    __syncthreads();
+    if (part == 0 && i < m) v[i] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// backward, own columns c: r_c = y_c / d_c - sum_i L[i][c] x_B[i]
+__global__ void __launch_bounds__(256) k_bwd_gemv(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                  const double *__restrict__ arena, const double *__restrict__ x,
+                                                  double *__restrict__ vec) {
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], c0 = tasks[3 * t + 1];
+    int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    const int32_t *rows = fd.rows + fd.rows_off[f];
+    double *v = vec + fd.vec_off[f];
+    int lane = threadIdx.x % 64, wv = threadIdx.x / 64;
+    int c1 = min(c0 + 64, s);
+    for (int c = c0 + wv; c < c1; c += 4) {
+        const double *col = F + (int64_t)c * m;
+        double acc = 0.0;
+        for (int i = s + lane; i < m; i += 64) acc += col[i] * x[rows[i]];
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+        if (lane == 0) v[c] = v[c] / col[c] - acc;
+    }
+}
+
+// backward triangle: L11^T x = r (own), scatter x to the global solution
+__global__ void __launch_bounds__(256) k_bwd(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                             const double *__restrict__ arena, double *__restrict__ vec,
+                                             double *__restrict__ x) {
+    __shared__ double Lp[64][65];
+    __shared__ double ts[64];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t];
+    int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    const int32_t *rows = fd.rows + fd.rows_off[f];
+    double *v = vec + fd.vec_off[f];
+    int lane = threadIdx.x % 64, wv = threadIdx.x / 64;
+    int npan = (s + 63) / 64;
+    for (int p = npan - 1; p >= 0; p--) {
+        int k0 = p * 64, kb = min(64, s - k0);
+        // contributions of already-solved own rows below the panel
+        for (int c = k0 + wv; c < k0 + kb; c += 4) {
+            const double *col = F + (int64_t)c * m;
+            double acc = 0.0;
+            for (int i = k0 + kb + lane; i < s; i += 64) acc += col[i] * v[i];
+            for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
+            if (lane == 0) ts[c - k0] = v[c] - acc;
+        }
+        for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
+            int j = idx / kb, i = idx % kb;
+            if (i > j) Lp[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            double xv = lane < kb ? ts[lane] : 0.0;
+            for (int j = kb - 1; j >= 0; j--) {
+                double xj = __shfl(xv, j);
+                if (lane < j) xv -= Lp[j][lane] * xj;
+            }
+            if (lane < kb) v[k0 + lane] = xv;
+        }
+        __syncthreads();
+    }
+    for (int r = threadIdx.x; r < s; r += blockDim.x) x[rows[r]] = v[r];
+}
+
+// ------------------------------------------------------------------------------------------
+// state update, reductions
+// ------------------------------------------------------------------------------------------
+__global__ void k_update_state(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
+                               double *__restrict__ scales, double *__restrict__ tg) {
+    int i = TID;
+    int64_t pbase = 6 * (int64_t)Q + S;
+    if (i < P) {
+        points[3 * (int64_t)i] += dx[pbase + 3 * (int64_t)i];
+        points[3 * (int64_t)i + 1] += dx[pbase + 3 * (int64_t)i + 1];
+        points[3 * (int64_t)i + 2] += dx[pbase + 3 * (int64_t)i + 2];
+    }
+    if (i < S) scales[i] += dx[6 * (int64_t)Q + i];
+    if (i < Q) {
+        double u[6];
+        for (int k = 0; k < 6; k++) u[k] = dx[6 * (int64_t)i + k];
+        SE3 T = se3_load(tg + 7 * i);
+        SE3 Ex = se3_exp(u);
+        SE3 Tn = se3_mul(Ex, T);
+        se3_store(Tn, tg + 7 * i);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sum_partial(int64_t n, const double *__restrict__ a,
+                                                     const double *__restrict__ b, double lambda, int mode,
+                                                     double *__restrict__ part) {
+    // mode 0: sum a ; 1: sum a*(lambda*a + b) ; 2: max |a| over diag handled elsewhere
+    __shared__ double red[256];
+    int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    double acc = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        double v = a[i];
+        acc += (mode == 0) ? v : v * (lambda * v + b[i]);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_sum_final(int n, const double *__restrict__ part, double *__restrict__ out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double acc = 0.0;
+        for (int i = 0; i < n; i++) acc += part[i];
+        *out = acc;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_maxdiag(int64_t nblocks, const int64_t *__restrict__ val_off,
+                                                 const int32_t *__restrict__ bcols, const int32_t *__restrict__ bdiag,
+                                                 const double *__restrict__ hval, double *__restrict__ part) {
+    __shared__ double red[256];
+    int64_t chunk = (nblocks + gridDim.x - 1) / gridDim.x;
+    int64_t lo = blockIdx.x * chunk, hi = min(nblocks, lo + chunk);
+    double mx = 0.0;
+    for (int64_t b = lo + threadIdx.x; b < hi; b += blockDim.x) {
+        if (!bdiag[b]) continue;
+        int c = bcols[b];
+        const double *h = hval + val_off[b];
+        for (int k = 0; k < c; k++) mx = fmax(mx, fabs(h[k * c + k]));
+    }
+    red[threadIdx.x] = mx;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + off]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_max_final(int n, const double *__restrict__ part, double *__restrict__ out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        double mx = 0.0;
+        for (int i = 0; i < n; i++) mx = fmax(mx, part[i]);
+        *out = mx;
+    }
+}
+
+// y = H x from the stored blocks (diagnostics; H symmetric, blocks hold the lower triangle)
+__global__ void k_hmul(int64_t nblocks, const int64_t *__restrict__ val_off, const int32_t *__restrict__ brows,
+                       const int32_t *__restrict__ bcols, const int64_t *__restrict__ brow_dof,
+                       const int64_t *__restrict__ bcol_dof, const int32_t *__restrict__ bdiag,
+                       const double *__restrict__ hval, const double *__restrict__ x, double *__restrict__ y) {
+    int64_t b = TID;
+    if (b >= nblocks) return;
+    int R = brows[b], Cc = bcols[b];
+    const double *h = hval + val_off[b];
+    int64_t r0 = brow_dof[b], c0 = bcol_dof[b];
+    for (int i = 0; i < R; i++)
+        for (int j = 0; j < Cc; j++) {
+            double hv = h[i * Cc + j];
+            atomicAdd(&y[r0 + i], hv * x[c0 + j]);          // diagnostics only (not on the LM path)
+            if (!bdiag[b]) atomicAdd(&y[c0 + j], hv * x[r0 + i]);
+        }
+}
+
+}  // namespace dev
+
+// ------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------
+static inline unsigned nb(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic) {
+    if (P.R > 0)
+        hipLaunchKernelGGL(dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), 0, st, P.R, P.rep_point, P.rep_cam,
+                           P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose, P.cam_R, P.cam_kb8, P.Jrep,
+                           P.Wrep, P.Erep, P.chi_rep, want_jac ? 1 : 0);
+    if (P.D > 0)
+        hipLaunchKernelGGL(dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), 0, st, P.D, P.dep_point, P.dep_scale,
+                           P.dep_cam, P.dep_meas, P.dep_info, P.points, P.scales, P.cam_pose, P.cam_R, P.Jdep,
+                           P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0);
+    if (P.E > 0)
+        hipLaunchKernelGGL(dev::k_lin_arap, dim3(nb(P.E, 128)), dim3(128), 0, st, P.E, P.arap_pts, P.arap_pair,
+                           P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg, P.Jarap, P.Warap,
+                           P.Earap, P.chi_arap, want_jac ? 1 : 0, analytic ? 1 : 0);
+}
+
+void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
+    dev::EdgeJ ej{P.Jrep, P.Wrep, P.Erep, P.Jdep, P.Wdep, P.Edep, P.Jarap, P.Warap, P.Earap};
+    if (L.nhchunks > 0)
+        hipLaunchKernelGGL(dev::k_hchunk, dim3(nb(L.nhchunks, 64)), dim3(64), 0, st, L.nhchunks, L.hcontrib,
+                           L.hchunk_begin, L.hchunk_len, ej, L.hpart);
+    if (L.nblocks > 0)
+        hipLaunchKernelGGL(dev::k_hfinal, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks,
+                           L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
+    if (L.nbchunks > 0)
+        hipLaunchKernelGGL(dev::k_bchunk, dim3(nb(L.nbchunks, 128)), dim3(128), 0, st, L.nbchunks, L.bcontrib,
+                           L.bchunk_begin, L.bchunk_len, ej, L.bpart);
+    if (L.nv > 0)
+        hipLaunchKernelGGL(dev::k_bfinal, dim3(nb(L.nv, 128)), dim3(128), 0, st, L.nv, L.bv_chunk_begin, L.voff,
+                           L.vdim, L.bpart, L.b);
+}
+
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
+    hipMemsetAsync(L.arena, 0, sizeof(double) * (size_t)L.arena_size, st);
+    if (L.nblocks > 0)
+        hipLaunchKernelGGL(dev::k_scatter, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks, L.blk_val_off,
+                           L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, lambda, L.arena);
+}
+
+void launch_factor(const DevPlan &L, hipStream_t st) {
+    for (size_t h = 0; h < L.levels.size(); h++) {
+        const auto &lv = L.levels[h];
+        for (int slot = 0; slot < 2; slot++)
+            if (lv.nea[slot] > 0)
+                hipLaunchKernelGGL(dev::k_ea, dim3(lv.nea[slot]), dim3(256), 0, st, lv.nea[slot],
+                                   L.tasks + 3 * lv.ea_off[slot], L.fd, L.arena);
+        for (const auto &stp : lv.steps) {
+            if (stp.ndiag > 0)
+                hipLaunchKernelGGL(dev::k_diag, dim3(stp.ndiag), dim3(256), 0, st, stp.ndiag, L.tasks + 3 * stp.diag_off,
+                                   L.fd, L.arena, L.flag);
+            if (stp.ntrsm > 0)
+                hipLaunchKernelGGL(dev::k_trsm, dim3(stp.ntrsm), dim3(64), 0, st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
+                                   L.fd, L.arena);
+            if (stp.nupd > 0)
+                hipLaunchKernelGGL(dev::k_update, dim3(stp.nupd), dim3(256), 0, st, stp.nupd, L.tasks + 3 * stp.upd_off,
+                                   stp.k0, L.fd, L.arena);
+        }
+    }
+}
+
+void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st) {
+    for (size_t h = 0; h < L.levels.size(); h++) {
+        const auto &lv = L.levels[h];
+        if (lv.nfwd > 0)
+            hipLaunchKernelGGL(dev::k_fwd, dim3(lv.nfwd), dim3(256), 0, st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
+                               L.arena, rhs, L.vec);
+        if (lv.ngemv > 0)
+            hipLaunchKernelGGL(dev::k_fwd_gemv, dim3(lv.ngemv), dim3(256), 0, st, lv.ngemv, L.tasks + 3 * lv.gemv_off,
+                               L.fd, L.arena, L.vec);
+    }
+    for (size_t hh = L.levels.size(); hh-- > 0;) {
+        const auto &lv = L.levels[hh];
+        if (lv.nbgemv > 0)
+            hipLaunchKernelGGL(dev::k_bwd_gemv, dim3(lv.nbgemv), dim3(256), 0, st, lv.nbgemv,
+                               L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.vec);
+        if (lv.nfwd > 0)
+            hipLaunchKernelGGL(dev::k_bwd, dim3(lv.nfwd), dim3(256), 0, st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
+                               L.arena, L.vec, x);
+    }
+}
+
+void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st) {
+    int n = P.P > P.S ? P.P : P.S;
+    if (P.Q > n) n = P.Q;
+    if (n > 0)
+        hipLaunchKernelGGL(dev::k_update_state, dim3(nb(n, 128)), dim3(128), 0, st, P.P, P.S, P.Q, dx, P.points,
+                           P.scales, P.tg);
+}
+
+void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
+                double *out, hipStream_t st) {
+    if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
+    hipLaunchKernelGGL(dev::k_sum_partial, dim3(nparts), dim3(256), 0, st, n, a, b, lambda, mode, part);
+    hipLaunchKernelGGL(dev::k_sum_final, dim3(1), dim3(64), 0, st, nparts, part, out);
+}
+
+void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st) {
+    hipLaunchKernelGGL(dev::k_maxdiag, dim3(nparts), dim3(256), 0, st, L.nblocks, L.blk_val_off, L.blk_cols,
+                       L.blk_diag, L.hval, part);
+    hipLaunchKernelGGL(dev::k_max_final, dim3(1), dim3(64), 0, st, nparts, part, out);
+}
+
+void launch_hmul(const DevPlan &L, const int64_t *brow_dof, const int64_t *bcol_dof, const double *x, double *y,
+                 int64_t n, hipStream_t st) {
+    hipMemsetAsync(y, 0, sizeof(double) * (size_t)n, st);
+    if (L.nblocks > 0)
+        hipLaunchKernelGGL(dev::k_hmul, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks, L.blk_val_off,
+                           L.blk_rows, L.blk_cols, brow_dof, bcol_dof, L.blk_diag, L.hval, x, y);
+}
+
+}  // namespace deftri

@@ -1,0 +1,706 @@
+// solver.cpp — C-ABI (include/deftri.h): context, upload, g2o-semantics Levenberg–Marquardt on
+// the device, download, diagnostics.  The LM control flow restates g2o's
+// OptimizationAlgorithmLevenberg::solve + SparseOptimizer::optimize as driven by the reference's
+// `optimizer.optimize(nOptIterations)` (Modules/Optimization/g2oBundleAdjustment.cc:959-962):
+//   per iteration: computeActiveErrors, activeRobustChi2, buildSystem, lambda init (it 0:
+//   tau * max diag H), then trials { push; setLambda; solve; update; restoreDiagonal;
+//   computeActiveErrors; rho = (chi_cur - chi_new) / (dx.(lambda dx + b) + 1e-3); accept
+//   (lambda *= max(1/3, min(2/3, 1-(2rho-1)^3)), ni = 2) or reject (lambda *= ni, ni *= 2, pop) }
+//   while rho < 0 && trials < maxTrials; Terminate if trials == maxTrials || rho == 0 || !finite(lambda).
+// Every arithmetic step runs on the GPU; the host only reads back the three scalars the control
+// flow branches on (chi2_new, dx.(lambda dx + b), zero-pivot flag) once per trial.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/deftri.h"
+#include "graph_builder.h"
+#include "kernels.h"
+#include "symbolic.h"
+
+using namespace deftri;
+
+namespace deftri {
+int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const double *rhs, double *x);
+}
+
+namespace {
+
+constexpr int kRedParts = 512;
+
+struct HostProblem {
+    deftri_problem_desc d{};
+    std::vector<double> points, tg, scales, cam_pose, rep_obs, rep_info, dep_meas, dep_info, arap_w, rot,
+        pair_area, pair_info, order_xy;
+    std::vector<float> cam_kb8;
+    std::vector<int32_t> rep_point, rep_cam, dep_point, dep_scale, dep_cam, arap_pts, arap_pair, arap_rot;
+};
+
+template <class T>
+static void cp(std::vector<T> &v, const T *p, int64_t n) {
+    v.assign(p ? p : nullptr, p ? p + n : nullptr);
+    if (!p) v.clear();
+}
+
+static void quat_norm(double *q) {      // SE3Quat::normalizeRotation
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int k = 0; k < 4; k++) q[k] /= n;
+}
+
+static void quat_mat(const double *q, double *R) {
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    double twx = tx * w, twy = ty * w, twz = tz * w;
+    double txx = tx * x, txy = ty * x, txz = tz * x;
+    double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+
+}  // namespace
+
+struct deftri_ctx {
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::string err;
+    bool have = false;        // uploaded to the device
+    bool analysed = false;    // symbolic plan available
+    HostProblem hp;
+    Symbolic S;
+    DevProblem P;
+    DevPlan L;
+    std::vector<void *> allocs;
+    double *d_dx = nullptr, *d_part = nullptr, *d_scal = nullptr;   // d_scal: [0]=chi2 [1]=scale [2]=maxdiag
+    std::vector<double *> init_state;       // device copies of the initial state
+    hipEvent_t ev[8]{};
+    // map-level graph (deftri_arap_build_graph)
+    GraphResult graph;
+};
+
+namespace {
+
+int fail(deftri_ctx *c, int code, const std::string &m) {
+    if (c) c->err = m;
+    return code;
+}
+
+#define HIPOK(expr)                                                                          \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(ctx, DEFTRI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+int dalloc(deftri_ctx *ctx, T **p, int64_t n) {
+    *p = nullptr;
+    if (n <= 0) n = 1;
+    void *v = nullptr;
+    hipError_t e = hipMalloc(&v, sizeof(T) * (size_t)n);
+    if (e != hipSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    ctx->allocs.push_back(v);
+    *p = (T *)v;
+    return 0;
+}
+
+template <class T>
+int dput(deftri_ctx *ctx, T **p, const T *h, int64_t n) {
+    int rc = dalloc(ctx, p, n);
+    if (rc) return rc;
+    if (n > 0 && h) HIPOK(hipMemcpy(*p, h, sizeof(T) * (size_t)n, hipMemcpyHostToDevice));
+    return 0;
+}
+
+template <class T>
+int dput(deftri_ctx *ctx, T **p, const std::vector<T> &v) { return dput(ctx, p, v.data(), (int64_t)v.size()); }
+
+void free_device(deftri_ctx *ctx) {
+    for (void *p : ctx->allocs) hipFree(p);
+    ctx->allocs.clear();
+    ctx->P = DevProblem();
+    ctx->L = DevPlan();
+    ctx->init_state.clear();
+    ctx->have = false;
+}
+
+int validate(deftri_ctx *ctx, const deftri_problem_desc *d) {
+    if (!d) return fail(ctx, DEFTRI_E_ARG, "null descriptor");
+    if (d->n_points < 0 || d->n_pairs < 0 || d->n_scales < 0 || d->n_cams < 0 || d->n_rep < 0 || d->n_depth < 0 ||
+        d->n_arap < 0 || d->n_rot < 0)
+        return fail(ctx, DEFTRI_E_ARG, "negative count");
+    auto need = [&](const void *p, int64_t n, const char *nm) -> bool {
+        if (n > 0 && !p) { ctx->err = std::string("missing array ") + nm; return false; }
+        return true;
+    };
+    if (!need(d->points, d->n_points, "points") || !need(d->tg, d->n_pairs, "tg") ||
+        !need(d->scales, d->n_scales, "scales") || !need(d->cam_kb8, d->n_cams, "cam_kb8") ||
+        !need(d->cam_pose, d->n_cams, "cam_pose") || !need(d->rep_point, d->n_rep, "rep_point") ||
+        !need(d->rep_cam, d->n_rep, "rep_cam") || !need(d->rep_obs, d->n_rep, "rep_obs") ||
+        !need(d->rep_info, d->n_rep, "rep_info") || !need(d->dep_point, d->n_depth, "dep_point") ||
+        !need(d->dep_scale, d->n_depth, "dep_scale") || !need(d->dep_cam, d->n_depth, "dep_cam") ||
+        !need(d->dep_meas, d->n_depth, "dep_meas") || !need(d->dep_info, d->n_depth, "dep_info") ||
+        !need(d->arap_pts, d->n_arap, "arap_pts") || !need(d->arap_pair, d->n_arap, "arap_pair") ||
+        !need(d->arap_rot, d->n_arap, "arap_rot") || !need(d->arap_w, d->n_arap, "arap_w") ||
+        !need(d->rot, d->n_rot, "rot") || !need(d->pair_area, d->n_pairs, "pair_area") ||
+        !need(d->pair_info, d->n_pairs, "pair_info"))
+        return DEFTRI_E_ARG;
+    auto in = [](int64_t v, int64_t hi) { return v >= 0 && v < hi; };
+    for (int e = 0; e < d->n_rep; e++)
+        if (!in(d->rep_point[e], d->n_points) || !in(d->rep_cam[e], d->n_cams))
+            return fail(ctx, DEFTRI_E_ARG, "reprojection edge " + std::to_string(e) + ": index out of range");
+    for (int e = 0; e < d->n_depth; e++)
+        if (!in(d->dep_point[e], d->n_points) || !in(d->dep_scale[e], d->n_scales) || !in(d->dep_cam[e], d->n_cams))
+            return fail(ctx, DEFTRI_E_ARG, "depth edge " + std::to_string(e) + ": index out of range");
+    for (int e = 0; e < d->n_arap; e++) {
+        const int32_t *v = d->arap_pts + 4 * (int64_t)e;
+        for (int k = 0; k < 4; k++)
+            if (!in(v[k], d->n_points)) return fail(ctx, DEFTRI_E_ARG, "ARAP edge " + std::to_string(e) + ": point index out of range");
+        for (int a = 0; a < 4; a++)
+            for (int b = a + 1; b < 4; b++)
+                if (v[a] == v[b]) return fail(ctx, DEFTRI_E_ARG, "ARAP edge " + std::to_string(e) + ": repeated vertex");
+        if (!in(d->arap_pair[e], d->n_pairs) || !in(d->arap_rot[2 * (int64_t)e], d->n_rot) ||
+            !in(d->arap_rot[2 * (int64_t)e + 1], d->n_rot))
+            return fail(ctx, DEFTRI_E_ARG, "ARAP edge " + std::to_string(e) + ": pair/rotation index out of range");
+    }
+    for (int64_t i = 0; i < 3 * (int64_t)d->n_points; i++)
+        if (!std::isfinite(d->points[i])) return fail(ctx, DEFTRI_E_ARG, "non-finite point coordinate");
+    return 0;
+}
+
+void copy_host(HostProblem &h, const deftri_problem_desc *d) {
+    int64_t P = d->n_points, Q = d->n_pairs, S = d->n_scales, C = d->n_cams, R = d->n_rep, D = d->n_depth,
+            E = d->n_arap, NR = d->n_rot;
+    cp(h.points, d->points, 3 * P); cp(h.tg, d->tg, 7 * Q); cp(h.scales, d->scales, S);
+    cp(h.cam_kb8, d->cam_kb8, 8 * C); cp(h.cam_pose, d->cam_pose, 7 * C);
+    cp(h.rep_point, d->rep_point, R); cp(h.rep_cam, d->rep_cam, R); cp(h.rep_obs, d->rep_obs, 2 * R);
+    cp(h.rep_info, d->rep_info, R);
+    cp(h.dep_point, d->dep_point, D); cp(h.dep_scale, d->dep_scale, D); cp(h.dep_cam, d->dep_cam, D);
+    cp(h.dep_meas, d->dep_meas, D); cp(h.dep_info, d->dep_info, D);
+    cp(h.arap_pts, d->arap_pts, 4 * E); cp(h.arap_pair, d->arap_pair, E); cp(h.arap_rot, d->arap_rot, 2 * E);
+    cp(h.arap_w, d->arap_w, E); cp(h.rot, d->rot, 9 * NR); cp(h.pair_area, d->pair_area, Q);
+    cp(h.pair_info, d->pair_info, Q);
+    cp(h.order_xy, d->order_xy, d->order_xy ? 2 * P : 0);
+    for (int64_t q = 0; q < Q; q++) quat_norm(&h.tg[7 * q]);        // SE3Quat(q, t) normalizes
+    for (int64_t c = 0; c < C; c++) quat_norm(&h.cam_pose[7 * c]);
+    h.d = *d;
+    h.d.points = h.points.data(); h.d.tg = h.tg.data(); h.d.scales = h.scales.data();
+    h.d.cam_kb8 = h.cam_kb8.data(); h.d.cam_pose = h.cam_pose.data();
+    h.d.rep_point = h.rep_point.data(); h.d.rep_cam = h.rep_cam.data(); h.d.rep_obs = h.rep_obs.data();
+    h.d.rep_info = h.rep_info.data();
+    h.d.dep_point = h.dep_point.data(); h.d.dep_scale = h.dep_scale.data(); h.d.dep_cam = h.dep_cam.data();
+    h.d.dep_meas = h.dep_meas.data(); h.d.dep_info = h.dep_info.data();
+    h.d.arap_pts = h.arap_pts.data(); h.d.arap_pair = h.arap_pair.data(); h.d.arap_rot = h.arap_rot.data();
+    h.d.arap_w = h.arap_w.data(); h.d.rot = h.rot.data(); h.d.pair_area = h.pair_area.data();
+    h.d.pair_info = h.pair_info.data();
+    h.d.order_xy = h.order_xy.empty() ? nullptr : h.order_xy.data();
+}
+
+int upload_device(deftri_ctx *ctx) {
+    const HostProblem &h = ctx->hp;
+    const deftri_problem_desc &d = h.d;
+    DevProblem &P = ctx->P;
+    P.P = d.n_points; P.Q = d.n_pairs; P.S = d.n_scales; P.C = d.n_cams;
+    P.R = d.n_rep; P.D = d.n_depth; P.E = d.n_arap; P.NR = d.n_rot;
+    P.huber_delta = d.huber_delta;
+    int rc;
+#define PUT(dst, src) if ((rc = dput(ctx, &(dst), src))) return rc
+    PUT(P.points, h.points); PUT(P.scales, h.scales); PUT(P.tg, h.tg);
+    if ((rc = dalloc(ctx, &P.points_bak, 3 * (int64_t)P.P))) return rc;
+    if ((rc = dalloc(ctx, &P.scales_bak, P.S))) return rc;
+    if ((rc = dalloc(ctx, &P.tg_bak, 7 * (int64_t)P.Q))) return rc;
+    PUT(P.cam_kb8, h.cam_kb8); PUT(P.cam_pose, h.cam_pose);
+    std::vector<double> camR(9 * (size_t)std::max(P.C, 1));
+    for (int c = 0; c < P.C; c++) quat_mat(&h.cam_pose[7 * c], &camR[9 * c]);
+    PUT(P.cam_R, camR);
+    PUT(P.rep_point, h.rep_point); PUT(P.rep_cam, h.rep_cam); PUT(P.rep_obs, h.rep_obs); PUT(P.rep_info, h.rep_info);
+    PUT(P.dep_point, h.dep_point); PUT(P.dep_scale, h.dep_scale); PUT(P.dep_cam, h.dep_cam);
+    PUT(P.dep_meas, h.dep_meas); PUT(P.dep_info, h.dep_info);
+    PUT(P.arap_pts, h.arap_pts); PUT(P.arap_pair, h.arap_pair); PUT(P.arap_rot, h.arap_rot);
+    PUT(P.arap_w, h.arap_w); PUT(P.rot, h.rot); PUT(P.pair_area, h.pair_area); PUT(P.pair_info, h.pair_info);
+    if ((rc = dalloc(ctx, &P.Jrep, 6 * (int64_t)P.R)) || (rc = dalloc(ctx, &P.Wrep, P.R)) ||
+        (rc = dalloc(ctx, &P.Erep, 2 * (int64_t)P.R)) || (rc = dalloc(ctx, &P.chi_rep, P.R)) ||
+        (rc = dalloc(ctx, &P.Jdep, 4 * (int64_t)P.D)) || (rc = dalloc(ctx, &P.Wdep, P.D)) ||
+        (rc = dalloc(ctx, &P.Edep, P.D)) || (rc = dalloc(ctx, &P.chi_dep, P.D)) ||
+        (rc = dalloc(ctx, &P.Jarap, 18 * (int64_t)P.E)) || (rc = dalloc(ctx, &P.Warap, P.E)) ||
+        (rc = dalloc(ctx, &P.Earap, P.E)) || (rc = dalloc(ctx, &P.chi_arap, P.E)))
+        return rc;
+    // keep the initial state for deftri_reset_state
+    ctx->init_state.resize(3);
+    if ((rc = dput(ctx, &ctx->init_state[0], h.points)) || (rc = dput(ctx, &ctx->init_state[1], h.scales)) ||
+        (rc = dput(ctx, &ctx->init_state[2], h.tg)))
+        return rc;
+
+    // plan
+    const Symbolic &S = ctx->S;
+    DevPlan &L = ctx->L;
+    L.nv = S.nv; L.ndof = S.ndof;
+    PUT(L.voff, S.voff); PUT(L.vdim, S.vdim);
+    L.nblocks = S.nblocks; L.hval_size = S.hval_size;
+    if ((rc = dalloc(ctx, &L.hval, S.hval_size))) return rc;
+    PUT(L.blk_val_off, S.blk_val_off); PUT(L.blk_arena, S.blk_arena); PUT(L.blk_rows, S.blk_rows);
+    PUT(L.blk_cols, S.blk_cols); PUT(L.blk_ld, S.blk_ld); PUT(L.blk_diag, S.blk_diag);
+    {
+        // dof of each block's row / column vertex (diagnostic H x product)
+        std::vector<int64_t> rd(S.nblocks), cd(S.nblocks);
+        for (int64_t c = 0, b = 0; c < S.nv; c++) {
+            (void)c;
+            (void)b;
+        }
+        // reconstruct from the arena map: row/col vertices are not stored, so rebuild from rows[]
+        for (int64_t b = 0; b < S.nblocks; b++) {
+            // find front by arena offset (blocks are emitted front-contiguous per column vertex)
+            rd[b] = 0; cd[b] = 0;
+        }
+        int32_t nf = (int32_t)S.fronts.size();
+        std::vector<int64_t> starts(nf);
+        for (int32_t f = 0; f < nf; f++) starts[f] = S.fronts[f].arena_off;
+        for (int64_t b = 0; b < S.nblocks; b++) {
+            int64_t a = S.blk_arena[b];
+            int32_t f = (int32_t)(std::upper_bound(starts.begin(), starts.end(), a) - starts.begin()) - 1;
+            const Front &F = S.fronts[f];
+            int64_t loc = a - F.arena_off;
+            int32_t lc = (int32_t)(loc / F.m), lr = (int32_t)(loc % F.m);
+            rd[b] = S.rows[F.rows_off + lr];
+            cd[b] = S.rows[F.rows_off + lc];
+        }
+        PUT(L.blk_row_dof, rd); PUT(L.blk_col_dof, cd);
+    }
+    L.nhchunks = (int64_t)S.hchunk_begin.size();
+    PUT(L.hcontrib, S.hcontrib); PUT(L.hchunk_begin, S.hchunk_begin); PUT(L.hchunk_len, S.hchunk_len);
+    PUT(L.hblk_chunk_begin, S.hblk_chunk_begin);
+    if ((rc = dalloc(ctx, &L.hpart, 36 * L.nhchunks))) return rc;
+    L.nbchunks = (int64_t)S.bchunk_begin.size();
+    PUT(L.bcontrib, S.bcontrib); PUT(L.bchunk_begin, S.bchunk_begin); PUT(L.bchunk_len, S.bchunk_len);
+    PUT(L.bv_chunk_begin, S.bv_chunk_begin);
+    if ((rc = dalloc(ctx, &L.bpart, 6 * L.nbchunks))) return rc;
+    if ((rc = dalloc(ctx, &L.b, S.ndof))) return rc;
+    L.arena_size = S.arena_size; L.vec_size = S.vec_size;
+    if ((rc = dalloc(ctx, &L.arena, S.arena_size))) return rc;
+    if ((rc = dalloc(ctx, &L.vec, S.vec_size))) return rc;
+    {
+        int32_t nf = (int32_t)S.fronts.size();
+        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf);
+        std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf);
+        for (int32_t f = 0; f < nf; f++) {
+            const Front &F = S.fronts[f];
+            m[f] = F.m; s[f] = F.s; par[f] = F.parent; nch[f] = F.nchild; c0[f] = F.child[0]; c1[f] = F.child[1];
+            ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off;
+        }
+        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *prows, *pbmap;
+        int64_t *pao, *pvo, *pro, *pbo;
+        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1);
+        PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo);
+        PUT(prows, S.rows); PUT(pbmap, S.bmap);
+        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pao, pvo, pro, pbo, prows, pbmap};
+    }
+    PUT(L.tasks, S.task_i32);
+    L.levels.clear();
+    for (const auto &lv : S.levels) {
+        LevelDev ld{};
+        for (int k = 0; k < 2; k++) { ld.ea_off[k] = lv.ea_off[k]; ld.nea[k] = lv.nea[k]; }
+        for (const auto &stp : lv.steps)
+            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0});
+        ld.fwd_off = lv.fwd_off; ld.nfwd = lv.nfwd;
+        ld.gemv_off = lv.gemv_off; ld.ngemv = lv.ngemv;
+        ld.bgemv_off = lv.bgemv_off; ld.nbgemv = lv.nbgemv;
+        L.levels.push_back(ld);
+    }
+    if ((rc = dalloc(ctx, &L.flag, 1))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_dx, S.ndof))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_part, kRedParts))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_scal, 8))) return rc;
+#undef PUT
+    HIPOK(hipDeviceSynchronize());
+    return 0;
+}
+
+// chi2 at the current state (computeActiveErrors + activeRobustChi2) into d_scal[slot]
+void eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot) {
+    DevProblem &P = ctx->P;
+    launch_linearize(P, ctx->st, want_jac, analytic);
+    // sum of the three chi arrays, in edge order rep, depth, arap (three partial sums, then add)
+    launch_sum(P.R, P.chi_rep, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 4, ctx->st);
+    launch_sum(P.D, P.chi_dep, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 5, ctx->st);
+    launch_sum(P.E, P.chi_arap, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 6, ctx->st);
+    launch_sum(3, ctx->d_scal + 4, nullptr, 0, 0, ctx->d_part, 1, ctx->d_scal + slot, ctx->st);
+}
+
+double read_scal(deftri_ctx *ctx, int slot) {
+    double v = 0;
+    hipMemcpyAsync(&v, ctx->d_scal + slot, sizeof(double), hipMemcpyDeviceToHost, ctx->st);
+    hipStreamSynchronize(ctx->st);
+    return v;
+}
+
+void push_state(deftri_ctx *ctx) {
+    DevProblem &P = ctx->P;
+    hipMemcpyAsync(P.points_bak, P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.scales_bak, P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.tg_bak, P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
+}
+
+void pop_state(deftri_ctx *ctx) {
+    DevProblem &P = ctx->P;
+    hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
+}
+
+float ev_ms(deftri_ctx *ctx, int a, int b) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
+    return ms;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C-ABI
+// ==========================================================================================
+extern "C" {
+
+int deftri_abi_version(void) { return DEFTRI_ABI_VERSION; }
+
+int deftri_ctx_create(int32_t device, deftri_ctx **out) {
+    if (!out) return DEFTRI_E_ARG;
+    *out = nullptr;
+    if (device < 0) {                    // host-only context
+        deftri_ctx *ctx = new deftri_ctx();
+        ctx->device = -1;
+        *out = ctx;
+        return 0;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DEFTRI_E_NODEVICE;
+    if (device < 0 || device >= n) return DEFTRI_E_NODEVICE;
+    deftri_ctx *ctx = new deftri_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return DEFTRI_E_HIP;
+    }
+    for (auto &e : ctx->ev) hipEventCreate(&e);
+    *out = ctx;
+    return 0;
+}
+
+int deftri_ctx_destroy(deftri_ctx *ctx) {
+    if (!ctx) return 0;
+    if (ctx->device < 0) { delete ctx; return 0; }
+    hipSetDevice(ctx->device);
+    free_device(ctx);
+    for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
+    if (ctx->st) hipStreamDestroy(ctx->st);
+    delete ctx;
+    return 0;
+}
+
+const char *deftri_last_error(const deftri_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int64_t deftri_num_unknowns(const deftri_ctx *ctx) { return (ctx && ctx->have) ? ctx->S.ndof : -1; }
+
+int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc) {
+    if (!ctx) return DEFTRI_E_ARG;
+    int rc = validate(ctx, desc);
+    if (rc) return rc;
+    if (ctx->device >= 0) { hipSetDevice(ctx->device); free_device(ctx); }
+    ctx->have = false;
+    copy_host(ctx->hp, desc);
+    if (!analyse(ctx->hp.d, ctx->S)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
+    ctx->analysed = true;
+    return 0;
+}
+
+int deftri_plan_stats(const deftri_ctx *ctx, deftri_report *rep) {
+    if (!ctx || !rep) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return DEFTRI_E_NOPROBLEM;
+    std::memset(rep, 0, sizeof(*rep));
+    rep->n_unknowns = ctx->S.ndof;
+    rep->nnz_factor = ctx->S.nnz_factor;
+    rep->factor_flops = ctx->S.factor_flops;
+    rep->n_fronts = (int32_t)ctx->S.fronts.size();
+    rep->n_levels = ctx->S.nlevels;
+    return 0;
+}
+
+int deftri_debug_plan_solve(deftri_ctx *ctx, const double *H, double lambda, const double *rhs, double *x,
+                            int64_t n) {
+    if (!ctx || !H || !rhs || !x) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem analysed");
+    if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    return plan_emulate_solve(ctx->S, H, lambda, rhs, x) == 0 ? 0 : fail(ctx, DEFTRI_E_NUMERIC, "zero pivot");
+}
+
+int64_t deftri_sizeof(int32_t which) {
+    switch (which) {
+        case 0: return (int64_t)sizeof(deftri_problem_desc);
+        case 1: return (int64_t)sizeof(deftri_lm_params);
+        case 2: return (int64_t)sizeof(deftri_report);
+        case 3: return (int64_t)sizeof(deftri_keyframe);
+        case 4: return (int64_t)sizeof(deftri_map);
+        default: return -1;
+    }
+}
+
+int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
+    if (!ctx) return DEFTRI_E_ARG;
+    if (ctx->device < 0) return fail(ctx, DEFTRI_E_NODEVICE, "host-only context");
+    hipSetDevice(ctx->device);
+    int rc = validate(ctx, desc);
+    if (rc) return rc;
+    free_device(ctx);
+    copy_host(ctx->hp, desc);
+    if (!analyse(ctx->hp.d, ctx->S)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
+    ctx->analysed = true;
+    rc = upload_device(ctx);
+    if (rc) { free_device(ctx); return rc; }
+    ctx->have = true;
+    return 0;
+}
+
+int deftri_reset_state(deftri_ctx *ctx) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    DevProblem &P = ctx->P;
+    HIPOK(hipMemcpyAsync(P.points, ctx->init_state[0], sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, ctx->st));
+    HIPOK(hipMemcpyAsync(P.scales, ctx->init_state[1], sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, ctx->st));
+    HIPOK(hipMemcpyAsync(P.tg, ctx->init_state[2], sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st));
+    HIPOK(hipStreamSynchronize(ctx->st));
+    return 0;
+}
+
+int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report *rep) {
+    if (!ctx || !prm) return DEFTRI_E_ARG;
+    if (!ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(ctx->device);
+    deftri_report local{};
+    deftri_report &R = rep ? *rep : local;
+    std::memset(&R, 0, sizeof(R));
+    R.n_unknowns = ctx->S.ndof;
+    R.nnz_factor = ctx->S.nnz_factor;
+    R.factor_flops = ctx->S.factor_flops;
+    R.n_fronts = (int32_t)ctx->S.fronts.size();
+    R.n_levels = ctx->S.nlevels;
+    const int max_trials = prm->max_trials > 0 ? prm->max_trials : 10;
+    const double tau = prm->tau > 0 ? prm->tau : 1e-5;
+    const bool analytic = prm->analytic_jacobians != 0;
+    DevProblem &P = ctx->P;
+    DevPlan &L = ctx->L;
+    auto t_start = std::chrono::steady_clock::now();
+    double lambda = 0, ni = 2;
+    double t_lin = 0, t_fac = 0, t_sol = 0, t_upd = 0;
+    int status = DEFTRI_STATUS_OK, it;
+    eval_chi2_dev(ctx, false, analytic, 0);
+    R.chi2_initial = read_scal(ctx, 0);
+    double currentChi = R.chi2_initial;
+    for (it = 0; it < prm->n_iterations; it++) {
+        hipEventRecord(ctx->ev[0], ctx->st);
+        eval_chi2_dev(ctx, true, analytic, 0);              // computeActiveErrors + linearizeOplus
+        launch_assemble(P, L, ctx->st);                      // buildSystem
+        if (it == 0) launch_maxdiag(L, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
+        hipEventRecord(ctx->ev[1], ctx->st);
+        double chis[3];
+        HIPOK(hipMemcpyAsync(chis, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+        HIPOK(hipStreamSynchronize(ctx->st));
+        t_lin += ev_ms(ctx, 0, 1);
+        currentChi = chis[0];
+        if (it == 0) {
+            lambda = prm->user_lambda > 0 ? prm->user_lambda : tau * chis[2];
+            ni = 2;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            push_state(ctx);
+            hipEventRecord(ctx->ev[2], ctx->st);
+            HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
+            launch_scatter(L, lambda, ctx->st);              // setLambda
+            launch_factor(L, ctx->st);
+            hipEventRecord(ctx->ev[3], ctx->st);
+            launch_solve(L, L.b, ctx->d_dx, ctx->st);
+            hipEventRecord(ctx->ev[4], ctx->st);
+            int flag = 0;
+            HIPOK(hipMemcpyAsync(&flag, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            HIPOK(hipStreamSynchronize(ctx->st));
+            bool ok2 = flag == 0;
+            if (!ok2) HIPOK(hipMemsetAsync(ctx->d_dx, 0, sizeof(double) * (size_t)ctx->S.ndof, ctx->st));
+            launch_update_state(P, ctx->d_dx, ctx->st);      // _optimizer->update(x)
+            eval_chi2_dev(ctx, false, analytic, 0);          // computeActiveErrors; activeRobustChi2
+            launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
+            hipEventRecord(ctx->ev[5], ctx->st);
+            double sc[2];
+            HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
+            HIPOK(hipStreamSynchronize(ctx->st));
+            t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
+            double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
+            rho = (currentChi - tempChi);
+            double scale = sc[1] + 1e-3;
+            rho /= scale;
+            R.trials_total++;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                pop_state(ctx);
+                R.trials_rejected++;
+            }
+            qmax++;
+        } while (rho < 0 && qmax < max_trials);
+        if (it < DEFTRI_MAX_REPORT_ITERS) { R.chi2_iter[it] = currentChi; R.trials_iter[it] = qmax; }
+        if (prm->verbose)
+            std::fprintf(stderr, "[deftri] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
+        if (qmax == max_trials || rho == 0 || !std::isfinite(lambda)) { status = DEFTRI_STATUS_TERMINATE; it++; break; }
+    }
+    eval_chi2_dev(ctx, false, analytic, 0);
+    R.chi2_final = read_scal(ctx, 0);
+    HIPOK(hipStreamSynchronize(ctx->st));
+    R.status = status;
+    R.iterations = it;
+    R.lambda_final = lambda;
+    R.ms_linearize = t_lin; R.ms_factor = t_fac; R.ms_solve = t_sol; R.ms_update = t_upd;
+    R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return 0;
+}
+
+int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(ctx->device);
+    DevProblem &P = ctx->P;
+    if (points) HIPOK(hipMemcpy(points, P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToHost));
+    if (scales) HIPOK(hipMemcpy(scales, P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToHost));
+    if (tg) HIPOK(hipMemcpy(tg, P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int deftri_eval_chi2(deftri_ctx *ctx, double *chi2) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(ctx->device);
+    eval_chi2_dev(ctx, false, true, 0);
+    *chi2 = read_scal(ctx, 0);
+    return 0;
+}
+
+int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(ctx->device);
+    eval_chi2_dev(ctx, true, true, 0);
+    launch_assemble(ctx->P, ctx->L, ctx->st);
+    HIPOK(hipStreamSynchronize(ctx->st));
+    if (b) HIPOK(hipMemcpy(b, ctx->L.b, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
+    if (hdiag) {
+        std::vector<double> hv(ctx->S.hval_size);
+        HIPOK(hipMemcpy(hv.data(), ctx->L.hval, sizeof(double) * hv.size(), hipMemcpyDeviceToHost));
+        // diagonal blocks: column vertex == row vertex; dof from the vertex layout
+        int64_t b0 = 0;
+        const Symbolic &S = ctx->S;
+        for (int64_t blk = 0; blk < S.nblocks; blk++) {
+            if (!S.blk_diag[blk]) continue;
+            (void)b0;
+            // the diagonal block of vertex v sits in v's own column at its own rows
+            int64_t a = S.blk_arena[blk];
+            int32_t f = 0;
+            for (int32_t ff = (int32_t)S.fronts.size() - 1; ff >= 0; ff--)
+                if (S.fronts[ff].arena_off <= a) { f = ff; break; }
+            const Front &F = S.fronts[f];
+            int32_t lr = (int32_t)((a - F.arena_off) % F.m);
+            int c = S.blk_cols[blk];
+            for (int k = 0; k < c; k++) hdiag[S.rows[F.rows_off + lr + k]] = hv[S.blk_val_off[blk] + k * c + k];
+        }
+    }
+    return 0;
+}
+
+int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (n != ctx->S.ndof || !x || !y) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(ctx->device);
+    double *dx = nullptr, *dy = nullptr;
+    HIPOK(hipMalloc(&dx, sizeof(double) * (size_t)n));
+    HIPOK(hipMalloc(&dy, sizeof(double) * (size_t)n));
+    hipMemcpy(dx, x, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
+    eval_chi2_dev(ctx, true, true, 0);
+    launch_assemble(ctx->P, ctx->L, ctx->st);
+    launch_hmul(ctx->L, ctx->L.blk_row_dof, ctx->L.blk_col_dof, dx, dy, n, ctx->st);
+    hipStreamSynchronize(ctx->st);
+    hipMemcpy(y, dy, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost);
+    hipFree(dx); hipFree(dy);
+    return 0;
+}
+
+int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n) {
+    if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (n != ctx->S.ndof || !rhs || !x) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(ctx->device);
+    double *dr = nullptr;
+    HIPOK(hipMalloc(&dr, sizeof(double) * (size_t)n));
+    hipMemcpy(dr, rhs, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
+    eval_chi2_dev(ctx, true, true, 0);
+    launch_assemble(ctx->P, ctx->L, ctx->st);
+    hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
+    launch_scatter(ctx->L, lambda, ctx->st);
+    launch_factor(ctx->L, ctx->st);
+    launch_solve(ctx->L, dr, ctx->d_dx, ctx->st);
+    int flag = 0;
+    hipMemcpyAsync(&flag, ctx->L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st);
+    hipStreamSynchronize(ctx->st);
+    hipMemcpy(x, ctx->d_dx, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost);
+    hipFree(dr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(ctx, DEFTRI_E_HIP, hipGetErrorString(e));
+    return flag ? fail(ctx, DEFTRI_E_NUMERIC, "zero pivot") : 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// map level
+// ---------------------------------------------------------------------------------------------
+int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight, double arap_weight,
+                            float depth_error, const deftri_problem_desc **desc_out) {
+    if (!ctx || !map || !desc_out) return DEFTRI_E_ARG;
+    std::string err;
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err))
+        return fail(ctx, DEFTRI_E_GRAPH, err);
+    *desc_out = &ctx->graph.desc;
+    return 0;
+}
+
+int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight, double global_weight,
+                             double arap_weight, double alpha, double beta, float depth_error,
+                             int32_t n_iterations, double *optimization_update, deftri_report *report) {
+    (void)global_weight; (void)alpha; (void)beta;   // stored but unused by the reference edges
+    if (!ctx || !map) return DEFTRI_E_ARG;
+    std::string err;
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err))
+        return fail(ctx, DEFTRI_E_GRAPH, err);
+    int rc = deftri_problem_upload(ctx, &ctx->graph.desc);
+    if (rc) return rc;
+    deftri_lm_params prm{};
+    prm.n_iterations = n_iterations;
+    prm.max_trials = 10;
+    prm.tau = 1e-5;
+    prm.analytic_jacobians = 1;
+    rc = deftri_solve_lm(ctx, &prm, report);
+    if (rc) return rc;
+    const GraphResult &g = ctx->graph;
+    std::vector<double> pts(3 * (size_t)g.desc.n_points), sc(g.desc.n_scales), tg(7 * (size_t)g.desc.n_pairs);
+    rc = deftri_download(ctx, pts.data(), sc.data(), tg.data());
+    if (rc) return rc;
+    writeback_arap(*map, g, pts, sc, tg, optimization_update);
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,395 @@
+// symbolic.cpp — nested-dissection ordering + multifrontal plan (see symbolic.h).
+#include "symbolic.h"
+
+#include <algorithm>
+#include <cmath>
+#include <numeric>
+
+namespace deftri {
+
+namespace {
+
+struct Builder {
+    const deftri_problem_desc &d;
+    Symbolic &S;
+    int leaf;
+    int32_t Q, NS, P;
+    std::vector<int64_t> adj_begin;       // vertex adjacency CSR (sorted, unique, no self)
+    std::vector<int64_t> adj;
+    std::vector<double> xy;               // point ordering coordinates
+    // front construction
+    std::vector<std::vector<int64_t>> own;        // per front: own vertices (elim order)
+    std::vector<std::vector<int64_t>> bnd;        // per front: boundary vertices (elim order)
+    std::vector<int32_t> vfront;                  // vertex -> owning front
+    int64_t next_pos = 0;
+    std::vector<int32_t> side;
+
+    Builder(const deftri_problem_desc &d_, Symbolic &S_, int leaf_) : d(d_), S(S_), leaf(leaf_) {
+        Q = d.n_pairs; NS = d.n_scales; P = d.n_points;
+    }
+
+    int64_t vT(int q) const { return q; }
+    int64_t vS(int k) const { return (int64_t)Q + k; }
+    int64_t vP(int p) const { return (int64_t)Q + NS + p; }
+
+    void build_adjacency() {
+        int64_t nv = S.nv;
+        std::vector<std::pair<int64_t, int64_t>> pr;
+        pr.reserve((size_t)d.n_depth * 2 + (size_t)d.n_arap * 20);
+        for (int e = 0; e < d.n_depth; e++) {
+            int64_t a = vP(d.dep_point[e]), b = vS(d.dep_scale[e]);
+            pr.emplace_back(a, b); pr.emplace_back(b, a);
+        }
+        for (int e = 0; e < d.n_arap; e++) {
+            int64_t v[5];
+            for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
+            v[4] = vT(d.arap_pair[e]);
+            for (int i = 0; i < 5; i++)
+                for (int j = 0; j < 5; j++)
+                    if (i != j && v[i] != v[j]) pr.emplace_back(v[i], v[j]);
+        }
+        std::sort(pr.begin(), pr.end());
+        pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
+        adj_begin.assign(nv + 1, 0);
+        adj.resize(pr.size());
+        for (size_t i = 0; i < pr.size(); i++) { adj_begin[pr[i].first + 1]++; adj[i] = pr[i].second; }
+        for (int64_t v = 0; v < nv; v++) adj_begin[v + 1] += adj_begin[v];
+    }
+
+    int32_t new_front(std::vector<int64_t> &&ownv, std::vector<int32_t> children) {
+        int32_t f = (int32_t)S.fronts.size();
+        Front F{};
+        F.parent = -1;
+        F.nchild = (int32_t)children.size();
+        F.child[0] = F.child[1] = -1;
+        for (size_t i = 0; i < children.size(); i++) { F.child[i] = children[i]; S.fronts[children[i]].parent = f; }
+        S.fronts.push_back(F);
+        for (int64_t v : ownv) { S.elim_pos[v] = next_pos++; vfront[v] = f; }
+        own.push_back(std::move(ownv));
+        bnd.emplace_back();
+        return f;
+    }
+
+    int32_t nd(std::vector<int64_t> &nodes, int depth) {
+        int64_t n = (int64_t)nodes.size();
+        if (n <= leaf || depth > 48) {
+            std::vector<int64_t> o(nodes.begin(), nodes.end());
+            std::sort(o.begin(), o.end());
+            std::vector<int64_t> ov;
+            for (int64_t p : o) ov.push_back(vP((int32_t)p));
+            return new_front(std::move(ov), {});
+        }
+        double mn[2] = {1e300, 1e300}, mx[2] = {-1e300, -1e300};
+        for (int64_t p : nodes)
+            for (int k = 0; k < 2; k++) { mn[k] = std::min(mn[k], xy[2 * p + k]); mx[k] = std::max(mx[k], xy[2 * p + k]); }
+        int ax = (mx[0] - mn[0] >= mx[1] - mn[1]) ? 0 : 1;
+        std::sort(nodes.begin(), nodes.end(), [&](int64_t a, int64_t b) {
+            double x = xy[2 * a + ax], y = xy[2 * b + ax];
+            return x < y || (x == y && a < b);
+        });
+        int64_t half = n / 2;
+        for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < half) ? 1 : 2;
+        for (int64_t i = 0; i < half; i++) {
+            int64_t v = vP((int32_t)nodes[i]);
+            for (int64_t k = adj_begin[v]; k < adj_begin[v + 1]; k++) {
+                int64_t u = adj[k] - ((int64_t)Q + NS);
+                if (u >= 0 && side[u] == 2) { side[nodes[i]] = 3; break; }
+            }
+        }
+        std::vector<int64_t> L, R, Sp;
+        for (int64_t p : nodes) {
+            if (side[p] == 1) L.push_back(p);
+            else if (side[p] == 2) R.push_back(p);
+            else Sp.push_back(p);
+        }
+        for (int64_t p : nodes) side[p] = 0;
+        if (L.empty() || R.empty()) {          // cannot split (degenerate coordinates)
+            std::vector<int64_t> ov;
+            std::sort(nodes.begin(), nodes.end());
+            for (int64_t p : nodes) ov.push_back(vP((int32_t)p));
+            return new_front(std::move(ov), {});
+        }
+        int32_t cl = nd(L, depth + 1);
+        int32_t cr = nd(R, depth + 1);
+        std::sort(Sp.begin(), Sp.end());
+        std::vector<int64_t> ov;
+        for (int64_t p : Sp) ov.push_back(vP((int32_t)p));
+        return new_front(std::move(ov), {cl, cr});
+    }
+
+    bool run() {
+        S.nv = (int64_t)Q + NS + P;
+        S.vdim.resize(S.nv);
+        S.voff.resize(S.nv);
+        int64_t off = 0;
+        for (int64_t v = 0; v < S.nv; v++) {
+            int dim = v < Q ? 6 : (v < Q + NS ? 1 : 3);
+            S.vdim[v] = dim; S.voff[v] = off; off += dim;
+        }
+        S.ndof = off;
+        S.elim_pos.assign(S.nv, -1);
+        vfront.assign(S.nv, -1);
+        build_adjacency();
+        xy.resize(2 * (size_t)std::max(P, 1));
+        for (int32_t p = 0; p < P; p++) {
+            if (d.order_xy) { xy[2 * p] = d.order_xy[2 * p]; xy[2 * p + 1] = d.order_xy[2 * p + 1]; }
+            else { xy[2 * p] = d.points[3 * (int64_t)p]; xy[2 * p + 1] = d.points[3 * (int64_t)p + 1]; }
+        }
+        side.assign(std::max(P, 1), 0);
+        std::vector<int32_t> rootch;
+        if (P > 0) {
+            std::vector<int64_t> nodes(P);
+            std::iota(nodes.begin(), nodes.end(), 0);
+            rootch.push_back(nd(nodes, 0));
+        }
+        std::vector<int64_t> gl;
+        for (int q = 0; q < Q; q++) gl.push_back(vT(q));
+        for (int k = 0; k < NS; k++) gl.push_back(vS(k));
+        if (!gl.empty() || rootch.empty()) new_front(std::move(gl), rootch);
+        // boundaries (fronts are in postorder: children precede parents)
+        int32_t nf = (int32_t)S.fronts.size();
+        std::vector<int64_t> cand;
+        for (int32_t f = 0; f < nf; f++) {
+            cand.clear();
+            int64_t last = -1;
+            for (int64_t v : own[f]) last = std::max(last, S.elim_pos[v]);
+            for (int64_t v : own[f])
+                for (int64_t k = adj_begin[v]; k < adj_begin[v + 1]; k++)
+                    if (S.elim_pos[adj[k]] > last) cand.push_back(adj[k]);
+            for (int c = 0; c < S.fronts[f].nchild; c++)
+                for (int64_t u : bnd[S.fronts[f].child[c]])
+                    if (S.elim_pos[u] > last) cand.push_back(u);
+            std::sort(cand.begin(), cand.end(), [&](int64_t a, int64_t b) { return S.elim_pos[a] < S.elim_pos[b]; });
+            cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
+            bnd[f] = cand;
+        }
+        // rows, sizes, offsets
+        std::vector<std::vector<int64_t>> fv(nf);       // vertex list (row order)
+        std::vector<std::vector<int32_t>> fvrow(nf);    // local row of each vertex
+        int64_t aoff = 0, voff2 = 0;
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            fv[f] = own[f];
+            fv[f].insert(fv[f].end(), bnd[f].begin(), bnd[f].end());
+            int32_t m = 0, s = 0;
+            F.rows_off = (int64_t)S.rows.size();
+            for (size_t i = 0; i < fv[f].size(); i++) {
+                int64_t v = fv[f][i];
+                fvrow[f].push_back(m);
+                for (int k = 0; k < S.vdim[v]; k++) S.rows.push_back((int32_t)(S.voff[v] + k));
+                m += S.vdim[v];
+                if (i < own[f].size()) s += S.vdim[v];
+            }
+            F.m = m; F.s = s;
+            F.arena_off = aoff; aoff += (int64_t)m * m;
+            F.vec_off = voff2; voff2 += m;
+            double sd = s, ud = m - s;
+            S.factor_flops += sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
+            S.nnz_factor += (int64_t)s * (s + 1) / 2 + (int64_t)(m - s) * s;
+        }
+        S.arena_size = aoff;
+        S.vec_size = voff2;
+        auto local_row = [&](int32_t f, int64_t v) -> int32_t {
+            const auto &L = fv[f];
+            int64_t pv = S.elim_pos[v];
+            auto it = std::lower_bound(L.begin(), L.end(), pv, [&](int64_t a, int64_t p) { return S.elim_pos[a] < p; });
+            if (it == L.end() || *it != v) return -1;
+            return fvrow[f][it - L.begin()];
+        };
+        // bmap
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            F.bmap_off = (int64_t)S.bmap.size();
+            if (F.parent < 0) continue;
+            for (int64_t v : bnd[f]) {
+                int32_t lr = local_row(F.parent, v);
+                if (lr < 0) { S.error = "internal: boundary vertex missing in parent front"; return false; }
+                for (int k = 0; k < S.vdim[v]; k++) S.bmap.push_back(lr + k);
+            }
+        }
+        // heights / levels
+        int32_t maxh = 0;
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            int32_t h = 0;
+            for (int c = 0; c < F.nchild; c++) h = std::max(h, S.fronts[F.child[c]].height + 1);
+            F.height = h;
+            maxh = std::max(maxh, h);
+        }
+        S.nlevels = maxh + 1;
+        S.level_fronts.assign(S.nlevels, {});
+        for (int32_t f = 0; f < nf; f++) S.level_fronts[S.fronts[f].height].push_back(f);
+
+        // ---------------- H blocks ----------------
+        // column vertex c, row vertices r with elim[r] >= elim[c], r coupled with c (or r == c)
+        std::vector<int64_t> blk_begin(S.nv + 1, 0);
+        std::vector<int64_t> blk_rowv;
+        for (int64_t c = 0; c < S.nv; c++) {
+            blk_begin[c] = (int64_t)blk_rowv.size();
+            std::vector<int64_t> rs;
+            rs.push_back(c);
+            for (int64_t k = adj_begin[c]; k < adj_begin[c + 1]; k++)
+                if (S.elim_pos[adj[k]] > S.elim_pos[c]) rs.push_back(adj[k]);
+            std::sort(rs.begin(), rs.end());
+            blk_rowv.insert(blk_rowv.end(), rs.begin(), rs.end());
+        }
+        blk_begin[S.nv] = (int64_t)blk_rowv.size();
+        S.nblocks = (int64_t)blk_rowv.size();
+        S.blk_val_off.resize(S.nblocks); S.blk_rows.resize(S.nblocks); S.blk_cols.resize(S.nblocks);
+        S.blk_arena.resize(S.nblocks); S.blk_ld.resize(S.nblocks); S.blk_diag.resize(S.nblocks);
+        int64_t hv = 0;
+        for (int64_t c = 0; c < S.nv; c++) {
+            int32_t f = vfront[c];
+            const Front &F = S.fronts[f];
+            int32_t lc = local_row(f, c);
+            for (int64_t b = blk_begin[c]; b < blk_begin[c + 1]; b++) {
+                int64_t r = blk_rowv[b];
+                int32_t lr = local_row(f, r);
+                if (lr < 0 || lc < 0) { S.error = "internal: block outside its front"; return false; }
+                S.blk_rows[b] = S.vdim[r]; S.blk_cols[b] = S.vdim[c];
+                S.blk_val_off[b] = hv; hv += (int64_t)S.vdim[r] * S.vdim[c];
+                S.blk_arena[b] = F.arena_off + (int64_t)lc * F.m + lr;
+                S.blk_ld[b] = F.m;
+                S.blk_diag[b] = (r == c) ? 1 : 0;
+            }
+        }
+        S.hval_size = hv;
+        auto block_id = [&](int64_t c, int64_t r) -> int64_t {
+            auto b0 = blk_rowv.begin() + blk_begin[c], b1 = blk_rowv.begin() + blk_begin[c + 1];
+            auto it = std::lower_bound(b0, b1, r);
+            if (it == b1 || *it != r) return -1;
+            return it - blk_rowv.begin();
+        };
+        // contributions
+        std::vector<std::pair<int64_t, uint64_t>> hc;      // (block, record)
+        std::vector<std::pair<int64_t, uint64_t>> bc;      // (vertex, record)
+        hc.reserve((size_t)d.n_rep + 3 * (size_t)d.n_depth + 15 * (size_t)d.n_arap);
+        bc.reserve((size_t)d.n_rep + 2 * (size_t)d.n_depth + 5 * (size_t)d.n_arap);
+        auto add_edge = [&](int kind, int64_t e, const int64_t *v, int nr) {
+            for (int a = 0; a < nr; a++) {
+                bc.emplace_back(v[a], contrib_pack(kind, e, a, a));
+                for (int b = 0; b < nr; b++) {
+                    int64_t c = v[a], r = v[b];
+                    if (S.elim_pos[r] < S.elim_pos[c]) continue;
+                    if (S.elim_pos[r] == S.elim_pos[c] && r != c) continue;
+                    int64_t bid = block_id(c, r);
+                    if (bid < 0) { S.error = "internal: missing block"; return false; }
+                    hc.emplace_back(bid, contrib_pack(kind, e, a, b));
+                }
+            }
+            return true;
+        };
+        for (int e = 0; e < d.n_rep; e++) {
+            int64_t v[1] = {vP(d.rep_point[e])};
+            if (!add_edge(EK_REP, e, v, 1)) return false;
+        }
+        for (int e = 0; e < d.n_depth; e++) {
+            int64_t v[2] = {vP(d.dep_point[e]), vS(d.dep_scale[e])};
+            if (!add_edge(EK_DEP, e, v, 2)) return false;
+        }
+        for (int e = 0; e < d.n_arap; e++) {
+            int64_t v[5];
+            for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
+            v[4] = vT(d.arap_pair[e]);
+            if (!add_edge(EK_ARAP, e, v, 5)) return false;
+        }
+        auto chunkify = [&](std::vector<std::pair<int64_t, uint64_t>> &lst, int64_t nkeys,
+                            std::vector<uint64_t> &recs, std::vector<int64_t> &cbeg,
+                            std::vector<int32_t> &clen, std::vector<int32_t> &ckey,
+                            std::vector<int64_t> &key_chunk) {
+            std::stable_sort(lst.begin(), lst.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+            recs.resize(lst.size());
+            for (size_t i = 0; i < lst.size(); i++) recs[i] = lst[i].second;
+            key_chunk.assign(nkeys + 1, 0);
+            size_t i = 0;
+            for (int64_t k = 0; k < nkeys; k++) {
+                key_chunk[k] = (int64_t)cbeg.size();
+                size_t j = i;
+                while (j < lst.size() && lst[j].first == k) j++;
+                for (size_t s0 = i; s0 < j; s0 += kChunk) {
+                    cbeg.push_back((int64_t)s0);
+                    clen.push_back((int32_t)std::min<size_t>(kChunk, j - s0));
+                    ckey.push_back((int32_t)k);
+                }
+                i = j;
+            }
+            key_chunk[nkeys] = (int64_t)cbeg.size();
+        };
+        chunkify(hc, S.nblocks, S.hcontrib, S.hchunk_begin, S.hchunk_len, S.hchunk_block, S.hblk_chunk_begin);
+        chunkify(bc, S.nv, S.bcontrib, S.bchunk_begin, S.bchunk_len, S.bchunk_vertex, S.bv_chunk_begin);
+
+        // ---------------- task lists ----------------
+        auto push3 = [&](int32_t a, int32_t b, int32_t c) {
+            S.task_i32.push_back(a); S.task_i32.push_back(b); S.task_i32.push_back(c);
+        };
+        S.levels.assign(S.nlevels, {});
+        for (int32_t h = 0; h < S.nlevels; h++) {
+            auto &LT = S.levels[h];
+            const auto &fs = S.level_fronts[h];
+            for (int slot = 0; slot < 2; slot++) {
+                LT.ea_off[slot] = (int64_t)S.task_i32.size() / 3;
+                int32_t cnt = 0;
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.nchild <= slot) continue;
+                    int32_t c = F.child[slot];
+                    int32_t u = S.fronts[c].m - S.fronts[c].s;
+                    for (int32_t j = 0; j < u; j += 16) { push3(c, j, 0); cnt++; }
+                }
+                LT.nea[slot] = cnt;
+            }
+            int32_t maxs = 0;
+            for (int32_t f : fs) maxs = std::max(maxs, S.fronts[f].s);
+            for (int32_t k0 = 0; k0 < maxs; k0 += kPanel) {
+                Symbolic::StepTasks st;
+                st.k0 = k0;
+                st.diag_off = (int64_t)S.task_i32.size() / 3;
+                for (int32_t f : fs) if (S.fronts[f].s > k0) { push3(f, k0, 0); st.ndiag++; }
+                st.trsm_off = (int64_t)S.task_i32.size() / 3;
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.s <= k0) continue;
+                    int32_t kb = std::min(kPanel, F.s - k0);
+                    for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) { push3(f, k0, r0); st.ntrsm++; }
+                }
+                st.upd_off = (int64_t)S.task_i32.size() / 3;
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.s <= k0) continue;
+                    int32_t kb = std::min(kPanel, F.s - k0);
+                    int32_t t0 = k0 + kb;
+                    for (int32_t ti = t0; ti < F.m; ti += 64)
+                        for (int32_t tj = t0; tj <= ti; tj += 64) {
+                            push3(f, ti, tj);      // k0 recovered from step (same for all tasks)
+                            st.nupd++;
+                        }
+                }
+                LT.steps.push_back(st);
+            }
+            LT.fwd_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t f : fs) { push3(f, 0, 0); LT.nfwd++; }
+            LT.gemv_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t f : fs) {
+                const Front &F = S.fronts[f];
+                if (F.s == 0) continue;
+                for (int32_t r0 = F.s; r0 < F.m; r0 += 64) { push3(f, r0, 0); LT.ngemv++; }
+            }
+            LT.bgemv_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t f : fs) {
+                const Front &F = S.fronts[f];
+                for (int32_t c0 = 0; c0 < F.s; c0 += 64) { push3(f, c0, 0); LT.nbgemv++; }
+            }
+        }
+        return true;
+    }
+};
+
+}  // namespace
+
+bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points) {
+    S = Symbolic();
+    Builder b(d, S, leaf_points);
+    return b.run();
+}
+
+}  // namespace deftri

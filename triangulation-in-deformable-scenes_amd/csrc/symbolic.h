@@ -1,0 +1,106 @@
+// symbolic.h — host-side analysis of the LM normal equations for the device LDL^T.
+//
+// Replaces g2o's BlockSolverX + LinearSolverEigen structure analysis
+// (reference g2oBundleAdjustment.cc:619-628 builds the solver; the LM calls buildStructure()
+// on iteration 0).  Instead of Eigen's AMD + SimplicialLDLT we build a multifrontal plan:
+//   * fill-reducing order: geometric nested dissection of the point vertices on their mesh-plane
+//     coordinates (the same 2-D plane the reference triangulates, Geometry.cc:317-368), global
+//     vertices (T_g, depth scales) last;
+//   * one dense front per dissection node (leaf subdomain or separator), column-major fp64 in one
+//     HBM arena; boundary rows = later-eliminated coupled vertices;
+//   * assembly lists: every entry of H (vertex-pair blocks) and of b is produced by a fixed-order
+//     gather over per-edge contributions (deterministic, no atomics);
+//   * per-level task lists for the batched dense kernels (diag LDL^T, TRSM, trailing update,
+//     extend-add, forward/backward substitution).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/deftri.h"
+
+namespace deftri {
+
+// edge kinds in contribution records
+enum : int { EK_REP = 0, EK_DEP = 1, EK_ARAP = 2 };
+
+// contribution record: (edge kind, edge index, role of the column vertex, role of the row vertex)
+static inline uint64_t contrib_pack(int kind, int64_t edge, int role_col, int role_row) {
+    return (uint64_t)edge | ((uint64_t)kind << 40) | ((uint64_t)role_col << 44) | ((uint64_t)role_row << 48);
+}
+
+constexpr int kPanel = 64;          // panel width of the blocked dense kernels
+constexpr int kChunk = 128;         // contributions per gather chunk
+
+struct Front {
+    int64_t arena_off;   // m*m doubles, column-major, ld = m
+    int64_t vec_off;     // m doubles of solve workspace
+    int64_t rows_off;    // m entries of `rows` (problem dof of each local row)
+    int64_t bmap_off;    // (m - s) entries of `bmap` (local row in the parent front)
+    int32_t m, s;
+    int32_t parent;
+    int32_t height;
+    int32_t nchild;
+    int32_t child[2];
+};
+
+struct Symbolic {
+    // vertices in problem order: [T_g per pair][scales][points]
+    int64_t nv = 0, ndof = 0;
+    std::vector<int32_t> vdim;
+    std::vector<int64_t> voff;
+    std::vector<int64_t> elim_pos;      // vertex -> elimination position
+    // fronts
+    std::vector<Front> fronts;
+    std::vector<int32_t> rows;
+    std::vector<int32_t> bmap;
+    int64_t arena_size = 0, vec_size = 0;
+    int32_t nlevels = 0;
+    std::vector<std::vector<int32_t>> level_fronts;   // by height, ascending
+    double factor_flops = 0;
+    int64_t nnz_factor = 0;
+
+    // H blocks: column vertex c (eliminated no later than the row vertex r)
+    int64_t nblocks = 0, hval_size = 0;
+    std::vector<int64_t> blk_val_off;    // offset into Hval (rows x cols, row-major)
+    std::vector<int32_t> blk_rows, blk_cols;
+    std::vector<int64_t> blk_arena;      // arena index of entry (0,0)
+    std::vector<int32_t> blk_ld;
+    std::vector<int32_t> blk_diag;       // 1 if diagonal block (row vertex == column vertex)
+    // contributions to H blocks, chunked
+    std::vector<uint64_t> hcontrib;
+    std::vector<int64_t> hchunk_begin;   // per chunk: first contribution
+    std::vector<int32_t> hchunk_len;
+    std::vector<int32_t> hchunk_block;
+    std::vector<int64_t> hblk_chunk_begin; // per block: first chunk (CSR, nblocks+1)
+    // contributions to b (per vertex), chunked the same way; role_row unused
+    std::vector<uint64_t> bcontrib;
+    std::vector<int64_t> bchunk_begin;
+    std::vector<int32_t> bchunk_len;
+    std::vector<int32_t> bchunk_vertex;
+    std::vector<int64_t> bv_chunk_begin;   // per vertex (nv+1)
+
+    // per-level task lists (device copies are flat arrays with offsets)
+    struct StepTasks {
+        int64_t diag_off = 0; int32_t ndiag = 0;      // fronts with own cols at this panel
+        int64_t trsm_off = 0; int32_t ntrsm = 0;      // (front, row-tile) pairs
+        int64_t upd_off = 0; int32_t nupd = 0;        // (front, tile-i, tile-j) triples
+        int32_t k0 = 0;
+    };
+    struct LevelTasks {
+        int64_t ea_off[2] = {0, 0}; int32_t nea[2] = {0, 0};   // extend-add (child slot 0/1): (parent, child col)
+        std::vector<StepTasks> steps;
+        int64_t fwd_off = 0; int32_t nfwd = 0;                 // fronts
+        int64_t gemv_off = 0; int32_t ngemv = 0;               // (front, row-tile) for boundary update
+        int64_t bgemv_off = 0; int32_t nbgemv = 0;             // (front, col-tile) for backward L21^T x
+    };
+    std::vector<LevelTasks> levels;
+    std::vector<int32_t> task_i32;     // flat task storage (3 ints per task record)
+
+    std::string error;
+};
+
+// Build the full plan for a validated problem.  Returns false (and sets error) on failure.
+bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points = 16);
+
+}  // namespace deftri

@@ -1,0 +1,87 @@
+"""ctypes mirror of include/deftri.h (the C-ABI boundary).
+
+Kept field-for-field identical to the header; tests/test_abi.py checks the struct sizes
+against the compiled library (deftri_sizeof_* exports).
+"""
+import ctypes as C
+
+i32, i64, f32, f64 = C.c_int32, C.c_int64, C.c_float, C.c_double
+P = C.POINTER
+
+DEFTRI_OK = 0
+DEFTRI_E_ARG = -1
+DEFTRI_E_HIP = -2
+DEFTRI_E_NOPROBLEM = -3
+DEFTRI_E_NUMERIC = -4
+DEFTRI_E_NODEVICE = -5
+DEFTRI_E_GRAPH = -6
+DEFTRI_STATUS_OK = 0
+DEFTRI_STATUS_TERMINATE = 1
+DEFTRI_MAX_REPORT_ITERS = 1024
+
+
+class ProblemDesc(C.Structure):
+    _fields_ = [
+        ("n_points", i32), ("n_pairs", i32), ("n_scales", i32), ("n_cams", i32),
+        ("n_rep", i32), ("n_depth", i32), ("n_arap", i32), ("n_rot", i32),
+        ("points", P(f64)), ("tg", P(f64)), ("scales", P(f64)),
+        ("cam_kb8", P(f32)), ("cam_pose", P(f64)),
+        ("rep_point", P(i32)), ("rep_cam", P(i32)), ("rep_obs", P(f64)), ("rep_info", P(f64)),
+        ("huber_delta", f64),
+        ("dep_point", P(i32)), ("dep_scale", P(i32)), ("dep_cam", P(i32)),
+        ("dep_meas", P(f64)), ("dep_info", P(f64)),
+        ("arap_pts", P(i32)), ("arap_pair", P(i32)), ("arap_rot", P(i32)), ("arap_w", P(f64)),
+        ("rot", P(f64)), ("pair_area", P(f64)), ("pair_info", P(f64)),
+        ("order_xy", P(f64)),
+    ]
+
+
+class LMParams(C.Structure):
+    _fields_ = [("n_iterations", i32), ("max_trials", i32), ("tau", f64), ("user_lambda", f64),
+                ("analytic_jacobians", i32), ("verbose", i32)]
+
+
+class Report(C.Structure):
+    _fields_ = [
+        ("status", i32), ("iterations", i32), ("trials_total", i32), ("trials_rejected", i32),
+        ("chi2_initial", f64), ("chi2_final", f64), ("lambda_final", f64),
+        ("chi2_iter", f64 * DEFTRI_MAX_REPORT_ITERS), ("trials_iter", i32 * DEFTRI_MAX_REPORT_ITERS),
+        ("ms_total", f64), ("ms_linearize", f64), ("ms_factor", f64), ("ms_solve", f64),
+        ("ms_update", f64),
+        ("n_unknowns", i64), ("nnz_factor", i64), ("factor_flops", f64), ("n_fronts", i32),
+        ("n_levels", i32),
+    ]
+
+    def as_dict(self):
+        it = min(self.iterations, DEFTRI_MAX_REPORT_ITERS)
+        return {
+            "status": self.status, "iterations": self.iterations,
+            "trials_total": self.trials_total, "trials_rejected": self.trials_rejected,
+            "chi2_initial": self.chi2_initial, "chi2_final": self.chi2_final,
+            "lambda_final": self.lambda_final,
+            "chi2_iter": list(self.chi2_iter[:it]), "trials_iter": list(self.trials_iter[:it]),
+            "ms_total": self.ms_total, "ms_linearize": self.ms_linearize,
+            "ms_factor": self.ms_factor, "ms_solve": self.ms_solve, "ms_update": self.ms_update,
+            "n_unknowns": self.n_unknowns, "nnz_factor": self.nnz_factor,
+            "factor_flops": self.factor_flops, "n_fronts": self.n_fronts, "n_levels": self.n_levels,
+        }
+
+
+class KeyFrameC(C.Structure):
+    _fields_ = [
+        ("id", i64), ("pose", f64 * 7), ("kb8", f32 * 8), ("n_scales", i32),
+        ("inv_sigma2", P(f32)), ("depth_scale", f64), ("n_slots", i32),
+        ("point_id", P(i64)), ("point_pos", P(f32)), ("obs_index", P(i32)),
+        ("kp_uv", P(f32)), ("kp_octave", P(i32)), ("depth", P(f32)), ("n_obs", i32),
+    ]
+
+
+class MapC(C.Structure):
+    _fields_ = [("n_keyframes", i32), ("keyframes", P(KeyFrameC)), ("global_t", f64 * 7)]
+
+
+def ptr(a, ctype):
+    """Pointer into a contiguous numpy array (None for None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(P(ctype))

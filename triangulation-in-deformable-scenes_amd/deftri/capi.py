@@ -1,0 +1,191 @@
+"""ctypes binding of libdeftri.so (include/deftri.h).
+
+The library is built in-tree (csrc/Makefile -> triangulation-in-deformable-scenes_amd/libdeftri.so).
+There is no CPU fallback: if the library is missing, `load()` raises, and every solve entry
+point runs on the GPU or returns an error.
+"""
+import ctypes as C
+import pathlib
+
+import numpy as np
+
+from . import _abi
+from .problem import Problem
+
+PKG_ROOT = pathlib.Path(__file__).resolve().parent.parent
+LIB_PATH = PKG_ROOT / "libdeftri.so"
+_lib = None
+
+
+class DeftriError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"deftri error {code}: {msg}")
+        self.code = code
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built — run __graft_entry__.build() (make -C csrc)")
+    lib = C.CDLL(str(LIB_PATH))
+    P = C.POINTER
+    sig = {
+        "deftri_abi_version": (C.c_int, []),
+        "deftri_ctx_create": (C.c_int, [C.c_int32, P(C.c_void_p)]),
+        "deftri_ctx_destroy": (C.c_int, [C.c_void_p]),
+        "deftri_last_error": (C.c_char_p, [C.c_void_p]),
+        "deftri_problem_upload": (C.c_int, [C.c_void_p, P(_abi.ProblemDesc)]),
+        "deftri_problem_analyse": (C.c_int, [C.c_void_p, P(_abi.ProblemDesc)]),
+        "deftri_plan_stats": (C.c_int, [C.c_void_p, P(_abi.Report)]),
+        "deftri_debug_plan_solve": (C.c_int, [C.c_void_p, P(C.c_double), C.c_double, P(C.c_double),
+                                              P(C.c_double), C.c_int64]),
+        "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
+        "deftri_download": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double)]),
+        "deftri_reset_state": (C.c_int, [C.c_void_p]),
+        "deftri_eval_chi2": (C.c_int, [C.c_void_p, P(C.c_double)]),
+        "deftri_eval_gradient": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), C.c_int64]),
+        "deftri_eval_hessian_product": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), C.c_int64]),
+        "deftri_eval_damped_solve": (C.c_int, [C.c_void_p, C.c_double, P(C.c_double), P(C.c_double), C.c_int64]),
+        "deftri_num_unknowns": (C.c_int64, [C.c_void_p]),
+        "deftri_sizeof": (C.c_int64, [C.c_int32]),
+        "deftri_arap_build_graph": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_float,
+                                              P(P(_abi.ProblemDesc))]),
+        "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
+                                               C.c_double, C.c_double, C.c_float, C.c_int32, P(C.c_double),
+                                               P(_abi.Report)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+EXPORTED = [
+    "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
+    "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
+    "deftri_solve_lm", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
+    "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
+]
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Context:
+    """One solver context (one per host thread).  device < 0 = host-only (graph / analysis)."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.deftri_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise DeftriError(rc, "deftri_ctx_create failed (no usable gfx950 device?)" if device >= 0 else "ctx")
+        self.h = h
+        self.device = device
+        self._desc = None
+        self._prob = None
+
+    def close(self):
+        if self.h:
+            self.lib.deftri_ctx_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise DeftriError(rc, (self.lib.deftri_last_error(self.h) or b"").decode())
+
+    # flat-graph API ------------------------------------------------------------------------
+    def upload(self, prob: Problem):
+        self._prob = prob
+        self._desc = prob.to_desc()
+        self._check(self.lib.deftri_problem_upload(self.h, C.byref(self._desc)))
+
+    def analyse(self, prob: Problem):
+        self._prob = prob
+        self._desc = prob.to_desc()
+        self._check(self.lib.deftri_problem_analyse(self.h, C.byref(self._desc)))
+
+    def plan_stats(self):
+        r = _abi.Report()
+        self._check(self.lib.deftri_plan_stats(self.h, C.byref(r)))
+        return {k: v for k, v in r.as_dict().items() if k in ("n_unknowns", "nnz_factor", "factor_flops", "n_fronts", "n_levels")}
+
+    def debug_plan_solve(self, H, lam, rhs):
+        H = np.ascontiguousarray(H, dtype=np.float64)
+        r = np.ascontiguousarray(rhs, dtype=np.float64)
+        x = np.zeros_like(r)
+        self._check(self.lib.deftri_debug_plan_solve(self.h, _dp(H), float(lam), _dp(r), _dp(x), len(r)))
+        return x
+
+    def solve_lm(self, n_iterations=10, analytic=True, tau=1e-5, max_trials=10, user_lambda=0.0, verbose=False):
+        prm = _abi.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=user_lambda,
+                            analytic_jacobians=1 if analytic else 0, verbose=1 if verbose else 0)
+        rep = _abi.Report()
+        self._check(self.lib.deftri_solve_lm(self.h, C.byref(prm), C.byref(rep)))
+        return rep.as_dict()
+
+    def download(self):
+        p = self._prob
+        pts = np.zeros((p.n_points, 3)); sc = np.zeros(p.n_scales); tg = np.zeros((p.n_pairs, 7))
+        self._check(self.lib.deftri_download(self.h, _dp(pts), _dp(sc), _dp(tg)))
+        return pts, sc, tg
+
+    def reset_state(self):
+        self._check(self.lib.deftri_reset_state(self.h))
+
+    def chi2(self):
+        v = C.c_double()
+        self._check(self.lib.deftri_eval_chi2(self.h, C.byref(v)))
+        return v.value
+
+    def gradient(self):
+        n = self._prob.n_unknowns
+        b = np.zeros(n); d = np.zeros(n)
+        self._check(self.lib.deftri_eval_gradient(self.h, _dp(b), _dp(d), n))
+        return b, d
+
+    def hessian_product(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.zeros_like(x)
+        self._check(self.lib.deftri_eval_hessian_product(self.h, _dp(x), _dp(y), len(x)))
+        return y
+
+    def damped_solve(self, lam, rhs):
+        r = np.ascontiguousarray(rhs, dtype=np.float64)
+        x = np.zeros_like(r)
+        self._check(self.lib.deftri_eval_damped_solve(self.h, float(lam), _dp(r), _dp(x), len(r)))
+        return x
+
+    # map-level API -------------------------------------------------------------------------
+    def build_graph(self, m, rep_weight, arap_weight, depth_error):
+        mc, keep = m.to_c()
+        out = C.POINTER(_abi.ProblemDesc)()
+        self._check(self.lib.deftri_arap_build_graph(self.h, C.byref(mc), float(rep_weight), float(arap_weight),
+                                                     C.c_float(depth_error), C.byref(out)))
+        return Problem.from_desc(out.contents)
+
+    def arap_optimization(self, m, rep_weight, global_weight, arap_weight, alpha, beta, depth_error,
+                          n_iterations, want_update=True):
+        mc, keep = m.to_c()
+        upd = C.c_double(0.0)
+        rep = _abi.Report()
+        self._check(self.lib.deftri_arap_optimization(
+            self.h, C.byref(mc), float(rep_weight), float(global_weight), float(arap_weight), float(alpha),
+            float(beta), C.c_float(depth_error), int(n_iterations), C.byref(upd) if want_update else None,
+            C.byref(rep)))
+        m.from_c(mc, keep)
+        return upd.value, rep.as_dict()

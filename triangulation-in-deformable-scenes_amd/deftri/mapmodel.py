@@ -1,0 +1,206 @@
+"""Minimal mirror of the reference's Map / KeyFrame / MapPoint (Modules/Map/*) — only what the
+solver reads and writes (SURVEY §8b "Ownership"):
+
+  MapPoint  : id, fp32 world position            (MapPoint.cc:22-49)
+  KeyFrame  : id, pose T_cw (SE3f), KB8 calibration, keypoints + octaves, per-index simulated
+              depth, invSigma2 table, estimatedDepthScale_, MapPoint slots (KeyFrame.cc:93-210)
+  Map       : keyframes (unordered_map<ID,KF>), map points, observations
+              (Map::addObservation / isMapPointInKeyFrame, Map.cc:100-132, 257-264),
+              global KF-pair transformations (Map.cc:323-330)
+
+Iteration order of the reference's `std::unordered_map<ID, KeyFrame_>` (libstdc++, integer
+hash): nodes whose buckets are distinct are iterated in reverse insertion order, which is what
+makes pKF1 = KF 0 and pKF2 = KF 1 for the two-view case.  `Map.kf_order()`
+returns that order and is what the C-ABI receives.
+"""
+import ctypes as C
+import numpy as np
+
+from . import _abi
+
+
+def quat_from_mat(R):
+    """Eigen Quaternion(Matrix3) (quaternionbase_assign_impl) — returns x, y, z, w (f64)."""
+    m = np.asarray(R, dtype=np.float64)
+    t = m[0, 0] + m[1, 1] + m[2, 2]
+    if t > 0:
+        t = np.sqrt(t + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        return np.array([(m[2, 1] - m[1, 2]) * t, (m[0, 2] - m[2, 0]) * t, (m[1, 0] - m[0, 1]) * t, w])
+    i = 0
+    if m[1, 1] > m[0, 0]:
+        i = 1
+    if m[2, 2] > m[i, i]:
+        i = 2
+    j, k = (i + 1) % 3, (i + 2) % 3
+    c = np.zeros(3)
+    t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+    c[i] = 0.5 * t
+    t = 0.5 / t
+    w = (m[k, j] - m[j, k]) * t
+    c[j] = (m[j, i] + m[i, j]) * t
+    c[k] = (m[k, i] + m[i, k]) * t
+    return np.array([c[0], c[1], c[2], w])
+
+
+def mat_from_quat(q):
+    x, y, z, w = q
+    tx, ty, tz = 2 * x, 2 * y, 2 * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    return np.array([[1 - (tyy + tzz), txy - twz, txz + twy],
+                     [txy + twz, 1 - (txx + tzz), tyz - twx],
+                     [txz - twy, tyz + twx, 1 - (txx + tyy)]])
+
+
+class SE3f:
+    """Sophus::SE3f stand-in: rotation (fp32 3x3) + translation (fp32)."""
+    def __init__(self, R=None, t=None):
+        self.R = np.eye(3, dtype=np.float32) if R is None else np.asarray(R, dtype=np.float32)
+        self.t = np.zeros(3, dtype=np.float32) if t is None else np.asarray(t, dtype=np.float32)
+
+    def __mul__(self, o):
+        if isinstance(o, SE3f):
+            return SE3f(self.R @ o.R, self.R @ o.t + self.t)
+        return (np.asarray(o, dtype=np.float32) @ self.R.T + self.t).astype(np.float32)
+
+    def inverse(self):
+        return SE3f(self.R.T, -(self.R.T @ self.t))
+
+    def unit_quaternion(self):
+        q = quat_from_mat(self.R.astype(np.float64))
+        return q / np.linalg.norm(q)
+
+    def as7(self):
+        """g2o::SE3Quat(unit_quaternion().cast<double>(), translation().cast<double>())."""
+        q = self.unit_quaternion().astype(np.float32).astype(np.float64)
+        if q[3] < 0:
+            q = -q
+        q = q / np.linalg.norm(q)
+        return np.concatenate([q, self.t.astype(np.float64)])
+
+    @staticmethod
+    def from7(a):
+        a = np.asarray(a, dtype=np.float64)
+        q = a[:4] / np.linalg.norm(a[:4])
+        return SE3f(mat_from_quat(q).astype(np.float32), a[4:7].astype(np.float32))
+
+
+class MapPoint:
+    _next_id = 0
+
+    def __init__(self, position, pid=None):
+        self.position = np.asarray(position, dtype=np.float32).copy()
+        if pid is None:
+            pid = MapPoint._next_id
+            MapPoint._next_id += 1
+        self.id = int(pid)
+
+
+class KeyFrame:
+    def __init__(self, kid, pose, kb8, n_slots, inv_sigma2, keypoints=None, octaves=None, depth=None):
+        self.id = int(kid)
+        self.pose = pose                              # SE3f, T_cw
+        self.kb8 = np.asarray(kb8, dtype=np.float32)
+        self.inv_sigma2 = np.asarray(inv_sigma2, dtype=np.float32)
+        self.keypoints = np.zeros((n_slots, 2), np.float32) if keypoints is None else np.asarray(keypoints, np.float32)
+        self.octaves = np.zeros(n_slots, np.int32) if octaves is None else np.asarray(octaves, np.int32)
+        self.depth = np.zeros(n_slots, np.float32) if depth is None else np.asarray(depth, np.float32)
+        self.map_points = [None] * n_slots
+        self.estimated_depth_scale = 1.0               # KeyFrame.h:198 default
+
+    @property
+    def n_slots(self):
+        return len(self.map_points)
+
+
+class Map:
+    def __init__(self):
+        self.keyframes = {}           # insertion-ordered
+        self.map_points = {}
+        self.kf_obs = {}              # kf id -> {mp id -> idx}
+        self.global_T = {}            # (kf1, kf2) -> SE3f
+
+    def insert_keyframe(self, kf):
+        self.keyframes[kf.id] = kf
+        self.kf_obs.setdefault(kf.id, {})
+
+    def insert_map_point(self, mp):
+        self.map_points[mp.id] = mp
+
+    def add_observation(self, kf_id, mp_id, idx):
+        assert mp_id not in self.kf_obs[kf_id]
+        self.kf_obs[kf_id][mp_id] = int(idx)
+
+    def is_map_point_in_keyframe(self, mp_id, kf_id):
+        return self.kf_obs.get(kf_id, {}).get(mp_id, -1)
+
+    def kf_order(self):
+        """libstdc++ unordered_map<ID,KF> iteration order (reverse insertion, see module doc)."""
+        return list(reversed(list(self.keyframes.keys())))
+
+    def insert_global_T(self, kf1, kf2, T):
+        self.global_T[(kf1, kf2)] = T
+        self.global_T[(kf2, kf1)] = T.inverse()
+
+    def get_global_T(self, kf1, kf2):
+        return self.global_T.get((kf1, kf2), SE3f())
+
+    # ---- C-ABI view -------------------------------------------------------------------------
+    def to_c(self):
+        """Build a deftri_map view.  Returns (MapC, keep) — keep owns the arrays; positions and
+        depth scales are written back through `from_c`."""
+        order = self.kf_order()
+        kfs = (_abi.KeyFrameC * len(order))()
+        keep = {"kfs": kfs, "arrays": []}
+        for n, kid in enumerate(order):
+            kf = self.keyframes[kid]
+            c = kfs[n]
+            c.id = kf.id
+            c.pose[:] = list(kf.pose.as7())
+            c.kb8[:] = [float(v) for v in kf.kb8]
+            c.n_scales = len(kf.inv_sigma2)
+            inv = np.ascontiguousarray(kf.inv_sigma2, np.float32)
+            c.inv_sigma2 = _abi.ptr(inv, _abi.f32)
+            c.depth_scale = kf.estimated_depth_scale
+            ns = kf.n_slots
+            c.n_slots = ns
+            pid = np.array([mp.id if mp is not None else -1 for mp in kf.map_points], np.int64)
+            pos = np.zeros((ns, 3), np.float32)
+            obs = np.full(ns, -1, np.int32)
+            for i, mp in enumerate(kf.map_points):
+                if mp is not None:
+                    pos[i] = mp.position
+                    obs[i] = self.is_map_point_in_keyframe(mp.id, kf.id)
+            uv = np.ascontiguousarray(kf.keypoints, np.float32)
+            octv = np.ascontiguousarray(kf.octaves, np.int32)
+            dep = np.ascontiguousarray(kf.depth, np.float32)
+            c.point_id, c.point_pos, c.obs_index = _abi.ptr(pid, _abi.i64), _abi.ptr(pos, _abi.f32), _abi.ptr(obs, _abi.i32)
+            c.kp_uv, c.kp_octave, c.depth = _abi.ptr(uv, _abi.f32), _abi.ptr(octv, _abi.i32), _abi.ptr(dep, _abi.f32)
+            c.n_obs = len(kf.keypoints)
+            keep["arrays"].append((kid, pid, pos, obs, uv, octv, dep, inv))
+        m = _abi.MapC()
+        m.n_keyframes = len(order)
+        m.keyframes = C.cast(kfs, C.POINTER(_abi.KeyFrameC))
+        if len(order) >= 2:
+            # read-back key of g2oBundleAdjustment.cc:664: (k2->first, k1->first) of the first pair
+            T = self.get_global_T(order[1], order[0])
+            m.global_t[:] = list(T.as7())
+        else:
+            m.global_t[:] = [0, 0, 0, 1, 0, 0, 0]
+        return m, keep
+
+    def from_c(self, m, keep):
+        """Write back positions (fp32), depth scales and the global T (reference :967-1007)."""
+        for n, (kid, pid, pos, *_rest) in enumerate(keep["arrays"]):
+            kf = self.keyframes[kid]
+            kf.estimated_depth_scale = float(m.keyframes[n].depth_scale)
+            for i, mp in enumerate(kf.map_points):
+                if mp is not None:
+                    mp.position = pos[i].copy()
+        if m.n_keyframes >= 2:
+            ids = sorted(self.keyframes.keys())
+            # reference hard-codes insertGlobalKeyFramesTransformation(0, 1, T) (:1007)
+            self.insert_global_T(ids[0], ids[1], SE3f.from7(np.array(m.global_t[:])))
