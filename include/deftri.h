@@ -181,6 +181,19 @@ int deftri_plan_stats(const deftri_ctx *ctx, deftri_report *report);
    any solve path. */
 int deftri_debug_plan_solve(deftri_ctx *ctx, const double *H, double lambda, const double *rhs,
                             double *x, int64_t n);
+/* Per-kernel device timing of one LM trial (linearize + assemble + setLambda + LDL^T + solve),
+   each launch bracketed by HIP events on the solver's stream.  flops are algorithmic counts
+   for the dense factor kernels (0 where not defined). */
+typedef struct deftri_kernel_stat {
+    char    name[32];
+    int64_t launches;
+    double  ms;          /* summed device time */
+    double  flops;       /* algorithmic flops of all launches */
+    double  bytes;       /* algorithmic HBM bytes of all launches (0 where not defined) */
+} deftri_kernel_stat;
+int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *stats,
+                         int32_t max_stats, int32_t *n_stats);
+
 /* sizeof() of the ABI structs (deftri_problem_desc, deftri_lm_params, deftri_report,
    deftri_keyframe, deftri_map) for binding checks. */
 int64_t deftri_sizeof(int32_t which);

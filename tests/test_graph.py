@@ -1,0 +1,112 @@
+"""Graph construction parity: the product's C++ builder (csrc/graph_builder.cpp, reached through
+deftri_arap_build_graph) against the oracle restatement (oracle/graph_ref.py, scipy qhull) of the
+reference's arapOptimization graph build (g2oBundleAdjustment.cc:640-953).
+Index arrays must be bit-exact; floats within rounding (summation order differs)."""
+import json
+
+import numpy as np
+import pytest
+from scipy.spatial import ConvexHull, Delaunay
+
+from conftest import GOLDEN
+from deftri import capi, sim
+from deftri.problem import Problem
+from oracle import graph_ref
+
+INT_FIELDS = ["rep_point", "rep_cam", "dep_point", "dep_scale", "dep_cam", "arap_pts", "arap_pair", "arap_rot"]
+F_FIELDS = ["points", "scales", "tg", "rep_obs", "rep_info", "dep_meas", "dep_info", "arap_w", "rot", "pair_area",
+            "pair_info", "cam_pose"]
+
+
+def compare(pr, pc, rtol=1e-12):
+    for k in INT_FIELDS:
+        a, b = getattr(pr, k), getattr(pc, k)
+        assert a.shape == b.shape, k
+        assert np.array_equal(a, b), k
+    for k in F_FIELDS:
+        a, b = getattr(pr, k), getattr(pc, k)
+        assert a.shape == b.shape, k
+        if a.size:
+            assert np.abs(a - b).max() <= rtol * max(1.0, np.abs(a).max()), k
+    assert np.array_equal(pr.cam_kb8, pc.cam_kb8)
+    assert pr.huber_delta == pc.huber_delta
+
+
+@pytest.fixture(scope="module")
+def host():
+    return capi.Context(-1)
+
+
+def test_golden_graphs_reproduced(host, golden_cases):
+    import importlib, sys
+    sys.path.insert(0, str(GOLDEN))
+    mg = importlib.import_module("make_golden")
+    for name in golden_cases:
+        m, st, sigma = mg.scene(name)
+        pg = Problem.load(GOLDEN / name / "problem.npz")
+        pc = host.build_graph(m, st.rep, st.arap, sigma)
+        compare(pg, pc)
+        kw, info = graph_ref.build_arap_graph(m, st.rep, st.arap, sigma)
+        compare(Problem(**kw), pg, rtol=0)                  # oracle is deterministic
+
+
+@pytest.mark.parametrize("n,seed", [(300, 3), (1500, 4)])
+def test_builder_matches_oracle_sim(host, n, seed):
+    m, _ = sim.simulate_two_view(n=n, seed=seed)
+    kw, info = graph_ref.build_arap_graph(m, 1.0, 2e5, np.float32(0.003))
+    compare(Problem(**kw), host.build_graph(m, 1.0, 2e5, np.float32(0.003)))
+
+
+def test_null_slot_quirk(host):
+    """Null slots: the reference uses the KF slot index as a position index and the position
+    index as a slot index.  Both builders must reproduce that."""
+    m, _ = sim.simulate_two_view(n=200, seed=5)
+    kf0, kf1 = m.keyframes[0], m.keyframes[1]
+    for s in (3, 40, 41, 150):                  # drop correspondences -> null slots in both KFs
+        for kf in (kf0, kf1):
+            mp = kf.map_points[s]
+            kf.map_points[s] = None
+            m.kf_obs[kf.id].pop(mp.id, None)
+    kw, info = graph_ref.build_arap_graph(m, 1.0, 2e5, np.float32(0.003))
+    pr = Problem(**kw)
+    compare(pr, host.build_graph(m, 1.0, 2e5, np.float32(0.003)))
+    # the quirk really changes the graph: some ARAP edges join non-adjacent slots
+    assert len(pr.arap_pair) > 0
+
+
+def test_triangle_count_is_qhull_facet_count():
+    rng = np.random.default_rng(9)
+    for n in (10, 120, 1000):
+        xy = rng.normal(size=(n, 2))
+        lifted = np.c_[xy, (xy * xy).sum(1)]
+        T = len(ConvexHull(lifted).simplices)
+        assert T == 2 * n - 4
+        lower = len(Delaunay(xy).simplices)
+        h = len(ConvexHull(xy).vertices)
+        assert lower == 2 * n - 2 - h
+
+
+def test_eigen_jacobi_svd_restatement():
+    rng = np.random.default_rng(10)
+    for _ in range(50):
+        S = rng.normal(size=(3, 3)) * 10.0 ** rng.uniform(-6, 2)
+        U, s, V = graph_ref.eigen_jacobi_svd3(S)
+        assert np.allclose(U @ np.diag(s) @ V.T, S, atol=1e-12 * np.abs(S).max())
+        assert np.allclose(s, np.linalg.svd(S)[1], rtol=1e-10)
+        assert np.allclose(U.T @ U, np.eye(3), atol=1e-12)
+        R = graph_ref.procrustes(S)
+        assert np.isclose(np.linalg.det(R), 1.0) and np.allclose(R.T @ R, np.eye(3), atol=1e-12)
+
+
+def test_problem_roundtrip(tmp_path, golden_cases):
+    p = Problem.load(GOLDEN / golden_cases[0] / "problem.npz")
+    p.save(tmp_path / "p.npz")
+    q = Problem.load(tmp_path / "p.npz")
+    compare(p, q, rtol=0)
+
+
+def test_graph_errors(host):
+    m, _ = sim.simulate_two_view(n=2, seed=1)
+    with pytest.raises(capi.DeftriError) as e:
+        host.build_graph(m, 1.0, 2e5, np.float32(0.003))
+    assert e.value.code == -6

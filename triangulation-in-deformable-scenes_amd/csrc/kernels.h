@@ -75,6 +75,15 @@ struct DevPlan {
     int *flag = nullptr;
 };
 
+// per-launch device timing for deftri_profile_trial (never active on the solve path)
+struct KProfRec { const char *name; hipEvent_t e0, e1; };
+struct KProf {
+    std::vector<hipEvent_t> pool;
+    size_t next = 0;
+    std::vector<KProfRec> recs;
+};
+void set_profiler(KProf *p);
+
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);

@@ -741,17 +741,37 @@ __global__ void k_hmul(int64_t nblocks, const int64_t *__restrict__ val_off, con
 // ------------------------------------------------------------------------------------------
 static inline unsigned nb(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// optional per-launch device timing (deftri_profile_trial); off on the solve path
+thread_local KProf *g_prof = nullptr;
+void set_profiler(KProf *p) { g_prof = p; }
+static hipEvent_t prof_event() {
+    KProf &P = *g_prof;
+    if (P.next == P.pool.size()) { hipEvent_t e; hipEventCreate(&e); P.pool.push_back(e); }
+    return P.pool[P.next++];
+}
+#define LAUNCH(NAME, KER, GRID, BLOCK, ST, ...)                                     \
+    do {                                                                             \
+        hipEvent_t e0_ = nullptr;                                                    \
+        if (g_prof) { e0_ = prof_event(); hipEventRecord(e0_, ST); }                 \
+        hipLaunchKernelGGL(KER, GRID, BLOCK, 0, ST, __VA_ARGS__);                    \
+        if (g_prof) {                                                                \
+            hipEvent_t e1_ = prof_event();                                           \
+            hipEventRecord(e1_, ST);                                                 \
+            g_prof->recs.push_back({NAME, e0_, e1_});                                \
+        }                                                                            \
+    } while (0)
+
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic) {
     if (P.R > 0)
-        hipLaunchKernelGGL(dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), 0, st, P.R, P.rep_point, P.rep_cam,
+        LAUNCH("lin_rep", dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), st, P.R, P.rep_point, P.rep_cam,
                            P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose, P.cam_R, P.cam_kb8, P.Jrep,
                            P.Wrep, P.Erep, P.chi_rep, want_jac ? 1 : 0);
     if (P.D > 0)
-        hipLaunchKernelGGL(dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), 0, st, P.D, P.dep_point, P.dep_scale,
+        LAUNCH("lin_dep", dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), st, P.D, P.dep_point, P.dep_scale,
                            P.dep_cam, P.dep_meas, P.dep_info, P.points, P.scales, P.cam_pose, P.cam_R, P.Jdep,
                            P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0);
     if (P.E > 0)
-        hipLaunchKernelGGL(dev::k_lin_arap, dim3(nb(P.E, 128)), dim3(128), 0, st, P.E, P.arap_pts, P.arap_pair,
+        LAUNCH("lin_arap", dev::k_lin_arap, dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
                            P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg, P.Jarap, P.Warap,
                            P.Earap, P.chi_arap, want_jac ? 1 : 0, analytic ? 1 : 0);
 }
@@ -759,23 +779,23 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
     dev::EdgeJ ej{P.Jrep, P.Wrep, P.Erep, P.Jdep, P.Wdep, P.Edep, P.Jarap, P.Warap, P.Earap};
     if (L.nhchunks > 0)
-        hipLaunchKernelGGL(dev::k_hchunk, dim3(nb(L.nhchunks, 64)), dim3(64), 0, st, L.nhchunks, L.hcontrib,
+        LAUNCH("hchunk", dev::k_hchunk, dim3(nb(L.nhchunks, 64)), dim3(64), st, L.nhchunks, L.hcontrib,
                            L.hchunk_begin, L.hchunk_len, ej, L.hpart);
     if (L.nblocks > 0)
-        hipLaunchKernelGGL(dev::k_hfinal, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks,
+        LAUNCH("hfinal", dev::k_hfinal, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks,
                            L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
     if (L.nbchunks > 0)
-        hipLaunchKernelGGL(dev::k_bchunk, dim3(nb(L.nbchunks, 128)), dim3(128), 0, st, L.nbchunks, L.bcontrib,
+        LAUNCH("bchunk", dev::k_bchunk, dim3(nb(L.nbchunks, 128)), dim3(128), st, L.nbchunks, L.bcontrib,
                            L.bchunk_begin, L.bchunk_len, ej, L.bpart);
     if (L.nv > 0)
-        hipLaunchKernelGGL(dev::k_bfinal, dim3(nb(L.nv, 128)), dim3(128), 0, st, L.nv, L.bv_chunk_begin, L.voff,
+        LAUNCH("bfinal", dev::k_bfinal, dim3(nb(L.nv, 128)), dim3(128), st, L.nv, L.bv_chunk_begin, L.voff,
                            L.vdim, L.bpart, L.b);
 }
 
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
     hipMemsetAsync(L.arena, 0, sizeof(double) * (size_t)L.arena_size, st);
     if (L.nblocks > 0)
-        hipLaunchKernelGGL(dev::k_scatter, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks, L.blk_val_off,
+        LAUNCH("scatter", dev::k_scatter, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks, L.blk_val_off,
                            L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, lambda, L.arena);
 }
 
@@ -784,17 +804,17 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
         const auto &lv = L.levels[h];
         for (int slot = 0; slot < 2; slot++)
             if (lv.nea[slot] > 0)
-                hipLaunchKernelGGL(dev::k_ea, dim3(lv.nea[slot]), dim3(256), 0, st, lv.nea[slot],
+                LAUNCH("ea", dev::k_ea, dim3(lv.nea[slot]), dim3(256), st, lv.nea[slot],
                                    L.tasks + 3 * lv.ea_off[slot], L.fd, L.arena);
         for (const auto &stp : lv.steps) {
             if (stp.ndiag > 0)
-                hipLaunchKernelGGL(dev::k_diag, dim3(stp.ndiag), dim3(256), 0, st, stp.ndiag, L.tasks + 3 * stp.diag_off,
+                LAUNCH("diag", dev::k_diag, dim3(stp.ndiag), dim3(256), st, stp.ndiag, L.tasks + 3 * stp.diag_off,
                                    L.fd, L.arena, L.flag);
             if (stp.ntrsm > 0)
-                hipLaunchKernelGGL(dev::k_trsm, dim3(stp.ntrsm), dim3(64), 0, st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
+                LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(64), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
                                    L.fd, L.arena);
             if (stp.nupd > 0)
-                hipLaunchKernelGGL(dev::k_update, dim3(stp.nupd), dim3(256), 0, st, stp.nupd, L.tasks + 3 * stp.upd_off,
+                LAUNCH("update", dev::k_update, dim3(stp.nupd), dim3(256), st, stp.nupd, L.tasks + 3 * stp.upd_off,
                                    stp.k0, L.fd, L.arena);
         }
     }
@@ -804,19 +824,19 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         if (lv.nfwd > 0)
-            hipLaunchKernelGGL(dev::k_fwd, dim3(lv.nfwd), dim3(256), 0, st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
+            LAUNCH("fwd", dev::k_fwd, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
                                L.arena, rhs, L.vec);
         if (lv.ngemv > 0)
-            hipLaunchKernelGGL(dev::k_fwd_gemv, dim3(lv.ngemv), dim3(256), 0, st, lv.ngemv, L.tasks + 3 * lv.gemv_off,
+            LAUNCH("fwd_gemv", dev::k_fwd_gemv, dim3(lv.ngemv), dim3(256), st, lv.ngemv, L.tasks + 3 * lv.gemv_off,
                                L.fd, L.arena, L.vec);
     }
     for (size_t hh = L.levels.size(); hh-- > 0;) {
         const auto &lv = L.levels[hh];
         if (lv.nbgemv > 0)
-            hipLaunchKernelGGL(dev::k_bwd_gemv, dim3(lv.nbgemv), dim3(256), 0, st, lv.nbgemv,
+            LAUNCH("bwd_gemv", dev::k_bwd_gemv, dim3(lv.nbgemv), dim3(256), st, lv.nbgemv,
                                L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.vec);
         if (lv.nfwd > 0)
-            hipLaunchKernelGGL(dev::k_bwd, dim3(lv.nfwd), dim3(256), 0, st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
+            LAUNCH("bwd", dev::k_bwd, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
                                L.arena, L.vec, x);
     }
 }
@@ -825,28 +845,28 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st) 
     int n = P.P > P.S ? P.P : P.S;
     if (P.Q > n) n = P.Q;
     if (n > 0)
-        hipLaunchKernelGGL(dev::k_update_state, dim3(nb(n, 128)), dim3(128), 0, st, P.P, P.S, P.Q, dx, P.points,
+        LAUNCH("update_state", dev::k_update_state, dim3(nb(n, 128)), dim3(128), st, P.P, P.S, P.Q, dx, P.points,
                            P.scales, P.tg);
 }
 
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
                 double *out, hipStream_t st) {
     if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
-    hipLaunchKernelGGL(dev::k_sum_partial, dim3(nparts), dim3(256), 0, st, n, a, b, lambda, mode, part);
-    hipLaunchKernelGGL(dev::k_sum_final, dim3(1), dim3(64), 0, st, nparts, part, out);
+    LAUNCH("sum_partial", dev::k_sum_partial, dim3(nparts), dim3(256), st, n, a, b, lambda, mode, part);
+    LAUNCH("sum_final", dev::k_sum_final, dim3(1), dim3(64), st, nparts, part, out);
 }
 
 void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st) {
-    hipLaunchKernelGGL(dev::k_maxdiag, dim3(nparts), dim3(256), 0, st, L.nblocks, L.blk_val_off, L.blk_cols,
+    LAUNCH("maxdiag", dev::k_maxdiag, dim3(nparts), dim3(256), st, L.nblocks, L.blk_val_off, L.blk_cols,
                        L.blk_diag, L.hval, part);
-    hipLaunchKernelGGL(dev::k_max_final, dim3(1), dim3(64), 0, st, nparts, part, out);
+    LAUNCH("max_final", dev::k_max_final, dim3(1), dim3(64), st, nparts, part, out);
 }
 
 void launch_hmul(const DevPlan &L, const int64_t *brow_dof, const int64_t *bcol_dof, const double *x, double *y,
                  int64_t n, hipStream_t st) {
     hipMemsetAsync(y, 0, sizeof(double) * (size_t)n, st);
     if (L.nblocks > 0)
-        hipLaunchKernelGGL(dev::k_hmul, dim3(nb(L.nblocks, 128)), dim3(128), 0, st, L.nblocks, L.blk_val_off,
+        LAUNCH("hmul", dev::k_hmul, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks, L.blk_val_off,
                            L.blk_rows, L.blk_cols, brow_dof, bcol_dof, L.blk_diag, L.hval, x, y);
 }
 

@@ -440,6 +440,49 @@ int deftri_debug_plan_solve(deftri_ctx *ctx, const double *H, double lambda, con
     return plan_emulate_solve(ctx->S, H, lambda, rhs, x) == 0 ? 0 : fail(ctx, DEFTRI_E_NUMERIC, "zero pivot");
 }
 
+int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *stats, int32_t max_stats,
+                         int32_t *n_stats) {
+    if (!ctx || !stats || !n_stats) return DEFTRI_E_ARG;
+    if (!ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(ctx->device);
+    HIPOK(hipStreamSynchronize(ctx->st));
+    KProf prof;
+    set_profiler(&prof);
+    eval_chi2_dev(ctx, true, true, 0);
+    launch_assemble(ctx->P, ctx->L, ctx->st);
+    hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
+    launch_scatter(ctx->L, lambda, ctx->st);
+    launch_factor(ctx->L, ctx->st);
+    launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st);
+    set_profiler(nullptr);
+    HIPOK(hipStreamSynchronize(ctx->st));
+    int32_t n = 0;
+    for (const auto &r : prof.recs) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, r.e0, r.e1);
+        int32_t k = 0;
+        for (; k < n; k++) if (std::strcmp(stats[k].name, r.name) == 0) break;
+        if (k == n) {
+            if (n >= max_stats) continue;
+            std::memset(&stats[n], 0, sizeof(stats[n]));
+            std::strncpy(stats[n].name, r.name, sizeof(stats[n].name) - 1);
+            n++;
+        }
+        stats[k].launches++;
+        stats[k].ms += ms;
+    }
+    const Symbolic &S = ctx->S;
+    for (int32_t k = 0; k < n; k++) {
+        if (!std::strcmp(stats[k].name, "update")) stats[k].flops = S.update_flops;
+        if (!std::strcmp(stats[k].name, "diag")) stats[k].flops = S.diag_flops;
+        if (!std::strcmp(stats[k].name, "trsm")) stats[k].flops = S.trsm_flops;
+        if (!std::strcmp(stats[k].name, "lin_arap")) stats[k].bytes = (double)ctx->P.E * (16 + 8 * 12 + 8 * 18 + 3 * 8);
+    }
+    for (hipEvent_t e : prof.pool) hipEventDestroy(e);
+    *n_stats = n;
+    return 0;
+}
+
 int64_t deftri_sizeof(int32_t which) {
     switch (which) {
         case 0: return (int64_t)sizeof(deftri_problem_desc);

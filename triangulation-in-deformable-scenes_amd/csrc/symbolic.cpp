@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <numeric>
 
 namespace deftri {
@@ -103,6 +105,7 @@ struct Builder {
             else Sp.push_back(p);
         }
         for (int64_t p : nodes) side[p] = 0;
+        if (std::getenv("DEFTRI_DEBUG_PLAN") && depth < 3) std::fprintf(stderr, "[nd] depth %d n %lld L %zu R %zu S %zu ax %d\n", depth, (long long)n, L.size(), R.size(), Sp.size(), ax);
         if (L.empty() || R.empty()) {          // cannot split (degenerate coordinates)
             std::vector<int64_t> ov;
             std::sort(nodes.begin(), nodes.end());
@@ -219,6 +222,19 @@ struct Builder {
         S.nlevels = maxh + 1;
         S.level_fronts.assign(S.nlevels, {});
         for (int32_t f = 0; f < nf; f++) S.level_fronts[S.fronts[f].height].push_back(f);
+        if (std::getenv("DEFTRI_DEBUG_PLAN")) {
+            for (int32_t h = 0; h < S.nlevels; h++) {
+                int32_t ms = 0, mm = 0; double fl = 0;
+                for (int32_t f : S.level_fronts[h]) {
+                    const Front &F = S.fronts[f];
+                    ms = std::max(ms, F.s); mm = std::max(mm, F.m);
+                    double sd = F.s, ud = F.m - F.s;
+                    fl += sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
+                }
+                std::fprintf(stderr, "[plan] level %d fronts %zu max_s %d max_m %d flops %.3g\n", h,
+                             S.level_fronts[h].size(), ms, mm, fl);
+            }
+        }
 
         // ---------------- H blocks ----------------
         // column vertex c, row vertices r with elim[r] >= elim[c], r coupled with c (or r == c)
@@ -344,13 +360,20 @@ struct Builder {
                 Symbolic::StepTasks st;
                 st.k0 = k0;
                 st.diag_off = (int64_t)S.task_i32.size() / 3;
-                for (int32_t f : fs) if (S.fronts[f].s > k0) { push3(f, k0, 0); st.ndiag++; }
+                for (int32_t f : fs) if (S.fronts[f].s > k0) {
+                    push3(f, k0, 0); st.ndiag++;
+                    double kb = std::min(kPanel, S.fronts[f].s - k0);
+                    S.diag_flops += kb * kb * kb / 3.0;
+                }
                 st.trsm_off = (int64_t)S.task_i32.size() / 3;
                 for (int32_t f : fs) {
                     const Front &F = S.fronts[f];
                     if (F.s <= k0) continue;
                     int32_t kb = std::min(kPanel, F.s - k0);
-                    for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) { push3(f, k0, r0); st.ntrsm++; }
+                    for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) {
+                        push3(f, k0, r0); st.ntrsm++;
+                        S.trsm_flops += (double)std::min(64, F.m - r0) * kb * kb;
+                    }
                 }
                 st.upd_off = (int64_t)S.task_i32.size() / 3;
                 for (int32_t f : fs) {
@@ -362,6 +385,7 @@ struct Builder {
                         for (int32_t tj = t0; tj <= ti; tj += 64) {
                             push3(f, ti, tj);      // k0 recovered from step (same for all tasks)
                             st.nupd++;
+                            S.update_flops += 2.0 * std::min(64, F.m - ti) * std::min(64, F.m - tj) * kb;
                         }
                 }
                 LT.steps.push_back(st);

@@ -58,6 +58,7 @@ struct Symbolic {
     int32_t nlevels = 0;
     std::vector<std::vector<int32_t>> level_fronts;   // by height, ascending
     double factor_flops = 0;
+    double update_flops = 0, diag_flops = 0, trsm_flops = 0;   // per factorization, by kernel
     int64_t nnz_factor = 0;
 
     // H blocks: column vertex c (eliminated no later than the row vertex r)

@@ -80,6 +80,10 @@ class MapC(C.Structure):
     _fields_ = [("n_keyframes", i32), ("keyframes", P(KeyFrameC)), ("global_t", f64 * 7)]
 
 
+class KernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 32), ("launches", i64), ("ms", f64), ("flops", f64), ("bytes", f64)]
+
+
 def ptr(a, ctype):
     """Pointer into a contiguous numpy array (None for None)."""
     if a is None:

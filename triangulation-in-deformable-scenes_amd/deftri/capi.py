@@ -50,6 +50,7 @@ def load():
         "deftri_eval_damped_solve": (C.c_int, [C.c_void_p, C.c_double, P(C.c_double), P(C.c_double), C.c_int64]),
         "deftri_num_unknowns": (C.c_int64, [C.c_void_p]),
         "deftri_sizeof": (C.c_int64, [C.c_int32]),
+        "deftri_profile_trial": (C.c_int, [C.c_void_p, C.c_double, P(_abi.KernelStat), C.c_int32, P(C.c_int32)]),
         "deftri_arap_build_graph": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_float,
                                               P(P(_abi.ProblemDesc))]),
         "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
@@ -70,6 +71,7 @@ EXPORTED = [
     "deftri_solve_lm", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
+    "deftri_profile_trial",
 ]
 
 
@@ -169,6 +171,14 @@ class Context:
         x = np.zeros_like(r)
         self._check(self.lib.deftri_eval_damped_solve(self.h, float(lam), _dp(r), _dp(x), len(r)))
         return x
+
+    def profile_trial(self, lam):
+        """Per-kernel device time of one LM trial: {name: {launches, ms, flops, bytes}}."""
+        arr = (_abi.KernelStat * 64)()
+        n = C.c_int32()
+        self._check(self.lib.deftri_profile_trial(self.h, float(lam), arr, 64, C.byref(n)))
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].ms, "flops": arr[i].flops,
+                                       "bytes": arr[i].bytes} for i in range(n.value)}
 
     # map-level API -------------------------------------------------------------------------
     def build_graph(self, m, rep_weight, arap_weight, depth_error):

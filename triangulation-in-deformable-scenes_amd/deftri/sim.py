@@ -129,13 +129,23 @@ def triangulate_nrslam_far(xn1, xn2, T1w, T2w):
 def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.12),
                       c2=(0.14, 0.01, 0.06), kb8=SIM_KB8, rep_error=1.0, decimals=1,
                       depth_error=3.0, depth_scales=(0.4, 1.7), min_cos=0.9998, n_scales=8,
-                      scale_factor=1.2, rigid=0.0025, gaussian=0.0025):
+                      scale_factor=1.2, rigid=0.0025, gaussian=0.0025, scale_scene=False, compact=False):
     """The reference's Execution/simulation.cc flow up to deformationOptimization.
 
+    scale_scene: for large n the cloud extents grow by sqrt(n/120) (generate_points); this also
+      scales the camera positions and the 0.2 m depth offset, so the viewing geometry of the
+      reference's 120-point scene is kept (otherwise points fall behind / beside the cameras).
+    compact: drop correspondences that fail the triangulation checks before slots are assigned
+      (the reference leaves null slots, which triggers its slot/position index quirk; see
+      SURVEY Appendix B.2 — a compacted scene is the same as running the reference on the
+      filtered point files).
     Returns (Map, ground_truth dict)."""
     rng = np.random.default_rng(seed + 1000003)
     if orig is None:
-        orig, moved = generate_points(n, rigid=rigid, gaussian=gaussian, seed=seed)
+        sc = np.sqrt(n / 120.0) if scale_scene else 1.0
+        orig, moved = generate_points(n, rigid=rigid, gaussian=gaussian, seed=seed,
+                                      mean=(0.0, 0.0, 0.2 * sc))
+        c1 = tuple(np.asarray(c1) * sc); c2 = tuple(np.asarray(c2) * sc)
     orig = np.asarray(orig, np.float32); moved = np.asarray(moved, np.float32)
     n = len(orig)
     T1w = SE3f(np.eye(3, dtype=np.float32), np.asarray(c1, np.float32))
@@ -169,6 +179,12 @@ def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.1
     ray1 /= np.linalg.norm(ray1, axis=1, keepdims=True); ray2 /= np.linalg.norm(ray2, axis=1, keepdims=True)
     cosp = (ray1 * ray2).sum(1) / (np.linalg.norm(ray1, axis=1) * np.linalg.norm(ray2, axis=1))
     valid = (z1 >= 0) & (z2 >= 0) & (cosp <= min_cos) & np.all(np.isfinite(x3d1), 1) & np.all(np.isfinite(x3d2), 1)
+    if compact and not valid.all():
+        keep = np.where(valid)[0]
+        return simulate_two_view(n=len(keep), seed=seed, orig=orig[keep], moved=moved[keep], c1=c1, c2=c2,
+                                 kb8=kb8, rep_error=rep_error, decimals=decimals, depth_error=depth_error,
+                                 depth_scales=depth_scales, min_cos=min_cos, n_scales=n_scales,
+                                 scale_factor=scale_factor, compact=True)
     next_id = 0
     for i in range(n):
         if not valid[i]:
