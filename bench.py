@@ -71,7 +71,7 @@ def cpu_baseline(n_full, full_flops, gpu_trials_per_iter, n_sample=10000):
     per_trial = dt / trials
     t_iter_full = per_trial * (full_flops / f_sample) * gpu_trials_per_iter
     return {"value": 1.0 / t_iter_full, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"oracle LM, 1 iteration ({trials} trials) on {p.n_points} correspondences: "
+            "sample": f"oracle LM, 1 iteration ({trials} trials) on {p.n_points // 2} correspondences x 2 views: "
                       f"{dt:.1f} s measured; extrapolated to the {n_full}-point workload by the "
                       f"factorization flop ratio {full_flops / f_sample:.1f}x at "
                       f"{gpu_trials_per_iter:.2f} trials/iteration"}

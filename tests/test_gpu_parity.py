@@ -3,7 +3,8 @@ fixtures.  Tolerances:
   * chi2, b, H x, diag(H)             rel 1e-11  (fp64 everywhere; fp32 KB8 projection in both)
   * damped LDL^T solve                 rel 1e-8 vs the oracle's sparse LDL^T (different elimination order)
   * LM trajectory (analytic J)         chi2 per iteration rel 1e-6, same iteration/trial counts
-  * LM in g2o numeric-J mode vs golden final reprojection RMSE within 1e-4 px (north-star tolerance)
+  * LM in g2o numeric-J mode vs golden: final reprojection RMSE within 1e-4 px (north-star
+    tolerance), chi2 rel 1e-5, points within 1e-6 m
   * full size (C2, 100k corr.)         size-independent properties: backward error of the solve,
                                        monotone accepted chi2, run-to-run bit-identical results
 """
@@ -77,7 +78,10 @@ def test_numeric_jacobian_mode_matches_golden_rmse(gpu_ctx, golden_cases):
         z = np.load(GOLDEN / name / "expected_lm.npz")
         gpu_ctx.upload(p)
         r = gpu_ctx.solve_lm(exp["n_iterations"], analytic=False)
-        assert r["chi2_final"] == pytest.approx(exp["chi2_final"], rel=1e-6)
+        # central differences at delta=1e-9 amplify last-ulp differences between the device and host
+        # computeError (FMA contraction, ocml vs glibc sin/cos) to ~1e-7 relative in J, so the
+        # trajectories agree to ~1e-6 in chi2, not bitwise; the north-star criterion is the RMSE
+        assert r["chi2_final"] == pytest.approx(exp["chi2_final"], rel=1e-5)
         pts, sc, tg = gpu_ctx.download()
         m, st, sigma = mg.scene(name)
         metrics.apply_solution(m, exp["point_ids"], pts)
