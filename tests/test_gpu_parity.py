@@ -164,6 +164,6 @@ def test_full_size_properties(gpu_ctx):
 def test_profile_trial_reports_kernels(gpu_ctx, golden_cases):
     gpu_ctx.upload(_golden(golden_cases[0]))
     st = gpu_ctx.profile_trial(1e3)
-    for k in ("lin_arap", "hchunk", "scatter", "diag", "update", "fwd", "bwd"):
+    for k in ("lin_arap", "hchunk", "scatter", "diag", "trsm", "update", "fwd_step", "bwd_step"):
         assert k in st and st[k]["launches"] > 0
     assert st["update"]["flops"] > 0

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Quick GPU check: parity tests + one bench line (no CPU baseline, no profiler).
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-quick}
+mkdir -p $OUT
+cd $R
+timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { tail -60 $OUT/pytest_gpu.log; exit 1; }
+tail -3 $OUT/pytest_gpu.log
+timeout -k 10 600 python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json

@@ -7,6 +7,8 @@
 
 namespace deftri {
 
+constexpr int64_t kHeavyChunks = 16;   // chunk count above which an H block / b vertex is reduced by a workgroup
+
 // problem arrays resident in HBM (layout = deftri_problem_desc, SoA)
 struct DevProblem {
     int32_t P = 0, Q = 0, S = 0, C = 0, R = 0, D = 0, E = 0, NR = 0;
@@ -32,16 +34,17 @@ struct DevProblem {
 
 struct FrontDev {
     const int32_t *m, *s, *parent, *nchild, *child0, *child1;
-    const int64_t *arena_off, *vec_off, *rows_off, *bmap_off;
+    const int64_t *arena_off, *vec_off, *rows_off, *bmap_off, *inv_off;
     const int32_t *rows, *bmap;
 };
 
 struct LevelDev {
     int64_t ea_off[2]; int32_t nea[2];
-    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0; };
+    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner; };
     std::vector<Step> steps;
     int64_t fwd_off; int32_t nfwd;
-    int64_t gemv_off; int32_t ngemv;
+    struct SolveStep { int64_t off; int32_t n; };
+    std::vector<SolveStep> fsteps, bsteps;
     int64_t bgemv_off; int32_t nbgemv;
 };
 
@@ -60,6 +63,8 @@ struct DevPlan {
     int64_t *hchunk_begin = nullptr, *hblk_chunk_begin = nullptr;
     int32_t *hchunk_len = nullptr;
     double *hpart = nullptr;
+    int64_t nheavy_h = 0, nheavy_b = 0;
+    int64_t *heavy_h = nullptr, *heavy_b = nullptr;     // blocks / vertices with > kHeavyChunks chunks
     int64_t nbchunks = 0;
     uint64_t *bcontrib = nullptr;
     int64_t *bchunk_begin = nullptr, *bv_chunk_begin = nullptr;
@@ -68,7 +73,9 @@ struct DevPlan {
     double *b = nullptr;
     // factor
     int64_t arena_size = 0, vec_size = 0;
-    double *arena = nullptr, *vec = nullptr;
+    int64_t inv_size = 0;
+    double *inv = nullptr;       // panel-triangle inverses (Front::inv_off)
+    double *arena = nullptr, *vec = nullptr, *yvec = nullptr;   // yvec: forward solution y per front row
     FrontDev fd{};
     int32_t *tasks = nullptr;
     std::vector<LevelDev> levels;
@@ -76,7 +83,7 @@ struct DevPlan {
 };
 
 // per-launch device timing for deftri_profile_trial (never active on the solve path)
-struct KProfRec { const char *name; hipEvent_t e0, e1; };
+struct KProfRec { const char *name; hipEvent_t e0, e1; unsigned grid; };
 struct KProf {
     std::vector<hipEvent_t> pool;
     size_t next = 0;

@@ -19,6 +19,7 @@
 
 #include "device_math.h"
 #include "kernels.h"
+#include "symbolic.h"
 
 namespace deftri {
 namespace dev {
@@ -302,11 +303,46 @@ __global__ void k_hfinal(int64_t nblocks, const int64_t *__restrict__ blk_chunk_
                          double *__restrict__ hval) {
     int64_t b = TID;
     if (b >= nblocks) return;
+    int64_t c0 = blk_chunk_begin[b], c1 = blk_chunk_begin[b + 1];
+    if (c1 - c0 > kHeavyChunks) return;                 // k_hfinal_heavy
     int n = brows[b] * bcols[b];
     double *o = hval + val_off[b];
     for (int k = 0; k < n; k++) o[k] = 0.0;
-    for (int64_t c = blk_chunk_begin[b]; c < blk_chunk_begin[b + 1]; c++)
+    for (int64_t c = c0; c < c1; c++)
         for (int k = 0; k < n; k++) o[k] += part[36 * c + k];
+}
+
+// blocks fed by thousands of chunks (the global T_g / depth-scale rows): one workgroup per block,
+// strided per-thread sums then an in-order sum over the 256 partials — fixed order, no atomics
+template <int W>
+__device__ __forceinline__ void heavy_sum(int64_t c0, int64_t c1, int n, const double *__restrict__ part,
+                                          double *__restrict__ o) {
+    __shared__ double red[256][W + 1];
+    double acc[W];
+#pragma unroll
+    for (int k = 0; k < W; k++) acc[k] = 0.0;
+    for (int64_t c = c0 + threadIdx.x; c < c1; c += 256)
+#pragma unroll
+        for (int k = 0; k < W; k++)
+            if (k < n) acc[k] += part[W * c + k];
+#pragma unroll
+    for (int k = 0; k < W; k++) red[threadIdx.x][k] = acc[k];
+    __syncthreads();
+    if (threadIdx.x < n) {
+        double s = 0.0;
+        for (int t = 0; t < 256; t++) s += red[t][threadIdx.x];
+        o[threadIdx.x] = s;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_hfinal_heavy(const int64_t *__restrict__ heavy,
+                                                      const int64_t *__restrict__ blk_chunk_begin,
+                                                      const int64_t *__restrict__ val_off,
+                                                      const int32_t *__restrict__ brows,
+                                                      const int32_t *__restrict__ bcols,
+                                                      const double *__restrict__ part, double *__restrict__ hval) {
+    int64_t b = heavy[blockIdx.x];
+    heavy_sum<36>(blk_chunk_begin[b], blk_chunk_begin[b + 1], brows[b] * bcols[b], part, hval + val_off[b]);
 }
 
 __global__ void k_bchunk(int64_t nchunks, const uint64_t *__restrict__ contrib, const int64_t *__restrict__ cbeg,
@@ -339,11 +375,20 @@ __global__ void k_bfinal(int64_t nv, const int64_t *__restrict__ v_chunk_begin, 
                          const int32_t *__restrict__ vdim, const double *__restrict__ part, double *__restrict__ b) {
     int64_t v = TID;
     if (v >= nv) return;
+    if (v_chunk_begin[v + 1] - v_chunk_begin[v] > kHeavyChunks) return;   // k_bfinal_heavy
     int dim = vdim[v];
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int64_t c = v_chunk_begin[v]; c < v_chunk_begin[v + 1]; c++)
         for (int i = 0; i < 6; i++) acc[i] += part[6 * c + i];
     for (int i = 0; i < dim; i++) b[voff[v] + i] = acc[i];
+}
+
+__global__ void __launch_bounds__(256) k_bfinal_heavy(const int64_t *__restrict__ heavy,
+                                                      const int64_t *__restrict__ v_chunk_begin,
+                                                      const int64_t *__restrict__ voff, const int32_t *__restrict__ vdim,
+                                                      const double *__restrict__ part, double *__restrict__ b) {
+    int64_t v = heavy[blockIdx.x];
+    heavy_sum<6>(v_chunk_begin[v], v_chunk_begin[v + 1], vdim[v], part, b + voff[v]);
 }
 
 // H (+ lambda I) -> fronts
@@ -382,133 +427,285 @@ __global__ void k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDe
     }
 }
 
-// LDL^T of the kb x kb diagonal block of panel k0 (lower triangle, unit L, D on the diagonal)
-__global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                              double *__restrict__ arena, int *__restrict__ flag) {
-    __shared__ double A[64][65];
-    int t = blockIdx.x;
-    if (t >= ntask) return;
-    int f = tasks[3 * t], k0 = tasks[3 * t + 1];
-    int m = fd.m[f], s = fd.s[f];
-    int kb = min(64, s - k0);
-    double *F = arena + fd.arena_off[f];
-    for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
-        int j = idx / kb, i = idx % kb;
-        if (i >= j) A[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
-    }
-    __syncthreads();
-    for (int j = 0; j < kb; j++) {
-        double d = A[j][j];
-        if (threadIdx.x == 0 && d == 0.0) atomicOr(flag, 1);
-        for (int i = j + 1 + threadIdx.x; i < kb; i += blockDim.x) A[i][j] = A[i][j] / d;
-        __syncthreads();
-        int w = kb - 1 - j;
-        for (int idx = threadIdx.x; idx < w * w; idx += blockDim.x) {
-            int ii = idx / w, cc = idx % w;
-            if (ii >= cc) {
-                int i = j + 1 + ii, c2 = j + 1 + cc;
-                A[i][c2] -= A[i][j] * d * A[c2][j];
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Blocked LDL^T + unit-lower inverse of one 64x64 panel diagonal block held in LDS (256 threads).
+//   in : S[r][c] (c <= r) = A (rows/cols >= kb padded with the identity), S[c][r] (r > c) = 0
+//   out: S[r][c] (c < r) = L, S[r][r] = D, S[c][r] (r > c) = Linv[r][c]
+// Four 16-column sub-panels: wave 0 factors the 16x16 diagonal block and its inverse (16 dependent
+// steps, wave-synchronous), then all 256 threads do the sub-panel TRSM and the trailing update;
+// finally the off-diagonal blocks of Linv are formed block-row by block-row
+// (X_IJ = -X_II sum_K L_IK X_KJ).  T is 16x48 scratch.
+constexpr int DP = 65;
+__device__ __forceinline__ void diag_block(double (*S)[DP], double (*T)[48], int *flag) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int sp = 0; sp < 4; sp++) {
+        const int j0 = 16 * sp;
+        if (wv == 0) {
+            const int r = lane & 15, g = lane >> 4;
+            for (int j = 0; j < 16; j++) {
+                double d = S[j0 + j][j0 + j];
+                if (lane == 0 && d == 0.0) atomicOr(flag, 1);
+                if (g == 0 && r > j) S[j0 + r][j0 + j] = S[j0 + r][j0 + j] / d;
+                wave_sync();
+                if (r > j) {
+                    double li = S[j0 + r][j0 + j];
+                    double lid = li * d;
+                    for (int c = j + 1 + g; c <= r; c += 4) S[j0 + r][j0 + c] -= lid * S[j0 + c][j0 + j];
+                    for (int c = g; c <= j; c += 4) {
+                        double xjc = (c == j) ? 1.0 : S[j0 + c][j0 + j];      // X[j][c]
+                        S[j0 + c][j0 + r] -= li * xjc;                        // X[r][c]
+                    }
+                }
+                wave_sync();
             }
         }
         __syncthreads();
+        if (sp == 3) break;
+        const int nrow = 64 - (j0 + 16);
+        // TRSM: L[r][c] = (sum_{j0 <= j <= c} A[r][j] X[c][j]) / d_c for rows r >= j0+16, c in the sub-panel
+        double out[3];
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            int o = tid + 256 * q;
+            out[q] = 0.0;
+            if (o < nrow * 16) {
+                int r = j0 + 16 + o % nrow, c = j0 + o / nrow;
+                double acc = S[r][c];
+                for (int j = j0; j < c; j++) acc += S[r][j] * S[j][c];           // X[c][j] at S[j][c]
+                out[q] = acc / S[c][c];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            int o = tid + 256 * q;
+            if (o < nrow * 16) S[j0 + 16 + o % nrow][j0 + o / nrow] = out[q];
+        }
+        __syncthreads();
+        // trailing update of the lower triangle: A[r][c] -= sum_j L[r][j] d_j L[c][j]
+        for (int o = tid; o < nrow * nrow; o += 256) {
+            int r = j0 + 16 + o % nrow, c = j0 + 16 + o / nrow;
+            if (c > r) continue;
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) acc += S[r][j0 + j] * S[j0 + j][j0 + j] * S[c][j0 + j];
+            S[r][c] -= acc;
+        }
+        __syncthreads();
     }
-    for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
-        int j = idx / kb, i = idx % kb;
-        if (i >= j) F[(int64_t)(k0 + j) * m + k0 + i] = A[i][j];
+    // off-diagonal inverse blocks, block row I: T = sum_{K=J}^{I-1} L_IK X_KJ, X_IJ = -X_II T
+    for (int I = 1; I < 4; I++) {
+        const int r0 = 16 * I, ncol = r0;
+        for (int o = tid; o < 16 * ncol; o += 256) {
+            int r = r0 + (o & 15), c = o >> 4;
+            double acc = S[r][c];                                                   // j == c: X[c][c] = 1
+            for (int j = c + 1; j < r0; j++) acc += S[r][j] * S[c][j];              // X[j][c] at S[c][j]
+            T[o & 15][c] = acc;
+        }
+        __syncthreads();
+        for (int o = tid; o < 16 * ncol; o += 256) {
+            int rr = o & 15, c = o >> 4;
+            double acc = T[rr][c];                                                  // k == r: X[r][r] = 1
+            for (int k = 0; k < rr; k++) acc += S[r0 + k][r0 + rr] * T[k][c];       // X[r][k] at S[k][r]
+            S[c][r0 + rr] = -acc;
+        }
+        __syncthreads();
     }
 }
 
-// rows r0..r0+63 below the panel: L_i = F_i L11^{-T} D^{-1}
-__global__ void __launch_bounds__(64) k_trsm(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                             double *__restrict__ arena) {
-    __shared__ double L[64][65];
-    __shared__ double X[64][65];
+// load the panel diagonal block of (front F, panel k0) into S (identity padding), factor, store L/D
+// into the front and Linv (kb x kb, column-major) into the inverse arena
+__device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, double *Li, double (*S)[DP],
+                                           double (*T)[48], int *flag) {
+    const int kb = min(64, s - k0);
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+        int c = idx >> 6, r = idx & 63;
+        double v;
+        if (r < kb && c < kb) v = (r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : 0.0;
+        else v = (r == c) ? 1.0 : 0.0;
+        S[r][c] = v;
+    }
+    __syncthreads();
+    diag_block(S, T, flag);
+    for (int idx = threadIdx.x; idx < kb * kb; idx += 256) {
+        int c = idx / kb, r = idx % kb;
+        if (r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
+        Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
+    }
+}
+
+// standalone panel factorization (first panel of every front of a level; later panels are
+// factored by the update launch of the previous panel, see k_update)
+__global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                              double *__restrict__ arena, double *__restrict__ inv,
+                                              int *__restrict__ flag) {
+    __shared__ double S[64][DP];
+    __shared__ double T[16][48];
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int f = tasks[3 * t], k0 = tasks[3 * t + 1];
+    diag_panel(arena + fd.arena_off[f], fd.m[f], fd.s[f], k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S, T,
+               flag);
+}
+
+// f64 MFMA tile: C(64x64) = sum_k P[k][c] Q[k][r], P/Q k-major in LDS ([k][index]); wave w owns the
+// 32x32 quadrant (rows (w&1)*32, cols (w>>1)*32) as 2x2 v_mfma_f64_16x16x4 tiles.  The MFMA A operand
+// is indexed by the column c and B by the row r, so the accumulator's lane&15 runs along rows r:
+// 16 consecutive doubles per store of the column-major front.  acc[a][b][reg]: column
+// cb + 16a + (lane>>4) + 4 reg, row rb + 16b + (lane&15).
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int LDP = 66;
+
+__device__ __forceinline__ void mfma_tile(const double (*P)[LDP], const double (*Q)[LDP], int kb4, dbl4 acc[2][2]) {
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int rb = (w & 1) * 32, cb = (w >> 1) * 32;
+    int kl = lane >> 4, il = lane & 15;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < kb4; k += 4) {
+        double p0 = P[k + kl][cb + il], p1 = P[k + kl][cb + 16 + il];
+        double q0 = Q[k + kl][rb + il], q1 = Q[k + kl][rb + 16 + il];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
+    }
+}
+
+// rows r0..r0+63 below the panel: L_r = F_r L11^{-T} D^{-1}  (GEMM with the panel inverse)
+__global__ void __launch_bounds__(256) k_trsm(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                              double *__restrict__ arena, const double *__restrict__ inv) {
+    __shared__ double Qs[64][LDP];   // Qs[k][r] = F[r0 + r][k0 + k]
+    __shared__ double Ps[64][LDP];   // Ps[k][c] = Linv[c][k] / d_c
     int t = blockIdx.x;
     if (t >= ntask) return;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
-    int kb = min(64, s - k0);
+    int kb = min(64, s - k0), kb4 = (kb + 3) & ~3;
     double *F = arena + fd.arena_off[f];
-    int lane = threadIdx.x;
-    for (int j = 0; j < kb; j++) {
-        if (lane >= j && lane < kb) L[lane][j] = F[(int64_t)(k0 + j) * m + k0 + lane];
+    const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
+    for (int idx = threadIdx.x; idx < kb4 * 64; idx += 256) {
+        int k = idx >> 6, r = idx & 63;
+        bool ok = k < kb;
+        Qs[k][r] = (ok && r0 + r < m) ? F[(int64_t)(k0 + k) * m + r0 + r] : 0.0;
+        Ps[k][r] = (ok && r < kb) ? Li[(int64_t)k * kb + r] / F[(int64_t)(k0 + r) * m + k0 + r] : 0.0;
     }
-    int i = r0 + lane;
-    bool act = i < m;
-    for (int j = 0; j < kb; j++) X[lane][j] = act ? F[(int64_t)(k0 + j) * m + i] : 0.0;
     __syncthreads();
-    if (act) {
-        for (int j = 0; j < kb; j++) {
-            double z = X[lane][j];
-            for (int c = 0; c < j; c++) z -= L[j][c] * X[lane][c];
-            X[lane][j] = z;
-        }
-        for (int j = 0; j < kb; j++) F[(int64_t)(k0 + j) * m + i] = X[lane][j] / L[j][j];
-    }
+    dbl4 acc[2][2];
+    mfma_tile(Ps, Qs, kb4, acc);
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int rb = (w & 1) * 32, cb = (w >> 1) * 32;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                int c = cb + 16 * a + (lane >> 4) + 4 * g, r = rb + 16 * b + (lane & 15);
+                if (c < kb && r0 + r < m) F[(int64_t)(k0 + c) * m + r0 + r] = acc[a][b][g];
+            }
 }
 
-// trailing update of tile (ti, tj): C -= L_i D L_j^T over the panel
-__global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int k0,
-                                                const FrontDev fd, double *__restrict__ arena) {
-    __shared__ double As[64][64];
-    __shared__ double Bs[64][64];
-    int t = blockIdx.x;
+// XCD-aware task order: the 8 XCDs receive blockIdx round-robin, so block b runs task
+// (b % 8) * ceil(n/8) + b / 8 — each XCD works through one contiguous slice of the task list (nearby
+// tiles share panel rows in that XCD's L2).  The grid is rounded up to a multiple of 8.
+__device__ __forceinline__ int xcd_task(int ntask) {
+    int per = (ntask + 7) >> 3;
+    return (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+}
+
+// trailing update of tile (ti, tj): C -= L_i D L_j^T over L columns [kA, kA + K),
+// K = min(kmax, s - kA) (one 64-panel for the inner updates, a whole outer block otherwise).
+// MFMA operands are loaded straight from the front (16 consecutive rows per 128-B segment,
+// L2-resident panel) — no LDS on this path — and the C tile is fetched before the MFMA chain.
+__global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
+                                                int inner, const FrontDev fd, double *__restrict__ arena,
+                                                double *__restrict__ inv, int *__restrict__ flag) {
+    __shared__ double S[64][DP];
+    __shared__ double T[16][48];
+    int t = xcd_task(ntask);
     if (t >= ntask) return;
     int f = tasks[3 * t], ti = tasks[3 * t + 1], tj = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
-    int kb = min(64, s - k0);
+    int K = min(kmax, s - kA);
+    // inner updates stop at the end of the outer block (own columns): a tile straddling it must not
+    // touch the columns the outer update will cover
+    int cend = inner ? min(s, (kA / kOuter + 1) * kOuter) : m;
     double *F = arena + fd.arena_off[f];
-    for (int idx = threadIdx.x; idx < 64 * kb; idx += blockDim.x) {
-        int c = idx / 64, r = idx % 64;
-        int64_t col = (int64_t)(k0 + c) * m;
-        double dcc = F[col + k0 + c];
-        As[c][r] = (ti + r < m) ? F[col + ti + r] : 0.0;
-        Bs[c][r] = (tj + r < m) ? F[col + tj + r] * dcc : 0.0;
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int rb = ti + (w & 1) * 32, cb = tj + (w >> 1) * 32;
+    int kl = lane >> 4, il = lane & 15;
+    // C prefetch: acc layout (a, b, g) -> column cb + 16a + kl + 4g, row rb + 16b + il
+    double cv[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                cv[a][b][g] = (c < m && r < m) ? F[(int64_t)c * m + r] : 0.0;
+            }
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const bool p0ok = cb + il < m, p1ok = cb + 16 + il < m, q0ok = rb + il < m, q1ok = rb + 16 + il < m;
+    for (int k16 = 0; k16 < K; k16 += 16)
+#pragma unroll
+    for (int k = k16; k < k16 + 16; k += 4) {
+        int kk = k + kl;
+        bool ok = kk < K;
+        const double *col = F + (int64_t)(kA + kk) * m;
+        double dk = ok ? col[kA + kk] : 0.0;
+        double p0 = (ok && p0ok) ? col[cb + il] * dk : 0.0;
+        double p1 = (ok && p1ok) ? col[cb + 16 + il] * dk : 0.0;
+        double q0 = (ok && q0ok) ? col[rb + il] : 0.0;
+        double q1 = (ok && q1ok) ? col[rb + 16 + il] : 0.0;
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
     }
-    __syncthreads();
-    int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-    double acc[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; a++)
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 4; b++) acc[a][b] = 0.0;
-    for (int c = 0; c < kb; c++) {
-        double av[4], bv[4];
+        for (int b = 0; b < 2; b++)
 #pragma unroll
-        for (int a = 0; a < 4; a++) av[a] = As[c][ty * 4 + a];
-#pragma unroll
-        for (int b = 0; b < 4; b++) bv[b] = Bs[c][tx * 4 + b];
-#pragma unroll
-        for (int a = 0; a < 4; a++)
-#pragma unroll
-            for (int b = 0; b < 4; b++) acc[a][b] += av[a] * bv[b];
-    }
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        int col = tj + tx * 4 + b;
-        if (col >= m) continue;
-#pragma unroll
-        for (int a = 0; a < 4; a++) {
-            int row = ti + ty * 4 + a;
-            if (row < m) F[(int64_t)col * m + row] -= acc[a][b];
-        }
+            for (int g = 0; g < 4; g++) {
+                int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                if (c < cend && r < m) F[(int64_t)c * m + r] = cv[a][b][g] - acc[a][b][g];
+            }
+    // the diagonal tile of the next panel is final once this tile is: factor it here (its LDL^T
+    // overlaps the rest of this launch instead of costing its own launch on the critical path;
+    // these tiles are first in the task list)
+    int k1 = kA + K;
+    if (ti == tj && ti == k1 && s > k1) {
+        __syncthreads();
+        __threadfence_block();
+        diag_panel(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, S, T, flag);
     }
 }
 
 // ------------------------------------------------------------------------------------------
 // substitution
 // ------------------------------------------------------------------------------------------
-// forward: gather rhs + children's update vectors, solve the own unit-lower triangle
-__global__ void __launch_bounds__(256) k_fwd(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                             const double *__restrict__ arena, const double *__restrict__ rhs,
-                                             double *__restrict__ vec) {
-    __shared__ double Lp[64][65];
-    __shared__ double ts[64];
+// forward gather: v = [rhs of own rows; 0 on boundary rows] + the children's update vectors (slot 0
+// then slot 1: fixed order)
+__global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                    const double *__restrict__ rhs, double *__restrict__ vec) {
     int t = blockIdx.x;
     if (t >= ntask) return;
     int f = tasks[3 * t];
     int m = fd.m[f], s = fd.s[f];
-    const double *F = arena + fd.arena_off[f];
     const int32_t *rows = fd.rows + fd.rows_off[f];
     double *v = vec + fd.vec_off[f];
     for (int r = threadIdx.x; r < m; r += blockDim.x) v[r] = (r < s) ? rhs[rows[r]] : 0.0;
@@ -521,117 +718,111 @@ __global__ void __launch_bounds__(256) k_fwd(int ntask, const int32_t *__restric
         for (int i = threadIdx.x; i < uc; i += blockDim.x) v[bm[i]] += vc[i];
         __syncthreads();
     }
-    for (int k0 = 0; k0 < s; k0 += 64) {
-        int kb = min(64, s - k0);
-        for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
-            int j = idx / kb, i = idx % kb;
-            if (i > j) Lp[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
-        }
-        if (threadIdx.x < kb) ts[threadIdx.x] = v[k0 + threadIdx.x];
-        __syncthreads();
-        if (threadIdx.x < 64) {                     // wave 0: triangle
-            int lane = threadIdx.x;
-            double x = lane < kb ? ts[lane] : 0.0;
-            for (int j = 0; j < kb; j++) {
-                double yj = __shfl(x, j);
-                if (lane > j && lane < kb) x -= Lp[lane][j] * yj;
-            }
-            if (lane < kb) ts[lane] = x;
-        }
-        __syncthreads();
-        if (threadIdx.x < kb) v[k0 + threadIdx.x] = ts[threadIdx.x];
-        for (int i = k0 + kb + threadIdx.x; i < s; i += blockDim.x) {
-            double acc = 0.0;
-            for (int j = 0; j < kb; j++) acc += F[(int64_t)(k0 + j) * m + i] * ts[j];
-            v[i] -= acc;
-        }
-        __syncthreads();
-    }
 }
 
-// boundary rows: t_B -= L21 y
-__global__ void __launch_bounds__(256) k_fwd_gemv(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                                  const double *__restrict__ arena, double *__restrict__ vec) {
+// forward panel step (front f, panel k0): every task forms y_p = L_pp^{-1} v_p from the stored
+// panel inverse (64x64 GEMV from L2); task r0 == k0 publishes y_p, tasks r0 > k0 update the 64 rows
+// r0.. below the panel: v_r -= L[r, panel] y_p
+__global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                  const double *__restrict__ arena, const double *__restrict__ inv,
+                                                  double *__restrict__ vec, double *__restrict__ yvec) {
+    __shared__ double vs[64];
+    __shared__ double ys[64];
     __shared__ double red[4][64];
     int t = blockIdx.x;
     if (t >= ntask) return;
-    int f = tasks[3 * t], r0 = tasks[3 * t + 1];
+    int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
+    int kb = min(64, s - k0);
     const double *F = arena + fd.arena_off[f];
+    const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
     double *v = vec + fd.vec_off[f];
-    int lane = threadIdx.x % 64, part = threadIdx.x / 64;
-    int i = r0 + lane;
+    int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+    if (threadIdx.x < kb) vs[threadIdx.x] = v[k0 + threadIdx.x];
+    __syncthreads();
     double acc = 0.0;
-    if (i < m)
-        for (int c = part; c < s; c += 4) acc += F[(int64_t)c * m + i] * v[c];
+    if (lane < kb)
+        for (int j = part; j <= lane; j += 4) acc += Li[(int64_t)j * kb + lane] * vs[j];
     red[part][lane] = acc;
     __syncthreads();
-    if (part == 0 && i < m) v[i] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (threadIdx.x < 64) ys[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
+    if (r0 == k0) {
+        if (threadIdx.x < kb) yvec[fd.vec_off[f] + k0 + threadIdx.x] = ys[threadIdx.x];
+        return;
+    }
+    int r = r0 + lane;
+    acc = 0.0;
+    if (r < m)
+        for (int c = part; c < kb; c += 4) acc += F[(int64_t)(k0 + c) * m + r] * ys[c];
+    red[part][lane] = acc;
+    __syncthreads();
+    if (part == 0 && r < m) v[r] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-// backward, own columns c: r_c = y_c / d_c - sum_i L[i][c] x_B[i]
-__global__ void __launch_bounds__(256) k_bwd_gemv(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+// backward init (front f, own columns c0..c0+15): w_c = y_c / d_c - sum_{i >= s} L[i][c] x[rows[i]]
+__global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ x,
-                                                  double *__restrict__ vec) {
+                                                  const double *__restrict__ yvec, double *__restrict__ vec) {
     int t = blockIdx.x;
     if (t >= ntask) return;
     int f = tasks[3 * t], c0 = tasks[3 * t + 1];
     int m = fd.m[f], s = fd.s[f];
     const double *F = arena + fd.arena_off[f];
     const int32_t *rows = fd.rows + fd.rows_off[f];
-    double *v = vec + fd.vec_off[f];
-    int lane = threadIdx.x % 64, wv = threadIdx.x / 64;
-    int c1 = min(c0 + 64, s);
+    int64_t vo = fd.vec_off[f];
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int c1 = min(c0 + kBwdCols, s);
     for (int c = c0 + wv; c < c1; c += 4) {
         const double *col = F + (int64_t)c * m;
         double acc = 0.0;
         for (int i = s + lane; i < m; i += 64) acc += col[i] * x[rows[i]];
         for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-        if (lane == 0) v[c] = v[c] / col[c] - acc;
+        if (lane == 0) vec[vo + c] = yvec[vo + c] / col[c] - acc;
     }
 }
 
-// backward triangle: L11^T x = r (own), scatter x to the global solution
-__global__ void __launch_bounds__(256) k_bwd(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                             const double *__restrict__ arena, double *__restrict__ vec,
-                                             double *__restrict__ x) {
-    __shared__ double Lp[64][65];
-    __shared__ double ts[64];
+// backward panel step (front f, panel k0; panels run in descending order): every task forms
+// x_p = L_pp^{-T} w_p from the panel inverse; task q0 == k0 scatters x_p to the global solution,
+// tasks q0 < k0 update w[q0..q0+63] -= L[panel rows, q]^T x_p
+__global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                  const double *__restrict__ arena, const double *__restrict__ inv,
+                                                  double *__restrict__ vec, double *__restrict__ x) {
+    __shared__ double ws[64];
+    __shared__ double xs[64];
     int t = blockIdx.x;
     if (t >= ntask) return;
-    int f = tasks[3 * t];
+    int f = tasks[3 * t], k0 = tasks[3 * t + 1], q0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
+    int kb = min(64, s - k0);
     const double *F = arena + fd.arena_off[f];
-    const int32_t *rows = fd.rows + fd.rows_off[f];
-    double *v = vec + fd.vec_off[f];
-    int lane = threadIdx.x % 64, wv = threadIdx.x / 64;
-    int npan = (s + 63) / 64;
-    for (int p = npan - 1; p >= 0; p--) {
-        int k0 = p * 64, kb = min(64, s - k0);
-        // contributions of already-solved own rows below the panel
-        for (int c = k0 + wv; c < k0 + kb; c += 4) {
-            const double *col = F + (int64_t)c * m;
-            double acc = 0.0;
-            for (int i = k0 + kb + lane; i < s; i += 64) acc += col[i] * v[i];
-            for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-            if (lane == 0) ts[c - k0] = v[c] - acc;
-        }
-        for (int idx = threadIdx.x; idx < kb * kb; idx += blockDim.x) {
-            int j = idx / kb, i = idx % kb;
-            if (i > j) Lp[i][j] = F[(int64_t)(k0 + j) * m + k0 + i];
-        }
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            double xv = lane < kb ? ts[lane] : 0.0;
-            for (int j = kb - 1; j >= 0; j--) {
-                double xj = __shfl(xv, j);
-                if (lane < j) xv -= Lp[j][lane] * xj;
-            }
-            if (lane < kb) v[k0 + lane] = xv;
-        }
-        __syncthreads();
+    const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
+    double *w = vec + fd.vec_off[f];
+    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x < kb) ws[threadIdx.x] = w[k0 + threadIdx.x];
+    __syncthreads();
+    // x_i = sum_{j >= i} Linv[j][i] w_j: wave wv owns outputs i = wv*16 .. +15, lanes over j
+    double wl = lane < kb ? ws[lane] : 0.0;
+    for (int ii = 0; ii < 16; ii++) {
+        int i = wv * 16 + ii;
+        double p = (lane < kb && i < kb && lane >= i) ? Li[(int64_t)i * kb + lane] * wl : 0.0;
+        for (int off = 32; off > 0; off >>= 1) p += __shfl_down(p, off);
+        if (lane == 0) xs[i] = p;
     }
-    for (int r = threadIdx.x; r < s; r += blockDim.x) x[rows[r]] = v[r];
+    __syncthreads();
+    if (q0 == k0) {
+        const int32_t *rows = fd.rows + fd.rows_off[f];
+        if (threadIdx.x < kb) x[rows[k0 + threadIdx.x]] = xs[threadIdx.x];
+        return;
+    }
+    // 4 waves x 16 columns; lanes over the kb panel rows
+    double xl = lane < kb ? xs[lane] : 0.0;
+    for (int cc = 0; cc < 16; cc++) {
+        int q = q0 + wv * 16 + cc;
+        double p = lane < kb ? F[(int64_t)q * m + k0 + lane] * xl : 0.0;
+        for (int off = 32; off > 0; off >>= 1) p += __shfl_down(p, off);
+        if (lane == 0) w[q] -= p;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -757,7 +948,7 @@ static hipEvent_t prof_event() {
         if (g_prof) {                                                                \
             hipEvent_t e1_ = prof_event();                                           \
             hipEventRecord(e1_, ST);                                                 \
-            g_prof->recs.push_back({NAME, e0_, e1_});                                \
+            g_prof->recs.push_back({NAME, e0_, e1_, dim3(GRID).x});                  \
         }                                                                            \
     } while (0)
 
@@ -784,12 +975,18 @@ void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
     if (L.nblocks > 0)
         LAUNCH("hfinal", dev::k_hfinal, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks,
                            L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
+    if (L.nheavy_h > 0)
+        LAUNCH("hfinal_heavy", dev::k_hfinal_heavy, dim3((unsigned)L.nheavy_h), dim3(256), st, L.heavy_h,
+                           L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
     if (L.nbchunks > 0)
         LAUNCH("bchunk", dev::k_bchunk, dim3(nb(L.nbchunks, 128)), dim3(128), st, L.nbchunks, L.bcontrib,
                            L.bchunk_begin, L.bchunk_len, ej, L.bpart);
     if (L.nv > 0)
         LAUNCH("bfinal", dev::k_bfinal, dim3(nb(L.nv, 128)), dim3(128), st, L.nv, L.bv_chunk_begin, L.voff,
                            L.vdim, L.bpart, L.b);
+    if (L.nheavy_b > 0)
+        LAUNCH("bfinal_heavy", dev::k_bfinal_heavy, dim3((unsigned)L.nheavy_b), dim3(256), st, L.heavy_b,
+                           L.bv_chunk_begin, L.voff, L.vdim, L.bpart, L.b);
 }
 
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
@@ -809,13 +1006,14 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
         for (const auto &stp : lv.steps) {
             if (stp.ndiag > 0)
                 LAUNCH("diag", dev::k_diag, dim3(stp.ndiag), dim3(256), st, stp.ndiag, L.tasks + 3 * stp.diag_off,
-                                   L.fd, L.arena, L.flag);
+                                   L.fd, L.arena, L.inv, L.flag);
             if (stp.ntrsm > 0)
-                LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(64), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
-                                   L.fd, L.arena);
+                LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(256), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
+                                   L.fd, L.arena, L.inv);
             if (stp.nupd > 0)
-                LAUNCH("update", dev::k_update, dim3(stp.nupd), dim3(256), st, stp.nupd, L.tasks + 3 * stp.upd_off,
-                                   stp.k0, L.fd, L.arena);
+                LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), st, stp.nupd,
+                       L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
+                       L.arena, L.inv, L.flag);
         }
     }
 }
@@ -824,20 +1022,22 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         if (lv.nfwd > 0)
-            LAUNCH("fwd", dev::k_fwd, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
-                               L.arena, rhs, L.vec);
-        if (lv.ngemv > 0)
-            LAUNCH("fwd_gemv", dev::k_fwd_gemv, dim3(lv.ngemv), dim3(256), st, lv.ngemv, L.tasks + 3 * lv.gemv_off,
-                               L.fd, L.arena, L.vec);
+            LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off,
+                   L.fd, rhs, L.vec);
+        for (const auto &sp : lv.fsteps)
+            if (sp.n > 0)
+                LAUNCH("fwd_step", dev::k_fwd_step, dim3(sp.n), dim3(256), st, sp.n, L.tasks + 3 * sp.off, L.fd,
+                       L.arena, L.inv, L.vec, L.yvec);
     }
     for (size_t hh = L.levels.size(); hh-- > 0;) {
         const auto &lv = L.levels[hh];
         if (lv.nbgemv > 0)
-            LAUNCH("bwd_gemv", dev::k_bwd_gemv, dim3(lv.nbgemv), dim3(256), st, lv.nbgemv,
-                               L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.vec);
-        if (lv.nfwd > 0)
-            LAUNCH("bwd", dev::k_bwd, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off, L.fd,
-                               L.arena, L.vec, x);
+            LAUNCH("bwd_init", dev::k_bwd_init, dim3(lv.nbgemv), dim3(256), st, lv.nbgemv,
+                   L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.yvec, L.vec);
+        for (const auto &sp : lv.bsteps)
+            if (sp.n > 0)
+                LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n), dim3(256), st, sp.n, L.tasks + 3 * sp.off, L.fd,
+                       L.arena, L.inv, L.vec, x);
     }
 }
 

@@ -40,6 +40,20 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
     }
     auto Fp = [&](int32_t f) { return arena.data() + S.fronts[f].arena_off; };
     const int32_t *T = S.task_i32.data();
+    auto diag = [&](int f, int k0) -> bool {
+        const Front &F = S.fronts[f];
+        double *A = Fp(f);
+        int kb = std::min(64, F.s - k0), m = F.m;
+        for (int j = 0; j < kb; j++) {
+            double d = A[(int64_t)(k0 + j) * m + k0 + j];
+            if (d == 0.0) return false;
+            for (int i = j + 1; i < kb; i++) A[(int64_t)(k0 + j) * m + k0 + i] /= d;
+            for (int c = j + 1; c < kb; c++)
+                for (int i = c; i < kb; i++)
+                    A[(int64_t)(k0 + c) * m + k0 + i] -= A[(int64_t)(k0 + j) * m + k0 + i] * d * A[(int64_t)(k0 + j) * m + k0 + c];
+        }
+        return true;
+    };
     for (const auto &lv : S.levels) {
         for (int slot = 0; slot < 2; slot++)
             for (int32_t t = 0; t < lv.nea[slot]; t++) {
@@ -56,18 +70,7 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
         for (const auto &st : lv.steps) {
             for (int32_t t = 0; t < st.ndiag; t++) {
                 const int32_t *tk = T + 3 * (st.diag_off + t);
-                int f = tk[0], k0 = tk[1];
-                const Front &F = S.fronts[f];
-                double *A = Fp(f);
-                int kb = std::min(64, F.s - k0), m = F.m;
-                for (int j = 0; j < kb; j++) {
-                    double d = A[(int64_t)(k0 + j) * m + k0 + j];
-                    if (d == 0.0) return -1;
-                    for (int i = j + 1; i < kb; i++) A[(int64_t)(k0 + j) * m + k0 + i] /= d;
-                    for (int c = j + 1; c < kb; c++)
-                        for (int i = c; i < kb; i++)
-                            A[(int64_t)(k0 + c) * m + k0 + i] -= A[(int64_t)(k0 + j) * m + k0 + i] * d * A[(int64_t)(k0 + j) * m + k0 + c];
-                }
+                if (!diag(tk[0], tk[1])) return -1;
             }
             for (int32_t t = 0; t < st.ntrsm; t++) {
                 const int32_t *tk = T + 3 * (st.trsm_off + t);
@@ -90,8 +93,9 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                 int f = tk[0], ti = tk[1], tj = tk[2];
                 const Front &F = S.fronts[f];
                 double *A = Fp(f);
-                int k0 = st.k0, kb = std::min(64, F.s - k0), m = F.m;
-                for (int c = tj; c < std::min(tj + 64, m); c++)
+                int k0 = st.kA, kb = std::min(st.kmax, F.s - k0), m = F.m;
+                int cend = st.inner ? std::min(F.s, (k0 / kOuter + 1) * kOuter) : m;
+                for (int c = tj; c < std::min(tj + 64, cend); c++)
                     for (int r = ti; r < std::min(ti + 64, m); r++) {
                         double acc = 0;
                         for (int k = 0; k < kb; k++)
@@ -99,14 +103,26 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                         A[(int64_t)c * m + r] -= acc;
                     }
             }
+            // fused panel factorization of the next panel (k_update on the diagonal tile)
+            for (int32_t t = 0; t < st.nupd; t++) {
+                const int32_t *tk = T + 3 * (st.upd_off + t);
+                const Front &F = S.fronts[tk[0]];
+                int k1 = st.kA + std::min(st.kmax, F.s - st.kA);
+                if (tk[1] == tk[2] && tk[1] == k1 && F.s > k1 && !diag(tk[0], k1)) return -1;
+            }
         }
     }
-    // forward
+    // forward: gather, then panel steps (same task semantics as k_fwd_gather / k_fwd_step)
+    std::vector<double> yv((size_t)S.vec_size, 0.0);
+    auto lower_solve = [&](const Front &F, const double *A, int k0, int kb, const double *b, double *y) {
+        for (int i = 0; i < kb; i++) y[i] = b[i];
+        for (int j = 0; j < kb; j++)
+            for (int i = j + 1; i < kb; i++) y[i] -= A[(int64_t)(k0 + j) * F.m + k0 + i] * y[j];
+    };
     for (const auto &lv : S.levels) {
         for (int32_t t = 0; t < lv.nfwd; t++) {
             int f = T[3 * (lv.fwd_off + t)];
             const Front &F = S.fronts[f];
-            const double *A = Fp(f);
             double *v = vec.data() + F.vec_off;
             const int32_t *rows = S.rows.data() + F.rows_off;
             for (int r = 0; r < F.m; r++) v[r] = r < F.s ? rhs[rows[r]] : 0.0;
@@ -115,18 +131,31 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                 const int32_t *bm = S.bmap.data() + C.bmap_off;
                 for (int i = 0; i < C.m - C.s; i++) v[bm[i]] += vec[C.vec_off + C.s + i];
             }
-            for (int j = 0; j < F.s; j++)
-                for (int i = j + 1; i < F.s; i++) v[i] -= A[(int64_t)j * F.m + i] * v[j];
         }
-        for (int32_t t = 0; t < lv.ngemv; t++) {
-            const int32_t *tk = T + 3 * (lv.gemv_off + t);
-            const Front &F = S.fronts[tk[0]];
-            const double *A = Fp(tk[0]);
-            double *v = vec.data() + F.vec_off;
-            for (int i = tk[1]; i < std::min(tk[1] + 64, F.m); i++) {
-                double acc = 0;
-                for (int c = 0; c < F.s; c++) acc += A[(int64_t)c * F.m + i] * v[c];
-                v[i] -= acc;
+        for (const auto &sp : lv.fsteps) {
+            // all tasks of a step read the panel rows before any task writes (device: one launch)
+            std::vector<std::vector<double>> ys(sp.n);
+            for (int32_t t = 0; t < sp.n; t++) {
+                const int32_t *tk = T + 3 * (sp.off + t);
+                const Front &F = S.fronts[tk[0]];
+                int k0 = tk[1], kb = std::min(64, F.s - k0);
+                ys[t].resize(kb);
+                lower_solve(F, Fp(tk[0]), k0, kb, vec.data() + F.vec_off + k0, ys[t].data());
+            }
+            for (int32_t t = 0; t < sp.n; t++) {
+                const int32_t *tk = T + 3 * (sp.off + t);
+                const Front &F = S.fronts[tk[0]];
+                const double *A = Fp(tk[0]);
+                int k0 = tk[1], r0 = tk[2], kb = std::min(64, F.s - k0);
+                if (r0 == k0) {
+                    for (int i = 0; i < kb; i++) yv[F.vec_off + k0 + i] = ys[t][i];
+                    continue;
+                }
+                for (int r = r0; r < std::min(r0 + 64, F.m); r++) {
+                    double acc = 0;
+                    for (int c = 0; c < kb; c++) acc += A[(int64_t)(k0 + c) * F.m + r] * ys[t][c];
+                    vec[F.vec_off + r] -= acc;
+                }
             }
         }
     }
@@ -137,26 +166,41 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
             const int32_t *tk = T + 3 * (lv.bgemv_off + t);
             const Front &F = S.fronts[tk[0]];
             const double *A = Fp(tk[0]);
-            double *v = vec.data() + F.vec_off;
             const int32_t *rows = S.rows.data() + F.rows_off;
-            for (int c = tk[1]; c < std::min(tk[1] + 64, F.s); c++) {
+            for (int c = tk[1]; c < std::min(tk[1] + kBwdCols, F.s); c++) {
                 double acc = 0;
                 for (int i = F.s; i < F.m; i++) acc += A[(int64_t)c * F.m + i] * x[rows[i]];
-                v[c] = v[c] / A[(int64_t)c * F.m + c] - acc;
+                vec[F.vec_off + c] = yv[F.vec_off + c] / A[(int64_t)c * F.m + c] - acc;
             }
         }
-        for (int32_t t = 0; t < lv.nfwd; t++) {
-            int f = T[3 * (lv.fwd_off + t)];
-            const Front &F = S.fronts[f];
-            const double *A = Fp(f);
-            double *v = vec.data() + F.vec_off;
-            const int32_t *rows = S.rows.data() + F.rows_off;
-            for (int j = F.s - 1; j >= 0; j--) {
-                double acc = v[j];
-                for (int i = j + 1; i < F.s; i++) acc -= A[(int64_t)j * F.m + i] * v[i];
-                v[j] = acc;
+        for (const auto &sp : lv.bsteps) {
+            std::vector<std::vector<double>> xs(sp.n);
+            for (int32_t t = 0; t < sp.n; t++) {
+                const int32_t *tk = T + 3 * (sp.off + t);
+                const Front &F = S.fronts[tk[0]];
+                const double *A = Fp(tk[0]);
+                int k0 = tk[1], kb = std::min(64, F.s - k0);
+                std::vector<double> &xp = xs[t];
+                xp.assign(vec.begin() + F.vec_off + k0, vec.begin() + F.vec_off + k0 + kb);
+                for (int j = kb - 1; j >= 0; j--)
+                    for (int i = 0; i < j; i++) xp[i] -= A[(int64_t)(k0 + i) * F.m + k0 + j] * xp[j];
             }
-            for (int r = 0; r < F.s; r++) x[rows[r]] = v[r];
+            for (int32_t t = 0; t < sp.n; t++) {
+                const int32_t *tk = T + 3 * (sp.off + t);
+                const Front &F = S.fronts[tk[0]];
+                const double *A = Fp(tk[0]);
+                int k0 = tk[1], q0 = tk[2], kb = std::min(64, F.s - k0);
+                if (q0 == k0) {
+                    const int32_t *rows = S.rows.data() + F.rows_off;
+                    for (int i = 0; i < kb; i++) x[rows[k0 + i]] = xs[t][i];
+                    continue;
+                }
+                for (int q = q0; q < q0 + 64; q++) {
+                    double acc = 0;
+                    for (int i = 0; i < kb; i++) acc += A[(int64_t)q * F.m + k0 + i] * xs[t][i];
+                    vec[F.vec_off + q] -= acc;
+                }
+            }
         }
     }
     return 0;

@@ -15,6 +15,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -282,25 +283,38 @@ int upload_device(deftri_ctx *ctx) {
     PUT(L.bcontrib, S.bcontrib); PUT(L.bchunk_begin, S.bchunk_begin); PUT(L.bchunk_len, S.bchunk_len);
     PUT(L.bv_chunk_begin, S.bv_chunk_begin);
     if ((rc = dalloc(ctx, &L.bpart, 6 * L.nbchunks))) return rc;
+    {
+        std::vector<int64_t> hh, hb;
+        for (int64_t b = 0; b < S.nblocks; b++)
+            if (S.hblk_chunk_begin[b + 1] - S.hblk_chunk_begin[b] > kHeavyChunks) hh.push_back(b);
+        for (int64_t v = 0; v < S.nv; v++)
+            if (S.bv_chunk_begin[v + 1] - S.bv_chunk_begin[v] > kHeavyChunks) hb.push_back(v);
+        L.nheavy_h = (int64_t)hh.size(); L.nheavy_b = (int64_t)hb.size();
+        if (!hh.empty()) PUT(L.heavy_h, hh);
+        if (!hb.empty()) PUT(L.heavy_b, hb);
+    }
     if ((rc = dalloc(ctx, &L.b, S.ndof))) return rc;
     L.arena_size = S.arena_size; L.vec_size = S.vec_size;
     if ((rc = dalloc(ctx, &L.arena, S.arena_size))) return rc;
     if ((rc = dalloc(ctx, &L.vec, S.vec_size))) return rc;
+    if ((rc = dalloc(ctx, &L.yvec, S.vec_size))) return rc;
+    L.inv_size = S.inv_size;
+    if ((rc = dalloc(ctx, &L.inv, S.inv_size))) return rc;
     {
         int32_t nf = (int32_t)S.fronts.size();
         std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf);
-        std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf);
+        std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf), io(nf);
         for (int32_t f = 0; f < nf; f++) {
             const Front &F = S.fronts[f];
             m[f] = F.m; s[f] = F.s; par[f] = F.parent; nch[f] = F.nchild; c0[f] = F.child[0]; c1[f] = F.child[1];
-            ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off;
+            ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off; io[f] = F.inv_off;
         }
         int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *prows, *pbmap;
-        int64_t *pao, *pvo, *pro, *pbo;
+        int64_t *pao, *pvo, *pro, *pbo, *pio;
         PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1);
-        PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo);
+        PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo); PUT(pio, io);
         PUT(prows, S.rows); PUT(pbmap, S.bmap);
-        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pao, pvo, pro, pbo, prows, pbmap};
+        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pao, pvo, pro, pbo, pio, prows, pbmap};
     }
     PUT(L.tasks, S.task_i32);
     L.levels.clear();
@@ -308,9 +322,10 @@ int upload_device(deftri_ctx *ctx) {
         LevelDev ld{};
         for (int k = 0; k < 2; k++) { ld.ea_off[k] = lv.ea_off[k]; ld.nea[k] = lv.nea[k]; }
         for (const auto &stp : lv.steps)
-            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0});
+            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner});
         ld.fwd_off = lv.fwd_off; ld.nfwd = lv.nfwd;
-        ld.gemv_off = lv.gemv_off; ld.ngemv = lv.ngemv;
+        for (const auto &x : lv.fsteps) ld.fsteps.push_back({x.off, x.n});
+        for (const auto &x : lv.bsteps) ld.bsteps.push_back({x.off, x.n});
         ld.bgemv_off = lv.bgemv_off; ld.nbgemv = lv.nbgemv;
         L.levels.push_back(ld);
     }
@@ -457,9 +472,11 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     set_profiler(nullptr);
     HIPOK(hipStreamSynchronize(ctx->st));
     int32_t n = 0;
+    const bool dump = std::getenv("DEFTRI_PROFILE_DUMP") != nullptr;
     for (const auto &r : prof.recs) {
         float ms = 0;
         hipEventElapsedTime(&ms, r.e0, r.e1);
+        if (dump) std::fprintf(stderr, "[prof] %s %u %.4f\n", r.name, r.grid, ms);
         int32_t k = 0;
         for (; k < n; k++) if (std::strcmp(stats[k].name, r.name) == 0) break;
         if (k == n) {

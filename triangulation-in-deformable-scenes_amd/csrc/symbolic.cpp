@@ -169,7 +169,7 @@ struct Builder {
         // rows, sizes, offsets
         std::vector<std::vector<int64_t>> fv(nf);       // vertex list (row order)
         std::vector<std::vector<int32_t>> fvrow(nf);    // local row of each vertex
-        int64_t aoff = 0, voff2 = 0;
+        int64_t aoff = 0, voff2 = 0, ioff = 0;
         for (int32_t f = 0; f < nf; f++) {
             Front &F = S.fronts[f];
             fv[f] = own[f];
@@ -186,12 +186,15 @@ struct Builder {
             F.m = m; F.s = s;
             F.arena_off = aoff; aoff += (int64_t)m * m;
             F.vec_off = voff2; voff2 += m;
+            F.inv_off = ioff;
+            if (s > 0) ioff += (int64_t)((s - 1) / kPanel) * kPanel * kPanel + (int64_t)((s - 1) % kPanel + 1) * ((s - 1) % kPanel + 1);
             double sd = s, ud = m - s;
             S.factor_flops += sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
             S.nnz_factor += (int64_t)s * (s + 1) / 2 + (int64_t)(m - s) * s;
         }
         S.arena_size = aoff;
         S.vec_size = voff2;
+        S.inv_size = ioff;
         auto local_row = [&](int32_t f, int64_t v) -> int32_t {
             const auto &L = fv[f];
             int64_t pv = S.elim_pos[v];
@@ -356,52 +359,105 @@ struct Builder {
             }
             int32_t maxs = 0;
             for (int32_t f : fs) maxs = std::max(maxs, S.fronts[f].s);
-            for (int32_t k0 = 0; k0 < maxs; k0 += kPanel) {
-                Symbolic::StepTasks st;
-                st.k0 = k0;
-                st.diag_off = (int64_t)S.task_i32.size() / 3;
-                for (int32_t f : fs) if (S.fronts[f].s > k0) {
-                    push3(f, k0, 0); st.ndiag++;
-                    double kb = std::min(kPanel, S.fronts[f].s - k0);
-                    S.diag_flops += kb * kb * kb / 3.0;
-                }
-                st.trsm_off = (int64_t)S.task_i32.size() / 3;
-                for (int32_t f : fs) {
-                    const Front &F = S.fronts[f];
-                    if (F.s <= k0) continue;
-                    int32_t kb = std::min(kPanel, F.s - k0);
-                    for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) {
-                        push3(f, k0, r0); st.ntrsm++;
-                        S.trsm_flops += (double)std::min(64, F.m - r0) * kb * kb;
-                    }
-                }
+            // two-level right-looking schedule.  Outer blocks of kOuter own columns; inside one, each
+            // 64-wide panel k0 gets [diag (k0 == 0 only; later panels are factored by the update
+            // launch that finishes their diagonal tile)] + trsm + an inner update restricted to the
+            // block's remaining own columns; after the block, one outer update with K = the block
+            // width covers every trailing column (own and contribution block).
+            auto push_update = [&](Symbolic::StepTasks &st, int32_t kA, int32_t kmax, bool inner) {
                 st.upd_off = (int64_t)S.task_i32.size() / 3;
+                st.kA = kA; st.kmax = kmax; st.inner = inner ? 1 : 0;
+                // pass 0: the tiles that carry a fused panel factorization go first in the launch
+                for (int pass = 0; pass < 2; pass++)
+                    for (int32_t f : fs) {
+                        const Front &F = S.fronts[f];
+                        if (F.s <= kA) continue;
+                        int32_t K = std::min(kmax, F.s - kA);
+                        int32_t t0 = kA + K;
+                        int32_t tend = inner ? std::min(F.s, (kA / kOuter + 1) * kOuter) : F.m;
+                        if (inner && t0 >= tend) continue;
+                        bool has_diag = F.s > t0;
+                        if (pass == 0) {
+                            if (has_diag) { push3(f, t0, t0); st.nupd++; }
+                            continue;
+                        }
+                        for (int32_t tj = t0; tj < tend; tj += 64)
+                            for (int32_t ti = tj; ti < F.m; ti += 64) {
+                                if (has_diag && ti == t0 && tj == t0) continue;
+                                push3(f, ti, tj); st.nupd++;
+                            }
+                    }
                 for (int32_t f : fs) {
                     const Front &F = S.fronts[f];
-                    if (F.s <= k0) continue;
-                    int32_t kb = std::min(kPanel, F.s - k0);
-                    int32_t t0 = k0 + kb;
-                    for (int32_t ti = t0; ti < F.m; ti += 64)
-                        for (int32_t tj = t0; tj <= ti; tj += 64) {
-                            push3(f, ti, tj);      // k0 recovered from step (same for all tasks)
-                            st.nupd++;
-                            S.update_flops += 2.0 * std::min(64, F.m - ti) * std::min(64, F.m - tj) * kb;
-                        }
+                    if (F.s <= kA) continue;
+                    int32_t K = std::min(kmax, F.s - kA);
+                    int32_t t0 = kA + K;
+                    int32_t tend = inner ? std::min(F.s, (kA / kOuter + 1) * kOuter) : F.m;
+                    for (int32_t tj = t0; tj < tend; tj += 64)
+                        for (int32_t ti = tj; ti < F.m; ti += 64)
+                            S.update_flops += 2.0 * std::min(64, F.m - ti) * std::min(64, F.m - tj) * K;
                 }
-                LT.steps.push_back(st);
+            };
+            for (int32_t P0 = 0; P0 < maxs; P0 += kOuter) {
+                for (int32_t k0 = P0; k0 < std::min(maxs, P0 + kOuter); k0 += kPanel) {
+                    Symbolic::StepTasks st;
+                    st.k0 = k0;
+                    st.diag_off = (int64_t)S.task_i32.size() / 3;
+                    for (int32_t f : fs) if (S.fronts[f].s > k0) {
+                        if (k0 == 0) { push3(f, k0, 0); st.ndiag++; }
+                        double kb = std::min(kPanel, S.fronts[f].s - k0);
+                        S.diag_flops += kb * kb * kb / 3.0;
+                    }
+                    st.trsm_off = (int64_t)S.task_i32.size() / 3;
+                    for (int32_t f : fs) {
+                        const Front &F = S.fronts[f];
+                        if (F.s <= k0) continue;
+                        int32_t kb = std::min(kPanel, F.s - k0);
+                        for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) {
+                            push3(f, k0, r0); st.ntrsm++;
+                            S.trsm_flops += (double)std::min(64, F.m - r0) * kb * kb;
+                        }
+                    }
+                    push_update(st, k0, kPanel, true);
+                    LT.steps.push_back(st);
+                }
+                Symbolic::StepTasks so;
+                so.k0 = P0;
+                so.diag_off = so.trsm_off = (int64_t)S.task_i32.size() / 3;
+                push_update(so, P0, kOuter, false);
+                LT.steps.push_back(so);
             }
             LT.fwd_off = (int64_t)S.task_i32.size() / 3;
             for (int32_t f : fs) { push3(f, 0, 0); LT.nfwd++; }
-            LT.gemv_off = (int64_t)S.task_i32.size() / 3;
-            for (int32_t f : fs) {
-                const Front &F = S.fronts[f];
-                if (F.s == 0) continue;
-                for (int32_t r0 = F.s; r0 < F.m; r0 += 64) { push3(f, r0, 0); LT.ngemv++; }
+            for (int32_t k0 = 0; k0 < maxs; k0 += kPanel) {
+                Symbolic::LevelTasks::SolveStep st;
+                st.off = (int64_t)S.task_i32.size() / 3;
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.s <= k0) continue;
+                    int32_t kb = std::min(kPanel, F.s - k0);
+                    push3(f, k0, k0); st.n++;
+                    for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) { push3(f, k0, r0); st.n++; }
+                }
+                LT.fsteps.push_back(st);
             }
             LT.bgemv_off = (int64_t)S.task_i32.size() / 3;
             for (int32_t f : fs) {
                 const Front &F = S.fronts[f];
-                for (int32_t c0 = 0; c0 < F.s; c0 += 64) { push3(f, c0, 0); LT.nbgemv++; }
+                for (int32_t c0 = 0; c0 < F.s; c0 += kBwdCols) { push3(f, c0, 0); LT.nbgemv++; }
+            }
+            int32_t npan = (maxs + kPanel - 1) / kPanel;
+            for (int32_t p = npan - 1; p >= 0; p--) {
+                int32_t k0 = p * kPanel;
+                Symbolic::LevelTasks::SolveStep st;
+                st.off = (int64_t)S.task_i32.size() / 3;
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.s <= k0) continue;
+                    push3(f, k0, k0); st.n++;
+                    for (int32_t q0 = 0; q0 < k0; q0 += 64) { push3(f, k0, q0); st.n++; }
+                }
+                LT.bsteps.push_back(st);
             }
         }
         return true;

@@ -30,13 +30,17 @@ static inline uint64_t contrib_pack(int kind, int64_t edge, int role_col, int ro
 }
 
 constexpr int kPanel = 64;          // panel width of the blocked dense kernels
+constexpr int kOuter = 256;         // outer block: trailing updates beyond it use K = 256
 constexpr int kChunk = 128;         // contributions per gather chunk
+constexpr int kBwdCols = 16;        // own columns per backward-init task
 
 struct Front {
     int64_t arena_off;   // m*m doubles, column-major, ld = m
     int64_t vec_off;     // m doubles of solve workspace
     int64_t rows_off;    // m entries of `rows` (problem dof of each local row)
     int64_t bmap_off;    // (m - s) entries of `bmap` (local row in the parent front)
+    int64_t inv_off;     // inverses of the unit-lower panel triangles: panel p at inv_off + p*64*64
+                         // (kb x kb, column-major, ld = kb)
     int32_t m, s;
     int32_t parent;
     int32_t height;
@@ -54,7 +58,7 @@ struct Symbolic {
     std::vector<Front> fronts;
     std::vector<int32_t> rows;
     std::vector<int32_t> bmap;
-    int64_t arena_size = 0, vec_size = 0;
+    int64_t arena_size = 0, vec_size = 0, inv_size = 0;
     int32_t nlevels = 0;
     std::vector<std::vector<int32_t>> level_fronts;   // by height, ascending
     double factor_flops = 0;
@@ -86,14 +90,22 @@ struct Symbolic {
         int64_t diag_off = 0; int32_t ndiag = 0;      // fronts with own cols at this panel
         int64_t trsm_off = 0; int32_t ntrsm = 0;      // (front, row-tile) pairs
         int64_t upd_off = 0; int32_t nupd = 0;        // (front, tile-i, tile-j) triples
-        int32_t k0 = 0;
+        int32_t k0 = 0;                               // panel of diag / trsm
+        int32_t kA = 0, kmax = 0;                     // update: L columns [kA, kA + min(kmax, s - kA))
+        int32_t inner = 0;                            // 1: columns clipped at the outer block end
     };
     struct LevelTasks {
         int64_t ea_off[2] = {0, 0}; int32_t nea[2] = {0, 0};   // extend-add (child slot 0/1): (parent, child col)
         std::vector<StepTasks> steps;
-        int64_t fwd_off = 0; int32_t nfwd = 0;                 // fronts
-        int64_t gemv_off = 0; int32_t ngemv = 0;               // (front, row-tile) for boundary update
-        int64_t bgemv_off = 0; int32_t nbgemv = 0;             // (front, col-tile) for backward L21^T x
+        // substitution: forward = gather (one task per front) then one launch per panel step with
+        // (front, k0, r0) tasks — r0 == k0: solve the panel triangle and publish y; r0 > k0: rows
+        // r0..r0+63 below the panel -= L[r, panel] y.  Backward = init (front, c0: 16 own columns,
+        // w = y/d - L21^T x_B) then panel steps in descending order with (front, k0, q0) tasks —
+        // q0 == k0: solve L_pp^T x = w_p and scatter x; q0 < k0: w[q0..q0+63] -= L[panel, q]^T x_p.
+        int64_t fwd_off = 0; int32_t nfwd = 0;                 // fronts (gather)
+        struct SolveStep { int64_t off = 0; int32_t n = 0; };
+        std::vector<SolveStep> fsteps, bsteps;                 // bsteps: already in execution order
+        int64_t bgemv_off = 0; int32_t nbgemv = 0;             // (front, c0) backward init, 16 columns each
     };
     std::vector<LevelTasks> levels;
     std::vector<int32_t> task_i32;     // flat task storage (3 ints per task record)
