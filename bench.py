@@ -77,6 +77,18 @@ def cpu_baseline(n_full, full_flops, gpu_trials_per_iter, n_sample=10000):
                       f"{gpu_trials_per_iter:.2f} trials/iteration"}
 
 
+def reduce_stats(dt, iters, trials, world, device):
+    """Whole-job numbers from per-rank ones: max wall time over ranks, summed iterations/trials.
+    The replicas share nothing else (no data-path collective)."""
+    if world <= 1:
+        return dt, iters, trials
+    v = torch.tensor([dt], dtype=torch.float64, device=device)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    s = torch.tensor([iters, trials], dtype=torch.float64, device=device)
+    dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return float(v.item()), int(s[0].item()), int(s[1].item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -123,13 +135,7 @@ def main():
     if iters != args.steps:
         log(f"[rank {rank}] WARNING: LM terminated after {iters} of {args.steps} iterations")
 
-    t_max, it_sum, tr_sum = dt, iters, rep["trials_total"]
-    if world > 1:
-        v = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        s = torch.tensor([iters, rep["trials_total"]], dtype=torch.float64, device="cuda")
-        dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        t_max, it_sum, tr_sum = float(v.item()), int(s[0].item()), int(s[1].item())
+    t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, "cuda")
 
     # profiled trial (HIP events on the solver stream), at the final lambda of the timed run
     stats = ctx.profile_trial(rep["lambda_final"])
