@@ -9,7 +9,11 @@ if os.environ.get("DEFTRI_PROF_CHILD") is None:
     print(r.stdout)
     if r.returncode:
         print(r.stderr[-3000:]); sys.exit(r.returncode)
-    seq = [(n, int(g), float(ms)) for _, n, g, ms in rows]
+    seq = [(n, int(g), float(ms)) for _, n, g, ms, _w in rows]
+    upd = [(int(g), float(ms), float(w)) for _, n, g, ms, w in rows if n == "update"]
+    print("update launches (grid, us, GF, TF/s), in order:")
+    for i, (g, ms, w) in enumerate(upd):
+        print(f"  {i:3d} grid {g:6d} {1e3 * ms:9.1f} us {w / 1e9:8.3f} GF {w / (ms * 1e-3) / 1e12:6.2f} TF/s")
     agg = collections.defaultdict(lambda: [0, 0.0])
     for n, g, ms in seq:
         b = 1 if g <= 4 else 16 if g <= 64 else 256 if g <= 512 else 4096 if g <= 4096 else 10**9

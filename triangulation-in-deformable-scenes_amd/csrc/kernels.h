@@ -40,7 +40,7 @@ struct FrontDev {
 
 struct LevelDev {
     int64_t ea_off[2]; int32_t nea[2];
-    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner; };
+    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner; double upd_flops; };
     std::vector<Step> steps;
     int64_t fwd_off; int32_t nfwd;
     struct SolveStep { int64_t off; int32_t n; };
@@ -83,7 +83,7 @@ struct DevPlan {
 };
 
 // per-launch device timing for deftri_profile_trial (never active on the solve path)
-struct KProfRec { const char *name; hipEvent_t e0, e1; unsigned grid; };
+struct KProfRec { const char *name; hipEvent_t e0, e1; unsigned grid; double work; };
 struct KProf {
     std::vector<hipEvent_t> pool;
     size_t next = 0;

@@ -427,6 +427,15 @@ __global__ void k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDe
     }
 }
 
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __builtin_amdgcn_readlane(p.x, lane);
+    p.y = __builtin_amdgcn_readlane(p.y, lane);
+    return __builtin_bit_cast(double, p);
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -446,73 +455,113 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], double (*T)[48], int
     for (int sp = 0; sp < 4; sp++) {
         const int j0 = 16 * sp;
         if (wv == 0) {
-            const int r = lane & 15, g = lane >> 4;
-            for (int j = 0; j < 16; j++) {
-                double d = S[j0 + j][j0 + j];
-                if (lane == 0 && d == 0.0) atomicOr(flag, 1);
-                if (g == 0 && r > j) S[j0 + r][j0 + j] = S[j0 + r][j0 + j] / d;
-                wave_sync();
-                if (r > j) {
-                    double li = S[j0 + r][j0 + j];
-                    double lid = li * d;
-                    for (int c = j + 1 + g; c <= r; c += 4) S[j0 + r][j0 + c] -= lid * S[j0 + c][j0 + j];
-                    for (int c = g; c <= j; c += 4) {
-                        double xjc = (c == j) ? 1.0 : S[j0 + c][j0 + j];      // X[j][c]
-                        S[j0 + c][j0 + r] -= li * xjc;                        // X[r][c]
-                    }
-                }
-                wave_sync();
+            // 16x16 diagonal sub-block in registers: lane r (mod 16) holds row r of A and of
+            // X = L^{-1}; the pivot column / X row are broadcast with v_readlane (unrolled: every
+            // lane and register index is a constant)
+            const int r = lane & 15;
+            double a[16], x[16];
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                a[c] = (c <= r) ? S[j0 + r][j0 + c] : 0.0;
+                x[c] = (c == r) ? 1.0 : 0.0;
             }
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const double d = readlane_d(a[j], j);
+                if (lane == 0 && d == 0.0) atomicOr(flag, 1);
+                const double l = (r > j) ? a[j] / d : a[j];
+                a[j] = l;
+                const double ld = l * d;
+#pragma unroll
+                for (int c = j + 1; c < 16; c++) {
+                    const double lc = readlane_d(l, c);
+                    if (r >= c) a[c] -= ld * lc;
+                }
+#pragma unroll
+                for (int c = 0; c <= j; c++) {
+                    const double xjc = readlane_d(x[c], j);
+                    if (r > j) x[c] -= l * xjc;
+                }
+            }
+            if (lane < 16)
+#pragma unroll
+                for (int c = 0; c < 16; c++) {
+                    if (c <= r) S[j0 + r][j0 + c] = a[c];
+                    if (c < r) S[j0 + c][j0 + r] = x[c];       // X[r][c] stored in the upper triangle
+                }
         }
         __syncthreads();
         if (sp == 3) break;
-        const int nrow = 64 - (j0 + 16);
-        // TRSM: L[r][c] = (sum_{j0 <= j <= c} A[r][j] X[c][j]) / d_c for rows r >= j0+16, c in the sub-panel
-        double out[3];
+        const int nrt = 3 - sp;                      // 16-row tiles below the sub-panel
+        const int li = lane & 15, lk = lane >> 4;
+        // (a) TRSM on f64 MFMA: L[r][c] = sum_k A[r][j0+k] Xd[c][k] / d_c, one row tile per wave
+        if (wv < nrt) {
+            const int R = j0 + 16 + 16 * wv, c = j0 + li;
+            const double rdc = 1.0 / S[c][c];
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int q = 0; q < 3; q++) {
-            int o = tid + 256 * q;
-            out[q] = 0.0;
-            if (o < nrow * 16) {
-                int r = j0 + 16 + o % nrow, c = j0 + o / nrow;
-                double acc = S[r][c];
-                for (int j = j0; j < c; j++) acc += S[r][j] * S[j][c];           // X[c][j] at S[j][c]
-                out[q] = acc / S[c][c];
+            for (int k4 = 0; k4 < 16; k4 += 4) {
+                const int k = k4 + lk;
+                const double av = S[R + li][j0 + k];
+                const double wk = ((k < li) ? S[j0 + k][c] : (k == li ? 1.0 : 0.0)) * rdc;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, wk, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) S[R + lk + 4 * g][c] = acc[g];
+        }
+        __syncthreads();
+        // (b) trailing update of the lower triangle on MFMA: 16x16 tiles (Rt >= Ct)
+        const int ntile = nrt * (nrt + 1) / 2;
+        for (int t = wv; t < ntile; t += 4) {
+            int Rt = 0, Ct = t;
+            while (Ct > Rt) { Ct -= Rt + 1; Rt++; }
+            const int R = j0 + 16 + 16 * Rt, C = j0 + 16 + 16 * Ct;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k4 = 0; k4 < 16; k4 += 4) {
+                const int k = j0 + k4 + lk;
+                const double av = S[R + li][k] * S[k][k];
+                const double bv = S[C + li][k];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int r = R + lk + 4 * g, c = C + li;
+                if (r >= c) S[r][c] -= acc[g];
             }
         }
         __syncthreads();
-#pragma unroll
-        for (int q = 0; q < 3; q++) {
-            int o = tid + 256 * q;
-            if (o < nrow * 16) S[j0 + 16 + o % nrow][j0 + o / nrow] = out[q];
-        }
-        __syncthreads();
-        // trailing update of the lower triangle: A[r][c] -= sum_j L[r][j] d_j L[c][j]
-        for (int o = tid; o < nrow * nrow; o += 256) {
-            int r = j0 + 16 + o % nrow, c = j0 + 16 + o / nrow;
-            if (c > r) continue;
-            double acc = 0.0;
-#pragma unroll
-            for (int j = 0; j < 16; j++) acc += S[r][j0 + j] * S[j0 + j][j0 + j] * S[c][j0 + j];
-            S[r][c] -= acc;
-        }
-        __syncthreads();
     }
-    // off-diagonal inverse blocks, block row I: T = sum_{K=J}^{I-1} L_IK X_KJ, X_IJ = -X_II T
+    // (c) off-diagonal inverse blocks, block row I (rows r0..r0+15), one 16-column tile per wave:
+    //     T = L_{I,<r0} X_{<r0}, then X_I = -X_II T
+    const int li = lane & 15, lk = lane >> 4;
     for (int I = 1; I < 4; I++) {
-        const int r0 = 16 * I, ncol = r0;
-        for (int o = tid; o < 16 * ncol; o += 256) {
-            int r = r0 + (o & 15), c = o >> 4;
-            double acc = S[r][c];                                                   // j == c: X[c][c] = 1
-            for (int j = c + 1; j < r0; j++) acc += S[r][j] * S[c][j];              // X[j][c] at S[c][j]
-            T[o & 15][c] = acc;
+        const int r0 = 16 * I;
+        if (wv < I) {
+            const int C = 16 * wv, cidx = C + li;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+            for (int k4 = C; k4 < r0; k4 += 4) {
+                const int k = k4 + lk;
+                const double av = S[r0 + li][k];
+                const double bv = (k == cidx) ? 1.0 : (k > cidx ? S[cidx][k] : 0.0);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) T[lk + 4 * g][cidx] = acc[g];
         }
         __syncthreads();
-        for (int o = tid; o < 16 * ncol; o += 256) {
-            int rr = o & 15, c = o >> 4;
-            double acc = T[rr][c];                                                  // k == r: X[r][r] = 1
-            for (int k = 0; k < rr; k++) acc += S[r0 + k][r0 + rr] * T[k][c];       // X[r][k] at S[k][r]
-            S[c][r0 + rr] = -acc;
+        if (wv < I) {
+            const int C = 16 * wv;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k4 = 0; k4 < 16; k4 += 4) {
+                const int k = k4 + lk;
+                const double av = (k == li) ? 1.0 : (k < li ? S[r0 + k][r0 + li] : 0.0);
+                const double bv = T[k][C + li];
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) S[C + li][r0 + lk + 4 * g] = -acc[g];
         }
         __syncthreads();
     }
@@ -523,19 +572,27 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], double (*T)[48], int
 __device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, double *Li, double (*S)[DP],
                                            double (*T)[48], int *flag) {
     const int kb = min(64, s - k0);
-    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-        int c = idx >> 6, r = idx & 63;
-        double v;
-        if (r < kb && c < kb) v = (r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : 0.0;
-        else v = (r == c) ? 1.0 : 0.0;
-        S[r][c] = v;
+    // all 16 loads per thread in flight at once (unrolled), then the LDS stores
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+        v[q] = (r < kb && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+        S[r][c] = v[q];
     }
     __syncthreads();
     diag_block(S, T, flag);
-    for (int idx = threadIdx.x; idx < kb * kb; idx += 256) {
-        int c = idx / kb, r = idx % kb;
-        if (r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
-        Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+        if (r < kb && c < kb) {
+            if (r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
+            Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
+        }
     }
 }
 
@@ -558,7 +615,6 @@ __global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restri
 // is indexed by the column c and B by the row r, so the accumulator's lane&15 runs along rows r:
 // 16 consecutive doubles per store of the column-major front.  acc[a][b][reg]: column
 // cb + 16a + (lane>>4) + 4 reg, row rb + 16b + (lane&15).
-typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int LDP = 66;
 
 __device__ __forceinline__ void mfma_tile(const double (*P)[LDP], const double (*Q)[LDP], int kb4, dbl4 acc[2][2]) {
@@ -591,11 +647,25 @@ __global__ void __launch_bounds__(256) k_trsm(int ntask, const int32_t *__restri
     int kb = min(64, s - k0), kb4 = (kb + 3) & ~3;
     double *F = arena + fd.arena_off[f];
     const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
-    for (int idx = threadIdx.x; idx < kb4 * 64; idx += 256) {
-        int k = idx >> 6, r = idx & 63;
-        bool ok = k < kb;
-        Qs[k][r] = (ok && r0 + r < m) ? F[(int64_t)(k0 + k) * m + r0 + r] : 0.0;
-        Ps[k][r] = (ok && r < kb) ? Li[(int64_t)k * kb + r] / F[(int64_t)(k0 + r) * m + k0 + r] : 0.0;
+    {
+        // r is fixed per thread (stride 256 = 4 rows of 64): one d_c, then all loads in flight
+        const int r = threadIdx.x & 63, kq = threadIdx.x >> 6;
+        const double rdc = (r < kb) ? 1.0 / F[(int64_t)(k0 + r) * m + k0 + r] : 0.0;
+        const bool rok = r0 + r < m;
+        double qv[16], pv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int k = kq + 4 * q;
+            bool ok = k < kb;
+            qv[q] = (ok && rok) ? F[(int64_t)(k0 + k) * m + r0 + r] : 0.0;
+            pv[q] = (ok && r < kb) ? Li[(int64_t)k * kb + r] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int k = kq + 4 * q;
+            Qs[k][r] = qv[q];
+            Ps[k][r] = pv[q] * rdc;
+        }
     }
     __syncthreads();
     dbl4 acc[2][2];
@@ -624,12 +694,16 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // trailing update of tile (ti, tj): C -= L_i D L_j^T over L columns [kA, kA + K),
 // K = min(kmax, s - kA) (one 64-panel for the inner updates, a whole outer block otherwise).
 // MFMA operands are loaded straight from the front (16 consecutive rows per 128-B segment,
-// L2-resident panel) — no LDS on this path — and the C tile is fetched before the MFMA chain.
+// L2-resident panel), software-pipelined 16 columns ahead; the C tile is fetched before the K
+// loop.  (An LDS-staged variant measured slower on MI355X: the f64 MFMA pipe, ~48 TF/s sustained,
+// not operand bandwidth, bounds the big launches.)  LDS here is only the fused panel
+// factorization's.
+struct DiagSmem { double S[64][DP]; double T[16][48]; };
+
 __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
                                                 double *__restrict__ inv, int *__restrict__ flag) {
-    __shared__ double S[64][DP];
-    __shared__ double T[16][48];
+    __shared__ DiagSmem sm;
     int t = xcd_task(ntask);
     if (t >= ntask) return;
     int f = tasks[3 * t], ti = tasks[3 * t + 1], tj = tasks[3 * t + 2];
@@ -659,21 +733,35 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
     const bool p0ok = cb + il < m, p1ok = cb + 16 + il < m, q0ok = rb + il < m, q1ok = rb + 16 + il < m;
-    for (int k16 = 0; k16 < K; k16 += 16)
+    double cd[4], c0[4], c1[4], c2[4], c3[4], nd[4], n0[4], n1[4], n2[4], n3[4];
+    auto load16 = [&](int k16, double *d, double *x0, double *x1, double *y0, double *y1) {
 #pragma unroll
-    for (int k = k16; k < k16 + 16; k += 4) {
-        int kk = k + kl;
-        bool ok = kk < K;
-        const double *col = F + (int64_t)(kA + kk) * m;
-        double dk = ok ? col[kA + kk] : 0.0;
-        double p0 = (ok && p0ok) ? col[cb + il] * dk : 0.0;
-        double p1 = (ok && p1ok) ? col[cb + 16 + il] * dk : 0.0;
-        double q0 = (ok && q0ok) ? col[rb + il] : 0.0;
-        double q1 = (ok && q1ok) ? col[rb + 16 + il] : 0.0;
-        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
+        for (int u = 0; u < 4; u++) {
+            int kk = k16 + 4 * u + kl;
+            bool ok = kk < K;
+            const double *col = F + (int64_t)(kA + kk) * m;
+            d[u] = ok ? col[kA + kk] : 0.0;
+            x0[u] = (ok && p0ok) ? col[cb + il] : 0.0;
+            x1[u] = (ok && p1ok) ? col[cb + 16 + il] : 0.0;
+            y0[u] = (ok && q0ok) ? col[rb + il] : 0.0;
+            y1[u] = (ok && q1ok) ? col[rb + 16 + il] : 0.0;
+        }
+    };
+    load16(0, cd, c0, c1, c2, c3);
+    for (int k16 = 0; k16 < K; k16 += 16) {
+        const bool more = k16 + 16 < K;
+        if (more) load16(k16 + 16, nd, n0, n1, n2, n3);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            double p0 = c0[u] * cd[u], p1 = c1[u] * cd[u];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c2[u], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c3[u], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, c2[u], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, c3[u], acc[1][1], 0, 0, 0);
+        }
+        if (more)
+#pragma unroll
+            for (int u = 0; u < 4; u++) { cd[u] = nd[u]; c0[u] = n0[u]; c1[u] = n1[u]; c2[u] = n2[u]; c3[u] = n3[u]; }
     }
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -691,7 +779,7 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
     if (ti == tj && ti == k1 && s > k1) {
         __syncthreads();
         __threadfence_block();
-        diag_panel(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, S, T, flag);
+        diag_panel(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, sm.T, flag);
     }
 }
 
@@ -742,7 +830,11 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
     __syncthreads();
     double acc = 0.0;
     if (lane < kb)
-        for (int j = part; j <= lane; j += 4) acc += Li[(int64_t)j * kb + lane] * vs[j];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int j = part + 4 * q;
+            if (j <= lane) acc += Li[(int64_t)j * kb + lane] * vs[j];
+        }
     red[part][lane] = acc;
     __syncthreads();
     if (threadIdx.x < 64) ys[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
@@ -754,7 +846,11 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
     int r = r0 + lane;
     acc = 0.0;
     if (r < m)
-        for (int c = part; c < kb; c += 4) acc += F[(int64_t)(k0 + c) * m + r] * ys[c];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            int c = part + 4 * q;
+            if (c < kb) acc += F[(int64_t)(k0 + c) * m + r] * ys[c];
+        }
     red[part][lane] = acc;
     __syncthreads();
     if (part == 0 && r < m) v[r] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
@@ -803,6 +899,7 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
     __syncthreads();
     // x_i = sum_{j >= i} Linv[j][i] w_j: wave wv owns outputs i = wv*16 .. +15, lanes over j
     double wl = lane < kb ? ws[lane] : 0.0;
+#pragma unroll
     for (int ii = 0; ii < 16; ii++) {
         int i = wv * 16 + ii;
         double p = (lane < kb && i < kb && lane >= i) ? Li[(int64_t)i * kb + lane] * wl : 0.0;
@@ -817,6 +914,7 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
     }
     // 4 waves x 16 columns; lanes over the kb panel rows
     double xl = lane < kb ? xs[lane] : 0.0;
+#pragma unroll
     for (int cc = 0; cc < 16; cc++) {
         int q = q0 + wv * 16 + cc;
         double p = lane < kb ? F[(int64_t)q * m + k0 + lane] * xl : 0.0;
@@ -934,6 +1032,7 @@ static inline unsigned nb(int64_t n, int bs) { return (unsigned)((n + bs - 1) / 
 
 // optional per-launch device timing (deftri_profile_trial); off on the solve path
 thread_local KProf *g_prof = nullptr;
+thread_local double g_work = 0;   // algorithmic work of the next launch (profiling only)
 void set_profiler(KProf *p) { g_prof = p; }
 static hipEvent_t prof_event() {
     KProf &P = *g_prof;
@@ -948,7 +1047,8 @@ static hipEvent_t prof_event() {
         if (g_prof) {                                                                \
             hipEvent_t e1_ = prof_event();                                           \
             hipEventRecord(e1_, ST);                                                 \
-            g_prof->recs.push_back({NAME, e0_, e1_, dim3(GRID).x});                  \
+            g_prof->recs.push_back({NAME, e0_, e1_, dim3(GRID).x, g_work});          \
+            g_work = 0;                                                              \
         }                                                                            \
     } while (0)
 
@@ -1010,10 +1110,12 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
             if (stp.ntrsm > 0)
                 LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(256), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
                                    L.fd, L.arena, L.inv);
-            if (stp.nupd > 0)
+            if (stp.nupd > 0) {
+                g_work = stp.upd_flops;
                 LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), st, stp.nupd,
                        L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
                        L.arena, L.inv, L.flag);
+            }
         }
     }
 }

@@ -322,7 +322,7 @@ int upload_device(deftri_ctx *ctx) {
         LevelDev ld{};
         for (int k = 0; k < 2; k++) { ld.ea_off[k] = lv.ea_off[k]; ld.nea[k] = lv.nea[k]; }
         for (const auto &stp : lv.steps)
-            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner});
+            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner, stp.upd_flops});
         ld.fwd_off = lv.fwd_off; ld.nfwd = lv.nfwd;
         for (const auto &x : lv.fsteps) ld.fsteps.push_back({x.off, x.n});
         for (const auto &x : lv.bsteps) ld.bsteps.push_back({x.off, x.n});
@@ -476,7 +476,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     for (const auto &r : prof.recs) {
         float ms = 0;
         hipEventElapsedTime(&ms, r.e0, r.e1);
-        if (dump) std::fprintf(stderr, "[prof] %s %u %.4f\n", r.name, r.grid, ms);
+        if (dump) std::fprintf(stderr, "[prof] %s %u %.4f %.6g\n", r.name, r.grid, ms, r.work);
         int32_t k = 0;
         for (; k < n; k++) if (std::strcmp(stats[k].name, r.name) == 0) break;
         if (k == n) {

@@ -394,8 +394,11 @@ struct Builder {
                     int32_t t0 = kA + K;
                     int32_t tend = inner ? std::min(F.s, (kA / kOuter + 1) * kOuter) : F.m;
                     for (int32_t tj = t0; tj < tend; tj += 64)
-                        for (int32_t ti = tj; ti < F.m; ti += 64)
-                            S.update_flops += 2.0 * std::min(64, F.m - ti) * std::min(64, F.m - tj) * K;
+                        for (int32_t ti = tj; ti < F.m; ti += 64) {
+                            double fl = 2.0 * std::min(64, F.m - ti) * std::min(64, std::min(F.m, tend) - tj) * K;
+                            S.update_flops += fl;
+                            st.upd_flops += fl;
+                        }
                 }
             };
             for (int32_t P0 = 0; P0 < maxs; P0 += kOuter) {

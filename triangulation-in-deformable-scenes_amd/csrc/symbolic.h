@@ -93,6 +93,7 @@ struct Symbolic {
         int32_t k0 = 0;                               // panel of diag / trsm
         int32_t kA = 0, kmax = 0;                     // update: L columns [kA, kA + min(kmax, s - kA))
         int32_t inner = 0;                            // 1: columns clipped at the outer block end
+        double upd_flops = 0;                         // algorithmic flops of this update launch
     };
     struct LevelTasks {
         int64_t ea_off[2] = {0, 0}; int32_t nea[2] = {0, 0};   // extend-add (child slot 0/1): (parent, child col)
