@@ -409,22 +409,38 @@ __global__ void k_scatter(int64_t nblocks, const int64_t *__restrict__ val_off, 
 // ------------------------------------------------------------------------------------------
 // multifrontal LDL^T
 // ------------------------------------------------------------------------------------------
-__global__ void k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd, double *__restrict__ arena) {
+// extend-add of one child contribution block into its parent: task (child, j0, i0) covers CB columns
+// j0..j0+15 and rows i0..i0+255 (lower triangle).  Each thread owns one CB row: its parent row index
+// and the 16 child/parent values are loaded up front (one latency round); each parent entry is
+// written by exactly one thread of the launch (slot-0 and slot-1 children run in separate launches,
+// so the summation order is fixed).
+__global__ void __launch_bounds__(256) k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                            double *__restrict__ arena) {
     int t = blockIdx.x;
     if (t >= ntask) return;
-    int c = tasks[3 * t], j0 = tasks[3 * t + 1];
+    int c = tasks[3 * t], j0 = tasks[3 * t + 1], i0 = tasks[3 * t + 2];
     int p = fd.parent[c];
     int mc = fd.m[c], sc = fd.s[c], mp = fd.m[p];
     int u = mc - sc;
     const int32_t *bm = fd.bmap + fd.bmap_off[c];
-    const double *Fc = arena + fd.arena_off[c];
+    const double *Fc = arena + fd.arena_off[c] + (int64_t)sc * mc + sc;
     double *Fp = arena + fd.arena_off[p];
-    int j1 = min(j0 + 16, u);
-    for (int j = j0; j < j1; j++) {
-        int64_t pj = (int64_t)bm[j] * mp;
-        const double *src = Fc + (int64_t)(sc + j) * mc + sc;
-        for (int i = j + threadIdx.x; i < u; i += blockDim.x) Fp[pj + bm[i]] += src[i];
+    const int i = i0 + (int)threadIdx.x;
+    if (i >= u) return;
+    const int bi = bm[i];
+    const int nj = min(16, min(u - j0, i - j0 + 1));       // columns j0..j0+nj-1 with j <= i
+    double cv[16], pv[16];
+    int64_t pj[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        pj[q] = (q < nj) ? (int64_t)bm[j0 + q] * mp + bi : 0;
+        cv[q] = (q < nj) ? Fc[(int64_t)(j0 + q) * mc + i] : 0.0;
     }
+#pragma unroll
+    for (int q = 0; q < 16; q++) pv[q] = (q < nj) ? Fp[pj[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+        if (q < nj) Fp[pj[q]] = pv[q] + cv[q];
 }
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
@@ -444,57 +460,59 @@ __device__ __forceinline__ void wave_sync() {
 
 // Blocked LDL^T + unit-lower inverse of one 64x64 panel diagonal block held in LDS (256 threads).
 //   in : S[r][c] (c <= r) = A (rows/cols >= kb padded with the identity), S[c][r] (r > c) = 0
-//   out: S[r][c] (c < r) = L, S[r][r] = D, S[c][r] (r > c) = Linv[r][c]
-// Four 16-column sub-panels: wave 0 factors the 16x16 diagonal block and its inverse (16 dependent
-// steps, wave-synchronous), then all 256 threads do the sub-panel TRSM and the trailing update;
-// finally the off-diagonal blocks of Linv are formed block-row by block-row
-// (X_IJ = -X_II sum_K L_IK X_KJ).  T is 16x48 scratch.
+//   out: S[r][c] (c < r) = L, S[r][r] = D, S[c][r] (r > c) = X[r][c], X = L^{-1}
+// Four 16-column sub-panels K.  Per sub-panel:
+//   F  the 16x16 diagonal block: thread (r, c) owns one element; 16 right-looking steps, one
+//      barrier each (A[r][c] -= l_r a_c, X[r][c] -= l_r X[j][c]);
+//   X  (waves nrt..) finishes the inverse blocks of block row K: X_KJ = -X_KK T_KJ, J < K;
+//   TR (waves 0..nrt-1) the sub-panel TRSM below it: L_IK = A_IK X_KK^T D_K^{-1};
+//   U  the trailing Schur update on the lower triangle and the inverse accumulators
+//      T_IJ += L_IK X_KJ (I > K, J <= K), all 16x16x16 f64 MFMA tiles.
+// T_IJ accumulates in place in the upper-triangle slot of X_IJ (zero on entry).
 constexpr int DP = 65;
-__device__ __forceinline__ void diag_block(double (*S)[DP], double (*T)[48], int *flag) {
+__device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int sp = 0; sp < 4; sp++) {
-        const int j0 = 16 * sp;
-        if (wv == 0) {
-            // 16x16 diagonal sub-block in registers: lane r (mod 16) holds row r of A and of
-            // X = L^{-1}; the pivot column / X row are broadcast with v_readlane (unrolled: every
-            // lane and register index is a constant)
-            const int r = lane & 15;
-            double a[16], x[16];
-#pragma unroll
-            for (int c = 0; c < 16; c++) {
-                a[c] = (c <= r) ? S[j0 + r][j0 + c] : 0.0;
-                x[c] = (c == r) ? 1.0 : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const double d = readlane_d(a[j], j);
-                if (lane == 0 && d == 0.0) atomicOr(flag, 1);
-                const double l = (r > j) ? a[j] / d : a[j];
-                a[j] = l;
-                const double ld = l * d;
-#pragma unroll
-                for (int c = j + 1; c < 16; c++) {
-                    const double lc = readlane_d(l, c);
-                    if (r >= c) a[c] -= ld * lc;
-                }
-#pragma unroll
-                for (int c = 0; c <= j; c++) {
-                    const double xjc = readlane_d(x[c], j);
-                    if (r > j) x[c] -= l * xjc;
+    const int li = lane & 15, lk = lane >> 4;
+    const int er = tid & 15, ec = tid >> 4;                    // element of the 16x16 block
+    // rows/cols >= kb are identity padding: sub-blocks past nsub and pivot steps past kb are no-ops
+    const int nsub = (kb + 15) >> 4;
+    for (int K = 0; K < nsub; K++) {
+        const int j0 = 16 * K;
+        const int jend = min(16, kb - j0);
+        // ---- F: factor the diagonal block + its inverse, element per thread ----
+        for (int j = 0; j < jend; j++) {
+            const double d = S[j0 + j][j0 + j];
+            const double ar = S[j0 + er][j0 + j], ac = S[j0 + ec][j0 + j];
+            const double rd = 1.0 / d;
+            const double lr = ar * rd;
+            if (er > j) {
+                if (ec > j && er >= ec) S[j0 + er][j0 + ec] -= lr * ac;                  // A -= l_r d l_c
+                if (ec <= j) {
+                    const double xjc = (ec == j) ? 1.0 : S[j0 + ec][j0 + j];             // X[j][c]
+                    S[j0 + ec][j0 + er] -= lr * xjc;                                      // X[r][c]
                 }
             }
-            if (lane < 16)
-#pragma unroll
-                for (int c = 0; c < 16; c++) {
-                    if (c <= r) S[j0 + r][j0 + c] = a[c];
-                    if (c < r) S[j0 + c][j0 + r] = x[c];       // X[r][c] stored in the upper triangle
-                }
+            if (tid == 0 && d == 0.0) atomicOr(flag, 1);
+            __syncthreads();
+            if (ec == j && er > j) S[j0 + er][j0 + j] = lr;                              // scale column j
         }
         __syncthreads();
-        if (sp == 3) break;
-        const int nrt = 3 - sp;                      // 16-row tiles below the sub-panel
-        const int li = lane & 15, lk = lane >> 4;
-        // (a) TRSM on f64 MFMA: L[r][c] = sum_k A[r][j0+k] Xd[c][k] / d_c, one row tile per wave
+        const int nrt = nsub - 1 - K;                          // 16-row tiles below the sub-panel
+        // ---- X: X_KJ = -X_KK T_KJ for J < K (T_KJ at S[16J + c][j0 + r]) ----
+        if (wv >= nrt && wv - nrt < K) {
+            const int J = wv - nrt, cidx = 16 * J + li;
+            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k4 = 0; k4 < 16; k4 += 4) {
+                const int k = k4 + lk;
+                const double av = (k == li) ? 1.0 : (k < li ? S[j0 + k][j0 + li] : 0.0);  // X_KK[li][k]
+                const double bv = S[cidx][j0 + k];                                        // T_KJ[k][li]
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int g = 0; g < 4; g++) S[cidx][j0 + lk + 4 * g] = -acc[g];             // X[j0+r][cidx]
+        }
+        // ---- TR: L[r][c] = sum_k A[r][j0+k] X[c][k] / d_c, one row tile per wave ----
         if (wv < nrt) {
             const int R = j0 + 16 + 16 * wv, c = j0 + li;
             const double rdc = 1.0 / S[c][c];
@@ -509,69 +527,56 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], double (*T)[48], int
 #pragma unroll
             for (int g = 0; g < 4; g++) S[R + lk + 4 * g][c] = acc[g];
         }
+        if (K == nsub - 1) break;
         __syncthreads();
-        // (b) trailing update of the lower triangle on MFMA: 16x16 tiles (Rt >= Ct)
-        const int ntile = nrt * (nrt + 1) / 2;
-        for (int t = wv; t < ntile; t += 4) {
-            int Rt = 0, Ct = t;
-            while (Ct > Rt) { Ct -= Rt + 1; Rt++; }
-            const int R = j0 + 16 + 16 * Rt, C = j0 + 16 + 16 * Ct;
+        // ---- U: Schur tiles (Rt >= Ct) then inverse accumulators (I > K, J <= K) ----
+        const int nsch = nrt * (nrt + 1) / 2, ninv = nrt * (K + 1);
+        for (int t = wv; t < nsch + ninv; t += 4) {
             dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+            if (t < nsch) {
+                int Rt = 0, Ct = t;
+                while (Ct > Rt) { Ct -= Rt + 1; Rt++; }
+                const int R = j0 + 16 + 16 * Rt, C = j0 + 16 + 16 * Ct;
 #pragma unroll
-            for (int k4 = 0; k4 < 16; k4 += 4) {
-                const int k = j0 + k4 + lk;
-                const double av = S[R + li][k] * S[k][k];
-                const double bv = S[C + li][k];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
+                for (int k4 = 0; k4 < 16; k4 += 4) {
+                    const int k = j0 + k4 + lk;
+                    const double av = S[R + li][k] * S[k][k];
+                    const double bv = S[C + li][k];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const int r = R + lk + 4 * g, c = C + li;
-                if (r >= c) S[r][c] -= acc[g];
+                for (int g = 0; g < 4; g++) {
+                    const int r = R + lk + 4 * g, c = C + li;
+                    if (r >= c) S[r][c] -= acc[g];
+                }
+            } else {
+                const int q = t - nsch, I = K + 1 + q / (K + 1), J = q % (K + 1);
+                const int cidx = 16 * J + li;
+#pragma unroll
+                for (int k4 = 0; k4 < 16; k4 += 4) {
+                    const int k = k4 + lk, kk = j0 + k;
+                    const double av = S[16 * I + li][kk];                                 // L[16I+li][kk]
+                    double bv;                                                            // X[kk][cidx]
+                    if (J < K) bv = S[cidx][kk];
+                    else bv = (k == li) ? 1.0 : (k > li ? S[cidx][kk] : 0.0);
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+#pragma unroll
+                for (int g = 0; g < 4; g++) S[cidx][16 * I + lk + 4 * g] += acc[g];       // T_IJ[r][c]
             }
         }
         __syncthreads();
     }
-    // (c) off-diagonal inverse blocks, block row I (rows r0..r0+15), one 16-column tile per wave:
-    //     T = L_{I,<r0} X_{<r0}, then X_I = -X_II T
-    const int li = lane & 15, lk = lane >> 4;
-    for (int I = 1; I < 4; I++) {
-        const int r0 = 16 * I;
-        if (wv < I) {
-            const int C = 16 * wv, cidx = C + li;
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-            for (int k4 = C; k4 < r0; k4 += 4) {
-                const int k = k4 + lk;
-                const double av = S[r0 + li][k];
-                const double bv = (k == cidx) ? 1.0 : (k > cidx ? S[cidx][k] : 0.0);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g++) T[lk + 4 * g][cidx] = acc[g];
-        }
-        __syncthreads();
-        if (wv < I) {
-            const int C = 16 * wv;
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k4 = 0; k4 < 16; k4 += 4) {
-                const int k = k4 + lk;
-                const double av = (k == li) ? 1.0 : (k < li ? S[r0 + k][r0 + li] : 0.0);
-                const double bv = T[k][C + li];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g++) S[C + li][r0 + lk + 4 * g] = -acc[g];
-        }
-        __syncthreads();
-    }
+    __syncthreads();
 }
 
 // load the panel diagonal block of (front F, panel k0) into S (identity padding), factor, store L/D
 // into the front and Linv (kb x kb, column-major) into the inverse arena
-__device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, double *Li, double (*S)[DP],
-                                           double (*T)[48], int *flag) {
+__device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, double *Li, double (*S)[DP], int *flag) {
     const int kb = min(64, s - k0);
+#ifdef DEFTRI_DIAG_TIMING
+    long long tm0 = clock64();
+#endif
     // all 16 loads per thread in flight at once (unrolled), then the LDS stores
     double v[16];
 #pragma unroll
@@ -585,7 +590,13 @@ __device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, doub
         S[r][c] = v[q];
     }
     __syncthreads();
-    diag_block(S, T, flag);
+#ifdef DEFTRI_DIAG_TIMING
+    long long tm1 = clock64();
+#endif
+    diag_block(S, kb, flag);
+#ifdef DEFTRI_DIAG_TIMING
+    long long tm2 = clock64();
+#endif
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
@@ -594,6 +605,12 @@ __device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, doub
             Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
         }
     }
+#ifdef DEFTRI_DIAG_TIMING
+    __syncthreads();
+    long long tm3 = clock64();
+    if (threadIdx.x == 0 && (blockIdx.x & 1023) == 0)
+        printf("[diagtime] blk %d load %lld block %lld store %lld\n", (int)blockIdx.x, tm1 - tm0, tm2 - tm1, tm3 - tm2);
+#endif
 }
 
 // standalone panel factorization (first panel of every front of a level; later panels are
@@ -602,11 +619,10 @@ __global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restri
                                               double *__restrict__ arena, double *__restrict__ inv,
                                               int *__restrict__ flag) {
     __shared__ double S[64][DP];
-    __shared__ double T[16][48];
     int t = blockIdx.x;
     if (t >= ntask) return;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1];
-    diag_panel(arena + fd.arena_off[f], fd.m[f], fd.s[f], k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S, T,
+    diag_panel(arena + fd.arena_off[f], fd.m[f], fd.s[f], k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S,
                flag);
 }
 
@@ -698,7 +714,7 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // loop.  (An LDS-staged variant measured slower on MI355X: the f64 MFMA pipe, ~48 TF/s sustained,
 // not operand bandwidth, bounds the big launches.)  LDS here is only the fused panel
 // factorization's.
-struct DiagSmem { double S[64][DP]; double T[16][48]; };
+struct DiagSmem { double S[64][DP]; };
 
 __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
@@ -779,7 +795,7 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
     if (ti == tj && ti == k1 && s > k1) {
         __syncthreads();
         __threadfence_block();
-        diag_panel(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, sm.T, flag);
+        diag_panel(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, flag);
     }
 }
 
@@ -810,7 +826,8 @@ __global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__
 
 // forward panel step (front f, panel k0): every task forms y_p = L_pp^{-1} v_p from the stored
 // panel inverse (64x64 GEMV from L2); task r0 == k0 publishes y_p, tasks r0 > k0 update the 64 rows
-// r0.. below the panel: v_r -= L[r, panel] y_p
+// r0.. below the panel: v_r -= L[r, panel] y_p.  All global loads of a task are issued up front
+// (these launches are latency-bound: one load round instead of three).
 __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ inv,
                                                   double *__restrict__ vec, double *__restrict__ yvec) {
@@ -825,16 +842,22 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
     const double *F = arena + fd.arena_off[f];
     const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
     double *v = vec + fd.vec_off[f];
-    int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
-    if (threadIdx.x < kb) vs[threadIdx.x] = v[k0 + threadIdx.x];
+    const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const int r = r0 + lane;
+    const bool below = r0 != k0 && r < m;
+    double vk = (threadIdx.x < kb) ? v[k0 + threadIdx.x] : 0.0;
+    double li[16], fv[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        int j = part + 4 * q;
+        li[q] = (j <= lane && lane < kb) ? Li[(int64_t)j * kb + lane] : 0.0;
+        fv[q] = (below && j < kb) ? F[(int64_t)(k0 + j) * m + r] : 0.0;
+    }
+    if (threadIdx.x < 64) vs[threadIdx.x] = vk;
     __syncthreads();
     double acc = 0.0;
-    if (lane < kb)
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int j = part + 4 * q;
-            if (j <= lane) acc += Li[(int64_t)j * kb + lane] * vs[j];
-        }
+    for (int q = 0; q < 16; q++) acc += li[q] * vs[part + 4 * q];
     red[part][lane] = acc;
     __syncthreads();
     if (threadIdx.x < 64) ys[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
@@ -843,14 +866,9 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
         if (threadIdx.x < kb) yvec[fd.vec_off[f] + k0 + threadIdx.x] = ys[threadIdx.x];
         return;
     }
-    int r = r0 + lane;
     acc = 0.0;
-    if (r < m)
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int c = part + 4 * q;
-            if (c < kb) acc += F[(int64_t)(k0 + c) * m + r] * ys[c];
-        }
+    for (int q = 0; q < 16; q++) acc += fv[q] * ys[part + 4 * q];
     red[part][lane] = acc;
     __syncthreads();
     if (part == 0 && r < m) v[r] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
@@ -880,12 +898,14 @@ __global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__re
 
 // backward panel step (front f, panel k0; panels run in descending order): every task forms
 // x_p = L_pp^{-T} w_p from the panel inverse; task q0 == k0 scatters x_p to the global solution,
-// tasks q0 < k0 update w[q0..q0+63] -= L[panel rows, q]^T x_p
+// tasks q0 < k0 update w[q0..q0+63] -= L[panel rows, q]^T x_p.  Thread (lane, part) owns output
+// lane and every 4th term; loads issued up front, partial sums reduced through LDS in fixed order.
 __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ inv,
                                                   double *__restrict__ vec, double *__restrict__ x) {
     __shared__ double ws[64];
     __shared__ double xs[64];
+    __shared__ double red[4][64];
     int t = blockIdx.x;
     if (t >= ntask) return;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1], q0 = tasks[3 * t + 2];
@@ -894,33 +914,37 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
     const double *F = arena + fd.arena_off[f];
     const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
     double *w = vec + fd.vec_off[f];
-    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (threadIdx.x < kb) ws[threadIdx.x] = w[k0 + threadIdx.x];
-    __syncthreads();
-    // x_i = sum_{j >= i} Linv[j][i] w_j: wave wv owns outputs i = wv*16 .. +15, lanes over j
-    double wl = lane < kb ? ws[lane] : 0.0;
+    const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const bool own = q0 == k0;
+    double wk = (threadIdx.x < kb) ? w[k0 + threadIdx.x] : 0.0;
+    double lv[16], fv[16];
+    const double *Fq = F + (int64_t)(q0 + lane) * m + k0;
 #pragma unroll
-    for (int ii = 0; ii < 16; ii++) {
-        int i = wv * 16 + ii;
-        double p = (lane < kb && i < kb && lane >= i) ? Li[(int64_t)i * kb + lane] * wl : 0.0;
-        for (int off = 32; off > 0; off >>= 1) p += __shfl_down(p, off);
-        if (lane == 0) xs[i] = p;
+    for (int q = 0; q < 16; q++) {
+        int j = part + 4 * q;
+        lv[q] = (lane < kb && j < kb && j >= lane) ? Li[(int64_t)lane * kb + j] : 0.0;   // Linv[j][lane]
+        fv[q] = (!own && j < kb) ? Fq[j] : 0.0;                                         // L[k0+j][q0+lane]
     }
+    if (threadIdx.x < 64) ws[threadIdx.x] = wk;
     __syncthreads();
-    if (q0 == k0) {
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc += lv[q] * ws[part + 4 * q];
+    red[part][lane] = acc;
+    __syncthreads();
+    if (threadIdx.x < 64) xs[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
+    if (own) {
         const int32_t *rows = fd.rows + fd.rows_off[f];
         if (threadIdx.x < kb) x[rows[k0 + threadIdx.x]] = xs[threadIdx.x];
         return;
     }
-    // 4 waves x 16 columns; lanes over the kb panel rows
-    double xl = lane < kb ? xs[lane] : 0.0;
+    acc = 0.0;
 #pragma unroll
-    for (int cc = 0; cc < 16; cc++) {
-        int q = q0 + wv * 16 + cc;
-        double p = lane < kb ? F[(int64_t)q * m + k0 + lane] * xl : 0.0;
-        for (int off = 32; off > 0; off >>= 1) p += __shfl_down(p, off);
-        if (lane == 0) w[q] -= p;
-    }
+    for (int q = 0; q < 16; q++) acc += fv[q] * xs[part + 4 * q];
+    red[part][lane] = acc;
+    __syncthreads();
+    if (part == 0) w[q0 + lane] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 // ------------------------------------------------------------------------------------------

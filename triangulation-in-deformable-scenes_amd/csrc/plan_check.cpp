@@ -58,13 +58,13 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
         for (int slot = 0; slot < 2; slot++)
             for (int32_t t = 0; t < lv.nea[slot]; t++) {
                 const int32_t *tk = T + 3 * (lv.ea_off[slot] + t);
-                int c = tk[0], j0 = tk[1];
+                int c = tk[0], j0 = tk[1], i0 = tk[2];
                 const Front &C = S.fronts[c];
                 const Front &Pf = S.fronts[C.parent];
                 int u = C.m - C.s;
                 const int32_t *bm = S.bmap.data() + C.bmap_off;
                 for (int j = j0; j < std::min(j0 + 16, u); j++)
-                    for (int i = j; i < u; i++)
+                    for (int i = std::max(j, i0); i < std::min(i0 + 256, u); i++)
                         Fp(C.parent)[(int64_t)bm[j] * Pf.m + bm[i]] += Fp(c)[(int64_t)(C.s + j) * C.m + C.s + i];
             }
         for (const auto &st : lv.steps) {

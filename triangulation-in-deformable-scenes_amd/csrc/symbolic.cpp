@@ -353,7 +353,9 @@ struct Builder {
                     if (F.nchild <= slot) continue;
                     int32_t c = F.child[slot];
                     int32_t u = S.fronts[c].m - S.fronts[c].s;
-                    for (int32_t j = 0; j < u; j += 16) { push3(c, j, 0); cnt++; }
+                    // (child, 16 CB columns j0.., 256 CB rows i0..), lower triangle only
+                    for (int32_t j = 0; j < u; j += 16)
+                        for (int32_t i = j; i < u; i += 256) { push3(c, j, i); cnt++; }
                 }
                 LT.nea[slot] = cnt;
             }

@@ -5,6 +5,7 @@ There is no CPU fallback: if the library is missing, `load()` raises, and every 
 point runs on the GPU or returns an error.
 """
 import ctypes as C
+import os
 import pathlib
 
 import numpy as np
@@ -13,7 +14,7 @@ from . import _abi
 from .problem import Problem
 
 PKG_ROOT = pathlib.Path(__file__).resolve().parent.parent
-LIB_PATH = PKG_ROOT / "libdeftri.so"
+LIB_PATH = pathlib.Path(os.environ.get("DEFTRI_LIB", PKG_ROOT / "libdeftri.so"))   # DEFTRI_LIB: dev builds
 _lib = None
 
 
