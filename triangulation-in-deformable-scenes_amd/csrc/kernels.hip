@@ -716,7 +716,7 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // factorization's.
 struct DiagSmem { double S[64][DP]; };
 
-__global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
                                                 double *__restrict__ inv, int *__restrict__ flag) {
     __shared__ DiagSmem sm;
@@ -749,11 +749,12 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
     const bool p0ok = cb + il < m, p1ok = cb + 16 + il < m, q0ok = rb + il < m, q1ok = rb + 16 + il < m;
-    double cd[4], c0[4], c1[4], c2[4], c3[4], nd[4], n0[4], n1[4], n2[4], n3[4];
-    auto load16 = [&](int k16, double *d, double *x0, double *x1, double *y0, double *y1) {
+    constexpr int PD = 2;                                      // k-steps (of 4) per prefetch stage
+    double cd[PD], c0[PD], c1[PD], c2[PD], c3[PD], nd[PD], n0[PD], n1[PD], n2[PD], n3[PD];
+    auto loadk = [&](int kb0, double *d, double *x0, double *x1, double *y0, double *y1) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            int kk = k16 + 4 * u + kl;
+        for (int u = 0; u < PD; u++) {
+            int kk = kb0 + 4 * u + kl;
             bool ok = kk < K;
             const double *col = F + (int64_t)(kA + kk) * m;
             d[u] = ok ? col[kA + kk] : 0.0;
@@ -763,12 +764,12 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
             y1[u] = (ok && q1ok) ? col[rb + 16 + il] : 0.0;
         }
     };
-    load16(0, cd, c0, c1, c2, c3);
-    for (int k16 = 0; k16 < K; k16 += 16) {
-        const bool more = k16 + 16 < K;
-        if (more) load16(k16 + 16, nd, n0, n1, n2, n3);
+    loadk(0, cd, c0, c1, c2, c3);
+    for (int kb0 = 0; kb0 < K; kb0 += 4 * PD) {
+        const bool more = kb0 + 4 * PD < K;
+        if (more) loadk(kb0 + 4 * PD, nd, n0, n1, n2, n3);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < PD; u++) {
             double p0 = c0[u] * cd[u], p1 = c1[u] * cd[u];
             acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c2[u], acc[0][0], 0, 0, 0);
             acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c3[u], acc[0][1], 0, 0, 0);
@@ -777,7 +778,7 @@ __global__ void __launch_bounds__(256) k_update(int ntask, const int32_t *__rest
         }
         if (more)
 #pragma unroll
-            for (int u = 0; u < 4; u++) { cd[u] = nd[u]; c0[u] = n0[u]; c1[u] = n1[u]; c2[u] = n2[u]; c3[u] = n3[u]; }
+            for (int u = 0; u < PD; u++) { cd[u] = nd[u]; c0[u] = n0[u]; c1[u] = n1[u]; c2[u] = n2[u]; c3[u] = n3[u]; }
     }
 #pragma unroll
     for (int a = 0; a < 2; a++)
