@@ -651,10 +651,11 @@ __device__ __forceinline__ void mfma_tile(const double (*P)[LDP], const double (
     }
 }
 
-// rows r0..r0+63 below the panel: L_r = F_r L11^{-T} D^{-1}  (GEMM with the panel inverse)
+// rows r0..r0+63 below the panel: L_r = F_r L11^{-T} D^{-1}  (GEMM with the panel inverse).
+// The inverse (scaled by 1/d_c) is staged once in LDS (shared by the 4 waves); each wave's row
+// operands come straight from the front, all issued before the MFMA chain.
 __global__ void __launch_bounds__(256) k_trsm(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                               double *__restrict__ arena, const double *__restrict__ inv) {
-    __shared__ double Qs[64][LDP];   // Qs[k][r] = F[r0 + r][k0 + k]
     __shared__ double Ps[64][LDP];   // Ps[k][c] = Linv[c][k] / d_c
     int t = blockIdx.x;
     if (t >= ntask) return;
@@ -663,38 +664,54 @@ __global__ void __launch_bounds__(256) k_trsm(int ntask, const int32_t *__restri
     int kb = min(64, s - k0), kb4 = (kb + 3) & ~3;
     double *F = arena + fd.arena_off[f];
     const double *Li = inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rb = (w & 1) * 32, cb = (w >> 1) * 32;
+    const int kl = lane >> 4, il = lane & 15;
+    // row operands of this wave: rows r0 + rb + il (+16), columns k0 + 4j + kl
+    const bool q0ok = r0 + rb + il < m, q1ok = r0 + rb + 16 + il < m;
+    double q0v[16], q1v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int k = 4 * j + kl;
+        const double *col = F + (int64_t)(k0 + k) * m + r0 + rb + il;
+        q0v[j] = (k < kb && q0ok) ? col[0] : 0.0;
+        q1v[j] = (k < kb && q1ok) ? col[16] : 0.0;
+    }
     {
-        // r is fixed per thread (stride 256 = 4 rows of 64): one d_c, then all loads in flight
-        const int r = threadIdx.x & 63, kq = threadIdx.x >> 6;
-        const double rdc = (r < kb) ? 1.0 / F[(int64_t)(k0 + r) * m + k0 + r] : 0.0;
-        const bool rok = r0 + r < m;
-        double qv[16], pv[16];
+        const int c = threadIdx.x & 63, kq = threadIdx.x >> 6;
+        const double rdc = (c < kb) ? 1.0 / F[(int64_t)(k0 + c) * m + k0 + c] : 0.0;
+        double pv[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) {
             int k = kq + 4 * q;
-            bool ok = k < kb;
-            qv[q] = (ok && rok) ? F[(int64_t)(k0 + k) * m + r0 + r] : 0.0;
-            pv[q] = (ok && r < kb) ? Li[(int64_t)k * kb + r] : 0.0;
+            pv[q] = (k < kb && c < kb) ? Li[(int64_t)k * kb + c] : 0.0;
         }
 #pragma unroll
-        for (int q = 0; q < 16; q++) {
-            int k = kq + 4 * q;
-            Qs[k][r] = qv[q];
-            Ps[k][r] = pv[q] * rdc;
-        }
+        for (int q = 0; q < 16; q++) Ps[kq + 4 * q][c] = pv[q] * rdc;
     }
     __syncthreads();
     dbl4 acc[2][2];
-    mfma_tile(Ps, Qs, kb4, acc);
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int rb = (w & 1) * 32, cb = (w >> 1) * 32;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (4 * j < kb4) {
+            const double p0 = Ps[4 * j + kl][cb + il], p1 = Ps[4 * j + kl][cb + 16 + il];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0v[j], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1v[j], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0v[j], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1v[j], acc[1][1], 0, 0, 0);
+        }
+    }
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int g = 0; g < 4; g++) {
-                int c = cb + 16 * a + (lane >> 4) + 4 * g, r = rb + 16 * b + (lane & 15);
+                int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
                 if (c < kb && r0 + r < m) F[(int64_t)(k0 + c) * m + r0 + r] = acc[a][b][g];
             }
 }
