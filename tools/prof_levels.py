@@ -9,8 +9,15 @@ if os.environ.get("DEFTRI_PROF_CHILD") is None:
     print(r.stdout)
     if r.returncode:
         print(r.stderr[-3000:]); sys.exit(r.returncode)
-    seq = [(n, int(g), float(ms)) for _, n, g, ms, _w in rows]
-    upd = [(int(g), float(ms), float(w)) for _, n, g, ms, w in rows if n == "update"]
+    seq = [(n, int(g), float(ms)) for _, n, g, ms, _w, _l in rows]
+    upd = [(int(g), float(ms), float(w)) for _, n, g, ms, w, _l in rows if n == "update"]
+    lev = collections.defaultdict(lambda: collections.defaultdict(float))
+    for _, n, g, ms, w, l in rows:
+        lev[int(l)][n] += float(ms)
+    print("per level (ms):")
+    for l in sorted(lev):
+        tot_l = sum(lev[l].values())
+        print(f"  level {l:3d} total {tot_l:7.3f} " + " ".join(f"{k}={v:.3f}" for k, v in sorted(lev[l].items(), key=lambda kv: -kv[1])))
     print("update launches (grid, us, GF, TF/s), in order:")
     for i, (g, ms, w) in enumerate(upd):
         print(f"  {i:3d} grid {g:6d} {1e3 * ms:9.1f} us {w / 1e9:8.3f} GF {w / (ms * 1e-3) / 1e12:6.2f} TF/s")

@@ -33,7 +33,7 @@ struct DevProblem {
 };
 
 struct FrontDev {
-    const int32_t *m, *s, *parent, *nchild, *child0, *child1;
+    const int32_t *m, *s, *parent, *nchild, *child0, *child1, *direct;
     const int64_t *arena_off, *vec_off, *rows_off, *bmap_off, *inv_off;
     const int32_t *rows, *bmap;
 };
@@ -83,7 +83,7 @@ struct DevPlan {
 };
 
 // per-launch device timing for deftri_profile_trial (never active on the solve path)
-struct KProfRec { const char *name; hipEvent_t e0, e1; unsigned grid; double work; };
+struct KProfRec { const char *name; hipEvent_t e0, e1; unsigned grid; double work; int level; };
 struct KProf {
     std::vector<hipEvent_t> pool;
     size_t next = 0;

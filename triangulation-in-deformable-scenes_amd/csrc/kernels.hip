@@ -797,15 +797,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
             for (int u = 0; u < PD; u++) { cd[u] = nd[u]; c0[u] = n0[u]; c1[u] = n1[u]; c2[u] = n2[u]; c3[u] = n3[u]; }
     }
+    // the front's last trailing update produces its final contribution block: a direct front adds
+    // it straight into the parent (lower triangle; bmap is monotone, each parent entry has one writer
+    // in this launch) instead of leaving it for an extend-add
+    if (!inner && kA + K == s && fd.direct[f]) {
+        const int p = fd.parent[f], mp = fd.m[p];
+        const int32_t *bm = fd.bmap + fd.bmap_off[f] - s;
+        double *Fp = arena + fd.arena_off[p];
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+        for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 2; b++)
+            for (int b = 0; b < 2; b++)
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
-                if (c < cend && r < m) F[(int64_t)c * m + r] = cv[a][b][g] - acc[a][b][g];
-            }
+                for (int g = 0; g < 4; g++) {
+                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    if (c < m && r < m && r >= c) Fp[(int64_t)bm[c] * mp + bm[r]] += cv[a][b][g] - acc[a][b][g];
+                }
+    } else {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    if (c < cend && r < m) F[(int64_t)c * m + r] = cv[a][b][g] - acc[a][b][g];
+                }
+    }
     // the diagonal tile of the next panel is final once this tile is: factor it here (its LDL^T
     // overlaps the rest of this launch instead of costing its own launch on the critical path;
     // these tiles are first in the task list)
@@ -1075,6 +1093,7 @@ static inline unsigned nb(int64_t n, int bs) { return (unsigned)((n + bs - 1) / 
 // optional per-launch device timing (deftri_profile_trial); off on the solve path
 thread_local KProf *g_prof = nullptr;
 thread_local double g_work = 0;   // algorithmic work of the next launch (profiling only)
+thread_local int g_level = -1;    // elimination-tree level of the launches being issued (profiling only)
 void set_profiler(KProf *p) { g_prof = p; }
 static hipEvent_t prof_event() {
     KProf &P = *g_prof;
@@ -1089,7 +1108,7 @@ static hipEvent_t prof_event() {
         if (g_prof) {                                                                \
             hipEvent_t e1_ = prof_event();                                           \
             hipEventRecord(e1_, ST);                                                 \
-            g_prof->recs.push_back({NAME, e0_, e1_, dim3(GRID).x, g_work});          \
+            g_prof->recs.push_back({NAME, e0_, e1_, dim3(GRID).x, g_work, g_level}); \
             g_work = 0;                                                              \
         }                                                                            \
     } while (0)
@@ -1141,6 +1160,7 @@ void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
 void launch_factor(const DevPlan &L, hipStream_t st) {
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
+        g_level = (int)h;
         for (int slot = 0; slot < 2; slot++)
             if (lv.nea[slot] > 0)
                 LAUNCH("ea", dev::k_ea, dim3(lv.nea[slot]), dim3(256), st, lv.nea[slot],
@@ -1165,6 +1185,7 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st) {
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
+        g_level = (int)h;
         if (lv.nfwd > 0)
             LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off,
                    L.fd, rhs, L.vec);
@@ -1175,6 +1196,7 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
     }
     for (size_t hh = L.levels.size(); hh-- > 0;) {
         const auto &lv = L.levels[hh];
+        g_level = (int)hh;
         if (lv.nbgemv > 0)
             LAUNCH("bwd_init", dev::k_bwd_init, dim3(lv.nbgemv), dim3(256), st, lv.nbgemv,
                    L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.yvec, L.vec);

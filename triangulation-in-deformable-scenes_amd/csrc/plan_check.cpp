@@ -102,6 +102,14 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                             acc += A[(int64_t)(k0 + k) * m + r] * (A[(int64_t)(k0 + k) * m + c] * A[(int64_t)(k0 + k) * m + k0 + k]);
                         A[(int64_t)c * m + r] -= acc;
                     }
+                // direct assembly (k_update): the front's final contribution block goes to the parent
+                if (!st.inner && k0 + kb == F.s && F.direct) {
+                    const Front &Pf = S.fronts[F.parent];
+                    const int32_t *bm = S.bmap.data() + F.bmap_off - F.s;
+                    for (int c = tj; c < std::min(tj + 64, m); c++)
+                        for (int r = std::max(ti, c); r < std::min(ti + 64, m); r++)
+                            Fp(F.parent)[(int64_t)bm[c] * Pf.m + bm[r]] += A[(int64_t)c * m + r];
+                }
             }
             // fused panel factorization of the next panel (k_update on the diagonal tile)
             for (int32_t t = 0; t < st.nupd; t++) {

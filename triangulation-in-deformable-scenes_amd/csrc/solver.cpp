@@ -302,19 +302,20 @@ int upload_device(deftri_ctx *ctx) {
     if ((rc = dalloc(ctx, &L.inv, S.inv_size))) return rc;
     {
         int32_t nf = (int32_t)S.fronts.size();
-        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf);
+        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf), dir(nf);
         std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf), io(nf);
         for (int32_t f = 0; f < nf; f++) {
             const Front &F = S.fronts[f];
             m[f] = F.m; s[f] = F.s; par[f] = F.parent; nch[f] = F.nchild; c0[f] = F.child[0]; c1[f] = F.child[1];
+            dir[f] = F.direct;
             ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off; io[f] = F.inv_off;
         }
-        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *prows, *pbmap;
+        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *pdir, *prows, *pbmap;
         int64_t *pao, *pvo, *pro, *pbo, *pio;
-        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1);
+        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1); PUT(pdir, dir);
         PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo); PUT(pio, io);
         PUT(prows, S.rows); PUT(pbmap, S.bmap);
-        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pao, pvo, pro, pbo, pio, prows, pbmap};
+        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pdir, pao, pvo, pro, pbo, pio, prows, pbmap};
     }
     PUT(L.tasks, S.task_i32);
     L.levels.clear();
@@ -476,7 +477,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     for (const auto &r : prof.recs) {
         float ms = 0;
         hipEventElapsedTime(&ms, r.e0, r.e1);
-        if (dump) std::fprintf(stderr, "[prof] %s %u %.4f %.6g\n", r.name, r.grid, ms, r.work);
+        if (dump) std::fprintf(stderr, "[prof] %s %u %.4f %.6g %d\n", r.name, r.grid, ms, r.work, r.level);
         int32_t k = 0;
         for (; k < n; k++) if (std::strcmp(stats[k].name, r.name) == 0) break;
         if (k == n) {

@@ -223,6 +223,19 @@ struct Builder {
             maxh = std::max(maxh, h);
         }
         S.nlevels = maxh + 1;
+        // direct assembly: a child adds its final contribution block into the parent from its last
+        // trailing-update launch, unless a sibling of the same level (slot 0) does so in that same
+        // launch — then this one (slot 1) goes through the extend-add launch after it, so every
+        // parent entry is summed in a fixed order
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            F.direct = 0;
+            if (F.parent < 0 || F.m == F.s || F.s == 0) continue;
+            const Front &Pf = S.fronts[F.parent];
+            bool slot1 = Pf.nchild > 1 && Pf.child[1] == f;
+            bool same = Pf.nchild > 1 && S.fronts[Pf.child[0]].height == S.fronts[Pf.child[1]].height;
+            F.direct = (slot1 && same) ? 0 : 1;
+        }
         S.level_fronts.assign(S.nlevels, {});
         for (int32_t f = 0; f < nf; f++) S.level_fronts[S.fronts[f].height].push_back(f);
         if (std::getenv("DEFTRI_DEBUG_PLAN")) {
@@ -352,6 +365,7 @@ struct Builder {
                     const Front &F = S.fronts[f];
                     if (F.nchild <= slot) continue;
                     int32_t c = F.child[slot];
+                    if (S.fronts[c].direct) continue;           // assembled by its own last update
                     int32_t u = S.fronts[c].m - S.fronts[c].s;
                     // (child, 16 CB columns j0.., 256 CB rows i0..), lower triangle only
                     for (int32_t j = 0; j < u; j += 16)

@@ -44,6 +44,8 @@ struct Front {
     int32_t m, s;
     int32_t parent;
     int32_t height;
+    int32_t direct;      // 1: the final trailing update adds this front's contribution block straight
+                         //    into the parent (no extend-add); 0: extend-add (a same-level slot-1 sibling)
     int32_t nchild;
     int32_t child[2];
 };
