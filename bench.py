@@ -2,7 +2,7 @@
 optimizer.optimize(nIterations), reference Modules/Optimization/g2oBundleAdjustment.cc) at
 config C2 of BASELINE.json: 100k two-view correspondences, per GPU.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 100000] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--corr 100000] [--no-cpu-baseline]
 
 A "step" is one accepted LM iteration of the device solver (linearize, assemble H, then up to 10
 damped trials of scatter + multifrontal LDL^T + solve + update + chi2 each).  The scene is
@@ -94,7 +94,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--corr", type=int, default=100000, help="correspondences per GPU (C2: 100k)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -104,14 +104,22 @@ def main():
     have_gpu = torch.cuda.is_available()
     if not have_gpu:
         raise SystemExit("bench.py needs a gfx950 GPU (no CPU path)")
-    torch.cuda.set_device(local)
+    # one process per GPU (RCCL); DEFTRI_DIST_BACKEND=gloo + DEFTRI_GPU_OVERRIDE=0 rehearse several
+    # ranks on one GPU (the path has no data-path collective: only the barrier and the timing reduce)
+    backend = os.environ.get("DEFTRI_DIST_BACKEND", "nccl")
+    gpu = int(os.environ.get("DEFTRI_GPU_OVERRIDE", local))
+    torch.cuda.set_device(gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     t0 = time.perf_counter()
-    prob = build_problem(args.n, 1 + rank)
+    prob = build_problem(args.corr, 1 + rank)
     log(f"[rank {rank}] graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
-    ctx = capi.Context(local)
+    ctx = capi.Context(gpu)
     t0 = time.perf_counter()
     ctx.upload(prob)
     log(f"[rank {rank}] upload + symbolic analysis {time.perf_counter() - t0:.1f}s")
@@ -135,7 +143,7 @@ def main():
     if iters != args.steps:
         log(f"[rank {rank}] WARNING: LM terminated after {iters} of {args.steps} iterations")
 
-    t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, "cuda")
+    t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
 
     # profiled trial (HIP events on the solver stream), at the final lambda of the timed run
     stats = ctx.profile_trial(rep["lambda_final"])
@@ -152,7 +160,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         t0 = time.perf_counter()
-        cpu = cpu_baseline(args.n, factor_flops, rep["trials_total"] / max(iters, 1))
+        cpu = cpu_baseline(args.corr, factor_flops, rep["trials_total"] / max(iters, 1))
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     if rank == 0:
@@ -162,7 +170,7 @@ def main():
             "value": it_sum / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2", "correspondences_per_gpu": args.n, "views": 2,
+            "config": {"workload": "C2" if args.corr == 100000 else f"two-view-{args.corr}", "correspondences_per_gpu": args.corr, "views": 2,
                        "points": prob.n_points, "arap_edges": len(prob.arap_pair), "unknowns": rep["n_unknowns"],
                        "fronts": rep["n_fronts"], "nnz_factor": rep["nnz_factor"],
                        "factor_gflop": round(factor_flops / 1e9, 3),

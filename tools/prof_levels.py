@@ -14,6 +14,9 @@ if os.environ.get("DEFTRI_PROF_CHILD") is None:
     lev = collections.defaultdict(lambda: collections.defaultdict(float))
     for _, n, g, ms, w, l in rows:
         lev[int(l)][n] += float(ms)
+    with open(ROOT / "gpurun_out" / "prof_seq.txt", "w") as fo:
+        for _, n, g, ms, w, l in rows:
+            fo.write(f"{l} {n} {g} {1e3 * float(ms):.1f} {float(w) / 1e9:.4f}\n")
     print("per level (ms):")
     for l in sorted(lev):
         tot_l = sum(lev[l].values())
