@@ -452,6 +452,16 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __builtin_bit_cast(double, p);
 }
 
+// 1/d from v_rcp_f64 and two Newton steps (≈0.5 ulp for the normal, positive pivots of an SPD
+// block): a fraction of the latency of the IEEE division sequence on the 64-step pivot chain
+__device__ __forceinline__ double rcp_d(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -476,14 +486,46 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
     const int er = tid & 15, ec = tid >> 4;                    // element of the 16x16 block
     // rows/cols >= kb are identity padding: sub-blocks past nsub and pivot steps past kb are no-ops
     const int nsub = (kb + 15) >> 4;
+#ifdef DEFTRI_DIAG_TIMING
+    long long tp[16]; int ntp = 0;
+    tp[ntp++] = clock64();
+#endif
     for (int K = 0; K < nsub; K++) {
         const int j0 = 16 * K;
         const int jend = min(16, kb - j0);
-        // ---- F: factor the diagonal block + its inverse, element per thread ----
-        for (int j = 0; j < jend; j++) {
+        // ---- F: factor the diagonal block + its inverse, element per thread, two pivot columns per
+        //      step (one barrier per pair): with l_x0 d0 = a_x0 and a'_x1 = a_x1 - a_x0 l10,
+        //      A[r][c] -= a_r0 a_c0 / d0 + a'_r1 a'_c1 / d1,  X[r][:] -= l_r0 X[j][:] + l_r1 X'[j+1][:]
+        int j = 0;
+        for (; j + 1 < jend; j += 2) {
+            const double a00 = S[j0 + j][j0 + j], a10 = S[j0 + j + 1][j0 + j], a11 = S[j0 + j + 1][j0 + j + 1];
+            const double ar0 = S[j0 + er][j0 + j], ar1 = S[j0 + er][j0 + j + 1];
+            const double ac0 = S[j0 + ec][j0 + j], ac1 = S[j0 + ec][j0 + j + 1];
+            const double xj = (ec == j) ? 1.0 : (ec < j ? S[j0 + ec][j0 + j] : 0.0);          // X[j][c]
+            const double xj1o = (ec < j) ? S[j0 + ec][j0 + j + 1] : 0.0;                      // X[j+1][c] (old)
+            const double rd0 = rcp_d(a00);
+            const double l10 = a10 * rd0;
+            const double d1 = a11 - l10 * a10;
+            const double rd1 = rcp_d(d1);
+            const double lr0 = ar0 * rd0;
+            const double ar1p = ar1 - ar0 * l10;
+            const double lr1 = ar1p * rd1;
+            const double xj1 = (ec == j + 1) ? 1.0 : (ec < j ? xj1o - l10 * xj : (ec == j ? -l10 : 0.0));  // X'[j+1][c]
+            if (er > j + 1) {
+                if (ec > j + 1 && er >= ec) S[j0 + er][j0 + ec] -= ar0 * ac0 * rd0 + ar1p * (ac1 - ac0 * l10) * rd1;
+                if (ec <= j + 1) S[j0 + ec][j0 + er] -= lr0 * xj + lr1 * xj1;
+            }
+            if (tid == 0 && (a00 == 0.0 || d1 == 0.0)) atomicOr(flag, 1);
+            __syncthreads();
+            if (ec == j && er > j) S[j0 + er][j0 + j] = lr0;                                   // L[:, j]
+            if (ec == j + 1 && er > j + 1) S[j0 + er][j0 + j + 1] = lr1;                       // L[:, j+1]
+            if (ec == j + 1 && er == j + 1) S[j0 + j + 1][j0 + j + 1] = d1;                    // D[j+1]
+            if (er == j + 1 && ec <= j) S[j0 + ec][j0 + j + 1] = xj1;                          // X[j+1][c]
+        }
+        for (; j < jend; j++) {
             const double d = S[j0 + j][j0 + j];
             const double ar = S[j0 + er][j0 + j], ac = S[j0 + ec][j0 + j];
-            const double rd = 1.0 / d;
+            const double rd = rcp_d(d);
             const double lr = ar * rd;
             if (er > j) {
                 if (ec > j && er >= ec) S[j0 + er][j0 + ec] -= lr * ac;                  // A -= l_r d l_c
@@ -497,6 +539,9 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
             if (ec == j && er > j) S[j0 + er][j0 + j] = lr;                              // scale column j
         }
         __syncthreads();
+#ifdef DEFTRI_DIAG_TIMING
+        tp[ntp++] = clock64();
+#endif
         const int nrt = nsub - 1 - K;                          // 16-row tiles below the sub-panel
         // ---- X: X_KJ = -X_KK T_KJ for J < K (T_KJ at S[16J + c][j0 + r]) ----
         if (wv >= nrt && wv - nrt < K) {
@@ -529,6 +574,9 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
         }
         if (K == nsub - 1) break;
         __syncthreads();
+#ifdef DEFTRI_DIAG_TIMING
+        tp[ntp++] = clock64();
+#endif
         // ---- U: Schur tiles (Rt >= Ct) then inverse accumulators (I > K, J <= K) ----
         const int nsch = nrt * (nrt + 1) / 2, ninv = nrt * (K + 1);
         for (int t = wv; t < nsch + ninv; t += 4) {
@@ -566,8 +614,20 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
             }
         }
         __syncthreads();
+#ifdef DEFTRI_DIAG_TIMING
+        tp[ntp++] = clock64();
+#endif
     }
     __syncthreads();
+#ifdef DEFTRI_DIAG_TIMING
+    tp[ntp++] = clock64();
+    if (threadIdx.x == 0 && (blockIdx.x & 1023) == 0) {
+        long long d[13];
+        for (int q = 0; q < 13; q++) d[q] = (q + 1 < ntp) ? tp[q + 1] - tp[q] : 0;
+        printf("[diagphase] kb %d: %lld %lld %lld | %lld %lld %lld | %lld %lld %lld | %lld %lld %lld | %lld\n", kb, d[0],
+               d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12]);
+    }
+#endif
 }
 
 // load the panel diagonal block of (front F, panel k0) into S (identity padding), factor, store L/D
