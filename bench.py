@@ -37,6 +37,7 @@ import numpy as np  # noqa: E402
 from deftri import capi, sim  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6
+MFMA_F64_SUSTAINED_TFLOPS = 48.3   # v_mfma_f64_16x16x4 back-to-back on this box (tools/micro/mfma_f64_peak.hip)
 BASELINE_METRIC = "LM iterations/sec + ms/iter at 100k corr \u00d7 2 views; 1/2/4/8-GPU scaling"
 REP_W, ARAP_W, DEPTH_SIGMA = 1.0, 2e5, np.float32(3.0 / 1000.0)
 
@@ -150,9 +151,19 @@ def main():
     upd = stats["update"]
     factor_flops = rep["factor_flops"]
     achieved = upd["flops"] / (upd["ms"] * 1e-3) / 1e12
+    # HBM bytes of k_update per factorization from the committed rocprofv3 PMC pass (tools/gpu_pmc.sh +
+    # tools/pmc_summary.py), attached only when it was collected on this same plan
+    traffic = None
+    pmc = sorted(ROOT.glob("profiles/*_pmc_k_update.json"))
+    if pmc:
+        pj = json.loads(pmc[-1].read_text())
+        if abs(pj.get("update_flops_per_factorization", -1) - upd["flops"]) < 1e-6 * upd["flops"]:
+            traffic = pj["traffic_bytes_per_factorization"]
     roofline = {"bound": "mfma", "kernel": "k_update", "achieved": round(achieved, 3),
                 "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
-                "traffic": None, "launches": upd["launches"],
+                "peak_sustained_measured": MFMA_F64_SUSTAINED_TFLOPS,
+                "traffic": traffic, "traffic_unit": "bytes per factorization (all k_update launches)",
+                "launches": upd["launches"],
                 "avg_launch_us": round(1e3 * upd["ms"] / max(upd["launches"], 1), 3),
                 "flops_per_factorization": upd["flops"]}
     trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
