@@ -64,3 +64,12 @@ def test_plan_scaling_is_subquadratic(host):
         sizes.append(p.n_unknowns); nnz.append(host.plan_stats()["nnz_factor"])
     growth = np.log(nnz[1] / nnz[0]) / np.log(sizes[1] / sizes[0])
     assert growth < 1.5
+
+
+def test_plan_lookahead_split(host, monkeypatch):
+    """The optional LOOK/REST split of the outer updates (side-stream overlap, off by default)
+    must factor exactly like the single trailing update."""
+    monkeypatch.setenv("DEFTRI_LOOKAHEAD_MIN_M", "0")
+    m, _ = sim.simulate_two_view(n=1500, seed=5, scale_scene=True, compact=True)   # root front s = 288 > one outer block
+    p = host.build_graph(m, 1.0, 2e5, np.float32(0.003))
+    check(host, p)

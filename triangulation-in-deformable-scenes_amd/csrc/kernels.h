@@ -40,7 +40,7 @@ struct FrontDev {
 
 struct LevelDev {
     int64_t ea_off[2]; int32_t nea[2];
-    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner; double upd_flops; };
+    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner, stream, wait_side; double upd_flops; };
     std::vector<Step> steps;
     int64_t fwd_off; int32_t nfwd;
     struct SolveStep { int64_t off; int32_t n; };
@@ -94,7 +94,7 @@ void set_profiler(KProf *p);
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);
-void launch_factor(const DevPlan &L, hipStream_t st);
+void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev);
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st);
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st);
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "device_math.h"
 #include "kernels.h"
@@ -804,7 +805,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     int K = min(kmax, s - kA);
     // inner updates stop at the end of the outer block (own columns): a tile straddling it must not
     // touch the columns the outer update will cover
-    int cend = inner ? min(s, (kA / kOuter + 1) * kOuter) : m;
+    int cend = inner == 1 ? min(s, (kA / kOuter + 1) * kOuter) : inner == 2 ? min(s, (kA / kOuter + 2) * kOuter) : m;
     double *F = arena + fd.arena_off[f];
     int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int rb = ti + (w & 1) * 32, cb = tj + (w >> 1) * 32;
@@ -1217,7 +1218,9 @@ void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
                            L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, lambda, L.arena);
 }
 
-void launch_factor(const DevPlan &L, hipStream_t st) {
+void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev) {
+    int evi = 0;
+    hipEvent_t prev_side = nullptr, cur_side = nullptr;   // events of the last two side-stream updates
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         g_level = (int)h;
@@ -1232,6 +1235,26 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
             if (stp.ntrsm > 0)
                 LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(256), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
                                    L.fd, L.arena, L.inv);
+            static const bool no_side = std::getenv("DEFTRI_NO_SIDE_STREAM") != nullptr;   // A/B experiments
+            if (stp.stream == 1 && !no_side) {
+                // "rest" update of an outer block: after the block's panel chain on the main stream,
+                // concurrent with the next block's lookahead + panel chain there
+                prev_side = cur_side;
+                cur_side = nullptr;
+                if (stp.nupd > 0) {
+                    hipEvent_t e = ev[evi++ % nev];
+                    hipEventRecord(e, st);
+                    hipStreamWaitEvent(side, e, 0);
+                    g_work = stp.upd_flops;
+                    LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), side, stp.nupd,
+                           L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv, L.flag);
+                    cur_side = ev[evi++ % nev];
+                    hipEventRecord(cur_side, side);
+                }
+                continue;
+            }
+            if (stp.wait_side >= 1 && prev_side) hipStreamWaitEvent(st, prev_side, 0);
+            if (stp.wait_side == 2 && cur_side) hipStreamWaitEvent(st, cur_side, 0);
             if (stp.nupd > 0) {
                 g_work = stp.upd_flops;
                 LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), st, stp.nupd,
@@ -1239,6 +1262,10 @@ void launch_factor(const DevPlan &L, hipStream_t st) {
                        L.arena, L.inv, L.flag);
             }
         }
+        // the level's side-stream work must be complete before the next level (or the solve) reads it
+        if (cur_side) hipStreamWaitEvent(st, cur_side, 0);
+        if (prev_side) hipStreamWaitEvent(st, prev_side, 0);
+        prev_side = cur_side = nullptr;
     }
 }
 

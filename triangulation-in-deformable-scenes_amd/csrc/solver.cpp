@@ -72,6 +72,8 @@ static void quat_mat(const double *q, double *R) {
 struct deftri_ctx {
     int device = 0;
     hipStream_t st = nullptr;
+    hipStream_t side = nullptr;                 // trailing "rest" updates overlapping the panel chain
+    hipEvent_t sync_ev[64]{};                   // cross-stream ordering events (timing disabled)
     std::string err;
     bool have = false;        // uploaded to the device
     bool analysed = false;    // symbolic plan available
@@ -323,7 +325,7 @@ int upload_device(deftri_ctx *ctx) {
         LevelDev ld{};
         for (int k = 0; k < 2; k++) { ld.ea_off[k] = lv.ea_off[k]; ld.nea[k] = lv.nea[k]; }
         for (const auto &stp : lv.steps)
-            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner, stp.upd_flops});
+            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner, stp.stream, stp.wait_side, stp.upd_flops});
         ld.fwd_off = lv.fwd_off; ld.nfwd = lv.nfwd;
         for (const auto &x : lv.fsteps) ld.fsteps.push_back({x.off, x.n});
         for (const auto &x : lv.bsteps) ld.bsteps.push_back({x.off, x.n});
@@ -400,11 +402,18 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
     if (device < 0 || device >= n) return DEFTRI_E_NODEVICE;
     deftri_ctx *ctx = new deftri_ctx();
     ctx->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+    // the main stream (panel chain: the critical path) gets the higher priority; the side stream's
+    // big trailing updates fill the CUs it leaves free
+    int prio_lo = 0, prio_hi = 0;
+    if (hipSetDevice(device) == hipSuccess) hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         delete ctx;
         return DEFTRI_E_HIP;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
+    hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
+    for (auto &e : ctx->sync_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     *out = ctx;
     return 0;
 }
@@ -415,6 +424,8 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     hipSetDevice(ctx->device);
     free_device(ctx);
     for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
+    for (auto &e : ctx->sync_ev) if (e) hipEventDestroy(e);
+    if (ctx->side) hipStreamDestroy(ctx->side);
     if (ctx->st) hipStreamDestroy(ctx->st);
     delete ctx;
     return 0;
@@ -468,7 +479,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     launch_assemble(ctx->P, ctx->L, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     launch_scatter(ctx->L, lambda, ctx->st);
-    launch_factor(ctx->L, ctx->st);
+    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
     launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st);
     set_profiler(nullptr);
     HIPOK(hipStreamSynchronize(ctx->st));
@@ -584,7 +595,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             hipEventRecord(ctx->ev[2], ctx->st);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
             launch_scatter(L, lambda, ctx->st);              // setLambda
-            launch_factor(L, ctx->st);
+            launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64);
             hipEventRecord(ctx->ev[3], ctx->st);
             launch_solve(L, L.b, ctx->d_dx, ctx->st);
             hipEventRecord(ctx->ev[4], ctx->st);
@@ -714,7 +725,7 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
     launch_assemble(ctx->P, ctx->L, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     launch_scatter(ctx->L, lambda, ctx->st);
-    launch_factor(ctx->L, ctx->st);
+    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
     launch_solve(ctx->L, dr, ctx->d_dx, ctx->st);
     int flag = 0;
     hipMemcpyAsync(&flag, ctx->L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st);

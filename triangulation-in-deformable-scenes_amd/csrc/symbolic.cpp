@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <limits>
 #include <numeric>
 
 namespace deftri {
@@ -380,19 +381,35 @@ struct Builder {
             // launch that finishes their diagonal tile)] + trsm + an inner update restricted to the
             // block's remaining own columns; after the block, one outer update with K = the block
             // width covers every trailing column (own and contribution block).
-            auto push_update = [&](Symbolic::StepTasks &st, int32_t kA, int32_t kmax, bool inner) {
+            // update modes: INNER = panel kA's update of the outer block's remaining own columns;
+            // FULL = block kA's update of every trailing column; LOOK = the next block's columns only
+            // (carries the fused factorization of its first panel); REST = the columns past the next
+            // block (and the whole trailing part of fronts that end in this block).
+            enum { UP_INNER = 1, UP_FULL = 0, UP_LOOK = 2, UP_REST = 3 };
+            auto push_update = [&](Symbolic::StepTasks &st, int32_t kA, int32_t kmax, int mode) {
                 st.upd_off = (int64_t)S.task_i32.size() / 3;
-                st.kA = kA; st.kmax = kmax; st.inner = inner ? 1 : 0;
+                st.kA = kA; st.kmax = kmax;
+                st.inner = mode == UP_INNER ? 1 : mode == UP_LOOK ? 2 : 0;
+                const int32_t Pend = (kA / kOuter + 1) * kOuter;
                 // pass 0: the tiles that carry a fused panel factorization go first in the launch
+                std::vector<std::array<int32_t, 4>> spans;   // (front, t0 column, tend column, has_diag)
+                for (int32_t f : fs) {
+                    const Front &F = S.fronts[f];
+                    if (F.s <= kA) continue;
+                    const int32_t K = std::min(kmax, F.s - kA);
+                    int32_t t0 = kA + K, tend = F.m;
+                    if (mode == UP_INNER) tend = std::min(F.s, Pend);
+                    if (mode == UP_LOOK) { if (F.s <= Pend) continue; t0 = Pend; tend = std::min(F.s, Pend + kOuter); }
+                    if (mode == UP_REST && F.s > Pend) t0 = std::min(F.s, Pend + kOuter);
+                    if (t0 >= tend) continue;
+                    const bool has_diag = (mode == UP_INNER || mode == UP_LOOK || mode == UP_FULL) && F.s > t0 && t0 == kA + K;
+                    spans.push_back({f, t0, tend, has_diag ? 1 : 0});
+                }
                 for (int pass = 0; pass < 2; pass++)
-                    for (int32_t f : fs) {
+                    for (const auto &sp : spans) {
+                        const int32_t f = sp[0], t0 = sp[1], tend = sp[2];
+                        const bool has_diag = sp[3] != 0;
                         const Front &F = S.fronts[f];
-                        if (F.s <= kA) continue;
-                        int32_t K = std::min(kmax, F.s - kA);
-                        int32_t t0 = kA + K;
-                        int32_t tend = inner ? std::min(F.s, (kA / kOuter + 1) * kOuter) : F.m;
-                        if (inner && t0 >= tend) continue;
-                        bool has_diag = F.s > t0;
                         if (pass == 0) {
                             if (has_diag) { push3(f, t0, t0); st.nupd++; }
                             continue;
@@ -403,15 +420,12 @@ struct Builder {
                                 push3(f, ti, tj); st.nupd++;
                             }
                     }
-                for (int32_t f : fs) {
-                    const Front &F = S.fronts[f];
-                    if (F.s <= kA) continue;
-                    int32_t K = std::min(kmax, F.s - kA);
-                    int32_t t0 = kA + K;
-                    int32_t tend = inner ? std::min(F.s, (kA / kOuter + 1) * kOuter) : F.m;
+                for (const auto &sp : spans) {
+                    const Front &F = S.fronts[sp[0]];
+                    const int32_t K = std::min(kmax, F.s - kA), t0 = sp[1], tend = sp[2];
                     for (int32_t tj = t0; tj < tend; tj += 64)
                         for (int32_t ti = tj; ti < F.m; ti += 64) {
-                            double fl = 2.0 * std::min(64, F.m - ti) * std::min(64, std::min(F.m, tend) - tj) * K;
+                            double fl = 2.0 * std::min(64, F.m - ti) * std::min(64, tend - tj) * K;
                             S.update_flops += fl;
                             st.upd_flops += fl;
                         }
@@ -437,14 +451,36 @@ struct Builder {
                             S.trsm_flops += (double)std::min(64, F.m - r0) * kb * kb;
                         }
                     }
-                    push_update(st, k0, kPanel, true);
+                    push_update(st, k0, kPanel, UP_INNER);
                     LT.steps.push_back(st);
                 }
-                Symbolic::StepTasks so;
-                so.k0 = P0;
-                so.diag_off = so.trsm_off = (int64_t)S.task_i32.size() / 3;
-                push_update(so, P0, kOuter, false);
-                LT.steps.push_back(so);
+                // outer update of block P0: when some front continues past the block, split it into
+                // REST (side stream, overlaps the next block's panel chain) and LOOK (main stream: the
+                // next block's columns + the fused factorization of its first panel)
+                // Measured at C2 on MI355X: the split (one more launch per block) costs more than the
+                // overlap recovers (19.2 vs 18.9 LM it/s), so it is off unless DEFTRI_LOOKAHEAD_MIN_M
+                // names the smallest front order that should use it.
+                const char *la_env = std::getenv("DEFTRI_LOOKAHEAD_MIN_M");
+                const int32_t la_min_m = la_env ? std::atoi(la_env) : std::numeric_limits<int32_t>::max();
+                bool cont = false;
+                int32_t maxm = 0;
+                for (int32_t f : fs) { cont = cont || S.fronts[f].s > P0 + kOuter; maxm = std::max(maxm, S.fronts[f].m); }
+                cont = cont && maxm >= la_min_m;
+                auto outer_step = [&](int mode, int stream, int wait_side) {
+                    Symbolic::StepTasks so;
+                    so.k0 = P0;
+                    so.diag_off = so.trsm_off = (int64_t)S.task_i32.size() / 3;
+                    push_update(so, P0, kOuter, mode);
+                    so.stream = stream; so.wait_side = wait_side;
+                    LT.steps.push_back(so);
+                };
+                if (cont) {
+                    outer_step(UP_REST, 1, 0);
+                    outer_step(UP_LOOK, 0, 1);
+                } else {
+                    // touches the trailing columns an earlier REST (side stream) may still be updating
+                    outer_step(UP_FULL, 0, 2);
+                }
             }
             LT.fwd_off = (int64_t)S.task_i32.size() / 3;
             for (int32_t f : fs) { push3(f, 0, 0); LT.nfwd++; }

@@ -94,7 +94,12 @@ struct Symbolic {
         int64_t upd_off = 0; int32_t nupd = 0;        // (front, tile-i, tile-j) triples
         int32_t k0 = 0;                               // panel of diag / trsm
         int32_t kA = 0, kmax = 0;                     // update: L columns [kA, kA + min(kmax, s - kA))
-        int32_t inner = 0;                            // 1: columns clipped at the outer block end
+        int32_t inner = 0;                            // column clip: 0 none, 1 end of this outer block
+                                                      // (inner update), 2 end of the next block (lookahead)
+        int32_t stream = 0;                           // 0: main stream; 1: side stream (trailing "rest"
+                                                      // update, overlaps the next block's panel chain)
+        int32_t wait_side = 0;                        // main stream waits for side launches first:
+                                                      // 1 the one before the latest, 2 all of them
         double upd_flops = 0;                         // algorithmic flops of this update launch
     };
     struct LevelTasks {
