@@ -523,6 +523,7 @@ struct Builder {
 
 bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points) {
     S = Symbolic();
+    if (const char *e = std::getenv("DEFTRI_ND_LEAF")) leaf_points = std::max(2, std::atoi(e));   // tuning
     Builder b(d, S, leaf_points);
     return b.run();
 }

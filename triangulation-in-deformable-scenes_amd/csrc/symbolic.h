@@ -122,6 +122,6 @@ struct Symbolic {
 };
 
 // Build the full plan for a validated problem.  Returns false (and sets error) on failure.
-bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points = 16);
+bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points = 32);   // leaf 32: best of 8..64 at C2
 
 }  // namespace deftri
