@@ -82,23 +82,56 @@ struct Builder {
             for (int64_t p : o) ov.push_back(vP((int32_t)p));
             return new_front(std::move(ov), {});
         }
-        double mn[2] = {1e300, 1e300}, mx[2] = {-1e300, -1e300};
-        for (int64_t p : nodes)
-            for (int k = 0; k < 2; k++) { mn[k] = std::min(mn[k], xy[2 * p + k]); mx[k] = std::max(mx[k], xy[2 * p + k]); }
-        int ax = (mx[0] - mn[0] >= mx[1] - mn[1]) ? 0 : 1;
-        std::sort(nodes.begin(), nodes.end(), [&](int64_t a, int64_t b) {
-            double x = xy[2 * a + ax], y = xy[2 * b + ax];
-            return x < y || (x == y && a < b);
-        });
-        int64_t half = n / 2;
-        for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < half) ? 1 : 2;
-        for (int64_t i = 0; i < half; i++) {
-            int64_t v = vP((int32_t)nodes[i]);
-            for (int64_t k = adj_begin[v]; k < adj_begin[v + 1]; k++) {
-                int64_t u = adj[k] - ((int64_t)Q + NS);
-                if (u >= 0 && side[u] == 2) { side[nodes[i]] = 3; break; }
+        // vertex separator: order along a direction, cut, take the boundary vertices of the side with
+        // fewer of them (the cut edges need one endpoint each).  Four directions (x, y, both
+        // diagonals) x three cut positions (45/50/55 %) are tried; the smallest separator wins.
+        auto boundary = [&](int64_t cut, bool left, std::vector<int64_t> *out) -> int64_t {
+            for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < cut) ? 1 : 2;
+            const int other = left ? 2 : 1;
+            int64_t cnt = 0;
+            for (int64_t i = left ? 0 : cut; i < (left ? cut : n); i++) {
+                int64_t v = vP((int32_t)nodes[i]);
+                for (int64_t k = adj_begin[v]; k < adj_begin[v + 1]; k++) {
+                    int64_t u = adj[k] - ((int64_t)Q + NS);
+                    if (u >= 0 && side[u] == other) { cnt++; if (out) out->push_back(nodes[i]); break; }
+                }
+            }
+            return cnt;
+        };
+        constexpr int ND_DIRS = 4;
+        double dirs[ND_DIRS][2];
+        for (int d = 0; d < ND_DIRS; d++) { dirs[d][0] = std::cos(M_PI * d / ND_DIRS); dirs[d][1] = std::sin(M_PI * d / ND_DIRS); }
+        // membership of the k smallest (key, index) is all a cut needs: nth_element, O(n) per cut
+        auto place = [&](int d, int64_t lo, int64_t hi, int64_t cut) {
+            auto less = [&](int64_t a, int64_t b) {
+                double x = dirs[d][0] * xy[2 * a] + dirs[d][1] * xy[2 * a + 1];
+                double y = dirs[d][0] * xy[2 * b] + dirs[d][1] * xy[2 * b + 1];
+                return x < y || (x == y && a < b);
+            };
+            std::nth_element(nodes.begin() + lo, nodes.begin() + cut, nodes.begin() + hi, less);
+        };
+        int64_t best_cut = n / 2, best_sz = -1;
+        int best_dir = 0;
+        bool best_left = true;
+        const int64_t c50 = n / 2, c45 = (n * 9) / 20, c55 = (n * 11) / 20;
+        for (int d = 0; d < ND_DIRS; d++) {
+            place(d, 0, n, c50);
+            if (c45 > 0) place(d, 0, c50, c45);
+            if (c55 < n && c55 > c50) place(d, c50, n, c55);
+            for (int64_t cut : {c50, c45, c55}) {
+                if (cut <= 0 || cut >= n) continue;
+                for (bool left : {true, false}) {
+                    int64_t sz = boundary(cut, left, nullptr);
+                    if (best_sz < 0 || sz < best_sz) { best_sz = sz; best_cut = cut; best_left = left; best_dir = d; }
+                }
             }
         }
+        place(best_dir, 0, n, best_cut);
+        const int ax = best_dir;
+        std::vector<int64_t> sep;
+        boundary(best_cut, best_left, &sep);
+        for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < best_cut) ? 1 : 2;
+        for (int64_t p : sep) side[p] = 3;
         std::vector<int64_t> L, R, Sp;
         for (int64_t p : nodes) {
             if (side[p] == 1) L.push_back(p);
