@@ -26,6 +26,13 @@ struct Builder {
     std::vector<int32_t> vfront;                  // vertex -> owning front
     int64_t next_pos = 0;
     std::vector<int32_t> side;
+    std::vector<int32_t> stamp;      // distinct-count scratch
+    int32_t stamp_id = 0;
+    int nd_dirs = 4;
+    int nd_passes = 8;
+    int nd_try = 3;
+    double nd_bal = 0.55;
+    std::vector<int64_t> spos;       // index of a point in the separator list being refined
 
     Builder(const deftri_problem_desc &d_, Symbolic &S_, int leaf_) : d(d_), S(S_), leaf(leaf_) {
         Q = d.n_pairs; NS = d.n_scales; P = d.n_points;
@@ -73,6 +80,76 @@ struct Builder {
         return f;
     }
 
+    // Fiduccia-Mattheyses-style vertex-separator refinement on the current subdomain (side[] = 1/2 for
+    // the halves, 3 for the separator).  A move takes a separator point to one half and pulls its
+    // neighbours in the other half into the separator (size change: -1 + that count).  Each pass
+    // makes the best balanced move repeatedly (hill-climbing through non-positive gains, moved
+    // points locked) and rolls back to the smallest separator seen.
+    void refine_sep(std::vector<int64_t> &sep, int64_t &nA, int64_t &nB, int64_t ntot) {
+        const int64_t cap = (int64_t)std::ceil(nd_bal * (double)ntot);
+        for (size_t i = 0; i < sep.size(); i++) spos[sep[i]] = (int64_t)i;
+        auto sep_add = [&](int64_t u) { spos[u] = (int64_t)sep.size(); sep.push_back(u); };
+        auto sep_del = [&](int64_t u) {
+            int64_t i = spos[u], last = sep.back();
+            sep[i] = last; spos[last] = i; sep.pop_back(); spos[u] = -1;
+        };
+        auto nbrs = [&](int64_t v, auto &&fn) {
+            int64_t gv = vP((int32_t)v);
+            for (int64_t k = adj_begin[gv]; k < adj_begin[gv + 1]; k++) {
+                int64_t u = adj[k] - ((int64_t)Q + NS);
+                if (u >= 0) fn(u);
+            }
+        };
+        struct Move { int64_t v; int t; size_t p0, p1; };
+        for (int pass = 0; pass < nd_passes; pass++) {
+            std::vector<Move> log;
+            std::vector<int64_t> pulled;
+            size_t best_len = 0;
+            int64_t best_sz = (int64_t)sep.size(), best_imb = std::llabs(nA - nB);
+            const int32_t lock = ++stamp_id;
+            const int64_t maxsteps = (int64_t)sep.size();
+            for (int64_t step = 0; step < maxsteps; step++) {
+                int64_t bv = -1, bg = 0, bimb = 0;
+                int bt = 0;
+                for (int64_t v : sep) {
+                    if (stamp[v] == lock) continue;
+                    int64_t cA = 0, cB = 0;
+                    nbrs(v, [&](int64_t u) { cA += side[u] == 1; cB += side[u] == 2; });
+                    for (int t = 1; t <= 2; t++) {
+                        const int64_t k = t == 1 ? cB : cA;
+                        const int64_t a2 = t == 1 ? nA + 1 : nA - cA, b2 = t == 1 ? nB - cB : nB + 1;
+                        if (std::max(a2, b2) > cap || std::min(a2, b2) < 1) continue;
+                        const int64_t g = 1 - k, imb = std::llabs(a2 - b2);
+                        if (bv < 0 || g > bg || (g == bg && imb < bimb)) { bv = v; bt = t; bg = g; bimb = imb; }
+                    }
+                }
+                if (bv < 0) break;
+                const int other = 3 - bt;
+                sep_del(bv);
+                side[bv] = bt;
+                stamp[bv] = lock;
+                const size_t p0 = pulled.size();
+                nbrs(bv, [&](int64_t u) { if (side[u] == other) { side[u] = 3; sep_add(u); pulled.push_back(u); } });
+                const int64_t k = (int64_t)(pulled.size() - p0);
+                if (bt == 1) { nA += 1; nB -= k; } else { nB += 1; nA -= k; }
+                log.push_back({bv, bt, p0, pulled.size()});
+                const int64_t sz = (int64_t)sep.size(), imb = std::llabs(nA - nB);
+                if (sz < best_sz || (sz == best_sz && imb < best_imb)) { best_sz = sz; best_imb = imb; best_len = log.size(); }
+            }
+            for (size_t i = log.size(); i > best_len; i--) {      // roll back past the best state
+                const Move &m = log[i - 1];
+                const int other = 3 - m.t;
+                for (size_t j = m.p0; j < m.p1; j++) { side[pulled[j]] = other; sep_del(pulled[j]); }
+                const int64_t k = (int64_t)(m.p1 - m.p0);
+                if (m.t == 1) { nA -= 1; nB += k; } else { nB -= 1; nA += k; }
+                side[m.v] = 3;
+                sep_add(m.v);
+            }
+            if (best_len == 0) break;
+        }
+        for (int64_t p : sep) spos[p] = -1;
+    }
+
     int32_t nd(std::vector<int64_t> &nodes, int depth) {
         int64_t n = (int64_t)nodes.size();
         if (n <= leaf || depth > 48) {
@@ -82,9 +159,10 @@ struct Builder {
             for (int64_t p : o) ov.push_back(vP((int32_t)p));
             return new_front(std::move(ov), {});
         }
-        // vertex separator: order along a direction, cut, take the boundary vertices of the side with
-        // fewer of them (the cut edges need one endpoint each).  Four directions (x, y, both
-        // diagonals) x three cut positions (45/50/55 %) are tried; the smallest separator wins.
+        // vertex separator: order along a direction, cut, take the boundary vertices of one side (the
+        // cut edges need one endpoint each).  Four directions (x, y, both diagonals) x three cut
+        // positions (45/50/55 %) x two sides are candidates; the nd_try smallest are refined
+        // (refine_sep) and the smallest refined separator wins.
         auto boundary = [&](int64_t cut, bool left, std::vector<int64_t> *out) -> int64_t {
             for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < cut) ? 1 : 2;
             const int other = left ? 2 : 1;
@@ -98,8 +176,8 @@ struct Builder {
             }
             return cnt;
         };
-        constexpr int ND_DIRS = 4;
-        double dirs[ND_DIRS][2];
+        const int ND_DIRS = nd_dirs;
+        double dirs[16][2];
         for (int d = 0; d < ND_DIRS; d++) { dirs[d][0] = std::cos(M_PI * d / ND_DIRS); dirs[d][1] = std::sin(M_PI * d / ND_DIRS); }
         // membership of the k smallest (key, index) is all a cut needs: nth_element, O(n) per cut
         auto place = [&](int d, int64_t lo, int64_t hi, int64_t cut) {
@@ -110,9 +188,8 @@ struct Builder {
             };
             std::nth_element(nodes.begin() + lo, nodes.begin() + cut, nodes.begin() + hi, less);
         };
-        int64_t best_cut = n / 2, best_sz = -1;
-        int best_dir = 0;
-        bool best_left = true;
+        struct Cand { double score; int d; int64_t cut; bool left; };
+        std::vector<Cand> cands;
         const int64_t c50 = n / 2, c45 = (n * 9) / 20, c55 = (n * 11) / 20;
         for (int d = 0; d < ND_DIRS; d++) {
             place(d, 0, n, c50);
@@ -121,17 +198,38 @@ struct Builder {
             for (int64_t cut : {c50, c45, c55}) {
                 if (cut <= 0 || cut >= n) continue;
                 for (bool left : {true, false}) {
-                    int64_t sz = boundary(cut, left, nullptr);
-                    if (best_sz < 0 || sz < best_sz) { best_sz = sz; best_cut = cut; best_left = left; best_dir = d; }
+                    const double score = (double)boundary(cut, left, nullptr);
+                    cands.push_back({score, d, cut, left});
                 }
             }
         }
-        place(best_dir, 0, n, best_cut);
-        const int ax = best_dir;
+        std::stable_sort(cands.begin(), cands.end(), [](const Cand &a, const Cand &b) { return a.score < b.score; });
+        // the separator of candidate c, refined; side[] left set for the subdomain
         std::vector<int64_t> sep;
-        boundary(best_cut, best_left, &sep);
-        for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < best_cut) ? 1 : 2;
-        for (int64_t p : sep) side[p] = 3;
+        auto realise = [&](const Cand &c) {
+            place(c.d, 0, n, c.cut);
+            sep.clear();
+            boundary(c.cut, c.left, &sep);
+            for (int64_t i = 0; i < n; i++) side[nodes[i]] = (i < c.cut) ? 1 : 2;
+            for (int64_t p : sep) side[p] = 3;
+            if (nd_passes > 0) {
+                int64_t nA = 0, nB = 0;
+                for (int64_t p : nodes) { nA += side[p] == 1; nB += side[p] == 2; }
+                refine_sep(sep, nA, nB, n);
+            }
+        };
+        size_t best = 0;
+        const size_t ntry = std::min(cands.size(), (size_t)std::max(1, nd_try));
+        if (ntry > 1) {
+            size_t best_sz = SIZE_MAX;
+            for (size_t c = 0; c < ntry; c++) {
+                realise(cands[c]);
+                if (sep.size() < best_sz) { best_sz = sep.size(); best = c; }
+                for (int64_t p : nodes) side[p] = 0;
+            }
+        }
+        realise(cands[best]);
+        const int ax = cands[best].d;
         std::vector<int64_t> L, R, Sp;
         for (int64_t p : nodes) {
             if (side[p] == 1) L.push_back(p);
@@ -173,6 +271,12 @@ struct Builder {
             else { xy[2 * p] = d.points[3 * (int64_t)p]; xy[2 * p + 1] = d.points[3 * (int64_t)p + 1]; }
         }
         side.assign(std::max(P, 1), 0);
+        stamp.assign(std::max(P, 1), 0);
+        spos.assign(std::max(P, 1), -1);
+        if (const char *e = std::getenv("DEFTRI_ND_TRY")) nd_try = std::atoi(e);
+        if (const char *e = std::getenv("DEFTRI_ND_PASSES")) nd_passes = std::atoi(e);
+        if (const char *e = std::getenv("DEFTRI_ND_BAL")) nd_bal = std::atof(e);
+        if (const char *e = std::getenv("DEFTRI_ND_DIRS")) nd_dirs = std::min(16, std::max(1, std::atoi(e)));
         std::vector<int32_t> rootch;
         if (P > 0) {
             std::vector<int64_t> nodes(P);
