@@ -194,8 +194,8 @@ typedef struct deftri_kernel_stat {
 int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *stats,
                          int32_t max_stats, int32_t *n_stats);
 
-/* sizeof() of the ABI structs (deftri_problem_desc, deftri_lm_params, deftri_report,
-   deftri_keyframe, deftri_map) for binding checks. */
+/* sizeof() of the ABI structs for binding checks: 0 deftri_problem_desc, 1 deftri_lm_params,
+   2 deftri_report, 3 deftri_keyframe, 4 deftri_map, 5 deftri_ba_desc. */
 int64_t deftri_sizeof(int32_t which);
 
 /* ---- map-level API (Modules/Optimization/g2oBundleAdjustment.h:56-60) ---------------- */
@@ -239,6 +239,89 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,
                             double arap_weight, float depth_error,
                             const deftri_problem_desc **desc_out);
+
+/* ==== bundle adjustment ============================================
+ * The BlockSolver_6_3 Schur LM of the reference's BA entry points:
+ *   bundleAdjustment(Map*)             g2oBundleAdjustment.cc:38-138   (optimize(20), KF 0 fixed)
+ *   localBundleAdjustment(Map*, ID)    g2oBundleAdjustment.cc:245-444  (optimize(5), outlier
+ *                                      levels, robust kernels off, optimize(10))
+ *   poseOnlyOptimization(Frame&)       g2oBundleAdjustment.cc:140-243  (4 rounds x optimize(10))
+ * Vertices: poses g2o::VertexSE3Expmap (6 dof, T <- exp(d) * T), points VertexSBAPointXYZ
+ * (3 dof, marginalized).  Edges: EdgeSE3ProjectXYZ (g2oTypes.h:150-189, linearizeOplus
+ * g2oTypes.cc:121-142) with info = invSigma2(octave) * I2 and optional Huber; with every point
+ * fixed the edges are EdgeSE3ProjectXYZOnlyPose (g2oTypes.h:191-229, g2oTypes.cc:173-189).
+ * On the device: per-edge residual/Jacobian, per-point 3x3 blocks, per-pose 6x6 blocks, the
+ * Schur complement S = Hpp - sum_l Hpl Hll^-1 Hlp (dense, 6 x free poses), a dense LDL^T of S,
+ * point back-substitution.  Points may be sharded over ranks (one rank per GPU): each rank
+ * uploads every pose but only its points and their edges; the pose blocks and S are summed
+ * across ranks (RCCL all-reduce, or a caller-provided all-reduce) once per LM trial. */
+typedef struct deftri_ba_ctx deftri_ba_ctx;
+
+typedef struct deftri_ba_desc {
+    int32_t n_poses;             /* K  VertexSE3Expmap                                      */
+    int32_t n_points;            /* P  VertexSBAPointXYZ (marginalized)                      */
+    int32_t n_edges;             /* E  EdgeSE3ProjectXYZ                                     */
+    int32_t reserved;
+    const double  *poses;        /* [K*7] T_cw: qx qy qz qw tx ty tz                         */
+    const uint8_t *pose_fixed;   /* [K] 1 = setFixed(true); NULL = none                      */
+    const float   *pose_kb8;     /* [K*8] KannalaBrandt8 fx fy cx cy k0..k3 of each pose's KF */
+    const double  *points;       /* [P*3] world positions                                   */
+    const uint8_t *point_fixed;  /* [P] 1 = constant (poseOnly's Xworld); NULL = none        */
+    const int32_t *edge_point;   /* [E] */
+    const int32_t *edge_pose;    /* [E] */
+    const double  *edge_obs;     /* [E*2] keypoint (u, v)                                   */
+    const double  *edge_info;    /* [E]   information = edge_info * I2                      */
+    const uint8_t *edge_level;   /* [E] g2o edge level; NULL = all 0                        */
+    const uint8_t *edge_robust;  /* [E] 1 = RobustKernelHuber(huber_delta); NULL = all 1     */
+    double huber_delta;          /* reference: (float)sqrt(5.99)                            */
+} deftri_ba_desc;
+
+/* Caller-supplied all-reduce over ranks (tests, non-RCCL transports): n doubles in HOST memory,
+   reduced in place; op 0 = sum, 1 = max.  The library stages the device buffer through host
+   memory around the call (the RCCL path reduces device-resident buffers directly).  Returns 0
+   on success. */
+typedef int (*deftri_allreduce_fn)(void *user, double *host_buf, int64_t n, int32_t op);
+
+int deftri_ba_create(int32_t device, deftri_ba_ctx **out);
+int deftri_ba_destroy(deftri_ba_ctx *ctx);
+const char *deftri_ba_last_error(const deftri_ba_ctx *ctx);
+/* Copy the graph to HBM (edges are kept in point order internally; per-edge in/out arrays of
+   this API always use the caller's edge order). */
+int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *desc);
+/* vertex->setEstimate(): replace poses [K*7] and/or points [P*3] (NULL = unchanged). */
+int deftri_ba_set_state(deftri_ba_ctx *ctx, const double *poses, const double *points);
+/* e->setLevel() / e->setRobustKernel(0 or Huber) for every edge (NULL = unchanged). */
+int deftri_ba_set_edge_flags(deftri_ba_ctx *ctx, const uint8_t *level, const uint8_t *robust);
+/* optimizer.initializeOptimization(level); optimizer.optimize(params->n_iterations).  Active
+   edges = level `level` with a non-fixed vertex; active vertices = those with an active edge. */
+int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *params, int32_t level,
+                       deftri_report *report);
+/* e->computeError() on every edge (active or not) whose mask entry is non-zero (caller edge
+   order; NULL = every edge). */
+int deftri_ba_compute_errors(deftri_ba_ctx *ctx, const uint8_t *mask);
+/* Per edge (caller order): e->chi2() of the cached error (no robust kernel) and
+   e->isDepthPositive() at the current state.  Either output may be NULL. */
+int deftri_ba_edge_chi2(deftri_ba_ctx *ctx, double *chi2, uint8_t *depth_positive);
+/* Current estimates: poses [K*7], points [P*3] (either may be NULL). */
+int deftri_ba_download(deftri_ba_ctx *ctx, double *poses, double *points);
+/* Diagnostics (parity tests): initializeOptimization(level), linearize at the current state and
+   form the damped Schur system at `lambda`.  Outputs (any may be NULL): chi2 (activeRobustChi2,
+   summed over ranks), S [ns*ns] (row-major, full) and rhs [ns] of the reduced pose system, dx
+   [6K + 3P] (poses in pose order, 0 for fixed/inactive; then points), b [6K + 3P] (g2o sign).
+   *ns receives 6 x (number of free active poses). */
+int deftri_ba_eval_system(deftri_ba_ctx *ctx, int32_t level, double lambda, double *chi2, double *S,
+                          double *rhs, double *dx, double *b, int32_t *ns);
+/* Point-sharded multi-GPU: this context is rank `rank` of `nranks`.  Either RCCL (the
+   production path: ncclCommInitRank over xGMI, all-reduce on the solver stream; the 128-byte id
+   comes from deftri_rccl_unique_id on rank 0, shared by the caller) or a caller-supplied
+   all-reduce (tests: e.g. gloo through host memory).  nranks == 1 clears the setting. */
+int deftri_rccl_unique_id(uint8_t id[128]);
+int deftri_ba_dist_init_rccl(deftri_ba_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int deftri_ba_dist_set_allreduce(deftri_ba_ctx *ctx, int32_t nranks, int32_t rank, deftri_allreduce_fn fn,
+                                 void *user);
+/* Per-kernel device timing of one LM trial of the BA path (HIP events on the solver stream). */
+int deftri_ba_profile_trial(deftri_ba_ctx *ctx, double lambda, deftri_kernel_stat *stats, int32_t max_stats,
+                            int32_t *n_stats);
 
 #ifdef __cplusplus
 }

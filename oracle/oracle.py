@@ -91,3 +91,59 @@ def solve_lm(prob, n_iterations=10, analytic=False, tau=1e-5, max_trials=10, ver
     lib().oracle_solve_lm(C.byref(d), C.byref(prm), _p(pts, C.c_double), _p(sc, C.c_double),
                           _p(tg, C.c_double), C.byref(rep))
     return {"points": pts, "scales": sc, "tg": tg, "report": rep.as_dict()}
+
+
+# ---- bundle adjustment (ba_oracle.c) ------------------------------------------------------
+def _u8(a):
+    return None if a is None else np.ascontiguousarray(a, np.uint8).ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def ba_solve(prob, n_iterations=10, level=0, edge_level=None, edge_robust=None, poses=None, points=None, err=None,
+             tau=1e-5, max_trials=10, verbose=False):
+    """initializeOptimization(level); optimize(n) on a BAProblem; state and cached errors in/out."""
+    A = _abi()
+    d = prob.to_desc()
+    prm = A.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=0.0,
+                     analytic_jacobians=1, verbose=1 if verbose else 0)
+    rep = A.Report()
+    ps = np.array(prob.poses if poses is None else poses, np.float64, copy=True)
+    pt = np.array(prob.points if points is None else points, np.float64, copy=True)
+    er = np.zeros((prob.n_edges, 2)) if err is None else np.array(err, np.float64, copy=True)
+    lv = prob.edge_level if edge_level is None else edge_level
+    rb = prob.edge_robust if edge_robust is None else edge_robust
+    lib().oracle_ba_solve(C.byref(d), _u8(lv), _u8(rb), C.c_int32(level), C.byref(prm), _p(ps, C.c_double),
+                          _p(pt, C.c_double), _p(er, C.c_double), C.byref(rep))
+    return {"poses": ps, "points": pt, "err": er, "report": rep.as_dict()}
+
+
+def ba_compute_errors(prob, poses, points):
+    d = prob.to_desc()
+    er = np.zeros((prob.n_edges, 2))
+    ps = np.ascontiguousarray(poses, np.float64); pt = np.ascontiguousarray(points, np.float64)
+    lib().oracle_ba_compute_errors(C.byref(d), _p(ps, C.c_double), _p(pt, C.c_double), _p(er, C.c_double))
+    return er
+
+
+def ba_edge_chi2(prob, poses, points, err):
+    d = prob.to_desc()
+    chi = np.zeros(prob.n_edges); dp = np.zeros(prob.n_edges, np.uint8)
+    ps = np.ascontiguousarray(poses, np.float64); pt = np.ascontiguousarray(points, np.float64)
+    er = np.ascontiguousarray(err, np.float64)
+    lib().oracle_ba_edge_chi2(C.byref(d), _p(ps, C.c_double), _p(pt, C.c_double), _p(er, C.c_double),
+                              _p(chi, C.c_double), dp.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return chi, dp.astype(bool)
+
+
+def ba_eval_system(prob, lam, level=0, edge_level=None, edge_robust=None):
+    d = prob.to_desc()
+    K, P = prob.n_poses, prob.n_points
+    S = np.zeros((6 * K, 6 * K)); rhs = np.zeros(6 * K); dx = np.zeros(6 * K + 3 * P); b = np.zeros(6 * K + 3 * P)
+    chi = C.c_double(); ns = C.c_int32()
+    lv = prob.edge_level if edge_level is None else edge_level
+    rb = prob.edge_robust if edge_robust is None else edge_robust
+    rc = lib().oracle_ba_eval_system(C.byref(d), _u8(lv), _u8(rb), C.c_int32(level), _p(prob.poses, C.c_double),
+                                     _p(prob.points, C.c_double), C.c_double(lam), C.byref(chi), _p(S, C.c_double),
+                                     _p(rhs, C.c_double), _p(dx, C.c_double), _p(b, C.c_double), C.byref(ns))
+    n = ns.value
+    return {"chi2": chi.value, "S": S.reshape(-1)[:n * n].reshape(n, n).copy(), "rhs": rhs[:n].copy(), "dx": dx,
+            "b": b, "ns": n, "ok": rc == 0}

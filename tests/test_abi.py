@@ -34,6 +34,21 @@ def test_abi_version_and_struct_sizes():
     assert lib.deftri_sizeof(2) == C.sizeof(_abi.Report)
     assert lib.deftri_sizeof(3) == C.sizeof(_abi.KeyFrameC)
     assert lib.deftri_sizeof(4) == C.sizeof(_abi.MapC)
+    assert lib.deftri_sizeof(5) == C.sizeof(_abi.BADesc)
+
+
+def test_ba_context_needs_a_device():
+    with pytest.raises(capi.DeftriError) as e:
+        capi.BAContext(0) if not _has_gpu() else (_ for _ in ()).throw(capi.DeftriError(_abi.DEFTRI_E_NODEVICE, "skip"))
+    assert e.value.code == _abi.DEFTRI_E_NODEVICE
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:      # noqa: BLE001
+        return False
 
 
 def test_host_only_context_rejects_device_work(golden_cases):

@@ -1,0 +1,244 @@
+"""GPU parity of the bundle-adjustment path (deftri_ba_*, ba.hip) against the oracle
+(oracle/ba_oracle.c).  Both sides project in fp32 as the reference does (KannalaBrandt8, fp32
+atan2f / sinf / cosf): the device's ocml and the host's glibc differ by an ulp on some edges, a
+~3e-5 px change of one residual, so the fp64 quantities agree to fp32-projection level, not to
+fp64 level.  Tolerances:
+  * chi2                            rel 1e-6
+  * b, damped Schur system S, rhs   rel 1e-6
+  * step dx (dense LDL^T of S)      rel 1e-5
+  * LM trajectory (gauge fixed)      chi2 per iteration rel 1e-6 and identical trial counts until chi2
+                                    stalls at the fp32 noise floor; final chi2 rel 1e-6, poses / points
+                                    within 1e-5 (1e-7..1e-6 observed)
+  * gauge-free BA (only KF 0 fixed) chi2 rel 1e-4, inlier RMSE within 5e-3 px (scale-gauge drift)
+  * map-level flows (bundle, local, pose-only): identical outlier decisions, slot edits and
+                                    observation tables; pose-only pose within 1e-5 after the fp32
+                                    write-back; bundle / local (scale gauge free) chi2 rel 1e-4
+  * point-sharded, 2 ranks (gloo transport on one GPU): chi2 trajectory rel 1e-10 vs one rank
+  * bench size (C3 shape, 50k points x 8 KFs): monotone chi2, S dx = rhs backward error
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+from ba_oracle_ctx import OracleBA
+from deftri import ba, capi
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bactx():
+    c = capi.BAContext(0)
+    yield c
+    c.close()
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300)
+
+
+def _problems():
+    p1 = ba.make_ba_problem(n=200, k=4, seed=1, outliers=0.05)
+    p2 = ba.make_ba_problem(n=300, k=6, seed=2, visibility=0.7, outliers=0.02)
+    # levels, robust flags, a fixed point, a duplicated (point, pose) observation
+    p3 = ba.make_ba_problem(n=150, k=3, seed=3, outliers=0.05)
+    rng = np.random.default_rng(0)
+    p3.edge_level[rng.random(p3.n_edges) < 0.1] = 1
+    p3.edge_robust[rng.random(p3.n_edges) < 0.3] = 0
+    p3.point_fixed = np.zeros(p3.n_points, np.uint8); p3.point_fixed[5] = 1
+    dup = 7
+    p3 = ba.BAProblem(p3.poses, p3.pose_kb8, p3.points, np.append(p3.edge_point, p3.edge_point[dup]),
+                      np.append(p3.edge_pose, p3.edge_pose[dup]), np.vstack([p3.edge_obs, p3.edge_obs[dup] + 0.5]),
+                      np.append(p3.edge_info, 2.0), pose_fixed=p3.pose_fixed, point_fixed=p3.point_fixed,
+                      edge_level=np.append(p3.edge_level, 0), edge_robust=np.append(p3.edge_robust, 1))
+    # pose only: every point fixed
+    p4 = ba.make_ba_problem(n=120, k=2, seed=4, outliers=0.05)
+    m = p4.edge_pose == 1
+    p4 = ba.BAProblem(p4.poses[1:2], p4.pose_kb8[1:2], p4.points, p4.edge_point[m], np.zeros(int(m.sum()), np.int32),
+                      p4.edge_obs[m], p4.edge_info[m], point_fixed=np.ones(p4.n_points, np.uint8))
+    return {"dense": p1, "partial_visibility": p2, "flags": p3, "pose_only": p4}
+
+
+@pytest.mark.parametrize("name", ["dense", "partial_visibility", "flags", "pose_only"])
+def test_schur_system_matches_oracle(bactx, name):
+    p = _problems()[name]
+    bactx.upload(p)
+    # monocular BA keeps a scale gauge after fixing KF 0, so S is near-singular without damping:
+    # compare at LM-like damping (g2o's initial lambda is 1e-5 max diag H)
+    dmax = np.abs(np.diag(oracle.ba_eval_system(p, 1.0)["S"])).max()     # (lambda 0: singular Hll of 1-edge points)
+    for lam_rel in (1e-5, 1e-2):
+        lam = lam_rel * dmax
+        g = bactx.eval_system(lam)
+        o = oracle.ba_eval_system(p, lam)
+        assert g["ns"] == o["ns"]
+        d = {"chi2": abs(g["chi2"] - o["chi2"]) / o["chi2"], "b": rel(g["b"], o["b"]), "S": rel(g["S"], o["S"]),
+             "rhs": rel(g["rhs"], o["rhs"]), "dx": rel(g["dx"], o["dx"])}
+        print(name, lam_rel, d)
+        assert d["chi2"] < 1e-6, d
+        assert d["b"] < 1e-6 and d["S"] < 1e-6 and d["rhs"] < 1e-6, d
+        assert d["dx"] < 1e-5, d
+        # the device's own solve: backward error of S xp = rhs
+        ns = g["ns"]
+        if ns:
+            xp = np.concatenate([g["dx"][6 * k:6 * k + 6] for k in range(p.n_poses) if not p.pose_fixed[k]])
+            assert np.linalg.norm(g["S"] @ xp - g["rhs"]) / (np.linalg.norm(g["S"], 2) * np.linalg.norm(xp)) < 1e-14
+
+
+def _gauge_fixed(p):
+    """Fix KF 1 as well as KF 0: monocular BA with one fixed pose keeps a free scale, along which
+    LM drifts by amounts set by last-bit differences (any two correct solvers disagree there)."""
+    if p.n_poses > 1:
+        p.pose_fixed = p.pose_fixed.copy()
+        p.pose_fixed[:2] = 1
+    return p
+
+
+@pytest.mark.parametrize("name", ["dense", "partial_visibility", "flags", "pose_only"])
+def test_lm_matches_oracle(bactx, name):
+    p = _gauge_fixed(_problems()[name])
+    bactx.upload(p)
+    r = bactx.solve_lm(15)
+    poses, pts = bactx.download()
+    o = oracle.ba_solve(p, 15)
+    ro = o["report"]
+    print(name, "chi2", r["chi2_iter"][-1], ro["chi2_iter"][-1], "pose", np.abs(poses - o["poses"]).max(),
+          "pts", np.abs(pts - o["points"]).max(), r["trials_iter"], ro["trials_iter"])
+    # once chi2 stalls near the fp32-projection noise floor (relative decrease < 1e-6) the rho test
+    # compares noise: trial counts after that point are not a parity property
+    c = [ro["chi2_initial"]] + ro["chi2_iter"]
+    n_cmp = next((i for i in range(1, len(c)) if c[i - 1] - c[i] < 1e-6 * c[i]), len(c) - 1)
+    assert r["trials_iter"][:n_cmp] == ro["trials_iter"][:n_cmp]
+    assert r["chi2_initial"] == pytest.approx(ro["chi2_initial"], rel=1e-6)
+    np.testing.assert_allclose(r["chi2_iter"][:n_cmp], ro["chi2_iter"][:n_cmp], rtol=1e-6)
+    assert r["chi2_final"] == pytest.approx(ro["chi2_final"], rel=1e-6)
+    assert np.abs(poses - o["poses"]).max() < 1e-5
+    assert np.abs(pts - o["points"]).max() < 1e-5
+    # cached errors hold the last trial's state (possibly a rejected one, which differs between
+    # the two once trials are noise-driven): compare e->computeError() at the final state
+    bactx.compute_errors()
+    chi, dpos = bactx.edge_chi2()
+    chi_o, dpos_o = oracle.ba_edge_chi2(p, o["poses"], o["points"],
+                                        oracle.ba_compute_errors(p, o["poses"], o["points"]))
+    # per edge: fp32 uv quantum ~3e-5 px plus the final-state difference (1e-6 -> ~2e-4 px on a 30 px outlier)
+    np.testing.assert_allclose(chi, chi_o, rtol=1e-4, atol=5e-2)
+    assert np.array_equal(dpos, dpos_o)
+
+
+def _rmse(chi, info):
+    return float(np.sqrt(np.mean(chi / info / 2.0)))
+
+
+def test_lm_gauge_free_matches_oracle_in_rmse(bactx):
+    """Only KF 0 fixed (the reference's bundleAdjustment gauge): monocular BA keeps the scale free,
+    and LM slides along that flat valley by amounts set by last-bit differences (observed: chi2
+    4651.73 vs 4651.93 after 15 iterations, poses 7e-3 apart).  Gauge-invariant comparison: chi2
+    rel 1e-4 and inlier reprojection RMSE within 5e-3 px (observed 1.8e-3).  The gauge-fixed
+    problems above meet the 1e-6 trajectory bar."""
+    p = _problems()["dense"]
+    bactx.upload(p)
+    r = bactx.solve_lm(15)
+    o = oracle.ba_solve(p, 15)
+    bactx.compute_errors()
+    chi, _ = bactx.edge_chi2()
+    chi_o, _ = oracle.ba_edge_chi2(p, o["poses"], o["points"], oracle.ba_compute_errors(p, o["poses"], o["points"]))
+    inl = chi_o < 5.991
+    d = abs(_rmse(chi[inl], p.edge_info[inl]) - _rmse(chi_o[inl], p.edge_info[inl]))
+    print("gauge-free: chi2", r["chi2_final"], o["report"]["chi2_final"], "inlier RMSE delta px", d)
+    assert r["chi2_final"] == pytest.approx(o["report"]["chi2_final"], rel=1e-4)
+    assert d < 5e-3
+
+
+@pytest.mark.parametrize("flow", ["bundle", "local", "pose_only"])
+def test_map_flows_match_oracle(bactx, flow):
+    m_gpu, _ = ba.simulate_ba_map(n=200, k=5, seed=6, outliers=0.05, visibility=0.85, min_common_obs=15)
+    m_ora = copy.deepcopy(m_gpu)
+    out = []
+    for m, ctx in ((m_gpu, bactx), (m_ora, OracleBA())):
+        if flow == "bundle":
+            out.append(ba.bundleAdjustment(m, ctx=ctx))
+        elif flow == "local":
+            out.append(ba.localBundleAdjustment(m, 3, ctx=ctx))
+        else:
+            out.append(ba.poseOnlyOptimization(m.keyframes[4], ctx=ctx))
+    if flow == "pose_only":
+        assert out[0] == out[1]
+    elif flow == "local":
+        assert out[0]["outliers_removed"] == out[1]["outliers_removed"]
+        assert out[0]["second"]["chi2_final"] == pytest.approx(out[1]["second"]["chi2_final"], rel=1e-4)
+    else:
+        assert out[0]["chi2_final"] == pytest.approx(out[1]["chi2_final"], rel=1e-4)
+    for kid in m_gpu.keyframes:
+        a, b = m_gpu.keyframes[kid], m_ora.keyframes[kid]
+        assert [mp is None for mp in a.map_points] == [mp is None for mp in b.map_points]
+        if flow == "pose_only":          # no gauge freedom: one pose, fixed points
+            assert np.abs(a.pose.R - b.pose.R).max() < 1e-5 and np.abs(a.pose.t - b.pose.t).max() < 1e-5
+    assert m_gpu.kf_obs == m_ora.kf_obs
+
+
+def _dist_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = ba.make_ba_problem(n=2000, k=6, seed=8, outliers=0.02)
+    sub, (lo, hi), _ = p.shard(rank, world)
+    ctx = capi.BAContext(0)
+
+    def allreduce(buf, op):
+        t = torch.from_numpy(buf)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
+
+    ctx.dist_set_allreduce(world, rank, allreduce)
+    ctx.upload(sub)
+    r = ctx.solve_lm(10)
+    poses, pts = ctx.download()
+    q.put((rank, r["chi2_iter"], r["trials_total"], poses, pts, lo, hi))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_point_sharded_two_ranks_match_single(bactx):
+    import torch.multiprocessing as mp
+    p = ba.make_ba_problem(n=2000, k=6, seed=8, outliers=0.02)
+    bactx.upload(p)
+    r1 = bactx.solve_lm(10)
+    poses1, pts1 = bactx.download()
+    world = 2
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctxm.Process(target=_dist_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, chi_iter, trials, poses, pts, lo, hi in out:
+        assert trials == r1["trials_total"]
+        np.testing.assert_allclose(chi_iter, r1["chi2_iter"], rtol=1e-10)
+        assert np.abs(poses - poses1).max() < 1e-9
+        assert np.abs(pts - pts1[lo:hi]).max() < 1e-9
+    # every rank holds the same poses (replicated reduced solve)
+    assert np.array_equal(out[0][3], out[1][3])
+
+
+def test_bench_size_properties(bactx):
+    p = ba.make_ba_problem(n=50000, k=8, seed=1, outliers=0.01)
+    bactx.upload(p)
+    g = bactx.eval_system(1e-2)
+    S, rhs = g["S"], g["rhs"]
+    xp = np.concatenate([g["dx"][6 * k:6 * k + 6] for k in range(1, 8)])
+    assert np.linalg.norm(S @ xp - rhs) / (np.linalg.norm(S, 2) * np.linalg.norm(xp)) < 1e-13
+    r = bactx.solve_lm(10)
+    c = [r["chi2_initial"]] + r["chi2_iter"]
+    assert all(b <= a for a, b in zip(c, c[1:]))
+    poses_a, pts_a = bactx.download()
+    bactx.upload(p)
+    r2 = bactx.solve_lm(10)
+    poses_b, pts_b = bactx.download()
+    assert r2["chi2_iter"] == r["chi2_iter"]                 # deterministic (no atomics)
+    assert np.array_equal(poses_a, poses_b) and np.array_equal(pts_a, pts_b)

@@ -138,7 +138,10 @@ __device__ __forceinline__ SE3 se3_mul(const SE3 &A, const SE3 &B) {
 }
 
 // ---- Kannala–Brandt 8, fp32 ---------------------------------------------------------------
+// fp32 without FMA contraction, like the reference's x86-64 build (no -march): only the ocml vs
+// glibc transcendental (atan2f, sinf, cosf) ulp differences remain against the oracle.
 __device__ __forceinline__ void kb8_project(const float *k, const float p[3], float uv[2]) {
+#pragma clang fp contract(off)
     const float x2_plus_y2 = p[0] * p[0] + p[1] * p[1];
     const float theta = atan2f(sqrtf(x2_plus_y2), p[2]);
     const float psi = atan2f(p[1], p[0]);
@@ -153,6 +156,7 @@ __device__ __forceinline__ void kb8_project(const float *k, const float p[3], fl
 }
 
 __device__ __forceinline__ void kb8_project_jac(const float *k, const float p[3], float J[6]) {
+#pragma clang fp contract(off)
     float x2 = p[0] * p[0], y2 = p[1] * p[1], z2 = p[2] * p[2];
     float r2 = x2 + y2;
     float r = sqrtf(r2);

@@ -519,6 +519,7 @@ int64_t deftri_sizeof(int32_t which) {
         case 2: return (int64_t)sizeof(deftri_report);
         case 3: return (int64_t)sizeof(deftri_keyframe);
         case 4: return (int64_t)sizeof(deftri_map);
+        case 5: return (int64_t)sizeof(deftri_ba_desc);
         default: return -1;
     }
 }

@@ -84,6 +84,21 @@ class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", i64), ("ms", f64), ("flops", f64), ("bytes", f64)]
 
 
+class BADesc(C.Structure):
+    _fields_ = [
+        ("n_poses", i32), ("n_points", i32), ("n_edges", i32), ("reserved", i32),
+        ("poses", P(f64)), ("pose_fixed", P(C.c_uint8)), ("pose_kb8", P(f32)),
+        ("points", P(f64)), ("point_fixed", P(C.c_uint8)),
+        ("edge_point", P(i32)), ("edge_pose", P(i32)), ("edge_obs", P(f64)), ("edge_info", P(f64)),
+        ("edge_level", P(C.c_uint8)), ("edge_robust", P(C.c_uint8)),
+        ("huber_delta", f64),
+    ]
+
+
+# int (*)(void *user, double *host_buf, int64_t n, int32_t op)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, P(f64), i64, i32)
+
+
 def ptr(a, ctype):
     """Pointer into a contiguous numpy array (None for None)."""
     if a is None:

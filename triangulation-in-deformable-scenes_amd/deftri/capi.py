@@ -57,6 +57,25 @@ def load():
         "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
                                                C.c_double, C.c_double, C.c_float, C.c_int32, P(C.c_double),
                                                P(_abi.Report)]),
+        # bundle adjustment
+        "deftri_ba_create": (C.c_int, [C.c_int32, P(C.c_void_p)]),
+        "deftri_ba_destroy": (C.c_int, [C.c_void_p]),
+        "deftri_ba_last_error": (C.c_char_p, [C.c_void_p]),
+        "deftri_ba_upload": (C.c_int, [C.c_void_p, P(_abi.BADesc)]),
+        "deftri_ba_set_state": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double)]),
+        "deftri_ba_set_edge_flags": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_uint8)]),
+        "deftri_ba_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), C.c_int32, P(_abi.Report)]),
+        "deftri_ba_compute_errors": (C.c_int, [C.c_void_p, P(C.c_uint8)]),
+        "deftri_ba_edge_chi2": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_uint8)]),
+        "deftri_ba_download": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double)]),
+        "deftri_ba_eval_system": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, P(C.c_double), P(C.c_double),
+                                            P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_int32)]),
+        "deftri_rccl_unique_id": (C.c_int, [P(C.c_uint8)]),
+        "deftri_ba_dist_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint8)]),
+        "deftri_ba_dist_set_allreduce": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _abi.ALLREDUCE_FN,
+                                                   C.c_void_p]),
+        "deftri_ba_profile_trial": (C.c_int, [C.c_void_p, C.c_double, P(_abi.KernelStat), C.c_int32,
+                                              P(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -73,6 +92,10 @@ EXPORTED = [
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
     "deftri_profile_trial",
+    "deftri_ba_create", "deftri_ba_destroy", "deftri_ba_last_error", "deftri_ba_upload", "deftri_ba_set_state",
+    "deftri_ba_set_edge_flags", "deftri_ba_solve_lm", "deftri_ba_compute_errors", "deftri_ba_edge_chi2",
+    "deftri_ba_download", "deftri_ba_eval_system", "deftri_rccl_unique_id", "deftri_ba_dist_init_rccl",
+    "deftri_ba_dist_set_allreduce", "deftri_ba_profile_trial",
 ]
 
 
@@ -200,3 +223,120 @@ class Context:
             C.byref(rep)))
         m.from_c(mc, keep)
         return upd.value, rep.as_dict()
+
+
+class BAContext:
+    """Bundle-adjustment solver context on one GPU (deftri_ba_*).  `prob` is a ba.BAProblem."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = C.c_void_p()
+        rc = self.lib.deftri_ba_create(int(device), C.byref(h))
+        if rc != 0:
+            raise DeftriError(rc, "deftri_ba_create failed (no usable gfx950 device?)")
+        self.h = h
+        self.device = device
+        self._prob = None
+        self._desc = None
+        self._cb = None
+
+    def close(self):
+        if self.h:
+            self.lib.deftri_ba_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise DeftriError(rc, (self.lib.deftri_ba_last_error(self.h) or b"").decode())
+
+    def upload(self, prob):
+        self._prob = prob
+        self._desc = prob.to_desc()
+        self._check(self.lib.deftri_ba_upload(self.h, C.byref(self._desc)))
+
+    def set_state(self, poses=None, points=None):
+        p = None if poses is None else np.ascontiguousarray(poses, np.float64)
+        q = None if points is None else np.ascontiguousarray(points, np.float64)
+        self._check(self.lib.deftri_ba_set_state(self.h, None if p is None else _dp(p), None if q is None else _dp(q)))
+
+    def set_edge_flags(self, level=None, robust=None):
+        lv = None if level is None else np.ascontiguousarray(level, np.uint8)
+        rb = None if robust is None else np.ascontiguousarray(robust, np.uint8)
+        self._check(self.lib.deftri_ba_set_edge_flags(self.h, _abi.ptr(lv, C.c_uint8), _abi.ptr(rb, C.c_uint8)))
+
+    def solve_lm(self, n_iterations=10, level=0, tau=1e-5, max_trials=10, user_lambda=0.0, verbose=False):
+        prm = _abi.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=user_lambda,
+                            analytic_jacobians=1, verbose=1 if verbose else 0)
+        rep = _abi.Report()
+        self._check(self.lib.deftri_ba_solve_lm(self.h, C.byref(prm), int(level), C.byref(rep)))
+        return rep.as_dict()
+
+    def compute_errors(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        self._check(self.lib.deftri_ba_compute_errors(self.h, _abi.ptr(m, C.c_uint8)))
+
+    def edge_chi2(self):
+        n = self._prob.n_edges
+        chi = np.zeros(n); dp = np.zeros(n, np.uint8)
+        self._check(self.lib.deftri_ba_edge_chi2(self.h, _dp(chi), _abi.ptr(dp, C.c_uint8)))
+        return chi, dp.astype(bool)
+
+    def download(self):
+        p = self._prob
+        poses = np.zeros((p.n_poses, 7)); pts = np.zeros((p.n_points, 3))
+        self._check(self.lib.deftri_ba_download(self.h, _dp(poses), _dp(pts)))
+        return poses, pts
+
+    def eval_system(self, lam, level=0):
+        p = self._prob
+        K, P = p.n_poses, p.n_points
+        ns_max = 6 * K
+        S = np.zeros((ns_max, ns_max)); rhs = np.zeros(ns_max)
+        dx = np.zeros(6 * K + 3 * P); b = np.zeros(6 * K + 3 * P)
+        chi = C.c_double(); ns = C.c_int32()
+        self._check(self.lib.deftri_ba_eval_system(self.h, int(level), float(lam), C.byref(chi), _dp(S), _dp(rhs),
+                                                   _dp(dx), _dp(b), C.byref(ns)))
+        n = ns.value
+        S = S.reshape(-1)[:n * n].reshape(n, n).copy()
+        return {"chi2": chi.value, "S": S, "rhs": rhs[:n].copy(), "dx": dx, "b": b, "ns": n}
+
+    def dist_init_rccl(self, nranks, rank, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._check(self.lib.deftri_ba_dist_init_rccl(self.h, int(nranks), int(rank), buf))
+
+    def dist_set_allreduce(self, nranks, rank, fn):
+        """fn(np.ndarray view of the host buffer, op) -> None, reducing in place (op 0 sum, 1 max)."""
+        def _cb(user, buf, n, op):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(n,)), int(op))
+                return 0
+            except Exception:                       # noqa: BLE001 — reported as a failed call
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._cb = _abi.ALLREDUCE_FN(_cb)
+        self._check(self.lib.deftri_ba_dist_set_allreduce(self.h, int(nranks), int(rank), self._cb, None))
+
+    def profile_trial(self, lam):
+        arr = (_abi.KernelStat * 64)()
+        n = C.c_int32()
+        self._check(self.lib.deftri_ba_profile_trial(self.h, float(lam), arr, 64, C.byref(n)))
+        return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].ms, "flops": arr[i].flops,
+                                       "bytes": arr[i].bytes} for i in range(n.value)}
+
+
+def rccl_unique_id():
+    lib = load()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.deftri_rccl_unique_id(buf)
+    if rc != 0:
+        raise DeftriError(rc, "ncclGetUniqueId failed")
+    return bytes(buf)

@@ -117,10 +117,13 @@ class KeyFrame:
 
 
 class Map:
-    def __init__(self):
+    def __init__(self, min_common_obs=15):
         self.keyframes = {}           # insertion-ordered
         self.map_points = {}
-        self.kf_obs = {}              # kf id -> {mp id -> idx}
+        self.kf_obs = {}              # kf id -> {mp id -> idx}        (Map::mKeyFrameObs_)
+        self.mp_obs = {}              # mp id -> {kf id -> idx}        (Map::mMapPointObs_)
+        self.covis = {}               # kf id -> {kf id -> count}      (Map::mCovisibilityGraph_)
+        self.min_common_obs = min_common_obs   # Map.minObs (Simulation.yaml:42)
         self.global_T = {}            # (kf1, kf2) -> SE3f
 
     def insert_keyframe(self, kf):
@@ -131,8 +134,40 @@ class Map:
         self.map_points[mp.id] = mp
 
     def add_observation(self, kf_id, mp_id, idx):
+        """Map::addObservation (Map.cc:100-132): observation tables + covisibility counts."""
         assert mp_id not in self.kf_obs[kf_id]
         self.kf_obs[kf_id][mp_id] = int(idx)
+        obs = self.mp_obs.setdefault(mp_id, {})
+        obs[kf_id] = int(idx)
+        for cov in obs:
+            if cov == kf_id:
+                continue
+            a = self.covis.setdefault(kf_id, {})
+            a[cov] = a.get(cov, 0) + 1
+            b = self.covis.setdefault(cov, {})
+            b[kf_id] = b.get(kf_id, 0) + 1
+
+    def remove_observation(self, kf_id, mp_id):
+        """Map::removeObservation (Map.cc:134-149)."""
+        del self.kf_obs[kf_id][mp_id]
+        del self.mp_obs[mp_id][kf_id]
+        for cov in self.mp_obs[mp_id]:
+            self.covis[kf_id][cov] -= 1
+            self.covis[cov][kf_id] -= 1
+
+    def get_local_map_of_keyframe(self, kf_id):
+        """Map::getLocalMapOfKeyFrame (Map.cc:178-209): (local map point ids, local KF ids, fixed KF
+        ids), each sorted ascending like the reference's std::set<ID>."""
+        local_kfs = {kf_id}
+        local_mps = set(self.kf_obs.get(kf_id, {}).keys())
+        for cov, n in self.covis.get(kf_id, {}).items():
+            if n > self.min_common_obs:
+                local_kfs.add(cov)
+                local_mps.update(self.kf_obs.get(cov, {}).keys())
+        all_kfs = set()
+        for mp in local_mps:
+            all_kfs.update(self.mp_obs.get(mp, {}).keys())
+        return sorted(local_mps), sorted(local_kfs), sorted(all_kfs - local_kfs)
 
     def is_map_point_in_keyframe(self, mp_id, kf_id):
         return self.kf_obs.get(kf_id, {}).get(mp_id, -1)

@@ -10,7 +10,8 @@ over the C-ABI.  Same names, argument meaning and write-back behaviour:
       ("g2oArap" selection).  The NLopt / Eigen weight tuning of "twoOptimizations" is the next
       component and raises NotImplementedError here.
   bundleAdjustment / localBundleAdjustment / poseOnlyOptimization
-      BA entry points without callers at the reference's HEAD — not yet built.
+      BA entry points (no callers at the reference's HEAD): the BlockSolver_6_3 Schur
+      LM on the device (deftri/ba.py over deftri_ba_*).
 """
 import threading
 
@@ -67,13 +68,19 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
     return rounds
 
 
-def bundleAdjustment(pMap):
-    raise NotImplementedError("bundleAdjustment (BlockSolver_6_3 Schur path) is not built yet")
+def bundleAdjustment(pMap, device=0, report=None):
+    """g2oBundleAdjustment.cc:38-138 on the device BA path (deftri/ba.py)."""
+    from . import ba
+    return ba.bundleAdjustment(pMap, device=device, report=report)
 
 
-def localBundleAdjustment(pMap, currKeyFrameId):
-    raise NotImplementedError("localBundleAdjustment is not built yet")
+def localBundleAdjustment(pMap, currKeyFrameId, device=0, report=None):
+    """g2oBundleAdjustment.cc:245-444 on the device BA path (deftri/ba.py)."""
+    from . import ba
+    return ba.localBundleAdjustment(pMap, currKeyFrameId, device=device, report=report)
 
 
-def poseOnlyOptimization(currFrame):
-    raise NotImplementedError("poseOnlyOptimization is not built yet")
+def poseOnlyOptimization(currFrame, device=0, report=None):
+    """g2oBundleAdjustment.cc:140-243 on the device BA path (deftri/ba.py); returns the inlier count."""
+    from . import ba
+    return ba.poseOnlyOptimization(currFrame, device=device, report=report)
