@@ -3,6 +3,7 @@ optimizer.optimize(nIterations), reference Modules/Optimization/g2oBundleAdjustm
 config C2 of BASELINE.json: 100k two-view correspondences, per GPU.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--corr 100000] [--no-cpu-baseline]
+  python bench.py --workload ba [--ba-points 500000] [--ba-kfs 8] [--ba-scaling strong|weak] ...
 
 A "step" is one accepted LM iteration of the device solver (linearize, assemble H, then up to 10
 damped trials of scatter + multifrontal LDL^T + solve + update + chi2 each).  The scene is
@@ -78,6 +79,97 @@ def cpu_baseline(n_full, full_flops, gpu_trials_per_iter, n_sample=10000):
                       f"{gpu_trials_per_iter:.2f} trials/iteration"}
 
 
+def ba_cpu_baseline(n_full_edges, trials_per_iter, n_sample=4000, k=8):
+    """The BA oracle (oracle/ba_oracle.c, 1 thread) on a 4k-point x 8-KF scene: 2 LM iterations
+    timed, scaled to the benchmark's edge count (every stage of the BA LM is linear in the edges;
+    the 42x42 Schur solve is negligible)."""
+    sys.path.insert(0, str(ROOT))
+    from deftri import ba
+    from oracle import oracle
+    p = ba.make_ba_problem(n=n_sample, k=k, seed=1, outliers=0.01)
+    t = time.perf_counter()
+    r = oracle.ba_solve(p, 2)["report"]
+    dt = time.perf_counter() - t
+    per_trial = dt / max(r["trials_total"], 1)
+    t_iter = per_trial * (n_full_edges / p.n_edges) * trials_per_iter
+    return {"value": 1.0 / t_iter, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"BA oracle LM, {r['iterations']} iterations ({r['trials_total']} trials) on {n_sample} points x "
+                      f"{k} KFs ({p.n_edges} edges): {dt:.2f} s measured; scaled by the edge ratio "
+                      f"{n_full_edges / p.n_edges:.1f}x at {trials_per_iter:.2f} trials/iteration"}
+
+
+def main_ba(args, world, rank, gpu, backend):
+    """Point-sharded bundle adjustment (SURVEY §8 a14 / e): the BlockSolver_6_3 Schur LM on every
+    rank's point shard, RCCL all-reduce of the pose blocks and the Schur complement per LM trial.
+    strong: the --ba-points scene split over the ranks; weak: --ba-points per rank."""
+    from deftri import ba
+    n_total = args.ba_points if args.ba_scaling == "strong" else args.ba_points * world
+    t0 = time.perf_counter()
+    full = ba.make_ba_problem(n=n_total, k=args.ba_kfs, seed=1, outliers=0.01)
+    prob, (lo, hi), _ = full.shard(rank, world)
+    log(f"[rank {rank}] BA scene {full.n_points} points x {full.n_poses} KFs, {full.n_edges} edges; shard "
+        f"[{lo}, {hi}) with {prob.n_edges} edges, built in {time.perf_counter() - t0:.1f}s")
+    ctx = capi.BAContext(gpu)
+    if world > 1:
+        if backend == "nccl":
+            uid = [capi.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            ctx.dist_init_rccl(world, rank, uid[0])
+        else:
+            def allreduce(buf, op):
+                t = torch.from_numpy(buf)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX)
+            ctx.dist_set_allreduce(world, rank, allreduce)
+    ctx.upload(prob)
+    if args.warmup > 0:
+        ctx.solve_lm(args.warmup)
+    ctx.set_state(poses=prob.poses, points=prob.points)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rep = ctx.solve_lm(args.steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    log(f"[rank {rank}] BA {rep['iterations']} iterations / {rep['trials_total']} trials in {dt * 1e3:.1f} ms; "
+        f"chi2 {rep['chi2_initial']:.6e} -> {rep['chi2_final']:.6e}")
+    iters = rep["iterations"]
+    t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, "cuda" if backend == "nccl" else "cpu")
+    stats = ctx.profile_trial(rep["lambda_final"])
+    # roofline: the edge linearization kernel (the dominant HBM stream): algorithmic bytes of one
+    # trial's two ba_edges launches / their device time
+    ed = stats.get("ba_edges", {"ms": 0.0, "bytes": 0.0, "launches": 0})
+    achieved = ed["bytes"] / max(ed["ms"] * 1e-3, 1e-12) / 1e9
+    roofline = {"bound": "hbm", "kernel": "ba_edges", "achieved": round(achieved, 1), "peak": 8000.0,
+                "unit": "GB/s", "frac": round(achieved / 8000.0, 4), "traffic": None,
+                "bytes_per_trial": ed["bytes"], "launches": ed["launches"],
+                "avg_launch_us": round(1e3 * ed["ms"] / max(ed["launches"], 1), 3)}
+    trial_ms = {k: round(v["ms"], 4) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = ba_cpu_baseline(full.n_edges, rep["trials_total"] / max(iters, 1), k=args.ba_kfs)
+        log(f"BA cpu baseline: {cpu}")
+    if rank == 0:
+        out = {
+            "metric": "BA LM iterations/sec (BlockSolver_6_3 Schur, point-sharded)",
+            "value": iters / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * t_max / max(iters, 1), "higher_is_better": True,
+            "scaling": args.ba_scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"BA-{full.n_points // 1000}k-x{full.n_poses}", "points": full.n_points,
+                       "keyframes": full.n_poses, "edges": full.n_edges, "points_per_gpu": hi - lo,
+                       "free_pose_dofs": 6 * (full.n_poses - 1),
+                       "trials_per_iteration": round(rep["trials_total"] / max(iters, 1), 3),
+                       "parallelism": f"points{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "trial_kernel_ms": trial_ms,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def reduce_stats(dt, iters, trials, world, device):
     """Whole-job numbers from per-rank ones: max wall time over ranks, summed iterations/trials.
     The replicas share nothing else (no data-path collective)."""
@@ -97,6 +189,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--corr", type=int, default=100000, help="correspondences per GPU (C2: 100k)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["c2", "ba"], default="c2",
+                    help="c2: the headline ARAP LM (BASELINE.json); ba: point-sharded bundle adjustment")
+    ap.add_argument("--ba-points", type=int, default=500000)
+    ap.add_argument("--ba-kfs", type=int, default=8)
+    ap.add_argument("--ba-scaling", choices=["strong", "weak"], default="strong")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,6 +213,8 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = "cuda" if backend == "nccl" else "cpu"
+    if args.workload == "ba":
+        return main_ba(args, world, rank, gpu, backend)
 
     t0 = time.perf_counter()
     prob = build_problem(args.corr, 1 + rank)

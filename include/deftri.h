@@ -314,7 +314,8 @@ int deftri_ba_eval_system(deftri_ba_ctx *ctx, int32_t level, double lambda, doub
 /* Point-sharded multi-GPU: this context is rank `rank` of `nranks`.  Either RCCL (the
    production path: ncclCommInitRank over xGMI, all-reduce on the solver stream; the 128-byte id
    comes from deftri_rccl_unique_id on rank 0, shared by the caller) or a caller-supplied
-   all-reduce (tests: e.g. gloo through host memory).  nranks == 1 clears the setting. */
+   all-reduce (tests: e.g. gloo through host memory).  nranks == 1 with a NULL id / fn clears the
+   setting (an RCCL communicator of one rank is kept when an id is given). */
 int deftri_rccl_unique_id(uint8_t id[128]);
 int deftri_ba_dist_init_rccl(deftri_ba_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int deftri_ba_dist_set_allreduce(deftri_ba_ctx *ctx, int32_t nranks, int32_t rank, deftri_allreduce_fn fn,

@@ -242,3 +242,20 @@ def test_bench_size_properties(bactx):
     poses_b, pts_b = bactx.download()
     assert r2["chi2_iter"] == r["chi2_iter"]                 # deterministic (no atomics)
     assert np.array_equal(poses_a, poses_b) and np.array_equal(pts_a, pts_b)
+
+
+def test_rccl_one_rank_path_matches(bactx):
+    """The production transport: an RCCL communicator (one rank on the single-GPU box) all-reduces
+    the pose blocks / Schur complement in place on the solver stream; results are unchanged."""
+    p = ba.make_ba_problem(n=3000, k=5, seed=12, outliers=0.02)
+    bactx.upload(p)
+    r0 = bactx.solve_lm(8)
+    poses0, pts0 = bactx.download()
+    c = capi.BAContext(0)
+    c.dist_init_rccl(1, 0, capi.rccl_unique_id())
+    c.upload(p)
+    r1 = c.solve_lm(8)
+    poses1, pts1 = c.download()
+    c.close()
+    assert r1["chi2_iter"] == r0["chi2_iter"] and r1["trials_total"] == r0["trials_total"]
+    assert np.array_equal(poses0, poses1) and np.array_equal(pts0, pts1)

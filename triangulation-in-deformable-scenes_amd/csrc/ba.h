@@ -42,7 +42,8 @@ struct BADev {
     int32_t *pose_chunk_ptr = nullptr;     // [K+1]
     // Schur GEMM stages: contiguous point ranges with <= kBaStageEdges edges each
     int32_t nstage = 0, ngroup = 0;
-    int32_t *stage_pt = nullptr;           // [nstage+1] first point of each stage
+    int32_t *stage_pt = nullptr;           // [nstage+1] first point of each stage (VALU path, ns >= 128)
+    int32_t mgroup = 0, mstages_per_group = 0;   // MFMA path: 16-point stages, consecutive per workgroup
     int32_t *group_stage = nullptr;        // [ngroup+1] stages per workgroup
     int32_t *pslot = nullptr;              // [E] Schur block of the edge's pose (-1: not in S); set on the
                                            //     lead edge of each (point, pose) pair only
@@ -55,6 +56,7 @@ struct BADev {
     double *v = nullptr;                   // [E*6]  Hpl (Dinv bl)
     // per point
     double *Hll = nullptr, *bl = nullptr, *Dinv = nullptr, *dxl = nullptr;
+    double *dbl = nullptr;                 // [P*3] Dinv bl
     // per pose
     double *pchunk = nullptr;              // [nchunk*27]: lower-triangle Hpp (21) + bp (6)
     double *Hpp = nullptr, *bp = nullptr;  // [K*36], [K*6]

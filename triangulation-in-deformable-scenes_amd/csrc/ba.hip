@@ -250,7 +250,7 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
                                   const uint8_t *__restrict__ pt_free, const int32_t *__restrict__ pslot,
                                   const double *__restrict__ Hll, const double *__restrict__ bl,
                                   const double *__restrict__ Wb, double *__restrict__ Dinv, double *__restrict__ Y,
-                                  double *__restrict__ v) {
+                                  double *__restrict__ v, double *__restrict__ dbo) {
     int l = TID;
     if (l >= P || !pt_free[l]) return;
     double m[9];
@@ -275,6 +275,8 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
     double db[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * b[0] + Di[3 * i + 1] * b[1] + Di[3 * i + 2] * b[2];
+#pragma unroll
+    for (int i = 0; i < 3; i++) dbo[3 * (int64_t)l + i] = db[i];
     for (int e = pt_ptr[l]; e < pt_ptr[l + 1]; e++) {
         if (pslot[e] < 0) continue;
         const double *B = Wb + 18 * (int64_t)e;
@@ -371,6 +373,101 @@ __global__ void __launch_bounds__(256) k_ba_schur_gemm(int ns, int nfree, const 
         const int idx = tile * 256 * kEpt + q * 256 + t;
         if (idx < NE) Spart[(int64_t)g * NE + idx] = acc[q];
     }
+}
+
+// MFMA Schur complement: per 16-point stage, the stage's Hpl Dinv (Y) and Hpl (W) blocks are
+// densified in LDS as k-major matrices Yd, Wd of npad rows (Schur dofs; row ns of Yd holds Dinv bl)
+// and K = 48 columns (3 per point), then D += Yd Wd^T with v_mfma_f64_16x16x4 on the lower block
+// triangle of 16x16 tiles.  D[i][j] (j <= i < ns) = sum Hpl_a Dinv Hlp_b; D[ns][j] = sum Hpl_b Dinv bl.
+// One workgroup per group of consecutive stages (fixed order), partials reduced by k_ba_schur_reduce4.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kMSP = 16;                 // points per MFMA stage
+
+template <int NT>
+__global__ void __launch_bounds__(256) k_ba_schur_mfma(int ns, int P, int stages_per_group,
+                                                       const int32_t *__restrict__ pt_ptr,
+                                                       const int32_t *__restrict__ ept,
+                                                       const int32_t *__restrict__ pslot,
+                                                       const uint8_t *__restrict__ pt_free,
+                                                       const double *__restrict__ Y, const double *__restrict__ Wb,
+                                                       const double *__restrict__ dbl, double *__restrict__ Spart) {
+    constexpr int NP = 16 * NT, LDR = NP + 4, KD = 3 * kMSP;
+    constexpr int NTILE = NT * (NT + 1) / 2, TPW = (NTILE + 3) / 4;
+    __shared__ double Ys[KD * LDR], Ws[KD * LDR];
+    const int g = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6, kl = lane >> 4, il = lane & 15;
+    const int ntri = ns * (ns + 1) / 2, NE = ntri + ns;
+    int tti[TPW], ttj[TPW];
+    dbl4 acc[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; q++) {
+        int idx = w + 4 * q;
+        tti[q] = -1; ttj[q] = 0;
+        if (idx < NTILE) {
+            int i = 0;
+            while ((i + 1) * (i + 2) / 2 <= idx) i++;
+            tti[q] = i; ttj[q] = idx - i * (i + 1) / 2;
+        }
+        acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    }
+    const int nstage = (P + kMSP - 1) / kMSP;
+    const int s0 = g * stages_per_group, s1 = min(nstage, s0 + stages_per_group);
+    for (int s = s0; s < s1; s++) {
+        const int p0 = s * kMSP, p1 = min(P, p0 + kMSP);
+        const int e0 = pt_ptr[p0], e1 = pt_ptr[p1];
+        __syncthreads();
+        for (int i = t; i < KD * LDR; i += 256) { Ys[i] = 0.0; Ws[i] = 0.0; }
+        __syncthreads();
+        for (int i = t; i < (e1 - e0) * 18; i += 256) {
+            const int e = e0 + i / 18, q = i % 18;
+            const int sl = pslot[e];
+            if (sl < 0) continue;
+            const int lp = ept[e] - p0, r = q / 3, c = q % 3;
+            Ys[(3 * lp + c) * LDR + 6 * sl + r] = Y[18 * (int64_t)e + q];
+            Ws[(3 * lp + c) * LDR + 6 * sl + r] = Wb[18 * (int64_t)e + q];
+        }
+        for (int i = t; i < (p1 - p0) * 3; i += 256) {
+            const int lp = i / 3, c = i % 3, l = p0 + lp;
+            Ys[(3 * lp + c) * LDR + ns] = pt_free[l] ? dbl[3 * (int64_t)l + c] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TPW; q++) {
+            if (tti[q] < 0) continue;
+            const int ra = 16 * tti[q] + il, rb = 16 * ttj[q] + il;
+#pragma unroll
+            for (int kb = 0; kb < KD; kb += 4) {
+                const double a = Ys[(kb + kl) * LDR + ra], b = Ws[(kb + kl) * LDR + rb];
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q], 0, 0, 0);
+            }
+        }
+    }
+    double *out = Spart + (int64_t)g * NE;
+#pragma unroll
+    for (int q = 0; q < TPW; q++) {
+        if (tti[q] < 0) continue;
+#pragma unroll
+        for (int gg = 0; gg < 4; gg++) {
+            const int i = 16 * tti[q] + kl + 4 * gg, j = 16 * ttj[q] + il;
+            if (i < ns && j <= i) out[i * (i + 1) / 2 + j] = acc[q][gg];
+            else if (i == ns && j < ns) out[ntri + j] = acc[q][gg];
+        }
+    }
+}
+
+// Sred = -(sum over groups of the partials), groups in fixed order: 4 waves each sum a contiguous
+// quarter of the groups for 64 entries, then the quarters are added in order
+__global__ void __launch_bounds__(256) k_ba_schur_reduce4(int NE, int ngroup, const double *__restrict__ Spart,
+                                                          double *__restrict__ Sred) {
+    __shared__ double red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int idx = blockIdx.x * 64 + lane;
+    const int q = (ngroup + 3) / 4, g0 = w * q, g1 = min(ngroup, g0 + q);
+    double s = 0.0;
+    if (idx < NE)
+        for (int g = g0; g < g1; g++) s += Spart[(int64_t)g * NE + idx];
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && idx < NE) Sred[idx] = -((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]));
 }
 
 __global__ void k_ba_schur_reduce(int NE, int ngroup, const double *__restrict__ Spart, double *__restrict__ Sred) {
@@ -585,10 +682,28 @@ static size_t schur_lds(int nfree) {
 void ba_launch_schur(const BADev &B, double lambda, hipStream_t st) {
     if (B.P > 0)
         BALAUNCH("ba_schur_points", dev::k_ba_schur_points, dim3(nbk(B.P, 128)), dim3(128), 0, st, B.P, lambda,
-                 B.pt_ptr, B.pt_free, B.pslot, B.Hll, B.bl, B.Wb, B.Dinv, B.Y, B.v);
+                 B.pt_ptr, B.pt_free, B.pslot, B.Hll, B.bl, B.Wb, B.Dinv, B.Y, B.v, B.dbl);
     const int NE = B.ns * (B.ns + 1) / 2 + B.ns;
     if (B.ns == 0) return;
-    if (B.ngroup > 0) {
+    if (B.mgroup > 0 && B.ns < 128) {                   // MFMA path (npad = 16 NT > ns)
+        const int nt = B.ns / 16 + 1;
+#define MF(NTV)                                                                                         \
+        BALAUNCH("ba_schur_mfma", dev::k_ba_schur_mfma<NTV>, dim3(B.mgroup), dim3(256), 0, st, B.ns, B.P,   \
+                 B.mstages_per_group, B.pt_ptr, B.e_point, B.pslot, B.pt_free, B.Y, B.Wb, B.dbl, B.Spart)
+        switch (nt) {
+            case 1: MF(1); break;
+            case 2: MF(2); break;
+            case 3: MF(3); break;
+            case 4: MF(4); break;
+            case 5: MF(5); break;
+            case 6: MF(6); break;
+            case 7: MF(7); break;
+            default: MF(8); break;
+        }
+#undef MF
+        BALAUNCH("ba_schur_reduce", dev::k_ba_schur_reduce4, dim3(nbk(NE, 64)), dim3(256), 0, st, NE, B.mgroup,
+                 B.Spart, B.Sred);
+    } else if (B.ngroup > 0) {
         const int ntile = (NE + 256 * dev::kEpt - 1) / (256 * dev::kEpt);
         static bool attr = false;
         if (!attr) {

@@ -111,12 +111,13 @@ void free_device(deftri_ba_ctx *ctx) {
 
 // in-place sum / max over ranks of n device doubles (no-op on one rank)
 int allreduce(deftri_ba_ctx *ctx, double *buf, int64_t n, int op) {
-    if (ctx->nranks <= 1 || n <= 0) return 0;
-    if (ctx->comm) {
+    if (n <= 0) return 0;
+    if (ctx->comm) {                          // RCCL (also with one rank: exercises the path)
         ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, op == 0 ? ncclSum : ncclMax, ctx->comm, ctx->st);
         if (r != ncclSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
         return 0;
     }
+    if (ctx->nranks <= 1) return 0;
     if (!ctx->fn) return fail(ctx, DEFTRI_E_ARG, "distributed context without a transport");
     if ((int64_t)ctx->stage.size() < n) ctx->stage.resize((size_t)n);
     HIPOK(hipMemcpyAsync(ctx->stage.data(), buf, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, ctx->st));
@@ -155,7 +156,7 @@ int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
         act[s] = (ctx->level[o] == level && !all_fixed) ? 1 : 0;
         if (act[s]) { pose_cnt[k] += 1.0; pt_act[l] = 1; }
     }
-    if (ctx->nranks > 1 && K > 0) {          // a pose is active if any rank holds an active edge of it
+    if ((ctx->nranks > 1 || ctx->comm) && K > 0) {   // a pose is active if any rank holds an active edge of it
         double *d = B.Spart;                 // scratch (allocated with >= K doubles at upload)
         HIPOK(hipMemcpyAsync(d, pose_cnt.data(), sizeof(double) * K, hipMemcpyHostToDevice, ctx->st));
         int rc = allreduce(ctx, d, K, 0);
@@ -188,7 +189,7 @@ int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
     const int64_t NE = (int64_t)B.ns * (B.ns + 1) / 2 + B.ns;
     if (B.ns > ctx->cap_ns) {
         int rc;
-        const int64_t grp = std::max<int64_t>(B.ngroup, 1);
+        const int64_t grp = std::max<int64_t>(std::max(B.ngroup, B.mgroup), 1);
         if ((rc = dalloc(ctx, &B.Spart, std::max<int64_t>(grp * NE, K)))) return rc;
         if ((rc = dalloc(ctx, &B.Sred, NE))) return rc;
         if ((rc = dalloc(ctx, &B.S, (int64_t)B.ns * B.ns))) return rc;
@@ -348,7 +349,13 @@ int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
     std::vector<int32_t> group_stage;
     for (int32_t s = 0; s < nstage; s += per_group) group_stage.push_back(s);
     group_stage.push_back(nstage);
+    // MFMA path: 16-point stages grouped per workgroup (about 1024 groups)
+    const int32_t nmstage = (P + 15) / 16;
+    const int64_t max_mgroups = std::max<int64_t>(1, std::min<int64_t>(1024, (16ll << 20) / std::max<int64_t>(ne_max, 1)));
+    const int32_t mper = (int32_t)std::max<int64_t>(1, (nmstage + max_mgroups - 1) / max_mgroups);
     BADev &B = ctx->B;
+    B.mstages_per_group = mper;
+    B.mgroup = P > 0 ? (nmstage + mper - 1) / mper : 0;
     B.K = K; B.P = P; B.E = E;
     B.huber = d->huber_delta;
     B.nchunk = (int32_t)chunk_beg.size();
@@ -375,7 +382,7 @@ int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
     ALLOC(B.wgt, E); ALLOC(B.chi, E); ALLOC(B.chi2raw, E);
     ALLOC(B.Jp, 6 * (int64_t)E); ALLOC(B.JT, 12 * (int64_t)E);
     ALLOC(B.Wb, 18 * (int64_t)E); ALLOC(B.Y, 18 * (int64_t)E); ALLOC(B.v, 6 * (int64_t)E);
-    ALLOC(B.Hll, 9 * (int64_t)P); ALLOC(B.bl, 3 * (int64_t)P); ALLOC(B.Dinv, 9 * (int64_t)P); ALLOC(B.dxl, 3 * (int64_t)P);
+    ALLOC(B.Hll, 9 * (int64_t)P); ALLOC(B.bl, 3 * (int64_t)P); ALLOC(B.dbl, 3 * (int64_t)P); ALLOC(B.Dinv, 9 * (int64_t)P); ALLOC(B.dxl, 3 * (int64_t)P);
     ALLOC(B.pchunk, 27 * (int64_t)std::max(B.nchunk, 1));
     ALLOC(ctx->hb, 1 + 42 * (int64_t)K);
     B.Hpp = ctx->hb + 1;
@@ -390,7 +397,7 @@ int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
     }
     // Schur scratch for the all-pose-free system (re-sized in prepare_active if needed)
     const int64_t ns = 6 * (int64_t)K, NE = ns * (ns + 1) / 2 + ns;
-    ALLOC(B.Spart, std::max<int64_t>((int64_t)std::max(B.ngroup, 1) * NE, K));
+    ALLOC(B.Spart, std::max<int64_t>((int64_t)std::max(std::max(B.ngroup, B.mgroup), 1) * NE, K));
     ALLOC(B.Sred, NE); ALLOC(B.S, ns * ns); ALLOC(B.xp, std::max<int64_t>(ns, 1));
     ctx->cap_ns = (int32_t)ns;
 #undef PUT
@@ -660,7 +667,7 @@ int deftri_ba_dist_init_rccl(deftri_ba_ctx *ctx, int32_t nranks, int32_t rank, c
     if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
     ctx->fn = nullptr;
     ctx->nranks = nranks; ctx->rank = rank;
-    if (nranks == 1) return 0;
+    if (!id) return 0;                        // one rank without RCCL
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
