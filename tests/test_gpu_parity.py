@@ -210,3 +210,27 @@ def test_lookahead_split_matches(gpu_ctx, monkeypatch):
     x1 = gpu_ctx.damped_solve(lam, b)
     assert np.array_equal(x0, x1)
     assert _normwise_bwd(gpu_ctx, x1, b, lam) < 1e-14
+
+
+def test_weight_search_matches_oracle():
+    """deformationOptimization's NLopt Nelder-Mead weight search (Simulation.yaml default
+    selection) with the device arapOptimization vs the same loop on the oracle: the same sequence of
+    evaluated weights, objective values (log^2 of the per-camera pixel deviations) within 1e-6."""
+    import importlib, sys
+    from arap_oracle_fn import oracle_arap
+    from deftri import optimization
+    sys.path.insert(0, str(GOLDEN))
+    mg = importlib.import_module("make_golden")
+    out = []
+    for fn in (None, oracle_arap):
+        m, st, _ = mg.scene("sim_default")
+        st.depth_weight = 3.0
+        st.n_optimizations, st.nlopt_iterations, st.n_iterations = 1, 6, 5
+        out.append(optimization.deformationOptimization(m, st, arap_fn=fn)[0])
+    g, o = out
+    assert len(g["evaluations"]) == len(o["evaluations"])
+    for eg, eo in zip(g["evaluations"], o["evaluations"]):
+        np.testing.assert_allclose(eg["x"], eo["x"], rtol=1e-9)
+        assert eg["f"] == pytest.approx(eo["f"], rel=1e-6)
+    np.testing.assert_allclose(g["weights"], o["weights"], rtol=1e-9)
+    assert g["update"] == pytest.approx(o["update"], rel=1e-5)

@@ -110,12 +110,15 @@ __global__ void k_ba_points(int P, const int32_t *__restrict__ pt_ptr, const uin
     if (l >= P || !pt_free[l]) return;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     const int ebeg = pt_ptr[l], eend = pt_ptr[l + 1];
-    for (int e = ebeg; e < eend; e++)
-        if (pslot[e] >= 0)
-#pragma unroll
-            for (int i = 0; i < 18; i++) Wb[18 * (int64_t)e + i] = 0.0;
     for (int e = ebeg; e < eend; e++) {
-        if (!active[e]) continue;
+        const int ld = lead[e];
+        if (!active[e]) {
+            // an inactive lead of a pair whose duplicate is active still carries the pair's block
+            if (ld == e && pslot[e] >= 0)
+#pragma unroll
+                for (int i = 0; i < 18; i++) Wb[18 * (int64_t)e + i] = 0.0;
+            continue;
+        }
         const double w = wgt[e];
         const double *J = Jp + 6 * (int64_t)e;
         const double r0 = wr[2 * (int64_t)e], r1 = wr[2 * (int64_t)e + 1];
@@ -126,14 +129,20 @@ __global__ void k_ba_points(int P, const int32_t *__restrict__ pt_ptr, const uin
             for (int d = 0; d < 3; d++) H[3 * c + d] += a0 * J[d] + a1 * J[3 + d];
             b[c] += J[c] * r0 + J[3 + c] * r1;
         }
-        const int ld = lead[e];
         if (pslot[ld] >= 0) {
             const double *B = JT + 12 * (int64_t)e;
             double *o = Wb + 18 * (int64_t)ld;
+            if (ld == e) {
 #pragma unroll
-            for (int j = 0; j < 6; j++)
+                for (int j = 0; j < 6; j++)
 #pragma unroll
-                for (int c = 0; c < 3; c++) o[3 * j + c] += (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
+                    for (int c = 0; c < 3; c++) o[3 * j + c] = (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
+            } else {                               // duplicate observation: add into the lead's block
+#pragma unroll
+                for (int j = 0; j < 6; j++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) o[3 * j + c] += (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
+            }
         }
     }
 #pragma unroll
@@ -189,13 +198,17 @@ __global__ void __launch_bounds__(256) k_ba_pose_chunk(const int32_t *__restrict
 }
 
 // Hpp (full 6x6) and bp per pose from its chunks in order; zeros for fixed / inactive poses
-__global__ void k_ba_pose_final(int K, const int32_t *__restrict__ pose_chunk_ptr, const double *__restrict__ pchunk,
-                                double *__restrict__ Hpp, double *__restrict__ bp) {
-    int id = TID;
+__global__ void __launch_bounds__(64) k_ba_pose_final(int K, const int32_t *__restrict__ pose_chunk_ptr,
+                                                      const double *__restrict__ pchunk, double *__restrict__ Hpp,
+                                                      double *__restrict__ bp) {
+    const int id = blockIdx.x, lane = threadIdx.x;
     if (id >= K * 27) return;
     const int k = id / 27, q = id % 27;
     double s = 0.0;
-    for (int c = pose_chunk_ptr[k]; c < pose_chunk_ptr[k + 1]; c++) s += pchunk[27 * (int64_t)c + q];
+    for (int c = pose_chunk_ptr[k] + lane; c < pose_chunk_ptr[k + 1]; c += 64) s += pchunk[27 * (int64_t)c + q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane != 0) return;
     if (q < 21) {
         int i = 0;
         while ((i + 1) * (i + 2) / 2 <= q) i++;
@@ -250,7 +263,7 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
                                   const uint8_t *__restrict__ pt_free, const int32_t *__restrict__ pslot,
                                   const double *__restrict__ Hll, const double *__restrict__ bl,
                                   const double *__restrict__ Wb, double *__restrict__ Dinv, double *__restrict__ Y,
-                                  double *__restrict__ v, double *__restrict__ dbo) {
+                                  double *__restrict__ v, double *__restrict__ dbo, int want_v) {
     int l = TID;
     if (l >= P || !pt_free[l]) return;
     double m[9];
@@ -286,7 +299,7 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
 #pragma unroll
             for (int c = 0; c < 3; c++)
                 y[3 * j + c] = B[3 * j] * Di[c] + B[3 * j + 1] * Di[3 + c] + B[3 * j + 2] * Di[6 + c];
-            vv[j] = B[3 * j] * db[0] + B[3 * j + 1] * db[1] + B[3 * j + 2] * db[2];
+            if (want_v) vv[j] = B[3 * j] * db[0] + B[3 * j + 1] * db[1] + B[3 * j + 2] * db[2];
         }
     }
 }
@@ -665,7 +678,7 @@ void ba_launch_poses(const BADev &B, hipStream_t st) {
         BALAUNCH("ba_pose_chunk", dev::k_ba_pose_chunk, dim3(B.nchunk), dim3(256), 0, st, B.chunk_beg, B.chunk_len,
                  B.pose_edges, B.active, B.wgt, B.wr, B.JT, B.pchunk);
     if (B.K > 0)
-        BALAUNCH("ba_pose_final", dev::k_ba_pose_final, dim3(nbk(27 * (int64_t)B.K, 128)), dim3(128), 0, st, B.K,
+        BALAUNCH("ba_pose_final", dev::k_ba_pose_final, dim3(27 * B.K), dim3(64), 0, st, B.K,
                  B.pose_chunk_ptr, B.pchunk, B.Hpp, B.bp);
 }
 
@@ -682,7 +695,8 @@ static size_t schur_lds(int nfree) {
 void ba_launch_schur(const BADev &B, double lambda, hipStream_t st) {
     if (B.P > 0)
         BALAUNCH("ba_schur_points", dev::k_ba_schur_points, dim3(nbk(B.P, 128)), dim3(128), 0, st, B.P, lambda,
-                 B.pt_ptr, B.pt_free, B.pslot, B.Hll, B.bl, B.Wb, B.Dinv, B.Y, B.v, B.dbl);
+                 B.pt_ptr, B.pt_free, B.pslot, B.Hll, B.bl, B.Wb, B.Dinv, B.Y, B.v, B.dbl,
+                 (B.mgroup > 0 && B.ns < 128) ? 0 : 1);
     const int NE = B.ns * (B.ns + 1) / 2 + B.ns;
     if (B.ns == 0) return;
     if (B.mgroup > 0 && B.ns < 128) {                   // MFMA path (npad = 16 NT > ns)

@@ -1088,12 +1088,14 @@ __global__ void __launch_bounds__(256) k_sum_partial(int64_t n, const double *__
     if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
+// one wave: lane l sums partials l, l+64, ... in order, then a fixed butterfly (deterministic)
 __global__ void k_sum_final(int n, const double *__restrict__ part, double *__restrict__ out) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        double acc = 0.0;
-        for (int i = 0; i < n; i++) acc += part[i];
-        *out = acc;
-    }
+    const int lane = threadIdx.x;
+    double acc = 0.0;
+    for (int i = lane; i < n; i += 64) acc += part[i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) *out = acc;
 }
 
 __global__ void __launch_bounds__(256) k_maxdiag(int64_t nblocks, const int64_t *__restrict__ val_off,
@@ -1119,11 +1121,12 @@ __global__ void __launch_bounds__(256) k_maxdiag(int64_t nblocks, const int64_t 
 }
 
 __global__ void k_max_final(int n, const double *__restrict__ part, double *__restrict__ out) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        double mx = 0.0;
-        for (int i = 0; i < n; i++) mx = fmax(mx, part[i]);
-        *out = mx;
-    }
+    const int lane = threadIdx.x;
+    double mx = 0.0;
+    for (int i = lane; i < n; i += 64) mx = fmax(mx, part[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off, 64));
+    if (lane == 0) *out = mx;
 }
 
 // y = H x from the stored blocks (diagnostics; H symmetric, blocks hold the lower triangle)

@@ -6,9 +6,10 @@ over the C-ABI.  Same names, argument meaning and write-back behaviour:
       depth scales and the global KF-pair transformation; returns sum ||p_old - p_new||
       (g2oBundleAdjustment.cc:608-1008).
   deformationOptimization(pMap, settings, originalPoints, movedPoints)
-      outer rounds until sum ||dp|| < 1e-4 * |MapPoints| (:446-606) with fixed weights
-      ("g2oArap" selection).  The NLopt / Eigen weight tuning of "twoOptimizations" is the next
-      component and raises NotImplementedError here.
+      outer rounds until sum ||dp|| < 1e-4 * |MapPoints| (:446-606): fixed weights ("g2oArap") or
+      the NLopt Nelder-Mead weight search ("twoOptimizations" + "nlopt", deftri/nlopt_nm.py) whose
+      every evaluation is an arapOptimization on a map clone (outerObjective,
+      nloptOptimization.cc:5-38).
   bundleAdjustment / localBundleAdjustment / poseOnlyOptimization
       BA entry points (no callers at the reference's HEAD): the BlockSolver_6_3 Schur
       LM on the device (deftri/ba.py over deftri_ba_*).
@@ -45,25 +46,72 @@ def arapOptimization(pMap, repBalanceWeight, globalBalanceWeight, arapBalanceWei
     return upd
 
 
-def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=None, device=0, log=None):
+def outerObjective(x, pMap, settings, arap_fn=None, device=0):
+    """nloptOptimization.cc:5-38: arapOptimization on a clone of the map with weights x = (rep,
+    global, arap), then (log desvc1)^2 + (log desvc2)^2 of calculatePixelsStandDev."""
+    import copy
+    import math
+    from . import metrics
+    clone = copy.deepcopy(pMap)                 # pData->pMap->clone()
+    fn = arap_fn or (lambda m, *a: arapOptimization(m, *a, device=device))
+    fn(clone, float(x[0]), float(x[1]), float(x[2]), settings.alpha, settings.beta, settings.depth_sigma,
+       settings.n_iterations)
+    pe = metrics.pixels_stand_dev(clone)
+
+    def lg2(v):
+        return math.log(v) ** 2 if v > 0 else math.inf
+    return lg2(pe["desvc1"]) + lg2(pe["desvc2"])
+
+
+def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=None, device=0, log=None,
+                            arap_fn=None):
+    """g2oBundleAdjustment.cc:446-606.  Outer rounds until sum ||dp|| < 1e-4 |MapPoints| or
+    numberOfOptimizations; per round either the fixed weights ("g2oArap") or the weight search
+    ("twoOptimizations" + "nlopt": Nelder-Mead over (rep, global, arap) within the nlopt bounds,
+    each evaluation an arapOptimization on a map clone, then arapOptimization on the map with the
+    optimum, which becomes the next round's start).  `arap_fn` (tests only) replaces the device
+    arapOptimization with another implementation of the same signature."""
+    import copy
+    from .nlopt_nm import nelder_mead
     settings.validate_for_solver()
-    if settings.selection == "twoOptimizations":
-        raise NotImplementedError("twoOptimizations (NLopt/Eigen weight tuning) is the next component; "
-                                  "use selection 'g2oArap' (fixed weights)")
     if settings.selection == "open3DArap":
         raise NotImplementedError("open3DArap is a different algorithm (Open3D DeformAsRigidAsPossible), out of scope")
+    if settings.selection == "twoOptimizations" and settings.weights_selection != "nlopt":
+        raise NotImplementedError("twoOptimizations with the Eigen LM weight search (EigenOptimization.h) is not "
+                                  "built: its functor declares 2 inputs but reads 3 (SURVEY §2 row 3); use nlopt")
+
+    def run_arap(m, rep, glob, arap):
+        if arap_fn is not None:
+            return arap_fn(m, rep, glob, arap, settings.alpha, settings.beta, settings.depth_sigma,
+                           settings.n_iterations)
+        return arapOptimization(m, rep, glob, arap, settings.alpha, settings.beta, settings.depth_sigma,
+                                settings.n_iterations, device=device)
+
     n_mp = len(pMap.map_points)
+    rep_w, glob_w, arap_w = settings.rep, settings.global_, settings.arap
     update = 100.0
     rounds = []
     i = 1
     while i <= settings.n_optimizations and update >= 0.0001 * n_mp:
-        rep = {}
-        update = arapOptimization(pMap, settings.rep, settings.global_, settings.arap, settings.alpha,
-                                  settings.beta, settings.depth_sigma, settings.n_iterations, device=device,
-                                  report=rep)
-        rounds.append({"round": i, "update": update, "chi2_final": rep.get("chi2_final")})
+        info = {"round": i}
+        if settings.selection == "twoOptimizations":
+            base = copy.deepcopy(pMap)            # optData.pMap = pMap->clone()
+            evals = []
+            x, minf, res, nev = nelder_mead(
+                lambda x: outerObjective(x, base, settings, arap_fn=arap_fn, device=device),
+                [rep_w, glob_w, arap_w],
+                [settings.nlopt_rep_lb, settings.nlopt_global_lb, settings.nlopt_arap_lb],
+                [settings.nlopt_rep_ub, settings.nlopt_global_ub, settings.nlopt_arap_ub],
+                xtol_rel=settings.nlopt_rel_tol, xtol_abs=settings.nlopt_abs_tol,
+                maxeval=int(settings.nlopt_iterations), log=evals.append)
+            rep_w, glob_w, arap_w = (float(v) for v in x)
+            info.update({"weights": [rep_w, glob_w, arap_w], "minf": minf, "nlopt_result": res,
+                         "evaluations": evals})
+        update = run_arap(pMap, rep_w, glob_w, arap_w)
+        info["update"] = update
+        rounds.append(info)
         if log:
-            log(rounds[-1])
+            log(info)
         i += 1
     return rounds
 
