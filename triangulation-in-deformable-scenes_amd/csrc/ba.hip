@@ -290,6 +290,7 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
     for (int i = 0; i < 3; i++) db[i] = Di[3 * i] * b[0] + Di[3 * i + 1] * b[1] + Di[3 * i + 2] * b[2];
 #pragma unroll
     for (int i = 0; i < 3; i++) dbo[3 * (int64_t)l + i] = db[i];
+    if (!want_v) return;
     for (int e = pt_ptr[l]; e < pt_ptr[l + 1]; e++) {
         if (pslot[e] < 0) continue;
         const double *B = Wb + 18 * (int64_t)e;
@@ -299,7 +300,7 @@ __global__ void k_ba_schur_points(int P, double lambda, const int32_t *__restric
 #pragma unroll
             for (int c = 0; c < 3; c++)
                 y[3 * j + c] = B[3 * j] * Di[c] + B[3 * j + 1] * Di[3 + c] + B[3 * j + 2] * Di[6 + c];
-            if (want_v) vv[j] = B[3 * j] * db[0] + B[3 * j + 1] * db[1] + B[3 * j + 2] * db[2];
+            vv[j] = B[3 * j] * db[0] + B[3 * j + 1] * db[1] + B[3 * j + 2] * db[2];
         }
     }
 }
@@ -402,7 +403,7 @@ __global__ void __launch_bounds__(256) k_ba_schur_mfma(int ns, int P, int stages
                                                        const int32_t *__restrict__ ept,
                                                        const int32_t *__restrict__ pslot,
                                                        const uint8_t *__restrict__ pt_free,
-                                                       const double *__restrict__ Y, const double *__restrict__ Wb,
+                                                       const double *__restrict__ Dinv, const double *__restrict__ Wb,
                                                        const double *__restrict__ dbl, double *__restrict__ Spart) {
     constexpr int NP = 16 * NT, LDR = NP + 4, KD = 3 * kMSP;
     constexpr int NTILE = NT * (NT + 1) / 2, TPW = (NTILE + 3) / 4;
@@ -434,9 +435,11 @@ __global__ void __launch_bounds__(256) k_ba_schur_mfma(int ns, int P, int stages
             const int e = e0 + i / 18, q = i % 18;
             const int sl = pslot[e];
             if (sl < 0) continue;
-            const int lp = ept[e] - p0, r = q / 3, c = q % 3;
-            Ys[(3 * lp + c) * LDR + 6 * sl + r] = Y[18 * (int64_t)e + q];
-            Ws[(3 * lp + c) * LDR + 6 * sl + r] = Wb[18 * (int64_t)e + q];
+            const int l = ept[e], lp = l - p0, r = q / 3, c = q % 3;
+            const double *wr = Wb + 18 * (int64_t)e + 3 * r, *di = Dinv + 9 * (int64_t)l + c;
+            // Y = Hpl Dinv (BDinv of BlockSolver::solve), formed here instead of stored
+            Ys[(3 * lp + c) * LDR + 6 * sl + r] = wr[0] * di[0] + wr[1] * di[3] + wr[2] * di[6];
+            Ws[(3 * lp + c) * LDR + 6 * sl + r] = wr[c];
         }
         for (int i = t; i < (p1 - p0) * 3; i += 256) {
             const int lp = i / 3, c = i % 3, l = p0 + lp;
@@ -703,7 +706,7 @@ void ba_launch_schur(const BADev &B, double lambda, hipStream_t st) {
         const int nt = B.ns / 16 + 1;
 #define MF(NTV)                                                                                         \
         BALAUNCH("ba_schur_mfma", dev::k_ba_schur_mfma<NTV>, dim3(B.mgroup), dim3(256), 0, st, B.ns, B.P,   \
-                 B.mstages_per_group, B.pt_ptr, B.e_point, B.pslot, B.pt_free, B.Y, B.Wb, B.dbl, B.Spart)
+                 B.mstages_per_group, B.pt_ptr, B.e_point, B.pslot, B.pt_free, B.Dinv, B.Wb, B.dbl, B.Spart)
         switch (nt) {
             case 1: MF(1); break;
             case 2: MF(2); break;

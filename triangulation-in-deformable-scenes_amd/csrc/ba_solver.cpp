@@ -59,6 +59,8 @@ struct deftri_ba_ctx {
     deftri_allreduce_fn fn = nullptr;
     void *fn_user = nullptr;
     std::vector<double> stage;                // host staging for the callback all-reduce
+    double *hpin = nullptr;                   // pinned host staging of the per-trial scalars
+    int *ipin = nullptr;
     int32_t n_free_points = 0;
 };
 
@@ -250,6 +252,11 @@ int deftri_ba_create(int32_t device, deftri_ba_ctx **out) {
         return DEFTRI_E_HIP;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
+    if (hipHostMalloc((void **)&ctx->hpin, 16 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->ipin, 16 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        delete ctx;
+        return DEFTRI_E_HIP;
+    }
     *out = ctx;
     return 0;
 }
@@ -262,6 +269,8 @@ int deftri_ba_destroy(deftri_ba_ctx *ctx) {
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
     if (ctx->st) hipStreamDestroy(ctx->st);
+    if (ctx->hpin) hipHostFree(ctx->hpin);
+    if (ctx->ipin) hipHostFree(ctx->ipin);
     delete ctx;
     return 0;
 }
@@ -469,9 +478,9 @@ int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *prm, int32_t 
             if ((rc = allreduce(ctx, B.scal + 2, 1, 1))) return rc;
         }
         hipEventRecord(ctx->ev[1], ctx->st);
-        double head[3];
+        double *head = ctx->hpin;            // pinned: a pageable readback costs ~100 us per call
         HIPOK(hipMemcpyAsync(&head[0], ctx->hb, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
-        HIPOK(hipMemcpyAsync(&head[2], B.scal + 2, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
+        if (it == 0) HIPOK(hipMemcpyAsync(&head[2], B.scal + 2, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
         HIPOK(hipStreamSynchronize(ctx->st));
         t_lin += ev_ms(ctx, 0, 1);
         currentChi = head[0];
@@ -496,11 +505,11 @@ int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *prm, int32_t 
             ba_launch_scale(B, lambda, B.scal + 1, B.scal + 3, ctx->st);
             if ((rc = allreduce(ctx, B.scal, 2, 0))) return rc;
             hipEventRecord(ctx->ev[5], ctx->st);
-            double sc[4];
-            int flag = 0;
+            double *sc = ctx->hpin + 4;
             HIPOK(hipMemcpyAsync(sc, B.scal, sizeof(double) * 4, hipMemcpyDeviceToHost, ctx->st));
-            HIPOK(hipMemcpyAsync(&flag, B.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            HIPOK(hipMemcpyAsync(ctx->ipin, B.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
             HIPOK(hipStreamSynchronize(ctx->st));
+            const int flag = *ctx->ipin;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             const bool ok2 = flag == 0;
             const double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();

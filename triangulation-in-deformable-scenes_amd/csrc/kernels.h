@@ -96,7 +96,7 @@ void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev);
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st);
-void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st);
+void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
                 double *out, hipStream_t st);
 void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st);

@@ -1047,9 +1047,11 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
 // ------------------------------------------------------------------------------------------
 // state update, reductions
 // ------------------------------------------------------------------------------------------
+// skipped when the factorization flagged a zero pivot (the trial is rejected and the state restored)
 __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
-                               double *__restrict__ scales, double *__restrict__ tg) {
+                               double *__restrict__ scales, double *__restrict__ tg, const int *__restrict__ flag) {
     int i = TID;
+    if (flag && *flag) return;
     int64_t pbase = 6 * (int64_t)Q + S;
     if (i < P) {
         points[3 * (int64_t)i] += dx[pbase + 3 * (int64_t)i];
@@ -1297,12 +1299,12 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
     }
 }
 
-void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st) {
+void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag) {
     int n = P.P > P.S ? P.P : P.S;
     if (P.Q > n) n = P.Q;
     if (n > 0)
         LAUNCH("update_state", dev::k_update_state, dim3(nb(n, 128)), dim3(128), st, P.P, P.S, P.Q, dx, P.points,
-                           P.scales, P.tg);
+                           P.scales, P.tg, flag);
 }
 
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,

@@ -83,6 +83,8 @@ struct deftri_ctx {
     DevPlan L;
     std::vector<void *> allocs;
     double *d_dx = nullptr, *d_part = nullptr, *d_scal = nullptr;   // d_scal: [0]=chi2 [1]=scale [2]=maxdiag
+    double *hpin = nullptr;                 // pinned host staging of the per-trial scalars (16 doubles)
+    int *ipin = nullptr;                    // pinned host staging of the zero-pivot flag
     std::vector<double *> init_state;       // device copies of the initial state
     hipEvent_t ev[8]{};
     // map-level graph (deftri_arap_build_graph)
@@ -353,10 +355,9 @@ void eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot) {
 }
 
 double read_scal(deftri_ctx *ctx, int slot) {
-    double v = 0;
-    hipMemcpyAsync(&v, ctx->d_scal + slot, sizeof(double), hipMemcpyDeviceToHost, ctx->st);
+    hipMemcpyAsync(ctx->hpin, ctx->d_scal + slot, sizeof(double), hipMemcpyDeviceToHost, ctx->st);
     hipStreamSynchronize(ctx->st);
-    return v;
+    return ctx->hpin[0];
 }
 
 void push_state(deftri_ctx *ctx) {
@@ -412,6 +413,11 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
         return DEFTRI_E_HIP;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
+    if (hipHostMalloc((void **)&ctx->hpin, 16 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->ipin, 16 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        delete ctx;
+        return DEFTRI_E_HIP;
+    }
     hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
     for (auto &e : ctx->sync_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     *out = ctx;
@@ -427,6 +433,8 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     for (auto &e : ctx->sync_ev) if (e) hipEventDestroy(e);
     if (ctx->side) hipStreamDestroy(ctx->side);
     if (ctx->st) hipStreamDestroy(ctx->st);
+    if (ctx->hpin) hipHostFree(ctx->hpin);
+    if (ctx->ipin) hipHostFree(ctx->ipin);
     delete ctx;
     return 0;
 }
@@ -580,7 +588,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         launch_assemble(P, L, ctx->st);                      // buildSystem
         if (it == 0) launch_maxdiag(L, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
         hipEventRecord(ctx->ev[1], ctx->st);
-        double chis[3];
+        double *chis = ctx->hpin;           // pinned: a pageable readback costs ~100 us per call
         HIPOK(hipMemcpyAsync(chis, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
         HIPOK(hipStreamSynchronize(ctx->st));
         t_lin += ev_ms(ctx, 0, 1);
@@ -600,18 +608,15 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             hipEventRecord(ctx->ev[3], ctx->st);
             launch_solve(L, L.b, ctx->d_dx, ctx->st);
             hipEventRecord(ctx->ev[4], ctx->st);
-            int flag = 0;
-            HIPOK(hipMemcpyAsync(&flag, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-            HIPOK(hipStreamSynchronize(ctx->st));
-            bool ok2 = flag == 0;
-            if (!ok2) HIPOK(hipMemsetAsync(ctx->d_dx, 0, sizeof(double) * (size_t)ctx->S.ndof, ctx->st));
-            launch_update_state(P, ctx->d_dx, ctx->st);      // _optimizer->update(x)
+            launch_update_state(P, ctx->d_dx, ctx->st, L.flag);   // _optimizer->update(x) (skipped on a zero pivot)
             eval_chi2_dev(ctx, false, analytic, 0);          // computeActiveErrors; activeRobustChi2
             launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
             hipEventRecord(ctx->ev[5], ctx->st);
-            double sc[2];
+            double *sc = ctx->hpin + 4;
             HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
-            HIPOK(hipStreamSynchronize(ctx->st));
+            HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
+            const bool ok2 = *ctx->ipin == 0;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
             rho = (currentChi - tempChi);
