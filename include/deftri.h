@@ -5,10 +5,10 @@
  * luicalrob/Triangulation-in-Deformable-Scenes: the g2o Levenberg–Marquardt
  * solve inside `arapOptimization` (Modules/Optimization/g2oBundleAdjustment.cc:608-1008
  * at the surveyed revision; the LM call is `optimizer.optimize(nOptIterations)`
- * at g2oBundleAdjustment.cc:962).  The reference's C++ entry points
- * (Modules/Optimization/g2oBundleAdjustment.h:36-75) are kept by the C++ adapter
- * (csrc/adapter.cpp, deftri_adapter.h) and by the Python mirror (deftri/optimization.py);
- * both sit on top of this plain C interface.
+ * at g2oBundleAdjustment.cc:962), and the BlockSolver_6_3 Schur LM of its BA entry
+ * points (:38-444).  The reference's C++ entry points (Modules/Optimization/g2oBundleAdjustment.h:36-75)
+ * are mirrored by deftri/optimization.py and deftri/ba.py; the adapter a C++ maintainer would put
+ * behind those signatures is shown in INTEGRATION.md.  Both sit on this plain C interface.
  *
  * Conventions
  *  - every function returns int: 0 = OK, < 0 = error (see DEFTRI_E_*); the message
