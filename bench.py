@@ -190,6 +190,8 @@ def main():
     ap.add_argument("--ba-points", type=int, default=500000)
     ap.add_argument("--ba-kfs", type=int, default=8)
     ap.add_argument("--ba-scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="speculative LM lambda lanes (0: library default, 1: sequential trials)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -218,6 +220,7 @@ def main():
     ctx = capi.Context(gpu)
     t0 = time.perf_counter()
     ctx.upload(prob)
+    ctx.set_lm_lanes(args.lanes)
     log(f"[rank {rank}] upload + symbolic analysis {time.perf_counter() - t0:.1f}s")
 
     if args.warmup > 0:
@@ -281,6 +284,8 @@ def main():
                        "fronts": rep["n_fronts"], "nnz_factor": rep["nnz_factor"],
                        "factor_gflop": round(factor_flops / 1e9, 3),
                        "trials_per_iteration": round(tr_sum / max(it_sum, 1), 3),
+                       "lm_lanes": rep["lanes"],
+                       "trials_executed_per_iteration": round(rep["trials_executed"] / max(iters, 1), 3),
                        "parallelism": f"replicas{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -237,3 +237,47 @@ def test_weight_search_matches_oracle():
         assert eg["f"] == pytest.approx(eo["f"], rel=2e-3)
     np.testing.assert_allclose(g["weights"], o["weights"], rtol=1e-9)
     assert g["update"] == pytest.approx(o["update"], rel=1e-5)
+
+
+def _lm_run(ctx, lanes, n_it, **kw):
+    ctx.set_lm_lanes(lanes)
+    ctx.reset_state()
+    r = ctx.solve_lm(n_it, analytic=True, **kw)
+    pts, sc, tg = ctx.download()
+    return r, pts, sc, tg
+
+
+@pytest.mark.parametrize("kw", [{}, {"max_trials": 3}, {"user_lambda": 1e-9}])
+def test_speculative_lanes_bit_identical(gpu_ctx, kw):
+    """Speculative lambda lanes replay g2o's trial sequence: identical to sequential trials, bit for
+    bit (chi2 per iteration, trial counts, final lambda, state), for any lane count, including
+    rounds cut short by max_trials and iterations that need several rounds (tiny initial lambda)."""
+    m, _ = sim.simulate_two_view(n=3000, seed=7, scale_scene=True, compact=True)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    gpu_ctx.upload(p)
+    r1, *s1 = _lm_run(gpu_ctx, 1, 8, **kw)
+    assert r1["lanes"] == 1 and r1["trials_executed"] == r1["trials_total"]
+    for lanes in (2, 3, 8):
+        r, *s = _lm_run(gpu_ctx, lanes, 8, **kw)
+        assert r["lanes"] == min(lanes, kw.get("max_trials", 10))
+        for k in ("chi2_iter", "trials_iter", "trials_total", "trials_rejected", "lambda_final", "chi2_final",
+                  "iterations", "status"):
+            assert r[k] == r1[k], (lanes, k)
+        assert r["trials_executed"] >= r["trials_total"]
+        for a, b in zip(s, s1):
+            assert np.array_equal(a, b)
+    gpu_ctx.set_lm_lanes(0)
+
+
+def test_speculative_lanes_full_size(gpu_ctx):
+    """C2 (100k correspondences): three lanes reproduce the sequential trajectory."""
+    m, _ = sim.simulate_two_view(n=100000, seed=1, scale_scene=True, compact=True)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    gpu_ctx.upload(p)
+    r1, *s1 = _lm_run(gpu_ctx, 1, 3)
+    r3, *s3 = _lm_run(gpu_ctx, 3, 3)
+    gpu_ctx.set_lm_lanes(0)
+    assert r3["lanes"] == 3
+    assert r3["chi2_iter"] == r1["chi2_iter"] and r3["trials_iter"] == r1["trials_iter"]
+    for a, b in zip(s3, s1):
+        assert np.array_equal(a, b)

@@ -48,6 +48,14 @@ struct LevelDev {
     int64_t bgemv_off; int32_t nbgemv;
 };
 
+// batched LM trials ("lambda lanes"): every factor/solve launch carries a second grid dimension,
+// lane = blockIdx.y, whose buffers sit at these strides from lane 0's (all zero for one lane)
+constexpr int kMaxLanes = 8;
+struct LaneOff {
+    int64_t arena = 0, inv = 0, vec = 0, x = 0;   // doubles between consecutive lanes' buffers
+    double lam[kMaxLanes] = {0, 0, 0, 0, 0, 0, 0, 0};   // setLambda of each lane (k_scatter)
+};
+
 struct DevPlan {
     int64_t nv = 0, ndof = 0;
     int64_t *voff = nullptr;
@@ -79,7 +87,9 @@ struct DevPlan {
     FrontDev fd{};
     int32_t *tasks = nullptr;
     std::vector<LevelDev> levels;
-    int *flag = nullptr;
+    int *flag = nullptr;          // one zero-pivot flag per lane
+    int nlanes = 1;               // lanes the factor / solve launches cover (blockIdx.y)
+    LaneOff lo{};
 };
 
 // per-launch device timing for deftri_profile_trial (never active on the solve path)
@@ -93,7 +103,8 @@ void set_profiler(KProf *p);
 
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
-void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);   // lane 0 / one lane
+void launch_scatter_lanes(const DevPlan &L, hipStream_t st);            // L.nlanes lanes, L.lo.lam
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev);
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st);
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);

@@ -396,9 +396,11 @@ __global__ void __launch_bounds__(256) k_bfinal_heavy(const int64_t *__restrict_
 __global__ void k_scatter(int64_t nblocks, const int64_t *__restrict__ val_off, const int32_t *__restrict__ brows,
                           const int32_t *__restrict__ bcols, const int64_t *__restrict__ barena,
                           const int32_t *__restrict__ bld, const int32_t *__restrict__ bdiag,
-                          const double *__restrict__ hval, double lambda, double *__restrict__ arena) {
+                          const double *__restrict__ hval, const LaneOff lo, double *__restrict__ arena) {
     int64_t b = TID;
     if (b >= nblocks) return;
+    const double lambda = lo.lam[blockIdx.y];
+    arena += blockIdx.y * lo.arena;
     int R = brows[b], Cc = bcols[b], ld = bld[b];
     const double *h = hval + val_off[b];
     double *a = arena + barena[b];
@@ -416,9 +418,10 @@ __global__ void k_scatter(int64_t nblocks, const int64_t *__restrict__ val_off, 
 // written by exactly one thread of the launch (slot-0 and slot-1 children run in separate launches,
 // so the summation order is fixed).
 __global__ void __launch_bounds__(256) k_ea(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                            double *__restrict__ arena) {
+                                            double *__restrict__ arena, const LaneOff lo) {
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena;
     int c = tasks[3 * t], j0 = tasks[3 * t + 1], i0 = tasks[3 * t + 2];
     int p = fd.parent[c];
     int mc = fd.m[c], sc = fd.s[c], mp = fd.m[p];
@@ -678,10 +681,11 @@ __device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, doub
 // factored by the update launch of the previous panel, see k_update)
 __global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                               double *__restrict__ arena, double *__restrict__ inv,
-                                              int *__restrict__ flag) {
+                                              int *__restrict__ flag, const LaneOff lo) {
     __shared__ double S[64][DP];
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1];
     diag_panel(arena + fd.arena_off[f], fd.m[f], fd.s[f], k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S,
                flag);
@@ -716,10 +720,12 @@ __device__ __forceinline__ void mfma_tile(const double (*P)[LDP], const double (
 // The inverse (scaled by 1/d_c) is staged once in LDS (shared by the 4 waves); each wave's row
 // operands come straight from the front, all issued before the MFMA chain.
 __global__ void __launch_bounds__(256) k_trsm(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                              double *__restrict__ arena, const double *__restrict__ inv) {
+                                              double *__restrict__ arena, const double *__restrict__ inv,
+                                              const LaneOff lo) {
     __shared__ double Ps[64][LDP];   // Ps[k][c] = Linv[c][k] / d_c
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
     int kb = min(64, s - k0), kb4 = (kb + 3) & ~3;
@@ -793,13 +799,18 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // not operand bandwidth, bounds the big launches.)  LDS here is only the fused panel
 // factorization's.
 struct DiagSmem { double S[64][DP]; };
+#ifndef DEFTRI_UPD_WPE
+#define DEFTRI_UPD_WPE 4
+#endif
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
-                                                double *__restrict__ inv, int *__restrict__ flag) {
+                                                double *__restrict__ inv, int *__restrict__ flag,
+                                                const LaneOff lo) {
     __shared__ DiagSmem sm;
     int t = xcd_task(ntask);
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y;
     int f = tasks[3 * t], ti = tasks[3 * t + 1], tj = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
     int K = min(kmax, s - kA);
@@ -902,9 +913,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 // forward gather: v = [rhs of own rows; 0 on boundary rows] + the children's update vectors (slot 0
 // then slot 1: fixed order)
 __global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                                    const double *__restrict__ rhs, double *__restrict__ vec) {
+                                                    const double *__restrict__ rhs, double *__restrict__ vec,
+                                                    const LaneOff lo) {
     int t = blockIdx.x;
     if (t >= ntask) return;
+    vec += blockIdx.y * lo.vec;
     int f = tasks[3 * t];
     int m = fd.m[f], s = fd.s[f];
     const int32_t *rows = fd.rows + fd.rows_off[f];
@@ -927,12 +940,14 @@ __global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__
 // (these launches are latency-bound: one load round instead of three).
 __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ inv,
-                                                  double *__restrict__ vec, double *__restrict__ yvec) {
+                                                  double *__restrict__ vec, double *__restrict__ yvec,
+                                                  const LaneOff lo) {
     __shared__ double vs[64];
     __shared__ double ys[64];
     __shared__ double red[4][64];
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; vec += blockIdx.y * lo.vec; yvec += blockIdx.y * lo.vec;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
     int kb = min(64, s - k0);
@@ -974,9 +989,11 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
 // backward init (front f, own columns c0..c0+15): w_c = y_c / d_c - sum_{i >= s} L[i][c] x[rows[i]]
 __global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ x,
-                                                  const double *__restrict__ yvec, double *__restrict__ vec) {
+                                                  const double *__restrict__ yvec, double *__restrict__ vec,
+                                                  const LaneOff lo) {
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; x += blockIdx.y * lo.x; yvec += blockIdx.y * lo.vec; vec += blockIdx.y * lo.vec;
     int f = tasks[3 * t], c0 = tasks[3 * t + 1];
     int m = fd.m[f], s = fd.s[f];
     const double *F = arena + fd.arena_off[f];
@@ -999,12 +1016,14 @@ __global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__re
 // lane and every 4th term; loads issued up front, partial sums reduced through LDS in fixed order.
 __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ inv,
-                                                  double *__restrict__ vec, double *__restrict__ x) {
+                                                  double *__restrict__ vec, double *__restrict__ x,
+                                                  const LaneOff lo) {
     __shared__ double ws[64];
     __shared__ double xs[64];
     __shared__ double red[4][64];
     int t = blockIdx.x;
     if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; vec += blockIdx.y * lo.vec; x += blockIdx.y * lo.x;
     int f = tasks[3 * t], k0 = tasks[3 * t + 1], q0 = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
     int kb = min(64, s - k0);
@@ -1216,11 +1235,20 @@ void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
                            L.bv_chunk_begin, L.voff, L.vdim, L.bpart, L.b);
 }
 
-void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
-    hipMemsetAsync(L.arena, 0, sizeof(double) * (size_t)L.arena_size, st);
+void launch_scatter_lanes(const DevPlan &L, hipStream_t st) {
+    // lanes' arenas are contiguous (stride lo.arena >= arena_size): one fill covers them all
+    const int64_t span = L.nlanes > 1 ? (int64_t)(L.nlanes - 1) * L.lo.arena + L.arena_size : L.arena_size;
+    hipMemsetAsync(L.arena, 0, sizeof(double) * (size_t)span, st);
     if (L.nblocks > 0)
-        LAUNCH("scatter", dev::k_scatter, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks, L.blk_val_off,
-                           L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, lambda, L.arena);
+        LAUNCH("scatter", dev::k_scatter, dim3(nb(L.nblocks, 128), L.nlanes), dim3(128), st, L.nblocks,
+               L.blk_val_off, L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, L.lo, L.arena);
+}
+
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
+    DevPlan one = L;
+    one.nlanes = 1;
+    one.lo.lam[0] = lambda;
+    launch_scatter_lanes(one, st);
 }
 
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev) {
@@ -1231,15 +1259,15 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
         g_level = (int)h;
         for (int slot = 0; slot < 2; slot++)
             if (lv.nea[slot] > 0)
-                LAUNCH("ea", dev::k_ea, dim3(lv.nea[slot]), dim3(256), st, lv.nea[slot],
-                                   L.tasks + 3 * lv.ea_off[slot], L.fd, L.arena);
+                LAUNCH("ea", dev::k_ea, dim3(lv.nea[slot], L.nlanes), dim3(256), st, lv.nea[slot],
+                                   L.tasks + 3 * lv.ea_off[slot], L.fd, L.arena, L.lo);
         for (const auto &stp : lv.steps) {
             if (stp.ndiag > 0)
-                LAUNCH("diag", dev::k_diag, dim3(stp.ndiag), dim3(256), st, stp.ndiag, L.tasks + 3 * stp.diag_off,
-                                   L.fd, L.arena, L.inv, L.flag);
+                LAUNCH("diag", dev::k_diag, dim3(stp.ndiag, L.nlanes), dim3(256), st, stp.ndiag,
+                                   L.tasks + 3 * stp.diag_off, L.fd, L.arena, L.inv, L.flag, L.lo);
             if (stp.ntrsm > 0)
-                LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm), dim3(256), st, stp.ntrsm, L.tasks + 3 * stp.trsm_off,
-                                   L.fd, L.arena, L.inv);
+                LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm, L.nlanes), dim3(256), st, stp.ntrsm,
+                                   L.tasks + 3 * stp.trsm_off, L.fd, L.arena, L.inv, L.lo);
             static const bool no_side = std::getenv("DEFTRI_NO_SIDE_STREAM") != nullptr;   // A/B experiments
             if (stp.stream == 1 && !no_side) {
                 // "rest" update of an outer block: after the block's panel chain on the main stream,
@@ -1251,8 +1279,9 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
                     hipEventRecord(e, st);
                     hipStreamWaitEvent(side, e, 0);
                     g_work = stp.upd_flops;
-                    LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), side, stp.nupd,
-                           L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv, L.flag);
+                    LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), side, stp.nupd,
+                           L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv, L.flag,
+                           L.lo);
                     cur_side = ev[evi++ % nev];
                     hipEventRecord(cur_side, side);
                 }
@@ -1262,9 +1291,9 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
             if (stp.wait_side == 2 && cur_side) hipStreamWaitEvent(st, cur_side, 0);
             if (stp.nupd > 0) {
                 g_work = stp.upd_flops;
-                LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8)), dim3(256), st, stp.nupd,
+                LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), st, stp.nupd,
                        L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
-                       L.arena, L.inv, L.flag);
+                       L.arena, L.inv, L.flag, L.lo);
             }
         }
         // the level's side-stream work must be complete before the next level (or the solve) reads it
@@ -1279,23 +1308,23 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
         const auto &lv = L.levels[h];
         g_level = (int)h;
         if (lv.nfwd > 0)
-            LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd), dim3(256), st, lv.nfwd, L.tasks + 3 * lv.fwd_off,
-                   L.fd, rhs, L.vec);
+            LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd, L.nlanes), dim3(256), st, lv.nfwd,
+                   L.tasks + 3 * lv.fwd_off, L.fd, rhs, L.vec, L.lo);
         for (const auto &sp : lv.fsteps)
             if (sp.n > 0)
-                LAUNCH("fwd_step", dev::k_fwd_step, dim3(sp.n), dim3(256), st, sp.n, L.tasks + 3 * sp.off, L.fd,
-                       L.arena, L.inv, L.vec, L.yvec);
+                LAUNCH("fwd_step", dev::k_fwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
+                       L.fd, L.arena, L.inv, L.vec, L.yvec, L.lo);
     }
     for (size_t hh = L.levels.size(); hh-- > 0;) {
         const auto &lv = L.levels[hh];
         g_level = (int)hh;
         if (lv.nbgemv > 0)
-            LAUNCH("bwd_init", dev::k_bwd_init, dim3(lv.nbgemv), dim3(256), st, lv.nbgemv,
-                   L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.yvec, L.vec);
+            LAUNCH("bwd_init", dev::k_bwd_init, dim3(lv.nbgemv, L.nlanes), dim3(256), st, lv.nbgemv,
+                   L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.yvec, L.vec, L.lo);
         for (const auto &sp : lv.bsteps)
             if (sp.n > 0)
-                LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n), dim3(256), st, sp.n, L.tasks + 3 * sp.off, L.fd,
-                       L.arena, L.inv, L.vec, x);
+                LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
+                       L.fd, L.arena, L.inv, L.vec, x, L.lo);
     }
 }
 

@@ -69,6 +69,20 @@ static void quat_mat(const double *q, double *R) {
 
 }  // namespace
 
+// Speculative LM trials ("lambda lanes").  g2o's trial sequence inside an iteration is fixed in
+// advance: trial q uses lambda_q, and a rejection sets lambda_{q+1} = lambda_q * ni_q,
+// ni_{q+1} = 2 ni_q.  A round factors and solves the next nl trials in ONE batched pass: every
+// factor/solve launch carries the lanes in blockIdx.y, each lane with its own arena, panel inverses,
+// solve vectors and dx (DevPlan::lo strides), so the latency-bound panel chain is paid once for nl
+// trials.  Each lane's update then goes to a scratch copy of the state where its chi2 is evaluated;
+// the host replays the accept/reject sequence in trial order.  Every lane computes exactly the
+// numbers the sequential loop would (same kernels, same order of operations, no atomics).
+constexpr int kDefaultLanes = 1;   // measured: speculation does not pay at C2
+struct Lane {
+    DevProblem P;         // points / scales / tg / chi_* are the lane's scratch; the rest is shared
+    double *part = nullptr, *scal = nullptr;   // scal: [0] chi2 [1] scale [4..6] partial chi2
+};
+
 struct deftri_ctx {
     int device = 0;
     hipStream_t st = nullptr;
@@ -89,6 +103,13 @@ struct deftri_ctx {
     hipEvent_t ev[8]{};
     // map-level graph (deftri_arap_build_graph)
     GraphResult graph;
+    // speculative lambda lanes (see Lane)
+    int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES or kDefaultLanes)
+    std::vector<Lane> lanes;                // device buffers: per uploaded problem
+    DevPlan LB;                             // batched plan view: lanes' arenas / inverses / vectors / flags
+    double *dx_lanes = nullptr;             // [lane][ndof]
+    double *lane_pin = nullptr;             // pinned: [2t] chi2_new, [2t+1] dx.(lambda dx + b)
+    int *lane_ipin = nullptr;               // pinned: zero-pivot flag per lane
 };
 
 namespace {
@@ -133,6 +154,9 @@ void free_device(deftri_ctx *ctx) {
     ctx->allocs.clear();
     ctx->P = DevProblem();
     ctx->L = DevPlan();
+    ctx->lanes.clear();
+    ctx->LB = DevPlan();
+    ctx->dx_lanes = nullptr;
     ctx->init_state.clear();
     ctx->have = false;
 }
@@ -374,6 +398,94 @@ void pop_state(deftri_ctx *ctx) {
     hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
 }
 
+int lane_count(const deftri_ctx *ctx) {
+    int n = ctx->max_lanes;
+    if (n <= 0) {
+        n = kDefaultLanes;
+        if (const char *e = std::getenv("DEFTRI_LM_LANES")) n = std::atoi(e);
+    }
+    return std::max(1, std::min(kMaxLanes, n));
+}
+
+// allocate lanes up to `want` (fewer if they would not fit in half of the free HBM); returns the
+// number available (>= 1), or < 0 on an allocation error
+int ensure_lanes(deftri_ctx *ctx, int want) {
+    if ((int)ctx->lanes.size() >= want) return want;
+    const DevProblem &P0 = ctx->P;
+    const DevPlan &L0 = ctx->L;
+    const int64_t plan_doubles = L0.arena_size + L0.inv_size + 2 * L0.vec_size + L0.ndof;
+    const int64_t lane_doubles = 3 * (int64_t)P0.P + P0.S + 7 * (int64_t)P0.Q + P0.R + P0.D + P0.E + kRedParts + 8;
+    size_t free_b = 0, total_b = 0;
+    hipMemGetInfo(&free_b, &total_b);
+    // the batched buffers are re-allocated for the new lane count (the old ones stay until the
+    // problem is freed: lanes only grow)
+    int n = want;
+    while (n > 1 && 8.0 * (double)n * (double)(plan_doubles + lane_doubles) > 0.5 * (double)free_b) n--;
+    if (n <= (int)ctx->lanes.size()) return std::max(1, (int)ctx->lanes.size());
+    DevPlan LB = L0;
+    LB.nlanes = n;
+    LB.lo = LaneOff{};
+    LB.lo.arena = L0.arena_size; LB.lo.inv = L0.inv_size; LB.lo.vec = L0.vec_size; LB.lo.x = L0.ndof;
+    if (dalloc(ctx, &LB.arena, n * L0.arena_size) || dalloc(ctx, &LB.inv, n * std::max<int64_t>(L0.inv_size, 1)) ||
+        dalloc(ctx, &LB.vec, n * L0.vec_size) || dalloc(ctx, &LB.yvec, n * L0.vec_size) ||
+        dalloc(ctx, &LB.flag, n) || dalloc(ctx, &ctx->dx_lanes, n * L0.ndof))
+        return -1;
+    ctx->LB = LB;
+    while ((int)ctx->lanes.size() < n) {
+        Lane ln;
+        ln.P = P0;
+        ln.P.points_bak = ln.P.scales_bak = ln.P.tg_bak = nullptr;
+        if (dalloc(ctx, &ln.P.points, 3 * (int64_t)P0.P) || dalloc(ctx, &ln.P.scales, P0.S) ||
+            dalloc(ctx, &ln.P.tg, 7 * (int64_t)P0.Q) || dalloc(ctx, &ln.P.chi_rep, P0.R) ||
+            dalloc(ctx, &ln.P.chi_dep, P0.D) || dalloc(ctx, &ln.P.chi_arap, P0.E) ||
+            dalloc(ctx, &ln.part, kRedParts) || dalloc(ctx, &ln.scal, 8))
+            return -1;
+        ctx->lanes.push_back(ln);
+    }
+    return n;
+}
+
+// one speculative round of nl trials with lambdas lam[0..nl): setLambda + factor + solve batched
+// over the lanes, then per lane the update on a scratch copy of the state (skipped on a zero
+// pivot), computeActiveErrors + activeRobustChi2 there and the rho denominator; the scalars land
+// in the pinned slots (read after the caller's synchronize)
+void lanes_round(deftri_ctx *ctx, int nl, const double *lam, bool analytic) {
+    hipStream_t st = ctx->st;
+    const DevProblem &P = ctx->P;
+    DevPlan LB = ctx->LB;
+    LB.nlanes = nl;
+    for (int t = 0; t < nl; t++) LB.lo.lam[t] = lam[t];
+    hipMemsetAsync(LB.flag, 0, sizeof(int) * nl, st);
+    launch_scatter_lanes(LB, st);
+    launch_factor(LB, st, st, ctx->sync_ev, 64);
+    launch_solve(LB, ctx->L.b, ctx->dx_lanes, st);
+    for (int t = 0; t < nl; t++) {
+        Lane &ln = ctx->lanes[t];
+        const double *dx = ctx->dx_lanes + (int64_t)t * ctx->L.ndof;
+        hipMemcpyAsync(ln.P.points, P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st);
+        hipMemcpyAsync(ln.P.scales, P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st);
+        hipMemcpyAsync(ln.P.tg, P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st);
+        launch_update_state(ln.P, dx, st, LB.flag + t);
+        launch_linearize(ln.P, st, false, analytic);
+        launch_sum(P.R, ln.P.chi_rep, nullptr, 0, 0, ln.part, kRedParts, ln.scal + 4, st);
+        launch_sum(P.D, ln.P.chi_dep, nullptr, 0, 0, ln.part, kRedParts, ln.scal + 5, st);
+        launch_sum(P.E, ln.P.chi_arap, nullptr, 0, 0, ln.part, kRedParts, ln.scal + 6, st);
+        launch_sum(3, ln.scal + 4, nullptr, 0, 0, ln.part, 1, ln.scal, st);
+        launch_sum(ctx->S.ndof, dx, ctx->L.b, lam[t], 1, ln.part, kRedParts, ln.scal + 1, st);
+        hipMemcpyAsync(ctx->lane_pin + 2 * t, ln.scal, sizeof(double) * 2, hipMemcpyDeviceToHost, st);
+    }
+    hipMemcpyAsync(ctx->lane_ipin, LB.flag, sizeof(int) * nl, hipMemcpyDeviceToHost, st);
+}
+
+// the accepted lane's state becomes the optimizer's state
+void adopt_lane_state(deftri_ctx *ctx, int t) {
+    DevProblem &P = ctx->P;
+    const Lane &ln = ctx->lanes[t];
+    hipMemcpyAsync(P.points, ln.P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.scales, ln.P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, ctx->st);
+    hipMemcpyAsync(P.tg, ln.P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
+}
+
 float ev_ms(deftri_ctx *ctx, int a, int b) {
     float ms = 0;
     hipEventElapsedTime(&ms, ctx->ev[a], ctx->ev[b]);
@@ -420,6 +532,11 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
     }
     hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
     for (auto &e : ctx->sync_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (hipHostMalloc((void **)&ctx->lane_pin, 2 * kMaxLanes * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->lane_ipin, kMaxLanes * sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        deftri_ctx_destroy(ctx);
+        return DEFTRI_E_HIP;
+    }
     *out = ctx;
     return 0;
 }
@@ -431,6 +548,8 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     free_device(ctx);
     for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
     for (auto &e : ctx->sync_ev) if (e) hipEventDestroy(e);
+    if (ctx->lane_pin) hipHostFree(ctx->lane_pin);
+    if (ctx->lane_ipin) hipHostFree(ctx->lane_ipin);
     if (ctx->side) hipStreamDestroy(ctx->side);
     if (ctx->st) hipStreamDestroy(ctx->st);
     if (ctx->hpin) hipHostFree(ctx->hpin);
@@ -440,6 +559,12 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
 }
 
 const char *deftri_last_error(const deftri_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes) {
+    if (!ctx || lanes < 0 || lanes > kMaxLanes) return DEFTRI_E_ARG;
+    ctx->max_lanes = lanes;
+    return 0;
+}
 
 int64_t deftri_num_unknowns(const deftri_ctx *ctx) { return (ctx && ctx->have) ? ctx->S.ndof : -1; }
 
@@ -582,6 +707,12 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     eval_chi2_dev(ctx, false, analytic, 0);
     R.chi2_initial = read_scal(ctx, 0);
     double currentChi = R.chi2_initial;
+    int nlanes = std::min(lane_count(ctx), max_trials);
+    if (nlanes > 1) {
+        nlanes = ensure_lanes(ctx, nlanes);
+        if (nlanes < 1) return fail(ctx, DEFTRI_E_HIP, "lane allocation failed: " + ctx->err);
+    }
+    R.lanes = nlanes;
     for (it = 0; it < prm->n_iterations; it++) {
         hipEventRecord(ctx->ev[0], ctx->st);
         eval_chi2_dev(ctx, true, analytic, 0);              // computeActiveErrors + linearizeOplus
@@ -599,7 +730,48 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         }
         double rho = 0;
         int qmax = 0;
-        do {
+        if (nlanes > 1) {
+            // speculative rounds: lanes 0..nl-1 run trials qmax..qmax+nl-1 concurrently; the host then
+            // replays g2o's accept/reject sequence over their scalars in trial order
+            bool done = false;
+            while (!done) {
+                const int nl = std::min(nlanes, max_trials - qmax);
+                double lam[kMaxLanes];
+                double lc = lambda, nc = ni;
+                for (int t = 0; t < nl; t++) { lam[t] = lc; lc *= nc; nc *= 2; }
+                hipEventRecord(ctx->ev[2], ctx->st);
+                lanes_round(ctx, nl, lam, analytic);
+                hipEventRecord(ctx->ev[5], ctx->st);
+                HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a round
+                t_fac += ev_ms(ctx, 2, 5);
+                R.trials_executed += nl;
+                int acc = -1;
+                for (int t = 0; t < nl && !done; t++) {
+                    const bool ok2 = ctx->lane_ipin[t] == 0;
+                    double tempChi = ok2 ? ctx->lane_pin[2 * t] : std::numeric_limits<double>::max();
+                    rho = (currentChi - tempChi);
+                    double scale = ctx->lane_pin[2 * t + 1] + 1e-3;
+                    rho /= scale;
+                    R.trials_total++;
+                    if (rho > 0 && std::isfinite(tempChi)) {
+                        double alpha = 1. - std::pow((2 * rho - 1), 3);
+                        alpha = std::min(alpha, 2. / 3.);
+                        double scaleFactor = std::max(1. / 3., alpha);
+                        lambda *= scaleFactor;
+                        ni = 2;
+                        currentChi = tempChi;
+                        acc = t;
+                    } else {
+                        lambda *= ni;
+                        ni *= 2;
+                        R.trials_rejected++;
+                    }
+                    qmax++;
+                    if (!(rho < 0 && qmax < max_trials)) done = true;
+                }
+                if (acc >= 0) adopt_lane_state(ctx, acc);
+            }
+        } else do {
             push_state(ctx);
             hipEventRecord(ctx->ev[2], ctx->st);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
@@ -623,6 +795,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             double scale = sc[1] + 1e-3;
             rho /= scale;
             R.trials_total++;
+            R.trials_executed++;
             if (rho > 0 && std::isfinite(tempChi)) {
                 double alpha = 1. - std::pow((2 * rho - 1), 3);
                 alpha = std::min(alpha, 2. / 3.);

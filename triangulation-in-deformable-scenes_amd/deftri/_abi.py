@@ -49,7 +49,7 @@ class Report(C.Structure):
         ("ms_total", f64), ("ms_linearize", f64), ("ms_factor", f64), ("ms_solve", f64),
         ("ms_update", f64),
         ("n_unknowns", i64), ("nnz_factor", i64), ("factor_flops", f64), ("n_fronts", i32),
-        ("n_levels", i32),
+        ("n_levels", i32), ("lanes", i32), ("trials_executed", i32),
     ]
 
     def as_dict(self):
@@ -64,6 +64,7 @@ class Report(C.Structure):
             "ms_factor": self.ms_factor, "ms_solve": self.ms_solve, "ms_update": self.ms_update,
             "n_unknowns": self.n_unknowns, "nnz_factor": self.nnz_factor,
             "factor_flops": self.factor_flops, "n_fronts": self.n_fronts, "n_levels": self.n_levels,
+            "lanes": self.lanes, "trials_executed": self.trials_executed,
         }
 
 

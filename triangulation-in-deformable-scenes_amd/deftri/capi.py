@@ -43,6 +43,7 @@ def load():
         "deftri_debug_plan_solve": (C.c_int, [C.c_void_p, P(C.c_double), C.c_double, P(C.c_double),
                                               P(C.c_double), C.c_int64]),
         "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
+        "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_download": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double)]),
         "deftri_reset_state": (C.c_int, [C.c_void_p]),
         "deftri_eval_chi2": (C.c_int, [C.c_void_p, P(C.c_double)]),
@@ -88,7 +89,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -156,6 +157,10 @@ class Context:
         x = np.zeros_like(r)
         self._check(self.lib.deftri_debug_plan_solve(self.h, _dp(H), float(lam), _dp(r), _dp(x), len(r)))
         return x
+
+    def set_lm_lanes(self, lanes):
+        """Speculative lambda lanes (0 = default, 1 = sequential trials); results are identical."""
+        self._check(self.lib.deftri_set_lm_lanes(self.h, int(lanes)))
 
     def solve_lm(self, n_iterations=10, analytic=True, tau=1e-5, max_trials=10, user_lambda=0.0, verbose=False):
         prm = _abi.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=user_lambda,
