@@ -208,7 +208,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
                          int32_t max_stats, int32_t *n_stats);
 
 /* sizeof() of the ABI structs for binding checks: 0 deftri_problem_desc, 1 deftri_lm_params,
-   2 deftri_report, 3 deftri_keyframe, 4 deftri_map, 5 deftri_ba_desc. */
+   2 deftri_report, 3 deftri_keyframe, 4 deftri_map, 5 deftri_ba_desc, 6 deftri_pixels_error. */
 int64_t deftri_sizeof(int32_t which);
 
 /* ---- map-level API (Modules/Optimization/g2oBundleAdjustment.h:56-60) ---------------- */
@@ -246,6 +246,19 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
                              double global_weight, double arap_weight, double alpha,
                              double beta, float depth_error, int32_t n_iterations,
                              double *optimization_update, deftri_report *report);
+
+/* PixelsError (Modules/Utils/CommonTypes.h:23-30). */
+typedef struct deftri_pixels_error {
+    double avgc1, avgc2, avg;      /* mean |obs - proj| per camera (last pair), their average */
+    double desvc1, desvc2, desv;   /* RMS |obs - proj| per camera (last pair), their average */
+} deftri_pixels_error;
+
+/* calculatePixelsStandDev(Map, PixelsError&) (Modules/Utils/Geometry.cc:370-498) on the device:
+   for every keyframe pair (k1, k2 > k1 in map order; camera 1 = k2, camera 2 = k1) and every slot
+   whose MapPoints both exist and are observed, the fp32 homogeneous projection error; per pair the
+   reference's formulas (nMatches and the mean accumulators carry across pairs, the squared sums
+   do not; the values of the last pair are returned).  Reads the map's fp32 positions. */
+int deftri_pixels_stand_dev(deftri_ctx *ctx, const deftri_map *map, deftri_pixels_error *out);
 
 /* Build the flattened graph only (no solve): the arrays are owned by the context and stay
    valid until the next call on it.  Used by the parity tests to compare indexing. */

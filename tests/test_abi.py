@@ -35,6 +35,7 @@ def test_abi_version_and_struct_sizes():
     assert lib.deftri_sizeof(3) == C.sizeof(_abi.KeyFrameC)
     assert lib.deftri_sizeof(4) == C.sizeof(_abi.MapC)
     assert lib.deftri_sizeof(5) == C.sizeof(_abi.BADesc)
+    assert lib.deftri_sizeof(6) == C.sizeof(_abi.PixelsError)
 
 
 def test_ba_context_needs_a_device():

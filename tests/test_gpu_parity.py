@@ -281,3 +281,24 @@ def test_speculative_lanes_full_size(gpu_ctx):
     assert r3["chi2_iter"] == r1["chi2_iter"] and r3["trials_iter"] == r1["trials_iter"]
     for a, b in zip(s3, s1):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("case", ["golden", "multi_view", "full_size"])
+def test_pixels_stand_dev_device(gpu_ctx, golden_cases, case):
+    """calculatePixelsStandDev on the device (deftri_pixels_stand_dev) vs the host restatement
+    (deftri/metrics.py): same matches, same fp32 homogeneous projection; the sums differ only in
+    order and ocml vs glibc fp32 transcendentals (an ulp of a pixel coordinate on some matches):
+    rel 1e-6.  Multi-view covers the reference's carried mean accumulators across pairs."""
+    import importlib, sys
+    if case == "golden":
+        sys.path.insert(0, str(GOLDEN))
+        m, _, _ = importlib.import_module("make_golden").scene("sim_default")
+    elif case == "multi_view":
+        m, _ = sim.simulate_multi_view(n=500, k=4, seed=9)
+    else:
+        m, _ = sim.simulate_two_view(n=100000, seed=1, scale_scene=True, compact=True)
+    dev = gpu_ctx.pixels_stand_dev(m)
+    ref = metrics.pixels_stand_dev(m)
+    for k in ("avgc1", "avgc2", "avg", "desvc1", "desvc2", "desv"):
+        assert dev[k] == pytest.approx(ref[k], rel=1e-6), k
+    assert dev["desv"] > 0

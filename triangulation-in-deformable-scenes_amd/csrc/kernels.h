@@ -111,6 +111,10 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, 
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
                 double *out, hipStream_t st);
 void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st);
+// calculatePixelsStandDev partial sums (metrics.hip): 8 doubles per 256-match block
+void launch_pixel_partials(int nblk, const int32_t *blk_first, const int32_t *blk_last, const int32_t *blk_pair,
+                           const int32_t *pair_cams, const float *cams, const float *pts, const float *obs,
+                           double *part, hipStream_t st);
 void launch_hmul(const DevPlan &L, const int64_t *brow_dof, const int64_t *bcol_dof, const double *x, double *y,
                  int64_t n, hipStream_t st);
 

@@ -653,6 +653,7 @@ int64_t deftri_sizeof(int32_t which) {
         case 3: return (int64_t)sizeof(deftri_keyframe);
         case 4: return (int64_t)sizeof(deftri_map);
         case 5: return (int64_t)sizeof(deftri_ba_desc);
+        case 6: return (int64_t)sizeof(deftri_pixels_error);
         default: return -1;
     }
 }
@@ -824,6 +825,98 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     R.lambda_final = lambda;
     R.ms_linearize = t_lin; R.ms_factor = t_fac; R.ms_solve = t_sol; R.ms_update = t_upd;
     R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return 0;
+}
+
+int deftri_pixels_stand_dev(deftri_ctx *ctx, const deftri_map *map, deftri_pixels_error *out) {
+    if (!ctx || !map || !out || map->n_keyframes < 0 || (map->n_keyframes > 0 && !map->keyframes)) return DEFTRI_E_ARG;
+    if (ctx->device < 0) return fail(ctx, DEFTRI_E_NODEVICE, "host-only context");
+    hipSetDevice(ctx->device);
+    const int K = map->n_keyframes;
+    // per keyframe: R (fp32, Eigen toRotationMatrix of the fp32 unit quaternion), t, kb8
+    std::vector<float> cams(20 * (size_t)std::max(K, 1));
+    for (int k = 0; k < K; k++) {
+        const deftri_keyframe &kf = map->keyframes[k];
+        float x = (float)kf.pose[0], y = (float)kf.pose[1], z = (float)kf.pose[2], w = (float)kf.pose[3];
+        float tx = 2 * x, ty = 2 * y, tz = 2 * z, twx = tx * w, twy = ty * w, twz = tz * w;
+        float txx = tx * x, txy = ty * x, txz = tz * x, tyy = ty * y, tyz = tz * y, tzz = tz * z;
+        float *c = &cams[20 * (size_t)k];
+        c[0] = 1 - (tyy + tzz); c[1] = txy - twz;       c[2] = txz + twy;
+        c[3] = txy + twz;       c[4] = 1 - (txx + tzz); c[5] = tyz - twx;
+        c[6] = txz - twy;       c[7] = tyz + twx;       c[8] = 1 - (txx + tyy);
+        for (int q = 0; q < 3; q++) c[9 + q] = (float)kf.pose[4 + q];
+        for (int q = 0; q < 8; q++) c[12 + q] = kf.kb8[q];
+    }
+    // matches of each pair in the reference's loop order (:386-416)
+    std::vector<float> pts, obs;
+    std::vector<int32_t> pair_cams, pair_first{0};
+    for (int a = 0; a < K; a++)
+        for (int b = a + 1; b < K; b++) {
+            const deftri_keyframe &k1 = map->keyframes[b], &k2 = map->keyframes[a];
+            pair_cams.push_back(b); pair_cams.push_back(a);
+            const int n = std::min(k1.n_slots, k2.n_slots);
+            for (int i = 0; i < n; i++) {
+                if (k1.point_id[i] < 0 || k2.point_id[i] < 0) continue;
+                const int o1 = k1.obs_index[i], o2 = k2.obs_index[i];
+                if (o1 < 0 || o2 < 0) continue;
+                if (o1 >= k1.n_obs || o2 >= k2.n_obs) return fail(ctx, DEFTRI_E_ARG, "observation index out of range");
+                for (int q = 0; q < 3; q++) pts.push_back(k1.point_pos[3 * (int64_t)i + q]);
+                for (int q = 0; q < 3; q++) pts.push_back(k2.point_pos[3 * (int64_t)i + q]);
+                obs.push_back(k1.kp_uv[2 * (int64_t)o1]); obs.push_back(k1.kp_uv[2 * (int64_t)o1 + 1]);
+                obs.push_back(k2.kp_uv[2 * (int64_t)o2]); obs.push_back(k2.kp_uv[2 * (int64_t)o2 + 1]);
+            }
+            pair_first.push_back((int32_t)(pts.size() / 6));
+        }
+    const int npair = (int)pair_cams.size() / 2;
+    std::vector<int32_t> bf, bl, bp;
+    for (int p = 0; p < npair; p++)
+        for (int32_t s = pair_first[p]; s < pair_first[p + 1]; s += 256) {
+            bf.push_back(s); bl.push_back(std::min(s + 256, pair_first[p + 1])); bp.push_back(p);
+        }
+    const int nblk = (int)bf.size();
+    std::vector<double> part(8 * (size_t)std::max(nblk, 1), 0.0);
+    if (nblk > 0) {
+        // scratch buffers of this call (one allocation, freed before returning)
+        const size_t nb_i = 3 * (size_t)nblk + 2 * (size_t)npair, nb_f = cams.size() + pts.size() + obs.size();
+        const size_t bytes = 8 * part.size() + 4 * nb_f + 4 * nb_i + 64;
+        char *dbuf = nullptr;
+        HIPOK(hipMalloc(&dbuf, bytes));
+        double *d_part = (double *)dbuf;
+        float *d_cams = (float *)(d_part + part.size());
+        float *d_pts = d_cams + cams.size(), *d_obs = d_pts + pts.size();
+        int32_t *d_bf = (int32_t *)(d_obs + obs.size()), *d_bl = d_bf + nblk, *d_bp = d_bl + nblk, *d_pc = d_bp + nblk;
+        hipMemcpyAsync(d_cams, cams.data(), 4 * cams.size(), hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_pts, pts.data(), 4 * pts.size(), hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_obs, obs.data(), 4 * obs.size(), hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_bf, bf.data(), 4 * (size_t)nblk, hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_bl, bl.data(), 4 * (size_t)nblk, hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_bp, bp.data(), 4 * (size_t)nblk, hipMemcpyHostToDevice, ctx->st);
+        hipMemcpyAsync(d_pc, pair_cams.data(), 4 * pair_cams.size(), hipMemcpyHostToDevice, ctx->st);
+        launch_pixel_partials(nblk, d_bf, d_bl, d_bp, d_pc, d_cams, d_pts, d_obs, d_part, ctx->st);
+        hipMemcpyAsync(part.data(), d_part, 8 * part.size(), hipMemcpyDeviceToHost, ctx->st);
+        hipError_t e = hipStreamSynchronize(ctx->st);
+        hipFree(dbuf);
+        if (e != hipSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("pixels_stand_dev: ") + hipGetErrorString(e));
+    }
+    // the reference's per-pair formulas (:454-485); meanUV and nMatches carry over pairs
+    double mUV1[2] = {0, 0}, mUV2[2] = {0, 0};
+    double mC1 = 0, mC2 = 0, dC1 = 0, dC2 = 0;
+    size_t nMatches = 0;
+    for (int p = 0, blk = 0; p < npair; p++) {
+        double sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (; blk < nblk && bp[blk] == p; blk++)
+            for (int q = 0; q < 8; q++) sum[q] += part[8 * (size_t)blk + q];
+        nMatches += (size_t)(pair_first[p + 1] - pair_first[p]);
+        const double nm = (double)nMatches;
+        for (int q = 0; q < 2; q++) { mUV1[q] += sum[q]; mUV2[q] += sum[4 + q]; }
+        for (int q = 0; q < 2; q++) { mUV1[q] /= nm; mUV2[q] /= nm; }
+        mC1 = (mUV1[0] + mUV1[1]) / 2.0;
+        mC2 = (mUV2[0] + mUV2[1]) / 2.0;
+        dC1 = (std::sqrt(sum[2] / nm) + std::sqrt(sum[3] / nm)) / 2.0;
+        dC2 = (std::sqrt(sum[6] / nm) + std::sqrt(sum[7] / nm)) / 2.0;
+    }
+    out->avgc1 = mC1; out->avgc2 = mC2; out->avg = (mC1 + mC2) / 2.0;
+    out->desvc1 = dC1; out->desvc2 = dC2; out->desv = (dC1 + dC2) / 2.0;
     return 0;
 }
 

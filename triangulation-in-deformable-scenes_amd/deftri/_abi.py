@@ -68,6 +68,13 @@ class Report(C.Structure):
         }
 
 
+class PixelsError(C.Structure):
+    _fields_ = [("avgc1", f64), ("avgc2", f64), ("avg", f64), ("desvc1", f64), ("desvc2", f64), ("desv", f64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class KeyFrameC(C.Structure):
     _fields_ = [
         ("id", i64), ("pose", f64 * 7), ("kb8", f32 * 8), ("n_scales", i32),

@@ -44,6 +44,7 @@ def load():
                                               P(C.c_double), C.c_int64]),
         "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
         "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
         "deftri_download": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double)]),
         "deftri_reset_state": (C.c_int, [C.c_void_p]),
         "deftri_eval_chi2": (C.c_int, [C.c_void_p, P(C.c_double)]),
@@ -89,7 +90,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_pixels_stand_dev", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -216,6 +217,13 @@ class Context:
         self._check(self.lib.deftri_arap_build_graph(self.h, C.byref(mc), float(rep_weight), float(arap_weight),
                                                      C.c_float(depth_error), C.byref(out)))
         return Problem.from_desc(out.contents)
+
+    def pixels_stand_dev(self, m):
+        """calculatePixelsStandDev (Geometry.cc:370-498) of a Map on the device."""
+        mc, keep = m.to_c()
+        out = _abi.PixelsError()
+        self._check(self.lib.deftri_pixels_stand_dev(self.h, C.byref(mc), C.byref(out)))
+        return out.as_dict()
 
     def arap_optimization(self, m, rep_weight, global_weight, arap_weight, alpha, beta, depth_error,
                           n_iterations, want_update=True):

@@ -11,24 +11,42 @@ import numpy as np
 from .sim import kb8_project
 
 
+def _pose_matrix_f32(kf):
+    """Sophus::SE3f::matrix(): Eigen toRotationMatrix of the fp32 unit quaternion, in fp32."""
+    a = kf.pose.as7()
+    x, y, z, w = (np.float32(v) for v in a[:4])
+    two = np.float32(2)
+    tx, ty, tz = two * x, two * y, two * z
+    twx, twy, twz = tx * w, ty * w, tz * w
+    txx, txy, txz = tx * x, ty * x, tz * x
+    tyy, tyz, tzz = ty * y, tz * y, tz * z
+    one = np.float32(1)
+    R = np.array([[one - (tyy + tzz), txy - twz, txz + twy],
+                  [txy + twz, one - (txx + tzz), tyz - twx],
+                  [txz - twy, tyz + twx, one - (txx + tyy)]], np.float32)
+    return R, np.asarray(a[4:7], np.float64).astype(np.float32)
+
+
 def _project_h(kf, p3w):
-    """T1w.matrix() * [p;1] in fp32, then KB8 project (Geometry.cc:423-431)."""
-    T = np.eye(4, dtype=np.float32)
-    T[:3, :3] = kf.pose.R
-    T[:3, 3] = kf.pose.t
-    ph = np.concatenate([p3w.astype(np.float32), np.ones((len(p3w), 1), np.float32)], 1)
-    pc = (ph @ T.T)[:, :3].astype(np.float32)
-    return kb8_project(kf.kb8, pc)
+    """T1w.matrix() * [p;1] in fp32, column by column as Eigen's lazy product (no FMA), then KB8
+    project (Geometry.cc:423-431)."""
+    R, t = _pose_matrix_f32(kf)
+    p = np.asarray(p3w, np.float32)
+    pc = np.stack([((R[r, 0] * p[:, 0] + R[r, 1] * p[:, 1]) + R[r, 2] * p[:, 2]) + t[r] for r in range(3)], 1)
+    return kb8_project(kf.kb8, pc.astype(np.float32))
 
 
 def pixels_stand_dev(m):
+    """Host restatement (tests, oracle side).  Like the reference, nMatches and the mean
+    accumulators carry over pairs (:454-456 divide the running sums in place), the squared sums do
+    not, and the values of the last pair are returned (0 when the map has fewer than two KFs)."""
     order = m.kf_order()
     n_matches = 0
-    out = None
+    mean1 = np.zeros(2); mean2 = np.zeros(2)
+    out = {"avgc1": 0.0, "avgc2": 0.0, "desvc1": 0.0, "desvc2": 0.0}
     for a in range(len(order)):
         for b in range(a + 1, len(order)):
             kf1, kf2 = m.keyframes[order[b]], m.keyframes[order[a]]
-            e1, e2 = [], []
             p1s, p2s, o1s, o2s = [], [], [], []
             for i in range(min(kf1.n_slots, kf2.n_slots)):
                 mp1, mp2 = kf1.map_points[i], kf2.map_points[i]
@@ -40,24 +58,22 @@ def pixels_stand_dev(m):
                     continue
                 p1s.append(mp1.position); p2s.append(mp2.position)
                 o1s.append(kf1.keypoints[i1]); o2s.append(kf2.keypoints[i2])
-            if not p1s:
-                continue
-            uv1 = _project_h(kf1, np.array(p1s)).astype(np.float64)
-            uv2 = _project_h(kf2, np.array(p2s)).astype(np.float64)
-            err1 = np.abs(np.array(o1s, np.float64) - uv1)
-            err2 = np.abs(np.array(o2s, np.float64) - uv2)
+            err1 = np.zeros((0, 2)); err2 = np.zeros((0, 2))
+            if p1s:
+                uv1 = _project_h(kf1, np.array(p1s)).astype(np.float64)
+                uv2 = _project_h(kf2, np.array(p2s)).astype(np.float64)
+                err1 = np.abs(np.array(o1s, np.float64) - uv1)
+                err2 = np.abs(np.array(o2s, np.float64) - uv2)
             n_matches += len(p1s)
-            mean1 = err1.sum(0) / n_matches
-            mean2 = err2.sum(0) / n_matches
-            var1 = (err1 ** 2).sum(0) / n_matches
-            var2 = (err2 ** 2).sum(0) / n_matches
-            sd1, sd2 = np.sqrt(var1), np.sqrt(var2)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                mean1 = (mean1 + err1.sum(0)) / n_matches
+                mean2 = (mean2 + err2.sum(0)) / n_matches
+                sd1 = np.sqrt((err1 ** 2).sum(0) / n_matches)
+                sd2 = np.sqrt((err2 ** 2).sum(0) / n_matches)
             out = {
                 "avgc1": (mean1[0] + mean1[1]) / 2.0, "avgc2": (mean2[0] + mean2[1]) / 2.0,
                 "desvc1": (sd1[0] + sd1[1]) / 2.0, "desvc2": (sd2[0] + sd2[1]) / 2.0,
             }
-    if out is None:
-        return {"avgc1": 0.0, "avgc2": 0.0, "avg": 0.0, "desvc1": 0.0, "desvc2": 0.0, "desv": 0.0}
     out["avg"] = (out["avgc1"] + out["avgc2"]) / 2.0
     out["desv"] = (out["desvc1"] + out["desvc2"]) / 2.0
     return out

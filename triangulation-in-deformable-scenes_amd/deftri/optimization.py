@@ -56,7 +56,9 @@ def outerObjective(x, pMap, settings, arap_fn=None, device=0):
     fn = arap_fn or (lambda m, *a: arapOptimization(m, *a, device=device))
     fn(clone, float(x[0]), float(x[1]), float(x[2]), settings.alpha, settings.beta, settings.depth_sigma,
        settings.n_iterations)
-    pe = metrics.pixels_stand_dev(clone)
+    # calculatePixelsStandDev: on the device (deftri_pixels_stand_dev); the host restatement only
+    # when a test substitutes the solver (arap_fn)
+    pe = metrics.pixels_stand_dev(clone) if arap_fn is not None else _ctx(device).pixels_stand_dev(clone)
 
     def lg2(v):
         return math.log(v) ** 2 if v > 0 else math.inf
