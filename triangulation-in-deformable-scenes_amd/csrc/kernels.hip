@@ -476,8 +476,8 @@ __device__ __forceinline__ void wave_sync() {
 //   in : S[r][c] (c <= r) = A (rows/cols >= kb padded with the identity), S[c][r] (r > c) = 0
 //   out: S[r][c] (c < r) = L, S[r][r] = D, S[c][r] (r > c) = X[r][c], X = L^{-1}
 // Four 16-column sub-panels K.  Per sub-panel:
-//   F  the 16x16 diagonal block: thread (r, c) owns one element; 16 right-looking steps, one
-//      barrier each (A[r][c] -= l_r a_c, X[r][c] -= l_r X[j][c]);
+//   F  the 16x16 diagonal block and its inverse in the registers of wave 0: 16 right-looking
+//      steps with cross-lane broadcasts, no barrier (A[r][c] -= l_r a_c, X[r][c] -= l_r X[j][c]);
 //   X  (waves nrt..) finishes the inverse blocks of block row K: X_KJ = -X_KK T_KJ, J < K;
 //   TR (waves 0..nrt-1) the sub-panel TRSM below it: L_IK = A_IK X_KK^T D_K^{-1};
 //   U  the trailing Schur update on the lower triangle and the inverse accumulators
@@ -487,7 +487,6 @@ constexpr int DP = 65;
 __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int er = tid & 15, ec = tid >> 4;                    // element of the 16x16 block
     // rows/cols >= kb are identity padding: sub-blocks past nsub and pivot steps past kb are no-ops
     const int nsub = (kb + 15) >> 4;
 #ifdef DEFTRI_DIAG_TIMING
@@ -497,50 +496,50 @@ __device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
     for (int K = 0; K < nsub; K++) {
         const int j0 = 16 * K;
         const int jend = min(16, kb - j0);
-        // ---- F: factor the diagonal block + its inverse, element per thread, two pivot columns per
-        //      step (one barrier per pair): with l_x0 d0 = a_x0 and a'_x1 = a_x1 - a_x0 l10,
-        //      A[r][c] -= a_r0 a_c0 / d0 + a'_r1 a'_c1 / d1,  X[r][:] -= l_r0 X[j][:] + l_r1 X'[j+1][:]
-        int j = 0;
-        for (; j + 1 < jend; j += 2) {
-            const double a00 = S[j0 + j][j0 + j], a10 = S[j0 + j + 1][j0 + j], a11 = S[j0 + j + 1][j0 + j + 1];
-            const double ar0 = S[j0 + er][j0 + j], ar1 = S[j0 + er][j0 + j + 1];
-            const double ac0 = S[j0 + ec][j0 + j], ac1 = S[j0 + ec][j0 + j + 1];
-            const double xj = (ec == j) ? 1.0 : (ec < j ? S[j0 + ec][j0 + j] : 0.0);          // X[j][c]
-            const double xj1o = (ec < j) ? S[j0 + ec][j0 + j + 1] : 0.0;                      // X[j+1][c] (old)
-            const double rd0 = rcp_d(a00);
-            const double l10 = a10 * rd0;
-            const double d1 = a11 - l10 * a10;
-            const double rd1 = rcp_d(d1);
-            const double lr0 = ar0 * rd0;
-            const double ar1p = ar1 - ar0 * l10;
-            const double lr1 = ar1p * rd1;
-            const double xj1 = (ec == j + 1) ? 1.0 : (ec < j ? xj1o - l10 * xj : (ec == j ? -l10 : 0.0));  // X'[j+1][c]
-            if (er > j + 1) {
-                if (ec > j + 1 && er >= ec) S[j0 + er][j0 + ec] -= ar0 * ac0 * rd0 + ar1p * (ac1 - ac0 * l10) * rd1;
-                if (ec <= j + 1) S[j0 + ec][j0 + er] -= lr0 * xj + lr1 * xj1;
+        // ---- F: factor the diagonal block + its inverse in the registers of wave 0 (no barrier on
+        //      the pivot chain).  Lane (r, g) = (lane & 15, lane >> 4) holds A[r][c] and X[r][c]
+        //      for c = g, g+4, g+8, g+12 (both triangles of A, so row j is A[j][c] in lanes
+        //      (j, g)); right-looking step j: d = A[j][j] (readlane), l_r = A[r][j] / d,
+        //      A[r][c] -= l_r A[j][c] (r, c > j), X[r][c] -= l_r X[j][c] (r > j >= c).
+        if (wv == 0) {
+            const int r = lane & 15, g = lane >> 4, rowbase = lane & 48;
+            double a[4], x[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = g + 4 * q;
+                a[q] = (c <= r) ? S[j0 + r][j0 + c] : S[j0 + c][j0 + r];
+                x[q] = (c == r) ? 1.0 : 0.0;
             }
-            if (tid == 0 && (a00 == 0.0 || d1 == 0.0)) atomicOr(flag, 1);
-            __syncthreads();
-            if (ec == j && er > j) S[j0 + er][j0 + j] = lr0;                                   // L[:, j]
-            if (ec == j + 1 && er > j + 1) S[j0 + er][j0 + j + 1] = lr1;                       // L[:, j+1]
-            if (ec == j + 1 && er == j + 1) S[j0 + j + 1][j0 + j + 1] = d1;                    // D[j+1]
-            if (er == j + 1 && ec <= j) S[j0 + ec][j0 + j + 1] = xj1;                          // X[j+1][c]
-        }
-        for (; j < jend; j++) {
-            const double d = S[j0 + j][j0 + j];
-            const double ar = S[j0 + er][j0 + j], ac = S[j0 + ec][j0 + j];
-            const double rd = rcp_d(d);
-            const double lr = ar * rd;
-            if (er > j) {
-                if (ec > j && er >= ec) S[j0 + er][j0 + ec] -= lr * ac;                  // A -= l_r d l_c
-                if (ec <= j) {
-                    const double xjc = (ec == j) ? 1.0 : S[j0 + ec][j0 + j];             // X[j][c]
-                    S[j0 + ec][j0 + er] -= lr * xjc;                                      // X[r][c]
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                if (j < jend) {
+                    const double d = readlane_d(a[j >> 2], j + 16 * (j & 3));          // A[j][j]
+                    const double arj = __shfl(a[j >> 2], r + 16 * (j & 3));            // A[r][j]
+                    double ajc[4], xjc[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        ajc[q] = __shfl(a[q], rowbase | j);                            // A[j][c_q]
+                        xjc[q] = __shfl(x[q], rowbase | j);                            // X[j][c_q]
+                    }
+                    const double lr = arj * rcp_d(d);
+                    if (r > j) {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const int c = g + 4 * q;
+                            if (c > j) a[q] -= lr * ajc[q];
+                            else x[q] -= lr * xjc[q];
+                            if (c == j) a[q] = lr;                                     // L[r][j]
+                        }
+                    }
+                    if (lane == 0 && d == 0.0) atomicOr(flag, 1);
                 }
             }
-            if (tid == 0 && d == 0.0) atomicOr(flag, 1);
-            __syncthreads();
-            if (ec == j && er > j) S[j0 + er][j0 + j] = lr;                              // scale column j
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int c = g + 4 * q;
+                if (c <= r) S[j0 + r][j0 + c] = a[q];                                  // L (c < r), D (c == r)
+                if (c < r) S[j0 + c][j0 + r] = x[q];                                   // X[r][c]
+            }
         }
         __syncthreads();
 #ifdef DEFTRI_DIAG_TIMING
