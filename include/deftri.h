@@ -157,14 +157,15 @@ int deftri_abi_version(void);
 int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc);
 /* Run g2o-semantics Levenberg–Marquardt on the device. */
 int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *params, deftri_report *report);
-/* Speculative lambda lanes (0 = default: env DEFTRI_LM_LANES, else 1; 1 = strictly sequential
+/* Speculative lambda lanes (0 = default: env DEFTRI_LM_LANES, else 2 below 3e10 flops per
+   factorization (latency-bound) and 1 above; 1 = strictly sequential
    trials; at most 8).  g2o's trials within an iteration use a lambda sequence fixed in advance
    (reject: lambda *= ni, ni *= 2), so up to `lanes` consecutive trials are factored and solved in
    one batched pass (the lane is the second grid dimension of every factor/solve launch), each in
    its own arena and scratch state, and the accept/reject decisions are replayed in trial order:
    results are bit-identical to lanes = 1.  Fewer lanes are used when their buffers would not fit
-   in half of the free device memory.  Pays off when the factorization is latency-bound (small
-   problems); at C2 a 3-lane round costs 2.1 trials. */
+   in half of the free device memory.  Pays off when the factorization is latency-bound (1k-30k
+   correspondences: 11-24% per iteration); at C2 a 3-lane round costs 2.1 trials. */
 int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes);
 /* Copy the current state back: points [P*3], scales [S], tg [Q*7] (any may be NULL). */
 int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg);

@@ -985,11 +985,16 @@ __global__ void __launch_bounds__(256) k_fwd_step(int ntask, const int32_t *__re
     if (part == 0 && r < m) v[r] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-// backward init (front f, own columns c0..c0+15): w_c = y_c / d_c - sum_{i >= s} L[i][c] x[rows[i]]
+// backward init (front f, own columns c0..c0+15): w_c = y_c / d_c - sum_{i >= s} L[i][c] x[rows[i]].
+// The boundary solution x_B (gathered through rows[]) is staged once in LDS for the task's 16
+// columns; wave w accumulates its 4 columns together (4 independent coalesced column streams).
+// Per column the lane-strided order and the shuffle tree are the single-column ones.
+constexpr int kBwdStage = 4096;
 __global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
                                                   const double *__restrict__ arena, const double *__restrict__ x,
                                                   const double *__restrict__ yvec, double *__restrict__ vec,
                                                   const LaneOff lo) {
+    __shared__ double xb[kBwdStage];
     int t = blockIdx.x;
     if (t >= ntask) return;
     arena += blockIdx.y * lo.arena; x += blockIdx.y * lo.x; yvec += blockIdx.y * lo.vec; vec += blockIdx.y * lo.vec;
@@ -998,14 +1003,45 @@ __global__ void __launch_bounds__(256) k_bwd_init(int ntask, const int32_t *__re
     const double *F = arena + fd.arena_off[f];
     const int32_t *rows = fd.rows + fd.rows_off[f];
     int64_t vo = fd.vec_off[f];
-    int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    int c1 = min(c0 + kBwdCols, s);
-    for (int c = c0 + wv; c < c1; c += 4) {
-        const double *col = F + (int64_t)c * m;
-        double acc = 0.0;
-        for (int i = s + lane; i < m; i += 64) acc += col[i] * x[rows[i]];
-        for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off);
-        if (lane == 0) vec[vo + c] = yvec[vo + c] / col[c] - acc;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c1 = min(c0 + kBwdCols, s);
+    const int u = m - s;
+    const bool staged = u <= kBwdStage;
+    if (staged) {
+        for (int i = threadIdx.x; i < u; i += 256) xb[i] = x[rows[s + i]];
+        __syncthreads();
+    }
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    const double *col[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int c = c0 + wv + 4 * k;
+        ok[k] = c < c1;
+        col[k] = F + (int64_t)(ok[k] ? c : c0) * m + s;
+    }
+    // 4 row strides per round: 16 column loads in flight per lane, accumulated in row order
+    for (int i0 = lane; i0 < u; i0 += 256) {
+        double xv[4], lv[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int i = i0 + 64 * j;
+            const bool in = i < u;
+            xv[j] = in ? (staged ? xb[i] : x[rows[s + i]]) : 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) lv[k][j] = (in && ok[k]) ? col[k][i] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (i0 + 64 * j < u && ok[k]) acc[k] += lv[k][j] * xv[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_down(acc[k], off);
+        const int c = c0 + wv + 4 * k;
+        if (lane == 0 && ok[k]) vec[vo + c] = yvec[vo + c] / F[(int64_t)c * m + c] - acc[k];
     }
 }
 

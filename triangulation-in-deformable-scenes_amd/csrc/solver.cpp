@@ -77,7 +77,11 @@ static void quat_mat(const double *q, double *R) {
 // trials.  Each lane's update then goes to a scratch copy of the state where its chi2 is evaluated;
 // the host replays the accept/reject sequence in trial order.  Every lane computes exactly the
 // numbers the sequential loop would (same kernels, same order of operations, no atomics).
-constexpr int kDefaultLanes = 1;   // measured: speculation does not pay at C2
+// default lanes: 2 while a factorization is latency-bound (measured ms/iteration over 25 LM
+// iterations, 1 -> 2 lanes: 1k corr. 1.93 -> 1.46, 10k 5.08 -> 4.51, 30k 9.86 -> 8.45), 1 once the
+// big trailing updates saturate the MFMA pipes (100k / C2: 23.2 -> 25.4, a 3-lane round costs 2.1
+// trials); the switch sits between 30k (~13 GFLOP per factorization) and C2 (80 GFLOP)
+constexpr double kLaneFlopLimit = 3e10;
 struct Lane {
     DevProblem P;         // points / scales / tg / chi_* are the lane's scratch; the rest is shared
     double *part = nullptr, *scal = nullptr;   // scal: [0] chi2 [1] scale [4..6] partial chi2
@@ -104,7 +108,7 @@ struct deftri_ctx {
     // map-level graph (deftri_arap_build_graph)
     GraphResult graph;
     // speculative lambda lanes (see Lane)
-    int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES or kDefaultLanes)
+    int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES, else by factorization size)
     std::vector<Lane> lanes;                // device buffers: per uploaded problem
     DevPlan LB;                             // batched plan view: lanes' arenas / inverses / vectors / flags
     double *dx_lanes = nullptr;             // [lane][ndof]
@@ -401,7 +405,7 @@ void pop_state(deftri_ctx *ctx) {
 int lane_count(const deftri_ctx *ctx) {
     int n = ctx->max_lanes;
     if (n <= 0) {
-        n = kDefaultLanes;
+        n = ctx->S.factor_flops < kLaneFlopLimit ? 2 : 1;
         if (const char *e = std::getenv("DEFTRI_LM_LANES")) n = std::atoi(e);
     }
     return std::max(1, std::min(kMaxLanes, n));
