@@ -799,7 +799,10 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // factorization's.
 struct DiagSmem { double S[64][DP]; };
 #ifndef DEFTRI_UPD_WPE
-#define DEFTRI_UPD_WPE 4
+#define DEFTRI_UPD_WPE 4   // waves per EU of k_update (tuning knob)
+#endif
+#ifndef DEFTRI_UPD_PD
+#define DEFTRI_UPD_PD 2    // prefetch stage depth of k_update (tuning knob)
 #endif
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
@@ -837,7 +840,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
     const bool p0ok = cb + il < m, p1ok = cb + 16 + il < m, q0ok = rb + il < m, q1ok = rb + 16 + il < m;
-    constexpr int PD = 2;                                      // k-steps (of 4) per prefetch stage
+    constexpr int PD = DEFTRI_UPD_PD;                          // k-steps (of 4) per prefetch stage
     double cd[PD], c0[PD], c1[PD], c2[PD], c3[PD], nd[PD], n0[PD], n1[PD], n2[PD], n3[PD];
     auto loadk = [&](int kb0, double *d, double *x0, double *x1, double *y0, double *y1) {
 #pragma unroll
