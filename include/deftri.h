@@ -261,6 +261,16 @@ typedef struct deftri_pixels_error {
    do not; the values of the last pair are returned).  Reads the map's fp32 positions. */
 int deftri_pixels_stand_dev(deftri_ctx *ctx, const deftri_map *map, deftri_pixels_error *out);
 
+/* Mapping::triangulateSimulatedMapPoints (Modules/Mapping/Mapping.cc:280-349) for Triangulation.method
+   "NRSLAM", seed.location "FarPoints" (Simulation.yaml): per correspondence i, KB8 unproject of
+   uv1[i] / uv2[i] (KannalaBrandt8.cc:51-83), triangulateNRSLAM (Geometry.cc:103-153) and
+   isValidParallax (Mapping.cc:351-366: both depths >= 0, cos parallax <= min_cos).  Poses are
+   T_cw as 3x4 fp32 row-major [R | t] (Sophus::SE3f::matrix3x4()).  Outputs: world points for KF 1
+   and KF 2 [n*3] and valid[n] (the reference's `continue` skips invalid ones). */
+int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, const float *uv2,
+                              const float *kb8_1, const float *kb8_2, const float *T1w, const float *T2w,
+                              float min_cos, float *x3d_1, float *x3d_2, uint8_t *valid);
+
 /* Build the flattened graph only (no solve): the arrays are owned by the context and stay
    valid until the next call on it.  Used by the parity tests to compare indexing. */
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,

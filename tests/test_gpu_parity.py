@@ -302,3 +302,20 @@ def test_pixels_stand_dev_device(gpu_ctx, golden_cases, case):
     for k in ("avgc1", "avgc2", "avg", "desvc1", "desvc2", "desv"):
         assert dev[k] == pytest.approx(ref[k], rel=1e-6), k
     assert dev["desv"] > 0
+
+
+@pytest.mark.parametrize("n", [120, 100000])
+def test_triangulate_nrslam_device(gpu_ctx, n):
+    """Mapping::triangulateSimulatedMapPoints (NRSLAM, FarPoints) on the device vs the host fp32
+    restatement on the simulator's keypoints: identical valid flags, points within rel 1e-4 (the
+    per-point Newton stop, sin/cos/sqrt ulps and the 3x3 product order differ by float ulps; the
+    two-ray intersection amplifies them by ~1/parallax)."""
+    m, gt = sim.simulate_two_view(n=n, seed=3, scale_scene=n > 120)
+    kf0, kf1 = m.keyframes[0], m.keyframes[1]
+    ref1, ref2, refv = sim.triangulate_simulated(kf0.kb8, kf1.kb8, kf0.keypoints, kf1.keypoints, kf0.pose, kf1.pose)
+    x1, x2, v = gpu_ctx.triangulate_nrslam(kf0.keypoints, kf1.keypoints, kf0.kb8, kf1.kb8, kf0.pose, kf1.pose)
+    assert v.sum() > 0.9 * n
+    np.testing.assert_array_equal(v, refv)
+    for a, b in ((x1, ref1), (x2, ref2)):
+        d = np.linalg.norm(a[v] - b[v], axis=1) / np.linalg.norm(b[v], axis=1)
+        assert d.max() < 1e-4, d.max()

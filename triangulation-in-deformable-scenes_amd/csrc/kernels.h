@@ -115,6 +115,9 @@ void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hip
 void launch_pixel_partials(int nblk, const int32_t *blk_first, const int32_t *blk_last, const int32_t *blk_pair,
                            const int32_t *pair_cams, const float *cams, const float *pts, const float *obs,
                            double *part, hipStream_t st);
+// Mapping::triangulateSimulatedMapPoints, NRSLAM / FarPoints (triangulate.hip)
+void launch_triangulate_nrslam(int n, const float *uv1, const float *uv2, const float *kb1, const float *kb2,
+                               const float *Tp, float min_cos, float *x1, float *x2, uint8_t *valid, hipStream_t st);
 void launch_hmul(const DevPlan &L, const int64_t *brow_dof, const int64_t *bcol_dof, const double *x, double *y,
                  int64_t n, hipStream_t st);
 

@@ -924,6 +924,51 @@ int deftri_pixels_stand_dev(deftri_ctx *ctx, const deftri_map *map, deftri_pixel
     return 0;
 }
 
+int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, const float *uv2, const float *kb8_1,
+                              const float *kb8_2, const float *T1w, const float *T2w, float min_cos, float *x3d_1,
+                              float *x3d_2, uint8_t *valid) {
+    if (!ctx || n < 0 || (n > 0 && (!uv1 || !uv2 || !x3d_1 || !x3d_2 || !valid)) || !kb8_1 || !kb8_2 || !T1w || !T2w)
+        return DEFTRI_E_ARG;
+    if (ctx->device < 0) return fail(ctx, DEFTRI_E_NODEVICE, "host-only context");
+    if (n == 0) return 0;
+    hipSetDevice(ctx->device);
+    // Sophus: T1w.inverse() = [R1^T | -(R1^T t1)], T21 = T2w * T1w.inverse(), T2w.inverse()
+    auto inverse = [](const float *T, float *Ti) {
+        for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) Ti[4 * i + j] = T[4 * j + i];
+        for (int i = 0; i < 3; i++) Ti[4 * i + 3] = -(Ti[4 * i] * T[3] + Ti[4 * i + 1] * T[7] + Ti[4 * i + 2] * T[11]);
+    };
+    float Tp[48], T1i[12];
+    std::memcpy(Tp, T1w, 12 * sizeof(float));
+    std::memcpy(Tp + 12, T2w, 12 * sizeof(float));
+    inverse(T1w, T1i);
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++)
+            Tp[24 + 4 * i + j] = T2w[4 * i] * T1i[j] + T2w[4 * i + 1] * T1i[4 + j] + T2w[4 * i + 2] * T1i[8 + j];
+        Tp[24 + 4 * i + 3] = (T2w[4 * i] * T1i[3] + T2w[4 * i + 1] * T1i[7] + T2w[4 * i + 2] * T1i[11]) + T2w[4 * i + 3];
+    }
+    inverse(T2w, Tp + 36);
+    const size_t N = (size_t)n;
+    const size_t bytes = 4 * (2 * N + 2 * N + 8 + 8 + 48 + 3 * N + 3 * N) + N + 64;
+    char *dbuf = nullptr;
+    HIPOK(hipMalloc(&dbuf, bytes));
+    float *d_uv1 = (float *)dbuf, *d_uv2 = d_uv1 + 2 * N, *d_k1 = d_uv2 + 2 * N, *d_k2 = d_k1 + 8, *d_T = d_k2 + 8;
+    float *d_x1 = d_T + 48, *d_x2 = d_x1 + 3 * N;
+    uint8_t *d_v = (uint8_t *)(d_x2 + 3 * N);
+    hipMemcpyAsync(d_uv1, uv1, 8 * N, hipMemcpyHostToDevice, ctx->st);
+    hipMemcpyAsync(d_uv2, uv2, 8 * N, hipMemcpyHostToDevice, ctx->st);
+    hipMemcpyAsync(d_k1, kb8_1, 32, hipMemcpyHostToDevice, ctx->st);
+    hipMemcpyAsync(d_k2, kb8_2, 32, hipMemcpyHostToDevice, ctx->st);
+    hipMemcpyAsync(d_T, Tp, sizeof(Tp), hipMemcpyHostToDevice, ctx->st);
+    launch_triangulate_nrslam(n, d_uv1, d_uv2, d_k1, d_k2, d_T, min_cos, d_x1, d_x2, d_v, ctx->st);
+    hipMemcpyAsync(x3d_1, d_x1, 12 * N, hipMemcpyDeviceToHost, ctx->st);
+    hipMemcpyAsync(x3d_2, d_x2, 12 * N, hipMemcpyDeviceToHost, ctx->st);
+    hipMemcpyAsync(valid, d_v, N, hipMemcpyDeviceToHost, ctx->st);
+    hipError_t e = hipStreamSynchronize(ctx->st);
+    hipFree(dbuf);
+    if (e != hipSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("triangulate: ") + hipGetErrorString(e));
+    return 0;
+}
+
 int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(ctx->device);

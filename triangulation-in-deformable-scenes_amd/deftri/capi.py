@@ -45,6 +45,9 @@ def load():
         "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
         "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
+        "deftri_triangulate_nrslam": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float),
+                                                P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float),
+                                                P(C.c_float), P(C.c_uint8)]),
         "deftri_download": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_double)]),
         "deftri_reset_state": (C.c_int, [C.c_void_p]),
         "deftri_eval_chi2": (C.c_int, [C.c_void_p, P(C.c_double)]),
@@ -90,7 +93,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_pixels_stand_dev", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -224,6 +227,21 @@ class Context:
         out = _abi.PixelsError()
         self._check(self.lib.deftri_pixels_stand_dev(self.h, C.byref(mc), C.byref(out)))
         return out.as_dict()
+
+    def triangulate_nrslam(self, uv1, uv2, kb8_1, kb8_2, T1w, T2w, min_cos=0.9998):
+        """Mapping::triangulateSimulatedMapPoints (NRSLAM, FarPoints) on the device.  T1w/T2w: SE3f
+        (R, t).  Returns (x3d_1 [n,3], x3d_2 [n,3], valid [n] bool), fp32."""
+        f = lambda a: np.ascontiguousarray(a, np.float32)
+        uv1, uv2 = f(uv1), f(uv2)
+        n = len(uv1)
+        T = [f(np.concatenate([np.asarray(Tx.R, np.float32), np.asarray(Tx.t, np.float32)[:, None]], 1)) for Tx in (T1w, T2w)]
+        k1, k2 = f(kb8_1), f(kb8_2)
+        x1 = np.zeros((n, 3), np.float32); x2 = np.zeros((n, 3), np.float32); v = np.zeros(n, np.uint8)
+        fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+        self._check(self.lib.deftri_triangulate_nrslam(self.h, n, fp(uv1), fp(uv2), fp(k1), fp(k2), fp(T[0]), fp(T[1]),
+                                                      float(min_cos), fp(x1), fp(x2),
+                                                      v.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return x1, x2, v.astype(bool)
 
     def arap_optimization(self, m, rep_weight, global_weight, arap_weight, alpha, beta, depth_error,
                           n_iterations, want_update=True):

@@ -126,6 +126,22 @@ def triangulate_nrslam_far(xn1, xn2, T1w, T2w):
     return (Ti * p3d1.astype(np.float32)), (Ti * p3d2.astype(np.float32))
 
 
+def triangulate_simulated(kb8_1, kb8_2, uv1, uv2, T1w, T2w, min_cos=0.9998):
+    """Mapping::triangulateSimulatedMapPoints (Mapping.cc:280-349; NRSLAM, FarPoints) with
+    isValidParallax (:351-366), vectorised fp32 host restatement.  The device version is
+    deftri_triangulate_nrslam.  Returns (x3d_1, x3d_2, valid)."""
+    xn1 = kb8_unproject(kb8_1, uv1); xn2 = kb8_unproject(kb8_2, uv2)
+    xn1 = xn1 / np.linalg.norm(xn1, axis=1, keepdims=True)
+    xn2 = xn2 / np.linalg.norm(xn2, axis=1, keepdims=True)
+    x3d1, x3d2 = triangulate_nrslam_far(xn1, xn2, T1w, T2w)
+    z1 = (T1w * x3d1)[:, 2]; z2 = (T2w * x3d2)[:, 2]
+    ray1 = xn1 @ T1w.inverse().R.T; ray2 = xn2 @ T2w.inverse().R.T
+    ray1 /= np.linalg.norm(ray1, axis=1, keepdims=True); ray2 /= np.linalg.norm(ray2, axis=1, keepdims=True)
+    cosp = (ray1 * ray2).sum(1) / (np.linalg.norm(ray1, axis=1) * np.linalg.norm(ray2, axis=1))
+    valid = (z1 >= 0) & (z2 >= 0) & (cosp <= min_cos) & np.all(np.isfinite(x3d1), 1) & np.all(np.isfinite(x3d2), 1)
+    return x3d1, x3d2, valid
+
+
 def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.12),
                       c2=(0.14, 0.01, 0.06), kb8=SIM_KB8, rep_error=1.0, decimals=1,
                       depth_error=3.0, depth_scales=(0.4, 1.7), min_cos=0.9998, n_scales=8,
@@ -168,17 +184,7 @@ def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.1
     m = Map()
     m.insert_keyframe(kf0)
     m.insert_keyframe(kf1)
-    # Mapping::triangulateSimulatedMapPoints
-    xn1 = kb8_unproject(kb8, uv1); xn2 = kb8_unproject(kb8, uv2)
-    xn1 = xn1 / np.linalg.norm(xn1, axis=1, keepdims=True)
-    xn2 = xn2 / np.linalg.norm(xn2, axis=1, keepdims=True)
-    x3d1, x3d2 = triangulate_nrslam_far(xn1, xn2, T1w, T2w)
-    # isValidParallax
-    z1 = (T1w * x3d1)[:, 2]; z2 = (T2w * x3d2)[:, 2]
-    ray1 = xn1 @ T1w.inverse().R.T; ray2 = xn2 @ T2w.inverse().R.T
-    ray1 /= np.linalg.norm(ray1, axis=1, keepdims=True); ray2 /= np.linalg.norm(ray2, axis=1, keepdims=True)
-    cosp = (ray1 * ray2).sum(1) / (np.linalg.norm(ray1, axis=1) * np.linalg.norm(ray2, axis=1))
-    valid = (z1 >= 0) & (z2 >= 0) & (cosp <= min_cos) & np.all(np.isfinite(x3d1), 1) & np.all(np.isfinite(x3d2), 1)
+    x3d1, x3d2, valid = triangulate_simulated(kb8, kb8, uv1, uv2, T1w, T2w, min_cos)
     if compact and not valid.all():
         keep = np.where(valid)[0]
         return simulate_two_view(n=len(keep), seed=seed, orig=orig[keep], moved=moved[keep], c1=c1, c2=c2,
