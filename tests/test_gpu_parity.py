@@ -319,3 +319,28 @@ def test_triangulate_nrslam_device(gpu_ctx, n):
     for a, b in ((x1, ref1), (x2, ref2)):
         d = np.linalg.norm(a[v] - b[v], axis=1) / np.linalg.norm(b[v], axis=1)
         assert d.max() < 1e-4, d.max()
+
+
+def test_weight_search_multi_worker_matches_sequential():
+    """deformationOptimization with the Nelder-Mead candidates evaluated by two worker processes
+    (deftri.workers.ObjectiveWorkers; here both on GPU 0, on a node one per GPU) reproduces the
+    sequential weight search exactly: same evaluated points and objective values, weights, update."""
+    import importlib, sys
+    from deftri import optimization
+    from deftri.workers import ObjectiveWorkers
+    sys.path.insert(0, str(GOLDEN))
+    mg = importlib.import_module("make_golden")
+    out = []
+    for w in (None, ObjectiveWorkers([0, 0])):
+        m, st, _ = mg.scene("sim_default")
+        st.depth_weight = 3.0
+        st.n_optimizations, st.nlopt_iterations, st.n_iterations = 1, 6, 5
+        try:
+            out.append(optimization.deformationOptimization(m, st, workers=w)[0])
+        finally:
+            if w is not None:
+                w.close()
+    a, b = out
+    assert [e["x"] for e in a["evaluations"]] == [e["x"] for e in b["evaluations"]]
+    assert [e["f"] for e in a["evaluations"]] == [e["f"] for e in b["evaluations"]]
+    assert a["weights"] == b["weights"] and a["update"] == b["update"]

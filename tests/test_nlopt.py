@@ -77,3 +77,26 @@ def test_weight_search_outer_loop_on_oracle():
     assert r["evaluations"][0]["x"] == SIM_X0
     assert r["minf"] == min(e["f"] for e in r["evaluations"])
     assert r["weights"][:2] == [1.0, 50.0] and r["update"] > 0
+
+
+@pytest.mark.parametrize("case", ["rosen2d", "quad3d_maxeval", "bounded1d", "sim_weights"])
+def test_speculative_prefetch_matches_sequential(case):
+    """nelder_mead(prefetch=...) evaluates the candidate points of each step in one batch (the
+    multi-GPU weight search) and must reproduce the sequential run exactly: same x, minf, result,
+    nevals and evaluation log."""
+    f, x0, lb, ub, tr, ta, me = {
+        "rosen2d": (lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2, [-1.2, 1.0], [-5, -5], [5, 5], 1e-10, 1e-12, 400),
+        "quad3d_maxeval": (lambda x: (x[0] - 1) ** 2 + 2 * (x[1] + 2) ** 2 + 3 * x[2] ** 2, [0, 0, 1], [-4, -4, -4], [4, 4, 4], 0, 0, 57),
+        "bounded1d": (lambda x: (x[0] + 3.0) ** 2, [1.0], [0.0], [2.0], 1e-6, 1e-9, 200),
+        "sim_weights": (lambda x: math.log(x[2] / 3e5) ** 2 + 0.1 * math.sin(x[2] / 1e5), SIM_X0, SIM_LB, SIM_UB, 0.15, 0.15, 30),
+    }[case]
+    seq_log, spec_log, batches = [], [], []
+
+    def prefetch(xs):
+        batches.append(len(xs))
+        return [f(x) for x in xs]
+    a = nlopt_nm.nelder_mead(f, x0, lb, ub, tr, ta, me, log=seq_log.append)
+    b = nlopt_nm.nelder_mead(f, x0, lb, ub, tr, ta, me, log=spec_log.append, prefetch=prefetch)
+    assert np.array_equal(a[0], b[0]) and a[1:] == b[1:]
+    assert seq_log == spec_log
+    assert max(batches) > 1                                     # candidates really were batched

@@ -74,14 +74,37 @@ def _reflect(c, scale, xold, lb, ub):
     return None if (equalc or equalold) else xnew
 
 
+def _simplex_vertex(x, xstep, lo, hi, i):
+    """Initial simplex vertex i of nldrmd_minimize (x + xstep_i e_i, kept inside the bounds)."""
+    pt = x.copy()
+    pt[i] += xstep[i]
+    if pt[i] > hi[i]:
+        pt[i] = hi[i] if hi[i] - x[i] > abs(xstep[i]) * 0.1 else x[i] - abs(xstep[i])
+    if pt[i] < lo[i]:
+        if x[i] - lo[i] > abs(xstep[i]) * 0.1:
+            pt[i] = lo[i]
+        else:
+            pt[i] = x[i] + abs(xstep[i])
+            if pt[i] > hi[i]:
+                pt[i] = 0.5 * ((hi[i] if hi[i] - x[i] > x[i] - lo[i] else lo[i]) + x[i])
+    return pt
+
+
 class _Stop(Exception):
     def __init__(self, code):
         super().__init__(code)
         self.code = code
 
 
-def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
-    """opt.optimize(x, minf) of an LN_NELDERMEAD nlopt::opt.  Returns (x, minf, result, nevals)."""
+def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None, prefetch=None):
+    """opt.optimize(x, minf) of an LN_NELDERMEAD nlopt::opt.  Returns (x, minf, result, nevals).
+
+    prefetch (optional): callable(list of full x) -> list of f values, called with every point the
+    next sequential step may evaluate (the initial simplex; reflection, expansion and both
+    contractions; the shrink points), so a caller can evaluate them concurrently (e.g. one LM solve
+    per GPU).  The algorithm then consumes the values in NLopt's order: results, the evaluation
+    log and nevals are those of the sequential run; points NLopt would not have evaluated are
+    computed and discarded."""
     x0 = np.asarray(x0, np.float64)
     lb = np.asarray(lb, np.float64)
     ub = np.asarray(ub, np.float64)
@@ -91,11 +114,31 @@ def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
     free = np.nonzero(lb != ub)[0]
     xfull = x0.copy()
     state = {"nevals": 0, "minf": math.inf, "x": x0.copy()}
+    cache = {}
 
-    def feval(xr):
+    def full(xr):
         xf = xfull.copy()
         xf[free] = xr
-        v = float(f(xf))
+        return xf
+
+    def spec(points):
+        if prefetch is None:
+            return
+        todo = []
+        for xr in points:
+            if xr is None:
+                continue
+            k = tuple(full(xr).tolist())
+            if k not in cache and k not in [tuple(t.tolist()) for t in todo]:
+                todo.append(full(xr))
+        if todo:
+            for xf, v in zip(todo, prefetch(todo)):
+                cache[tuple(xf.tolist())] = float(v)
+
+    def feval(xr):
+        xf = full(xr)
+        k = tuple(xf.tolist())
+        v = cache.pop(k) if k in cache else float(f(xf))
         state["nevals"] += 1
         if log:
             log({"eval": state["nevals"], "x": xf.tolist(), "f": v})
@@ -118,6 +161,7 @@ def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
             return state["x"], state["minf"], SUCCESS, state["nevals"]
         lo, hi = lb[free], ub[free]
         xstep = default_initial_step(x, lo, hi)
+        spec([x] + [_simplex_vertex(x, xstep, lo, hi, i) for i in range(n)])
         fx = feval(x)                                                   # nldrmd_minimize: f(x0) first
         check(x, fx)
         pts = np.zeros((n + 1, n))
@@ -125,17 +169,7 @@ def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
         pts[0] = x
         fv[0] = fx
         for i in range(n):
-            pt = x.copy()
-            pt[i] += xstep[i]
-            if pt[i] > hi[i]:
-                pt[i] = hi[i] if hi[i] - x[i] > abs(xstep[i]) * 0.1 else x[i] - abs(xstep[i])
-            if pt[i] < lo[i]:
-                if x[i] - lo[i] > abs(xstep[i]) * 0.1:
-                    pt[i] = lo[i]
-                else:
-                    pt[i] = x[i] + abs(xstep[i])
-                    if pt[i] > hi[i]:
-                        pt[i] = 0.5 * ((hi[i] if hi[i] - x[i] > x[i] - lo[i] else lo[i]) + x[i])
+            pt = _simplex_vertex(x, xstep, lo, hi, i)
             if _close(pt[i], x[i]):
                 raise _Stop(FAILURE)
             pts[i + 1] = pt
@@ -157,6 +191,7 @@ def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
             xr = _reflect(c, ALPHA, xh, lo, hi)
             if xr is None:
                 raise _Stop(XTOL_REACHED)
+            spec([xr, _reflect(c, GAMMA, xh, lo, hi), _reflect(c, -BETA, xh, lo, hi), _reflect(c, BETA, xh, lo, hi)])
             fr = feval(xr)
             check(xr, fr)
             if fr < fl:                                                 # new best: expand
@@ -180,6 +215,7 @@ def nelder_mead(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0, log=None):
                 if fc < fr and fc < fh:
                     pts[ih], fv[ih] = xc, fc
                 else:                                                   # shrink towards the best
+                    spec([_reflect(xl, -DELTA, pts[k], lo, hi) for k in range(n + 1) if k != il])
                     for k in range(n + 1):
                         if k == il:
                             continue

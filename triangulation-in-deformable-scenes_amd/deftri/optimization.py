@@ -66,13 +66,15 @@ def outerObjective(x, pMap, settings, arap_fn=None, device=0):
 
 
 def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=None, device=0, log=None,
-                            arap_fn=None):
+                            arap_fn=None, workers=None):
     """g2oBundleAdjustment.cc:446-606.  Outer rounds until sum ||dp|| < 1e-4 |MapPoints| or
     numberOfOptimizations; per round either the fixed weights ("g2oArap") or the weight search
     ("twoOptimizations" + "nlopt": Nelder-Mead over (rep, global, arap) within the nlopt bounds,
     each evaluation an arapOptimization on a map clone, then arapOptimization on the map with the
     optimum, which becomes the next round's start).  `arap_fn` (tests only) replaces the device
-    arapOptimization with another implementation of the same signature."""
+    arapOptimization with another implementation of the same signature.  `workers`
+    (deftri.workers.ObjectiveWorkers) evaluates each Nelder-Mead step's candidate points on several
+    GPUs at once; the search and its result are those of the sequential run."""
     import copy
     from .nlopt_nm import nelder_mead
     settings.validate_for_solver()
@@ -99,13 +101,16 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
         if settings.selection == "twoOptimizations":
             base = copy.deepcopy(pMap)            # optData.pMap = pMap->clone()
             evals = []
+            prefetch = None
+            if workers is not None and arap_fn is None:
+                prefetch = lambda xs, base=base: workers.map_objective(xs, base, settings)
             x, minf, res, nev = nelder_mead(
                 lambda x: outerObjective(x, base, settings, arap_fn=arap_fn, device=device),
                 [rep_w, glob_w, arap_w],
                 [settings.nlopt_rep_lb, settings.nlopt_global_lb, settings.nlopt_arap_lb],
                 [settings.nlopt_rep_ub, settings.nlopt_global_ub, settings.nlopt_arap_ub],
                 xtol_rel=settings.nlopt_rel_tol, xtol_abs=settings.nlopt_abs_tol,
-                maxeval=int(settings.nlopt_iterations), log=evals.append)
+                maxeval=int(settings.nlopt_iterations), log=evals.append, prefetch=prefetch)
             rep_w, glob_w, arap_w = (float(v) for v in x)
             info.update({"weights": [rep_w, glob_w, arap_w], "minf": minf, "nlopt_result": res,
                          "evaluations": evals})
