@@ -3,7 +3,7 @@
 //
 // Stage (g2o)                                   kernel                 parallel unit
 // computeActiveErrors + linearizeOplus          k_ba_edges             edge
-// buildSystem: Hll, bl, Hpl (= Wb)              k_ba_points            point (edges in CSR order)
+// buildSystem: Hll, bl; Hpl (= Wb)            k_ba_points; k_ba_hpl  point (edges in CSR order); lead edge
 // buildSystem: Hpp, bp                          k_ba_pose_chunk/final  256-edge chunk of one pose, then pose x entry
 // setLambda + Dinv, Hpl Dinv, Hpl Dinv bl       k_ba_schur_points      point
 // Hschur = Hpp - sum Hpl Dinv Hlp, bschur       k_ba_schur_gemm        (entry tile, point group); LDS-staged edges
@@ -101,24 +101,15 @@ __global__ void k_ba_edges(int E, const int32_t *__restrict__ ept, const int32_t
 // pose) pair, Wb = sum J_T^T w J_p (6x3), stored at the pair's lead edge (duplicate observations of
 // one point in one pose add into the same block, as g2o's Hpl)
 __global__ void k_ba_points(int P, const int32_t *__restrict__ pt_ptr, const uint8_t *__restrict__ pt_free,
-                            const uint8_t *__restrict__ active, const int32_t *__restrict__ lead,
-                            const int32_t *__restrict__ pslot, const double *__restrict__ wgt,
-                            const double *__restrict__ wr, const double *__restrict__ Jp,
-                            const double *__restrict__ JT, double *__restrict__ Hll, double *__restrict__ bl,
-                            double *__restrict__ Wb) {
+                            const uint8_t *__restrict__ active, const double *__restrict__ wgt,
+                            const double *__restrict__ wr, const double *__restrict__ Jp, double *__restrict__ Hll,
+                            double *__restrict__ bl) {
     int l = TID;
     if (l >= P || !pt_free[l]) return;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     const int ebeg = pt_ptr[l], eend = pt_ptr[l + 1];
     for (int e = ebeg; e < eend; e++) {
-        const int ld = lead[e];
-        if (!active[e]) {
-            // an inactive lead of a pair whose duplicate is active still carries the pair's block
-            if (ld == e && pslot[e] >= 0)
-#pragma unroll
-                for (int i = 0; i < 18; i++) Wb[18 * (int64_t)e + i] = 0.0;
-            continue;
-        }
+        if (!active[e]) continue;
         const double w = wgt[e];
         const double *J = Jp + 6 * (int64_t)e;
         const double r0 = wr[2 * (int64_t)e], r1 = wr[2 * (int64_t)e + 1];
@@ -129,26 +120,45 @@ __global__ void k_ba_points(int P, const int32_t *__restrict__ pt_ptr, const uin
             for (int d = 0; d < 3; d++) H[3 * c + d] += a0 * J[d] + a1 * J[3 + d];
             b[c] += J[c] * r0 + J[3 + c] * r1;
         }
-        if (pslot[ld] >= 0) {
-            const double *B = JT + 12 * (int64_t)e;
-            double *o = Wb + 18 * (int64_t)ld;
-            if (ld == e) {
-#pragma unroll
-                for (int j = 0; j < 6; j++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) o[3 * j + c] = (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
-            } else {                               // duplicate observation: add into the lead's block
-#pragma unroll
-                for (int j = 0; j < 6; j++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) o[3 * j + c] += (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
-            }
-        }
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) Hll[9 * (int64_t)l + i] = H[i];
 #pragma unroll
     for (int i = 0; i < 3; i++) bl[3 * (int64_t)l + i] = b[i];
+}
+
+// Hpl block of each (point, free pose) pair, one thread per lead edge (edge-parallel: coalesced
+// J / JT reads and Wb writes).  The lead's own product (zero if the lead is inactive), then the
+// active duplicate observations of the pair in edge order (g2o adds every edge's block).
+__device__ __forceinline__ void ba_hpl_product(const double *J, const double *B, double w, double o[18], bool add) {
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const double v = (J[c] * w) * B[j] + (J[3 + c] * w) * B[6 + j];
+            o[3 * j + c] = add ? o[3 * j + c] + v : v;
+        }
+}
+
+__global__ void k_ba_hpl(int E, const int32_t *__restrict__ e_point, const int32_t *__restrict__ pt_ptr,
+                         const uint8_t *__restrict__ pt_free, const uint8_t *__restrict__ active,
+                         const int32_t *__restrict__ lead, const int32_t *__restrict__ pslot,
+                         const double *__restrict__ wgt, const double *__restrict__ Jp,
+                         const double *__restrict__ JT, double *__restrict__ Wb) {
+    const int e = TID;
+    if (e >= E || lead[e] != e || pslot[e] < 0) return;
+    const int l = e_point[e];
+    if (!pt_free[l]) return;
+    double o[18];
+    if (active[e]) ba_hpl_product(Jp + 6 * (int64_t)e, JT + 12 * (int64_t)e, wgt[e], o, false);
+    else
+#pragma unroll
+        for (int i = 0; i < 18; i++) o[i] = 0.0;
+    const int eend = pt_ptr[l + 1];
+    for (int e2 = e + 1; e2 < eend; e2++)
+        if (lead[e2] == e && active[e2]) ba_hpl_product(Jp + 6 * (int64_t)e2, JT + 12 * (int64_t)e2, wgt[e2], o, true);
+#pragma unroll
+    for (int i = 0; i < 18; i++) Wb[18 * (int64_t)e + i] = o[i];
 }
 
 // per-chunk partial sums of Hpp (36, full) and bp (6) of one free pose; 256 edges per chunk.
@@ -672,7 +682,10 @@ void ba_launch_chi2_sum(const BADev &B, double *out, hipStream_t st) {
 void ba_launch_points(const BADev &B, hipStream_t st) {
     if (B.P <= 0) return;
     BALAUNCH("ba_points", dev::k_ba_points, dim3(nbk(B.P, 128)), dim3(128), 0, st, B.P, B.pt_ptr, B.pt_free,
-             B.active, B.lead, B.pslot, B.wgt, B.wr, B.Jp, B.JT, B.Hll, B.bl, B.Wb);
+             B.active, B.wgt, B.wr, B.Jp, B.Hll, B.bl);
+    if (B.E > 0)
+        BALAUNCH("ba_hpl", dev::k_ba_hpl, dim3(nbk(B.E, 256)), dim3(256), 0, st, B.E, B.e_point, B.pt_ptr, B.pt_free,
+                 B.active, B.lead, B.pslot, B.wgt, B.Jp, B.JT, B.Wb);
 }
 
 void ba_launch_poses(const BADev &B, hipStream_t st) {
