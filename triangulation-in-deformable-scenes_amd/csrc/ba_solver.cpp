@@ -480,11 +480,14 @@ int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *prm, int32_t 
         hipEventRecord(ctx->ev[1], ctx->st);
         double *head = ctx->hpin;            // pinned: a pageable readback costs ~100 us per call
         HIPOK(hipMemcpyAsync(&head[0], ctx->hb, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
-        if (it == 0) HIPOK(hipMemcpyAsync(&head[2], B.scal + 2, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
-        HIPOK(hipStreamSynchronize(ctx->st));
-        t_lin += ev_ms(ctx, 0, 1);
-        currentChi = head[0];
+        // only iteration 0 needs a value before its first trial (lambda from max diag); later
+        // iterations read this iteration's chi2 together with the first trial's scalars
+        bool chi_pending = true;
         if (it == 0) {
+            HIPOK(hipMemcpyAsync(&head[2], B.scal + 2, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
+            HIPOK(hipStreamSynchronize(ctx->st));
+            currentChi = head[0];
+            chi_pending = false;
             R.chi2_initial = currentChi;
             lambda = prm->user_lambda > 0 ? prm->user_lambda : tau * head[2];
             ni = 2;
@@ -509,6 +512,8 @@ int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *prm, int32_t 
             HIPOK(hipMemcpyAsync(sc, B.scal, sizeof(double) * 4, hipMemcpyDeviceToHost, ctx->st));
             HIPOK(hipMemcpyAsync(ctx->ipin, B.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
             HIPOK(hipStreamSynchronize(ctx->st));
+            if (chi_pending) { currentChi = head[0]; chi_pending = false; }
+            if (qmax == 0) t_lin += ev_ms(ctx, 0, 1);
             const int flag = *ctx->ipin;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             const bool ok2 = flag == 0;

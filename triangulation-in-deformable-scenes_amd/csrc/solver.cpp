@@ -726,10 +726,14 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         hipEventRecord(ctx->ev[1], ctx->st);
         double *chis = ctx->hpin;           // pinned: a pageable readback costs ~100 us per call
         HIPOK(hipMemcpyAsync(chis, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
-        HIPOK(hipStreamSynchronize(ctx->st));
-        t_lin += ev_ms(ctx, 0, 1);
-        currentChi = chis[0];
+        // only iteration 0 needs a value before its first trial (lambda from max diag); later
+        // iterations read this iteration's chi2 with the first trial's (or round's) scalars
+        bool chi_pending = true;
         if (it == 0) {
+            HIPOK(hipStreamSynchronize(ctx->st));
+            t_lin += ev_ms(ctx, 0, 1);
+            currentChi = chis[0];
+            chi_pending = false;
             lambda = prm->user_lambda > 0 ? prm->user_lambda : tau * chis[2];
             ni = 2;
         }
@@ -748,6 +752,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 lanes_round(ctx, nl, lam, analytic);
                 hipEventRecord(ctx->ev[5], ctx->st);
                 HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a round
+                if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
                 t_fac += ev_ms(ctx, 2, 5);
                 R.trials_executed += nl;
                 int acc = -1;
@@ -793,6 +798,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
             HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
             HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
+            if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
             const bool ok2 = *ctx->ipin == 0;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
