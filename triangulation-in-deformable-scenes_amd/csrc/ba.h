@@ -48,6 +48,12 @@ struct BADev {
     int32_t *pslot = nullptr;              // [E] Schur block of the edge's pose (-1: not in S); set on the
                                            //     lead edge of each (point, pose) pair only
     int32_t *lead = nullptr;               // [E] first edge of the same (point, pose) pair
+    // initializeOptimization(level) inputs / scratch (device-side active set)
+    uint8_t *e_level = nullptr;            // [E] edge level (point order)
+    uint8_t *pt_fixed = nullptr, *pose_fixed = nullptr;   // [P], [K]
+    int32_t *pose_flag = nullptr;          // [K] pose has an active edge on this rank
+    uint8_t *pt_act = nullptr;             // [P] point has an active edge
+    int32_t *icount = nullptr;             // [1] free points
     // linearization (per edge)
     double *err = nullptr, *wgt = nullptr, *chi = nullptr, *chi2raw = nullptr;
     double *wr = nullptr;                  // [E*2] omega_r = -rho' Omega e
@@ -84,6 +90,10 @@ void ba_launch_schur(const BADev &B, double lambda, hipStream_t st);
 void ba_launch_dense_solve(const BADev &B, double lambda, hipStream_t st);
 void ba_launch_backsub_update(const BADev &B, hipStream_t st);
 void ba_launch_scale(const BADev &B, double lambda, double *out_pts, double *out_pose, hipStream_t st);
+// initializeOptimization(level) on the device: active edges, per-pose / per-point activity
+void ba_launch_active(const BADev &B, int level, hipStream_t st);
+// free points (count into icount) and the Schur slot of each pair's lead edge, given pose_sidx
+void ba_launch_free_slots(const BADev &B, hipStream_t st);
 void ba_launch_edge_chi2(const BADev &B, const int32_t *perm, double *chi2_out, uint8_t *dpos_out, hipStream_t st);
 
 }  // namespace deftri

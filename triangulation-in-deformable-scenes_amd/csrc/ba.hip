@@ -675,6 +675,63 @@ void ba_launch_edges(const BADev &B, hipStream_t st, bool want_jac, bool all_edg
              B.wr, B.Jp, B.JT, want_jac ? 1 : 0, all_edges ? 1 : 0);
 }
 
+namespace dev {
+// initializeOptimization(level) (g2o; reference g2oBundleAdjustment.cc:56-60 / 297-305): an edge
+// is active at `level` unless both its vertices are fixed; a pose / point is active when one of its
+// edges is.  Flags are set with plain stores of 1 (idempotent: the result has no order).
+__global__ void k_ba_active(int E, int level, const uint8_t *__restrict__ e_level, const int32_t *__restrict__ e_point,
+                            const int32_t *__restrict__ e_pose, const uint8_t *__restrict__ pt_fixed,
+                            const uint8_t *__restrict__ pose_fixed, uint8_t *__restrict__ active,
+                            int32_t *__restrict__ pose_flag, uint8_t *__restrict__ pt_act) {
+    const int s = TID;
+    if (s >= E) return;
+    const int l = e_point[s], k = e_pose[s];
+    const bool a = e_level[s] == level && !(pt_fixed[l] && pose_fixed[k]);
+    active[s] = a ? 1 : 0;
+    if (a) { pose_flag[k] = 1; pt_act[l] = 1; }
+}
+
+__global__ void k_ba_free_points(int P, const uint8_t *__restrict__ pt_act, const uint8_t *__restrict__ pt_fixed,
+                                 uint8_t *__restrict__ pt_free, int32_t *__restrict__ count) {
+    const int l = TID;
+    if (l >= P) return;
+    const bool f = pt_act[l] && !pt_fixed[l];
+    pt_free[l] = f ? 1 : 0;
+    if (f) atomicAdd(count, 1);                       // integer count: order-independent
+}
+
+// Schur slot on the lead edge of each (point, pose) pair with an active edge, free point and free
+// pose (every such edge of the pair writes the same value)
+__global__ void k_ba_pslot(int E, const uint8_t *__restrict__ active, const int32_t *__restrict__ e_point,
+                           const int32_t *__restrict__ e_pose, const uint8_t *__restrict__ pt_free,
+                           const int32_t *__restrict__ pose_sidx, const int32_t *__restrict__ lead,
+                           int32_t *__restrict__ pslot) {
+    const int s = TID;
+    if (s >= E || !active[s]) return;
+    const int l = e_point[s], k = e_pose[s];
+    if (pt_free[l] && pose_sidx[k] >= 0) pslot[lead[s]] = pose_sidx[k];
+}
+}  // namespace dev
+
+void ba_launch_active(const BADev &B, int level, hipStream_t st) {
+    hipMemsetAsync(B.pose_flag, 0, sizeof(int32_t) * (size_t)std::max(B.K, 1), st);
+    hipMemsetAsync(B.pt_act, 0, (size_t)std::max(B.P, 1), st);
+    if (B.E > 0)
+        BALAUNCH("ba_active", dev::k_ba_active, dim3(nbk(B.E, 256)), dim3(256), 0, st, B.E, level, B.e_level,
+                 B.e_point, B.e_pose, B.pt_fixed, B.pose_fixed, B.active, B.pose_flag, B.pt_act);
+}
+
+void ba_launch_free_slots(const BADev &B, hipStream_t st) {
+    hipMemsetAsync(B.icount, 0, sizeof(int32_t), st);
+    hipMemsetAsync(B.pslot, 0xFF, sizeof(int32_t) * (size_t)std::max(B.E, 1), st);     // -1
+    if (B.P > 0)
+        BALAUNCH("ba_free_points", dev::k_ba_free_points, dim3(nbk(B.P, 256)), dim3(256), 0, st, B.P, B.pt_act,
+                 B.pt_fixed, B.pt_free, B.icount);
+    if (B.E > 0)
+        BALAUNCH("ba_pslot", dev::k_ba_pslot, dim3(nbk(B.E, 256)), dim3(256), 0, st, B.E, B.active, B.e_point,
+                 B.e_pose, B.pt_free, B.pose_sidx, B.lead, B.pslot);
+}
+
 void ba_launch_chi2_sum(const BADev &B, double *out, hipStream_t st) {
     launch_sum(B.E, B.chi, nullptr, 0, 0, B.part, 256, out, st);
 }

@@ -146,18 +146,17 @@ int validate(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
 
 // initializeOptimization(level): activity of edges and vertices, Schur indices, LDS tables.
 int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
+    // initializeOptimization(level) on the device: the edge / vertex activity is computed by
+    // kernels; only the K pose flags come to the host (Schur slots of the free poses, K <= 200)
     BADev &B = ctx->B;
-    const int32_t K = ctx->K, P = ctx->P, E = ctx->E;
-    std::vector<uint8_t> act(E);
+    const int32_t K = ctx->K, P = ctx->P;
+    if (level < 0 || level > 255) return fail(ctx, DEFTRI_E_ARG, "level out of range");
+    ba_launch_active(B, level, ctx->st);
+    std::vector<int32_t> pflag(std::max(K, 1), 0);
+    if (K > 0) HIPOK(hipMemcpyAsync(pflag.data(), B.pose_flag, sizeof(int32_t) * K, hipMemcpyDeviceToHost, ctx->st));
+    HIPOK(hipStreamSynchronize(ctx->st));
     std::vector<double> pose_cnt(K, 0.0);
-    std::vector<uint8_t> pt_act(P, 0);
-    for (int32_t s = 0; s < E; s++) {
-        const int32_t o = ctx->perm[s];
-        const int32_t l = ctx->e_point[s], k = ctx->e_pose[s];
-        const bool all_fixed = ctx->point_fixed[l] && ctx->pose_fixed[k];
-        act[s] = (ctx->level[o] == level && !all_fixed) ? 1 : 0;
-        if (act[s]) { pose_cnt[k] += 1.0; pt_act[l] = 1; }
-    }
+    for (int32_t k = 0; k < K; k++) pose_cnt[k] = pflag[k] ? 1.0 : 0.0;
     if ((ctx->nranks > 1 || ctx->comm) && K > 0) {   // a pose is active if any rank holds an active edge of it
         double *d = B.Spart;                 // scratch (allocated with >= K doubles at upload)
         HIPOK(hipMemcpyAsync(d, pose_cnt.data(), sizeof(double) * K, hipMemcpyHostToDevice, ctx->st));
@@ -166,24 +165,18 @@ int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
         HIPOK(hipMemcpyAsync(pose_cnt.data(), d, sizeof(double) * K, hipMemcpyDeviceToHost, ctx->st));
         HIPOK(hipStreamSynchronize(ctx->st));
     }
-    std::vector<int32_t> sidx(K, -1);
+    std::vector<int32_t> sidx(std::max(K, 1), -1);
     int32_t nfree = 0;
     for (int32_t k = 0; k < K; k++)
         if (pose_cnt[k] > 0 && !ctx->pose_fixed[k]) sidx[k] = nfree++;
     if (nfree > 200) return fail(ctx, DEFTRI_E_ARG, "more than 200 free poses in one Schur system");
-    std::vector<uint8_t> pfree(P, 0);
-    int32_t nfp = 0;
-    for (int32_t l = 0; l < P; l++) {
-        pfree[l] = (pt_act[l] && !ctx->point_fixed[l]) ? 1 : 0;
-        nfp += pfree[l];
-    }
-    // Schur slot on the lead edge of each (point, pose) pair with an active edge, free point and free pose
-    std::vector<int32_t> pslot(E, -1);
-    for (int32_t s = 0; s < E; s++) {
-        if (!act[s]) continue;
-        const int32_t l = ctx->e_point[s], k = ctx->e_pose[s];
-        if (pfree[l] && sidx[k] >= 0) pslot[ctx->lead[s]] = sidx[k];
-    }
+    if (K > 0) HIPOK(hipMemcpyAsync(B.pose_sidx, sidx.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice, ctx->st));
+    ba_launch_free_slots(B, ctx->st);
+    int32_t *nfp_h = ctx->ipin + 1;          // pinned
+    HIPOK(hipMemcpyAsync(nfp_h, B.icount, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->st));
+    HIPOK(hipMemsetAsync(B.dxl, 0, sizeof(double) * 3 * (size_t)std::max(P, 1), ctx->st));
+    HIPOK(hipStreamSynchronize(ctx->st));
+    const int32_t nfp = *nfp_h;
     B.nfree = nfree;
     B.ns = 6 * nfree;
     B.dense_positive = nfp == 0 ? 1 : 0;      // poses only: LinearSolverDense (Eigen LDLT, isPositive)
@@ -198,11 +191,14 @@ int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
         if ((rc = dalloc(ctx, &B.xp, std::max(B.ns, 1)))) return rc;
         ctx->cap_ns = B.ns;
     }
-    HIPOK(hipMemcpyAsync(B.active, act.data(), E, hipMemcpyHostToDevice, ctx->st));
-    HIPOK(hipMemcpyAsync(B.pt_free, pfree.data(), P, hipMemcpyHostToDevice, ctx->st));
-    HIPOK(hipMemcpyAsync(B.pose_sidx, sidx.data(), sizeof(int32_t) * K, hipMemcpyHostToDevice, ctx->st));
-    HIPOK(hipMemcpyAsync(B.pslot, pslot.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice, ctx->st));
-    HIPOK(hipMemsetAsync(B.dxl, 0, sizeof(double) * 3 * (size_t)std::max(P, 1), ctx->st));
+    return 0;
+}
+
+// edge levels (original edge order) -> device, point order
+int upload_levels(deftri_ba_ctx *ctx) {
+    std::vector<uint8_t> lv(std::max(ctx->E, 1));
+    for (int32_t s = 0; s < ctx->E; s++) lv[s] = ctx->level[ctx->perm[s]];
+    HIPOK(hipMemcpyAsync(ctx->B.e_level, lv.data(), ctx->E, hipMemcpyHostToDevice, ctx->st));
     HIPOK(hipStreamSynchronize(ctx->st));
     return 0;
 }
@@ -387,6 +383,8 @@ int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
     PUT(B.stage_pt, stage_pt); PUT(B.group_stage, group_stage);
     ALLOC(B.pslot, E);
     PUT(B.lead, ctx->lead);
+    ALLOC(B.e_level, E); ALLOC(B.pose_flag, K); ALLOC(B.pt_act, P); ALLOC(B.icount, 1);
+    PUT(B.pt_fixed, ctx->point_fixed); PUT(B.pose_fixed, ctx->pose_fixed);
     ALLOC(B.err, 2 * (int64_t)E); ALLOC(B.wr, 2 * (int64_t)E);
     ALLOC(B.wgt, E); ALLOC(B.chi, E); ALLOC(B.chi2raw, E);
     ALLOC(B.Jp, 6 * (int64_t)E); ALLOC(B.JT, 12 * (int64_t)E);
@@ -409,6 +407,7 @@ int deftri_ba_upload(deftri_ba_ctx *ctx, const deftri_ba_desc *d) {
     ALLOC(B.Spart, std::max<int64_t>((int64_t)std::max(std::max(B.ngroup, B.mgroup), 1) * NE, K));
     ALLOC(B.Sred, NE); ALLOC(B.S, ns * ns); ALLOC(B.xp, std::max<int64_t>(ns, 1));
     ctx->cap_ns = (int32_t)ns;
+    if ((rc = upload_levels(ctx))) return rc;
 #undef PUT
 #undef ALLOC
     HIPOK(hipMemset(B.err, 0, sizeof(double) * 2 * (size_t)std::max(E, 1)));
@@ -434,7 +433,11 @@ int deftri_ba_set_state(deftri_ba_ctx *ctx, const double *poses, const double *p
 int deftri_ba_set_edge_flags(deftri_ba_ctx *ctx, const uint8_t *level, const uint8_t *robust) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(ctx->device);
-    if (level) ctx->level.assign(level, level + ctx->E);
+    if (level) {
+        ctx->level.assign(level, level + ctx->E);
+        int rc = upload_levels(ctx);
+        if (rc) return rc;
+    }
     if (robust) {
         ctx->robust.assign(robust, robust + ctx->E);
         std::vector<uint8_t> rob(ctx->E);
