@@ -30,7 +30,10 @@ static inline uint64_t contrib_pack(int kind, int64_t edge, int role_col, int ro
 }
 
 constexpr int kPanel = 64;          // panel width of the blocked dense kernels
-constexpr int kOuter = 256;         // outer block: trailing updates beyond it use K = 256
+#ifndef DEFTRI_OUTER
+#define DEFTRI_OUTER 256
+#endif
+constexpr int kOuter = DEFTRI_OUTER; // outer block: trailing updates beyond it use K = kOuter (tuning knob)
 constexpr int kChunk = 128;         // contributions per gather chunk
 constexpr int kBwdCols = 16;        // own columns per backward-init task
 
