@@ -344,3 +344,48 @@ def test_weight_search_multi_worker_matches_sequential():
     assert [e["x"] for e in a["evaluations"]] == [e["x"] for e in b["evaluations"]]
     assert [e["f"] for e in a["evaluations"]] == [e["f"] for e in b["evaluations"]]
     assert a["weights"] == b["weights"] and a["update"] == b["update"]
+
+
+def _single_kf_map():
+    from deftri.mapmodel import Map
+    m, _ = sim.simulate_two_view(n=200, seed=1)
+    m1 = Map()
+    kf = m.keyframes[0]
+    m1.insert_keyframe(kf)
+    for i, mp in enumerate(kf.map_points):
+        if mp is not None:
+            m1.insert_map_point(mp)
+            m1.add_observation(kf.id, mp.id, i)
+    return m1
+
+
+def test_degenerate_maps():
+    """Edge cases of the map-level entry points: a one-keyframe map has no KF pair, so the
+    reference's pair loop builds an empty graph (arapOptimization changes nothing, update 0) and
+    calculatePixelsStandDev reports zeros; an empty correspondence set triangulates to nothing."""
+    from deftri import optimization
+    m1 = _single_kf_map()
+    before = {k: mp.position.copy() for k, mp in m1.map_points.items()}
+    upd = [1.0]
+    optimization.arapOptimization(m1, 1.0, 50.0, 2e5, 0.0, 0.0, np.float32(0.003), 5, upd)
+    assert upd[0] == 0.0
+    assert all(np.array_equal(before[k], mp.position) for k, mp in m1.map_points.items())
+    ctx = capi.Context(0)
+    pe = ctx.pixels_stand_dev(m1)
+    assert all(v == 0.0 for v in pe.values())
+    kf = m1.keyframes[0]
+    x1, x2, v = ctx.triangulate_nrslam(np.zeros((0, 2)), np.zeros((0, 2)), kf.kb8, kf.kb8, kf.pose, kf.pose)
+    assert x1.shape == (0, 3) and v.shape == (0,)
+
+
+@pytest.mark.parametrize("n", [3, 4, 5])
+def test_minimal_meshes_match_oracle(gpu_ctx, n):
+    """The smallest two-view problems (one or a few Delaunay triangles) through the device LM."""
+    m, _ = sim.simulate_two_view(n=n, seed=2)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    gpu_ctx.upload(p)
+    assert gpu_ctx.chi2() == pytest.approx(oracle.chi2(p), rel=1e-11)
+    r = gpu_ctx.solve_lm(5, analytic=True)
+    ref = oracle.solve_lm(p, 5, analytic=True)["report"]
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
