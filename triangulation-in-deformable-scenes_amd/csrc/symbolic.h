@@ -34,7 +34,10 @@ constexpr int kPanel = 64;          // panel width of the blocked dense kernels
 #define DEFTRI_OUTER 256
 #endif
 constexpr int kOuter = DEFTRI_OUTER; // outer block: trailing updates beyond it use K = kOuter (tuning knob)
-constexpr int kChunk = 128;         // contributions per gather chunk
+#ifndef DEFTRI_CHUNK
+#define DEFTRI_CHUNK 64
+#endif
+constexpr int kChunk = DEFTRI_CHUNK; // contributions per gather chunk (A/B 32/64/128: 64 best, tuning knob)
 constexpr int kBwdCols = 16;        // own columns per backward-init task
 
 struct Front {
