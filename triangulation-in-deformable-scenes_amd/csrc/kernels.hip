@@ -306,11 +306,21 @@ __global__ void k_hfinal(int64_t nblocks, const int64_t *__restrict__ blk_chunk_
     if (b >= nblocks) return;
     int64_t c0 = blk_chunk_begin[b], c1 = blk_chunk_begin[b + 1];
     if (c1 - c0 > kHeavyChunks) return;                 // k_hfinal_heavy
-    int n = brows[b] * bcols[b];
+    const int n = brows[b] * bcols[b];
     double *o = hval + val_off[b];
-    for (int k = 0; k < n; k++) o[k] = 0.0;
-    for (int64_t c = c0; c < c1; c++)
-        for (int k = 0; k < n; k++) o[k] += part[36 * c + k];
+    // partials summed in chunk order in registers (one store per entry)
+    double acc[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) acc[k] = 0.0;
+    for (int64_t c = c0; c < c1; c++) {
+        const double *pc = part + 36 * c;
+#pragma unroll
+        for (int k = 0; k < 36; k++)
+            if (k < n) acc[k] += pc[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 36; k++)
+        if (k < n) o[k] = acc[k];
 }
 
 // blocks fed by thousands of chunks (the global T_g / depth-scale rows): one workgroup per block,
