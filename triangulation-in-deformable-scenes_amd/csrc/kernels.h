@@ -73,6 +73,7 @@ struct DevPlan {
     double *hpart = nullptr;
     int64_t nheavy_h = 0, nheavy_b = 0;
     int64_t *heavy_h = nullptr, *heavy_b = nullptr;     // blocks / vertices with > kHeavyChunks chunks
+    double *heavy_scratch = nullptr;                     // per heavy item x 32 slices x 36 partial sums
     int64_t nbchunks = 0;
     uint64_t *bcontrib = nullptr;
     int64_t *bchunk_begin = nullptr, *bv_chunk_begin = nullptr;

@@ -323,8 +323,10 @@ __global__ void k_hfinal(int64_t nblocks, const int64_t *__restrict__ blk_chunk_
         if (k < n) o[k] = acc[k];
 }
 
-// blocks fed by thousands of chunks (the global T_g / depth-scale rows): one workgroup per block,
-// strided per-thread sums then an in-order sum over the 256 partials — fixed order, no atomics
+// blocks fed by thousands of chunks (the global T_g / depth-scale rows): each of kHeavySplit
+// workgroups takes a contiguous slice of the chunks, strided per-thread sums then an in-order sum
+// over the 256 partials; the slices are then added in order — fixed order, no atomics
+constexpr int kHeavySplit = 32;
 template <int W>
 __device__ __forceinline__ void heavy_sum(int64_t c0, int64_t c1, int n, const double *__restrict__ part,
                                           double *__restrict__ o) {
@@ -346,14 +348,30 @@ __device__ __forceinline__ void heavy_sum(int64_t c0, int64_t c1, int n, const d
     }
 }
 
-__global__ void __launch_bounds__(256) k_hfinal_heavy(const int64_t *__restrict__ heavy,
-                                                      const int64_t *__restrict__ blk_chunk_begin,
-                                                      const int64_t *__restrict__ val_off,
-                                                      const int32_t *__restrict__ brows,
-                                                      const int32_t *__restrict__ bcols,
-                                                      const double *__restrict__ part, double *__restrict__ hval) {
-    int64_t b = heavy[blockIdx.x];
-    heavy_sum<36>(blk_chunk_begin[b], blk_chunk_begin[b + 1], brows[b] * bcols[b], part, hval + val_off[b]);
+// heavy blocks split over kHeavySplit workgroups each: workgroup g sums its contiguous slice of
+// the block's chunks (heavy_sum order) into scratch; k_heavy_final adds the slices in slice order
+template <int W>
+__global__ void __launch_bounds__(256) k_heavy_split(const int64_t *__restrict__ heavy,
+                                                     const int64_t *__restrict__ chunk_begin,
+                                                     const double *__restrict__ part, double *__restrict__ scratch) {
+    const int64_t h = blockIdx.x / kHeavySplit, g = blockIdx.x % kHeavySplit;
+    const int64_t v = heavy[h];
+    const int64_t c0 = chunk_begin[v], len = chunk_begin[v + 1] - c0;
+    heavy_sum<W>(c0 + g * len / kHeavySplit, c0 + (g + 1) * len / kHeavySplit, W, part,
+                 scratch + (h * kHeavySplit + g) * W);
+}
+
+template <int W>
+__global__ void k_heavy_final(const int64_t *__restrict__ heavy, const int64_t *__restrict__ off,
+                              const int32_t *__restrict__ nr, const int32_t *__restrict__ nc,
+                              const double *__restrict__ scratch, double *__restrict__ out) {
+    const int64_t h = blockIdx.x, v = heavy[h];
+    const int n = nc ? nr[v] * nc[v] : nr[v];
+    const int k = threadIdx.x;
+    if (k >= n) return;
+    double s = 0.0;
+    for (int g = 0; g < kHeavySplit; g++) s += scratch[(h * kHeavySplit + g) * W + k];
+    out[off[v] + k] = s;
 }
 
 __global__ void k_bchunk(int64_t nchunks, const uint64_t *__restrict__ contrib, const int64_t *__restrict__ cbeg,
@@ -392,14 +410,6 @@ __global__ void k_bfinal(int64_t nv, const int64_t *__restrict__ v_chunk_begin, 
     for (int64_t c = v_chunk_begin[v]; c < v_chunk_begin[v + 1]; c++)
         for (int i = 0; i < 6; i++) acc[i] += part[6 * c + i];
     for (int i = 0; i < dim; i++) b[voff[v] + i] = acc[i];
-}
-
-__global__ void __launch_bounds__(256) k_bfinal_heavy(const int64_t *__restrict__ heavy,
-                                                      const int64_t *__restrict__ v_chunk_begin,
-                                                      const int64_t *__restrict__ voff, const int32_t *__restrict__ vdim,
-                                                      const double *__restrict__ part, double *__restrict__ b) {
-    int64_t v = heavy[blockIdx.x];
-    heavy_sum<6>(v_chunk_begin[v], v_chunk_begin[v + 1], vdim[v], part, b + voff[v]);
 }
 
 // H (+ lambda I) -> fronts
@@ -1269,18 +1279,24 @@ void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
     if (L.nblocks > 0)
         LAUNCH("hfinal", dev::k_hfinal, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks,
                            L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
-    if (L.nheavy_h > 0)
-        LAUNCH("hfinal_heavy", dev::k_hfinal_heavy, dim3((unsigned)L.nheavy_h), dim3(256), st, L.heavy_h,
-                           L.hblk_chunk_begin, L.blk_val_off, L.blk_rows, L.blk_cols, L.hpart, L.hval);
+    if (L.nheavy_h > 0) {
+        LAUNCH("hfinal_heavy", dev::k_heavy_split<36>, dim3((unsigned)(L.nheavy_h * dev::kHeavySplit)), dim3(256), st,
+               L.heavy_h, L.hblk_chunk_begin, L.hpart, L.heavy_scratch);
+        LAUNCH("hfinal_heavy", dev::k_heavy_final<36>, dim3((unsigned)L.nheavy_h), dim3(64), st, L.heavy_h,
+               L.blk_val_off, L.blk_rows, L.blk_cols, L.heavy_scratch, L.hval);
+    }
     if (L.nbchunks > 0)
         LAUNCH("bchunk", dev::k_bchunk, dim3(nb(L.nbchunks, 128)), dim3(128), st, L.nbchunks, L.bcontrib,
                            L.bchunk_begin, L.bchunk_len, ej, L.bpart);
     if (L.nv > 0)
         LAUNCH("bfinal", dev::k_bfinal, dim3(nb(L.nv, 128)), dim3(128), st, L.nv, L.bv_chunk_begin, L.voff,
                            L.vdim, L.bpart, L.b);
-    if (L.nheavy_b > 0)
-        LAUNCH("bfinal_heavy", dev::k_bfinal_heavy, dim3((unsigned)L.nheavy_b), dim3(256), st, L.heavy_b,
-                           L.bv_chunk_begin, L.voff, L.vdim, L.bpart, L.b);
+    if (L.nheavy_b > 0) {
+        LAUNCH("bfinal_heavy", dev::k_heavy_split<6>, dim3((unsigned)(L.nheavy_b * dev::kHeavySplit)), dim3(256), st,
+               L.heavy_b, L.bv_chunk_begin, L.bpart, L.heavy_scratch);
+        LAUNCH("bfinal_heavy", dev::k_heavy_final<6>, dim3((unsigned)L.nheavy_b), dim3(64), st, L.heavy_b, L.voff,
+               L.vdim, (const int32_t *)nullptr, L.heavy_scratch, L.b);
+    }
 }
 
 void launch_scatter_lanes(const DevPlan &L, hipStream_t st) {

@@ -324,6 +324,7 @@ int upload_device(deftri_ctx *ctx) {
         L.nheavy_h = (int64_t)hh.size(); L.nheavy_b = (int64_t)hb.size();
         if (!hh.empty()) PUT(L.heavy_h, hh);
         if (!hb.empty()) PUT(L.heavy_b, hb);
+        if ((rc = dalloc(ctx, &L.heavy_scratch, 32 * std::max<int64_t>(36 * L.nheavy_h, 6 * L.nheavy_b)))) return rc;
     }
     if ((rc = dalloc(ctx, &L.b, S.ndof))) return rc;
     L.arena_size = S.arena_size; L.vec_size = S.vec_size;
