@@ -267,8 +267,12 @@ __global__ void k_hchunk(int64_t nchunks, const uint64_t *__restrict__ contrib, 
     int rows = 0, cols = 0;
     int64_t b0 = cbeg[c];
     int n = clen[c];
+    // the next record is fetched while the current one is accumulated (breaks the
+    // record -> Jacobian load chain of consecutive contributions)
+    uint64_t rec_next = n > 0 ? contrib[b0] : 0;
     for (int t = 0; t < n; t++) {
-        uint64_t rec = contrib[b0 + t];
+        const uint64_t rec = rec_next;
+        if (t + 1 < n) rec_next = contrib[b0 + t + 1];
         int64_t e = (int64_t)(rec & 0xFFFFFFFFFFull);
         int kind = (int)((rec >> 40) & 0xF), rcol = (int)((rec >> 44) & 0xF), rrow = (int)((rec >> 48) & 0xF);
         const double *Jc, *Jr, *er;
