@@ -60,8 +60,7 @@ __global__ void k_ba_edges(int E, const int32_t *__restrict__ ept, const int32_t
     const double e0 = obs[2 * e] - (double)uv[0], e1 = obs[2 * e + 1] - (double)uv[1];
     const double om = info[e];
     const double c2 = e0 * (om * e0) + e1 * (om * e1);     // _error.dot(information() * _error)
-    err[2 * (int64_t)e] = e0;
-    err[2 * (int64_t)e + 1] = e1;
+    reinterpret_cast<double2 *>(err)[e] = double2{e0, e1};        // 16-B stores (per-edge records are 16-B aligned)
     chi2raw[e] = c2;
     double rho0 = c2, rho1 = 1.0;
     if (robust[e]) ba_huber(hdelta, c2, rho0, rho1);
@@ -74,27 +73,28 @@ __global__ void k_ba_edges(int E, const int32_t *__restrict__ ept, const int32_t
     for (int i = 0; i < 6; i++) A[i] = -(double)jf[i];
     double R[9];
     quat_to_mat(T.r, R);
+    {
+        double jp[6];
 #pragma unroll
-    for (int r = 0; r < 2; r++)
+        for (int r = 0; r < 2; r++)
 #pragma unroll
-        for (int c = 0; c < 3; c++)
-            Jp[6 * (int64_t)e + 3 * r + c] = A[3 * r] * R[c] + A[3 * r + 1] * R[3 + c] + A[3 * r + 2] * R[6 + c];
+            for (int c = 0; c < 3; c++)
+                jp[3 * r + c] = A[3 * r] * R[c] + A[3 * r + 1] * R[3 + c] + A[3 * r + 2] * R[6 + c];
+        double2 *o2 = reinterpret_cast<double2 *>(Jp + 6 * (int64_t)e);
+        o2[0] = double2{jp[0], jp[1]}; o2[1] = double2{jp[2], jp[3]}; o2[2] = double2{jp[4], jp[5]};
+    }
     const double x = pc[0], y = pc[1], z = pc[2];
     // SE3deriv rows: [0 z -y 1 0 0; -z 0 x 0 1 0; y -x 0 0 0 1]
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         const double a0 = A[3 * r], a1 = A[3 * r + 1], a2 = A[3 * r + 2];
-        double *o = JT + 12 * (int64_t)e + 6 * r;
-        o[0] = a1 * (-z) + a2 * y;
-        o[1] = a0 * z + a2 * (-x);
-        o[2] = a0 * (-y) + a1 * x;
-        o[3] = a0;
-        o[4] = a1;
-        o[5] = a2;
+        double2 *o2 = reinterpret_cast<double2 *>(JT + 12 * (int64_t)e + 6 * r);
+        o2[0] = double2{a1 * (-z) + a2 * y, a0 * z + a2 * (-x)};
+        o2[1] = double2{a0 * (-y) + a1 * x, a0};
+        o2[2] = double2{a1, a2};
     }
     wgt[e] = rho1 * om;                                    // robustInformation = rho' * Omega
-    wr[2 * (int64_t)e] = (-(om * e0)) * rho1;              // omega_r = -Omega e; omega_r *= rho'
-    wr[2 * (int64_t)e + 1] = (-(om * e1)) * rho1;
+    reinterpret_cast<double2 *>(wr)[e] = double2{(-(om * e0)) * rho1, (-(om * e1)) * rho1};   // omega_r = -Omega e; *= rho'
 }
 
 // per point: Hll = sum J_p^T w J_p, bl = sum J_p^T omega_r, and the Hpl block of each (point, free
