@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 1
+#define DEFTRI_ABI_VERSION 2
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -167,6 +167,11 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *params, deftri_repo
    in half of the free device memory.  Pays off when the factorization is latency-bound (1k-30k
    correspondences: 11-24% per iteration); at C2 a 3-lane round costs 2.1 trials. */
 int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes);
+/* Jacobians used by deftri_arap_optimization: 0 (default) g2o's numeric central differences
+   (delta 1e-9) for the ARAP and depth edges, as the reference (EdgeARAP has no linearizeOplus,
+   g2oTypes.h:341; its analytic one is commented out, g2oTypes.cc:308-331); 1 the closed-form
+   Jacobians (an opt-in speed-up, not the reference's arithmetic). */
+int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic);
 /* Copy the current state back: points [P*3], scales [S], tg [Q*7] (any may be NULL). */
 int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg);
 /* Reset the device state to the uploaded initial values (no re-analysis). */
@@ -232,10 +237,23 @@ typedef struct deftri_keyframe {
     int32_t n_obs;
 } deftri_keyframe;
 
+/* One entry of Map::mGTransformation_ (Modules/Map/Map.cc:323-343): the transformation stored for
+   the ordered KeyFrame-id pair (kf1, kf2).  insertGlobalKeyFramesTransformation stores T for
+   (kf1, kf2) and T.inverse() (Sophus, fp32) for (kf2, kf1): pass both entries. */
+typedef struct deftri_global_entry {
+    int64_t kf1, kf2;
+    double  t[7];                 /* qx qy qz qw tx ty tz */
+} deftri_global_entry;
+
 typedef struct deftri_map {
     int32_t n_keyframes;
     deftri_keyframe *keyframes;   /* in the reference's unordered_map iteration order */
-    double global_t[7];           /* Map::getGlobalKeyFramesTransformation(kf1,kf2) in; written back (out) */
+    double global_t[7];           /* out: the optimized T_g, stored by the reference as (0, 1) (:1007).
+                                     in (legacy, only when n_global == 0): T for the first pair */
+    int32_t n_global;             /* in: entries of the map's global-transformation table */
+    const deftri_global_entry *globals;   /* every pair (kf1, kf2) of the graph starts from
+                                     getGlobalKeyFramesTransformation(kf1.id, kf2.id) (:664): the
+                                     entry for that ordered id pair, identity when absent */
 } deftri_map;
 
 /* arapOptimization(Map*, rep, global, arap, alpha, beta, depthError, nIt, optimizationUpdate)

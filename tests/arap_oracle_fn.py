@@ -13,7 +13,7 @@ from oracle import graph_ref, oracle
 def oracle_arap(m, rep, glob, arap, alpha, beta, depth_sigma, n_it):
     kw, info = graph_ref.build_arap_graph(m, rep, arap, depth_sigma)
     prob = Problem(**kw)
-    ref = oracle.solve_lm(prob, int(n_it), analytic=True)
+    ref = oracle.solve_lm(prob, int(n_it), analytic=False)   # the reference: numeric J
     upd = 0.0
     for k in range(prob.n_points):
         mp = m.map_points[info["point_ids"][k]]
@@ -24,6 +24,5 @@ def oracle_arap(m, rep, glob, arap, alpha, beta, depth_sigma, n_it):
     for s, kid in enumerate(info["scale_kf"]):
         m.keyframes[kid].estimated_depth_scale = float(ref["scales"][s])
     if prob.n_pairs:
-        ids = sorted(m.keyframes)
-        m.insert_global_T(ids[0], ids[1], SE3f.from7(ref["tg"][-1]))
+        m.insert_global_T(0, 1, SE3f.from7(ref["tg"][-1]))      # reference :1007 (KF ids 0, 1)
     return upd

@@ -110,3 +110,24 @@ def test_graph_errors(host):
     with pytest.raises(capi.DeftriError) as e:
         host.build_graph(m, 1.0, 2e5, np.float32(0.003))
     assert e.value.code == -6
+
+
+def test_global_transform_lookup_per_pair(host):
+    """Every KF pair starts from getGlobalKeyFramesTransformation(kf1.id, kf2.id)
+    (g2oBundleAdjustment.cc:664, Map.cc:332-343): T for the stored (0, 1) entry, its fp32 inverse for
+    (1, 0), identity otherwise.  With 3 KFs in reverse-insertion order the pair holding the stored T
+    is the last one, so a first-pair-only lookup would start it from identity."""
+    from deftri.mapmodel import SE3f, mat_from_quat
+    m, _ = sim.simulate_multi_view(n=150, k=3, seed=6)
+    q = np.array([0.02, -0.01, 0.03, 1.0]); q /= np.linalg.norm(q)
+    m.insert_global_T(0, 1, SE3f(mat_from_quat(q).astype(np.float32), np.array([0.004, -0.002, 0.001], np.float32)))
+    for _round in range(2):          # second round: the map carries the written-back T
+        kw, info = graph_ref.build_arap_graph(m, 1.0, 2e5, np.float32(0.003))
+        pr = Problem(**kw)
+        pc = host.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        compare(pr, pc)
+        ident = np.array([0, 0, 0, 1, 0, 0, 0], float)
+        non_identity = [not np.allclose(t, ident) for t in pc.tg.reshape(-1, 7)]
+        assert sum(non_identity) == 1, non_identity        # only the pair (KF 1, KF 0) has a stored T
+        t_new = pc.tg.reshape(-1, 7)[int(np.argmax(non_identity))] * np.r_[1, 1, 1, 1, 1.5, 1.5, 1.5]
+        m.insert_global_T(0, 1, SE3f.from7(t_new))

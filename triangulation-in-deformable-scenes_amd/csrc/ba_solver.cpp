@@ -62,6 +62,7 @@ struct deftri_ba_ctx {
     double *hpin = nullptr;                   // pinned host staging of the per-trial scalars
     int *ipin = nullptr;
     int32_t n_free_points = 0;
+    int64_t n_free_points_global = 0;        // summed over the point shards
 };
 
 namespace {
@@ -177,10 +178,24 @@ int prepare_active(deftri_ba_ctx *ctx, int32_t level) {
     HIPOK(hipMemsetAsync(B.dxl, 0, sizeof(double) * 3 * (size_t)std::max(P, 1), ctx->st));
     HIPOK(hipStreamSynchronize(ctx->st));
     const int32_t nfp = *nfp_h;
+    // the pose-solve rule and the nothing-to-optimize exit must agree on every rank: they follow the
+    // free points of the whole graph, not of this rank's shard
+    int64_t nfp_global = nfp;
+    if (ctx->nranks > 1 || ctx->comm) {
+        double *d = B.Spart;
+        ctx->hpin[8] = (double)nfp;
+        HIPOK(hipMemcpyAsync(d, ctx->hpin + 8, sizeof(double), hipMemcpyHostToDevice, ctx->st));
+        int rc = allreduce(ctx, d, 1, 0);
+        if (rc) return rc;
+        HIPOK(hipMemcpyAsync(ctx->hpin + 8, d, sizeof(double), hipMemcpyDeviceToHost, ctx->st));
+        HIPOK(hipStreamSynchronize(ctx->st));
+        nfp_global = (int64_t)ctx->hpin[8];
+    }
     B.nfree = nfree;
     B.ns = 6 * nfree;
-    B.dense_positive = nfp == 0 ? 1 : 0;      // poses only: LinearSolverDense (Eigen LDLT, isPositive)
+    B.dense_positive = nfp_global == 0 ? 1 : 0;   // poses only: LinearSolverDense (Eigen LDLT, isPositive)
     ctx->n_free_points = nfp;
+    ctx->n_free_points_global = nfp_global;
     const int64_t NE = (int64_t)B.ns * (B.ns + 1) / 2 + B.ns;
     if (B.ns > ctx->cap_ns) {
         int rc;
@@ -464,7 +479,7 @@ int deftri_ba_solve_lm(deftri_ba_ctx *ctx, const deftri_lm_params *prm, int32_t 
     const int max_trials = prm->max_trials > 0 ? prm->max_trials : 10;
     const double tau = prm->tau > 0 ? prm->tau : 1e-5;
     auto t_start = std::chrono::steady_clock::now();
-    if (B.ns == 0 && ctx->n_free_points == 0) {      // SparseOptimizer::optimize: nothing to optimize
+    if (B.ns == 0 && ctx->n_free_points_global == 0) {   // SparseOptimizer::optimize: nothing to optimize
         R.status = DEFTRI_STATUS_TERMINATE;
         return 0;
     }

@@ -304,9 +304,18 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             Mesh M;
             if (!build_mesh(pos1, n1, M, err)) return false;
             // T_global: map transformation for (kf1, kf2) or identity (:664-677)
-            double Tg[7];
-            for (int i = 0; i < 7; i++) Tg[i] = map.global_t[i];
-            if (a > 0 || b > 1) { Tg[0] = Tg[1] = Tg[2] = 0; Tg[3] = 1; Tg[4] = Tg[5] = Tg[6] = 0; }
+            // getGlobalKeyFramesTransformation(k2->first, k1->first) = (kf1.id, kf2.id): the table
+            // entry for that ordered pair, a default (identity) SE3f when absent (Map.cc:332-343)
+            double Tg[7] = {0, 0, 0, 1, 0, 0, 0};
+            if (map.n_global > 0) {
+                for (int32_t e = 0; e < map.n_global; e++)
+                    if (map.globals[e].kf1 == kf1.id && map.globals[e].kf2 == kf2.id) {
+                        for (int i = 0; i < 7; i++) Tg[i] = map.globals[e].t[i];
+                        break;
+                    }
+            } else if (a == 0 && b == 1) {
+                for (int i = 0; i < 7; i++) Tg[i] = map.global_t[i];
+            }
             {
                 float tn = std::sqrt((float)Tg[4] * (float)Tg[4] + (float)Tg[5] * (float)Tg[5] + (float)Tg[6] * (float)Tg[6]);
                 double qn = std::sqrt(Tg[0] * Tg[0] + Tg[1] * Tg[1] + Tg[2] * Tg[2] + Tg[3] * Tg[3]);

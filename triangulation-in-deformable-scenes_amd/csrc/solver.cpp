@@ -108,6 +108,7 @@ struct deftri_ctx {
     // map-level graph (deftri_arap_build_graph)
     GraphResult graph;
     // speculative lambda lanes (see Lane)
+    int analytic_jac = 0;                   // deftri_arap_optimization: 0 g2o numeric (reference), 1 analytic
     int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES, else by factorization size)
     std::vector<Lane> lanes;                // device buffers: per uploaded problem
     DevPlan LB;                             // batched plan view: lanes' arenas / inverses / vectors / flags
@@ -565,6 +566,12 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
 
 const char *deftri_last_error(const deftri_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic) {
+    if (!ctx || analytic < 0 || analytic > 1) return DEFTRI_E_ARG;
+    ctx->analytic_jac = analytic;
+    return 0;
+}
+
 int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes) {
     if (!ctx || lanes < 0 || lanes > kMaxLanes) return DEFTRI_E_ARG;
     ctx->max_lanes = lanes;
@@ -778,7 +785,8 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                         R.trials_rejected++;
                     }
                     qmax++;
-                    if (!(rho < 0 && qmax < max_trials)) done = true;
+                    // g2o: `if (!g2o_isfinite(_currentLambda)) break;` after a rejected trial
+                    if (!(rho < 0 && qmax < max_trials) || !std::isfinite(lambda)) done = true;
                 }
                 if (acc >= 0) adopt_lane_state(ctx, acc);
             }
@@ -820,6 +828,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 ni *= 2;
                 pop_state(ctx);
                 R.trials_rejected++;
+                if (!std::isfinite(lambda)) { qmax++; break; }   // g2o OptimizationAlgorithmLevenberg::solve
             }
             qmax++;
         } while (rho < 0 && qmax < max_trials);
@@ -1092,7 +1101,7 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
     prm.n_iterations = n_iterations;
     prm.max_trials = 10;
     prm.tau = 1e-5;
-    prm.analytic_jacobians = 1;
+    prm.analytic_jacobians = ctx->analytic_jac;   // 0 (default): g2o numeric ARAP/depth Jacobians, as the reference
     rc = deftri_solve_lm(ctx, &prm, report);
     if (rc) return rc;
     const GraphResult &g = ctx->graph;

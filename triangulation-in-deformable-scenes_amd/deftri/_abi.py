@@ -84,8 +84,13 @@ class KeyFrameC(C.Structure):
     ]
 
 
+class GlobalEntryC(C.Structure):
+    _fields_ = [("kf1", i64), ("kf2", i64), ("t", f64 * 7)]
+
+
 class MapC(C.Structure):
-    _fields_ = [("n_keyframes", i32), ("keyframes", P(KeyFrameC)), ("global_t", f64 * 7)]
+    _fields_ = [("n_keyframes", i32), ("keyframes", P(KeyFrameC)), ("global_t", f64 * 7),
+                ("n_global", i32), ("globals", P(GlobalEntryC))]
 
 
 class KernelStat(C.Structure):

@@ -44,6 +44,7 @@ def load():
                                               P(C.c_double), C.c_int64]),
         "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
         "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_set_jacobian_mode": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
         "deftri_triangulate_nrslam": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float),
                                                 P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float),
@@ -93,7 +94,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -166,7 +167,7 @@ class Context:
         """Speculative lambda lanes (0 = default, 1 = sequential trials); results are identical."""
         self._check(self.lib.deftri_set_lm_lanes(self.h, int(lanes)))
 
-    def solve_lm(self, n_iterations=10, analytic=True, tau=1e-5, max_trials=10, user_lambda=0.0, verbose=False):
+    def solve_lm(self, n_iterations=10, analytic=False, tau=1e-5, max_trials=10, user_lambda=0.0, verbose=False):
         prm = _abi.LMParams(n_iterations=n_iterations, max_trials=max_trials, tau=tau, user_lambda=user_lambda,
                             analytic_jacobians=1 if analytic else 0, verbose=1 if verbose else 0)
         rep = _abi.Report()
@@ -244,7 +245,9 @@ class Context:
         return x1, x2, v.astype(bool)
 
     def arap_optimization(self, m, rep_weight, global_weight, arap_weight, alpha, beta, depth_error,
-                          n_iterations, want_update=True):
+                          n_iterations, want_update=True, analytic=False):
+        """analytic=False (default): g2o numeric ARAP/depth Jacobians, the reference's arithmetic."""
+        self._check(self.lib.deftri_set_jacobian_mode(self.h, 1 if analytic else 0))
         mc, keep = m.to_c()
         upd = C.c_double(0.0)
         rep = _abi.Report()

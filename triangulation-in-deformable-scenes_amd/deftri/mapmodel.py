@@ -219,12 +219,17 @@ class Map:
         m = _abi.MapC()
         m.n_keyframes = len(order)
         m.keyframes = C.cast(kfs, C.POINTER(_abi.KeyFrameC))
-        if len(order) >= 2:
-            # read-back key of g2oBundleAdjustment.cc:664: (k2->first, k1->first) of the first pair
-            T = self.get_global_T(order[1], order[0])
-            m.global_t[:] = list(T.as7())
-        else:
-            m.global_t[:] = [0, 0, 0, 1, 0, 0, 0]
+        m.global_t[:] = [0, 0, 0, 1, 0, 0, 0]
+        # Map::mGTransformation_ (both directions, as insertGlobalKeyFramesTransformation stores
+        # them): every pair looks up (k2->first, k1->first), g2oBundleAdjustment.cc:664
+        entries = sorted(self.global_T.items())
+        glob = (_abi.GlobalEntryC * max(1, len(entries)))()
+        for n, ((k1, k2), T) in enumerate(entries):
+            glob[n].kf1, glob[n].kf2 = int(k1), int(k2)
+            glob[n].t[:] = list(T.as7())
+        m.n_global = len(entries)
+        m.globals = C.cast(glob, C.POINTER(_abi.GlobalEntryC))
+        keep["globals"] = glob
         return m, keep
 
     def from_c(self, m, keep):
@@ -236,6 +241,6 @@ class Map:
                 if mp is not None:
                     mp.position = pos[i].copy()
         if m.n_keyframes >= 2:
-            ids = sorted(self.keyframes.keys())
-            # reference hard-codes insertGlobalKeyFramesTransformation(0, 1, T) (:1007)
-            self.insert_global_T(ids[0], ids[1], SE3f.from7(np.array(m.global_t[:])))
+            # the reference hard-codes insertGlobalKeyFramesTransformation(0, 1, T) (:1007): KF ids 0
+            # and 1, whatever the map's keyframe ids are
+            self.insert_global_T(0, 1, SE3f.from7(np.array(m.global_t[:])))
