@@ -1,23 +1,34 @@
 """Headline benchmark: LM iterations/s of the g2o ARAP solve (arapOptimization's
-optimizer.optimize(nIterations), reference Modules/Optimization/g2oBundleAdjustment.cc) at
-config C2 of BASELINE.json: 100k two-view correspondences, per GPU.
+optimizer.optimize(nIterations), reference Modules/Optimization/g2oBundleAdjustment.cc:959-962) at
+config C2 of BASELINE.json: 100k two-view correspondences.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--corr 100000] [--no-cpu-baseline]
+                  [--analytic] [--replicas] [--cpu-full-iteration]
   python bench.py --workload ba [--ba-points 500000] [--ba-kfs 8] [--ba-scaling strong|weak] ...
 
-A "step" is one accepted LM iteration of the device solver (linearize, assemble H, then up to 10
-damped trials of scatter + multifrontal LDL^T + solve + update + chi2 each).  The scene is
-synthetic (deftri.sim: the reference's simulation recipe scaled to n points, seed 1+rank); the
-graph is built on the host once, then resident in HBM before the timed region starts.
+A "step" is one LM iteration of the device solver (linearize with g2o's numeric ARAP/depth
+Jacobians — the reference's arithmetic — assemble H, then up to 10 damped trials of scatter +
+multifrontal LDL^T + solve + update + chi2 each).  The scene is synthetic (deftri.sim: the
+reference's simulation recipe scaled to n points); the graph is built on the host once, then
+resident in HBM before the timed region starts.
 
-Multi-GPU: the path does not shard (one ARAP graph is one coupled sparse system), so N ranks run
-N independent replicas on their own scenes (weak scaling, no data-path collective); the barrier
-and the max-over-ranks time use torch.distributed.
+Multi-GPU (N > 1): ONE C2 problem point-sharded over the N ranks (DistPlan, csrc/symbolic.cpp: a
+subtree of the nested-dissection tree per rank, separator fronts on the leading ranks; per LM
+trial RCCL send/recv of one packed contribution block, one forward vector and one boundary
+solution per rank, all-reduce of chi2 / rho denominator / pivot flags) — strong scaling.
+--replicas runs N independent C2 problems instead (weak scaling, no collective).  The barrier and
+the max-over-ranks time use torch.distributed.
 
 Printed roofline: the dominant factorization kernel ("update": the Schur-complement GEMM of each
 front) — algorithmic flops of one factorization ÷ its summed device time, both from a profiled
 trial run right after the timed region with HIP events on the solver's own stream.  FP64 peak
 78.6 TFLOP/s is AMD's MI355X specification (the microarch guide lists no FP64 row).
+
+CPU baseline: the oracle (oracle/deftri_oracle.c: the reference LM restated in scalar C, g2o
+numeric Jacobians, SimplicialLDLT) on the SAME full-size C2 problem with the device plan's
+elimination order, 1 thread: one linearization and one trial are measured; the per-iteration
+figure is linearization + (GPU trials per iteration) x trial.  --cpu-full-iteration times a
+complete first LM iteration instead.
 """
 import argparse
 import json
@@ -55,28 +66,45 @@ def build_problem(n, seed):
     return p
 
 
-def cpu_baseline(n_full, full_flops, gpu_trials_per_iter, n_sample=10000):
-    """The oracle (oracle/deftri_oracle.c, scalar C, 1 thread) on a 10k-correspondence scene:
-    one LM iteration timed; scaled to the 100k workload by the factorization flop ratio of the
-    same nested-dissection ordering (the factorization is >95 % of the oracle's time)."""
+def host_cpu_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_baseline(prob, order, gpu_trials_per_iter, full_iteration=False):
+    """The oracle (scalar C, 1 thread) on the benchmark's own full-size problem, eliminating in the
+    device plan's order.  Measured: one linearization + one LM trial (or, with full_iteration, the
+    first LM iteration with all its trials)."""
     sys.path.insert(0, str(ROOT))
     from oracle import oracle
-    p = build_problem(n_sample, 1)
-    host = capi.Context(-1)
-    host.analyse(p)
-    f_sample = host.plan_stats()["factor_flops"]
-    host.close()
+    oracle.set_vertex_order(order)
     t = time.perf_counter()
-    r = oracle.solve_lm(p, 1, analytic=True)["report"]
+    r = oracle.solve_lm(prob, 1, analytic=False, max_trials=10 if full_iteration else 1)["report"]
     dt = time.perf_counter() - t
+    oracle.set_vertex_order(None)
     trials = max(r["trials_total"], 1)
-    per_trial = dt / trials
-    t_iter_full = per_trial * (full_flops / f_sample) * gpu_trials_per_iter
-    return {"value": 1.0 / t_iter_full, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"oracle LM, 1 iteration ({trials} trials) on {p.n_points // 2} correspondences x 2 views: "
-                      f"{dt:.1f} s measured; extrapolated to the {n_full}-point workload by the "
-                      f"factorization flop ratio {full_flops / f_sample:.1f}x at "
-                      f"{gpu_trials_per_iter:.2f} trials/iteration"}
+    lin = r["ms_linearize"] * 1e-3
+    per_trial = (r["ms_factor"] + r["ms_solve"] + r["ms_update"]) * 1e-3 / trials
+    if full_iteration:
+        t_iter, how = dt, f"first LM iteration measured whole ({trials} trials, {dt:.1f} s)"
+    else:
+        t_iter = lin + gpu_trials_per_iter * per_trial
+        how = (f"measured: linearization {lin:.2f} s + one trial {per_trial:.2f} s (factor + solve + update + chi2); "
+               f"per iteration = linearization + {gpu_trials_per_iter:.2f} trials (the GPU's trials per iteration)")
+    info = host_cpu_info()
+    return {"value": 1.0 / t_iter, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"oracle LM (g2o numeric J, SimplicialLDLT in the device plan's elimination order) on the full "
+                      f"{prob.n_points // 2}-correspondence x 2-view problem, 1 thread; {how}; "
+                      f"host {info['cpu_model']}, nproc {info['nproc']}",
+            "seconds_per_iteration": round(t_iter, 3), "seconds_per_trial": round(per_trial, 3),
+            "seconds_linearize": round(lin, 3), "nproc": info["nproc"], "cpu_model": info["cpu_model"]}
 
 
 def ba_cpu_baseline(prob, n_iter=3):
@@ -192,6 +220,12 @@ def main():
     ap.add_argument("--ba-scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--lanes", type=int, default=0,
                     help="speculative LM lambda lanes (0: library default, 1: sequential trials)")
+    ap.add_argument("--analytic", action="store_true",
+                    help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: N independent C2 problems (weak scaling) instead of one point-sharded problem")
+    ap.add_argument("--cpu-full-iteration", action="store_true",
+                    help="CPU baseline: time the oracle's whole first LM iteration (all trials)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -201,7 +235,7 @@ def main():
     if not have_gpu:
         raise SystemExit("bench.py needs a gfx950 GPU (no CPU path)")
     # one process per GPU (RCCL); DEFTRI_DIST_BACKEND=gloo + DEFTRI_GPU_OVERRIDE=0 rehearse several
-    # ranks on one GPU (the path has no data-path collective: only the barrier and the timing reduce)
+    # ranks on one GPU (the sharded solve then moves its transfers through host memory over gloo)
     backend = os.environ.get("DEFTRI_DIST_BACKEND", "nccl")
     gpu = int(os.environ.get("DEFTRI_GPU_OVERRIDE", local))
     torch.cuda.set_device(gpu)
@@ -214,24 +248,32 @@ def main():
     if args.workload == "ba":
         return main_ba(args, world, rank, gpu, backend)
 
+    sharded = world > 1 and not args.replicas
     t0 = time.perf_counter()
-    prob = build_problem(args.corr, 1 + rank)
+    prob = build_problem(args.corr, 1 if sharded else 1 + rank)
     log(f"[rank {rank}] graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
     ctx = capi.Context(gpu)
+    if sharded:
+        from deftri import dist as ddist
+        if backend == "nccl":
+            ddist.init_rccl(ctx, rank, world)
+        else:
+            ctx.dist_set_transport(world, rank, ddist.torch_transport())
     t0 = time.perf_counter()
     ctx.upload(prob)
     ctx.set_lm_lanes(args.lanes)
     log(f"[rank {rank}] upload + symbolic analysis {time.perf_counter() - t0:.1f}s")
+    analytic = args.analytic
 
     if args.warmup > 0:
-        ctx.solve_lm(args.warmup, analytic=True)
+        ctx.solve_lm(args.warmup, analytic=analytic)
     ctx.reset_state()
 
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    rep = ctx.solve_lm(args.steps, analytic=True)
+    rep = ctx.solve_lm(args.steps, analytic=analytic)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -242,18 +284,23 @@ def main():
     if iters != args.steps:
         log(f"[rank {rank}] WARNING: LM terminated after {iters} of {args.steps} iterations")
 
-    t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
+    if sharded:      # one problem: every rank ran the same iterations; the job takes the slowest rank
+        t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
+        it_sum, tr_sum = iters, rep["trials_total"]
+    else:
+        t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
 
     # profiled trial (HIP events on the solver stream), at the final lambda of the timed run
+    # (a collective on a sharded context: each rank times its own part of the same trial)
     stats = ctx.profile_trial(rep["lambda_final"])
     upd = stats["update"]
-    factor_flops = rep["factor_flops"]
+    factor_flops = rep["factor_flops_total"] if sharded else rep["factor_flops"]
     achieved = upd["flops"] / (upd["ms"] * 1e-3) / 1e12
     # HBM bytes of k_update per factorization from the committed rocprofv3 PMC pass (tools/gpu_pmc.sh +
     # tools/pmc_summary.py), attached only when it was collected on this same plan
     traffic = None
     pmc = sorted(ROOT.glob("profiles/*_pmc_k_update.json"))
-    if pmc:
+    if pmc and not sharded:
         pj = json.loads(pmc[-1].read_text())
         if abs(pj.get("update_flops_per_factorization", -1) - upd["flops"]) < 1e-6 * upd["flops"]:
             traffic = pj["traffic_bytes_per_factorization"]
@@ -263,30 +310,35 @@ def main():
                 "traffic": traffic, "traffic_unit": "bytes per factorization (all k_update launches)",
                 "launches": upd["launches"],
                 "avg_launch_us": round(1e3 * upd["ms"] / max(upd["launches"], 1), 3),
-                "flops_per_factorization": upd["flops"]}
+                "flops_per_factorization": upd["flops"], "rank": rank}
     trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         t0 = time.perf_counter()
-        cpu = cpu_baseline(args.corr, factor_flops, rep["trials_total"] / max(iters, 1))
+        cpu = cpu_baseline(prob, ctx.vertex_order(), rep["trials_total"] / max(iters, 1), args.cpu_full_iteration)
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     if rank == 0:
         ms_per_step = 1e3 * t_max / max(iters, 1)
+        trials_per_it = tr_sum / max(it_sum, 1)
         out = {
             "metric": BASELINE_METRIC,
             "value": it_sum / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2" if args.corr == 100000 else f"two-view-{args.corr}", "correspondences_per_gpu": args.corr, "views": 2,
+            "scaling": "strong" if sharded or world == 1 else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "C2" if args.corr == 100000 else f"two-view-{args.corr}",
+                       "correspondences": args.corr, "views": 2,
                        "points": prob.n_points, "arap_edges": len(prob.arap_pair), "unknowns": rep["n_unknowns"],
                        "fronts": rep["n_fronts"], "nnz_factor": rep["nnz_factor"],
                        "factor_gflop": round(factor_flops / 1e9, 3),
-                       "trials_per_iteration": round(tr_sum / max(it_sum, 1), 3),
+                       "jacobians": "analytic" if analytic else "g2o numeric (reference)",
+                       "trials_per_iteration": round(trials_per_it, 3),
+                       "ms_per_trial": round(ms_per_step / max(trials_per_it, 1e-9), 3),
                        "lm_lanes": rep["lanes"],
                        "trials_executed_per_iteration": round(rep["trials_executed"] / max(iters, 1), 3),
-                       "parallelism": f"replicas{world}"},
+                       "parallelism": (f"points{world}" if sharded else f"replicas{world}") if world > 1 else "single"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "breakdown_ms": {"total": rep["ms_total"], "linearize": rep["ms_linearize"],

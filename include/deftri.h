@@ -142,6 +142,11 @@ typedef struct deftri_report {
        including those past the accepted one (their results are discarded) */
     int32_t lanes;
     int32_t trials_executed;
+    /* point-sharded solves (deftri_dist_*): this rank, the rank count, the factorization flops of
+       all ranks (factor_flops and nnz_factor above are this rank's fronts) */
+    int32_t rank;
+    int32_t nranks;
+    double  factor_flops_total;
 } deftri_report;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -172,6 +177,40 @@ int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes);
    g2oTypes.h:341; its analytic one is commented out, g2oTypes.cc:308-331); 1 the closed-form
    Jacobians (an opt-in speed-up, not the reference's arithmetic). */
 int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic);
+/* ---- point-sharded ARAP solve (multi-GPU) -------------------------------------------------
+   One context per GPU, rank `rank` of `nranks`; every rank uploads the same full problem.  The
+   nested-dissection tree is split by rank ranges (a rank owns one subtree, the leading ranks of
+   each range also the separator fronts above it); each rank linearizes the edges whose
+   first-eliminated vertex it owns, assembles and factors its fronts, and per LM trial sends one
+   packed contribution block (lower triangle) up to the owner of its top front's parent, one
+   forward-update vector up and receives the boundary solution back; chi2, dx.(lambda dx + b) and
+   the zero-pivot flags are all-reduced (sum), the lambda init takes the max of the all-reduced
+   diagonal.  Every rank then holds the solution of its own vertices and of its top front's
+   boundary vertices (deftri_dist_vertex_owner tells which rank is authoritative for each vertex).
+   Transport: RCCL (ncclCommInitRank from a deftri_rccl_unique_id shared by the caller; send/recv
+   and all-reduce on the solver stream, over xGMI) or a caller callback through host memory (tests:
+   gloo).  Set before deftri_problem_upload / deftri_problem_analyse (it discards the uploaded
+   problem); nranks == 1 restores the single-GPU plan.  Diagnostics entry points other than
+   deftri_eval_chi2 refuse a sharded context.
+   Callback: op 0 all-reduce sum / 1 all-reduce max of n doubles in place (peer = -1), 2 send n
+   doubles to `peer`, 3 receive n doubles from `peer`; returns 0 on success.  Every rank makes the
+   calls in the same global order. */
+typedef int (*deftri_xfer_fn)(void *user, int32_t op, int32_t peer, double *buf, int64_t n);
+int deftri_dist_init_rccl(deftri_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int deftri_dist_set_transport(deftri_ctx *ctx, int32_t nranks, int32_t rank, deftri_xfer_fn fn, void *user);
+/* Elimination order of the analysed plan: order[k] = vertex [T_g per pair][scales][points]
+   eliminated k-th (nv entries). */
+int deftri_plan_vertex_order(const deftri_ctx *ctx, int64_t *order, int64_t nv);
+/* Owning rank of every vertex [T_g per pair][scales][points] of the analysed problem (nv entries). */
+int deftri_dist_vertex_owner(const deftri_ctx *ctx, int32_t *owner, int64_t nv);
+/* 0/1 per edge of the analysed problem: edges this rank linearizes (any output may be NULL). */
+int deftri_dist_owned_edges(const deftri_ctx *ctx, uint8_t *rep, uint8_t *dep, uint8_t *arap);
+/* TEST ONLY: host emulation of this rank's damped solve (H_q + lambda on its diagonal) x = b_q, with
+   H_q, b_q this rank's partial system (row-major n x n, the sum over ranks is H, b), exchanging
+   through the callback transport; x receives the solution of the rank's own and boundary dofs. */
+int deftri_debug_plan_solve_dist(deftri_ctx *ctx, const double *Hq, double lambda, const double *bq, double *x,
+                                 int64_t n);
+
 /* Copy the current state back: points [P*3], scales [S], tg [Q*7] (any may be NULL). */
 int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg);
 /* Reset the device state to the uploaded initial values (no re-analysis). */

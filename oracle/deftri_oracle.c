@@ -668,10 +668,26 @@ static void nd_rec(const bsr *H, const problem *pb, const double *xy, int64_t *n
     for (int64_t i = 0; i < ns; i++) out[(*nout)++] = nodes[nl + nr + i];
 }
 
+/* An externally supplied elimination order (bench.py's CPU baseline: the device plan's nested
+   dissection, so the oracle's SimplicialLDLT runs the same fill and flop count as the device). */
+static int64_t *g_vorder = NULL, g_vorder_n = 0;
+void oracle_set_vertex_order(const int64_t *order, int64_t nv) {
+    free(g_vorder); g_vorder = NULL; g_vorder_n = 0;
+    if (!order || nv <= 0) return;
+    g_vorder = (int64_t *)malloc(sizeof(int64_t) * (size_t)nv);
+    memcpy(g_vorder, order, sizeof(int64_t) * (size_t)nv);
+    g_vorder_n = nv;
+}
+
 /* returns vertex permutation perm[k] = vertex eliminated k-th */
 static int64_t *nd_order(const bsr *H, const problem *pb) {
     const deftri_problem_desc *d = pb->d;
     int64_t P = d->n_points, nv = pb->nv;
+    if (g_vorder && g_vorder_n == nv) {
+        int64_t *o = (int64_t *)malloc(sizeof(int64_t) * (size_t)nv);
+        memcpy(o, g_vorder, sizeof(int64_t) * (size_t)nv);
+        return o;
+    }
     double *xy = (double *)malloc(sizeof(double) * 2 * (size_t)(P > 0 ? P : 1));
     for (int64_t p = 0; p < P; p++) {
         if (d->order_xy) { xy[2 * p] = d->order_xy[2 * p]; xy[2 * p + 1] = d->order_xy[2 * p + 1]; }

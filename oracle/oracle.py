@@ -81,6 +81,16 @@ def damped_solve(prob, lam, rhs, analytic=True):
     return x
 
 
+def set_vertex_order(order):
+    """Elimination order (vertex eliminated k-th) for the oracle's LDL^T; None restores its own
+    nested dissection."""
+    if order is None:
+        lib().oracle_set_vertex_order(None, C.c_int64(0))
+        return
+    o = np.ascontiguousarray(order, dtype=np.int64)
+    lib().oracle_set_vertex_order(_p(o, C.c_int64), C.c_int64(len(o)))
+
+
 def solve_lm(prob, n_iterations=10, analytic=False, tau=1e-5, max_trials=10, verbose=False):
     A = _abi()
     d = prob.to_desc()

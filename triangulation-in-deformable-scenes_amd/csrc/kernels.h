@@ -33,7 +33,7 @@ struct DevProblem {
 };
 
 struct FrontDev {
-    const int32_t *m, *s, *parent, *nchild, *child0, *child1, *direct;
+    const int32_t *m, *s, *parent, *nchild, *child0, *child1, *direct, *rhs_bnd;
     const int64_t *arena_off, *vec_off, *rows_off, *bmap_off, *inv_off;
     const int32_t *rows, *bmap;
 };
@@ -106,11 +106,24 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
 void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);   // lane 0 / one lane
 void launch_scatter_lanes(const DevPlan &L, hipStream_t st);            // L.nlanes lanes, L.lo.lam
-void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev);
-void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st);
+// point-sharded plan: called by launch_factor before level h (contribution blocks from other ranks),
+// by launch_solve before forward level h and after backward level h (DistPlan transfers of that level)
+enum { kHookFactor = 0, kHookForward = 1, kHookBackward = 2 };
+typedef void (*LevelHook)(void *user, int phase, int level);
+void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev,
+                   LevelHook hook = nullptr, void *hook_user = nullptr);
+void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st, const double *bpart = nullptr,
+                  LevelHook hook = nullptr, void *hook_user = nullptr);
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
-                double *out, hipStream_t st);
+                double *out, hipStream_t st, const double *w = nullptr);
+void launch_pack_cb(const DevPlan &L, int64_t arena_off, int m, int s, double *buf, hipStream_t st);
+void launch_ea_packed(const DevPlan &L, int64_t ea_off, int nea, const double *buf, hipStream_t st);
+void launch_gather_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st);
+void launch_scatter_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st);
+void launch_diag_entries(const DevPlan &L, double *diagv, hipStream_t st);
+void launch_absmax(int64_t n, const double *a, double *part, int nparts, double *out, hipStream_t st);
+void launch_int_to_double(int n, const int *a, double *out, hipStream_t st);
 void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st);
 // calculatePixelsStandDev partial sums (metrics.hip): 8 doubles per 256-match block
 void launch_pixel_partials(int nblk, const int32_t *blk_first, const int32_t *blk_last, const int32_t *blk_pair,

@@ -938,9 +938,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
 // ------------------------------------------------------------------------------------------
 // forward gather: v = [rhs of own rows; 0 on boundary rows] + the children's update vectors (slot 0
 // then slot 1: fixed order)
+// (point-sharded plan: the rank's top front starts its boundary rows from the rank's partial b of
+// those remote vertices, `bpart`; they travel up with the forward-update vector)
 __global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
-                                                    const double *__restrict__ rhs, double *__restrict__ vec,
-                                                    const LaneOff lo) {
+                                                    const double *__restrict__ rhs, const double *__restrict__ bpart,
+                                                    double *__restrict__ vec, const LaneOff lo) {
     int t = blockIdx.x;
     if (t >= ntask) return;
     vec += blockIdx.y * lo.vec;
@@ -948,7 +950,8 @@ __global__ void __launch_bounds__(256) k_fwd_gather(int ntask, const int32_t *__
     int m = fd.m[f], s = fd.s[f];
     const int32_t *rows = fd.rows + fd.rows_off[f];
     double *v = vec + fd.vec_off[f];
-    for (int r = threadIdx.x; r < m; r += blockDim.x) v[r] = (r < s) ? rhs[rows[r]] : 0.0;
+    const bool inject = bpart != nullptr && fd.rhs_bnd[f] != 0;
+    for (int r = threadIdx.x; r < m; r += blockDim.x) v[r] = (r < s) ? rhs[rows[r]] : (inject ? bpart[rows[r]] : 0.0);
     __syncthreads();
     for (int slot = 0; slot < fd.nchild[f]; slot++) {
         int c = (slot == 0) ? fd.child0[f] : fd.child1[f];
@@ -1152,15 +1155,16 @@ __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ d
 
 __global__ void __launch_bounds__(256) k_sum_partial(int64_t n, const double *__restrict__ a,
                                                      const double *__restrict__ b, double lambda, int mode,
-                                                     double *__restrict__ part) {
-    // mode 0: sum a ; 1: sum a*(lambda*a + b) ; 2: max |a| over diag handled elsewhere
+                                                     const double *__restrict__ w, double *__restrict__ part) {
+    // mode 0: sum a ; 1: sum a*(lambda*a + b) ; 3: sum a*(lambda*w*a + b) (point-sharded: w = 1 on
+    // this rank's dofs, so the lambda term counts every dof once over the ranks while b is partial)
     __shared__ double red[256];
     int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
     int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
     double acc = 0.0;
     for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
         double v = a[i];
-        acc += (mode == 0) ? v : v * (lambda * v + b[i]);
+        acc += (mode == 0) ? v : (mode == 1) ? v * (lambda * v + b[i]) : v * (lambda * w[i] * v + b[i]);
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -1228,6 +1232,93 @@ __global__ void k_hmul(int64_t nblocks, const int64_t *__restrict__ val_off, con
             atomicAdd(&y[r0 + i], hv * x[c0 + j]);          // diagnostics only (not on the LM path)
             if (!bdiag[b]) atomicAdd(&y[c0 + j], hv * x[r0 + i]);
         }
+}
+
+// ------------------------------------------------------------------------------------------
+// point-sharded plan: cross-rank transfers (DistPlan in symbolic.h)
+// ------------------------------------------------------------------------------------------
+// lower triangle of a contribution block (u x u at (s, s) of a column-major m x m front) packed
+// column by column: column j holds rows j..u-1 at j*u - j(j-1)/2 (contiguous in the arena too)
+__global__ void __launch_bounds__(256) k_pack_cb(const double *__restrict__ cb, int m, int u, double *__restrict__ buf) {
+    const int j = blockIdx.x;
+    if (j >= u) return;
+    const int64_t off = (int64_t)j * u - (int64_t)j * (j - 1) / 2;
+    const double *src = cb + (int64_t)j * m;
+    for (int i = j + (int)threadIdx.x; i < u; i += blockDim.x) buf[off + (i - j)] = src[i];
+}
+
+// extend-add of a packed contribution block received from another rank into the parent front
+// (task shape and fixed per-entry order as k_ea)
+__global__ void __launch_bounds__(256) k_ea_packed(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                   const double *__restrict__ buf, double *__restrict__ arena) {
+    int t = blockIdx.x;
+    if (t >= ntask) return;
+    int c = tasks[3 * t], j0 = tasks[3 * t + 1], i0 = tasks[3 * t + 2];
+    int p = fd.parent[c];
+    int u = fd.m[c] - fd.s[c], mp = fd.m[p];
+    const int32_t *bm = fd.bmap + fd.bmap_off[c];
+    double *Fp = arena + fd.arena_off[p];
+    const int i = i0 + (int)threadIdx.x;
+    if (i >= u) return;
+    const int bi = bm[i];
+    const int nj = min(16, min(u - j0, i - j0 + 1));
+    double cv[16], pv[16];
+    int64_t pj[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int j = j0 + q;
+        pj[q] = (q < nj) ? (int64_t)bm[j] * mp + bi : 0;
+        cv[q] = (q < nj) ? buf[(int64_t)j * u - (int64_t)j * (j - 1) / 2 + (i - j)] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) pv[q] = (q < nj) ? Fp[pj[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++)
+        if (q < nj) Fp[pj[q]] = pv[q] + cv[q];
+}
+
+__global__ void k_gather_idx(int n, const int32_t *__restrict__ idx, const double *__restrict__ src,
+                             double *__restrict__ dst) {
+    int i = TID;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+__global__ void k_scatter_idx(int n, const int32_t *__restrict__ idx, const double *__restrict__ src,
+                              double *__restrict__ dst) {
+    int i = TID;
+    if (i < n) dst[idx[i]] = src[i];
+}
+
+// diagonal entries of this rank's diagonal blocks (its own and the partial ones of remote vertices)
+// into a dof vector; summed over the ranks it is diag(H) (lambda init, g2o computeLambdaInit)
+__global__ void k_diag_entries(int64_t nblocks, const int64_t *__restrict__ val_off, const int32_t *__restrict__ bcols,
+                               const int64_t *__restrict__ brow_dof, const int64_t *__restrict__ bcol_dof,
+                               const double *__restrict__ hval, double *__restrict__ diagv) {
+    int64_t b = TID;
+    if (b >= nblocks || brow_dof[b] != bcol_dof[b]) return;
+    const int c = bcols[b];
+    const double *h = hval + val_off[b];
+    for (int k = 0; k < c; k++) diagv[bcol_dof[b] + k] = h[k * c + k];
+}
+
+__global__ void __launch_bounds__(256) k_absmax_partial(int64_t n, const double *__restrict__ a, double *__restrict__ part) {
+    __shared__ double red[256];
+    int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    double mx = 0.0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) mx = fmax(mx, fabs(a[i]));
+    red[threadIdx.x] = mx;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + off]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void k_int_to_double(int n, const int *__restrict__ a, double *__restrict__ out) {
+    int i = TID;
+    if (i < n) out[i] = (double)a[i];
 }
 
 }  // namespace dev
@@ -1319,12 +1410,14 @@ void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
     launch_scatter_lanes(one, st);
 }
 
-void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev) {
+void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev, LevelHook hook,
+                   void *hook_user) {
     int evi = 0;
     hipEvent_t prev_side = nullptr, cur_side = nullptr;   // events of the last two side-stream updates
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         g_level = (int)h;
+        if (hook) hook(hook_user, kHookFactor, (int)h);      // cross-rank contribution blocks into this level
         for (int slot = 0; slot < 2; slot++)
             if (lv.nea[slot] > 0)
                 LAUNCH("ea", dev::k_ea, dim3(lv.nea[slot], L.nlanes), dim3(256), st, lv.nea[slot],
@@ -1371,13 +1464,15 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
     }
 }
 
-void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st) {
+void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st, const double *bpart,
+                  LevelHook hook, void *hook_user) {
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         g_level = (int)h;
+        if (hook) hook(hook_user, kHookForward, (int)h);     // cross-rank forward-update vectors
         if (lv.nfwd > 0)
             LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd, L.nlanes), dim3(256), st, lv.nfwd,
-                   L.tasks + 3 * lv.fwd_off, L.fd, rhs, L.vec, L.lo);
+                   L.tasks + 3 * lv.fwd_off, L.fd, rhs, bpart, L.vec, L.lo);
         for (const auto &sp : lv.fsteps)
             if (sp.n > 0)
                 LAUNCH("fwd_step", dev::k_fwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
@@ -1393,7 +1488,44 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
             if (sp.n > 0)
                 LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
                        L.fd, L.arena, L.inv, L.vec, x, L.lo);
+        if (hook) hook(hook_user, kHookBackward, (int)hh);   // boundary solutions down to other ranks
     }
+}
+
+void launch_pack_cb(const DevPlan &L, int64_t arena_off, int m, int s, double *buf, hipStream_t st) {
+    const int u = m - s;
+    if (u > 0)
+        LAUNCH("pack_cb", dev::k_pack_cb, dim3(u), dim3(256), st, L.arena + arena_off + (int64_t)s * m + s, m, u, buf);
+}
+
+void launch_ea_packed(const DevPlan &L, int64_t ea_off, int nea, const double *buf, hipStream_t st) {
+    if (nea > 0)
+        LAUNCH("ea_packed", dev::k_ea_packed, dim3(nea), dim3(256), st, nea, L.tasks + 3 * ea_off, L.fd, buf, L.arena);
+}
+
+void launch_gather_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st) {
+    if (n > 0) LAUNCH("gather_idx", dev::k_gather_idx, dim3(nb(n, 256)), dim3(256), st, n, idx, src, dst);
+}
+
+void launch_scatter_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st) {
+    if (n > 0) LAUNCH("scatter_idx", dev::k_scatter_idx, dim3(nb(n, 256)), dim3(256), st, n, idx, src, dst);
+}
+
+void launch_diag_entries(const DevPlan &L, double *diagv, hipStream_t st) {
+    hipMemsetAsync(diagv, 0, sizeof(double) * (size_t)L.ndof, st);
+    if (L.nblocks > 0)
+        LAUNCH("diag_entries", dev::k_diag_entries, dim3(nb(L.nblocks, 128)), dim3(128), st, L.nblocks, L.blk_val_off,
+               L.blk_cols, L.blk_row_dof, L.blk_col_dof, L.hval, diagv);
+}
+
+void launch_absmax(int64_t n, const double *a, double *part, int nparts, double *out, hipStream_t st) {
+    if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
+    LAUNCH("absmax_partial", dev::k_absmax_partial, dim3(nparts), dim3(256), st, n, a, part);
+    LAUNCH("max_final", dev::k_max_final, dim3(1), dim3(64), st, nparts, part, out);
+}
+
+void launch_int_to_double(int n, const int *a, double *out, hipStream_t st) {
+    if (n > 0) LAUNCH("int_to_double", dev::k_int_to_double, dim3(nb(n, 64)), dim3(64), st, n, a, out);
 }
 
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag) {
@@ -1405,9 +1537,9 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, 
 }
 
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
-                double *out, hipStream_t st) {
+                double *out, hipStream_t st, const double *w) {
     if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
-    LAUNCH("sum_partial", dev::k_sum_partial, dim3(nparts), dim3(256), st, n, a, b, lambda, mode, part);
+    LAUNCH("sum_partial", dev::k_sum_partial, dim3(nparts), dim3(256), st, n, a, b, lambda, mode, w, part);
     LAUNCH("sum_final", dev::k_sum_final, dim3(1), dim3(64), st, nparts, part, out);
 }
 

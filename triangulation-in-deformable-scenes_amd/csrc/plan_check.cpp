@@ -5,30 +5,35 @@
 // caller.  It exists so the symbolic analysis (ordering, boundary sets, child->parent maps, arena
 // offsets, task lists) can be verified in the CPU test suite without a GPU.  It is never called by
 // the solve path (deftri_solve_lm et al. run only on the device) — see DESIGN.md §3.
+#include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "symbolic.h"
 
 namespace deftri {
 
-int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const double *rhs, double *x) {
+// xfer (point-sharded plan only): op 2 send / 3 receive n doubles to / from `peer` (the transport
+// of deftri_dist_set_transport).  bpart: the rank's partial b, injected on its top front's boundary.
+int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const double *rhs, double *x,
+                       const std::function<int(int, int, double *, int64_t)> *xfer, const double *bpart) {
     const int64_t n = S.ndof;
+    const DistPlan &D = S.dist;
     std::vector<double> arena((size_t)S.arena_size, 0.0), vec((size_t)S.vec_size, 0.0);
     // scatter: every block entry from the dense H (row-major n x n)
     int32_t nf = (int32_t)S.fronts.size();
+    std::vector<std::pair<int64_t, int32_t>> starts;       // this rank's fronts by arena offset
+    for (int32_t f = 0; f < nf; f++)
+        if (S.fronts[f].owner == D.rank) starts.emplace_back(S.fronts[f].arena_off, f);
+    std::sort(starts.begin(), starts.end());
     for (int64_t b = 0; b < S.nblocks; b++) {
         int64_t a = S.blk_arena[b];
-        int32_t f = 0;
-        {
-            int32_t lo = 0, hi = nf - 1;
-            while (lo < hi) {
-                int32_t mid = (lo + hi + 1) / 2;
-                if (S.fronts[mid].arena_off <= a) lo = mid; else hi = mid - 1;
-            }
-            f = lo;
-        }
+        auto it = std::upper_bound(starts.begin(), starts.end(), std::make_pair(a, (int32_t)nf));
+        const int32_t f = (it - 1)->second;
         const Front &F = S.fronts[f];
         int32_t lc = (int32_t)((a - F.arena_off) / F.m), lr = (int32_t)((a - F.arena_off) % F.m);
         for (int i = 0; i < S.blk_rows[b]; i++)
@@ -40,6 +45,17 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
     }
     auto Fp = [&](int32_t f) { return arena.data() + S.fronts[f].arena_off; };
     const int32_t *T = S.task_i32.data();
+    if (std::getenv("DEFTRI_DEBUG_EMU")) {
+        int64_t nd = 0, nl = 0;
+        for (int64_t b = 0; b < S.nblocks; b++) if (S.blk_diag[b]) { nd++; nl += S.blk_cols[b]; }
+        int64_t nown = 0;
+        for (auto v : D.dof_local) nown += v;
+        std::fprintf(stderr, "[emu] rank %d blocks %lld diag blocks %lld lambda dofs %lld own dofs %lld top %d xfers %zu\n",
+                     D.rank, (long long)S.nblocks, (long long)nd, (long long)nl, (long long)nown, D.top, D.xfers.size());
+        for (const auto &xf : D.xfers) std::fprintf(stderr, "[emu]   xfer child %d parent %d %d->%d level %d u %d\n", xf.child, xf.parent, xf.src, xf.dst, xf.level, xf.u);
+        for (int32_t f = 0; f < nf; f++) if (S.fronts[f].parent < 0 || S.fronts[f].height >= S.nlevels - 3)
+            std::fprintf(stderr, "[emu]   front %d m %d s %d owner %d parent %d h %d direct %d\n", f, S.fronts[f].m, S.fronts[f].s, S.fronts[f].owner, S.fronts[f].parent, S.fronts[f].height, S.fronts[f].direct);
+    }
     auto diag = [&](int f, int k0) -> bool {
         const Front &F = S.fronts[f];
         double *A = Fp(f);
@@ -54,7 +70,31 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
         }
         return true;
     };
-    for (const auto &lv : S.levels) {
+    // the DistPlan transfers of one level (global order; this rank's part)
+    auto level_xfers = [&](int32_t h) {
+        std::vector<const DistPlan::Xfer *> v;
+        for (const auto &xf : D.xfers)
+            if (xf.level == h && (xf.src == D.rank || xf.dst == D.rank)) v.push_back(&xf);
+        return v;
+    };
+    for (int32_t h = 0; h < (int32_t)S.levels.size(); h++) {
+        const auto &lv = S.levels[h];
+        for (const auto *xf : level_xfers(h)) {                 // packed contribution blocks (k_pack_cb / k_ea_packed)
+            const Front &C = S.fronts[xf->child];
+            const int u = xf->u;
+            std::vector<double> buf((size_t)u * (u + 1) / 2);
+            if (xf->src == D.rank) {
+                for (int j = 0, o = 0; j < u; j++)
+                    for (int i = j; i < u; i++) buf[o++] = Fp(xf->child)[(int64_t)(C.s + j) * C.m + C.s + i];
+                if ((*xfer)(2, xf->dst, buf.data(), (int64_t)buf.size())) return -2;
+            } else {
+                if ((*xfer)(3, xf->src, buf.data(), (int64_t)buf.size())) return -2;
+                const Front &Pf = S.fronts[C.parent];
+                const int32_t *bm = S.bmap.data() + C.bmap_off;
+                for (int j = 0, o = 0; j < u; j++)
+                    for (int i = j; i < u; i++) Fp(C.parent)[(int64_t)bm[j] * Pf.m + bm[i]] += buf[o++];
+            }
+        }
         for (int slot = 0; slot < 2; slot++)
             for (int32_t t = 0; t < lv.nea[slot]; t++) {
                 const int32_t *tk = T + 3 * (lv.ea_off[slot] + t);
@@ -128,13 +168,20 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
         for (int j = 0; j < kb; j++)
             for (int i = j + 1; i < kb; i++) y[i] -= A[(int64_t)(k0 + j) * F.m + k0 + i] * y[j];
     };
-    for (const auto &lv : S.levels) {
+    for (int32_t h = 0; h < (int32_t)S.levels.size(); h++) {
+        const auto &lv = S.levels[h];
+        for (const auto *xf : level_xfers(h)) {                 // forward-update vectors
+            const Front &C = S.fronts[xf->child];
+            double *v = vec.data() + C.vec_off + C.s;
+            if ((*xfer)(xf->src == D.rank ? 2 : 3, xf->src == D.rank ? xf->dst : xf->src, v, xf->u)) return -2;
+        }
         for (int32_t t = 0; t < lv.nfwd; t++) {
             int f = T[3 * (lv.fwd_off + t)];
             const Front &F = S.fronts[f];
             double *v = vec.data() + F.vec_off;
             const int32_t *rows = S.rows.data() + F.rows_off;
-            for (int r = 0; r < F.m; r++) v[r] = r < F.s ? rhs[rows[r]] : 0.0;
+            const bool inject = bpart && F.rhs_bnd;
+            for (int r = 0; r < F.m; r++) v[r] = r < F.s ? rhs[rows[r]] : (inject ? bpart[rows[r]] : 0.0);
             for (int sl = 0; sl < F.nchild; sl++) {
                 const Front &C = S.fronts[F.child[sl]];
                 const int32_t *bm = S.bmap.data() + C.bmap_off;
@@ -209,6 +256,18 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                     for (int i = 0; i < kb; i++) acc += A[(int64_t)q * F.m + k0 + i] * xs[t][i];
                     vec[F.vec_off + q] -= acc;
                 }
+            }
+        }
+        for (const auto *xf : level_xfers((int32_t)hh)) {        // boundary solutions down
+            const Front &C = S.fronts[xf->child];
+            const int32_t *rows = S.rows.data() + C.rows_off + C.s;
+            std::vector<double> buf((size_t)xf->u);
+            if (xf->dst == D.rank) {
+                for (int i = 0; i < xf->u; i++) buf[i] = x[rows[i]];
+                if ((*xfer)(2, xf->src, buf.data(), xf->u)) return -2;
+            } else {
+                if ((*xfer)(3, xf->dst, buf.data(), xf->u)) return -2;
+                for (int i = 0; i < xf->u; i++) x[rows[i]] = buf[i];
             }
         }
     }

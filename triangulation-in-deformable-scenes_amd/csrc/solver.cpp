@@ -10,6 +10,7 @@
 // Every arithmetic step runs on the GPU; the host only reads back the three scalars the control
 // flow branches on (chi2_new, dx.(lambda dx + b), zero-pivot flag) once per trial.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -17,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <string>
 #include <vector>
@@ -29,7 +31,9 @@
 using namespace deftri;
 
 namespace deftri {
-int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const double *rhs, double *x);
+int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const double *rhs, double *x,
+                       const std::function<int(int, int, double *, int64_t)> *xfer = nullptr,
+                       const double *bpart = nullptr);
 }
 
 namespace {
@@ -109,12 +113,27 @@ struct deftri_ctx {
     GraphResult graph;
     // speculative lambda lanes (see Lane)
     int analytic_jac = 0;                   // deftri_arap_optimization: 0 g2o numeric (reference), 1 analytic
+    bool prof_analytic = false;             // deftri_profile_trial linearizes like the last solve_lm
     int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES, else by factorization size)
     std::vector<Lane> lanes;                // device buffers: per uploaded problem
     DevPlan LB;                             // batched plan view: lanes' arenas / inverses / vectors / flags
     double *dx_lanes = nullptr;             // [lane][ndof]
     double *lane_pin = nullptr;             // pinned: [2t] chi2_new, [2t+1] dx.(lambda dx + b)
     int *lane_ipin = nullptr;               // pinned: zero-pivot flag per lane
+    // point-sharded plan (DistPlan, symbolic.h): this context is rank `rank` of `nranks`; transfers
+    // and all-reduces go through RCCL on the solver stream or through a caller-supplied host callback
+    int rank = 0, nranks = 1;
+    ncclComm_t comm = nullptr;
+    deftri_xfer_fn xfn = nullptr;
+    void *xuser = nullptr;
+    std::vector<double> xstage;             // host staging of the callback transport
+    HostProblem hloc;                       // the rank's problem: full state, owned edges only
+    double *d_xbuf = nullptr;               // staging of the rank's transfers (DistPlan::Xfer::buf_off)
+    double *d_diagv = nullptr;              // diag(H) partials (lambda init)
+    double *d_dofw = nullptr;               // 1 on the dofs of this rank's fronts
+    double *hook_x = nullptr;               // solution vector of the solve in flight (backward transfers)
+    int hook_rc = 0;                        // first transport error inside a level hook
+    bool dist() const { return nranks > 1; }
 };
 
 namespace {
@@ -238,8 +257,7 @@ void copy_host(HostProblem &h, const deftri_problem_desc *d) {
     h.d.order_xy = h.order_xy.empty() ? nullptr : h.order_xy.data();
 }
 
-int upload_device(deftri_ctx *ctx) {
-    const HostProblem &h = ctx->hp;
+int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     const deftri_problem_desc &d = h.d;
     DevProblem &P = ctx->P;
     P.P = d.n_points; P.Q = d.n_pairs; P.S = d.n_scales; P.C = d.n_cams;
@@ -336,20 +354,20 @@ int upload_device(deftri_ctx *ctx) {
     if ((rc = dalloc(ctx, &L.inv, S.inv_size))) return rc;
     {
         int32_t nf = (int32_t)S.fronts.size();
-        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf), dir(nf);
+        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf), dir(nf), rb(nf);
         std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf), io(nf);
         for (int32_t f = 0; f < nf; f++) {
             const Front &F = S.fronts[f];
             m[f] = F.m; s[f] = F.s; par[f] = F.parent; nch[f] = F.nchild; c0[f] = F.child[0]; c1[f] = F.child[1];
-            dir[f] = F.direct;
+            dir[f] = F.direct; rb[f] = F.rhs_bnd;
             ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off; io[f] = F.inv_off;
         }
-        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *pdir, *prows, *pbmap;
+        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *pdir, *prb, *prows, *pbmap;
         int64_t *pao, *pvo, *pro, *pbo, *pio;
-        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1); PUT(pdir, dir);
+        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1); PUT(pdir, dir); PUT(prb, rb);
         PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo); PUT(pio, io);
         PUT(prows, S.rows); PUT(pbmap, S.bmap);
-        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pdir, pao, pvo, pro, pbo, pio, prows, pbmap};
+        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pdir, prb, pao, pvo, pro, pbo, pio, prows, pbmap};
     }
     PUT(L.tasks, S.task_i32);
     L.levels.clear();
@@ -366,15 +384,158 @@ int upload_device(deftri_ctx *ctx) {
     }
     if ((rc = dalloc(ctx, &L.flag, 1))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_dx, S.ndof))) return rc;
+    HIPOK(hipMemset(ctx->d_dx, 0, sizeof(double) * (size_t)std::max<int64_t>(S.ndof, 1)));   // dofs no solve writes stay 0
     if ((rc = dalloc(ctx, &ctx->d_part, kRedParts))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_scal, 8))) return rc;
+    if (ctx->dist()) {
+        if ((rc = dalloc(ctx, &ctx->d_xbuf, S.dist.xbuf_size))) return rc;
+        if ((rc = dalloc(ctx, &ctx->d_diagv, S.ndof))) return rc;
+        std::vector<double> w(S.dist.dof_local.begin(), S.dist.dof_local.end());
+        PUT(ctx->d_dofw, w);
+    }
 #undef PUT
     HIPOK(hipDeviceSynchronize());
     return 0;
 }
 
-// chi2 at the current state (computeActiveErrors + activeRobustChi2) into d_scal[slot]
-void eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot) {
+// ---- point-sharded transport ----------------------------------------------------------------
+// in-place sum (op 0) / max (op 1) over the ranks of n device doubles (no-op on one rank)
+int dist_allreduce(deftri_ctx *ctx, double *buf, int64_t n, int op) {
+    if (!ctx->dist() || n <= 0) return 0;
+    if (ctx->comm) {
+        ncclResult_t r = ncclAllReduce(buf, buf, (size_t)n, ncclDouble, op == 0 ? ncclSum : ncclMax, ctx->comm, ctx->st);
+        if (r != ncclSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return 0;
+    }
+    if (!ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "point-sharded context without a transport");
+    if ((int64_t)ctx->xstage.size() < n) ctx->xstage.resize((size_t)n);
+    HIPOK(hipMemcpyAsync(ctx->xstage.data(), buf, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, ctx->st));
+    HIPOK(hipStreamSynchronize(ctx->st));
+    if (ctx->xfn(ctx->xuser, op, -1, ctx->xstage.data(), n) != 0) return fail(ctx, DEFTRI_E_ARG, "all-reduce callback failed");
+    HIPOK(hipMemcpyAsync(buf, ctx->xstage.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice, ctx->st));
+    return 0;
+}
+
+// point-to-point transfers of one step, in the DistPlan's global order (every rank walks the same
+// list, so the host transport's blocking send/recv cannot cross); RCCL groups them
+struct P2P { int peer; bool send; double *buf; int64_t n; };
+int dist_p2p(deftri_ctx *ctx, const std::vector<P2P> &ops) {
+    if (ops.empty()) return 0;
+    if (ctx->comm) {
+        ncclGroupStart();
+        for (const P2P &o : ops) {
+            ncclResult_t r = o.send ? ncclSend(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, ctx->st)
+                                    : ncclRecv(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, ctx->st);
+            if (r != ncclSuccess) { ncclGroupEnd(); return fail(ctx, DEFTRI_E_HIP, std::string("ncclSend/Recv: ") + ncclGetErrorString(r)); }
+        }
+        ncclResult_t r = ncclGroupEnd();
+        if (r != ncclSuccess) return fail(ctx, DEFTRI_E_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(r));
+        return 0;
+    }
+    if (!ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "point-sharded context without a transport");
+    HIPOK(hipStreamSynchronize(ctx->st));
+    for (const P2P &o : ops) {
+        if ((int64_t)ctx->xstage.size() < o.n) ctx->xstage.resize((size_t)o.n);
+        if (o.send) {
+            HIPOK(hipMemcpy(ctx->xstage.data(), o.buf, sizeof(double) * (size_t)o.n, hipMemcpyDeviceToHost));
+            if (ctx->xfn(ctx->xuser, 2, o.peer, ctx->xstage.data(), o.n) != 0) return fail(ctx, DEFTRI_E_ARG, "send callback failed");
+        } else {
+            if (ctx->xfn(ctx->xuser, 3, o.peer, ctx->xstage.data(), o.n) != 0) return fail(ctx, DEFTRI_E_ARG, "recv callback failed");
+            HIPOK(hipMemcpy(o.buf, ctx->xstage.data(), sizeof(double) * (size_t)o.n, hipMemcpyHostToDevice));
+        }
+    }
+    return 0;
+}
+
+// LevelHook of the factor / solve launchers: the DistPlan transfers whose parent front sits at
+// `level` — packed contribution blocks up (factor), forward-update vectors up (forward), boundary
+// solutions down (after the parent's backward level)
+void dist_hook(void *user, int phase, int level) {
+    deftri_ctx *ctx = (deftri_ctx *)user;
+    if (ctx->hook_rc) return;
+    const Symbolic &S = ctx->S;
+    const DistPlan &D = S.dist;
+    const DevPlan &L = ctx->L;
+    std::vector<P2P> ops;
+    std::vector<const DistPlan::Xfer *> mine;
+    for (const auto &x : D.xfers)
+        if (x.level == level && (x.src == D.rank || x.dst == D.rank)) mine.push_back(&x);
+    if (mine.empty()) return;
+    int rc = 0;
+    if (phase == kHookFactor) {
+        for (const auto *x : mine) {
+            const Front &C = S.fronts[x->child];
+            const int64_t n = (int64_t)x->u * (x->u + 1) / 2;
+            if (x->src == D.rank) launch_pack_cb(L, C.arena_off, C.m, C.s, ctx->d_xbuf + x->buf_off, ctx->st);
+            ops.push_back({x->src == D.rank ? x->dst : x->src, x->src == D.rank, ctx->d_xbuf + x->buf_off, n});
+        }
+        rc = dist_p2p(ctx, ops);
+        if (!rc)
+            for (const auto *x : mine)
+                if (x->dst == D.rank) launch_ea_packed(L, x->ea_off, x->nea, ctx->d_xbuf + x->buf_off, ctx->st);
+    } else if (phase == kHookForward) {
+        for (const auto *x : mine) {
+            const Front &C = S.fronts[x->child];
+            ops.push_back({x->src == D.rank ? x->dst : x->src, x->src == D.rank, L.vec + C.vec_off + C.s, (int64_t)x->u});
+        }
+        rc = dist_p2p(ctx, ops);
+    } else {
+        for (const auto *x : mine) {
+            const Front &C = S.fronts[x->child];
+            const int32_t *idx = L.fd.rows + C.rows_off + C.s;
+            if (x->dst == D.rank) launch_gather_idx(x->u, idx, ctx->hook_x, ctx->d_xbuf + x->buf_off, ctx->st);
+            ops.push_back({x->dst == D.rank ? x->src : x->dst, x->dst == D.rank, ctx->d_xbuf + x->buf_off, (int64_t)x->u});
+        }
+        rc = dist_p2p(ctx, ops);
+        if (!rc)
+            for (const auto *x : mine) {
+                const Front &C = S.fronts[x->child];
+                if (x->src == D.rank)
+                    launch_scatter_idx(x->u, L.fd.rows + C.rows_off + C.s, ctx->d_xbuf + x->buf_off, ctx->hook_x, ctx->st);
+            }
+    }
+    if (rc) ctx->hook_rc = rc;
+}
+
+// the rank's problem: the whole state, the edges it owns (DistPlan::own_*)
+void subset_edges(const HostProblem &full, const DistPlan &D, HostProblem &h) {
+    h = HostProblem();
+    h.points = full.points; h.tg = full.tg; h.scales = full.scales; h.cam_pose = full.cam_pose;
+    h.cam_kb8 = full.cam_kb8; h.rot = full.rot; h.pair_area = full.pair_area; h.pair_info = full.pair_info;
+    for (int32_t e : D.own_rep) {
+        h.rep_point.push_back(full.rep_point[e]); h.rep_cam.push_back(full.rep_cam[e]);
+        h.rep_obs.push_back(full.rep_obs[2 * (size_t)e]); h.rep_obs.push_back(full.rep_obs[2 * (size_t)e + 1]);
+        h.rep_info.push_back(full.rep_info[e]);
+    }
+    for (int32_t e : D.own_dep) {
+        h.dep_point.push_back(full.dep_point[e]); h.dep_scale.push_back(full.dep_scale[e]);
+        h.dep_cam.push_back(full.dep_cam[e]); h.dep_meas.push_back(full.dep_meas[e]);
+        h.dep_info.push_back(full.dep_info[e]);
+    }
+    for (int32_t e : D.own_arap) {
+        for (int k = 0; k < 4; k++) h.arap_pts.push_back(full.arap_pts[4 * (size_t)e + k]);
+        h.arap_pair.push_back(full.arap_pair[e]);
+        h.arap_rot.push_back(full.arap_rot[2 * (size_t)e]); h.arap_rot.push_back(full.arap_rot[2 * (size_t)e + 1]);
+        h.arap_w.push_back(full.arap_w[e]);
+    }
+    h.d = full.d;
+    h.d.n_rep = (int32_t)D.own_rep.size(); h.d.n_depth = (int32_t)D.own_dep.size(); h.d.n_arap = (int32_t)D.own_arap.size();
+    h.d.points = h.points.data(); h.d.tg = h.tg.data(); h.d.scales = h.scales.data();
+    h.d.cam_kb8 = h.cam_kb8.data(); h.d.cam_pose = h.cam_pose.data();
+    h.d.rep_point = h.rep_point.data(); h.d.rep_cam = h.rep_cam.data(); h.d.rep_obs = h.rep_obs.data();
+    h.d.rep_info = h.rep_info.data();
+    h.d.dep_point = h.dep_point.data(); h.d.dep_scale = h.dep_scale.data(); h.d.dep_cam = h.dep_cam.data();
+    h.d.dep_meas = h.dep_meas.data(); h.d.dep_info = h.dep_info.data();
+    h.d.arap_pts = h.arap_pts.data(); h.d.arap_pair = h.arap_pair.data(); h.d.arap_rot = h.arap_rot.data();
+    h.d.arap_w = h.arap_w.data(); h.d.rot = h.rot.data(); h.d.pair_area = h.pair_area.data();
+    h.d.pair_info = h.pair_info.data();
+    h.d.order_xy = nullptr;
+}
+
+// chi2 at the current state (computeActiveErrors + activeRobustChi2) into d_scal[slot]; point-sharded:
+// this rank's edges, summed over the ranks unless `reduce` is false (the caller reduces it together
+// with other scalars)
+int eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot, bool reduce = true) {
     DevProblem &P = ctx->P;
     launch_linearize(P, ctx->st, want_jac, analytic);
     // sum of the three chi arrays, in edge order rep, depth, arap (three partial sums, then add)
@@ -382,6 +543,7 @@ void eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot) {
     launch_sum(P.D, P.chi_dep, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 5, ctx->st);
     launch_sum(P.E, P.chi_arap, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 6, ctx->st);
     launch_sum(3, ctx->d_scal + 4, nullptr, 0, 0, ctx->d_part, 1, ctx->d_scal + slot, ctx->st);
+    return reduce ? dist_allreduce(ctx, ctx->d_scal + slot, 1, 0) : 0;
 }
 
 double read_scal(deftri_ctx *ctx, int slot) {
@@ -405,6 +567,7 @@ void pop_state(deftri_ctx *ctx) {
 }
 
 int lane_count(const deftri_ctx *ctx) {
+    if (ctx->dist()) return 1;              // point-sharded: one trial at a time (the transfers are per trial)
     int n = ctx->max_lanes;
     if (n <= 0) {
         n = ctx->S.factor_flops < kLaneFlopLimit ? 2 : 1;
@@ -552,6 +715,7 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     if (ctx->device < 0) { delete ctx; return 0; }
     hipSetDevice(ctx->device);
     free_device(ctx);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
     for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
     for (auto &e : ctx->sync_ev) if (e) hipEventDestroy(e);
     if (ctx->lane_pin) hipHostFree(ctx->lane_pin);
@@ -578,6 +742,62 @@ int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes) {
     return 0;
 }
 
+int deftri_dist_init_rccl(deftri_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || !id) return DEFTRI_E_ARG;
+    if (ctx->device < 0) return fail(ctx, DEFTRI_E_NODEVICE, "host-only context");
+    hipSetDevice(ctx->device);
+    free_device(ctx);
+    ctx->analysed = false;
+    if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ctx->xfn = nullptr; ctx->xuser = nullptr;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        ctx->comm = nullptr;
+        return fail(ctx, DEFTRI_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    ctx->rank = rank; ctx->nranks = nranks;
+    return 0;
+}
+
+int deftri_dist_set_transport(deftri_ctx *ctx, int32_t nranks, int32_t rank, deftri_xfer_fn fn, void *user) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return DEFTRI_E_ARG;
+    if (ctx->device >= 0) { hipSetDevice(ctx->device); free_device(ctx); }
+    ctx->analysed = false;
+    if (ctx->comm) { ncclCommDestroy(ctx->comm); ctx->comm = nullptr; }
+    ctx->xfn = fn; ctx->xuser = user;
+    ctx->rank = rank; ctx->nranks = nranks;
+    return 0;
+}
+
+int deftri_plan_vertex_order(const deftri_ctx *ctx, int64_t *order, int64_t nv) {
+    if (!ctx || !order) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return DEFTRI_E_NOPROBLEM;
+    if (nv != ctx->S.nv) return DEFTRI_E_ARG;
+    for (int64_t v = 0; v < nv; v++) order[ctx->S.elim_pos[v]] = v;
+    return 0;
+}
+
+int deftri_dist_vertex_owner(const deftri_ctx *ctx, int32_t *owner, int64_t nv) {
+    if (!ctx || !owner) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return DEFTRI_E_NOPROBLEM;
+    if (nv != ctx->S.nv) return DEFTRI_E_ARG;
+    std::memcpy(owner, ctx->S.dist.vertex_owner.data(), sizeof(int32_t) * (size_t)nv);
+    return 0;
+}
+
+int deftri_dist_owned_edges(const deftri_ctx *ctx, uint8_t *rep, uint8_t *dep, uint8_t *arap) {
+    if (!ctx) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return DEFTRI_E_NOPROBLEM;
+    const DistPlan &D = ctx->S.dist;
+    const deftri_problem_desc &d = ctx->hp.d;
+    if (rep) { std::memset(rep, 0, (size_t)d.n_rep); for (int32_t e : D.own_rep) rep[e] = 1; }
+    if (dep) { std::memset(dep, 0, (size_t)d.n_depth); for (int32_t e : D.own_dep) dep[e] = 1; }
+    if (arap) { std::memset(arap, 0, (size_t)d.n_arap); for (int32_t e : D.own_arap) arap[e] = 1; }
+    return 0;
+}
+
 int64_t deftri_num_unknowns(const deftri_ctx *ctx) { return (ctx && ctx->have) ? ctx->S.ndof : -1; }
 
 int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc) {
@@ -587,7 +807,7 @@ int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     if (ctx->device >= 0) { hipSetDevice(ctx->device); free_device(ctx); }
     ctx->have = false;
     copy_host(ctx->hp, desc);
-    if (!analyse(ctx->hp.d, ctx->S)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
+    if (!analyse(ctx->hp.d, ctx->S, 32, ctx->rank, ctx->nranks)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
     ctx->analysed = true;
     return 0;
 }
@@ -601,6 +821,9 @@ int deftri_plan_stats(const deftri_ctx *ctx, deftri_report *rep) {
     rep->factor_flops = ctx->S.factor_flops;
     rep->n_fronts = (int32_t)ctx->S.fronts.size();
     rep->n_levels = ctx->S.nlevels;
+    rep->rank = ctx->rank;
+    rep->nranks = ctx->nranks;
+    rep->factor_flops_total = ctx->S.dist.factor_flops_total;
     return 0;
 }
 
@@ -612,6 +835,22 @@ int deftri_debug_plan_solve(deftri_ctx *ctx, const double *H, double lambda, con
     return plan_emulate_solve(ctx->S, H, lambda, rhs, x) == 0 ? 0 : fail(ctx, DEFTRI_E_NUMERIC, "zero pivot");
 }
 
+int deftri_debug_plan_solve_dist(deftri_ctx *ctx, const double *Hq, double lambda, const double *bq, double *x,
+                                 int64_t n) {
+    if (!ctx || !Hq || !bq || !x) return DEFTRI_E_ARG;
+    if (!ctx->analysed) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem analysed");
+    if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    if (ctx->dist() && !ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "the emulation needs the callback transport");
+    std::function<int(int, int, double *, int64_t)> xf = [ctx](int op, int peer, double *buf, int64_t cnt) {
+        return ctx->xfn(ctx->xuser, op, peer, buf, cnt);
+    };
+    // forward gather reads the full rhs on the rank's own rows and the partial one on the boundary
+    // of its top front: both are b_q here (the test's b_q is zero outside the rank's contributions)
+    const int rc = plan_emulate_solve(ctx->S, Hq, lambda, bq, x, ctx->dist() ? &xf : nullptr, ctx->dist() ? bq : nullptr);
+    if (rc == -2) return fail(ctx, DEFTRI_E_ARG, "transfer callback failed");
+    return rc == 0 ? 0 : fail(ctx, DEFTRI_E_NUMERIC, "zero pivot");
+}
+
 int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *stats, int32_t max_stats,
                          int32_t *n_stats) {
     if (!ctx || !stats || !n_stats) return DEFTRI_E_ARG;
@@ -620,13 +859,19 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     HIPOK(hipStreamSynchronize(ctx->st));
     KProf prof;
     set_profiler(&prof);
-    eval_chi2_dev(ctx, true, true, 0);
+    // point-sharded: a collective (every rank profiles its part of the same trial)
+    LevelHook hook = ctx->dist() ? dist_hook : nullptr;
+    ctx->hook_rc = 0;
+    ctx->hook_x = ctx->d_dx;
+    int rc = eval_chi2_dev(ctx, true, ctx->prof_analytic, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     launch_scatter(ctx->L, lambda, ctx->st);
-    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
-    launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st);
+    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
+    launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st, ctx->dist() ? ctx->L.b : nullptr, hook, ctx);
     set_profiler(nullptr);
+    if (rc) return rc;
+    if (ctx->hook_rc) return ctx->hook_rc;
     HIPOK(hipStreamSynchronize(ctx->st));
     int32_t n = 0;
     const bool dump = std::getenv("DEFTRI_PROFILE_DUMP") != nullptr;
@@ -678,9 +923,10 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     if (rc) return rc;
     free_device(ctx);
     copy_host(ctx->hp, desc);
-    if (!analyse(ctx->hp.d, ctx->S)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
+    if (!analyse(ctx->hp.d, ctx->S, 32, ctx->rank, ctx->nranks)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
     ctx->analysed = true;
-    rc = upload_device(ctx);
+    if (ctx->dist()) subset_edges(ctx->hp, ctx->S.dist, ctx->hloc);
+    rc = upload_device(ctx, ctx->dist() ? ctx->hloc : ctx->hp);
     if (rc) { free_device(ctx); return rc; }
     ctx->have = true;
     return 0;
@@ -708,16 +954,24 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     R.factor_flops = ctx->S.factor_flops;
     R.n_fronts = (int32_t)ctx->S.fronts.size();
     R.n_levels = ctx->S.nlevels;
+    R.rank = ctx->rank;
+    R.nranks = ctx->nranks;
+    R.factor_flops_total = ctx->S.dist.factor_flops_total;
     const int max_trials = prm->max_trials > 0 ? prm->max_trials : 10;
     const double tau = prm->tau > 0 ? prm->tau : 1e-5;
     const bool analytic = prm->analytic_jacobians != 0;
+    ctx->prof_analytic = analytic;
+    const bool dist = ctx->dist();
+    ctx->hook_rc = 0;
+    LevelHook hook = dist ? dist_hook : nullptr;
+    int rc = 0;
     DevProblem &P = ctx->P;
     DevPlan &L = ctx->L;
     auto t_start = std::chrono::steady_clock::now();
     double lambda = 0, ni = 2;
     double t_lin = 0, t_fac = 0, t_sol = 0, t_upd = 0;
     int status = DEFTRI_STATUS_OK, it;
-    eval_chi2_dev(ctx, false, analytic, 0);
+    if ((rc = eval_chi2_dev(ctx, false, analytic, 0))) return rc;
     R.chi2_initial = read_scal(ctx, 0);
     double currentChi = R.chi2_initial;
     int nlanes = std::min(lane_count(ctx), max_trials);
@@ -728,9 +982,17 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     R.lanes = nlanes;
     for (it = 0; it < prm->n_iterations; it++) {
         hipEventRecord(ctx->ev[0], ctx->st);
-        eval_chi2_dev(ctx, true, analytic, 0);              // computeActiveErrors + linearizeOplus
+        if ((rc = eval_chi2_dev(ctx, true, analytic, 0))) return rc;   // computeActiveErrors + linearizeOplus
         launch_assemble(P, L, ctx->st);                      // buildSystem
-        if (it == 0) launch_maxdiag(L, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
+        if (it == 0) {
+            if (dist) {                                      // max of the rank-summed diagonal
+                launch_diag_entries(L, ctx->d_diagv, ctx->st);
+                if ((rc = dist_allreduce(ctx, ctx->d_diagv, L.ndof, 0))) return rc;
+                launch_absmax(L.ndof, ctx->d_diagv, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
+            } else {
+                launch_maxdiag(L, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
+            }
+        }
         hipEventRecord(ctx->ev[1], ctx->st);
         double *chis = ctx->hpin;           // pinned: a pageable readback costs ~100 us per call
         HIPOK(hipMemcpyAsync(chis, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
@@ -795,20 +1057,34 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             hipEventRecord(ctx->ev[2], ctx->st);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
             launch_scatter(L, lambda, ctx->st);              // setLambda
-            launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64);
+            launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
             hipEventRecord(ctx->ev[3], ctx->st);
-            launch_solve(L, L.b, ctx->d_dx, ctx->st);
+            ctx->hook_x = ctx->d_dx;
+            launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
+            if (ctx->hook_rc) return ctx->hook_rc;
             hipEventRecord(ctx->ev[4], ctx->st);
             launch_update_state(P, ctx->d_dx, ctx->st, L.flag);   // _optimizer->update(x) (skipped on a zero pivot)
-            eval_chi2_dev(ctx, false, analytic, 0);          // computeActiveErrors; activeRobustChi2
-            launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
-            hipEventRecord(ctx->ev[5], ctx->st);
             double *sc = ctx->hpin + 4;
-            HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
-            HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            if (dist) {
+                // chi2 of the rank's edges, dx.(lambda dx + b) with b partial and lambda once per dof,
+                // the zero-pivot flag: one all-reduce of the three (a zero pivot on any rank rejects)
+                if ((rc = eval_chi2_dev(ctx, false, analytic, 0, false))) return rc;
+                launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 3, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st,
+                           ctx->d_dofw);
+                launch_int_to_double(1, L.flag, ctx->d_scal + 2, ctx->st);
+                if ((rc = dist_allreduce(ctx, ctx->d_scal, 3, 0))) return rc;
+                hipEventRecord(ctx->ev[5], ctx->st);
+                HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+            } else {
+                eval_chi2_dev(ctx, false, analytic, 0);      // computeActiveErrors; activeRobustChi2
+                launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
+                hipEventRecord(ctx->ev[5], ctx->st);
+                HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
+                HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+            }
             HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
-            const bool ok2 = *ctx->ipin == 0;
+            const bool ok2 = dist ? sc[2] == 0.0 : *ctx->ipin == 0;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
             rho = (currentChi - tempChi);
@@ -837,7 +1113,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             std::fprintf(stderr, "[deftri] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
         if (qmax == max_trials || rho == 0 || !std::isfinite(lambda)) { status = DEFTRI_STATUS_TERMINATE; it++; break; }
     }
-    eval_chi2_dev(ctx, false, analytic, 0);
+    if ((rc = eval_chi2_dev(ctx, false, analytic, 0))) return rc;
     R.chi2_final = read_scal(ctx, 0);
     HIPOK(hipStreamSynchronize(ctx->st));
     R.status = status;
@@ -1004,6 +1280,7 @@ int deftri_eval_chi2(deftri_ctx *ctx, double *chi2) {
 }
 
 int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
+    if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
@@ -1035,6 +1312,7 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
 }
 
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n) {
+    if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (n != ctx->S.ndof || !x || !y) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
@@ -1052,6 +1330,7 @@ int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int
 }
 
 int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n) {
+    if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (n != ctx->S.ndof || !rhs || !x) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);

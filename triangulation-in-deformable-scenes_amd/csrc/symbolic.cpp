@@ -34,7 +34,9 @@ struct Builder {
     double nd_bal = 0.55;
     std::vector<int64_t> spos;       // index of a point in the separator list being refined
 
-    Builder(const deftri_problem_desc &d_, Symbolic &S_, int leaf_) : d(d_), S(S_), leaf(leaf_) {
+    int rank = 0, nranks = 1;
+    Builder(const deftri_problem_desc &d_, Symbolic &S_, int leaf_, int rank_, int nranks_)
+        : d(d_), S(S_), leaf(leaf_), rank(rank_), nranks(nranks_) {
         Q = d.n_pairs; NS = d.n_scales; P = d.n_points;
     }
 
@@ -304,10 +306,9 @@ struct Builder {
             cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
             bnd[f] = cand;
         }
-        // rows, sizes, offsets
+        // rows and sizes (every rank knows the whole tree)
         std::vector<std::vector<int64_t>> fv(nf);       // vertex list (row order)
         std::vector<std::vector<int32_t>> fvrow(nf);    // local row of each vertex
-        int64_t aoff = 0, voff2 = 0, ioff = 0;
         for (int32_t f = 0; f < nf; f++) {
             Front &F = S.fronts[f];
             fv[f] = own[f];
@@ -322,13 +323,76 @@ struct Builder {
                 if (i < own[f].size()) s += S.vdim[v];
             }
             F.m = m; F.s = s;
-            F.arena_off = aoff; aoff += (int64_t)m * m;
-            F.vec_off = voff2; voff2 += m;
-            F.inv_off = ioff;
-            if (s > 0) ioff += (int64_t)((s - 1) / kPanel) * kPanel * kPanel + (int64_t)((s - 1) % kPanel + 1) * ((s - 1) % kPanel + 1);
-            double sd = s, ud = m - s;
-            S.factor_flops += sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
-            S.nnz_factor += (int64_t)s * (s + 1) / 2 + (int64_t)(m - s) * s;
+            F.owner = 0; F.rhs_bnd = 0;
+        }
+        auto front_flops = [&](const Front &F) {
+            double sd = F.s, ud = F.m - F.s;
+            return sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
+        };
+        // heights / levels (global: every rank walks the same level sequence)
+        int32_t maxh = 0;
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            int32_t h = 0;
+            for (int c = 0; c < F.nchild; c++) h = std::max(h, S.fronts[F.child[c]].height + 1);
+            F.height = h;
+            maxh = std::max(maxh, h);
+        }
+        S.nlevels = maxh + 1;
+        // ---------------- ranks ----------------
+        DistPlan &D = S.dist;
+        D.rank = rank; D.nranks = nranks;
+        {
+            std::vector<double> sub(nf, 0.0);              // subtree flops (fronts are in postorder)
+            for (int32_t f = 0; f < nf; f++) {
+                sub[f] += front_flops(S.fronts[f]);
+                if (S.fronts[f].parent >= 0) sub[S.fronts[f].parent] += sub[f];
+            }
+            std::vector<int32_t> rlo(nf, 0), rhi(nf, nranks);
+            for (int32_t f = nf - 1; f >= 0; f--) {        // parents before children
+                Front &F = S.fronts[f];
+                if (F.parent < 0) { rlo[f] = 0; rhi[f] = nranks; }
+                const int32_t lo = rlo[f], hi = rhi[f];
+                F.owner = lo;
+                if (F.nchild == 2 && hi - lo > 1) {
+                    const double a = sub[F.child[0]], b = sub[F.child[1]];
+                    int32_t mid = lo + (int32_t)std::lround((double)(hi - lo) * a / std::max(a + b, 1e-300));
+                    mid = std::min(std::max(mid, lo + 1), hi - 1);
+                    rlo[F.child[0]] = lo; rhi[F.child[0]] = mid;
+                    rlo[F.child[1]] = mid; rhi[F.child[1]] = hi;
+                } else {
+                    for (int c = 0; c < F.nchild; c++) { rlo[F.child[c]] = lo; rhi[F.child[c]] = hi; }
+                }
+            }
+        }
+        auto local = [&](int32_t f) { return S.fronts[f].owner == rank; };
+        for (int32_t f = 0; f < nf; f++) {
+            const Front &F = S.fronts[f];
+            if (local(f) && F.parent >= 0 && !local(F.parent)) {
+                if (D.top >= 0) { S.error = "internal: two top fronts on one rank"; return false; }
+                D.top = f;
+            }
+        }
+        if (D.top >= 0) S.fronts[D.top].rhs_bnd = 1;
+        // offsets: arena / inverses for this rank's fronts, solve vectors also for remote children of
+        // them (the forward transfer lands there)
+        int64_t aoff = 0, voff2 = 0, ioff = 0;
+        for (int32_t f = 0; f < nf; f++) {
+            Front &F = S.fronts[f];
+            const bool loc = local(f);
+            const bool needvec = loc || (F.parent >= 0 && local(F.parent));
+            const int32_t m = F.m, s = F.s;
+            F.arena_off = loc ? aoff : 0;
+            F.vec_off = needvec ? voff2 : 0;
+            F.inv_off = loc ? ioff : 0;
+            if (loc) aoff += (int64_t)m * m;
+            if (needvec) voff2 += m;
+            if (loc && s > 0) ioff += (int64_t)((s - 1) / kPanel) * kPanel * kPanel + (int64_t)((s - 1) % kPanel + 1) * ((s - 1) % kPanel + 1);
+            const double fl = front_flops(F);
+            const int64_t nz = (int64_t)s * (s + 1) / 2 + (int64_t)(m - s) * s;
+            D.factor_flops_total += fl;
+            D.nnz_factor_total += nz;
+            if (loc) { S.factor_flops += fl; S.nnz_factor += nz; }
         }
         S.arena_size = aoff;
         S.vec_size = voff2;
@@ -351,57 +415,106 @@ struct Builder {
                 for (int k = 0; k < S.vdim[v]; k++) S.bmap.push_back(lr + k);
             }
         }
-        // heights / levels
-        int32_t maxh = 0;
-        for (int32_t f = 0; f < nf; f++) {
-            Front &F = S.fronts[f];
-            int32_t h = 0;
-            for (int c = 0; c < F.nchild; c++) h = std::max(h, S.fronts[F.child[c]].height + 1);
-            F.height = h;
-            maxh = std::max(maxh, h);
-        }
-        S.nlevels = maxh + 1;
         // direct assembly: a child adds its final contribution block into the parent from its last
         // trailing-update launch, unless a sibling of the same level (slot 0) does so in that same
         // launch — then this one (slot 1) goes through the extend-add launch after it, so every
-        // parent entry is summed in a fixed order
+        // parent entry is summed in a fixed order.  A child under a remote parent keeps its
+        // contribution block (it is packed and sent).
         for (int32_t f = 0; f < nf; f++) {
             Front &F = S.fronts[f];
             F.direct = 0;
             if (F.parent < 0 || F.m == F.s || F.s == 0) continue;
+            if (!local(f) || !local(F.parent)) continue;
             const Front &Pf = S.fronts[F.parent];
             bool slot1 = Pf.nchild > 1 && Pf.child[1] == f;
-            bool same = Pf.nchild > 1 && S.fronts[Pf.child[0]].height == S.fronts[Pf.child[1]].height;
+            bool same = Pf.nchild > 1 && S.fronts[Pf.child[0]].height == S.fronts[Pf.child[1]].height &&
+                        local(Pf.child[0]);
             F.direct = (slot1 && same) ? 0 : 1;
         }
         S.level_fronts.assign(S.nlevels, {});
-        for (int32_t f = 0; f < nf; f++) S.level_fronts[S.fronts[f].height].push_back(f);
+        for (int32_t f = 0; f < nf; f++)
+            if (local(f)) S.level_fronts[S.fronts[f].height].push_back(f);
+        // cross-rank transfers (one per rank > 0 with work): child = that rank's top front
+        for (int32_t f = 0; f < nf; f++) {
+            const Front &F = S.fronts[f];
+            if (F.parent < 0 || S.fronts[F.parent].owner == F.owner || F.m == F.s) continue;
+            DistPlan::Xfer x;
+            x.child = f; x.parent = F.parent; x.src = F.owner; x.dst = S.fronts[F.parent].owner;
+            x.level = S.fronts[F.parent].height; x.u = F.m - F.s;
+            D.xfers.push_back(x);
+        }
+        std::stable_sort(D.xfers.begin(), D.xfers.end(), [](const DistPlan::Xfer &a, const DistPlan::Xfer &b) {
+            return a.level < b.level || (a.level == b.level && a.child < b.child);
+        });
+        for (auto &x : D.xfers)
+            if (x.src == rank || x.dst == rank) {
+                x.buf_off = D.xbuf_size;
+                D.xbuf_size += (int64_t)x.u * (x.u + 1) / 2;
+            }
+        // edge ownership: the owner of the front of the edge's first-eliminated vertex
+        auto first_owner = [&](const int64_t *v, int n) {
+            int64_t best = v[0];
+            for (int k = 1; k < n; k++) if (S.elim_pos[v[k]] < S.elim_pos[best]) best = v[k];
+            return S.fronts[vfront[best]].owner;
+        };
+        for (int e = 0; e < d.n_rep; e++) {
+            int64_t v[1] = {vP(d.rep_point[e])};
+            if (first_owner(v, 1) == rank) D.own_rep.push_back(e);
+        }
+        for (int e = 0; e < d.n_depth; e++) {
+            int64_t v[2] = {vP(d.dep_point[e]), vS(d.dep_scale[e])};
+            if (first_owner(v, 2) == rank) D.own_dep.push_back(e);
+        }
+        for (int e = 0; e < d.n_arap; e++) {
+            int64_t v[5];
+            for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
+            v[4] = vT(d.arap_pair[e]);
+            if (first_owner(v, 5) == rank) D.own_arap.push_back(e);
+        }
+        D.vertex_owner.resize(S.nv);
+        D.dof_local.assign(S.ndof, 0);
+        for (int64_t v = 0; v < S.nv; v++) {
+            D.vertex_owner[v] = S.fronts[vfront[v]].owner;
+            if (D.vertex_owner[v] == rank)
+                for (int k = 0; k < S.vdim[v]; k++) D.dof_local[S.voff[v] + k] = 1;
+        }
         if (std::getenv("DEFTRI_DEBUG_PLAN")) {
             for (int32_t h = 0; h < S.nlevels; h++) {
                 int32_t ms = 0, mm = 0; double fl = 0;
                 for (int32_t f : S.level_fronts[h]) {
                     const Front &F = S.fronts[f];
                     ms = std::max(ms, F.s); mm = std::max(mm, F.m);
-                    double sd = F.s, ud = F.m - F.s;
-                    fl += sd * sd * sd / 3.0 + ud * sd * sd + ud * ud * sd;
+                    fl += front_flops(F);
                 }
-                std::fprintf(stderr, "[plan] level %d fronts %zu max_s %d max_m %d flops %.3g\n", h,
+                std::fprintf(stderr, "[plan] rank %d level %d fronts %zu max_s %d max_m %d flops %.3g\n", rank, h,
                              S.level_fronts[h].size(), ms, mm, fl);
             }
         }
 
         // ---------------- H blocks ----------------
-        // column vertex c, row vertices r with elim[r] >= elim[c], r coupled with c (or r == c)
+        // column vertex c, row vertices r with elim[r] >= elim[c], r coupled with c (or r == c).  A
+        // column of this rank's fronts: every coupled row (blocks no owned edge feeds stay zero; the
+        // other ranks' parts arrive through their contribution blocks).  A remote column in the top
+        // front's boundary: the coupled rows inside that front, placed in its contribution-block
+        // region (no lambda there: the owner adds it).
+        const int32_t X = D.top;
         std::vector<int64_t> blk_begin(S.nv + 1, 0);
         std::vector<int64_t> blk_rowv;
+        std::vector<int32_t> blk_front;
         for (int64_t c = 0; c < S.nv; c++) {
             blk_begin[c] = (int64_t)blk_rowv.size();
+            int32_t tf = -1;
+            if (local(vfront[c])) tf = vfront[c];
+            else if (X >= 0 && local_row(X, c) >= 0) tf = X;
+            if (tf < 0) continue;
             std::vector<int64_t> rs;
             rs.push_back(c);
             for (int64_t k = adj_begin[c]; k < adj_begin[c + 1]; k++)
-                if (S.elim_pos[adj[k]] > S.elim_pos[c]) rs.push_back(adj[k]);
+                if (S.elim_pos[adj[k]] > S.elim_pos[c] && (tf != X || vfront[c] == X || local_row(X, adj[k]) >= 0))
+                    rs.push_back(adj[k]);
             std::sort(rs.begin(), rs.end());
             blk_rowv.insert(blk_rowv.end(), rs.begin(), rs.end());
+            blk_front.insert(blk_front.end(), rs.size(), tf);
         }
         blk_begin[S.nv] = (int64_t)blk_rowv.size();
         S.nblocks = (int64_t)blk_rowv.size();
@@ -409,10 +522,10 @@ struct Builder {
         S.blk_arena.resize(S.nblocks); S.blk_ld.resize(S.nblocks); S.blk_diag.resize(S.nblocks);
         int64_t hv = 0;
         for (int64_t c = 0; c < S.nv; c++) {
-            int32_t f = vfront[c];
-            const Front &F = S.fronts[f];
-            int32_t lc = local_row(f, c);
             for (int64_t b = blk_begin[c]; b < blk_begin[c + 1]; b++) {
+                const int32_t f = blk_front[b];
+                const Front &F = S.fronts[f];
+                const int32_t lc = local_row(f, c);
                 int64_t r = blk_rowv[b];
                 int32_t lr = local_row(f, r);
                 if (lr < 0 || lc < 0) { S.error = "internal: block outside its front"; return false; }
@@ -420,7 +533,7 @@ struct Builder {
                 S.blk_val_off[b] = hv; hv += (int64_t)S.vdim[r] * S.vdim[c];
                 S.blk_arena[b] = F.arena_off + (int64_t)lc * F.m + lr;
                 S.blk_ld[b] = F.m;
-                S.blk_diag[b] = (r == c) ? 1 : 0;
+                S.blk_diag[b] = (r == c && f == vfront[c]) ? 1 : 0;
             }
         }
         S.hval_size = hv;
@@ -433,8 +546,8 @@ struct Builder {
         // contributions
         std::vector<std::pair<int64_t, uint64_t>> hc;      // (block, record)
         std::vector<std::pair<int64_t, uint64_t>> bc;      // (vertex, record)
-        hc.reserve((size_t)d.n_rep + 3 * (size_t)d.n_depth + 15 * (size_t)d.n_arap);
-        bc.reserve((size_t)d.n_rep + 2 * (size_t)d.n_depth + 5 * (size_t)d.n_arap);
+        hc.reserve(D.own_rep.size() + 3 * D.own_dep.size() + 15 * D.own_arap.size());
+        bc.reserve(D.own_rep.size() + 2 * D.own_dep.size() + 5 * D.own_arap.size());
         auto add_edge = [&](int kind, int64_t e, const int64_t *v, int nr) {
             for (int a = 0; a < nr; a++) {
                 bc.emplace_back(v[a], contrib_pack(kind, e, a, a));
@@ -449,19 +562,23 @@ struct Builder {
             }
             return true;
         };
-        for (int e = 0; e < d.n_rep; e++) {
+        // owned edges only, numbered in this rank's (compacted) edge arrays
+        for (size_t k = 0; k < D.own_rep.size(); k++) {
+            const int e = D.own_rep[k];
             int64_t v[1] = {vP(d.rep_point[e])};
-            if (!add_edge(EK_REP, e, v, 1)) return false;
+            if (!add_edge(EK_REP, (int64_t)k, v, 1)) return false;
         }
-        for (int e = 0; e < d.n_depth; e++) {
+        for (size_t k = 0; k < D.own_dep.size(); k++) {
+            const int e = D.own_dep[k];
             int64_t v[2] = {vP(d.dep_point[e]), vS(d.dep_scale[e])};
-            if (!add_edge(EK_DEP, e, v, 2)) return false;
+            if (!add_edge(EK_DEP, (int64_t)k, v, 2)) return false;
         }
-        for (int e = 0; e < d.n_arap; e++) {
+        for (size_t k = 0; k < D.own_arap.size(); k++) {
+            const int e = D.own_arap[k];
             int64_t v[5];
-            for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
+            for (int q = 0; q < 4; q++) v[q] = vP(d.arap_pts[4 * (int64_t)e + q]);
             v[4] = vT(d.arap_pair[e]);
-            if (!add_edge(EK_ARAP, e, v, 5)) return false;
+            if (!add_edge(EK_ARAP, (int64_t)k, v, 5)) return false;
         }
         auto chunkify = [&](std::vector<std::pair<int64_t, uint64_t>> &lst, int64_t nkeys,
                             std::vector<uint64_t> &recs, std::vector<int64_t> &cbeg,
@@ -504,6 +621,7 @@ struct Builder {
                     if (F.nchild <= slot) continue;
                     int32_t c = F.child[slot];
                     if (S.fronts[c].direct) continue;           // assembled by its own last update
+                    if (!local(c)) continue;                     // another rank's: packed transfer (DistPlan)
                     int32_t u = S.fronts[c].m - S.fronts[c].s;
                     // (child, 16 CB columns j0.., 256 CB rows i0..), lower triangle only
                     for (int32_t j = 0; j < u; j += 16)
@@ -652,16 +770,25 @@ struct Builder {
                 LT.bsteps.push_back(st);
             }
         }
+        // packed extend-add of the contribution blocks received from other ranks (same task shape as
+        // the extend-add: 16 CB columns x 256 CB rows, lower triangle)
+        for (auto &x : D.xfers) {
+            if (x.dst != rank) continue;
+            x.ea_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t j = 0; j < x.u; j += 16)
+                for (int32_t i = j; i < x.u; i += 256) { push3(x.child, j, i); x.nea++; }
+        }
         return true;
     }
 };
 
 }  // namespace
 
-bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points) {
+bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points, int rank, int nranks) {
     S = Symbolic();
+    if (nranks < 1 || rank < 0 || rank >= nranks) { S.error = "bad rank / nranks"; return false; }
     if (const char *e = std::getenv("DEFTRI_ND_LEAF")) leaf_points = std::max(2, std::atoi(e));   // tuning
-    Builder b(d, S, leaf_points);
+    Builder b(d, S, leaf_points, rank, nranks);
     return b.run();
 }
 

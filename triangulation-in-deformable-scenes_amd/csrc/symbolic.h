@@ -54,6 +54,36 @@ struct Front {
                          //    into the parent (no extend-add); 0: extend-add (a same-level slot-1 sibling)
     int32_t nchild;
     int32_t child[2];
+    int32_t owner;       // rank that assembles and factors this front (0 on one rank)
+    int32_t rhs_bnd;     // 1: this rank's top front under a remote parent — its boundary rows start the
+                         //    forward solve from the rank's partial b of those (remote) vertices
+};
+
+// Point-sharded plan (subtree-to-rank mapping of the nested-dissection tree).  Every rank runs the
+// same analysis; the top of the tree is split by rank ranges (a front with ranks [lo, hi) is owned by
+// lo, its children get [lo, mid) and [mid, hi), mid by subtree flops) until a range holds one rank,
+// whose whole subtree it then owns.  An edge is owned (linearized, chi2-summed) by the owner of the
+// front of its first-eliminated vertex.  Its contributions to blocks of a remote front (an ancestor)
+// are assembled into the contribution-block region of the rank's top front instead — those rows are
+// boundary rows there — so they reach the owner through the one cross-rank transfer per rank: the
+// packed lower triangle of that top front's contribution block (factorization), its forward-update
+// vector (forward solve) and, back down, the solution of its boundary rows (backward solve).
+struct DistPlan {
+    int32_t rank = 0, nranks = 1;
+    int32_t top = -1;                  // this rank's top front when its parent is remote, else -1
+    struct Xfer {
+        int32_t child = 0, parent = 0, src = 0, dst = 0, level = 0;   // level = height of the parent
+        int32_t u = 0;                 // contribution-block order of the child
+        int64_t buf_off = 0;           // this rank's staging buffer (packed u(u+1)/2 doubles), if a party
+        int64_t ea_off = 0; int32_t nea = 0;   // receiver: packed extend-add tasks (child, j0, i0)
+    };
+    std::vector<Xfer> xfers;           // global list (identical on every rank), by level then child
+    int64_t xbuf_size = 0;
+    std::vector<int32_t> own_rep, own_dep, own_arap;   // global ids of the edges this rank owns
+    std::vector<int32_t> vertex_owner;                 // per vertex (problem order)
+    std::vector<uint8_t> dof_local;                    // per dof: its front is factored on this rank
+    double factor_flops_total = 0;                     // all ranks
+    int64_t nnz_factor_total = 0;
 };
 
 struct Symbolic {
@@ -68,8 +98,8 @@ struct Symbolic {
     std::vector<int32_t> bmap;
     int64_t arena_size = 0, vec_size = 0, inv_size = 0;
     int32_t nlevels = 0;
-    std::vector<std::vector<int32_t>> level_fronts;   // by height, ascending
-    double factor_flops = 0;
+    std::vector<std::vector<int32_t>> level_fronts;   // this rank's fronts by height, ascending
+    double factor_flops = 0;          // this rank's fronts
     double update_flops = 0, diag_flops = 0, trsm_flops = 0;   // per factorization, by kernel
     int64_t nnz_factor = 0;
 
@@ -124,10 +154,13 @@ struct Symbolic {
     std::vector<LevelTasks> levels;
     std::vector<int32_t> task_i32;     // flat task storage (3 ints per task record)
 
+    DistPlan dist;
     std::string error;
 };
 
-// Build the full plan for a validated problem.  Returns false (and sets error) on failure.
-bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points = 32);   // leaf 32: best of 8..64 at C2
+// Build the plan of rank `rank` of `nranks` for a validated problem (nranks = 1: the whole plan).
+// Returns false (and sets error) on failure.
+bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points = 32, int rank = 0,
+             int nranks = 1);   // leaf 32: best of 8..64 at C2
 
 }  // namespace deftri

@@ -50,6 +50,7 @@ class Report(C.Structure):
         ("ms_update", f64),
         ("n_unknowns", i64), ("nnz_factor", i64), ("factor_flops", f64), ("n_fronts", i32),
         ("n_levels", i32), ("lanes", i32), ("trials_executed", i32),
+        ("rank", i32), ("nranks", i32), ("factor_flops_total", f64),
     ]
 
     def as_dict(self):
@@ -65,6 +66,7 @@ class Report(C.Structure):
             "n_unknowns": self.n_unknowns, "nnz_factor": self.nnz_factor,
             "factor_flops": self.factor_flops, "n_fronts": self.n_fronts, "n_levels": self.n_levels,
             "lanes": self.lanes, "trials_executed": self.trials_executed,
+            "rank": self.rank, "nranks": self.nranks, "factor_flops_total": self.factor_flops_total,
         }
 
 
@@ -110,6 +112,8 @@ class BADesc(C.Structure):
 
 # int (*)(void *user, double *host_buf, int64_t n, int32_t op)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, P(f64), i64, i32)
+# int (*)(void *user, int32_t op, int32_t peer, double *buf, int64_t n)   (deftri_xfer_fn)
+XFER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, i32, i32, P(f64), i64)
 
 
 def ptr(a, ctype):

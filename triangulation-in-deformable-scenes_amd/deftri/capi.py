@@ -77,6 +77,13 @@ def load():
         "deftri_ba_eval_system": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, P(C.c_double), P(C.c_double),
                                             P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_int32)]),
         "deftri_rccl_unique_id": (C.c_int, [P(C.c_uint8)]),
+        "deftri_dist_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint8)]),
+        "deftri_dist_set_transport": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _abi.XFER_FN, C.c_void_p]),
+        "deftri_dist_vertex_owner": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int64]),
+        "deftri_plan_vertex_order": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64]),
+        "deftri_dist_owned_edges": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_uint8), P(C.c_uint8)]),
+        "deftri_debug_plan_solve_dist": (C.c_int, [C.c_void_p, P(C.c_double), C.c_double, P(C.c_double),
+                                                   P(C.c_double), C.c_int64]),
         "deftri_ba_dist_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint8)]),
         "deftri_ba_dist_set_allreduce": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _abi.ALLREDUCE_FN,
                                                    C.c_void_p]),
@@ -102,6 +109,8 @@ EXPORTED = [
     "deftri_ba_set_edge_flags", "deftri_ba_solve_lm", "deftri_ba_compute_errors", "deftri_ba_edge_chi2",
     "deftri_ba_download", "deftri_ba_eval_system", "deftri_rccl_unique_id", "deftri_ba_dist_init_rccl",
     "deftri_ba_dist_set_allreduce", "deftri_ba_profile_trial",
+    "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_dist_owned_edges",
+    "deftri_debug_plan_solve_dist",
 ]
 
 
@@ -161,6 +170,52 @@ class Context:
         r = np.ascontiguousarray(rhs, dtype=np.float64)
         x = np.zeros_like(r)
         self._check(self.lib.deftri_debug_plan_solve(self.h, _dp(H), float(lam), _dp(r), _dp(x), len(r)))
+        return x
+
+    # point-sharded solve ---------------------------------------------------------------------
+    def dist_init_rccl(self, nranks, rank, uid):
+        """RCCL communicator (uid: 128 bytes from rccl_unique_id() on rank 0)."""
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._check(self.lib.deftri_dist_init_rccl(self.h, int(nranks), int(rank), buf))
+
+    def dist_set_transport(self, nranks, rank, transport):
+        """Host-memory transport: `transport(op, peer, array)` with op 0 sum / 1 max all-reduce in
+        place, 2 send, 3 receive (array: float64 view of the staging buffer); returns 0."""
+        def cb(_user, op, peer, buf, n):
+            try:
+                arr = np.ctypeslib.as_array(buf, shape=(int(n),)) if n > 0 else np.zeros(0)
+                return int(transport(int(op), int(peer), arr) or 0)
+            except Exception as e:           # never let an exception cross the C frames
+                import sys
+                print(f"deftri transport callback failed: {e!r}", file=sys.stderr, flush=True)
+                return -1
+        self._xfer_cb = _abi.XFER_FN(cb) if nranks > 1 else _abi.XFER_FN()
+        self._check(self.lib.deftri_dist_set_transport(self.h, int(nranks), int(rank), self._xfer_cb, None))
+
+    def vertex_owner(self):
+        nv = self._prob.n_pairs + self._prob.n_scales + self._prob.n_points
+        out = np.zeros(nv, np.int32)
+        self._check(self.lib.deftri_dist_vertex_owner(self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), nv))
+        return out
+
+    def vertex_order(self):
+        nv = self._prob.n_pairs + self._prob.n_scales + self._prob.n_points
+        out = np.zeros(nv, np.int64)
+        self._check(self.lib.deftri_plan_vertex_order(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), nv))
+        return out
+
+    def owned_edges(self):
+        p = self._prob
+        r, d, a = (np.zeros(max(k, 1), np.uint8) for k in (len(p.rep_point), len(p.dep_point), len(p.arap_pair)))
+        u8 = lambda x: x.ctypes.data_as(C.POINTER(C.c_uint8))
+        self._check(self.lib.deftri_dist_owned_edges(self.h, u8(r), u8(d), u8(a)))
+        return (r[:len(p.rep_point)].astype(bool), d[:len(p.dep_point)].astype(bool), a[:len(p.arap_pair)].astype(bool))
+
+    def debug_plan_solve_dist(self, Hq, lam, bq):
+        Hq = np.ascontiguousarray(Hq, dtype=np.float64)
+        bq = np.ascontiguousarray(bq, dtype=np.float64)
+        x = np.zeros_like(bq)
+        self._check(self.lib.deftri_debug_plan_solve_dist(self.h, _dp(Hq), float(lam), _dp(bq), _dp(x), len(bq)))
         return x
 
     def set_lm_lanes(self, lanes):
