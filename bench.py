@@ -59,11 +59,7 @@ def log(*a):
 
 
 def build_problem(n, seed):
-    m, _ = sim.simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True)
-    host = capi.Context(-1)
-    p = host.build_graph(m, REP_W, ARAP_W, DEPTH_SIGMA)
-    host.close()
-    return p
+    return sim.two_view_problem(n, seed, REP_W, ARAP_W, DEPTH_SIGMA)
 
 
 def host_cpu_info():
@@ -84,9 +80,20 @@ def cpu_baseline(prob, order, gpu_trials_per_iter, full_iteration=False):
     first LM iteration with all its trials)."""
     sys.path.insert(0, str(ROOT))
     from oracle import oracle
+    import threading
     oracle.set_vertex_order(order)
     t = time.perf_counter()
-    r = oracle.solve_lm(prob, 1, analytic=False, max_trials=10 if full_iteration else 1)["report"]
+    done = threading.Event()
+
+    def heartbeat():                 # the oracle call is one long C call (ctypes drops the GIL)
+        while not done.wait(30.0):
+            log(f"cpu baseline: oracle running, {time.perf_counter() - t:.0f} s")
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        r = oracle.solve_lm(prob, 1, analytic=False, max_trials=10 if full_iteration else 1)["report"]
+    finally:
+        done.set()
     dt = time.perf_counter() - t
     oracle.set_vertex_order(None)
     trials = max(r["trials_total"], 1)

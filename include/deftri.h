@@ -147,6 +147,9 @@ typedef struct deftri_report {
     int32_t rank;
     int32_t nranks;
     double  factor_flops_total;
+    /* uploads on this context that found the same structure (index arrays and counts) as the
+       analysed plan and only copied the values (no ordering / symbolic analysis / plan upload) */
+    int64_t plan_reuses;
 } deftri_report;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -158,7 +161,9 @@ const char *deftri_last_error(const deftri_ctx *ctx);
 int deftri_abi_version(void);
 
 /* ---- flat-graph API ---------------------------------------------------------------- */
-/* Validate, order (nested dissection), analyse (multifrontal symbolic) and copy to HBM. */
+/* Validate, order (nested dissection), analyse (multifrontal symbolic) and copy to HBM.  A problem
+   with the same structure (counts and index arrays) as the one uploaded before keeps the plan and
+   the device buffers: only the values are copied (deftri_report.plan_reuses counts these). */
 int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc);
 /* Run g2o-semantics Levenberg–Marquardt on the device. */
 int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *params, deftri_report *report);
@@ -177,6 +182,20 @@ int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes);
    g2oTypes.h:341; its analytic one is commented out, g2oTypes.cc:308-331); 1 the closed-form
    Jacobians (an opt-in speed-up, not the reference's arithmetic). */
 int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic);
+/* ---- simulated observations (upstream producer, host) --------------------------------------
+   SLAM::setCameraPoses + getSimulatedDepthMeasurements + createKeyPoints (Modules/System/SLAM.cc:
+   223-338): T1w = (I, c1), T2w = (lookAt(c2, moved[0]), c2) as Sophus SE3f (pose = the fp32 unit
+   quaternion qx qy qz qw + t); depth_k = z_c * depth_scale_k + N(0, depth_error_mm / 1000) and
+   keypoints = KB8 project + N(0, rep_error) rounded to `decimals`, from libstdc++'s
+   std::default_random_engine + std::normal_distribution<float> (one fresh engine per function, as
+   the reference).  orig / moved [n*3], uv [n*2], depth [n]. */
+int deftri_sim_two_view(int32_t n, const float *orig, const float *moved, const float c1[3], const float c2[3],
+                        const float kb8_1[8], const float kb8_2[8], float rep_error, int32_t decimals,
+                        float depth_error_mm, float depth_scale_1, float depth_scale_2, float *uv1, float *uv2,
+                        float *depth1, float *depth2, float pose1[7], float pose2[7]);
+/* n draws of one fresh std::default_random_engine + std::normal_distribution<float>(mean, stddev). */
+int deftri_sim_normal_stream(int64_t n, float mean, float stddev, float *out);
+
 /* ---- point-sharded ARAP solve (multi-GPU) -------------------------------------------------
    One context per GPU, rank `rank` of `nranks`; every rank uploads the same full problem.  The
    nested-dissection tree is split by rank ranges (a rank owns one subtree, the leading ranks of
@@ -330,6 +349,9 @@ int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, cons
 
 /* Build the flattened graph only (no solve): the arrays are owned by the context and stay
    valid until the next call on it.  Used by the parity tests to compare indexing. */
+/* MapPoint id of every point vertex of the last graph deftri_arap_build_graph built (n = its
+   n_points): the write-back key of :974-990. */
+int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n);
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,
                             double arap_weight, float depth_error,
                             const deftri_problem_desc **desc_out);

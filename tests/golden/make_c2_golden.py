@@ -1,0 +1,55 @@
+"""Golden fixture of the headline workload (C2: 100k correspondences x 2 views, bench.py's scene):
+the oracle (oracle/deftri_oracle.c, g2o numeric Jacobians = the reference's arithmetic,
+SimplicialLDLT in the device plan's elimination order) runs the first N_IT LM iterations on the
+full-size problem.  Stored: chi2 per iteration, trials per iteration, final lambda, a fixed
+subsample of the solved points (every 97th), sums of all coordinates, and the reprojection RMSE
+(calculatePixelsStandDev) of the solved map.  The scene is regenerated from its seed by the tests
+(deterministic host code), so only these numbers are committed.
+
+Usage: python tests/golden/make_c2_golden.py   (about 10 minutes of one core)
+"""
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT / "triangulation-in-deformable-scenes_amd"))
+sys.path.insert(0, str(ROOT))
+from deftri import capi, metrics, sim               # noqa: E402
+from oracle import oracle                             # noqa: E402
+
+N_CORR, SEED, N_IT, STRIDE = 100000, 1, 2, 97
+
+
+def main():
+    p, m = sim.two_view_problem(N_CORR, SEED, return_map=True)
+    host = capi.Context(-1)
+    host.analyse(p)
+    oracle.set_vertex_order(host.vertex_order())
+    t = time.time()
+    res = oracle.solve_lm(p, N_IT, analytic=False)
+    dt = time.time() - t
+    R = res["report"]
+    rms0 = metrics.pixels_stand_dev(m)
+    metrics.apply_solution(m, list(p.point_ids), res["points"])
+    rms1 = metrics.pixels_stand_dev(m)
+    d = HERE / "c2"
+    d.mkdir(exist_ok=True)
+    pts = res["points"]
+    np.savez_compressed(d / "expected_c2.npz", points_sub=pts[::STRIDE], chi2_iter=np.array(R["chi2_iter"]),
+                        trials_iter=np.array(R["trials_iter"]))
+    meta = {"n_corr": N_CORR, "seed": SEED, "n_iterations": N_IT, "stride": STRIDE,
+            "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"], "lambda_final": R["lambda_final"],
+            "iterations": R["iterations"], "trials_total": R["trials_total"],
+            "point_sum": pts.sum(0).tolist(), "scales": res["scales"].tolist(), "tg": res["tg"].tolist(),
+            "rms_initial": rms0, "rms_final": rms1, "summary": p.summary(), "oracle_seconds": round(dt, 1)}
+    (d / "expected_c2.json").write_text(json.dumps(meta, indent=1))
+    print(json.dumps(meta))
+
+
+if __name__ == "__main__":
+    main()

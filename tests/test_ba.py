@@ -56,6 +56,9 @@ def test_oracle_gradient_matches_finite_differences():
         pp[l, c] += h; pm[l, c] -= h
         g = (_chi2_at(p, p.poses, pp) - _chi2_at(p, p.poses, pm)) / (2 * h)
         assert g == pytest.approx(-2 * s["b"][6 * K + 3 * l + c], rel=2e-3, abs=1e-2)
+    # the fp32 projection leaves ~1e-7 relative noise on every chi2 term, so the difference quotient
+    # of one component is only good to ~1e-5 of the largest gradient component
+    gmax = np.abs(2 * s["b"][6:6 * K]).max()
     for k in (1, 2):                        # pose (rotation, translation), left-multiplied exp
         for c in range(6):
             h = 1e-4
@@ -63,7 +66,7 @@ def test_oracle_gradient_matches_finite_differences():
             Pp, Pm = p.poses.copy(), p.poses.copy()
             Pp[k] = _se3_left(p.poses[k], u); Pm[k] = _se3_left(p.poses[k], -u)
             g = (_chi2_at(p, Pp, p.points) - _chi2_at(p, Pm, p.points)) / (2 * h)
-            assert g == pytest.approx(-2 * s["b"][6 * k + c], rel=5e-3, abs=1e-1)
+            assert g == pytest.approx(-2 * s["b"][6 * k + c], rel=5e-3, abs=2e-5 * gmax)
 
 
 def test_oracle_schur_step_solves_reduced_system():

@@ -389,3 +389,30 @@ def test_minimal_meshes_match_oracle(gpu_ctx, n):
     ref = oracle.solve_lm(p, 5, analytic=True)["report"]
     assert r["trials_total"] == ref["trials_total"]
     np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+
+
+def test_plan_reuse_same_structure(golden_cases):
+    """A second upload with the same structure (here: the arap weight changed, as in NLopt's weight
+    search) keeps the plan and only copies the values; the solve equals a fresh context's bit for
+    bit."""
+    p = _golden(golden_cases[0])
+    q = Problem.load(GOLDEN / golden_cases[0] / "problem.npz")
+    q.pair_info = q.pair_info * 3.7
+    q.points = q.points + 1e-4
+    with capi.Context(0) as a, capi.Context(0) as b:
+        a.upload(p)
+        a.solve_lm(3)
+        a.upload(q)
+        ra = a.solve_lm(4)
+        pa = a.download()[0]
+        assert ra["plan_reuses"] == 1
+        b.upload(q)
+        rb = b.solve_lm(4)
+        assert rb["plan_reuses"] == 0
+        assert ra["chi2_iter"] == rb["chi2_iter"] and ra["trials_total"] == rb["trials_total"]
+        assert np.array_equal(pa, b.download()[0])
+        r = Problem.load(GOLDEN / golden_cases[0] / "problem.npz")
+        r.arap_pts = r.arap_pts[:-1].copy(); r.arap_pair = r.arap_pair[:-1].copy()
+        r.arap_rot = r.arap_rot[:-1].copy(); r.arap_w = r.arap_w[:-1].copy()
+        a.upload(r)                                        # other structure: analysed again
+        assert a.solve_lm(1)["plan_reuses"] == 1

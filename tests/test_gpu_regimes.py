@@ -1,0 +1,75 @@
+"""Device parity outside the Simulation.yaml regime: the conditioning and
+camera models of the other configs, against the oracle on the same graph.
+  * Realcolon KB8 (d0..d3 != 0, Data/Realcolon.yaml:15-23) with the Realcolon weights (arap 0.1,
+    DepthWeight 0.001 -> sigma_d = 1e-6 m, information 1e12; :101,110)
+  * Drunkard weights (rep 1, arap 1e7, DepthWeight 0.3 -> sigma_d = 3e-4 m; Data/Drunkard.yaml:68,77)
+    with the Drunkard camera
+  * a C3-shaped all-pairs multi-keyframe graph (g2oBundleAdjustment.cc:640-641) at 4 keyframes
+Tolerances as tests/test_gpu_parity.py: linearization rel 1e-11, damped-solve backward error
+< 1e-13, analytic-J LM trajectory chi2 rel 1e-6 with identical trial counts, numeric-J (the
+reference's arithmetic) chi2 rel 1e-5."""
+import numpy as np
+import pytest
+
+from deftri import capi, sim
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+REGIMES = {
+    "realcolon": dict(kb8=sim.REALCOLON_KB8, rep=1.0, arap=0.1, sigma=np.float32(0.001) / np.float32(1000.0)),
+    "drunkard": dict(kb8=sim.DRUNKARD_KB8, rep=1.0, arap=1e7, sigma=np.float32(0.3) / np.float32(1000.0)),
+}
+
+
+def _problem(regime, n=400, seed=5):
+    r = REGIMES[regime]
+    m, _ = sim.simulate_two_view(n=n, seed=seed, kb8=r["kb8"], compact=True)
+    return capi.Context(-1).build_graph(m, r["rep"], r["arap"], np.float32(r["sigma"]))
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300)
+
+
+@pytest.mark.parametrize("regime", sorted(REGIMES))
+def test_linearization_and_solve(gpu_ctx, regime):
+    p = _problem(regime)
+    gpu_ctx.upload(p)
+    assert gpu_ctx.chi2() == pytest.approx(oracle.chi2(p), rel=1e-11)
+    b, d = gpu_ctx.gradient()
+    b_ref, H_ref, _ = oracle.linearize(p, analytic=True, dense=True)
+    assert rel(b, b_ref) < 1e-11
+    assert rel(d, np.diag(H_ref)) < 1e-11
+    assert np.abs(np.diag(H_ref)).max() / np.abs(np.diag(H_ref)).min() > 1e3      # an ill-conditioned regime
+    for lam_rel in (1e-5, 1e-2):
+        lam = lam_rel * np.abs(np.diag(H_ref)).max()
+        x = gpu_ctx.damped_solve(lam, b_ref)
+        A = H_ref + lam * np.eye(len(b_ref))
+        assert np.linalg.norm(A @ x - b_ref) / (np.linalg.norm(A, 2) * np.linalg.norm(x)) < 1e-13
+
+
+@pytest.mark.parametrize("regime", sorted(REGIMES))
+@pytest.mark.parametrize("analytic,tol", [(True, 1e-6), (False, 1e-5)])
+def test_lm_trajectory(gpu_ctx, regime, analytic, tol):
+    p = _problem(regime)
+    gpu_ctx.upload(p)
+    r = gpu_ctx.solve_lm(8, analytic=analytic)
+    ref = oracle.solve_lm(p, 8, analytic=analytic)["report"]
+    assert r["iterations"] == ref["iterations"]
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=tol)
+
+
+def test_all_pairs_multi_keyframe(gpu_ctx):
+    """C3 shape at test size: 4 keyframes, all 6 pairs, each KF's copy of a vertex coupled with every
+    other (24 dofs per mesh vertex at K=8; 12 here), Drunkard camera."""
+    m, _ = sim.simulate_multi_view(n=150, k=4, seed=8)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    assert p.n_pairs == 6
+    gpu_ctx.upload(p)
+    assert gpu_ctx.chi2() == pytest.approx(oracle.chi2(p), rel=1e-11)
+    r = gpu_ctx.solve_lm(5, analytic=False)
+    ref = oracle.solve_lm(p, 5, analytic=False)["report"]
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)

@@ -134,6 +134,8 @@ struct deftri_ctx {
     double *hook_x = nullptr;               // solution vector of the solve in flight (backward transfers)
     int hook_rc = 0;                        // first transport error inside a level hook
     bool dist() const { return nranks > 1; }
+    uint64_t plan_hash = 0;                 // structure_hash of the analysed problem
+    int64_t plan_reuses = 0;                // uploads that reused the plan (values only)
 };
 
 namespace {
@@ -255,6 +257,51 @@ void copy_host(HostProblem &h, const deftri_problem_desc *d) {
     h.d.arap_w = h.arap_w.data(); h.d.rot = h.rot.data(); h.d.pair_area = h.pair_area.data();
     h.d.pair_info = h.pair_info.data();
     h.d.order_xy = h.order_xy.empty() ? nullptr : h.order_xy.data();
+}
+
+// Structure of the normal equations: the counts and every index array (what Eigen's AMD ordering
+// and the symbolic analysis see).  Two problems with the same hash share the plan: NLopt's
+// outerObjective evaluations (nloptOptimization.cc:4-37) rebuild the same graph on clones of one
+// map with other weights, so every evaluation after the first reuses the analysis and the device
+// plan and only copies the values.
+uint64_t structure_hash(const deftri_problem_desc &d) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+        const unsigned char *b = (const unsigned char *)p;
+        for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
+    };
+    const int32_t cnt[8] = {d.n_points, d.n_pairs, d.n_scales, d.n_cams, d.n_rep, d.n_depth, d.n_arap, d.n_rot};
+    mix(cnt, sizeof(cnt));
+    mix(d.rep_point, sizeof(int32_t) * (size_t)d.n_rep);
+    mix(d.rep_cam, sizeof(int32_t) * (size_t)d.n_rep);
+    mix(d.dep_point, sizeof(int32_t) * (size_t)d.n_depth);
+    mix(d.dep_scale, sizeof(int32_t) * (size_t)d.n_depth);
+    mix(d.dep_cam, sizeof(int32_t) * (size_t)d.n_depth);
+    mix(d.arap_pts, sizeof(int32_t) * 4 * (size_t)d.n_arap);
+    mix(d.arap_pair, sizeof(int32_t) * (size_t)d.n_arap);
+    mix(d.arap_rot, sizeof(int32_t) * 2 * (size_t)d.n_arap);
+    return h;
+}
+
+// same structure as the uploaded plan: copy the values (state, cameras, measurements, weights,
+// rotations) into the existing device buffers
+int refresh_values(deftri_ctx *ctx, const HostProblem &h) {
+    DevProblem &P = ctx->P;
+    auto put = [&](auto *dst, const auto &v) -> hipError_t {
+        return v.empty() ? hipSuccess : hipMemcpy(dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice);
+    };
+    std::vector<double> camR(9 * (size_t)std::max(P.C, 1));
+    for (int c = 0; c < P.C; c++) quat_mat(&h.cam_pose[7 * c], &camR[9 * c]);
+    HIPOK(put(P.points, h.points)); HIPOK(put(P.scales, h.scales)); HIPOK(put(P.tg, h.tg));
+    HIPOK(put(ctx->init_state[0], h.points)); HIPOK(put(ctx->init_state[1], h.scales));
+    HIPOK(put(ctx->init_state[2], h.tg));
+    HIPOK(put(P.cam_kb8, h.cam_kb8)); HIPOK(put(P.cam_pose, h.cam_pose)); HIPOK(put(P.cam_R, camR));
+    HIPOK(put(P.rep_obs, h.rep_obs)); HIPOK(put(P.rep_info, h.rep_info));
+    HIPOK(put(P.dep_meas, h.dep_meas)); HIPOK(put(P.dep_info, h.dep_info));
+    HIPOK(put(P.arap_w, h.arap_w)); HIPOK(put(P.rot, h.rot));
+    HIPOK(put(P.pair_area, h.pair_area)); HIPOK(put(P.pair_info, h.pair_info));
+    P.huber_delta = h.d.huber_delta;
+    return 0;
 }
 
 int upload_device(deftri_ctx *ctx, const HostProblem &h) {
@@ -807,6 +854,7 @@ int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     if (ctx->device >= 0) { hipSetDevice(ctx->device); free_device(ctx); }
     ctx->have = false;
     copy_host(ctx->hp, desc);
+    ctx->plan_hash = 0;
     if (!analyse(ctx->hp.d, ctx->S, 32, ctx->rank, ctx->nranks)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
     ctx->analysed = true;
     return 0;
@@ -824,6 +872,7 @@ int deftri_plan_stats(const deftri_ctx *ctx, deftri_report *rep) {
     rep->rank = ctx->rank;
     rep->nranks = ctx->nranks;
     rep->factor_flops_total = ctx->S.dist.factor_flops_total;
+    rep->plan_reuses = ctx->plan_reuses;
     return 0;
 }
 
@@ -921,7 +970,18 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     hipSetDevice(ctx->device);
     int rc = validate(ctx, desc);
     if (rc) return rc;
+    const uint64_t hsh = structure_hash(*desc);
+    static const bool no_cache = std::getenv("DEFTRI_NO_PLAN_CACHE") != nullptr;
+    if (ctx->have && ctx->analysed && hsh == ctx->plan_hash && !no_cache) {
+        copy_host(ctx->hp, desc);
+        if (ctx->dist()) subset_edges(ctx->hp, ctx->S.dist, ctx->hloc);
+        rc = refresh_values(ctx, ctx->dist() ? ctx->hloc : ctx->hp);
+        if (rc) { free_device(ctx); return rc; }
+        ctx->plan_reuses++;
+        return 0;
+    }
     free_device(ctx);
+    ctx->plan_hash = hsh;
     copy_host(ctx->hp, desc);
     if (!analyse(ctx->hp.d, ctx->S, 32, ctx->rank, ctx->nranks)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
     ctx->analysed = true;
@@ -957,6 +1017,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     R.rank = ctx->rank;
     R.nranks = ctx->nranks;
     R.factor_flops_total = ctx->S.dist.factor_flops_total;
+    R.plan_reuses = ctx->plan_reuses;
     const int max_trials = prm->max_trials > 0 ? prm->max_trials : 10;
     const double tau = prm->tau > 0 ? prm->tau : 1e-5;
     const bool analytic = prm->analytic_jacobians != 0;
@@ -1363,6 +1424,13 @@ int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_w
     if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err))
         return fail(ctx, DEFTRI_E_GRAPH, err);
     *desc_out = &ctx->graph.desc;
+    return 0;
+}
+
+int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n) {
+    if (!ctx || !ids) return DEFTRI_E_ARG;
+    if (n != (int64_t)ctx->graph.point_mpid.size()) return DEFTRI_E_ARG;
+    std::memcpy(ids, ctx->graph.point_mpid.data(), sizeof(int64_t) * (size_t)n);
     return 0;
 }
 

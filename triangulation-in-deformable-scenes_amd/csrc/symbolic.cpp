@@ -2,11 +2,14 @@
 #include "symbolic.h"
 
 #include <algorithm>
+#include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
 #include <numeric>
+#include <thread>
 
 namespace deftri {
 
@@ -25,16 +28,41 @@ struct Builder {
     std::vector<std::vector<int64_t>> bnd;        // per front: boundary vertices (elim order)
     std::vector<int32_t> vfront;                  // vertex -> owning front
     int64_t next_pos = 0;
-    std::vector<int32_t> side;
-    std::vector<int32_t> stamp;      // distinct-count scratch
-    int32_t stamp_id = 0;
+    // per-thread scratch of the nested dissection, indexed by point (the subdomains of concurrent
+    // tasks are disjoint, but their separator searches read the neighbours' sides)
+    struct Scratch {
+        std::vector<int32_t> side;
+        std::vector<int32_t> stamp;      // distinct-count scratch
+        int32_t stamp_id = 0;
+        std::vector<int64_t> spos;       // index of a point in the separator list being refined
+        explicit Scratch(int32_t n) : side(std::max(n, 1), 0), stamp(std::max(n, 1), 0), spos(std::max(n, 1), -1) {}
+    };
+    // dissection tree under construction: fronts in postorder (own vertices, children; -1 = none)
+    struct LocalTree {
+        std::vector<std::vector<int64_t>> own;
+        std::vector<std::array<int32_t, 2>> ch;
+        int32_t add(std::vector<int64_t> &&ov, int32_t c0, int32_t c1) {
+            own.push_back(std::move(ov));
+            ch.push_back({c0, c1});
+            return (int32_t)own.size() - 1;
+        }
+        int32_t append(LocalTree &&o) {          // o's fronts after ours; returns the index offset
+            const int32_t off = (int32_t)own.size();
+            for (size_t i = 0; i < o.own.size(); i++) {
+                own.push_back(std::move(o.own[i]));
+                ch.push_back({o.ch[i][0] < 0 ? -1 : o.ch[i][0] + off, o.ch[i][1] < 0 ? -1 : o.ch[i][1] + off});
+            }
+            return off;
+        }
+    };
     int nd_dirs = 4;
     int nd_passes = 8;
     int nd_try = 3;
     double nd_bal = 0.55;
-    std::vector<int64_t> spos;       // index of a point in the separator list being refined
 
     int rank = 0, nranks = 1;
+    int par_depth = 3;                   // dissection levels whose halves run concurrently (2^3 threads)
+    static constexpr int64_t par_min = 4096;   // smallest subdomain worth a thread
     Builder(const deftri_problem_desc &d_, Symbolic &S_, int leaf_, int rank_, int nranks_)
         : d(d_), S(S_), leaf(leaf_), rank(rank_), nranks(nranks_) {
         Q = d.n_pairs; NS = d.n_scales; P = d.n_points;
@@ -44,28 +72,50 @@ struct Builder {
     int64_t vS(int k) const { return (int64_t)Q + k; }
     int64_t vP(int p) const { return (int64_t)Q + NS + p; }
 
+    // vertex adjacency (sorted, unique, no self): bucket the coupled pairs by vertex, then sort and
+    // deduplicate every vertex's list (threads over vertex ranges)
     void build_adjacency() {
-        int64_t nv = S.nv;
-        std::vector<std::pair<int64_t, int64_t>> pr;
-        pr.reserve((size_t)d.n_depth * 2 + (size_t)d.n_arap * 20);
-        for (int e = 0; e < d.n_depth; e++) {
-            int64_t a = vP(d.dep_point[e]), b = vS(d.dep_scale[e]);
-            pr.emplace_back(a, b); pr.emplace_back(b, a);
+        const int64_t nv = S.nv;
+        auto each_pair = [&](auto &&fn) {
+            for (int e = 0; e < d.n_depth; e++) {
+                int64_t a = vP(d.dep_point[e]), b = vS(d.dep_scale[e]);
+                fn(a, b); fn(b, a);
+            }
+            for (int e = 0; e < d.n_arap; e++) {
+                int64_t v[5];
+                for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
+                v[4] = vT(d.arap_pair[e]);
+                for (int i = 0; i < 5; i++)
+                    for (int j = 0; j < 5; j++)
+                        if (i != j && v[i] != v[j]) fn(v[i], v[j]);
+            }
+        };
+        std::vector<int64_t> cnt(nv + 1, 0);
+        each_pair([&](int64_t a, int64_t) { cnt[a + 1]++; });
+        for (int64_t v = 0; v < nv; v++) cnt[v + 1] += cnt[v];
+        std::vector<int64_t> raw((size_t)cnt[nv]);
+        {
+            std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+            each_pair([&](int64_t a, int64_t b) { raw[pos[a]++] = b; });
         }
-        for (int e = 0; e < d.n_arap; e++) {
-            int64_t v[5];
-            for (int k = 0; k < 4; k++) v[k] = vP(d.arap_pts[4 * (int64_t)e + k]);
-            v[4] = vT(d.arap_pair[e]);
-            for (int i = 0; i < 5; i++)
-                for (int j = 0; j < 5; j++)
-                    if (i != j && v[i] != v[j]) pr.emplace_back(v[i], v[j]);
-        }
-        std::sort(pr.begin(), pr.end());
-        pr.erase(std::unique(pr.begin(), pr.end()), pr.end());
+        std::vector<int64_t> len(nv, 0);
+        const int nt = (int)std::max<unsigned>(1, std::min<unsigned>(8, std::thread::hardware_concurrency()));
+        auto work = [&](int t) {
+            for (int64_t v = t; v < nv; v += nt) {
+                auto b = raw.begin() + cnt[v], e = raw.begin() + cnt[v + 1];
+                std::sort(b, e);
+                len[v] = std::unique(b, e) - b;
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; t++) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
         adj_begin.assign(nv + 1, 0);
-        adj.resize(pr.size());
-        for (size_t i = 0; i < pr.size(); i++) { adj_begin[pr[i].first + 1]++; adj[i] = pr[i].second; }
-        for (int64_t v = 0; v < nv; v++) adj_begin[v + 1] += adj_begin[v];
+        for (int64_t v = 0; v < nv; v++) adj_begin[v + 1] = adj_begin[v] + len[v];
+        adj.resize((size_t)adj_begin[nv]);
+        for (int64_t v = 0; v < nv; v++)
+            std::copy(raw.begin() + cnt[v], raw.begin() + cnt[v] + len[v], adj.begin() + adj_begin[v]);
     }
 
     int32_t new_front(std::vector<int64_t> &&ownv, std::vector<int32_t> children) {
@@ -87,7 +137,8 @@ struct Builder {
     // neighbours in the other half into the separator (size change: -1 + that count).  Each pass
     // makes the best balanced move repeatedly (hill-climbing through non-positive gains, moved
     // points locked) and rolls back to the smallest separator seen.
-    void refine_sep(std::vector<int64_t> &sep, int64_t &nA, int64_t &nB, int64_t ntot) {
+    void refine_sep(std::vector<int64_t> &sep, int64_t &nA, int64_t &nB, int64_t ntot, Scratch &sc) {
+        auto &side = sc.side; auto &stamp = sc.stamp; auto &spos = sc.spos;
         const int64_t cap = (int64_t)std::ceil(nd_bal * (double)ntot);
         for (size_t i = 0; i < sep.size(); i++) spos[sep[i]] = (int64_t)i;
         auto sep_add = [&](int64_t u) { spos[u] = (int64_t)sep.size(); sep.push_back(u); };
@@ -108,7 +159,7 @@ struct Builder {
             std::vector<int64_t> pulled;
             size_t best_len = 0;
             int64_t best_sz = (int64_t)sep.size(), best_imb = std::llabs(nA - nB);
-            const int32_t lock = ++stamp_id;
+            const int32_t lock = ++sc.stamp_id;
             const int64_t maxsteps = (int64_t)sep.size();
             for (int64_t step = 0; step < maxsteps; step++) {
                 int64_t bv = -1, bg = 0, bimb = 0;
@@ -152,14 +203,19 @@ struct Builder {
         for (int64_t p : sep) spos[p] = -1;
     }
 
-    int32_t nd(std::vector<int64_t> &nodes, int depth) {
+    // nested dissection of `nodes` into T (postorder); returns the subtree's root.  The two halves of
+    // a large subdomain near the top are dissected concurrently (left on a new thread with its own
+    // scratch, right here) and appended in the sequential order, so the tree — and every elimination
+    // position — is the same as a one-thread run.
+    int32_t nd(std::vector<int64_t> &nodes, int depth, Scratch &sc, LocalTree &T) {
+        auto &side = sc.side;
         int64_t n = (int64_t)nodes.size();
         if (n <= leaf || depth > 48) {
             std::vector<int64_t> o(nodes.begin(), nodes.end());
             std::sort(o.begin(), o.end());
             std::vector<int64_t> ov;
             for (int64_t p : o) ov.push_back(vP((int32_t)p));
-            return new_front(std::move(ov), {});
+            return T.add(std::move(ov), -1, -1);
         }
         // vertex separator: order along a direction, cut, take the boundary vertices of one side (the
         // cut edges need one endpoint each).  Four directions (x, y, both diagonals) x three cut
@@ -217,7 +273,7 @@ struct Builder {
             if (nd_passes > 0) {
                 int64_t nA = 0, nB = 0;
                 for (int64_t p : nodes) { nA += side[p] == 1; nB += side[p] == 2; }
-                refine_sep(sep, nA, nB, n);
+                refine_sep(sep, nA, nB, n, sc);
             }
         };
         size_t best = 0;
@@ -244,14 +300,35 @@ struct Builder {
             std::vector<int64_t> ov;
             std::sort(nodes.begin(), nodes.end());
             for (int64_t p : nodes) ov.push_back(vP((int32_t)p));
-            return new_front(std::move(ov), {});
+            return T.add(std::move(ov), -1, -1);
         }
-        int32_t cl = nd(L, depth + 1);
-        int32_t cr = nd(R, depth + 1);
+        int32_t cl, cr;
+        if (depth < par_depth && n >= par_min) {
+            LocalTree TL, TR;
+            int32_t rl = -1;
+            std::thread th([&] { Scratch sl(P); rl = nd(L, depth + 1, sl, TL); });
+            const int32_t rr = nd(R, depth + 1, sc, TR);
+            th.join();
+            cl = T.append(std::move(TL)) + rl;
+            cr = T.append(std::move(TR)) + rr;
+        } else {
+            cl = nd(L, depth + 1, sc, T);
+            cr = nd(R, depth + 1, sc, T);
+        }
         std::sort(Sp.begin(), Sp.end());
         std::vector<int64_t> ov;
         for (int64_t p : Sp) ov.push_back(vP((int32_t)p));
-        return new_front(std::move(ov), {cl, cr});
+        return T.add(std::move(ov), cl, cr);
+    }
+
+    // phase timing of the analysis (DEFTRI_DEBUG_TIME)
+    std::chrono::steady_clock::time_point t_last = std::chrono::steady_clock::now();
+    bool dbg_time = std::getenv("DEFTRI_DEBUG_TIME") != nullptr;
+    void tick(const char *what) {
+        if (!dbg_time) return;
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[analyse] %-24s %8.3f s\n", what, std::chrono::duration<double>(now - t_last).count());
+        t_last = now;
     }
 
     bool run() {
@@ -267,23 +344,34 @@ struct Builder {
         S.elim_pos.assign(S.nv, -1);
         vfront.assign(S.nv, -1);
         build_adjacency();
+        tick("adjacency");
         xy.resize(2 * (size_t)std::max(P, 1));
         for (int32_t p = 0; p < P; p++) {
             if (d.order_xy) { xy[2 * p] = d.order_xy[2 * p]; xy[2 * p + 1] = d.order_xy[2 * p + 1]; }
             else { xy[2 * p] = d.points[3 * (int64_t)p]; xy[2 * p + 1] = d.points[3 * (int64_t)p + 1]; }
         }
-        side.assign(std::max(P, 1), 0);
-        stamp.assign(std::max(P, 1), 0);
-        spos.assign(std::max(P, 1), -1);
+
         if (const char *e = std::getenv("DEFTRI_ND_TRY")) nd_try = std::atoi(e);
         if (const char *e = std::getenv("DEFTRI_ND_PASSES")) nd_passes = std::atoi(e);
         if (const char *e = std::getenv("DEFTRI_ND_BAL")) nd_bal = std::atof(e);
         if (const char *e = std::getenv("DEFTRI_ND_DIRS")) nd_dirs = std::min(16, std::max(1, std::atoi(e)));
+        if (const char *e = std::getenv("DEFTRI_ND_THREADS")) par_depth = std::max(0, std::atoi(e));
         std::vector<int32_t> rootch;
         if (P > 0) {
             std::vector<int64_t> nodes(P);
             std::iota(nodes.begin(), nodes.end(), 0);
-            rootch.push_back(nd(nodes, 0));
+            Scratch sc(P);
+            LocalTree T;
+            const int32_t root = nd(nodes, 0, sc, T);
+            // postorder -> fronts (elimination positions in the same order as a sequential run)
+            std::vector<int32_t> gid(T.own.size(), -1);
+            for (size_t i = 0; i < T.own.size(); i++) {
+                std::vector<int32_t> chl;
+                for (int c = 0; c < 2; c++) if (T.ch[i][c] >= 0) chl.push_back(gid[T.ch[i][c]]);
+                gid[i] = new_front(std::move(T.own[i]), chl);
+            }
+            rootch.push_back(gid[root]);
+        tick("nested dissection");
         }
         std::vector<int64_t> gl;
         for (int q = 0; q < Q; q++) gl.push_back(vT(q));
@@ -306,6 +394,7 @@ struct Builder {
             cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
             bnd[f] = cand;
         }
+        tick("boundaries");
         // rows and sizes (every rank knows the whole tree)
         std::vector<std::vector<int64_t>> fv(nf);       // vertex list (row order)
         std::vector<std::vector<int32_t>> fvrow(nf);    // local row of each vertex
@@ -491,6 +580,7 @@ struct Builder {
             }
         }
 
+        tick("fronts/ranks/offsets");
         // ---------------- H blocks ----------------
         // column vertex c, row vertices r with elim[r] >= elim[c], r coupled with c (or r == c).  A
         // column of this rank's fronts: every coupled row (blocks no owned edge feeds stay zero; the
@@ -584,27 +674,32 @@ struct Builder {
                             std::vector<uint64_t> &recs, std::vector<int64_t> &cbeg,
                             std::vector<int32_t> &clen, std::vector<int32_t> &ckey,
                             std::vector<int64_t> &key_chunk) {
-            std::stable_sort(lst.begin(), lst.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+            // stable counting sort by key (the records of a key keep their edge order)
+            std::vector<int64_t> kbeg(nkeys + 1, 0);
+            for (const auto &x : lst) kbeg[x.first + 1]++;
+            for (int64_t k = 0; k < nkeys; k++) kbeg[k + 1] += kbeg[k];
             recs.resize(lst.size());
-            for (size_t i = 0; i < lst.size(); i++) recs[i] = lst[i].second;
+            {
+                std::vector<int64_t> pos(kbeg.begin(), kbeg.end() - 1);
+                for (const auto &x : lst) recs[pos[x.first]++] = x.second;
+            }
+            std::vector<std::pair<int64_t, uint64_t>>().swap(lst);
             key_chunk.assign(nkeys + 1, 0);
-            size_t i = 0;
             for (int64_t k = 0; k < nkeys; k++) {
                 key_chunk[k] = (int64_t)cbeg.size();
-                size_t j = i;
-                while (j < lst.size() && lst[j].first == k) j++;
-                for (size_t s0 = i; s0 < j; s0 += kChunk) {
-                    cbeg.push_back((int64_t)s0);
-                    clen.push_back((int32_t)std::min<size_t>(kChunk, j - s0));
+                for (int64_t s0 = kbeg[k]; s0 < kbeg[k + 1]; s0 += kChunk) {
+                    cbeg.push_back(s0);
+                    clen.push_back((int32_t)std::min<int64_t>(kChunk, kbeg[k + 1] - s0));
                     ckey.push_back((int32_t)k);
                 }
-                i = j;
             }
             key_chunk[nkeys] = (int64_t)cbeg.size();
         };
         chunkify(hc, S.nblocks, S.hcontrib, S.hchunk_begin, S.hchunk_len, S.hchunk_block, S.hblk_chunk_begin);
+        tick("blocks+contributions");
         chunkify(bc, S.nv, S.bcontrib, S.bchunk_begin, S.bchunk_len, S.bchunk_vertex, S.bv_chunk_begin);
 
+        tick("chunking");
         // ---------------- task lists ----------------
         auto push3 = [&](int32_t a, int32_t b, int32_t c) {
             S.task_i32.push_back(a); S.task_i32.push_back(b); S.task_i32.push_back(c);
@@ -770,6 +865,7 @@ struct Builder {
                 LT.bsteps.push_back(st);
             }
         }
+        tick("task lists");
         // packed extend-add of the contribution blocks received from other ranks (same task shape as
         // the extend-add: 16 CB columns x 256 CB rows, lower triangle)
         for (auto &x : D.xfers) {

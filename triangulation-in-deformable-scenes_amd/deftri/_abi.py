@@ -50,7 +50,7 @@ class Report(C.Structure):
         ("ms_update", f64),
         ("n_unknowns", i64), ("nnz_factor", i64), ("factor_flops", f64), ("n_fronts", i32),
         ("n_levels", i32), ("lanes", i32), ("trials_executed", i32),
-        ("rank", i32), ("nranks", i32), ("factor_flops_total", f64),
+        ("rank", i32), ("nranks", i32), ("factor_flops_total", f64), ("plan_reuses", i64),
     ]
 
     def as_dict(self):
@@ -67,6 +67,7 @@ class Report(C.Structure):
             "factor_flops": self.factor_flops, "n_fronts": self.n_fronts, "n_levels": self.n_levels,
             "lanes": self.lanes, "trials_executed": self.trials_executed,
             "rank": self.rank, "nranks": self.nranks, "factor_flops_total": self.factor_flops_total,
+            "plan_reuses": self.plan_reuses,
         }
 
 

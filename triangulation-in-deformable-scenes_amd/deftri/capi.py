@@ -58,6 +58,7 @@ def load():
         "deftri_num_unknowns": (C.c_int64, [C.c_void_p]),
         "deftri_sizeof": (C.c_int64, [C.c_int32]),
         "deftri_profile_trial": (C.c_int, [C.c_void_p, C.c_double, P(_abi.KernelStat), C.c_int32, P(C.c_int32)]),
+        "deftri_arap_graph_point_ids": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64]),
         "deftri_arap_build_graph": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_float,
                                               P(P(_abi.ProblemDesc))]),
         "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
@@ -81,6 +82,11 @@ def load():
         "deftri_dist_set_transport": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _abi.XFER_FN, C.c_void_p]),
         "deftri_dist_vertex_owner": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int64]),
         "deftri_plan_vertex_order": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64]),
+        "deftri_sim_normal_stream": (C.c_int, [C.c_int64, C.c_float, C.c_float, P(C.c_float)]),
+        "deftri_sim_two_view": (C.c_int, [C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_float),
+                                          P(C.c_float), P(C.c_float), C.c_float, C.c_int32, C.c_float, C.c_float,
+                                          C.c_float, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_float),
+                                          P(C.c_float), P(C.c_float)]),
         "deftri_dist_owned_edges": (C.c_int, [C.c_void_p, P(C.c_uint8), P(C.c_uint8), P(C.c_uint8)]),
         "deftri_debug_plan_solve_dist": (C.c_int, [C.c_void_p, P(C.c_double), C.c_double, P(C.c_double),
                                                    P(C.c_double), C.c_int64]),
@@ -103,13 +109,13 @@ EXPORTED = [
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
     "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
-    "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_optimization",
+    "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_graph_point_ids", "deftri_arap_optimization",
     "deftri_profile_trial",
     "deftri_ba_create", "deftri_ba_destroy", "deftri_ba_last_error", "deftri_ba_upload", "deftri_ba_set_state",
     "deftri_ba_set_edge_flags", "deftri_ba_solve_lm", "deftri_ba_compute_errors", "deftri_ba_edge_chi2",
     "deftri_ba_download", "deftri_ba_eval_system", "deftri_rccl_unique_id", "deftri_ba_dist_init_rccl",
     "deftri_ba_dist_set_allreduce", "deftri_ba_profile_trial",
-    "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_dist_owned_edges",
+    "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream", "deftri_dist_owned_edges",
     "deftri_debug_plan_solve_dist",
 ]
 
@@ -275,7 +281,11 @@ class Context:
         out = C.POINTER(_abi.ProblemDesc)()
         self._check(self.lib.deftri_arap_build_graph(self.h, C.byref(mc), float(rep_weight), float(arap_weight),
                                                      C.c_float(depth_error), C.byref(out)))
-        return Problem.from_desc(out.contents)
+        p = Problem.from_desc(out.contents)
+        ids = np.zeros(p.n_points, np.int64)
+        self._check(self.lib.deftri_arap_graph_point_ids(self.h, ids.ctypes.data_as(C.POINTER(C.c_int64)), p.n_points))
+        p.point_ids = ids
+        return p
 
     def pixels_stand_dev(self, m):
         """calculatePixelsStandDev (Geometry.cc:370-498) of a Map on the device."""
@@ -420,6 +430,25 @@ class BAContext:
         self._check(self.lib.deftri_ba_profile_trial(self.h, float(lam), arr, 64, C.byref(n)))
         return {arr[i].name.decode(): {"launches": arr[i].launches, "ms": arr[i].ms, "flops": arr[i].flops,
                                        "bytes": arr[i].bytes} for i in range(n.value)}
+
+
+def sim_two_view(orig, moved, c1, c2, kb8_1, kb8_2, rep_error, decimals, depth_error_mm, depth_scales):
+    """deftri_sim_two_view: the reference's simulated keypoints / depths / camera poses (SLAM.cc:223-338)."""
+    lib = load()
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)
+    orig, moved = f32(orig).reshape(-1, 3), f32(moved).reshape(-1, 3)
+    n = len(orig)
+    c1, c2, k1, k2 = f32(c1), f32(c2), f32(kb8_1), f32(kb8_2)
+    uv1 = np.zeros((n, 2), np.float32); uv2 = np.zeros((n, 2), np.float32)
+    d1 = np.zeros(n, np.float32); d2 = np.zeros(n, np.float32)
+    p1 = np.zeros(7, np.float32); p2 = np.zeros(7, np.float32)
+    fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+    rc = lib.deftri_sim_two_view(n, fp(orig), fp(moved), fp(c1), fp(c2), fp(k1), fp(k2), float(rep_error),
+                                 int(decimals), float(depth_error_mm), float(depth_scales[0]),
+                                 float(depth_scales[1]), fp(uv1), fp(uv2), fp(d1), fp(d2), fp(p1), fp(p2))
+    if rc != 0:
+        raise DeftriError(rc, "deftri_sim_two_view")
+    return uv1, uv2, d1, d2, p1, p2
 
 
 def rccl_unique_id():

@@ -57,9 +57,12 @@ def mat_from_quat(q):
 
 class SE3f:
     """Sophus::SE3f stand-in: rotation (fp32 3x3) + translation (fp32)."""
-    def __init__(self, R=None, t=None):
+    def __init__(self, R=None, t=None, q=None):
         self.R = np.eye(3, dtype=np.float32) if R is None else np.asarray(R, dtype=np.float32)
         self.t = np.zeros(3, dtype=np.float32) if t is None else np.asarray(t, dtype=np.float32)
+        # Sophus stores the rotation as an fp32 unit quaternion (x y z w); when the pose was built
+        # the reference's way (deftri_sim_two_view) that exact quaternion is kept for as7()
+        self.q = None if q is None else np.asarray(q, dtype=np.float32)
 
     def __mul__(self, o):
         if isinstance(o, SE3f):
@@ -75,7 +78,7 @@ class SE3f:
 
     def as7(self):
         """g2o::SE3Quat(unit_quaternion().cast<double>(), translation().cast<double>())."""
-        q = self.unit_quaternion().astype(np.float32).astype(np.float64)
+        q = (self.q if self.q is not None else self.unit_quaternion().astype(np.float32)).astype(np.float64)
         if q[3] < 0:
             q = -q
         q = q / np.linalg.norm(q)

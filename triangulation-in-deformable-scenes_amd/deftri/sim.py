@@ -13,9 +13,12 @@ Recipe, per reference file:
               triangulateNRSLAM(..., "FarPoints") Geometry.cc:103-153 and isValidParallax
               Mapping.cc:351-364 (fp32 math)
   sigma table Frame.cc:61-75 (nScales, scale factor)
-Noise uses numpy's PCG64 with a fixed seed (the reference uses libstdc++'s default_random_engine;
-the solver's parity tests feed the same generated inputs to both sides, so the stream itself is not
-part of the parity claim).
+Noise streams: the keypoint and depth noise and the camera poses come from deftri_sim_two_view
+(csrc/sim_host.cpp): libstdc++'s std::default_random_engine (minstd_rand0, seed 1) and
+std::normal_distribution<float>, one fresh engine per function as in SLAM.cc, Sophus-style SE3f
+(fp32 unit quaternion) poses — the reference's own numbers for the reference's inputs.  The point
+clouds follow create_data.py, whose np.random is unseeded; here a seeded legacy RandomState drawn in
+the script's order (x, y, z columns, then x, y, z motion noise per point).
 
 Multi-keyframe scenes (configs C3-C5) extend the same recipe: K cameras on an arc, each observing
 its own deformed copy of the cloud.
@@ -48,16 +51,18 @@ def rotate_points(points, ax, ay, az):
 
 def generate_points(n, rigid=0.0025, gaussian=0.0025, seed=0, scale_density=True,
                     stds=(0.03, 0.001, 0.01), mean=(0.0, 0.0, 0.2), angles=(-45, 0, 45)):
-    """create_data.py:27-66 (Planar motion along y)."""
-    rng = np.random.default_rng(seed)
+    """create_data.py:27-66 (Planar motion along y), its draw order with np.random seeded: the three
+    coordinate columns, then per point the rigid offset and N(0, gaussian) on x, y, z (drawn even at
+    gaussian = 0, as np.random.normal(scale=0) is)."""
+    rs = np.random.RandomState(seed)
     s = np.sqrt(n / 120.0) if scale_density else 1.0
     orig = np.zeros((n, 3))
-    orig[:, 0] = rng.normal(0.0, stds[0] * s, n)
-    orig[:, 1] = rng.normal(0.0, stds[1] * s, n)
-    orig[:, 2] = rng.normal(0.0, stds[2] * s, n)
+    orig[:, 0] = rs.normal(0.0, stds[0] * s, n)
+    orig[:, 1] = rs.normal(0.0, stds[1] * s, n)
+    orig[:, 2] = rs.normal(0.0, stds[2] * s, n)
     moved = orig.copy()
     moved[:, 1] += rigid
-    moved += rng.normal(0.0, gaussian, (n, 3)) if gaussian > 0 else 0.0
+    moved += rs.normal(0.0, gaussian, (n, 3))
     orig = rotate_points(orig, *angles) + np.asarray(mean)
     moved = rotate_points(moved, *angles) + np.asarray(mean)
     return orig, moved
@@ -156,7 +161,6 @@ def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.1
       SURVEY Appendix B.2 — a compacted scene is the same as running the reference on the
       filtered point files).
     Returns (Map, ground_truth dict)."""
-    rng = np.random.default_rng(seed + 1000003)
     if orig is None:
         sc = np.sqrt(n / 120.0) if scale_scene else 1.0
         orig, moved = generate_points(n, rigid=rigid, gaussian=gaussian, seed=seed,
@@ -164,20 +168,13 @@ def simulate_two_view(n=120, seed=0, orig=None, moved=None, c1=(-0.10, 0.02, 0.1
         c1 = tuple(np.asarray(c1) * sc); c2 = tuple(np.asarray(c2) * sc)
     orig = np.asarray(orig, np.float32); moved = np.asarray(moved, np.float32)
     n = len(orig)
-    T1w = SE3f(np.eye(3, dtype=np.float32), np.asarray(c1, np.float32))
-    T2w = SE3f(look_at(c2, moved[0]), np.asarray(c2, np.float32))
-    pc1 = T1w * orig
-    pc2 = T2w * moved
-    # SLAM::getSimulatedDepthMeasurements
-    dn = rng.normal(0.0, depth_error / 1000.0, (n, 2)).astype(np.float32)
-    d1 = (pc1[:, 2] * np.float32(depth_scales[0]) + dn[:, 0]).astype(np.float32)
-    d2 = (pc2[:, 2] * np.float32(depth_scales[1]) + dn[:, 1]).astype(np.float32)
-    # SLAM::createKeyPoints
-    kn = rng.normal(0.0, rep_error, (n, 4)).astype(np.float32)
-    uv1 = kb8_project(kb8, pc1); uv2 = kb8_project(kb8, pc2)
-    f = 10.0 ** decimals
-    uv1 = (np.round((uv1.astype(np.float64) + kn[:, :2]) * f) / f).astype(np.float32)
-    uv2 = (np.round((uv2.astype(np.float64) + kn[:, 2:]) * f) / f).astype(np.float32)
+    # SLAM::setCameraPoses + getSimulatedDepthMeasurements + createKeyPoints (SLAM.cc:223-338): the
+    # reference's noise streams and Sophus poses (host C++, deftri_sim_two_view)
+    from . import capi
+    uv1, uv2, d1, d2, q1, q2 = capi.sim_two_view(orig, moved, c1, c2, kb8, kb8, rep_error, decimals, depth_error,
+                                                 depth_scales)
+    T1w = SE3f(np.eye(3, dtype=np.float32), np.asarray(c1, np.float32), q=q1[:4])
+    T2w = SE3f(look_at(c2, moved[0]), np.asarray(c2, np.float32), q=q2[:4])
     inv_s2 = inv_sigma2_table(n_scales, scale_factor)
     kf0 = KeyFrame(0, T1w, kb8, n, inv_s2, uv1, np.zeros(n, np.int32), d1)
     kf1 = KeyFrame(1, T2w, kb8, n, inv_s2, uv2, np.zeros(n, np.int32), d2)
@@ -236,3 +233,15 @@ def simulate_multi_view(n=1000, k=8, seed=0, kb8=DRUNKARD_KB8, radius=0.12, rep_
             m.add_observation(kk, mp.id, i)
             kf.map_points[i] = mp
     return m, {"base": base}
+
+
+def two_view_problem(n, seed=1, rep_weight=1.0, arap_weight=2e5, depth_sigma=np.float32(0.003), return_map=False):
+    """The benchmark scene (BASELINE C1/C2 shapes): simulate_two_view with the extents scaled to n
+    correspondences and failed triangulations dropped, then the arapOptimization graph built by the
+    product's host builder (deftri_arap_build_graph)."""
+    from . import capi
+    m, _ = simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True)
+    host = capi.Context(-1)
+    p = host.build_graph(m, rep_weight, arap_weight, depth_sigma)
+    host.close()
+    return (p, m) if return_map else p
