@@ -87,6 +87,10 @@ def test_schur_system_matches_oracle(bactx, name):
             assert np.linalg.norm(g["S"] @ xp - g["rhs"]) / (np.linalg.norm(g["S"], 2) * np.linalg.norm(xp)) < 1e-14
 
 
+def _rmse(chi, info):
+    return float(np.sqrt(np.mean(chi / info / 2.0)))
+
+
 def _gauge_fixed(p):
     """Fix KF 1 as well as KF 0: monocular BA with one fixed pose keeps a free scale, along which
     LM drifts by amounts set by last-bit differences (any two correct solvers disagree there)."""
@@ -98,57 +102,63 @@ def _gauge_fixed(p):
 
 @pytest.mark.parametrize("name", ["dense", "partial_visibility", "flags", "pose_only"])
 def test_lm_matches_oracle(bactx, name):
+    """The LM trajectory up to the fp32 noise floor (iterations whose chi2 still decreases by more
+    than 1e-6 relative): identical trial counts, chi2 rel 1e-6 and the states at that iteration
+    within 1e-5.  Past it the rho test compares projection noise, so trial counts and the exact
+    resting point are not parity properties: the 15-iteration runs compare chi2 rel 1e-6 and the
+    per-edge errors at their final states."""
     p = _gauge_fixed(_problems()[name])
-    bactx.upload(p)
-    r = bactx.solve_lm(15)
-    poses, pts = bactx.download()
-    o = oracle.ba_solve(p, 15)
-    ro = o["report"]
-    print(name, "chi2", r["chi2_iter"][-1], ro["chi2_iter"][-1], "pose", np.abs(poses - o["poses"]).max(),
-          "pts", np.abs(pts - o["points"]).max(), r["trials_iter"], ro["trials_iter"])
-    # once chi2 stalls near the fp32-projection noise floor (relative decrease < 1e-6) the rho test
-    # compares noise: trial counts after that point are not a parity property
-    c = [ro["chi2_initial"]] + ro["chi2_iter"]
+    o15 = oracle.ba_solve(p, 15)
+    c = [o15["report"]["chi2_initial"]] + o15["report"]["chi2_iter"]
     n_cmp = next((i for i in range(1, len(c)) if c[i - 1] - c[i] < 1e-6 * c[i]), len(c) - 1)
-    assert r["trials_iter"][:n_cmp] == ro["trials_iter"][:n_cmp]
+    n_cmp = max(n_cmp, 1)
+    bactx.upload(p)
+    r = bactx.solve_lm(n_cmp)
+    poses, pts = bactx.download()
+    o = oracle.ba_solve(p, n_cmp)
+    ro = o["report"]
+    print(name, n_cmp, "chi2", r["chi2_iter"][-1], ro["chi2_iter"][-1], "pose", np.abs(poses - o["poses"]).max(),
+          "pts", np.abs(pts - o["points"]).max(), r["trials_iter"], ro["trials_iter"])
+    assert r["trials_iter"] == ro["trials_iter"]
     assert r["chi2_initial"] == pytest.approx(ro["chi2_initial"], rel=1e-6)
-    np.testing.assert_allclose(r["chi2_iter"][:n_cmp], ro["chi2_iter"][:n_cmp], rtol=1e-6)
-    assert r["chi2_final"] == pytest.approx(ro["chi2_final"], rel=1e-6)
+    np.testing.assert_allclose(r["chi2_iter"], ro["chi2_iter"], rtol=1e-6)
     assert np.abs(poses - o["poses"]).max() < 1e-5
     assert np.abs(pts - o["points"]).max() < 1e-5
-    # cached errors hold the last trial's state (possibly a rejected one, which differs between
-    # the two once trials are noise-driven): compare e->computeError() at the final state
+    # per-edge e->computeError() at that state (the cached errors hold the last trial's state)
     bactx.compute_errors()
     chi, dpos = bactx.edge_chi2()
-    chi_o, dpos_o = oracle.ba_edge_chi2(p, o["poses"], o["points"],
-                                        oracle.ba_compute_errors(p, o["poses"], o["points"]))
-    # per edge: fp32 uv quantum ~3e-5 px plus the final-state difference (1e-6 -> ~2e-4 px on a 30 px outlier)
-    np.testing.assert_allclose(chi, chi_o, rtol=1e-4, atol=5e-2)
+    chi_o, dpos_o = oracle.ba_edge_chi2(p, o["poses"], o["points"], oracle.ba_compute_errors(p, o["poses"], o["points"]))
+    np.testing.assert_allclose(chi, chi_o, rtol=1e-4, atol=1e-3)     # fp32 uv quantum ~3e-5 px
     assert np.array_equal(dpos, dpos_o)
-
-
-def _rmse(chi, info):
-    return float(np.sqrt(np.mean(chi / info / 2.0)))
+    inl = chi_o < 5.991
+    assert abs(_rmse(chi[inl], p.edge_info[inl]) - _rmse(chi_o[inl], p.edge_info[inl])) < 1e-4
+    # the whole 15-iteration run: past the floor both rest anywhere in the noise band of the
+    # objective (pose_only: poses 4e-5 apart, inlier RMSE 3e-4 px — not an objective, so not
+    # stationary there); the objective itself agrees
+    bactx.upload(p)
+    r15 = bactx.solve_lm(15)
+    assert r15["chi2_final"] == pytest.approx(o15["report"]["chi2_final"], rel=1e-6)
 
 
 def test_lm_gauge_free_matches_oracle_in_rmse(bactx):
     """Only KF 0 fixed (the reference's bundleAdjustment gauge): monocular BA keeps the scale free,
-    and LM slides along that flat valley by amounts set by last-bit differences (observed: chi2
-    4651.73 vs 4651.93 after 15 iterations, poses 7e-3 apart).  Gauge-invariant comparison: chi2
-    rel 1e-4 and inlier reprojection RMSE within 5e-3 px (observed 1.8e-3).  The gauge-fixed
-    problems above meet the 1e-6 trajectory bar."""
+    and LM slides along that flat valley by amounts set by last-bit differences, so after a few
+    iterations the two solvers sit at different points of it.  Gauge-invariant comparison: run both
+    to convergence (the reprojection residuals do not depend on the scale gauge) and compare
+    chi2 rel 1e-6 and the inlier reprojection RMSE within the north-star 1e-4 px."""
     p = _problems()["dense"]
     bactx.upload(p)
-    r = bactx.solve_lm(15)
-    o = oracle.ba_solve(p, 15)
+    r = bactx.solve_lm(80)
+    o = oracle.ba_solve(p, 80)
     bactx.compute_errors()
     chi, _ = bactx.edge_chi2()
     chi_o, _ = oracle.ba_edge_chi2(p, o["poses"], o["points"], oracle.ba_compute_errors(p, o["poses"], o["points"]))
     inl = chi_o < 5.991
     d = abs(_rmse(chi[inl], p.edge_info[inl]) - _rmse(chi_o[inl], p.edge_info[inl]))
-    print("gauge-free: chi2", r["chi2_final"], o["report"]["chi2_final"], "inlier RMSE delta px", d)
-    assert r["chi2_final"] == pytest.approx(o["report"]["chi2_final"], rel=1e-4)
-    assert d < 5e-3
+    print("gauge-free: chi2", r["chi2_final"], o["report"]["chi2_final"], "iterations", r["iterations"],
+          o["report"]["iterations"], "inlier RMSE delta px", d)
+    assert r["chi2_final"] == pytest.approx(o["report"]["chi2_final"], rel=1e-6)
+    assert d < 1e-4
 
 
 @pytest.mark.parametrize("flow", ["bundle", "local", "pose_only"])
