@@ -28,6 +28,9 @@ def _problem():
 
 
 def _worker(rank, world, port, q):
+    import faulthandler
+    import sys
+    faulthandler.enable()
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -42,6 +45,8 @@ def _worker(rank, world, port, q):
     for analytic in (True, False):
         ctx.reset_state()
         r = ctx.solve_lm(N_IT, analytic=analytic)
+        print(f"[rank {rank}] analytic={analytic}: {r['iterations']} iterations, {r['trials_total']} trials, "
+              f"chi2 {r['chi2_final']:.12e}", file=sys.stderr, flush=True)
         pts, sc, tg = ctx.download()
         owner = ctx.vertex_owner()
         P, S, T = ddist.gather_state(p, owner, rank, pts, sc, tg, lambda a: dist.all_reduce(torch.from_numpy(a)))

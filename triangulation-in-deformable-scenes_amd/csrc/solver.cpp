@@ -347,32 +347,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     if ((rc = dalloc(ctx, &L.hval, S.hval_size))) return rc;
     PUT(L.blk_val_off, S.blk_val_off); PUT(L.blk_arena, S.blk_arena); PUT(L.blk_rows, S.blk_rows);
     PUT(L.blk_cols, S.blk_cols); PUT(L.blk_ld, S.blk_ld); PUT(L.blk_diag, S.blk_diag);
-    {
-        // dof of each block's row / column vertex (diagnostic H x product)
-        std::vector<int64_t> rd(S.nblocks), cd(S.nblocks);
-        for (int64_t c = 0, b = 0; c < S.nv; c++) {
-            (void)c;
-            (void)b;
-        }
-        // reconstruct from the arena map: row/col vertices are not stored, so rebuild from rows[]
-        for (int64_t b = 0; b < S.nblocks; b++) {
-            // find front by arena offset (blocks are emitted front-contiguous per column vertex)
-            rd[b] = 0; cd[b] = 0;
-        }
-        int32_t nf = (int32_t)S.fronts.size();
-        std::vector<int64_t> starts(nf);
-        for (int32_t f = 0; f < nf; f++) starts[f] = S.fronts[f].arena_off;
-        for (int64_t b = 0; b < S.nblocks; b++) {
-            int64_t a = S.blk_arena[b];
-            int32_t f = (int32_t)(std::upper_bound(starts.begin(), starts.end(), a) - starts.begin()) - 1;
-            const Front &F = S.fronts[f];
-            int64_t loc = a - F.arena_off;
-            int32_t lc = (int32_t)(loc / F.m), lr = (int32_t)(loc % F.m);
-            rd[b] = S.rows[F.rows_off + lr];
-            cd[b] = S.rows[F.rows_off + lc];
-        }
-        PUT(L.blk_row_dof, rd); PUT(L.blk_col_dof, cd);
-    }
+    PUT(L.blk_row_dof, S.blk_row_dof); PUT(L.blk_col_dof, S.blk_col_dof);   // H x product, diag(H) partials
     L.nhchunks = (int64_t)S.hchunk_begin.size();
     PUT(L.hcontrib, S.hcontrib); PUT(L.hchunk_begin, S.hchunk_begin); PUT(L.hchunk_len, S.hchunk_len);
     PUT(L.hblk_chunk_begin, S.hblk_chunk_begin);
@@ -1352,21 +1327,12 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
     if (hdiag) {
         std::vector<double> hv(ctx->S.hval_size);
         HIPOK(hipMemcpy(hv.data(), ctx->L.hval, sizeof(double) * hv.size(), hipMemcpyDeviceToHost));
-        // diagonal blocks: column vertex == row vertex; dof from the vertex layout
-        int64_t b0 = 0;
+        // diagonal blocks: column vertex == row vertex
         const Symbolic &S = ctx->S;
         for (int64_t blk = 0; blk < S.nblocks; blk++) {
             if (!S.blk_diag[blk]) continue;
-            (void)b0;
-            // the diagonal block of vertex v sits in v's own column at its own rows
-            int64_t a = S.blk_arena[blk];
-            int32_t f = 0;
-            for (int32_t ff = (int32_t)S.fronts.size() - 1; ff >= 0; ff--)
-                if (S.fronts[ff].arena_off <= a) { f = ff; break; }
-            const Front &F = S.fronts[f];
-            int32_t lr = (int32_t)((a - F.arena_off) % F.m);
-            int c = S.blk_cols[blk];
-            for (int k = 0; k < c; k++) hdiag[S.rows[F.rows_off + lr + k]] = hv[S.blk_val_off[blk] + k * c + k];
+            const int c = S.blk_cols[blk];
+            for (int k = 0; k < c; k++) hdiag[S.blk_col_dof[blk] + k] = hv[S.blk_val_off[blk] + k * c + k];
         }
     }
     return 0;

@@ -610,6 +610,7 @@ struct Builder {
         S.nblocks = (int64_t)blk_rowv.size();
         S.blk_val_off.resize(S.nblocks); S.blk_rows.resize(S.nblocks); S.blk_cols.resize(S.nblocks);
         S.blk_arena.resize(S.nblocks); S.blk_ld.resize(S.nblocks); S.blk_diag.resize(S.nblocks);
+        S.blk_row_dof.resize(S.nblocks); S.blk_col_dof.resize(S.nblocks);
         int64_t hv = 0;
         for (int64_t c = 0; c < S.nv; c++) {
             for (int64_t b = blk_begin[c]; b < blk_begin[c + 1]; b++) {
@@ -624,6 +625,8 @@ struct Builder {
                 S.blk_arena[b] = F.arena_off + (int64_t)lc * F.m + lr;
                 S.blk_ld[b] = F.m;
                 S.blk_diag[b] = (r == c && f == vfront[c]) ? 1 : 0;
+                S.blk_row_dof[b] = S.voff[r];
+                S.blk_col_dof[b] = S.voff[c];
             }
         }
         S.hval_size = hv;

@@ -110,6 +110,7 @@ struct Symbolic {
     std::vector<int64_t> blk_arena;      // arena index of entry (0,0)
     std::vector<int32_t> blk_ld;
     std::vector<int32_t> blk_diag;       // 1 if diagonal block (row vertex == column vertex)
+    std::vector<int64_t> blk_row_dof, blk_col_dof;   // first dof of the block's row / column vertex
     // contributions to H blocks, chunked
     std::vector<uint64_t> hcontrib;
     std::vector<int64_t> hchunk_begin;   // per chunk: first contribution
