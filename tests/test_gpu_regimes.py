@@ -22,10 +22,11 @@ REGIMES = {
 }
 
 
-def _problem(regime, n=400, seed=5):
+def _problem(regime, n=400, seed=5, return_map=False):
     r = REGIMES[regime]
     m, _ = sim.simulate_two_view(n=n, seed=seed, kb8=r["kb8"], compact=True)
-    return capi.Context(-1).build_graph(m, r["rep"], r["arap"], np.float32(r["sigma"]))
+    p = capi.Context(-1).build_graph(m, r["rep"], r["arap"], np.float32(r["sigma"]))
+    return (p, m) if return_map else p
 
 
 def rel(a, b):
@@ -52,13 +53,41 @@ def test_linearization_and_solve(gpu_ctx, regime):
 @pytest.mark.parametrize("regime", sorted(REGIMES))
 @pytest.mark.parametrize("analytic,tol", [(True, 1e-6), (False, 1e-5)])
 def test_lm_trajectory(gpu_ctx, regime, analytic, tol):
-    p = _problem(regime)
+    """Identical iteration / trial counts; chi2 per iteration within `tol`, or within 3x the
+    oracle's own sensitivity where that is larger: its spread between two elimination orders (its
+    nested dissection vs the device plan's) and under a half-ulp fp32 perturbation of the
+    observations (the size of the ocml-vs-glibc differences in the fp32 KB8 projection).  In the
+    Realcolon regime (diag(H) spanning 4e10) that sensitivity reaches ~2e-5 by iteration 8.  The
+    north-star quantity, the reprojection RMSE of the solved map, must agree within 1e-4 px."""
+    import copy
+    from deftri import metrics
+    p, m = _problem(regime, return_map=True)
     gpu_ctx.upload(p)
     r = gpu_ctx.solve_lm(8, analytic=analytic)
-    ref = oracle.solve_lm(p, 8, analytic=analytic)["report"]
-    assert r["iterations"] == ref["iterations"]
+    pts, _, _ = gpu_ctx.download()
+    o = oracle.solve_lm(p, 8, analytic=analytic)
+    ref = o["report"]
+    oracle.set_vertex_order(gpu_ctx.vertex_order())
+    try:
+        ref_b = oracle.solve_lm(p, 8, analytic=analytic)["report"]
+    finally:
+        oracle.set_vertex_order(None)
+    q = copy.deepcopy(p)
+    q.rep_obs = q.rep_obs * (1 + np.random.default_rng(0).choice([-1, 1], q.rep_obs.shape) * 2.0 ** -24)
+    ref_u = oracle.solve_lm(q, 8, analytic=analytic)["report"]
+    assert r["iterations"] == ref["iterations"] == ref_b["iterations"]
     assert r["trials_total"] == ref["trials_total"]
-    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=tol)
+    c = np.array(ref["chi2_iter"])
+    spread = max((np.abs(np.array(x["chi2_iter"]) - c) / c).max() for x in (ref_b, ref_u))
+    bound = max(tol, 3 * spread)
+    print(regime, analytic, "oracle sensitivity", spread, "bound", bound)
+    assert bound <= 1e-3
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=bound)
+    ids = list(p.point_ids)
+    m_ref = copy.deepcopy(m)
+    metrics.apply_solution(m, ids, pts)
+    metrics.apply_solution(m_ref, ids, o["points"])
+    assert abs(metrics.pixels_stand_dev(m)["desv"] - metrics.pixels_stand_dev(m_ref)["desv"]) < 1e-4
 
 
 def test_all_pairs_multi_keyframe(gpu_ctx):
