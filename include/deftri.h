@@ -337,6 +337,35 @@ typedef struct deftri_pixels_error {
    do not; the values of the last pair are returned).  Reads the map's fp32 positions. */
 int deftri_pixels_stand_dev(deftri_ctx *ctx, const deftri_map *map, deftri_pixels_error *out);
 
+/* ---- map-error measurements (Modules/Utils/Measurements.cc) --------------------------------- */
+/* measureSimAbsoluteMapErrors (:8-98): MapPoints 2j and 2j+1 (by id) against original[j] / moved[j]
+   for j < (#MapPoints)/2; the figures the reference prints / writes to Experiment.txt, in mm. */
+typedef struct deftri_abs_errors {
+    double average_movement;        /* mean |original - moved| */
+    double average_error_original;  /* mean |p_2j - original| */
+    double average_error_moved;     /* mean |p_2j+1 - moved| */
+    double average_error;           /* (sum of both) / #MapPoints ("Av. error") */
+    double rmse;                    /* sqrt(sum of squared errors / #MapPoints) ("RMSE") */
+    int64_t point_count;            /* #MapPoints */
+} deftri_abs_errors;
+int deftri_measure_sim_absolute_map_errors(int32_t device, const deftri_map *map, int32_t n_points,
+                                           const float *original, const float *moved, deftri_abs_errors *out);
+/* measureRelativeMapErrors (:350-518), per keyframe pair in the map's order: the values after that
+   pair (the accumulators carry over pairs, as in the reference).  Depth uses the per-index simulated
+   measurement (the reference's depth-image lookup throws in the simulation). */
+typedef struct deftri_rel_errors {
+    int64_t kf1, kf2;               /* KeyFrame ids (k2->first, k1->first) */
+    int32_t reported;               /* validPairs > 1: the reference prints / writes the pair */
+    double rel_error;               /* sum ||(pi2 - pj2) - (pi1 - pj1)||^2 / mesh area ("Rel. error") */
+    double depth_error;             /* sum (d - z s)^2 ("depthError") */
+    double global_t_error;          /* sum ||(R pi2 - t - pi1) + (R pj2 - t - pj1)||^2 / area */
+    double area;                    /* the pair's mesh surface area */
+    int64_t valid_pairs, n_matches;
+} deftri_rel_errors;
+int deftri_measure_relative_map_errors(int32_t device, const deftri_map *map, deftri_rel_errors *out,
+                                       int32_t max_pairs, int32_t *n_pairs);
+
+
 /* Mapping::triangulateSimulatedMapPoints (Modules/Mapping/Mapping.cc:280-349) for Triangulation.method
    "NRSLAM", seed.location "FarPoints" (Simulation.yaml): per correspondence i, KB8 unproject of
    uv1[i] / uv2[i] (KannalaBrandt8.cc:51-83), triangulateNRSLAM (Geometry.cc:103-153) and

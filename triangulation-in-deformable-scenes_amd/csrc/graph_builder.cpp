@@ -251,6 +251,16 @@ bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err
 
 }  // namespace
 
+bool mesh_adjacency(const std::vector<double> &pos, int n, std::vector<std::vector<int32_t>> &adj,
+                    std::vector<int32_t> &pos_index, double &area, std::string &err) {
+    Mesh M;
+    if (!build_mesh(pos, n, M, err)) return false;
+    adj = std::move(M.adj);
+    area = M.area;
+    pos_index = vector_map(pos, n);
+    return true;
+}
+
 void procrustes_rotation(const double S[9], double R[9]) {
     double U[9], s[3], V[9];
     eigen_jacobi_svd3(S, U, s, V);

@@ -31,6 +31,11 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
 void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<double> &points,
                     const std::vector<double> &scales, const std::vector<double> &tg, double *optimization_update);
 
+// Delaunay mesh of the positions' (x, y) (ComputeDelaunayTriangulation3D + ComputeAdjacencyList,
+// Geometry.cc:317-368): sorted neighbour lists, GetSurfaceArea, createVectorMap (vertex -> position)
+bool mesh_adjacency(const std::vector<double> &pos, int n, std::vector<std::vector<int32_t>> &adj,
+                    std::vector<int32_t> &pos_index, double &area, std::string &err);
+
 // 3x3 helpers exported for tests
 void procrustes_rotation(const double S[9], double R[9]);
 

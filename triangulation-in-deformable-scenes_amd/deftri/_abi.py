@@ -96,6 +96,16 @@ class MapC(C.Structure):
                 ("n_global", i32), ("globals", P(GlobalEntryC))]
 
 
+class AbsErrorsC(C.Structure):
+    _fields_ = [("average_movement", f64), ("average_error_original", f64), ("average_error_moved", f64),
+                ("average_error", f64), ("rmse", f64), ("point_count", i64)]
+
+
+class RelErrorsC(C.Structure):
+    _fields_ = [("kf1", i64), ("kf2", i64), ("reported", i32), ("rel_error", f64), ("depth_error", f64),
+                ("global_t_error", f64), ("area", f64), ("valid_pairs", i64), ("n_matches", i64)]
+
+
 class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 32), ("launches", i64), ("ms", f64), ("flops", f64), ("bytes", f64)]
 

@@ -82,6 +82,10 @@ def load():
         "deftri_dist_set_transport": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _abi.XFER_FN, C.c_void_p]),
         "deftri_dist_vertex_owner": (C.c_int, [C.c_void_p, P(C.c_int32), C.c_int64]),
         "deftri_plan_vertex_order": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64]),
+        "deftri_measure_sim_absolute_map_errors": (C.c_int, [C.c_int32, P(_abi.MapC), C.c_int32, P(C.c_float),
+                                                             P(C.c_float), P(_abi.AbsErrorsC)]),
+        "deftri_measure_relative_map_errors": (C.c_int, [C.c_int32, P(_abi.MapC), P(_abi.RelErrorsC), C.c_int32,
+                                                         P(C.c_int32)]),
         "deftri_sim_normal_stream": (C.c_int, [C.c_int64, C.c_float, C.c_float, P(C.c_float)]),
         "deftri_sim_two_view": (C.c_int, [C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float), P(C.c_float),
                                           P(C.c_float), P(C.c_float), C.c_float, C.c_int32, C.c_float, C.c_float,
@@ -115,7 +119,8 @@ EXPORTED = [
     "deftri_ba_set_edge_flags", "deftri_ba_solve_lm", "deftri_ba_compute_errors", "deftri_ba_edge_chi2",
     "deftri_ba_download", "deftri_ba_eval_system", "deftri_rccl_unique_id", "deftri_ba_dist_init_rccl",
     "deftri_ba_dist_set_allreduce", "deftri_ba_profile_trial",
-    "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream", "deftri_dist_owned_edges",
+    "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream",
+    "deftri_measure_sim_absolute_map_errors", "deftri_measure_relative_map_errors", "deftri_dist_owned_edges",
     "deftri_debug_plan_solve_dist",
 ]
 
@@ -449,6 +454,34 @@ def sim_two_view(orig, moved, c1, c2, kb8_1, kb8_2, rep_error, decimals, depth_e
     if rc != 0:
         raise DeftriError(rc, "deftri_sim_two_view")
     return uv1, uv2, d1, d2, p1, p2
+
+
+def measure_sim_absolute(m, original, moved, device=0):
+    """deftri_measure_sim_absolute_map_errors (Measurements.cc:8-98); values in mm."""
+    lib = load()
+    mc, keep = m.to_c()
+    o = np.ascontiguousarray(original, np.float32).reshape(-1, 3)
+    mv = np.ascontiguousarray(moved, np.float32).reshape(-1, 3)
+    out = _abi.AbsErrorsC()
+    fp = lambda a: a.ctypes.data_as(C.POINTER(C.c_float))
+    rc = lib.deftri_measure_sim_absolute_map_errors(int(device), C.byref(mc), len(o), fp(o), fp(mv), C.byref(out))
+    if rc != 0:
+        raise DeftriError(rc, "deftri_measure_sim_absolute_map_errors")
+    return {k: getattr(out, k) for k, _ in _abi.AbsErrorsC._fields_}
+
+
+def measure_relative(m, device=0):
+    """deftri_measure_relative_map_errors (Measurements.cc:350-518): one record per keyframe pair."""
+    lib = load()
+    mc, keep = m.to_c()
+    K = len(m.keyframes)
+    npair = max(1, K * (K - 1) // 2)
+    out = (_abi.RelErrorsC * npair)()
+    n = C.c_int32()
+    rc = lib.deftri_measure_relative_map_errors(int(device), C.byref(mc), out, npair, C.byref(n))
+    if rc != 0:
+        raise DeftriError(rc, "deftri_measure_relative_map_errors")
+    return [{k: getattr(out[i], k) for k, _ in _abi.RelErrorsC._fields_} for i in range(n.value)]
 
 
 def rccl_unique_id():

@@ -84,3 +84,17 @@ def apply_solution(m, prob_graph_ids, points):
     prob_graph_ids: MapPoint id of each graph point (GraphResult order)."""
     for pid, p in zip(prob_graph_ids, points):
         m.map_points[int(pid)].position = np.asarray(p, np.float32)
+
+
+def measureSimAbsoluteMapErrors(pMap, originalPoints, movedPoints, device=0):
+    """Modules/Utils/Measurements.cc:8-98 on the device: {"average_movement", "average_error",
+    "rmse", ...} in mm (the Experiment.txt figures)."""
+    from . import capi
+    return capi.measure_sim_absolute(pMap, originalPoints, movedPoints, device)
+
+
+def measureRelativeMapErrors(pMap, device=0):
+    """Modules/Utils/Measurements.cc:350-518 on the device: per keyframe pair (map order) the
+    accumulated "Rel. error", "depthError" and "gloablTError" after that pair."""
+    from . import capi
+    return capi.measure_relative(pMap, device)
