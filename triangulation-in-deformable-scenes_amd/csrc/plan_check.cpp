@@ -135,7 +135,8 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                 double *A = Fp(f);
                 int k0 = st.kA, kb = std::min(st.kmax, F.s - k0), m = F.m;
                 int cend = st.inner == 1 ? std::min(F.s, (k0 / kOuter + 1) * kOuter)
-                         : st.inner == 2 ? std::min(F.s, (k0 / kOuter + 2) * kOuter) : m;
+                         : st.inner == 2 ? std::min(F.s, (k0 / kOuter + 2) * kOuter)
+                         : st.inner == 3 ? F.s : m;
                 for (int c = tj; c < std::min(tj + 64, cend); c++)
                     for (int r = ti; r < std::min(ti + 64, m); r++) {
                         double acc = 0;

@@ -738,11 +738,15 @@ struct Builder {
             // FULL = block kA's update of every trailing column; LOOK = the next block's columns only
             // (carries the fused factorization of its first panel); REST = the columns past the next
             // block (and the whole trailing part of fronts that end in this block).
-            enum { UP_INNER = 1, UP_FULL = 0, UP_LOOK = 2, UP_REST = 3 };
+            // OWN = FULL restricted to the front's own trailing columns (carries the fused panel
+            // factorization; main stream); CB = FULL restricted to the contribution-block columns (needed
+            // only by the parent's assembly at the next level: side stream, overlapping the rest of the
+            // level's panel chain).
+            enum { UP_INNER = 1, UP_FULL = 0, UP_LOOK = 2, UP_REST = 3, UP_OWN = 4, UP_CB = 5 };
             auto push_update = [&](Symbolic::StepTasks &st, int32_t kA, int32_t kmax, int mode) {
                 st.upd_off = (int64_t)S.task_i32.size() / 3;
                 st.kA = kA; st.kmax = kmax;
-                st.inner = mode == UP_INNER ? 1 : mode == UP_LOOK ? 2 : 0;
+                st.inner = mode == UP_INNER ? 1 : mode == UP_LOOK ? 2 : mode == UP_OWN ? 3 : 0;
                 const int32_t Pend = (kA / kOuter + 1) * kOuter;
                 // pass 0: the tiles that carry a fused panel factorization go first in the launch
                 std::vector<std::array<int32_t, 4>> spans;   // (front, t0 column, tend column, has_diag)
@@ -754,8 +758,11 @@ struct Builder {
                     if (mode == UP_INNER) tend = std::min(F.s, Pend);
                     if (mode == UP_LOOK) { if (F.s <= Pend) continue; t0 = Pend; tend = std::min(F.s, Pend + kOuter); }
                     if (mode == UP_REST && F.s > Pend) t0 = std::min(F.s, Pend + kOuter);
+                    if (mode == UP_OWN) tend = F.s;                 // k_update stores c < s only (inner 3)
+                    if (mode == UP_CB) t0 = std::max(t0, F.s);
                     if (t0 >= tend) continue;
-                    const bool has_diag = (mode == UP_INNER || mode == UP_LOOK || mode == UP_FULL) && F.s > t0 && t0 == kA + K;
+                    const bool has_diag = (mode == UP_INNER || mode == UP_LOOK || mode == UP_FULL || mode == UP_OWN) &&
+                                          F.s > t0 && t0 == kA + K;
                     spans.push_back({f, t0, tend, has_diag ? 1 : 0});
                 }
                 for (int pass = 0; pass < 2; pass++)
@@ -818,6 +825,7 @@ struct Builder {
                 bool cont = false;
                 int32_t maxm = 0;
                 for (int32_t f : fs) { cont = cont || S.fronts[f].s > P0 + kOuter; maxm = std::max(maxm, S.fronts[f].m); }
+                const bool cont_any = cont;
                 cont = cont && maxm >= la_min_m;
                 auto outer_step = [&](int mode, int stream, int wait_side) {
                     Symbolic::StepTasks so;
@@ -827,9 +835,20 @@ struct Builder {
                     so.stream = stream; so.wait_side = wait_side;
                     LT.steps.push_back(so);
                 };
+                // DEFTRI_CB_SIDE: 0 = off, 1 = only when some front of the level continues past this block
+                // (there is a panel chain to overlap), 2 = always
+                static const int cb_side = [] {
+                    const char *e = std::getenv("DEFTRI_CB_SIDE");
+                    return e ? std::atoi(e) : 0;   // measured at C2: 1 and 2 slower (side-stream contention)
+                }();
                 if (cont) {
                     outer_step(UP_REST, 1, 0);
                     outer_step(UP_LOOK, 0, 1);
+                } else if (cb_side == 2 || (cb_side == 1 && cont_any)) {
+                    // CB first: its launch on the side stream waits only for this block's panel chain;
+                    // the OWN update then runs on the main stream concurrently with it
+                    outer_step(UP_CB, 1, 0);
+                    outer_step(UP_OWN, 0, 0);
                 } else {
                     // touches the trailing columns an earlier REST (side stream) may still be updating
                     outer_step(UP_FULL, 0, 2);
@@ -888,7 +907,16 @@ bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points, int ran
     if (nranks < 1 || rank < 0 || rank >= nranks) { S.error = "bad rank / nranks"; return false; }
     if (const char *e = std::getenv("DEFTRI_ND_LEAF")) leaf_points = std::max(2, std::atoi(e));   // tuning
     Builder b(d, S, leaf_points, rank, nranks);
-    return b.run();
+    const bool ok = b.run();
+    if (const char *path = std::getenv("DEFTRI_DUMP_FRONTS"); ok && path) {   // plan inspection (tools/)
+        if (FILE *fp = std::fopen(path, "w")) {
+            for (int32_t h = 0; h < S.nlevels; h++)
+                for (int32_t f : S.level_fronts[h])
+                    std::fprintf(fp, "%d %d %d %d %d\n", h, f, S.fronts[f].m, S.fronts[f].s, S.fronts[f].parent);
+            std::fclose(fp);
+        }
+    }
+    return ok;
 }
 
 }  // namespace deftri
