@@ -10,6 +10,7 @@ namespace deftri {
 namespace dev {
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     int2 p = __builtin_bit_cast(int2, v);

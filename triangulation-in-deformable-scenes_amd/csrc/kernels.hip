@@ -589,24 +589,35 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 
 // trailing update of tile (ti, tj): C -= L_i D L_j^T over L columns [kA, kA + K),
 // K = min(kmax, s - kA) (one 64-panel for the inner updates, a whole outer block otherwise).
-// MFMA operands are loaded straight from the front (16 consecutive rows per 128-B segment,
-// L2-resident panel), software-pipelined 16 columns ahead; the C tile is fetched before the K
-// loop.  (An LDS-staged variant measured slower on MI355X: the f64 MFMA pipe, ~48 TF/s sustained,
-// not operand bandwidth, bounds the big launches.)  LDS here is only the fused panel
-// factorization's.
-struct DiagSmem { double S[64][DP]; };
+// Operands are staged through LDS one k-chunk (16 columns) at a time: thread t loads column
+// t / 16 of the chunk, rows 4 (t % 16) .. +3 of both 64-row panels (L_j scaled by d_k once, at
+// staging) with 16-byte loads — one d load + four 16-byte loads per thread per 16 k instead of 20
+// scalar loads per lane — double-buffered (chunk c+1's loads in flight during chunk c's MFMAs), one
+// barrier per chunk; each wave reads its 32x32 quadrant's fragments from LDS.  Same products and
+// summation order as the register-streaming kernel it replaced (bit-identical), 1.3-1.5x faster
+// (tools/micro/upd_bench.hip: 30 -> 42 TF/s on 2000-row fronts, K = 256).  The C tile is fetched
+// before the K loop.  The staging buffers alias the fused panel factorization's LDS.
+constexpr int kUpdKC = 16;                 // k columns per staged chunk
+// two consecutive column entries p[0..1] of which nvalid remain in the column (16-byte load when
+// aligned; odd m gives odd column starts)
+__device__ __forceinline__ dbl2 ld2(const double *p, int nvalid) {
+    if (nvalid >= 2 && ((uintptr_t)p & 15) == 0) return *(const dbl2 *)p;
+    return dbl2{nvalid > 0 ? p[0] : 0.0, nvalid > 1 ? p[1] : 0.0};
+}
+constexpr int kUpdLQ = 64 + 4;             // padded staged column (doubles)
+union UpdSmem {
+    struct { double P[2][kUpdKC][kUpdLQ], Q[2][kUpdKC][kUpdLQ]; } st;
+    double S[64][DP];
+};
 #ifndef DEFTRI_UPD_WPE
 #define DEFTRI_UPD_WPE 4   // waves per EU of k_update (tuning knob)
-#endif
-#ifndef DEFTRI_UPD_PD
-#define DEFTRI_UPD_PD 2    // prefetch stage depth of k_update (tuning knob)
 #endif
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
                                                 double *__restrict__ inv, int *__restrict__ flag,
                                                 const LaneOff lo) {
-    __shared__ DiagSmem sm;
+    __shared__ UpdSmem sm;
     int t = xcd_task(ntask);
     if (t >= ntask) return;
     arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y;
@@ -618,9 +629,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     int cend = inner == 1 ? min(s, (kA / kOuter + 1) * kOuter) : inner == 2 ? min(s, (kA / kOuter + 2) * kOuter)
              : inner == 3 ? s : m;
     double *F = arena + fd.arena_off[f];
-    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int rb = ti + (w & 1) * 32, cb = tj + (w >> 1) * 32;
-    int kl = lane >> 4, il = lane & 15;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int rb = ti + (w & 1) * 32, cb = tj + (w >> 1) * 32;
+    const int kl = lane >> 4, il = lane & 15;
+    const int qr = (w & 1) * 32, pc = (w >> 1) * 32;     // quadrant offsets inside the staged panels
+    // staging role: column sk of the chunk, rows sr..sr+3 of both panels
+    const int sk = tid >> 4, sr = (tid & 15) * 4;
+    const int pn = m - (tj + sr), qn = m - (ti + sr);   // rows left in the column from the staged rows
+    dbl2 pv0, pv1, qv0, qv1;
+    double dv;
+    auto stage_load = [&](int c0) {
+        const int kk = c0 + sk;
+        const bool ok = kk < K;
+        const double *col = F + (int64_t)(kA + kk) * m;
+        dv = ok ? col[kA + kk] : 0.0;
+        pv0 = ld2(col + tj + sr, ok ? pn : 0);
+        pv1 = ld2(col + tj + sr + 2, ok ? pn - 2 : 0);
+        qv0 = ld2(col + ti + sr, ok ? qn : 0);
+        qv1 = ld2(col + ti + sr + 2, ok ? qn - 2 : 0);
+    };
+    auto stage_store = [&](int buf) {
+        *(dbl2 *)&sm.st.P[buf][sk][sr] = pv0 * dv;
+        *(dbl2 *)&sm.st.P[buf][sk][sr + 2] = pv1 * dv;
+        *(dbl2 *)&sm.st.Q[buf][sk][sr] = qv0;
+        *(dbl2 *)&sm.st.Q[buf][sk][sr + 2] = qv1;
+    };
+    stage_load(0);
     // C prefetch: acc layout (a, b, g) -> column cb + 16a + kl + 4g, row rb + 16b + il
     double cv[2][2][4];
 #pragma unroll
@@ -637,37 +671,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-    const bool p0ok = cb + il < m, p1ok = cb + 16 + il < m, q0ok = rb + il < m, q1ok = rb + 16 + il < m;
-    constexpr int PD = DEFTRI_UPD_PD;                          // k-steps (of 4) per prefetch stage
-    double cd[PD], c0[PD], c1[PD], c2[PD], c3[PD], nd[PD], n0[PD], n1[PD], n2[PD], n3[PD];
-    auto loadk = [&](int kb0, double *d, double *x0, double *x1, double *y0, double *y1) {
+    stage_store(0);
+    __syncthreads();
+    const int nch = (K + kUpdKC - 1) / kUpdKC;
+    for (int c = 0; c < nch; c++) {
+        const int buf = c & 1;
+        if (c + 1 < nch) stage_load((c + 1) * kUpdKC);
 #pragma unroll
-        for (int u = 0; u < PD; u++) {
-            int kk = kb0 + 4 * u + kl;
-            bool ok = kk < K;
-            const double *col = F + (int64_t)(kA + kk) * m;
-            d[u] = ok ? col[kA + kk] : 0.0;
-            x0[u] = (ok && p0ok) ? col[cb + il] : 0.0;
-            x1[u] = (ok && p1ok) ? col[cb + 16 + il] : 0.0;
-            y0[u] = (ok && q0ok) ? col[rb + il] : 0.0;
-            y1[u] = (ok && q1ok) ? col[rb + 16 + il] : 0.0;
+        for (int k4 = 0; k4 < kUpdKC; k4 += 4) {
+            const double p0 = sm.st.P[buf][k4 + kl][pc + il], p1 = sm.st.P[buf][k4 + kl][pc + 16 + il];
+            const double q0 = sm.st.Q[buf][k4 + kl][qr + il], q1 = sm.st.Q[buf][k4 + kl][qr + 16 + il];
+            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
         }
-    };
-    loadk(0, cd, c0, c1, c2, c3);
-    for (int kb0 = 0; kb0 < K; kb0 += 4 * PD) {
-        const bool more = kb0 + 4 * PD < K;
-        if (more) loadk(kb0 + 4 * PD, nd, n0, n1, n2, n3);
-#pragma unroll
-        for (int u = 0; u < PD; u++) {
-            double p0 = c0[u] * cd[u], p1 = c1[u] * cd[u];
-            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c2[u], acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, c3[u], acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, c2[u], acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, c3[u], acc[1][1], 0, 0, 0);
-        }
-        if (more)
-#pragma unroll
-            for (int u = 0; u < PD; u++) { cd[u] = nd[u]; c0[u] = n0[u]; c1[u] = n1[u]; c2[u] = n2[u]; c3[u] = n3[u]; }
+        if (c + 1 < nch) stage_store(buf ^ 1);
+        __syncthreads();
     }
     // the front's last trailing update produces its final contribution block: a direct front adds
     // it straight into the parent (lower triangle; bmap is monotone, each parent entry has one writer
