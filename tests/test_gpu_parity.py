@@ -10,6 +10,8 @@ fixtures.  Tolerances:
 """
 import json
 
+import os
+
 import numpy as np
 import pytest
 
@@ -163,7 +165,9 @@ def test_full_size_properties(gpu_ctx):
 def test_profile_trial_reports_kernels(gpu_ctx, golden_cases):
     gpu_ctx.upload(_golden(golden_cases[0]))
     st = gpu_ctx.profile_trial(1e3)
-    for k in ("lin_arap", "hchunk", "scatter", "diag", "trsm", "update", "fwd_step", "bwd_step"):
+    # the panel TRSM has its own launches unless DEFTRI_TRSM_FUSE=1 folds them into diag / update
+    fused = os.environ.get("DEFTRI_TRSM_FUSE") == "1"
+    for k in ("lin_arap", "hchunk", "scatter", "diag", "update", "fwd_step", "bwd_step") + (() if fused else ("trsm",)):
         assert k in st and st[k]["launches"] > 0
     assert st["update"]["flops"] > 0
 

@@ -93,10 +93,11 @@ k_updA(int ntask, const int *__restrict__ tasks, int kA, int K, int m, double *_
 // chunk, rows 4 (t % 16) .. +3 of both 64-row operand panels (two 16-byte loads each); P = L_c d_k
 // is scaled once at staging.  Double-buffered: chunk c+1's loads are in flight while chunk c's MFMAs
 // run; one barrier per chunk. ----
-constexpr int KC = 16;
 constexpr int LQ = 64 + 4;   // padded row length (doubles) of one staged k-column
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+template <int KC, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 k_updB(int ntask, const int *__restrict__ tasks, int kA, int K, int m, double *__restrict__ arena) {
+    static_assert(KC == 16 || KC == 32, "KC");
     __shared__ double Ps[2][KC][LQ], Qs[2][KC][LQ];
     int t = xcd_task(ntask);
     if (t >= ntask) return;
@@ -106,25 +107,27 @@ k_updB(int ntask, const int *__restrict__ tasks, int kA, int K, int m, double *_
     const int rb = (w & 1) * 32, cb = (w >> 1) * 32;   // quadrant inside the tile
     const int kl = lane >> 4, il = lane & 15;
     // staging role
-    const int sk = tid >> 4, sr = (tid & 15) * 4;
-    const bool pok0 = tj + sr < m, pok1 = tj + sr + 2 < m, qok0 = ti + sr < m, qok1 = ti + sr + 2 < m;
-    dbl2 pv0, pv1, qv0, qv1;
+    constexpr int NV = KC / 8;                       // dbl2 per panel per thread
+    const int sk = tid / (256 / KC), sr = (tid % (256 / KC)) * (2 * NV);
+    dbl2 pv[NV], qv[NV];
     double dv;
     auto stage_load = [&](int c0) {
         const int kk = c0 + sk;
         const bool ok = kk < K;
         const double *col = F + (int64_t)(kA + kk) * m;
         dv = ok ? col[kA + kk] : 0.0;
-        pv0 = (ok && pok0) ? *(const dbl2 *)(col + tj + sr) : dbl2{0.0, 0.0};
-        pv1 = (ok && pok1) ? *(const dbl2 *)(col + tj + sr + 2) : dbl2{0.0, 0.0};
-        qv0 = (ok && qok0) ? *(const dbl2 *)(col + ti + sr) : dbl2{0.0, 0.0};
-        qv1 = (ok && qok1) ? *(const dbl2 *)(col + ti + sr + 2) : dbl2{0.0, 0.0};
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+            pv[v] = (ok && tj + sr + 2 * v < m) ? *(const dbl2 *)(col + tj + sr + 2 * v) : dbl2{0.0, 0.0};
+            qv[v] = (ok && ti + sr + 2 * v < m) ? *(const dbl2 *)(col + ti + sr + 2 * v) : dbl2{0.0, 0.0};
+        }
     };
     auto stage_store = [&](int buf) {
-        *(dbl2 *)&Ps[buf][sk][sr] = pv0 * dv;
-        *(dbl2 *)&Ps[buf][sk][sr + 2] = pv1 * dv;
-        *(dbl2 *)&Qs[buf][sk][sr] = qv0;
-        *(dbl2 *)&Qs[buf][sk][sr + 2] = qv1;
+#pragma unroll
+        for (int v = 0; v < NV; v++) {
+            *(dbl2 *)&Ps[buf][sk][sr + 2 * v] = pv[v] * dv;
+            *(dbl2 *)&Qs[buf][sk][sr + 2 * v] = qv[v];
+        }
     };
     stage_load(0);
     // C prefetch (this wave's quadrant)
@@ -172,7 +175,7 @@ k_updB(int ntask, const int *__restrict__ tasks, int kA, int K, int m, double *_
             }
 }
 
-static void run_case(int nf, int m, int K) {
+static void run_case(int nf, int m, int K, int VB) {
     std::vector<int> tasks;
     for (int f = 0; f < nf; f++)
         for (int tj = K; tj < m; tj += 64)
@@ -189,12 +192,13 @@ static void run_case(int nf, int m, int K) {
     for (auto &x : h) x = rand() / (double)RAND_MAX - 0.5;
     double *dA, *dB; int *dt;
     HC(hipMalloc(&dA, n * 8)); HC(hipMalloc(&dB, n * 8)); HC(hipMalloc(&dt, tasks.size() * 4));
+    auto kB = VB == 0 ? k_updB<16, 4> : VB == 1 ? k_updB<32, 2> : VB == 2 ? k_updB<16, 2> : k_updB<32, 4>;
     HC(hipMemcpy(dt, tasks.data(), tasks.size() * 4, hipMemcpyHostToDevice));
     HC(hipMemcpy(dA, h.data(), n * 8, hipMemcpyHostToDevice));
     HC(hipMemcpy(dB, h.data(), n * 8, hipMemcpyHostToDevice));
     const unsigned grid = 8 * ((nt + 7) / 8);
     hipLaunchKernelGGL(k_updA, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dA);
-    hipLaunchKernelGGL(k_updB, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dB);
+    hipLaunchKernelGGL(kB, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dB);
     HC(hipDeviceSynchronize());
     std::vector<double> a(n), b(n);
     HC(hipMemcpy(a.data(), dA, n * 8, hipMemcpyDeviceToHost));
@@ -209,25 +213,26 @@ static void run_case(int nf, int m, int K) {
         HC(hipEventRecord(e0));
         for (int r = 0; r < reps; r++) {
             if (v == 0) hipLaunchKernelGGL(k_updA, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dA);
-            else hipLaunchKernelGGL(k_updB, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dB);
+            else hipLaunchKernelGGL(kB, dim3(grid), dim3(256), 0, 0, nt, dt, 0, K, m, dB);
         }
         HC(hipEventRecord(e1));
         HC(hipEventSynchronize(e1));
         HC(hipEventElapsedTime(v == 0 ? &msA : &msB, e0, e1));
     }
     msA /= reps; msB /= reps;
-    printf("fronts %4d m %5d K %3d tiles %6d: A %8.1f us %6.2f TF/s | B %8.1f us %6.2f TF/s | %zu differ\n", nf, m, K, nt,
-           1e3 * msA, flops / (msA * 1e-3) / 1e12, 1e3 * msB, flops / (msB * 1e-3) / 1e12, bad);
+    printf("B%d fronts %4d m %5d K %3d tiles %6d: A %8.1f us %6.2f TF/s | B %8.1f us %6.2f TF/s | %zu differ\n",
+           VB, nf, m, K, nt, 1e3 * msA, flops / (msA * 1e-3) / 1e12, 1e3 * msB, flops / (msB * 1e-3) / 1e12, bad);
     HC(hipFree(dA)); HC(hipFree(dB)); HC(hipFree(dt));
 }
 
 int main() {
-    run_case(1, 2048, 256);
-    run_case(3, 2800, 256);
-    run_case(11, 2000, 256);
-    run_case(34, 1300, 256);
-    run_case(129, 650, 162);
-    run_case(872, 290, 66);
-    run_case(6322, 170, 96);
+    for (int vb = 0; vb < 4; vb++) {
+        run_case(1, 2048, 256, vb);
+        run_case(11, 2000, 256, vb);
+        run_case(34, 1300, 256, vb);
+        run_case(129, 650, 162, vb);
+        run_case(872, 290, 66, vb);
+        run_case(6322, 170, 96, vb);
+    }
     return 0;
 }

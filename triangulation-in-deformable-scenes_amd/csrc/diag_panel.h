@@ -35,212 +35,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+constexpr int DP = 65;   // padded LDS row (doubles) of the 64 x 64 diagonal block
+
+// ------------------------------------------------------------------------------------------
 // Blocked LDL^T + unit-lower inverse of one 64x64 panel diagonal block held in LDS (256 threads).
 //   in : S[r][c] (c <= r) = A (rows/cols >= kb padded with the identity), S[c][r] (r > c) = 0
 //   out: S[r][c] (c < r) = L, S[r][r] = D, S[c][r] (r > c) = X[r][c], X = L^{-1}
-// Four 16-column sub-panels K.  Per sub-panel:
-//   F  the 16x16 diagonal block and its inverse in the registers of wave 0: 16 right-looking
-//      steps with cross-lane broadcasts, no barrier (A[r][c] -= l_r a_c, X[r][c] -= l_r X[j][c]);
-//   X  (waves nrt..) finishes the inverse blocks of block row K: X_KJ = -X_KK T_KJ, J < K;
-//   TR (waves 0..nrt-1) the sub-panel TRSM below it: L_IK = A_IK X_KK^T D_K^{-1};
-//   U  the trailing Schur update on the lower triangle and the inverse accumulators
-//      T_IJ += L_IK X_KJ (I > K, J <= K), all 16x16x16 f64 MFMA tiles.
-// T_IJ accumulates in place in the upper-triangle slot of X_IJ (zero on entry).
-constexpr int DP = 65;
-__device__ __forceinline__ void diag_block(double (*S)[DP], int kb, int *flag) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int li = lane & 15, lk = lane >> 4;
-    // rows/cols >= kb are identity padding: sub-blocks past nsub and pivot steps past kb are no-ops
-    const int nsub = (kb + 15) >> 4;
-#ifdef DEFTRI_DIAG_TIMING
-    long long tp[16]; int ntp = 0;
-    tp[ntp++] = clock64();
-#endif
-    for (int K = 0; K < nsub; K++) {
-        const int j0 = 16 * K;
-        const int jend = min(16, kb - j0);
-        // ---- F: factor the diagonal block + its inverse in the registers of wave 0 (no barrier on
-        //      the pivot chain).  Lane (r, g) = (lane & 15, lane >> 4) holds A[r][c] and X[r][c]
-        //      for c = g, g+4, g+8, g+12 (both triangles of A, so row j is A[j][c] in lanes
-        //      (j, g)); right-looking step j: d = A[j][j] (readlane), l_r = A[r][j] / d,
-        //      A[r][c] -= l_r A[j][c] (r, c > j), X[r][c] -= l_r X[j][c] (r > j >= c).
-        if (wv == 0) {
-            const int r = lane & 15, g = lane >> 4, rowbase = lane & 48;
-            double a[4], x[4];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int c = g + 4 * q;
-                a[q] = (c <= r) ? S[j0 + r][j0 + c] : S[j0 + c][j0 + r];
-                x[q] = (c == r) ? 1.0 : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                if (j < jend) {
-                    const double d = readlane_d(a[j >> 2], j + 16 * (j & 3));          // A[j][j]
-                    const double arj = __shfl(a[j >> 2], r + 16 * (j & 3));            // A[r][j]
-                    double ajc[4], xjc[4];
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        ajc[q] = __shfl(a[q], rowbase | j);                            // A[j][c_q]
-                        xjc[q] = __shfl(x[q], rowbase | j);                            // X[j][c_q]
-                    }
-                    const double lr = arj * rcp_d(d);
-                    if (r > j) {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const int c = g + 4 * q;
-                            if (c > j) a[q] -= lr * ajc[q];
-                            else x[q] -= lr * xjc[q];
-                            if (c == j) a[q] = lr;                                     // L[r][j]
-                        }
-                    }
-                    if (lane == 0 && d == 0.0) atomicOr(flag, 1);
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int c = g + 4 * q;
-                if (c <= r) S[j0 + r][j0 + c] = a[q];                                  // L (c < r), D (c == r)
-                if (c < r) S[j0 + c][j0 + r] = x[q];                                   // X[r][c]
-            }
-        }
-        __syncthreads();
-#ifdef DEFTRI_DIAG_TIMING
-        tp[ntp++] = clock64();
-#endif
-        const int nrt = nsub - 1 - K;                          // 16-row tiles below the sub-panel
-        // ---- X: X_KJ = -X_KK T_KJ for J < K (T_KJ at S[16J + c][j0 + r]) ----
-        if (wv >= nrt && wv - nrt < K) {
-            const int J = wv - nrt, cidx = 16 * J + li;
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k4 = 0; k4 < 16; k4 += 4) {
-                const int k = k4 + lk;
-                const double av = (k == li) ? 1.0 : (k < li ? S[j0 + k][j0 + li] : 0.0);  // X_KK[li][k]
-                const double bv = S[cidx][j0 + k];                                        // T_KJ[k][li]
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g++) S[cidx][j0 + lk + 4 * g] = -acc[g];             // X[j0+r][cidx]
-        }
-        // ---- TR: L[r][c] = sum_k A[r][j0+k] X[c][k] / d_c, one row tile per wave ----
-        if (wv < nrt) {
-            const int R = j0 + 16 + 16 * wv, c = j0 + li;
-            const double rdc = 1.0 / S[c][c];
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int k4 = 0; k4 < 16; k4 += 4) {
-                const int k = k4 + lk;
-                const double av = S[R + li][j0 + k];
-                const double wk = ((k < li) ? S[j0 + k][c] : (k == li ? 1.0 : 0.0)) * rdc;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, wk, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g++) S[R + lk + 4 * g][c] = acc[g];
-        }
-        if (K == nsub - 1) break;
-        __syncthreads();
-#ifdef DEFTRI_DIAG_TIMING
-        tp[ntp++] = clock64();
-#endif
-        // ---- U: Schur tiles (Rt >= Ct) then inverse accumulators (I > K, J <= K) ----
-        const int nsch = nrt * (nrt + 1) / 2, ninv = nrt * (K + 1);
-        for (int t = wv; t < nsch + ninv; t += 4) {
-            dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-            if (t < nsch) {
-                int Rt = 0, Ct = t;
-                while (Ct > Rt) { Ct -= Rt + 1; Rt++; }
-                const int R = j0 + 16 + 16 * Rt, C = j0 + 16 + 16 * Ct;
-#pragma unroll
-                for (int k4 = 0; k4 < 16; k4 += 4) {
-                    const int k = j0 + k4 + lk;
-                    const double av = S[R + li][k] * S[k][k];
-                    const double bv = S[C + li][k];
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int r = R + lk + 4 * g, c = C + li;
-                    if (r >= c) S[r][c] -= acc[g];
-                }
-            } else {
-                const int q = t - nsch, I = K + 1 + q / (K + 1), J = q % (K + 1);
-                const int cidx = 16 * J + li;
-#pragma unroll
-                for (int k4 = 0; k4 < 16; k4 += 4) {
-                    const int k = k4 + lk, kk = j0 + k;
-                    const double av = S[16 * I + li][kk];                                 // L[16I+li][kk]
-                    double bv;                                                            // X[kk][cidx]
-                    if (J < K) bv = S[cidx][kk];
-                    else bv = (k == li) ? 1.0 : (k > li ? S[cidx][kk] : 0.0);
-                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-                }
-#pragma unroll
-                for (int g = 0; g < 4; g++) S[cidx][16 * I + lk + 4 * g] += acc[g];       // T_IJ[r][c]
-            }
-        }
-        __syncthreads();
-#ifdef DEFTRI_DIAG_TIMING
-        tp[ntp++] = clock64();
-#endif
-    }
-    __syncthreads();
-#ifdef DEFTRI_DIAG_TIMING
-    tp[ntp++] = clock64();
-    if (threadIdx.x == 0 && (blockIdx.x & 1023) == 0) {
-        long long d[13];
-        for (int q = 0; q < 13; q++) d[q] = (q + 1 < ntp) ? tp[q + 1] - tp[q] : 0;
-        printf("[diagphase] kb %d: %lld %lld %lld | %lld %lld %lld | %lld %lld %lld | %lld %lld %lld | %lld\n", kb, d[0],
-               d[1], d[2], d[3], d[4], d[5], d[6], d[7], d[8], d[9], d[10], d[11], d[12]);
-    }
-#endif
-}
-
-// load the panel diagonal block of (front F, panel k0) into S (identity padding), factor, store L/D
-// into the front and Linv (kb x kb, column-major) into the inverse arena
-__device__ __forceinline__ void diag_panel(double *F, int m, int s, int k0, double *Li, double (*S)[DP], int *flag) {
-    const int kb = min(64, s - k0);
-#ifdef DEFTRI_DIAG_TIMING
-    long long tm0 = clock64();
-#endif
-    // all 16 loads per thread in flight at once (unrolled), then the LDS stores
-    double v[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        v[q] = (r < kb && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        S[r][c] = v[q];
-    }
-    __syncthreads();
-#ifdef DEFTRI_DIAG_TIMING
-    long long tm1 = clock64();
-#endif
-    diag_block(S, kb, flag);
-#ifdef DEFTRI_DIAG_TIMING
-    long long tm2 = clock64();
-#endif
-#pragma unroll
-    for (int q = 0; q < 16; q++) {
-        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        if (r < kb && c < kb) {
-            if (r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
-            Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
-        }
-    }
-#ifdef DEFTRI_DIAG_TIMING
-    __syncthreads();
-    long long tm3 = clock64();
-    if (threadIdx.x == 0 && (blockIdx.x & 1023) == 0)
-        printf("[diagtime] blk %d load %lld block %lld store %lld\n", (int)blockIdx.x, tm1 - tm0, tm2 - tm1, tm3 - tm2);
-#endif
-}
-
-// ------------------------------------------------------------------------------------------
-// v2: the same arithmetic (bit-identical L, D, X), shorter critical path
+// Four 16-column sub-panels K, each: the 16x16 diagonal block's pivot chain in the registers of
+// wave 0 (F), the inverse blocks of block row K and the sub-panel TRSM below it (B, f64 MFMA), the
+// trailing Schur update and the inverse accumulators (U, f64 MFMA tiles).  Critical-path design
+// (bit-identical to the first, ds_bpermute-based version; 21.0 -> 18.4 us per panel in isolation):
 //   * the 16-step pivot chain broadcasts through DPP / permlane instead of ds_bpermute: row j of
 //     the block (same 16-lane DPP row) by v_mov_b64_dpp row_newbcast:j, column j (one lane per
 //     row, in DPP row j&3) by v_permlane16_swap + v_permlane32_swap;
@@ -282,7 +86,7 @@ __device__ __forceinline__ double bcast_row(double v) {
 }
 
 // pivot chain of one 16x16 diagonal block in the registers of one wave (lane = r + 16 g holds
-// A[r][g + 4q], X[r][g + 4q], q = 0..3); same operations as diag_block's F phase.  Branch-free
+// A[r][g + 4q], X[r][g + 4q], q = 0..3): right-looking steps over the block's 16 pivots.  Branch-free
 // steps (selects), the zero-pivot test folded into one flag write at the end.
 template <bool FULL>
 __device__ __forceinline__ void f_chain(double (*S)[DP], int j0, int jend, int *flag) {
@@ -418,10 +222,14 @@ __device__ long long g_diag_t2[64];
 #define T2MARK(i) do {} while (0)
 #define T2MARKW(i, w) do {} while (0)
 #endif
-__device__ __forceinline__ void diag_block_v2(double (*S)[DP], int kb, int *flag) {
+// rows kb..nrows-1 (nrows <= 64) below the kb x kb pivot block carry the panel's next rows: the
+// right-looking steps of the kb pivots turn them into L21 = A21 L11^{-T} D^{-1} (the TRSM of the
+// tile's remaining rows); their own "pivots" are never taken (steps past kb are no-ops) and the
+// trailing part they update is scratch
+__device__ __forceinline__ void diag_block_v2(double (*S)[DP], int kb, int nrows, int *flag) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int nsub = (kb + 15) >> 4;
+    const int nsub = (max(kb, nrows) + 15) >> 4;
     T2MARK(1);
     for (int K = 0; K < nsub; K++) {
         const int j0 = 16 * K;
@@ -488,14 +296,19 @@ __device__ __forceinline__ void diag_block_v2(double (*S)[DP], int kb, int *flag
     T2MARK(40);
 }
 
-__device__ __forceinline__ void diag_panel_v2(double *F, int m, int s, int k0, double *Li, double (*S)[DP], int *flag) {
-    const int kb = min(64, s - k0);
+// panel k0 of front F (m rows, s own columns): the kb x kb diagonal block's LDL^T + inverse; with
+// tail_rows (the fused-TRSM plan) also the TRSM of the remaining rows of the 64-row diagonal tile
+// (rows k0+kb .. min(m, k0+64)), so the row tiles start at k0+64.  Without it (measured faster:
+// partial panels then need only nsub sub-panels) k_trsm solves rows k0+kb..
+__device__ __forceinline__ void diag_panel_v2(double *F, int m, int s, int k0, double *Li, double (*S)[DP], int *flag,
+                                              bool tail_rows) {
+    const int kb = min(64, s - k0), mt = tail_rows ? min(64, m - k0) : kb;
     T2MARK(0);
     double v[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        v[q] = (r < kb && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
+        v[q] = (r < mt && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
     }
 #pragma unroll
     for (int q = 0; q < 16; q++) {
@@ -503,14 +316,12 @@ __device__ __forceinline__ void diag_panel_v2(double *F, int m, int s, int k0, d
         S[r][c] = v[q];
     }
     __syncthreads();
-    diag_block_v2(S, kb, flag);
+    diag_block_v2(S, kb, mt, flag);
 #pragma unroll
     for (int q = 0; q < 16; q++) {
         int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        if (r < kb && c < kb) {
-            if (r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
-            Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
-        }
+        if (r < mt && c < kb && r >= c) F[(int64_t)(k0 + c) * m + k0 + r] = S[r][c];
+        if (r < kb && c < kb) Li[(int64_t)c * kb + r] = (r > c) ? S[c][r] : (r == c ? 1.0 : 0.0);
     }
 #ifdef DEFTRI_DIAG_T2
     __syncthreads();

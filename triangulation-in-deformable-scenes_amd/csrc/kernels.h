@@ -33,14 +33,14 @@ struct DevProblem {
 };
 
 struct FrontDev {
-    const int32_t *m, *s, *parent, *nchild, *child0, *child1, *direct, *rhs_bnd;
+    const int32_t *m, *s, *parent, *nchild, *child0, *child1, *direct, *rhs_bnd, *panel_off;
     const int64_t *arena_off, *vec_off, *rows_off, *bmap_off, *inv_off;
     const int32_t *rows, *bmap;
 };
 
 struct LevelDev {
     int64_t ea_off[2]; int32_t nea[2];
-    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner, stream, wait_side; double upd_flops; };
+    struct Step { int64_t diag_off; int32_t ndiag; int64_t trsm_off; int32_t ntrsm; int64_t upd_off; int32_t nupd; int32_t k0, kA, kmax, inner, stream, wait_side; double upd_flops; int32_t ntail, ndiag_tail; };
     std::vector<Step> steps;
     int64_t fwd_off; int32_t nfwd;
     struct SolveStep { int64_t off; int32_t n; };
@@ -51,8 +51,13 @@ struct LevelDev {
 // batched LM trials ("lambda lanes"): every factor/solve launch carries a second grid dimension,
 // lane = blockIdx.y, whose buffers sit at these strides from lane 0's (all zero for one lane)
 constexpr int kMaxLanes = 8;
+// status flag bits: 1 = zero pivot (the trial fails, as g2o's); kStatusWaitTimeout = a fused-TRSM tile
+// gave up waiting for its panel (a plan / dispatch bug: the solve reports DEFTRI_E_HIP).  Large so a
+// cross-rank sum of zero-pivot flags never reaches it.
+constexpr int kStatusWaitTimeout = 1 << 20;
 struct LaneOff {
     int64_t arena = 0, inv = 0, vec = 0, x = 0;   // doubles between consecutive lanes' buffers
+    int64_t pflag = 0;                            // panels between consecutive lanes' flags (x 4096: wbuf doubles)
     double lam[kMaxLanes] = {0, 0, 0, 0, 0, 0, 0, 0};   // setLambda of each lane (k_scatter)
 };
 
@@ -88,7 +93,10 @@ struct DevPlan {
     FrontDev fd{};
     int32_t *tasks = nullptr;
     std::vector<LevelDev> levels;
-    int *flag = nullptr;          // one zero-pivot flag per lane
+    int *flag = nullptr;          // one status flag per lane (1 zero pivot, kStatusWaitTimeout)
+    int64_t npanels = 0;
+    int *pflag = nullptr;         // per panel (x lanes): the factorization epoch that last factored it
+    double *wbuf = nullptr;       // per panel (x lanes): 64 x 64 TRSM operand W = Linv^T D^{-1} (fused TRSM)
     int nlanes = 1;               // lanes the factor / solve launches cover (blockIdx.y)
     LaneOff lo{};
 };

@@ -15,6 +15,7 @@
 // no floating-point atomics anywhere on the path.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 
@@ -475,16 +476,133 @@ __global__ void __launch_bounds__(256) k_ea(int ntask, const int32_t *__restrict
 
 // standalone panel factorization (first panel of every front of a level; later panels are
 // factored by the update launch of the previous panel, see k_update)
-__global__ void __launch_bounds__(256) k_diag(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+// ---- fused TRSM: the row tiles of a panel are solved by the launch that factors its diagonal tile.
+// Cross-workgroup hand-off inside one launch, across XCDs (each has its own L2): the factoring
+// workgroup writes W = Linv^T D^{-1} (the TRSM operand, 64 x 64) to the panel's slot of `wbuf` with
+// agent-coherent stores (relaxed agent-scope atomics: sc1 stores, no L2 write-back), waits for them
+// to complete, then stores the factorization epoch into the panel's flag the same way.  A row-tile
+// workgroup — placed after every diagonal task of its launch, so dispatched after it (in-order
+// dispatch: it never holds a slot the diagonal task needs) — polls the flag with coherent loads and
+// reads W coherently.  No release/acquire fences: at agent scope those write back / invalidate the
+// whole L2.  A poll that outlives kSpinLimit sets kStatusWaitTimeout (a device error) instead of
+// hanging.
+constexpr int kSpinLimit = 1 << 22;
+__device__ __forceinline__ void st_coherent(double *p, double v) {
+    __hip_atomic_store((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coherent(const double *p) {
+    return __builtin_bit_cast(double, __hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// W[k][c] = Linv[c][k] / d_c from the factored block in LDS (X[c][k] at S[k][c], D at S[c][c]) —
+// the products k_trsm forms from the stored inverse and the front's diagonal
+__device__ __forceinline__ void publish_panel(const double (*S)[DP], int kb, double *W, int *pf, int epoch) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int idx = threadIdx.x + 256 * q, kk = idx >> 6, c = idx & 63;
+        double v = 0.0;
+        if (kk < kb && c < kb) v = (c > kk ? S[kk][c] : (c == kk ? 1.0 : 0.0)) * (1.0 / S[c][c]);
+        st_coherent(W + idx, v);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): this thread's W stores are complete
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(pf, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wait_panel(const int *pf, int epoch, int *flag) {
+    if (threadIdx.x == 0) {
+        int it = 0;
+        while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            if (++it > kSpinLimit) { atomicOr(flag, kStatusWaitTimeout); break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+// rows r0..r0+63 of panel k1 (kb columns), pre-solve values in T[c][r] (LDS): L = T W, stored to the
+// front — k_trsm's arithmetic (same products, same MFMA order).  One 4-k-step group at a time with
+// scheduling barriers: unconstrained, the scheduler hoists every load and k_update spills.
+__device__ __forceinline__ void tile_trsm(const double (*T)[DP], double *F, int m, int k1, int kb, int r0,
+                                          const double *W) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int rb = (w & 1) * 32, cb = (w >> 1) * 32;
+    const int kl = lane >> 4, il = lane & 15;
+    const int kb4 = (kb + 3) & ~3;
+    dbl4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int grp = 0; grp < 4; grp++) {
+        if (16 * grp >= kb4) break;
+        double p0[4], p1[4], q0[4], q1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int kk = 16 * grp + 4 * u + kl;
+            p0[u] = ld_coherent(W + kk * 64 + cb + il);
+            p1[u] = ld_coherent(W + kk * 64 + cb + 16 + il);
+            q0[u] = T[kk][rb + il];
+            q1[u] = T[kk][rb + 16 + il];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (16 * grp + 4 * u < kb4) {
+                acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0[u], q0[u], acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0[u], q1[u], acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1[u], q0[u], acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1[u], q1[u], acc[1][1], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                if (c < kb && r0 + r < m) F[(int64_t)(k1 + c) * m + r0 + r] = acc[a][b][g];
+            }
+}
+
+// the first panel of every front of a level (later panels are factored by the update launch that
+// finishes their diagonal tile, see k_update); tasks past ndiag are that panel's row tiles (fused TRSM)
+// TAIL: tasks past ndiag are fused-TRSM tiles (separate instantiation, as k_update's)
+template <bool TAIL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 1 : 4))) k_diag(int ntask, int ndiag, const int32_t *__restrict__ tasks, const FrontDev fd,
                                               double *__restrict__ arena, double *__restrict__ inv,
-                                              int *__restrict__ flag, const LaneOff lo) {
+                                              int *__restrict__ flag, int *__restrict__ pflag, double *__restrict__ wbuf,
+                                              int epoch, const LaneOff lo) {
     __shared__ double S[64][DP];
     int t = blockIdx.x;
     if (t >= ntask) return;
-    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y;
-    int f = tasks[3 * t], k0 = tasks[3 * t + 1];
-    diag_panel_v2(arena + fd.arena_off[f], fd.m[f], fd.s[f], k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S,
-               flag);
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y; pflag += blockIdx.y * lo.pflag;
+    if (wbuf) wbuf += blockIdx.y * lo.pflag * 4096;
+    const int f = tasks[3 * t], k0 = tasks[3 * t + 1], r0 = tasks[3 * t + 2];
+    const int m = fd.m[f], s = fd.s[f];
+    double *F = arena + fd.arena_off[f];
+    const int pid = fd.panel_off[f] + k0 / 64;
+    if (t < ndiag) {
+        diag_panel_v2(F, m, s, k0, inv + fd.inv_off[f] + (int64_t)(k0 / 64) * 4096, S, flag, TAIL);
+        if (TAIL) publish_panel(S, min(64, s - k0), wbuf + (int64_t)pid * 4096, pflag + pid, epoch);
+        return;
+    }
+    if (!TAIL) return;
+    const int kb = min(64, s - k0);
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+        v[q] = (c < kb && r0 + r < m) ? F[(int64_t)(k0 + c) * m + r0 + r] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+        S[c][r] = v[q];
+    }
+    wait_panel(pflag + pid, epoch, flag);
+    tile_trsm(S, F, m, k0, kb, r0, wbuf + (int64_t)pid * 4096);
 }
 
 // f64 MFMA tile: C(64x64) = sum_k P[k][c] Q[k][r], P/Q k-major in LDS ([k][index]); wave w owns the
@@ -595,8 +713,8 @@ __device__ __forceinline__ int xcd_task(int ntask) {
 // scalar loads per lane — double-buffered (chunk c+1's loads in flight during chunk c's MFMAs), one
 // barrier per chunk; each wave reads its 32x32 quadrant's fragments from LDS.  Same products and
 // summation order as the register-streaming kernel it replaced (bit-identical), 1.3-1.5x faster
-// (tools/micro/upd_bench.hip: 30 -> 42 TF/s on 2000-row fronts, K = 256).  The C tile is fetched
-// before the K loop.  The staging buffers alias the fused panel factorization's LDS.
+// (tools/micro/upd_bench.hip: 30 -> 42 TF/s on 2000-row fronts, K = 256).  The staging buffers
+// alias the fused panel factorization's LDS.
 constexpr int kUpdKC = 16;                 // k columns per staged chunk
 // two consecutive column entries p[0..1] of which nvalid remain in the column (16-byte load when
 // aligned; odd m gives odd column starts)
@@ -613,14 +731,19 @@ union UpdSmem {
 #define DEFTRI_UPD_WPE 4   // waves per EU of k_update (tuning knob)
 #endif
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, const int32_t *__restrict__ tasks, int kA, int kmax,
+// TAIL: the launch carries fused-TRSM tail tiles (a separate instantiation: the tail path's registers
+// would otherwise spill the plain launches' main loop)
+template <bool TAIL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, int ntail, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
                                                 double *__restrict__ inv, int *__restrict__ flag,
+                                                int *__restrict__ pflag, double *__restrict__ wbuf, int epoch,
                                                 const LaneOff lo) {
     __shared__ UpdSmem sm;
     int t = xcd_task(ntask);
     if (t >= ntask) return;
-    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; flag += blockIdx.y; pflag += blockIdx.y * lo.pflag;
+    if (wbuf) wbuf += blockIdx.y * lo.pflag * 4096;
     int f = tasks[3 * t], ti = tasks[3 * t + 1], tj = tasks[3 * t + 2];
     int m = fd.m[f], s = fd.s[f];
     int K = min(kmax, s - kA);
@@ -655,17 +778,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         *(dbl2 *)&sm.st.Q[buf][sk][sr + 2] = qv1;
     };
     stage_load(0);
-    // C prefetch: acc layout (a, b, g) -> column cb + 16a + kl + 4g, row rb + 16b + il
+    // C tile: acc layout (a, b, g) -> column cb + 16a + kl + 4g, row rb + 16b + il.  Plain launches
+    // fetch it before the K loop; TAIL launches during the last chunk (registers)
     double cv[2][2][4];
+    auto load_c = [&]() {
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+        for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 2; b++)
+            for (int b = 0; b < 2; b++)
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
-                cv[a][b][g] = (c < m && r < m) ? F[(int64_t)c * m + r] : 0.0;
-            }
+                for (int g = 0; g < 4; g++) {
+                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    cv[a][b][g] = (c < m && r < m) ? F[(int64_t)c * m + r] : 0.0;
+                }
+    };
+    if (!TAIL) load_c();
     dbl4 acc[2][2];
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -673,10 +800,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
     stage_store(0);
     __syncthreads();
-    const int nch = (K + kUpdKC - 1) / kUpdKC;
-    for (int c = 0; c < nch; c++) {
-        const int buf = c & 1;
-        if (c + 1 < nch) stage_load((c + 1) * kUpdKC);
+    auto mfma_chunk = [&](int buf) {
 #pragma unroll
         for (int k4 = 0; k4 < kUpdKC; k4 += 4) {
             const double p0 = sm.st.P[buf][k4 + kl][pc + il], p1 = sm.st.P[buf][k4 + kl][pc + 16 + il];
@@ -686,8 +810,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
         }
-        if (c + 1 < nch) stage_store(buf ^ 1);
+    };
+    const int nch = (K + kUpdKC - 1) / kUpdKC;
+    if constexpr (TAIL) {
+        for (int c = 0; c + 1 < nch; c++) {
+            stage_load((c + 1) * kUpdKC);
+            mfma_chunk(c & 1);
+            stage_store((c + 1) & 1);
+            __syncthreads();
+        }
+        load_c();
+        mfma_chunk((nch - 1) & 1);
         __syncthreads();
+    } else {
+        for (int c = 0; c < nch; c++) {
+            const int buf = c & 1;
+            if (c + 1 < nch) stage_load((c + 1) * kUpdKC);
+            mfma_chunk(buf);
+            if (c + 1 < nch) stage_store(buf ^ 1);
+            __syncthreads();
+        }
+    }
+    // fused TRSM tile (i > k1, k1) of the panel this launch factors: the updated tile goes to LDS
+    // (columns past the panel, if any, are stored as plain update results), then, once the panel's
+    // factorization is published, its rows are solved in place
+    if (TAIL && t >= ntask - ntail) {
+        const int k1 = kA + K, kb = min(64, s - k1);
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int cl = cb - tj + 16 * a + kl + 4 * g, rl = rb - ti + 16 * b + il;
+                    const double v = cv[a][b][g] - acc[a][b][g];
+                    if (cl < kb) sm.S[cl][rl] = v;
+                    else if (tj + cl < cend && ti + rl < m) F[(int64_t)(tj + cl) * m + ti + rl] = v;
+                }
+        const int pid = fd.panel_off[f] + k1 / 64;
+        wait_panel(pflag + pid, epoch, flag);
+        tile_trsm(sm.S, F, m, k1, kb, ti, wbuf + (int64_t)pid * 4096);
+        return;
     }
     // the front's last trailing update produces its final contribution block: a direct front adds
     // it straight into the parent (lower triangle; bmap is monotone, each parent entry has one writer
@@ -723,7 +886,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     if (ti == tj && ti == k1 && s > k1) {
         __syncthreads();
         __threadfence_block();
-        diag_panel_v2(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, flag);
+        diag_panel_v2(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, flag, TAIL);
+        if (TAIL) {
+            const int pid = fd.panel_off[f] + k1 / 64;
+            publish_panel(sm.S, min(64, s - k1), wbuf + (int64_t)pid * 4096, pflag + pid, epoch);
+        }
     }
 }
 
@@ -1206,6 +1373,10 @@ void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
 
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev, LevelHook hook,
                    void *hook_user) {
+    // a fresh epoch per factorization: the panel flags never need clearing
+    static std::atomic<int> g_epoch{0};
+    int epoch = ++g_epoch;
+    if (epoch <= 0) { g_epoch = 1; epoch = 1; }
     int evi = 0;
     hipEvent_t prev_side = nullptr, cur_side = nullptr;   // events of the last two side-stream updates
     for (size_t h = 0; h < L.levels.size(); h++) {
@@ -1218,8 +1389,9 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
                                    L.tasks + 3 * lv.ea_off[slot], L.fd, L.arena, L.lo);
         for (const auto &stp : lv.steps) {
             if (stp.ndiag > 0)
-                LAUNCH("diag", dev::k_diag, dim3(stp.ndiag, L.nlanes), dim3(256), st, stp.ndiag,
-                                   L.tasks + 3 * stp.diag_off, L.fd, L.arena, L.inv, L.flag, L.lo);
+                LAUNCH("diag", stp.ndiag_tail ? dev::k_diag<true> : dev::k_diag<false>, dim3(stp.ndiag + stp.ndiag_tail, L.nlanes), dim3(256), st,
+                       stp.ndiag + stp.ndiag_tail, stp.ndiag, L.tasks + 3 * stp.diag_off, L.fd, L.arena, L.inv, L.flag,
+                       L.pflag, L.wbuf, epoch, L.lo);
             if (stp.ntrsm > 0)
                 LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm, L.nlanes), dim3(256), st, stp.ntrsm,
                                    L.tasks + 3 * stp.trsm_off, L.fd, L.arena, L.inv, L.lo);
@@ -1234,9 +1406,9 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
                     hipEventRecord(e, st);
                     hipStreamWaitEvent(side, e, 0);
                     g_work = stp.upd_flops;
-                    LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), side, stp.nupd,
-                           L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv, L.flag,
-                           L.lo);
+                    LAUNCH("update", stp.ntail ? dev::k_update<true> : dev::k_update<false>, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), side, stp.nupd,
+                           stp.ntail, L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv,
+                           L.flag, L.pflag, L.wbuf, epoch, L.lo);
                     cur_side = ev[evi++ % nev];
                     hipEventRecord(cur_side, side);
                 }
@@ -1246,9 +1418,9 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
             if (stp.wait_side == 2 && cur_side) hipStreamWaitEvent(st, cur_side, 0);
             if (stp.nupd > 0) {
                 g_work = stp.upd_flops;
-                LAUNCH("update", dev::k_update, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), st, stp.nupd,
-                       L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
-                       L.arena, L.inv, L.flag, L.lo);
+                LAUNCH("update", stp.ntail ? dev::k_update<true> : dev::k_update<false>, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), st, stp.nupd,
+                       stp.ntail, L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
+                       L.arena, L.inv, L.flag, L.pflag, L.wbuf, epoch, L.lo);
             }
         }
         // the level's side-stream work must be complete before the next level (or the solve) reads it

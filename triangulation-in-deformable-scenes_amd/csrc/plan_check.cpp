@@ -59,13 +59,14 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
     auto diag = [&](int f, int k0) -> bool {
         const Front &F = S.fronts[f];
         double *A = Fp(f);
-        int kb = std::min(64, F.s - k0), m = F.m;
+        // kb pivots; in the fused-TRSM plan rows kb..mt-1 of the 64-row diagonal tile become L21 too
+        int kb = std::min(64, F.s - k0), m = F.m, mt = S.trsm_fused ? std::min(64, F.m - k0) : kb;
         for (int j = 0; j < kb; j++) {
             double d = A[(int64_t)(k0 + j) * m + k0 + j];
             if (d == 0.0) return false;
-            for (int i = j + 1; i < kb; i++) A[(int64_t)(k0 + j) * m + k0 + i] /= d;
+            for (int i = j + 1; i < mt; i++) A[(int64_t)(k0 + j) * m + k0 + i] /= d;
             for (int c = j + 1; c < kb; c++)
-                for (int i = c; i < kb; i++)
+                for (int i = c; i < mt; i++)
                     A[(int64_t)(k0 + c) * m + k0 + i] -= A[(int64_t)(k0 + j) * m + k0 + i] * d * A[(int64_t)(k0 + j) * m + k0 + c];
         }
         return true;
@@ -107,26 +108,33 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                     for (int i = std::max(j, i0); i < std::min(i0 + 256, u); i++)
                         Fp(C.parent)[(int64_t)bm[j] * Pf.m + bm[i]] += Fp(c)[(int64_t)(C.s + j) * C.m + C.s + i];
             }
+        // rows r0..r0+63 of panel k0: L = A L11^{-T} D^{-1} (k_trsm / the fused TRSM tiles)
+        auto trsm = [&](int f, int k0, int r0) {
+            const Front &F = S.fronts[f];
+            double *A = Fp(f);
+            int kb = std::min(64, F.s - k0), m = F.m;
+            for (int i = r0; i < std::min(r0 + 64, m); i++) {
+                double z[64];
+                for (int j = 0; j < kb; j++) {
+                    double v = A[(int64_t)(k0 + j) * m + i];
+                    for (int c = 0; c < j; c++) v -= A[(int64_t)(k0 + c) * m + k0 + j] * z[c];
+                    z[j] = v;
+                }
+                for (int j = 0; j < kb; j++) A[(int64_t)(k0 + j) * m + i] = z[j] / A[(int64_t)(k0 + j) * m + k0 + j];
+            }
+        };
         for (const auto &st : lv.steps) {
             for (int32_t t = 0; t < st.ndiag; t++) {
                 const int32_t *tk = T + 3 * (st.diag_off + t);
                 if (!diag(tk[0], tk[1])) return -1;
             }
+            for (int32_t t = st.ndiag; t < st.ndiag + st.ndiag_tail; t++) {      // fused TRSM tiles of the diag launch
+                const int32_t *tk = T + 3 * (st.diag_off + t);
+                trsm(tk[0], tk[1], tk[2]);
+            }
             for (int32_t t = 0; t < st.ntrsm; t++) {
                 const int32_t *tk = T + 3 * (st.trsm_off + t);
-                int f = tk[0], k0 = tk[1], r0 = tk[2];
-                const Front &F = S.fronts[f];
-                double *A = Fp(f);
-                int kb = std::min(64, F.s - k0), m = F.m;
-                for (int i = r0; i < std::min(r0 + 64, m); i++) {
-                    double z[64];
-                    for (int j = 0; j < kb; j++) {
-                        double v = A[(int64_t)(k0 + j) * m + i];
-                        for (int c = 0; c < j; c++) v -= A[(int64_t)(k0 + c) * m + k0 + j] * z[c];
-                        z[j] = v;
-                    }
-                    for (int j = 0; j < kb; j++) A[(int64_t)(k0 + j) * m + i] = z[j] / A[(int64_t)(k0 + j) * m + k0 + j];
-                }
+                trsm(tk[0], tk[1], tk[2]);
             }
             for (int32_t t = 0; t < st.nupd; t++) {
                 const int32_t *tk = T + 3 * (st.upd_off + t);
@@ -159,6 +167,11 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
                 const Front &F = S.fronts[tk[0]];
                 int k1 = st.kA + std::min(st.kmax, F.s - st.kA);
                 if (tk[1] == tk[2] && tk[1] == k1 && F.s > k1 && !diag(tk[0], k1)) return -1;
+            }
+            // fused TRSM tiles: the launch's last ntail tasks (ti, k1) solve their rows once k1 is factored
+            for (int32_t t = st.nupd - st.ntail; t < st.nupd; t++) {
+                const int32_t *tk = T + 3 * (st.upd_off + t);
+                trsm(tk[0], tk[2], tk[1]);
             }
         }
     }

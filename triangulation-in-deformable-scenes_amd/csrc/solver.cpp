@@ -376,20 +376,20 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     if ((rc = dalloc(ctx, &L.inv, S.inv_size))) return rc;
     {
         int32_t nf = (int32_t)S.fronts.size();
-        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf), dir(nf), rb(nf);
+        std::vector<int32_t> m(nf), s(nf), par(nf), nch(nf), c0(nf), c1(nf), dir(nf), rb(nf), po(nf);
         std::vector<int64_t> ao(nf), vo(nf), ro(nf), bo(nf), io(nf);
         for (int32_t f = 0; f < nf; f++) {
             const Front &F = S.fronts[f];
             m[f] = F.m; s[f] = F.s; par[f] = F.parent; nch[f] = F.nchild; c0[f] = F.child[0]; c1[f] = F.child[1];
-            dir[f] = F.direct; rb[f] = F.rhs_bnd;
+            dir[f] = F.direct; rb[f] = F.rhs_bnd; po[f] = F.panel_off;
             ao[f] = F.arena_off; vo[f] = F.vec_off; ro[f] = F.rows_off; bo[f] = F.bmap_off; io[f] = F.inv_off;
         }
-        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *pdir, *prb, *prows, *pbmap;
+        int32_t *pm, *ps, *pp, *pn, *pc0, *pc1, *pdir, *prb, *ppo, *prows, *pbmap;
         int64_t *pao, *pvo, *pro, *pbo, *pio;
-        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1); PUT(pdir, dir); PUT(prb, rb);
+        PUT(pm, m); PUT(ps, s); PUT(pp, par); PUT(pn, nch); PUT(pc0, c0); PUT(pc1, c1); PUT(pdir, dir); PUT(prb, rb); PUT(ppo, po);
         PUT(pao, ao); PUT(pvo, vo); PUT(pro, ro); PUT(pbo, bo); PUT(pio, io);
         PUT(prows, S.rows); PUT(pbmap, S.bmap);
-        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pdir, prb, pao, pvo, pro, pbo, pio, prows, pbmap};
+        L.fd = FrontDev{pm, ps, pp, pn, pc0, pc1, pdir, prb, ppo, pao, pvo, pro, pbo, pio, prows, pbmap};
     }
     PUT(L.tasks, S.task_i32);
     L.levels.clear();
@@ -397,7 +397,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
         LevelDev ld{};
         for (int k = 0; k < 2; k++) { ld.ea_off[k] = lv.ea_off[k]; ld.nea[k] = lv.nea[k]; }
         for (const auto &stp : lv.steps)
-            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner, stp.stream, stp.wait_side, stp.upd_flops});
+            ld.steps.push_back({stp.diag_off, stp.ndiag, stp.trsm_off, stp.ntrsm, stp.upd_off, stp.nupd, stp.k0, stp.kA, stp.kmax, stp.inner, stp.stream, stp.wait_side, stp.upd_flops, stp.ntail, stp.ndiag_tail});
         ld.fwd_off = lv.fwd_off; ld.nfwd = lv.nfwd;
         for (const auto &x : lv.fsteps) ld.fsteps.push_back({x.off, x.n});
         for (const auto &x : lv.bsteps) ld.bsteps.push_back({x.off, x.n});
@@ -405,6 +405,10 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
         L.levels.push_back(ld);
     }
     if ((rc = dalloc(ctx, &L.flag, 1))) return rc;
+    L.npanels = S.npanels;
+    if ((rc = dalloc(ctx, &L.pflag, std::max<int64_t>(S.npanels, 1)))) return rc;
+    HIPOK(hipMemset(L.pflag, 0, sizeof(int) * (size_t)std::max<int64_t>(S.npanels, 1)));
+    if (S.trsm_fused && (rc = dalloc(ctx, &L.wbuf, 4096 * std::max<int64_t>(S.npanels, 1)))) return rc;   // else nullptr: no W
     if ((rc = dalloc(ctx, &ctx->d_dx, S.ndof))) return rc;
     HIPOK(hipMemset(ctx->d_dx, 0, sizeof(double) * (size_t)std::max<int64_t>(S.ndof, 1)));   // dofs no solve writes stay 0
     if ((rc = dalloc(ctx, &ctx->d_part, kRedParts))) return rc;
@@ -617,10 +621,13 @@ int ensure_lanes(deftri_ctx *ctx, int want) {
     LB.nlanes = n;
     LB.lo = LaneOff{};
     LB.lo.arena = L0.arena_size; LB.lo.inv = L0.inv_size; LB.lo.vec = L0.vec_size; LB.lo.x = L0.ndof;
+    LB.lo.pflag = std::max<int64_t>(L0.npanels, 1);
     if (dalloc(ctx, &LB.arena, n * L0.arena_size) || dalloc(ctx, &LB.inv, n * std::max<int64_t>(L0.inv_size, 1)) ||
         dalloc(ctx, &LB.vec, n * L0.vec_size) || dalloc(ctx, &LB.yvec, n * L0.vec_size) ||
-        dalloc(ctx, &LB.flag, n) || dalloc(ctx, &ctx->dx_lanes, n * L0.ndof))
+        dalloc(ctx, &LB.flag, n) || dalloc(ctx, &LB.pflag, n * LB.lo.pflag) || (ctx->S.trsm_fused && dalloc(ctx, &LB.wbuf, 4096 * n * LB.lo.pflag)) ||
+        dalloc(ctx, &ctx->dx_lanes, n * L0.ndof))
         return -1;
+    if (hipMemset(LB.pflag, 0, sizeof(int) * (size_t)(n * LB.lo.pflag)) != hipSuccess) return -1;
     ctx->LB = LB;
     while ((int)ctx->lanes.size() < n) {
         Lane ln;
@@ -1062,6 +1069,9 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 t_fac += ev_ms(ctx, 2, 5);
                 R.trials_executed += nl;
                 int acc = -1;
+                for (int t = 0; t < nl; t++)
+                    if (ctx->lane_ipin[t] & kStatusWaitTimeout)
+                        return fail(ctx, DEFTRI_E_HIP, "factorization: a fused TRSM tile timed out waiting for its panel");
                 for (int t = 0; t < nl && !done; t++) {
                     const bool ok2 = ctx->lane_ipin[t] == 0;
                     double tempChi = ok2 ? ctx->lane_pin[2 * t] : std::numeric_limits<double>::max();
@@ -1120,6 +1130,8 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             }
             HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
+            if (dist ? sc[2] >= kStatusWaitTimeout : (*ctx->ipin & kStatusWaitTimeout) != 0)
+                return fail(ctx, DEFTRI_E_HIP, "factorization: a fused TRSM tile timed out waiting for its panel");
             const bool ok2 = dist ? sc[2] == 0.0 : *ctx->ipin == 0;
             t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
             double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
@@ -1377,6 +1389,7 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
     hipFree(dr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(ctx, DEFTRI_E_HIP, hipGetErrorString(e));
+    if (flag & kStatusWaitTimeout) return fail(ctx, DEFTRI_E_HIP, "factorization: a fused TRSM tile timed out waiting for its panel");
     return flag ? fail(ctx, DEFTRI_E_NUMERIC, "zero pivot") : 0;
 }
 

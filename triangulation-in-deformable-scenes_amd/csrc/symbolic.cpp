@@ -10,6 +10,7 @@
 #include <limits>
 #include <numeric>
 #include <thread>
+#include <unordered_set>
 
 namespace deftri {
 
@@ -465,7 +466,7 @@ struct Builder {
         if (D.top >= 0) S.fronts[D.top].rhs_bnd = 1;
         // offsets: arena / inverses for this rank's fronts, solve vectors also for remote children of
         // them (the forward transfer lands there)
-        int64_t aoff = 0, voff2 = 0, ioff = 0;
+        int64_t aoff = 0, voff2 = 0, ioff = 0, poff = 0;
         for (int32_t f = 0; f < nf; f++) {
             Front &F = S.fronts[f];
             const bool loc = local(f);
@@ -474,6 +475,8 @@ struct Builder {
             F.arena_off = loc ? aoff : 0;
             F.vec_off = needvec ? voff2 : 0;
             F.inv_off = loc ? ioff : 0;
+            F.panel_off = loc ? (int32_t)poff : 0;
+            if (loc) poff += (s + kPanel - 1) / kPanel;
             if (loc) aoff += (int64_t)m * m;
             if (needvec) voff2 += m;
             if (loc && s > 0) ioff += (int64_t)((s - 1) / kPanel) * kPanel * kPanel + (int64_t)((s - 1) % kPanel + 1) * ((s - 1) % kPanel + 1);
@@ -486,6 +489,7 @@ struct Builder {
         S.arena_size = aoff;
         S.vec_size = voff2;
         S.inv_size = ioff;
+        S.npanels = poff;
         auto local_row = [&](int32_t f, int64_t v) -> int32_t {
             const auto &L = fv[f];
             int64_t pv = S.elim_pos[v];
@@ -708,6 +712,15 @@ struct Builder {
             S.task_i32.push_back(a); S.task_i32.push_back(b); S.task_i32.push_back(c);
         };
         S.levels.assign(S.nlevels, {});
+        // DEFTRI_TRSM_FUSE=1: the panel TRSM rides the launch that factors the diagonal tile (tail
+        // tiles); measured at C2: 12.15 vs 12.36 ms per trial against separate k_trsm launches with the
+        // same W publication, but slower than the plain schedule without it (11.8) — off by default
+        static const bool trsm_fuse = [] {
+            const char *e = std::getenv("DEFTRI_TRSM_FUSE");
+            return e && std::atoi(e) == 1;
+        }();
+        std::unordered_set<int64_t> trsm_fused;             // (front, panel k0) whose TRSM rides an earlier launch
+        S.trsm_fused = trsm_fuse;
         for (int32_t h = 0; h < S.nlevels; h++) {
             auto &LT = S.levels[h];
             const auto &fs = S.level_fronts[h];
@@ -765,7 +778,9 @@ struct Builder {
                                           F.s > t0 && t0 == kA + K;
                     spans.push_back({f, t0, tend, has_diag ? 1 : 0});
                 }
-                for (int pass = 0; pass < 2; pass++)
+                // pass 1: the other tiles; pass 2 (trsm_fuse): the column tiles below each fused diagonal
+                // tile, last in the launch (they wait for that panel's factorization)
+                for (int pass = 0; pass < 3; pass++)
                     for (const auto &sp : spans) {
                         const int32_t f = sp[0], t0 = sp[1], tend = sp[2];
                         const bool has_diag = sp[3] != 0;
@@ -774,9 +789,17 @@ struct Builder {
                             if (has_diag) { push3(f, t0, t0); st.nupd++; }
                             continue;
                         }
+                        const bool fuse = has_diag && trsm_fuse;
+                        if (pass == 2) {
+                            if (!fuse) continue;
+                            for (int32_t ti = t0 + kPanel; ti < F.m; ti += 64) { push3(f, ti, t0); st.nupd++; st.ntail++; }
+                            trsm_fused.insert(((int64_t)f << 32) | (uint32_t)t0);
+                            continue;
+                        }
                         for (int32_t tj = t0; tj < tend; tj += 64)
                             for (int32_t ti = tj; ti < F.m; ti += 64) {
                                 if (has_diag && ti == t0 && tj == t0) continue;
+                                if (fuse && tj == t0) continue;
                                 push3(f, ti, tj); st.nupd++;
                             }
                     }
@@ -801,10 +824,25 @@ struct Builder {
                         double kb = std::min(kPanel, S.fronts[f].s - k0);
                         S.diag_flops += kb * kb * kb / 3.0;
                     }
+                    if (k0 == 0 && trsm_fuse)               // the level's first panel: TRSM tiles ride the diag launch
+                        for (int32_t f : fs) {
+                            const Front &F = S.fronts[f];
+                            if (F.s <= 0) continue;
+                            for (int32_t r0 = kPanel; r0 < F.m; r0 += 64) {
+                                push3(f, 0, r0); st.ndiag_tail++;
+                                S.trsm_flops += (double)std::min(64, F.m - r0) * std::min(kPanel, F.s) * std::min(kPanel, F.s);
+                            }
+                            trsm_fused.insert(((int64_t)f << 32) | 0u);
+                        }
                     st.trsm_off = (int64_t)S.task_i32.size() / 3;
                     for (int32_t f : fs) {
                         const Front &F = S.fronts[f];
                         if (F.s <= k0) continue;
+                        if (trsm_fused.count(((int64_t)f << 32) | (uint32_t)k0)) {
+                            const int32_t kb = std::min(kPanel, F.s - k0);
+                            for (int32_t r0 = k0 + kPanel; r0 < F.m; r0 += 64) S.trsm_flops += (double)std::min(64, F.m - r0) * kb * kb;
+                            continue;
+                        }
                         int32_t kb = std::min(kPanel, F.s - k0);
                         for (int32_t r0 = k0 + kb; r0 < F.m; r0 += 64) {
                             push3(f, k0, r0); st.ntrsm++;

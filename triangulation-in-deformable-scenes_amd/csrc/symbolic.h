@@ -57,6 +57,7 @@ struct Front {
     int32_t owner;       // rank that assembles and factors this front (0 on one rank)
     int32_t rhs_bnd;     // 1: this rank's top front under a remote parent — its boundary rows start the
                          //    forward solve from the rank's partial b of those (remote) vertices
+    int32_t panel_off;   // index of this front's first panel in the plan's per-panel "factored" flags
 };
 
 // Point-sharded plan (subtree-to-rank mapping of the nested-dissection tree).  Every rank runs the
@@ -97,6 +98,8 @@ struct Symbolic {
     std::vector<int32_t> rows;
     std::vector<int32_t> bmap;
     int64_t arena_size = 0, vec_size = 0, inv_size = 0;
+    int64_t npanels = 0;                         // panels of this rank's fronts (flag slots)
+    bool trsm_fused = false;                     // task lists carry fused-TRSM tail tiles (DEFTRI_TRSM_FUSE=1)
     int32_t nlevels = 0;
     std::vector<std::vector<int32_t>> level_fronts;   // this rank's fronts by height, ascending
     double factor_flops = 0;          // this rank's fronts
@@ -129,6 +132,11 @@ struct Symbolic {
         int64_t diag_off = 0; int32_t ndiag = 0;      // fronts with own cols at this panel
         int64_t trsm_off = 0; int32_t ntrsm = 0;      // (front, row-tile) pairs
         int64_t upd_off = 0; int32_t nupd = 0;        // (front, tile-i, tile-j) triples
+        // fused TRSM: the last ntail update tasks are the column tiles (i > k1, k1) of a panel whose
+        // diagonal tile this launch factors — after their update they wait for that panel's flag and
+        // solve their rows in place; the diag launch likewise carries ndiag_tail (front, k0, r0) tiles
+        // right after its ndiag tasks
+        int32_t ntail = 0, ndiag_tail = 0;
         int32_t k0 = 0;                               // panel of diag / trsm
         int32_t kA = 0, kmax = 0;                     // update: L columns [kA, kA + min(kmax, s - kA))
         int32_t inner = 0;                            // column clip: 0 none, 1 end of this outer block
