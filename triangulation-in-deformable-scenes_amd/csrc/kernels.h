@@ -109,11 +109,13 @@ struct KProf {
     std::vector<KProfRec> recs;
 };
 void set_profiler(KProf *p);
+bool profiling();
 
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);
-void launch_scatter(const DevPlan &L, double lambda, hipStream_t st);   // lane 0 / one lane
-void launch_scatter_lanes(const DevPlan &L, hipStream_t st);            // L.nlanes lanes, L.lo.lam
+// lam_dev (optional): lambda read on the device (captured graphs); otherwise the argument / L.lo.lam
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st, const double *lam_dev = nullptr);   // one lane
+void launch_scatter_lanes(const DevPlan &L, hipStream_t st, const double *lam_dev = nullptr);         // L.nlanes lanes
 // point-sharded plan: called by launch_factor before level h (contribution blocks from other ranks),
 // by launch_solve before forward level h and after backward level h (DistPlan transfers of that level)
 enum { kHookFactor = 0, kHookForward = 1, kHookBackward = 2 };

@@ -422,10 +422,12 @@ __global__ void k_bfinal(int64_t nv, const int64_t *__restrict__ v_chunk_begin, 
 __global__ void k_scatter(int64_t nblocks, const int64_t *__restrict__ val_off, const int32_t *__restrict__ brows,
                           const int32_t *__restrict__ bcols, const int64_t *__restrict__ barena,
                           const int32_t *__restrict__ bld, const int32_t *__restrict__ bdiag,
-                          const double *__restrict__ hval, const LaneOff lo, double *__restrict__ arena) {
+                          const double *__restrict__ hval, const LaneOff lo, const double *__restrict__ lam_dev,
+                          double *__restrict__ arena) {
     int64_t b = TID;
     if (b >= nblocks) return;
-    const double lambda = lo.lam[blockIdx.y];
+    // lam_dev: lambda read from device memory (the captured trial graph's launches keep one argument set)
+    const double lambda = lam_dev ? lam_dev[blockIdx.y] : lo.lam[blockIdx.y];
     arena += blockIdx.y * lo.arena;
     int R = brows[b], Cc = bcols[b], ld = bld[b];
     const double *h = hval + val_off[b];
@@ -1294,6 +1296,7 @@ thread_local KProf *g_prof = nullptr;
 thread_local double g_work = 0;   // algorithmic work of the next launch (profiling only)
 thread_local int g_level = -1;    // elimination-tree level of the launches being issued (profiling only)
 void set_profiler(KProf *p) { g_prof = p; }
+bool profiling() { return g_prof != nullptr; }
 static hipEvent_t prof_event() {
     KProf &P = *g_prof;
     if (P.next == P.pool.size()) { hipEvent_t e; hipEventCreate(&e); P.pool.push_back(e); }
@@ -1355,20 +1358,21 @@ void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
     }
 }
 
-void launch_scatter_lanes(const DevPlan &L, hipStream_t st) {
+void launch_scatter_lanes(const DevPlan &L, hipStream_t st, const double *lam_dev) {
     // lanes' arenas are contiguous (stride lo.arena >= arena_size): one fill covers them all
     const int64_t span = L.nlanes > 1 ? (int64_t)(L.nlanes - 1) * L.lo.arena + L.arena_size : L.arena_size;
     hipMemsetAsync(L.arena, 0, sizeof(double) * (size_t)span, st);
     if (L.nblocks > 0)
         LAUNCH("scatter", dev::k_scatter, dim3(nb(L.nblocks, 128), L.nlanes), dim3(128), st, L.nblocks,
-               L.blk_val_off, L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, L.lo, L.arena);
+               L.blk_val_off, L.blk_rows, L.blk_cols, L.blk_arena, L.blk_ld, L.blk_diag, L.hval, L.lo, lam_dev,
+               L.arena);
 }
 
-void launch_scatter(const DevPlan &L, double lambda, hipStream_t st) {
+void launch_scatter(const DevPlan &L, double lambda, hipStream_t st, const double *lam_dev) {
     DevPlan one = L;
     one.nlanes = 1;
     one.lo.lam[0] = lambda;
-    launch_scatter_lanes(one, st);
+    launch_scatter_lanes(one, st, lam_dev);
 }
 
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev, LevelHook hook,

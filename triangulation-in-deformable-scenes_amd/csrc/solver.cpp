@@ -136,6 +136,12 @@ struct deftri_ctx {
     bool dist() const { return nranks > 1; }
     uint64_t plan_hash = 0;                 // structure_hash of the analysed problem
     int64_t plan_reuses = 0;                // uploads that reused the plan (values only)
+    // one sequential trial's device work (setLambda scatter + factorization + solve: ~500 launches
+    // at C2) captured once per uploaded plan and replayed as one graph launch; lambda travels through
+    // d_lam.  Built lazily; dropped with the device buffers.
+    hipGraphExec_t trial_graph = nullptr;
+    bool trial_graph_failed = false;
+    double *d_lam = nullptr;
 };
 
 namespace {
@@ -175,7 +181,14 @@ int dput(deftri_ctx *ctx, T **p, const T *h, int64_t n) {
 template <class T>
 int dput(deftri_ctx *ctx, T **p, const std::vector<T> &v) { return dput(ctx, p, v.data(), (int64_t)v.size()); }
 
+void drop_trial_graph(deftri_ctx *ctx) {
+    if (ctx->trial_graph) hipGraphExecDestroy(ctx->trial_graph);
+    ctx->trial_graph = nullptr;
+    ctx->trial_graph_failed = false;
+}
+
 void free_device(deftri_ctx *ctx) {
+    drop_trial_graph(ctx);
     for (void *p : ctx->allocs) hipFree(p);
     ctx->allocs.clear();
     ctx->P = DevProblem();
@@ -405,6 +418,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
         L.levels.push_back(ld);
     }
     if ((rc = dalloc(ctx, &L.flag, 1))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_lam, 1))) return rc;
     L.npanels = S.npanels;
     if ((rc = dalloc(ctx, &L.pflag, std::max<int64_t>(S.npanels, 1)))) return rc;
     HIPOK(hipMemset(L.pflag, 0, sizeof(int) * (size_t)std::max<int64_t>(S.npanels, 1)));
@@ -984,6 +998,49 @@ int deftri_reset_state(deftri_ctx *ctx) {
     return 0;
 }
 
+namespace {
+// the sequential trial (scatter + factorization + solve) as one graph launch: single stream, no
+// cross-rank hooks, no per-launch profiling, no fused-TRSM epochs (DEFTRI_GRAPH=0 disables)
+bool trial_graph_usable(const deftri_ctx *ctx) {
+    static const bool off = [] { const char *e = std::getenv("DEFTRI_GRAPH"); return e && std::atoi(e) == 0; }();
+    if (off || ctx->trial_graph_failed || ctx->dist() || ctx->S.trsm_fused || profiling()) return false;
+    for (const auto &lv : ctx->L.levels)
+        for (const auto &stp : lv.steps)
+            if (stp.stream != 0) return false;
+    return true;
+}
+
+// enqueue one trial's scatter + factor + solve at lambda (already in ctx->d_lam on the stream's
+// timeline); returns false when the caller must launch the kernels itself
+bool launch_trial_graph(deftri_ctx *ctx) {
+    if (!trial_graph_usable(ctx)) return false;
+    if (!ctx->trial_graph) {
+        hipGraph_t g = nullptr;
+        if (hipStreamBeginCapture(ctx->st, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+            if (std::getenv("DEFTRI_GRAPH_LOG")) std::fprintf(stderr, "[deftri] trial graph: capture refused\n");
+            ctx->trial_graph_failed = true;
+            return false;
+        }
+        launch_scatter(ctx->L, 0.0, ctx->st, ctx->d_lam);
+        launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
+        launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st);
+        hipGraphExec_t ex = nullptr;
+        if (hipStreamEndCapture(ctx->st, &g) != hipSuccess || !g ||
+            hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) {
+            if (g) hipGraphDestroy(g);
+            (void)hipGetLastError();
+            if (std::getenv("DEFTRI_GRAPH_LOG")) std::fprintf(stderr, "[deftri] trial graph: capture failed\n");
+            ctx->trial_graph_failed = true;
+            return false;
+        }
+        hipGraphDestroy(g);
+        ctx->trial_graph = ex;
+        if (std::getenv("DEFTRI_GRAPH_LOG")) std::fprintf(stderr, "[deftri] trial graph captured\n");
+    }
+    return hipGraphLaunch(ctx->trial_graph, ctx->st) == hipSuccess;
+}
+}  // namespace
+
 int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report *rep) {
     if (!ctx || !prm) return DEFTRI_E_ARG;
     if (!ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
@@ -1102,12 +1159,18 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             push_state(ctx);
             hipEventRecord(ctx->ev[2], ctx->st);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
-            launch_scatter(L, lambda, ctx->st);              // setLambda
-            launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
-            hipEventRecord(ctx->ev[3], ctx->st);
-            ctx->hook_x = ctx->d_dx;
-            launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
-            if (ctx->hook_rc) return ctx->hook_rc;
+            ctx->hpin[12] = lambda;                          // pinned: read by the copy at its turn in the stream
+            HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
+            if (launch_trial_graph(ctx)) {
+                hipEventRecord(ctx->ev[3], ctx->st);         // factor + solve in one graph: timed as factor
+            } else {
+                launch_scatter(L, lambda, ctx->st);          // setLambda
+                launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
+                hipEventRecord(ctx->ev[3], ctx->st);
+                ctx->hook_x = ctx->d_dx;
+                launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
+                if (ctx->hook_rc) return ctx->hook_rc;
+            }
             hipEventRecord(ctx->ev[4], ctx->st);
             launch_update_state(P, ctx->d_dx, ctx->st, L.flag);   // _optimizer->update(x) (skipped on a zero pivot)
             double *sc = ctx->hpin + 4;
