@@ -1011,6 +1011,34 @@ int oracle_linearize(const deftri_problem_desc *d, int analytic, double *b, doub
     return 0;
 }
 
+/* The assembled H at the initial linearization as COO triplets (every stored block entry; nnz = 0 on
+   entry asks for the count only).  Test infrastructure (tests/pcg_evidence.py). */
+int oracle_hessian_coo(const deftri_problem_desc *d, int analytic, int64_t *nnz, int64_t *ri, int64_t *ci,
+                       double *v) {
+    problem pb; state s; bsr H;
+    problem_init(&pb, d);
+    state_alloc(&pb, &s);
+    state_from_desc(&pb, &s);
+    bsr_build(&pb, &H);
+    build_system(&pb, &s, &H, analytic);
+    int64_t k = 0;
+    for (int64_t a = 0; a < pb.nv; a++)
+        for (int64_t q = H.rowptr[a]; q < H.rowptr[a + 1]; q++) {
+            int64_t bb = H.col[q];
+            for (int i = 0; i < pb.vdim[a]; i++)
+                for (int j = 0; j < pb.vdim[bb]; j++) {
+                    if (*nnz > 0 && k < *nnz) {
+                        ri[k] = pb.voff[a] + i; ci[k] = pb.voff[bb] + j;
+                        v[k] = H.val[H.valoff[q] + i * pb.vdim[bb] + j];
+                    }
+                    k++;
+                }
+        }
+    *nnz = k;
+    bsr_free(&H); state_free(&s); problem_free(&pb);
+    return 0;
+}
+
 /* Solve (H + lambda I) x = rhs at the initial linearization with the sparse LDL^T. */
 int oracle_damped_solve(const deftri_problem_desc *d, int analytic, double lambda, const double *rhs,
                         double *x) {

@@ -70,6 +70,17 @@ def linearize(prob, analytic=True, dense=False, x=None):
     return b, H, y
 
 
+def hessian_coo(prob, analytic=True):
+    """(rows, cols, vals) of H at the initial linearization, every stored block entry."""
+    d = prob.to_desc()
+    n = C.c_int64(0)
+    lib().oracle_hessian_coo(C.byref(d), C.c_int(1 if analytic else 0), C.byref(n), None, None, None)
+    ri = np.zeros(n.value, np.int64); ci = np.zeros(n.value, np.int64); v = np.zeros(n.value)
+    lib().oracle_hessian_coo(C.byref(d), C.c_int(1 if analytic else 0), C.byref(n), _p(ri, C.c_int64),
+                             _p(ci, C.c_int64), _p(v, C.c_double))
+    return ri, ci, v
+
+
 def damped_solve(prob, lam, rhs, analytic=True):
     d = prob.to_desc()
     x = np.zeros(prob.n_unknowns)

@@ -102,3 +102,45 @@ def test_all_pairs_multi_keyframe(gpu_ctx):
     ref = oracle.solve_lm(p, 5, analytic=False)["report"]
     assert r["trials_total"] == ref["trials_total"]
     np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)
+
+
+def test_all_pairs_eight_keyframes(gpu_ctx):
+    """C3 shape (BASELINE configs[2]: 8 keyframes, all 28 pairs, g2oBundleAdjustment.cc:640-641) at
+    test size against the oracle: identical trials, chi2 per iteration rel 1e-5 (numeric J)."""
+    m, _ = sim.simulate_multi_view(n=100, k=8, seed=11)    # 2624 unknowns: the oracle takes ~6 s
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    assert p.n_pairs == 28
+    gpu_ctx.upload(p)
+    assert gpu_ctx.chi2() == pytest.approx(oracle.chi2(p), rel=1e-11)
+    r = gpu_ctx.solve_lm(2, analytic=False)
+    ref = oracle.solve_lm(p, 2, analytic=False)["report"]
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)
+
+
+def test_all_pairs_eight_keyframes_large(gpu_ctx):
+    """C3 shape at 4000 correspondences x 8 keyframes (beyond the oracle's budget): the damped solve's
+    backward error, monotone accepted chi2, and bit-identical repeated runs."""
+    m, _ = sim.simulate_multi_view(n=4000, k=8, seed=12)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    assert p.n_pairs == 28
+    gpu_ctx.upload(p)
+    b, d = gpu_ctx.gradient()
+    lam = 1e-5 * np.abs(d).max()
+    x = gpu_ctx.damped_solve(lam, b)
+    v = np.random.default_rng(3).normal(size=len(b))
+    for _ in range(30):                                   # ||H + lam I||_2 by power iteration
+        w = gpu_ctx.hessian_product(v) + lam * v
+        v = w / np.linalg.norm(w)
+    norm_a = np.linalg.norm(gpu_ctx.hessian_product(v) + lam * v)
+    res = gpu_ctx.hessian_product(x) + lam * x - b
+    assert np.linalg.norm(res) / (norm_a * np.linalg.norm(x)) < 1e-13
+    gpu_ctx.reset_state()
+    r1 = gpu_ctx.solve_lm(3, analytic=False)
+    p1, _, _ = gpu_ctx.download()
+    chis = [r1["chi2_initial"]] + r1["chi2_iter"]
+    assert all(b_ <= a_ for a_, b_ in zip(chis, chis[1:]))
+    gpu_ctx.reset_state()
+    r2 = gpu_ctx.solve_lm(3, analytic=False)
+    p2, _, _ = gpu_ctx.download()
+    assert r1["chi2_iter"] == r2["chi2_iter"] and np.array_equal(p1, p2)
