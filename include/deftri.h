@@ -182,6 +182,13 @@ int deftri_set_lm_lanes(deftri_ctx *ctx, int32_t lanes);
    g2oTypes.h:341; its analytic one is commented out, g2oTypes.cc:308-331); 1 the closed-form
    Jacobians (an opt-in speed-up, not the reference's arithmetic). */
 int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic);
+/* Arithmetic of the factorization's trailing (Schur-complement) updates: 0 (default) fp64
+   v_mfma_f64_16x16x4, the reference's precision (SimplicialLDLT in double); 1 fp32 products on
+   v_mfma_f32_16x16x4 (operands rounded to fp32, fp32 accumulation per update launch, the result
+   subtracted from the fp64 front), the panel factorizations, TRSM and substitution staying fp64.
+   For the fp32-vs-fp64 sweep of BASELINE config C5 (tests/test_precision_sweep.py);
+   not the reference's arithmetic. */
+int deftri_set_factor_precision(deftri_ctx *ctx, int32_t fp32_updates);
 /* ---- simulated observations (upstream producer, host) --------------------------------------
    SLAM::setCameraPoses + getSimulatedDepthMeasurements + createKeyPoints (Modules/System/SLAM.cc:
    223-338): T1w = (I, c1), T2w = (lookAt(c2, moved[0]), c2) as Sophus SE3f (pose = the fp32 unit

@@ -98,6 +98,7 @@ struct DevPlan {
     int *pflag = nullptr;         // per panel (x lanes): the factorization epoch that last factored it
     double *wbuf = nullptr;       // per panel (x lanes): 64 x 64 TRSM operand W = Linv^T D^{-1} (fused TRSM)
     int nlanes = 1;               // lanes the factor / solve launches cover (blockIdx.y)
+    int f32_update = 0;           // 1: trailing updates on fp32 MFMA (deftri_set_factor_precision)
     LaneOff lo{};
 };
 

@@ -734,8 +734,12 @@ union UpdSmem {
 #endif
 
 // TAIL: the launch carries fused-TRSM tail tiles (a separate instantiation: the tail path's registers
-// would otherwise spill the plain launches' main loop)
-template <bool TAIL>
+// would otherwise spill the plain launches' main loop).  F32 (deftri_set_factor_precision, the
+// fp32-vs-fp64 sweep): the products run on v_mfma_f32_16x16x4 (operands rounded to fp32 at the
+// fragment read, fp32 accumulation over the launch's K columns, the result subtracted from the fp64
+// C tile); its accumulator's row map differs from the f64 instruction's (row = 4 (lane >> 4) + reg).
+typedef float flt4 __attribute__((ext_vector_type(4)));
+template <bool TAIL, bool F32 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_UPD_WPE))) k_update(int ntask, int ntail, const int32_t *__restrict__ tasks, int kA, int kmax,
                                                 int inner, const FrontDev fd, double *__restrict__ arena,
                                                 double *__restrict__ inv, int *__restrict__ flag,
@@ -780,8 +784,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         *(dbl2 *)&sm.st.Q[buf][sk][sr + 2] = qv1;
     };
     stage_load(0);
-    // C tile: acc layout (a, b, g) -> column cb + 16a + kl + 4g, row rb + 16b + il.  Plain launches
+    // C tile: acc layout (a, b, g) -> column cb + ccol(a, g), row rb + 16b + il.  Plain launches
     // fetch it before the K loop; TAIL launches during the last chunk (registers)
+    auto ccol = [&](int a, int g) { return 16 * a + (F32 ? 4 * kl + g : kl + 4 * g); };
     double cv[2][2][4];
     auto load_c = [&]() {
 #pragma unroll
@@ -790,16 +795,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             for (int b = 0; b < 2; b++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    int c = cb + ccol(a, g), r = rb + 16 * b + il;
                     cv[a][b][g] = (c < m && r < m) ? F[(int64_t)c * m + r] : 0.0;
                 }
     };
     if (!TAIL) load_c();
     dbl4 acc[2][2];
+    flt4 accf[2][2];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int b = 0; b < 2; b++) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < 2; b++) { acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0}; accf[a][b] = flt4{0.f, 0.f, 0.f, 0.f}; }
     stage_store(0);
     __syncthreads();
     auto mfma_chunk = [&](int buf) {
@@ -807,10 +813,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         for (int k4 = 0; k4 < kUpdKC; k4 += 4) {
             const double p0 = sm.st.P[buf][k4 + kl][pc + il], p1 = sm.st.P[buf][k4 + kl][pc + 16 + il];
             const double q0 = sm.st.Q[buf][k4 + kl][qr + il], q1 = sm.st.Q[buf][k4 + kl][qr + 16 + il];
-            acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
+            if constexpr (F32) {
+                const float p0f = (float)p0, p1f = (float)p1, q0f = (float)q0, q1f = (float)q1;
+                accf[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p0f, q0f, accf[0][0], 0, 0, 0);
+                accf[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p0f, q1f, accf[0][1], 0, 0, 0);
+                accf[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p1f, q0f, accf[1][0], 0, 0, 0);
+                accf[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p1f, q1f, accf[1][1], 0, 0, 0);
+            } else {
+                acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, q1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, q1, acc[1][1], 0, 0, 0);
+            }
         }
     };
     const int nch = (K + kUpdKC - 1) / kUpdKC;
@@ -833,6 +847,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             __syncthreads();
         }
     }
+    if constexpr (F32) {
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) acc[a][b][g] = (double)accf[a][b][g];
+    }
     // fused TRSM tile (i > k1, k1) of the panel this launch factors: the updated tile goes to LDS
     // (columns past the panel, if any, are stored as plain update results), then, once the panel's
     // factorization is published, its rows are solved in place
@@ -844,7 +866,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             for (int b = 0; b < 2; b++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const int cl = cb - tj + 16 * a + kl + 4 * g, rl = rb - ti + 16 * b + il;
+                    const int cl = cb - tj + ccol(a, g), rl = rb - ti + 16 * b + il;
                     const double v = cv[a][b][g] - acc[a][b][g];
                     if (cl < kb) sm.S[cl][rl] = v;
                     else if (tj + cl < cend && ti + rl < m) F[(int64_t)(tj + cl) * m + ti + rl] = v;
@@ -867,7 +889,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             for (int b = 0; b < 2; b++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    int c = cb + ccol(a, g), r = rb + 16 * b + il;
                     if (c < m && r < m && r >= c) Fp[(int64_t)bm[c] * mp + bm[r]] += cv[a][b][g] - acc[a][b][g];
                 }
     } else {
@@ -877,7 +899,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             for (int b = 0; b < 2; b++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    int c = cb + 16 * a + kl + 4 * g, r = rb + 16 * b + il;
+                    int c = cb + ccol(a, g), r = rb + 16 * b + il;
                     if (c < cend && r < m) F[(int64_t)c * m + r] = cv[a][b][g] - acc[a][b][g];
                 }
     }
@@ -1410,7 +1432,7 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
                     hipEventRecord(e, st);
                     hipStreamWaitEvent(side, e, 0);
                     g_work = stp.upd_flops;
-                    LAUNCH("update", stp.ntail ? dev::k_update<true> : dev::k_update<false>, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), side, stp.nupd,
+                    LAUNCH("update", (stp.ntail ? dev::k_update<true> : L.f32_update ? dev::k_update<false, true> : dev::k_update<false>), dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), side, stp.nupd,
                            stp.ntail, L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd, L.arena, L.inv,
                            L.flag, L.pflag, L.wbuf, epoch, L.lo);
                     cur_side = ev[evi++ % nev];
@@ -1422,7 +1444,7 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
             if (stp.wait_side == 2 && cur_side) hipStreamWaitEvent(st, cur_side, 0);
             if (stp.nupd > 0) {
                 g_work = stp.upd_flops;
-                LAUNCH("update", stp.ntail ? dev::k_update<true> : dev::k_update<false>, dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), st, stp.nupd,
+                LAUNCH("update", (stp.ntail ? dev::k_update<true> : L.f32_update ? dev::k_update<false, true> : dev::k_update<false>), dim3(8 * nb(stp.nupd, 8), L.nlanes), dim3(256), st, stp.nupd,
                        stp.ntail, L.tasks + 3 * stp.upd_off, stp.kA, stp.kmax, stp.inner, L.fd,
                        L.arena, L.inv, L.flag, L.pflag, L.wbuf, epoch, L.lo);
             }

@@ -115,6 +115,7 @@ struct deftri_ctx {
     int analytic_jac = 0;                   // deftri_arap_optimization: 0 g2o numeric (reference), 1 analytic
     bool prof_analytic = false;             // deftri_profile_trial linearizes like the last solve_lm
     int max_lanes = 0;                      // 0: default (DEFTRI_LM_LANES, else by factorization size)
+    int f32_update = 0;                     // deftri_set_factor_precision
     std::vector<Lane> lanes;                // device buffers: per uploaded problem
     DevPlan LB;                             // batched plan view: lanes' arenas / inverses / vectors / flags
     double *dx_lanes = nullptr;             // [lane][ndof]
@@ -420,6 +421,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     if ((rc = dalloc(ctx, &L.flag, 1))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_lam, 1))) return rc;
     L.npanels = S.npanels;
+    L.f32_update = ctx->f32_update;
     if ((rc = dalloc(ctx, &L.pflag, std::max<int64_t>(S.npanels, 1)))) return rc;
     HIPOK(hipMemset(L.pflag, 0, sizeof(int) * (size_t)std::max<int64_t>(S.npanels, 1)));
     if (S.trsm_fused && (rc = dalloc(ctx, &L.wbuf, 4096 * std::max<int64_t>(S.npanels, 1)))) return rc;   // else nullptr: no W
@@ -776,6 +778,15 @@ const char *deftri_last_error(const deftri_ctx *ctx) { return ctx ? ctx->err.c_s
 int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic) {
     if (!ctx || analytic < 0 || analytic > 1) return DEFTRI_E_ARG;
     ctx->analytic_jac = analytic;
+    return 0;
+}
+
+int deftri_set_factor_precision(deftri_ctx *ctx, int32_t fp32_updates) {
+    if (!ctx || fp32_updates < 0 || fp32_updates > 1) return DEFTRI_E_ARG;
+    ctx->f32_update = fp32_updates;
+    ctx->L.f32_update = fp32_updates;
+    ctx->LB.f32_update = fp32_updates;
+    drop_trial_graph(ctx);                 // the captured trial holds the previous kernel choice
     return 0;
 }
 

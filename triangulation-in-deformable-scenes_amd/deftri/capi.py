@@ -45,6 +45,7 @@ def load():
         "deftri_solve_lm": (C.c_int, [C.c_void_p, P(_abi.LMParams), P(_abi.Report)]),
         "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_set_jacobian_mode": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_set_factor_precision": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
         "deftri_triangulate_nrslam": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float),
                                                 P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float),
@@ -111,7 +112,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_set_factor_precision", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_graph_point_ids", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -228,6 +229,10 @@ class Context:
         x = np.zeros_like(bq)
         self._check(self.lib.deftri_debug_plan_solve_dist(self.h, _dp(Hq), float(lam), _dp(bq), _dp(x), len(bq)))
         return x
+
+    def set_factor_precision(self, fp32_updates):
+        """1: trailing updates on fp32 MFMA (the C5 precision sweep); 0: fp64 (default, the reference's)."""
+        self._check(self.lib.deftri_set_factor_precision(self.h, 1 if fp32_updates else 0))
 
     def set_lm_lanes(self, lanes):
         """Speculative lambda lanes (0 = default, 1 = sequential trials); results are identical."""
