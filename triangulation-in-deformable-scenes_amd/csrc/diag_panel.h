@@ -300,20 +300,24 @@ __device__ __forceinline__ void diag_block_v2(double (*S)[DP], int kb, int nrows
 // tail_rows (the fused-TRSM plan) also the TRSM of the remaining rows of the 64-row diagonal tile
 // (rows k0+kb .. min(m, k0+64)), so the row tiles start at k0+64.  Without it (measured faster:
 // partial panels then need only nsub sub-panels) k_trsm solves rows k0+kb..
+// from_lds: the caller (k_update's diagonal-tile workgroup) already holds the block in S — lower
+// kb x kb triangle, zero upper triangle, identity padding — so it skips the global round trip
 __device__ __forceinline__ void diag_panel_v2(double *F, int m, int s, int k0, double *Li, double (*S)[DP], int *flag,
-                                              bool tail_rows) {
+                                              bool tail_rows, bool from_lds = false) {
     const int kb = min(64, s - k0), mt = tail_rows ? min(64, m - k0) : kb;
     T2MARK(0);
-    double v[16];
+    if (!from_lds) {
+        double v[16];
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        v[q] = (r < mt && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
-    }
+        for (int q = 0; q < 16; q++) {
+            int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+            v[q] = (r < mt && c < kb && r >= c) ? F[(int64_t)(k0 + c) * m + k0 + r] : ((r == c && r >= kb) ? 1.0 : 0.0);
+        }
 #pragma unroll
-    for (int q = 0; q < 16; q++) {
-        int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
-        S[r][c] = v[q];
+        for (int q = 0; q < 16; q++) {
+            int idx = threadIdx.x + 256 * q, c = idx >> 6, r = idx & 63;
+            S[r][c] = v[q];
+        }
     }
     __syncthreads();
     diag_block_v2(S, kb, mt, flag);

@@ -892,6 +892,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
                     int c = cb + ccol(a, g), r = rb + 16 * b + il;
                     if (c < m && r < m && r >= c) Fp[(int64_t)bm[c] * mp + bm[r]] += cv[a][b][g] - acc[a][b][g];
                 }
+    } else if (!TAIL && ti == tj && ti == kA + K && s > kA + K) {
+        // the tile that carries the next panel's factorization: its kb x kb diagonal block goes
+        // straight into the factorization's LDS layout (lower triangle, zero upper, identity
+        // padding), the rest of the tile to the front
+        const int kb = min(64, s - (kA + K));
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int cl = cb - tj + ccol(a, g), rl = rb - ti + 16 * b + il;
+                    const double v = cv[a][b][g] - acc[a][b][g];
+                    if (cl < kb && rl < kb) {
+                        sm.S[rl][cl] = (rl >= cl) ? v : 0.0;
+                    } else {
+                        sm.S[rl][cl] = (rl == cl) ? 1.0 : 0.0;
+                        if (tj + cl < cend && ti + rl < m) F[(int64_t)(tj + cl) * m + ti + rl] = v;
+                    }
+                }
     } else {
 #pragma unroll
         for (int a = 0; a < 2; a++)
@@ -910,7 +930,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     if (ti == tj && ti == k1 && s > k1) {
         __syncthreads();
         __threadfence_block();
-        diag_panel_v2(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, flag, TAIL);
+        diag_panel_v2(F, m, s, k1, inv + fd.inv_off[f] + (int64_t)(k1 / 64) * 4096, sm.S, flag, TAIL, !TAIL);
         if (TAIL) {
             const int pid = fd.panel_off[f] + k1 / 64;
             publish_panel(sm.S, min(64, s - k1), wbuf + (int64_t)pid * 4096, pflag + pid, epoch);

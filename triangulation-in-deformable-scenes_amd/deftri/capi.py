@@ -101,7 +101,10 @@ def load():
         "deftri_ba_profile_trial": (C.c_int, [C.c_void_p, C.c_double, P(_abi.KernelStat), C.c_int32,
                                               P(C.c_int32)]),
     }
+    dev_build = "DEFTRI_LIB" in os.environ          # an older build under A/B may lack newer entry points
     for name, (res, args) in sig.items():
+        if dev_build and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
