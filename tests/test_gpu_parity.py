@@ -167,7 +167,11 @@ def test_profile_trial_reports_kernels(gpu_ctx, golden_cases):
     st = gpu_ctx.profile_trial(1e3)
     # the panel TRSM has its own launches unless DEFTRI_TRSM_FUSE=1 folds them into diag / update
     fused = os.environ.get("DEFTRI_TRSM_FUSE") == "1"
-    for k in ("lin_arap", "hchunk", "scatter", "diag", "update", "fwd_step", "bwd_step") + (() if fused else ("trsm",)):
+    for k in ("lin_arap", "hchunk", "scatter", "diag", "update") + (() if fused else ("trsm",)):
+        assert k in st and st[k]["launches"] > 0
+    # substitution: one chained launch per level and direction, or per-panel steps (DEFTRI_SOLVE_CHAIN=0)
+    chain = os.environ.get("DEFTRI_SOLVE_CHAIN") != "0"
+    for k in (("fwd_chain", "bwd_chain") if chain else ("fwd_step", "bwd_step")):
         assert k in st and st[k]["launches"] > 0
     assert st["update"]["flops"] > 0
 

@@ -46,6 +46,8 @@ struct LevelDev {
     struct SolveStep { int64_t off; int32_t n; };
     std::vector<SolveStep> fsteps, bsteps;
     int64_t bgemv_off; int32_t nbgemv;
+    int64_t fchain_off; int32_t nfchain;
+    int64_t bchain_off; int32_t nbchain;
 };
 
 // batched LM trials ("lambda lanes"): every factor/solve launch carries a second grid dimension,

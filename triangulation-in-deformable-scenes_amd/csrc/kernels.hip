@@ -1133,6 +1133,170 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
     if (part == 0) w[q0 + lane] -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
+// ---- chained substitution: one launch per level and direction.  The per-panel launches above
+// become cross-workgroup hand-offs inside one launch (the protocol of the fused TRSM: agent-coherent
+// stores of the panel's 64-entry result, an epoch flag, bounded polls).  A workgroup only waits on
+// workgroups with smaller indices (forward: row tiles in ascending order, backward: column tiles in
+// descending order), so in-order dispatch guarantees progress.  Per row / column the arithmetic is
+// k_fwd_step's / k_bwd_step's (same products, same reduction order): bit-identical results.
+__device__ __forceinline__ void poll_flag(const int *pf, int epoch, int *flag) {
+    if (threadIdx.x == 0) {
+        int it = 0;
+        while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            if (++it > kSpinLimit) { atomicOr(flag, kStatusWaitTimeout); break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ void raise_flag(int *pf, int epoch) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): this thread's coherent stores are complete
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(pf, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// forward: task (front f, rows r0..r0+63).  Panels k0 < min(r0, s): wait for y_k0, v_rows -= L y;
+// then, if r0 < s, the tile's own panel: y = L_pp^{-1} v_p, published (coherent) in yvec, and the
+// tile's rows below the panel (r >= s when the panel is partial) take its update too.
+__global__ void __launch_bounds__(256) k_fwd_chain(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                   const double *__restrict__ arena, const double *__restrict__ inv,
+                                                   double *__restrict__ vec, double *__restrict__ yvec,
+                                                   int *__restrict__ pflag, int epoch, int *__restrict__ flag,
+                                                   const LaneOff lo) {
+    __shared__ double vs[64];
+    __shared__ double ys[64];
+    __shared__ double red[4][64];
+    const int t = blockIdx.x;
+    if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; vec += blockIdx.y * lo.vec; yvec += blockIdx.y * lo.vec;
+    pflag += blockIdx.y * lo.pflag; flag += blockIdx.y;
+    const int f = tasks[3 * t], r0 = tasks[3 * t + 1];
+    const int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    double *v = vec + fd.vec_off[f];
+    double *yv = yvec + fd.vec_off[f];
+    const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const int r = r0 + lane;
+    double vr = (part == 0 && r < m) ? v[r] : 0.0;
+    const int kend = min(r0, s);
+    for (int k0 = 0; k0 < kend; k0 += 64) {
+        const int kb = min(64, s - k0);
+        double fv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int j = part + 4 * q;
+            fv[q] = (r < m && j < kb) ? F[(int64_t)(k0 + j) * m + r] : 0.0;    // issued before the wait
+        }
+        poll_flag(pflag + fd.panel_off[f] + k0 / 64, epoch, flag);
+        if (threadIdx.x < 64) ys[threadIdx.x] = threadIdx.x < kb ? ld_coherent(yv + k0 + threadIdx.x) : 0.0;
+        __syncthreads();
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc += fv[q] * ys[part + 4 * q];
+        red[part][lane] = acc;
+        __syncthreads();
+        if (part == 0) vr -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        __syncthreads();
+    }
+    if (r0 < s) {
+        const int kb = min(64, s - r0);
+        const double *Li = inv + fd.inv_off[f] + (int64_t)(r0 / 64) * 4096;
+        double li[16], fv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int j = part + 4 * q;
+            li[q] = (j <= lane && lane < kb) ? Li[(int64_t)j * kb + lane] : 0.0;
+            fv[q] = (lane >= kb && r < m && j < kb) ? F[(int64_t)(r0 + j) * m + r] : 0.0;
+        }
+        if (part == 0) vs[lane] = lane < kb ? vr : 0.0;
+        __syncthreads();
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc += li[q] * vs[part + 4 * q];
+        red[part][lane] = acc;
+        __syncthreads();
+        if (threadIdx.x < 64) ys[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        __syncthreads();
+        if (threadIdx.x < kb) st_coherent(yv + r0 + threadIdx.x, ys[threadIdx.x]);
+        raise_flag(pflag + fd.panel_off[f] + r0 / 64, epoch);
+        if (kb < 64) {                                     // rows s.. of this tile: this panel's update
+            acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) acc += fv[q] * ys[part + 4 * q];
+            red[part][lane] = acc;
+            __syncthreads();
+            if (part == 0 && lane >= kb) vr -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        }
+    }
+    if (part == 0 && r < m && r >= s) v[r] = vr;           // the contribution rows the parent gathers
+}
+
+// backward: task (front f, own columns c0..c0+63), after k_bwd_init.  Panels k0 > c0, descending:
+// wait for x_k0, w_cols -= L[panel rows, cols]^T x; then the tile's own panel: x = L_pp^{-T} w_p,
+// published (coherent) in yvec (whose y this level's k_bwd_init has consumed) and scattered to x.
+__global__ void __launch_bounds__(256) k_bwd_chain(int ntask, const int32_t *__restrict__ tasks, const FrontDev fd,
+                                                   const double *__restrict__ arena, const double *__restrict__ inv,
+                                                   double *__restrict__ vec, double *__restrict__ yvec,
+                                                   double *__restrict__ x, int *__restrict__ pflag, int epoch,
+                                                   int *__restrict__ flag, const LaneOff lo) {
+    __shared__ double ws[64];
+    __shared__ double xs[64];
+    __shared__ double red[4][64];
+    const int t = blockIdx.x;
+    if (t >= ntask) return;
+    arena += blockIdx.y * lo.arena; inv += blockIdx.y * lo.inv; vec += blockIdx.y * lo.vec; yvec += blockIdx.y * lo.vec;
+    x += blockIdx.y * lo.x; pflag += blockIdx.y * lo.pflag; flag += blockIdx.y;
+    const int f = tasks[3 * t], c0 = tasks[3 * t + 1];
+    const int m = fd.m[f], s = fd.s[f];
+    const double *F = arena + fd.arena_off[f];
+    const double *w = vec + fd.vec_off[f];
+    double *yv = yvec + fd.vec_off[f];
+    const int lane = threadIdx.x & 63, part = threadIdx.x >> 6;
+    const int kbq = min(64, s - c0);
+    double wq = (part == 0 && lane < kbq) ? w[c0 + lane] : 0.0;
+    const double *Fq = F + (int64_t)(c0 + lane) * m;
+    for (int k0 = ((s - 1) / 64) * 64; k0 > c0; k0 -= 64) {
+        const int kb = min(64, s - k0);
+        double fv[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const int j = part + 4 * q;
+            fv[q] = (j < kb) ? Fq[k0 + j] : 0.0;                            // L[k0+j][c0+lane]
+        }
+        poll_flag(pflag + fd.panel_off[f] + k0 / 64, epoch, flag);
+        if (threadIdx.x < 64) xs[threadIdx.x] = threadIdx.x < kb ? ld_coherent(yv + k0 + threadIdx.x) : 0.0;
+        __syncthreads();
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) acc += fv[q] * xs[part + 4 * q];
+        red[part][lane] = acc;
+        __syncthreads();
+        if (part == 0) wq -= (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        __syncthreads();
+    }
+    const double *Li = inv + fd.inv_off[f] + (int64_t)(c0 / 64) * 4096;
+    double lv[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        const int j = part + 4 * q;
+        lv[q] = (lane < kbq && j < kbq && j >= lane) ? Li[(int64_t)lane * kbq + j] : 0.0;   // Linv[j][lane]
+    }
+    if (part == 0) ws[lane] = wq;
+    __syncthreads();
+    double acc = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) acc += lv[q] * ws[part + 4 * q];
+    red[part][lane] = acc;
+    __syncthreads();
+    if (threadIdx.x < 64) xs[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    __syncthreads();
+    if (threadIdx.x < kbq) {
+        st_coherent(yv + c0 + threadIdx.x, xs[threadIdx.x]);
+        x[fd.rows[fd.rows_off[f] + c0 + threadIdx.x]] = xs[threadIdx.x];
+    }
+    raise_flag(pflag + fd.panel_off[f] + c0 / 64, epoch);
+}
+
 // ------------------------------------------------------------------------------------------
 // state update, reductions
 // ------------------------------------------------------------------------------------------
@@ -1417,12 +1581,17 @@ void launch_scatter(const DevPlan &L, double lambda, hipStream_t st, const doubl
     launch_scatter_lanes(one, st, lam_dev);
 }
 
+// a fresh epoch per factorization / substitution: the panel flags never need clearing
+static std::atomic<int> g_epoch{16};      // factorization epochs start past the substitution's fixed 1 / 2
+static int next_epoch() {
+    int e = ++g_epoch;
+    if (e <= 16) { g_epoch = 17; e = 17; }
+    return e;
+}
+
 void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_t *ev, int nev, LevelHook hook,
                    void *hook_user) {
-    // a fresh epoch per factorization: the panel flags never need clearing
-    static std::atomic<int> g_epoch{0};
-    int epoch = ++g_epoch;
-    if (epoch <= 0) { g_epoch = 1; epoch = 1; }
+    const int epoch = next_epoch();
     int evi = 0;
     hipEvent_t prev_side = nullptr, cur_side = nullptr;   // events of the last two side-stream updates
     for (size_t h = 0; h < L.levels.size(); h++) {
@@ -1478,6 +1647,16 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
 
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st, const double *bpart,
                   LevelHook hook, void *hook_user) {
+    // chained substitution (one launch per level and direction) unless DEFTRI_SOLVE_CHAIN=0
+    static const bool chain = [] { const char *e = std::getenv("DEFTRI_SOLVE_CHAIN"); return !(e && std::atoi(e) == 0); }();
+    const bool ch = chain && L.pflag != nullptr;
+    // the flags are cleared per substitution and the epochs fixed (1 forward, 2 backward), so a
+    // captured trial graph replays correctly
+    const int fe = 1, be = 2;
+    if (ch) {
+        const int64_t span = (L.nlanes > 1 ? (int64_t)(L.nlanes - 1) * L.lo.pflag : 0) + std::max<int64_t>(L.npanels, 1);
+        hipMemsetAsync(L.pflag, 0, sizeof(int) * (size_t)span, st);
+    }
     for (size_t h = 0; h < L.levels.size(); h++) {
         const auto &lv = L.levels[h];
         g_level = (int)h;
@@ -1485,6 +1664,12 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
         if (lv.nfwd > 0)
             LAUNCH("fwd_gather", dev::k_fwd_gather, dim3(lv.nfwd, L.nlanes), dim3(256), st, lv.nfwd,
                    L.tasks + 3 * lv.fwd_off, L.fd, rhs, bpart, L.vec, L.lo);
+        if (ch) {
+            if (lv.nfchain > 0)
+                LAUNCH("fwd_chain", dev::k_fwd_chain, dim3(lv.nfchain, L.nlanes), dim3(256), st, lv.nfchain,
+                       L.tasks + 3 * lv.fchain_off, L.fd, L.arena, L.inv, L.vec, L.yvec, L.pflag, fe, L.flag, L.lo);
+            continue;
+        }
         for (const auto &sp : lv.fsteps)
             if (sp.n > 0)
                 LAUNCH("fwd_step", dev::k_fwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
@@ -1496,10 +1681,16 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
         if (lv.nbgemv > 0)
             LAUNCH("bwd_init", dev::k_bwd_init, dim3(lv.nbgemv, L.nlanes), dim3(256), st, lv.nbgemv,
                    L.tasks + 3 * lv.bgemv_off, L.fd, L.arena, x, L.yvec, L.vec, L.lo);
-        for (const auto &sp : lv.bsteps)
-            if (sp.n > 0)
-                LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
-                       L.fd, L.arena, L.inv, L.vec, x, L.lo);
+        if (ch) {
+            if (lv.nbchain > 0)
+                LAUNCH("bwd_chain", dev::k_bwd_chain, dim3(lv.nbchain, L.nlanes), dim3(256), st, lv.nbchain,
+                       L.tasks + 3 * lv.bchain_off, L.fd, L.arena, L.inv, L.vec, L.yvec, x, L.pflag, be, L.flag, L.lo);
+        } else {
+            for (const auto &sp : lv.bsteps)
+                if (sp.n > 0)
+                    LAUNCH("bwd_step", dev::k_bwd_step, dim3(sp.n, L.nlanes), dim3(256), st, sp.n, L.tasks + 3 * sp.off,
+                           L.fd, L.arena, L.inv, L.vec, x, L.lo);
+        }
         if (hook) hook(hook_user, kHookBackward, (int)hh);   // boundary solutions down to other ranks
     }
 }

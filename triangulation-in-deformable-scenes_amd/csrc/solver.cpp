@@ -416,6 +416,8 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
         for (const auto &x : lv.fsteps) ld.fsteps.push_back({x.off, x.n});
         for (const auto &x : lv.bsteps) ld.bsteps.push_back({x.off, x.n});
         ld.bgemv_off = lv.bgemv_off; ld.nbgemv = lv.nbgemv;
+        ld.fchain_off = lv.fchain_off; ld.nfchain = lv.nfchain;
+        ld.bchain_off = lv.bchain_off; ld.nbchain = lv.nbchain;
         L.levels.push_back(ld);
     }
     if ((rc = dalloc(ctx, &L.flag, 1))) return rc;

@@ -906,6 +906,17 @@ struct Builder {
                 }
                 LT.fsteps.push_back(st);
             }
+            LT.fchain_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t f : fs) {
+                const Front &F = S.fronts[f];
+                for (int32_t r0 = 0; r0 < F.m; r0 += 64) { push3(f, r0, 0); LT.nfchain++; }
+            }
+            LT.bchain_off = (int64_t)S.task_i32.size() / 3;
+            for (int32_t f : fs) {
+                const Front &F = S.fronts[f];
+                if (F.s <= 0) continue;
+                for (int32_t c0 = ((F.s - 1) / 64) * 64; c0 >= 0; c0 -= 64) { push3(f, c0, 0); LT.nbchain++; }
+            }
             LT.bgemv_off = (int64_t)S.task_i32.size() / 3;
             for (int32_t f : fs) {
                 const Front &F = S.fronts[f];

@@ -159,6 +159,12 @@ struct Symbolic {
         struct SolveStep { int64_t off = 0; int32_t n = 0; };
         std::vector<SolveStep> fsteps, bsteps;                 // bsteps: already in execution order
         int64_t bgemv_off = 0; int32_t nbgemv = 0;             // (front, c0) backward init, 16 columns each
+        // chained substitution (one launch per level and direction, k_fwd_chain / k_bwd_chain):
+        // forward (front, r0) row tiles of 64 in ascending r0 per front — each waits for the panels
+        // above it, applies them, and publishes its own panel's y; backward (front, c0) own-column
+        // tiles in descending c0 per front — each waits for the panels after it and publishes x
+        int64_t fchain_off = 0; int32_t nfchain = 0;
+        int64_t bchain_off = 0; int32_t nbchain = 0;
     };
     std::vector<LevelTasks> levels;
     std::vector<int32_t> task_i32;     // flat task storage (3 ints per task record)
