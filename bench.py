@@ -49,6 +49,7 @@ import numpy as np  # noqa: E402
 from deftri import capi, sim  # noqa: E402
 
 FP64_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.29 TB/s measured copy)
 MFMA_F64_SUSTAINED_TFLOPS = 48.3   # v_mfma_f64_16x16x4 back-to-back on this box (tools/micro/mfma_f64_peak.hip)
 BASELINE_METRIC = "LM iterations/sec + ms/iter at 100k corr \u00d7 2 views; 1/2/4/8-GPU scaling"
 REP_W, ARAP_W, DEPTH_SIGMA = 1.0, 2e5, np.float32(3.0 / 1000.0)
@@ -247,6 +248,8 @@ def main():
     ap.add_argument("--ba-scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--lanes", type=int, default=0,
                     help="speculative LM lambda lanes (0: library default, 1: sequential trials)")
+    ap.add_argument("--solver", choices=["pcg", "direct"], default="pcg",
+                    help="LM step solver: block-Jacobi PCG with LDL^T fallback (library default) or the LDL^T")
     ap.add_argument("--analytic", action="store_true",
                     help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
     ap.add_argument("--replicas", action="store_true",
@@ -290,6 +293,7 @@ def main():
     t0 = time.perf_counter()
     ctx.upload(prob)
     ctx.set_lm_lanes(args.lanes)
+    ctx.set_linear_solver(args.solver)
     log(f"[rank {rank}] upload + symbolic analysis {time.perf_counter() - t0:.1f}s")
     analytic = args.analytic
 
@@ -321,7 +325,29 @@ def main():
     # profiled trial (HIP events on the solver stream), at the final lambda of the timed run
     # (a collective on a sharded context: each rank times its own part of the same trial)
     stats = ctx.profile_trial(rep["lambda_final"])
-    upd = stats["update"]
+    pcg_prof = None
+    if "pcg_product" in stats:
+        # PCG steps: the dominant kernel is the product (HBM-bound row gathers); the factorization's
+        # update kernel is profiled too (fallback path, and the direct solver's roofline)
+        pp = stats["pcg_product"]
+        its = max(pp["launches"] - 1, 1)           # the last launch only runs the convergence test
+        gbs = pp["bytes"] / max(pp["ms"] * 1e-3, 1e-12) / 1e9
+        pcg_prof = {"bound": "hbm", "kernel": "k_pcg_product", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                    "traffic_unit": "bytes per launch", "bytes_per_launch": pp["bytes"] / its,
+                    "launches": pp["launches"], "avg_launch_us": round(1e3 * pp["ms"] / max(pp["launches"], 1), 3),
+                    "cg_iterations": its, "lambda": rep["lambda_final"], "rank": rank}
+        pmcp = sorted(ROOT.glob("profiles/*_pmc_pcg_product.json"))
+        if pmcp and not sharded:
+            pj = json.loads(pmcp[-1].read_text())
+            if abs(pj.get("bytes_per_launch_algorithmic", -1) - pcg_prof["bytes_per_launch"]) < 1e-6 * pcg_prof["bytes_per_launch"]:
+                pcg_prof["traffic"] = pj["traffic_bytes_per_launch"]
+        ctx.set_linear_solver("direct")
+        stats_f = ctx.profile_trial(rep["lambda_final"])
+        ctx.set_linear_solver(args.solver)
+    else:
+        stats_f = stats
+    upd = stats_f["update"]
     factor_flops = rep["factor_flops_total"] if sharded else rep["factor_flops"]
     achieved = upd["flops"] / (upd["ms"] * 1e-3) / 1e12
     # HBM bytes of k_update per factorization from the committed rocprofv3 PMC pass (tools/gpu_pmc.sh +
@@ -332,14 +358,16 @@ def main():
         pj = json.loads(pmc[-1].read_text())
         if abs(pj.get("update_flops_per_factorization", -1) - upd["flops"]) < 1e-6 * upd["flops"]:
             traffic = pj["traffic_bytes_per_factorization"]
-    roofline = {"bound": "mfma", "kernel": "k_update", "achieved": round(achieved, 3),
+    roofline_f = {"bound": "mfma", "kernel": "k_update", "achieved": round(achieved, 3),
                 "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
                 "peak_sustained_measured": MFMA_F64_SUSTAINED_TFLOPS,
                 "traffic": traffic, "traffic_unit": "bytes per factorization (all k_update launches)",
                 "launches": upd["launches"],
                 "avg_launch_us": round(1e3 * upd["ms"] / max(upd["launches"], 1), 3),
                 "flops_per_factorization": upd["flops"], "rank": rank}
+    roofline = pcg_prof if pcg_prof else roofline_f
     trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
+    factor_trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats_f.items(), key=lambda kv: -kv[1]["ms"])}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -370,13 +398,19 @@ def main():
                        "trials_per_iteration": round(trials_per_it, 3),
                        "ms_per_trial": round(ms_per_step / max(trials_per_it, 1e-9), 3),
                        "lm_lanes": rep["lanes"],
+                       "step_solver": args.solver if not sharded else "direct (point-sharded LDL^T)",
+                       "pcg_trials": rep["pcg_trials"], "pcg_fallbacks": rep["pcg_fallbacks"],
+                       "cg_iterations_per_pcg_trial": round(rep["pcg_iterations"] / max(rep["pcg_trials"], 1), 2),
                        "trials_executed_per_iteration": round(rep["trials_executed"] / max(iters, 1), 3),
                        "parallelism": (f"points{world}" if sharded else f"replicas{world}") if world > 1 else "single"},
             "roofline": roofline,
+            "roofline_factorization": roofline_f if pcg_prof else None,
             "cpu_baseline": cpu,
             "breakdown_ms": {"total": rep["ms_total"], "linearize": rep["ms_linearize"],
-                             "factor": rep["ms_factor"], "solve": rep["ms_solve"], "update": rep["ms_update"]},
+                             "factor": rep["ms_factor"], "solve": rep["ms_solve"], "update": rep["ms_update"],
+                             "pcg": rep["ms_pcg"]},
             "trial_kernel_ms": trial_ms,
+            "factorization_trial_kernel_ms": factor_trial_ms if pcg_prof else None,
             "end_to_end_arap_optimization": e2e,
         }
         print(json.dumps(out), flush=True)

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 2
+#define DEFTRI_ABI_VERSION 3
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -150,6 +150,13 @@ typedef struct deftri_report {
     /* uploads on this context that found the same structure (index arrays and counts) as the
        analysed plan and only copied the values (no ordering / symbolic analysis / plan upload) */
     int64_t plan_reuses;
+    /* PCG steps (deftri_set_linear_solver): trials solved by PCG, their CG iterations, trials that
+       fell back to the factorization, and the device time of the PCG solves (ms, host-timed around
+       the solve's final synchronization) */
+    int32_t pcg_trials;
+    int32_t pcg_fallbacks;
+    int64_t pcg_iterations;
+    double  ms_pcg;
 } deftri_report;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -189,6 +196,20 @@ int deftri_set_jacobian_mode(deftri_ctx *ctx, int32_t analytic);
    For the fp32-vs-fp64 sweep of BASELINE config C5 (tests/test_precision_sweep.py);
    not the reference's arithmetic. */
 int deftri_set_factor_precision(deftri_ctx *ctx, int32_t fp32_updates);
+/* Linear solver of the LM step (H + lambda I) dx = b inside deftri_solve_lm /
+   deftri_arap_optimization (the reference: g2o BlockSolver + LinearSolverEigen, an exact sparse
+   LDL^T).  DEFTRI_SOLVER_PCG (default): conjugate gradients preconditioned by the vertex blocks of
+   H + lambda I (6x6 T_g, 1x1 scale, 3x3 point), stopped at ||b - A dx|| <= tol ||b|| (tol <= 0:
+   1e-12), with the multifrontal LDL^T as the fallback for a solve that has not converged after
+   max_iterations or breaks down.  max_iterations <= 0: a budget of about one factorization's cost,
+   from the plan's sizes (deterministic per problem structure; ~70 at 100k correspondences, ~25 for
+   a few hundred points).  Single-rank contexts only (point-sharded contexts always factor).  DEFTRI_SOLVER_DIRECT: the multifrontal LDL^T for every trial. */
+#define DEFTRI_SOLVER_DIRECT 0
+#define DEFTRI_SOLVER_PCG    1
+int deftri_set_linear_solver(deftri_ctx *ctx, int32_t solver, double tol, int32_t max_iterations);
+/* The last PCG step of this context (solve_lm trial or eval_damped_solve): CG iterations and
+   whether it converged (0: the LDL^T solved that step). */
+int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_t *pcg_converged);
 /* ---- simulated observations (upstream producer, host) --------------------------------------
    SLAM::setCameraPoses + getSimulatedDepthMeasurements + createKeyPoints (Modules/System/SLAM.cc:
    223-338): T1w = (I, c1), T2w = (lookAt(c2, moved[0]), c2) as Sophus SE3f (pose = the fp32 unit
@@ -250,7 +271,8 @@ int deftri_eval_chi2(deftri_ctx *ctx, double *chi2);
 int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n);
 /* y = H x for the current linearization (same vertex order). */
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n);
-/* Solve (H + lambda I) x = rhs with the device LDL^T. */
+/* Solve (H + lambda I) x = rhs (analytic-Jacobian linearization at the current state) with the
+   configured step solver (deftri_set_linear_solver: PCG with LDL^T fallback, or the LDL^T). */
 int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n);
 /* Number of unknowns of the uploaded problem. */
 int64_t deftri_num_unknowns(const deftri_ctx *ctx);

@@ -4,8 +4,8 @@ sketched.  Test infrastructure (uses the oracle's assembled 
     python tests/pcg_evidence.py 10000 30000 100000 > profiles/r02_pcg_evidence.json
 
 For the two-view benchmark scene at n correspondences: the damped system (H + lam I) dx = b of the
-first LM iteration (lam = tau * max diag H, tau = 1e-5, g2o's initial damping) and of a later,
-weaker damping (lam / 100), solved by conjugate gradients with the block-Jacobi preconditioner
+first LM iteration (lam = tau * max diag H, tau = 1e-5, g2o's initial damping) and of later, weaker
+dampings (1e-7 and 1e-9 of max diag H), solved by conjugate gradients with the block-Jacobi preconditioner
 (one block of H + lam I per vertex: 6x6 T_g, 1x1 scale, 3x3 point; at most 10000 iterations) — the preconditioner the PCG plan named —
 against the direct solve (the oracle's sparse LDL^T).  Reported: CG iterations to relative residual
 1e-4 / 1e-6 / 1e-8 / 1e-10 and the relative error of the step at those points.
@@ -87,7 +87,9 @@ def main():
         dmax = np.abs(H.diagonal()).max()
         case = {"correspondences": n, "unknowns": N, "nnz_H": int(H.nnz),
                 "diag_H_range": [float(np.abs(H.diagonal()).min()), float(dmax)]}
-        for name, lam in (("initial", 1e-5 * dmax), ("weak", 1e-7 * dmax)):
+        # g2o starts at tau * max diag H (tau = 1e-5) and each accepted trial scales lambda by 1/3..2/3:
+        # after ~10 / ~20 accepted iterations it is 1e-2 / 1e-4 of the start or less
+        for name, lam in (("initial", 1e-5 * dmax), ("later_1e-7", 1e-7 * dmax), ("later_1e-9", 1e-9 * dmax)):
             A = (H + lam * sp.identity(N, format="csr")).tocsr()
             M = block_jacobi(A, dims)
             t1 = time.time()

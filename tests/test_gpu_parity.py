@@ -164,7 +164,11 @@ def test_full_size_properties(gpu_ctx):
 
 def test_profile_trial_reports_kernels(gpu_ctx, golden_cases):
     gpu_ctx.upload(_golden(golden_cases[0]))
-    st = gpu_ctx.profile_trial(1e3)
+    gpu_ctx.set_linear_solver("direct")          # the factorization's kernels (PCG: test_gpu_pcg.py)
+    try:
+        st = gpu_ctx.profile_trial(1e3)
+    finally:
+        gpu_ctx.set_linear_solver("pcg")
     # the panel TRSM has its own launches unless DEFTRI_TRSM_FUSE=1 folds them into diag / update
     fused = os.environ.get("DEFTRI_TRSM_FUSE") == "1"
     for k in ("lin_arap", "hchunk", "scatter", "diag", "update") + (() if fused else ("trsm",)):
@@ -248,9 +252,14 @@ def test_weight_search_matches_oracle():
 
 
 def _lm_run(ctx, lanes, n_it, **kw):
+    # lanes batch factorizations: the direct step solver (PCG steps run sequential trials)
     ctx.set_lm_lanes(lanes)
+    ctx.set_linear_solver("direct")
     ctx.reset_state()
-    r = ctx.solve_lm(n_it, analytic=True, **kw)
+    try:
+        r = ctx.solve_lm(n_it, analytic=True, **kw)
+    finally:
+        ctx.set_linear_solver("pcg")
     pts, sc, tg = ctx.download()
     return r, pts, sc, tg
 

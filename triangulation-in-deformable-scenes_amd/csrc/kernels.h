@@ -113,6 +113,8 @@ struct KProf {
 };
 void set_profiler(KProf *p);
 bool profiling();
+hipEvent_t prof_begin(hipStream_t st);   // nullptr unless profiling
+void prof_end(const char *name, hipEvent_t e0, unsigned grid, double work, hipStream_t st);
 
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic);
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st);

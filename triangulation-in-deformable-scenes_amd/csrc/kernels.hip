@@ -1508,6 +1508,19 @@ static hipEvent_t prof_event() {
     if (P.next == P.pool.size()) { hipEvent_t e; hipEventCreate(&e); P.pool.push_back(e); }
     return P.pool[P.next++];
 }
+// the same timing for launches issued from other translation units (pcg.hip)
+hipEvent_t prof_begin(hipStream_t st) {
+    if (!g_prof) return nullptr;
+    hipEvent_t e = prof_event();
+    hipEventRecord(e, st);
+    return e;
+}
+void prof_end(const char *name, hipEvent_t e0, unsigned grid, double work, hipStream_t st) {
+    if (!g_prof || !e0) return;
+    hipEvent_t e1 = prof_event();
+    hipEventRecord(e1, st);
+    g_prof->recs.push_back({name, e0, e1, grid, work, g_level});
+}
 #define LAUNCH(NAME, KER, GRID, BLOCK, ST, ...)                                     \
     do {                                                                             \
         hipEvent_t e0_ = nullptr;                                                    \

@@ -26,6 +26,7 @@
 #include "../../include/deftri.h"
 #include "graph_builder.h"
 #include "kernels.h"
+#include "pcg.h"
 #include "symbolic.h"
 
 using namespace deftri;
@@ -39,6 +40,9 @@ int plan_emulate_solve(const Symbolic &S, const double *H, double lambda, const 
 namespace {
 
 constexpr int kRedParts = 512;
+constexpr double kPcgDefaultTol = 1e-12;    // relative residual ||b - A x|| / ||b||
+constexpr int kPcgDefaultMaxIt = 200;     // before a plan is uploaded
+constexpr int kPcgMaxIt = 4096;
 
 struct HostProblem {
     deftri_problem_desc d{};
@@ -105,7 +109,7 @@ struct deftri_ctx {
     DevPlan L;
     std::vector<void *> allocs;
     double *d_dx = nullptr, *d_part = nullptr, *d_scal = nullptr;   // d_scal: [0]=chi2 [1]=scale [2]=maxdiag
-    double *hpin = nullptr;                 // pinned host staging of the per-trial scalars (16 doubles)
+    double *hpin = nullptr;                 // pinned host staging of the per-trial scalars (32 doubles; [16..23] PCG record)
     int *ipin = nullptr;                    // pinned host staging of the zero-pivot flag
     std::vector<double *> init_state;       // device copies of the initial state
     hipEvent_t ev[8]{};
@@ -143,6 +147,17 @@ struct deftri_ctx {
     hipGraphExec_t trial_graph = nullptr;
     bool trial_graph_failed = false;
     double *d_lam = nullptr;
+    // LM step by block-Jacobi PCG (pcg.h) with the factorization as the fallback
+    int lin_solver = DEFTRI_SOLVER_PCG;     // deftri_set_linear_solver
+    double pcg_tol = kPcgDefaultTol;
+    int pcg_max_it = 0;                     // 0: pcg_auto_it
+    bool pcg_avail = false;                 // single-rank plan with a row view on the device
+    std::string pcg_why;                    // why not, when not
+    PcgDev G;
+    double pcg_bytes = 0, pcg_flops = 0;    // per product launch (profile_trial roofline)
+    int pcg_auto_it = kPcgDefaultMaxIt;     // default budget of the uploaded plan (cost model)
+    int pcg_last_its = 8;                   // iterations of the last converged solve (first chunk size)
+    int pcg_step_its = 0, pcg_step_solved = 0;   // the last PCG step (deftri_last_step_info)
 };
 
 namespace {
@@ -431,6 +446,59 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     HIPOK(hipMemset(ctx->d_dx, 0, sizeof(double) * (size_t)std::max<int64_t>(S.ndof, 1)));   // dofs no solve writes stay 0
     if ((rc = dalloc(ctx, &ctx->d_part, kRedParts))) return rc;
     if ((rc = dalloc(ctx, &ctx->d_scal, 8))) return rc;
+    ctx->pcg_avail = false;
+    ctx->pcg_why.clear();
+    if (ctx->dist()) {
+        ctx->pcg_why = "point-sharded plan";
+    } else {
+        PcgHost ph;
+        if (!build_pcg_host(S.nv, S.voff, S.vdim, S.blk_val_off, S.blk_rows, S.blk_cols, S.blk_row_dof, S.blk_col_dof,
+                            ph, ctx->pcg_why)) {
+            ctx->pcg_why = "row view: " + ctx->pcg_why;
+        } else {
+            PcgDev &G = ctx->G;
+            G = PcgDev();
+            G.nv = S.nv; G.ndof = S.ndof;
+            G.nlight = (int32_t)ph.light_v.size();
+            G.nheavy = (int32_t)ph.heavy_v.size();
+            G.nhchunks = (int32_t)ph.hc_vertex.size();
+            G.nheavy_dofs = ph.h_dofbase.back();
+            G.nA_light = (G.nlight + 255) / 256;
+            G.nB = (int32_t)((S.nv + 255) / 256);
+            int64_t *eb, *hb, *he, *dg, *mo;
+            PcgEnt *en;
+            int32_t *lv, *hv, *hcv, *hf, *hdb, *vh;
+            PUT(eb, ph.ent_begin); PUT(en, ph.ent); PUT(lv, ph.light_v); PUT(hv, ph.heavy_v); PUT(hcv, ph.hc_vertex);
+            PUT(hb, ph.hc_beg); PUT(he, ph.hc_end); PUT(hf, ph.h_first); PUT(hdb, ph.h_dofbase); PUT(vh, ph.v_heavy);
+            PUT(dg, ph.diag_off); PUT(mo, ph.moff);
+            G.ent_begin = eb; G.ent = en; G.light_v = lv; G.heavy_v = hv; G.hc_vertex = hcv; G.hc_beg = hb;
+            G.hc_end = he; G.h_first = hf; G.h_dofbase = hdb; G.v_heavy = vh; G.diag_off = dg; G.moff = mo;
+            G.voff = L.voff; G.vdim = L.vdim;
+            if ((rc = dalloc(ctx, &G.minv, ph.msize)) || (rc = dalloc(ctx, &G.r, S.ndof)) ||
+                (rc = dalloc(ctx, &G.z, S.ndof)) || (rc = dalloc(ctx, &G.p[0], S.ndof)) ||
+                (rc = dalloc(ctx, &G.p[1], S.ndof)) || (rc = dalloc(ctx, &G.q, S.ndof)) ||
+                (rc = dalloc(ctx, &G.hq, 6 * (int64_t)std::max(G.nhchunks, 1))) ||
+                (rc = dalloc(ctx, &G.partA, std::max(G.nA_light, 1))) || (rc = dalloc(ctx, &G.partB, 2 * (int64_t)G.nB)) ||
+                (rc = dalloc(ctx, &G.rec, (int64_t)kPcgRec * (kPcgMaxIt + 2))))
+                return rc;
+            ctx->pcg_avail = true;
+            double by = 32.0 * (double)S.ndof, fl = 0;
+            for (int64_t v = 0; v < S.nv; v++)
+                for (int64_t e = ph.ent_begin[v]; e < ph.ent_begin[v + 1]; e++) {
+                    by += 16.0 + 8.0 * S.vdim[v] * ph.ent[e].odim;
+                    fl += 2.0 * S.vdim[v] * ph.ent[e].odim;
+                }
+            ctx->pcg_bytes = by;
+            ctx->pcg_flops = fl;
+            // default budget: CG iterations that cost about one factorization + substitution, from
+            // plan sizes only (deterministic: the same problem always takes the same path).  Rates
+            // measured at C2: the LDL^T trial ~7 TF/s + ~50 us per tree level, a CG iteration ~2 TB/s
+            // of its product's bytes + ~15 us of launch latency
+            const double t_fac = S.factor_flops / 7e9 + 0.05 * S.nlevels;   // ms
+            const double t_it = by / 2e9 + 0.015;
+            ctx->pcg_auto_it = (int)std::min<double>(kPcgMaxIt, std::max(8.0, std::ceil(t_fac / t_it)));
+        }
+    }
     if (ctx->dist()) {
         if ((rc = dalloc(ctx, &ctx->d_xbuf, S.dist.xbuf_size))) return rc;
         if ((rc = dalloc(ctx, &ctx->d_diagv, S.ndof))) return rc;
@@ -610,8 +678,11 @@ void pop_state(deftri_ctx *ctx) {
     hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
 }
 
+bool use_pcg(const deftri_ctx *ctx) { return ctx->lin_solver == DEFTRI_SOLVER_PCG && ctx->pcg_avail; }
+
 int lane_count(const deftri_ctx *ctx) {
     if (ctx->dist()) return 1;              // point-sharded: one trial at a time (the transfers are per trial)
+    if (use_pcg(ctx)) return 1;             // PCG steps: sequential trials (the lanes batch factorizations)
     int n = ctx->max_lanes;
     if (n <= 0) {
         n = ctx->S.factor_flops < kLaneFlopLimit ? 2 : 1;
@@ -741,7 +812,7 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
         return DEFTRI_E_HIP;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
-    if (hipHostMalloc((void **)&ctx->hpin, 16 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
+    if (hipHostMalloc((void **)&ctx->hpin, 32 * sizeof(double), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void **)&ctx->ipin, 16 * sizeof(int), hipHostMallocDefault) != hipSuccess) {
         delete ctx;
         return DEFTRI_E_HIP;
@@ -789,6 +860,23 @@ int deftri_set_factor_precision(deftri_ctx *ctx, int32_t fp32_updates) {
     ctx->L.f32_update = fp32_updates;
     ctx->LB.f32_update = fp32_updates;
     drop_trial_graph(ctx);                 // the captured trial holds the previous kernel choice
+    return 0;
+}
+
+int deftri_set_linear_solver(deftri_ctx *ctx, int32_t solver, double tol, int32_t max_iterations) {
+    if (!ctx || (solver != DEFTRI_SOLVER_DIRECT && solver != DEFTRI_SOLVER_PCG) || !(tol < 1.0) ||
+        max_iterations > kPcgMaxIt)
+        return DEFTRI_E_ARG;
+    ctx->lin_solver = solver;
+    ctx->pcg_tol = tol > 0 ? tol : kPcgDefaultTol;
+    ctx->pcg_max_it = max_iterations > 0 ? max_iterations : 0;   // 0: the plan's cost-model budget
+    return 0;
+}
+
+int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_t *pcg_converged) {
+    if (!ctx || !pcg_iterations || !pcg_converged) return DEFTRI_E_ARG;
+    *pcg_iterations = ctx->pcg_step_its;
+    *pcg_converged = ctx->pcg_step_solved;
     return 0;
 }
 
@@ -909,6 +997,10 @@ int deftri_debug_plan_solve_dist(deftri_ctx *ctx, const double *Hq, double lambd
     return rc == 0 ? 0 : fail(ctx, DEFTRI_E_NUMERIC, "zero pivot");
 }
 
+namespace {
+int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, int &its);
+}
+
 int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *stats, int32_t max_stats,
                          int32_t *n_stats) {
     if (!ctx || !stats || !n_stats) return DEFTRI_E_ARG;
@@ -924,9 +1016,29 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     int rc = eval_chi2_dev(ctx, true, ctx->prof_analytic, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
-    launch_scatter(ctx->L, lambda, ctx->st);
-    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
-    launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st, ctx->dist() ? ctx->L.b : nullptr, hook, ctx);
+    bool solved = false;
+    int its = 0;
+    if (!rc && use_pcg(ctx)) {
+        // the configured PCG step: solved once to learn its iteration count, then replayed with
+        // exactly that many (update, product) pairs under the profiler
+        set_profiler(nullptr);
+        rc = pcg_step(ctx, lambda, ctx->L.b, solved, its);
+        set_profiler(&prof);
+        if (!rc && solved) {
+            const PcgDev &G = ctx->G;
+            launch_pcg_setup(G, ctx->L.hval, ctx->L.b, lambda, ctx->d_dx, ctx->st);
+            launch_pcg_product(G, 0, ctx->L.hval, lambda, ctx->st);
+            for (int j = 0; j < its; j++) {
+                launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
+                launch_pcg_product(G, j + 1, ctx->L.hval, lambda, ctx->st);
+            }
+        }
+    }
+    if (!solved) {
+        launch_scatter(ctx->L, lambda, ctx->st);
+        launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
+        launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st, ctx->dist() ? ctx->L.b : nullptr, hook, ctx);
+    }
     set_profiler(nullptr);
     if (rc) return rc;
     if (ctx->hook_rc) return ctx->hook_rc;
@@ -954,6 +1066,10 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
         if (!std::strcmp(stats[k].name, "diag")) stats[k].flops = S.diag_flops;
         if (!std::strcmp(stats[k].name, "trsm")) stats[k].flops = S.trsm_flops;
         if (!std::strcmp(stats[k].name, "lin_arap")) stats[k].bytes = (double)ctx->P.E * (16 + 8 * 12 + 8 * 18 + 3 * 8);
+        // the product's compulsory traffic per active launch: entries + block values
+        // in both orientations + p_prev / z of the row's own dofs + p / q written
+        if (!std::strcmp(stats[k].name, "pcg_product")) stats[k].bytes = ctx->pcg_bytes * its;
+        if (!std::strcmp(stats[k].name, "pcg_product")) stats[k].flops = ctx->pcg_flops * its;
     }
     for (hipEvent_t e : prof.pool) hipEventDestroy(e);
     *n_stats = n;
@@ -1012,6 +1128,51 @@ int deftri_reset_state(deftri_ctx *ctx) {
 }
 
 namespace {
+// One LM step by PCG into ctx->d_dx.  Launches go out in chunks (update, product) x n; the host
+// reads the record of the last product after each chunk (the product launch carries the
+// convergence test, so launches past convergence return at once).  The first chunk is sized by the
+// previous converged solve.  solved = false: budget exhausted, breakdown, or a preconditioner block
+// not positive definite — the caller factors instead.
+int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, int &its) {
+    PcgDev &G = ctx->G;
+    const DevPlan &L = ctx->L;
+    G.max_it = ctx->pcg_max_it > 0 ? ctx->pcg_max_it : ctx->pcg_auto_it;
+    G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
+    solved = false;
+    its = 0;
+    launch_pcg_setup(G, L.hval, rhs, lambda, ctx->d_dx, ctx->st);
+    launch_pcg_product(G, 0, L.hval, lambda, ctx->st);
+    int j = 0;
+    int chunk = std::max(2, ctx->pcg_last_its + 1);
+    double *rec = ctx->hpin + 16;
+    for (;;) {
+        const int n = std::min(chunk, G.max_it - j);
+        for (int k = 0; k < n; k++, j++) {
+            launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
+            launch_pcg_product(G, j + 1, L.hval, lambda, ctx->st);
+        }
+        HIPOK(hipMemcpyAsync(rec, G.rec + (size_t)kPcgRec * (j + 1), sizeof(double) * kPcgRec, hipMemcpyDeviceToHost,
+                             ctx->st));
+        HIPOK(hipStreamSynchronize(ctx->st));
+        const int status = (int)rec[PR_STATUS];
+        if (status == kPcgConverged) {
+            its = (int)rec[PR_ITS];
+            ctx->pcg_last_its = its;
+            solved = true;
+            ctx->pcg_step_its = its;
+            ctx->pcg_step_solved = 1;
+            return 0;
+        }
+        if (status != kPcgRunning || j >= G.max_it) {
+            its = j;
+            ctx->pcg_step_its = its;
+            ctx->pcg_step_solved = 0;
+            return 0;
+        }
+        chunk = 4;
+    }
+}
+
 // the sequential trial (scatter + factorization + solve) as one graph launch: single stream, no
 // cross-rank hooks, no per-launch profiling, no fused-TRSM epochs (DEFTRI_GRAPH=0 disables)
 bool trial_graph_usable(const deftri_ctx *ctx) {
@@ -1093,6 +1254,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         if (nlanes < 1) return fail(ctx, DEFTRI_E_HIP, "lane allocation failed: " + ctx->err);
     }
     R.lanes = nlanes;
+    const bool pcg = nlanes == 1 && use_pcg(ctx);
     for (it = 0; it < prm->n_iterations; it++) {
         hipEventRecord(ctx->ev[0], ctx->st);
         if ((rc = eval_chi2_dev(ctx, true, analytic, 0))) return rc;   // computeActiveErrors + linearizeOplus
@@ -1170,11 +1332,27 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             }
         } else do {
             push_state(ctx);
-            hipEventRecord(ctx->ev[2], ctx->st);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
-            ctx->hpin[12] = lambda;                          // pinned: read by the copy at its turn in the stream
-            HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
-            if (launch_trial_graph(ctx)) {
+            bool solved = false;
+            if (pcg) {
+                auto t0 = std::chrono::steady_clock::now();
+                int its = 0;
+                if ((rc = pcg_step(ctx, lambda, L.b, solved, its))) return rc;
+                R.ms_pcg += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                R.pcg_iterations += its;
+                if (solved) R.pcg_trials++;
+                else R.pcg_fallbacks++;
+                if (prm->verbose)
+                    std::fprintf(stderr, "[deftri] pcg lambda %.6e iterations %d %s\n", lambda, its, solved ? "converged" : "-> LDL^T");
+            }
+            hipEventRecord(ctx->ev[2], ctx->st);
+            if (!solved) {
+                ctx->hpin[12] = lambda;                      // pinned: read by the copy at its turn in the stream
+                HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
+            }
+            if (solved) {
+                hipEventRecord(ctx->ev[3], ctx->st);         // PCG step: timed in ms_pcg
+            } else if (launch_trial_graph(ctx)) {
                 hipEventRecord(ctx->ev[3], ctx->st);         // factor + solve in one graph: timed as factor
             } else {
                 launch_scatter(L, lambda, ctx->st);          // setLambda
@@ -1449,15 +1627,24 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (n != ctx->S.ndof || !rhs || !x) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
+    (void)hipGetLastError();                    // the status check below reads this call's errors only
     double *dr = nullptr;
     HIPOK(hipMalloc(&dr, sizeof(double) * (size_t)n));
     hipMemcpy(dr, rhs, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
     eval_chi2_dev(ctx, true, true, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
-    launch_scatter(ctx->L, lambda, ctx->st);
-    launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
-    launch_solve(ctx->L, dr, ctx->d_dx, ctx->st);
+    bool solved = false;
+    if (use_pcg(ctx)) {                         // the configured step solver, as deftri_solve_lm uses it
+        int its = 0;
+        const int rc = pcg_step(ctx, lambda, dr, solved, its);
+        if (rc) { hipFree(dr); return rc; }
+    }
+    if (!solved) {
+        launch_scatter(ctx->L, lambda, ctx->st);
+        launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64);
+        launch_solve(ctx->L, dr, ctx->d_dx, ctx->st);
+    }
     int flag = 0;
     hipMemcpyAsync(&flag, ctx->L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st);
     hipStreamSynchronize(ctx->st);

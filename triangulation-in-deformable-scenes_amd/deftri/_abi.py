@@ -17,6 +17,8 @@ DEFTRI_E_NODEVICE = -5
 DEFTRI_E_GRAPH = -6
 DEFTRI_STATUS_OK = 0
 DEFTRI_STATUS_TERMINATE = 1
+DEFTRI_SOLVER_DIRECT = 0
+DEFTRI_SOLVER_PCG = 1
 DEFTRI_MAX_REPORT_ITERS = 1024
 
 
@@ -51,6 +53,7 @@ class Report(C.Structure):
         ("n_unknowns", i64), ("nnz_factor", i64), ("factor_flops", f64), ("n_fronts", i32),
         ("n_levels", i32), ("lanes", i32), ("trials_executed", i32),
         ("rank", i32), ("nranks", i32), ("factor_flops_total", f64), ("plan_reuses", i64),
+        ("pcg_trials", i32), ("pcg_fallbacks", i32), ("pcg_iterations", i64), ("ms_pcg", f64),
     ]
 
     def as_dict(self):
@@ -68,6 +71,8 @@ class Report(C.Structure):
             "lanes": self.lanes, "trials_executed": self.trials_executed,
             "rank": self.rank, "nranks": self.nranks, "factor_flops_total": self.factor_flops_total,
             "plan_reuses": self.plan_reuses,
+            "pcg_trials": self.pcg_trials, "pcg_fallbacks": self.pcg_fallbacks,
+            "pcg_iterations": self.pcg_iterations, "ms_pcg": self.ms_pcg,
         }
 
 

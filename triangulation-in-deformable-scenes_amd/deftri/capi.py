@@ -46,6 +46,8 @@ def load():
         "deftri_set_lm_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_set_jacobian_mode": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_set_factor_precision": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_set_linear_solver": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32]),
+        "deftri_last_step_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
         "deftri_triangulate_nrslam": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float),
                                                 P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float),
@@ -115,7 +117,7 @@ def load():
 EXPORTED = [
     "deftri_abi_version", "deftri_ctx_create", "deftri_ctx_destroy", "deftri_last_error",
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
-    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_set_factor_precision", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
+    "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_set_factor_precision", "deftri_set_linear_solver", "deftri_last_step_info", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
     "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_graph_point_ids", "deftri_arap_optimization",
     "deftri_profile_trial",
@@ -146,6 +148,7 @@ class Context:
         self.device = device
         self._desc = None
         self._prob = None
+        self._solver = ("pcg", 0.0, 0)
 
     def close(self):
         if self.h:
@@ -233,6 +236,18 @@ class Context:
         self._check(self.lib.deftri_debug_plan_solve_dist(self.h, _dp(Hq), float(lam), _dp(bq), _dp(x), len(bq)))
         return x
 
+    def set_linear_solver(self, solver="pcg", tol=0.0, max_iterations=0):
+        """LM step solver: "pcg" (block-Jacobi PCG, LDL^T fallback; default) or "direct" (multifrontal LDL^T)."""
+        code = {"direct": _abi.DEFTRI_SOLVER_DIRECT, "pcg": _abi.DEFTRI_SOLVER_PCG}[solver]
+        self._check(self.lib.deftri_set_linear_solver(self.h, code, float(tol), int(max_iterations)))
+        self._solver = (solver, tol, max_iterations)
+
+    def last_step_info(self):
+        """(CG iterations, converged) of the last PCG step."""
+        it, ok = C.c_int32(), C.c_int32()
+        self._check(self.lib.deftri_last_step_info(self.h, C.byref(it), C.byref(ok)))
+        return it.value, bool(ok.value)
+
     def set_factor_precision(self, fp32_updates):
         """1: trailing updates on fp32 MFMA (the C5 precision sweep); 0: fp64 (default, the reference's)."""
         self._check(self.lib.deftri_set_factor_precision(self.h, 1 if fp32_updates else 0))
@@ -274,10 +289,17 @@ class Context:
         self._check(self.lib.deftri_eval_hessian_product(self.h, _dp(x), _dp(y), len(x)))
         return y
 
-    def damped_solve(self, lam, rhs):
+    def damped_solve(self, lam, rhs, solver="direct", tol=0.0, max_iterations=0):
+        """(H + lam I) x = rhs with `solver` ("direct" LDL^T or "pcg"); the context's solver setting
+        is restored afterwards."""
         r = np.ascontiguousarray(rhs, dtype=np.float64)
         x = np.zeros_like(r)
-        self._check(self.lib.deftri_eval_damped_solve(self.h, float(lam), _dp(r), _dp(x), len(r)))
+        prev = self._solver
+        self.set_linear_solver(solver, tol, max_iterations)
+        try:
+            self._check(self.lib.deftri_eval_damped_solve(self.h, float(lam), _dp(r), _dp(x), len(r)))
+        finally:
+            self.set_linear_solver(*prev)
         return x
 
     def profile_trial(self, lam):
