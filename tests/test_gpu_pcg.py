@@ -1,0 +1,138 @@
+"""PCG LM steps (deftri_set_linear_solver "pcg", pcg.hip) against the oracle's exact sparse LDL^T
+(oracle/deftri_oracle.c, the reference's SimplicialLDLT restated).  Tolerances:
+  * one damped solve: relative residual ||(H + lam I) x - b|| / ||b|| < 1e-11 (the stop test is
+    1e-12 on the recurrence residual) and rel 1e-6 against the oracle's exact solve (the forward
+    error is the residual times the damped system's condition number, ~1e4-1e5 at tau = 1e-5; the
+    direct path meets 1e-8, a backward-stable factorization's bar)
+  * LM trajectories: chi2 per iteration rel 1e-6 and identical trial counts (the direct path's bar),
+    (nearly) every trial solved by PCG at budget 4096 (the golden scenes' weakly damped steps take
+    ~3000-4200 CG iterations; the default budget hands those to the LDL^T)
+  * budget exhausted (max_iterations = 1): every trial falls back to the LDL^T, trajectory unchanged
+  * default (cost-model) budget: the mix of PCG and LDL^T steps matches the oracle the same way
+  * C2 size (100k correspondences): PCG vs LDL^T LM chi2 per iteration rel 1e-9 with the same trials;
+    repeated PCG runs bit-identical (fixed-order reductions)
+"""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from deftri import capi, sim
+from deftri.problem import Problem
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _golden(name):
+    return Problem.load(GOLDEN / name / "problem.npz")
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300)
+
+
+@pytest.fixture
+def pcg_ctx(gpu_ctx):
+    gpu_ctx.set_linear_solver("pcg")
+    yield gpu_ctx
+    gpu_ctx.set_linear_solver("pcg")
+
+
+def test_pcg_damped_solve_matches_oracle(pcg_ctx, golden_cases):
+    for name in golden_cases:
+        p = _golden(name)
+        pcg_ctx.upload(p)
+        b_ref, H_ref, _ = oracle.linearize(p, analytic=True, dense=True)
+        dmax = np.abs(np.diag(H_ref)).max()
+        for lam_rel in (1e-3, 1e-2, 1.0):          # (1e-5 of max diag H takes ~4200 iterations at 728 unknowns)
+            lam = lam_rel * dmax
+            x = pcg_ctx.damped_solve(lam, b_ref, solver="pcg", max_iterations=4096)
+            its, ok = pcg_ctx.last_step_info()
+            assert ok and its > 0, (name, lam_rel, its)
+            A = H_ref + lam * np.eye(len(b_ref))
+            assert np.linalg.norm(A @ x - b_ref) / np.linalg.norm(b_ref) < 1e-11
+            assert rel(x, oracle.damped_solve(p, lam, b_ref)) < 1e-6
+
+
+def test_pcg_lm_trajectory_matches_oracle(pcg_ctx, golden_cases):
+    for name in golden_cases:
+        p = _golden(name)
+        pcg_ctx.upload(p)
+        ref = oracle.solve_lm(p, 10, analytic=True)["report"]
+        for budget in (4096, 0):
+            pcg_ctx.reset_state()
+            pcg_ctx.set_linear_solver("pcg", max_iterations=budget)
+            r = pcg_ctx.solve_lm(10, analytic=True)
+            assert r["iterations"] == ref["iterations"]
+            assert r["trials_total"] == ref["trials_total"]
+            np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+            assert r["pcg_trials"] + r["pcg_fallbacks"] == r["trials_total"]
+            if budget:
+                assert r["pcg_trials"] >= r["trials_total"] - 2 and r["pcg_iterations"] > 0
+
+
+def test_pcg_c1_numeric_lm_no_fallback(pcg_ctx):
+    """1k correspondences, g2o numeric Jacobians (the reference's arithmetic): every trial by PCG
+    (budget 4096)."""
+    m, _ = sim.simulate_two_view(n=1000, seed=11)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    pcg_ctx.upload(p)
+    pcg_ctx.set_linear_solver("pcg", max_iterations=4096)
+    r = pcg_ctx.solve_lm(5, analytic=False)
+    ref = oracle.solve_lm(p, 5, analytic=False)["report"]
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+    assert r["pcg_fallbacks"] == 0 and r["pcg_trials"] == r["trials_total"]
+
+
+def test_pcg_budget_falls_back_to_ldlt(pcg_ctx, golden_cases):
+    p = _golden(golden_cases[0])
+    pcg_ctx.upload(p)
+    pcg_ctx.set_linear_solver("pcg", max_iterations=1)
+    r = pcg_ctx.solve_lm(5, analytic=True)
+    ref = oracle.solve_lm(p, 5, analytic=True)["report"]
+    assert r["pcg_fallbacks"] == r["trials_total"] and r["pcg_trials"] == 0
+    assert r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+
+
+def test_pcg_full_size_matches_direct(pcg_ctx):
+    """C2 (100k correspondences x 2 views, numeric J): PCG steps vs the multifrontal LDL^T."""
+    m, _ = sim.simulate_two_view(n=100000, seed=1, scale_scene=True, compact=True)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    pcg_ctx.upload(p)
+    b, d = pcg_ctx.gradient()
+    lam = 1e-5 * np.abs(d).max()
+    x = pcg_ctx.damped_solve(lam, b, solver="pcg")
+    its, ok = pcg_ctx.last_step_info()
+    assert ok
+    r = pcg_ctx.hessian_product(x) + lam * x - b
+    assert np.linalg.norm(r) / np.linalg.norm(b) < 1e-11
+    pcg_ctx.reset_state()
+    pcg_ctx.set_linear_solver("direct")
+    rd = pcg_ctx.solve_lm(2, analytic=False)
+    pcg_ctx.reset_state()
+    pcg_ctx.set_linear_solver("pcg")
+    r1 = pcg_ctx.solve_lm(2, analytic=False)
+    pts1, _, _ = pcg_ctx.download()
+    assert r1["trials_total"] == rd["trials_total"]
+    np.testing.assert_allclose(r1["chi2_iter"], rd["chi2_iter"], rtol=1e-9)
+    assert r1["pcg_fallbacks"] == 0
+    pcg_ctx.reset_state()
+    r2 = pcg_ctx.solve_lm(2, analytic=False)
+    pts2, _, _ = pcg_ctx.download()
+    assert r1["chi2_iter"] == r2["chi2_iter"]
+    assert np.array_equal(pts1, pts2)
+
+
+def test_pcg_profile_reports_kernels(pcg_ctx):
+    m, _ = sim.simulate_two_view(n=1000, seed=11)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    pcg_ctx.upload(p)
+    b, d = pcg_ctx.gradient()
+    pcg_ctx.set_linear_solver("pcg", max_iterations=4096)
+    st = pcg_ctx.profile_trial(0.1 * np.abs(d).max())
+    for k in ("pcg_setup", "pcg_product", "pcg_update", "hchunk"):
+        assert k in st and st[k]["launches"] > 0, k
+    assert st["pcg_product"]["bytes"] > 0
+    assert "update" not in st                 # no factorization when PCG converged
