@@ -4,7 +4,9 @@
     1e-12 on the recurrence residual) and rel 1e-6 against the oracle's exact solve (the forward
     error is the residual times the damped system's condition number, ~1e4-1e5 at tau = 1e-5; the
     direct path meets 1e-8, a backward-stable factorization's bar)
-  * LM trajectories: chi2 per iteration rel 1e-6 and identical trial counts (the direct path's bar),
+  * LM trajectories: identical trial counts, chi2 per iteration rel 1e-5 (the direct path holds 1e-6:
+    a CG step carries the residual tolerance times the condition number, ~1e-8 relative on the
+    golden scenes' weakly damped steps, and ten LM iterations amplify it to ~2e-6 in chi2),
     (nearly) every trial solved by PCG at budget 4096 (the golden scenes' weakly damped steps take
     ~3000-4200 CG iterations; the default budget hands those to the LDL^T)
   * budget exhausted (max_iterations = 1): every trial falls back to the LDL^T, trajectory unchanged
@@ -65,10 +67,35 @@ def test_pcg_lm_trajectory_matches_oracle(pcg_ctx, golden_cases):
             r = pcg_ctx.solve_lm(10, analytic=True)
             assert r["iterations"] == ref["iterations"]
             assert r["trials_total"] == ref["trials_total"]
-            np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+            np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)
             assert r["pcg_trials"] + r["pcg_fallbacks"] == r["trials_total"]
             if budget:
                 assert r["pcg_trials"] >= r["trials_total"] - 2 and r["pcg_iterations"] > 0
+
+
+def test_pcg_numeric_golden_rmse(pcg_ctx, golden_cases):
+    """The north-star criterion with PCG steps only (budget 4096) in g2o numeric-Jacobian mode: the
+    final reprojection RMSE (calculatePixelsStandDev) within 1e-4 px of the golden oracle run."""
+    import importlib
+    import json
+    import sys
+    from deftri import metrics
+    sys.path.insert(0, str(GOLDEN))
+    mg = importlib.import_module("make_golden")
+    for name in golden_cases:
+        p = _golden(name)
+        exp = json.loads((GOLDEN / name / "expected.json").read_text())
+        pcg_ctx.upload(p)
+        pcg_ctx.set_linear_solver("pcg", max_iterations=4096)
+        r = pcg_ctx.solve_lm(exp["n_iterations"], analytic=False)
+        assert r["pcg_trials"] >= r["trials_total"] - 2
+        assert r["chi2_final"] == pytest.approx(exp["chi2_final"], rel=1e-5)
+        pts, _, _ = pcg_ctx.download()
+        m, _, _ = mg.scene(name)
+        metrics.apply_solution(m, exp["point_ids"], pts)
+        rms = metrics.pixels_stand_dev(m)
+        assert abs(rms["desv"] - exp["rms_final"]["desv"]) < 1e-4
+        assert abs(rms["desvc1"] - exp["rms_final"]["desvc1"]) < 1e-4
 
 
 def test_pcg_c1_numeric_lm_no_fallback(pcg_ctx):

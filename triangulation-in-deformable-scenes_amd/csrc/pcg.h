@@ -4,9 +4,18 @@
 // H stays in the assembled vertex-pair blocks (DevPlan::hval: one block per coupled vertex pair,
 // lower triangle in elimination order).  The plan adds a row view of them: per vertex v, the entries
 // (block, other vertex's first dof and dimension, transposed?) that make row v of H, so the product
-// is a gather (one thread per vertex, fixed entry order, no atomics).  Rows with more than
-// kPcgHeavy entries (the global T_g and scale vertices, coupled to every point) are split over
-// workgroups of kPcgChunk entries whose partial rows are summed in chunk order.
+// is a gather (fixed entry order, no atomics).  Three row classes:
+//   * sliced rows (3-dof points, the bulk): 64 rows per slice (one wave), taken in the plan's
+//     nested-dissection order (a slice's rows are mesh neighbours, so the lanes' gathers share
+//     cache lines) and sorted by their count of 3x3 point-point blocks inside windows of
+//     kPcgSortWindow rows so a slice pads little; those blocks are repacked once per LM iteration
+//     (after the assembly) into slot-major, lane-interleaved copies in the rows' orientation —
+//     every load of the product is coalesced; the row's other couplings (T_g, scale) follow as
+//     per-lane entries;
+//   * other light rows: one thread per row over its entries;
+//   * heavy rows (> kPcgHeavy entries: the global T_g and scale vertices, coupled to every point):
+//     workgroups of kPcgChunk entries whose partial rows are summed in chunk order.
+// The vectors the product gathers are interleaved per dof: zp = (z, p_prev) and pq = (p, q).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -20,6 +29,7 @@ constexpr int kPcgHeavy = 128;      // entries above which a row is reduced by w
 constexpr int kPcgChunk = 2048;     // entries per workgroup of a heavy row
 constexpr int kPcgRec = 8;          // doubles per iteration record
 constexpr int kPcgMaxHeavyDofs = 2048;
+constexpr int kPcgSortWindow = 512;
 // iteration record fields (record 0: setup; record k + 1: iteration k)
 enum { PR_RZ = 0, PR_RR = 1, PR_PQ = 2, PR_ALPHA = 3, PR_STATUS = 4, PR_ITS = 5 };
 // PR_STATUS: 0 running, 1 converged, 2 breakdown (p.Ap <= 0 / non-finite), 3 preconditioner block
@@ -40,23 +50,58 @@ struct PcgHost {
     std::vector<int32_t> light_v;        // vertices handled one per thread, in vertex order
     std::vector<int32_t> heavy_v;        // heavy vertices
     std::vector<int32_t> hc_vertex;      // per heavy chunk: heavy index
-    std::vector<int64_t> hc_beg, hc_end; // entry range of the chunk
+    std::vector<int64_t> hc_beg, hc_end; // entry range of the chunk (in hres)
     std::vector<int32_t> h_first;        // per heavy vertex: first chunk (nheavy + 1)
     std::vector<int32_t> h_dofbase;      // per heavy vertex: first heavy dof (nheavy + 1)
     std::vector<int32_t> v_heavy;        // per vertex: heavy index or -1
     std::vector<int64_t> diag_off;       // per vertex: val_off of its diagonal block
     std::vector<int64_t> moff;           // per vertex: offset of its preconditioner block (dim^2)
     int64_t msize = 0;
+    // sliced rows: slice s covers rows sl_v[64 s .. 64 s + 63] (-1: padding), 3x3 slots
+    // sl_off[s] .. sl_off[s] + sl_n[s] - 1 (global slot g: values [g][9][64], dof of the other
+    // point [g][64], source block [g][64] = val_off | transposed << 62, -1 padding), extra entries
+    // slots sl_xoff[s] .. + sl_nx[s] - 1 ([g][64], odim 0 = padding)
+    std::vector<int32_t> sl_v, sl_n, sl_nx;
+    std::vector<int64_t> sl_off, sl_xoff;
+    std::vector<int32_t> sl_col;
+    std::vector<int64_t> sl_map;
+    std::vector<PcgEnt> sl_x;
+    // heavy slots: slice s couples to heavy vertices through slots sl_hoff[s] .. + sl_hn[s] - 1;
+    // slot g: heavy index hs_hk[g], source block per lane hs_map[g][64] (3 x od in the row's
+    // orientation, od = the heavy vertex's dimension); per heavy vertex its slots in ascending order
+    // (hv_slot_begin; slot g's partial at position hs_pos[g]); heavy rows keep as entries (hres, chunked) only their couplings
+    // to vertices outside the slices
+    std::vector<int32_t> sl_hn, hs_hk;
+    std::vector<int64_t> hs_voff;        // per heavy slot: first double2 of its values (ceil(3 od / 2) x 64)
+    int64_t hs_size = 0;                 // doubles of all heavy slots' values
+    std::vector<int64_t> sl_hoff, hs_map, hv_slot_begin, hs_pos;
+    std::vector<PcgEnt> hres;
+    double product_bytes = 0, product_flops = 0;   // per product launch (roofline)
 };
 bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vector<int32_t> &vdim,
                     const std::vector<int64_t> &blk_val_off, const std::vector<int32_t> &blk_rows,
                     const std::vector<int32_t> &blk_cols, const std::vector<int64_t> &blk_row_dof,
-                    const std::vector<int64_t> &blk_col_dof, PcgHost &out, std::string &err);
+                    const std::vector<int64_t> &blk_col_dof, const std::vector<int64_t> &elim_pos, PcgHost &out,
+                    std::string &err);
 
 struct PcgDev {
     int64_t nv = 0, ndof = 0;
     int32_t nlight = 0, nheavy = 0, nhchunks = 0, nheavy_dofs = 0;
     int32_t nA_light = 0;                // workgroups of the light part of the product launch
+    int32_t nsl = 0, nA_sl = 0;          // slices; their workgroups (one per slice) lead the launch
+    int64_t nslots = 0;                  // 3x3 slots of all slices
+    const int32_t *sl_v = nullptr, *sl_n = nullptr, *sl_nx = nullptr, *sl_col = nullptr;
+    const int64_t *sl_off = nullptr, *sl_xoff = nullptr, *sl_map = nullptr;
+    const PcgEnt *sl_x = nullptr;
+    double *sl_val = nullptr;            // repacked 3x3 blocks: nslots x 5 x 64 double2 (9 values + column dof)
+    int64_t nhslots = 0;
+    const int32_t *sl_hn = nullptr, *hs_hk = nullptr;
+    const int64_t *sl_hoff = nullptr, *hs_map = nullptr, *hv_slot_begin = nullptr, *hs_pos = nullptr;
+    const int64_t *hs_voff = nullptr;
+    const PcgEnt *hres = nullptr;        // heavy rows' remaining entries (hc_beg / hc_end index these)
+    double *hs_val = nullptr;            // repacked heavy-slot blocks: per slot ceil(3 od / 2) x 64 double2
+    double *hs_part = nullptr;           // per heavy slot: 6 partial sums of the heavy row
+    double *hqf = nullptr;               // per heavy dof: q = (H + lambda I) p of the heavy rows
     int32_t nB = 0;                      // workgroups of the vertex launches (setup / update)
     const int64_t *ent_begin = nullptr;
     const PcgEnt *ent = nullptr;
@@ -66,21 +111,27 @@ struct PcgDev {
     const int64_t *voff = nullptr;
     const int32_t *vdim = nullptr;
     double *minv = nullptr;              // (H_vv + lambda I)^-1 per vertex
-    double *r = nullptr, *z = nullptr, *p[2] = {nullptr, nullptr}, *q = nullptr;
+    double *r = nullptr;
+    double *zp = nullptr;                // (z, p_prev) per dof
+    double *pq = nullptr;                // (p, q) per dof
     double *hq = nullptr;                // per heavy chunk: 6 partial row sums
-    double *partA = nullptr;             // per light workgroup of the product: p.q
+    double *partA = nullptr;             // per sliced / light workgroup of the product: p.q
     double *partB = nullptr;             // per vertex workgroup: (r.z, r.r)
     double *rec = nullptr;               // (max_it + 2) x kPcgRec
     int32_t max_it = 0;
     double tol2 = 0;                     // squared relative residual tolerance
 };
 
+// after an assembly: the sliced rows' 3x3 blocks from hval into sl_val
+void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st);
 // one solve's launches (x = dx).  setup: preconditioner blocks at lambda, r = b, z = M r, x = 0.
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
                       hipStream_t st);
 // iteration it: product q = (H + lambda I) p (p = z + beta p_prev formed on the fly) after the
 // convergence test of the residual the previous update left
 void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st);
+// iteration it: the heavy rows' q from their slot partials and chunk partials (one workgroup per dof)
+void launch_pcg_heavy(const PcgDev &G, int it, double lambda, hipStream_t st);
 // iteration it: alpha, x += alpha p, r -= alpha q, z = M r, partial (r.z, r.r)
 void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStream_t st);
 

@@ -21,10 +21,19 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 
 #include "kernels.h"
 #include "pcg.h"
+
+// launch shape of the product (A/B builds: make PCG_WPE=.. PCG_BATCH=..)
+#ifndef DEFTRI_PCG_WPE
+#define DEFTRI_PCG_WPE 4
+#endif
+#ifndef DEFTRI_PCG_BATCH
+#define DEFTRI_PCG_BATCH 1
+#endif
 
 namespace deftri {
 namespace dev {
@@ -40,20 +49,19 @@ __device__ __forceinline__ PcgEnt load_ent(const PcgEnt *__restrict__ ent, int64
 }
 
 // p of a dof, formed where it is read: z + beta p_prev (one fma everywhere, so every reader agrees)
-__device__ __forceinline__ double pval(const double *__restrict__ z, const double *__restrict__ pp, double beta,
-                                       int64_t i) {
-    return __fma_rn(beta, pp[i], z[i]);
+__device__ __forceinline__ double pval(const double *__restrict__ zp, double beta, int64_t i) {
+    const double2 v = reinterpret_cast<const double2 *>(zp)[i];
+    return __fma_rn(beta, v.y, v.x);
 }
 
 // acc[0..d) += B p_other for one entry of the row (B the block in this row's orientation)
 __device__ __forceinline__ void ent_acc(const PcgEnt &E, int d, const double *__restrict__ hval,
-                                        const double *__restrict__ z, const double *__restrict__ pp, double beta,
-                                        double acc[6]) {
+                                        const double *__restrict__ zp, double beta, double acc[6]) {
     const double *h = hval + E.val_off;
     const int od = E.odim;
     double pj[6];
 #pragma unroll
-    for (int j = 0; j < 6; j++) pj[j] = j < od ? pval(z, pp, beta, E.odof + j) : 0.0;
+    for (int j = 0; j < 6; j++) pj[j] = j < od ? pval(zp, beta, E.odof + j) : 0.0;
     if (!E.tr) {
 #pragma unroll
         for (int i = 0; i < 6; i++)
@@ -101,6 +109,105 @@ __device__ __forceinline__ void wg_sum2(const double *__restrict__ part, int n, 
     s0 = red[0][0];
     s1 = red[1][0];
     __syncthreads();
+}
+
+__device__ __forceinline__ void wg_pair_tree(double a0, double a1, double (*red)[256], double *out) {
+    red[0][threadIdx.x] = a0;
+    red[1][threadIdx.x] = a1;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + off];
+            red[1][threadIdx.x] += red[1][threadIdx.x + off];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { out[0] = red[0][0]; out[1] = red[1][0]; }
+}
+
+// one heavy slot of a slice (heavy vertex of dimension OD): the row side acc += B p_heavy, and the
+// heavy row's side B^T p_row summed over the 64 lanes by a fixed butterfly into part[0..OD).  B is
+// 3 x OD in the row's orientation, row-major, in ceil(3 OD / 2) lane-interleaved double2.
+template <int OD>
+__device__ __forceinline__ void heavy_slot(const double2 *__restrict__ hb, int64_t oh, const double *__restrict__ zp,
+                                           double beta, const double pv[3], double acc[6], double *__restrict__ part,
+                                           int lane) {
+    constexpr int NQ = (3 * OD + 1) / 2;
+    double B[2 * NQ], ph[OD], cc[OD];
+#pragma unroll
+    for (int q2 = 0; q2 < NQ; q2++) {
+        const double2 t = hb[q2 * 64];
+        B[2 * q2] = t.x;
+        B[2 * q2 + 1] = t.y;
+    }
+#pragma unroll
+    for (int j = 0; j < OD; j++) ph[j] = pval(zp, beta, oh + j);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < OD; j++) acc[i] += B[i * OD + j] * ph[j];
+#pragma unroll
+    for (int j = 0; j < OD; j++) cc[j] = (B[j] * pv[0] + B[OD + j] * pv[1]) + B[2 * OD + j] * pv[2];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int j = 0; j < OD; j++) cc[j] += __shfl_xor(cc[j], off, 64);
+    if (lane < OD) {
+        double cj = cc[0];
+#pragma unroll
+        for (int j = 1; j < OD; j++) cj = lane == j ? cc[j] : cj;
+        part[lane] = cj;
+    }
+}
+
+// sliced rows' 3x3 blocks -> slot-major, lane-interleaved copies in the rows' orientation
+__global__ void __launch_bounds__(256) k_pcg_repack(const PcgDev G, const double *__restrict__ hval) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= G.nslots * 64) {
+        // heavy slots: 3 x od blocks (row orientation) into 3 x 6, zero padded
+        const int64_t u = t - G.nslots * 64;
+        if (u >= G.nhslots * 64) return;
+        const int64_t g = u >> 6;
+        const int64_t m = G.hs_map[u];
+        double2 *dst = reinterpret_cast<double2 *>(G.hs_val) + G.hs_voff[g] + (u & 63);
+        const int od = G.vdim[G.heavy_v[G.hs_hk[g]]];
+        const double *h = hval + (m < 0 ? 0 : (m & ((1LL << 62) - 1)));
+        const bool tr = m >= 0 && ((m >> 62) & 1);
+        double v[18];
+#pragma unroll
+        for (int q = 0; q < 18; q++) v[q] = 0.0;
+        if (m >= 0)
+#pragma unroll
+            for (int i = 0; i < 3; i++)
+#pragma unroll
+                for (int j = 0; j < 6; j++)
+                    if (j < od) v[i * od + j] = tr ? h[j * 3 + i] : h[i * od + j];
+        const int nq = (3 * od + 1) / 2;
+#pragma unroll
+        for (int q2 = 0; q2 < 9; q2++)
+            if (q2 < nq) dst[q2 * 64] = make_double2(v[2 * q2], v[2 * q2 + 1]);
+        return;
+    }
+    const int64_t m = G.sl_map[t];
+    double2 *dst = reinterpret_cast<double2 *>(G.sl_val) + (t >> 6) * 320 + (t & 63);
+    double v[10];
+    if (m < 0) {
+#pragma unroll
+        for (int q = 0; q < 9; q++) v[q] = 0.0;
+    } else {
+        const double *h = hval + (m & ((1LL << 62) - 1));
+        const bool tr = (m >> 62) & 1;
+        double u[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) u[q] = h[q];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) v[i * 3 + j] = tr ? u[j * 3 + i] : u[i * 3 + j];
+    }
+    v[9] = __longlong_as_double((long long)G.sl_col[t]);
+#pragma unroll
+    for (int q2 = 0; q2 < 5; q2++) dst[q2 * 64] = make_double2(v[2 * q2], v[2 * q2 + 1]);
 }
 
 // per vertex: M_v = (H_vv + lambda I)^-1 through its Cholesky factor; r = b, z = M r, x = 0, p = 0
@@ -170,6 +277,7 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
         }
 #pragma unroll
         for (int i = 0; i < 6; i++) rv[i] = i < d ? b[o + i] : 0.0;
+        double2 *zp = reinterpret_cast<double2 *>(G.zp);
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             if (i < d) {
@@ -178,29 +286,17 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
                 for (int j = 0; j < 6; j++)
                     if (j < d) zi += Mi[i * 6 + j] * rv[j];
                 G.r[o + i] = rv[i];
-                G.z[o + i] = zi;
-                G.p[0][o + i] = 0.0;
-                G.p[1][o + i] = 0.0;
+                zp[o + i] = make_double2(zi, 0.0);
                 x[o + i] = 0.0;
                 rz += rv[i] * zi;
                 rr += rv[i] * rv[i];
             }
         }
     }
-    red[0][threadIdx.x] = rz;
-    red[1][threadIdx.x] = rr;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + off];
-            red[1][threadIdx.x] += red[1][threadIdx.x + off];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) { G.partB[2 * blockIdx.x] = red[0][0]; G.partB[2 * blockIdx.x + 1] = red[1][0]; }
+    wg_pair_tree(rz, rr, red, G.partB + 2 * blockIdx.x);
 }
 
-__global__ void __launch_bounds__(256) k_pcg_product(int it, const PcgDev G, const double *__restrict__ hval,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_PCG_WPE))) k_pcg_product(int it, const PcgDev G, const double *__restrict__ hval,
                                                      double lam) {
     __shared__ double red[6][256];
     double *rec = G.rec + kPcgRec * (it + 1);
@@ -222,42 +318,128 @@ __global__ void __launch_bounds__(256) k_pcg_product(int it, const PcgDev G, con
     }
     if (conv) return;
     const double beta = it == 0 ? 0.0 : rz / prv[PR_RZ];
-    const double *pp = G.p[it & 1];
-    double *pn = G.p[(it + 1) & 1];
-    const double *z = G.z;
-    if ((int)blockIdx.x < G.nA_light) {
-        const int k = blockIdx.x * 256 + tid;
-        double pq = 0.0;
+    const double *zp = G.zp;
+    double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
+    if ((int)blockIdx.x < G.nA_sl) {
+        // sliced rows: one slice (64 rows, lane = row) per workgroup; its four waves take every
+        // fourth slot of each kind, so a wave's dependent chain (column index -> gather) is a
+        // quarter of the slice's; every load is coalesced but the (z, p_prev) gathers.  The four
+        // partial row sums meet in LDS in a fixed order.
+        const int sl = blockIdx.x;
+        const int w = tid >> 6, lane = tid & 63;
+        const int v = G.sl_v[sl * 64 + lane];
+        const int64_t o = v >= 0 ? G.voff[v] : 0;
+        double pv[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) pv[i] = v >= 0 ? pval(zp, beta, o + i) : 0.0;
+        double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        const int64_t g0 = G.sl_off[sl];
+        const int ns = G.sl_n[sl];
+        constexpr int kSlotBatch = DEFTRI_PCG_BATCH;   // slots of one wave in flight together
+        const double2 *slv = reinterpret_cast<const double2 *>(G.sl_val);
+        for (int k0 = w; k0 < ns; k0 += 4 * kSlotBatch) {
+            // per lane and slot: five 16-byte loads = the 3x3 block + the column dof
+            int c[kSlotBatch];
+            double h[kSlotBatch][10], pj[kSlotBatch][3];
+#pragma unroll
+            for (int u = 0; u < kSlotBatch; u++) {
+                const bool in = k0 + 4 * u < ns;
+                const double2 *hv = slv + (g0 + k0 + 4 * u) * 320 + lane;
+#pragma unroll
+                for (int q2 = 0; q2 < 5; q2++) {
+                    const double2 t = in ? hv[q2 * 64] : make_double2(0.0, 0.0);
+                    h[u][2 * q2] = t.x;
+                    h[u][2 * q2 + 1] = t.y;
+                }
+                c[u] = in ? (int)__double_as_longlong(h[u][9]) : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kSlotBatch; u++)
+#pragma unroll
+                for (int j = 0; j < 3; j++) pj[u][j] = c[u] >= 0 ? pval(zp, beta, c[u] + j) : 0.0;
+#pragma unroll
+            for (int u = 0; u < kSlotBatch; u++)
+                if (c[u] >= 0)
+#pragma unroll
+                    for (int i = 0; i < 3; i++)
+#pragma unroll
+                        for (int j = 0; j < 3; j++) acc[i] += h[u][i * 3 + j] * pj[u][j];
+        }
+        // couplings to heavy vertices: the row side B p_heavy, and the heavy row's side B^T p_row
+        // reduced over the slice's lanes (fixed butterfly) into the slot's partial
+        const int64_t h0 = G.sl_hoff[sl];
+        const int nh = G.sl_hn[sl];
+        for (int k = w; k < nh; k += 4) {
+            const int64_t g = h0 + k;
+            const int hv = G.heavy_v[G.hs_hk[g]];
+            const int64_t oh = G.voff[hv];
+            const double2 *hb = reinterpret_cast<const double2 *>(G.hs_val) + G.hs_voff[g] + lane;
+            double *part = G.hs_part + G.hs_pos[g] * 6;     // heavy-vertex-major: k_pcg_heavy reads runs
+            switch (G.vdim[hv]) {
+                case 6: heavy_slot<6>(hb, oh, zp, beta, pv, acc, part, lane); break;
+                case 1: heavy_slot<1>(hb, oh, zp, beta, pv, acc, part, lane); break;
+                case 2: heavy_slot<2>(hb, oh, zp, beta, pv, acc, part, lane); break;
+                case 3: heavy_slot<3>(hb, oh, zp, beta, pv, acc, part, lane); break;
+                case 4: heavy_slot<4>(hb, oh, zp, beta, pv, acc, part, lane); break;
+                default: heavy_slot<5>(hb, oh, zp, beta, pv, acc, part, lane); break;
+            }
+        }
+        const int64_t x0 = G.sl_xoff[sl];
+        const int nx = G.sl_nx[sl];
+        for (int k = w; k < nx; k += 4) {
+            const PcgEnt E = load_ent(G.sl_x, (x0 + k) * 64 + lane);
+            if (E.odim) ent_acc(E, 3, hval, zp, beta, acc);
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) red[i][tid] = acc[i];
+        __syncthreads();
+        double pqs = 0.0;
+        if (w == 0 && v >= 0) {
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const double a = (red[i][lane] + red[i][64 + lane]) + (red[i][128 + lane] + red[i][192 + lane]);
+                const double qv = a + lam * pv[i];
+                pq2[o + i] = make_double2(pv[i], qv);
+                pqs += pv[i] * qv;
+            }
+        }
+        __syncthreads();
+        const double s = wg_tree(pqs, red[3]);
+        if (tid == 0) G.partA[blockIdx.x] = s;
+        return;
+    }
+    if ((int)blockIdx.x < G.nA_sl + G.nA_light) {
+        const int k = (blockIdx.x - G.nA_sl) * 256 + tid;
+        double pqs = 0.0;
         if (k < G.nlight) {
             const int v = G.light_v[k];
             const int d = G.vdim[v];
             const int64_t o = G.voff[v];
             double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
             const int64_t e1 = G.ent_begin[v + 1];
-            for (int64_t e = G.ent_begin[v]; e < e1; e++) ent_acc(load_ent(G.ent, e), d, hval, z, pp, beta, acc);
+            for (int64_t e = G.ent_begin[v]; e < e1; e++) ent_acc(load_ent(G.ent, e), d, hval, zp, beta, acc);
 #pragma unroll
             for (int i = 0; i < 6; i++) {
                 if (i < d) {
-                    const double pv = pval(z, pp, beta, o + i);
+                    const double pv = pval(zp, beta, o + i);
                     const double qv = acc[i] + lam * pv;
-                    pn[o + i] = pv;
-                    G.q[o + i] = qv;
-                    pq += pv * qv;
+                    pq2[o + i] = make_double2(pv, qv);
+                    pqs += pv * qv;
                 }
             }
         }
-        const double s = wg_tree(pq, red[0]);
+        const double s = wg_tree(pqs, red[0]);
         if (tid == 0) G.partA[blockIdx.x] = s;
         return;
     }
     // a chunk of a heavy row: partial sums of its entries, reduced in a fixed tree
-    const int c = blockIdx.x - G.nA_light;
+    const int c = blockIdx.x - G.nA_sl - G.nA_light;
     const int hk = G.hc_vertex[c];
     const int v = G.heavy_v[hk];
     const int d = G.vdim[v];
     double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     const int64_t e1 = G.hc_end[c];
-    for (int64_t e = G.hc_beg[c] + tid; e < e1; e += 256) ent_acc(load_ent(G.ent, e), d, hval, z, pp, beta, acc);
+    for (int64_t e = G.hc_beg[c] + tid; e < e1; e += 256) ent_acc(load_ent(G.hres, e), d, hval, zp, beta, acc);
 #pragma unroll
     for (int i = 0; i < 6; i++) red[i][tid] = acc[i];
     __syncthreads();
@@ -271,39 +453,55 @@ __global__ void __launch_bounds__(256) k_pcg_product(int it, const PcgDev G, con
         G.hq[6 * c + tid] = red[tid][0];
         if (c == G.h_first[hk]) {
             const int64_t o = G.voff[v];
-            pn[o + tid] = pval(z, pp, beta, o + tid);
+            pq2[o + tid] = make_double2(pval(zp, beta, o + tid), 0.0);
         }
+    }
+}
+
+// one workgroup per heavy dof: q = (slot partials, fixed tree) + (chunk partials, in order) + lambda p
+__global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, double lam) {
+    __shared__ double red[256];
+    const double *rec = G.rec + kPcgRec * (it + 1);
+    if (rec[PR_STATUS] != 0.0) return;
+    const int k = blockIdx.x;
+    int hk = 0;
+    while (G.h_dofbase[hk + 1] <= k) hk++;
+    const int i = k - G.h_dofbase[hk];
+    const int64_t b0 = G.hv_slot_begin[hk], b1 = G.hv_slot_begin[hk + 1];
+    // four independent strided streams per thread (loads in flight together), combined in order
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t t = b0 + threadIdx.x; t < b1; t += 1024)
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (t + 256 * u < b1) a[u] += G.hs_part[(t + 256 * u) * 6 + i];
+    const double s = wg_tree((a[0] + a[1]) + (a[2] + a[3]), red);
+    if (threadIdx.x == 0) {
+        double q = s;
+        for (int c = G.h_first[hk]; c < G.h_first[hk + 1]; c++) q += G.hq[6 * c + i];
+        const double pv = reinterpret_cast<const double2 *>(G.pq)[G.voff[G.heavy_v[hk]] + i].x;
+        G.hqf[k] = q + lam * pv;
     }
 }
 
 __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, double lam, double *__restrict__ x) {
     __shared__ double red[2][256];
-    __shared__ double hqs[kPcgMaxHeavyDofs];
-    __shared__ double hps[kPcgMaxHeavyDofs];
     double *rec = G.rec + kPcgRec * (it + 1);
     if (rec[PR_STATUS] != 0.0) return;
     const int tid = threadIdx.x;
-    const double *pn = G.p[(it + 1) & 1];
+    const double2 *pq2 = reinterpret_cast<const double2 *>(G.pq);
+    const int nA = G.nA_sl + G.nA_light;
     const double pq_light = wg_tree([&] {
         double a = 0.0;
-        for (int i = tid; i < G.nA_light; i += 256) a += G.partA[i];
+        for (int i = tid; i < nA; i += 256) a += G.partA[i];
         return a;
     }(), red[0]);
-    // the heavy rows: chunk partials summed in chunk order, + lambda p
-    for (int k = tid; k < G.nheavy_dofs; k += 256) {
-        int hk = 0;
-        while (G.h_dofbase[hk + 1] <= k) hk++;
-        const int i = k - G.h_dofbase[hk];
-        double s = 0.0;
-        for (int c = G.h_first[hk]; c < G.h_first[hk + 1]; c++) s += G.hq[6 * c + i];
-        const double pv = pn[G.voff[G.heavy_v[hk]] + i];
-        hqs[k] = s + lam * pv;
-        hps[k] = pv;
-    }
-    __syncthreads();
+    // the heavy rows' p.q (their q from k_pcg_heavy), in heavy-dof order
     if (tid == 0) {
         double a = 0.0;
-        for (int k = 0; k < G.nheavy_dofs; k++) a += hps[k] * hqs[k];
+        for (int hk = 0; hk < G.nheavy; hk++) {
+            const int64_t o = G.voff[G.heavy_v[hk]];
+            for (int i = 0; i < G.h_dofbase[hk + 1] - G.h_dofbase[hk]; i++) a += pq2[o + i].x * G.hqf[G.h_dofbase[hk] + i];
+        }
         red[1][0] = a;
     }
     __syncthreads();
@@ -321,18 +519,22 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
         const int d = G.vdim[v];
         const int64_t o = G.voff[v];
         const int hk = G.v_heavy[v];
-        double rv[6];
+        double rv[6], pv[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             rv[i] = 0.0;
+            pv[i] = 0.0;
             if (i < d) {
-                const double qv = hk < 0 ? G.q[o + i] : hqs[G.h_dofbase[hk] + i];
-                x[o + i] += alpha * pn[o + i];
+                const double2 w = pq2[o + i];
+                const double qv = hk < 0 ? w.y : G.hqf[G.h_dofbase[hk] + i];
+                pv[i] = w.x;
+                x[o + i] += alpha * w.x;
                 rv[i] = G.r[o + i] - alpha * qv;
                 G.r[o + i] = rv[i];
             }
         }
         const double *M = G.minv + G.moff[v];
+        double2 *zp = reinterpret_cast<double2 *>(G.zp);
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             if (i < d) {
@@ -340,26 +542,24 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
 #pragma unroll
                 for (int j = 0; j < 6; j++)
                     if (j < d) zi += M[i * d + j] * rv[j];
-                G.z[o + i] = zi;
+                zp[o + i] = make_double2(zi, pv[i]);
                 rz += rv[i] * zi;
                 rr += rv[i] * rv[i];
             }
         }
     }
-    red[0][tid] = rz;
-    red[1][tid] = rr;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off) {
-            red[0][tid] += red[0][tid + off];
-            red[1][tid] += red[1][tid + off];
-        }
-        __syncthreads();
-    }
-    if (tid == 0) { G.partB[2 * blockIdx.x] = red[0][0]; G.partB[2 * blockIdx.x + 1] = red[1][0]; }
+    wg_pair_tree(rz, rr, red, G.partB + 2 * blockIdx.x);
 }
 
 }  // namespace dev
+
+void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st) {
+    if (G.nslots + G.nhslots <= 0) return;
+    hipEvent_t e0 = prof_begin(st);
+    const unsigned grid = (unsigned)(((G.nslots + G.nhslots) * 64 + 255) / 256);
+    hipLaunchKernelGGL(dev::k_pcg_repack, dim3(grid), dim3(256), 0, st, G, hval);
+    prof_end("pcg_repack", e0, grid, 0.0, st);
+}
 
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
                       hipStream_t st) {
@@ -371,8 +571,16 @@ void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, doub
 
 void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st) {
     hipEvent_t e0 = prof_begin(st);
-    hipLaunchKernelGGL(dev::k_pcg_product, dim3(G.nA_light + G.nhchunks), dim3(256), 0, st, it, G, hval, lambda);
-    prof_end("pcg_product", e0, G.nA_light + G.nhchunks, 0.0, st);
+    const unsigned grid = (unsigned)(G.nA_sl + G.nA_light + G.nhchunks);
+    hipLaunchKernelGGL(dev::k_pcg_product, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
+    prof_end("pcg_product", e0, grid, 0.0, st);
+}
+
+void launch_pcg_heavy(const PcgDev &G, int it, double lambda, hipStream_t st) {
+    if (G.nheavy_dofs <= 0) return;
+    hipEvent_t e0 = prof_begin(st);
+    hipLaunchKernelGGL(dev::k_pcg_heavy, dim3(G.nheavy_dofs), dim3(256), 0, st, it, G, lambda);
+    prof_end("pcg_heavy", e0, G.nheavy_dofs, 0.0, st);
 }
 
 void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStream_t st) {
@@ -385,7 +593,8 @@ void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStr
 bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vector<int32_t> &vdim,
                     const std::vector<int64_t> &blk_val_off, const std::vector<int32_t> &blk_rows,
                     const std::vector<int32_t> &blk_cols, const std::vector<int64_t> &blk_row_dof,
-                    const std::vector<int64_t> &blk_col_dof, PcgHost &H, std::string &err) {
+                    const std::vector<int64_t> &blk_col_dof, const std::vector<int64_t> &elim_pos, PcgHost &H,
+                    std::string &err) {
     H = PcgHost();
     const int64_t nb = (int64_t)blk_val_off.size();
     int64_t ndof = nv > 0 ? voff[nv - 1] + vdim[nv - 1] : 0;
@@ -422,21 +631,154 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     H.v_heavy.assign(nv, -1);
     H.h_first.push_back(0);
     H.h_dofbase.push_back(0);
+    // A/B knobs (measurements in DESIGN.md): heavy-row chunk size, rows sliced or all generic
+    static const int64_t chunk = [] { const char *e = std::getenv("DEFTRI_PCG_CHUNK"); return e ? std::max(64, std::atoi(e)) : kPcgChunk; }();
+    static const bool no_slice = std::getenv("DEFTRI_PCG_NO_SLICE") != nullptr;
+    std::vector<int32_t> sliced;
     for (int64_t v = 0; v < nv; v++) {
         const int64_t n = H.ent_begin[v + 1] - H.ent_begin[v];
-        if (n <= kPcgHeavy) { H.light_v.push_back((int32_t)v); continue; }
-        const int32_t hk = (int32_t)H.heavy_v.size();
-        H.v_heavy[v] = hk;
-        H.heavy_v.push_back((int32_t)v);
-        for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e += kPcgChunk) {
-            H.hc_vertex.push_back(hk);
-            H.hc_beg.push_back(e);
-            H.hc_end.push_back(std::min<int64_t>(e + kPcgChunk, H.ent_begin[v + 1]));
+        if (n > kPcgHeavy) {
+            H.v_heavy[v] = (int32_t)H.heavy_v.size();
+            H.heavy_v.push_back((int32_t)v);
+            H.h_dofbase.push_back(H.h_dofbase.back() + vdim[v]);
+        } else if (vdim[v] == 3 && !no_slice) {
+            sliced.push_back((int32_t)v);
+        } else {
+            H.light_v.push_back((int32_t)v);
         }
-        H.h_first.push_back((int32_t)H.hc_vertex.size());
-        H.h_dofbase.push_back(H.h_dofbase.back() + vdim[v]);
     }
     if (H.h_dofbase.back() > kPcgMaxHeavyDofs) { err = "pcg: too many heavy-row dofs"; return false; }
+    std::vector<char> is_sliced(nv, 0);
+    for (int32_t v : sliced) is_sliced[v] = 1;
+    // heavy rows: the entries whose other vertex is not a sliced row stay as entries, in chunks (the
+    // sliced rows' couplings to heavy vertices come back as per-slice reductions)
+    H.hres.clear();
+    for (int32_t hk = 0; hk < (int32_t)H.heavy_v.size(); hk++) {
+        const int32_t v = H.heavy_v[hk];
+        const int64_t b0 = (int64_t)H.hres.size();
+        for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e++) {
+            const int32_t u = dof_v[H.ent[e].odof];
+            if (!is_sliced[u]) H.hres.push_back(H.ent[e]);
+        }
+        const int64_t b1 = (int64_t)H.hres.size();
+        for (int64_t e = b0; e < b1; e += chunk) {
+            H.hc_vertex.push_back(hk);
+            H.hc_beg.push_back(e);
+            H.hc_end.push_back(std::min<int64_t>(e + chunk, b1));
+        }
+        H.h_first.push_back((int32_t)H.hc_vertex.size());
+    }
+    // sliced rows: nested-dissection order, by descending count of 3x3 blocks inside each window
+    // (ties in that order), 64 per slice.  A row's entries: 3x3 blocks to light points -> 3x3 slots;
+    // blocks to heavy vertices -> heavy slots (one per heavy vertex the slice couples to, shared by
+    // its lanes); the rest -> extra entries
+    auto cls = [&](const PcgEnt &E) {      // 0: 3x3 slot, 1: heavy slot, 2: extra entry
+        const int32_t u = dof_v[E.odof];
+        if (H.v_heavy[u] >= 0) return 1;
+        return E.odim == 3 ? 0 : 2;
+    };
+    std::vector<int64_t> cnt3(nv, 0), cntx(nv, 0);
+    for (int32_t v : sliced)
+        for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e++) {
+            const int c = cls(H.ent[e]);
+            cnt3[v] += c == 0;
+            cntx[v] += c == 2;
+        }
+    std::sort(sliced.begin(), sliced.end(), [&](int32_t a, int32_t b) { return elim_pos[a] < elim_pos[b]; });
+    for (size_t w = 0; w < sliced.size(); w += kPcgSortWindow)
+        std::stable_sort(sliced.begin() + w, sliced.begin() + std::min(sliced.size(), w + kPcgSortWindow),
+                         [&](int32_t a, int32_t b) { return cnt3[a] > cnt3[b]; });
+    const int64_t nsl = ((int64_t)sliced.size() + 63) / 64;
+    H.sl_v.assign(nsl * 64, -1);
+    H.sl_n.resize(nsl); H.sl_nx.resize(nsl); H.sl_off.resize(nsl); H.sl_xoff.resize(nsl);
+    H.sl_hn.resize(nsl); H.sl_hoff.resize(nsl);
+    std::vector<std::vector<int32_t>> sl_heavy(nsl);        // heavy vertices each slice couples to
+    int64_t slots = 0, xslots = 0, hslots = 0;
+    for (int64_t sl = 0; sl < nsl; sl++) {
+        int64_t mn = 0, mx = 0;
+        for (int l = 0; l < 64 && sl * 64 + l < (int64_t)sliced.size(); l++) {
+            const int32_t v = sliced[sl * 64 + l];
+            H.sl_v[sl * 64 + l] = v;
+            mn = std::max(mn, cnt3[v]);
+            mx = std::max(mx, cntx[v]);
+            for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e++)
+                if (cls(H.ent[e]) == 1) sl_heavy[sl].push_back(H.v_heavy[dof_v[H.ent[e].odof]]);
+        }
+        std::sort(sl_heavy[sl].begin(), sl_heavy[sl].end());
+        sl_heavy[sl].erase(std::unique(sl_heavy[sl].begin(), sl_heavy[sl].end()), sl_heavy[sl].end());
+        H.sl_n[sl] = (int32_t)mn; H.sl_nx[sl] = (int32_t)mx; H.sl_hn[sl] = (int32_t)sl_heavy[sl].size();
+        H.sl_off[sl] = slots; H.sl_xoff[sl] = xslots; H.sl_hoff[sl] = hslots;
+        slots += mn; xslots += mx; hslots += (int64_t)sl_heavy[sl].size();
+    }
+    H.sl_map.assign(slots * 64, -1);
+    H.sl_col.assign(slots * 64, 0);
+    H.sl_x.assign(xslots * 64, PcgEnt{0, 0, 0, 0});
+    H.hs_map.assign(hslots * 64, -1);
+    H.hs_hk.resize(hslots);
+    H.hs_voff.resize(hslots);
+    for (int64_t sl = 0; sl < nsl; sl++) {
+        for (size_t k = 0; k < sl_heavy[sl].size(); k++) H.hs_hk[H.sl_hoff[sl] + k] = sl_heavy[sl][k];
+        for (int l = 0; l < 64; l++) {
+            const int32_t v = H.sl_v[sl * 64 + l];
+            if (v < 0) continue;
+            int64_t k3 = 0, kx = 0;
+            for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e++) {
+                const PcgEnt &E = H.ent[e];
+                const int c = cls(E);
+                if (c == 0) {
+                    const int64_t g = H.sl_off[sl] + k3++;
+                    H.sl_map[g * 64 + l] = E.val_off | ((int64_t)(E.tr ? 1 : 0) << 62);
+                    H.sl_col[g * 64 + l] = E.odof;
+                } else if (c == 1) {
+                    const int32_t hk = H.v_heavy[dof_v[E.odof]];
+                    const auto it = std::lower_bound(sl_heavy[sl].begin(), sl_heavy[sl].end(), hk);
+                    const int64_t g = H.sl_hoff[sl] + (it - sl_heavy[sl].begin());
+                    if (H.hs_map[g * 64 + l] != -1) { err = "pcg: two blocks between one row and one heavy vertex"; return false; }
+                    H.hs_map[g * 64 + l] = E.val_off | ((int64_t)(E.tr ? 1 : 0) << 62);
+                } else {
+                    H.sl_x[(H.sl_xoff[sl] + kx++) * 64 + l] = E;
+                }
+            }
+        }
+    }
+    int64_t hsv = 0, hs_bytes = 0;
+    for (int64_t g = 0; g < hslots; g++) {
+        const int nq = (3 * vdim[H.heavy_v[H.hs_hk[g]]] + 1) / 2;
+        H.hs_voff[g] = hsv;
+        hsv += 64 * (int64_t)nq;
+        hs_bytes += 64 * 16 * (int64_t)nq;
+    }
+    H.hs_size = 2 * hsv;
+    // per heavy vertex: its slots, ascending (the order its row sums their partials in); a slot's
+    // partial lands at its position in that order
+    H.hv_slot_begin.assign(H.heavy_v.size() + 1, 0);
+    for (int64_t g = 0; g < hslots; g++) H.hv_slot_begin[H.hs_hk[g] + 1]++;
+    for (size_t k = 0; k < H.heavy_v.size(); k++) H.hv_slot_begin[k + 1] += H.hv_slot_begin[k];
+    H.hs_pos.resize(hslots);
+    {
+        std::vector<int64_t> f(H.hv_slot_begin.begin(), H.hv_slot_begin.end() - 1);
+        for (int64_t g = 0; g < hslots; g++) H.hs_pos[g] = f[H.hs_hk[g]]++;
+    }
+    // bytes a product launch loads / stores apart from the neighbours' (z, p_prev) gathers: own
+    // (z, p_prev) read and (p, q) written, repacked 3x3 slots with column indices and heavy slots
+    // (padding included), the extra entries with their blocks, the generic rows' and heavy rows'
+    // remaining entries with their blocks; flops: 2 per block entry of H
+    {
+        int64_t ndof_ = nv > 0 ? voff[nv - 1] + vdim[nv - 1] : 0;
+        double by = 32.0 * (double)ndof_ + 64.0 * 80.0 * (double)slots + (double)hs_bytes +
+                    16.0 * (double)H.sl_x.size() + 8.0 * 6.0 * (double)hslots;
+        double fl = 0;
+        for (int64_t v = 0; v < nv; v++)
+            for (int64_t e = H.ent_begin[v]; e < H.ent_begin[v + 1]; e++) {
+                const PcgEnt &E = H.ent[e];
+                fl += 2.0 * vdim[v] * E.odim;
+                if (is_sliced[v]) { if (cls(E) == 2) by += 8.0 * 3 * E.odim; continue; }
+                if (H.v_heavy[v] >= 0 && is_sliced[dof_v[E.odof]]) continue;   // via the heavy slots
+                by += 16.0 + 8.0 * vdim[v] * E.odim;
+            }
+        H.product_bytes = by;
+        H.product_flops = fl;
+    }
     H.moff.resize(nv);
     for (int64_t v = 0; v < nv; v++) { H.moff[v] = H.msize; H.msize += (int64_t)vdim[v] * vdim[v]; }
     return true;

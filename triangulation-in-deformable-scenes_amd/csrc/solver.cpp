@@ -158,6 +158,7 @@ struct deftri_ctx {
     int pcg_auto_it = kPcgDefaultMaxIt;     // default budget of the uploaded plan (cost model)
     int pcg_last_its = 8;                   // iterations of the last converged solve (first chunk size)
     int pcg_step_its = 0, pcg_step_solved = 0;   // the last PCG step (deftri_last_step_info)
+    bool pcg_packed = false;                // sliced blocks repacked from the current assembly
 };
 
 namespace {
@@ -453,7 +454,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     } else {
         PcgHost ph;
         if (!build_pcg_host(S.nv, S.voff, S.vdim, S.blk_val_off, S.blk_rows, S.blk_cols, S.blk_row_dof, S.blk_col_dof,
-                            ph, ctx->pcg_why)) {
+                            S.elim_pos, ph, ctx->pcg_why)) {
             ctx->pcg_why = "row view: " + ctx->pcg_why;
         } else {
             PcgDev &G = ctx->G;
@@ -464,6 +465,9 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
             G.nhchunks = (int32_t)ph.hc_vertex.size();
             G.nheavy_dofs = ph.h_dofbase.back();
             G.nA_light = (G.nlight + 255) / 256;
+            G.nsl = (int32_t)ph.sl_n.size();
+            G.nA_sl = G.nsl;                  // one workgroup per slice
+            G.nslots = (int64_t)ph.sl_map.size() / 64;
             G.nB = (int32_t)((S.nv + 255) / 256);
             int64_t *eb, *hb, *he, *dg, *mo;
             PcgEnt *en;
@@ -474,20 +478,39 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
             G.ent_begin = eb; G.ent = en; G.light_v = lv; G.heavy_v = hv; G.hc_vertex = hcv; G.hc_beg = hb;
             G.hc_end = he; G.h_first = hf; G.h_dofbase = hdb; G.v_heavy = vh; G.diag_off = dg; G.moff = mo;
             G.voff = L.voff; G.vdim = L.vdim;
+            {
+                int32_t *sv, *sn, *snx, *scol;
+                int64_t *soff, *sxoff, *smap;
+                PcgEnt *sx;
+                PUT(sv, ph.sl_v); PUT(sn, ph.sl_n); PUT(snx, ph.sl_nx); PUT(scol, ph.sl_col);
+                PUT(soff, ph.sl_off); PUT(sxoff, ph.sl_xoff); PUT(smap, ph.sl_map); PUT(sx, ph.sl_x);
+                G.sl_v = sv; G.sl_n = sn; G.sl_nx = snx; G.sl_col = scol; G.sl_off = soff; G.sl_xoff = sxoff;
+                G.sl_map = smap; G.sl_x = sx;
+                if ((rc = dalloc(ctx, &G.sl_val, 640 * std::max<int64_t>(G.nslots, 1)))) return rc;
+                int32_t *shn, *hshk;
+                int64_t *shoff, *hsmap, *hvb, *hvs;
+                PcgEnt *hres;
+                PUT(shn, ph.sl_hn); PUT(hshk, ph.hs_hk); PUT(shoff, ph.sl_hoff); PUT(hsmap, ph.hs_map);
+                PUT(hvb, ph.hv_slot_begin); PUT(hvs, ph.hs_pos); PUT(hres, ph.hres);
+                int64_t *hsvo;
+                PUT(hsvo, ph.hs_voff);
+                G.hs_voff = hsvo;
+                G.sl_hn = shn; G.hs_hk = hshk; G.sl_hoff = shoff; G.hs_map = hsmap; G.hv_slot_begin = hvb;
+                G.hs_pos = hvs; G.hres = hres;
+                G.nhslots = (int64_t)ph.hs_hk.size();
+                if ((rc = dalloc(ctx, &G.hs_val, std::max<int64_t>(ph.hs_size, 2))) ||
+                    (rc = dalloc(ctx, &G.hs_part, 6 * std::max<int64_t>(G.nhslots, 1))) ||
+                    (rc = dalloc(ctx, &G.hqf, std::max(G.nheavy_dofs, 1))))
+                    return rc;
+            }
             if ((rc = dalloc(ctx, &G.minv, ph.msize)) || (rc = dalloc(ctx, &G.r, S.ndof)) ||
-                (rc = dalloc(ctx, &G.z, S.ndof)) || (rc = dalloc(ctx, &G.p[0], S.ndof)) ||
-                (rc = dalloc(ctx, &G.p[1], S.ndof)) || (rc = dalloc(ctx, &G.q, S.ndof)) ||
+                (rc = dalloc(ctx, &G.zp, 2 * S.ndof)) || (rc = dalloc(ctx, &G.pq, 2 * S.ndof)) ||
                 (rc = dalloc(ctx, &G.hq, 6 * (int64_t)std::max(G.nhchunks, 1))) ||
-                (rc = dalloc(ctx, &G.partA, std::max(G.nA_light, 1))) || (rc = dalloc(ctx, &G.partB, 2 * (int64_t)G.nB)) ||
+                (rc = dalloc(ctx, &G.partA, std::max(G.nA_sl + G.nA_light, 1))) || (rc = dalloc(ctx, &G.partB, 2 * (int64_t)G.nB)) ||
                 (rc = dalloc(ctx, &G.rec, (int64_t)kPcgRec * (kPcgMaxIt + 2))))
                 return rc;
             ctx->pcg_avail = true;
-            double by = 32.0 * (double)S.ndof, fl = 0;
-            for (int64_t v = 0; v < S.nv; v++)
-                for (int64_t e = ph.ent_begin[v]; e < ph.ent_begin[v + 1]; e++) {
-                    by += 16.0 + 8.0 * S.vdim[v] * ph.ent[e].odim;
-                    fl += 2.0 * S.vdim[v] * ph.ent[e].odim;
-                }
+            const double by = ph.product_bytes, fl = ph.product_flops;
             ctx->pcg_bytes = by;
             ctx->pcg_flops = fl;
             // default budget: CG iterations that cost about one factorization + substitution, from
@@ -1015,6 +1038,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     ctx->hook_x = ctx->d_dx;
     int rc = eval_chi2_dev(ctx, true, ctx->prof_analytic, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
+    ctx->pcg_packed = false;
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     bool solved = false;
     int its = 0;
@@ -1026,9 +1050,11 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
         set_profiler(&prof);
         if (!rc && solved) {
             const PcgDev &G = ctx->G;
+            launch_pcg_repack(G, ctx->L.hval, ctx->st);      // once per LM iteration (after the assembly)
             launch_pcg_setup(G, ctx->L.hval, ctx->L.b, lambda, ctx->d_dx, ctx->st);
             launch_pcg_product(G, 0, ctx->L.hval, lambda, ctx->st);
             for (int j = 0; j < its; j++) {
+                launch_pcg_heavy(G, j, lambda, ctx->st);
                 launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
                 launch_pcg_product(G, j + 1, ctx->L.hval, lambda, ctx->st);
             }
@@ -1140,6 +1166,10 @@ int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, in
     G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
     solved = false;
     its = 0;
+    if (!ctx->pcg_packed) {
+        launch_pcg_repack(G, L.hval, ctx->st);
+        ctx->pcg_packed = true;
+    }
     launch_pcg_setup(G, L.hval, rhs, lambda, ctx->d_dx, ctx->st);
     launch_pcg_product(G, 0, L.hval, lambda, ctx->st);
     int j = 0;
@@ -1148,6 +1178,7 @@ int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, in
     for (;;) {
         const int n = std::min(chunk, G.max_it - j);
         for (int k = 0; k < n; k++, j++) {
+            launch_pcg_heavy(G, j, lambda, ctx->st);
             launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
             launch_pcg_product(G, j + 1, L.hval, lambda, ctx->st);
         }
@@ -1259,6 +1290,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         hipEventRecord(ctx->ev[0], ctx->st);
         if ((rc = eval_chi2_dev(ctx, true, analytic, 0))) return rc;   // computeActiveErrors + linearizeOplus
         launch_assemble(P, L, ctx->st);                      // buildSystem
+        ctx->pcg_packed = false;
         if (it == 0) {
             if (dist) {                                      // max of the rank-summed diagonal
                 launch_diag_entries(L, ctx->d_diagv, ctx->st);
@@ -1588,6 +1620,7 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
     hipSetDevice(ctx->device);
     eval_chi2_dev(ctx, true, true, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
+    ctx->pcg_packed = false;
     HIPOK(hipStreamSynchronize(ctx->st));
     if (b) HIPOK(hipMemcpy(b, ctx->L.b, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
     if (hdiag) {
@@ -1615,6 +1648,7 @@ int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int
     hipMemcpy(dx, x, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
     eval_chi2_dev(ctx, true, true, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
+    ctx->pcg_packed = false;
     launch_hmul(ctx->L, ctx->L.blk_row_dof, ctx->L.blk_col_dof, dx, dy, n, ctx->st);
     hipStreamSynchronize(ctx->st);
     hipMemcpy(y, dy, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost);
@@ -1633,6 +1667,7 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
     hipMemcpy(dr, rhs, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
     eval_chi2_dev(ctx, true, true, 0);
     launch_assemble(ctx->P, ctx->L, ctx->st);
+    ctx->pcg_packed = false;
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     bool solved = false;
     if (use_pcg(ctx)) {                         // the configured step solver, as deftri_solve_lm uses it
