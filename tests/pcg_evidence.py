@@ -2,6 +2,7 @@
 sketched.  Test infrastructure (uses the oracle's assembled H); run by hand:
 
     python tests/pcg_evidence.py 10000 30000 100000 > profiles/r02_pcg_evidence.json
+    python tests/pcg_evidence.py --observed 10000 > profiles/r02_pcg_evidence_observed.json
 
 For the two-view benchmark scene at n correspondences: the damped system (H + lam I) dx = b of the
 first LM iteration (lam = tau * max diag H, tau = 1e-5, g2o's initial damping) and of later, weaker
@@ -72,8 +73,16 @@ def pcg(A, b, M, x_ref, tols, max_it):
     return out
 
 
+OBSERVED = False
+
+
 def main():
-    sizes = [int(a) for a in sys.argv[1:]] or [10000]
+    global OBSERVED
+    args = sys.argv[1:]
+    if "--observed" in args:
+        OBSERVED = True
+        args.remove("--observed")
+    sizes = [int(a) for a in args] or [10000]
     res = {"what": __doc__.strip().splitlines()[0], "cases": []}
     for n in sizes:
         t0 = time.time()
@@ -89,14 +98,20 @@ def main():
                 "diag_H_range": [float(np.abs(H.diagonal()).min()), float(dmax)]}
         # g2o starts at tau * max diag H (tau = 1e-5) and each accepted trial scales lambda by 1/3..2/3:
         # after ~10 / ~20 accepted iterations it is 1e-2 / 1e-4 of the start or less
-        for name, lam in (("initial", 1e-5 * dmax), ("later_1e-7", 1e-7 * dmax), ("later_1e-9", 1e-9 * dmax)):
+        lams = (("initial", 1e-5 * dmax), ("later_1e-7", 1e-7 * dmax), ("later_1e-9", 1e-9 * dmax))
+        if OBSERVED:
+            # the dampings g2o's LM actually visits on this scene: after the first iteration's
+            # rejections lambda sits between ~7e-3 and ~1.7 of max diag H (oracle LM, 25 iterations
+            # at 10k correspondences: 1.0e15 .. 2.6e17 against max diag 1.5e17)
+            lams = tuple((f"observed_{f:g}", f * dmax) for f in (7e-3, 0.1, 1.0))
+        for name, lam in lams:
             A = (H + lam * sp.identity(N, format="csr")).tocsr()
             M = block_jacobi(A, dims)
             t1 = time.time()
             x_ref = oracle.damped_solve(p, lam, b, analytic=False)
             t_direct = time.time() - t1
             t1 = time.time()
-            out = pcg(A, b, M, x_ref, [1e-4, 1e-6, 1e-8, 1e-10], 10000)
+            out = pcg(A, b, M, x_ref, [1e-4, 1e-6, 1e-8, 1e-10] + ([1e-12] if OBSERVED else []), 10000)
             case[name] = {"lambda": lam, "cpu_direct_s": t_direct, "cpu_pcg_s": time.time() - t1, "pcg": out}
             print(n, name, json.dumps(out), file=sys.stderr, flush=True)
         case["wall_s"] = time.time() - t0

@@ -49,8 +49,8 @@ struct PcgHost {
     std::vector<PcgEnt> ent;
     std::vector<int32_t> light_v;        // vertices handled one per thread, in vertex order
     std::vector<int32_t> heavy_v;        // heavy vertices
-    std::vector<int32_t> hc_vertex;      // per heavy chunk: heavy index
-    std::vector<int64_t> hc_beg, hc_end; // entry range of the chunk (in hres)
+    std::vector<int32_t> hc_vertex;      // per heavy chunk (kPcgChunk entries of hres): heavy index
+    std::vector<int64_t> hc_beg, hc_end; // entry range of the chunk (in hres; a heavy vertex's chunks are contiguous)
     std::vector<int32_t> h_first;        // per heavy vertex: first chunk (nheavy + 1)
     std::vector<int32_t> h_dofbase;      // per heavy vertex: first heavy dof (nheavy + 1)
     std::vector<int32_t> v_heavy;        // per vertex: heavy index or -1
@@ -114,7 +114,6 @@ struct PcgDev {
     double *r = nullptr;
     double *zp = nullptr;                // (z, p_prev) per dof
     double *pq = nullptr;                // (p, q) per dof
-    double *hq = nullptr;                // per heavy chunk: 6 partial row sums
     double *partA = nullptr;             // per sliced / light workgroup of the product: p.q
     double *partB = nullptr;             // per vertex workgroup: (r.z, r.r)
     double *rec = nullptr;               // (max_it + 2) x kPcgRec
@@ -130,8 +129,9 @@ void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, doub
 // iteration it: product q = (H + lambda I) p (p = z + beta p_prev formed on the fly) after the
 // convergence test of the residual the previous update left
 void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st);
-// iteration it: the heavy rows' q from their slot partials and chunk partials (one workgroup per dof)
-void launch_pcg_heavy(const PcgDev &G, int it, double lambda, hipStream_t st);
+// iteration it, after the product: the heavy rows' q (one workgroup per dof: slot partials +
+// remaining entries) and the generic light rows
+void launch_pcg_heavy(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st);
 // iteration it: alpha, x += alpha p, r -= alpha q, z = M r, partial (r.z, r.r)
 void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStream_t st);
 

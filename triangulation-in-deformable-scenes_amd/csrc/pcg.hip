@@ -127,36 +127,47 @@ __device__ __forceinline__ void wg_pair_tree(double a0, double a1, double (*red)
 
 // one heavy slot of a slice (heavy vertex of dimension OD): the row side acc += B p_heavy, and the
 // heavy row's side B^T p_row summed over the 64 lanes by a fixed butterfly into part[0..OD).  B is
-// 3 x OD in the row's orientation, row-major, in ceil(3 OD / 2) lane-interleaved double2.
-template <int OD>
-__device__ __forceinline__ void heavy_slot(const double2 *__restrict__ hb, int64_t oh, const double *__restrict__ zp,
+// 3 x OD in the row's orientation, stored per lane as 3-column sub-blocks (row-major 3 x 3 + one pad
+// = five double2 each; OD = 1: three values in two double2), taken one sub-block at a time so
+// the live registers stay those of a 3 x 3 slot.
+// columns [0, nc) of a 3 x 3 sub-block B (row-major, row stride 3; nc <= 3, the rest zero)
+__device__ __forceinline__ void heavy_cols(const double *B, int nc, int64_t oh, const double *__restrict__ zp,
                                            double beta, const double pv[3], double acc[6], double *__restrict__ part,
                                            int lane) {
-    constexpr int NQ = (3 * OD + 1) / 2;
-    double B[2 * NQ], ph[OD], cc[OD];
+    double ph[3], cc[3];
 #pragma unroll
-    for (int q2 = 0; q2 < NQ; q2++) {
-        const double2 t = hb[q2 * 64];
-        B[2 * q2] = t.x;
-        B[2 * q2 + 1] = t.y;
-    }
-#pragma unroll
-    for (int j = 0; j < OD; j++) ph[j] = pval(zp, beta, oh + j);
+    for (int j = 0; j < 3; j++) ph[j] = j < nc ? pval(zp, beta, oh + j) : 0.0;
 #pragma unroll
     for (int i = 0; i < 3; i++)
 #pragma unroll
-        for (int j = 0; j < OD; j++) acc[i] += B[i * OD + j] * ph[j];
+        for (int j = 0; j < 3; j++) acc[i] += B[i * 3 + j] * ph[j];
 #pragma unroll
-    for (int j = 0; j < OD; j++) cc[j] = (B[j] * pv[0] + B[OD + j] * pv[1]) + B[2 * OD + j] * pv[2];
+    for (int j = 0; j < 3; j++) cc[j] = (B[j] * pv[0] + B[3 + j] * pv[1]) + B[6 + j] * pv[2];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-        for (int j = 0; j < OD; j++) cc[j] += __shfl_xor(cc[j], off, 64);
-    if (lane < OD) {
-        double cj = cc[0];
+        for (int j = 0; j < 3; j++) cc[j] += __shfl_xor(cc[j], off, 64);
+    if (lane < nc) part[lane] = lane == 0 ? cc[0] : lane == 1 ? cc[1] : cc[2];
+}
+
+__device__ __forceinline__ void heavy_slot(const double2 *__restrict__ hb, int od, int64_t oh,
+                                           const double *__restrict__ zp, double beta, const double pv[3], double acc[6],
+                                           double *__restrict__ part, int lane) {
+    if (od == 1) {
+        const double2 t0 = hb[0], t1 = hb[64];
+        const double B[9] = {t0.x, 0.0, 0.0, t0.y, 0.0, 0.0, t1.x, 0.0, 0.0};
+        heavy_cols(B, 1, oh, zp, beta, pv, acc, part, lane);
+        return;
+    }
+    for (int sb = 0; 3 * sb < od; sb++) {
+        double B[10];
 #pragma unroll
-        for (int j = 1; j < OD; j++) cj = lane == j ? cc[j] : cj;
-        part[lane] = cj;
+        for (int q2 = 0; q2 < 5; q2++) {
+            const double2 t = hb[(5 * sb + q2) * 64];
+            B[2 * q2] = t.x;
+            B[2 * q2 + 1] = t.y;
+        }
+        heavy_cols(B, min(3, od - 3 * sb), oh + 3 * sb, zp, beta, pv, acc, part + 3 * sb, lane);
     }
 }
 
@@ -173,19 +184,28 @@ __global__ void __launch_bounds__(256) k_pcg_repack(const PcgDev G, const double
         const int od = G.vdim[G.heavy_v[G.hs_hk[g]]];
         const double *h = hval + (m < 0 ? 0 : (m & ((1LL << 62) - 1)));
         const bool tr = m >= 0 && ((m >> 62) & 1);
-        double v[18];
+        double B[18];                          // B[i][j] of the 3 x od block, row orientation
 #pragma unroll
-        for (int q = 0; q < 18; q++) v[q] = 0.0;
-        if (m >= 0)
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 6; j++) B[i * 6 + j] = (m >= 0 && j < od) ? (tr ? h[j * 3 + i] : h[i * od + j]) : 0.0;
+        if (od == 1) {
+            dst[0] = make_double2(B[0], B[6]);
+            dst[64] = make_double2(B[12], 0.0);
+            return;
+        }
+#pragma unroll
+        for (int sb = 0; sb < 2; sb++) {
+            if (3 * sb >= od) break;
+            double v[10];
 #pragma unroll
             for (int i = 0; i < 3; i++)
 #pragma unroll
-                for (int j = 0; j < 6; j++)
-                    if (j < od) v[i * od + j] = tr ? h[j * 3 + i] : h[i * od + j];
-        const int nq = (3 * od + 1) / 2;
+                for (int j = 0; j < 3; j++) v[i * 3 + j] = B[i * 6 + 3 * sb + j];
+            v[9] = 0.0;
 #pragma unroll
-        for (int q2 = 0; q2 < 9; q2++)
-            if (q2 < nq) dst[q2 * 64] = make_double2(v[2 * q2], v[2 * q2 + 1]);
+            for (int q2 = 0; q2 < 5; q2++) dst[(5 * sb + q2) * 64] = make_double2(v[2 * q2], v[2 * q2 + 1]);
+        }
         return;
     }
     const int64_t m = G.sl_map[t];
@@ -296,6 +316,8 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
     wg_pair_tree(rz, rr, red, G.partB + 2 * blockIdx.x);
 }
 
+// the sliced rows (one workgroup per slice); the heavy rows and the generic light rows follow in
+// k_pcg_heavy (their own launch: this kernel's register budget is the slices')
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_PCG_WPE))) k_pcg_product(int it, const PcgDev G, const double *__restrict__ hval,
                                                      double lam) {
     __shared__ double red[6][256];
@@ -320,21 +342,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     const double beta = it == 0 ? 0.0 : rz / prv[PR_RZ];
     const double *zp = G.zp;
     double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
-    if ((int)blockIdx.x < G.nA_sl) {
+    {
         // sliced rows: one slice (64 rows, lane = row) per workgroup; its four waves take every
         // fourth slot of each kind, so a wave's dependent chain (column index -> gather) is a
         // quarter of the slice's; every load is coalesced but the (z, p_prev) gathers.  The four
         // partial row sums meet in LDS in a fixed order.
         const int sl = blockIdx.x;
+        const bool live = sl < G.nsl;              // the launch has one workgroup even with no slices
         const int w = tid >> 6, lane = tid & 63;
-        const int v = G.sl_v[sl * 64 + lane];
+        const int v = live ? G.sl_v[sl * 64 + lane] : -1;
         const int64_t o = v >= 0 ? G.voff[v] : 0;
         double pv[3];
 #pragma unroll
         for (int i = 0; i < 3; i++) pv[i] = v >= 0 ? pval(zp, beta, o + i) : 0.0;
         double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        const int64_t g0 = G.sl_off[sl];
-        const int ns = G.sl_n[sl];
+        const int64_t g0 = live ? G.sl_off[sl] : 0;
+        const int ns = live ? G.sl_n[sl] : 0;
         constexpr int kSlotBatch = DEFTRI_PCG_BATCH;   // slots of one wave in flight together
         const double2 *slv = reinterpret_cast<const double2 *>(G.sl_val);
         for (int k0 = w; k0 < ns; k0 += 4 * kSlotBatch) {
@@ -367,25 +390,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         }
         // couplings to heavy vertices: the row side B p_heavy, and the heavy row's side B^T p_row
         // reduced over the slice's lanes (fixed butterfly) into the slot's partial
-        const int64_t h0 = G.sl_hoff[sl];
-        const int nh = G.sl_hn[sl];
+        const int64_t h0 = live ? G.sl_hoff[sl] : 0;
+        const int nh = live ? G.sl_hn[sl] : 0;
         for (int k = w; k < nh; k += 4) {
             const int64_t g = h0 + k;
             const int hv = G.heavy_v[G.hs_hk[g]];
             const int64_t oh = G.voff[hv];
             const double2 *hb = reinterpret_cast<const double2 *>(G.hs_val) + G.hs_voff[g] + lane;
             double *part = G.hs_part + G.hs_pos[g] * 6;     // heavy-vertex-major: k_pcg_heavy reads runs
-            switch (G.vdim[hv]) {
-                case 6: heavy_slot<6>(hb, oh, zp, beta, pv, acc, part, lane); break;
-                case 1: heavy_slot<1>(hb, oh, zp, beta, pv, acc, part, lane); break;
-                case 2: heavy_slot<2>(hb, oh, zp, beta, pv, acc, part, lane); break;
-                case 3: heavy_slot<3>(hb, oh, zp, beta, pv, acc, part, lane); break;
-                case 4: heavy_slot<4>(hb, oh, zp, beta, pv, acc, part, lane); break;
-                default: heavy_slot<5>(hb, oh, zp, beta, pv, acc, part, lane); break;
-            }
+            heavy_slot(hb, G.vdim[hv], oh, zp, beta, pv, acc, part, lane);
         }
-        const int64_t x0 = G.sl_xoff[sl];
-        const int nx = G.sl_nx[sl];
+        const int64_t x0 = live ? G.sl_xoff[sl] : 0;
+        const int nx = live ? G.sl_nx[sl] : 0;
         for (int k = w; k < nx; k += 4) {
             const PcgEnt E = load_ent(G.sl_x, (x0 + k) * 64 + lane);
             if (E.odim) ent_acc(E, 3, hval, zp, beta, acc);
@@ -405,11 +421,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         }
         __syncthreads();
         const double s = wg_tree(pqs, red[3]);
-        if (tid == 0) G.partA[blockIdx.x] = s;
+        if (tid == 0 && sl < G.nsl) G.partA[blockIdx.x] = s;
         return;
     }
-    if ((int)blockIdx.x < G.nA_sl + G.nA_light) {
-        const int k = (blockIdx.x - G.nA_sl) * 256 + tid;
+}
+
+// After the sliced product, iteration it: one workgroup per heavy dof — q = (its slots' partials,
+// fixed tree) + (the heavy row's remaining entries: its diagonal block and couplings outside the
+// slices, fixed tree) + lambda p — then the generic light rows, one thread each (their p.q partials
+// follow the slices' in partA).  beta comes from the record the product's workgroup 0 wrote.
+__global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const double *__restrict__ hval,
+                                                   double lam) {
+    __shared__ double red[256];
+    const double *rec = G.rec + kPcgRec * (it + 1);
+    if (rec[PR_STATUS] != 0.0) return;
+    const double beta = it == 0 ? 0.0 : rec[PR_RZ] / G.rec[kPcgRec * it + PR_RZ];
+    const double *zp = G.zp;
+    double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= G.nheavy_dofs) {
+        const int k = (blockIdx.x - G.nheavy_dofs) * 256 + tid;
         double pqs = 0.0;
         if (k < G.nlight) {
             const int v = G.light_v[k];
@@ -428,41 +459,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
                 }
             }
         }
-        const double s = wg_tree(pqs, red[0]);
-        if (tid == 0) G.partA[blockIdx.x] = s;
+        const double s = wg_tree(pqs, red);
+        if (tid == 0) G.partA[G.nA_sl + blockIdx.x - G.nheavy_dofs] = s;
         return;
     }
-    // a chunk of a heavy row: partial sums of its entries, reduced in a fixed tree
-    const int c = blockIdx.x - G.nA_sl - G.nA_light;
-    const int hk = G.hc_vertex[c];
-    const int v = G.heavy_v[hk];
-    const int d = G.vdim[v];
-    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    const int64_t e1 = G.hc_end[c];
-    for (int64_t e = G.hc_beg[c] + tid; e < e1; e += 256) ent_acc(load_ent(G.hres, e), d, hval, zp, beta, acc);
-#pragma unroll
-    for (int i = 0; i < 6; i++) red[i][tid] = acc[i];
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off)
-#pragma unroll
-            for (int i = 0; i < 6; i++) red[i][tid] += red[i][tid + off];
-        __syncthreads();
-    }
-    if (tid < d) {
-        G.hq[6 * c + tid] = red[tid][0];
-        if (c == G.h_first[hk]) {
-            const int64_t o = G.voff[v];
-            pq2[o + tid] = make_double2(pval(zp, beta, o + tid), 0.0);
-        }
-    }
-}
-
-// one workgroup per heavy dof: q = (slot partials, fixed tree) + (chunk partials, in order) + lambda p
-__global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, double lam) {
-    __shared__ double red[256];
-    const double *rec = G.rec + kPcgRec * (it + 1);
-    if (rec[PR_STATUS] != 0.0) return;
     const int k = blockIdx.x;
     int hk = 0;
     while (G.h_dofbase[hk + 1] <= k) hk++;
@@ -470,16 +470,26 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, doubl
     const int64_t b0 = G.hv_slot_begin[hk], b1 = G.hv_slot_begin[hk + 1];
     // four independent strided streams per thread (loads in flight together), combined in order
     double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t t = b0 + threadIdx.x; t < b1; t += 1024)
+    for (int64_t t = b0 + tid; t < b1; t += 1024)
 #pragma unroll
         for (int u = 0; u < 4; u++)
             if (t + 256 * u < b1) a[u] += G.hs_part[(t + 256 * u) * 6 + i];
-    const double s = wg_tree((a[0] + a[1]) + (a[2] + a[3]), red);
-    if (threadIdx.x == 0) {
-        double q = s;
-        for (int c = G.h_first[hk]; c < G.h_first[hk + 1]; c++) q += G.hq[6 * c + i];
-        const double pv = reinterpret_cast<const double2 *>(G.pq)[G.voff[G.heavy_v[hk]] + i].x;
-        G.hqf[k] = q + lam * pv;
+    const double s_slots = wg_tree((a[0] + a[1]) + (a[2] + a[3]), red);
+    const int v = G.heavy_v[hk];
+    const int d = G.vdim[v];
+    const int f0 = G.h_first[hk], f1 = G.h_first[hk + 1];
+    const int64_t e0 = f0 < f1 ? G.hc_beg[f0] : 0, e1 = f0 < f1 ? G.hc_end[f1 - 1] : 0;
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int64_t e = e0 + tid; e < e1; e += 256) ent_acc(load_ent(G.hres, e), d, hval, zp, beta, acc);
+    double ai = acc[0];
+#pragma unroll
+    for (int u = 1; u < 6; u++) ai = i == u ? acc[u] : ai;
+    const double s_rest = wg_tree(ai, red);
+    if (tid == 0) {
+        const int64_t o = G.voff[v] + i;
+        const double pv = pval(zp, beta, o);
+        pq2[o] = make_double2(pv, 0.0);
+        G.hqf[k] = (s_slots + s_rest) + lam * pv;
     }
 }
 
@@ -571,16 +581,18 @@ void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, doub
 
 void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st) {
     hipEvent_t e0 = prof_begin(st);
-    const unsigned grid = (unsigned)(G.nA_sl + G.nA_light + G.nhchunks);
+    // always launched (also with no slices): its workgroup 0 writes the iteration record
+    const unsigned grid = (unsigned)std::max(G.nA_sl, 1);
     hipLaunchKernelGGL(dev::k_pcg_product, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
     prof_end("pcg_product", e0, grid, 0.0, st);
 }
 
-void launch_pcg_heavy(const PcgDev &G, int it, double lambda, hipStream_t st) {
-    if (G.nheavy_dofs <= 0) return;
+void launch_pcg_heavy(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st) {
+    const unsigned grid = (unsigned)(G.nheavy_dofs + G.nA_light);
+    if (grid == 0) return;
     hipEvent_t e0 = prof_begin(st);
-    hipLaunchKernelGGL(dev::k_pcg_heavy, dim3(G.nheavy_dofs), dim3(256), 0, st, it, G, lambda);
-    prof_end("pcg_heavy", e0, G.nheavy_dofs, 0.0, st);
+    hipLaunchKernelGGL(dev::k_pcg_heavy, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
+    prof_end("pcg_heavy", e0, grid, 0.0, st);
 }
 
 void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStream_t st) {
@@ -743,7 +755,8 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     }
     int64_t hsv = 0, hs_bytes = 0;
     for (int64_t g = 0; g < hslots; g++) {
-        const int nq = (3 * vdim[H.heavy_v[H.hs_hk[g]]] + 1) / 2;
+        const int od = vdim[H.heavy_v[H.hs_hk[g]]];
+        const int nq = od == 1 ? 2 : 5 * ((od + 2) / 3);
         H.hs_voff[g] = hsv;
         hsv += 64 * (int64_t)nq;
         hs_bytes += 64 * 16 * (int64_t)nq;

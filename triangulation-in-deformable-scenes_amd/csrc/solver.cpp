@@ -505,7 +505,6 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
             }
             if ((rc = dalloc(ctx, &G.minv, ph.msize)) || (rc = dalloc(ctx, &G.r, S.ndof)) ||
                 (rc = dalloc(ctx, &G.zp, 2 * S.ndof)) || (rc = dalloc(ctx, &G.pq, 2 * S.ndof)) ||
-                (rc = dalloc(ctx, &G.hq, 6 * (int64_t)std::max(G.nhchunks, 1))) ||
                 (rc = dalloc(ctx, &G.partA, std::max(G.nA_sl + G.nA_light, 1))) || (rc = dalloc(ctx, &G.partB, 2 * (int64_t)G.nB)) ||
                 (rc = dalloc(ctx, &G.rec, (int64_t)kPcgRec * (kPcgMaxIt + 2))))
                 return rc;
@@ -1054,7 +1053,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
             launch_pcg_setup(G, ctx->L.hval, ctx->L.b, lambda, ctx->d_dx, ctx->st);
             launch_pcg_product(G, 0, ctx->L.hval, lambda, ctx->st);
             for (int j = 0; j < its; j++) {
-                launch_pcg_heavy(G, j, lambda, ctx->st);
+                launch_pcg_heavy(G, j, ctx->L.hval, lambda, ctx->st);
                 launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
                 launch_pcg_product(G, j + 1, ctx->L.hval, lambda, ctx->st);
             }
@@ -1154,54 +1153,84 @@ int deftri_reset_state(deftri_ctx *ctx) {
 }
 
 namespace {
-// One LM step by PCG into ctx->d_dx.  Launches go out in chunks (update, product) x n; the host
-// reads the record of the last product after each chunk (the product launch carries the
-// convergence test, so launches past convergence return at once).  The first chunk is sized by the
-// previous converged solve.  solved = false: budget exhausted, breakdown, or a preconditioner block
-// not positive definite — the caller factors instead.
-int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, int &its) {
+// One LM step by PCG into ctx->d_dx, in two halves so the LM loop can enqueue the trial's update
+// and chi2 behind the first one and pay a single host round trip when the prediction holds:
+//   pcg_start: repack (after an assembly), setup, product(0), then n x (heavy, update, product) with
+//              n = the previous converged solve's count + 1 (the product launch carries the
+//              convergence test; launches past convergence return at once); no synchronization.
+//   pcg_poll:  reads the record of the last product; while still running, further chunks of 4
+//              iterations with a read-back each.  solved = false: budget exhausted, breakdown, or a
+//              preconditioner block not positive definite — the caller factors instead.
+void pcg_start(deftri_ctx *ctx, double lambda, const double *rhs, int &j) {
     PcgDev &G = ctx->G;
     const DevPlan &L = ctx->L;
     G.max_it = ctx->pcg_max_it > 0 ? ctx->pcg_max_it : ctx->pcg_auto_it;
     G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
-    solved = false;
-    its = 0;
     if (!ctx->pcg_packed) {
         launch_pcg_repack(G, L.hval, ctx->st);
         ctx->pcg_packed = true;
     }
     launch_pcg_setup(G, L.hval, rhs, lambda, ctx->d_dx, ctx->st);
     launch_pcg_product(G, 0, L.hval, lambda, ctx->st);
-    int j = 0;
-    int chunk = std::max(2, ctx->pcg_last_its + 1);
-    double *rec = ctx->hpin + 16;
-    for (;;) {
-        const int n = std::min(chunk, G.max_it - j);
-        for (int k = 0; k < n; k++, j++) {
-            launch_pcg_heavy(G, j, lambda, ctx->st);
-            launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
-            launch_pcg_product(G, j + 1, L.hval, lambda, ctx->st);
-        }
-        HIPOK(hipMemcpyAsync(rec, G.rec + (size_t)kPcgRec * (j + 1), sizeof(double) * kPcgRec, hipMemcpyDeviceToHost,
-                             ctx->st));
-        HIPOK(hipStreamSynchronize(ctx->st));
-        const int status = (int)rec[PR_STATUS];
-        if (status == kPcgConverged) {
-            its = (int)rec[PR_ITS];
-            ctx->pcg_last_its = its;
-            solved = true;
-            ctx->pcg_step_its = its;
-            ctx->pcg_step_solved = 1;
-            return 0;
-        }
-        if (status != kPcgRunning || j >= G.max_it) {
-            its = j;
-            ctx->pcg_step_its = its;
-            ctx->pcg_step_solved = 0;
-            return 0;
-        }
-        chunk = 4;
+    j = 0;
+    const int n = std::min(std::max(2, ctx->pcg_last_its + 1), G.max_it);
+    for (int k = 0; k < n; k++, j++) {
+        launch_pcg_heavy(G, j, ctx->L.hval, lambda, ctx->st);
+        launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
+        launch_pcg_product(G, j + 1, L.hval, lambda, ctx->st);
     }
+}
+
+// the record of product j (iteration j's convergence verdict) into the pinned staging
+int pcg_fetch(deftri_ctx *ctx, int j) {
+    HIPOK(hipMemcpyAsync(ctx->hpin + 16, ctx->G.rec + (size_t)kPcgRec * (j + 1), sizeof(double) * kPcgRec,
+                         hipMemcpyDeviceToHost, ctx->st));
+    return 0;
+}
+
+// after a synchronization that covered pcg_fetch(j): 1 converged, 0 still running, -1 given up
+int pcg_verdict(deftri_ctx *ctx, int j, int &its) {
+    const double *rec = ctx->hpin + 16;
+    const int status = (int)rec[PR_STATUS];
+    if (status == kPcgConverged) {
+        its = (int)rec[PR_ITS];
+        ctx->pcg_last_its = its;
+        ctx->pcg_step_its = its;
+        ctx->pcg_step_solved = 1;
+        return 1;
+    }
+    if (status != kPcgRunning || j >= ctx->G.max_it) {
+        its = j;
+        ctx->pcg_step_its = its;
+        ctx->pcg_step_solved = 0;
+        return -1;
+    }
+    return 0;
+}
+
+int pcg_poll(deftri_ctx *ctx, double lambda, int &j, bool &solved, int &its) {
+    PcgDev &G = ctx->G;
+    for (;;) {
+        int rc = pcg_fetch(ctx, j);
+        if (rc) return rc;
+        HIPOK(hipStreamSynchronize(ctx->st));
+        const int v = pcg_verdict(ctx, j, its);
+        if (v != 0) { solved = v > 0; return 0; }
+        const int n = std::min(4, G.max_it - j);
+        for (int k = 0; k < n; k++, j++) {
+            launch_pcg_heavy(G, j, ctx->L.hval, lambda, ctx->st);
+            launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
+            launch_pcg_product(G, j + 1, ctx->L.hval, lambda, ctx->st);
+        }
+    }
+}
+
+int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, int &its) {
+    int j = 0;
+    solved = false;
+    its = 0;
+    pcg_start(ctx, lambda, rhs, j);
+    return pcg_poll(ctx, lambda, j, solved, its);
 }
 
 // the sequential trial (scatter + factorization + solve) as one graph launch: single stream, no
@@ -1365,55 +1394,76 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         } else do {
             push_state(ctx);
             HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
-            bool solved = false;
+            double *sc = ctx->hpin + 4;
+            // the trial's evaluation: _optimizer->update(x) (skipped on a zero pivot), chi2, rho's
+            // denominator, read-backs (one host round trip)
+            auto evaluate = [&]() -> int {
+                hipEventRecord(ctx->ev[4], ctx->st);
+                launch_update_state(P, ctx->d_dx, ctx->st, L.flag);
+                if (dist) {
+                    // chi2 of the rank's edges, dx.(lambda dx + b) with b partial and lambda once per dof,
+                    // the zero-pivot flag: one all-reduce of the three (a zero pivot on any rank rejects)
+                    int r2 = eval_chi2_dev(ctx, false, analytic, 0, false);
+                    if (r2) return r2;
+                    launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 3, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st,
+                               ctx->d_dofw);
+                    launch_int_to_double(1, L.flag, ctx->d_scal + 2, ctx->st);
+                    if ((r2 = dist_allreduce(ctx, ctx->d_scal, 3, 0))) return r2;
+                    hipEventRecord(ctx->ev[5], ctx->st);
+                    HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
+                } else {
+                    eval_chi2_dev(ctx, false, analytic, 0);      // computeActiveErrors; activeRobustChi2
+                    launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
+                    hipEventRecord(ctx->ev[5], ctx->st);
+                    HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
+                    HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+                }
+                return 0;
+            };
+            bool solved = false, evaluated = false;
+            hipEventRecord(ctx->ev[2], ctx->st);
             if (pcg) {
+                // PCG step with the evaluation queued behind the predicted iteration count: when the
+                // solve has converged by then, the trial costs one round trip; otherwise the state
+                // is restored, the solve continues (or falls back) and the evaluation is redone
                 auto t0 = std::chrono::steady_clock::now();
-                int its = 0;
-                if ((rc = pcg_step(ctx, lambda, L.b, solved, its))) return rc;
+                int j = 0, its = 0;
+                pcg_start(ctx, lambda, L.b, j);
+                hipEventRecord(ctx->ev[3], ctx->st);
+                if ((rc = evaluate())) return rc;
+                if ((rc = pcg_fetch(ctx, j))) return rc;
+                HIPOK(hipStreamSynchronize(ctx->st));
+                const int v = pcg_verdict(ctx, j, its);
+                if (v > 0) {
+                    solved = evaluated = true;
+                } else {
+                    pop_state(ctx);
+                    if (v == 0 && (rc = pcg_poll(ctx, lambda, j, solved, its))) return rc;
+                }
                 R.ms_pcg += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 R.pcg_iterations += its;
                 if (solved) R.pcg_trials++;
                 else R.pcg_fallbacks++;
                 if (prm->verbose)
                     std::fprintf(stderr, "[deftri] pcg lambda %.6e iterations %d %s\n", lambda, its, solved ? "converged" : "-> LDL^T");
+                if (!solved) hipEventRecord(ctx->ev[2], ctx->st);
             }
-            hipEventRecord(ctx->ev[2], ctx->st);
             if (!solved) {
                 ctx->hpin[12] = lambda;                      // pinned: read by the copy at its turn in the stream
                 HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
+                if (launch_trial_graph(ctx)) {
+                    hipEventRecord(ctx->ev[3], ctx->st);     // factor + solve in one graph: timed as factor
+                } else {
+                    launch_scatter(L, lambda, ctx->st);      // setLambda
+                    launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
+                    hipEventRecord(ctx->ev[3], ctx->st);
+                    ctx->hook_x = ctx->d_dx;
+                    launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
+                    if (ctx->hook_rc) return ctx->hook_rc;
+                }
             }
-            if (solved) {
-                hipEventRecord(ctx->ev[3], ctx->st);         // PCG step: timed in ms_pcg
-            } else if (launch_trial_graph(ctx)) {
-                hipEventRecord(ctx->ev[3], ctx->st);         // factor + solve in one graph: timed as factor
-            } else {
-                launch_scatter(L, lambda, ctx->st);          // setLambda
-                launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
-                hipEventRecord(ctx->ev[3], ctx->st);
-                ctx->hook_x = ctx->d_dx;
-                launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
-                if (ctx->hook_rc) return ctx->hook_rc;
-            }
-            hipEventRecord(ctx->ev[4], ctx->st);
-            launch_update_state(P, ctx->d_dx, ctx->st, L.flag);   // _optimizer->update(x) (skipped on a zero pivot)
-            double *sc = ctx->hpin + 4;
-            if (dist) {
-                // chi2 of the rank's edges, dx.(lambda dx + b) with b partial and lambda once per dof,
-                // the zero-pivot flag: one all-reduce of the three (a zero pivot on any rank rejects)
-                if ((rc = eval_chi2_dev(ctx, false, analytic, 0, false))) return rc;
-                launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 3, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st,
-                           ctx->d_dofw);
-                launch_int_to_double(1, L.flag, ctx->d_scal + 2, ctx->st);
-                if ((rc = dist_allreduce(ctx, ctx->d_scal, 3, 0))) return rc;
-                hipEventRecord(ctx->ev[5], ctx->st);
-                HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
-            } else {
-                eval_chi2_dev(ctx, false, analytic, 0);      // computeActiveErrors; activeRobustChi2
-                launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
-                hipEventRecord(ctx->ev[5], ctx->st);
-                HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
-                HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
-            }
+            if (solved && !evaluated) hipEventRecord(ctx->ev[3], ctx->st);
+            if (!evaluated && (rc = evaluate())) return rc;
             HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
             if (dist ? sc[2] >= kStatusWaitTimeout : (*ctx->ipin & kStatusWaitTimeout) != 0)
