@@ -3,26 +3,34 @@ optimizer.optimize(nIterations), reference Modules/Optimization/g2oBundleAdjustm
 config C2 of BASELINE.json: 100k two-view correspondences.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--corr 100000] [--no-cpu-baseline]
-                  [--analytic] [--replicas] [--cpu-full-iteration]
+                  [--analytic] [--solver pcg|direct] [--sharded] [--cpu-full-iteration]
   python bench.py --workload ba [--ba-points 500000] [--ba-kfs 8] [--ba-scaling strong|weak] ...
 
 A "step" is one LM iteration of the device solver (linearize with g2o's numeric ARAP/depth
-Jacobians — the reference's arithmetic — assemble H, then up to 10 damped trials of scatter +
-multifrontal LDL^T + solve + update + chi2 each).  The scene is synthetic (deftri.sim: the
+Jacobians — the reference's arithmetic — assemble H, then up to 10 damped trials, each a step
+solve (block-Jacobi PCG, or the multifrontal LDL^T) + update + chi2).  The scene is synthetic (deftri.sim: the
 reference's simulation recipe scaled to n points); the graph is built on the host once, then
 resident in HBM before the timed region starts.
 
-Multi-GPU (N > 1): ONE C2 problem point-sharded over the N ranks (DistPlan, csrc/symbolic.cpp: a
-subtree of the nested-dissection tree per rank, separator fronts on the leading ranks; per LM
-trial RCCL send/recv of one packed contribution block, one forward vector and one boundary
-solution per rank, all-reduce of chi2 / rho denominator / pivot flags) — strong scaling.
---replicas runs N independent C2 problems instead (weak scaling, no collective).  The barrier and
-the max-over-ranks time use torch.distributed.
+Multi-GPU (N > 1): N independent C2 problems, one per GPU (weak scaling, no data-path collective):
+with PCG steps a C2 LM iteration is ~5 ms and a CG iteration ~0.1 ms of HBM-bound work, less than
+the latency of the halo exchange and two all-reduces a point-sharded CG iteration would need
+(DESIGN.md §7).  --sharded runs ONE C2 problem point-sharded over the N ranks with the multifrontal
+LDL^T (DistPlan, csrc/symbolic.cpp: a subtree of the nested-dissection tree per rank, separator
+fronts on the leading ranks; per LM trial RCCL send/recv of one packed contribution block, one
+forward vector and one boundary solution per rank, all-reduce of chi2 / rho denominator / pivot
+flags) — strong scaling.  The barrier and the max-over-ranks time use torch.distributed.
 
-Printed roofline: the dominant factorization kernel ("update": the Schur-complement GEMM of each
-front) — algorithmic flops of one factorization ÷ its summed device time, both from a profiled
-trial run right after the timed region with HIP events on the solver's own stream.  FP64 peak
-78.6 TFLOP/s is AMD's MI355X specification (the microarch guide lists no FP64 row).
+Printed roofline: the dominant kernel of the configured step solver.  PCG (default): the product
+k_pcg_product, HBM-bound — its compulsory bytes per launch (repacked slot records, heavy slots,
+own (z, p_prev) and (p, q); csrc/pcg.hip PcgHost::product_bytes) x active launches / their summed
+device time, against 8 TB/s; `traffic` from the committed rocprofv3 PMC pass when it matches the
+plan.  The factorization's k_update roofline (algorithmic flops / device time, FP64 peak 78.6
+TFLOP/s, AMD's MI355X specification) is reported beside it as roofline_factorization.  Both from
+profiled trials right after the timed region, HIP events on the solver's own stream.
+
+A "step" is one LM iteration; with PCG steps each trial is setup + CG iterations (product, heavy
+rows, update) instead of scatter + factorization + substitution.
 
 CPU baseline: the oracle (oracle/deftri_oracle.c: the reference LM restated in scalar C, g2o
 numeric Jacobians, SimplicialLDLT) on the SAME full-size C2 problem with the device plan's
@@ -252,8 +260,10 @@ def main():
                     help="LM step solver: block-Jacobi PCG with LDL^T fallback (library default) or the LDL^T")
     ap.add_argument("--analytic", action="store_true",
                     help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
-    ap.add_argument("--replicas", action="store_true",
-                    help="N > 1: N independent C2 problems (weak scaling) instead of one point-sharded problem")
+    ap.add_argument("--sharded", action="store_true",
+                    help="N > 1: one C2 problem point-sharded over the ranks (LDL^T, strong scaling) instead of "
+                         "N independent problems (the default)")
+    ap.add_argument("--replicas", action="store_true", help="N > 1: independent problems (the default; kept for scripts)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end arapOptimization timing")
     ap.add_argument("--cpu-full-iteration", action="store_true",
                     help="CPU baseline: time the oracle's whole first LM iteration (all trials)")
@@ -279,7 +289,7 @@ def main():
     if args.workload == "ba":
         return main_ba(args, world, rank, gpu, backend)
 
-    sharded = world > 1 and not args.replicas
+    sharded = world > 1 and args.sharded
     t0 = time.perf_counter()
     prob, prob_map = build_problem(args.corr, 1 if sharded else 1 + rank)
     log(f"[rank {rank}] graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
@@ -336,6 +346,7 @@ def main():
                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                     "traffic_unit": "bytes per launch", "bytes_per_launch": pp["bytes"] / its,
                     "launches": pp["launches"], "avg_launch_us": round(1e3 * pp["ms"] / max(pp["launches"], 1), 3),
+                    "avg_active_launch_us": round(1e3 * pp["ms"] / its, 3),
                     "cg_iterations": its, "lambda": rep["lambda_final"], "rank": rank}
         pmcp = sorted(ROOT.glob("profiles/*_pmc_pcg_product.json"))
         if pmcp and not sharded:
