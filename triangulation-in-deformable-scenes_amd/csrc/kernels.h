@@ -30,6 +30,7 @@ struct DevProblem {
     double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr, *chi_rep = nullptr;
     double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr, *chi_dep = nullptr;
     double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr, *chi_arap = nullptr;
+    double *tg_pre = nullptr;   // per pair: T_g and its 12 numeric-Jacobian perturbations (k_arap_pre)
 };
 
 struct FrontDev {

@@ -126,17 +126,16 @@ __global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t 
     E[e] = err;
 }
 
-__device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
-                                           const double *v2j, const SE3 &T, const double *Ri,
-                                           const double *Rj, double w, double area) {
-    double Rg[9];
-    quat_to_mat(T.r, Rg);
+// the ARAP energy with the global transformation given as (rotation matrix, translation)
+__device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v2i, const double *v1j,
+                                              const double *v2j, const double *Rg, const double *tt,
+                                              const double *Ri, const double *Rj, double w, double area) {
     double dg[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
         double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
-        dg[k] = ((a - T.t[k]) - v1i[k]) + ((b - T.t[k]) - v1j[k]);
+        dg[k] = ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
     }
     double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
     double d1i[3], d2i[3], d1j[3], d2j[3];
@@ -155,11 +154,45 @@ __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i,
     return (w * (fn + gn) + eg) - 0.0;
 }
 
-__global__ void k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+__device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
+                                           const double *v2j, const SE3 &T, const double *Ri,
+                                           const double *Rj, double w, double area) {
+    double Rg[9];
+    quat_to_mat(T.r, Rg);
+    return arap_err_rt(v1i, v2i, v1j, v2j, Rg, T.t, Ri, Rj, w, area);
+}
+
+// g2o's numeric Jacobian of an ARAP edge perturbs the pair's T_g by exp(+-delta e_d) * T_g; those
+// 12 transformations (and T_g itself) are the same for every edge of the pair, so they are formed
+// once per pair here: per pair kArapPre x (rotation matrix 9, translation 3), transformation 0 the
+// unperturbed one, 1 + 2d / 2 + 2d the +delta / -delta perturbations of twist coordinate d.
+constexpr int kArapPre = 13;
+__global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restrict__ pre) {
+    const int t = TID;
+    if (t >= Q * kArapPre) return;
+    const int q = t / kArapPre, k = t % kArapPre;
+    const SE3 T = se3_load(tg + 7 * q);
+    SE3 X = T;
+    if (k > 0) {
+        const double delta = 1e-9;
+        double uu[6] = {0, 0, 0, 0, 0, 0};
+        uu[(k - 1) >> 1] = (k & 1) ? delta : -delta;
+        X = se3_mul(se3_exp(uu), T);
+    }
+    double *o = pre + 12 * (int64_t)t;
+    quat_to_mat(X.r, o);
+    o[9] = X.t[0]; o[10] = X.t[1]; o[11] = X.t[2];
+}
+
+// MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian (one kernel per
+// mode: each gets the registers of its own path)
+template <int MODE>
+__global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
                            const int32_t *__restrict__ arot, const double *__restrict__ aw,
                            const double *__restrict__ rot, const double *__restrict__ parea,
                            const double *__restrict__ pinfo, const double *__restrict__ points,
-                           const double *__restrict__ tg, double *__restrict__ J, double *__restrict__ W,
+                           const double *__restrict__ tg, const double *__restrict__ tg_pre,
+                           double *__restrict__ J, double *__restrict__ W,
                            double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
     int e = TID;
     if (e >= E_) return;
@@ -177,9 +210,9 @@ __global__ void k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32
     double w = aw[e], area = parea[q], om = pinfo[q];
     double err = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
     chi[e] = err * (om * err);
-    if (!want_jac) return;
+    if (MODE == 0) return;
     double Jv[18];
-    if (analytic) {
+    if (MODE == 1) {
         double Rg[9];
         quat_to_mat(T.r, Rg);
         double d1[3], d2[3], a[3], c[3], g[3], u[3], s2[3];
@@ -209,28 +242,38 @@ __global__ void k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32
         Jv[13] = 2.0 * (u[2] * g[0] - u[0] * g[2]);
         Jv[14] = 2.0 * (u[0] * g[1] - u[1] * g[0]);
         Jv[15] = -4.0 * g[0]; Jv[16] = -4.0 * g[1]; Jv[17] = -4.0 * g[2];
-    } else {                                       // g2o BaseMultiEdge numeric, delta 1e-9
-        const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    } else {                                       // g2o BaseMultiEdge numeric, delta 1e-9,
+        const double delta = 1e-9, scalar = 1.0 / (2 * delta);   // the pair's transformations precomputed
+        const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
+        double Rg[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) Rg[k] = X[k];
+        // one coordinate at a time: x + delta (the others + 0.0, which leaves them unchanged), the
+        // coordinate loop kept rolled so a single evaluation's registers are live
+#pragma unroll
         for (int vi = 0; vi < 4; vi++)
+#pragma unroll 1
             for (int dd = 0; dd < 3; dd++) {
-                double bak = P[vi][dd];
-                P[vi][dd] = bak + delta;
-                double ep = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
-                P[vi][dd] = bak - delta;
-                double em = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
-                P[vi][dd] = bak;
-                Jv[3 * vi + dd] = scalar * (ep - em);
+                double Pp[4][3], Pm[4][3];
+#pragma unroll
+                for (int a = 0; a < 4; a++)
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const double d = (a == vi && k == dd) ? delta : 0.0;
+                        Pp[a][k] = P[a][k] + d;
+                        Pm[a][k] = P[a][k] - d;
+                    }
+                double ep = arap_err_rt(Pp[0], Pp[1], Pp[2], Pp[3], Rg, Rg + 9, Ri, Rj, w, area);
+                double em = arap_err_rt(Pm[0], Pm[1], Pm[2], Pm[3], Rg, Rg + 9, Ri, Rj, w, area);
+                const double jv = scalar * (ep - em);
+                if (dd == 0) Jv[3 * vi] = jv;
+                else if (dd == 1) Jv[3 * vi + 1] = jv;
+                else Jv[3 * vi + 2] = jv;
             }
         for (int dd = 0; dd < 6; dd++) {
-            double uu[6] = {0, 0, 0, 0, 0, 0};
-            uu[dd] = delta;
-            SE3 Ep = se3_exp(uu);
-            SE3 Tp = se3_mul(Ep, T);
-            uu[dd] = -delta;
-            SE3 Em = se3_exp(uu);
-            SE3 Tm = se3_mul(Em, T);
-            double ep = arap_err(P[0], P[1], P[2], P[3], Tp, Ri, Rj, w, area);
-            double em = arap_err(P[0], P[1], P[2], P[3], Tm, Ri, Rj, w, area);
+            const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
+            double ep = arap_err_rt(P[0], P[1], P[2], P[3], Xp, Xp + 9, Ri, Rj, w, area);
+            double em = arap_err_rt(P[0], P[1], P[2], P[3], Xm, Xm + 9, Ri, Rj, w, area);
             Jv[12 + dd] = scalar * (ep - em);
         }
     }
@@ -1543,10 +1586,16 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
         LAUNCH("lin_dep", dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), st, P.D, P.dep_point, P.dep_scale,
                            P.dep_cam, P.dep_meas, P.dep_info, P.points, P.scales, P.cam_pose, P.cam_R, P.Jdep,
                            P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0);
+    const bool pre = want_jac && !analytic && P.E > 0;   // the numeric Jacobians read the pair table
+    if (pre)
+        LAUNCH("arap_pre", dev::k_arap_pre, dim3(nb((int64_t)P.Q * dev::kArapPre, 64)), dim3(64), st, P.Q, P.tg,
+               P.tg_pre);
     if (P.E > 0)
-        LAUNCH("lin_arap", dev::k_lin_arap, dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
-                           P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg, P.Jarap, P.Warap,
-                           P.Earap, P.chi_arap, want_jac ? 1 : 0, analytic ? 1 : 0);
+        LAUNCH("lin_arap", (!want_jac ? dev::k_lin_arap<0> : analytic ? dev::k_lin_arap<1> : dev::k_lin_arap<2>),
+                           dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
+                           P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg,
+                           pre ? P.tg_pre : nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, want_jac ? 1 : 0,
+                           analytic ? 1 : 0);
 }
 
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {

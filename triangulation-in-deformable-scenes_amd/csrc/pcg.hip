@@ -701,6 +701,22 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
         std::stable_sort(sliced.begin() + w, sliced.begin() + std::min(sliced.size(), w + kPcgSortWindow),
                          [&](int32_t a, int32_t b) { return cnt3[a] > cnt3[b]; });
     const int64_t nsl = ((int64_t)sliced.size() + 63) / 64;
+    // XCD-aware slice order.  The product's workgroup b takes slice b, and workgroups b and b + 8 run
+    // on one XCD (its own 4 MiB L2).  The 64-row groups of the nested-dissection order are dealt so
+    // that each XCD's slices (b = x mod 8) are one contiguous run of that order: a slice's neighbour
+    // (z, p_prev) gathers then hit lines its XCD's L2 already holds instead of every XCD fetching
+    // the whole vector.
+    std::vector<int32_t> rows(nsl * 64, -1);
+    {
+        static const bool no_xcd = std::getenv("DEFTRI_PCG_NO_XCD") != nullptr;
+        const int nx = (!no_xcd && nsl >= 16) ? 8 : 1;
+        std::vector<int64_t> start(nx + 1, 0);
+        for (int x = 0; x < nx; x++) start[x + 1] = start[x] + (nsl - x + nx - 1) / nx;
+        for (int64_t b = 0; b < nsl; b++) {
+            const int64_t g = start[b % nx] + b / nx;         // spatial group of slice b
+            for (int l = 0; l < 64 && g * 64 + l < (int64_t)sliced.size(); l++) rows[b * 64 + l] = sliced[g * 64 + l];
+        }
+    }
     H.sl_v.assign(nsl * 64, -1);
     H.sl_n.resize(nsl); H.sl_nx.resize(nsl); H.sl_off.resize(nsl); H.sl_xoff.resize(nsl);
     H.sl_hn.resize(nsl); H.sl_hoff.resize(nsl);
@@ -708,8 +724,9 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     int64_t slots = 0, xslots = 0, hslots = 0;
     for (int64_t sl = 0; sl < nsl; sl++) {
         int64_t mn = 0, mx = 0;
-        for (int l = 0; l < 64 && sl * 64 + l < (int64_t)sliced.size(); l++) {
-            const int32_t v = sliced[sl * 64 + l];
+        for (int l = 0; l < 64; l++) {
+            const int32_t v = rows[sl * 64 + l];
+            if (v < 0) continue;
             H.sl_v[sl * 64 + l] = v;
             mn = std::max(mn, cnt3[v]);
             mx = std::max(mx, cntx[v]);

@@ -360,7 +360,8 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
         (rc = dalloc(ctx, &P.Jdep, 4 * (int64_t)P.D)) || (rc = dalloc(ctx, &P.Wdep, P.D)) ||
         (rc = dalloc(ctx, &P.Edep, P.D)) || (rc = dalloc(ctx, &P.chi_dep, P.D)) ||
         (rc = dalloc(ctx, &P.Jarap, 18 * (int64_t)P.E)) || (rc = dalloc(ctx, &P.Warap, P.E)) ||
-        (rc = dalloc(ctx, &P.Earap, P.E)) || (rc = dalloc(ctx, &P.chi_arap, P.E)))
+        (rc = dalloc(ctx, &P.Earap, P.E)) || (rc = dalloc(ctx, &P.chi_arap, P.E)) ||
+        (rc = dalloc(ctx, &P.tg_pre, 12 * 13 * (int64_t)std::max(P.Q, 1))))
         return rc;
     // keep the initial state for deftri_reset_state
     ctx->init_state.resize(3);
