@@ -159,7 +159,10 @@ def test_pcg_profile_reports_kernels(pcg_ctx):
     b, d = pcg_ctx.gradient()
     pcg_ctx.set_linear_solver("pcg", max_iterations=4096)
     st = pcg_ctx.profile_trial(0.1 * np.abs(d).max())
-    for k in ("pcg_setup", "pcg_product", "pcg_update", "hchunk"):
+    # matrix-free product (default): the step builds b and the diagonal blocks only (mf_lin); H is
+    # assembled (hchunk) only for a step that falls back to the LDL^T
+    for k in ("mf_lin", "pcg_setup", "pcg_product", "pcg_update"):
         assert k in st and st[k]["launches"] > 0, k
     assert st["pcg_product"]["bytes"] > 0
+    assert "hchunk" not in st
     assert "update" not in st                 # no factorization when PCG converged

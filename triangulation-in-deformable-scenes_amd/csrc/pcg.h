@@ -84,8 +84,60 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
                     const std::vector<int64_t> &blk_col_dof, const std::vector<int64_t> &elim_pos, PcgHost &out,
                     std::string &err);
 
+// Matrix-free product (round 2, default where the plan fits): H is never assembled for a PCG step.
+// Every 3-dof point is a sliced row (64 per slice, nested-dissection order dealt to XCDs); a slice's
+// workgroup loads the linearized edges touching its points ("local edges": ARAP first, then
+// reprojection, then depth; an edge touching several slices is loaded by each), forms
+// s_e = W_e (J_e p) once per edge and stores J_{e,v}^T s_e per point role in LDS; each lane then
+// sums its row's incidences.  The global rows (T_g, depth scales) are summed from per-slice
+// partials of the edges a slice owns (an edge is owned by the first slice holding one of its
+// points).  The block-Jacobi preconditioner's diagonal blocks and b come from the same structure
+// once per LM iteration (k_mf_lin).  H + b are assembled only if a step falls back to the LDL^T.
+constexpr int kMfMaxH = 4;          // heavy vertices one slice's owned edges may touch (record field: < 8)
+constexpr int kMfMaxLds = 5120;     // doubles of per-slice contributions in LDS (40 KB)
+constexpr int kMfLin = 27;          // per heavy slot of k_mf_lin: 21 (lower 6x6) + 6 (b)
+enum { MF_ARAP = 0, MF_REP = 1, MF_DEP = 2 };
+
+struct PcgMfHost {
+    std::vector<int32_t> heavy_v, h_dofbase, v_heavy, h_first;
+    std::vector<int32_t> sl_v;                     // nsl * 64 rows (-1 padding)
+    std::vector<int64_t> le_off;                   // per slice: first local edge
+    std::vector<int32_t> le_n, le_na;              // per slice: local edges, of which ARAP
+    // local edge record: kind << 62 | role mask << 58 | (heavy slot + 1, 0 = not owned) << 55 |
+    // LDS base << 40 | edge; the roles whose point is in the slice get consecutive 3-vectors at base
+    std::vector<int64_t> le;
+    std::vector<int64_t> in_off;                   // per slice: first incidence slot
+    std::vector<int32_t> in_n;                     // per slice: incidence slots
+    std::vector<int32_t> inc;                      // [slot][64]: LDS offset of the row's 3-vector (-1 padding)
+    std::vector<int32_t> inc2;                     // [slot][64]: local edge << 2 | role (-1 padding)
+    std::vector<int32_t> sl_hn, hs_hk;
+    std::vector<int64_t> sl_hoff, hv_slot_begin, hs_pos;
+    std::vector<int32_t> adof, atdof, rdof, ddof;  // dofs of the edges' vertices
+    std::vector<int64_t> moff;
+    int64_t msize = 0;
+    int32_t max_lds = 0;
+    double product_bytes = 0, product_flops = 0;
+};
+// edges: rep_point[R], dep_point/dep_scale[D], arap_pts[4E], arap_pair[E]; vertex ids T_g q -> q,
+// scale k -> Q + k, point p -> Q + S + p.  False (with err) when the plan does not fit the kernels.
+bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vector<int32_t> &vdim,
+                  const std::vector<int64_t> &elim_pos, int Q, int S, int R, int D, int E,
+                  const int32_t *rep_point, const int32_t *dep_point, const int32_t *dep_scale,
+                  const int32_t *arap_pts, const int32_t *arap_pair, PcgMfHost &out, std::string &err);
+
 struct PcgDev {
     int64_t nv = 0, ndof = 0;
+    int32_t mf = 0, mf_lds = 0;          // matrix-free product; its dynamic LDS (doubles)
+    const int64_t *mf_le_off = nullptr, *mf_le = nullptr, *mf_in_off = nullptr;
+    const int32_t *mf_le_n = nullptr, *mf_le_na = nullptr, *mf_in_n = nullptr, *mf_inc = nullptr, *mf_inc2 = nullptr;
+    const int32_t *mf_adof = nullptr, *mf_atdof = nullptr, *mf_rdof = nullptr, *mf_ddof = nullptr;
+    const double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr;
+    const double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr;
+    const double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr;
+    double *mf_diag = nullptr;           // per vertex (moff): its diagonal block of H
+    double *mf_hlin = nullptr;           // per heavy slot position: kMfLin partials
+    double *mf_dvec = nullptr;           // diagonal of H per dof (max diag)
+    double *b = nullptr;                 // the plan's b (k_mf_lin writes it)
     int32_t nlight = 0, nheavy = 0, nhchunks = 0, nheavy_dofs = 0;
     int32_t nA_light = 0;                // workgroups of the light part of the product launch
     int32_t nsl = 0, nA_sl = 0;          // slices; their workgroups (one per slice) lead the launch
@@ -123,6 +175,9 @@ struct PcgDev {
 
 // after an assembly: the sliced rows' 3x3 blocks from hval into sl_val
 void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st);
+// matrix-free: per LM iteration (after the linearization) the diagonal blocks and b; with
+// want_dvec the diagonal of H per dof too (max diag for the initial lambda)
+void launch_mf_lin(const PcgDev &G, bool want_dvec, hipStream_t st);
 // one solve's launches (x = dx).  setup: preconditioner blocks at lambda, r = b, z = M r, x = 0.
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
                       hipStream_t st);

@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
     if (v < G.nv) {
         const int d = G.vdim[v];
         const int64_t o = G.voff[v];
-        const double *D = hval + G.diag_off[v];
+        const double *D = G.mf ? G.mf_diag + G.moff[v] : hval + G.diag_off[v];
         double A[36];
 #pragma unroll
         for (int i = 0; i < 6; i++)
@@ -561,6 +561,305 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
     wg_pair_tree(rz, rr, red, G.partB + 2 * blockIdx.x);
 }
 
+
+// ---- matrix-free product (pcg.h) ----------------------------------------------------------------
+__device__ __forceinline__ void mf_rec(int64_t r, int &kind, int &mask, int &hs, int &base, int64_t &e) {
+    kind = (int)((uint64_t)r >> 62);
+    mask = (int)((r >> 58) & 0xf);
+    hs = (int)((r >> 55) & 0x7);
+    base = (int)((r >> 40) & 0x7fff);
+    e = r & 0xffffffffffLL;
+}
+
+// fixed butterfly over the wave, then the four waves in order: one value per call
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_PCG_WPE))) k_mf_product(int it, const PcgDev G, double lam) {
+    extern __shared__ double C[];                     // per local edge and point role: J^T s
+    __shared__ double red[4][256];
+    double *rec = G.rec + kPcgRec * (it + 1);
+    const double *prv = G.rec + kPcgRec * it;
+    const int tid = threadIdx.x;
+    if (prv[PR_STATUS] != 0.0) {
+        if (blockIdx.x == 0 && tid == 0) { rec[PR_STATUS] = prv[PR_STATUS]; rec[PR_ITS] = prv[PR_ITS]; }
+        return;
+    }
+    double rz, rr;
+    wg_sum2(G.partB, G.nB, rz, rr, red);
+    const double bb = it == 0 ? rr : G.rec[kPcgRec + PR_RR];
+    const bool conv = rr <= G.tol2 * bb;
+    if (blockIdx.x == 0 && tid == 0) {
+        rec[PR_RZ] = rz;
+        rec[PR_RR] = rr;
+        rec[PR_STATUS] = conv ? kPcgConverged : kPcgRunning;
+        rec[PR_ITS] = it;
+    }
+    if (conv) return;
+    const double beta = it == 0 ? 0.0 : rz / prv[PR_RZ];
+    const double *zp = G.zp;
+    const int sl = blockIdx.x;
+    const bool live = sl < G.nsl;
+    const int w = tid >> 6, lane = tid & 63;
+    // phase A: s_e = W_e (J_e p) per local edge, J_{e,v}^T s_e into LDS, owned edges' heavy parts
+    const int64_t l0 = live ? G.mf_le_off[sl] : 0;
+    const int ne = live ? G.mf_le_n[sl] : 0;
+    double hacc[kMfMaxH][6];
+#pragma unroll
+    for (int h = 0; h < kMfMaxH; h++)
+#pragma unroll
+        for (int i = 0; i < 6; i++) hacc[h][i] = 0.0;
+    for (int k = tid; k < ne; k += 256) {
+        int kind, mask, hs, base;
+        int64_t e;
+        mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
+        double hv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (kind == MF_ARAP) {
+            const int4 d = reinterpret_cast<const int4 *>(G.mf_adof)[e];
+            const int td = G.mf_atdof[e];
+            const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e;
+            double J[18];
+#pragma unroll
+            for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J[2 * q] = t.x; J[2 * q + 1] = t.y; }
+            const int dd[4] = {d.x, d.y, d.z, d.w};
+            double dot = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int i = 0; i < 3; i++) dot += J[3 * r + i] * pval(zp, beta, dd[r] + i);
+#pragma unroll
+            for (int i = 0; i < 6; i++) dot += J[12 + i] * pval(zp, beta, td + i);
+            const double sv = G.Warap[e] * dot;
+            int pos = base;                           // the roles whose point is in this slice
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if ((mask >> r) & 1) {
+#pragma unroll
+                    for (int i = 0; i < 3; i++) C[pos + i] = J[3 * r + i] * sv;
+                    pos += 3;
+                }
+#pragma unroll
+            for (int i = 0; i < 6; i++) hv[i] = J[12 + i] * sv;
+        } else if (kind == MF_REP) {
+            const int pd = G.mf_rdof[e];
+            const double *J = G.Jrep + 6 * e;
+            double p3[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) p3[i] = pval(zp, beta, pd + i);
+            const double wv = G.Wrep[e];
+            const double s0 = wv * ((J[0] * p3[0] + J[1] * p3[1]) + J[2] * p3[2]);
+            const double s1 = wv * ((J[3] * p3[0] + J[4] * p3[1]) + J[5] * p3[2]);
+#pragma unroll
+            for (int i = 0; i < 3; i++) C[base + i] = J[i] * s0 + J[3 + i] * s1;
+        } else {
+            const int pd = G.mf_ddof[2 * e], sd = G.mf_ddof[2 * e + 1];
+            const double *J = G.Jdep + 4 * e;
+            const double sv = G.Wdep[e] * (((J[0] * pval(zp, beta, pd) + J[1] * pval(zp, beta, pd + 1)) +
+                                            J[2] * pval(zp, beta, pd + 2)) + J[3] * pval(zp, beta, sd));
+#pragma unroll
+            for (int i = 0; i < 3; i++) C[base + i] = J[i] * sv;
+            hv[0] = J[3] * sv;
+        }
+        if (hs > 0)
+#pragma unroll
+            for (int h = 0; h < kMfMaxH; h++)
+                if (h == hs - 1)
+#pragma unroll
+                    for (int i = 0; i < 6; i++) hacc[h][i] += hv[i];
+    }
+    // the owned edges' heavy-row partials: per heavy slot, butterfly per wave, waves in order
+    const int nh = live ? G.sl_hn[sl] : 0;
+    for (int h = 0; h < nh; h++) {
+        double hh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < kMfMaxH; q++)
+            if (q == h)
+#pragma unroll
+                for (int i = 0; i < 6; i++) hh[i] = hacc[q][i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const double v = wave_sum(hh[i]);
+            if (lane == 0) red[0][4 * i + w] = v;     // 6 values x 4 waves
+        }
+        __syncthreads();
+        if (tid < 6) {
+            const double *r4 = &red[0][4 * tid];
+            const double v = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+            G.hs_part[G.hs_pos[G.sl_hoff[sl] + h] * 6 + tid] = v;
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    // phase B: lane = row; the four waves take every fourth incidence slot, partial rows meet in LDS
+    const int v = live ? G.sl_v[sl * 64 + lane] : -1;
+    const int64_t o = v >= 0 ? G.voff[v] : 0;
+    double pv[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) pv[i] = v >= 0 ? pval(zp, beta, o + i) : 0.0;
+    double acc[3] = {0.0, 0.0, 0.0};
+    const int64_t i0 = live ? G.mf_in_off[sl] : 0;
+    const int ni = live ? G.mf_in_n[sl] : 0;
+    for (int k = w; k < ni; k += 4) {
+        const int off = G.mf_inc[(i0 + k) * 64 + lane];
+        if (off >= 0)
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[i] += C[off + i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) red[i][tid] = acc[i];
+    __syncthreads();
+    double pqs = 0.0;
+    double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
+    if (w == 0 && v >= 0) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const double a = (red[i][lane] + red[i][64 + lane]) + (red[i][128 + lane] + red[i][192 + lane]);
+            const double qv = a + lam * pv[i];
+            pq2[o + i] = make_double2(pv[i], qv);
+            pqs += pv[i] * qv;
+        }
+    }
+    __syncthreads();
+    const double sum = wg_tree(pqs, red[3]);
+    if (tid == 0 && live) G.partA[blockIdx.x] = sum;
+}
+
+// lower-triangle index of (a, b), a >= b, in a 6 x 6 block
+__device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; }
+
+// per LM iteration: point rows' diagonal blocks and b from their incidences; the owned edges' heavy
+// diagonal blocks and b as per-slot partials (k_mf_lin_heavy sums them)
+__global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
+    __shared__ double red[12][256];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int sl = blockIdx.x;
+    const int64_t l0 = G.mf_le_off[sl];
+    const int ne = G.mf_le_n[sl];
+    const int nh = G.sl_hn[sl];
+    for (int h = 0; h < nh; h++) {
+        double a[kMfLin];
+#pragma unroll
+        for (int q = 0; q < kMfLin; q++) a[q] = 0.0;
+        for (int k = tid; k < ne; k += 256) {
+            int kind, mask, hs, base;
+            int64_t e;
+            mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
+            if (hs != h + 1) continue;
+            if (kind == MF_ARAP) {
+                const double *J = G.Jarap + 18 * e + 12;
+                const double wv = G.Warap[e], er = G.Earap[e];
+#pragma unroll
+                for (int i = 0; i < 6; i++) {
+                    const double ai = J[i] * wv;
+#pragma unroll
+                    for (int j = 0; j <= i; j++) a[tri6(i, j)] += ai * J[j];
+                    a[21 + i] -= J[i] * (wv * er);
+                }
+            } else if (kind == MF_DEP) {
+                const double Js = G.Jdep[4 * e + 3], wv = G.Wdep[e], er = G.Edep[e];
+                a[0] += (Js * wv) * Js;
+                a[21] -= Js * (wv * er);
+            }
+        }
+        double *out = G.mf_hlin + G.hs_pos[G.sl_hoff[sl] + h] * kMfLin;
+        for (int q0 = 0; q0 < kMfLin; q0 += 12) {
+#pragma unroll
+            for (int q = 0; q < 12; q++) {
+                double vq = 0.0;
+#pragma unroll
+                for (int u = 0; u < kMfLin; u++)
+                    if (u == q0 + q) vq = a[u];
+                vq = wave_sum(vq);
+                if (lane == 0) red[q][w] = vq;
+            }
+            __syncthreads();
+            if (tid < 12 && q0 + tid < kMfLin)
+                out[q0 + tid] = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+            __syncthreads();
+        }
+    }
+    // point rows
+    const int v = G.sl_v[sl * 64 + lane];
+    double acc[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) acc[q] = 0.0;
+    const int64_t i0 = G.mf_in_off[sl];
+    const int ni = G.mf_in_n[sl];
+    for (int k = w; k < ni; k += 4) {
+        const int ir = G.mf_inc2[(i0 + k) * 64 + lane];
+        if (ir < 0) continue;
+        const int kl = ir >> 2, role = ir & 3;
+        int kind, mask, hs, base;
+        int64_t e;
+        mf_rec(G.mf_le[l0 + kl], kind, mask, hs, base, e);
+        const double *J;
+        double wv, er0, er1 = 0.0;
+        int m = 1;
+        if (kind == MF_ARAP) { J = G.Jarap + 18 * e + 3 * role; wv = G.Warap[e]; er0 = G.Earap[e]; }
+        else if (kind == MF_REP) { J = G.Jrep + 6 * e; wv = G.Wrep[e]; er0 = G.Erep[2 * e]; er1 = G.Erep[2 * e + 1]; m = 2; }
+        else { J = G.Jdep + 4 * e; wv = G.Wdep[e]; er0 = G.Edep[e]; }
+        for (int r = 0; r < m; r++) {
+            const double er = r == 0 ? er0 : er1;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const double ai = J[3 * r + i] * wv;
+#pragma unroll
+                for (int j = 0; j < 3; j++) acc[3 * i + j] += ai * J[3 * r + j];
+                acc[9 + i] -= J[3 * r + i] * (wv * er);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 12; q++) red[q][tid] = acc[q];
+    __syncthreads();
+    if (w == 0 && v >= 0) {
+        double *D = G.mf_diag + G.moff[v];
+        const int64_t o = G.voff[v];
+#pragma unroll
+        for (int q = 0; q < 12; q++) {
+            const double t = (red[q][lane] + red[q][64 + lane]) + (red[q][128 + lane] + red[q][192 + lane]);
+            if (q < 9) D[q] = t;
+            else G.b[o + q - 9] = t;
+        }
+    }
+}
+
+// heavy rows: workgroup (heavy vertex, value) sums the value over the vertex's slot partials in
+// position order (strided per thread, fixed tree); values 0..20 the lower 6 x 6 block, 21..26 b
+__global__ void __launch_bounds__(256) k_mf_lin_heavy(const PcgDev G) {
+    __shared__ double red[256];
+    const int hk = blockIdx.x / kMfLin, q = blockIdx.x % kMfLin;
+    const int v = G.heavy_v[hk], d = G.vdim[v];
+    int a = 0, bcol = 0;
+    if (q < 21) { while ((a + 1) * (a + 2) / 2 <= q) a++; bcol = q - a * (a + 1) / 2; if (a >= d) return; }
+    else if (q - 21 >= d) return;
+    const int64_t p0 = G.hv_slot_begin[hk], p1 = G.hv_slot_begin[hk + 1];
+    double s = 0.0;
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) s += G.mf_hlin[p * kMfLin + q];
+    s = wg_tree(s, red);
+    if (threadIdx.x == 0) {
+        if (q < 21) {
+            double *D = G.mf_diag + G.moff[v];
+            D[a * d + bcol] = s;
+            D[bcol * d + a] = s;
+        } else {
+            G.b[G.voff[v] + q - 21] = s;
+        }
+    }
+}
+
+// the diagonal of H per dof (for max diag)
+__global__ void k_mf_dvec(const PcgDev G) {
+    const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (v >= G.nv) return;
+    const int d = G.vdim[v];
+    const double *D = G.mf_diag + G.moff[v];
+    for (int i = 0; i < d; i++) G.mf_dvec[G.voff[v] + i] = D[i * d + i];
+}
+
 }  // namespace dev
 
 void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st) {
@@ -569,6 +868,21 @@ void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st) {
     const unsigned grid = (unsigned)(((G.nslots + G.nhslots) * 64 + 255) / 256);
     hipLaunchKernelGGL(dev::k_pcg_repack, dim3(grid), dim3(256), 0, st, G, hval);
     prof_end("pcg_repack", e0, grid, 0.0, st);
+}
+
+void launch_mf_lin(const PcgDev &G, bool want_dvec, hipStream_t st) {
+    if (G.nsl > 0) {
+        hipEvent_t e0 = prof_begin(st);
+        hipLaunchKernelGGL(dev::k_mf_lin, dim3(G.nsl), dim3(256), 0, st, G);
+        prof_end("mf_lin", e0, G.nsl, 0.0, st);
+    }
+    if (G.nheavy > 0) {
+        hipEvent_t e0 = prof_begin(st);
+        hipLaunchKernelGGL(dev::k_mf_lin_heavy, dim3(G.nheavy * kMfLin), dim3(256), 0, st, G);
+        prof_end("mf_lin_heavy", e0, G.nheavy * kMfLin, 0.0, st);
+    }
+    if (want_dvec && G.nv > 0)
+        hipLaunchKernelGGL(dev::k_mf_dvec, dim3((unsigned)((G.nv + 255) / 256)), dim3(256), 0, st, G);
 }
 
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
@@ -583,7 +897,11 @@ void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lamb
     hipEvent_t e0 = prof_begin(st);
     // always launched (also with no slices): its workgroup 0 writes the iteration record
     const unsigned grid = (unsigned)std::max(G.nA_sl, 1);
-    hipLaunchKernelGGL(dev::k_pcg_product, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
+    if (G.mf)
+        hipLaunchKernelGGL(dev::k_mf_product, dim3(grid), dim3(256), sizeof(double) * (size_t)G.mf_lds, st, it, G,
+                           lambda);
+    else
+        hipLaunchKernelGGL(dev::k_pcg_product, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
     prof_end("pcg_product", e0, grid, 0.0, st);
 }
 
@@ -811,6 +1129,215 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     }
     H.moff.resize(nv);
     for (int64_t v = 0; v < nv; v++) { H.moff[v] = H.msize; H.msize += (int64_t)vdim[v] * vdim[v]; }
+    return true;
+}
+
+// ---- host: the matrix-free plan -----------------------------------------------------------------
+bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vector<int32_t> &vdim,
+                  const std::vector<int64_t> &elim_pos, int Q, int S, int R, int D, int E,
+                  const int32_t *rep_point, const int32_t *dep_point, const int32_t *dep_scale,
+                  const int32_t *arap_pts, const int32_t *arap_pair, PcgMfHost &H, std::string &err) {
+    H = PcgMfHost();
+    const int64_t ndof = nv > 0 ? voff[nv - 1] + vdim[nv - 1] : 0;
+    if (ndof >= (int64_t)INT32_MAX) { err = "dof count exceeds int32"; return false; }
+    const int64_t P = nv - Q - S;
+    if (P < 0) { err = "vertex count below pairs + scales"; return false; }
+    auto vP = [&](int64_t p) { return (int64_t)Q + S + p; };
+    // vertex classes: 3-dof points are sliced rows; every other vertex (T_g, scales) a heavy row
+    H.v_heavy.assign(nv, -1);
+    H.h_dofbase.push_back(0);
+    std::vector<int32_t> sliced;
+    for (int64_t v = 0; v < nv; v++) {
+        if (vdim[v] < 1 || vdim[v] > 6) { err = "vertex dimension outside 1..6"; return false; }
+        if (v >= (int64_t)Q + S && vdim[v] == 3) {
+            sliced.push_back((int32_t)v);
+        } else {
+            H.v_heavy[v] = (int32_t)H.heavy_v.size();
+            H.heavy_v.push_back((int32_t)v);
+            H.h_dofbase.push_back(H.h_dofbase.back() + vdim[v]);
+        }
+    }
+    if (H.h_dofbase.back() > kPcgMaxHeavyDofs) { err = "too many heavy-row dofs"; return false; }
+    H.h_first.assign(H.heavy_v.size() + 1, 0);
+    // incidences per point (edge kind, edge, role)
+    std::vector<int32_t> cnt(P + 1, 0);
+    for (int e = 0; e < R; e++) cnt[rep_point[e] + 1]++;
+    for (int e = 0; e < D; e++) cnt[dep_point[e] + 1]++;
+    for (int64_t e = 0; e < E; e++)
+        for (int r = 0; r < 4; r++) cnt[arap_pts[4 * e + r] + 1]++;
+    for (int i = 0; i < P; i++)
+        if (vdim[vP(i)] != 3) { err = "point vertex not 3-dof"; return false; }
+    // rows: nested-dissection order, by descending incidence count inside windows, 64 per slice,
+    // dealt to XCDs in contiguous runs (as build_pcg_host)
+    std::sort(sliced.begin(), sliced.end(), [&](int32_t a, int32_t b) { return elim_pos[a] < elim_pos[b]; });
+    auto pidx = [&](int32_t v) { return (int64_t)v - Q - S; };
+    for (size_t w = 0; w < sliced.size(); w += kPcgSortWindow)
+        std::stable_sort(sliced.begin() + w, sliced.begin() + std::min(sliced.size(), w + kPcgSortWindow),
+                         [&](int32_t a, int32_t b) { return cnt[pidx(a) + 1] > cnt[pidx(b) + 1]; });
+    const int64_t nsl = ((int64_t)sliced.size() + 63) / 64;
+    H.sl_v.assign(nsl * 64, -1);
+    {
+        static const bool no_xcd = std::getenv("DEFTRI_PCG_NO_XCD") != nullptr;
+        const int nx = (!no_xcd && nsl >= 16) ? 8 : 1;
+        std::vector<int64_t> start(nx + 1, 0);
+        for (int x = 0; x < nx; x++) start[x + 1] = start[x] + (nsl - x + nx - 1) / nx;
+        for (int64_t b = 0; b < nsl; b++) {
+            const int64_t g = start[b % nx] + b / nx;
+            for (int l = 0; l < 64 && g * 64 + l < (int64_t)sliced.size(); l++) H.sl_v[b * 64 + l] = sliced[g * 64 + l];
+        }
+    }
+    std::vector<int32_t> pslice(P, -1), plane(P, -1);
+    for (int64_t sl = 0; sl < nsl; sl++)
+        for (int l = 0; l < 64; l++) {
+            const int32_t v = H.sl_v[sl * 64 + l];
+            if (v >= 0) { pslice[pidx(v)] = (int32_t)sl; plane[pidx(v)] = l; }
+        }
+    // per slice: its local edges (an edge is listed by every slice holding one of its points)
+    std::vector<std::vector<int64_t>> sl_edges(nsl);      // kind << 40 | edge
+    auto add_local = [&](int kind, int64_t e, const int32_t *pts, int np) {
+        int32_t seen[4];
+        int ns = 0;
+        for (int r = 0; r < np; r++) {
+            const int32_t s0 = pslice[pts[r]];
+            bool dup = false;
+            for (int q = 0; q < ns; q++) dup |= seen[q] == s0;
+            if (!dup) { seen[ns++] = s0; sl_edges[s0].push_back(((int64_t)kind << 40) | e); }
+        }
+    };
+    if ((int64_t)E >= (1LL << 40) || kMfMaxLds > 0x7fff || kMfMaxH > 7) { err = "record fields overflow"; return false; }
+    for (int64_t e = 0; e < E; e++) add_local(MF_ARAP, e, arap_pts + 4 * e, 4);
+    for (int e = 0; e < R; e++) add_local(MF_REP, e, rep_point + e, 1);
+    for (int e = 0; e < D; e++) add_local(MF_DEP, e, dep_point + e, 1);
+    H.le_off.resize(nsl); H.le_n.resize(nsl); H.le_na.resize(nsl);
+    H.in_off.resize(nsl); H.in_n.resize(nsl); H.sl_hn.resize(nsl); H.sl_hoff.resize(nsl);
+    int64_t nle = 0, nin = 0, hslots = 0;
+    std::vector<std::vector<int32_t>> sl_heavy(nsl);
+    auto owner = [&](int kind, int64_t e) -> int32_t {
+        if (kind == MF_REP) return pslice[rep_point[e]];
+        if (kind == MF_DEP) return pslice[dep_point[e]];
+        int32_t o = INT32_MAX;
+        for (int r = 0; r < 4; r++) o = std::min(o, pslice[arap_pts[4 * e + r]]);
+        return o;
+    };
+    auto heavy_of = [&](int kind, int64_t e) -> int32_t {   // heavy index of the edge's global vertex, -1 none
+        if (kind == MF_ARAP) return H.v_heavy[arap_pair[e]];
+        if (kind == MF_DEP) return H.v_heavy[(int64_t)Q + dep_scale[e]];
+        return -1;
+    };
+    for (int64_t sl = 0; sl < nsl; sl++) {
+        auto &L = sl_edges[sl];
+        std::sort(L.begin(), L.end());        // ARAP, then reprojection, then depth, edges ascending
+        int32_t na = 0;
+        for (int64_t x : L) na += (x >> 40) == MF_ARAP;
+        for (int64_t x : L) {
+            const int kind = (int)(x >> 40);
+            const int64_t e = x & 0xffffffffffLL;
+            const int32_t hk = heavy_of(kind, e);
+            if (hk >= 0 && owner(kind, e) == sl) sl_heavy[sl].push_back(hk);
+        }
+        std::sort(sl_heavy[sl].begin(), sl_heavy[sl].end());
+        sl_heavy[sl].erase(std::unique(sl_heavy[sl].begin(), sl_heavy[sl].end()), sl_heavy[sl].end());
+        if ((int)sl_heavy[sl].size() > kMfMaxH) { err = "a slice owns edges of more than kMfMaxH global vertices"; return false; }
+        int64_t lds = 0;                      // one 3-vector per (local edge, role in this slice)
+        for (int64_t x : L) {
+            const int kind = (int)(x >> 40);
+            const int64_t e = x & 0xffffffffffLL;
+            if (kind != MF_ARAP) { lds += 3; continue; }
+            for (int r = 0; r < 4; r++) lds += 3 * (pslice[arap_pts[4 * e + r]] == sl);
+        }
+        if (lds > kMfMaxLds) { err = "a slice's local edges exceed the LDS budget"; return false; }
+        H.max_lds = std::max<int32_t>(H.max_lds, (int32_t)lds);
+        H.le_off[sl] = nle; H.le_n[sl] = (int32_t)L.size(); H.le_na[sl] = na;
+        H.sl_hn[sl] = (int32_t)sl_heavy[sl].size(); H.sl_hoff[sl] = hslots;
+        nle += (int64_t)L.size();
+        hslots += (int64_t)sl_heavy[sl].size();
+    }
+    H.le.resize(nle);
+    H.hs_hk.resize(hslots);
+    // incidences: per row, (local edge, role) in local-edge order
+    std::vector<std::vector<int32_t>> rowinc(64), rowinc2(64);
+    for (int64_t sl = 0; sl < nsl; sl++) {
+        const auto &L = sl_edges[sl];
+        for (size_t k = 0; k < sl_heavy[sl].size(); k++) H.hs_hk[H.sl_hoff[sl] + k] = sl_heavy[sl][k];
+        for (auto &r : rowinc) r.clear();
+        for (auto &r : rowinc2) r.clear();
+        int32_t base = 0;
+        for (size_t k = 0; k < L.size(); k++) {
+            const int kind = (int)(L[k] >> 40);
+            const int64_t e = L[k] & 0xffffffffffLL;
+            int64_t hs = 0;
+            const int32_t hk = heavy_of(kind, e);
+            if (hk >= 0 && owner(kind, e) == sl)
+                hs = 1 + (std::lower_bound(sl_heavy[sl].begin(), sl_heavy[sl].end(), hk) - sl_heavy[sl].begin());
+            int64_t mask = 0;
+            const int32_t b0 = base;
+            if (kind == MF_ARAP) {
+                for (int r = 0; r < 4; r++) {
+                    const int32_t p = arap_pts[4 * e + r];
+                    if (pslice[p] != sl) continue;
+                    mask |= 1LL << r;
+                    rowinc[plane[p]].push_back(base);
+                    rowinc2[plane[p]].push_back(((int32_t)k << 2) | r);
+                    base += 3;
+                }
+            } else {
+                const int32_t p = kind == MF_REP ? rep_point[e] : dep_point[e];
+                mask = 1;
+                rowinc[plane[p]].push_back(base);
+                rowinc2[plane[p]].push_back((int32_t)k << 2);
+                base += 3;
+            }
+            H.le[H.le_off[sl] + k] = ((int64_t)kind << 62) | (mask << 58) | (hs << 55) | ((int64_t)b0 << 40) | e;
+        }
+        size_t mx = 0;
+        for (const auto &r : rowinc) mx = std::max(mx, r.size());
+        H.in_off[sl] = nin; H.in_n[sl] = (int32_t)mx;
+        H.inc.resize((size_t)(nin + (int64_t)mx) * 64, -1);
+        H.inc2.resize((size_t)(nin + (int64_t)mx) * 64, -1);
+        for (int l = 0; l < 64; l++)
+            for (size_t k = 0; k < rowinc[l].size(); k++) {
+                H.inc[(nin + (int64_t)k) * 64 + l] = rowinc[l][k];
+                H.inc2[(nin + (int64_t)k) * 64 + l] = rowinc2[l][k];
+            }
+        nin += (int64_t)mx;
+    }
+    H.hv_slot_begin.assign(H.heavy_v.size() + 1, 0);
+    for (int64_t g = 0; g < hslots; g++) H.hv_slot_begin[H.hs_hk[g] + 1]++;
+    for (size_t k = 0; k < H.heavy_v.size(); k++) H.hv_slot_begin[k + 1] += H.hv_slot_begin[k];
+    H.hs_pos.resize(hslots);
+    {
+        std::vector<int64_t> f(H.hv_slot_begin.begin(), H.hv_slot_begin.end() - 1);
+        for (int64_t g = 0; g < hslots; g++) H.hs_pos[g] = f[H.hs_hk[g]]++;
+    }
+    // the edges' vertex dofs
+    H.adof.resize(4 * (size_t)E); H.atdof.resize(E); H.rdof.resize(R); H.ddof.resize(2 * (size_t)D);
+    for (int64_t e = 0; e < E; e++) {
+        for (int r = 0; r < 4; r++) H.adof[4 * e + r] = (int32_t)voff[vP(arap_pts[4 * e + r])];
+        H.atdof[e] = (int32_t)voff[arap_pair[e]];
+    }
+    for (int e = 0; e < R; e++) H.rdof[e] = (int32_t)voff[vP(rep_point[e])];
+    for (int e = 0; e < D; e++) {
+        H.ddof[2 * e] = (int32_t)voff[vP(dep_point[e])];
+        H.ddof[2 * e + 1] = (int32_t)voff[(int64_t)Q + dep_scale[e]];
+    }
+    H.moff.resize(nv);
+    for (int64_t v = 0; v < nv; v++) { H.moff[v] = H.msize; H.msize += (int64_t)vdim[v] * vdim[v]; }
+    // bytes one product launch loads / stores apart from the edges' (z, p_prev) gathers: per local
+    // edge its record, Jacobian, weight and vertex dofs (an edge touching k slices counted k times),
+    // the incidence slots, own (z, p_prev) read and (p, q) written, heavy partials; flops: 2 per
+    // Jacobian entry for J p and J^T s
+    {
+        double by = 32.0 * (double)ndof + 4.0 * 64.0 * (double)nin + 48.0 * (double)hslots, fl = 0;
+        for (int64_t sl = 0; sl < nsl; sl++)
+            for (int k = 0; k < H.le_n[sl]; k++) {
+                const int kind = (int)((uint64_t)H.le[H.le_off[sl] + k] >> 62);
+                if (kind == MF_ARAP) { by += 8 + 144 + 8 + 16 + 4; fl += 4 * 18; }
+                else if (kind == MF_REP) { by += 8 + 48 + 8 + 4; fl += 4 * 6; }
+                else { by += 8 + 32 + 8 + 8; fl += 4 * 4; }
+            }
+        H.product_bytes = by;
+        H.product_flops = fl;
+    }
     return true;
 }
 

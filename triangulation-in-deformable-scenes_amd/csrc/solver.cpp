@@ -152,13 +152,15 @@ struct deftri_ctx {
     double pcg_tol = kPcgDefaultTol;
     int pcg_max_it = 0;                     // 0: pcg_auto_it
     bool pcg_avail = false;                 // single-rank plan with a row view on the device
-    std::string pcg_why;                    // why not, when not
+    std::string pcg_why;                    // why not (or why not matrix-free), when not
+    bool pcg_mf = false;                    // the matrix-free product (pcg.h)
     PcgDev G;
     double pcg_bytes = 0, pcg_flops = 0;    // per product launch (profile_trial roofline)
     int pcg_auto_it = kPcgDefaultMaxIt;     // default budget of the uploaded plan (cost model)
     int pcg_last_its = 8;                   // iterations of the last converged solve (first chunk size)
     int pcg_step_its = 0, pcg_step_solved = 0;   // the last PCG step (deftri_last_step_info)
     bool pcg_packed = false;                // sliced blocks repacked from the current assembly
+    bool assembled = false;                 // L.hval / L.b hold the current linearization's H, b
 };
 
 namespace {
@@ -334,6 +336,80 @@ int refresh_values(deftri_ctx *ctx, const HostProblem &h) {
     return 0;
 }
 
+bool mf_wanted() {
+    static const bool on = [] { const char *e = std::getenv("DEFTRI_PCG_MF"); return !e || std::atoi(e) != 0; }();
+    return on;
+}
+
+// the PCG budget: CG iterations that cost about one factorization + substitution, from plan sizes
+// only (deterministic: the same problem always takes the same path).  Rates measured at C2: the
+// LDL^T trial ~7 TF/s + ~50 us per tree level, a CG iteration ~2 TB/s of its product's bytes + ~15 us
+// of launch latency
+int pcg_budget(const Symbolic &S, double product_bytes) {
+    const double t_fac = S.factor_flops / 7e9 + 0.05 * S.nlevels;   // ms
+    const double t_it = product_bytes / 2e9 + 0.015;
+    return (int)std::min<double>(kPcgMaxIt, std::max(8.0, std::ceil(t_fac / t_it)));
+}
+
+// the matrix-free PCG plan on the device (single-rank); 0 when available, else ctx->pcg_why says why
+int upload_pcg_mf(deftri_ctx *ctx, const HostProblem &h) {
+    const Symbolic &S = ctx->S;
+    const deftri_problem_desc &d = h.d;
+    const DevProblem &P = ctx->P;
+    PcgMfHost mh;
+    std::string why;
+    if (!build_pcg_mf(S.nv, S.voff, S.vdim, S.elim_pos, d.n_pairs, d.n_scales, d.n_rep, d.n_depth, d.n_arap,
+                      h.rep_point.data(), h.dep_point.data(), h.dep_scale.data(), h.arap_pts.data(),
+                      h.arap_pair.data(), mh, why)) {
+        ctx->pcg_why = "matrix-free plan: " + why;
+        return -1;
+    }
+    int rc;
+#define PUT(dst, src) if ((rc = dput(ctx, &(dst), src))) return rc
+    PcgDev &G = ctx->G;
+    G = PcgDev();
+    G.mf = 1;
+    G.mf_lds = std::max(mh.max_lds, 1);
+    G.nv = S.nv; G.ndof = S.ndof;
+    G.nheavy = (int32_t)mh.heavy_v.size();
+    G.nheavy_dofs = mh.h_dofbase.back();
+    G.nsl = (int32_t)mh.le_n.size();
+    G.nA_sl = G.nsl;
+    G.nB = (int32_t)((S.nv + 255) / 256);
+    int32_t *hv, *hdb, *vh, *hf, *sv, *len, *lena, *inn, *inc, *inc2, *shn, *hshk, *ad, *atd, *rd, *dd;
+    int64_t *mo, *leo, *le, *ino, *shoff, *hvb, *hvs;
+    PUT(hv, mh.heavy_v); PUT(hdb, mh.h_dofbase); PUT(vh, mh.v_heavy); PUT(hf, mh.h_first); PUT(mo, mh.moff);
+    PUT(sv, mh.sl_v); PUT(leo, mh.le_off); PUT(len, mh.le_n); PUT(lena, mh.le_na); PUT(le, mh.le);
+    PUT(ino, mh.in_off); PUT(inn, mh.in_n); PUT(inc, mh.inc); PUT(inc2, mh.inc2);
+    PUT(shn, mh.sl_hn); PUT(hshk, mh.hs_hk); PUT(shoff, mh.sl_hoff); PUT(hvb, mh.hv_slot_begin); PUT(hvs, mh.hs_pos);
+    PUT(ad, mh.adof); PUT(atd, mh.atdof); PUT(rd, mh.rdof); PUT(dd, mh.ddof);
+#undef PUT
+    G.heavy_v = hv; G.h_dofbase = hdb; G.v_heavy = vh; G.h_first = hf; G.moff = mo;
+    G.sl_v = sv; G.mf_le_off = leo; G.mf_le_n = len; G.mf_le_na = lena; G.mf_le = le;
+    G.mf_in_off = ino; G.mf_in_n = inn; G.mf_inc = inc; G.mf_inc2 = inc2;
+    G.sl_hn = shn; G.hs_hk = hshk; G.sl_hoff = shoff; G.hv_slot_begin = hvb; G.hs_pos = hvs;
+    G.nhslots = (int64_t)mh.hs_hk.size();
+    G.mf_adof = ad; G.mf_atdof = atd; G.mf_rdof = rd; G.mf_ddof = dd;
+    G.voff = ctx->L.voff; G.vdim = ctx->L.vdim;
+    G.Jarap = P.Jarap; G.Warap = P.Warap; G.Earap = P.Earap;
+    G.Jrep = P.Jrep; G.Wrep = P.Wrep; G.Erep = P.Erep;
+    G.Jdep = P.Jdep; G.Wdep = P.Wdep; G.Edep = P.Edep;
+    G.b = ctx->L.b;
+    if ((rc = dalloc(ctx, &G.hs_part, 6 * std::max<int64_t>(G.nhslots, 1))) ||
+        (rc = dalloc(ctx, &G.mf_hlin, kMfLin * std::max<int64_t>(G.nhslots, 1))) ||
+        (rc = dalloc(ctx, &G.hqf, std::max(G.nheavy_dofs, 1))) || (rc = dalloc(ctx, &G.mf_diag, mh.msize)) ||
+        (rc = dalloc(ctx, &G.mf_dvec, S.ndof)) || (rc = dalloc(ctx, &G.minv, mh.msize)) ||
+        (rc = dalloc(ctx, &G.r, S.ndof)) || (rc = dalloc(ctx, &G.zp, 2 * S.ndof)) ||
+        (rc = dalloc(ctx, &G.pq, 2 * S.ndof)) || (rc = dalloc(ctx, &G.partA, std::max(G.nA_sl, 1))) ||
+        (rc = dalloc(ctx, &G.partB, 2 * (int64_t)G.nB)) || (rc = dalloc(ctx, &G.rec, (int64_t)kPcgRec * (kPcgMaxIt + 2))))
+        return rc;
+    ctx->pcg_avail = true;
+    ctx->pcg_bytes = mh.product_bytes;
+    ctx->pcg_flops = mh.product_flops;
+    ctx->pcg_auto_it = pcg_budget(S, mh.product_bytes);
+    return 0;
+}
+
 int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     const deftri_problem_desc &d = h.d;
     DevProblem &P = ctx->P;
@@ -450,8 +526,11 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     if ((rc = dalloc(ctx, &ctx->d_scal, 8))) return rc;
     ctx->pcg_avail = false;
     ctx->pcg_why.clear();
+    ctx->pcg_mf = false;
     if (ctx->dist()) {
         ctx->pcg_why = "point-sharded plan";
+    } else if (mf_wanted() && upload_pcg_mf(ctx, h) == 0) {
+        ctx->pcg_mf = true;                   // matrix-free product (pcg.h)
     } else {
         PcgHost ph;
         if (!build_pcg_host(S.nv, S.voff, S.vdim, S.blk_val_off, S.blk_rows, S.blk_cols, S.blk_row_dof, S.blk_col_dof,
@@ -513,15 +592,12 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
             const double by = ph.product_bytes, fl = ph.product_flops;
             ctx->pcg_bytes = by;
             ctx->pcg_flops = fl;
-            // default budget: CG iterations that cost about one factorization + substitution, from
-            // plan sizes only (deterministic: the same problem always takes the same path).  Rates
-            // measured at C2: the LDL^T trial ~7 TF/s + ~50 us per tree level, a CG iteration ~2 TB/s
-            // of its product's bytes + ~15 us of launch latency
-            const double t_fac = S.factor_flops / 7e9 + 0.05 * S.nlevels;   // ms
-            const double t_it = by / 2e9 + 0.015;
-            ctx->pcg_auto_it = (int)std::min<double>(kPcgMaxIt, std::max(8.0, std::ceil(t_fac / t_it)));
+            ctx->pcg_auto_it = pcg_budget(S, by);
         }
     }
+    if (std::getenv("DEFTRI_PCG_LOG"))
+        std::fprintf(stderr, "[deftri] pcg: %s (budget %d)%s%s\n", !ctx->pcg_avail ? "unavailable" : ctx->pcg_mf ? "matrix-free" : "assembled",
+                     ctx->pcg_auto_it, ctx->pcg_why.empty() ? "" : ": ", ctx->pcg_why.c_str());
     if (ctx->dist()) {
         if ((rc = dalloc(ctx, &ctx->d_xbuf, S.dist.xbuf_size))) return rc;
         if ((rc = dalloc(ctx, &ctx->d_diagv, S.ndof))) return rc;
@@ -702,6 +778,25 @@ void pop_state(deftri_ctx *ctx) {
 }
 
 bool use_pcg(const deftri_ctx *ctx) { return ctx->lin_solver == DEFTRI_SOLVER_PCG && ctx->pcg_avail; }
+
+// buildSystem after a linearization.  A matrix-free PCG step reads only b and the diagonal blocks
+// (k_mf_lin; with want_dvec also the diagonal per dof for max diag); every other step solver
+// assembles H and b.  ensure_assembled: H for a step that falls back to the LDL^T.
+void build_system(deftri_ctx *ctx, bool pcg_step, bool want_dvec = false) {
+    ctx->pcg_packed = false;
+    if (pcg_step && ctx->G.mf) {
+        launch_mf_lin(ctx->G, want_dvec, ctx->st);
+        ctx->assembled = false;
+    } else {
+        launch_assemble(ctx->P, ctx->L, ctx->st);
+        ctx->assembled = true;
+    }
+}
+void ensure_assembled(deftri_ctx *ctx) {
+    if (ctx->assembled) return;
+    launch_assemble(ctx->P, ctx->L, ctx->st);
+    ctx->assembled = true;
+}
 
 int lane_count(const deftri_ctx *ctx) {
     if (ctx->dist()) return 1;              // point-sharded: one trial at a time (the transfers are per trial)
@@ -1037,8 +1132,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     ctx->hook_rc = 0;
     ctx->hook_x = ctx->d_dx;
     int rc = eval_chi2_dev(ctx, true, ctx->prof_analytic, 0);
-    launch_assemble(ctx->P, ctx->L, ctx->st);
-    ctx->pcg_packed = false;
+    build_system(ctx, use_pcg(ctx));
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     bool solved = false;
     int its = 0;
@@ -1050,7 +1144,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
         set_profiler(&prof);
         if (!rc && solved) {
             const PcgDev &G = ctx->G;
-            launch_pcg_repack(G, ctx->L.hval, ctx->st);      // once per LM iteration (after the assembly)
+            if (!G.mf) launch_pcg_repack(G, ctx->L.hval, ctx->st);   // once per LM iteration (after the assembly)
             launch_pcg_setup(G, ctx->L.hval, ctx->L.b, lambda, ctx->d_dx, ctx->st);
             launch_pcg_product(G, 0, ctx->L.hval, lambda, ctx->st);
             for (int j = 0; j < its; j++) {
@@ -1061,6 +1155,7 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
         }
     }
     if (!solved) {
+        ensure_assembled(ctx);
         launch_scatter(ctx->L, lambda, ctx->st);
         launch_factor(ctx->L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
         launch_solve(ctx->L, ctx->L.b, ctx->d_dx, ctx->st, ctx->dist() ? ctx->L.b : nullptr, hook, ctx);
@@ -1167,7 +1262,7 @@ void pcg_start(deftri_ctx *ctx, double lambda, const double *rhs, int &j) {
     const DevPlan &L = ctx->L;
     G.max_it = ctx->pcg_max_it > 0 ? ctx->pcg_max_it : ctx->pcg_auto_it;
     G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
-    if (!ctx->pcg_packed) {
+    if (!ctx->pcg_packed && !G.mf) {
         launch_pcg_repack(G, L.hval, ctx->st);
         ctx->pcg_packed = true;
     }
@@ -1319,13 +1414,14 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     for (it = 0; it < prm->n_iterations; it++) {
         hipEventRecord(ctx->ev[0], ctx->st);
         if ((rc = eval_chi2_dev(ctx, true, analytic, 0))) return rc;   // computeActiveErrors + linearizeOplus
-        launch_assemble(P, L, ctx->st);                      // buildSystem
-        ctx->pcg_packed = false;
+        build_system(ctx, pcg, it == 0);                    // buildSystem
         if (it == 0) {
             if (dist) {                                      // max of the rank-summed diagonal
                 launch_diag_entries(L, ctx->d_diagv, ctx->st);
                 if ((rc = dist_allreduce(ctx, ctx->d_diagv, L.ndof, 0))) return rc;
                 launch_absmax(L.ndof, ctx->d_diagv, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
+            } else if (!ctx->assembled) {                    // matrix-free: the diagonal from k_mf_lin
+                launch_absmax(L.ndof, ctx->G.mf_dvec, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
             } else {
                 launch_maxdiag(L, ctx->d_part, kRedParts, ctx->d_scal + 2, ctx->st);
             }
@@ -1450,6 +1546,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 if (!solved) hipEventRecord(ctx->ev[2], ctx->st);
             }
             if (!solved) {
+                ensure_assembled(ctx);                       // a matrix-free PCG step left H unassembled
                 ctx->hpin[12] = lambda;                      // pinned: read by the copy at its turn in the stream
                 HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
                 if (launch_trial_graph(ctx)) {
@@ -1670,8 +1767,7 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
     if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
     eval_chi2_dev(ctx, true, true, 0);
-    launch_assemble(ctx->P, ctx->L, ctx->st);
-    ctx->pcg_packed = false;
+    build_system(ctx, false);
     HIPOK(hipStreamSynchronize(ctx->st));
     if (b) HIPOK(hipMemcpy(b, ctx->L.b, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost));
     if (hdiag) {
@@ -1698,8 +1794,7 @@ int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int
     HIPOK(hipMalloc(&dy, sizeof(double) * (size_t)n));
     hipMemcpy(dx, x, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
     eval_chi2_dev(ctx, true, true, 0);
-    launch_assemble(ctx->P, ctx->L, ctx->st);
-    ctx->pcg_packed = false;
+    build_system(ctx, false);
     launch_hmul(ctx->L, ctx->L.blk_row_dof, ctx->L.blk_col_dof, dx, dy, n, ctx->st);
     hipStreamSynchronize(ctx->st);
     hipMemcpy(y, dy, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost);
@@ -1717,8 +1812,8 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
     HIPOK(hipMalloc(&dr, sizeof(double) * (size_t)n));
     hipMemcpy(dr, rhs, sizeof(double) * (size_t)n, hipMemcpyHostToDevice);
     eval_chi2_dev(ctx, true, true, 0);
-    launch_assemble(ctx->P, ctx->L, ctx->st);
-    ctx->pcg_packed = false;
+    build_system(ctx, false);                   // H for the LDL^T; a matrix-free PCG step reads k_mf_lin's
+    if (use_pcg(ctx) && ctx->G.mf) launch_mf_lin(ctx->G, false, ctx->st);
     hipMemsetAsync(ctx->L.flag, 0, sizeof(int), ctx->st);
     bool solved = false;
     if (use_pcg(ctx)) {                         // the configured step solver, as deftri_solve_lm uses it
