@@ -1159,21 +1159,34 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
     }
     if (H.h_dofbase.back() > kPcgMaxHeavyDofs) { err = "too many heavy-row dofs"; return false; }
     H.h_first.assign(H.heavy_v.size() + 1, 0);
-    // incidences per point (edge kind, edge, role)
-    std::vector<int32_t> cnt(P + 1, 0);
-    for (int e = 0; e < R; e++) cnt[rep_point[e] + 1]++;
-    for (int e = 0; e < D; e++) cnt[dep_point[e] + 1]++;
-    for (int64_t e = 0; e < E; e++)
-        for (int r = 0; r < 4; r++) cnt[arap_pts[4 * e + r] + 1]++;
     for (int i = 0; i < P; i++)
         if (vdim[vP(i)] != 3) { err = "point vertex not 3-dof"; return false; }
-    // rows: nested-dissection order, by descending incidence count inside windows, 64 per slice,
-    // dealt to XCDs in contiguous runs (as build_pcg_host)
-    std::sort(sliced.begin(), sliced.end(), [&](int32_t a, int32_t b) { return elim_pos[a] < elim_pos[b]; });
+    // rows: the copies of one mesh vertex (the points an ARAP edge pairs at roles (0, 1) and (2, 3):
+    // the same vertex in the pair's two keyframes) kept together, groups in nested-dissection order
+    // (a group at its first member's position), 64 rows per slice, dealt to XCDs in contiguous runs
+    // (as build_pcg_host).  Every ARAP edge then touches one copy group per mesh vertex, so a slice
+    // holds most of its edges' roles and few edges are loaded by two slices.
     auto pidx = [&](int32_t v) { return (int64_t)v - Q - S; };
-    for (size_t w = 0; w < sliced.size(); w += kPcgSortWindow)
-        std::stable_sort(sliced.begin() + w, sliced.begin() + std::min(sliced.size(), w + kPcgSortWindow),
-                         [&](int32_t a, int32_t b) { return cnt[pidx(a) + 1] > cnt[pidx(b) + 1]; });
+    std::vector<int32_t> grp(P);
+    for (int64_t i = 0; i < P; i++) grp[i] = (int32_t)i;
+    auto find = [&](int32_t x) {
+        while (grp[x] != x) { grp[x] = grp[grp[x]]; x = grp[x]; }
+        return x;
+    };
+    for (int64_t e = 0; e < E; e++)
+        for (int r = 0; r < 4; r += 2) {
+            const int32_t a = find(arap_pts[4 * e + r]), b = find(arap_pts[4 * e + r + 1]);
+            if (a != b) grp[std::max(a, b)] = std::min(a, b);
+        }
+    std::vector<int64_t> gpos(P, INT64_MAX);
+    for (int64_t i = 0; i < P; i++) {
+        const int32_t g = find((int32_t)i);
+        gpos[g] = std::min(gpos[g], elim_pos[vP(i)]);
+    }
+    std::sort(sliced.begin(), sliced.end(), [&](int32_t a, int32_t b) {
+        const int64_t ga = gpos[find((int32_t)pidx(a))], gb = gpos[find((int32_t)pidx(b))];
+        return ga != gb ? ga < gb : elim_pos[a] < elim_pos[b];
+    });
     const int64_t nsl = ((int64_t)sliced.size() + 63) / 64;
     H.sl_v.assign(nsl * 64, -1);
     {
