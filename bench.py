@@ -21,11 +21,12 @@ fronts on the leading ranks; per LM trial RCCL send/recv of one packed contribut
 forward vector and one boundary solution per rank, all-reduce of chi2 / rho denominator / pivot
 flags) — strong scaling.  The barrier and the max-over-ranks time use torch.distributed.
 
-Printed roofline: the dominant kernel of the configured step solver.  PCG (default): the product
-k_pcg_product, HBM-bound — its compulsory bytes per launch (repacked slot records, heavy slots,
-own (z, p_prev) and (p, q); csrc/pcg.hip PcgHost::product_bytes) x active launches / their summed
-device time, against 8 TB/s; `traffic` from the committed rocprofv3 PMC pass when it matches the
-plan.  The factorization's k_update roofline (algorithmic flops / device time, FP64 peak 78.6
+Printed roofline: the dominant kernel of the configured step solver.  PCG (default): the product,
+HBM-bound — k_mf_product (matrix-free, the default where the plan fits: per local edge its
+linearized J, W, vertex dofs and record, the incidence slots, own (z, p_prev) and (p, q); csrc/pcg.hip
+PcgMfHost::product_bytes) or k_pcg_product (assembled H: repacked slot records, heavy slots;
+PcgHost::product_bytes) — bytes per launch x active launches / their summed device time, against
+8 TB/s; `traffic` from the committed rocprofv3 PMC pass when it matches the plan.  The factorization's k_update roofline (algorithmic flops / device time, FP64 peak 78.6
 TFLOP/s, AMD's MI355X specification) is reported beside it as roofline_factorization.  Both from
 profiled trials right after the timed region, HIP events on the solver's own stream.
 
@@ -342,17 +343,19 @@ def main():
         pp = stats["pcg_product"]
         its = max(pp["launches"] - 1, 1)           # the last launch only runs the convergence test
         gbs = pp["bytes"] / max(pp["ms"] * 1e-3, 1e-12) / 1e9
-        pcg_prof = {"bound": "hbm", "kernel": "k_pcg_product", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+        mf = "mf_lin" in stats                     # matrix-free product (b + diagonal blocks only)
+        pcg_prof = {"bound": "hbm", "kernel": "k_mf_product" if mf else "k_pcg_product", "achieved": round(gbs, 1),
+                    "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                     "traffic_unit": "bytes per launch", "bytes_per_launch": pp["bytes"] / its,
                     "launches": pp["launches"], "avg_launch_us": round(1e3 * pp["ms"] / max(pp["launches"], 1), 3),
                     "avg_active_launch_us": round(1e3 * pp["ms"] / its, 3),
                     "cg_iterations": its, "lambda": rep["lambda_final"], "rank": rank}
-        pmcp = sorted(ROOT.glob("profiles/*_pmc_pcg_product.json"))
-        if pmcp and not sharded:
-            pj = json.loads(pmcp[-1].read_text())
+        for pm in sorted(ROOT.glob("profiles/*_pmc_*product.json")) if not sharded else []:
+            pj = json.loads(pm.read_text())
             if abs(pj.get("bytes_per_launch_algorithmic", -1) - pcg_prof["bytes_per_launch"]) < 1e-6 * pcg_prof["bytes_per_launch"]:
                 pcg_prof["traffic"] = pj["traffic_bytes_per_launch"]
+                pcg_prof["traffic_source"] = pm.name
         ctx.set_linear_solver("direct")
         stats_f = ctx.profile_trial(rep["lambda_final"])
         ctx.set_linear_solver(args.solver)
@@ -410,6 +413,7 @@ def main():
                        "ms_per_trial": round(ms_per_step / max(trials_per_it, 1e-9), 3),
                        "lm_lanes": rep["lanes"],
                        "step_solver": args.solver if not sharded else "direct (point-sharded LDL^T)",
+                       "pcg_product": ("matrix-free" if "mf_lin" in stats else "assembled") if pcg_prof else None,
                        "pcg_trials": rep["pcg_trials"], "pcg_fallbacks": rep["pcg_fallbacks"],
                        "cg_iterations_per_pcg_trial": round(rep["pcg_iterations"] / max(rep["pcg_trials"], 1), 2),
                        "trials_executed_per_iteration": round(rep["trials_executed"] / max(iters, 1), 3),

@@ -7,7 +7,8 @@ than 10 % of the largest are counted as active.  On gfx950 FETCH_SIZE reports 1/
 16-byte-per-lane coalesced reads (MI355X_MICROARCH.md, HBM section); the product's slot records and
 gathers are 16-byte loads, so the corrected fetch doubles the counter.
 
-usage: python tools/pmc_pcg_summary.py gpurun_out/pmcpcg2 profiles/r02_pmc_pcg_product.json
+usage: python tools/pmc_pcg_summary.py gpurun_out/pmcpcg2 profiles/r02_pmc_pcg_product.json [kernel]
+       (kernel: k_pcg_product, the default, or k_mf_product)
 """
 import collections
 import csv
@@ -27,7 +28,7 @@ def per_dispatch(path, ctr, kernel):
 
 def main():
     src, dst = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2])
-    k = "k_pcg_product"
+    k = sys.argv[3] if len(sys.argv) > 3 else "k_pcg_product"
     f = per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)
     w = per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE", k)
     fmax = max(f.values())
