@@ -13,7 +13,7 @@ reference's simulation recipe scaled to n points); the graph is built on the hos
 resident in HBM before the timed region starts.
 
 Multi-GPU (N > 1): N independent C2 problems, one per GPU (weak scaling, no data-path collective):
-with PCG steps a C2 LM iteration is ~5 ms and a CG iteration ~0.1 ms of HBM-bound work, less than
+with PCG steps a C2 LM iteration is ~3 ms and a CG iteration ~0.13 ms of latency-bound work, less than
 the latency of the halo exchange and two all-reduces a point-sharded CG iteration would need
 (DESIGN.md §7).  --sharded runs ONE C2 problem point-sharded over the N ranks with the multifrontal
 LDL^T (DistPlan, csrc/symbolic.cpp: a subtree of the nested-dissection tree per rank, separator
