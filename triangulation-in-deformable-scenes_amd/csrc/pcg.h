@@ -86,14 +86,16 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
 
 // Matrix-free product (round 2, default where the plan fits): H is never assembled for a PCG step.
 // Every 3-dof point is a sliced row (64 per slice, nested-dissection order dealt to XCDs); a slice's
-// workgroup loads the linearized edges touching its points ("local edges": ARAP first, then
-// reprojection, then depth; an edge touching several slices is loaded by each), forms
+// workgroup loads the linearized ARAP edges touching its points ("local edges"; an edge touching
+// several slices is loaded by each), forms
 // s_e = W_e (J_e p) once per edge and stores J_{e,v}^T s_e per point role in LDS; each lane then
-// sums its row's incidences.  The global rows (T_g, depth scales) are summed from per-slice
+// sums its row's incidences and its own single-point edges (reprojection, depth).  The global rows
+// (T_g, depth scales) are summed from per-slice
 // partials of the edges a slice owns (an edge is owned by the first slice holding one of its
 // points).  The block-Jacobi preconditioner's diagonal blocks and b come from the same structure
 // once per LM iteration (k_mf_lin).  H + b are assembled only if a step falls back to the LDL^T.
-constexpr int kMfMaxH = 4;          // heavy vertices one slice's owned edges may touch (record field: < 8)
+constexpr int kMfMaxT = 2;          // T_g vertices one slice's owned ARAP edges may touch (record field: < 8)
+constexpr int kMfMaxS = 4;          // depth scales one slice's depth edges may touch
 constexpr int kMfMaxLds = 5120;     // doubles of per-slice contributions in LDS (40 KB)
 constexpr int kMfLin = 27;          // per heavy slot of k_mf_lin: 21 (lower 6x6) + 6 (b)
 enum { MF_ARAP = 0, MF_REP = 1, MF_DEP = 2 };
@@ -110,8 +112,14 @@ struct PcgMfHost {
     std::vector<int32_t> in_n;                     // per slice: incidence slots
     std::vector<int32_t> inc;                      // [slot][64]: LDS offset of the row's 3-vector (-1 padding)
     std::vector<int32_t> inc2;                     // [slot][64]: local edge << 2 | role (-1 padding)
-    std::vector<int32_t> sl_hn, hs_hk;
+    // per slice its heavy slots: the T_g vertices of its owned ARAP edges (sl_nt of them, first),
+    // then the scales of its points' depth edges
+    std::vector<int32_t> sl_hn, sl_nt, hs_hk;
     std::vector<int64_t> sl_hoff, hv_slot_begin, hs_pos;
+    // the rows' single-point edges (reprojection, depth), summed by their own lane:
+    // [slot][64] = depth << 30 | (scale slot + 1) << 27 | edge, -1 padding
+    std::vector<int64_t> own_off;
+    std::vector<int32_t> own_n, own;
     std::vector<int32_t> adof, atdof, rdof, ddof;  // dofs of the edges' vertices
     std::vector<int64_t> moff;
     int64_t msize = 0;
@@ -131,6 +139,8 @@ struct PcgDev {
     const int64_t *mf_le_off = nullptr, *mf_le = nullptr, *mf_in_off = nullptr;
     const int32_t *mf_le_n = nullptr, *mf_le_na = nullptr, *mf_in_n = nullptr, *mf_inc = nullptr, *mf_inc2 = nullptr;
     const int32_t *mf_adof = nullptr, *mf_atdof = nullptr, *mf_rdof = nullptr, *mf_ddof = nullptr;
+    const int32_t *mf_sl_nt = nullptr, *mf_own_n = nullptr, *mf_own = nullptr;
+    const int64_t *mf_own_off = nullptr;
     const double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr;
     const double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr;
     const double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr;

@@ -604,101 +604,78 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     const int sl = blockIdx.x;
     const bool live = sl < G.nsl;
     const int w = tid >> 6, lane = tid & 63;
-    // phase A: s_e = W_e (J_e p) per local edge, J_{e,v}^T s_e into LDS, owned edges' heavy parts
-    const int64_t l0 = live ? G.mf_le_off[sl] : 0;
-    const int ne = live ? G.mf_le_n[sl] : 0;
-    double hacc[kMfMaxH][6];
-#pragma unroll
-    for (int h = 0; h < kMfMaxH; h++)
-#pragma unroll
-        for (int i = 0; i < 6; i++) hacc[h][i] = 0.0;
-    for (int k = tid; k < ne; k += 256) {
-        int kind, mask, hs, base;
-        int64_t e;
-        mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
-        double hv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        if (kind == MF_ARAP) {
-            const int4 d = reinterpret_cast<const int4 *>(G.mf_adof)[e];
-            const int td = G.mf_atdof[e];
-            const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e;
-            double J[18];
-#pragma unroll
-            for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J[2 * q] = t.x; J[2 * q + 1] = t.y; }
-            const int dd[4] = {d.x, d.y, d.z, d.w};
-            double dot = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int i = 0; i < 3; i++) dot += J[3 * r + i] * pval(zp, beta, dd[r] + i);
-#pragma unroll
-            for (int i = 0; i < 6; i++) dot += J[12 + i] * pval(zp, beta, td + i);
-            const double sv = G.Warap[e] * dot;
-            int pos = base;                           // the roles whose point is in this slice
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-                if ((mask >> r) & 1) {
-#pragma unroll
-                    for (int i = 0; i < 3; i++) C[pos + i] = J[3 * r + i] * sv;
-                    pos += 3;
-                }
-#pragma unroll
-            for (int i = 0; i < 6; i++) hv[i] = J[12 + i] * sv;
-        } else if (kind == MF_REP) {
-            const int pd = G.mf_rdof[e];
-            const double *J = G.Jrep + 6 * e;
-            double p3[3];
-#pragma unroll
-            for (int i = 0; i < 3; i++) p3[i] = pval(zp, beta, pd + i);
-            const double wv = G.Wrep[e];
-            const double s0 = wv * ((J[0] * p3[0] + J[1] * p3[1]) + J[2] * p3[2]);
-            const double s1 = wv * ((J[3] * p3[0] + J[4] * p3[1]) + J[5] * p3[2]);
-#pragma unroll
-            for (int i = 0; i < 3; i++) C[base + i] = J[i] * s0 + J[3 + i] * s1;
-        } else {
-            const int pd = G.mf_ddof[2 * e], sd = G.mf_ddof[2 * e + 1];
-            const double *J = G.Jdep + 4 * e;
-            const double sv = G.Wdep[e] * (((J[0] * pval(zp, beta, pd) + J[1] * pval(zp, beta, pd + 1)) +
-                                            J[2] * pval(zp, beta, pd + 2)) + J[3] * pval(zp, beta, sd));
-#pragma unroll
-            for (int i = 0; i < 3; i++) C[base + i] = J[i] * sv;
-            hv[0] = J[3] * sv;
-        }
-        if (hs > 0)
-#pragma unroll
-            for (int h = 0; h < kMfMaxH; h++)
-                if (h == hs - 1)
-#pragma unroll
-                    for (int i = 0; i < 6; i++) hacc[h][i] += hv[i];
-    }
-    // the owned edges' heavy-row partials: per heavy slot, butterfly per wave, waves in order
-    const int nh = live ? G.sl_hn[sl] : 0;
-    for (int h = 0; h < nh; h++) {
-        double hh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int q = 0; q < kMfMaxH; q++)
-            if (q == h)
-#pragma unroll
-                for (int i = 0; i < 6; i++) hh[i] = hacc[q][i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const double v = wave_sum(hh[i]);
-            if (lane == 0) red[0][4 * i + w] = v;     // 6 values x 4 waves
-        }
-        __syncthreads();
-        if (tid < 6) {
-            const double *r4 = &red[0][4 * tid];
-            const double v = (r4[0] + r4[1]) + (r4[2] + r4[3]);
-            G.hs_part[G.hs_pos[G.sl_hoff[sl] + h] * 6 + tid] = v;
-        }
-        __syncthreads();
-    }
-    __syncthreads();
-    // phase B: lane = row; the four waves take every fourth incidence slot, partial rows meet in LDS
     const int v = live ? G.sl_v[sl * 64 + lane] : -1;
     const int64_t o = v >= 0 ? G.voff[v] : 0;
     double pv[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) pv[i] = v >= 0 ? pval(zp, beta, o + i) : 0.0;
+    // phase A: s_e = W_e (J_e p) per local (ARAP) edge, J_{e,v}^T s_e into LDS for the in-slice
+    // roles, the owned edges' T_g parts
+    const int64_t l0 = live ? G.mf_le_off[sl] : 0;
+    const int ne = live ? G.mf_le_n[sl] : 0;
+    double hT[kMfMaxT][6];
+#pragma unroll
+    for (int h = 0; h < kMfMaxT; h++)
+#pragma unroll
+        for (int i = 0; i < 6; i++) hT[h][i] = 0.0;
+    for (int k = tid; k < ne; k += 256) {
+        int kind, mask, hs, base;
+        int64_t e;
+        mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
+        const int4 d = reinterpret_cast<const int4 *>(G.mf_adof)[e];
+        const int td = G.mf_atdof[e];
+        const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e;
+        double J[18];
+#pragma unroll
+        for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J[2 * q] = t.x; J[2 * q + 1] = t.y; }
+        const int dd[4] = {d.x, d.y, d.z, d.w};
+        double dot = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) dot += J[3 * r + i] * pval(zp, beta, dd[r] + i);
+#pragma unroll
+        for (int i = 0; i < 6; i++) dot += J[12 + i] * pval(zp, beta, td + i);
+        const double sv = G.Warap[e] * dot;
+        int pos = base;                               // the roles whose point is in this slice
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+            if ((mask >> r) & 1) {
+#pragma unroll
+                for (int i = 0; i < 3; i++) C[pos + i] = J[3 * r + i] * sv;
+                pos += 3;
+            }
+        if (hs > 0)
+#pragma unroll
+            for (int h = 0; h < kMfMaxT; h++)
+                if (h == hs - 1)
+#pragma unroll
+                    for (int i = 0; i < 6; i++) hT[h][i] += J[12 + i] * sv;
+    }
+    // the owned edges' T_g partials: per slot, butterfly per wave, waves in order
+    const int nh = live ? G.sl_hn[sl] : 0, nt = live ? G.mf_sl_nt[sl] : 0;
+    for (int h = 0; h < nt; h++) {
+        double hh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < kMfMaxT; q++)
+            if (q == h)
+#pragma unroll
+                for (int i = 0; i < 6; i++) hh[i] = hT[q][i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const double x = wave_sum(hh[i]);
+            if (lane == 0) red[0][4 * i + w] = x;     // 6 values x 4 waves
+        }
+        __syncthreads();
+        if (tid < 6) {
+            const double *r4 = &red[0][4 * tid];
+            G.hs_part[G.hs_pos[G.sl_hoff[sl] + h] * 6 + tid] = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    // phase B: lane = row; the four waves take every fourth incidence slot and every fourth own
+    // (single-point) edge slot; partial rows meet in LDS in a fixed order
     double acc[3] = {0.0, 0.0, 0.0};
     const int64_t i0 = live ? G.mf_in_off[sl] : 0;
     const int ni = live ? G.mf_in_n[sl] : 0;
@@ -707,6 +684,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         if (off >= 0)
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[i] += C[off + i];
+    }
+    double hS[kMfMaxS] = {0.0, 0.0, 0.0, 0.0};
+    const int64_t o0 = live ? G.mf_own_off[sl] : 0;
+    const int no = live ? G.mf_own_n[sl] : 0;
+    for (int k = w; k < no; k += 4) {
+        const int x = G.mf_own[(o0 + k) * 64 + lane];
+        if (x < 0) continue;
+        const int e = x & ((1 << 27) - 1), ss = (x >> 27) & 7;
+        if (!(x >> 30)) {                              // reprojection (2 rows)
+            const double *J = G.Jrep + 6 * (int64_t)e;
+            const double wv = G.Wrep[e];
+            const double s0 = wv * ((J[0] * pv[0] + J[1] * pv[1]) + J[2] * pv[2]);
+            const double s1 = wv * ((J[3] * pv[0] + J[4] * pv[1]) + J[5] * pv[2]);
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[i] += J[i] * s0 + J[3 + i] * s1;
+        } else {                                       // depth (point, scale)
+            const double *J = G.Jdep + 4 * (int64_t)e;
+            const int sd = G.mf_ddof[2 * e + 1];
+            const double sv = G.Wdep[e] * (((J[0] * pv[0] + J[1] * pv[1]) + J[2] * pv[2]) + J[3] * pval(zp, beta, sd));
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[i] += J[i] * sv;
+#pragma unroll
+            for (int q = 0; q < kMfMaxS; q++)
+                if (q == ss - 1) hS[q] += J[3] * sv;
+        }
+    }
+    // the scale partials: per slot, butterfly per wave, waves in order
+    for (int j = 0; j < nh - nt; j++) {
+        double hh = 0.0;
+#pragma unroll
+        for (int q = 0; q < kMfMaxS; q++)
+            if (q == j) hh = hS[q];
+        const double x = wave_sum(hh);
+        if (lane == 0) red[3][w] = x;
+        __syncthreads();
+        if (tid == 0)
+            G.hs_part[G.hs_pos[G.sl_hoff[sl] + nt + j] * 6] = (red[3][0] + red[3][1]) + (red[3][2] + red[3][3]);
+        __syncthreads();
     }
 #pragma unroll
     for (int i = 0; i < 3; i++) red[i][tid] = acc[i];
@@ -738,8 +753,9 @@ __global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
     const int sl = blockIdx.x;
     const int64_t l0 = G.mf_le_off[sl];
     const int ne = G.mf_le_n[sl];
-    const int nh = G.sl_hn[sl];
-    for (int h = 0; h < nh; h++) {
+    const int nh = G.sl_hn[sl], nt = G.mf_sl_nt[sl];
+    // T_g slots: the owned ARAP edges' 6 x 6 blocks (lower triangle) and b parts
+    for (int h = 0; h < nt; h++) {
         double a[kMfLin];
 #pragma unroll
         for (int q = 0; q < kMfLin; q++) a[q] = 0.0;
@@ -748,20 +764,14 @@ __global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
             int64_t e;
             mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
             if (hs != h + 1) continue;
-            if (kind == MF_ARAP) {
-                const double *J = G.Jarap + 18 * e + 12;
-                const double wv = G.Warap[e], er = G.Earap[e];
+            const double *J = G.Jarap + 18 * e + 12;
+            const double wv = G.Warap[e], er = G.Earap[e];
 #pragma unroll
-                for (int i = 0; i < 6; i++) {
-                    const double ai = J[i] * wv;
+            for (int i = 0; i < 6; i++) {
+                const double ai = J[i] * wv;
 #pragma unroll
-                    for (int j = 0; j <= i; j++) a[tri6(i, j)] += ai * J[j];
-                    a[21 + i] -= J[i] * (wv * er);
-                }
-            } else if (kind == MF_DEP) {
-                const double Js = G.Jdep[4 * e + 3], wv = G.Wdep[e], er = G.Edep[e];
-                a[0] += (Js * wv) * Js;
-                a[21] -= Js * (wv * er);
+                for (int j = 0; j <= i; j++) a[tri6(i, j)] += ai * J[j];
+                a[21 + i] -= J[i] * (wv * er);
             }
         }
         double *out = G.mf_hlin + G.hs_pos[G.sl_hoff[sl] + h] * kMfLin;
@@ -781,26 +791,12 @@ __global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
             __syncthreads();
         }
     }
-    // point rows
+    // point rows: their ARAP incidences, then their own reprojection / depth edges
     const int v = G.sl_v[sl * 64 + lane];
     double acc[12];
 #pragma unroll
     for (int q = 0; q < 12; q++) acc[q] = 0.0;
-    const int64_t i0 = G.mf_in_off[sl];
-    const int ni = G.mf_in_n[sl];
-    for (int k = w; k < ni; k += 4) {
-        const int ir = G.mf_inc2[(i0 + k) * 64 + lane];
-        if (ir < 0) continue;
-        const int kl = ir >> 2, role = ir & 3;
-        int kind, mask, hs, base;
-        int64_t e;
-        mf_rec(G.mf_le[l0 + kl], kind, mask, hs, base, e);
-        const double *J;
-        double wv, er0, er1 = 0.0;
-        int m = 1;
-        if (kind == MF_ARAP) { J = G.Jarap + 18 * e + 3 * role; wv = G.Warap[e]; er0 = G.Earap[e]; }
-        else if (kind == MF_REP) { J = G.Jrep + 6 * e; wv = G.Wrep[e]; er0 = G.Erep[2 * e]; er1 = G.Erep[2 * e + 1]; m = 2; }
-        else { J = G.Jdep + 4 * e; wv = G.Wdep[e]; er0 = G.Edep[e]; }
+    auto add_rows = [&](const double *J, int m, double wv, double er0, double er1) {
         for (int r = 0; r < m; r++) {
             const double er = r == 0 ? er0 : er1;
 #pragma unroll
@@ -810,6 +806,36 @@ __global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
                 for (int j = 0; j < 3; j++) acc[3 * i + j] += ai * J[3 * r + j];
                 acc[9 + i] -= J[3 * r + i] * (wv * er);
             }
+        }
+    };
+    const int64_t i0 = G.mf_in_off[sl];
+    const int ni = G.mf_in_n[sl];
+    for (int k = w; k < ni; k += 4) {
+        const int ir = G.mf_inc2[(i0 + k) * 64 + lane];
+        if (ir < 0) continue;
+        const int kl = ir >> 2, role = ir & 3;
+        int kind, mask, hs, base;
+        int64_t e;
+        mf_rec(G.mf_le[l0 + kl], kind, mask, hs, base, e);
+        add_rows(G.Jarap + 18 * e + 3 * role, 1, G.Warap[e], G.Earap[e], 0.0);
+    }
+    double hS[kMfMaxS][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+    const int64_t o0 = G.mf_own_off[sl];
+    const int no = G.mf_own_n[sl];
+    for (int k = w; k < no; k += 4) {
+        const int x = G.mf_own[(o0 + k) * 64 + lane];
+        if (x < 0) continue;
+        const int64_t e = x & ((1 << 27) - 1);
+        const int ss = (x >> 27) & 7;
+        if (!(x >> 30)) {
+            add_rows(G.Jrep + 6 * e, 2, G.Wrep[e], G.Erep[2 * e], G.Erep[2 * e + 1]);
+        } else {
+            const double *J = G.Jdep + 4 * e;
+            const double wv = G.Wdep[e], er = G.Edep[e];
+            add_rows(J, 1, wv, er, 0.0);
+#pragma unroll
+            for (int q = 0; q < kMfMaxS; q++)
+                if (q == ss - 1) { hS[q][0] += (J[3] * wv) * J[3]; hS[q][1] -= J[3] * (wv * er); }
         }
     }
 #pragma unroll
@@ -824,6 +850,23 @@ __global__ void __launch_bounds__(256) k_mf_lin(const PcgDev G) {
             if (q < 9) D[q] = t;
             else G.b[o + q - 9] = t;
         }
+    }
+    __syncthreads();
+    // scale slots: diagonal entry and b part of the depth edges
+    for (int j = 0; j < nh - nt; j++) {
+        double h0 = 0.0, h1 = 0.0;
+#pragma unroll
+        for (int q = 0; q < kMfMaxS; q++)
+            if (q == j) { h0 = hS[q][0]; h1 = hS[q][1]; }
+        h0 = wave_sum(h0);
+        h1 = wave_sum(h1);
+        if (lane == 0) { red[0][w] = h0; red[1][w] = h1; }
+        __syncthreads();
+        if (tid < 2) {
+            double *out = G.mf_hlin + G.hs_pos[G.sl_hoff[sl] + nt + j] * kMfLin;
+            out[tid == 0 ? 0 : 21] = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+        }
+        __syncthreads();
     }
 }
 
@@ -1217,54 +1260,78 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
             if (!dup) { seen[ns++] = s0; sl_edges[s0].push_back(((int64_t)kind << 40) | e); }
         }
     };
-    if ((int64_t)E >= (1LL << 40) || kMfMaxLds > 0x7fff || kMfMaxH > 7) { err = "record fields overflow"; return false; }
+    if ((int64_t)E >= (1LL << 40) || kMfMaxLds > 0x7fff || kMfMaxT > 7 || kMfMaxS > 7 || R >= (1 << 27) ||
+        D >= (1 << 27)) {
+        err = "record fields overflow";
+        return false;
+    }
     for (int64_t e = 0; e < E; e++) add_local(MF_ARAP, e, arap_pts + 4 * e, 4);
-    for (int e = 0; e < R; e++) add_local(MF_REP, e, rep_point + e, 1);
-    for (int e = 0; e < D; e++) add_local(MF_DEP, e, dep_point + e, 1);
+    // the points' single-point edges (their own lane sums them): CSR by point, edges ascending
+    std::vector<int64_t> own_beg(P + 1, 0);
+    for (int e = 0; e < R; e++) own_beg[rep_point[e] + 1]++;
+    for (int e = 0; e < D; e++) own_beg[dep_point[e] + 1]++;
+    for (int64_t i = 0; i < P; i++) own_beg[i + 1] += own_beg[i];
+    std::vector<int32_t> own_e(own_beg[P]);      // MF_REP / MF_DEP << 30 | edge
+    {
+        std::vector<int64_t> f(own_beg.begin(), own_beg.end() - 1);
+        for (int e = 0; e < R; e++) own_e[f[rep_point[e]]++] = e;
+        for (int e = 0; e < D; e++) own_e[f[dep_point[e]]++] = (1 << 30) | e;
+    }
     H.le_off.resize(nsl); H.le_n.resize(nsl); H.le_na.resize(nsl);
-    H.in_off.resize(nsl); H.in_n.resize(nsl); H.sl_hn.resize(nsl); H.sl_hoff.resize(nsl);
+    H.in_off.resize(nsl); H.in_n.resize(nsl); H.sl_hn.resize(nsl); H.sl_nt.resize(nsl); H.sl_hoff.resize(nsl);
+    H.own_off.resize(nsl); H.own_n.resize(nsl);
     int64_t nle = 0, nin = 0, hslots = 0;
     std::vector<std::vector<int32_t>> sl_heavy(nsl);
-    auto owner = [&](int kind, int64_t e) -> int32_t {
-        if (kind == MF_REP) return pslice[rep_point[e]];
-        if (kind == MF_DEP) return pslice[dep_point[e]];
+    auto owner = [&](int64_t e) -> int32_t {     // of an ARAP edge: the first slice holding one of its points
         int32_t o = INT32_MAX;
         for (int r = 0; r < 4; r++) o = std::min(o, pslice[arap_pts[4 * e + r]]);
         return o;
     };
-    auto heavy_of = [&](int kind, int64_t e) -> int32_t {   // heavy index of the edge's global vertex, -1 none
-        if (kind == MF_ARAP) return H.v_heavy[arap_pair[e]];
-        if (kind == MF_DEP) return H.v_heavy[(int64_t)Q + dep_scale[e]];
-        return -1;
-    };
+    // per slice: heavy slots = the T_g of its owned ARAP edges (first: T_g vertices precede the
+    // scales in vertex order), then the scales of its points' depth edges
+    std::vector<std::vector<int32_t>> sl_scales(nsl);
+    int64_t nown = 0;
     for (int64_t sl = 0; sl < nsl; sl++) {
         auto &L = sl_edges[sl];
-        std::sort(L.begin(), L.end());        // ARAP, then reprojection, then depth, edges ascending
-        int32_t na = 0;
-        for (int64_t x : L) na += (x >> 40) == MF_ARAP;
+        std::sort(L.begin(), L.end());
         for (int64_t x : L) {
-            const int kind = (int)(x >> 40);
             const int64_t e = x & 0xffffffffffLL;
-            const int32_t hk = heavy_of(kind, e);
-            if (hk >= 0 && owner(kind, e) == sl) sl_heavy[sl].push_back(hk);
+            if (owner(e) == sl) sl_heavy[sl].push_back(H.v_heavy[arap_pair[e]]);
         }
         std::sort(sl_heavy[sl].begin(), sl_heavy[sl].end());
         sl_heavy[sl].erase(std::unique(sl_heavy[sl].begin(), sl_heavy[sl].end()), sl_heavy[sl].end());
-        if ((int)sl_heavy[sl].size() > kMfMaxH) { err = "a slice owns edges of more than kMfMaxH global vertices"; return false; }
+        const int nt = (int)sl_heavy[sl].size();
+        int64_t mo = 0;
+        for (int l = 0; l < 64; l++) {
+            const int32_t v = H.sl_v[sl * 64 + l];
+            if (v < 0) continue;
+            const int64_t p = pidx(v);
+            mo = std::max(mo, own_beg[p + 1] - own_beg[p]);
+            for (int64_t k = own_beg[p]; k < own_beg[p + 1]; k++)
+                if (own_e[k] >> 30) sl_scales[sl].push_back(H.v_heavy[(int64_t)Q + dep_scale[own_e[k] & ((1 << 30) - 1)]]);
+        }
+        std::sort(sl_scales[sl].begin(), sl_scales[sl].end());
+        sl_scales[sl].erase(std::unique(sl_scales[sl].begin(), sl_scales[sl].end()), sl_scales[sl].end());
+        if (nt > kMfMaxT || (int)sl_scales[sl].size() > kMfMaxS) {
+            err = "a slice couples to more global vertices than the kernels' accumulators";
+            return false;
+        }
+        sl_heavy[sl].insert(sl_heavy[sl].end(), sl_scales[sl].begin(), sl_scales[sl].end());
         int64_t lds = 0;                      // one 3-vector per (local edge, role in this slice)
         for (int64_t x : L) {
-            const int kind = (int)(x >> 40);
             const int64_t e = x & 0xffffffffffLL;
-            if (kind != MF_ARAP) { lds += 3; continue; }
             for (int r = 0; r < 4; r++) lds += 3 * (pslice[arap_pts[4 * e + r]] == sl);
         }
         if (lds > kMfMaxLds) { err = "a slice's local edges exceed the LDS budget"; return false; }
         H.max_lds = std::max<int32_t>(H.max_lds, (int32_t)lds);
-        H.le_off[sl] = nle; H.le_n[sl] = (int32_t)L.size(); H.le_na[sl] = na;
-        H.sl_hn[sl] = (int32_t)sl_heavy[sl].size(); H.sl_hoff[sl] = hslots;
+        H.le_off[sl] = nle; H.le_n[sl] = (int32_t)L.size(); H.le_na[sl] = (int32_t)L.size();
+        H.sl_hn[sl] = (int32_t)sl_heavy[sl].size(); H.sl_nt[sl] = nt; H.sl_hoff[sl] = hslots;
+        H.own_off[sl] = nown; H.own_n[sl] = (int32_t)mo;
         nle += (int64_t)L.size();
+        nown += mo;
         hslots += (int64_t)sl_heavy[sl].size();
     }
+    H.own.assign((size_t)nown * 64, -1);
     H.le.resize(nle);
     H.hs_hk.resize(hslots);
     // incidences: per row, (local edge, role) in local-edge order
@@ -1278,26 +1345,18 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
         for (size_t k = 0; k < L.size(); k++) {
             const int kind = (int)(L[k] >> 40);
             const int64_t e = L[k] & 0xffffffffffLL;
-            int64_t hs = 0;
-            const int32_t hk = heavy_of(kind, e);
-            if (hk >= 0 && owner(kind, e) == sl)
-                hs = 1 + (std::lower_bound(sl_heavy[sl].begin(), sl_heavy[sl].end(), hk) - sl_heavy[sl].begin());
+            int64_t hs = 0;                   // T_g slot (+1) of an owned edge
+            if (owner(e) == sl)
+                hs = 1 + (std::find(sl_heavy[sl].begin(), sl_heavy[sl].begin() + H.sl_nt[sl], H.v_heavy[arap_pair[e]]) -
+                          sl_heavy[sl].begin());
             int64_t mask = 0;
             const int32_t b0 = base;
-            if (kind == MF_ARAP) {
-                for (int r = 0; r < 4; r++) {
-                    const int32_t p = arap_pts[4 * e + r];
-                    if (pslice[p] != sl) continue;
-                    mask |= 1LL << r;
-                    rowinc[plane[p]].push_back(base);
-                    rowinc2[plane[p]].push_back(((int32_t)k << 2) | r);
-                    base += 3;
-                }
-            } else {
-                const int32_t p = kind == MF_REP ? rep_point[e] : dep_point[e];
-                mask = 1;
+            for (int r = 0; r < 4; r++) {
+                const int32_t p = arap_pts[4 * e + r];
+                if (pslice[p] != sl) continue;
+                mask |= 1LL << r;
                 rowinc[plane[p]].push_back(base);
-                rowinc2[plane[p]].push_back((int32_t)k << 2);
+                rowinc2[plane[p]].push_back(((int32_t)k << 2) | r);
                 base += 3;
             }
             H.le[H.le_off[sl] + k] = ((int64_t)kind << 62) | (mask << 58) | (hs << 55) | ((int64_t)b0 << 40) | e;
@@ -1313,6 +1372,22 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
                 H.inc2[(nin + (int64_t)k) * 64 + l] = rowinc2[l][k];
             }
         nin += (int64_t)mx;
+        // own edges: per lane in point-edge order; depth edges carry their scale slot (+1)
+        for (int l = 0; l < 64; l++) {
+            const int32_t v = H.sl_v[sl * 64 + l];
+            if (v < 0) continue;
+            const int64_t p = pidx(v);
+            for (int64_t k = own_beg[p]; k < own_beg[p + 1]; k++) {
+                int32_t x = own_e[k];
+                if (x >> 30) {
+                    const int32_t hk = H.v_heavy[(int64_t)Q + dep_scale[x & ((1 << 30) - 1)]];
+                    const int32_t j = (int32_t)(std::lower_bound(sl_scales[sl].begin(), sl_scales[sl].end(), hk) -
+                                                sl_scales[sl].begin());
+                    x |= (j + 1) << 27;
+                }
+                H.own[(H.own_off[sl] + (k - own_beg[p])) * 64 + l] = x;
+            }
+        }
     }
     H.hv_slot_begin.assign(H.heavy_v.size() + 1, 0);
     for (int64_t g = 0; g < hslots; g++) H.hv_slot_begin[H.hs_hk[g] + 1]++;
@@ -1340,14 +1415,11 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
     // the incidence slots, own (z, p_prev) read and (p, q) written, heavy partials; flops: 2 per
     // Jacobian entry for J p and J^T s
     {
-        double by = 32.0 * (double)ndof + 4.0 * 64.0 * (double)nin + 48.0 * (double)hslots, fl = 0;
-        for (int64_t sl = 0; sl < nsl; sl++)
-            for (int k = 0; k < H.le_n[sl]; k++) {
-                const int kind = (int)((uint64_t)H.le[H.le_off[sl] + k] >> 62);
-                if (kind == MF_ARAP) { by += 8 + 144 + 8 + 16 + 4; fl += 4 * 18; }
-                else if (kind == MF_REP) { by += 8 + 48 + 8 + 4; fl += 4 * 6; }
-                else { by += 8 + 32 + 8 + 8; fl += 4 * 4; }
-            }
+        // per ARAP local edge: record 8 + J 144 + W 8 + dofs 20; per own edge: reprojection J 48 +
+        // W 8, depth J 32 + W 8 + scale dof 4; slot entries 4 B per lane
+        double by = 32.0 * (double)ndof + 4.0 * 64.0 * (double)(nin + nown) + 48.0 * (double)hslots, fl = 0;
+        by += (double)nle * (8 + 144 + 8 + 20) + (double)R * (48 + 8) + (double)D * (32 + 8 + 4);
+        fl += 4.0 * 18 * (double)nle + 4.0 * 6 * R + 4.0 * 4 * D;
         H.product_bytes = by;
         H.product_flops = fl;
     }

@@ -383,6 +383,10 @@ int upload_pcg_mf(deftri_ctx *ctx, const HostProblem &h) {
     PUT(ino, mh.in_off); PUT(inn, mh.in_n); PUT(inc, mh.inc); PUT(inc2, mh.inc2);
     PUT(shn, mh.sl_hn); PUT(hshk, mh.hs_hk); PUT(shoff, mh.sl_hoff); PUT(hvb, mh.hv_slot_begin); PUT(hvs, mh.hs_pos);
     PUT(ad, mh.adof); PUT(atd, mh.atdof); PUT(rd, mh.rdof); PUT(dd, mh.ddof);
+    int32_t *snt, *own_n, *own;
+    int64_t *own_off;
+    PUT(snt, mh.sl_nt); PUT(own_n, mh.own_n); PUT(own, mh.own); PUT(own_off, mh.own_off);
+    G.mf_sl_nt = snt; G.mf_own_n = own_n; G.mf_own = own; G.mf_own_off = own_off;
 #undef PUT
     G.heavy_v = hv; G.h_dofbase = hdb; G.v_heavy = vh; G.h_first = hf; G.moff = mo;
     G.sl_v = sv; G.mf_le_off = leo; G.mf_le_n = len; G.mf_le_na = lena; G.mf_le = le;
