@@ -96,6 +96,7 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
 // once per LM iteration (k_mf_lin).  H + b are assembled only if a step falls back to the LDL^T.
 constexpr int kMfMaxT = 2;          // T_g vertices one slice's owned ARAP edges may touch (record field: < 8)
 constexpr int kMfMaxS = 4;          // depth scales one slice's depth edges may touch
+constexpr int kMfMaxH = kMfMaxT + kMfMaxS;
 constexpr int kMfMaxLds = 5120;     // doubles of per-slice contributions in LDS (40 KB)
 constexpr int kMfLin = 27;          // per heavy slot of k_mf_lin: 21 (lower 6x6) + 6 (b)
 enum { MF_ARAP = 0, MF_REP = 1, MF_DEP = 2 };
@@ -118,6 +119,8 @@ struct PcgMfHost {
     std::vector<int64_t> sl_hoff, hv_slot_begin, hs_pos;
     // the rows' single-point edges (reprojection, depth), summed by their own lane:
     // [slot][64] = depth << 30 | (scale slot + 1) << 27 | edge, -1 padding
+    std::vector<int64_t> sl_meta;                  // per slice: le_off, in_off, own_off, counts (ne | ni << 16 | no << 24 | nt << 32 | nh << 36)
+    std::vector<int32_t> sl_hpos;                  // per slice, kMfMaxH: its heavy slots' partial positions
     std::vector<int64_t> own_off;
     std::vector<int32_t> own_n, own;
     std::vector<int32_t> adof, atdof, rdof, ddof;  // dofs of the edges' vertices
@@ -140,7 +143,8 @@ struct PcgDev {
     const int32_t *mf_le_n = nullptr, *mf_le_na = nullptr, *mf_in_n = nullptr, *mf_inc = nullptr, *mf_inc2 = nullptr;
     const int32_t *mf_adof = nullptr, *mf_atdof = nullptr, *mf_rdof = nullptr, *mf_ddof = nullptr;
     const int32_t *mf_sl_nt = nullptr, *mf_own_n = nullptr, *mf_own = nullptr;
-    const int64_t *mf_own_off = nullptr;
+    const int64_t *mf_own_off = nullptr, *mf_sl_meta = nullptr;
+    const int32_t *mf_sl_hpos = nullptr;
     const double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr;
     const double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr;
     const double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr;

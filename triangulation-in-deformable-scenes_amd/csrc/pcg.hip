@@ -578,12 +578,77 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_PCG_WPE))) k_mf_product(int it, const PcgDev G, double lam) {
-    extern __shared__ double C[];                     // per local edge and point role: J^T s
+#ifndef DEFTRI_MF_WPE
+#define DEFTRI_MF_WPE 4
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_MF_WPE))) k_mf_product(int it, const PcgDev G, double lam) {
+    extern __shared__ double C[];                     // per local edge and in-slice role: J^T s
     __shared__ double red[4][256];
     double *rec = G.rec + kPcgRec * (it + 1);
     const double *prv = G.rec + kPcgRec * it;
     const int tid = threadIdx.x;
+    const int sl = blockIdx.x;
+    const bool live = sl < G.nsl;
+    const int w = tid >> 6, lane = tid & 63;
+    // The workgroup's chain of dependent loads bounds this kernel (SQ: ~70 % of wave cycles
+    // waiting), so every load that does not need this iteration's scalars is issued first and stays
+    // in flight while the status and the (r.z, r.r) partials arrive: the slice's metadata (one
+    // 32-byte record), then the row, its first local edge, its first incidence slots, its first own
+    // edge, then their dofs / Jacobians / weights.
+    int64_t l0 = 0, i0 = 0, o0 = 0;
+    int ne = 0, ni = 0, no = 0, nt = 0, nh = 0;
+    if (live) {
+        const longlong2 m0 = reinterpret_cast<const longlong2 *>(G.mf_sl_meta)[2 * sl];
+        const longlong2 m1 = reinterpret_cast<const longlong2 *>(G.mf_sl_meta)[2 * sl + 1];
+        l0 = m0.x; i0 = m0.y; o0 = m1.x;
+        const int64_t c = m1.y;
+        ne = (int)(c & 0xffff); ni = (int)((c >> 16) & 0xff); no = (int)((c >> 24) & 0xff);
+        nt = (int)((c >> 32) & 0xf); nh = (int)((c >> 36) & 0xf);
+    }
+    const int v = live ? G.sl_v[sl * 64 + lane] : -1;
+    // first local edge of this thread
+    const bool has1 = tid < ne;
+    int kind1 = 0, mask1 = 0, hs1 = 0, base1 = 0;
+    int64_t e1 = 0;
+    if (has1) mf_rec(G.mf_le[l0 + tid], kind1, mask1, hs1, base1, e1);
+    // incidence slots (every fourth, the first kPre) and the first own edge of this wave
+    constexpr int kPre = 4;
+    int offs[kPre];
+#pragma unroll
+    for (int u = 0; u < kPre; u++) offs[u] = (w + 4 * u < ni) ? G.mf_inc[(i0 + w + 4 * u) * 64 + lane] : -1;
+    const int x1 = w < no ? G.mf_own[(o0 + w) * 64 + lane] : -1;
+    int4 d1 = make_int4(0, 0, 0, 0);
+    int td1 = 0;
+    double J1[18], W1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 18; q++) J1[q] = 0.0;
+    if (has1) {
+        d1 = reinterpret_cast<const int4 *>(G.mf_adof)[e1];
+        td1 = G.mf_atdof[e1];
+        const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e1;
+#pragma unroll
+        for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J1[2 * q] = t.x; J1[2 * q + 1] = t.y; }
+        W1 = G.Warap[e1];
+    }
+    // the own edge: reprojection J (2 x 3) + W, or depth J (4) + W + the scale's dof
+    double Jo[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, Wo = 0.0;
+    int so = 0;
+    if (x1 >= 0) {
+        const int64_t e = x1 & ((1 << 27) - 1);
+        if (!(x1 >> 30)) {
+            const double2 *J2 = reinterpret_cast<const double2 *>(G.Jrep) + 3 * e;
+#pragma unroll
+            for (int q = 0; q < 3; q++) { const double2 t = J2[q]; Jo[2 * q] = t.x; Jo[2 * q + 1] = t.y; }
+            Wo = G.Wrep[e];
+        } else {
+            const double2 *J2 = reinterpret_cast<const double2 *>(G.Jdep) + 2 * e;
+#pragma unroll
+            for (int q = 0; q < 2; q++) { const double2 t = J2[q]; Jo[2 * q] = t.x; Jo[2 * q + 1] = t.y; }
+            Wo = G.Wdep[e];
+            so = G.mf_ddof[2 * e + 1];
+        }
+    }
+    const int64_t o = v >= 0 ? G.voff[v] : 0;
     if (prv[PR_STATUS] != 0.0) {
         if (blockIdx.x == 0 && tid == 0) { rec[PR_STATUS] = prv[PR_STATUS]; rec[PR_ITS] = prv[PR_ITS]; }
         return;
@@ -601,59 +666,54 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     if (conv) return;
     const double beta = it == 0 ? 0.0 : rz / prv[PR_RZ];
     const double *zp = G.zp;
-    const int sl = blockIdx.x;
-    const bool live = sl < G.nsl;
-    const int w = tid >> 6, lane = tid & 63;
-    const int v = live ? G.sl_v[sl * 64 + lane] : -1;
-    const int64_t o = v >= 0 ? G.voff[v] : 0;
     double pv[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) pv[i] = v >= 0 ? pval(zp, beta, o + i) : 0.0;
     // phase A: s_e = W_e (J_e p) per local (ARAP) edge, J_{e,v}^T s_e into LDS for the in-slice
     // roles, the owned edges' T_g parts
-    const int64_t l0 = live ? G.mf_le_off[sl] : 0;
-    const int ne = live ? G.mf_le_n[sl] : 0;
     double hT[kMfMaxT][6];
 #pragma unroll
     for (int h = 0; h < kMfMaxT; h++)
 #pragma unroll
         for (int i = 0; i < 6; i++) hT[h][i] = 0.0;
     for (int k = tid; k < ne; k += 256) {
-        int kind, mask, hs, base;
-        int64_t e;
-        mf_rec(G.mf_le[l0 + k], kind, mask, hs, base, e);
-        const int4 d = reinterpret_cast<const int4 *>(G.mf_adof)[e];
-        const int td = G.mf_atdof[e];
-        const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e;
-        double J[18];
+        if (k != tid) {                               // later passes load here (the first is prefetched)
+            mf_rec(G.mf_le[l0 + k], kind1, mask1, hs1, base1, e1);
+            d1 = reinterpret_cast<const int4 *>(G.mf_adof)[e1];
+            td1 = G.mf_atdof[e1];
+            const double2 *J2 = reinterpret_cast<const double2 *>(G.Jarap) + 9 * e1;
 #pragma unroll
-        for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J[2 * q] = t.x; J[2 * q + 1] = t.y; }
-        const int dd[4] = {d.x, d.y, d.z, d.w};
+            for (int q = 0; q < 9; q++) { const double2 t = J2[q]; J1[2 * q] = t.x; J1[2 * q + 1] = t.y; }
+            W1 = G.Warap[e1];
+        }
         double dot = 0.0;
 #pragma unroll
+        for (int i = 0; i < 3; i++) dot += J1[i] * pval(zp, beta, d1.x + i);
+#pragma unroll
+        for (int i = 0; i < 3; i++) dot += J1[3 + i] * pval(zp, beta, d1.y + i);
+#pragma unroll
+        for (int i = 0; i < 3; i++) dot += J1[6 + i] * pval(zp, beta, d1.z + i);
+#pragma unroll
+        for (int i = 0; i < 3; i++) dot += J1[9 + i] * pval(zp, beta, d1.w + i);
+#pragma unroll
+        for (int i = 0; i < 6; i++) dot += J1[12 + i] * pval(zp, beta, td1 + i);
+        const double sv = W1 * dot;
+        int pos = base1;                              // the roles whose point is in this slice
+#pragma unroll
         for (int r = 0; r < 4; r++)
+            if ((mask1 >> r) & 1) {
 #pragma unroll
-            for (int i = 0; i < 3; i++) dot += J[3 * r + i] * pval(zp, beta, dd[r] + i);
-#pragma unroll
-        for (int i = 0; i < 6; i++) dot += J[12 + i] * pval(zp, beta, td + i);
-        const double sv = G.Warap[e] * dot;
-        int pos = base;                               // the roles whose point is in this slice
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-            if ((mask >> r) & 1) {
-#pragma unroll
-                for (int i = 0; i < 3; i++) C[pos + i] = J[3 * r + i] * sv;
+                for (int i = 0; i < 3; i++) C[pos + i] = J1[3 * r + i] * sv;
                 pos += 3;
             }
-        if (hs > 0)
+        if (hs1 > 0)
 #pragma unroll
             for (int h = 0; h < kMfMaxT; h++)
-                if (h == hs - 1)
+                if (h == hs1 - 1)
 #pragma unroll
-                    for (int i = 0; i < 6; i++) hT[h][i] += J[12 + i] * sv;
+                    for (int i = 0; i < 6; i++) hT[h][i] += J1[12 + i] * sv;
     }
     // the owned edges' T_g partials: per slot, butterfly per wave, waves in order
-    const int nh = live ? G.sl_hn[sl] : 0, nt = live ? G.mf_sl_nt[sl] : 0;
     for (int h = 0; h < nt; h++) {
         double hh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -669,7 +729,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         __syncthreads();
         if (tid < 6) {
             const double *r4 = &red[0][4 * tid];
-            G.hs_part[G.hs_pos[G.sl_hoff[sl] + h] * 6 + tid] = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+            G.hs_part[(int64_t)G.mf_sl_hpos[sl * kMfMaxH + h] * 6 + tid] = (r4[0] + r4[1]) + (r4[2] + r4[3]);
         }
         __syncthreads();
     }
@@ -677,38 +737,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
     // phase B: lane = row; the four waves take every fourth incidence slot and every fourth own
     // (single-point) edge slot; partial rows meet in LDS in a fixed order
     double acc[3] = {0.0, 0.0, 0.0};
-    const int64_t i0 = live ? G.mf_in_off[sl] : 0;
-    const int ni = live ? G.mf_in_n[sl] : 0;
-    for (int k = w; k < ni; k += 4) {
+#pragma unroll
+    for (int u = 0; u < kPre; u++)
+        if (offs[u] >= 0)
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[i] += C[offs[u] + i];
+    for (int k = w + 4 * kPre; k < ni; k += 4) {
         const int off = G.mf_inc[(i0 + k) * 64 + lane];
         if (off >= 0)
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[i] += C[off + i];
     }
     double hS[kMfMaxS] = {0.0, 0.0, 0.0, 0.0};
-    const int64_t o0 = live ? G.mf_own_off[sl] : 0;
-    const int no = live ? G.mf_own_n[sl] : 0;
-    for (int k = w; k < no; k += 4) {
-        const int x = G.mf_own[(o0 + k) * 64 + lane];
-        if (x < 0) continue;
-        const int e = x & ((1 << 27) - 1), ss = (x >> 27) & 7;
+    auto own_edge = [&](int x, const double (&J)[6], double wv, int sd) __attribute__((always_inline)) {
+        const int ss = (x >> 27) & 7;
         if (!(x >> 30)) {                              // reprojection (2 rows)
-            const double *J = G.Jrep + 6 * (int64_t)e;
-            const double wv = G.Wrep[e];
             const double s0 = wv * ((J[0] * pv[0] + J[1] * pv[1]) + J[2] * pv[2]);
             const double s1 = wv * ((J[3] * pv[0] + J[4] * pv[1]) + J[5] * pv[2]);
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[i] += J[i] * s0 + J[3 + i] * s1;
         } else {                                       // depth (point, scale)
-            const double *J = G.Jdep + 4 * (int64_t)e;
-            const int sd = G.mf_ddof[2 * e + 1];
-            const double sv = G.Wdep[e] * (((J[0] * pv[0] + J[1] * pv[1]) + J[2] * pv[2]) + J[3] * pval(zp, beta, sd));
+            const double sv = wv * (((J[0] * pv[0] + J[1] * pv[1]) + J[2] * pv[2]) + J[3] * pval(zp, beta, sd));
 #pragma unroll
             for (int i = 0; i < 3; i++) acc[i] += J[i] * sv;
 #pragma unroll
             for (int q = 0; q < kMfMaxS; q++)
                 if (q == ss - 1) hS[q] += J[3] * sv;
         }
+    };
+    if (x1 >= 0) own_edge(x1, Jo, Wo, so);
+    for (int k = w + 4; k < no; k += 4) {
+        const int x = G.mf_own[(o0 + k) * 64 + lane];
+        if (x < 0) continue;
+        const int64_t e = x & ((1 << 27) - 1);
+        double J[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        double wv;
+        int sd = 0;
+        if (!(x >> 30)) {
+#pragma unroll
+            for (int q = 0; q < 6; q++) J[q] = G.Jrep[6 * e + q];
+            wv = G.Wrep[e];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++) J[q] = G.Jdep[4 * e + q];
+            wv = G.Wdep[e];
+            sd = G.mf_ddof[2 * e + 1];
+        }
+        own_edge(x, J, wv, sd);
     }
     // the scale partials: per slot, butterfly per wave, waves in order
     for (int j = 0; j < nh - nt; j++) {
@@ -720,7 +795,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         if (lane == 0) red[3][w] = x;
         __syncthreads();
         if (tid == 0)
-            G.hs_part[G.hs_pos[G.sl_hoff[sl] + nt + j] * 6] = (red[3][0] + red[3][1]) + (red[3][2] + red[3][3]);
+            G.hs_part[(int64_t)G.mf_sl_hpos[sl * kMfMaxH + nt + j] * 6] = (red[3][0] + red[3][1]) + (red[3][2] + red[3][3]);
         __syncthreads();
     }
 #pragma unroll
@@ -1396,6 +1471,22 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
     {
         std::vector<int64_t> f(H.hv_slot_begin.begin(), H.hv_slot_begin.end() - 1);
         for (int64_t g = 0; g < hslots; g++) H.hs_pos[g] = f[H.hs_hk[g]]++;
+    }
+    // per slice: one 32-byte metadata record (the product reads it with two 16-byte loads) and the
+    // partial positions of its heavy slots
+    H.sl_meta.assign(4 * (size_t)nsl, 0);
+    H.sl_hpos.assign((size_t)nsl * kMfMaxH, 0);
+    for (int64_t sl = 0; sl < nsl; sl++) {
+        if (H.le_n[sl] > 0xffff || H.in_n[sl] > 0xff || H.own_n[sl] > 0xff || H.sl_hn[sl] > kMfMaxH) {
+            err = "slice metadata fields overflow";
+            return false;
+        }
+        H.sl_meta[4 * sl] = H.le_off[sl];
+        H.sl_meta[4 * sl + 1] = H.in_off[sl];
+        H.sl_meta[4 * sl + 2] = H.own_off[sl];
+        H.sl_meta[4 * sl + 3] = (int64_t)H.le_n[sl] | ((int64_t)H.in_n[sl] << 16) | ((int64_t)H.own_n[sl] << 24) |
+                                ((int64_t)H.sl_nt[sl] << 32) | ((int64_t)H.sl_hn[sl] << 36);
+        for (int h = 0; h < H.sl_hn[sl]; h++) H.sl_hpos[sl * kMfMaxH + h] = (int32_t)H.hs_pos[H.sl_hoff[sl] + h];
     }
     // the edges' vertex dofs
     H.adof.resize(4 * (size_t)E); H.atdof.resize(E); H.rdof.resize(R); H.ddof.resize(2 * (size_t)D);

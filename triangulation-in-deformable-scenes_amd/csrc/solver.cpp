@@ -387,6 +387,10 @@ int upload_pcg_mf(deftri_ctx *ctx, const HostProblem &h) {
     int64_t *own_off;
     PUT(snt, mh.sl_nt); PUT(own_n, mh.own_n); PUT(own, mh.own); PUT(own_off, mh.own_off);
     G.mf_sl_nt = snt; G.mf_own_n = own_n; G.mf_own = own; G.mf_own_off = own_off;
+    int64_t *smeta;
+    int32_t *shpos;
+    PUT(smeta, mh.sl_meta); PUT(shpos, mh.sl_hpos);
+    G.mf_sl_meta = smeta; G.mf_sl_hpos = shpos;
 #undef PUT
     G.heavy_v = hv; G.h_dofbase = hdb; G.v_heavy = vh; G.h_first = hf; G.moff = mo;
     G.sl_v = sv; G.mf_le_off = leo; G.mf_le_n = len; G.mf_le_na = lena; G.mf_le = le;
