@@ -31,7 +31,10 @@ constexpr int kPcgRec = 8;          // doubles per iteration record
 constexpr int kPcgMaxHeavyDofs = 2048;
 constexpr int kPcgSortWindow = 512;
 // iteration record fields (record 0: setup; record k + 1: iteration k)
-enum { PR_RZ = 0, PR_RR = 1, PR_PQ = 2, PR_ALPHA = 3, PR_STATUS = 4, PR_ITS = 5 };
+enum { PR_RZ = 0, PR_RR = 1, PR_PQ = 2, PR_ALPHA = 3, PR_STATUS = 4, PR_ITS = 5, PR_PQA = 6 };
+// PR_PQA (matrix-free plans): the sliced rows' p.q, summed once by k_pcg_heavy's last workgroup
+// instead of by every update workgroup; likewise k_pcg_dots sums the (r.z, r.r) partials once per
+// iteration for the product
 // PR_STATUS: 0 running, 1 converged, 2 breakdown (p.Ap <= 0 / non-finite), 3 preconditioner block
 // not positive definite
 enum { kPcgRunning = 0, kPcgConverged = 1, kPcgBreakdown = 2, kPcgBadBlock = 3 };

@@ -439,6 +439,17 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
     const double *zp = G.zp;
     double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
     const int tid = threadIdx.x;
+    if (G.mf && (int)blockIdx.x == G.nheavy_dofs) {
+        // matrix-free plans (no light rows): the product's p.q partials, once, in a fixed order
+        const int nA = G.nA_sl;
+        const double a = wg_tree([&] {
+            double t = 0.0;
+            for (int i = tid; i < nA; i += 256) t += G.partA[i];
+            return t;
+        }(), red);
+        if (tid == 0) G.rec[kPcgRec * (it + 1) + PR_PQA] = a;
+        return;
+    }
     if ((int)blockIdx.x >= G.nheavy_dofs) {
         const int k = (blockIdx.x - G.nheavy_dofs) * 256 + tid;
         double pqs = 0.0;
@@ -500,7 +511,7 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
     const int tid = threadIdx.x;
     const double2 *pq2 = reinterpret_cast<const double2 *>(G.pq);
     const int nA = G.nA_sl + G.nA_light;
-    const double pq_light = wg_tree([&] {
+    const double pq_light = G.mf ? rec[PR_PQA] : wg_tree([&] {
         double a = 0.0;
         for (int i = tid; i < nA; i += 256) a += G.partA[i];
         return a;
@@ -581,6 +592,27 @@ __device__ __forceinline__ double wave_sum(double v) {
 #ifndef DEFTRI_MF_WPE
 #define DEFTRI_MF_WPE 4
 #endif
+// matrix-free plans, before product it: the update's (r.z, r.r) partials summed once (fixed order),
+// the convergence test and the record of iteration it (carried over when an earlier one ended)
+__global__ void __launch_bounds__(256) k_pcg_dots(int it, const PcgDev G) {
+    __shared__ double red[2][256];
+    double *rec = G.rec + kPcgRec * (it + 1);
+    const double *prv = G.rec + kPcgRec * it;
+    if (prv[PR_STATUS] != 0.0) {
+        if (threadIdx.x == 0) { rec[PR_STATUS] = prv[PR_STATUS]; rec[PR_ITS] = prv[PR_ITS]; }
+        return;
+    }
+    double rz, rr;
+    wg_sum2(G.partB, G.nB, rz, rr, red);
+    if (threadIdx.x == 0) {
+        const double bb = it == 0 ? rr : G.rec[kPcgRec + PR_RR];
+        rec[PR_RZ] = rz;
+        rec[PR_RR] = rr;
+        rec[PR_STATUS] = rr <= G.tol2 * bb ? kPcgConverged : kPcgRunning;
+        rec[PR_ITS] = it;
+    }
+}
+
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI_MF_WPE))) k_mf_product(int it, const PcgDev G, double lam) {
     extern __shared__ double C[];                     // per local edge and in-slice role: J^T s
     __shared__ double red[4][256];
@@ -649,22 +681,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
         }
     }
     const int64_t o = v >= 0 ? G.voff[v] : 0;
-    if (prv[PR_STATUS] != 0.0) {
-        if (blockIdx.x == 0 && tid == 0) { rec[PR_STATUS] = prv[PR_STATUS]; rec[PR_ITS] = prv[PR_ITS]; }
-        return;
-    }
-    double rz, rr;
-    wg_sum2(G.partB, G.nB, rz, rr, red);
-    const double bb = it == 0 ? rr : G.rec[kPcgRec + PR_RR];
-    const bool conv = rr <= G.tol2 * bb;
-    if (blockIdx.x == 0 && tid == 0) {
-        rec[PR_RZ] = rz;
-        rec[PR_RR] = rr;
-        rec[PR_STATUS] = conv ? kPcgConverged : kPcgRunning;
-        rec[PR_ITS] = it;
-    }
-    if (conv) return;
-    const double beta = it == 0 ? 0.0 : rz / prv[PR_RZ];
+    if (rec[PR_STATUS] != 0.0) return;                // k_pcg_dots: converged / failed
+    const double beta = it == 0 ? 0.0 : rec[PR_RZ] / prv[PR_RZ];
     const double *zp = G.zp;
     double pv[3];
 #pragma unroll
@@ -812,9 +830,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEFTRI
             pqs += pv[i] * qv;
         }
     }
-    __syncthreads();
-    const double sum = wg_tree(pqs, red[3]);
-    if (tid == 0 && live) G.partA[blockIdx.x] = sum;
+    // p.q of the slice: only wave 0 holds rows, so one fixed butterfly (no workgroup barrier)
+    if (w == 0) {
+        const double sum = wave_sum(pqs);
+        if (lane == 0 && live) G.partA[blockIdx.x] = sum;
+    }
 }
 
 // lower-triangle index of (a, b), a >= b, in a 6 x 6 block
@@ -1015,16 +1035,18 @@ void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lamb
     hipEvent_t e0 = prof_begin(st);
     // always launched (also with no slices): its workgroup 0 writes the iteration record
     const unsigned grid = (unsigned)std::max(G.nA_sl, 1);
-    if (G.mf)
+    if (G.mf) {
+        hipLaunchKernelGGL(dev::k_pcg_dots, dim3(1), dim3(256), 0, st, it, G);
         hipLaunchKernelGGL(dev::k_mf_product, dim3(grid), dim3(256), sizeof(double) * (size_t)G.mf_lds, st, it, G,
                            lambda);
+    }
     else
         hipLaunchKernelGGL(dev::k_pcg_product, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
     prof_end("pcg_product", e0, grid, 0.0, st);
 }
 
 void launch_pcg_heavy(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st) {
-    const unsigned grid = (unsigned)(G.nheavy_dofs + G.nA_light);
+    const unsigned grid = (unsigned)(G.nheavy_dofs + G.nA_light + (G.mf ? 1 : 0));
     if (grid == 0) return;
     hipEvent_t e0 = prof_begin(st);
     hipLaunchKernelGGL(dev::k_pcg_heavy, dim3(grid), dim3(256), 0, st, it, G, hval, lambda);
