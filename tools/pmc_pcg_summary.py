@@ -2,8 +2,8 @@
 k_pcg_product per active launch (FETCH_SIZE and WRITE_SIZE from separate rocprofv3 passes, KB*1024),
 keyed by the plan's algorithmic bytes per launch so bench.py only attaches it to the same plan.
 
-Launches past convergence return after the convergence test (a few KB): only launches fetching more
-than 10 % of the largest are counted as active.  On gfx950 FETCH_SIZE reports 1/2 of the bytes of
+Launches past convergence return after the convergence test: only launches running longer than 30 %
+of the longest are counted as active.  On gfx950 FETCH_SIZE reports 1/2 of the bytes of
 16-byte-per-lane coalesced reads (MI355X_MICROARCH.md, HBM section); the product's slot records and
 gathers are 16-byte loads, so the corrected fetch doubles the counter.
 
@@ -18,23 +18,30 @@ import sys
 
 
 def per_dispatch(path, ctr, kernel):
+    """per dispatch: (bytes, duration ns)"""
     vals = collections.defaultdict(float)
+    dur = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != ctr or kernel not in r["Kernel_Name"]:
             continue
         vals[r["Dispatch_Id"]] += float(r["Counter_Value"]) * 1024.0
-    return vals
+        dur[r["Dispatch_Id"]] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    return vals, dur
+
+
+def active(vals, dur):
+    """launches that ran the product (not only the convergence test): duration above 30 % of the
+    longest (the matrix-free product issues its first loads before the test, so bytes alone do not
+    separate them)"""
+    dmax = max(dur.values())
+    return [v for k, v in vals.items() if dur[k] > 0.3 * dmax]
 
 
 def main():
     src, dst = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2])
     k = sys.argv[3] if len(sys.argv) > 3 else "k_pcg_product"
-    f = per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE", k)
-    w = per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE", k)
-    fmax = max(f.values())
-    act_f = [v for v in f.values() if v > 0.1 * fmax]
-    wmax = max(w.values())
-    act_w = [v for v in w.values() if v > 0.1 * wmax]
+    act_f = active(*per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE", k))
+    act_w = active(*per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE", k))
     bench = json.loads((src / "fetch.json").read_text())
     alg = bench["roofline"]["bytes_per_launch"]
     fetch = sum(act_f) / len(act_f)
