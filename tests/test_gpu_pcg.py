@@ -166,3 +166,48 @@ def test_pcg_profile_reports_kernels(pcg_ctx):
     assert st["pcg_product"]["bytes"] > 0
     assert "hchunk" not in st
     assert "update" not in st                 # no factorization when PCG converged
+
+
+def _assembled_worker(q):
+    """child process (spawn): the assembled row view, forced before the library reads the switch"""
+    import os
+    os.environ["DEFTRI_PCG_MF"] = "0"
+    m, _ = sim.simulate_two_view(n=20000, seed=1, scale_scene=True, compact=True)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    with capi.Context(0) as ctx:
+        ctx.upload(p)
+        ctx.set_linear_solver("pcg", max_iterations=4096)
+        st = ctx.profile_trial(1e10)
+        ctx.reset_state()
+        r = ctx.solve_lm(6, analytic=False)
+        pts, _, _ = ctx.download()
+    q.put({"chi2_iter": list(r["chi2_iter"]), "trials": r["trials_total"], "fallbacks": r["pcg_fallbacks"],
+           "pts": pts[:50].ravel().tolist(), "assembled": "pcg_repack" in st and "mf_lin" not in st})
+
+
+def test_matrix_free_matches_assembled_product(pcg_ctx):
+    """The matrix-free product (default) and the assembled row view (DEFTRI_PCG_MF=0, in a spawned
+    process: the switch is read once per process) take the same LM trajectory on the benchmark's
+    scene at 20k correspondences with the reference's numeric Jacobians: identical trial counts, no
+    fallback, chi2 rel 1e-8, points rel 1e-7 (the two products round differently; each step is
+    solved to a 1e-12 relative residual)."""
+    import torch.multiprocessing as mp
+    cm = mp.get_context("spawn")
+    q = cm.Queue()
+    pr = cm.Process(target=_assembled_worker, args=(q,))
+    pr.start()
+    ref = q.get(timeout=240)
+    pr.join(timeout=60)
+    assert pr.exitcode == 0 and ref["assembled"]
+    m, _ = sim.simulate_two_view(n=20000, seed=1, scale_scene=True, compact=True)
+    p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
+    pcg_ctx.upload(p)
+    pcg_ctx.set_linear_solver("pcg", max_iterations=4096)
+    st = pcg_ctx.profile_trial(1e10)
+    assert "mf_lin" in st                       # this process runs the matrix-free product
+    pcg_ctx.reset_state()
+    r = pcg_ctx.solve_lm(6, analytic=False)
+    pts, _, _ = pcg_ctx.download()
+    assert r["trials_total"] == ref["trials"] and r["pcg_fallbacks"] == ref["fallbacks"] == 0
+    np.testing.assert_allclose(r["chi2_iter"][:6], ref["chi2_iter"][:6], rtol=1e-8)
+    np.testing.assert_allclose(pts[:50].ravel(), ref["pts"], rtol=1e-7, atol=1e-10)
