@@ -133,6 +133,13 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);
 void launch_sum(int64_t n, const double *a, const double *b, double lambda, int mode, double *part, int nparts,
                 double *out, hipStream_t st, const double *w = nullptr);
+// several fixed-order sums in two launches (the per-array arithmetic of launch_sum: the same
+// partials and final butterfly), optionally total = (out0 + out2) + out1 — the order launch_sum's
+// three-value pass adds them in
+struct SumJob { int64_t n = 0; const double *a = nullptr, *b = nullptr, *w = nullptr; double lambda = 0; int mode = 0; double *out = nullptr; };
+constexpr int kMaxSumJobs = 4;
+struct SumJobs { SumJob j[kMaxSumJobs]; int nj = 0; double *total = nullptr; };
+void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st);
 void launch_pack_cb(const DevPlan &L, int64_t arena_off, int m, int s, double *buf, hipStream_t st);
 void launch_ea_packed(const DevPlan &L, int64_t ea_off, int nea, const double *buf, hipStream_t st);
 void launch_gather_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st);

@@ -1388,6 +1388,44 @@ __global__ void __launch_bounds__(256) k_sum_partial(int64_t n, const double *__
 }
 
 // one wave: lane l sums partials l, l+64, ... in order, then a fixed butterfly (deterministic)
+__global__ void __launch_bounds__(256) k_sum_multi_partial(const SumJobs J, double *__restrict__ part) {
+    const SumJob &jb = J.j[blockIdx.y];
+    __shared__ double red[256];
+    const int64_t n = jb.n;
+    int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    double acc = 0.0;
+    const int mode = jb.mode;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        double v = jb.a[i];
+        acc += (mode == 0) ? v : (mode == 1) ? v * (jb.lambda * v + jb.b[i]) : v * (jb.lambda * jb.w[i] * v + jb.b[i]);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+}
+
+// one wave per job: its parts strided over the lanes, then the butterfly (k_sum_final's order)
+__global__ void k_sum_multi_final(const SumJobs J, int nparts, const double *__restrict__ part) {
+    __shared__ double s[kMaxSumJobs];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double acc = 0.0;
+    for (int i = lane; i < nparts; i += 64) acc += part[(int64_t)w * nparts + i];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+        const double v = J.j[w].n > 0 ? acc : 0.0;
+        *J.j[w].out = v;
+        s[w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && J.total) *J.total = (s[0] + s[2]) + s[1];
+}
+
 __global__ void k_sum_final(int n, const double *__restrict__ part, double *__restrict__ out) {
     const int lane = threadIdx.x;
     double acc = 0.0;
@@ -1806,6 +1844,12 @@ void launch_sum(int64_t n, const double *a, const double *b, double lambda, int 
     if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
     LAUNCH("sum_partial", dev::k_sum_partial, dim3(nparts), dim3(256), st, n, a, b, lambda, mode, w, part);
     LAUNCH("sum_final", dev::k_sum_final, dim3(1), dim3(64), st, nparts, part, out);
+}
+
+void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st) {
+    if (J.nj <= 0) return;
+    LAUNCH("sum_partial", dev::k_sum_multi_partial, dim3(nparts, J.nj), dim3(256), st, J, part);
+    LAUNCH("sum_final", dev::k_sum_multi_final, dim3(1), dim3(64 * J.nj), st, J, nparts, part);
 }
 
 void launch_maxdiag(const DevPlan &L, double *part, int nparts, double *out, hipStream_t st) {

@@ -530,7 +530,7 @@ int upload_device(deftri_ctx *ctx, const HostProblem &h) {
     if (S.trsm_fused && (rc = dalloc(ctx, &L.wbuf, 4096 * std::max<int64_t>(S.npanels, 1)))) return rc;   // else nullptr: no W
     if ((rc = dalloc(ctx, &ctx->d_dx, S.ndof))) return rc;
     HIPOK(hipMemset(ctx->d_dx, 0, sizeof(double) * (size_t)std::max<int64_t>(S.ndof, 1)));   // dofs no solve writes stay 0
-    if ((rc = dalloc(ctx, &ctx->d_part, kRedParts))) return rc;
+    if ((rc = dalloc(ctx, &ctx->d_part, kMaxSumJobs * kRedParts))) return rc;   // launch_sum_multi: one run of parts per job
     if ((rc = dalloc(ctx, &ctx->d_scal, 8))) return rc;
     ctx->pcg_avail = false;
     ctx->pcg_why.clear();
@@ -754,14 +754,20 @@ void subset_edges(const HostProblem &full, const DistPlan &D, HostProblem &h) {
 // chi2 at the current state (computeActiveErrors + activeRobustChi2) into d_scal[slot]; point-sharded:
 // this rank's edges, summed over the ranks unless `reduce` is false (the caller reduces it together
 // with other scalars)
-int eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot, bool reduce = true) {
+// extra: one more fixed-order sum to run in the same two launches (the trial's rho denominator)
+int eval_chi2_dev(deftri_ctx *ctx, bool want_jac, bool analytic, int slot, bool reduce = true,
+                  const SumJob *extra = nullptr) {
     DevProblem &P = ctx->P;
     launch_linearize(P, ctx->st, want_jac, analytic);
     // sum of the three chi arrays, in edge order rep, depth, arap (three partial sums, then add)
-    launch_sum(P.R, P.chi_rep, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 4, ctx->st);
-    launch_sum(P.D, P.chi_dep, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 5, ctx->st);
-    launch_sum(P.E, P.chi_arap, nullptr, 0, 0, ctx->d_part, kRedParts, ctx->d_scal + 6, ctx->st);
-    launch_sum(3, ctx->d_scal + 4, nullptr, 0, 0, ctx->d_part, 1, ctx->d_scal + slot, ctx->st);
+    SumJobs J;
+    J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = ctx->d_scal + 4;
+    J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = ctx->d_scal + 5;
+    J.j[2].n = P.E; J.j[2].a = P.chi_arap; J.j[2].out = ctx->d_scal + 6;
+    J.nj = 3;
+    if (extra) J.j[J.nj++] = *extra;
+    J.total = ctx->d_scal + slot;
+    launch_sum_multi(J, ctx->d_part, kRedParts, ctx->st);
     return reduce ? dist_allreduce(ctx, ctx->d_scal + slot, 1, 0) : 0;
 }
 
@@ -1517,8 +1523,11 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                     hipEventRecord(ctx->ev[5], ctx->st);
                     HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
                 } else {
-                    eval_chi2_dev(ctx, false, analytic, 0);      // computeActiveErrors; activeRobustChi2
-                    launch_sum(ctx->S.ndof, ctx->d_dx, L.b, lambda, 1, ctx->d_part, kRedParts, ctx->d_scal + 1, ctx->st);
+                    // computeActiveErrors; activeRobustChi2; rho's denominator dx.(lambda dx + b)
+                    SumJob den;
+                    den.n = ctx->S.ndof; den.a = ctx->d_dx; den.b = L.b; den.lambda = lambda; den.mode = 1;
+                    den.out = ctx->d_scal + 1;
+                    eval_chi2_dev(ctx, false, analytic, 0, true, &den);
                     hipEventRecord(ctx->ev[5], ctx->st);
                     HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
                     HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
