@@ -423,6 +423,7 @@ def main():
             "cpu_baseline": cpu,
             "breakdown_ms": {"total": rep["ms_total"], "linearize": rep["ms_linearize"],
                              "factor": rep["ms_factor"], "solve": rep["ms_solve"], "update": rep["ms_update"],
+                             "note": "factor/solve/update of sequential trials only with DEFTRI_TRIAL_EVENTS=1",
                              "pcg": rep["ms_pcg"]},
             "trial_kernel_ms": trial_ms,
             "factorization_trial_kernel_ms": factor_trial_ms if pcg_prof else None,

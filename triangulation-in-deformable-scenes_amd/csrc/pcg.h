@@ -196,8 +196,9 @@ void launch_pcg_repack(const PcgDev &G, const double *hval, hipStream_t st);
 // want_dvec the diagonal of H per dof too (max diag for the initial lambda)
 void launch_mf_lin(const PcgDev &G, bool want_dvec, hipStream_t st);
 // one solve's launches (x = dx).  setup: preconditioner blocks at lambda, r = b, z = M r, x = 0.
+// rec_cleared: the records were cleared by the trial's prologue (launch_trial_begin)
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
-                      hipStream_t st);
+                      hipStream_t st, bool rec_cleared = false);
 // iteration it: product q = (H + lambda I) p (p = z + beta p_prev formed on the fly) after the
 // convergence test of the residual the previous update left
 void launch_pcg_product(const PcgDev &G, int it, const double *hval, double lambda, hipStream_t st);

@@ -1024,8 +1024,8 @@ void launch_mf_lin(const PcgDev &G, bool want_dvec, hipStream_t st) {
 }
 
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
-                      hipStream_t st) {
-    hipMemsetAsync(G.rec, 0, sizeof(double) * kPcgRec * (size_t)(G.max_it + 2), st);
+                      hipStream_t st, bool rec_cleared) {
+    if (!rec_cleared) hipMemsetAsync(G.rec, 0, sizeof(double) * kPcgRec * (size_t)(G.max_it + 2), st);
     hipEvent_t e0 = prof_begin(st);
     hipLaunchKernelGGL(dev::k_pcg_setup, dim3(G.nB), dim3(256), 0, st, G, hval, b, lambda, x);
     prof_end("pcg_setup", e0, G.nB, 0.0, st);

@@ -791,6 +791,24 @@ void pop_state(deftri_ctx *ctx) {
     hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
 }
 
+// DEFTRI_TRIAL_FUSE=0: the trial prologue / read-back as separate copies and fills (A/B)
+bool trial_fuse_on() {
+    static const bool on = [] { const char *e = std::getenv("DEFTRI_TRIAL_FUSE"); return !e || std::atoi(e) != 0; }();
+    return on;
+}
+
+// DEFTRI_TRIAL_EVENTS=1: per-trial timing events on the sequential trial path, for the factor /
+// solve / update split of the report (off by default: each event record is a barrier packet, ~6 us
+// of stream time per event, 4 per trial; measured 0.874 -> 0.849 ms per C2 PCG trial without them)
+bool trial_events_on() {
+    static const bool on = [] { const char *e = std::getenv("DEFTRI_TRIAL_EVENTS"); return e && std::atoi(e) != 0; }();
+    return on;
+}
+
+void trial_ev(deftri_ctx *ctx, hipEvent_t ev, hipStream_t st) {
+    if (trial_events_on()) hipEventRecord(ev, st);
+}
+
 bool use_pcg(const deftri_ctx *ctx) { return ctx->lin_solver == DEFTRI_SOLVER_PCG && ctx->pcg_avail; }
 
 // buildSystem after a linearization.  A matrix-free PCG step reads only b and the diagonal blocks
@@ -949,6 +967,7 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
         delete ctx;
         return DEFTRI_E_HIP;
     }
+    for (int i = 0; i < 32; i++) ctx->hpin[i] = 0.0;
     hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
     for (auto &e : ctx->sync_ev) hipEventCreateWithFlags(&e, hipEventDisableTiming);
     if (hipHostMalloc((void **)&ctx->lane_pin, 2 * kMaxLanes * sizeof(double), hipHostMallocDefault) != hipSuccess ||
@@ -1271,16 +1290,21 @@ namespace {
 //   pcg_poll:  reads the record of the last product; while still running, further chunks of 4
 //              iterations with a read-back each.  solved = false: budget exhausted, breakdown, or a
 //              preconditioner block not positive definite — the caller factors instead.
-void pcg_start(deftri_ctx *ctx, double lambda, const double *rhs, int &j) {
+void pcg_limits(deftri_ctx *ctx) {
+    ctx->G.max_it = ctx->pcg_max_it > 0 ? ctx->pcg_max_it : ctx->pcg_auto_it;
+    ctx->G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
+}
+
+// rec_cleared: the trial's prologue (launch_trial_begin, after pcg_limits) cleared the records
+void pcg_start(deftri_ctx *ctx, double lambda, const double *rhs, int &j, bool rec_cleared = false) {
     PcgDev &G = ctx->G;
     const DevPlan &L = ctx->L;
-    G.max_it = ctx->pcg_max_it > 0 ? ctx->pcg_max_it : ctx->pcg_auto_it;
-    G.tol2 = ctx->pcg_tol * ctx->pcg_tol;
+    pcg_limits(ctx);
     if (!ctx->pcg_packed && !G.mf) {
         launch_pcg_repack(G, L.hval, ctx->st);
         ctx->pcg_packed = true;
     }
-    launch_pcg_setup(G, L.hval, rhs, lambda, ctx->d_dx, ctx->st);
+    launch_pcg_setup(G, L.hval, rhs, lambda, ctx->d_dx, ctx->st, rec_cleared);
     launch_pcg_product(G, 0, L.hval, lambda, ctx->st);
     j = 0;
     const int n = std::min(std::max(2, ctx->pcg_last_its + 1), G.max_it);
@@ -1503,13 +1527,21 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 if (acc >= 0) adopt_lane_state(ctx, acc);
             }
         } else do {
-            push_state(ctx);
-            HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
+            // PCG trials on one rank: the prologue (state backup, flag and PCG records cleared) and
+            // the read-back (scalars, flag, the solve's record) are one launch each
+            const bool fused = pcg && !dist && trial_fuse_on();
+            if (fused) {
+                pcg_limits(ctx);
+                launch_trial_begin(P, L.flag, ctx->G.rec, (int64_t)kPcgRec * (ctx->G.max_it + 2), ctx->st);
+            } else {
+                push_state(ctx);
+                HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
+            }
             double *sc = ctx->hpin + 4;
             // the trial's evaluation: _optimizer->update(x) (skipped on a zero pivot), chi2, rho's
-            // denominator, read-backs (one host round trip)
-            auto evaluate = [&]() -> int {
-                hipEventRecord(ctx->ev[4], ctx->st);
+            // denominator, read-backs (one host round trip); rec_j: the PCG record read back with them
+            auto evaluate = [&](const double *rec_j) -> int {
+                trial_ev(ctx, ctx->ev[4], ctx->st);
                 launch_update_state(P, ctx->d_dx, ctx->st, L.flag);
                 if (dist) {
                     // chi2 of the rank's edges, dx.(lambda dx + b) with b partial and lambda once per dof,
@@ -1520,7 +1552,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                                ctx->d_dofw);
                     launch_int_to_double(1, L.flag, ctx->d_scal + 2, ctx->st);
                     if ((r2 = dist_allreduce(ctx, ctx->d_scal, 3, 0))) return r2;
-                    hipEventRecord(ctx->ev[5], ctx->st);
+                    trial_ev(ctx, ctx->ev[5], ctx->st);
                     HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, ctx->st));
                 } else {
                     // computeActiveErrors; activeRobustChi2; rho's denominator dx.(lambda dx + b)
@@ -1528,24 +1560,29 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                     den.n = ctx->S.ndof; den.a = ctx->d_dx; den.b = L.b; den.lambda = lambda; den.mode = 1;
                     den.out = ctx->d_scal + 1;
                     eval_chi2_dev(ctx, false, analytic, 0, true, &den);
-                    hipEventRecord(ctx->ev[5], ctx->st);
-                    HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
-                    HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+                    trial_ev(ctx, ctx->ev[5], ctx->st);
+                    if (fused) {
+                        launch_trial_readback(ctx->d_scal, 2, L.flag, rec_j, kPcgRec, sc, ctx->ipin, ctx->hpin + 16,
+                                              ctx->st);
+                    } else {
+                        HIPOK(hipMemcpyAsync(sc, ctx->d_scal, sizeof(double) * 2, hipMemcpyDeviceToHost, ctx->st));
+                        HIPOK(hipMemcpyAsync(ctx->ipin, L.flag, sizeof(int), hipMemcpyDeviceToHost, ctx->st));
+                    }
                 }
                 return 0;
             };
             bool solved = false, evaluated = false;
-            hipEventRecord(ctx->ev[2], ctx->st);
+            trial_ev(ctx, ctx->ev[2], ctx->st);
             if (pcg) {
                 // PCG step with the evaluation queued behind the predicted iteration count: when the
                 // solve has converged by then, the trial costs one round trip; otherwise the state
                 // is restored, the solve continues (or falls back) and the evaluation is redone
                 auto t0 = std::chrono::steady_clock::now();
                 int j = 0, its = 0;
-                pcg_start(ctx, lambda, L.b, j);
-                hipEventRecord(ctx->ev[3], ctx->st);
-                if ((rc = evaluate())) return rc;
-                if ((rc = pcg_fetch(ctx, j))) return rc;
+                pcg_start(ctx, lambda, L.b, j, fused);
+                trial_ev(ctx, ctx->ev[3], ctx->st);
+                if ((rc = evaluate(fused ? ctx->G.rec + (size_t)kPcgRec * (j + 1) : nullptr))) return rc;
+                if (!fused && (rc = pcg_fetch(ctx, j))) return rc;
                 HIPOK(hipStreamSynchronize(ctx->st));
                 const int v = pcg_verdict(ctx, j, its);
                 if (v > 0) {
@@ -1560,31 +1597,31 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 else R.pcg_fallbacks++;
                 if (prm->verbose)
                     std::fprintf(stderr, "[deftri] pcg lambda %.6e iterations %d %s\n", lambda, its, solved ? "converged" : "-> LDL^T");
-                if (!solved) hipEventRecord(ctx->ev[2], ctx->st);
+                if (!solved) trial_ev(ctx, ctx->ev[2], ctx->st);
             }
             if (!solved) {
                 ensure_assembled(ctx);                       // a matrix-free PCG step left H unassembled
                 ctx->hpin[12] = lambda;                      // pinned: read by the copy at its turn in the stream
                 HIPOK(hipMemcpyAsync(ctx->d_lam, ctx->hpin + 12, sizeof(double), hipMemcpyHostToDevice, ctx->st));
                 if (launch_trial_graph(ctx)) {
-                    hipEventRecord(ctx->ev[3], ctx->st);     // factor + solve in one graph: timed as factor
+                    trial_ev(ctx, ctx->ev[3], ctx->st);     // factor + solve in one graph: timed as factor
                 } else {
                     launch_scatter(L, lambda, ctx->st);      // setLambda
                     launch_factor(L, ctx->st, ctx->side, ctx->sync_ev, 64, hook, ctx);
-                    hipEventRecord(ctx->ev[3], ctx->st);
+                    trial_ev(ctx, ctx->ev[3], ctx->st);
                     ctx->hook_x = ctx->d_dx;
                     launch_solve(L, L.b, ctx->d_dx, ctx->st, dist ? L.b : nullptr, hook, ctx);
                     if (ctx->hook_rc) return ctx->hook_rc;
                 }
             }
-            if (solved && !evaluated) hipEventRecord(ctx->ev[3], ctx->st);
-            if (!evaluated && (rc = evaluate())) return rc;
+            if (solved && !evaluated) trial_ev(ctx, ctx->ev[3], ctx->st);
+            if (!evaluated && (rc = evaluate(nullptr))) return rc;
             HIPOK(hipStreamSynchronize(ctx->st));       // the one host round trip of a trial
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; t_lin += ev_ms(ctx, 0, 1); }
             if (dist ? sc[2] >= kStatusWaitTimeout : (*ctx->ipin & kStatusWaitTimeout) != 0)
                 return fail(ctx, DEFTRI_E_HIP, "factorization: a fused TRSM tile timed out waiting for its panel");
             const bool ok2 = dist ? sc[2] == 0.0 : *ctx->ipin == 0;
-            t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5);
+            if (trial_events_on()) { t_fac += ev_ms(ctx, 2, 3); t_sol += ev_ms(ctx, 3, 4); t_upd += ev_ms(ctx, 4, 5); }
             double tempChi = ok2 ? sc[0] : std::numeric_limits<double>::max();
             rho = (currentChi - tempChi);
             double scale = sc[1] + 1e-3;
