@@ -131,8 +131,10 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
 void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st, const double *bpart = nullptr,
                   LevelHook hook = nullptr, void *hook_user = nullptr);
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);
-// a trial's prologue: state backup, zero-pivot flag and nzero doubles at `zero` cleared, one launch
-void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st);
+// a trial's prologue: state backup (restore: the state restored from the backup), zero-pivot flag and
+// nzero doubles at `zero` cleared, one launch
+void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st,
+                        bool restore = false);
 // a trial's read-back: ns scalars, the flag and (rec != nullptr) nrec record values into pinned host memory
 void launch_trial_readback(const double *scal, int ns, const int *flag, const double *rec, int nrec, double *h_scal,
                            int *h_flag, double *h_rec, hipStream_t st);

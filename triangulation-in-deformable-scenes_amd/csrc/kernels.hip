@@ -1366,17 +1366,18 @@ __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ d
     }
 }
 
-// a trial's prologue in one launch: the state backup (push_state's three copies), the zero-pivot flag
-// and the PCG records cleared (two fills); grid-stride over the longest of them
-__global__ void __launch_bounds__(256) k_trial_begin(int P, int S, int Q, const double *__restrict__ points,
-                                                     const double *__restrict__ scales, const double *__restrict__ tg,
-                                                     double *__restrict__ points_bak, double *__restrict__ scales_bak,
-                                                     double *__restrict__ tg_bak, int *__restrict__ flag,
+// a trial's prologue in one launch: the state backup (push_state's three copies) — or, after a
+// rejected trial, its restore from the backup (pop_state's) — the zero-pivot flag and the PCG records
+// cleared (two fills); grid-stride over the longest of them
+__global__ void __launch_bounds__(256) k_trial_begin(int P, int S, int Q, const double *__restrict__ src_points,
+                                                     const double *__restrict__ src_scales, const double *__restrict__ src_tg,
+                                                     double *__restrict__ dst_points, double *__restrict__ dst_scales,
+                                                     double *__restrict__ dst_tg, int *__restrict__ flag,
                                                      double *__restrict__ zero, int64_t nzero, int64_t n) {
     for (int64_t i = TID; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (i < 3 * (int64_t)P) points_bak[i] = points[i];
-        if (i < S) scales_bak[i] = scales[i];
-        if (i < 7 * (int64_t)Q) tg_bak[i] = tg[i];
+        if (i < 3 * (int64_t)P) dst_points[i] = src_points[i];
+        if (i < S) dst_scales[i] = src_scales[i];
+        if (i < 7 * (int64_t)Q) dst_tg[i] = src_tg[i];
         if (i < nzero) zero[i] = 0.0;
         if (i == 0) *flag = 0;
     }
@@ -1870,12 +1871,16 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, 
                            P.scales, P.tg, flag);
 }
 
-void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st) {
+void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st, bool restore) {
     int64_t n = std::max<int64_t>(std::max<int64_t>(3 * (int64_t)P.P, 7 * (int64_t)P.Q), std::max<int64_t>(P.S, nzero));
     n = std::max<int64_t>(n, 1);
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
-    LAUNCH("trial_begin", dev::k_trial_begin, dim3(grid), dim3(256), st, P.P, P.S, P.Q, P.points, P.scales, P.tg,
-           P.points_bak, P.scales_bak, P.tg_bak, flag, zero, nzero, n);
+    if (restore)
+        LAUNCH("trial_begin", dev::k_trial_begin, dim3(grid), dim3(256), st, P.P, P.S, P.Q, P.points_bak, P.scales_bak,
+               P.tg_bak, P.points, P.scales, P.tg, flag, zero, nzero, n);
+    else
+        LAUNCH("trial_begin", dev::k_trial_begin, dim3(grid), dim3(256), st, P.P, P.S, P.Q, P.points, P.scales, P.tg,
+               P.points_bak, P.scales_bak, P.tg_bak, flag, zero, nzero, n);
 }
 
 void launch_trial_readback(const double *scal, int ns, const int *flag, const double *rec, int nrec, double *h_scal,

@@ -1480,6 +1480,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         }
         double rho = 0;
         int qmax = 0;
+        bool restore_pending = false;                        // a rejected fused trial's state not yet restored
         if (nlanes > 1) {
             // speculative rounds: lanes 0..nl-1 run trials qmax..qmax+nl-1 concurrently; the host then
             // replays g2o's accept/reject sequence over their scalars in trial order
@@ -1531,8 +1532,11 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             // the read-back (scalars, flag, the solve's record) are one launch each
             const bool fused = pcg && !dist && trial_fuse_on();
             if (fused) {
+                // after a rejected trial the prologue restores the state from the backup instead
                 pcg_limits(ctx);
-                launch_trial_begin(P, L.flag, ctx->G.rec, (int64_t)kPcgRec * (ctx->G.max_it + 2), ctx->st);
+                launch_trial_begin(P, L.flag, ctx->G.rec, (int64_t)kPcgRec * (ctx->G.max_it + 2), ctx->st,
+                                   restore_pending);
+                restore_pending = false;
             } else {
                 push_state(ctx);
                 HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
@@ -1638,12 +1642,14 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
             } else {
                 lambda *= ni;
                 ni *= 2;
-                pop_state(ctx);
+                if (fused) restore_pending = true;           // the next prologue (or the loop's end) restores
+                else pop_state(ctx);
                 R.trials_rejected++;
                 if (!std::isfinite(lambda)) { qmax++; break; }   // g2o OptimizationAlgorithmLevenberg::solve
             }
             qmax++;
         } while (rho < 0 && qmax < max_trials);
+        if (restore_pending) { pop_state(ctx); restore_pending = false; }
         if (it < DEFTRI_MAX_REPORT_ITERS) { R.chi2_iter[it] = currentChi; R.trials_iter[it] = qmax; }
         if (prm->verbose)
             std::fprintf(stderr, "[deftri] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
