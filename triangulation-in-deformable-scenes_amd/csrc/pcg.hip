@@ -507,9 +507,31 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
 __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, double lam, double *__restrict__ x) {
     __shared__ double red[2][256];
     double *rec = G.rec + kPcgRec * (it + 1);
-    if (rec[PR_STATUS] != 0.0) return;
     const int tid = threadIdx.x;
     const double2 *pq2 = reinterpret_cast<const double2 *>(G.pq);
+    // a 3-dof row (a point, not a heavy row) loads everything it needs that does not depend on alpha
+    // first — (p, q), r, x and M — so those loads are in flight while the status, the p.q sums and
+    // the heavy rows arrive; the arithmetic below is the generic path's, in the same order
+    const int64_t v = (int64_t)blockIdx.x * 256 + tid;
+    int d = 0, hk = -1;
+    int64_t o = 0;
+    bool fast = false;
+    double2 w3[3];
+    double r3[3], x3[3], M9[9];
+    if (v < G.nv) {
+        d = G.vdim[v];
+        o = G.voff[v];
+        hk = G.v_heavy[v];
+        fast = d == 3 && hk < 0;
+        if (fast) {
+            const double *M = G.minv + G.moff[v];
+#pragma unroll
+            for (int i = 0; i < 3; i++) { w3[i] = pq2[o + i]; r3[i] = G.r[o + i]; x3[i] = x[o + i]; }
+#pragma unroll
+            for (int k = 0; k < 9; k++) M9[k] = M[k];
+        }
+    }
+    if (rec[PR_STATUS] != 0.0) return;
     const int nA = G.nA_sl + G.nA_light;
     const double pq_light = G.mf ? rec[PR_PQA] : wg_tree([&] {
         double a = 0.0;
@@ -519,9 +541,9 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
     // the heavy rows' p.q (their q from k_pcg_heavy), in heavy-dof order
     if (tid == 0) {
         double a = 0.0;
-        for (int hk = 0; hk < G.nheavy; hk++) {
-            const int64_t o = G.voff[G.heavy_v[hk]];
-            for (int i = 0; i < G.h_dofbase[hk + 1] - G.h_dofbase[hk]; i++) a += pq2[o + i].x * G.hqf[G.h_dofbase[hk] + i];
+        for (int hh = 0; hh < G.nheavy; hh++) {
+            const int64_t oh = G.voff[G.heavy_v[hh]];
+            for (int i = 0; i < G.h_dofbase[hh + 1] - G.h_dofbase[hh]; i++) a += pq2[oh + i].x * G.hqf[G.h_dofbase[hh] + i];
         }
         red[1][0] = a;
     }
@@ -534,12 +556,26 @@ __global__ void __launch_bounds__(256) k_pcg_update(int it, const PcgDev G, doub
     }
     if (blockIdx.x == 0 && tid == 0) { rec[PR_PQ] = pq; rec[PR_ALPHA] = alpha; }
     __syncthreads();
-    const int64_t v = (int64_t)blockIdx.x * 256 + tid;
     double rz = 0.0, rr = 0.0;
-    if (v < G.nv) {
-        const int d = G.vdim[v];
-        const int64_t o = G.voff[v];
-        const int hk = G.v_heavy[v];
+    if (fast) {
+        double rv[3];
+        double2 *zp = reinterpret_cast<double2 *>(G.zp);
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            x[o + i] = x3[i] + alpha * w3[i].x;
+            rv[i] = r3[i] - alpha * w3[i].y;
+            G.r[o + i] = rv[i];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            double zi = 0.0;
+#pragma unroll
+            for (int j = 0; j < 3; j++) zi += M9[i * 3 + j] * rv[j];
+            zp[o + i] = make_double2(zi, w3[i].x);
+            rz += rv[i] * zi;
+            rr += rv[i] * rv[i];
+        }
+    } else if (v < G.nv) {
         double rv[6], pv[6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
