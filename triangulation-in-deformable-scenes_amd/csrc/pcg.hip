@@ -434,11 +434,11 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
                                                    double lam) {
     __shared__ double red[256];
     const double *rec = G.rec + kPcgRec * (it + 1);
-    if (rec[PR_STATUS] != 0.0) return;
-    const double beta = it == 0 ? 0.0 : rec[PR_RZ] / G.rec[kPcgRec * it + PR_RZ];
     const double *zp = G.zp;
     double2 *pq2 = reinterpret_cast<double2 *>(G.pq);
     const int tid = threadIdx.x;
+    // the partial sums below need no scalar of this iteration: they are loaded and summed before the
+    // status test (uniform per workgroup), beta only after it
     if (G.mf && (int)blockIdx.x == G.nheavy_dofs) {
         // matrix-free plans (no light rows): the product's p.q partials, once, in a fixed order
         const int nA = G.nA_sl;
@@ -447,10 +447,13 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
             for (int i = tid; i < nA; i += 256) t += G.partA[i];
             return t;
         }(), red);
+        if (rec[PR_STATUS] != 0.0) return;
         if (tid == 0) G.rec[kPcgRec * (it + 1) + PR_PQA] = a;
         return;
     }
     if ((int)blockIdx.x >= G.nheavy_dofs) {
+        if (rec[PR_STATUS] != 0.0) return;
+        const double beta = it == 0 ? 0.0 : rec[PR_RZ] / G.rec[kPcgRec * it + PR_RZ];
         const int k = (blockIdx.x - G.nheavy_dofs) * 256 + tid;
         double pqs = 0.0;
         if (k < G.nlight) {
@@ -486,6 +489,8 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
         for (int u = 0; u < 4; u++)
             if (t + 256 * u < b1) a[u] += G.hs_part[(t + 256 * u) * 6 + i];
     const double s_slots = wg_tree((a[0] + a[1]) + (a[2] + a[3]), red);
+    if (rec[PR_STATUS] != 0.0) return;
+    const double beta = it == 0 ? 0.0 : rec[PR_RZ] / G.rec[kPcgRec * it + PR_RZ];
     const int v = G.heavy_v[hk];
     const int d = G.vdim[v];
     const int f0 = G.h_first[hk], f1 = G.h_first[hk + 1];
