@@ -268,7 +268,11 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
         }
         if (!ok) G.rec[PR_STATUS] = kPcgBadBlock;   // record 0 (cleared before the launch)
         double *M = G.minv + G.moff[v];
-        double rv[6], Mi[36];
+        // z = M r accumulated column by column as M's columns are formed: z_i += M_ic r_c in c order,
+        // the same FMA sequence as a row-wise sum after the fact, without holding all of M (VGPRs)
+        double rv[6], z[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) { rv[i] = i < d ? b[o + i] : 0.0; z[i] = 0.0; }
 #pragma unroll
         for (int c = 0; c < 6; c++) {
             if (c < d) {
@@ -292,19 +296,14 @@ __global__ void __launch_bounds__(256) k_pcg_setup(const PcgDev G, const double 
                 }
 #pragma unroll
                 for (int i = 0; i < 6; i++)
-                    if (i < d) { M[i * d + c] = y[i]; Mi[i * 6 + c] = y[i]; }
+                    if (i < d) { M[i * d + c] = y[i]; z[i] += y[i] * rv[c]; }
             }
         }
-#pragma unroll
-        for (int i = 0; i < 6; i++) rv[i] = i < d ? b[o + i] : 0.0;
         double2 *zp = reinterpret_cast<double2 *>(G.zp);
 #pragma unroll
         for (int i = 0; i < 6; i++) {
             if (i < d) {
-                double zi = 0.0;
-#pragma unroll
-                for (int j = 0; j < 6; j++)
-                    if (j < d) zi += Mi[i * 6 + j] * rv[j];
+                const double zi = z[i];
                 G.r[o + i] = rv[i];
                 zp[o + i] = make_double2(zi, 0.0);
                 x[o + i] = 0.0;
