@@ -481,12 +481,23 @@ __global__ void __launch_bounds__(256) k_pcg_heavy(int it, const PcgDev G, const
     while (G.h_dofbase[hk + 1] <= k) hk++;
     const int i = k - G.h_dofbase[hk];
     const int64_t b0 = G.hv_slot_begin[hk], b1 = G.hv_slot_begin[hk + 1];
-    // four independent strided streams per thread (loads in flight together), combined in order
+    // four independent strided streams per thread, combined in order; four rounds of the streams
+    // (16 loads) are issued before any is added, so a heavy dof of up to 4096 slots waits on one
+    // round of load latency (same additions in the same order as a round-by-round loop)
     double a[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t t = b0 + tid; t < b1; t += 1024)
+    for (int64_t t0 = b0 + tid; t0 < b1; t0 += 4096) {
+        double h[16];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (t + 256 * u < b1) a[u] += G.hs_part[(t + 256 * u) * 6 + i];
+        for (int q = 0; q < 16; q++) {
+            const int64_t t = t0 + 256 * q;
+            h[q] = t < b1 ? G.hs_part[t * 6 + i] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (t0 + 1024 * r + 256 * u < b1) a[u] += h[4 * r + u];
+    }
     const double s_slots = wg_tree((a[0] + a[1]) + (a[2] + a[3]), red);
     if (rec[PR_STATUS] != 0.0) return;
     const double beta = it == 0 ? 0.0 : rec[PR_RZ] / G.rec[kPcgRec * it + PR_RZ];
