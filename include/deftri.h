@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 3
+#define DEFTRI_ABI_VERSION 4
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -210,6 +210,54 @@ int deftri_set_linear_solver(deftri_ctx *ctx, int32_t solver, double tol, int32_
 /* The last PCG step of this context (solve_lm trial or eval_damped_solve): CG iterations and
    whether it converged (0: the LDL^T solved that step). */
 int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_t *pcg_converged);
+
+/* ---- plan kind (round 3) ---------------------------------------------------------------------
+   DEFTRI_PLAN_MULTIFRONTAL: nested dissection + multifrontal LDL^T analysis at upload; PCG steps use
+   the sliced matrix-free product where it fits (one KF pair) with the LDL^T as fallback.
+   DEFTRI_PLAN_ITERATIVE: the point-sharded matrix-free PCG plan (csrc/spcg.h) — no factorization:
+   rows = points grouped by mesh vertex in Morton order, dealt to the ranks in contiguous
+   work-balanced ranges; per CG iteration an edge-parallel pass s_e = W_e J_e p over the rank's local
+   ARAP edges and a row-parallel gather q_v = sum J_{e,v}^T s_e (+ the folded reprojection / depth
+   blocks); sharded: one halo exchange of the boundary rows' (z, p) and two all-reduces (the dot
+   products, the global-vertex partials) per CG iteration.  A step whose PCG does not converge within
+   the budget (deftri_set_linear_solver max_iterations; <= 0: 1000) counts as a failed linear solve
+   (g2o: the trial is rejected).  Any keyframe count (all-pairs graphs, BASELINE C3-C5).
+   DEFTRI_PLAN_AUTO (default): ITERATIVE for point-sharded PCG contexts (nranks > 1 with
+   DEFTRI_SOLVER_PCG) and for multi-pair problems above 1M unknowns; MULTIFRONTAL otherwise.
+   Applies to the next deftri_problem_upload. */
+#define DEFTRI_PLAN_AUTO          0
+#define DEFTRI_PLAN_MULTIFRONTAL  1
+#define DEFTRI_PLAN_ITERATIVE     2
+int deftri_set_plan(deftri_ctx *ctx, int32_t plan);
+/* Storage of the ARAP Jacobians the iterative plan's product reads: 0 (default) fp64, 1 fp32 (the
+   C5 precision sweep: the product then applies the fp32-rounded J; b, the preconditioner, the
+   vectors and every reduction stay fp64).  Applies to the next deftri_problem_upload. */
+int deftri_set_jacobian_storage(deftri_ctx *ctx, int32_t fp32);
+typedef struct deftri_plan_info {
+    int32_t plan;              /* DEFTRI_PLAN_MULTIFRONTAL / DEFTRI_PLAN_ITERATIVE of the uploaded problem */
+    int32_t rank, nranks;
+    int32_t own_rows;          /* iterative: point rows this rank owns */
+    int64_t halo_rows;         /* iterative: rows received from other ranks per exchange */
+    int64_t local_arap_edges;  /* iterative: ARAP edges this rank evaluates (owned + halo-only) */
+    int64_t n_unknowns;
+    int32_t phase1_blocks, row_blocks;
+    double  product_bytes;     /* algorithmic bytes of one matrix-free product on this rank */
+    int32_t jacobian_fp32;
+    int32_t reserved;
+} deftri_plan_info;
+int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info);
+/* TEST ONLY (no GPU): host emulation of one product q = (H + lambda I) p with the iterative plan's
+   decomposition on this rank (deftri_dist_set_transport: rank / nranks and the callback): the rank
+   reads only its own rows of p, receives its halo rows through the callback's send / receive in the
+   device exchange's global order, all-reduces the global vertices' partials of its owned edges
+   (sum), and sums its rows' incidences.  H = sum_e J_e^T W_e J_e over the edges of `desc` with the
+   caller's per-edge Jacobians (jarap [E*18] as g2o orders an ARAP edge's vertices, jrep [R*6] 2x3,
+   jdep [D*4] point + scale) and scalar weights.  p, q [n], vertex order [T_g][scales][points]; q
+   receives this rank's point rows and the global vertices, zeros elsewhere.  stats (may be NULL):
+   own rows, halo rows, local ARAP edges, owned ARAP edges. */
+int deftri_debug_sp_product(deftri_ctx *ctx, const deftri_problem_desc *desc, const double *jarap, const double *warap,
+                            const double *jrep, const double *wrep, const double *jdep, const double *wdep,
+                            double lambda, const double *p, double *q, int64_t n, int64_t *stats);
 /* ---- simulated observations (upstream producer, host) --------------------------------------
    SLAM::setCameraPoses + getSimulatedDepthMeasurements + createKeyPoints (Modules/System/SLAM.cc:
    223-338): T1w = (I, c1), T2w = (lookAt(c2, moved[0]), c2) as Sophus SE3f (pose = the fp32 unit

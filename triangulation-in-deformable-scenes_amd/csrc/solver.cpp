@@ -23,10 +23,13 @@
 #include <string>
 #include <vector>
 
+#include <memory>
+
 #include "../../include/deftri.h"
 #include "graph_builder.h"
 #include "kernels.h"
 #include "pcg.h"
+#include "spcg.h"
 #include "symbolic.h"
 
 using namespace deftri;
@@ -161,6 +164,14 @@ struct deftri_ctx {
     int pcg_step_its = 0, pcg_step_solved = 0;   // the last PCG step (deftri_last_step_info)
     bool pcg_packed = false;                // sliced blocks repacked from the current assembly
     bool assembled = false;                 // L.hval / L.b hold the current linearization's H, b
+    // the point-sharded iterative plan (spcg.h; deftri_set_plan): when sp_on, every solve entry point
+    // runs on `sp` and no multifrontal plan exists
+    int plan_mode = DEFTRI_PLAN_AUTO;
+    int jac_fp32 = 0;                       // deftri_set_jacobian_storage
+    std::unique_ptr<SpSolver> sp;
+    bool sp_on = false;
+    SpTransport *sp_tr = nullptr;           // RCCL / callback transport of `sp` (owned)
+    int small_direct = 0;                   // PCG skipped for this problem (too small to win, see upload)
 };
 
 namespace {
@@ -207,6 +218,8 @@ void drop_trial_graph(deftri_ctx *ctx) {
 }
 
 void free_device(deftri_ctx *ctx) {
+    ctx->sp.reset();
+    ctx->sp_on = false;
     drop_trial_graph(ctx);
     for (void *p : ctx->allocs) hipFree(p);
     ctx->allocs.clear();
@@ -666,6 +679,28 @@ int dist_p2p(deftri_ctx *ctx, const std::vector<P2P> &ops) {
     return 0;
 }
 
+// the iterative plan's transport: the context's RCCL communicator or host callback
+struct CtxTransport : SpTransport {
+    deftri_ctx *ctx;
+    explicit CtxTransport(deftri_ctx *c) : ctx(c) {}
+    int allreduce(double *dev, int64_t n, int op, hipStream_t) override { return dist_allreduce(ctx, dev, n, op); }
+    int p2p(const std::vector<Op> &ops, hipStream_t) override {
+        std::vector<P2P> v;
+        v.reserve(ops.size());
+        for (const Op &o : ops) v.push_back({o.peer, o.send, o.buf, o.n});
+        return dist_p2p(ctx, v);
+    }
+};
+
+// plan kind of the next upload (deftri_set_plan)
+bool want_iterative(const deftri_ctx *ctx, const deftri_problem_desc *d) {
+    if (ctx->plan_mode == DEFTRI_PLAN_ITERATIVE) return true;
+    if (ctx->plan_mode == DEFTRI_PLAN_MULTIFRONTAL) return false;
+    if (ctx->nranks > 1) return ctx->lin_solver == DEFTRI_SOLVER_PCG;
+    const int64_t ndof = 6LL * d->n_pairs + d->n_scales + 3LL * d->n_points;
+    return d->n_pairs > 1 && ndof > 1000000;
+}
+
 // LevelHook of the factor / solve launchers: the DistPlan transfers whose parent front sits at
 // `level` — packed contribution blocks up (factor), forward-update vectors up (forward), boundary
 // solutions down (after the parent's backward level)
@@ -984,6 +1019,8 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     if (ctx->device < 0) { delete ctx; return 0; }
     hipSetDevice(ctx->device);
     free_device(ctx);
+    delete ctx->sp_tr;
+    ctx->sp_tr = nullptr;
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
     for (auto &e : ctx->sync_ev) if (e) hipEventDestroy(e);
@@ -1021,13 +1058,83 @@ int deftri_set_linear_solver(deftri_ctx *ctx, int32_t solver, double tol, int32_
     ctx->lin_solver = solver;
     ctx->pcg_tol = tol > 0 ? tol : kPcgDefaultTol;
     ctx->pcg_max_it = max_iterations > 0 ? max_iterations : 0;   // 0: the plan's cost-model budget
+    if (ctx->sp) { ctx->sp->tol = ctx->pcg_tol; ctx->sp->max_it = ctx->pcg_max_it; }
     return 0;
 }
 
 int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_t *pcg_converged) {
     if (!ctx || !pcg_iterations || !pcg_converged) return DEFTRI_E_ARG;
+    if (ctx->sp_on) {
+        *pcg_iterations = ctx->sp->step_its;
+        *pcg_converged = ctx->sp->step_solved;
+        return 0;
+    }
     *pcg_iterations = ctx->pcg_step_its;
     *pcg_converged = ctx->pcg_step_solved;
+    return 0;
+}
+
+int deftri_debug_sp_product(deftri_ctx *ctx, const deftri_problem_desc *desc, const double *jarap, const double *warap,
+                            const double *jrep, const double *wrep, const double *jdep, const double *wdep,
+                            double lambda, const double *p, double *q, int64_t n, int64_t *stats) {
+    if (!ctx || !desc || !p || !q) return DEFTRI_E_ARG;
+    int rc = validate(ctx, desc);
+    if (rc) return rc;
+    if ((desc->n_arap && (!jarap || !warap)) || (desc->n_rep && (!jrep || !wrep)) || (desc->n_depth && (!jdep || !wdep)))
+        return fail(ctx, DEFTRI_E_ARG, "missing Jacobian / weight arrays");
+    if (n != 6LL * desc->n_pairs + desc->n_scales + 3LL * desc->n_points) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
+    if (ctx->nranks > 1 && !ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "the emulation needs the callback transport");
+    SpPlanHost H;
+    std::string err;
+    if (!build_sp_plan(*desc, ctx->rank, ctx->nranks, false, H, err)) return fail(ctx, DEFTRI_E_ARG, err);
+    std::function<int(int, int, double *, int64_t)> xf = [ctx](int op, int peer, double *buf, int64_t cnt) {
+        return ctx->xfn(ctx->xuser, op, peer, buf, cnt);
+    };
+    rc = sp_emulate_product(*desc, H, jarap, warap, jrep, wrep, jdep, wdep, lambda, p, q, xf);
+    if (rc) return fail(ctx, DEFTRI_E_ARG, "transfer callback failed");
+    if (stats) {
+        stats[0] = H.hi - H.lo;
+        stats[1] = H.halo_rows;
+        stats[2] = (int64_t)H.arap_ids.size();
+        stats[3] = H.n_arap_owned;
+    }
+    return 0;
+}
+
+int deftri_set_plan(deftri_ctx *ctx, int32_t plan) {
+    if (!ctx || plan < DEFTRI_PLAN_AUTO || plan > DEFTRI_PLAN_ITERATIVE) return DEFTRI_E_ARG;
+    ctx->plan_mode = plan;
+    return 0;
+}
+
+int deftri_set_jacobian_storage(deftri_ctx *ctx, int32_t fp32) {
+    if (!ctx || fp32 < 0 || fp32 > 1) return DEFTRI_E_ARG;
+    ctx->jac_fp32 = fp32;
+    return 0;
+}
+
+int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info) {
+    if (!ctx || !info) return DEFTRI_E_ARG;
+    std::memset(info, 0, sizeof(*info));
+    info->rank = ctx->rank;
+    info->nranks = ctx->nranks;
+    if (ctx->sp_on) {
+        const SpSolver &s = *ctx->sp;
+        info->plan = DEFTRI_PLAN_ITERATIVE;
+        info->own_rows = s.own_rows();
+        info->halo_rows = s.halo_rows();
+        info->local_arap_edges = s.n_arap_local();
+        info->n_unknowns = s.ndof();
+        info->phase1_blocks = s.n_blocks();
+        info->row_blocks = s.n_row_blocks();
+        info->product_bytes = s.product_bytes();
+        info->jacobian_fp32 = s.fp32_jac;
+        return 0;
+    }
+    if (!ctx->have) return DEFTRI_E_NOPROBLEM;
+    info->plan = DEFTRI_PLAN_MULTIFRONTAL;
+    info->n_unknowns = ctx->S.ndof;
+    info->product_bytes = ctx->pcg_bytes;
     return 0;
 }
 
@@ -1076,6 +1183,7 @@ int deftri_plan_vertex_order(const deftri_ctx *ctx, int64_t *order, int64_t nv) 
 
 int deftri_dist_vertex_owner(const deftri_ctx *ctx, int32_t *owner, int64_t nv) {
     if (!ctx || !owner) return DEFTRI_E_ARG;
+    if (ctx->sp_on) return ctx->sp->vertex_owner(owner, nv);
     if (!ctx->analysed) return DEFTRI_E_NOPROBLEM;
     if (nv != ctx->S.nv) return DEFTRI_E_ARG;
     std::memcpy(owner, ctx->S.dist.vertex_owner.data(), sizeof(int32_t) * (size_t)nv);
@@ -1093,7 +1201,10 @@ int deftri_dist_owned_edges(const deftri_ctx *ctx, uint8_t *rep, uint8_t *dep, u
     return 0;
 }
 
-int64_t deftri_num_unknowns(const deftri_ctx *ctx) { return (ctx && ctx->have) ? ctx->S.ndof : -1; }
+int64_t deftri_num_unknowns(const deftri_ctx *ctx) {
+    if (ctx && ctx->sp_on) return ctx->sp->ndof();
+    return (ctx && ctx->have) ? ctx->S.ndof : -1;
+}
 
 int deftri_problem_analyse(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     if (!ctx) return DEFTRI_E_ARG;
@@ -1159,6 +1270,33 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     hipSetDevice(ctx->device);
     HIPOK(hipStreamSynchronize(ctx->st));
     KProf prof;
+    if (ctx->sp_on) {
+        int rc = ctx->sp->profile_trial(lambda, prof, ctx->prof_analytic);
+        if (rc) return fail(ctx, rc, ctx->sp->err);
+        const int its = ctx->sp->step_its;
+        int32_t n = 0;
+        for (const auto &r : prof.recs) {
+            float ms = 0;
+            hipEventElapsedTime(&ms, r.e0, r.e1);
+            int32_t k = 0;
+            for (; k < n; k++) if (std::strcmp(stats[k].name, r.name) == 0) break;
+            if (k == n) {
+                if (n >= max_stats) continue;
+                std::memset(&stats[n], 0, sizeof(stats[n]));
+                std::strncpy(stats[n].name, r.name, sizeof(stats[n].name) - 1);
+                n++;
+            }
+            stats[k].launches++;
+            stats[k].ms += ms;
+        }
+        for (int32_t k = 0; k < n; k++) {
+            if (!std::strcmp(stats[k].name, "sp_phase1")) stats[k].bytes = ctx->sp->product_bytes_phase(1) * its;
+            if (!std::strcmp(stats[k].name, "sp_phase2")) stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
+        }
+        for (hipEvent_t e : prof.pool) hipEventDestroy(e);
+        *n_stats = n;
+        return 0;
+    }
     set_profiler(&prof);
     // point-sharded: a collective (every rank profiles its part of the same trial)
     LevelHook hook = ctx->dist() ? dist_hook : nullptr;
@@ -1239,6 +1377,7 @@ int64_t deftri_sizeof(int32_t which) {
         case 4: return (int64_t)sizeof(deftri_map);
         case 5: return (int64_t)sizeof(deftri_ba_desc);
         case 6: return (int64_t)sizeof(deftri_pixels_error);
+        case 7: return (int64_t)sizeof(deftri_plan_info);
         default: return -1;
     }
 }
@@ -1249,6 +1388,23 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     hipSetDevice(ctx->device);
     int rc = validate(ctx, desc);
     if (rc) return rc;
+    if (want_iterative(ctx, desc)) {
+        // the point-sharded iterative plan: no ordering, no symbolic analysis, no factor
+        free_device(ctx);
+        ctx->plan_hash = 0;
+        ctx->analysed = false;
+        copy_host(ctx->hp, desc);
+        if (!ctx->sp_tr) ctx->sp_tr = new CtxTransport(ctx);
+        ctx->sp.reset(new SpSolver(ctx->device, ctx->st, ctx->rank, ctx->nranks, ctx->sp_tr));
+        ctx->sp->tol = ctx->pcg_tol;
+        ctx->sp->max_it = ctx->pcg_max_it;
+        ctx->sp->fp32_jac = ctx->jac_fp32;
+        rc = ctx->sp->upload(*desc);
+        if (rc) { ctx->err = ctx->sp->err; ctx->sp.reset(); return rc; }
+        ctx->sp_on = true;
+        ctx->have = true;
+        return 0;
+    }
     const uint64_t hsh = structure_hash(*desc);
     static const bool no_cache = std::getenv("DEFTRI_NO_PLAN_CACHE") != nullptr;
     if (ctx->have && ctx->analysed && hsh == ctx->plan_hash && !no_cache) {
@@ -1273,6 +1429,7 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
 
 int deftri_reset_state(deftri_ctx *ctx) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (ctx->sp_on) { int rc = ctx->sp->reset_state(); return rc ? fail(ctx, rc, ctx->sp->err) : 0; }
     DevProblem &P = ctx->P;
     HIPOK(hipMemcpyAsync(P.points, ctx->init_state[0], sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, ctx->st));
     HIPOK(hipMemcpyAsync(P.scales, ctx->init_state[1], sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, ctx->st));
@@ -1416,6 +1573,11 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     deftri_report local{};
     deftri_report &R = rep ? *rep : local;
     std::memset(&R, 0, sizeof(R));
+    if (ctx->sp_on) {
+        ctx->prof_analytic = prm->analytic_jacobians != 0;
+        int rc = ctx->sp->solve_lm(*prm, R);
+        return rc ? fail(ctx, rc, ctx->sp->err) : 0;
+    }
     R.n_unknowns = ctx->S.ndof;
     R.nnz_factor = ctx->S.nnz_factor;
     R.factor_flops = ctx->S.factor_flops;
@@ -1806,6 +1968,7 @@ int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, cons
 int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(ctx->device);
+    if (ctx->sp_on) { int rc = ctx->sp->download(points, scales, tg); return rc ? fail(ctx, rc, ctx->sp->err) : 0; }
     DevProblem &P = ctx->P;
     if (points) HIPOK(hipMemcpy(points, P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToHost));
     if (scales) HIPOK(hipMemcpy(scales, P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToHost));
@@ -1816,6 +1979,7 @@ int deftri_download(deftri_ctx *ctx, double *points, double *scales, double *tg)
 int deftri_eval_chi2(deftri_ctx *ctx, double *chi2) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(ctx->device);
+    if (ctx->sp_on) { int rc = ctx->sp->chi2(chi2); return rc ? fail(ctx, rc, ctx->sp->err) : 0; }
     eval_chi2_dev(ctx, false, true, 0);
     *chi2 = read_scal(ctx, 0);
     return 0;
@@ -1824,6 +1988,11 @@ int deftri_eval_chi2(deftri_ctx *ctx, double *chi2) {
 int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (ctx->sp_on) {
+        hipSetDevice(ctx->device);
+        int rc = ctx->sp->gradient(b, hdiag, n);
+        return rc ? fail(ctx, rc, ctx->sp->err) : 0;
+    }
     if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
     eval_chi2_dev(ctx, true, true, 0);
@@ -1847,6 +2016,7 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (ctx->sp_on) return fail(ctx, DEFTRI_E_ARG, "the iterative plan never assembles H");
     if (n != ctx->S.ndof || !x || !y) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
     double *dx = nullptr, *dy = nullptr;
@@ -1865,6 +2035,13 @@ int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int
 int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (ctx->sp_on) {
+        if (ctx->lin_solver != DEFTRI_SOLVER_PCG) return fail(ctx, DEFTRI_E_ARG, "the iterative plan has no factorization");
+        if (!rhs || !x) return fail(ctx, DEFTRI_E_ARG, "null array");
+        hipSetDevice(ctx->device);
+        int rc = ctx->sp->damped_solve(lambda, rhs, x, n);
+        return rc ? fail(ctx, rc, ctx->sp->err) : 0;
+    }
     if (n != ctx->S.ndof || !rhs || !x) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
     (void)hipGetLastError();                    // the status check below reads this call's errors only

@@ -1,0 +1,212 @@
+// spcg.h — the point-sharded matrix-free PCG plan ("iterative plan"): the LM step
+// (H + lambda I) dx = b of arapOptimization's g2o solve (reference Modules/Optimization/
+// g2oBundleAdjustment.cc:608-1008, optimizer call :959-962) for graphs of any keyframe count,
+// sharded over ranks (one GPU each) without the multifrontal analysis.
+//
+// Rows.  Every point is a row; the keyframe copies of a mesh vertex (the points an ARAP edge pairs
+// at roles (0, 1) and (2, 3), g2oBundleAdjustment.cc:871-953) form one group, groups are ordered
+// by the Morton code of their mesh-plane position (deftri_problem_desc.order_xy) and dealt to the
+// ranks in contiguous, work-balanced ranges.  The device state keeps the points in this row order;
+// dof layout [T_g 6 per pair][scales][rows 3 each].  The global vertices (T_g, depth scales) are
+// "heavy": replicated on every rank.
+//
+// Edges of a rank.  Reprojection and depth edges of its rows; ARAP edges with at least one point
+// in its rows ("local"), owned (chi2, heavy sums) by the rank of their point 0.  The points of
+// local edges on other ranks are the rank's halo.
+//
+// One product q = (H + lambda I) p, H = sum_e J_e^T W_e J_e, never assembled:
+//   phase 1 (per local ARAP edge, edge-parallel): s_e = W_e (J_e p) over the edge's 4 points and
+//            its pair's T_g; s_e stored; owned edges add J_T^T s_e into a per-block partial of
+//            their T_g; per depth edge (blocks by scale) c_e . p_row + W J_s^2 p_s into the
+//            scale's partial;
+//   phase 2 (per own row, row-parallel): q_v = lambda p_v + D_v p_v + sum_dep c_e p_s(e)
+//            + sum over its ARAP incidences J_{e,role}^T s_e, where D_v folds the row's
+//            reprojection and depth point blocks (single-point edges: camera fixed) and c_e = W J_p J_s;
+//   heavy  : q_h = (sum of its blocks' partials, all ranks) + lambda p_h.
+// No atomics; every sum has a fixed order, so a solve on a given rank count is bit-reproducible.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/deftri.h"
+#include "kernels.h"
+
+namespace deftri {
+
+constexpr int kSpBlock = 256;          // edges per phase-1 block / rows per row block
+constexpr int kSpRed = 16;             // doubles per iteration in the reduction record
+constexpr int kSpPart = 8;             // doubles per phase-1 block partial
+constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
+enum { SP_ARAP = 0, SP_DEP = 1 };
+// solve status (record word 0)
+enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4 };
+
+// the transport of a sharded solve (solver.cpp: RCCL on the solver stream, or the caller's host
+// callback); every rank issues the same calls in the same order
+struct SpTransport {
+    virtual ~SpTransport() {}
+    virtual int allreduce(double *dev, int64_t n, int op, hipStream_t st) = 0;   // op 0 sum, 1 max
+    struct Op { int peer; bool send; double *buf; int64_t n; };
+    virtual int p2p(const std::vector<Op> &ops, hipStream_t st) = 0;             // one global order
+};
+
+// host plan of one rank
+struct SpPlanHost {
+    int rank = 0, nranks = 1;
+    int32_t P = 0, Q = 0, S = 0;
+    int64_t hd = 0;                                    // heavy dofs 6Q + S
+    std::vector<int32_t> row_of_point, point_of_row;   // global row order
+    std::vector<int32_t> rank_row_begin;               // nranks + 1
+    int32_t lo = 0, hi = 0;                            // own rows
+    // local edges (global ids) in device order
+    std::vector<int32_t> arap_ids;                     // [owned (pair, row0) | halo-only (pair, row0)]
+    int32_t n_arap_owned = 0;
+    std::vector<int32_t> rep_ids, dep_ids;             // the own rows' edges, sorted by row (stable)
+    std::vector<int32_t> rot_ids;                      // rotation-table rows used, local index order
+    std::vector<int32_t> arap_rot_local;               // [2 * local arap]
+    // phase-1 blocks: (kind | owned << 8, heavy vertex (pair or scale), begin, end)
+    std::vector<int32_t> blk;                          // 4 per block
+    std::vector<int32_t> hv_blk;                       // per heavy vertex (Q + S): its partial blocks, CSR
+    std::vector<int64_t> hv_blk_off;                   // Q + S + 1
+    std::vector<int32_t> dperm;                        // local depth edges sorted by (scale, row)
+    // row CSR (own rows, local index)
+    std::vector<int64_t> inc_off;                      // nown + 1
+    std::vector<int32_t> inc;                          // local arap edge << 2 | role
+    std::vector<int32_t> rep_off, dep_off;             // nown + 1, into the local rep / dep arrays
+    // halo exchange: rows (global) sent to / received from each peer, ascending
+    std::vector<std::vector<int32_t>> send_rows, recv_rows;
+    int64_t halo_rows = 0;
+    double product_bytes = 0;                          // algorithmic bytes of phase 1 + 2 (one CG iteration)
+    double phase1_bytes = 0, phase2_bytes = 0;
+};
+// rank's plan of a validated problem; false (err) when the problem cannot be planned
+bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &out,
+                   std::string &err);
+// host emulation of one sharded product on the plan (tests; spcg_plan.cpp)
+int sp_emulate_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
+                       const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
+                       const double *p, double *q, const std::function<int(int, int, double *, int64_t)> &xfer);
+
+// device view (kernels)
+struct SpDev {
+    int32_t P = 0, Q = 0, S = 0;
+    int64_t hd = 0, ndof = 0;
+    int32_t row0 = 0, nown = 0;
+    int32_t nblk = 0, nrb = 0;                         // phase-1 blocks, row blocks
+    int32_t include_heavy = 1;                         // this rank counts the replicated heavy dofs in sums
+    const int4 *blk = nullptr;
+    const int32_t *hv_blk = nullptr;
+    const int64_t *hv_blk_off = nullptr;
+    const int32_t *apts = nullptr, *apair = nullptr;   // local ARAP edges: rows, pair
+    const double *Ja = nullptr, *Wa = nullptr, *Ea = nullptr;
+    const float *Ja32 = nullptr;                       // fp32 copy of Ja (deftri_set_jacobian_storage 1)
+    const double *Jr = nullptr, *Wr = nullptr, *Er = nullptr;
+    const double *Jd = nullptr, *Wd = nullptr, *Ed = nullptr;
+    const int32_t *dsc = nullptr, *drow = nullptr, *dperm = nullptr;
+    const int64_t *inc_off = nullptr;
+    const int32_t *inc = nullptr, *rep_off = nullptr, *dep_off = nullptr;
+    // per-LM-iteration
+    double *Hv = nullptr, *Dv = nullptr, *Mv = nullptr;   // own rows: 6 each (lower 3x3: 00 10 11 20 21 22)
+    double *cdep = nullptr, *wss = nullptr;               // per local depth edge: W J_p J_s (3), W J_s^2
+    double *hl = nullptr;                                 // [H_T lower 21 per pair | H_s per scale | b (ndof)]
+    double *b = nullptr;                                  // = hl + 21 Q + S
+    double *Mh = nullptr;                                 // heavy preconditioner: 36 per pair, 1 per scale
+    double *lpart = nullptr;                              // glin block partials [nblk][27]
+    double *mpart = nullptr;                              // row-block max diag
+    // CG
+    double *r = nullptr, *q = nullptr, *x = nullptr;
+    double2 *zp = nullptr;                                // (z, p) per dof
+    double *s = nullptr;                                  // phase-1 s_e per local ARAP edge
+    double *part = nullptr;                               // phase-1 block partials [nblk][8]
+    double *rpart = nullptr;                              // row-block partials: phase 2 p.q [nrb]; update (rz, rr) [nrb + 1][2]
+    double *upart = nullptr;
+    double *hbuf = nullptr;                               // [pq_rows, heavy sums (hd)]
+    double *red = nullptr;                                // [max_it + 2][kSpRed]: rz, rr, -, alpha
+    double *rec = nullptr;                                // [8]: status, its
+    int32_t max_it = 0;
+    double tol2 = 0;
+};
+
+// launchers (spcg.hip); `heavy_stage` of k_sp_heavy: 0 both halves (one rank), 1 sums, 2 finish
+void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st);   // rows + blocks + heavy sums (rank partial)
+void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st);   // rank max of the rows' diagonal
+void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);   // out = max(out, heavy diagonal)
+void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st);
+void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st);
+void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
+void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
+void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st);
+void sp_launch_update(const SpDev &G, int it, hipStream_t st);
+void sp_launch_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf, hipStream_t st);
+void sp_launch_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
+void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
+                          hipStream_t st);
+void sp_launch_permute_out(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
+                           hipStream_t st);
+
+// The LM solve on the iterative plan (one rank).  Owned by the C-ABI context (solver.cpp).
+class SpSolver {
+ public:
+    SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr);
+    ~SpSolver();
+    int upload(const deftri_problem_desc &d);
+    int solve_lm(const deftri_lm_params &prm, deftri_report &R);
+    int download(double *points, double *scales, double *tg);
+    int reset_state();
+    int chi2(double *out);
+    int gradient(double *b, double *hdiag, int64_t n);
+    int damped_solve(double lambda, const double *rhs, double *x, int64_t n);
+    int profile_trial(double lambda, KProf &prof, bool analytic);
+    int vertex_owner(int32_t *owner, int64_t nv) const;
+    int64_t ndof() const { return G.ndof; }
+    double product_bytes() const { return H.product_bytes; }
+    double product_bytes_phase(int k) const { return k == 1 ? H.phase1_bytes : H.phase2_bytes; }
+    int64_t halo_rows() const { return H.halo_rows; }
+    int32_t own_rows() const { return H.hi - H.lo; }
+    int32_t n_blocks() const { return G.nblk; }
+    int32_t n_row_blocks() const { return G.nrb; }
+    int32_t n_arap_local() const { return (int32_t)H.arap_ids.size(); }
+    // settings
+    double tol = 1e-12;
+    int max_it = 0;                  // 0: the default budget
+    int fp32_jac = 0;                // ARAP Jacobians stored in fp32 for the product
+    int last_its = 8;
+    int step_its = 0, step_solved = 0;
+    std::string err;
+
+ private:
+    int dev_ = 0;
+    hipStream_t st_ = nullptr;
+    int rank_ = 0, nranks_ = 1;
+    SpTransport *tr_ = nullptr;
+    SpPlanHost H;
+    SpDev G;
+    DevProblem P;
+    std::vector<void *> allocs_;
+    std::vector<double *> init_;      // initial state (points plan order, scales, tg)
+    double *d_scal = nullptr, *d_part = nullptr, *d_dx0 = nullptr, *d_tmp = nullptr;
+    int *d_flag = nullptr;
+    double *hpin = nullptr;
+    int *ipin = nullptr;
+    int32_t *d_send_rows = nullptr, *d_recv_rows = nullptr;
+    double *d_xbuf = nullptr;
+    std::vector<int64_t> send_off_, recv_off_;   // per peer, into the row lists (and x 6 per row)
+    int32_t *d_row_of_point = nullptr;
+    bool have_ = false;
+    template <class T> int alloc(T **p, int64_t n);
+    template <class T> int put(T **p, const std::vector<T> &v);
+    int fail(int code, const std::string &m) { err = m; return code; }
+    int budget() const;
+    int lin_iteration(bool analytic, bool want_max, bool &ok);
+    int eval_chi2(bool analytic, int slot, const SumJob *extra);
+    void cg_chain(double lambda, int from, int to);
+    int cg_tail(int n);
+    int halo(int width, double *vec, bool zp);
+    int pcg_solve(double lambda, const double *rhs, bool &solved, int &its);
+};
+
+}  // namespace deftri

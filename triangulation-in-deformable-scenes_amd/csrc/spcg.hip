@@ -1,0 +1,770 @@
+// spcg.hip — gfx950 kernels of the point-sharded matrix-free PCG plan (spcg.h).
+//
+// Replaces (reference / g2o): buildSystem + the linear solve of OptimizationAlgorithmLevenberg::solve
+// (BlockSolverX + LinearSolverEigen SimplicialLDLT, built at g2oBundleAdjustment.cc:619-628, run by
+// optimize() at :959-962) with block-Jacobi PCG on an operator that is never assembled.
+//
+// Per LM iteration (after the edges are linearized, kernels.hip k_lin_*):
+//   k_sp_glin_rows    own rows: the row's 3x3 diagonal block of H (incidences + folded single-point
+//                     edges), D_v (its reprojection / depth part), b_v, c_e = W J_p J_s per depth edge
+//   k_sp_glin_blocks  per phase-1 block: the heavy vertices' H / b partials (owned edges only)
+//   k_sp_glin_heavy   heavy H / b from the block partials (rank sums; all-reduced by the host)
+// Per CG iteration it (5 launches on one rank; the sharded solve splits k_sp_heavy and adds two
+// all-reduces and the halo exchange of the boundary rows' (z, p)):
+//   k_sp_dots    (r.z, r.r) from the previous update's row-block partials
+//   k_sp_phase1  per local ARAP edge s_e = W_e J_e p, per block J_T^T s (T_g) / depth-scale sums
+//   k_sp_phase2  per own row q_v (p formed from (z, p_prev) on the fly and stored), partial p.q
+//   k_sp_heavy   heavy q from the block partials, p.q, alpha (breakdown -> status)
+//   k_sp_update  x += alpha p, r -= alpha q, z = M r, partial (r.z, r.r)
+// Each kernel first tests the iteration's state from the reduced scalars (converged: ||r||^2 <=
+// tol^2 ||b||^2 on the recurrence residual; budget; breakdown) and returns at once past the end, so
+// the host may queue more iterations than a solve needs.  No atomics; fixed-order sums.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "spcg.h"
+
+namespace deftri {
+namespace sp {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// fixed-order sum of a 256-thread workgroup: wave butterflies, then (w0 + w1) + (w2 + w3)
+__device__ __forceinline__ double block_sum(double v, double *red4) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) red4[w] = v;
+    __syncthreads();
+    const double s = (red4[0] + red4[1]) + (red4[2] + red4[3]);
+    __syncthreads();
+    return s;
+}
+
+__device__ __forceinline__ double pval(const double2 *__restrict__ zp, double beta, int64_t i) {
+    const double2 v = zp[i];
+    return __fma_rn(beta, v.y, v.x);
+}
+
+// the state of CG iteration `it`: 0 run it (beta set), 1 converged before it, 2 stopped (budget, or a
+// status already recorded: breakdown, bad block, converged earlier)
+__device__ __forceinline__ int it_state(const SpDev &G, int it, double &beta) {
+    beta = 0.0;
+    if (G.rec[0] != 0.0) return 2;
+    const double *rk = G.red + (int64_t)kSpRed * it;
+    if (rk[1] <= G.tol2 * G.red[1]) return 1;
+    if (it >= G.max_it) return 2;
+    if (it > 0) beta = rk[0] / G.red[(int64_t)kSpRed * (it - 1)];
+    return 0;
+}
+
+__device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q ? 6 * h : 6 * G.Q + (h - G.Q); }
+
+template <class JT>
+__device__ __forceinline__ void load_j18(const JT *__restrict__ J, double *o);
+template <>
+__device__ __forceinline__ void load_j18<double>(const double *__restrict__ J, double *o) {
+    const double2 *J2 = reinterpret_cast<const double2 *>(J);
+#pragma unroll
+    for (int k = 0; k < 9; k++) { const double2 t = J2[k]; o[2 * k] = t.x; o[2 * k + 1] = t.y; }
+}
+template <>
+__device__ __forceinline__ void load_j18<float>(const float *__restrict__ J, double *o) {
+    const float2 *J2 = reinterpret_cast<const float2 *>(J);
+#pragma unroll
+    for (int k = 0; k < 9; k++) { const float2 t = J2[k]; o[2 * k] = t.x; o[2 * k + 1] = t.y; }
+}
+
+// ---- per LM iteration -----------------------------------------------------------------------------
+__device__ __forceinline__ int tri3(int a, int b) { return a * (a + 1) / 2 + b; }   // a >= b
+__device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; }
+
+__global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G) {
+    __shared__ double red4[4];
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    double mx = 0.0;
+    if (l < G.nown) {
+        double D[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
+        for (int j = G.rep_off[l]; j < G.rep_off[l + 1]; j++) {     // reprojection: 2 x 3, W scalar
+            const double *J = G.Jr + 6 * (int64_t)j;
+            const double w = G.Wr[j];
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const double er = G.Er[2 * (int64_t)j + r];
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const double ja = J[3 * r + a] * w;
+#pragma unroll
+                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[3 * r + c];
+                    bb[a] -= J[3 * r + a] * (w * er);
+                }
+            }
+        }
+        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
+            const double *J = G.Jd + 4 * (int64_t)j;
+            const double w = G.Wd[j], er = G.Ed[j];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double ja = J[a] * w;
+#pragma unroll
+                for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
+                bb[a] -= J[a] * (w * er);
+                G.cdep[3 * (int64_t)j + a] = ja * J[3];
+            }
+            G.wss[j] = (J[3] * w) * J[3];
+        }
+        double H[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) H[k] = D[k];
+        for (int64_t k = G.inc_off[l]; k < G.inc_off[l + 1]; k++) {  // ARAP incidences
+            const int v = G.inc[k];
+            const int64_t le = v >> 2;
+            const double *J = G.Ja + 18 * le + 3 * (v & 3);
+            const double w = G.Wa[le], er = G.Ea[le];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double ja = J[a] * w;
+#pragma unroll
+                for (int c = 0; c <= a; c++) H[tri3(a, c)] += ja * J[c];
+                bb[a] -= J[a] * (w * er);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) { G.Hv[6 * (int64_t)l + k] = H[k]; G.Dv[6 * (int64_t)l + k] = D[k]; }
+        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+#pragma unroll
+        for (int a = 0; a < 3; a++) G.b[o + a] = bb[a];
+        mx = fmax(fabs(H[0]), fmax(fabs(H[2]), fabs(H[5])));
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) G.mpart[blockIdx.x] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+}
+
+// heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1)
+__global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
+    __shared__ double red[kSpLin][4];
+    const int4 d = G.blk[blockIdx.x];
+    const int kind = d.x & 0xff, owned = d.x >> 8;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = d.z + threadIdx.x;
+    double *out = G.lpart + (int64_t)kSpLin * blockIdx.x;
+    if (kind == SP_ARAP) {
+        if (!owned) return;
+        double a[kSpLin];
+#pragma unroll
+        for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
+        if (i < d.w) {
+            const double *J = G.Ja + 18 * (int64_t)i + 12;
+            const double wv = G.Wa[i], er = G.Ea[i];
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const double jr = J[r] * wv;
+#pragma unroll
+                for (int c = 0; c <= r; c++) a[tri6(r, c)] += jr * J[c];
+                a[21 + r] -= J[r] * (wv * er);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSpLin; k++) {
+            const double v = wave_sum(a[k]);
+            if (lane == 0) red[k][w] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < kSpLin) {
+            const int k = threadIdx.x;
+            out[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+        }
+    } else {
+        double h = 0.0, bs = 0.0;
+        if (i < d.w) {
+            const int le = G.dperm[i];
+            const double js = G.Jd[4 * (int64_t)le + 3];
+            h = G.wss[le];
+            bs = -js * (G.Wd[le] * G.Ed[le]);
+        }
+        h = wave_sum(h);
+        bs = wave_sum(bs);
+        if (lane == 0) { red[0][w] = h; red[1][w] = bs; }
+        __syncthreads();
+        if (threadIdx.x < 2) {
+            const int k = threadIdx.x;
+            out[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+        }
+    }
+}
+
+// heavy H / b (rank sums): one wave per heavy vertex at a time, its blocks' partials in block order
+__global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int h = w; h < G.Q + G.S; h += 4) {
+        const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+        if (h < G.Q) {
+            double a[kSpLin];
+#pragma unroll
+            for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
+            for (int64_t k = k0 + lane; k < k1; k += 64) {
+                const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
+#pragma unroll
+                for (int q = 0; q < kSpLin; q++) a[q] += p[q];
+            }
+#pragma unroll
+            for (int q = 0; q < kSpLin; q++) {
+                const double v = wave_sum(a[q]);
+                if (lane == 0) {
+                    if (q < 21) G.hl[21 * (int64_t)h + q] = v;
+                    else G.b[6 * (int64_t)h + q - 21] = v;
+                }
+            }
+        } else {
+            double a0 = 0.0, a1 = 0.0;
+            for (int64_t k = k0 + lane; k < k1; k += 64) {
+                const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
+                a0 += p[0];
+                a1 += p[1];
+            }
+            a0 = wave_sum(a0);
+            a1 = wave_sum(a1);
+            if (lane == 0) {
+                G.hl[21 * (int64_t)G.Q + (h - G.Q)] = a0;
+                G.b[6 * (int64_t)G.Q + (h - G.Q)] = a1;
+            }
+        }
+    }
+}
+
+// rank max of the rows' diagonal (stage 0), or that (all-reduced) combined with the heavy diagonal
+__global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, int stage) {
+    __shared__ double red4[4];
+    double m = 0.0;
+    if (stage == 0) {
+        for (int i = threadIdx.x; i < G.nrb; i += 256) m = fmax(m, G.mpart[i]);
+    } else {
+        for (int h = threadIdx.x; h < G.Q; h += 256)
+#pragma unroll
+            for (int a = 0; a < 6; a++) m = fmax(m, fabs(G.hl[21 * (int64_t)h + tri6(a, a)]));
+        for (int s = threadIdx.x; s < G.S; s += 256) m = fmax(m, fabs(G.hl[21 * (int64_t)G.Q + s]));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double v = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+        out[0] = stage == 0 ? v : fmax(out[0], v);
+    }
+}
+
+__global__ void k_sp_cvt_j(const double *__restrict__ J, float *__restrict__ J32, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) J32[i] = (float)J[i];
+}
+
+// ---- CG ---------------------------------------------------------------------------------------------
+// (3x3 SPD, lower packed) -> inverse (lower packed) through its Cholesky factor; false if not SPD
+__device__ __forceinline__ bool inv3(const double *A, double lam, double *M) {
+    const double a00 = A[0] + lam, a10 = A[1], a11 = A[2] + lam, a20 = A[3], a21 = A[4], a22 = A[5] + lam;
+    if (!(a00 > 0.0)) return false;
+    const double l00 = sqrt(a00), l10 = a10 / l00, l20 = a20 / l00;
+    const double d1 = a11 - l10 * l10;
+    if (!(d1 > 0.0)) return false;
+    const double l11 = sqrt(d1), l21 = (a21 - l20 * l10) / l11;
+    const double d2 = a22 - l20 * l20 - l21 * l21;
+    if (!(d2 > 0.0)) return false;
+    const double l22 = sqrt(d2);
+    // L^-1 (lower)
+    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+    const double i10 = -l10 * i00 * i11;
+    const double i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    // M = L^-T L^-1
+    M[0] = i00 * i00 + i10 * i10 + i20 * i20;
+    M[1] = i11 * i10 + i21 * i20;
+    M[2] = i11 * i11 + i21 * i21;
+    M[3] = i22 * i20;
+    M[4] = i22 * i21;
+    M[5] = i22 * i22;
+    return true;
+}
+
+__device__ __forceinline__ void mul3(const double *M, const double r[3], double z[3]) {
+    z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
+    z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
+    z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
+}
+
+// 6x6 SPD (lower packed, + lam on the diagonal) -> full inverse (row-major 36); false if not SPD
+__device__ bool inv6(const double *Hl, double lam, double *Mo) {
+    double L[36];
+    for (int i = 0; i < 6; i++)
+        for (int j = 0; j < 6; j++) L[i * 6 + j] = j <= i ? Hl[tri6(i, j)] + (i == j ? lam : 0.0) : 0.0;
+    for (int j = 0; j < 6; j++) {
+        double s = L[j * 6 + j];
+        for (int k = 0; k < j; k++) s -= L[j * 6 + k] * L[j * 6 + k];
+        if (!(s > 0.0)) return false;
+        s = sqrt(s);
+        L[j * 6 + j] = s;
+        for (int i = j + 1; i < 6; i++) {
+            double t = L[i * 6 + j];
+            for (int k = 0; k < j; k++) t -= L[i * 6 + k] * L[j * 6 + k];
+            L[i * 6 + j] = t / s;
+        }
+    }
+    for (int c = 0; c < 6; c++) {
+        double y[6];
+        for (int i = 0; i < 6; i++) {
+            double t = i == c ? 1.0 : 0.0;
+            for (int k = 0; k < i; k++) t -= L[i * 6 + k] * y[k];
+            y[i] = t / L[i * 6 + i];
+        }
+        for (int i = 5; i >= 0; i--) {
+            double t = y[i];
+            for (int k = i + 1; k < 6; k++) t -= L[k * 6 + i] * y[k];
+            y[i] = t / L[i * 6 + i];
+        }
+        for (int i = 0; i < 6; i++) Mo[i * 6 + c] = y[i];
+    }
+    return true;
+}
+
+__device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    if (lane == 0) { red[0][w] = a0; red[1][w] = a1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        out[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    }
+}
+
+// setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
+// partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
+__global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
+    __shared__ double red[2][4];
+    double rz = 0.0, rr = 0.0;
+    if ((int)blockIdx.x < G.nrb) {
+        const int l = blockIdx.x * 256 + threadIdx.x;
+        if (l < G.nown) {
+            double M[6];
+            if (!inv3(G.Hv + 6 * (int64_t)l, lam, M)) {
+                G.rec[0] = kSpBadBlock;
+#pragma unroll
+                for (int k = 0; k < 6; k++) M[k] = 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < 6; k++) G.Mv[6 * (int64_t)l + k] = M[k];
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+            double r[3], z[3];
+#pragma unroll
+            for (int a = 0; a < 3; a++) r[a] = rhs[o + a];
+            mul3(M, r, z);
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                G.r[o + a] = r[a];
+                G.zp[o + a] = make_double2(z[a], 0.0);
+                G.x[o + a] = 0.0;
+                rz += r[a] * z[a];
+                rr += r[a] * r[a];
+            }
+        }
+    } else {
+        for (int h = threadIdx.x; h < G.Q + G.S; h += 256) {
+            const int o = heavy_dof(G, h);
+            if (h < G.Q) {
+                double *M = G.Mh + 36 * (int64_t)h;
+                if (!inv6(G.hl + 21 * (int64_t)h, lam, M)) {
+                    G.rec[0] = kSpBadBlock;
+                    for (int k = 0; k < 36; k++) M[k] = 0.0;
+                }
+                double r[6];
+                for (int a = 0; a < 6; a++) r[a] = rhs[o + a];
+                for (int a = 0; a < 6; a++) {
+                    double z = 0.0;
+                    for (int c = 0; c < 6; c++) z += M[a * 6 + c] * r[c];
+                    G.r[o + a] = r[a];
+                    G.zp[o + a] = make_double2(z, 0.0);
+                    G.x[o + a] = 0.0;
+                    rz += r[a] * z;
+                    rr += r[a] * r[a];
+                }
+            } else {
+                const double a = G.hl[21 * (int64_t)G.Q + (h - G.Q)] + lam;
+                double m = 0.0;
+                if (!(a > 0.0)) G.rec[0] = kSpBadBlock;
+                else m = 1.0 / a;
+                G.Mh[36 * (int64_t)G.Q + (h - G.Q)] = m;
+                const double r = rhs[o], z = m * r;
+                G.r[o] = r;
+                G.zp[o] = make_double2(z, 0.0);
+                G.x[o] = 0.0;
+                rz += r * z;
+                rr += r * r;
+            }
+        }
+        if (!G.include_heavy) rz = rr = 0.0;
+    }
+    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
+}
+
+// (r.z, r.r) of iteration it from the previous update's (or the setup's) partials, in order
+__global__ void __launch_bounds__(256) k_sp_dots(int it, const SpDev G) {
+    __shared__ double red[2][4];
+    if (G.rec[0] != 0.0) return;
+    double a0 = 0.0, a1 = 0.0;
+    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += G.upart[2 * i]; a1 += G.upart[2 * i + 1]; }
+    pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
+}
+
+template <class JT>
+__global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const JT *__restrict__ Jarap) {
+    __shared__ double red[6][4];
+    double beta;
+    if (it_state(G, it, beta)) return;
+    const int4 d = G.blk[blockIdx.x];
+    const int kind = d.x & 0xff, owned = d.x >> 8;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = d.z + threadIdx.x;
+    double *out = G.part + (int64_t)kSpPart * blockIdx.x;
+    if (kind == SP_ARAP) {
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        if (i < d.w) {
+            const int4 rw = reinterpret_cast<const int4 *>(G.apts)[i];
+            double J[18];
+            load_j18<JT>(Jarap + 18 * (int64_t)i, J);
+            const int rows[4] = {rw.x, rw.y, rw.z, rw.w};
+            double t = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int64_t o = G.hd + 3 * (int64_t)rows[k];
+#pragma unroll
+                for (int c = 0; c < 3; c++) t += J[3 * k + c] * pval(G.zp, beta, o + c);
+            }
+            const int64_t oT = 6 * (int64_t)d.y;
+#pragma unroll
+            for (int c = 0; c < 6; c++) t += J[12 + c] * pval(G.zp, beta, oT + c);
+            const double s = G.Wa[i] * t;
+            G.s[i] = s;
+            if (owned)
+#pragma unroll
+                for (int c = 0; c < 6; c++) acc[c] = J[12 + c] * s;
+        }
+        if (!owned) return;
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+            const double v = wave_sum(acc[c]);
+            if (lane == 0) red[c][w] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            const int c = threadIdx.x;
+            out[c] = (red[c][0] + red[c][1]) + (red[c][2] + red[c][3]);
+        }
+    } else {
+        double t = 0.0;
+        if (i < d.w) {
+            const int le = G.dperm[i];
+            const int64_t o = G.hd + 3 * (int64_t)G.drow[le];
+            const double *c = G.cdep + 3 * (int64_t)le;
+            t = (c[0] * pval(G.zp, beta, o) + c[1] * pval(G.zp, beta, o + 1)) + c[2] * pval(G.zp, beta, o + 2);
+            t += G.wss[le] * pval(G.zp, beta, 6 * (int64_t)G.Q + d.y);
+        }
+        t = wave_sum(t);
+        if (lane == 0) red[0][w] = t;
+        __syncthreads();
+        if (threadIdx.x == 0) out[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    }
+}
+
+template <class JT>
+__global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ Jarap) {
+    __shared__ double red4[4];
+    double beta;
+    if (it_state(G, it, beta)) return;
+    const int l = blockIdx.x * 256 + threadIdx.x;
+    double pq = 0.0;
+    if (l < G.nown) {
+        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+        double p[3], q[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const double2 v = G.zp[o + c];
+            p[c] = __fma_rn(beta, v.y, v.x);
+            G.zp[o + c] = make_double2(v.x, p[c]);
+        }
+        const double *D = G.Dv + 6 * (int64_t)l;
+        q[0] = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
+        q[1] = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
+        q[2] = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+        const int64_t os = 6 * (int64_t)G.Q;
+        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {
+            const double ps = pval(G.zp, beta, os + G.dsc[j]);
+            const double *c = G.cdep + 3 * (int64_t)j;
+#pragma unroll
+            for (int a = 0; a < 3; a++) q[a] += c[a] * ps;
+        }
+        const int64_t k0 = G.inc_off[l], k1 = G.inc_off[l + 1];
+        int64_t k = k0;
+        // four incidences per step: their indices, then their s and J loads, then the adds in order
+        for (; k + 4 <= k1; k += 4) {
+            int v[4];
+            double s[4], J[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = G.inc[k + u];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int64_t le = v[u] >> 2;
+                s[u] = G.s[le];
+                const JT *Jp = Jarap + 18 * le + 3 * (v[u] & 3);
+#pragma unroll
+                for (int a = 0; a < 3; a++) J[u][a] = Jp[a];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int a = 0; a < 3; a++) q[a] += J[u][a] * s[u];
+        }
+        for (; k < k1; k++) {
+            const int v = G.inc[k];
+            const int64_t le = v >> 2;
+            const double s = G.s[le];
+            const JT *Jp = Jarap + 18 * le + 3 * (v & 3);
+#pragma unroll
+            for (int a = 0; a < 3; a++) q[a] += (double)Jp[a] * s;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            G.q[o + c] = q[c];
+            pq += p[c] * q[c];
+        }
+    }
+    const double s = block_sum(pq, red4);
+    if (threadIdx.x == 0) G.rpart[blockIdx.x] = s;
+}
+
+// stage 0 (one rank): sums + finish; 1: the rank's sums into hbuf (all-reduced next); 2: finish;
+// 3: only the state of iteration it into the record (the tail of a queued chunk)
+__global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double lam, int stage) {
+    __shared__ double red4[4];
+    double beta;
+    const int st = it_state(G, it, beta);
+    if (st || stage == 3) {
+        if (st && stage != 2 && threadIdx.x == 0 && G.rec[0] == 0.0) {
+            G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
+            G.rec[1] = it;
+        }
+        return;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (stage != 2) {
+        double a = 0.0;
+        for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
+        const double pq_rows = block_sum(a, red4);
+        for (int h = w; h < G.Q + G.S; h += 4) {
+            const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+            const int dim = h < G.Q ? 6 : 1;
+            double acc[6] = {0, 0, 0, 0, 0, 0};
+            for (int64_t k = k0 + lane; k < k1; k += 64) {
+                const double *p = G.part + (int64_t)kSpPart * G.hv_blk[k];
+#pragma unroll
+                for (int c = 0; c < 6; c++)
+                    if (c < dim) acc[c] += p[c];
+            }
+            const int o = heavy_dof(G, h);
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                if (c < dim) {
+                    const double v = wave_sum(acc[c]);
+                    if (lane == 0) G.hbuf[1 + o + c] = v;
+                }
+            }
+        }
+        if (threadIdx.x == 0) G.hbuf[0] = pq_rows;
+        if (stage == 1) return;
+        __syncthreads();
+    }
+    double pqh = 0.0;
+    for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
+        const double2 v = G.zp[dd];
+        const double p = __fma_rn(beta, v.y, v.x);
+        const double qh = G.hbuf[1 + dd] + lam * p;
+        G.q[dd] = qh;
+        G.zp[dd] = make_double2(v.x, p);
+        pqh += p * qh;
+    }
+    pqh = block_sum(pqh, red4);
+    if (threadIdx.x == 0) {
+        const double pq = G.hbuf[0] + pqh;
+        const double alpha = G.red[(int64_t)kSpRed * it] / pq;
+        if (!(pq > 0.0) || !isfinite(alpha)) { G.rec[0] = kSpBreakdown; G.rec[1] = it; }
+        G.red[(int64_t)kSpRed * it + 3] = alpha;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
+    __shared__ double red[2][4];
+    if (G.rec[0] != 0.0) return;
+    const double alpha = G.red[(int64_t)kSpRed * it + 3];
+    double rz = 0.0, rr = 0.0;
+    if ((int)blockIdx.x < G.nrb) {
+        const int l = blockIdx.x * 256 + threadIdx.x;
+        if (l < G.nown) {
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+            double M[6], r[3], z[3], p[3];
+#pragma unroll
+            for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                p[a] = G.zp[o + a].y;
+                G.x[o + a] += alpha * p[a];
+                r[a] = G.r[o + a] - alpha * G.q[o + a];
+                G.r[o + a] = r[a];
+            }
+            mul3(M, r, z);
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                G.zp[o + a] = make_double2(z[a], p[a]);
+                rz += r[a] * z[a];
+                rr += r[a] * r[a];
+            }
+        }
+    } else {
+        for (int h = threadIdx.x; h < G.Q + G.S; h += 256) {
+            const int o = heavy_dof(G, h);
+            const int dim = h < G.Q ? 6 : 1;
+            double r[6], p[6];
+            for (int a = 0; a < dim; a++) {
+                p[a] = G.zp[o + a].y;
+                G.x[o + a] += alpha * p[a];
+                r[a] = G.r[o + a] - alpha * G.q[o + a];
+                G.r[o + a] = r[a];
+            }
+            const double *M = h < G.Q ? G.Mh + 36 * (int64_t)h : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+            for (int a = 0; a < dim; a++) {
+                double z = 0.0;
+                for (int c = 0; c < dim; c++) z += M[a * dim + c] * r[c];
+                G.zp[o + a] = make_double2(z, p[a]);
+                rz += r[a] * z;
+                rr += r[a] * r[a];
+            }
+        }
+        if (!G.include_heavy) rz = rr = 0.0;
+    }
+    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
+}
+
+// halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
+__global__ void k_sp_pack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ src,
+                          double *__restrict__ buf) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)n * width) return;
+    const int64_t i = t / width, c = t % width;
+    buf[t] = src[base + (int64_t)width * rows[i] + c];
+}
+
+__global__ void k_sp_unpack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ buf,
+                            double *__restrict__ dst) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)n * width) return;
+    const int64_t i = t / width, c = t % width;
+    dst[base + (int64_t)width * rows[i] + c] = buf[t];
+}
+
+// problem order [heavy][points by id] <-> plan order [heavy][rows]
+__global__ void k_sp_permute(int32_t P, int64_t hd, const int32_t *__restrict__ row_of_point, const double *__restrict__ src,
+                             double *__restrict__ dst, int to_plan) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < hd) { dst[t] = src[t]; return; }
+    const int64_t u = t - hd;
+    if (u >= 3 * (int64_t)P) return;
+    const int64_t pt = u / 3, c = u % 3;
+    const int64_t row = row_of_point[pt];
+    if (to_plan) dst[hd + 3 * row + c] = src[hd + 3 * pt + c];
+    else dst[hd + 3 * pt + c] = src[hd + 3 * row + c];
+}
+
+}  // namespace sp
+
+static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64_t>((n + bs - 1) / bs, 1); }
+
+#define SPL(NAME, KER, GRID, ...)                                          \
+    do {                                                                   \
+        hipEvent_t e0_ = prof_begin(st);                                   \
+        hipLaunchKernelGGL(KER, dim3(GRID), dim3(256), 0, st, __VA_ARGS__); \
+        prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                    \
+    } while (0)
+
+void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
+    (void)fp32;
+    SPL("sp_glin_rows", sp::k_sp_glin_rows, std::max(G.nrb, 1), G);
+    if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
+    if (G.Q + G.S > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, 1, G);
+}
+
+void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st) {
+    SPL("sp_maxdiag", sp::k_sp_maxdiag, 1, G, out, 0);
+}
+
+void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st) {
+    SPL("sp_maxdiag", sp::k_sp_maxdiag, 1, G, out, 1);
+}
+
+void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st) {
+    if (n > 0) SPL("sp_cvt_j", sp::k_sp_cvt_j, nblk(n, 256), J, J32, n);
+}
+
+void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st) {
+    SPL("sp_setup", sp::k_sp_setup, G.nrb + 1, G, rhs, lambda);
+}
+
+void sp_launch_dots(const SpDev &G, int it, hipStream_t st) {
+    SPL("sp_dots", sp::k_sp_dots, 1, it, G);
+}
+
+void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st) {
+    if (G.nblk > 0) {
+        if (fp32) SPL("sp_phase1", sp::k_sp_phase1<float>, G.nblk, it, G, G.Ja32);
+        else SPL("sp_phase1", sp::k_sp_phase1<double>, G.nblk, it, G, G.Ja);
+    }
+    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, std::max(G.nrb, 1), it, G, lambda, G.Ja32);
+    else SPL("sp_phase2", sp::k_sp_phase2<double>, std::max(G.nrb, 1), it, G, lambda, G.Ja);
+}
+
+void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {
+    SPL("sp_heavy", sp::k_sp_heavy, 1, it, G, lambda, stage);
+}
+
+void sp_launch_update(const SpDev &G, int it, hipStream_t st) {
+    SPL("sp_update", sp::k_sp_update, G.nrb + 1, it, G);
+}
+
+void sp_launch_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf, hipStream_t st) {
+    if (n > 0) SPL("sp_pack", sp::k_sp_pack, nblk((int64_t)n * width, 256), n, rows, width, base, src, buf);
+}
+
+void sp_launch_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st) {
+    if (n > 0) SPL("sp_unpack", sp::k_sp_unpack, nblk((int64_t)n * width, 256), n, rows, width, base, buf, dst);
+}
+
+void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
+                          hipStream_t st) {
+    SPL("sp_permute", sp::k_sp_permute, nblk(hd + 3 * (int64_t)P, 256), P, hd, row_of_point, src, dst, 1);
+}
+
+void sp_launch_permute_out(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
+                           hipStream_t st) {
+    SPL("sp_permute", sp::k_sp_permute, nblk(hd + 3 * (int64_t)P, 256), P, hd, row_of_point, src, dst, 0);
+}
+
+}  // namespace deftri

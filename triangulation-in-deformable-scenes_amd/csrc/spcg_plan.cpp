@@ -1,0 +1,373 @@
+// spcg_plan.cpp — host plan of the point-sharded matrix-free PCG (spcg.h) for one rank.
+//
+// Input: the flattened graph arapOptimization builds (g2oBundleAdjustment.cc:640-953: per KF pair
+// its reprojection / depth edges and the directed ARAP edges (p1_i, p2_i, p1_j, p2_j, T_g)).  All
+// passes are O(E + P) counting sorts and scans, so a 500k x 8-keyframe graph (84M ARAP edges,
+// SURVEY §8d C4) plans in seconds; nothing here depends on a fill-reducing ordering.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <numeric>
+
+#include "spcg.h"
+
+namespace deftri {
+
+namespace {
+
+// stable counting sort of `ids` by key(id) in [0, nkeys)
+template <class Key>
+void counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
+    std::vector<int64_t> cnt((size_t)nkeys + 1, 0);
+    for (int32_t i : ids) cnt[(size_t)key(i) + 1]++;
+    for (int64_t k = 0; k < nkeys; k++) cnt[k + 1] += cnt[k];
+    std::vector<int32_t> out(ids.size());
+    for (int32_t i : ids) out[(size_t)cnt[(size_t)key(i)]++] = i;
+    ids.swap(out);
+}
+
+inline uint64_t spread21(uint64_t v) {       // bits 0..20 -> every third bit
+    v &= 0x1fffff;
+    v = (v | v << 32) & 0x1f00000000ffffULL;
+    v = (v | v << 16) & 0x1f0000ff0000ffULL;
+    v = (v | v << 8) & 0x100f00f00f00f00fULL;
+    v = (v | v << 4) & 0x10c30c30c30c30c3ULL;
+    v = (v | v << 2) & 0x1249249249249249ULL;
+    return v;
+}
+
+}  // namespace
+
+bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &H,
+                   std::string &err) {
+    H = SpPlanHost();
+    if (nranks < 1 || rank < 0 || rank >= nranks) { err = "bad rank"; return false; }
+    H.rank = rank;
+    H.nranks = nranks;
+    const int32_t P = d.n_points, Q = d.n_pairs, S = d.n_scales;
+    const int64_t E = d.n_arap, R = d.n_rep, D = d.n_depth;
+    H.P = P; H.Q = Q; H.S = S;
+    H.hd = 6 * (int64_t)Q + S;
+    if (E >= (1LL << 29)) { err = "more than 2^29 ARAP edges"; return false; }
+    const int32_t *ap = d.arap_pts;
+
+    // 1. keyframe-copy groups: union-find over the ARAP edges' (p1_i, p2_i) and (p1_j, p2_j)
+    std::vector<int32_t> par(P);
+    std::iota(par.begin(), par.end(), 0);
+    auto find = [&](int32_t a) {
+        while (par[a] != a) { par[a] = par[par[a]]; a = par[a]; }
+        return a;
+    };
+    auto unite = [&](int32_t a, int32_t b) {
+        a = find(a); b = find(b);
+        if (a != b) { if (a < b) par[b] = a; else par[a] = b; }   // root = smallest point id
+    };
+    for (int64_t e = 0; e < E; e++) {
+        unite(ap[4 * e], ap[4 * e + 1]);
+        unite(ap[4 * e + 2], ap[4 * e + 3]);
+    }
+    std::vector<int32_t> gid(P, -1), grep;   // group of each point; representative (smallest id) per group
+    for (int32_t p = 0; p < P; p++) {
+        const int32_t r = find(p);
+        if (gid[r] < 0) { gid[r] = (int32_t)grep.size(); grep.push_back(r); }
+        gid[p] = gid[r];
+    }
+    const int32_t ng = (int32_t)grep.size();
+
+    // 2. groups in Morton order of the representative's mesh-plane position
+    auto xy = [&](int32_t p, int c) { return d.order_xy ? d.order_xy[2 * (int64_t)p + c] : d.points[3 * (int64_t)p + c]; };
+    double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
+    for (int32_t g = 0; g < ng; g++)
+        for (int c = 0; c < 2; c++) {
+            const double v = xy(grep[g], c);
+            if (std::isfinite(v)) { lo[c] = std::min(lo[c], v); hi[c] = std::max(hi[c], v); }
+        }
+    std::vector<uint64_t> key(ng);
+    for (int32_t g = 0; g < ng; g++) {
+        uint64_t k[2];
+        for (int c = 0; c < 2; c++) {
+            const double span = hi[c] > lo[c] ? hi[c] - lo[c] : 1.0;
+            double v = xy(grep[g], c);
+            double t = std::isfinite(v) ? (v - lo[c]) / span : 0.0;
+            t = std::min(1.0, std::max(0.0, t));
+            k[c] = (uint64_t)(t * 2097151.0);
+        }
+        key[g] = spread21(k[0]) | (spread21(k[1]) << 1);
+    }
+    std::vector<int32_t> gorder(ng);
+    std::iota(gorder.begin(), gorder.end(), 0);
+    std::sort(gorder.begin(), gorder.end(), [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : grep[a] < grep[b]; });
+    std::vector<int32_t> gpos(ng);
+    for (int32_t k = 0; k < ng; k++) gpos[gorder[k]] = k;
+
+    // 3. rows: groups in that order, points of a group by id
+    std::vector<int32_t> pts(P);
+    std::iota(pts.begin(), pts.end(), 0);
+    counting_sort(pts, ng, [&](int32_t p) { return gpos[gid[p]]; });
+    H.point_of_row = pts;
+    H.row_of_point.assign(P, 0);
+    for (int32_t r = 0; r < P; r++) H.row_of_point[pts[r]] = r;
+    const std::vector<int32_t> &row = H.row_of_point;
+
+    // 4. work-balanced contiguous group ranges per rank: weight of a row = 2 + its ARAP incidences
+    std::vector<int64_t> rw(P, 2);
+    for (int64_t e = 0; e < 4 * E; e++) rw[row[ap[e]]]++;
+    for (int64_t e = 0; e < R; e++) rw[row[d.rep_point[e]]]++;
+    for (int64_t e = 0; e < D; e++) rw[row[d.dep_point[e]]]++;
+    const double total = std::accumulate(rw.begin(), rw.end(), 0.0);
+    H.rank_row_begin.assign(nranks + 1, P);
+    H.rank_row_begin[0] = 0;
+    {
+        double cum = 0;
+        int next = 1;
+        for (int32_t r = 0; r < P && next < nranks; r++) {
+            // cut only between groups
+            const bool group_start = r == 0 || gid[pts[r]] != gid[pts[r - 1]];
+            if (group_start && r > 0 && cum >= total * next / nranks) H.rank_row_begin[next++] = r;
+            cum += (double)rw[r];
+        }
+        for (; next < nranks; next++) H.rank_row_begin[next] = P;
+    }
+    H.lo = H.rank_row_begin[rank];
+    H.hi = H.rank_row_begin[rank + 1];
+    const int32_t lo_r = H.lo, hi_r = H.hi;
+    auto own = [&](int32_t r) { return r >= lo_r && r < hi_r; };
+    const int32_t nown = hi_r - lo_r;
+
+    // 5. local ARAP edges: owned (point 0 here) first, then halo-only; each by (pair, row of point 0)
+    std::vector<int32_t> owned_e, halo_e;
+    for (int64_t e = 0; e < E; e++) {
+        const int32_t r0 = row[ap[4 * e]];
+        if (own(r0)) owned_e.push_back((int32_t)e);
+        else if (own(row[ap[4 * e + 1]]) || own(row[ap[4 * e + 2]]) || own(row[ap[4 * e + 3]])) halo_e.push_back((int32_t)e);
+    }
+    for (auto *lst : {&owned_e, &halo_e}) {
+        counting_sort(*lst, P, [&](int32_t e) { return row[ap[4 * (int64_t)e]]; });
+        counting_sort(*lst, std::max(Q, 1), [&](int32_t e) { return d.arap_pair[e]; });
+    }
+    H.n_arap_owned = (int32_t)owned_e.size();
+    H.arap_ids = owned_e;
+    H.arap_ids.insert(H.arap_ids.end(), halo_e.begin(), halo_e.end());
+    owned_e.clear(); owned_e.shrink_to_fit();
+    halo_e.clear(); halo_e.shrink_to_fit();
+    const int64_t nloc = (int64_t)H.arap_ids.size();
+
+    // rotation rows used by the local edges, compacted
+    {
+        std::vector<int32_t> map(std::max(d.n_rot, 1), -1);
+        H.arap_rot_local.resize(2 * (size_t)nloc);
+        for (int64_t le = 0; le < nloc; le++)
+            for (int k = 0; k < 2; k++) {
+                const int32_t g = d.arap_rot[2 * (int64_t)H.arap_ids[le] + k];
+                if (map[g] < 0) { map[g] = (int32_t)H.rot_ids.size(); H.rot_ids.push_back(g); }
+                H.arap_rot_local[2 * le + k] = map[g];
+            }
+    }
+
+    // 6. the own rows' reprojection / depth edges, by row
+    for (int64_t e = 0; e < R; e++) if (own(row[d.rep_point[e]])) H.rep_ids.push_back((int32_t)e);
+    for (int64_t e = 0; e < D; e++) if (own(row[d.dep_point[e]])) H.dep_ids.push_back((int32_t)e);
+    counting_sort(H.rep_ids, P, [&](int32_t e) { return row[d.rep_point[e]]; });
+    counting_sort(H.dep_ids, P, [&](int32_t e) { return row[d.dep_point[e]]; });
+    H.rep_off.assign(nown + 1, 0);
+    H.dep_off.assign(nown + 1, 0);
+    for (int32_t e : H.rep_ids) H.rep_off[row[d.rep_point[e]] - lo_r + 1]++;
+    for (int32_t e : H.dep_ids) H.dep_off[row[d.dep_point[e]] - lo_r + 1]++;
+    for (int32_t l = 0; l < nown; l++) { H.rep_off[l + 1] += H.rep_off[l]; H.dep_off[l + 1] += H.dep_off[l]; }
+
+    // 7. phase-1 blocks: ARAP (owned, then halo-only) per pair in runs of kSpBlock; depth edges by
+    //    (scale, row) per scale
+    const int32_t ndl = (int32_t)H.dep_ids.size();
+    H.dperm.resize(ndl);
+    std::iota(H.dperm.begin(), H.dperm.end(), 0);
+    counting_sort(H.dperm, std::max(S, 1), [&](int32_t j) { return d.dep_scale[H.dep_ids[j]]; });
+    auto add_blocks = [&](int kind, int owned, int64_t b0, int64_t b1, auto heavy_of) {
+        int64_t i = b0;
+        while (i < b1) {
+            const int32_t hv = heavy_of(i);
+            int64_t j = i;
+            while (j < b1 && j - i < kSpBlock && heavy_of(j) == hv) j++;
+            H.blk.push_back(kind | owned << 8);
+            H.blk.push_back(hv);
+            H.blk.push_back((int32_t)i);
+            H.blk.push_back((int32_t)j);
+            i = j;
+        }
+    };
+    auto pair_of = [&](int64_t le) { return d.arap_pair[H.arap_ids[le]]; };
+    add_blocks(SP_ARAP, 1, 0, H.n_arap_owned, pair_of);
+    add_blocks(SP_ARAP, 0, H.n_arap_owned, nloc, pair_of);
+    add_blocks(SP_DEP, 1, 0, ndl, [&](int64_t i) { return d.dep_scale[H.dep_ids[H.dperm[i]]]; });
+    const int64_t nb = (int64_t)H.blk.size() / 4;
+    H.hv_blk_off.assign(Q + S + 1, 0);
+    auto blk_heavy = [&](int64_t b) -> int32_t {
+        const int kind = H.blk[4 * b] & 0xff, owned = H.blk[4 * b] >> 8;
+        if (kind == SP_ARAP) return owned ? H.blk[4 * b + 1] : -1;
+        return Q + H.blk[4 * b + 1];
+    };
+    for (int64_t b = 0; b < nb; b++) { const int32_t h = blk_heavy(b); if (h >= 0) H.hv_blk_off[h + 1]++; }
+    for (int32_t h = 0; h < Q + S; h++) H.hv_blk_off[h + 1] += H.hv_blk_off[h];
+    H.hv_blk.resize((size_t)H.hv_blk_off[Q + S]);
+    {
+        std::vector<int64_t> pos(H.hv_blk_off.begin(), H.hv_blk_off.end() - 1);
+        for (int64_t b = 0; b < nb; b++) { const int32_t h = blk_heavy(b); if (h >= 0) H.hv_blk[pos[h]++] = (int32_t)b; }
+    }
+
+    // 8. own rows' ARAP incidences (local edge << 2 | role), each row's in local-edge order
+    H.inc_off.assign(nown + 1, 0);
+    for (int64_t le = 0; le < nloc; le++) {
+        const int64_t e = H.arap_ids[le];
+        for (int k = 0; k < 4; k++) { const int32_t r = row[ap[4 * e + k]]; if (own(r)) H.inc_off[r - lo_r + 1]++; }
+    }
+    for (int32_t l = 0; l < nown; l++) H.inc_off[l + 1] += H.inc_off[l];
+    H.inc.resize((size_t)H.inc_off[nown]);
+    {
+        std::vector<int64_t> pos(H.inc_off.begin(), H.inc_off.end() - 1);
+        for (int64_t le = 0; le < nloc; le++) {
+            const int64_t e = H.arap_ids[le];
+            for (int k = 0; k < 4; k++) {
+                const int32_t r = row[ap[4 * e + k]];
+                if (own(r)) H.inc[pos[r - lo_r]++] = (int32_t)(le << 2 | k);
+            }
+        }
+    }
+
+    // 9. halo exchange lists
+    H.send_rows.assign(nranks, {});
+    H.recv_rows.assign(nranks, {});
+    if (nranks > 1) {
+        std::vector<int32_t> owner(P);
+        for (int rr = 0; rr < nranks; rr++)
+            for (int32_t r = H.rank_row_begin[rr]; r < H.rank_row_begin[rr + 1]; r++) owner[r] = rr;
+        std::vector<uint8_t> need(P, 0);
+        for (int64_t le = 0; le < nloc; le++) {
+            const int64_t e = H.arap_ids[le];
+            for (int k = 0; k < 4; k++) { const int32_t r = row[ap[4 * e + k]]; if (!own(r)) need[r] = 1; }
+        }
+        for (int32_t r = 0; r < P; r++) if (need[r]) H.recv_rows[owner[r]].push_back(r);
+        // rows of this rank read by another rank's local edges
+        for (int64_t e = 0; e < E; e++) {
+            int32_t rr[4], oo[4];
+            bool mine = false, other = false;
+            for (int k = 0; k < 4; k++) {
+                rr[k] = row[ap[4 * e + k]]; oo[k] = owner[rr[k]];
+                mine |= oo[k] == rank;
+                other |= oo[k] != rank;
+            }
+            if (!mine || !other) continue;
+            for (int k = 0; k < 4; k++) {
+                if (oo[k] != rank) continue;
+                for (int j = 0; j < 4; j++) if (oo[j] != rank) H.send_rows[oo[j]].push_back(rr[k]);
+            }
+        }
+        for (auto &v : H.send_rows) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
+        for (auto &v : H.recv_rows) H.halo_rows += (int64_t)v.size();
+    }
+
+    // 10. algorithmic bytes of one product (phase 1 + phase 2): compulsory loads and
+    //     stores, the p gathers at an edge's other points not counted
+    const double jb = fp32_jac ? 72.0 : 144.0;
+    H.phase1_bytes = (double)nloc * (jb + 8 + 16 + 8)                  // J, W, rows, s
+                     + (double)ndl * (4 + 4 + 24 + 8);                  // dperm, row, c, W J_s^2
+    H.phase2_bytes = (double)nown * (48 + 48 + 48 + 24 + 8 + 4)        // (z,p) in / out, D, q, offsets
+                     + (double)H.inc.size() * (4 + 8 + jb / 6)           // incidence, s, J slice
+                     + (double)ndl * (4 + 24);                           // the row's depth couplings
+    H.product_bytes = H.phase1_bytes + H.phase2_bytes;
+    return true;
+}
+
+// Host emulation of one sharded product q = (H + lambda I) p on this rank's plan, with the device
+// kernels' decomposition (tests; no GPU): only the own rows of p are read from the input, the halo
+// rows arrive through `xfer` (op 2 send / 3 receive, the same global order as the device exchange),
+// the heavy partials of the owned edges are all-reduced (op 0).  J / W in the problem's edge order.
+// q receives the own rows (problem order) and the heavy dofs; the other rows are zero.
+int sp_emulate_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
+                       const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
+                       const double *p, double *q, const std::function<int(int, int, double *, int64_t)> &xfer) {
+    const int64_t hd = H.hd, ndof = hd + 3 * (int64_t)H.P;
+    const int32_t lo = H.lo, hi = H.hi, nown = hi - lo, Q = H.Q;
+    std::vector<double> pl(ndof, 0.0);
+    for (int64_t k = 0; k < hd; k++) pl[k] = p[k];
+    for (int32_t r = lo; r < hi; r++)
+        for (int c = 0; c < 3; c++) pl[hd + 3 * (int64_t)r + c] = p[hd + 3 * (int64_t)H.point_of_row[r] + c];
+    if (H.nranks > 1) {
+        for (int a = 0; a < H.nranks; a++)
+            for (int b = 0; b < H.nranks; b++) {
+                if (a == b) continue;
+                if (a == H.rank && !H.send_rows[b].empty()) {
+                    std::vector<double> buf;
+                    for (int32_t r : H.send_rows[b]) for (int c = 0; c < 3; c++) buf.push_back(pl[hd + 3 * (int64_t)r + c]);
+                    if (xfer(2, b, buf.data(), (int64_t)buf.size())) return -2;
+                }
+                if (b == H.rank && !H.recv_rows[a].empty()) {
+                    std::vector<double> buf(3 * H.recv_rows[a].size());
+                    if (xfer(3, a, buf.data(), (int64_t)buf.size())) return -2;
+                    for (size_t i = 0; i < H.recv_rows[a].size(); i++)
+                        for (int c = 0; c < 3; c++) pl[hd + 3 * (int64_t)H.recv_rows[a][i] + c] = buf[3 * i + c];
+                }
+            }
+    }
+    // phase 1
+    const int64_t nloc = (int64_t)H.arap_ids.size();
+    std::vector<double> s(nloc), hsum(hd, 0.0);
+    for (int64_t le = 0; le < nloc; le++) {
+        const int64_t e = H.arap_ids[le];
+        const double *J = Ja + 18 * e;
+        const int32_t q_ = d.arap_pair[e];
+        double t = 0;
+        for (int k = 0; k < 4; k++) {
+            const int64_t o = hd + 3 * (int64_t)H.row_of_point[d.arap_pts[4 * e + k]];
+            for (int c = 0; c < 3; c++) t += J[3 * k + c] * pl[o + c];
+        }
+        for (int c = 0; c < 6; c++) t += J[12 + c] * pl[6 * (int64_t)q_ + c];
+        s[le] = Wa[e] * t;
+        if (le < H.n_arap_owned)
+            for (int c = 0; c < 6; c++) hsum[6 * (int64_t)q_ + c] += J[12 + c] * s[le];
+    }
+    for (int32_t e : H.dep_ids) {
+        const double *J = Jd + 4 * (int64_t)e;
+        const int64_t o = hd + 3 * (int64_t)H.row_of_point[d.dep_point[e]];
+        const int32_t sc = d.dep_scale[e];
+        double t = 0;
+        for (int c = 0; c < 3; c++) t += Wd[e] * J[c] * J[3] * pl[o + c];
+        t += Wd[e] * J[3] * J[3] * pl[6 * (int64_t)Q + sc];
+        hsum[6 * (int64_t)Q + sc] += t;
+    }
+    if (H.nranks > 1 && hd > 0 && xfer(0, -1, hsum.data(), hd)) return -2;
+    // phase 2
+    for (int64_t k = 0; k < ndof; k++) q[k] = 0.0;
+    for (int32_t l = 0; l < nown; l++) {
+        const int32_t r = lo + l;
+        const int64_t o = hd + 3 * (int64_t)r;
+        double acc[3];
+        for (int c = 0; c < 3; c++) acc[c] = lambda * pl[o + c];
+        for (int32_t j = H.rep_off[l]; j < H.rep_off[l + 1]; j++) {
+            const int64_t e = H.rep_ids[j];
+            const double *J = Jr + 6 * e;
+            for (int rr = 0; rr < 2; rr++) {
+                double t = 0;
+                for (int c = 0; c < 3; c++) t += J[3 * rr + c] * pl[o + c];
+                for (int c = 0; c < 3; c++) acc[c] += J[3 * rr + c] * Wr[e] * t;
+            }
+        }
+        for (int32_t j = H.dep_off[l]; j < H.dep_off[l + 1]; j++) {
+            const int64_t e = H.dep_ids[j];
+            const double *J = Jd + 4 * e;
+            double t = J[3] * pl[6 * (int64_t)Q + d.dep_scale[e]];
+            for (int c = 0; c < 3; c++) t += J[c] * pl[o + c];
+            for (int c = 0; c < 3; c++) acc[c] += J[c] * Wd[e] * t;
+        }
+        for (int64_t k = H.inc_off[l]; k < H.inc_off[l + 1]; k++) {
+            const int v = H.inc[k];
+            const int64_t le = v >> 2, e = H.arap_ids[le];
+            for (int c = 0; c < 3; c++) acc[c] += Ja[18 * e + 3 * (v & 3) + c] * s[le];
+        }
+        const int64_t po = hd + 3 * (int64_t)H.point_of_row[r];
+        for (int c = 0; c < 3; c++) q[po + c] = acc[c];
+    }
+    for (int64_t k = 0; k < hd; k++) q[k] = hsum[k] + lambda * pl[k];
+    return 0;
+}
+
+}  // namespace deftri

@@ -1,0 +1,629 @@
+// spcg_solver.cpp — g2o-semantics Levenberg–Marquardt on the point-sharded matrix-free PCG plan
+// (spcg.h).  The control flow restates OptimizationAlgorithmLevenberg::solve as driven by
+// `optimizer.optimize(nOptIterations)` (reference g2oBundleAdjustment.cc:959-962),
+// exactly as solver.cpp's deftri_solve_lm does for the multifrontal plan:
+//   per iteration: computeActiveErrors + linearizeOplus, buildSystem (here: the rows' diagonal
+//   blocks, b and the heavy blocks only), lambda init at iteration 0 (tau * max diag H), then trials
+//   { setLambda; solve; update; computeActiveErrors; rho = (chi_cur - chi_new) /
+//   (dx.(lambda dx + b) + 1e-3); accept (lambda *= max(1/3, min(2/3, 1-(2rho-1)^3)), ni = 2) or
+//   reject (lambda *= ni, ni *= 2, pop) } while rho < 0 && trials < maxTrials.
+// A step whose PCG does not converge within the budget (or breaks down) counts as a failed solve,
+// as g2o treats a failed linear solve: chi_new = max, the trial is rejected.  There is no
+// factorization behind this plan (a 500k x 8-keyframe factor does not fit one GPU).
+//
+// Sharded (nranks > 1): every rank runs the same control flow on all-reduced scalars: chi2 of its
+// owned edges, the heavy H / b, (r.z, r.r) and (p.q + heavy sums) per CG iteration, the trial's
+// chi2 and rho denominator; the boundary rows' (z, p) are exchanged after every CG update and x
+// after the solve (SpTransport: RCCL on the solver stream or the caller's host callback).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+
+#include "spcg.h"
+
+namespace deftri {
+
+void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);
+
+namespace {
+constexpr int kSpMaxIt = 4096;
+constexpr int kSpDefaultIt = 1000;
+constexpr int kSpRedParts = 512;
+constexpr int kSpRecDoubles = 8;
+
+void quat_norm(double *q) {      // SE3Quat::normalizeRotation
+    if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
+    const double n = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    for (int k = 0; k < 4; k++) q[k] /= n;
+}
+
+void quat_mat(const double *q, double *R) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+}  // namespace
+
+#define SPOK(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return fail(DEFTRI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+SpSolver::SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr)
+    : dev_(device), st_(st), rank_(rank), nranks_(nranks), tr_(tr) {
+    hipHostMalloc((void **)&hpin, 32 * sizeof(double), hipHostMallocDefault);
+    hipHostMalloc((void **)&ipin, 16 * sizeof(int), hipHostMallocDefault);
+    for (int i = 0; i < 32; i++) hpin[i] = 0.0;
+}
+
+SpSolver::~SpSolver() {
+    hipSetDevice(dev_);
+    hipStreamSynchronize(st_);
+    for (void *p : allocs_) hipFree(p);
+    if (hpin) hipHostFree(hpin);
+    if (ipin) hipHostFree(ipin);
+}
+
+template <class T>
+int SpSolver::alloc(T **p, int64_t n) {
+    *p = nullptr;
+    if (n <= 0) n = 1;
+    void *v = nullptr;
+    hipError_t e = hipMalloc(&v, sizeof(T) * (size_t)n);
+    if (e != hipSuccess) return fail(DEFTRI_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    allocs_.push_back(v);
+    *p = (T *)v;
+    return 0;
+}
+
+template <class T>
+int SpSolver::put(T **p, const std::vector<T> &v) {
+    int rc = alloc(p, (int64_t)v.size());
+    if (rc) return rc;
+    if (!v.empty()) SPOK(hipMemcpy(*p, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int SpSolver::budget() const { return std::min(kSpMaxIt, max_it > 0 ? max_it : kSpDefaultIt); }
+
+int SpSolver::upload(const deftri_problem_desc &d) {
+    hipSetDevice(dev_);
+    hipStreamSynchronize(st_);
+    for (void *p : allocs_) hipFree(p);
+    allocs_.clear();
+    have_ = false;
+    P = DevProblem();
+    G = SpDev();
+    if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err)) return DEFTRI_E_ARG;
+    const int32_t NP = d.n_points, Q = d.n_pairs, S = d.n_scales, C = d.n_cams;
+    const int64_t nloc = (int64_t)H.arap_ids.size();
+    const int32_t nown = H.hi - H.lo;
+    // the rank's device problem, points in row order
+    std::vector<double> pts(3 * (size_t)NP), tg(d.tg, d.tg + 7 * (size_t)Q), sc(d.scales, d.scales + S);
+    for (int32_t r = 0; r < NP; r++)
+        for (int c = 0; c < 3; c++) pts[3 * (size_t)r + c] = d.points[3 * (size_t)H.point_of_row[r] + c];
+    for (int32_t q = 0; q < Q; q++) quat_norm(&tg[7 * (size_t)q]);
+    std::vector<double> cpose(d.cam_pose, d.cam_pose + 7 * (size_t)C), camR(9 * (size_t)std::max(C, 1));
+    for (int32_t c = 0; c < C; c++) { quat_norm(&cpose[7 * (size_t)c]); quat_mat(&cpose[7 * (size_t)c], &camR[9 * (size_t)c]); }
+    std::vector<float> kb8(d.cam_kb8, d.cam_kb8 + 8 * (size_t)C);
+    const size_t nr = H.rep_ids.size(), nd = H.dep_ids.size();
+    std::vector<int32_t> rp(nr), rc(nr), dp(nd), ds(nd), dc(nd);
+    std::vector<double> ro(2 * nr), ri(nr), dm(nd), di(nd);
+    for (size_t j = 0; j < nr; j++) {
+        const int32_t e = H.rep_ids[j];
+        rp[j] = H.row_of_point[d.rep_point[e]]; rc[j] = d.rep_cam[e];
+        ro[2 * j] = d.rep_obs[2 * (size_t)e]; ro[2 * j + 1] = d.rep_obs[2 * (size_t)e + 1]; ri[j] = d.rep_info[e];
+    }
+    for (size_t j = 0; j < nd; j++) {
+        const int32_t e = H.dep_ids[j];
+        dp[j] = H.row_of_point[d.dep_point[e]]; ds[j] = d.dep_scale[e]; dc[j] = d.dep_cam[e];
+        dm[j] = d.dep_meas[e]; di[j] = d.dep_info[e];
+    }
+    std::vector<int32_t> apts(4 * (size_t)nloc), apair(nloc);
+    std::vector<double> aw(nloc);
+    for (int64_t le = 0; le < nloc; le++) {
+        const int64_t e = H.arap_ids[le];
+        for (int k = 0; k < 4; k++) apts[4 * le + k] = H.row_of_point[d.arap_pts[4 * e + k]];
+        apair[le] = d.arap_pair[e];
+        aw[le] = d.arap_w[e];
+    }
+    std::vector<double> rot(9 * H.rot_ids.size());
+    for (size_t k = 0; k < H.rot_ids.size(); k++)
+        std::memcpy(&rot[9 * k], d.rot + 9 * (size_t)H.rot_ids[k], 9 * sizeof(double));
+    std::vector<double> parea(d.pair_area, d.pair_area + Q), pinfo(d.pair_info, d.pair_info + Q);
+    int rc_;
+#define PUT(dst, v) if ((rc_ = put(&(dst), v))) return rc_
+#define ALLOC(dst, n) if ((rc_ = alloc(&(dst), n))) return rc_
+    P.P = NP; P.Q = Q; P.S = S; P.C = C;
+    P.R = (int32_t)nr; P.D = (int32_t)nd; P.E = (int32_t)nloc; P.NR = (int32_t)H.rot_ids.size();
+    P.huber_delta = d.huber_delta;
+    PUT(P.points, pts); PUT(P.scales, sc); PUT(P.tg, tg);
+    ALLOC(P.points_bak, 3 * (int64_t)NP); ALLOC(P.scales_bak, S); ALLOC(P.tg_bak, 7 * (int64_t)Q);
+    PUT(P.cam_kb8, kb8); PUT(P.cam_pose, cpose); PUT(P.cam_R, camR);
+    PUT(P.rep_point, rp); PUT(P.rep_cam, rc); PUT(P.rep_obs, ro); PUT(P.rep_info, ri);
+    PUT(P.dep_point, dp); PUT(P.dep_scale, ds); PUT(P.dep_cam, dc); PUT(P.dep_meas, dm); PUT(P.dep_info, di);
+    PUT(P.arap_pts, apts); PUT(P.arap_pair, apair); PUT(P.arap_rot, H.arap_rot_local); PUT(P.arap_w, aw);
+    PUT(P.rot, rot); PUT(P.pair_area, parea); PUT(P.pair_info, pinfo);
+    ALLOC(P.Jrep, 6 * (int64_t)nr); ALLOC(P.Wrep, nr); ALLOC(P.Erep, 2 * (int64_t)nr); ALLOC(P.chi_rep, nr);
+    ALLOC(P.Jdep, 4 * (int64_t)nd); ALLOC(P.Wdep, nd); ALLOC(P.Edep, nd); ALLOC(P.chi_dep, nd);
+    ALLOC(P.Jarap, 18 * nloc); ALLOC(P.Warap, nloc); ALLOC(P.Earap, nloc); ALLOC(P.chi_arap, nloc);
+    ALLOC(P.tg_pre, 12 * 13 * (int64_t)std::max(Q, 1));
+    init_.assign(3, nullptr);
+    PUT(init_[0], pts); PUT(init_[1], sc); PUT(init_[2], tg);
+    pts.clear(); pts.shrink_to_fit();
+    apts.clear(); apts.shrink_to_fit();
+
+    // plan
+    G.P = NP; G.Q = Q; G.S = S;
+    G.hd = H.hd;
+    G.ndof = H.hd + 3 * (int64_t)NP;
+    G.row0 = H.lo; G.nown = nown;
+    G.nblk = (int32_t)(H.blk.size() / 4);
+    G.nrb = (nown + kSpBlock - 1) / kSpBlock;
+    G.include_heavy = rank_ == 0 ? 1 : 0;
+    int32_t *blk, *hvb, *dperm, *inc, *roff, *doff;
+    int64_t *hvbo, *inco;
+    PUT(blk, H.blk); PUT(hvb, H.hv_blk); PUT(hvbo, H.hv_blk_off); PUT(dperm, H.dperm);
+    PUT(inc, H.inc); PUT(inco, H.inc_off); PUT(roff, H.rep_off); PUT(doff, H.dep_off);
+    G.blk = reinterpret_cast<const int4 *>(blk);
+    G.hv_blk = hvb; G.hv_blk_off = hvbo; G.dperm = dperm;
+    G.inc = inc; G.inc_off = inco; G.rep_off = roff; G.dep_off = doff;
+    G.apts = P.arap_pts; G.apair = P.arap_pair;
+    G.Ja = P.Jarap; G.Wa = P.Warap; G.Ea = P.Earap;
+    G.Jr = P.Jrep; G.Wr = P.Wrep; G.Er = P.Erep;
+    G.Jd = P.Jdep; G.Wd = P.Wdep; G.Ed = P.Edep;
+    G.dsc = P.dep_scale; G.drow = P.dep_point;
+    if (fp32_jac) { float *j32; ALLOC(j32, 18 * nloc); G.Ja32 = j32; }
+    ALLOC(G.Hv, 6 * (int64_t)nown); ALLOC(G.Dv, 6 * (int64_t)nown); ALLOC(G.Mv, 6 * (int64_t)nown);
+    ALLOC(G.cdep, 3 * (int64_t)nd); ALLOC(G.wss, nd);
+    ALLOC(G.hl, 21 * (int64_t)Q + S + G.ndof);
+    G.b = G.hl + 21 * (int64_t)Q + S;
+    ALLOC(G.Mh, 36 * (int64_t)Q + S);
+    ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(G.nrb, 1));
+    ALLOC(G.r, G.ndof); ALLOC(G.q, G.ndof); ALLOC(G.x, G.ndof);
+    double *zp;
+    ALLOC(zp, 2 * G.ndof);
+    G.zp = reinterpret_cast<double2 *>(zp);
+    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
+    ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
+    ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
+    G.red = G.rec + kSpRecDoubles;
+    SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
+    SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
+    SPOK(hipMemset(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (kSpMaxIt + 2))));
+    ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1);
+    SPOK(hipMemset(d_flag, 0, sizeof(int)));
+    ALLOC(d_tmp, G.ndof); ALLOC(d_dx0, G.ndof);
+    PUT(d_row_of_point, H.row_of_point);
+    // halo lists: per peer, sends then receives, 6 doubles per row ((z, p) of 3 dofs)
+    std::vector<int32_t> srows, rrows;
+    send_off_.assign(nranks_ + 1, 0);
+    recv_off_.assign(nranks_ + 1, 0);
+    for (int p = 0; p < nranks_; p++) {
+        srows.insert(srows.end(), H.send_rows[p].begin(), H.send_rows[p].end());
+        rrows.insert(rrows.end(), H.recv_rows[p].begin(), H.recv_rows[p].end());
+        send_off_[p + 1] = (int64_t)srows.size();
+        recv_off_[p + 1] = (int64_t)rrows.size();
+    }
+    PUT(d_send_rows, srows); PUT(d_recv_rows, rrows);
+    ALLOC(d_xbuf, 6 * (int64_t)(srows.size() + rrows.size()));
+#undef PUT
+#undef ALLOC
+    SPOK(hipDeviceSynchronize());
+    have_ = true;
+    return 0;
+}
+
+// halo exchange of the boundary rows: zp (6 doubles per row: (z, p) of its 3 dofs) or x (3)
+int SpSolver::halo(int width, double *vec, bool zp) {
+    if (nranks_ <= 1) return 0;
+    const int64_t base = zp ? 2 * G.hd : G.hd;
+    const int64_t nsend = send_off_[nranks_];
+    double *sbuf = d_xbuf, *rbuf = d_xbuf + 6 * nsend;
+    sp_launch_pack((int)nsend, d_send_rows, width, base, vec, sbuf, st_);
+    // global order: for every (src, dst) pair in lexicographic order, the src sends and the dst receives
+    std::vector<SpTransport::Op> ops;
+    for (int a = 0; a < nranks_; a++)
+        for (int b = 0; b < nranks_; b++) {
+            if (a == b) continue;
+            if (a == rank_ && send_off_[b + 1] > send_off_[b])
+                ops.push_back({b, true, sbuf + width * send_off_[b], width * (send_off_[b + 1] - send_off_[b])});
+            if (b == rank_ && recv_off_[a + 1] > recv_off_[a])
+                ops.push_back({a, false, rbuf + width * recv_off_[a], width * (recv_off_[a + 1] - recv_off_[a])});
+        }
+    int rc = tr_->p2p(ops, st_);
+    if (rc) return rc;
+    sp_launch_unpack((int)recv_off_[nranks_], d_recv_rows, width, base, rbuf, vec, st_);
+    return 0;
+}
+
+// computeActiveErrors (+ linearizeOplus with jac) on the rank's edges, chi2 of its owned edges into
+// d_scal[slot]; `extra`: one more fixed-order sum in the same launches (the rho denominator)
+int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra) {
+    launch_linearize(P, st_, false, analytic);
+    SumJobs J;
+    J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+    J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+    J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+    J.nj = 3;
+    if (extra) J.j[J.nj++] = *extra;
+    J.total = d_scal + slot;
+    launch_sum_multi(J, d_part, kSpRedParts, st_);
+    return 0;
+}
+
+// per LM iteration: linearize, chi2 (reduced), the rows' / heavy blocks and b (heavy reduced), and at
+// iteration 0 max diag H into d_scal[2]
+int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
+    ok = true;
+    launch_linearize(P, st_, true, analytic);
+    SumJobs J;
+    J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+    J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+    J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+    J.nj = 3;
+    J.total = d_scal;
+    launch_sum_multi(J, d_part, kSpRedParts, st_);
+    int rc;
+    if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * (int64_t)P.E, st_);
+    sp_launch_glin(G, fp32_jac != 0, st_);
+    if (nranks_ > 1 && (rc = tr_->allreduce(G.hl, 21 * (int64_t)G.Q + G.S + G.hd, 0, st_))) return rc;
+    if (want_max) {
+        sp_launch_maxdiag(G, d_scal + 2, st_);
+        if (nranks_ > 1 && (rc = tr_->allreduce(d_scal + 2, 1, 1, st_))) return rc;
+        sp_launch_maxdiag_heavy(G, d_scal + 2, st_);
+    }
+    return 0;
+}
+
+// CG iterations [from, to) at lambda
+void SpSolver::cg_chain(double lambda, int from, int to) {
+    const bool dist = nranks_ > 1;
+    for (int it = from; it < to; it++) {
+        sp_launch_dots(G, it, st_);
+        if (dist) tr_->allreduce(G.red + (int64_t)kSpRed * it, 2, 0, st_);
+        sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
+        if (dist) {
+            sp_launch_heavy(G, it, lambda, 1, st_);
+            tr_->allreduce(G.hbuf, 1 + G.hd, 0, st_);
+            sp_launch_heavy(G, it, lambda, 2, st_);
+        } else {
+            sp_launch_heavy(G, it, lambda, 0, st_);
+        }
+        sp_launch_update(G, it, st_);
+        if (dist) halo(6, reinterpret_cast<double *>(G.zp), true);
+    }
+}
+
+// the state of iteration n into the record (converged / budget), no other effect
+int SpSolver::cg_tail(int n) {
+    sp_launch_dots(G, n, st_);
+    if (nranks_ > 1) {
+        int rc = tr_->allreduce(G.red + (int64_t)kSpRed * n, 2, 0, st_);
+        if (rc) return rc;
+    }
+    // k_sp_heavy stage 1 records the state of a finished solve and returns; a running one would
+    // compute its sums, so the tail records through stage 1 only when the state is final: launch
+    // the status-only variant (stage 3)
+    sp_launch_heavy(G, n, 0.0, 3, st_);
+    return 0;
+}
+
+// one step (H + lambda I) x = rhs into G.x with polling (diagnostics / profiling path)
+int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its) {
+    const int mx = budget();
+    G.max_it = mx;
+    G.tol2 = tol * tol;
+    SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (mx + 2)), st_));
+    sp_launch_setup(G, rhs, lambda, st_);
+    int j = 0;
+    int n = std::min(std::max(2, last_its + 1), mx);
+    for (;;) {
+        cg_chain(lambda, j, n);
+        j = n;
+        int rc = cg_tail(j);
+        if (rc) return rc;
+        SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
+        SPOK(hipStreamSynchronize(st_));
+        const int status = (int)hpin[16];
+        if (status == kSpConverged) { its = (int)hpin[17]; solved = true; break; }
+        if (status != kSpRunning || j >= mx) { its = j; solved = false; break; }
+        n = std::min(j + 4, mx);
+    }
+    if (solved) last_its = its;
+    step_its = its;
+    step_solved = solved ? 1 : 0;
+    return 0;
+}
+
+int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    const bool dist = nranks_ > 1;
+    R.n_unknowns = G.ndof;
+    R.rank = rank_;
+    R.nranks = nranks_;
+    R.lanes = 1;
+    const int max_trials = prm.max_trials > 0 ? prm.max_trials : 10;
+    const double tau = prm.tau > 0 ? prm.tau : 1e-5;
+    const bool analytic = prm.analytic_jacobians != 0;
+    auto t_start = std::chrono::steady_clock::now();
+    int rc;
+    eval_chi2(analytic, 0, nullptr);
+    if (dist && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    R.chi2_initial = hpin[0];
+    double currentChi = R.chi2_initial;
+    double lambda = 0, ni = 2;
+    int status = DEFTRI_STATUS_OK, it;
+    const int mx = budget();
+    const int64_t nrec = kSpRecDoubles + (int64_t)kSpRed * (mx + 2);
+    // the rank's share of dx.(lambda dx + b): its rows, plus the heavy dofs on rank 0 (contiguous
+    // with rank 0's rows)
+    const int64_t den_off = rank_ == 0 ? 0 : G.hd + 3 * (int64_t)G.row0;
+    const int64_t den_n = rank_ == 0 ? G.hd + 3 * (int64_t)G.nown : 3 * (int64_t)G.nown;
+    double t_lin = 0;
+    for (it = 0; it < prm.n_iterations; it++) {
+        auto t0 = std::chrono::steady_clock::now();
+        bool ok;
+        if ((rc = lin_iteration(analytic, it == 0, ok))) return rc;
+        double *chis = hpin;
+        SPOK(hipMemcpyAsync(chis, d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, st_));
+        bool chi_pending = true;
+        if (it == 0) {
+            SPOK(hipStreamSynchronize(st_));
+            currentChi = chis[0];
+            chi_pending = false;
+            lambda = prm.user_lambda > 0 ? prm.user_lambda : tau * chis[2];
+            ni = 2;
+        }
+        t_lin += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        double rho = 0;
+        int qmax = 0;
+        bool restore_pending = false;
+        do {
+            G.max_it = mx;
+            G.tol2 = tol * tol;
+            launch_trial_begin(P, d_flag, G.rec, nrec, st_, restore_pending);
+            restore_pending = false;
+            double *sc = hpin + 4;
+            // update (x, halo rows from their owners), chi2 of the owned edges, the rank's share of
+            // the rho denominator; one all-reduce of the two (sharded); one read-back
+            auto evaluate = [&]() -> int {
+                int r2;
+                if (dist && (r2 = halo(3, G.x, false))) return r2;
+                launch_update_state(P, G.x, st_, nullptr);
+                SumJob den;
+                den.n = den_n; den.a = G.x + den_off; den.b = G.b + den_off; den.lambda = lambda; den.mode = 1;
+                den.out = d_scal + 1;
+                eval_chi2(analytic, 0, &den);
+                if (dist && (r2 = tr_->allreduce(d_scal, 2, 0, st_))) return r2;
+                launch_trial_readback(d_scal, 2, d_flag, G.rec, kSpRecDoubles, sc, ipin, hpin + 16, st_);
+                return 0;
+            };
+            auto t0p = std::chrono::steady_clock::now();
+            sp_launch_setup(G, G.b, lambda, st_);
+            const int n = std::min(std::max(2, last_its + 1), mx);
+            cg_chain(lambda, 0, n);
+            int j = n;
+            if ((rc = cg_tail(j))) return rc;
+            if ((rc = evaluate())) return rc;
+            SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
+            if (chi_pending) { currentChi = chis[0]; chi_pending = false; }
+            int st = (int)hpin[16];
+            bool solved = st == kSpConverged, evaluated = solved;
+            int its = solved ? (int)hpin[17] : j;
+            if (!solved) {
+                // restore the state the evaluation changed; continue the solve in chunks of 4
+                SPOK(hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+                SPOK(hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+                SPOK(hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+                while (st == kSpRunning && j < mx) {
+                    const int n2 = std::min(j + 4, mx);
+                    cg_chain(lambda, j, n2);
+                    j = n2;
+                    if ((rc = cg_tail(j))) return rc;
+                    SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
+                    SPOK(hipStreamSynchronize(st_));
+                    st = (int)hpin[16];
+                }
+                solved = st == kSpConverged;
+                its = solved ? (int)hpin[17] : j;
+                if (solved) {
+                    if ((rc = evaluate())) return rc;
+                    SPOK(hipStreamSynchronize(st_));
+                    evaluated = true;
+                }
+            }
+            R.ms_pcg += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0p).count();
+            R.pcg_iterations += its;
+            step_its = its;
+            step_solved = solved ? 1 : 0;
+            if (solved) { R.pcg_trials++; last_its = its; }
+            else R.pcg_fallbacks++;
+            if (prm.verbose)
+                std::fprintf(stderr, "[deftri/sp] rank %d pcg lambda %.6e iterations %d %s\n", rank_, lambda, its,
+                             solved ? "converged" : "failed (trial rejected)");
+            const double tempChi = (solved && evaluated) ? sc[0] : std::numeric_limits<double>::max();
+            rho = currentChi - tempChi;
+            const double scale = (solved && evaluated ? sc[1] : 0.0) + 1e-3;
+            rho /= scale;
+            R.trials_total++;
+            R.trials_executed++;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                const double scaleFactor = std::max(1. / 3., alpha);
+                lambda *= scaleFactor;
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                restore_pending = true;                  // the next prologue (or the loop's end) restores
+                R.trials_rejected++;
+                if (!std::isfinite(lambda)) { qmax++; break; }
+            }
+            qmax++;
+        } while (rho < 0 && qmax < max_trials);
+        if (restore_pending) {
+            SPOK(hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+            SPOK(hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+            SPOK(hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+        }
+        if (it < DEFTRI_MAX_REPORT_ITERS) { R.chi2_iter[it] = currentChi; R.trials_iter[it] = qmax; }
+        if (prm.verbose)
+            std::fprintf(stderr, "[deftri/sp] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
+        if (qmax == max_trials || rho == 0 || !std::isfinite(lambda)) { status = DEFTRI_STATUS_TERMINATE; it++; break; }
+    }
+    eval_chi2(analytic, 0, nullptr);
+    if (dist && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    R.chi2_final = hpin[0];
+    R.status = status;
+    R.iterations = it;
+    R.lambda_final = lambda;
+    R.ms_linearize = t_lin;
+    R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return 0;
+}
+
+int SpSolver::download(double *points, double *scales, double *tg) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    SPOK(hipStreamSynchronize(st_));
+    if (points) {
+        std::vector<double> h(3 * (size_t)P.P);
+        SPOK(hipMemcpy(h.data(), P.points, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+        for (int32_t p = 0; p < P.P; p++)
+            for (int c = 0; c < 3; c++) points[3 * (size_t)p + c] = h[3 * (size_t)H.row_of_point[p] + c];
+    }
+    if (scales) SPOK(hipMemcpy(scales, P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToHost));
+    if (tg) SPOK(hipMemcpy(tg, P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int SpSolver::reset_state() {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    SPOK(hipMemcpyAsync(P.points, init_[0], sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+    SPOK(hipMemcpyAsync(P.scales, init_[1], sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+    SPOK(hipMemcpyAsync(P.tg, init_[2], sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+    SPOK(hipStreamSynchronize(st_));
+    return 0;
+}
+
+int SpSolver::chi2(double *out) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    eval_chi2(true, 0, nullptr);
+    int rc;
+    if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    *out = hpin[0];
+    return 0;
+}
+
+int SpSolver::gradient(double *b, double *hdiag, int64_t n) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (nranks_ > 1) return fail(DEFTRI_E_ARG, "not available on a point-sharded context");
+    if (n != G.ndof) return fail(DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(dev_);
+    bool ok;
+    int rc = lin_iteration(true, false, ok);
+    if (rc) return rc;
+    if (b) {
+        sp_launch_permute_out(G.P, G.hd, d_row_of_point, G.b, d_tmp, st_);
+        SPOK(hipMemcpyAsync(b, d_tmp, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st_));
+    }
+    SPOK(hipStreamSynchronize(st_));
+    if (hdiag) {
+        std::vector<double> hv(6 * (size_t)G.nown), hl(21 * (size_t)G.Q + G.S);
+        SPOK(hipMemcpy(hv.data(), G.Hv, sizeof(double) * hv.size(), hipMemcpyDeviceToHost));
+        SPOK(hipMemcpy(hl.data(), G.hl, sizeof(double) * hl.size(), hipMemcpyDeviceToHost));
+        const int diag3[3] = {0, 2, 5};
+        for (int32_t q = 0; q < G.Q; q++)
+            for (int a = 0; a < 6; a++) hdiag[6 * q + a] = hl[21 * (size_t)q + a * (a + 1) / 2 + a];
+        for (int32_t s = 0; s < G.S; s++) hdiag[6 * G.Q + s] = hl[21 * (size_t)G.Q + s];
+        for (int32_t p = 0; p < G.P; p++) {
+            const int32_t l = H.row_of_point[p] - H.lo;
+            for (int c = 0; c < 3; c++) hdiag[G.hd + 3 * (int64_t)p + c] = hv[6 * (size_t)l + diag3[c]];
+        }
+    }
+    return 0;
+}
+
+int SpSolver::damped_solve(double lambda, const double *rhs, double *x, int64_t n) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (nranks_ > 1) return fail(DEFTRI_E_ARG, "not available on a point-sharded context");
+    if (n != G.ndof) return fail(DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(dev_);
+    bool ok;
+    int rc = lin_iteration(true, false, ok);
+    if (rc) return rc;
+    SPOK(hipMemcpyAsync(d_dx0, rhs, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, st_));
+    sp_launch_permute_in(G.P, G.hd, d_row_of_point, d_dx0, d_tmp, st_);
+    bool solved = false;
+    int its = 0;
+    if ((rc = pcg_solve(lambda, d_tmp, solved, its))) return rc;
+    sp_launch_permute_out(G.P, G.hd, d_row_of_point, G.x, d_dx0, st_);
+    SPOK(hipMemcpyAsync(x, d_dx0, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    if (!solved) return fail(DEFTRI_E_NUMERIC, "PCG did not converge within its budget (" + std::to_string(its) + " iterations)");
+    return 0;
+}
+
+// one trial's kernels under the caller's profiler: linearize + lin, then (after an unprofiled solve
+// that learns the iteration count) the setup and exactly that many CG iterations
+int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    SPOK(hipStreamSynchronize(st_));
+    set_profiler(&prof);
+    bool ok;
+    int rc = lin_iteration(analytic, false, ok);
+    set_profiler(nullptr);
+    if (rc) return rc;
+    bool solved = false;
+    int its = 0;
+    if ((rc = pcg_solve(lambda, G.b, solved, its))) return rc;
+    set_profiler(&prof);
+    SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (G.max_it + 2)), st_));
+    sp_launch_setup(G, G.b, lambda, st_);
+    cg_chain(lambda, 0, its);
+    rc = cg_tail(its);
+    set_profiler(nullptr);
+    if (rc) return rc;
+    SPOK(hipStreamSynchronize(st_));
+    step_its = its;
+    step_solved = solved ? 1 : 0;
+    return 0;
+}
+
+int SpSolver::vertex_owner(int32_t *owner, int64_t nv) const {
+    if (nv != (int64_t)G.Q + G.S + G.P) return DEFTRI_E_ARG;
+    for (int32_t k = 0; k < G.Q + G.S; k++) owner[k] = 0;
+    for (int32_t p = 0; p < G.P; p++) {
+        const int32_t r = H.row_of_point[p];
+        int o = (int)(std::upper_bound(H.rank_row_begin.begin(), H.rank_row_begin.end(), r) - H.rank_row_begin.begin()) - 1;
+        owner[G.Q + G.S + p] = std::max(0, std::min(o, nranks_ - 1));
+    }
+    return 0;
+}
+
+}  // namespace deftri

@@ -19,6 +19,9 @@ DEFTRI_STATUS_OK = 0
 DEFTRI_STATUS_TERMINATE = 1
 DEFTRI_SOLVER_DIRECT = 0
 DEFTRI_SOLVER_PCG = 1
+DEFTRI_PLAN_AUTO = 0
+DEFTRI_PLAN_MULTIFRONTAL = 1
+DEFTRI_PLAN_ITERATIVE = 2
 DEFTRI_MAX_REPORT_ITERS = 1024
 
 
@@ -109,6 +112,17 @@ class AbsErrorsC(C.Structure):
 class RelErrorsC(C.Structure):
     _fields_ = [("kf1", i64), ("kf2", i64), ("reported", i32), ("rel_error", f64), ("depth_error", f64),
                 ("global_t_error", f64), ("area", f64), ("valid_pairs", i64), ("n_matches", i64)]
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("plan", i32), ("rank", i32), ("nranks", i32), ("own_rows", i32), ("halo_rows", i64),
+                ("local_arap_edges", i64), ("n_unknowns", i64), ("phase1_blocks", i32), ("row_blocks", i32),
+                ("product_bytes", f64), ("jacobian_fp32", i32), ("reserved", i32)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        d["plan"] = {DEFTRI_PLAN_MULTIFRONTAL: "multifrontal", DEFTRI_PLAN_ITERATIVE: "iterative"}.get(self.plan, "none")
+        return d
 
 
 class KernelStat(C.Structure):

@@ -48,6 +48,12 @@ def load():
         "deftri_set_factor_precision": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_set_linear_solver": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32]),
         "deftri_last_step_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+        "deftri_set_plan": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_set_jacobian_storage": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_get_plan_info": (C.c_int, [C.c_void_p, P(_abi.PlanInfo)]),
+        "deftri_debug_sp_product": (C.c_int, [C.c_void_p, P(_abi.ProblemDesc), P(C.c_double), P(C.c_double),
+                                              P(C.c_double), P(C.c_double), P(C.c_double), P(C.c_double),
+                                              C.c_double, P(C.c_double), P(C.c_double), C.c_int64, P(C.c_int64)]),
         "deftri_pixels_stand_dev": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.PixelsError)]),
         "deftri_triangulate_nrslam": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_float), P(C.c_float), P(C.c_float),
                                                 P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, P(C.c_float),
@@ -127,7 +133,8 @@ EXPORTED = [
     "deftri_ba_dist_set_allreduce", "deftri_ba_profile_trial",
     "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream",
     "deftri_measure_sim_absolute_map_errors", "deftri_measure_relative_map_errors", "deftri_dist_owned_edges",
-    "deftri_debug_plan_solve_dist",
+    "deftri_debug_plan_solve_dist", "deftri_set_plan", "deftri_set_jacobian_storage", "deftri_get_plan_info",
+    "deftri_debug_sp_product",
 ]
 
 
@@ -241,6 +248,36 @@ class Context:
         code = {"direct": _abi.DEFTRI_SOLVER_DIRECT, "pcg": _abi.DEFTRI_SOLVER_PCG}[solver]
         self._check(self.lib.deftri_set_linear_solver(self.h, code, float(tol), int(max_iterations)))
         self._solver = (solver, tol, max_iterations)
+
+    def set_plan(self, plan="auto"):
+        """Plan kind of the next upload: "auto", "multifrontal" (LDL^T analysis; sliced matrix-free PCG
+        where it fits) or "iterative" (point-sharded matrix-free PCG, no factorization; csrc/spcg.h)."""
+        code = {"auto": _abi.DEFTRI_PLAN_AUTO, "multifrontal": _abi.DEFTRI_PLAN_MULTIFRONTAL,
+                "iterative": _abi.DEFTRI_PLAN_ITERATIVE}[plan]
+        self._check(self.lib.deftri_set_plan(self.h, code))
+
+    def set_jacobian_storage(self, fp32):
+        """Iterative plan: the ARAP Jacobians the product reads in fp32 (1) or fp64 (0, default)."""
+        self._check(self.lib.deftri_set_jacobian_storage(self.h, 1 if fp32 else 0))
+
+    def plan_info(self):
+        info = _abi.PlanInfo()
+        self._check(self.lib.deftri_get_plan_info(self.h, C.byref(info)))
+        return info.as_dict()
+
+    def debug_sp_product(self, prob, jarap, warap, jrep, wrep, jdep, wdep, lam, p):
+        """Host emulation of the iterative plan's product on this rank (deftri_debug_sp_product):
+        returns (q with this rank's rows + the global vertices, [own rows, halo rows, local ARAP
+        edges, owned ARAP edges])."""
+        d = prob.to_desc()
+        f = lambda a: np.ascontiguousarray(a, dtype=np.float64)
+        arrs = [f(a) for a in (jarap, warap, jrep, wrep, jdep, wdep, p)]
+        q = np.zeros(prob.n_unknowns)
+        st = np.zeros(4, np.int64)
+        self._check(self.lib.deftri_debug_sp_product(self.h, C.byref(d), *[_dp(a) for a in arrs[:6]], float(lam),
+                                                     _dp(arrs[6]), _dp(q), prob.n_unknowns,
+                                                     st.ctypes.data_as(C.POINTER(C.c_int64))))
+        return q, st
 
     def last_step_info(self):
         """(CG iterations, converged) of the last PCG step."""
