@@ -243,28 +243,136 @@ def reduce_stats(dt, iters, trials, world, device):
     return float(v.item()), int(s[0].item()), int(s[1].item())
 
 
+# BASELINE workloads of the ARAP LM: scene recipe, weights (rep, arap, depth sigma) and
+# keyframe-pair window; --corr overrides the correspondences per keyframe
+WORKLOADS = {
+    "c2": {"k": 2, "n": 100000, "desc": "two-view deformable triangulation (Simulation.yaml weights)"},
+    "c3": {"k": 8, "n": 50000, "kb8": "drunkard", "w": (1.0, 1e7, 0.3), "window": 0,
+           "desc": "8 keyframes x 50k, all 28 pairs (Drunkard.yaml shapes / weights)"},
+    "c4": {"k": 8, "n": 500000, "kb8": "drunkard", "w": (1.0, 1e7, 0.3), "window": 0,
+           "desc": "500k map points per keyframe x 8 keyframes, all 28 pairs (Drunkard.yaml shapes / weights)"},
+    "c5": {"k": 20, "n": 200000, "kb8": "realcolon", "w": (1.0, 0.1, 1e-6), "window": 1,
+           "desc": "Realcolon.yaml: 20 keyframes x 200k, DepthWeight 0.001 (info 1e12), arap 0.1"},
+}
+
+
+def build_workload(wl, n, seed, window):
+    spec = WORKLOADS[wl]
+    if wl == "c2":
+        prob, m = build_problem(n, seed)
+        return prob, m
+    kb8 = sim.DRUNKARD_KB8 if spec["kb8"] == "drunkard" else sim.REALCOLON_KB8
+    rep, arap, sig = spec["w"]
+    return sim.multi_view_problem(n, spec["k"], seed=seed, kb8=kb8, rep_weight=rep, arap_weight=arap,
+                                  depth_sigma=np.float32(sig), pair_window=window), None
+
+
+def cpu_baseline_sample(wl, window, n_sample, gpu_trials_per_iter):
+    """The oracle (1 thread) on a bounded sample of a multi-keyframe workload: the same recipe at
+    n_sample correspondences per keyframe (the full C3-C5 sizes take hours in scalar SimplicialLDLT);
+    one linearization + one trial measured, per iteration = linearization + the GPU's trials per
+    iteration x trial."""
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle
+    prob, _ = build_workload(wl, n_sample, 1, window)
+    t = time.perf_counter()
+    r = oracle.solve_lm(prob, 1, analytic=False, max_trials=1)["report"]
+    dt = time.perf_counter() - t
+    lin = r["ms_linearize"] * 1e-3
+    per_trial = (r["ms_factor"] + r["ms_solve"] + r["ms_update"]) * 1e-3 / max(r["trials_total"], 1)
+    t_iter = lin + gpu_trials_per_iter * per_trial
+    info = host_cpu_info()
+    return {"value": 1.0 / t_iter, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"oracle LM (g2o numeric J, SimplicialLDLT) on the {wl} recipe at {n_sample} correspondences per "
+                      f"keyframe ({prob.n_unknowns} unknowns, {len(prob.arap_pair)} ARAP edges), 1 thread: linearization "
+                      f"{lin:.2f} s + one trial {per_trial:.2f} s, per iteration = linearization + "
+                      f"{gpu_trials_per_iter:.2f} trials; {dt:.1f} s measured; host {info['cpu_model']}",
+            "seconds_per_iteration": round(t_iter, 3), "sample_unknowns": prob.n_unknowns}
+
+
+def product_roofline(stats, rep, ctx, rank):
+    """Roofline of the step solver's dominant kernel from a profiled trial (HIP events on the solver
+    stream): active launches only (the profiled replay launches exactly the solve's CG iterations)."""
+    if "sp_phase1" in stats:
+        p1, p2 = stats["sp_phase1"], stats["sp_phase2"]
+        its = max(p2["launches"], 1)
+        by, ms = p1["bytes"] + p2["bytes"], p1["ms"] + p2["ms"]
+        gbs = by / max(ms * 1e-3, 1e-12) / 1e9
+        cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update") if k in stats)
+        return {"bound": "hbm", "kernel": "k_sp_phase1+k_sp_phase2 (matrix-free product)", "achieved": round(gbs, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "traffic_unit": "bytes per product", "bytes_per_launch": by / its, "launches": its,
+                "avg_active_launch_us": round(1e3 * ms / its, 3),
+                "phase1": {"us": round(1e3 * p1["ms"] / its, 3), "bytes": p1["bytes"] / its,
+                           "gbs": round(p1["bytes"] / max(p1["ms"] * 1e-3, 1e-12) / 1e9, 1)},
+                "phase2": {"us": round(1e3 * p2["ms"] / its, 3), "bytes": p2["bytes"] / its,
+                           "gbs": round(p2["bytes"] / max(p2["ms"] * 1e-3, 1e-12) / 1e9, 1)},
+                "cg_iterations": its, "cg_iteration_us": round(1e3 * cg / its, 3), "lambda": rep["lambda_final"],
+                "rank": rank}
+    if "pcg_product" in stats:
+        pp = stats["pcg_product"]
+        its = max(pp["launches"], 1)
+        gbs = pp["bytes"] / max(pp["ms"] * 1e-3, 1e-12) / 1e9
+        mf = "mf_lin" in stats
+        cg = sum(stats[k]["ms"] for k in ("pcg_product", "pcg_heavy", "pcg_update") if k in stats)
+        out = {"bound": "hbm", "kernel": "k_mf_product" if mf else "k_pcg_product", "achieved": round(gbs, 1),
+               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+               "traffic_unit": "bytes per launch", "bytes_per_launch": pp["bytes"] / its, "launches": its,
+               "avg_active_launch_us": round(1e3 * pp["ms"] / its, 3),
+               "cg_iterations": its, "cg_iteration_us": round(1e3 * cg / its, 3), "lambda": rep["lambda_final"],
+               "rank": rank}
+        for pm in sorted(ROOT.glob("profiles/*_pmc_*product.json")):
+            pj = json.loads(pm.read_text())
+            if abs(pj.get("bytes_per_launch_algorithmic", -1) - out["bytes_per_launch"]) < 1e-6 * out["bytes_per_launch"]:
+                out["traffic"] = pj["traffic_bytes_per_launch"]
+                out["traffic_source"] = pm.name
+        return out
+    return None
+
+
+def factor_roofline(stats_f, rank):
+    upd = stats_f["update"]
+    achieved = upd["flops"] / (upd["ms"] * 1e-3) / 1e12
+    traffic = None
+    pmc = sorted(ROOT.glob("profiles/*_pmc_k_update.json"))
+    if pmc:
+        pj = json.loads(pmc[-1].read_text())
+        if abs(pj.get("update_flops_per_factorization", -1) - upd["flops"]) < 1e-6 * upd["flops"]:
+            traffic = pj["traffic_bytes_per_factorization"]
+    return {"bound": "mfma", "kernel": "k_update", "achieved": round(achieved, 3),
+            "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
+            "peak_sustained_measured": MFMA_F64_SUSTAINED_TFLOPS,
+            "traffic": traffic, "traffic_unit": "bytes per factorization (all k_update launches)",
+            "launches": upd["launches"], "avg_launch_us": round(1e3 * upd["ms"] / max(upd["launches"], 1), 3),
+            "flops_per_factorization": upd["flops"], "rank": rank}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=25, help="LM iterations timed (Simulation.yaml numberOfIterations: 25)")
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--corr", type=int, default=100000, help="correspondences per GPU (C2: 100k)")
+    ap.add_argument("--corr", type=int, default=0, help="correspondences per keyframe (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["c2", "ba"], default="c2",
-                    help="c2: the headline ARAP LM (BASELINE.json); ba: point-sharded bundle adjustment")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "ba"], default="c2",
+                    help="c2: the headline (BASELINE.json metric); c3-c5: the multi-keyframe configs; ba: bundle adjustment")
+    ap.add_argument("--pair-window", type=int, default=-1,
+                    help="keyframe pairs: 0 every pair (the reference), w > 0 pairs at most w apart (default: the workload's)")
     ap.add_argument("--ba-points", type=int, default=500000)
     ap.add_argument("--ba-kfs", type=int, default=8)
     ap.add_argument("--ba-scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--lanes", type=int, default=0,
                     help="speculative LM lambda lanes (0: library default, 1: sequential trials)")
     ap.add_argument("--solver", choices=["pcg", "direct"], default="pcg",
-                    help="LM step solver: block-Jacobi PCG with LDL^T fallback (library default) or the LDL^T")
+                    help="LM step solver: block-Jacobi PCG (library default) or the multifrontal LDL^T")
+    ap.add_argument("--plan", choices=["auto", "multifrontal", "iterative"], default="auto",
+                    help="auto: multifrontal for one-GPU two-view PCG / any direct solve, iterative otherwise")
+    ap.add_argument("--jacobian-fp32", action="store_true", help="iterative plan: fp32-stored ARAP Jacobians")
     ap.add_argument("--analytic", action="store_true",
                     help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
-    ap.add_argument("--sharded", action="store_true",
-                    help="N > 1: one C2 problem point-sharded over the ranks (LDL^T, strong scaling) instead of "
-                         "N independent problems (the default)")
-    ap.add_argument("--replicas", action="store_true", help="N > 1: independent problems (the default; kept for scripts)")
+    ap.add_argument("--sharded", action="store_true", help="kept for scripts: N > 1 is point-sharded by default")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: N independent problems, one per GPU; value = per-problem LM it/s")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end arapOptimization timing")
     ap.add_argument("--cpu-full-iteration", action="store_true",
                     help="CPU baseline: time the oracle's whole first LM iteration (all trials)")
@@ -290,10 +398,17 @@ def main():
     if args.workload == "ba":
         return main_ba(args, world, rank, gpu, backend)
 
-    sharded = world > 1 and args.sharded
+    wl = args.workload
+    spec = WORKLOADS[wl]
+    n = args.corr or spec["n"]
+    window = args.pair_window if args.pair_window >= 0 else spec.get("window", 0)
+    sharded = world > 1 and not args.replicas
+    plan = args.plan
+    if plan == "auto":
+        plan = "multifrontal" if (args.solver == "direct" or (wl == "c2" and not sharded)) else "iterative"
     t0 = time.perf_counter()
-    prob, prob_map = build_problem(args.corr, 1 if sharded else 1 + rank)
-    log(f"[rank {rank}] graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
+    prob, prob_map = build_workload(wl, n, 1 if sharded else 1 + rank, window)
+    log(f"[rank {rank}] {wl} graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
     ctx = capi.Context(gpu)
     if sharded:
         from deftri import dist as ddist
@@ -301,11 +416,14 @@ def main():
             ddist.init_rccl(ctx, rank, world)
         else:
             ctx.dist_set_transport(world, rank, ddist.torch_transport())
+    ctx.set_plan(plan)
+    ctx.set_jacobian_storage(1 if args.jacobian_fp32 else 0)
+    ctx.set_linear_solver(args.solver)
     t0 = time.perf_counter()
     ctx.upload(prob)
     ctx.set_lm_lanes(args.lanes)
-    ctx.set_linear_solver(args.solver)
-    log(f"[rank {rank}] upload + symbolic analysis {time.perf_counter() - t0:.1f}s")
+    info = ctx.plan_info()
+    log(f"[rank {rank}] upload ({info['plan']} plan) {time.perf_counter() - t0:.1f}s: {info}")
     analytic = args.analytic
 
     if args.warmup > 0:
@@ -322,111 +440,84 @@ def main():
     if world > 1:
         dist.barrier()
     log(f"[rank {rank}] {rep['iterations']} iterations / {rep['trials_total']} trials in {dt * 1e3:.1f} ms; "
-        f"chi2 {rep['chi2_initial']:.6e} -> {rep['chi2_final']:.6e}")
+        f"chi2 {rep['chi2_initial']:.6e} -> {rep['chi2_final']:.6e}; lambda {rep['lambda_final']:.3e}; "
+        f"pcg {rep['pcg_trials']} / failed {rep['pcg_fallbacks']}, {rep['pcg_iterations']} CG iterations")
     iters = rep["iterations"]
     if iters != args.steps:
         log(f"[rank {rank}] WARNING: LM terminated after {iters} of {args.steps} iterations")
+    # one problem (sharded): every rank ran the same iterations, the job takes the slowest rank;
+    # replicas: the slowest rank's time for its own problem (value = per-problem rate, never a sum)
+    t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
 
-    if sharded:      # one problem: every rank ran the same iterations; the job takes the slowest rank
-        t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
-        it_sum, tr_sum = iters, rep["trials_total"]
-    else:
-        t_max, it_sum, tr_sum = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
-
-    # profiled trial (HIP events on the solver stream), at the final lambda of the timed run
-    # (a collective on a sharded context: each rank times its own part of the same trial)
+    # profiled trial (HIP events on the solver stream) at the final lambda of the timed run (a
+    # collective on a sharded context: each rank times its own part of the same trial)
     stats = ctx.profile_trial(rep["lambda_final"])
-    pcg_prof = None
-    if "pcg_product" in stats:
-        # PCG steps: the dominant kernel is the product (HBM-bound row gathers); the factorization's
-        # update kernel is profiled too (fallback path, and the direct solver's roofline)
-        pp = stats["pcg_product"]
-        its = max(pp["launches"] - 1, 1)           # the last launch only runs the convergence test
-        gbs = pp["bytes"] / max(pp["ms"] * 1e-3, 1e-12) / 1e9
-        mf = "mf_lin" in stats                     # matrix-free product (b + diagonal blocks only)
-        pcg_prof = {"bound": "hbm", "kernel": "k_mf_product" if mf else "k_pcg_product", "achieved": round(gbs, 1),
-                    "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                    "traffic_unit": "bytes per launch", "bytes_per_launch": pp["bytes"] / its,
-                    "launches": pp["launches"], "avg_launch_us": round(1e3 * pp["ms"] / max(pp["launches"], 1), 3),
-                    "avg_active_launch_us": round(1e3 * pp["ms"] / its, 3),
-                    "cg_iterations": its, "lambda": rep["lambda_final"], "rank": rank}
-        for pm in sorted(ROOT.glob("profiles/*_pmc_*product.json")) if not sharded else []:
-            pj = json.loads(pm.read_text())
-            if abs(pj.get("bytes_per_launch_algorithmic", -1) - pcg_prof["bytes_per_launch"]) < 1e-6 * pcg_prof["bytes_per_launch"]:
-                pcg_prof["traffic"] = pj["traffic_bytes_per_launch"]
-                pcg_prof["traffic_source"] = pm.name
-        ctx.set_linear_solver("direct")
-        stats_f = ctx.profile_trial(rep["lambda_final"])
-        ctx.set_linear_solver(args.solver)
-    else:
-        stats_f = stats
-    upd = stats_f["update"]
-    factor_flops = rep["factor_flops_total"] if sharded else rep["factor_flops"]
-    achieved = upd["flops"] / (upd["ms"] * 1e-3) / 1e12
-    # HBM bytes of k_update per factorization from the committed rocprofv3 PMC pass (tools/gpu_pmc.sh +
-    # tools/pmc_summary.py), attached only when it was collected on this same plan
-    traffic = None
-    pmc = sorted(ROOT.glob("profiles/*_pmc_k_update.json"))
-    if pmc and not sharded:
-        pj = json.loads(pmc[-1].read_text())
-        if abs(pj.get("update_flops_per_factorization", -1) - upd["flops"]) < 1e-6 * upd["flops"]:
-            traffic = pj["traffic_bytes_per_factorization"]
-    roofline_f = {"bound": "mfma", "kernel": "k_update", "achieved": round(achieved, 3),
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP64_PEAK_TFLOPS, 4),
-                "peak_sustained_measured": MFMA_F64_SUSTAINED_TFLOPS,
-                "traffic": traffic, "traffic_unit": "bytes per factorization (all k_update launches)",
-                "launches": upd["launches"],
-                "avg_launch_us": round(1e3 * upd["ms"] / max(upd["launches"], 1), 3),
-                "flops_per_factorization": upd["flops"], "rank": rank}
-    roofline = pcg_prof if pcg_prof else roofline_f
-    trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
-    factor_trial_ms = {k: round(v["ms"], 3) for k, v in sorted(stats_f.items(), key=lambda kv: -kv[1]["ms"])}
+    roofline = product_roofline(stats, rep, ctx, rank) if args.solver == "pcg" else None
+    roofline_f, stats_f = None, None
+    if plan == "multifrontal" and not sharded:
+        if args.solver == "pcg":
+            ctx.set_linear_solver("direct")
+            stats_f = ctx.profile_trial(rep["lambda_final"])
+            ctx.set_linear_solver(args.solver)
+        else:
+            stats_f = stats
+        roofline_f = factor_roofline(stats_f, rank)
+    if roofline is None:
+        roofline = roofline_f
+    trial_ms = {k: round(v["ms"], 4) for k, v in sorted(stats.items(), key=lambda kv: -kv[1]["ms"])}
 
     cpu = None
+    trials_per_it = rep["trials_total"] / max(iters, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         t0 = time.perf_counter()
-        cpu = cpu_baseline(prob, ctx.vertex_order(), rep["trials_total"] / max(iters, 1), args.cpu_full_iteration)
+        if wl == "c2" and plan == "multifrontal":
+            cpu = cpu_baseline(prob, ctx.vertex_order(), trials_per_it, args.cpu_full_iteration)
+        elif wl == "c2":
+            cpu = None
+        else:
+            cpu = cpu_baseline_sample(wl, window, {"c3": 400, "c4": 400, "c5": 600}[wl], trials_per_it)
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     e2e = None
-    if world == 1 and not args.no_e2e:
+    if world == 1 and not args.no_e2e and wl == "c2":
         e2e = end_to_end(ctx, prob_map)
         log(f"end-to-end arapOptimization: {e2e}")
 
     if rank == 0:
         ms_per_step = 1e3 * t_max / max(iters, 1)
-        trials_per_it = tr_sum / max(it_sum, 1)
+        workload = ("C2" if n == 100000 else f"two-view-{n}") if wl == "c2" else \
+            (wl.upper() if n == spec["n"] else f"{wl.upper()}-slice-{n}x{spec['k']}")
         out = {
-            "metric": BASELINE_METRIC,
-            "value": it_sum / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
+            "metric": BASELINE_METRIC if wl == "c2" else f"LM iterations/sec + ms/iter, {wl.upper()}: {spec['desc']}",
+            "value": iters / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if sharded or world == 1 else "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "weak" if (world > 1 and not sharded) else "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "C2" if args.corr == 100000 else f"two-view-{args.corr}",
-                       "correspondences": args.corr, "views": 2,
+            "config": {"workload": workload, "correspondences_per_keyframe": n, "keyframes": spec["k"],
+                       "pairs": prob.n_pairs, "pair_window": window,
                        "points": prob.n_points, "arap_edges": len(prob.arap_pair), "unknowns": rep["n_unknowns"],
-                       "fronts": rep["n_fronts"], "nnz_factor": rep["nnz_factor"],
-                       "factor_gflop": round(factor_flops / 1e9, 3),
+                       "plan": info["plan"], "jacobian_storage": "fp32" if info.get("jacobian_fp32") else "fp64",
                        "jacobians": "analytic" if analytic else "g2o numeric (reference)",
+                       "step_solver": args.solver,
                        "trials_per_iteration": round(trials_per_it, 3),
                        "ms_per_trial": round(ms_per_step / max(trials_per_it, 1e-9), 3),
-                       "lm_lanes": rep["lanes"],
-                       "step_solver": args.solver if not sharded else "direct (point-sharded LDL^T)",
-                       "pcg_product": ("matrix-free" if "mf_lin" in stats else "assembled") if pcg_prof else None,
-                       "pcg_trials": rep["pcg_trials"], "pcg_fallbacks": rep["pcg_fallbacks"],
+                       "pcg_trials": rep["pcg_trials"], "pcg_failed_or_fallback": rep["pcg_fallbacks"],
                        "cg_iterations_per_pcg_trial": round(rep["pcg_iterations"] / max(rep["pcg_trials"], 1), 2),
-                       "trials_executed_per_iteration": round(rep["trials_executed"] / max(iters, 1), 3),
-                       "parallelism": (f"points{world}" if sharded else f"replicas{world}") if world > 1 else "single"},
+                       "ms_per_cg_iteration_profiled": round(roofline["cg_iteration_us"] / 1e3, 4)
+                       if roofline and "cg_iteration_us" in roofline else None,
+                       "chi2_initial": rep["chi2_initial"], "chi2_final": rep["chi2_final"],
+                       "lambda_final": rep["lambda_final"],
+                       "own_rows_rank0": info.get("own_rows"), "halo_rows_rank0": info.get("halo_rows"),
+                       "parallelism": (f"points{world}" if sharded else f"replicas{world}") if world > 1 else "single",
+                       "value_semantics": "one problem, all ranks" if (world == 1 or sharded)
+                       else "per-problem LM it/s of N independent problems (not summed)"},
             "roofline": roofline,
-            "roofline_factorization": roofline_f if pcg_prof else None,
+            "roofline_factorization": roofline_f if roofline is not roofline_f else None,
             "cpu_baseline": cpu,
-            "breakdown_ms": {"total": rep["ms_total"], "linearize": rep["ms_linearize"],
-                             "factor": rep["ms_factor"], "solve": rep["ms_solve"], "update": rep["ms_update"],
-                             "note": "factor/solve/update of sequential trials only with DEFTRI_TRIAL_EVENTS=1",
-                             "pcg": rep["ms_pcg"]},
+            "breakdown_ms": {"total": rep["ms_total"], "linearize": rep["ms_linearize"], "pcg": rep["ms_pcg"]},
             "trial_kernel_ms": trial_ms,
-            "factorization_trial_kernel_ms": factor_trial_ms if pcg_prof else None,
+            "factorization_trial_kernel_ms": ({k: round(v["ms"], 3) for k, v in sorted(stats_f.items(), key=lambda kv: -kv[1]["ms"])}
+                                              if stats_f is not None and stats_f is not stats else None),
             "end_to_end_arap_optimization": e2e,
         }
         print(json.dumps(out), flush=True)

@@ -131,7 +131,9 @@ typedef struct deftri_report {
     double  ms_linearize;            /* residuals + Jacobians + H/b assembly */
     double  ms_factor;               /* multifrontal LDL^T numeric factorization */
     double  ms_solve;                /* forward/backward substitution */
-    double  ms_update;               /* oplus + chi2 re-evaluation */
+    double  ms_update;               /* oplus + chi2 re-evaluation; the three are -1 (not measured) for
+                                        sequential trials unless DEFTRI_TRIAL_EVENTS=1 and on the iterative
+                                        plan (per-trial events cost ~6 us of stream time each) */
     /* sizes of the sparse factorization */
     int64_t n_unknowns;
     int64_t nnz_factor;              /* entries of L (incl. dense fronts' boundary rows) */
@@ -154,9 +156,14 @@ typedef struct deftri_report {
        fell back to the factorization, and the device time of the PCG solves (ms, host-timed around
        the solve's final synchronization) */
     int32_t pcg_trials;
-    int32_t pcg_fallbacks;
+    int32_t pcg_fallbacks;           /* multifrontal plan: trials solved by the LDL^T instead; iterative
+                                        plan: trials whose PCG failed (rejected, as a failed g2o solve) */
     int64_t pcg_iterations;
     double  ms_pcg;
+    /* round 3 */
+    int32_t pcg_given_up;            /* multifrontal plan: 1 when two consecutive fallbacks sent the rest of
+                                        the call's trials straight to the LDL^T */
+    int32_t plan;                    /* DEFTRI_PLAN_MULTIFRONTAL / DEFTRI_PLAN_ITERATIVE */
 } deftri_report;
 
 /* ---- context ---------------------------------------------------------------------- */
@@ -458,6 +465,11 @@ int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, cons
 /* MapPoint id of every point vertex of the last graph deftri_arap_build_graph built (n = its
    n_points): the write-back key of :974-990. */
 int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n);
+/* Keyframe pairs of the graphs this context builds (deftri_arap_build_graph / _optimization): 0
+   (default) every pair (a, b > a) in map order, as the reference's loop (g2oBundleAdjustment.cc:
+   640-645); w > 0 only pairs with b - a <= w (a sliding window: the documented deviation used for
+   BASELINE C5's 20 keyframes, 19 consecutive pairs at w = 1). */
+int deftri_set_pair_window(deftri_ctx *ctx, int32_t window);
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,
                             double arap_weight, float depth_error,
                             const deftri_problem_desc **desc_out);

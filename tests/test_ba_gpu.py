@@ -9,7 +9,7 @@ fp64 level.  Tolerances:
   * LM trajectory (gauge fixed)      chi2 per iteration rel 1e-6 and identical trial counts until chi2
                                     stalls at the fp32 noise floor; final chi2 rel 1e-6, poses / points
                                     within 1e-5 (1e-7..1e-6 observed)
-  * gauge-free BA (only KF 0 fixed) chi2 rel 1e-4, inlier RMSE within 5e-3 px (scale-gauge drift)
+  * gauge-free BA (only KF 0 fixed) chi2 rel 1e-4, inlier RMSE within 1e-4 px (scale-gauge drift)
   * map-level flows (bundle, local, pose-only): identical outlier decisions, slot edits and
                                     observation tables; pose-only pose within 1e-5 after the fp32
                                     write-back; bundle / local (scale gauge free) chi2 rel 1e-4

@@ -9,8 +9,10 @@
     golden scenes' weakly damped steps, and ten LM iterations amplify it to ~2e-6 in chi2),
     (nearly) every trial solved by PCG at budget 4096 (the golden scenes' weakly damped steps take
     ~3000-4200 CG iterations; the default budget hands those to the LDL^T)
-  * budget exhausted (max_iterations = 1): every trial falls back to the LDL^T, trajectory unchanged
-  * default (cost-model) budget: the mix of PCG and LDL^T steps matches the oracle the same way
+  * budget exhausted (max_iterations = 1): two trials fall back, then the call gives PCG up and the
+    rest go straight to the LDL^T; trajectory unchanged
+  * default (cost-model) budget: on the golden scenes PCG is given up after two fallbacks; the
+    trajectory matches the oracle the same way
   * C2 size (100k correspondences): PCG vs LDL^T LM chi2 per iteration rel 1e-9 with the same trials;
     repeated PCG runs bit-identical (fixed-order reductions)
 """
@@ -68,7 +70,13 @@ def test_pcg_lm_trajectory_matches_oracle(pcg_ctx, golden_cases):
             assert r["iterations"] == ref["iterations"]
             assert r["trials_total"] == ref["trials_total"]
             np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)
-            assert r["pcg_trials"] + r["pcg_fallbacks"] == r["trials_total"]
+            if budget:
+                assert r["pcg_trials"] + r["pcg_fallbacks"] == r["trials_total"] and not r["pcg_given_up"]
+            else:
+                # the cost-model budget (~20 here) cannot solve these weakly damped 728-unknown steps:
+                # after two consecutive fallbacks the call stops paying for PCG
+                assert r["pcg_given_up"] == 1 and r["pcg_fallbacks"] >= 2
+                assert r["pcg_trials"] + r["pcg_fallbacks"] < r["trials_total"]
             if budget:
                 assert r["pcg_trials"] >= r["trials_total"] - 2 and r["pcg_iterations"] > 0
 
@@ -118,7 +126,8 @@ def test_pcg_budget_falls_back_to_ldlt(pcg_ctx, golden_cases):
     pcg_ctx.set_linear_solver("pcg", max_iterations=1)
     r = pcg_ctx.solve_lm(5, analytic=True)
     ref = oracle.solve_lm(p, 5, analytic=True)["report"]
-    assert r["pcg_fallbacks"] == r["trials_total"] and r["pcg_trials"] == 0
+    # two fallbacks in a row, then the rest of the call goes straight to the LDL^T
+    assert r["pcg_fallbacks"] == 2 and r["pcg_trials"] == 0 and r["pcg_given_up"] == 1
     assert r["trials_total"] == ref["trials_total"]
     np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
 

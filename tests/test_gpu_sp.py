@@ -1,0 +1,240 @@
+"""The iterative plan (deftri_set_plan ITERATIVE: point-sharded matrix-free PCG, csrc/spcg.h) on the
+device, against the oracle (oracle/deftri_oracle.c: the reference LM with an exact SimplicialLDLT
+step) and against the multifrontal plan.
+
+Tolerances (the PCG stop test is 1e-12 on the recurrence residual):
+  * gradient b and diag(H) rel 1e-13 vs the oracle's assembly
+  * one damped solve: residual ||(H + lam I) x - b|| / ||b|| < 1e-11, rel 1e-8 vs the exact solve
+  * LM trajectories (golden scenes, budget 4096): identical trial and iteration counts, chi2 per
+    iteration rel 1e-5 (the golden scenes' weakly damped steps, as tests/test_gpu_pcg.py)
+  * all-pairs 8-keyframe scene (BASELINE C3/C4 shape at 100 x 8; g2oBundleAdjustment.cc:640-953):
+    identical trials, chi2 rel 1e-8 analytic / 1e-6 g2o numeric Jacobians
+  * two-view 20k: iterative vs multifrontal plan, identical trials, chi2 rel 1e-8
+  * sharded: 2 and 3 ranks sharing the GPU (gloo host transport; RCCL in bench.py) on a two-view and
+    an all-pairs 8-keyframe scene: identical trials, chi2 rel 1e-8 analytic (1e-6 numeric), gathered
+    state rel 1e-8 against the one-rank plan
+  * fp32 Jacobian storage: identical trial counts on the golden-size all-pairs scene, RMSE within
+    1e-4 px of the fp64 run"""
+import os
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN
+from deftri import capi, sim
+from deftri.problem import Problem
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300)
+
+
+def mv_problem(n=100, k=8, seed=1):
+    m, _ = sim.simulate_multi_view(n=n, k=k, seed=seed)
+    host = capi.Context(-1)
+    p = host.build_graph(m, 1.0, 1e7, np.float32(0.3))
+    host.close()
+    return p
+
+
+def tv_problem(n, seed=2):
+    m, _ = sim.simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True)
+    host = capi.Context(-1)
+    p = host.build_graph(m, 1.0, 2e5, np.float32(0.003))
+    host.close()
+    return p
+
+
+def reprojection_rms(p, pts):
+    """RMS over the reprojection edges of |obs - KB8(T_cw p)| (the oracle's fp32 projection), px."""
+    import copy
+    q = copy.copy(p)
+    q.points = np.ascontiguousarray(pts, np.float64)
+    e_rep, _, _ = oracle.edge_errors(q)
+    return float(np.sqrt(np.mean(e_rep ** 2)))
+
+
+@pytest.fixture
+def it_ctx(gpu_ctx):
+    gpu_ctx.set_plan("iterative")
+    gpu_ctx.set_linear_solver("pcg", max_iterations=4096)
+    yield gpu_ctx
+    gpu_ctx.set_plan("auto")
+    gpu_ctx.set_linear_solver("pcg")
+    gpu_ctx.set_jacobian_storage(0)
+
+
+def test_iterative_gradient_and_solve_match_oracle(it_ctx, golden_cases):
+    for p in [Problem.load(GOLDEN / g / "problem.npz") for g in golden_cases] + [mv_problem()]:
+        it_ctx.upload(p)
+        assert it_ctx.plan_info()["plan"] == "iterative"
+        b_ref, H_ref, _ = oracle.linearize(p, analytic=True, dense=True)
+        b, d = it_ctx.gradient()
+        assert rel(b, b_ref) < 1e-13 and rel(d, np.diag(H_ref)) < 1e-13
+        dmax = np.abs(np.diag(H_ref)).max()
+        for lam_rel in (1e-2, 1.0):
+            lam = lam_rel * dmax
+            x = it_ctx.damped_solve(lam, b_ref, solver="pcg", max_iterations=4096)
+            its, ok = it_ctx.last_step_info()
+            assert ok and its > 0
+            A = H_ref + lam * np.eye(len(b_ref))
+            assert np.linalg.norm(A @ x - b_ref) / np.linalg.norm(b_ref) < 1e-11
+            assert rel(x, oracle.damped_solve(p, lam, b_ref)) < 1e-8
+
+
+def test_iterative_lm_matches_oracle_golden(it_ctx, golden_cases):
+    for g in golden_cases:
+        p = Problem.load(GOLDEN / g / "problem.npz")
+        it_ctx.upload(p)
+        r = it_ctx.solve_lm(10, analytic=True)
+        ref = oracle.solve_lm(p, 10, analytic=True)["report"]
+        assert r["iterations"] == ref["iterations"] and r["trials_total"] == ref["trials_total"]
+        np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-5)
+        assert r["pcg_fallbacks"] == 0 and r["pcg_trials"] == r["trials_total"]
+
+
+@pytest.mark.parametrize("analytic,tol", [(True, 1e-8), (False, 1e-6)])
+def test_iterative_lm_all_pairs_matches_oracle(it_ctx, analytic, tol):
+    """8 keyframes, all 28 pairs (the reference's pair loop), 100 correspondences per keyframe."""
+    p = mv_problem()
+    assert p.n_pairs == 28 and p.n_scales == 56
+    it_ctx.upload(p)
+    n_it = 6 if analytic else 4
+    r = it_ctx.solve_lm(n_it, analytic=analytic)
+    res = oracle.solve_lm(p, n_it, analytic=analytic)
+    ref = res["report"]
+    assert r["iterations"] == ref["iterations"] and r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=tol)
+    assert r["pcg_trials"] == r["trials_total"]
+    pts, sc, tg = it_ctx.download()
+    assert np.abs(pts - res["points"]).max() <= 1e-6 * max(np.abs(res["points"]).max(), 1.0)
+    np.testing.assert_allclose(sc, res["scales"], rtol=1e-6)
+
+
+def test_iterative_matches_multifrontal_two_view(gpu_ctx):
+    p = tv_problem(20000, seed=1)
+    out = {}
+    for plan in ("multifrontal", "iterative"):
+        gpu_ctx.set_plan(plan)
+        gpu_ctx.upload(p)
+        gpu_ctx.set_linear_solver("pcg", max_iterations=4096)
+        out[plan] = gpu_ctx.solve_lm(6, analytic=False)
+        assert gpu_ctx.plan_info()["plan"] == plan
+    gpu_ctx.set_plan("auto")
+    gpu_ctx.set_linear_solver("pcg")
+    a, b = out["iterative"], out["multifrontal"]
+    assert a["trials_total"] == b["trials_total"] and a["pcg_fallbacks"] == b["pcg_fallbacks"] == 0
+    np.testing.assert_allclose(a["chi2_iter"], b["chi2_iter"], rtol=1e-8)
+
+
+def test_iterative_repeatable_and_profiled(it_ctx):
+    p = tv_problem(5000, seed=3)
+    it_ctx.upload(p)
+    r1 = it_ctx.solve_lm(3, analytic=False)
+    pts1, _, _ = it_ctx.download()
+    it_ctx.reset_state()
+    r2 = it_ctx.solve_lm(3, analytic=False)
+    pts2, _, _ = it_ctx.download()
+    assert r1["chi2_iter"] == r2["chi2_iter"] and np.array_equal(pts1, pts2)   # fixed-order sums
+    st = it_ctx.profile_trial(r1["lambda_final"])
+    for k in ("sp_glin_rows", "sp_setup", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update"):
+        assert k in st and st[k]["launches"] > 0, k
+    assert st["sp_phase1"]["bytes"] > 0 and st["sp_phase2"]["bytes"] > 0
+    assert "update" not in st and "hchunk" not in st          # no factorization, no assembled H
+
+
+def test_fp32_jacobian_storage(it_ctx):
+    """C5's precision sweep on the timed path at test size: fp32-stored ARAP J in the product."""
+    p = mv_problem(n=80, k=5, seed=4)
+    res = {}
+    for fp32 in (0, 1):
+        it_ctx.set_jacobian_storage(fp32)
+        it_ctx.upload(p)
+        assert it_ctx.plan_info()["jacobian_fp32"] == fp32
+        r = it_ctx.solve_lm(5, analytic=False)
+        res[fp32] = (r, it_ctx.download()[0])
+    assert res[0][0]["trials_total"] == res[1][0]["trials_total"]
+    np.testing.assert_allclose(res[1][0]["chi2_iter"], res[0][0]["chi2_iter"], rtol=1e-3)
+    # reprojection RMS (px) of the final points, fp32 vs fp64 storage
+    e = [reprojection_rms(p, pts) for pts in (res[0][1], res[1][1])]
+    assert abs(e[0] - e[1]) < 1e-4, e
+
+
+# ---- sharded: ranks sharing the GPU over the gloo host transport ----------------------------------
+def _problem(kind):
+    return tv_problem(4000, seed=2) if kind == "tv" else mv_problem(n=120, k=8, seed=2)
+
+
+def _worker(rank, world, port, kind, q):
+    import faulthandler
+    import sys
+    faulthandler.enable()
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deftri import capi as c
+    from deftri import dist as ddist
+    p = _problem(kind)
+    ctx = c.Context(0)
+    ctx.dist_set_transport(world, rank, ddist.torch_transport())
+    ctx.set_linear_solver("pcg", max_iterations=4096)
+    ctx.upload(p)
+    info = ctx.plan_info()
+    res = {}
+    for analytic in (True, False):
+        ctx.reset_state()
+        r = ctx.solve_lm(4, analytic=analytic)
+        print(f"[rank {rank}] {kind} analytic={analytic}: {r['trials_total']} trials chi2 {r['chi2_final']:.12e}",
+              file=sys.stderr, flush=True)
+        pts, sc, tg = ctx.download()
+        owner = ctx.vertex_owner()
+        P, S, T = ddist.gather_state(p, owner, rank, pts, sc, tg, lambda a: dist.all_reduce(torch.from_numpy(a)))
+        res[analytic] = (r, P, S, T)
+    q.put((rank, info, res))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["tv", "mv"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_iterative_matches_one_rank(kind, world):
+    cm = mp.get_context("spawn")
+    q = cm.Queue()
+    port = 28900 + 31 * world + (7 if kind == "mv" else 0) + os.getpid() % 300
+    procs = [cm.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = {}
+    for _ in procs:
+        rank, info, res = q.get(timeout=300)
+        out[rank] = (info, res)
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    p = _problem(kind)
+    ref = {}
+    with capi.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.set_linear_solver("pcg", max_iterations=4096)
+        ctx.upload(p)
+        for analytic in (True, False):
+            ctx.reset_state()
+            ref[analytic] = (ctx.solve_lm(4, analytic=analytic), *ctx.download())
+    assert sum(out[r][0]["own_rows"] for r in range(world)) == p.n_points
+    for r in range(world):
+        info = out[r][0]
+        assert info["plan"] == "iterative" and info["nranks"] == world and info["halo_rows"] > 0
+    for analytic, tol in ((True, 1e-8), (False, 1e-6)):
+        rr, pts, sc, tg = ref[analytic]
+        for r in range(world):
+            rep, P, S, T = out[r][1][analytic]
+            assert rep["nranks"] == world and rep["rank"] == r
+            assert rep["iterations"] == rr["iterations"] and rep["trials_total"] == rr["trials_total"]
+            np.testing.assert_allclose(rep["chi2_iter"], rr["chi2_iter"], rtol=tol)
+            assert np.abs(P - pts).max() <= tol * np.abs(pts).max()
+            np.testing.assert_allclose(S, sc, rtol=tol)

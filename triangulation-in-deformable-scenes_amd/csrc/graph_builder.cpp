@@ -279,7 +279,7 @@ void procrustes_rotation(const double S[9], double R[9]) {
 }
 
 bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
-                      GraphResult &g, std::string &err) {
+                      GraphResult &g, std::string &err, int pair_window) {
     g = GraphResult();
     int K = map.n_keyframes;
     if (K < 0 || (K > 0 && !map.keyframes)) { err = "bad map"; return false; }
@@ -299,6 +299,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     int32_t rot_base = 0;
     for (int a = 0; a < K; a++) {
         for (int b = a + 1; b < K; b++) {
+            if (pair_window > 0 && b - a > pair_window) continue;
             const deftri_keyframe &kf1 = map.keyframes[b];   // pKF1 = k2->second
             const deftri_keyframe &kf2 = map.keyframes[a];   // pKF2 = k1->second
             int32_t q = (int32_t)g.pair_area.size();

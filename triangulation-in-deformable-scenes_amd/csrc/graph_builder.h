@@ -25,8 +25,10 @@ struct GraphResult {
     std::vector<int32_t> pair_hull;           // convex hull size per pair
 };
 
+// pair_window > 0: only keyframe pairs (a, b) with b - a <= pair_window in map order (the
+// sliding-window deviation of BASELINE C5; 0 = every pair, the reference's loop :640-645)
 bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
-                      GraphResult &g, std::string &err);
+                      GraphResult &g, std::string &err, int pair_window = 0);
 
 void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<double> &points,
                     const std::vector<double> &scales, const std::vector<double> &tg, double *optimization_update);

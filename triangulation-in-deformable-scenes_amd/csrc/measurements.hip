@@ -181,7 +181,10 @@ extern "C" int deftri_measure_sim_absolute_map_errors(int32_t device, const deft
         hipLaunchKernelGGL(dev::k_abs_terms, dim3(nblk(pairs, 256)), dim3(256), 0, st, (int)pairs, d1, d2, dg, dm, terms);
     double s[5] = {0, 0, 0, 0, 0};
     if (sums(terms, pairs, 5, part, dout, s, st)) return DEFTRI_E_HIP;
-    // the reference's float arithmetic on the totals (:65-79); point_count_in_kf = size / 2.0 -> int
+    // Deviation (documented): the reference accumulates these sums in float, one point at
+    // a time (Measurements.cc:17-53); here the per-point terms are summed in fp64 in a fixed order and
+    // only the totals are cast to float before the reference's float divisions (:65-79) — a closer
+    // sum, equal to the float one to its rounding at test sizes.  point_count_in_kf = size / 2.0 -> int
     const float tm = (float)s[0], te1 = (float)s[1], te2 = (float)s[2];
     const float te = (float)(s[1] + s[2]), tsq = (float)(s[3] + s[4]);
     const int in_kf = (int)(point_count / 2.0);

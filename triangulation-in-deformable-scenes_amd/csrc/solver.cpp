@@ -172,6 +172,7 @@ struct deftri_ctx {
     bool sp_on = false;
     SpTransport *sp_tr = nullptr;           // RCCL / callback transport of `sp` (owned)
     int small_direct = 0;                   // PCG skipped for this problem (too small to win, see upload)
+    int pair_window = 0;                    // deftri_set_pair_window (graph builds)
 };
 
 namespace {
@@ -328,6 +329,21 @@ uint64_t structure_hash(const deftri_problem_desc &d) {
     return h;
 }
 
+// the hash is only a pre-filter: the counts and every index array must match exactly before a plan is
+// reused (a collision would scatter H into the wrong blocks)
+bool same_structure(const deftri_problem_desc &a, const deftri_problem_desc &b) {
+    if (a.n_points != b.n_points || a.n_pairs != b.n_pairs || a.n_scales != b.n_scales || a.n_cams != b.n_cams ||
+        a.n_rep != b.n_rep || a.n_depth != b.n_depth || a.n_arap != b.n_arap || a.n_rot != b.n_rot)
+        return false;
+    auto eq = [](const int32_t *x, const int32_t *y, int64_t n) {
+        return n == 0 || (x && y && std::memcmp(x, y, sizeof(int32_t) * (size_t)n) == 0);
+    };
+    return eq(a.rep_point, b.rep_point, a.n_rep) && eq(a.rep_cam, b.rep_cam, a.n_rep) &&
+           eq(a.dep_point, b.dep_point, a.n_depth) && eq(a.dep_scale, b.dep_scale, a.n_depth) &&
+           eq(a.dep_cam, b.dep_cam, a.n_depth) && eq(a.arap_pts, b.arap_pts, 4 * (int64_t)a.n_arap) &&
+           eq(a.arap_pair, b.arap_pair, a.n_arap) && eq(a.arap_rot, b.arap_rot, 2 * (int64_t)a.n_arap);
+}
+
 // same structure as the uploaded plan: copy the values (state, cameras, measurements, weights,
 // rotations) into the existing device buffers
 int refresh_values(deftri_ctx *ctx, const HostProblem &h) {
@@ -357,10 +373,11 @@ bool mf_wanted() {
 // the PCG budget: CG iterations that cost about one factorization + substitution, from plan sizes
 // only (deterministic: the same problem always takes the same path).  Rates measured at C2: the
 // LDL^T trial ~7 TF/s + ~50 us per tree level, a CG iteration ~2 TB/s of its product's bytes + ~15 us
-// of launch latency
+// of launch latency, plus a quarter of a host round trip (~40 us; pcg_poll reads the record every
+// 4 iterations once the predicted count is exceeded)
 int pcg_budget(const Symbolic &S, double product_bytes) {
     const double t_fac = S.factor_flops / 7e9 + 0.05 * S.nlevels;   // ms
-    const double t_it = product_bytes / 2e9 + 0.015;
+    const double t_it = product_bytes / 2e9 + 0.015 + 0.04 / 4;
     return (int)std::min<double>(kPcgMaxIt, std::max(8.0, std::ceil(t_fac / t_it)));
 }
 
@@ -1101,6 +1118,12 @@ int deftri_debug_sp_product(deftri_ctx *ctx, const deftri_problem_desc *desc, co
     return 0;
 }
 
+int deftri_set_pair_window(deftri_ctx *ctx, int32_t window) {
+    if (!ctx || window < 0) return DEFTRI_E_ARG;
+    ctx->pair_window = window;
+    return 0;
+}
+
 int deftri_set_plan(deftri_ctx *ctx, int32_t plan) {
     if (!ctx || plan < DEFTRI_PLAN_AUTO || plan > DEFTRI_PLAN_ITERATIVE) return DEFTRI_E_ARG;
     ctx->plan_mode = plan;
@@ -1321,8 +1344,12 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
             for (int j = 0; j < its; j++) {
                 launch_pcg_heavy(G, j, ctx->L.hval, lambda, ctx->st);
                 launch_pcg_update(G, j, lambda, ctx->d_dx, ctx->st);
+                // the product after the last update only runs the convergence test: not profiled, so
+                // the product's statistics cover exactly the `its` active launches
+                if (j + 1 == its) set_profiler(nullptr);
                 launch_pcg_product(G, j + 1, ctx->L.hval, lambda, ctx->st);
             }
+            set_profiler(&prof);
         }
     }
     if (!solved) {
@@ -1407,7 +1434,7 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     }
     const uint64_t hsh = structure_hash(*desc);
     static const bool no_cache = std::getenv("DEFTRI_NO_PLAN_CACHE") != nullptr;
-    if (ctx->have && ctx->analysed && hsh == ctx->plan_hash && !no_cache) {
+    if (ctx->have && ctx->analysed && hsh == ctx->plan_hash && !no_cache && same_structure(ctx->hp.d, *desc)) {
         copy_host(ctx->hp, desc);
         if (ctx->dist()) subset_edges(ctx->hp, ctx->S.dist, ctx->hloc);
         rc = refresh_values(ctx, ctx->dist() ? ctx->hloc : ctx->hp);
@@ -1610,7 +1637,12 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         if (nlanes < 1) return fail(ctx, DEFTRI_E_HIP, "lane allocation failed: " + ctx->err);
     }
     R.lanes = nlanes;
-    const bool pcg = nlanes == 1 && use_pcg(ctx);
+    // PCG steps; after kPcgGiveUp consecutive fallbacks in one call the remaining trials go straight
+    // to the LDL^T (small, weakly damped problems where CG cannot win: their steps take thousands of
+    // iterations); deterministic, the same problem always takes the same path
+    bool pcg = nlanes == 1 && use_pcg(ctx);
+    int consec_fallbacks = 0;
+    constexpr int kPcgGiveUp = 2;
     for (it = 0; it < prm->n_iterations; it++) {
         hipEventRecord(ctx->ev[0], ctx->st);
         if ((rc = eval_chi2_dev(ctx, true, analytic, 0))) return rc;   // computeActiveErrors + linearizeOplus
@@ -1700,6 +1732,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                                    restore_pending);
                 restore_pending = false;
             } else {
+                if (restore_pending) { pop_state(ctx); restore_pending = false; }   // PCG just given up
                 push_state(ctx);
                 HIPOK(hipMemsetAsync(L.flag, 0, sizeof(int), ctx->st));
             }
@@ -1759,8 +1792,9 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
                 }
                 R.ms_pcg += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
                 R.pcg_iterations += its;
-                if (solved) R.pcg_trials++;
+                if (solved) { R.pcg_trials++; consec_fallbacks = 0; }
                 else R.pcg_fallbacks++;
+                if (!solved && ++consec_fallbacks >= kPcgGiveUp) { pcg = false; R.pcg_given_up = 1; }
                 if (prm->verbose)
                     std::fprintf(stderr, "[deftri] pcg lambda %.6e iterations %d %s\n", lambda, its, solved ? "converged" : "-> LDL^T");
                 if (!solved) trial_ev(ctx, ctx->ev[2], ctx->st);
@@ -1824,6 +1858,8 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     R.iterations = it;
     R.lambda_final = lambda;
     R.ms_linearize = t_lin; R.ms_factor = t_fac; R.ms_solve = t_sol; R.ms_update = t_upd;
+    if (nlanes == 1 && !trial_events_on()) R.ms_factor = R.ms_solve = R.ms_update = -1.0;   // not measured
+    R.plan = DEFTRI_PLAN_MULTIFRONTAL;
     R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return 0;
 }
@@ -2081,7 +2117,7 @@ int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_w
                             float depth_error, const deftri_problem_desc **desc_out) {
     if (!ctx || !map || !desc_out) return DEFTRI_E_ARG;
     std::string err;
-    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err))
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window))
         return fail(ctx, DEFTRI_E_GRAPH, err);
     *desc_out = &ctx->graph.desc;
     return 0;
@@ -2100,7 +2136,7 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
     (void)global_weight; (void)alpha; (void)beta;   // stored but unused by the reference edges
     if (!ctx || !map) return DEFTRI_E_ARG;
     std::string err;
-    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err))
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window))
         return fail(ctx, DEFTRI_E_GRAPH, err);
     int rc = deftri_problem_upload(ctx, &ctx->graph.desc);
     if (rc) return rc;

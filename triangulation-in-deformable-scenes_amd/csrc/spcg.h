@@ -203,6 +203,7 @@ class SpSolver {
     int budget() const;
     int lin_iteration(bool analytic, bool want_max, bool &ok);
     int eval_chi2(bool analytic, int slot, const SumJob *extra);
+    void cg_setup(double lambda, const double *rhs);
     void cg_chain(double lambda, int from, int to);
     int cg_tail(int n);
     int halo(int width, double *vec, bool zp);

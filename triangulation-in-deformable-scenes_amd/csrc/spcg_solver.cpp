@@ -288,6 +288,13 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
     return 0;
 }
 
+// the solve's setup (preconditioner at lambda, r = rhs, (z, p) = (M r, 0), x = 0); sharded: the
+// boundary rows' (z, p) to the ranks whose edges read them, as after every CG update
+void SpSolver::cg_setup(double lambda, const double *rhs) {
+    sp_launch_setup(G, rhs, lambda, st_);
+    if (nranks_ > 1) halo(6, reinterpret_cast<double *>(G.zp), true);
+}
+
 // CG iterations [from, to) at lambda
 void SpSolver::cg_chain(double lambda, int from, int to) {
     const bool dist = nranks_ > 1;
@@ -327,7 +334,7 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
     G.max_it = mx;
     G.tol2 = tol * tol;
     SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (mx + 2)), st_));
-    sp_launch_setup(G, rhs, lambda, st_);
+    cg_setup(lambda, rhs);
     int j = 0;
     int n = std::min(std::max(2, last_its + 1), mx);
     for (;;) {
@@ -415,7 +422,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 return 0;
             };
             auto t0p = std::chrono::steady_clock::now();
-            sp_launch_setup(G, G.b, lambda, st_);
+            cg_setup(lambda, G.b);
             const int n = std::min(std::max(2, last_its + 1), mx);
             cg_chain(lambda, 0, n);
             int j = n;
@@ -498,6 +505,8 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     R.iterations = it;
     R.lambda_final = lambda;
     R.ms_linearize = t_lin;
+    R.ms_factor = R.ms_solve = R.ms_update = -1.0;           // no factorization; not split
+    R.plan = DEFTRI_PLAN_ITERATIVE;
     R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     return 0;
 }
@@ -604,7 +613,7 @@ int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
     if ((rc = pcg_solve(lambda, G.b, solved, its))) return rc;
     set_profiler(&prof);
     SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (G.max_it + 2)), st_));
-    sp_launch_setup(G, G.b, lambda, st_);
+    cg_setup(lambda, G.b);
     cg_chain(lambda, 0, its);
     rc = cg_tail(its);
     set_profiler(nullptr);

@@ -49,6 +49,7 @@ def load():
         "deftri_set_linear_solver": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32]),
         "deftri_last_step_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
         "deftri_set_plan": (C.c_int, [C.c_void_p, C.c_int32]),
+        "deftri_set_pair_window": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_set_jacobian_storage": (C.c_int, [C.c_void_p, C.c_int32]),
         "deftri_get_plan_info": (C.c_int, [C.c_void_p, P(_abi.PlanInfo)]),
         "deftri_debug_sp_product": (C.c_int, [C.c_void_p, P(_abi.ProblemDesc), P(C.c_double), P(C.c_double),
@@ -134,7 +135,7 @@ EXPORTED = [
     "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream",
     "deftri_measure_sim_absolute_map_errors", "deftri_measure_relative_map_errors", "deftri_dist_owned_edges",
     "deftri_debug_plan_solve_dist", "deftri_set_plan", "deftri_set_jacobian_storage", "deftri_get_plan_info",
-    "deftri_debug_sp_product",
+    "deftri_debug_sp_product", "deftri_set_pair_window",
 ]
 
 
@@ -255,6 +256,10 @@ class Context:
         code = {"auto": _abi.DEFTRI_PLAN_AUTO, "multifrontal": _abi.DEFTRI_PLAN_MULTIFRONTAL,
                 "iterative": _abi.DEFTRI_PLAN_ITERATIVE}[plan]
         self._check(self.lib.deftri_set_plan(self.h, code))
+
+    def set_pair_window(self, window):
+        """Graph builds: 0 every keyframe pair (the reference), w > 0 pairs at most w apart in map order."""
+        self._check(self.lib.deftri_set_pair_window(self.h, int(window)))
 
     def set_jacobian_storage(self, fp32):
         """Iterative plan: the ARAP Jacobians the product reads in fp32 (1) or fp64 (0, default)."""

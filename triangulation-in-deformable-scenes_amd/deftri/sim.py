@@ -235,6 +235,101 @@ def simulate_multi_view(n=1000, k=8, seed=0, kb8=DRUNKARD_KB8, radius=0.12, rep_
     return m, {"base": base}
 
 
+class ArrayMap:
+    """A Map held as per-keyframe arrays (slot i of every keyframe = correspondence i, MapPoint id
+    k * n + i), for scenes too large for one Python object per MapPoint (C3-C5 sizes).  Exposes the
+    same C view as Map.to_c (keyframes in the libstdc++ unordered_map order: reverse insertion)."""
+
+    def __init__(self, kfs, kb8, inv_sigma2):
+        self.kfs = kfs                 # list of dicts: id, pose (SE3f), uv [n,2], depth [n], pos [n,3] f32
+        self.kb8 = np.asarray(kb8, np.float32)
+        self.inv_sigma2 = np.asarray(inv_sigma2, np.float32)
+
+    @property
+    def n_points(self):
+        return sum(len(k["pos"]) for k in self.kfs)
+
+    def to_c(self):
+        from . import _abi
+        order = list(reversed(range(len(self.kfs))))
+        kfs = (_abi.KeyFrameC * len(order))()
+        keep = {"kfs": kfs, "arrays": []}
+        for n, k in enumerate(order):
+            kf, c = self.kfs[k], kfs[n]
+            ns = len(kf["pos"])
+            c.id = kf["id"]
+            c.pose[:] = list(kf["pose"].as7())
+            c.kb8[:] = [float(v) for v in self.kb8]
+            c.n_scales = len(self.inv_sigma2)
+            c.inv_sigma2 = _abi.ptr(self.inv_sigma2, _abi.f32)
+            c.depth_scale = 1.0
+            c.n_slots = ns
+            pid = np.arange(ns, dtype=np.int64) + np.int64(kf["id"]) * ns
+            pos = np.ascontiguousarray(kf["pos"], np.float32)
+            obs = np.arange(ns, dtype=np.int32)
+            uv = np.ascontiguousarray(kf["uv"], np.float32)
+            octv = np.zeros(ns, np.int32)
+            dep = np.ascontiguousarray(kf["depth"], np.float32)
+            c.point_id, c.point_pos, c.obs_index = _abi.ptr(pid, _abi.i64), _abi.ptr(pos, _abi.f32), _abi.ptr(obs, _abi.i32)
+            c.kp_uv, c.kp_octave, c.depth = _abi.ptr(uv, _abi.f32), _abi.ptr(octv, _abi.i32), _abi.ptr(dep, _abi.f32)
+            c.n_obs = ns
+            keep["arrays"].append((k, pid, pos, obs, uv, octv, dep))
+        m = _abi.MapC()
+        m.n_keyframes = len(order)
+        m.keyframes = C_cast(kfs)
+        m.global_t[:] = [0, 0, 0, 1, 0, 0, 0]
+        m.n_global = 0
+        return m, keep
+
+
+def C_cast(kfs):
+    import ctypes
+    from . import _abi
+    return ctypes.cast(kfs, ctypes.POINTER(_abi.KeyFrameC))
+
+
+def multi_view_arrays(n=1000, k=8, seed=0, kb8=DRUNKARD_KB8, radius=0.12, rep_error=1.0, decimals=1,
+                      depth_error=3.0, deform=0.0025, noise3d=0.004, scale_scene=True):
+    """simulate_multi_view's recipe (K cameras on an arc, each keyframe its own deformed copy of the
+    cloud, initial MapPoints = truth + N(0, noise3d)) as an ArrayMap.  scale_scene: the camera arc
+    radius grows with the cloud's sqrt(n/120) extents (as two_view_problem's scale_scene), keeping
+    the reference's 120-point viewing geometry at C3-C5 sizes."""
+    rng = np.random.default_rng(seed + 7)
+    base, _ = generate_points(n, rigid=0.0, gaussian=0.0, seed=seed)
+    sc = np.sqrt(n / 120.0) if scale_scene else 1.0
+    center = base.mean(0)
+    kfs = []
+    for kk in range(k):
+        ang = np.deg2rad(-30 + 60 * kk / max(k - 1, 1))
+        cpos = center + np.array([radius * sc * np.sin(ang), 0.0, -radius * sc * np.cos(ang)])
+        pts = base + rng.normal(0, deform, base.shape) + np.array([0, deform * kk, 0])
+        R = look_at(cpos, center)
+        Tcw = SE3f(R.T, -(R.T @ cpos.astype(np.float32)))
+        pc = Tcw * pts.astype(np.float32)
+        uv = kb8_project(kb8, pc)
+        uv = (np.round((uv.astype(np.float64) + rng.normal(0, rep_error, uv.shape)) * 10 ** decimals)
+              / 10 ** decimals).astype(np.float32)
+        dep = (pc[:, 2] + rng.normal(0, depth_error / 1000.0, n)).astype(np.float32)
+        init = (pts + rng.normal(0, noise3d, pts.shape)).astype(np.float32)
+        kfs.append({"id": kk, "pose": Tcw, "uv": uv, "depth": dep, "pos": init})
+    return ArrayMap(kfs, kb8, inv_sigma2_table(8, 1.2))
+
+
+def multi_view_problem(n, k, seed=1, kb8=DRUNKARD_KB8, rep_weight=1.0, arap_weight=1e7, depth_sigma=np.float32(0.3),
+                       pair_window=0):
+    """The C3 / C4 / C5 benchmark graphs: multi_view_arrays + the product's host graph builder
+    (deftri_arap_build_graph; pair_window > 0: only keyframe pairs at most that far apart in map
+    order — the documented sliding-window deviation of C5)."""
+    from . import capi
+    m = multi_view_arrays(n=n, k=k, seed=seed, kb8=kb8)
+    host = capi.Context(-1)
+    if pair_window:
+        host.set_pair_window(pair_window)
+    p = host.build_graph(m, rep_weight, arap_weight, depth_sigma)
+    host.close()
+    return p
+
+
 def two_view_problem(n, seed=1, rep_weight=1.0, arap_weight=2e5, depth_sigma=np.float32(0.003), return_map=False):
     """The benchmark scene (BASELINE C1/C2 shapes): simulate_two_view with the extents scaled to n
     correspondences and failed triangulations dropped, then the arapOptimization graph built by the
