@@ -30,6 +30,8 @@ struct DevProblem {
     double *Jrep = nullptr, *Wrep = nullptr, *Erep = nullptr, *chi_rep = nullptr;
     double *Jdep = nullptr, *Wdep = nullptr, *Edep = nullptr, *chi_dep = nullptr;
     double *Jarap = nullptr, *Warap = nullptr, *Earap = nullptr, *chi_arap = nullptr;
+    int64_t jarap_ld = 0;       // 0: J per edge contiguous ([E][18], the multifrontal plan's kernels);
+                                // > 0: column-major [18][jarap_ld] (the iterative plan: coalesced loads)
     double *tg_pre = nullptr;   // per pair: T_g and its 12 numeric-Jacobian perturbations (k_arap_pre)
 };
 

@@ -194,7 +194,8 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
                            const double *__restrict__ pinfo, const double *__restrict__ points,
                            const double *__restrict__ tg, const double *__restrict__ tg_pre,
                            double *__restrict__ J, double *__restrict__ W,
-                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
+                           int64_t jld) {
     int e = TID;
     if (e >= E_) return;
     const int32_t *v = apts + 4 * (int64_t)e;
@@ -278,7 +279,12 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
             Jv[12 + dd] = scalar * (ep - em);
         }
     }
-    for (int k = 0; k < 18; k++) J[18 * (int64_t)e + k] = Jv[k];
+    if (jld) {
+#pragma unroll
+        for (int k = 0; k < 18; k++) J[k * jld + e] = Jv[k];
+    } else {
+        for (int k = 0; k < 18; k++) J[18 * (int64_t)e + k] = Jv[k];
+    }
     W[e] = om;
     E[e] = err;
 }
@@ -1665,7 +1671,7 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
                            dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
                            P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg,
                            pre ? P.tg_pre : nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, want_jac ? 1 : 0,
-                           analytic ? 1 : 0);
+                           analytic ? 1 : 0, P.jarap_ld);
 }
 
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {

@@ -41,6 +41,8 @@ constexpr int kSpBlock = 256;          // edges per phase-1 block / rows per row
 constexpr int kSpRed = 16;             // doubles per iteration in the reduction record
 constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
+constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
+constexpr int kSpHeavySplit = 512;     // heavy sums by one workgroup per heavy vertex above this many blocks
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0)
 enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4 };
@@ -77,6 +79,15 @@ struct SpPlanHost {
     std::vector<int64_t> inc_off;                      // nown + 1
     std::vector<int32_t> inc;                          // local arap edge << 2 | role
     std::vector<int32_t> rep_off, dep_off;             // nown + 1, into the local rep / dep arrays
+    // phase-2 wave layout: rows dealt to 64-lane waves (sorted by entry count inside windows of
+    // kSpSortWindow rows so a wave pads little); wave w's entries are slots woff[w] .. woff[w + 1] - 1,
+    // slot k of lane j at [k][64] + j.  pmap: ARAP incidence le << 2 | role, depth coupling -(2 + j)
+    // (local depth edge j), -1 padding; pidx (what phase 2 multiplies the slot's J by): s[le] for
+    // ARAP, -(2 + scale) for a depth coupling (p of the scale), -1 padding
+    std::vector<int32_t> rowmap;                       // [nwaves * 64]: local row per lane (-1 padding)
+    std::vector<int64_t> woff;                         // nwaves + 1, in slots
+    std::vector<int32_t> pmap, pidx;                   // [slots * 64]
+    int32_t max_heavy_blocks = 0;                      // most phase-1 blocks of one heavy vertex
     // halo exchange: rows (global) sent to / received from each peer, ascending
     std::vector<std::vector<int32_t>> send_rows, recv_rows;
     int64_t halo_rows = 0;
@@ -109,6 +120,13 @@ struct SpDev {
     const int32_t *dsc = nullptr, *drow = nullptr, *dperm = nullptr;
     const int64_t *inc_off = nullptr;
     const int32_t *inc = nullptr, *rep_off = nullptr, *dep_off = nullptr;
+    int64_t jld = 0;                                   // column stride of Ja / Ja32 ([18][jld])
+    int32_t nwaves = 0, heavy_split = 0;
+    int64_t nslots = 0;                                // wave-layout slots (x 64 lanes)
+    const int32_t *rowmap = nullptr, *pmap = nullptr, *pidx = nullptr;
+    const int64_t *woff = nullptr;
+    double *pj = nullptr;                              // packed J slices: [3][nslots * 64] (fp64)
+    float *pj32 = nullptr;                             // the same in fp32 (fp32 Jacobian storage)
     // per-LM-iteration
     double *Hv = nullptr, *Dv = nullptr, *Mv = nullptr;   // own rows: 6 each (lower 3x3: 00 10 11 20 21 22)
     double *cdep = nullptr, *wss = nullptr;               // per local depth edge: W J_p J_s (3), W J_s^2
@@ -136,13 +154,15 @@ void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st);   // rows + bloc
 void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st);   // rank max of the rows' diagonal
 void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);   // out = max(out, heavy diagonal)
 void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st);
+void sp_launch_pack(const SpDev &G, bool fp32, hipStream_t st);     // per LM iteration, after glin
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st);
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
-void sp_launch_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf, hipStream_t st);
-void sp_launch_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
+void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
+                         hipStream_t st);
+void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
 void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
                           hipStream_t st);
 void sp_launch_permute_out(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,

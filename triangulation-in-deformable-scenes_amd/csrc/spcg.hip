@@ -70,21 +70,6 @@ __device__ __forceinline__ int it_state(const SpDev &G, int it, double &beta) {
 
 __device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q ? 6 * h : 6 * G.Q + (h - G.Q); }
 
-template <class JT>
-__device__ __forceinline__ void load_j18(const JT *__restrict__ J, double *o);
-template <>
-__device__ __forceinline__ void load_j18<double>(const double *__restrict__ J, double *o) {
-    const double2 *J2 = reinterpret_cast<const double2 *>(J);
-#pragma unroll
-    for (int k = 0; k < 9; k++) { const double2 t = J2[k]; o[2 * k] = t.x; o[2 * k + 1] = t.y; }
-}
-template <>
-__device__ __forceinline__ void load_j18<float>(const float *__restrict__ J, double *o) {
-    const float2 *J2 = reinterpret_cast<const float2 *>(J);
-#pragma unroll
-    for (int k = 0; k < 9; k++) { const float2 t = J2[k]; o[2 * k] = t.x; o[2 * k + 1] = t.y; }
-}
-
 // ---- per LM iteration -----------------------------------------------------------------------------
 __device__ __forceinline__ int tri3(int a, int b) { return a * (a + 1) / 2 + b; }   // a >= b
 __device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; }
@@ -129,7 +114,8 @@ __global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G) {
         for (int64_t k = G.inc_off[l]; k < G.inc_off[l + 1]; k++) {  // ARAP incidences
             const int v = G.inc[k];
             const int64_t le = v >> 2;
-            const double *J = G.Ja + 18 * le + 3 * (v & 3);
+            const double *Jc = G.Ja + 3 * (v & 3) * G.jld + le;       // column-major [18][jld]
+            const double J[3] = {Jc[0], Jc[G.jld], Jc[2 * G.jld]};
             const double w = G.Wa[le], er = G.Ea[le];
 #pragma unroll
             for (int a = 0; a < 3; a++) {
@@ -166,7 +152,9 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
 #pragma unroll
         for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
         if (i < d.w) {
-            const double *J = G.Ja + 18 * (int64_t)i + 12;
+            double J[6];
+#pragma unroll
+            for (int r = 0; r < 6; r++) J[r] = G.Ja[(12 + r) * G.jld + i];
             const double wv = G.Wa[i], er = G.Ea[i];
 #pragma unroll
             for (int r = 0; r < 6; r++) {
@@ -205,43 +193,63 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
     }
 }
 
-// heavy H / b (rank sums): one wave per heavy vertex at a time, its blocks' partials in block order
+// heavy H / b (rank sums): one workgroup per heavy vertex, its blocks' partials strided over the
+// threads in block order, then the fixed workgroup tree per value
 __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int h = w; h < G.Q + G.S; h += 4) {
-        const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
-        if (h < G.Q) {
-            double a[kSpLin];
+    __shared__ double red4[4];
+    const int h = blockIdx.x;
+    const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+    if (h < G.Q) {
+        double a[kSpLin];
 #pragma unroll
-            for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
-            for (int64_t k = k0 + lane; k < k1; k += 64) {
-                const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
+        for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
+        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
+            const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
 #pragma unroll
-                for (int q = 0; q < kSpLin; q++) a[q] += p[q];
-            }
+            for (int q = 0; q < kSpLin; q++) a[q] += p[q];
+        }
 #pragma unroll
-            for (int q = 0; q < kSpLin; q++) {
-                const double v = wave_sum(a[q]);
-                if (lane == 0) {
-                    if (q < 21) G.hl[21 * (int64_t)h + q] = v;
-                    else G.b[6 * (int64_t)h + q - 21] = v;
-                }
-            }
-        } else {
-            double a0 = 0.0, a1 = 0.0;
-            for (int64_t k = k0 + lane; k < k1; k += 64) {
-                const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
-                a0 += p[0];
-                a1 += p[1];
-            }
-            a0 = wave_sum(a0);
-            a1 = wave_sum(a1);
-            if (lane == 0) {
-                G.hl[21 * (int64_t)G.Q + (h - G.Q)] = a0;
-                G.b[6 * (int64_t)G.Q + (h - G.Q)] = a1;
+        for (int q = 0; q < kSpLin; q++) {
+            const double v = block_sum(a[q], red4);
+            if (threadIdx.x == 0) {
+                if (q < 21) G.hl[21 * (int64_t)h + q] = v;
+                else G.b[6 * (int64_t)h + q - 21] = v;
             }
         }
+    } else {
+        double a0 = 0.0, a1 = 0.0;
+        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
+            const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
+            a0 += p[0];
+            a1 += p[1];
+        }
+        a0 = block_sum(a0, red4);
+        a1 = block_sum(a1, red4);
+        if (threadIdx.x == 0) {
+            G.hl[21 * (int64_t)G.Q + (h - G.Q)] = a0;
+            G.b[6 * (int64_t)G.Q + (h - G.Q)] = a1;
+        }
     }
+}
+
+// the phase-2 wave layout's J slices, once per LM iteration (after k_sp_glin_rows: the depth
+// couplings c_e): slot t <- ARAP J_{le, role} (column-major J) or c_e, zero for padding
+template <class JT>
+__global__ void __launch_bounds__(256) k_sp_pack_slots(const SpDev G, JT *__restrict__ pj) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = G.nslots * 64;
+    if (t >= n) return;
+    const int m = G.pmap[t];
+    double v[3] = {0.0, 0.0, 0.0};
+    if (m >= 0) {
+        const double *Jc = G.Ja + 3 * (m & 3) * G.jld + (m >> 2);
+        v[0] = Jc[0]; v[1] = Jc[G.jld]; v[2] = Jc[2 * G.jld];
+    } else if (m <= -2) {
+        const double *c = G.cdep + 3 * (int64_t)(-2 - m);
+        v[0] = c[0]; v[1] = c[1]; v[2] = c[2];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; a++) pj[a * n + t] = (JT)v[a];
 }
 
 // rank max of the rows' diagonal (stage 0), or that (all-reduced) combined with the heavy diagonal
@@ -442,7 +450,8 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
         if (i < d.w) {
             const int4 rw = reinterpret_cast<const int4 *>(G.apts)[i];
             double J[18];
-            load_j18<JT>(Jarap + 18 * (int64_t)i, J);
+#pragma unroll
+            for (int k = 0; k < 18; k++) J[k] = (double)Jarap[k * G.jld + i];
             const int rows[4] = {rw.x, rw.y, rw.z, rw.w};
             double t = 0.0;
 #pragma unroll
@@ -487,91 +496,122 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
     }
 }
 
+// one wave per 64 rows of the wave layout: per slot (coalesced [k][64]) the entry's J slice times
+// s_e (ARAP) or p of the depth edge's scale; then the row's own terms
 template <class JT>
-__global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ Jarap) {
+__global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     double beta;
     if (it_state(G, it, beta)) return;
-    const int l = blockIdx.x * 256 + threadIdx.x;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double pq = 0.0;
-    if (l < G.nown) {
-        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-        double p[3], q[3];
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const double2 v = G.zp[o + c];
-            p[c] = __fma_rn(beta, v.y, v.x);
-            G.zp[o + c] = make_double2(v.x, p[c]);
-        }
-        const double *D = G.Dv + 6 * (int64_t)l;
-        q[0] = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
-        q[1] = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
-        q[2] = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+    if (w < G.nwaves) {
+        const int l = G.rowmap[64 * w + lane];
+        const int64_t n = G.nslots * 64;
+        const JT *pjx = pj, *pjy = pj + n, *pjz = pj + 2 * n;
         const int64_t os = 6 * (int64_t)G.Q;
-        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {
-            const double ps = pval(G.zp, beta, os + G.dsc[j]);
-            const double *c = G.cdep + 3 * (int64_t)j;
-#pragma unroll
-            for (int a = 0; a < 3; a++) q[a] += c[a] * ps;
-        }
-        const int64_t k0 = G.inc_off[l], k1 = G.inc_off[l + 1];
-        int64_t k = k0;
-        // four incidences per step: their indices, then their s and J loads, then the adds in order
-        for (; k + 4 <= k1; k += 4) {
+        double q[3] = {0.0, 0.0, 0.0};
+        int64_t k = G.woff[w] * 64 + lane;
+        const int64_t k1 = G.woff[w + 1] * 64 + lane;
+        auto val = [&](int v) -> double {
+            return v >= 0 ? G.s[v] : (v <= -2 ? pval(G.zp, beta, os + (-2 - v)) : 0.0);
+        };
+        // four slots per step: their indices, then the values and J slices, then the adds in order
+        for (; k + 3 * 64 < k1; k += 4 * 64) {
             int v[4];
-            double s[4], J[4][3];
+            double sv[4], J[4][3];
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = G.inc[k + u];
+            for (int u = 0; u < 4; u++) v[u] = G.pidx[k + 64 * u];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const int64_t le = v[u] >> 2;
-                s[u] = G.s[le];
-                const JT *Jp = Jarap + 18 * le + 3 * (v[u] & 3);
-#pragma unroll
-                for (int a = 0; a < 3; a++) J[u][a] = Jp[a];
+                sv[u] = val(v[u]);
+                J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
             }
 #pragma unroll
             for (int u = 0; u < 4; u++)
 #pragma unroll
-                for (int a = 0; a < 3; a++) q[a] += J[u][a] * s[u];
+                for (int a = 0; a < 3; a++) q[a] += J[u][a] * sv[u];
         }
-        for (; k < k1; k++) {
-            const int v = G.inc[k];
-            const int64_t le = v >> 2;
-            const double s = G.s[le];
-            const JT *Jp = Jarap + 18 * le + 3 * (v & 3);
-#pragma unroll
-            for (int a = 0; a < 3; a++) q[a] += (double)Jp[a] * s;
+        for (; k < k1; k += 64) {
+            const double sv = val(G.pidx[k]);
+            q[0] += (double)pjx[k] * sv;
+            q[1] += (double)pjy[k] * sv;
+            q[2] += (double)pjz[k] * sv;
         }
+        if (l >= 0) {
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+            double p[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            G.q[o + c] = q[c];
-            pq += p[c] * q[c];
+            for (int c = 0; c < 3; c++) {
+                const double2 v = G.zp[o + c];
+                p[c] = __fma_rn(beta, v.y, v.x);
+                G.zp[o + c] = make_double2(v.x, p[c]);
+            }
+            const double *D = G.Dv + 6 * (int64_t)l;
+            q[0] += lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
+            q[1] += lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
+            q[2] += lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.q[o + c] = q[c];
+                pq += p[c] * q[c];
+            }
         }
     }
-    const double s = block_sum(pq, red4);
-    if (threadIdx.x == 0) G.rpart[blockIdx.x] = s;
+    const double sm = block_sum(pq, red4);
+    if (threadIdx.x == 0) G.rpart[blockIdx.x] = sm;
 }
 
-// stage 0 (one rank): sums + finish; 1: the rank's sums into hbuf (all-reduced next); 2: finish;
-// 3: only the state of iteration it into the record (the tail of a queued chunk)
+// heavy q, p.q and alpha of iteration it.  stage 0: one workgroup does all (small problems, one
+// rank); 1: the rank's sums into hbuf [p.q of its rows, per heavy dof the sum of its blocks'
+// partials] — one workgroup per heavy vertex (+ one for p.q) when launched with Q + S + 1 workgroups,
+// else one workgroup with a wave per vertex; 2: finish from hbuf (after the host's all-reduce, or
+// stage 1 on one rank); 3: only the state of iteration it into the record (the tail of a chunk)
 __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double lam, int stage) {
     __shared__ double red4[4];
     double beta;
     const int st = it_state(G, it, beta);
     if (st || stage == 3) {
-        if (st && stage != 2 && threadIdx.x == 0 && G.rec[0] == 0.0) {
+        if (st && stage != 2 && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
             G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
             G.rec[1] = it;
         }
         return;
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nh = G.Q + G.S;
+    if (stage == 1 && gridDim.x > 1) {
+        const int h = blockIdx.x;
+        if (h == nh) {
+            double a = 0.0;
+            for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
+            a = block_sum(a, red4);
+            if (threadIdx.x == 0) G.hbuf[0] = a;
+            return;
+        }
+        const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+        const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
+            const double *p = G.part + (int64_t)kSpPart * G.hv_blk[k];
+#pragma unroll
+            for (int c = 0; c < 6; c++)
+                if (c < dim) acc[c] += p[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+            if (c < dim) {
+                const double v = block_sum(acc[c], red4);
+                if (threadIdx.x == 0) G.hbuf[1 + o + c] = v;
+            }
+        }
+        return;
+    }
     if (stage != 2) {
         double a = 0.0;
         for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
         const double pq_rows = block_sum(a, red4);
-        for (int h = w; h < G.Q + G.S; h += 4) {
+        for (int h = w; h < nh; h += 4) {
             const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
             const int dim = h < G.Q ? 6 : 1;
             double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -706,10 +746,16 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
     } while (0)
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    (void)fp32;
     SPL("sp_glin_rows", sp::k_sp_glin_rows, std::max(G.nrb, 1), G);
     if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
-    if (G.Q + G.S > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, 1, G);
+    if (G.Q + G.S > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.Q + G.S, G);
+    sp_launch_pack(G, fp32, st);
+}
+
+void sp_launch_pack(const SpDev &G, bool fp32, hipStream_t st) {
+    if (G.nslots <= 0) return;
+    if (fp32) SPL("sp_pack_slots", sp::k_sp_pack_slots<float>, nblk(G.nslots * 64, 256), G, G.pj32);
+    else SPL("sp_pack_slots", sp::k_sp_pack_slots<double>, nblk(G.nslots * 64, 256), G, G.pj);
 }
 
 void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st) {
@@ -737,24 +783,28 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         if (fp32) SPL("sp_phase1", sp::k_sp_phase1<float>, G.nblk, it, G, G.Ja32);
         else SPL("sp_phase1", sp::k_sp_phase1<double>, G.nblk, it, G, G.Ja);
     }
-    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, std::max(G.nrb, 1), it, G, lambda, G.Ja32);
-    else SPL("sp_phase2", sp::k_sp_phase2<double>, std::max(G.nrb, 1), it, G, lambda, G.Ja);
+    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, std::max(G.nrb, 1), it, G, lambda, (const float *)G.pj32);
+    else SPL("sp_phase2", sp::k_sp_phase2<double>, std::max(G.nrb, 1), it, G, lambda, (const double *)G.pj);
 }
 
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {
-    SPL("sp_heavy", sp::k_sp_heavy, 1, it, G, lambda, stage);
+    // stage 1 over one workgroup per heavy vertex when the vertices have many blocks
+    const int grid = (stage == 1 && G.heavy_split) ? G.Q + G.S + 1 : 1;
+    SPL("sp_heavy", sp::k_sp_heavy, grid, it, G, lambda, stage);
 }
 
 void sp_launch_update(const SpDev &G, int it, hipStream_t st) {
     SPL("sp_update", sp::k_sp_update, G.nrb + 1, it, G);
 }
 
-void sp_launch_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf, hipStream_t st) {
-    if (n > 0) SPL("sp_pack", sp::k_sp_pack, nblk((int64_t)n * width, 256), n, rows, width, base, src, buf);
+void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
+                         hipStream_t st) {
+    if (n > 0) SPL("sp_halo_pack", sp::k_sp_pack, nblk((int64_t)n * width, 256), n, rows, width, base, src, buf);
 }
 
-void sp_launch_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st) {
-    if (n > 0) SPL("sp_unpack", sp::k_sp_unpack, nblk((int64_t)n * width, 256), n, rows, width, base, buf, dst);
+void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst,
+                           hipStream_t st) {
+    if (n > 0) SPL("sp_halo_unpack", sp::k_sp_unpack, nblk((int64_t)n * width, 256), n, rows, width, base, buf, dst);
 }
 
 void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,

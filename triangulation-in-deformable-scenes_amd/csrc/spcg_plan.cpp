@@ -233,6 +233,50 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         }
     }
 
+    // 8b. phase-2 wave layout: per own row its ARAP incidences then its depth couplings; rows sorted by
+    //     that count (descending, stable) inside windows of kSpSortWindow rows, 64 per wave
+    {
+        std::vector<int32_t> cnt(nown);
+        for (int32_t l = 0; l < nown; l++)
+            cnt[l] = (int32_t)(H.inc_off[l + 1] - H.inc_off[l]) + (H.dep_off[l + 1] - H.dep_off[l]);
+        std::vector<int32_t> order(nown);
+        std::iota(order.begin(), order.end(), 0);
+        for (int32_t w0 = 0; w0 < nown; w0 += kSpSortWindow) {
+            const int32_t w1 = std::min(nown, w0 + kSpSortWindow);
+            std::stable_sort(order.begin() + w0, order.begin() + w1, [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
+        }
+        const int32_t nw = (nown + 63) / 64;
+        H.rowmap.assign((size_t)nw * 64, -1);
+        H.woff.assign(nw + 1, 0);
+        for (int32_t w = 0; w < nw; w++) {
+            int32_t kmax = 0;
+            for (int j = 0; j < 64 && 64 * w + j < nown; j++) {
+                H.rowmap[64 * (size_t)w + j] = order[64 * w + j];
+                kmax = std::max(kmax, cnt[order[64 * w + j]]);
+            }
+            H.woff[w + 1] = H.woff[w] + kmax;
+        }
+        const int64_t nsl = H.woff[nw];
+        H.pmap.assign((size_t)nsl * 64, -1);
+        H.pidx.assign((size_t)nsl * 64, -1);
+        for (int32_t w = 0; w < nw; w++)
+            for (int j = 0; j < 64; j++) {
+                const int32_t l = H.rowmap[64 * (size_t)w + j];
+                if (l < 0) continue;
+                int64_t k = H.woff[w];
+                for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++, k++) {
+                    H.pmap[64 * k + j] = H.inc[x];
+                    H.pidx[64 * k + j] = H.inc[x] >> 2;
+                }
+                for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++, k++) {
+                    H.pmap[64 * k + j] = -(2 + x);
+                    H.pidx[64 * k + j] = -(2 + d.dep_scale[H.dep_ids[x]]);
+                }
+            }
+    }
+    for (int32_t h = 0; h < Q + S; h++)
+        H.max_heavy_blocks = std::max<int32_t>(H.max_heavy_blocks, (int32_t)(H.hv_blk_off[h + 1] - H.hv_blk_off[h]));
+
     // 9. halo exchange lists
     H.send_rows.assign(nranks, {});
     H.recv_rows.assign(nranks, {});
@@ -270,9 +314,9 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     const double jb = fp32_jac ? 72.0 : 144.0;
     H.phase1_bytes = (double)nloc * (jb + 8 + 16 + 8)                  // J, W, rows, s
                      + (double)ndl * (4 + 4 + 24 + 8);                  // dperm, row, c, W J_s^2
-    H.phase2_bytes = (double)nown * (48 + 48 + 48 + 24 + 8 + 4)        // (z,p) in / out, D, q, offsets
-                     + (double)H.inc.size() * (4 + 8 + jb / 6)           // incidence, s, J slice
-                     + (double)ndl * (4 + 24);                           // the row's depth couplings
+    H.phase2_bytes = (double)nown * (48 + 48 + 48 + 24 + 4)            // (z,p) in / out, D, q, row map
+                     + (double)H.inc.size() * (4 + 8 + jb / 6)           // slot index, s, packed J slice
+                     + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
     return true;
 }

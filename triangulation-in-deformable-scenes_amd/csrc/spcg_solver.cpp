@@ -148,6 +148,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     P.P = NP; P.Q = Q; P.S = S; P.C = C;
     P.R = (int32_t)nr; P.D = (int32_t)nd; P.E = (int32_t)nloc; P.NR = (int32_t)H.rot_ids.size();
     P.huber_delta = d.huber_delta;
+    P.jarap_ld = std::max<int64_t>(nloc, 1);        // column-major J: each of the 18 columns coalesced
     PUT(P.points, pts); PUT(P.scales, sc); PUT(P.tg, tg);
     ALLOC(P.points_bak, 3 * (int64_t)NP); ALLOC(P.scales_bak, S); ALLOC(P.tg_bak, 7 * (int64_t)Q);
     PUT(P.cam_kb8, kb8); PUT(P.cam_pose, cpose); PUT(P.cam_R, camR);
@@ -157,7 +158,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     PUT(P.rot, rot); PUT(P.pair_area, parea); PUT(P.pair_info, pinfo);
     ALLOC(P.Jrep, 6 * (int64_t)nr); ALLOC(P.Wrep, nr); ALLOC(P.Erep, 2 * (int64_t)nr); ALLOC(P.chi_rep, nr);
     ALLOC(P.Jdep, 4 * (int64_t)nd); ALLOC(P.Wdep, nd); ALLOC(P.Edep, nd); ALLOC(P.chi_dep, nd);
-    ALLOC(P.Jarap, 18 * nloc); ALLOC(P.Warap, nloc); ALLOC(P.Earap, nloc); ALLOC(P.chi_arap, nloc);
+    ALLOC(P.Jarap, 18 * std::max<int64_t>(nloc, 1)); ALLOC(P.Warap, nloc); ALLOC(P.Earap, nloc); ALLOC(P.chi_arap, nloc);
     ALLOC(P.tg_pre, 12 * 13 * (int64_t)std::max(Q, 1));
     init_.assign(3, nullptr);
     PUT(init_[0], pts); PUT(init_[1], sc); PUT(init_[2], tg);
@@ -184,7 +185,21 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G.Jr = P.Jrep; G.Wr = P.Wrep; G.Er = P.Erep;
     G.Jd = P.Jdep; G.Wd = P.Wdep; G.Ed = P.Edep;
     G.dsc = P.dep_scale; G.drow = P.dep_point;
-    if (fp32_jac) { float *j32; ALLOC(j32, 18 * nloc); G.Ja32 = j32; }
+    G.jld = P.jarap_ld;
+    if (fp32_jac) { float *j32; ALLOC(j32, 18 * G.jld); G.Ja32 = j32; }
+    G.nwaves = (int32_t)(H.woff.size() - 1);
+    G.nslots = H.woff.back();
+    G.heavy_split = H.max_heavy_blocks > kSpHeavySplit ? 1 : 0;
+    {
+        int32_t *rm, *pm, *pi;
+        int64_t *wo;
+        PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx);
+        G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi;
+        if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
+        else { ALLOC(G.pj, 3 * 64 * G.nslots); }
+        H.pmap.clear(); H.pmap.shrink_to_fit();
+        H.pidx.clear(); H.pidx.shrink_to_fit();
+    }
     ALLOC(G.Hv, 6 * (int64_t)nown); ALLOC(G.Dv, 6 * (int64_t)nown); ALLOC(G.Mv, 6 * (int64_t)nown);
     ALLOC(G.cdep, 3 * (int64_t)nd); ALLOC(G.wss, nd);
     ALLOC(G.hl, 21 * (int64_t)Q + S + G.ndof);
@@ -231,7 +246,7 @@ int SpSolver::halo(int width, double *vec, bool zp) {
     const int64_t base = zp ? 2 * G.hd : G.hd;
     const int64_t nsend = send_off_[nranks_];
     double *sbuf = d_xbuf, *rbuf = d_xbuf + 6 * nsend;
-    sp_launch_pack((int)nsend, d_send_rows, width, base, vec, sbuf, st_);
+    sp_launch_halo_pack((int)nsend, d_send_rows, width, base, vec, sbuf, st_);
     // global order: for every (src, dst) pair in lexicographic order, the src sends and the dst receives
     std::vector<SpTransport::Op> ops;
     for (int a = 0; a < nranks_; a++)
@@ -244,7 +259,7 @@ int SpSolver::halo(int width, double *vec, bool zp) {
         }
     int rc = tr_->p2p(ops, st_);
     if (rc) return rc;
-    sp_launch_unpack((int)recv_off_[nranks_], d_recv_rows, width, base, rbuf, vec, st_);
+    sp_launch_halo_unpack((int)recv_off_[nranks_], d_recv_rows, width, base, rbuf, vec, st_);
     return 0;
 }
 
@@ -277,7 +292,7 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
     launch_sum_multi(J, d_part, kSpRedParts, st_);
     int rc;
     if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
-    if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * (int64_t)P.E, st_);
+    if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_);
     sp_launch_glin(G, fp32_jac != 0, st_);
     if (nranks_ > 1 && (rc = tr_->allreduce(G.hl, 21 * (int64_t)G.Q + G.S + G.hd, 0, st_))) return rc;
     if (want_max) {
@@ -305,6 +320,9 @@ void SpSolver::cg_chain(double lambda, int from, int to) {
         if (dist) {
             sp_launch_heavy(G, it, lambda, 1, st_);
             tr_->allreduce(G.hbuf, 1 + G.hd, 0, st_);
+            sp_launch_heavy(G, it, lambda, 2, st_);
+        } else if (G.heavy_split) {
+            sp_launch_heavy(G, it, lambda, 1, st_);
             sp_launch_heavy(G, it, lambda, 2, st_);
         } else {
             sp_launch_heavy(G, it, lambda, 0, st_);
