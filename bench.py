@@ -403,9 +403,7 @@ def main():
     n = args.corr or spec["n"]
     window = args.pair_window if args.pair_window >= 0 else spec.get("window", 0)
     sharded = world > 1 and not args.replicas
-    plan = args.plan
-    if plan == "auto":
-        plan = "multifrontal" if (args.solver == "direct" or (wl == "c2" and not sharded)) else "iterative"
+    plan = args.plan              # auto: the library's choice (iterative for PCG from 50k unknowns / sharded)
     t0 = time.perf_counter()
     prob, prob_map = build_workload(wl, n, 1 if sharded else 1 + rank, window)
     log(f"[rank {rank}] {wl} graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
@@ -423,6 +421,7 @@ def main():
     ctx.upload(prob)
     ctx.set_lm_lanes(args.lanes)
     info = ctx.plan_info()
+    plan = info["plan"]
     log(f"[rank {rank}] upload ({info['plan']} plan) {time.perf_counter() - t0:.1f}s: {info}")
     analytic = args.analytic
 
@@ -470,10 +469,16 @@ def main():
     trials_per_it = rep["trials_total"] / max(iters, 1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         t0 = time.perf_counter()
-        if wl == "c2" and plan == "multifrontal":
-            cpu = cpu_baseline(prob, ctx.vertex_order(), trials_per_it, args.cpu_full_iteration)
-        elif wl == "c2":
-            cpu = None
+        if wl == "c2":
+            # the oracle eliminates in a nested-dissection order of the same problem (the host-only
+            # analysis of the multifrontal plan): SimplicialLDLT's fill at C2 needs a good ordering
+            if plan == "multifrontal":
+                order = ctx.vertex_order()
+            else:
+                with capi.Context(-1) as hc:
+                    hc.analyse(prob)
+                    order = hc.vertex_order()
+            cpu = cpu_baseline(prob, order, trials_per_it, args.cpu_full_iteration)
         else:
             cpu = cpu_baseline_sample(wl, window, {"c3": 400, "c4": 400, "c5": 600}[wl], trials_per_it)
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")

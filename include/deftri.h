@@ -229,9 +229,12 @@ int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_
    products, the global-vertex partials) per CG iteration.  A step whose PCG does not converge within
    the budget (deftri_set_linear_solver max_iterations; <= 0: 1000) counts as a failed linear solve
    (g2o: the trial is rejected).  Any keyframe count (all-pairs graphs, BASELINE C3-C5).
-   DEFTRI_PLAN_AUTO (default): ITERATIVE for point-sharded PCG contexts (nranks > 1 with
-   DEFTRI_SOLVER_PCG) and for multi-pair problems above 1M unknowns; MULTIFRONTAL otherwise.
-   Applies to the next deftri_problem_upload. */
+   DEFTRI_PLAN_AUTO (default): ITERATIVE when the step solver is DEFTRI_SOLVER_PCG at upload and the
+   context is point-sharded (nranks > 1) or the problem has >= 50,000 unknowns (measured faster from
+   C2 up); MULTIFRONTAL otherwise.  Applies to the next deftri_problem_upload.  A
+   context on the iterative plan that is asked for what only the factorization has (LDL^T steps or
+   solves after deftri_set_linear_solver(DIRECT), deftri_eval_hessian_product) analyses and uploads
+   the multifrontal plan at that point, continuing from its current state. */
 #define DEFTRI_PLAN_AUTO          0
 #define DEFTRI_PLAN_MULTIFRONTAL  1
 #define DEFTRI_PLAN_ITERATIVE     2

@@ -34,7 +34,10 @@ def golden_cases():
 
 @pytest.fixture(scope="session")
 def gpu_ctx():
+    """One device context for the session, pinned to the multifrontal plan (the LDL^T / sliced
+    matrix-free PCG suites); tests of the iterative plan set it explicitly and restore this."""
     from deftri import capi
     ctx = capi.Context(0)
+    ctx.set_plan("multifrontal")
     yield ctx
     ctx.close()

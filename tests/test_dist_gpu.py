@@ -40,6 +40,7 @@ def _worker(rank, world, port, q):
     p = _problem()
     ctx = capi.Context(0)
     ctx.dist_set_transport(world, rank, ddist.torch_transport())
+    ctx.set_plan("multifrontal")            # the sharded LDL^T (the iterative plan: test_gpu_sp.py)
     ctx.upload(p)
     res = {}
     for analytic in (True, False):
@@ -76,6 +77,7 @@ def test_sharded_lm_matches_single_gpu(world):
     ref = {}
     with capi.Context(0) as ctx:
         ctx.set_lm_lanes(1)
+        ctx.set_plan("multifrontal")
         ctx.upload(p)
         for analytic in (True, False):
             ctx.reset_state()

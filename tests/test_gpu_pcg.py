@@ -184,6 +184,7 @@ def _assembled_worker(q):
     m, _ = sim.simulate_two_view(n=20000, seed=1, scale_scene=True, compact=True)
     p = capi.Context(-1).build_graph(m, 1.0, 2e5, np.float32(0.003))
     with capi.Context(0) as ctx:
+        ctx.set_plan("multifrontal")
         ctx.upload(p)
         ctx.set_linear_solver("pcg", max_iterations=4096)
         st = ctx.profile_trial(1e10)

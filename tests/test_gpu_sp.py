@@ -63,7 +63,7 @@ def it_ctx(gpu_ctx):
     gpu_ctx.set_plan("iterative")
     gpu_ctx.set_linear_solver("pcg", max_iterations=4096)
     yield gpu_ctx
-    gpu_ctx.set_plan("auto")
+    gpu_ctx.set_plan("multifrontal")
     gpu_ctx.set_linear_solver("pcg")
     gpu_ctx.set_jacobian_storage(0)
 
@@ -124,7 +124,7 @@ def test_iterative_matches_multifrontal_two_view(gpu_ctx):
         gpu_ctx.set_linear_solver("pcg", max_iterations=4096)
         out[plan] = gpu_ctx.solve_lm(6, analytic=False)
         assert gpu_ctx.plan_info()["plan"] == plan
-    gpu_ctx.set_plan("auto")
+    gpu_ctx.set_plan("multifrontal")
     gpu_ctx.set_linear_solver("pcg")
     a, b = out["iterative"], out["multifrontal"]
     assert a["trials_total"] == b["trials_total"] and a["pcg_fallbacks"] == b["pcg_fallbacks"] == 0

@@ -46,6 +46,7 @@ constexpr int kRedParts = 512;
 constexpr double kPcgDefaultTol = 1e-12;    // relative residual ||b - A x|| / ||b||
 constexpr int kPcgDefaultMaxIt = 200;     // before a plan is uploaded
 constexpr int kPcgMaxIt = 4096;
+constexpr int64_t kIterativeMinUnknowns = 50000;   // DEFTRI_PLAN_AUTO: the iterative plan from here up
 
 struct HostProblem {
     deftri_problem_desc d{};
@@ -713,9 +714,13 @@ struct CtxTransport : SpTransport {
 bool want_iterative(const deftri_ctx *ctx, const deftri_problem_desc *d) {
     if (ctx->plan_mode == DEFTRI_PLAN_ITERATIVE) return true;
     if (ctx->plan_mode == DEFTRI_PLAN_MULTIFRONTAL) return false;
-    if (ctx->nranks > 1) return ctx->lin_solver == DEFTRI_SOLVER_PCG;
+    if (ctx->lin_solver != DEFTRI_SOLVER_PCG) return false;
+    if (ctx->nranks > 1) return true;
+    // one GPU: the iterative plan's product outruns the sliced multifrontal one from C2 up (734 vs
+    // 690 LM it/s at 100k x 2 views) and needs no analysis; small problems keep the
+    // factorization (their weakly damped steps take thousands of CG iterations)
     const int64_t ndof = 6LL * d->n_pairs + d->n_scales + 3LL * d->n_points;
-    return d->n_pairs > 1 && ndof > 1000000;
+    return ndof >= kIterativeMinUnknowns;
 }
 
 // LevelHook of the factor / solve launchers: the DistPlan transfers whose parent front sits at
@@ -801,6 +806,30 @@ void subset_edges(const HostProblem &full, const DistPlan &D, HostProblem &h) {
     h.d.arap_w = h.arap_w.data(); h.d.rot = h.rot.data(); h.d.pair_area = h.pair_area.data();
     h.d.pair_info = h.pair_info.data();
     h.d.order_xy = nullptr;
+}
+
+// a context on the iterative plan asked for what only the multifrontal plan has (the LDL^T, the
+// assembled H): analyse and upload it now from the uploaded problem, continuing from the iterative
+// plan's current state (deftri_reset_state still returns to the uploaded values)
+int ensure_multifrontal(deftri_ctx *ctx) {
+    if (!ctx->sp_on) return 0;
+    const deftri_problem_desc &d = ctx->hp.d;
+    std::vector<double> pts(3 * (size_t)d.n_points), sc(d.n_scales), tg(7 * (size_t)d.n_pairs);
+    int rc = ctx->sp->download(pts.data(), sc.data(), tg.data());
+    if (rc) return fail(ctx, rc, ctx->sp->err);
+    free_device(ctx);
+    if (!analyse(ctx->hp.d, ctx->S, 32, ctx->rank, ctx->nranks)) return fail(ctx, DEFTRI_E_ARG, "analysis failed: " + ctx->S.error);
+    ctx->analysed = true;
+    if (ctx->dist()) subset_edges(ctx->hp, ctx->S.dist, ctx->hloc);
+    rc = upload_device(ctx, ctx->dist() ? ctx->hloc : ctx->hp);
+    if (rc) { free_device(ctx); return rc; }
+    ctx->plan_hash = structure_hash(ctx->hp.d);
+    ctx->have = true;
+    DevProblem &P = ctx->P;
+    HIPOK(hipMemcpy(P.points, pts.data(), sizeof(double) * pts.size(), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(P.scales, sc.data(), sizeof(double) * sc.size(), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(P.tg, tg.data(), sizeof(double) * tg.size(), hipMemcpyHostToDevice));
+    return 0;
 }
 
 // chi2 at the current state (computeActiveErrors + activeRobustChi2) into d_scal[slot]; point-sharded:
@@ -1293,6 +1322,10 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
     hipSetDevice(ctx->device);
     HIPOK(hipStreamSynchronize(ctx->st));
     KProf prof;
+    if (ctx->sp_on && ctx->lin_solver != DEFTRI_SOLVER_PCG) {
+        const int rc0 = ensure_multifrontal(ctx);     // the factorization's kernels asked for
+        if (rc0) return rc0;
+    }
     if (ctx->sp_on) {
         int rc = ctx->sp->profile_trial(lambda, prof, ctx->prof_analytic);
         if (rc) return fail(ctx, rc, ctx->sp->err);
@@ -1600,6 +1633,10 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     deftri_report local{};
     deftri_report &R = rep ? *rep : local;
     std::memset(&R, 0, sizeof(R));
+    if (ctx->sp_on && ctx->lin_solver != DEFTRI_SOLVER_PCG) {
+        const int rc0 = ensure_multifrontal(ctx);     // LDL^T steps asked for: the multifrontal plan
+        if (rc0) return rc0;
+    }
     if (ctx->sp_on) {
         ctx->prof_analytic = prm->analytic_jacobians != 0;
         int rc = ctx->sp->solve_lm(*prm, R);
@@ -2052,7 +2089,10 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
-    if (ctx->sp_on) return fail(ctx, DEFTRI_E_ARG, "the iterative plan never assembles H");
+    if (ctx->sp_on) {                        // the iterative plan never assembles H
+        const int rc0 = ensure_multifrontal(ctx);
+        if (rc0) return rc0;
+    }
     if (n != ctx->S.ndof || !x || !y) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);
     double *dx = nullptr, *dy = nullptr;
@@ -2071,8 +2111,11 @@ int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int
 int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, double *x, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (ctx->sp_on && ctx->lin_solver != DEFTRI_SOLVER_PCG) {
+        const int rc0 = ensure_multifrontal(ctx);     // an LDL^T solve asked for
+        if (rc0) return rc0;
+    }
     if (ctx->sp_on) {
-        if (ctx->lin_solver != DEFTRI_SOLVER_PCG) return fail(ctx, DEFTRI_E_ARG, "the iterative plan has no factorization");
         if (!rhs || !x) return fail(ctx, DEFTRI_E_ARG, "null array");
         hipSetDevice(ctx->device);
         int rc = ctx->sp->damped_solve(lambda, rhs, x, n);
