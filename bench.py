@@ -299,7 +299,7 @@ def product_roofline(stats, rep, ctx, rank):
         by, ms = p1["bytes"] + p2["bytes"], p1["ms"] + p2["ms"]
         gbs = by / max(ms * 1e-3, 1e-12) / 1e9
         cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update") if k in stats)
-        return {"bound": "hbm", "kernel": "k_sp_phase1+k_sp_phase2 (matrix-free product)", "achieved": round(gbs, 1),
+        out = {"bound": "hbm", "kernel": "k_sp_phase1+k_sp_phase2 (matrix-free product)", "achieved": round(gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "traffic_unit": "bytes per product", "bytes_per_launch": by / its, "launches": its,
                 "avg_active_launch_us": round(1e3 * ms / its, 3),
@@ -309,6 +309,12 @@ def product_roofline(stats, rep, ctx, rank):
                            "gbs": round(p2["bytes"] / max(p2["ms"] * 1e-3, 1e-12) / 1e9, 1)},
                 "cg_iterations": its, "cg_iteration_us": round(1e3 * cg / its, 3), "lambda": rep["lambda_final"],
                 "rank": rank}
+        for pm in sorted(ROOT.glob("profiles/*_pmc_sp_product.json")):
+            pj = json.loads(pm.read_text())
+            if abs(pj.get("bytes_per_launch_algorithmic", -1) - out["bytes_per_launch"]) < 1e-6 * out["bytes_per_launch"]:
+                out["traffic"] = pj["traffic_bytes_per_launch"]
+                out["traffic_source"] = pm.name
+        return out
     if "pcg_product" in stats:
         pp = stats["pcg_product"]
         its = max(pp["launches"], 1)

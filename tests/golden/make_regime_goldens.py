@@ -1,0 +1,79 @@
+"""Golden fixtures of the three weight regimes at 10k correspondences x 2 views, 25 LM iterations
+(Simulation.yaml numberOfIterations, Data/Simulation.yaml:80), g2o numeric Jacobians (the reference's
+arithmetic), computed by the oracle (oracle/deftri_oracle.c: the reference LM restated in C with an
+exact SimplicialLDLT step, eliminating in the nested-dissection order of the host analysis):
+
+  simulation  Simulation.yaml   KB8 of Simulation.yaml, rep 1, arap 2e5, sigma_d 3 mm
+  drunkard    Drunkard.yaml     KB8 190.68, rep 1, arap 1e7, DepthWeight 0.3 -> sigma_d 3e-4 m (:68,77)
+  realcolon   Realcolon.yaml    KB8 with d0..d3 (:15-23), rep 1, arap 0.1, DepthWeight 0.001 -> 1e-6 m (:101,110)
+
+Unlike the C2 golden (whose near-stalled LM moves the RMSE by 3.6e-5 px) every one of these moves
+the reprojection RMSE (calculatePixelsStandDev) by more than 5e-3 px, so the north-star 1e-4 px
+criterion can fail.  Stored per regime: chi2 and trials per iteration, final lambda, the solved
+points' fixed subsample (every 53rd) and coordinate sums, the initial and final RMSE.  The scenes are
+regenerated from their seeds by the tests (deterministic host code).
+
+Usage: python tests/golden/make_regime_goldens.py   (about 5 minutes of one core)
+"""
+import copy
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT / "triangulation-in-deformable-scenes_amd"))
+sys.path.insert(0, str(ROOT))
+from deftri import capi, metrics, sim               # noqa: E402
+from oracle import oracle                             # noqa: E402
+
+N_CORR, SEED, N_IT, STRIDE = 10000, 5, 25, 53
+REGIMES = {
+    "simulation": dict(kb8="SIM_KB8", rep=1.0, arap=2e5, sigma=float(np.float32(0.003))),
+    "drunkard": dict(kb8="DRUNKARD_KB8", rep=1.0, arap=1e7, sigma=float(np.float32(0.3) / np.float32(1000.0))),
+    "realcolon": dict(kb8="REALCOLON_KB8", rep=1.0, arap=0.1, sigma=float(np.float32(0.001) / np.float32(1000.0))),
+}
+
+
+def scene(name):
+    r = REGIMES[name]
+    m, _ = sim.simulate_two_view(n=N_CORR, seed=SEED, kb8=getattr(sim, r["kb8"]), scale_scene=True, compact=True)
+    host = capi.Context(-1)
+    p = host.build_graph(m, r["rep"], r["arap"], np.float32(r["sigma"]))
+    return p, m, host
+
+
+def main():
+    d = HERE / "regimes"
+    d.mkdir(exist_ok=True)
+    for name in (sys.argv[1:] or REGIMES):
+        p, m, host = scene(name)
+        host.analyse(p)
+        oracle.set_vertex_order(host.vertex_order())
+        t = time.time()
+        res = oracle.solve_lm(p, N_IT, analytic=False)
+        dt = time.time() - t
+        oracle.set_vertex_order(None)
+        R = res["report"]
+        rms0 = metrics.pixels_stand_dev(m)
+        m1 = copy.deepcopy(m)
+        metrics.apply_solution(m1, list(p.point_ids), res["points"])
+        rms1 = metrics.pixels_stand_dev(m1)
+        pts = res["points"]
+        np.savez_compressed(d / f"{name}.npz", points_sub=pts[::STRIDE], chi2_iter=np.array(R["chi2_iter"]),
+                            trials_iter=np.array(R["trials_iter"]))
+        meta = {"regime": name, **REGIMES[name], "n_corr": N_CORR, "seed": SEED, "n_iterations": N_IT,
+                "stride": STRIDE, "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"],
+                "lambda_final": R["lambda_final"], "iterations": R["iterations"], "trials_total": R["trials_total"],
+                "point_sum": pts.sum(0).tolist(), "scales": res["scales"].tolist(), "tg": res["tg"].tolist(),
+                "rms_initial": rms0, "rms_final": rms1, "summary": p.summary(), "oracle_seconds": round(dt, 1)}
+        (d / f"{name}.json").write_text(json.dumps(meta, indent=1))
+        print(name, json.dumps({k: meta[k] for k in ("chi2_initial", "chi2_final", "trials_total", "oracle_seconds")}),
+              rms0["desv"], "->", rms1["desv"], flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -15,7 +15,10 @@
 #include "graph_builder.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 #include <numeric>
 #include <unordered_map>
@@ -312,8 +315,13 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 if (kf2.point_id[s] >= 0)
                     for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
             int n1 = (int)pos1.size() / 3, n2 = (int)pos2.size() / 3;
+            static const bool timing = std::getenv("DEFTRI_GRAPH_TIMING") != nullptr;
+            auto tnow = [] { return std::chrono::steady_clock::now(); };
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            auto t0 = tnow();
             Mesh M;
             if (!build_mesh(pos1, n1, M, err)) return false;
+            auto t1 = tnow();
             // T_global: map transformation for (kf1, kf2) or identity (:664-677)
             // getGlobalKeyFramesTransformation(k2->first, k1->first) = (kf1.id, kf2.id): the table
             // entry for that ordered pair, a default (identity) SE3f when absent (Map.cc:332-343)
@@ -336,6 +344,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             std::vector<int32_t> posIdx = vector_map(pos1, n1);
             std::unordered_map<int32_t, int32_t> inv;
             for (int v = 0; v < n1; v++) inv[posIdx[v]] = v;
+            auto t2 = tnow();
             // computeR
             std::vector<double> Rs(9 * (size_t)n1, 0.0);
             for (int v = 0; v < n1; v++) { Rs[9 * v] = Rs[9 * v + 4] = Rs[9 * v + 8] = 1.0; }
@@ -355,6 +364,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 }
                 procrustes_rotation(S, &Rs[9 * i]);
             }
+            auto t3 = tnow();
             g.rot.insert(g.rot.end(), Rs.begin(), Rs.end());
             for (int i = 0; i < 7; i++) g.tg.push_back(Tg[i]);
             int32_t s1 = (int32_t)g.scales.size();
@@ -419,6 +429,9 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 }
             }
             rot_base += n1;
+            if (timing)
+                std::fprintf(stderr, "[deftri graph] pair %d: mesh %.1f ms, vector map %.1f, computeR %.1f, edges %.1f\n", q,
+                             ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, tnow()));
         }
     }
     deftri_problem_desc &d = g.desc;
