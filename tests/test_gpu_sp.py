@@ -238,3 +238,32 @@ def test_sharded_iterative_matches_one_rank(kind, world):
             np.testing.assert_allclose(rep["chi2_iter"], rr["chi2_iter"], rtol=tol)
             assert np.abs(P - pts).max() <= tol * np.abs(pts).max()
             np.testing.assert_allclose(S, sc, rtol=tol)
+
+
+def test_iterative_plan_reuse_matches_fresh_upload():
+    """An upload with the uploaded problem's structure and ordering coordinates (NLopt's evaluations:
+    the same graph under other weights) keeps the iterative plan and copies only the values; the LM
+    result is bit-identical to a fresh context's."""
+    m, _ = sim.simulate_two_view(n=20000, seed=4, scale_scene=True, compact=True)
+    host = capi.Context(-1)
+    p1 = host.build_graph(m, 1.0, 2e5, np.float32(0.003))
+    p2 = host.build_graph(m, 2.0, 5e4, np.float32(0.01))
+    host.close()
+    a, b = capi.Context(0), capi.Context(0)
+    try:
+        for c in (a, b):
+            c.set_plan("iterative")
+        a.upload(p1)
+        a.solve_lm(3)
+        a.upload(p2)
+        ra = a.solve_lm(5)
+        b.upload(p2)
+        rb = b.solve_lm(5)
+        assert ra["plan_reuses"] == 1 and rb["plan_reuses"] == 0
+        assert ra["trials_iter"] == rb["trials_iter"]
+        assert ra["chi2_iter"] == rb["chi2_iter"]
+        for x, y in zip(a.download(), b.download()):
+            assert np.array_equal(x, y)
+    finally:
+        a.close()
+        b.close()

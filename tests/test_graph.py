@@ -131,3 +131,38 @@ def test_global_transform_lookup_per_pair(host):
         assert sum(non_identity) == 1, non_identity        # only the pair (KF 1, KF 0) has a stored T
         t_new = pc.tg.reshape(-1, 7)[int(np.argmax(non_identity))] * np.r_[1, 1, 1, 1, 1.5, 1.5, 1.5]
         m.insert_global_T(0, 1, SE3f.from7(t_new))
+
+
+def _equal_problems(a, b):
+    for k in INT_FIELDS + F_FIELDS + ["cam_kb8", "order_xy", "point_ids"]:
+        x, y = getattr(a, k), getattr(b, k)
+        assert np.array_equal(x, y), k
+
+
+def test_graph_memo_same_map_other_weights():
+    """A repeated call on an unchanged map (NLopt's clones, nloptOptimization.cc:4-37) is answered
+    from the graph memo; only the weights' entries are recomputed — bit-identical to a fresh build."""
+    import copy
+    m, _ = sim.simulate_two_view(n=1200, seed=11)
+    with capi.Context(-1) as c:
+        c.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        for w in ((2.0, 3e4, np.float32(0.01)), (1.0, 2e5, np.float32(0.003))):
+            got = c.build_graph(copy.deepcopy(m), *w)
+            with capi.Context(-1) as f:
+                _equal_problems(got, f.build_graph(m, *w))
+
+
+def test_graph_memo_miss_on_moved_point():
+    """Any input change (here one MapPoint moved, as after a write-back) rebuilds the graph."""
+    m, _ = sim.simulate_two_view(n=1200, seed=12)
+    with capi.Context(-1) as c:
+        p0 = c.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        mc, keep = m.to_c()
+        kf = mc.keyframes[0]
+        s = next(i for i in range(kf.n_slots) if kf.point_id[i] >= 0)
+        kf.point_pos[3 * s] += 1e-3
+        m.from_c(mc, keep)
+        p1 = c.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        with capi.Context(-1) as f:
+            _equal_problems(p1, f.build_graph(m, 1.0, 2e5, np.float32(0.003)))
+        assert not np.array_equal(p0.points, p1.points)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3: graph-build timings (host threads vs device computeR), plan reuse, e2e bench line
+set -o pipefail
+mkdir -p gpurun_out/r03g
+export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_graph_gpu.py tests/test_gpu_sp.py > gpurun_out/r03g/pytest.log 2>&1 &&
+for t in 1 4 16; do DEFTRI_HOST_THREADS=$t DEFTRI_NO_GRAPH_MEMO=1 DEFTRI_GRAPH_TIMING=1 timeout -k 10 120 python tools/graph_timing.py 100000 2 --check tools/graph_digest_c2.json >> gpurun_out/r03g/graph_host.log 2>&1 || exit 1; done &&
+DEFTRI_NO_GRAPH_MEMO=1 DEFTRI_GRAPH_TIMING=1 timeout -k 10 120 python tools/graph_timing.py 100000 3 --device 0 --check tools/graph_digest_c2.json > gpurun_out/r03g/graph_dev.log 2>&1 &&
+DEFTRI_GRAPH_TIMING=1 timeout -k 10 300 python bench.py --steps 25 --warmup 2 > gpurun_out/r03g/bench.json 2> gpurun_out/r03g/bench.err

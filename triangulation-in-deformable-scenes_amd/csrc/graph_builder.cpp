@@ -21,144 +21,14 @@
 #include <cstdlib>
 #include <limits>
 #include <numeric>
-#include <unordered_map>
+#include <thread>
 
 #include "delaunay.h"
+#include "procrustes.h"
 
 namespace deftri {
 
 namespace {
-
-// Eigen::JacobiSVD<Matrix3d>(S, ComputeFullU | ComputeFullV) restated (two-sided Jacobi with
-// real_2x2_jacobi_svd + JacobiRotation::makeJacobi, precision 2*eps, then sign fix and a
-// descending selection sort) — computeR (Geometry.cc:590) decomposes with it, and for
-// rank-deficient S_i the rotation depends on exactly these steps.
-struct Rot { double c, s; };
-inline void rot_left(double *M, int p, int q, Rot j) {     // M.applyOnTheLeft(p, q, j)
-    for (int i = 0; i < 3; i++) {
-        double x = M[3 * p + i], y = M[3 * q + i];
-        M[3 * p + i] = j.c * x + j.s * y;
-        M[3 * q + i] = -j.s * x + j.c * y;
-    }
-}
-inline void rot_right(double *M, int p, int q, Rot j) {    // M.applyOnTheRight(p, q, j)
-    Rot t{j.c, -j.s};
-    for (int i = 0; i < 3; i++) {
-        double x = M[3 * i + p], y = M[3 * i + q];
-        M[3 * i + p] = t.c * x + t.s * y;
-        M[3 * i + q] = -t.s * x + t.c * y;
-    }
-}
-void eigen_jacobi_svd3(const double Min[9], double U[9], double sv[3], double V[9]) {
-    const double precision = 2.0 * std::numeric_limits<double>::epsilon();
-    const double considerAsZero = std::numeric_limits<double>::min();
-    double scale = 0;
-    for (int i = 0; i < 9; i++) scale = std::max(scale, std::fabs(Min[i]));
-    if (scale == 0.0) scale = 1.0;
-    double W[9];
-    for (int i = 0; i < 9; i++) W[i] = Min[i] / scale;
-    for (int i = 0; i < 9; i++) U[i] = V[i] = (i % 4 == 0) ? 1.0 : 0.0;
-    double maxDiag = std::max(std::fabs(W[0]), std::max(std::fabs(W[4]), std::fabs(W[8])));
-    bool finished = false;
-    int guard = 0;
-    while (!finished && guard++ < 1000) {
-        finished = true;
-        for (int p = 1; p < 3; p++)
-            for (int q = 0; q < p; q++) {
-                double threshold = std::max(considerAsZero, precision * maxDiag);
-                if (std::fabs(W[3 * p + q]) > threshold || std::fabs(W[3 * q + p]) > threshold) {
-                    finished = false;
-                    // real_2x2_jacobi_svd(W, p, q)
-                    double m00 = W[3 * p + p], m01 = W[3 * p + q], m10 = W[3 * q + p], m11 = W[3 * q + q];
-                    Rot rot1;
-                    double t = m00 + m11, d = m10 - m01;
-                    if (std::fabs(d) < std::numeric_limits<double>::min()) { rot1.s = 0; rot1.c = 1; }
-                    else {
-                        double u = t / d, tmp = std::sqrt(1.0 + u * u);
-                        rot1.s = 1.0 / tmp; rot1.c = u / tmp;
-                    }
-                    // m.applyOnTheLeft(0, 1, rot1)
-                    double a0 = rot1.c * m00 + rot1.s * m10, a1 = rot1.c * m01 + rot1.s * m11;
-                    double b0 = -rot1.s * m00 + rot1.c * m10, b1 = -rot1.s * m01 + rot1.c * m11;
-                    m00 = a0; m01 = a1; m10 = b0; m11 = b1;
-                    // j_right.makeJacobi(m, 0, 1): x = m00, y = m01, z = m11
-                    Rot jr;
-                    double deno = 2.0 * std::fabs(m01);
-                    if (deno < std::numeric_limits<double>::min()) { jr.c = 1; jr.s = 0; }
-                    else {
-                        double tau = (m00 - m11) / deno;
-                        double w = std::sqrt(tau * tau + 1.0);
-                        double tt = tau > 0 ? 1.0 / (tau + w) : 1.0 / (tau - w);
-                        double sign_t = tt > 0 ? 1.0 : -1.0;
-                        double n = 1.0 / std::sqrt(tt * tt + 1.0);
-                        jr.s = -sign_t * (m01 / std::fabs(m01)) * std::fabs(tt) * n;
-                        jr.c = n;
-                    }
-                    // j_left = rot1 * j_right.transpose()
-                    Rot jrt{jr.c, -jr.s};
-                    Rot jl{rot1.c * jrt.c - rot1.s * jrt.s, rot1.c * jrt.s + rot1.s * jrt.c};
-                    rot_left(W, p, q, jl);
-                    rot_right(U, p, q, Rot{jl.c, -jl.s});
-                    rot_right(W, p, q, jr);
-                    rot_right(V, p, q, jr);
-                    maxDiag = std::max(maxDiag, std::max(std::fabs(W[3 * p + p]), std::fabs(W[3 * q + q])));
-                }
-            }
-    }
-    for (int i = 0; i < 3; i++) {
-        double a = W[3 * i + i];
-        sv[i] = std::fabs(a);
-        if (a < 0) for (int r = 0; r < 3; r++) U[3 * r + i] = -U[3 * r + i];
-    }
-    for (int i = 0; i < 3; i++) sv[i] *= scale;
-    for (int i = 0; i < 3; i++) {
-        int pos = i;
-        double mx = sv[i];
-        for (int k = i + 1; k < 3; k++) if (sv[k] > mx) { mx = sv[k]; pos = k; }
-        if (mx == 0.0) break;
-        if (pos != i) {
-            std::swap(sv[i], sv[pos]);
-            for (int r = 0; r < 3; r++) { std::swap(U[3 * r + i], U[3 * r + pos]); std::swap(V[3 * r + i], V[3 * r + pos]); }
-        }
-    }
-}
-
-double det3(const double M[9]) {     // Eigen determinant_impl<3>
-    auto h = [&](int a, int b, int c) { return M[a] * (M[3 + b] * M[6 + c] - M[3 + c] * M[6 + b]); };
-    return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
-}
-
-void quat_from_mat(const double m[9], double q[4]) {   // Eigen Quaternion(Matrix3), x y z w
-    double t = m[0] + m[4] + m[8];
-    if (t > 0) {
-        t = std::sqrt(t + 1.0);
-        q[3] = 0.5 * t;
-        t = 0.5 / t;
-        q[0] = (m[7] - m[5]) * t; q[1] = (m[2] - m[6]) * t; q[2] = (m[3] - m[1]) * t;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > m[3 * i + i]) i = 2;
-        int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = std::sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-        q[i] = 0.5 * t;
-        t = 0.5 / t;
-        q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
-        q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-    }
-}
-
-void mat_from_quat(const double q[4], double R[9]) {
-    double x = q[0], y = q[1], z = q[2], w = q[3];
-    double tx = 2 * x, ty = 2 * y, tz = 2 * z;
-    double twx = tx * w, twy = ty * w, twz = tz * w;
-    double txx = tx * x, txy = ty * x, txz = tz * x;
-    double tyy = ty * y, tyz = tz * y, tzz = tz * z;
-    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
-    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
-    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
-}
 
 // createVectorMap(vertices = pos, positions = pos, 1e-6): vertex k -> first position p with
 // (v_k - p).squaredNorm() <= 1e-12 * min(|v_k|^2, |p|^2)   (Eigen isApprox)
@@ -192,64 +62,150 @@ std::vector<int32_t> vector_map(const std::vector<double> &pos, int n) {
     return out;
 }
 
+// Delaunay mesh with CSR adjacency (ComputeAdjacencyList: sorted, unique neighbour lists) and the
+// cotangent weight of every CSR entry (i, adj[k]) (ComputeEdgeWeightsCot, Geometry.cc:272-298):
+// no hash maps — an edge's weight lives next to its neighbour index, found by a binary search in
+// the lower endpoint's row.
 struct Mesh {
     std::vector<int32_t> tris;
-    std::vector<std::vector<int32_t>> adj;    // sorted
-    std::unordered_map<uint64_t, double> w;   // ordered edge -> cot weight
-    double area = 0;
+    std::vector<int32_t> off, adj;    // CSR, rows sorted
+    std::vector<double> w;            // per CSR entry
+    double area = 0, ms_delaunay = 0;
     int T = 0, hull = 0;
+    int deg(int i) const { return off[i + 1] - off[i]; }
+    int64_t find(int i, int j) const {
+        const int32_t *b = adj.data() + off[i], *e = adj.data() + off[i + 1];
+        const int32_t *p = std::lower_bound(b, e, j);
+        return (p != e && *p == j) ? (int64_t)(p - adj.data()) : -1;
+    }
 };
-
-inline uint64_t ekey(int a, int b) { int lo = std::min(a, b), hi = std::max(a, b); return ((uint64_t)lo << 32) | (uint32_t)hi; }
 
 bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err) {
     if (n < 3) { err = "Not enough points to create a triangular mesh."; return false; }
     std::vector<double> xy(2 * (size_t)n);
     for (int i = 0; i < n; i++) { xy[2 * i] = pos[3 * i]; xy[2 * i + 1] = pos[3 * i + 1]; }
     int skipped = 0;
+    auto td = std::chrono::steady_clock::now();
     if (!delaunay2d(xy.data(), n, M.tris, M.hull, skipped)) { err = "Delaunay triangulation failed (collinear input)"; return false; }
-    int ntri = (int)M.tris.size() / 3;
+    M.ms_delaunay = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
+    const int ntri = (int)M.tris.size() / 3;
     M.T = ntri + std::max(0, M.hull - 2);       // qhull facets.count(): lower + upper Delaunay facets
-    M.adj.assign(n, {});
-    std::vector<std::pair<uint64_t, int32_t>> e2v;
-    e2v.reserve(3 * (size_t)ntri);
+    // adjacency: 2 candidate entries per triangle corner, then per-row sort + unique + compaction
+    std::vector<int32_t> cnt(n + 1, 0);
+    for (int k = 0; k < 3 * ntri; k++) cnt[M.tris[k] + 1] += 2;
+    for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> tmp(cnt[n]), fill(cnt.begin(), cnt.end() - 1);
     for (int t = 0; t < ntri; t++) {
-        int a = M.tris[3 * t], b = M.tris[3 * t + 1], c = M.tris[3 * t + 2];
-        M.adj[a].push_back(b); M.adj[a].push_back(c);
-        M.adj[b].push_back(a); M.adj[b].push_back(c);
-        M.adj[c].push_back(a); M.adj[c].push_back(b);
-        e2v.emplace_back(ekey(a, b), c);
-        e2v.emplace_back(ekey(b, c), a);
-        e2v.emplace_back(ekey(c, a), b);
+        const int a = M.tris[3 * t], b = M.tris[3 * t + 1], c = M.tris[3 * t + 2];
+        tmp[fill[a]++] = b; tmp[fill[a]++] = c;
+        tmp[fill[b]++] = a; tmp[fill[b]++] = c;
+        tmp[fill[c]++] = a; tmp[fill[c]++] = b;
         const double *p0 = &pos[3 * a], *p1 = &pos[3 * b], *p2 = &pos[3 * c];
         double x[3] = {p0[0] - p1[0], p0[1] - p1[1], p0[2] - p1[2]};
         double y[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
         double cr[3] = {x[1] * y[2] - x[2] * y[1], x[2] * y[0] - x[0] * y[2], x[0] * y[1] - x[1] * y[0]};
         M.area += 0.5 * std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
     }
-    for (auto &a : M.adj) { std::sort(a.begin(), a.end()); a.erase(std::unique(a.begin(), a.end()), a.end()); }
-    std::stable_sort(e2v.begin(), e2v.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
-    M.w.reserve(e2v.size());
-    for (size_t i = 0; i < e2v.size();) {
-        size_t j = i;
-        double sum = 0;
-        int cnt = 0;
-        int e0 = (int)(e2v[i].first >> 32), e1 = (int)(e2v[i].first & 0xFFFFFFFFu);
-        while (j < e2v.size() && e2v[j].first == e2v[i].first) {
-            int v2 = e2v[j].second;
+    M.off.assign(n + 1, 0);
+    M.adj.resize(tmp.size());
+    for (int i = 0; i < n; i++) {
+        int32_t *b = tmp.data() + cnt[i], *e = tmp.data() + cnt[i + 1];
+        std::sort(b, e);
+        e = std::unique(b, e);
+        std::copy(b, e, M.adj.data() + M.off[i]);
+        M.off[i + 1] = M.off[i] + (int32_t)(e - b);
+    }
+    M.adj.resize(M.off[n]);
+    // cot weights: per undirected edge (lo, hi), the mean of a.b / |a x b| over its opposite
+    // vertices (at most 2 in a planar triangulation, so the sum is order-independent), a = p_lo - v,
+    // b = p_hi - v, clamped at 0; stored on both CSR entries
+    std::vector<double> sum(M.adj.size(), 0.0);
+    std::vector<int32_t> num(M.adj.size(), 0);
+    for (int t = 0; t < ntri; t++) {
+        const int v3[3] = {M.tris[3 * t], M.tris[3 * t + 1], M.tris[3 * t + 2]};
+        for (int k = 0; k < 3; k++) {
+            const int e0 = std::min(v3[k], v3[(k + 1) % 3]), e1 = std::max(v3[k], v3[(k + 1) % 3]), v2 = v3[(k + 2) % 3];
             const double *A = &pos[3 * e0], *B = &pos[3 * e1], *V = &pos[3 * v2];
             double a[3] = {A[0] - V[0], A[1] - V[1], A[2] - V[2]};
             double b[3] = {B[0] - V[0], B[1] - V[1], B[2] - V[2]};
             double cr[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
-            sum += (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
-            cnt++;
-            j++;
+            const int64_t at = M.find(e0, e1);
+            sum[at] += (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+            num[at]++;
         }
-        double wt = cnt > 0 ? sum / cnt : 0;
-        M.w[e2v[i].first] = wt < 0.0 ? 0.0 : wt;
-        i = j;
     }
+    M.w.assign(M.adj.size(), 0.0);
+    for (int i = 0; i < n; i++)
+        for (int32_t k = M.off[i]; k < M.off[i + 1]; k++) {
+            const int j = M.adj[k];
+            if (j < i) continue;
+            const double wt = num[k] > 0 ? sum[k] / num[k] : 0;
+            M.w[k] = M.w[M.find(j, i)] = wt < 0.0 ? 0.0 : wt;
+        }
     return true;
+}
+
+// open-addressing MapPoint id -> graph point index (ids are >= 0)
+struct IdIndex {
+    std::vector<int64_t> key;
+    std::vector<int32_t> val;
+    uint64_t mask = 0;
+    int64_t size = 0;
+    void init(int64_t expect) {
+        uint64_t cap = 16;
+        while (cap < (uint64_t)std::max<int64_t>(expect, 8) * 2) cap <<= 1;
+        key.assign(cap, -1);
+        val.assign(cap, -1);
+        mask = cap - 1;
+        size = 0;
+    }
+    static uint64_t mix(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; return x; }
+    int32_t *slot(int64_t id) {
+        if ((uint64_t)(size + 1) * 2 > mask + 1) grow();
+        uint64_t h = mix((uint64_t)id) & mask;
+        while (key[h] != -1 && key[h] != id) h = (h + 1) & mask;
+        if (key[h] == -1) { key[h] = id; size++; }
+        return &val[h];
+    }
+    int32_t get(int64_t id) const {
+        uint64_t h = mix((uint64_t)id) & mask;
+        while (key[h] != -1) {
+            if (key[h] == id) return val[h];
+            h = (h + 1) & mask;
+        }
+        return -1;
+    }
+    void grow() {
+        std::vector<int64_t> k0 = std::move(key);
+        std::vector<int32_t> v0 = std::move(val);
+        const uint64_t cap = 2 * (mask + 1);
+        key.assign(cap, -1);
+        val.assign(cap, -1);
+        mask = cap - 1;
+        for (size_t i = 0; i < k0.size(); i++)
+            if (k0[i] != -1) {
+                uint64_t h = mix((uint64_t)k0[i]) & mask;
+                while (key[h] != -1) h = (h + 1) & mask;
+                key[h] = k0[i];
+                val[h] = v0[i];
+            }
+    }
+};
+
+// computeR over vertex ranges on a few host threads: every vertex is independent, so the result
+// does not depend on the split
+template <class F>
+void parallel_for(int n, int min_chunk, F f) {
+    static const int env_t = std::getenv("DEFTRI_HOST_THREADS") ? std::atoi(std::getenv("DEFTRI_HOST_THREADS")) : 0;
+    const int hw = env_t > 0 ? env_t : (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = std::max(1, std::min({hw, 16, n / std::max(min_chunk, 1)}));
+    if (nt <= 1) { f(0, n); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) {
+        const int b = (int)((int64_t)n * t / nt), e = (int)((int64_t)n * (t + 1) / nt);
+        th.emplace_back([=, &f] { f(b, e); });
+    }
+    for (auto &x : th) x.join();
 }
 
 }  // namespace
@@ -258,36 +214,102 @@ bool mesh_adjacency(const std::vector<double> &pos, int n, std::vector<std::vect
                     std::vector<int32_t> &pos_index, double &area, std::string &err) {
     Mesh M;
     if (!build_mesh(pos, n, M, err)) return false;
-    adj = std::move(M.adj);
+    adj.assign(n, {});
+    for (int i = 0; i < n; i++) adj[i].assign(M.adj.begin() + M.off[i], M.adj.begin() + M.off[i + 1]);
     area = M.area;
     pos_index = vector_map(pos, n);
     return true;
 }
 
-void procrustes_rotation(const double S[9], double R[9]) {
-    double U[9], s[3], V[9];
-    eigen_jacobi_svd3(S, U, s, V);
-    auto vut = [&](double *O) {
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) O[3 * i + j] = V[3 * i] * U[3 * j] + V[3 * i + 1] * U[3 * j + 1] + V[3 * i + 2] * U[3 * j + 2];
-    };
-    vut(R);
-    if (det3(R) < 0) {
-        for (int i = 0; i < 3; i++) U[3 * i + 2] *= -1;
-        vut(R);
+void procrustes_rotation(const double S[9], double R[9]) { procrustes_rotation_hd(S, R); }
+
+namespace {
+// every input of the graph build except the three weights, serialized: equal keys give an identical
+// graph (the NLopt objective's clones of one map, repeated calls on an unchanged map)
+void append(std::vector<unsigned char> &k, const void *p, size_t n) {
+    const unsigned char *c = static_cast<const unsigned char *>(p);
+    k.insert(k.end(), c, c + n);
+}
+template <class T> void append_v(std::vector<unsigned char> &k, const T &v) { append(k, &v, sizeof(T)); }
+std::vector<unsigned char> graph_key(const deftri_map &map, int pair_window) {
+    std::vector<unsigned char> k;
+    size_t sz = 64;
+    for (int a = 0; a < map.n_keyframes; a++) {
+        const deftri_keyframe &f = map.keyframes[a];
+        sz += 160 + (size_t)std::max(f.n_slots, 0) * 24 + (size_t)std::max(f.n_obs, 0) * 16 + 4 * (size_t)std::max(f.n_scales, 0);
     }
-    double q[4];
-    quat_from_mat(R, q);                  // Sophus::SO3d keeps the unit quaternion
-    mat_from_quat(q, R);
+    k.reserve(sz + (size_t)std::max(map.n_global, 0) * sizeof(deftri_global_entry));
+    append_v(k, map.n_keyframes); append_v(k, pair_window); append_v(k, map.n_global);
+    append(k, map.global_t, sizeof(map.global_t));
+    if (map.n_global > 0) append(k, map.globals, sizeof(deftri_global_entry) * (size_t)map.n_global);
+    for (int a = 0; a < map.n_keyframes; a++) {
+        const deftri_keyframe &f = map.keyframes[a];
+        append_v(k, f.id); append(k, f.pose, sizeof(f.pose)); append(k, f.kb8, sizeof(f.kb8));
+        append_v(k, f.n_scales); append_v(k, f.depth_scale); append_v(k, f.n_slots); append_v(k, f.n_obs);
+        if (f.n_scales > 0 && f.inv_sigma2) append(k, f.inv_sigma2, 4 * (size_t)f.n_scales);
+        if (f.n_slots > 0) {
+            append(k, f.point_id, 8 * (size_t)f.n_slots); append(k, f.point_pos, 12 * (size_t)f.n_slots);
+            append(k, f.obs_index, 4 * (size_t)f.n_slots);
+        }
+        if (f.n_obs > 0) { append(k, f.kp_uv, 8 * (size_t)f.n_obs); append(k, f.kp_octave, 4 * (size_t)f.n_obs); append(k, f.depth, 4 * (size_t)f.n_obs); }
+    }
+    return k;
 }
 
+bool map_ok(const deftri_map &map, std::string &err) {
+    if (map.n_keyframes < 0 || (map.n_keyframes > 0 && !map.keyframes)) { err = "bad map"; return false; }
+    if (map.n_global > 0 && !map.globals) { err = "bad map: globals"; return false; }
+    for (int a = 0; a < map.n_keyframes; a++) {
+        const deftri_keyframe &f = map.keyframes[a];
+        if (f.n_slots < 0 || f.n_obs < 0 || f.n_scales < 0 || (f.n_slots > 0 && (!f.point_id || !f.point_pos || !f.obs_index)) ||
+            (f.n_obs > 0 && (!f.kp_uv || !f.kp_octave || !f.depth)) || (f.n_scales > 0 && !f.inv_sigma2)) {
+            err = "bad map: keyframe arrays";
+            return false;
+        }
+    }
+    return true;
+}
+}  // namespace
+
 bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
-                      GraphResult &g, std::string &err, int pair_window) {
+                      GraphResult &g, std::string &err, int pair_window, GraphDevice *gdev) {
+    if (!map_ok(map, err)) return false;
+    const double info_dep = 1.0 / ((double)depth_error * (double)depth_error);
+    static const bool no_memo = std::getenv("DEFTRI_NO_GRAPH_MEMO") != nullptr;
+    std::vector<unsigned char> key = graph_key(map, pair_window);
+    if (!no_memo && g.memo_valid && key == g.memo_key) {
+        // the same map: only the weights can differ; recompute the information entries they scale
+        for (size_t e = 0; e < g.rep_info.size(); e++) g.rep_info[e] = g.rep_base[e] * rep_weight;
+        for (size_t q = 0; q < g.pair_info.size(); q++) g.pair_info[q] = arap_weight * std::pow((double)g.pair_T[q], 2);
+        std::fill(g.dep_info.begin(), g.dep_info.end(), info_dep);
+        g.memo_hits++;
+        return true;
+    }
+    const int64_t hits = g.memo_hits;
     g = GraphResult();
-    int K = map.n_keyframes;
-    if (K < 0 || (K > 0 && !map.keyframes)) { err = "bad map"; return false; }
+    g.memo_hits = hits;
+    const int K = map.n_keyframes;
     std::vector<int32_t> cam_of(K, -1);
-    std::unordered_map<int64_t, int32_t> pidx;
+    IdIndex pidx;
+    {
+        int64_t slots = 0, npairs = 0;
+        for (int a = 0; a < K; a++)
+            for (int b = a + 1; b < K; b++) {
+                if (pair_window > 0 && b - a > pair_window) continue;
+                slots += std::min(map.keyframes[a].n_slots, map.keyframes[b].n_slots);
+                npairs++;
+            }
+        pidx.init(2 * slots);
+        g.rep_point.reserve(2 * slots); g.rep_cam.reserve(2 * slots); g.rep_obs.reserve(4 * slots);
+        g.rep_info.reserve(2 * slots); g.rep_base.reserve(2 * slots);
+        g.dep_point.reserve(2 * slots); g.dep_scale.reserve(2 * slots); g.dep_cam.reserve(2 * slots);
+        g.dep_meas.reserve(2 * slots); g.dep_info.reserve(2 * slots);
+        g.arap_pts.reserve(4 * 6 * slots); g.arap_pair.reserve(6 * slots); g.arap_rot.reserve(2 * 6 * slots);
+        g.arap_w.reserve(6 * slots); g.rot.reserve(9 * slots);
+        g.point_mpid.reserve(2 * slots); g.points.reserve(6 * slots); g.point_orig.reserve(6 * slots);
+        g.order_xy.reserve(4 * slots);
+        (void)npairs;
+    }
     auto cam_index = [&](int k) {
         if (cam_of[k] < 0) {
             cam_of[k] = (int32_t)(g.cam_pose.size() / 7);
@@ -298,26 +320,27 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         return cam_of[k];
     };
     g.kf_scale.assign(K, -1);
-    const double info_dep = 1.0 / ((double)depth_error * (double)depth_error);
     int32_t rot_base = 0;
+    static const bool timing = std::getenv("DEFTRI_GRAPH_TIMING") != nullptr;
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     for (int a = 0; a < K; a++) {
         for (int b = a + 1; b < K; b++) {
             if (pair_window > 0 && b - a > pair_window) continue;
             const deftri_keyframe &kf1 = map.keyframes[b];   // pKF1 = k2->second
             const deftri_keyframe &kf2 = map.keyframes[a];   // pKF2 = k1->second
-            int32_t q = (int32_t)g.pair_area.size();
+            const int32_t q = (int32_t)g.pair_area.size();
             // extractPositions
             std::vector<double> pos1, pos2;
+            pos1.reserve(3 * (size_t)kf1.n_slots);
+            pos2.reserve(3 * (size_t)kf2.n_slots);
             for (int s = 0; s < kf1.n_slots; s++)
                 if (kf1.point_id[s] >= 0)
                     for (int k = 0; k < 3; k++) pos1.push_back((double)kf1.point_pos[3 * s + k]);
             for (int s = 0; s < kf2.n_slots; s++)
                 if (kf2.point_id[s] >= 0)
                     for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
-            int n1 = (int)pos1.size() / 3, n2 = (int)pos2.size() / 3;
-            static const bool timing = std::getenv("DEFTRI_GRAPH_TIMING") != nullptr;
-            auto tnow = [] { return std::chrono::steady_clock::now(); };
-            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            const int n1 = (int)pos1.size() / 3, n2 = (int)pos2.size() / 3;
             auto t0 = tnow();
             Mesh M;
             if (!build_mesh(pos1, n1, M, err)) return false;
@@ -341,97 +364,109 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 bool rot_id = qn > 0 && std::fabs(std::fabs(Tg[3] / qn) - 1.0) < 1e-10;
                 if (tn == 0.0f && rot_id) { Tg[0] = Tg[1] = Tg[2] = 0; Tg[3] = 1; Tg[4] = Tg[5] = Tg[6] = 0; }
             }
-            std::vector<int32_t> posIdx = vector_map(pos1, n1);
-            std::unordered_map<int32_t, int32_t> inv;
+            const std::vector<int32_t> posIdx = vector_map(pos1, n1);
+            std::vector<int32_t> inv(n1, -1);           // invertedPosIndexes: the last vertex wins
             for (int v = 0; v < n1; v++) inv[posIdx[v]] = v;
             auto t2 = tnow();
-            // computeR
-            std::vector<double> Rs(9 * (size_t)n1, 0.0);
-            for (int v = 0; v < n1; v++) { Rs[9 * v] = Rs[9 * v + 4] = Rs[9 * v + 8] = 1.0; }
-            for (int p = 0; p < n1; p++) {
-                auto it = inv.find(p);
-                if (it == inv.end()) continue;
-                int i = it->second;
-                double S[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-                for (int j : M.adj[i]) {
-                    double wt = M.w[ekey(i, j)];
-                    int pi = posIdx[i], pj = posIdx[j];
-                    if (pi >= n2 || pj >= n2) continue;
-                    double e1[3], e2[3];
-                    for (int k = 0; k < 3; k++) { e1[k] = pos1[3 * pi + k] - pos1[3 * pj + k]; e2[k] = pos2[3 * pi + k] - pos2[3 * pj + k]; }
-                    for (int r = 0; r < 3; r++)
-                        for (int c = 0; c < 3; c++) S[3 * r + c] += wt * e1[r] * e2[c];
-                }
-                procrustes_rotation(S, &Rs[9 * i]);
+            // computeR: one Procrustes rotation per vertex, identity where no position maps to it
+            const size_t rbase = g.rot.size();
+            g.rot.resize(rbase + 9 * (size_t)n1);
+            double *Rs = g.rot.data() + rbase;
+            if (gdev) {
+                if (!gdev->compute_r(n1, n2, M.off.data(), M.adj.data(), M.w.data(), (int64_t)M.adj.size(), posIdx.data(),
+                                     inv.data(), pos1.data(), pos2.data(), Rs, err))
+                    return false;
+            } else {
+                parallel_for(n1, 2048, [&](int lo, int hi) {
+                    for (int i = lo; i < hi; i++)
+                        compute_r_vertex(i, n2, M.off.data(), M.adj.data(), M.w.data(), posIdx.data(), inv.data(), pos1.data(),
+                                         pos2.data(), Rs + 9 * (size_t)i);
+                });
             }
             auto t3 = tnow();
-            g.rot.insert(g.rot.end(), Rs.begin(), Rs.end());
             for (int i = 0; i < 7; i++) g.tg.push_back(Tg[i]);
-            int32_t s1 = (int32_t)g.scales.size();
+            const int32_t s1 = (int32_t)g.scales.size();
             g.scales.push_back(kf1.depth_scale); g.kf_scale[b] = s1;
-            int32_t s2 = (int32_t)g.scales.size();
+            const int32_t s2 = (int32_t)g.scales.size();
             g.scales.push_back(kf2.depth_scale); g.kf_scale[a] = s2;
-            int32_t c1 = cam_index(b), c2 = cam_index(a);
+            const int32_t c1 = cam_index(b), c2 = cam_index(a);
             g.pair_area.push_back(M.area);
             g.pair_info.push_back(arap_weight * std::pow((double)M.T, 2));
             g.pair_kf1.push_back(b); g.pair_kf2.push_back(a);
             g.pair_T.push_back(M.T); g.pair_hull.push_back(M.hull);
             auto add_point = [&](int64_t id, const float *p, int ord_slot) {
-                auto it = pidx.find(id);
-                if (it != pidx.end()) return it->second;
-                int32_t k = (int32_t)g.point_mpid.size();
-                pidx[id] = k;
+                int32_t *v = pidx.slot(id);
+                if (*v >= 0) return *v;
+                const int32_t k = (int32_t)g.point_mpid.size();
+                *v = k;
                 g.point_mpid.push_back(id);
                 for (int c = 0; c < 3; c++) { g.points.push_back((double)p[c]); g.point_orig.push_back(p[c]); }
                 g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot]);
                 g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot + 1]);
                 return k;
             };
-            int nslots = kf1.n_slots;
+            // a slot's MapPoints are fixed within the pair: their graph indices are looked up once
+            // (creation order unchanged: a point is still created at its first encounter)
+            const int ns12 = std::min(kf1.n_slots, kf2.n_slots);
+            std::vector<int32_t> slot_pt(2 * (size_t)ns12, -1);
+            auto slot_points = [&](int slot, int32_t &a1, int32_t &a2) {
+                int32_t *c = &slot_pt[2 * (size_t)slot];
+                if (c[0] < 0) {
+                    c[0] = add_point(kf1.point_id[slot], kf1.point_pos + 3 * slot, slot);
+                    c[1] = add_point(kf2.point_id[slot], kf2.point_pos + 3 * slot, slot);
+                }
+                a1 = c[0];
+                a2 = c[1];
+            };
+            const int nslots = kf1.n_slots;
             for (int mp = 0; mp < nslots; mp++) {
                 if (mp >= kf2.n_slots) break;
-                int64_t id1 = kf1.point_id[mp], id2 = kf2.point_id[mp];
+                const int64_t id1 = kf1.point_id[mp], id2 = kf2.point_id[mp];
                 if (id1 < 0 || id2 < 0) continue;
-                int32_t p1 = add_point(id1, kf1.point_pos + 3 * mp, mp);
-                int32_t p2 = add_point(id2, kf2.point_pos + 3 * mp, mp);
-                int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
+                int32_t p1, p2;
+                slot_points(mp, p1, p2);
+                const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
                 if (o1 < 0 || o2 < 0) continue;
                 if (o1 >= kf1.n_obs || o2 >= kf2.n_obs) { err = "observation index out of range"; return false; }
+                const int32_t oc1 = kf1.kp_octave[o1], oc2 = kf2.kp_octave[o2];
+                if (oc1 < 0 || oc1 >= kf1.n_scales || oc2 < 0 || oc2 >= kf2.n_scales) { err = "keypoint octave out of range"; return false; }
                 // reprojection edges (:765-812)
+                const double base1 = (double)kf1.inv_sigma2[oc1], base2 = (double)kf2.inv_sigma2[oc2];
                 g.rep_point.push_back(p1); g.rep_cam.push_back(c1);
                 g.rep_obs.push_back((double)kf1.kp_uv[2 * o1]); g.rep_obs.push_back((double)kf1.kp_uv[2 * o1 + 1]);
-                g.rep_info.push_back((double)kf1.inv_sigma2[kf1.kp_octave[o1]] * rep_weight);
+                g.rep_base.push_back(base1); g.rep_info.push_back(base1 * rep_weight);
                 g.rep_point.push_back(p2); g.rep_cam.push_back(c2);
                 g.rep_obs.push_back((double)kf2.kp_uv[2 * o2]); g.rep_obs.push_back((double)kf2.kp_uv[2 * o2 + 1]);
-                g.rep_info.push_back((double)kf2.inv_sigma2[kf2.kp_octave[o2]] * rep_weight);
+                g.rep_base.push_back(base2); g.rep_info.push_back(base2 * rep_weight);
                 // depth edges (:816-856), simulated per-index depth
                 g.dep_point.push_back(p1); g.dep_scale.push_back(s1); g.dep_cam.push_back(c1);
                 g.dep_meas.push_back((double)kf1.depth[o1]); g.dep_info.push_back(info_dep);
                 g.dep_point.push_back(p2); g.dep_scale.push_back(s2); g.dep_cam.push_back(c2);
                 g.dep_meas.push_back((double)kf2.depth[o2]); g.dep_info.push_back(info_dep);
                 // ARAP edges (:871-953)
-                auto it = inv.find(mp);
-                if (it == inv.end()) continue;
-                int i = it->second;
-                if (M.adj[i].empty()) continue;
-                for (int j : M.adj[i]) {
-                    int slot = posIdx[j];
+                if (mp >= n1) continue;
+                const int i = inv[mp];
+                if (i < 0) continue;
+                for (int32_t k = M.off[i]; k < M.off[i + 1]; k++) {
+                    const int j = M.adj[k];
+                    const int slot = posIdx[j];
                     if (slot >= kf1.n_slots || slot >= kf2.n_slots) continue;
-                    int64_t j1 = kf1.point_id[slot], j2 = kf2.point_id[slot];
+                    const int64_t j1 = kf1.point_id[slot], j2 = kf2.point_id[slot];
                     if (j1 < 0 || j2 < 0) continue;
-                    int32_t pj1 = add_point(j1, kf1.point_pos + 3 * slot, slot);
-                    int32_t pj2 = add_point(j2, kf2.point_pos + 3 * slot, slot);
+                    int32_t pj1, pj2;
+                    slot_points(slot, pj1, pj2);
                     g.arap_pts.push_back(p1); g.arap_pts.push_back(p2);
                     g.arap_pts.push_back(pj1); g.arap_pts.push_back(pj2);
                     g.arap_pair.push_back(q);
                     g.arap_rot.push_back(rot_base + i); g.arap_rot.push_back(rot_base + j);
-                    g.arap_w.push_back(M.w[ekey(i, j)]);
+                    g.arap_w.push_back(M.w[k]);
                 }
             }
             rot_base += n1;
             if (timing)
-                std::fprintf(stderr, "[deftri graph] pair %d: mesh %.1f ms, vector map %.1f, computeR %.1f, edges %.1f\n", q,
-                             ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, tnow()));
+                std::fprintf(stderr, "[deftri graph] pair %d: mesh %.1f ms (delaunay %.1f), vector map %.1f, computeR %.1f%s (kernel %.3f), edges %.1f\n", q,
+                             ms(t0, t1), M.ms_delaunay, ms(t1, t2), ms(t2, t3), gdev ? " device" : " host", gdev ? gdev->ms_last : 0.0,
+                             ms(t3, tnow()));
         }
     }
     deftri_problem_desc &d = g.desc;
@@ -454,6 +489,8 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     d.arap_pts = g.arap_pts.data(); d.arap_pair = g.arap_pair.data(); d.arap_rot = g.arap_rot.data();
     d.arap_w = g.arap_w.data(); d.rot = g.rot.data(); d.pair_area = g.pair_area.data(); d.pair_info = g.pair_info.data();
     d.order_xy = g.order_xy.data();
+    g.memo_key = std::move(key);
+    g.memo_valid = true;
     return true;
 }
 
@@ -463,9 +500,9 @@ void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<dou
     for (int k = 0; k < map.n_keyframes; k++)
         if (g.kf_scale[k] >= 0) map.keyframes[k].depth_scale = scales[g.kf_scale[k]];
     // points: fp32 writeback + sum ||p_old - p_new|| (:974-990)
-    std::unordered_map<int64_t, int32_t> pidx;
-    pidx.reserve(g.point_mpid.size() * 2);
-    for (size_t i = 0; i < g.point_mpid.size(); i++) pidx[g.point_mpid[i]] = (int32_t)i;
+    IdIndex pidx;
+    pidx.init((int64_t)g.point_mpid.size());
+    for (size_t i = 0; i < g.point_mpid.size(); i++) *pidx.slot(g.point_mpid[i]) = (int32_t)i;
     double upd = 0;
     for (size_t i = 0; i < g.point_mpid.size(); i++) {
         float nf[3] = {(float)points[3 * i], (float)points[3 * i + 1], (float)points[3 * i + 2]};
@@ -476,9 +513,9 @@ void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<dou
         deftri_keyframe &kf = map.keyframes[k];
         for (int s = 0; s < kf.n_slots; s++) {
             if (kf.point_id[s] < 0) continue;
-            auto it = pidx.find(kf.point_id[s]);
-            if (it == pidx.end()) continue;
-            for (int c = 0; c < 3; c++) kf.point_pos[3 * s + c] = (float)points[3 * (size_t)it->second + c];
+            const int32_t i = pidx.get(kf.point_id[s]);
+            if (i < 0) continue;
+            for (int c = 0; c < 3; c++) kf.point_pos[3 * s + c] = (float)points[3 * (size_t)i + c];
         }
     }
     if (optimization_update) *optimization_update = upd;

@@ -1,6 +1,8 @@
 // graph_builder.h — the graph construction of the reference's arapOptimization
 // (Modules/Optimization/g2oBundleAdjustment.cc:640-953) over the deftri_map view.
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -23,12 +25,35 @@ struct GraphResult {
     std::vector<int32_t> pair_kf1, pair_kf2;  // per pair: keyframe indices (map order)
     std::vector<int32_t> pair_T;              // facets.count() per pair
     std::vector<int32_t> pair_hull;           // convex hull size per pair
+    std::vector<double> rep_base;             // per reprojection edge: invSigma2 of its octave
+    // memo: the serialized inputs (everything but the weights) of the graph held here
+    std::vector<unsigned char> memo_key;
+    bool memo_valid = false;
+    int64_t memo_hits = 0;                    // calls answered from the memo (kept across rebuilds)
+};
+
+// computeR on the device (graph_dev.hip): one thread per mesh vertex over the pair's CSR mesh,
+// the same arithmetic as the host loop (procrustes.h), so both give the same rotations bit for bit
+class GraphDevice {
+ public:
+    GraphDevice(int device, hipStream_t st) : dev_(device), st_(st) {}
+    ~GraphDevice();
+    bool compute_r(int n1, int n2, const int32_t *off, const int32_t *adj, const double *w, int64_t nadj,
+                   const int32_t *pos_idx, const int32_t *inv, const double *pos1, const double *pos2, double *R,
+                   std::string &err);
+    double ms_last = 0;          // device time of the last compute_r (kernel only)
+
+ private:
+    int dev_;
+    hipStream_t st_;
+    void *buf_ = nullptr;
+    size_t cap_ = 0;
 };
 
 // pair_window > 0: only keyframe pairs (a, b) with b - a <= pair_window in map order (the
 // sliding-window deviation of BASELINE C5; 0 = every pair, the reference's loop :640-645)
 bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
-                      GraphResult &g, std::string &err, int pair_window = 0);
+                      GraphResult &g, std::string &err, int pair_window = 0, GraphDevice *gdev = nullptr);
 
 void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<double> &points,
                     const std::vector<double> &scales, const std::vector<double> &tg, double *optimization_update);

@@ -119,6 +119,7 @@ struct deftri_ctx {
     hipEvent_t ev[8]{};
     // map-level graph (deftri_arap_build_graph)
     GraphResult graph;
+    std::unique_ptr<GraphDevice> gdev;      // computeR on this context's device (graph_dev.hip)
     // speculative lambda lanes (see Lane)
     int analytic_jac = 0;                   // deftri_arap_optimization: 0 g2o numeric (reference), 1 analytic
     bool prof_analytic = false;             // deftri_profile_trial linearizes like the last solve_lm
@@ -313,9 +314,16 @@ void copy_host(HostProblem &h, const deftri_problem_desc *d) {
 // plan and only copies the values.
 uint64_t structure_hash(const deftri_problem_desc &d) {
     uint64_t h = 1469598103934665603ull;
-    auto mix = [&](const void *p, size_t n) {
+    auto mix = [&](const void *p, size_t n) {      // 8 bytes per step (a pre-filter, see same_structure)
         const unsigned char *b = (const unsigned char *)p;
-        for (size_t i = 0; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t w;
+            std::memcpy(&w, b + i, 8);
+            h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+            h ^= h >> 29;
+        }
+        for (; i < n; i++) { h ^= b[i]; h *= 1099511628211ull; }
     };
     const int32_t cnt[8] = {d.n_points, d.n_pairs, d.n_scales, d.n_cams, d.n_rep, d.n_depth, d.n_arap, d.n_rot};
     mix(cnt, sizeof(cnt));
@@ -343,6 +351,14 @@ bool same_structure(const deftri_problem_desc &a, const deftri_problem_desc &b) 
            eq(a.dep_point, b.dep_point, a.n_depth) && eq(a.dep_scale, b.dep_scale, a.n_depth) &&
            eq(a.dep_cam, b.dep_cam, a.n_depth) && eq(a.arap_pts, b.arap_pts, 4 * (int64_t)a.n_arap) &&
            eq(a.arap_pair, b.arap_pair, a.n_arap) && eq(a.arap_rot, b.arap_rot, 2 * (int64_t)a.n_arap);
+}
+
+// the coordinates the row order is derived from (order_xy, else the points' x, y): equal on both
+// problems for the iterative plan to be reused
+bool same_order_coordinates(const deftri_problem_desc &a, const deftri_problem_desc &b) {
+    if (a.n_points != b.n_points || (a.order_xy == nullptr) != (b.order_xy == nullptr)) return false;
+    if (a.order_xy) return std::memcmp(a.order_xy, b.order_xy, sizeof(double) * 2 * (size_t)a.n_points) == 0;
+    return std::memcmp(a.points, b.points, sizeof(double) * 3 * (size_t)a.n_points) == 0;
 }
 
 // same structure as the uploaded plan: copy the values (state, cameras, measurements, weights,
@@ -1065,6 +1081,7 @@ int deftri_ctx_destroy(deftri_ctx *ctx) {
     if (ctx->device < 0) { delete ctx; return 0; }
     hipSetDevice(ctx->device);
     free_device(ctx);
+    ctx->gdev.reset();
     delete ctx->sp_tr;
     ctx->sp_tr = nullptr;
     if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -1449,6 +1466,19 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     int rc = validate(ctx, desc);
     if (rc) return rc;
     if (want_iterative(ctx, desc)) {
+        static const bool no_cache = std::getenv("DEFTRI_NO_PLAN_CACHE") != nullptr;
+        if (!no_cache && ctx->sp_on && ctx->sp && ctx->sp->fp32_jac == ctx->jac_fp32 && same_structure(ctx->hp.d, *desc) &&
+            same_order_coordinates(ctx->hp.d, *desc)) {
+            // the plan (row order, shards, wave layout) depends only on the structure and the
+            // ordering coordinates: reuse it and copy the values
+            copy_host(ctx->hp, desc);
+            ctx->sp->tol = ctx->pcg_tol;
+            ctx->sp->max_it = ctx->pcg_max_it;
+            rc = ctx->sp->refresh(*desc);
+            if (rc) { ctx->err = ctx->sp->err; free_device(ctx); return rc; }
+            ctx->plan_reuses++;
+            return 0;
+        }
         // the point-sharded iterative plan: no ordering, no symbolic analysis, no factor
         free_device(ctx);
         ctx->plan_hash = 0;
@@ -1640,6 +1670,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
     if (ctx->sp_on) {
         ctx->prof_analytic = prm->analytic_jacobians != 0;
         int rc = ctx->sp->solve_lm(*prm, R);
+        R.plan_reuses = ctx->plan_reuses;
         return rc ? fail(ctx, rc, ctx->sp->err) : 0;
     }
     R.n_unknowns = ctx->S.ndof;
@@ -2156,11 +2187,24 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
 // ---------------------------------------------------------------------------------------------
 // map level
 // ---------------------------------------------------------------------------------------------
+}  // extern "C"
+namespace {
+// a context with a device runs computeR there (DEFTRI_HOST_COMPUTE_R=1: on the host, for A/B timing)
+GraphDevice *graph_device(deftri_ctx *ctx) {
+    static const bool host_only = std::getenv("DEFTRI_HOST_COMPUTE_R") != nullptr;
+    if (ctx->device < 0 || host_only) return nullptr;
+    hipSetDevice(ctx->device);
+    if (!ctx->gdev) ctx->gdev.reset(new GraphDevice(ctx->device, ctx->st));
+    return ctx->gdev.get();
+}
+}  // namespace
+extern "C" {
+
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight, double arap_weight,
                             float depth_error, const deftri_problem_desc **desc_out) {
     if (!ctx || !map || !desc_out) return DEFTRI_E_ARG;
     std::string err;
-    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window))
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window, graph_device(ctx)))
         return fail(ctx, DEFTRI_E_GRAPH, err);
     *desc_out = &ctx->graph.desc;
     return 0;
@@ -2179,7 +2223,7 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
     (void)global_weight; (void)alpha; (void)beta;   // stored but unused by the reference edges
     if (!ctx || !map) return DEFTRI_E_ARG;
     std::string err;
-    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window))
+    if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window, graph_device(ctx)))
         return fail(ctx, DEFTRI_E_GRAPH, err);
     int rc = deftri_problem_upload(ctx, &ctx->graph.desc);
     if (rc) return rc;

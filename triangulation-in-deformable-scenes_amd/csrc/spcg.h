@@ -169,11 +169,18 @@ void sp_launch_permute_out(int32_t P, int64_t hd, const int32_t *row_of_point, c
                            hipStream_t st);
 
 // The LM solve on the iterative plan (one rank).  Owned by the C-ABI context (solver.cpp).
+// the value arrays of a problem in a plan's layout (SpSolver::gather_values)
+struct SpValues {
+    std::vector<double> pts, tg, sc, cpose, camR, ro, ri, dm, di, aw, rot, parea, pinfo;
+    std::vector<float> kb8;
+};
+
 class SpSolver {
  public:
     SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr);
     ~SpSolver();
     int upload(const deftri_problem_desc &d);
+    int refresh(const deftri_problem_desc &d);     // same structure: values only, plan kept
     int solve_lm(const deftri_lm_params &prm, deftri_report &R);
     int download(double *points, double *scales, double *tg);
     int reset_state();
@@ -228,6 +235,7 @@ class SpSolver {
     int cg_tail(int n);
     int halo(int width, double *vec, bool zp);
     int pcg_solve(double lambda, const double *rhs, bool &solved, int &its);
+    void gather_values(const deftri_problem_desc &d, SpValues &v) const;
 };
 
 }  // namespace deftri

@@ -97,6 +97,56 @@ int SpSolver::put(T **p, const std::vector<T> &v) {
 
 int SpSolver::budget() const { return std::min(kSpMaxIt, max_it > 0 ? max_it : kSpDefaultIt); }
 
+// the values of a problem in the plan's layout (points in row order, the rank's edges): everything
+// a structurally identical problem can change
+void SpSolver::gather_values(const deftri_problem_desc &d, SpValues &v) const {
+    const int32_t NP = d.n_points, Q = d.n_pairs, S = d.n_scales, C = d.n_cams;
+    v.pts.resize(3 * (size_t)NP);
+    for (int32_t r = 0; r < NP; r++)
+        for (int c = 0; c < 3; c++) v.pts[3 * (size_t)r + c] = d.points[3 * (size_t)H.point_of_row[r] + c];
+    v.tg.assign(d.tg, d.tg + 7 * (size_t)Q);
+    v.sc.assign(d.scales, d.scales + S);
+    for (int32_t q = 0; q < Q; q++) quat_norm(&v.tg[7 * (size_t)q]);
+    v.cpose.assign(d.cam_pose, d.cam_pose + 7 * (size_t)C);
+    v.camR.assign(9 * (size_t)std::max(C, 1), 0.0);
+    for (int32_t c = 0; c < C; c++) { quat_norm(&v.cpose[7 * (size_t)c]); quat_mat(&v.cpose[7 * (size_t)c], &v.camR[9 * (size_t)c]); }
+    v.kb8.assign(d.cam_kb8, d.cam_kb8 + 8 * (size_t)C);
+    const size_t nr = H.rep_ids.size(), nd = H.dep_ids.size(), nloc = H.arap_ids.size();
+    v.ro.resize(2 * nr); v.ri.resize(nr); v.dm.resize(nd); v.di.resize(nd); v.aw.resize(nloc);
+    for (size_t j = 0; j < nr; j++) {
+        const int32_t e = H.rep_ids[j];
+        v.ro[2 * j] = d.rep_obs[2 * (size_t)e]; v.ro[2 * j + 1] = d.rep_obs[2 * (size_t)e + 1]; v.ri[j] = d.rep_info[e];
+    }
+    for (size_t j = 0; j < nd; j++) { const int32_t e = H.dep_ids[j]; v.dm[j] = d.dep_meas[e]; v.di[j] = d.dep_info[e]; }
+    for (size_t le = 0; le < nloc; le++) v.aw[le] = d.arap_w[H.arap_ids[le]];
+    v.rot.resize(9 * H.rot_ids.size());
+    for (size_t k = 0; k < H.rot_ids.size(); k++)
+        std::memcpy(&v.rot[9 * k], d.rot + 9 * (size_t)H.rot_ids[k], 9 * sizeof(double));
+    v.parea.assign(d.pair_area, d.pair_area + Q);
+    v.pinfo.assign(d.pair_info, d.pair_info + Q);
+}
+
+// a problem with the uploaded one's structure (same counts and index arrays): copy its values into
+// the existing buffers; the plan, the wave layout and every allocation stay
+int SpSolver::refresh(const deftri_problem_desc &d) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    hipSetDevice(dev_);
+    SPOK(hipStreamSynchronize(st_));
+    SpValues v;
+    gather_values(d, v);
+    auto cp = [&](auto *dst, const auto &src) -> hipError_t {
+        return src.empty() ? hipSuccess : hipMemcpyAsync(dst, src.data(), sizeof(src[0]) * src.size(), hipMemcpyHostToDevice, st_);
+    };
+    SPOK(cp(P.points, v.pts)); SPOK(cp(P.scales, v.sc)); SPOK(cp(P.tg, v.tg));
+    SPOK(cp(init_[0], v.pts)); SPOK(cp(init_[1], v.sc)); SPOK(cp(init_[2], v.tg));
+    SPOK(cp(P.cam_kb8, v.kb8)); SPOK(cp(P.cam_pose, v.cpose)); SPOK(cp(P.cam_R, v.camR));
+    SPOK(cp(P.rep_obs, v.ro)); SPOK(cp(P.rep_info, v.ri)); SPOK(cp(P.dep_meas, v.dm)); SPOK(cp(P.dep_info, v.di));
+    SPOK(cp(P.arap_w, v.aw)); SPOK(cp(P.rot, v.rot)); SPOK(cp(P.pair_area, v.parea)); SPOK(cp(P.pair_info, v.pinfo));
+    P.huber_delta = d.huber_delta;
+    SPOK(hipStreamSynchronize(st_));
+    return 0;
+}
+
 int SpSolver::upload(const deftri_problem_desc &d) {
     hipSetDevice(dev_);
     hipStreamSynchronize(st_);
@@ -109,39 +159,26 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     const int32_t NP = d.n_points, Q = d.n_pairs, S = d.n_scales, C = d.n_cams;
     const int64_t nloc = (int64_t)H.arap_ids.size();
     const int32_t nown = H.hi - H.lo;
-    // the rank's device problem, points in row order
-    std::vector<double> pts(3 * (size_t)NP), tg(d.tg, d.tg + 7 * (size_t)Q), sc(d.scales, d.scales + S);
-    for (int32_t r = 0; r < NP; r++)
-        for (int c = 0; c < 3; c++) pts[3 * (size_t)r + c] = d.points[3 * (size_t)H.point_of_row[r] + c];
-    for (int32_t q = 0; q < Q; q++) quat_norm(&tg[7 * (size_t)q]);
-    std::vector<double> cpose(d.cam_pose, d.cam_pose + 7 * (size_t)C), camR(9 * (size_t)std::max(C, 1));
-    for (int32_t c = 0; c < C; c++) { quat_norm(&cpose[7 * (size_t)c]); quat_mat(&cpose[7 * (size_t)c], &camR[9 * (size_t)c]); }
-    std::vector<float> kb8(d.cam_kb8, d.cam_kb8 + 8 * (size_t)C);
+    SpValues v;
+    gather_values(d, v);
+    std::vector<double> &pts = v.pts, &tg = v.tg, &sc = v.sc, &cpose = v.cpose, &camR = v.camR;
+    std::vector<float> &kb8 = v.kb8;
+    // the rank's edges: structure (rows, cameras, scales, pairs) in the plan's numbering
     const size_t nr = H.rep_ids.size(), nd = H.dep_ids.size();
     std::vector<int32_t> rp(nr), rc(nr), dp(nd), ds(nd), dc(nd);
-    std::vector<double> ro(2 * nr), ri(nr), dm(nd), di(nd);
-    for (size_t j = 0; j < nr; j++) {
-        const int32_t e = H.rep_ids[j];
-        rp[j] = H.row_of_point[d.rep_point[e]]; rc[j] = d.rep_cam[e];
-        ro[2 * j] = d.rep_obs[2 * (size_t)e]; ro[2 * j + 1] = d.rep_obs[2 * (size_t)e + 1]; ri[j] = d.rep_info[e];
-    }
+    for (size_t j = 0; j < nr; j++) { const int32_t e = H.rep_ids[j]; rp[j] = H.row_of_point[d.rep_point[e]]; rc[j] = d.rep_cam[e]; }
     for (size_t j = 0; j < nd; j++) {
         const int32_t e = H.dep_ids[j];
         dp[j] = H.row_of_point[d.dep_point[e]]; ds[j] = d.dep_scale[e]; dc[j] = d.dep_cam[e];
-        dm[j] = d.dep_meas[e]; di[j] = d.dep_info[e];
     }
     std::vector<int32_t> apts(4 * (size_t)nloc), apair(nloc);
-    std::vector<double> aw(nloc);
     for (int64_t le = 0; le < nloc; le++) {
         const int64_t e = H.arap_ids[le];
         for (int k = 0; k < 4; k++) apts[4 * le + k] = H.row_of_point[d.arap_pts[4 * e + k]];
         apair[le] = d.arap_pair[e];
-        aw[le] = d.arap_w[e];
     }
-    std::vector<double> rot(9 * H.rot_ids.size());
-    for (size_t k = 0; k < H.rot_ids.size(); k++)
-        std::memcpy(&rot[9 * k], d.rot + 9 * (size_t)H.rot_ids[k], 9 * sizeof(double));
-    std::vector<double> parea(d.pair_area, d.pair_area + Q), pinfo(d.pair_info, d.pair_info + Q);
+    std::vector<double> &ro = v.ro, &ri = v.ri, &dm = v.dm, &di = v.di, &aw = v.aw, &rot = v.rot, &parea = v.parea,
+                        &pinfo = v.pinfo;
     int rc_;
 #define PUT(dst, v) if ((rc_ = put(&(dst), v))) return rc_
 #define ALLOC(dst, n) if ((rc_ = alloc(&(dst), n))) return rc_

@@ -5,6 +5,7 @@ There is no CPU fallback: if the library is missing, `load()` raises, and every 
 point runs on the GPU or returns an error.
 """
 import ctypes as C
+import time
 import os
 import pathlib
 
@@ -393,10 +394,13 @@ class Context:
         mc, keep = m.to_c()
         upd = C.c_double(0.0)
         rep = _abi.Report()
-        self._check(self.lib.deftri_arap_optimization(
+        t = time.perf_counter()
+        rc = self.lib.deftri_arap_optimization(
             self.h, C.byref(mc), float(rep_weight), float(global_weight), float(arap_weight), float(alpha),
             float(beta), C.c_float(depth_error), int(n_iterations), C.byref(upd) if want_update else None,
-            C.byref(rep)))
+            C.byref(rep))
+        self.last_call_s = time.perf_counter() - t     # the C-ABI call alone (no Python marshalling)
+        self._check(rc)
         m.from_c(mc, keep)
         return upd.value, rep.as_dict()
 
