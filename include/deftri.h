@@ -253,7 +253,9 @@ typedef struct deftri_plan_info {
     int32_t phase1_blocks, row_blocks;
     double  product_bytes;     /* algorithmic bytes of one matrix-free product on this rank */
     int32_t jacobian_fp32;
-    int32_t reserved;
+    int32_t cg_launches;       /* iterative: kernel launches per CG iteration (3 on one rank: the dots
+                                  and the heavy-vertex finish run in the last workgroup of the update /
+                                  product launches; 5-6 otherwise) */
 } deftri_plan_info;
 int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info);
 /* TEST ONLY (no GPU): host emulation of one product q = (H + lambda I) p with the iterative plan's

@@ -267,3 +267,36 @@ def test_iterative_plan_reuse_matches_fresh_upload():
     finally:
         a.close()
         b.close()
+
+
+def _fusion_worker(no_fuse, q):
+    if no_fuse:
+        os.environ["DEFTRI_SP_NO_FUSE"] = "1"      # read once, at the first upload of this process
+    from deftri import capi as c
+    p = tv_problem(20000, seed=6)
+    with c.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.upload(p)
+        info = ctx.plan_info()
+        r = ctx.solve_lm(5)
+        q.put((info["cg_launches"], r["chi2_iter"], r["trials_iter"], r["pcg_iterations"],
+               [a.tobytes() for a in ctx.download()]))
+
+
+def test_fused_cg_chain_matches_unfused():
+    """One rank: the dots in the update's last workgroup and the heavy finish in the product's last
+    workgroup (3 launches per CG iteration) form the same sums in the same order as the separate
+    k_sp_dots / k_sp_heavy launches (DEFTRI_SP_NO_FUSE=1): bit-identical LM runs."""
+    cm = mp.get_context("spawn")
+    out = {}
+    for no_fuse in (False, True):
+        q = cm.Queue()
+        pr = cm.Process(target=_fusion_worker, args=(no_fuse, q))
+        pr.start()
+        out[no_fuse] = q.get(timeout=300)
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = out[False], out[True]
+    assert l0 == 3 and l1 == 5
+    assert c0 == c1 and t0 == t1 and i0 == i1
+    assert s0 == s1

@@ -1198,6 +1198,7 @@ int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info) {
         info->row_blocks = s.n_row_blocks();
         info->product_bytes = s.product_bytes();
         info->jacobian_fp32 = s.fp32_jac;
+        info->cg_launches = s.cg_launches();
         return 0;
     }
     if (!ctx->have) return DEFTRI_E_NOPROBLEM;

@@ -42,7 +42,8 @@ constexpr int kSpRed = 16;             // doubles per iteration in the reduction
 constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
 constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
-constexpr int kSpHeavySplit = 512;     // heavy sums by one workgroup per heavy vertex above this many blocks
+constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
+constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0)
 enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4 };
@@ -145,6 +146,9 @@ struct SpDev {
     double *hbuf = nullptr;                               // [pq_rows, heavy sums (hd)]
     double *red = nullptr;                                // [max_it + 2][kSpRed]: rz, rr, -, alpha
     double *rec = nullptr;                                // [8]: status, its
+    int *cnt = nullptr;                                   // [4] last-workgroup counters (0 between launches)
+    int32_t fuse = 0;                                     // one rank: dots in the update's / setup's last workgroup
+    int32_t fuse_heavy = 0;                               // ... and k_sp_heavy in k_sp_phase2's last workgroup
     int32_t max_it = 0;
     double tol2 = 0;
 };
@@ -197,6 +201,10 @@ class SpSolver {
     int32_t n_blocks() const { return G.nblk; }
     int32_t n_row_blocks() const { return G.nrb; }
     int32_t n_arap_local() const { return (int32_t)H.arap_ids.size(); }
+    int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
+        const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;
+        return (G.fuse ? 0 : 1) + (G.nblk > 0 ? 1 : 0) + 1 + heavy + 1;
+    }
     // settings
     double tol = 1e-12;
     int max_it = 0;                  // 0: the default budget

@@ -9,8 +9,10 @@
 //                     edges), D_v (its reprojection / depth part), b_v, c_e = W J_p J_s per depth edge
 //   k_sp_glin_blocks  per phase-1 block: the heavy vertices' H / b partials (owned edges only)
 //   k_sp_glin_heavy   heavy H / b from the block partials (rank sums; all-reduced by the host)
-// Per CG iteration it (5 launches on one rank; the sharded solve splits k_sp_heavy and adds two
-// all-reduces and the halo exchange of the boundary rows' (z, p)):
+// Per CG iteration it (sharded: 6 launches, two all-reduces and the halo exchange of the boundary
+// rows' (z, p); one rank: 3 launches — k_sp_dots runs in the last workgroup of the update before it
+// (or of the setup), and k_sp_heavy in the last workgroup of k_sp_phase2 when the heavy vertices
+// have few block partials (G.fuse_heavy)):
 //   k_sp_dots    (r.z, r.r) from the previous update's row-block partials
 //   k_sp_phase1  per local ARAP edge s_e = W_e J_e p, per block J_T^T s (T_g) / depth-scale sums
 //   k_sp_phase2  per own row q_v (p formed from (z, p_prev) on the fly and stored), partial p.q
@@ -357,6 +359,27 @@ __device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4]
     }
 }
 
+// true in the last workgroup of the launch to get here (a counter only decides which workgroup
+// continues; the sums it then forms read the other workgroups' partials in a fixed order, so the
+// result does not depend on the arrival order).  The caller resets the counter in that workgroup.
+__device__ __forceinline__ bool last_block(int *cnt) {
+    __shared__ int last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(cnt, 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (last) __threadfence();
+    return last;
+}
+
+// (r.z, r.r) of iteration it from the row-block partials of the update before it (or the setup), in
+// order: k_sp_dots, or the last workgroup of that update / setup on one rank
+__device__ __forceinline__ void dots_block(const SpDev &G, int it, double (*red)[4]) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += G.upart[2 * i]; a1 += G.upart[2 * i + 1]; }
+    pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
+}
+
 // setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
 // partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
 __global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
@@ -424,15 +447,75 @@ __global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *_
         if (!G.include_heavy) rz = rr = 0.0;
     }
     pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
+    if (G.fuse && last_block(G.cnt + 2)) {
+        __syncthreads();
+        if (G.rec[0] == 0.0) dots_block(G, 0, red);
+        if (threadIdx.x == 0) G.cnt[2] = 0;
+    }
 }
 
 // (r.z, r.r) of iteration it from the previous update's (or the setup's) partials, in order
 __global__ void __launch_bounds__(256) k_sp_dots(int it, const SpDev G) {
     __shared__ double red[2][4];
     if (G.rec[0] != 0.0) return;
-    double a0 = 0.0, a1 = 0.0;
-    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += G.upart[2 * i]; a1 += G.upart[2 * i + 1]; }
-    pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
+    dots_block(G, it, red);
+}
+
+// heavy sums of one heavy vertex h into hbuf[1 + its dofs] (h == Q + S: p.q of the rank's rows into
+// hbuf[0]), one workgroup: thread (g, c) = (tid / 8, tid % 8) adds component c of every 32nd block
+// partial (8 lanes read one 64-byte partial), then the 32 groups are added in order through LDS
+__device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *red4, double *lds) {
+    const int nh = G.Q + G.S;
+    if (h == nh) {
+        double a = 0.0;
+        for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
+        a = block_sum(a, red4);
+        if (threadIdx.x == 0) G.hbuf[0] = a;
+        return;
+    }
+    const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+    const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+    const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
+    double acc = 0.0;
+    if (c < dim) {
+        int64_t k = k0 + g;
+        for (; k + 3 * 32 < k1; k += 4 * 32) {        // four partials in flight, added in order
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = G.part[(int64_t)kSpPart * G.hv_blk[k + 32 * u] + c];
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc += v[u];
+        }
+        for (; k < k1; k += 32) acc += G.part[(int64_t)kSpPart * G.hv_blk[k] + c];
+    }
+    lds[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < dim) {
+        double t = 0.0;
+        for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
+        G.hbuf[1 + o + threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+// heavy q (= sums + lam p), p formed and stored, p.q and alpha of iteration it from hbuf
+__device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam, double beta, double *red4) {
+    double pqh = 0.0;
+    for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
+        const double2 v = G.zp[dd];
+        const double p = __fma_rn(beta, v.y, v.x);
+        const double qh = G.hbuf[1 + dd] + lam * p;
+        G.q[dd] = qh;
+        G.zp[dd] = make_double2(v.x, p);
+        pqh += p * qh;
+    }
+    pqh = block_sum(pqh, red4);
+    if (threadIdx.x == 0) {
+        const double pq = G.hbuf[0] + pqh;
+        const double alpha = G.red[(int64_t)kSpRed * it] / pq;
+        if (!(pq > 0.0) || !isfinite(alpha)) { G.rec[0] = kSpBreakdown; G.rec[1] = it; }
+        G.red[(int64_t)kSpRed * it + 3] = alpha;
+    }
 }
 
 template <class JT>
@@ -560,13 +643,23 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
     }
     const double sm = block_sum(pq, red4);
     if (threadIdx.x == 0) G.rpart[blockIdx.x] = sm;
+    if (G.fuse_heavy && last_block(G.cnt)) {
+        // k_sp_heavy stages 1 + 2 of this iteration, in the last workgroup
+        __shared__ double lds[256];
+        for (int h = 0; h <= G.Q + G.S; h++) heavy_sums_block(G, h, red4, lds);
+        __syncthreads();
+        heavy_finish(G, it, lam, beta, red4);
+        if (threadIdx.x == 0) G.cnt[0] = 0;
+    }
 }
 
 // heavy q, p.q and alpha of iteration it.  stage 0: one workgroup does all (small problems, one
 // rank); 1: the rank's sums into hbuf [p.q of its rows, per heavy dof the sum of its blocks'
 // partials] — one workgroup per heavy vertex (+ one for p.q) when launched with Q + S + 1 workgroups,
-// else one workgroup with a wave per vertex; 2: finish from hbuf (after the host's all-reduce, or
-// stage 1 on one rank); 3: only the state of iteration it into the record (the tail of a chunk)
+// else one workgroup looping over the vertices; 2: finish from hbuf (after the host's all-reduce, or
+// stage 1 on one rank); 3: only the state of iteration it into the record (the tail of a chunk).
+// On one rank with few heavy partials (G.fuse_heavy) the last workgroup of k_sp_phase2 does stages
+// 1 and 2 instead.  Every path forms the same sums (heavy_sums_block, heavy_finish).
 __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double lam, int stage) {
     __shared__ double red4[4];
     double beta;
@@ -578,78 +671,17 @@ __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double 
         }
         return;
     }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nh = G.Q + G.S;
+    __shared__ double lds[256];
     if (stage == 1 && gridDim.x > 1) {
-        const int h = blockIdx.x;
-        if (h == nh) {
-            double a = 0.0;
-            for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
-            a = block_sum(a, red4);
-            if (threadIdx.x == 0) G.hbuf[0] = a;
-            return;
-        }
-        const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
-        const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
-        double acc[6] = {0, 0, 0, 0, 0, 0};
-        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
-            const double *p = G.part + (int64_t)kSpPart * G.hv_blk[k];
-#pragma unroll
-            for (int c = 0; c < 6; c++)
-                if (c < dim) acc[c] += p[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 6; c++) {
-            if (c < dim) {
-                const double v = block_sum(acc[c], red4);
-                if (threadIdx.x == 0) G.hbuf[1 + o + c] = v;
-            }
-        }
+        heavy_sums_block(G, blockIdx.x, red4, lds);
         return;
     }
     if (stage != 2) {
-        double a = 0.0;
-        for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
-        const double pq_rows = block_sum(a, red4);
-        for (int h = w; h < nh; h += 4) {
-            const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
-            const int dim = h < G.Q ? 6 : 1;
-            double acc[6] = {0, 0, 0, 0, 0, 0};
-            for (int64_t k = k0 + lane; k < k1; k += 64) {
-                const double *p = G.part + (int64_t)kSpPart * G.hv_blk[k];
-#pragma unroll
-                for (int c = 0; c < 6; c++)
-                    if (c < dim) acc[c] += p[c];
-            }
-            const int o = heavy_dof(G, h);
-#pragma unroll
-            for (int c = 0; c < 6; c++) {
-                if (c < dim) {
-                    const double v = wave_sum(acc[c]);
-                    if (lane == 0) G.hbuf[1 + o + c] = v;
-                }
-            }
-        }
-        if (threadIdx.x == 0) G.hbuf[0] = pq_rows;
+        for (int h = 0; h <= G.Q + G.S; h++) heavy_sums_block(G, h, red4, lds);
         if (stage == 1) return;
         __syncthreads();
     }
-    double pqh = 0.0;
-    for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
-        const double2 v = G.zp[dd];
-        const double p = __fma_rn(beta, v.y, v.x);
-        const double qh = G.hbuf[1 + dd] + lam * p;
-        G.q[dd] = qh;
-        G.zp[dd] = make_double2(v.x, p);
-        pqh += p * qh;
-    }
-    pqh = block_sum(pqh, red4);
-    if (threadIdx.x == 0) {
-        const double pq = G.hbuf[0] + pqh;
-        const double alpha = G.red[(int64_t)kSpRed * it] / pq;
-        if (!(pq > 0.0) || !isfinite(alpha)) { G.rec[0] = kSpBreakdown; G.rec[1] = it; }
-        G.red[(int64_t)kSpRed * it + 3] = alpha;
-    }
+    heavy_finish(G, it, lam, beta, red4);
 }
 
 __global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
@@ -702,6 +734,12 @@ __global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
         if (!G.include_heavy) rz = rr = 0.0;
     }
     pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
+    if (G.fuse && last_block(G.cnt + 1)) {
+        // k_sp_dots of iteration it + 1, in the last workgroup
+        __syncthreads();
+        dots_block(G, it + 1, red);
+        if (threadIdx.x == 0) G.cnt[1] = 0;
+    }
 }
 
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer

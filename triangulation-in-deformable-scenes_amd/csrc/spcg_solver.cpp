@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -228,6 +229,12 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G.nslots = H.woff.back();
     G.heavy_split = H.max_heavy_blocks > kSpHeavySplit ? 1 : 0;
     {
+        static const bool no_fuse = std::getenv("DEFTRI_SP_NO_FUSE") != nullptr;
+        const int64_t heavy_parts = H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back();
+        G.fuse = (nranks_ == 1 && !no_fuse) ? 1 : 0;
+        G.fuse_heavy = (G.fuse && heavy_parts <= kSpFuseHeavyMax && Q + S <= 64) ? 1 : 0;
+    }
+    {
         int32_t *rm, *pm, *pi;
         int64_t *wo;
         PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx);
@@ -250,6 +257,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
+    ALLOC(G.cnt, 4);
+    SPOK(hipMemset(G.cnt, 0, 4 * sizeof(int)));
     G.red = G.rec + kSpRecDoubles;
     SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
     SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
@@ -351,13 +360,15 @@ void SpSolver::cg_setup(double lambda, const double *rhs) {
 void SpSolver::cg_chain(double lambda, int from, int to) {
     const bool dist = nranks_ > 1;
     for (int it = from; it < to; it++) {
-        sp_launch_dots(G, it, st_);
+        if (!G.fuse) sp_launch_dots(G, it, st_);      // fused: the previous update's (setup's) last workgroup
         if (dist) tr_->allreduce(G.red + (int64_t)kSpRed * it, 2, 0, st_);
         sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
         if (dist) {
             sp_launch_heavy(G, it, lambda, 1, st_);
             tr_->allreduce(G.hbuf, 1 + G.hd, 0, st_);
             sp_launch_heavy(G, it, lambda, 2, st_);
+        } else if (G.fuse_heavy) {
+            // in k_sp_phase2's last workgroup
         } else if (G.heavy_split) {
             sp_launch_heavy(G, it, lambda, 1, st_);
             sp_launch_heavy(G, it, lambda, 2, st_);
@@ -371,7 +382,7 @@ void SpSolver::cg_chain(double lambda, int from, int to) {
 
 // the state of iteration n into the record (converged / budget), no other effect
 int SpSolver::cg_tail(int n) {
-    sp_launch_dots(G, n, st_);
+    if (!G.fuse) sp_launch_dots(G, n, st_);
     if (nranks_ > 1) {
         int rc = tr_->allreduce(G.red + (int64_t)kSpRed * n, 2, 0, st_);
         if (rc) return rc;
