@@ -149,6 +149,7 @@ struct SpDev {
     int *cnt = nullptr;                                   // [4] last-workgroup counters (0 between launches)
     int32_t fuse = 0;                                     // one rank: dots in the update's / setup's last workgroup
     int32_t fuse_heavy = 0;                               // ... and k_sp_heavy in k_sp_phase2's last workgroup
+    int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
     double tol2 = 0;
 };

@@ -347,28 +347,56 @@ __device__ bool inv6(const double *Hl, double lam, double *Mo) {
     return true;
 }
 
-__device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out) {
+__device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out, const SpDev *pub = nullptr) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     a0 = wave_sum(a0);
     a1 = wave_sum(a1);
     if (lane == 0) { red[0][w] = a0; red[1][w] = a1; }
     __syncthreads();
     if (threadIdx.x == 0) {
-        out[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-        out[1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        const double s0 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        const double s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        if (pub) {             // partials for a last-workgroup hand-off (publish)
+            if (pub->fence) { out[0] = s0; out[1] = s1; }
+            else {
+                __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            out[0] = s0;
+            out[1] = s1;
+        }
     }
 }
 
-// true in the last workgroup of the launch to get here (a counter only decides which workgroup
-// continues; the sums it then forms read the other workgroups' partials in a fixed order, so the
-// result does not depend on the arrival order).  The caller resets the counter in that workgroup.
-__device__ __forceinline__ bool last_block(int *cnt) {
+// Last-workgroup hand-off (G.fuse).  A workgroup's partials are published by thread 0 with
+// agent-scope relaxed atomic stores (coherent across the XCDs' L2s, no L2 write-back); after its
+// stores are acknowledged (s_waitcnt) it takes a ticket; the workgroup that draws the last ticket
+// reads every partial with agent-scope atomic loads and forms the sums in a fixed order, so the
+// result does not depend on the arrival order.  G.fence = 1: plain stores and loads around
+// __threadfence() instead (a whole-L2 write-back per workgroup on gfx950; kept for A/B).
+__device__ __forceinline__ void publish(const SpDev &G, double *p, double v) {
+    if (G.fence) *p = v;
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double fetch(const double *p) {     // a partial published in this launch
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// call with every thread after thread 0 published the workgroup's partials; true in the last one
+__device__ __forceinline__ bool last_block(const SpDev &G, int *cnt) {
     __shared__ int last;
-    __threadfence();
+    if (threadIdx.x == 0) {
+        if (G.fence) __threadfence();
+        else {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);         // the published stores acknowledged
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
+        last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+        if (last && G.fence) __threadfence();
+    }
     __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(cnt, 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (last) __threadfence();
     return last;
 }
 
@@ -376,7 +404,7 @@ __device__ __forceinline__ bool last_block(int *cnt) {
 // order: k_sp_dots, or the last workgroup of that update / setup on one rank
 __device__ __forceinline__ void dots_block(const SpDev &G, int it, double (*red)[4]) {
     double a0 = 0.0, a1 = 0.0;
-    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += G.upart[2 * i]; a1 += G.upart[2 * i + 1]; }
+    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += fetch(G.upart + 2 * i); a1 += fetch(G.upart + 2 * i + 1); }
     pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
 }
 
@@ -446,10 +474,11 @@ __global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *_
         }
         if (!G.include_heavy) rz = rr = 0.0;
     }
-    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
-    if (G.fuse && last_block(G.cnt + 2)) {
-        __syncthreads();
-        if (G.rec[0] == 0.0) dots_block(G, 0, red);
+    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x, G.fuse ? &G : nullptr);
+    if (G.fuse && last_block(G, G.cnt + 2)) {
+        // (a bad block recorded by any workgroup stops every later launch through rec[0], which the
+        // next launch sees; the sums formed here are then never read)
+        dots_block(G, 0, red);
         if (threadIdx.x == 0) G.cnt[2] = 0;
     }
 }
@@ -468,7 +497,7 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
     const int nh = G.Q + G.S;
     if (h == nh) {
         double a = 0.0;
-        for (int i = threadIdx.x; i < G.nrb; i += 256) a += G.rpart[i];
+        for (int i = threadIdx.x; i < G.nrb; i += 256) a += fetch(G.rpart + i);
         a = block_sum(a, red4);
         if (threadIdx.x == 0) G.hbuf[0] = a;
         return;
@@ -642,8 +671,11 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
         }
     }
     const double sm = block_sum(pq, red4);
-    if (threadIdx.x == 0) G.rpart[blockIdx.x] = sm;
-    if (G.fuse_heavy && last_block(G.cnt)) {
+    if (threadIdx.x == 0) {
+        if (G.fuse_heavy) publish(G, G.rpart + blockIdx.x, sm);
+        else G.rpart[blockIdx.x] = sm;
+    }
+    if (G.fuse_heavy && last_block(G, G.cnt)) {
         // k_sp_heavy stages 1 + 2 of this iteration, in the last workgroup
         __shared__ double lds[256];
         for (int h = 0; h <= G.Q + G.S; h++) heavy_sums_block(G, h, red4, lds);
@@ -733,10 +765,9 @@ __global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
         }
         if (!G.include_heavy) rz = rr = 0.0;
     }
-    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x);
-    if (G.fuse && last_block(G.cnt + 1)) {
+    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x, G.fuse ? &G : nullptr);
+    if (G.fuse && last_block(G, G.cnt + 1)) {
         // k_sp_dots of iteration it + 1, in the last workgroup
-        __syncthreads();
         dots_block(G, it + 1, red);
         if (threadIdx.x == 0) G.cnt[1] = 0;
     }

@@ -233,6 +233,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         const int64_t heavy_parts = H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back();
         G.fuse = (nranks_ == 1 && !no_fuse) ? 1 : 0;
         G.fuse_heavy = (G.fuse && heavy_parts <= kSpFuseHeavyMax && Q + S <= 64) ? 1 : 0;
+        static const bool fence = std::getenv("DEFTRI_SP_FENCE") != nullptr;
+        G.fence = fence ? 1 : 0;
     }
     {
         int32_t *rm, *pm, *pi;
