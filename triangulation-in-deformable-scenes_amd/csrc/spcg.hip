@@ -614,7 +614,14 @@ template <class JT>
 __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     double beta;
-    if (it_state(G, it, beta)) return;
+    if (const int st = it_state(G, it, beta)) {
+        // with the heavy finish folded in here, k_sp_heavy's record of the first stopped iteration too
+        if (G.fuse_heavy && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
+            G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
+            G.rec[1] = it;
+        }
+        return;
+    }
     const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double pq = 0.0;
     if (w < G.nwaves) {
