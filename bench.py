@@ -366,6 +366,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=25, help="LM iterations timed (Simulation.yaml numberOfIterations: 25)")
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--trace-markers", action="store_true",
+                    help="a tiny torch kernel right before and after the timed region (kernel-trace windows)")
     ap.add_argument("--corr", type=int, default=0, help="correspondences per keyframe (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "ba"], default="c2",
@@ -445,11 +447,17 @@ def main():
 
     if world > 1:
         dist.barrier()
+    marker = torch.ones(1, device=f"cuda:{gpu}") if args.trace_markers else None
+    if marker is not None:
+        marker.mul_(2.0)                  # a kernel trace's window start (tools/trace_gaps.py --window mul)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rep = ctx.solve_lm(args.steps, analytic=analytic)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    if marker is not None:
+        marker.mul_(2.0)                  # ... and end (outside the timed region)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     log(f"[rank {rank}] {rep['iterations']} iterations / {rep['trials_total']} trials in {dt * 1e3:.1f} ms; "
