@@ -5,7 +5,7 @@ trips, launch latency, dependency gaps).
 
 usage: python tools/trace_gaps.py KERNEL_TRACE.csv [--window NAME] [--json OUT]
   --window: the launches strictly between the first and the last kernel whose name contains NAME
-            (bench.py --trace-markers brackets the timed region with a torch `mul` kernel)
+            (bench.py --trace-markers brackets the timed region with a torch MulFunctor kernel)
 """
 import argparse
 import collections

@@ -404,7 +404,15 @@ __device__ __forceinline__ bool last_block(const SpDev &G, int *cnt) {
 // order: k_sp_dots, or the last workgroup of that update / setup on one rank
 __device__ __forceinline__ void dots_block(const SpDev &G, int it, double (*red)[4]) {
     double a0 = 0.0, a1 = 0.0;
-    for (int i = threadIdx.x; i <= G.nrb; i += 256) { a0 += fetch(G.upart + 2 * i); a1 += fetch(G.upart + 2 * i + 1); }
+    int i = threadIdx.x;
+    for (; i + 3 * 256 <= G.nrb; i += 4 * 256) {      // four pairs in flight, added in the strided order
+        double v[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; u++) { v[u][0] = fetch(G.upart + 2 * (i + 256 * u)); v[u][1] = fetch(G.upart + 2 * (i + 256 * u) + 1); }
+#pragma unroll
+        for (int u = 0; u < 4; u++) { a0 += v[u][0]; a1 += v[u][1]; }
+    }
+    for (; i <= G.nrb; i += 256) { a0 += fetch(G.upart + 2 * i); a1 += fetch(G.upart + 2 * i + 1); }
     pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
 }
 
@@ -497,9 +505,17 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
     const int nh = G.Q + G.S;
     if (h == nh) {
         double a = 0.0;
-        for (int i = threadIdx.x; i < G.nrb; i += 256) a += fetch(G.rpart + i);
+        int i = threadIdx.x;
+        for (; i + 3 * 256 < G.nrb; i += 4 * 256) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = fetch(G.rpart + i + 256 * u);
+#pragma unroll
+            for (int u = 0; u < 4; u++) a += v[u];
+        }
+        for (; i < G.nrb; i += 256) a += fetch(G.rpart + i);
         a = block_sum(a, red4);
-        if (threadIdx.x == 0) G.hbuf[0] = a;
+        if (threadIdx.x == 0) publish(G, G.hbuf, a);
         return;
     }
     const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
@@ -508,12 +524,12 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
     double acc = 0.0;
     if (c < dim) {
         int64_t k = k0 + g;
-        for (; k + 3 * 32 < k1; k += 4 * 32) {        // four partials in flight, added in order
-            double v[4];
+        for (; k + 7 * 32 < k1; k += 8 * 32) {        // eight partials in flight, added in order
+            double v[8];
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = G.part[(int64_t)kSpPart * G.hv_blk[k + 32 * u] + c];
+            for (int u = 0; u < 8; u++) v[u] = G.part[(int64_t)kSpPart * G.hv_blk[k + 32 * u] + c];
 #pragma unroll
-            for (int u = 0; u < 4; u++) acc += v[u];
+            for (int u = 0; u < 8; u++) acc += v[u];
         }
         for (; k < k1; k += 32) acc += G.part[(int64_t)kSpPart * G.hv_blk[k] + c];
     }
@@ -522,7 +538,7 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
     if ((int)threadIdx.x < dim) {
         double t = 0.0;
         for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
-        G.hbuf[1 + o + threadIdx.x] = t;
+        publish(G, G.hbuf + 1 + o + threadIdx.x, t);
     }
     __syncthreads();
 }
@@ -533,14 +549,14 @@ __device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam,
     for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
         const double2 v = G.zp[dd];
         const double p = __fma_rn(beta, v.y, v.x);
-        const double qh = G.hbuf[1 + dd] + lam * p;
+        const double qh = fetch(G.hbuf + 1 + dd) + lam * p;
         G.q[dd] = qh;
         G.zp[dd] = make_double2(v.x, p);
         pqh += p * qh;
     }
     pqh = block_sum(pqh, red4);
     if (threadIdx.x == 0) {
-        const double pq = G.hbuf[0] + pqh;
+        const double pq = fetch(G.hbuf) + pqh;
         const double alpha = G.red[(int64_t)kSpRed * it] / pq;
         if (!(pq > 0.0) || !isfinite(alpha)) { G.rec[0] = kSpBreakdown; G.rec[1] = it; }
         G.red[(int64_t)kSpRed * it + 3] = alpha;
@@ -622,6 +638,18 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
         }
         return;
     }
+    if (G.fuse_heavy && (int)blockIdx.x >= max(G.nrb, 1)) {
+        // the heavy vertices' sums (phase-1 partials only), concurrent with the rows
+        __shared__ double lds[256];
+        heavy_sums_block(G, blockIdx.x - max(G.nrb, 1), red4, lds);
+        if (last_block(G, G.cnt)) {
+            heavy_sums_block(G, G.Q + G.S, red4, lds);
+            __syncthreads();
+            heavy_finish(G, it, lam, beta, red4);
+            if (threadIdx.x == 0) G.cnt[0] = 0;
+        }
+        return;
+    }
     const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double pq = 0.0;
     if (w < G.nwaves) {
@@ -683,9 +711,9 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
         else G.rpart[blockIdx.x] = sm;
     }
     if (G.fuse_heavy && last_block(G, G.cnt)) {
-        // k_sp_heavy stages 1 + 2 of this iteration, in the last workgroup
+        // k_sp_heavy's finish of this iteration in the last workgroup (rows' p.q, heavy q, alpha)
         __shared__ double lds[256];
-        for (int h = 0; h <= G.Q + G.S; h++) heavy_sums_block(G, h, red4, lds);
+        heavy_sums_block(G, G.Q + G.S, red4, lds);
         __syncthreads();
         heavy_finish(G, it, lam, beta, red4);
         if (threadIdx.x == 0) G.cnt[0] = 0;
@@ -859,8 +887,10 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         if (fp32) SPL("sp_phase1", sp::k_sp_phase1<float>, G.nblk, it, G, G.Ja32);
         else SPL("sp_phase1", sp::k_sp_phase1<double>, G.nblk, it, G, G.Ja);
     }
-    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, std::max(G.nrb, 1), it, G, lambda, (const float *)G.pj32);
-    else SPL("sp_phase2", sp::k_sp_phase2<double>, std::max(G.nrb, 1), it, G, lambda, (const double *)G.pj);
+    // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) after the row blocks
+    const int grid = std::max(G.nrb, 1) + (G.fuse_heavy ? G.Q + G.S : 0);
+    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, grid, it, G, lambda, (const float *)G.pj32);
+    else SPL("sp_phase2", sp::k_sp_phase2<double>, grid, it, G, lambda, (const double *)G.pj);
 }
 
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {
