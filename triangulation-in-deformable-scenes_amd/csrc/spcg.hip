@@ -424,18 +424,19 @@ __global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *_
     if ((int)blockIdx.x < G.nrb) {
         const int l = blockIdx.x * 256 + threadIdx.x;
         if (l < G.nown) {
-            double M[6];
-            if (!inv3(G.Hv + 6 * (int64_t)l, lam, M)) {
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+            double Hl[6], M[6], r[3], z[3];
+#pragma unroll
+            for (int k = 0; k < 6; k++) Hl[k] = G.Hv[6 * (int64_t)l + k];
+#pragma unroll
+            for (int a = 0; a < 3; a++) r[a] = rhs[o + a];
+            if (!inv3(Hl, lam, M)) {
                 G.rec[0] = kSpBadBlock;
 #pragma unroll
                 for (int k = 0; k < 6; k++) M[k] = 0.0;
             }
 #pragma unroll
             for (int k = 0; k < 6; k++) G.Mv[6 * (int64_t)l + k] = M[k];
-            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double r[3], z[3];
-#pragma unroll
-            for (int a = 0; a < 3; a++) r[a] = rhs[o + a];
             mul3(M, r, z);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
@@ -687,19 +688,20 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
         }
         if (l >= 0) {
             const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double p[3];
+            double2 v[3];
+            double p[3], D[6];
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const double2 v = G.zp[o + c];
-                p[c] = __fma_rn(beta, v.y, v.x);
-                G.zp[o + c] = make_double2(v.x, p[c]);
-            }
-            const double *D = G.Dv + 6 * (int64_t)l;
+            for (int c = 0; c < 3; c++) v[c] = G.zp[o + c];
+#pragma unroll
+            for (int k = 0; k < 6; k++) D[k] = G.Dv[6 * (int64_t)l + k];
+#pragma unroll
+            for (int c = 0; c < 3; c++) p[c] = __fma_rn(beta, v[c].y, v[c].x);
             q[0] += lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
             q[1] += lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
             q[2] += lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
 #pragma unroll
             for (int c = 0; c < 3; c++) {
+                G.zp[o + c] = make_double2(v[c].x, p[c]);
                 G.q[o + c] = q[c];
                 pq += p[c] * q[c];
             }
@@ -759,20 +761,28 @@ __global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
     if ((int)blockIdx.x < G.nrb) {
         const int l = blockIdx.x * 256 + threadIdx.x;
         if (l < G.nown) {
+            // every load first (the stores below could alias them as far as the compiler knows)
             const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double M[6], r[3], z[3], p[3];
+            double M[6], r[3], z[3], p[3], x[3], q[3];
 #pragma unroll
             for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 p[a] = G.zp[o + a].y;
-                G.x[o + a] += alpha * p[a];
-                r[a] = G.r[o + a] - alpha * G.q[o + a];
-                G.r[o + a] = r[a];
+                x[a] = G.x[o + a];
+                r[a] = G.r[o + a];
+                q[a] = G.q[o + a];
+            }
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                x[a] += alpha * p[a];
+                r[a] = r[a] - alpha * q[a];
             }
             mul3(M, r, z);
 #pragma unroll
             for (int a = 0; a < 3; a++) {
+                G.x[o + a] = x[a];
+                G.r[o + a] = r[a];
                 G.zp[o + a] = make_double2(z[a], p[a]);
                 rz += r[a] * z[a];
                 rr += r[a] * r[a];
