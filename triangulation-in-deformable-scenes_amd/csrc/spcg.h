@@ -43,6 +43,7 @@ constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
 constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
+constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0)
@@ -147,6 +148,13 @@ struct SpDev {
     double *red = nullptr;                                // [max_it + 2][kSpRed]: rz, rr, -, alpha
     double *rec = nullptr;                                // [8]: status, its
     int *cnt = nullptr;                                   // [4] last-workgroup counters (0 between launches)
+    // k_sp_glin_heavy chunks: chunk j sums hv_blk[ch_lo[j] .. ch_lo[j + 1]) of heavy ch_h[j]; heavy h
+    // owns chunks hch_off[h] .. hch_off[h + 1] (at least one); chpart [nch][27]; hcnt per heavy
+    int32_t nch = 0;
+    const int32_t *ch_h = nullptr, *hch_off = nullptr;
+    const int64_t *ch_lo = nullptr;
+    double *chpart = nullptr;
+    int *hcnt = nullptr;
     int32_t fuse = 0;                                     // one rank: dots in the update's / setup's last workgroup
     int32_t fuse_heavy = 0;                               // ... and k_sp_heavy in k_sp_phase2's last workgroup
     int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
@@ -159,7 +167,6 @@ void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st);   // rows + bloc
 void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st);   // rank max of the rows' diagonal
 void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);   // out = max(out, heavy diagonal)
 void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st);
-void sp_launch_pack(const SpDev &G, bool fp32, hipStream_t st);     // per LM iteration, after glin
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st);
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);

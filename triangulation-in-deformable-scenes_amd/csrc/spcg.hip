@@ -72,67 +72,131 @@ __device__ __forceinline__ int it_state(const SpDev &G, int it, double &beta) {
 
 __device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q ? 6 * h : 6 * G.Q + (h - G.Q); }
 
+// Last-workgroup hand-off (G.fuse).  A workgroup's partials are published by thread 0 with
+// agent-scope relaxed atomic stores (coherent across the XCDs' L2s, no L2 write-back); after its
+// stores are acknowledged (s_waitcnt) it takes a ticket; the workgroup that draws the last ticket
+// reads every partial with agent-scope atomic loads and forms the sums in a fixed order, so the
+// result does not depend on the arrival order.  G.fence = 1: plain stores and loads around
+// __threadfence() instead (a whole-L2 write-back per workgroup on gfx950; kept for A/B).
+__device__ __forceinline__ void publish(const SpDev &G, double *p, double v) {
+    if (G.fence) *p = v;
+    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double fetch(const double *p) {     // a partial published in this launch
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- per LM iteration -----------------------------------------------------------------------------
 __device__ __forceinline__ int tri3(int a, int b) { return a * (a + 1) / 2 + b; }   // a >= b
 __device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; }
 
-__global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G) {
+// own rows in the phase-2 wave layout (one lane per row, 64 rows per wave): the row's 3x3 diagonal
+// block of H (reprojection and depth folded into D_v, then the ARAP incidences), b_v, the depth
+// couplings c_e = W J_p J_s; and, slot by slot, the packed J slices phase 2 reads (an ARAP slice is
+// gathered once: added into H_v and stored).  Slots of a row: its incidences in the plan's order,
+// then its depth couplings, then padding.
+template <class JT>
+__global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
-    const int l = blockIdx.x * 256 + threadIdx.x;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double mx = 0.0;
-    if (l < G.nown) {
+    if (w < G.nwaves) {
+        const int l = G.rowmap[64 * w + lane];
         double D[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
-        for (int j = G.rep_off[l]; j < G.rep_off[l + 1]; j++) {     // reprojection: 2 x 3, W scalar
-            const double *J = G.Jr + 6 * (int64_t)j;
-            const double w = G.Wr[j];
+        if (l >= 0) {
+            for (int j = G.rep_off[l]; j < G.rep_off[l + 1]; j++) {     // reprojection: 2 x 3, W scalar
+                const double *J = G.Jr + 6 * (int64_t)j;
+                const double wt = G.Wr[j];
 #pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const double er = G.Er[2 * (int64_t)j + r];
+                for (int r = 0; r < 2; r++) {
+                    const double er = G.Er[2 * (int64_t)j + r];
 #pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    const double ja = J[3 * r + a] * w;
+                    for (int a = 0; a < 3; a++) {
+                        const double ja = J[3 * r + a] * wt;
 #pragma unroll
-                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[3 * r + c];
-                    bb[a] -= J[3 * r + a] * (w * er);
+                        for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[3 * r + c];
+                        bb[a] -= J[3 * r + a] * (wt * er);
+                    }
                 }
             }
-        }
-        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
-            const double *J = G.Jd + 4 * (int64_t)j;
-            const double w = G.Wd[j], er = G.Ed[j];
+            for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
+                const double *J = G.Jd + 4 * (int64_t)j;
+                const double wt = G.Wd[j], er = G.Ed[j];
 #pragma unroll
-            for (int a = 0; a < 3; a++) {
-                const double ja = J[a] * w;
+                for (int a = 0; a < 3; a++) {
+                    const double ja = J[a] * wt;
 #pragma unroll
-                for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
-                bb[a] -= J[a] * (w * er);
-                G.cdep[3 * (int64_t)j + a] = ja * J[3];
+                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
+                    bb[a] -= J[a] * (wt * er);
+                    G.cdep[3 * (int64_t)j + a] = ja * J[3];
+                }
+                G.wss[j] = (J[3] * wt) * J[3];
             }
-            G.wss[j] = (J[3] * w) * J[3];
         }
         double H[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) H[k] = D[k];
-        for (int64_t k = G.inc_off[l]; k < G.inc_off[l + 1]; k++) {  // ARAP incidences
-            const int v = G.inc[k];
-            const int64_t le = v >> 2;
-            const double *Jc = G.Ja + 3 * (v & 3) * G.jld + le;       // column-major [18][jld]
-            const double J[3] = {Jc[0], Jc[G.jld], Jc[2 * G.jld]};
-            const double w = G.Wa[le], er = G.Ea[le];
+        const int64_t n = G.nslots * 64;
+        const int64_t k1 = G.woff[w + 1] * 64 + lane;
+        // one slot: its J slice (ARAP incidence le << 2 | role, or the depth coupling of the row's
+        // edge -2 - m), weight and error; added into H_v / b_v in slot order, stored packed
+        auto slot = [&](int m, double *v, double &wt, double &er) {
+            v[0] = v[1] = v[2] = 0.0;
+            wt = er = 0.0;
+            if (m >= 0) {
+                const int64_t le = m >> 2;
+                const double *Jc = G.Ja + 3 * (m & 3) * G.jld + le;   // column-major [18][jld]
+                v[0] = Jc[0]; v[1] = Jc[G.jld]; v[2] = Jc[2 * G.jld];
+                wt = G.Wa[le];
+                er = G.Ea[le];
+            } else if (m <= -2) {
+                const double *J = G.Jd + 4 * (int64_t)(-2 - m);
+                const double wd = G.Wd[-2 - m];
+#pragma unroll
+                for (int a = 0; a < 3; a++) v[a] = (J[a] * wd) * J[3];
+            }
+        };
+        auto add = [&](int m, const double *v, double wt, double er) {
+            if (m < 0) return;
 #pragma unroll
             for (int a = 0; a < 3; a++) {
-                const double ja = J[a] * w;
+                const double ja = v[a] * wt;
 #pragma unroll
-                for (int c = 0; c <= a; c++) H[tri3(a, c)] += ja * J[c];
-                bb[a] -= J[a] * (w * er);
+                for (int c = 0; c <= a; c++) H[tri3(a, c)] += ja * v[c];
+                bb[a] -= v[a] * (wt * er);
+            }
+        };
+        int64_t k = G.woff[w] * 64 + lane;
+        for (; k + 3 * 64 < k1; k += 4 * 64) {            // four slots: indices, gathers, then in order
+            int m[4];
+            double v[4][3], wt[4], er[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) m[u] = G.pmap[k + 64 * u];
+#pragma unroll
+            for (int u = 0; u < 4; u++) slot(m[u], v[u], wt[u], er[u]);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                add(m[u], v[u], wt[u], er[u]);
+#pragma unroll
+                for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[u][a];
             }
         }
+        for (; k < k1; k += 64) {
+            const int m = G.pmap[k];
+            double v[3], wt, er;
+            slot(m, v, wt, er);
+            add(m, v, wt, er);
 #pragma unroll
-        for (int k = 0; k < 6; k++) { G.Hv[6 * (int64_t)l + k] = H[k]; G.Dv[6 * (int64_t)l + k] = D[k]; }
-        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+            for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
+        }
+        if (l >= 0) {
 #pragma unroll
-        for (int a = 0; a < 3; a++) G.b[o + a] = bb[a];
-        mx = fmax(fabs(H[0]), fmax(fabs(H[2]), fabs(H[5])));
+            for (int k = 0; k < 6; k++) { G.Hv[6 * (int64_t)l + k] = H[k]; G.Dv[6 * (int64_t)l + k] = D[k]; }
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+#pragma unroll
+            for (int a = 0; a < 3; a++) G.b[o + a] = bb[a];
+            mx = fmax(fabs(H[0]), fmax(fabs(H[2]), fabs(H[5])));
+        }
     }
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
@@ -195,63 +259,70 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
     }
 }
 
-// heavy H / b (rank sums): one workgroup per heavy vertex, its blocks' partials strided over the
-// threads in block order, then the fixed workgroup tree per value
+// heavy H / b (rank sums) in two levels: one workgroup per chunk of a heavy vertex's block partials
+// (kSpHeavyChunk of them; thread (g, c) = (tid / 32, tid % 32) adds value c of every 8th partial,
+// the 8 groups added in order), then the vertex's last chunk to finish adds its chunks' sums in order
+// (same hand-off as the CG chain's last workgroups: coherent stores, a ticket per vertex)
 __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
-    __shared__ double red4[4];
-    const int h = blockIdx.x;
-    const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
-    if (h < G.Q) {
-        double a[kSpLin];
+    __shared__ double lds[8][32];
+    __shared__ int last;
+    const int ch = blockIdx.x, h = G.ch_h[ch];
+    const int dim = h < G.Q ? kSpLin : 2;
+    const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
+    double acc = 0.0;
+    if (c < dim) {
+        int64_t k = G.ch_lo[ch] + g;
+        const int64_t k1 = G.ch_lo[ch + 1];
+        for (; k + 7 * 8 < k1; k += 64) {
+            double v[8];
 #pragma unroll
-        for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
-        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
-            const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
+            for (int u = 0; u < 8; u++) v[u] = G.lpart[(int64_t)kSpLin * G.hv_blk[k + 8 * u] + c];
 #pragma unroll
-            for (int q = 0; q < kSpLin; q++) a[q] += p[q];
+            for (int u = 0; u < 8; u++) acc += v[u];
         }
+        for (; k < k1; k += 8) acc += G.lpart[(int64_t)kSpLin * G.hv_blk[k] + c];
+    }
+    lds[g][c] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < dim) {
+        double t = 0.0;
 #pragma unroll
-        for (int q = 0; q < kSpLin; q++) {
-            const double v = block_sum(a[q], red4);
-            if (threadIdx.x == 0) {
-                if (q < 21) G.hl[21 * (int64_t)h + q] = v;
-                else G.b[6 * (int64_t)h + q - 21] = v;
-            }
+        for (int gg = 0; gg < 8; gg++) t += lds[gg][threadIdx.x];
+        publish(G, G.chpart + (int64_t)kSpLin * ch + threadIdx.x, t);
+    }
+    const int c0 = G.hch_off[h], c1 = G.hch_off[h + 1];
+    if (threadIdx.x == 0) {
+        if (G.fence) __threadfence();
+        else {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
         }
-    } else {
-        double a0 = 0.0, a1 = 0.0;
-        for (int64_t k = k0 + threadIdx.x; k < k1; k += 256) {
-            const double *p = G.lpart + (int64_t)kSpLin * G.hv_blk[k];
-            a0 += p[0];
-            a1 += p[1];
-        }
-        a0 = block_sum(a0, red4);
-        a1 = block_sum(a1, red4);
-        if (threadIdx.x == 0) {
-            G.hl[21 * (int64_t)G.Q + (h - G.Q)] = a0;
-            G.b[6 * (int64_t)G.Q + (h - G.Q)] = a1;
+        last = __hip_atomic_fetch_add(G.hcnt + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c1 - c0 - 1;
+        if (last && G.fence) __threadfence();
+    }
+    __syncthreads();
+    if (!last) return;
+    acc = 0.0;
+    if (c < dim)
+        for (int j = c0 + g; j < c1; j += 8) acc += fetch(G.chpart + (int64_t)kSpLin * j + c);
+    __syncthreads();
+    lds[g][c] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < dim) {
+        double t = 0.0;
+#pragma unroll
+        for (int gg = 0; gg < 8; gg++) t += lds[gg][threadIdx.x];
+        const int q = threadIdx.x;
+        if (h < G.Q) {
+            if (q < 21) G.hl[21 * (int64_t)h + q] = t;
+            else G.b[6 * (int64_t)h + q - 21] = t;
+        } else {
+            if (q == 0) G.hl[21 * (int64_t)G.Q + (h - G.Q)] = t;
+            else G.b[6 * (int64_t)G.Q + (h - G.Q)] = t;
         }
     }
-}
-
-// the phase-2 wave layout's J slices, once per LM iteration (after k_sp_glin_rows: the depth
-// couplings c_e): slot t <- ARAP J_{le, role} (column-major J) or c_e, zero for padding
-template <class JT>
-__global__ void __launch_bounds__(256) k_sp_pack_slots(const SpDev G, JT *__restrict__ pj) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t n = G.nslots * 64;
-    if (t >= n) return;
-    const int m = G.pmap[t];
-    double v[3] = {0.0, 0.0, 0.0};
-    if (m >= 0) {
-        const double *Jc = G.Ja + 3 * (m & 3) * G.jld + (m >> 2);
-        v[0] = Jc[0]; v[1] = Jc[G.jld]; v[2] = Jc[2 * G.jld];
-    } else if (m <= -2) {
-        const double *c = G.cdep + 3 * (int64_t)(-2 - m);
-        v[0] = c[0]; v[1] = c[1]; v[2] = c[2];
-    }
-#pragma unroll
-    for (int a = 0; a < 3; a++) pj[a * n + t] = (JT)v[a];
+    if (threadIdx.x == 0) G.hcnt[h] = 0;
 }
 
 // rank max of the rows' diagonal (stage 0), or that (all-reduced) combined with the heavy diagonal
@@ -367,20 +438,6 @@ __device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4]
             out[1] = s1;
         }
     }
-}
-
-// Last-workgroup hand-off (G.fuse).  A workgroup's partials are published by thread 0 with
-// agent-scope relaxed atomic stores (coherent across the XCDs' L2s, no L2 write-back); after its
-// stores are acknowledged (s_waitcnt) it takes a ticket; the workgroup that draws the last ticket
-// reads every partial with agent-scope atomic loads and forms the sums in a fixed order, so the
-// result does not depend on the arrival order.  G.fence = 1: plain stores and loads around
-// __threadfence() instead (a whole-L2 write-back per workgroup on gfx950; kept for A/B).
-__device__ __forceinline__ void publish(const SpDev &G, double *p, double v) {
-    if (G.fence) *p = v;
-    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double fetch(const double *p) {     // a partial published in this launch
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // call with every thread after thread 0 published the workgroup's partials; true in the last one
@@ -860,16 +917,10 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
     } while (0)
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    SPL("sp_glin_rows", sp::k_sp_glin_rows, std::max(G.nrb, 1), G);
+    if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, std::max(G.nrb, 1), G, G.pj32);
+    else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, std::max(G.nrb, 1), G, G.pj);
     if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
-    if (G.Q + G.S > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.Q + G.S, G);
-    sp_launch_pack(G, fp32, st);
-}
-
-void sp_launch_pack(const SpDev &G, bool fp32, hipStream_t st) {
-    if (G.nslots <= 0) return;
-    if (fp32) SPL("sp_pack_slots", sp::k_sp_pack_slots<float>, nblk(G.nslots * 64, 256), G, G.pj32);
-    else SPL("sp_pack_slots", sp::k_sp_pack_slots<double>, nblk(G.nslots * 64, 256), G, G.pj);
+    if (G.nch > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.nch, G);
 }
 
 void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st) {

@@ -261,6 +261,30 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
     ALLOC(G.cnt, 4);
     SPOK(hipMemset(G.cnt, 0, 4 * sizeof(int)));
+    {
+        // heavy linearization chunks (k_sp_glin_heavy): kSpHeavyChunk block partials each, >= 1 per vertex
+        std::vector<int32_t> chh, hcho(Q + S + 1, 0);
+        std::vector<int64_t> chlo;
+        for (int32_t h = 0; h < Q + S; h++) {
+            const int64_t k0 = H.hv_blk_off[h], k1 = H.hv_blk_off[h + 1];
+            int64_t k = k0;
+            do {
+                chh.push_back(h);
+                chlo.push_back(k);
+                k = std::min<int64_t>(k + kSpHeavyChunk, k1);
+            } while (k < k1);
+            hcho[h + 1] = (int32_t)chh.size();
+        }
+        chlo.push_back(H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back());
+        G.nch = (int32_t)chh.size();
+        int32_t *d_chh, *d_hcho;
+        int64_t *d_chlo;
+        PUT(d_chh, chh); PUT(d_hcho, hcho); PUT(d_chlo, chlo);
+        G.ch_h = d_chh; G.hch_off = d_hcho; G.ch_lo = d_chlo;
+        ALLOC(G.chpart, (int64_t)kSpLin * std::max(G.nch, 1));
+        ALLOC(G.hcnt, std::max(Q + S, 1));
+        SPOK(hipMemset(G.hcnt, 0, sizeof(int) * (size_t)std::max(Q + S, 1)));
+    }
     G.red = G.rec + kSpRecDoubles;
     SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
     SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
