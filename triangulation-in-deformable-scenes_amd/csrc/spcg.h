@@ -43,6 +43,7 @@ constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
 constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
+constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one thread per dof)
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 enum { SP_ARAP = 0, SP_DEP = 1 };

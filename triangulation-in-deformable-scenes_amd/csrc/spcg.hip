@@ -475,37 +475,54 @@ __device__ __forceinline__ void dots_block(const SpDev &G, int it, double (*red)
 
 // setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
 // partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
-__global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
-    __shared__ double red[2][4];
+__global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
+    // the row blocks as in k_sp_update: one thread per dof for the vectors, one per row for the
+    // block inverse (through LDS)
+    __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
+    __shared__ double red[2][3 * kSpUpdRows / 64], dred[2][4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    constexpr int nw = 3 * kSpUpdRows / 64;
     double rz = 0.0, rr = 0.0;
     if ((int)blockIdx.x < G.nrb) {
-        const int l = blockIdx.x * 256 + threadIdx.x;
-        if (l < G.nown) {
-            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double Hl[6], M[6], r[3], z[3];
+        const int l0 = blockIdx.x * kSpUpdRows;
+        const int nrow = min(kSpUpdRows, G.nown - l0);
+        const int64_t o0 = G.hd + 3 * (int64_t)(G.row0 + l0);
+        const double *Hg = G.Hv + 6 * (int64_t)l0;
+        if (t < 6 * nrow) sM[t] = Hg[t];
+        if (t + 3 * kSpUpdRows < 6 * nrow) sM[t + 3 * kSpUpdRows] = Hg[t + 3 * kSpUpdRows];
+        const double r = t < 3 * nrow ? rhs[o0 + t] : 0.0;
+        sR[t] = r;
+        __syncthreads();
+        if (t < nrow) {
+            double Hl[6], M[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) Hl[k] = G.Hv[6 * (int64_t)l + k];
-#pragma unroll
-            for (int a = 0; a < 3; a++) r[a] = rhs[o + a];
+            for (int k = 0; k < 6; k++) Hl[k] = sM[6 * t + k];
             if (!inv3(Hl, lam, M)) {
                 G.rec[0] = kSpBadBlock;
 #pragma unroll
                 for (int k = 0; k < 6; k++) M[k] = 0.0;
             }
 #pragma unroll
-            for (int k = 0; k < 6; k++) G.Mv[6 * (int64_t)l + k] = M[k];
-            mul3(M, r, z);
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                G.r[o + a] = r[a];
-                G.zp[o + a] = make_double2(z[a], 0.0);
-                G.x[o + a] = 0.0;
-                rz += r[a] * z[a];
-                rr += r[a] * r[a];
-            }
+            for (int k = 0; k < 6; k++) sM[6 * t + k] = M[k];
         }
-    } else {
-        for (int h = threadIdx.x; h < G.Q + G.S; h += 256) {
+        __syncthreads();
+        double *Mg = G.Mv + 6 * (int64_t)l0;
+        if (t < 6 * nrow) Mg[t] = sM[t];
+        if (t + 3 * kSpUpdRows < 6 * nrow) Mg[t + 3 * kSpUpdRows] = sM[t + 3 * kSpUpdRows];
+        if (t < 3 * nrow) {
+            const int row = t / 3, a = t - 3 * row;
+            const double *M = sM + 6 * row;
+            const int i0 = a == 0 ? 0 : a == 1 ? 1 : 3, i1 = a == 0 ? 1 : a == 1 ? 2 : 4, i2 = a == 0 ? 3 : a == 1 ? 4 : 5;
+            const double *rv = sR + 3 * row;
+            const double z = M[i0] * rv[0] + M[i1] * rv[1] + M[i2] * rv[2];
+            G.r[o0 + t] = r;
+            G.zp[o0 + t] = make_double2(z, 0.0);
+            G.x[o0 + t] = 0.0;
+            rz = r * z;
+            rr = r * r;
+        }
+    } else if (t < 256) {
+        for (int h = t; h < G.Q + G.S; h += 256) {
             const int o = heavy_dof(G, h);
             if (h < G.Q) {
                 double *M = G.Mh + 36 * (int64_t)h;
@@ -540,12 +557,29 @@ __global__ void __launch_bounds__(256) k_sp_setup(const SpDev G, const double *_
         }
         if (!G.include_heavy) rz = rr = 0.0;
     }
-    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x, G.fuse ? &G : nullptr);
+    rz = wave_sum(rz);
+    rr = wave_sum(rr);
+    if (lane == 0) { red[0][wv] = rz; red[1][wv] = rr; }
+    __syncthreads();
+    if (t == 0) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
+        double *out = G.upart + 2 * blockIdx.x;
+        if (G.fuse && !G.fence) {
+            __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            out[0] = s0;
+            out[1] = s1;
+        }
+    }
     if (G.fuse && last_block(G, G.cnt + 2)) {
         // (a bad block recorded by any workgroup stops every later launch through rec[0], which the
         // next launch sees; the sums formed here are then never read)
-        dots_block(G, 0, red);
-        if (threadIdx.x == 0) G.cnt[2] = 0;
+        __syncthreads();
+        if (t < 256) dots_block(G, 0, dred);
+        if (t == 0) G.cnt[2] = 0;
     }
 }
 
@@ -810,43 +844,52 @@ __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double 
     heavy_finish(G, it, lam, beta, red4);
 }
 
-__global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
-    __shared__ double red[2][4];
+// x += alpha p, r -= alpha q, z = M r and the partial (r.z, r.r) of the rank's rows: one thread per
+// dof, kSpUpdRows rows (3 kSpUpdRows threads) per workgroup so every vector access is coalesced; the
+// rows' preconditioner blocks and the new r pass through LDS.  The workgroup after the row blocks
+// does the heavy dofs.  One rank: the last workgroup forms k_sp_dots of iteration it + 1.
+__global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDev G) {
+    static_assert(kSpUpdRows == kSpBlock, "update workgroups are the row blocks of the (r.z, r.r) partials");
+    __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
+    __shared__ double red[2][3 * kSpUpdRows / 64], dred[2][4];
     if (G.rec[0] != 0.0) return;
     const double alpha = G.red[(int64_t)kSpRed * it + 3];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    constexpr int nw = 3 * kSpUpdRows / 64;
     double rz = 0.0, rr = 0.0;
     if ((int)blockIdx.x < G.nrb) {
-        const int l = blockIdx.x * 256 + threadIdx.x;
-        if (l < G.nown) {
-            // every load first (the stores below could alias them as far as the compiler knows)
-            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double M[6], r[3], z[3], p[3], x[3], q[3];
-#pragma unroll
-            for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                p[a] = G.zp[o + a].y;
-                x[a] = G.x[o + a];
-                r[a] = G.r[o + a];
-                q[a] = G.q[o + a];
-            }
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                x[a] += alpha * p[a];
-                r[a] = r[a] - alpha * q[a];
-            }
-            mul3(M, r, z);
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                G.x[o + a] = x[a];
-                G.r[o + a] = r[a];
-                G.zp[o + a] = make_double2(z[a], p[a]);
-                rz += r[a] * z[a];
-                rr += r[a] * r[a];
-            }
+        const int l0 = blockIdx.x * kSpUpdRows;
+        const int nrow = min(kSpUpdRows, G.nown - l0);
+        const int64_t o0 = G.hd + 3 * (int64_t)(G.row0 + l0);
+        const bool on = t < 3 * nrow;
+        double p = 0.0, x = 0.0, r = 0.0, q = 0.0;
+        if (on) {
+            p = G.zp[o0 + t].y;
+            x = G.x[o0 + t];
+            r = G.r[o0 + t];
+            q = G.q[o0 + t];
         }
-    } else {
-        for (int h = threadIdx.x; h < G.Q + G.S; h += 256) {
+        const double *Mg = G.Mv + 6 * (int64_t)l0;
+        if (t < 6 * nrow) sM[t] = Mg[t];
+        if (t + 3 * kSpUpdRows < 6 * nrow) sM[t + 3 * kSpUpdRows] = Mg[t + 3 * kSpUpdRows];
+        x += alpha * p;
+        r = r - alpha * q;
+        sR[t] = r;
+        __syncthreads();
+        if (on) {
+            const int row = t / 3, a = t - 3 * row;
+            const double *M = sM + 6 * row, *rv = sR + 3 * row;
+            // mul3's row a of the packed symmetric block (00 10 11 20 21 22)
+            const int i0 = a == 0 ? 0 : a == 1 ? 1 : 3, i1 = a == 0 ? 1 : a == 1 ? 2 : 4, i2 = a == 0 ? 3 : a == 1 ? 4 : 5;
+            const double z = M[i0] * rv[0] + M[i1] * rv[1] + M[i2] * rv[2];
+            G.x[o0 + t] = x;
+            G.r[o0 + t] = r;
+            G.zp[o0 + t] = make_double2(z, p);
+            rz = r * z;
+            rr = r * r;
+        }
+    } else if (t < 256) {
+        for (int h = t; h < G.Q + G.S; h += 256) {
             const int o = heavy_dof(G, h);
             const int dim = h < G.Q ? 6 : 1;
             double r[6], p[6];
@@ -867,11 +910,29 @@ __global__ void __launch_bounds__(256) k_sp_update(int it, const SpDev G) {
         }
         if (!G.include_heavy) rz = rr = 0.0;
     }
-    pair_tree(rz, rr, red, G.upart + 2 * blockIdx.x, G.fuse ? &G : nullptr);
+    // fixed-order workgroup sums: wave butterflies, then the waves in order
+    rz = wave_sum(rz);
+    rr = wave_sum(rr);
+    if (lane == 0) { red[0][wv] = rz; red[1][wv] = rr; }
+    __syncthreads();
+    if (t == 0) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
+        double *out = G.upart + 2 * blockIdx.x;
+        if (G.fuse && !G.fence) {
+            __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            out[0] = s0;
+            out[1] = s1;
+        }
+    }
     if (G.fuse && last_block(G, G.cnt + 1)) {
-        // k_sp_dots of iteration it + 1, in the last workgroup
-        dots_block(G, it + 1, red);
-        if (threadIdx.x == 0) G.cnt[1] = 0;
+        // k_sp_dots of iteration it + 1, in the last workgroup (its first 256 threads)
+        __syncthreads();
+        if (t < 256) dots_block(G, it + 1, dred);
+        if (t == 0) G.cnt[1] = 0;
     }
 }
 
@@ -936,7 +997,10 @@ void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st) {
 }
 
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st) {
-    SPL("sp_setup", sp::k_sp_setup, G.nrb + 1, G, rhs, lambda);
+    const int grid = (G.nown + kSpUpdRows - 1) / kSpUpdRows + 1;
+    hipEvent_t e0_ = prof_begin(st);
+    hipLaunchKernelGGL(sp::k_sp_setup, dim3(grid), dim3(3 * kSpUpdRows), 0, st, G, rhs, lambda);
+    prof_end("sp_setup", e0_, (unsigned)grid, 0.0, st);
 }
 
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st) {
@@ -961,7 +1025,10 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
 }
 
 void sp_launch_update(const SpDev &G, int it, hipStream_t st) {
-    SPL("sp_update", sp::k_sp_update, G.nrb + 1, it, G);
+    const int grid = (G.nown + kSpUpdRows - 1) / kSpUpdRows + 1;
+    hipEvent_t e0_ = prof_begin(st);
+    hipLaunchKernelGGL(sp::k_sp_update, dim3(grid), dim3(3 * kSpUpdRows), 0, st, it, G);
+    prof_end("sp_update", e0_, (unsigned)grid, 0.0, st);
 }
 
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
