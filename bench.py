@@ -223,7 +223,7 @@ def main_ba(args, world, rank, gpu, backend):
     if rank == 0:
         out = {
             "metric": "BA LM iterations/sec (BlockSolver_6_3 Schur, point-sharded)",
-            "value": iters / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
+            "value": value, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / max(iters, 1), "higher_is_better": True,
             "scaling": args.ba_scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"BA-{full.n_points // 1000}k-x{full.n_poses}", "points": full.n_points,
@@ -249,6 +249,13 @@ def reduce_stats(dt, iters, trials, world, device):
     s = torch.tensor([iters, trials], dtype=torch.float64, device=device)
     dist.all_reduce(s, op=dist.ReduceOp.SUM)
     return float(v.item()), int(s[0].item()), int(s[1].item())
+
+
+def job_rate(t_max, iters):
+    """value and ms/step of the ARAP bench line: the LM iterations of ONE problem over the slowest
+    rank's wall time — sharded, every rank ran the same iterations of the one problem; replicas, each
+    rank its own copy, so the rate is per problem (never a sum over ranks)."""
+    return iters / t_max, 1e3 * t_max / max(iters, 1)
 
 
 # BASELINE workloads of the ARAP LM (SURVEY §8d): scene recipe, weights (rep, arap, depth sigma) and
@@ -469,6 +476,7 @@ def main():
     # one problem (sharded): every rank ran the same iterations, the job takes the slowest rank;
     # replicas: the slowest rank's time for its own problem (value = per-problem rate, never a sum)
     t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
+    value, ms_per_step = job_rate(t_max, iters)
 
     # profiled trial (HIP events on the solver stream) at the final lambda of the timed run (a
     # collective on a sharded context: each rank times its own part of the same trial)
@@ -516,12 +524,11 @@ def main():
         log(f"end-to-end arapOptimization: {e2e}")
 
     if rank == 0:
-        ms_per_step = 1e3 * t_max / max(iters, 1)
         workload = ("C2" if n == 100000 else f"two-view-{n}") if wl == "c2" else \
             (wl.upper() if n == spec["n"] else f"{wl.upper()}-slice-{n}x{spec['k']}")
         out = {
             "metric": BASELINE_METRIC if wl == "c2" else f"LM iterations/sec + ms/iter, {wl.upper()}: {spec['desc']}",
-            "value": iters / t_max, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
+            "value": value, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak" if (world > 1 and not sharded) else "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",

@@ -12,8 +12,11 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
     t, it, tr = bench.reduce_stats(0.5 + rank, 5, 12 + rank, world, "cpu")
+    # the sharded ARAP line: both ranks ran the same 5 iterations of one problem
+    t1, _, _ = bench.reduce_stats(0.020 + 0.005 * rank, 5, 9, world, "cpu")
+    value, ms = bench.job_rate(t1, 5)
     dist.barrier()
-    q.put((rank, t, it, tr))
+    q.put((rank, t, it, tr, value, ms))
     dist.destroy_process_group()
 
 
@@ -28,8 +31,10 @@ def test_reduce_stats_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, t, it, tr in out:
+    for rank, t, it, tr, value, ms in out:
         assert t == pytest.approx(1.5) and it == 10 and tr == 25
+        # value = iterations of the one problem over the slowest rank's time (not a sum over ranks)
+        assert value == pytest.approx(5 / 0.025) and ms == pytest.approx(5.0)
 
 
 def test_reduce_stats_single():
