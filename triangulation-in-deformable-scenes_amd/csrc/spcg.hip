@@ -176,22 +176,31 @@ __global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G, JT *__restr
         const int64_t n = G.nslots * 64;
         const int64_t k1 = G.woff[w + 1] * 64 + lane;
         // one slot: its J slice (ARAP incidence le << 2 | role, or the depth coupling of the row's
-        // edge -2 - m), weight and error; added into H_v / b_v in slot order, stored packed
-        auto slot = [&](int m, double *v, double &wt, double &er) {
-            v[0] = v[1] = v[2] = 0.0;
-            wt = er = 0.0;
-            if (m >= 0) {
-                const int64_t le = m >> 2;
-                const double *Jc = G.Ja + 3 * (m & 3) * G.jld + le;   // column-major [18][jld]
-                v[0] = Jc[0]; v[1] = Jc[G.jld]; v[2] = Jc[2 * G.jld];
-                wt = G.Wa[le];
-                er = G.Ea[le];
-            } else if (m <= -2) {
-                const double *J = G.Jd + 4 * (int64_t)(-2 - m);
-                const double wd = G.Wd[-2 - m];
-#pragma unroll
-                for (int a = 0; a < 3; a++) v[a] = (J[a] * wd) * J[3];
-            }
+        // edge -2 - m), weight and error (ARAP) / J_s (depth).  load(): the same five loads on every
+        // path (selected addresses; padding reads ARAP edge 0); value(): selects only — so the four
+        // slots of a step issue all their loads before the first is used
+        struct Raw { double j0, j1, j2, w, x; };
+        const double *__restrict__ Ja = G.Ja, *__restrict__ Wa = G.Wa, *__restrict__ Ea = G.Ea;
+        const double *__restrict__ Jd = G.Jd, *__restrict__ Wd = G.Wd;
+        const int64_t jld = G.jld;
+        auto load = [&](int m) -> Raw {
+            const bool dep = m <= -2;
+            const int mm = max(m, 0), jj = max(-2 - m, 0);
+            const double *pa = Ja + (int64_t)(3 * (mm & 3)) * jld + (mm >> 2);   // ARAP (padding: edge 0)
+            const double *pd = Jd + 4 * (int64_t)jj;
+            const double *Jc = dep ? pd : pa;
+            const int64_t st = dep ? 1 : jld;
+            const double *W = dep ? Wd + jj : Wa + (mm >> 2);
+            const double *X = dep ? pd + 3 : Ea + (mm >> 2);
+            return Raw{Jc[0], Jc[st], Jc[2 * st], *W, *X};
+        };
+        auto value = [&](int m, const Raw &r, double *v, double &wt, double &er) {
+            const bool arap = m >= 0, dep = m <= -2;
+            v[0] = dep ? (r.j0 * r.w) * r.x : arap ? r.j0 : 0.0;
+            v[1] = dep ? (r.j1 * r.w) * r.x : arap ? r.j1 : 0.0;
+            v[2] = dep ? (r.j2 * r.w) * r.x : arap ? r.j2 : 0.0;
+            wt = arap ? r.w : 0.0;
+            er = arap ? r.x : 0.0;
         };
         auto add = [&](int m, const double *v, double wt, double er) {
             if (m < 0) return;
@@ -204,24 +213,26 @@ __global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G, JT *__restr
             }
         };
         int64_t k = G.woff[w] * 64 + lane;
-        for (; k + 3 * 64 < k1; k += 4 * 64) {            // four slots: indices, gathers, then in order
+        for (; k + 3 * 64 < k1; k += 4 * 64) {            // four slots: indices, loads, then in order
             int m[4];
-            double v[4][3], wt[4], er[4];
+            Raw r[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) m[u] = G.pmap[k + 64 * u];
 #pragma unroll
-            for (int u = 0; u < 4; u++) slot(m[u], v[u], wt[u], er[u]);
+            for (int u = 0; u < 4; u++) r[u] = load(m[u]);
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                add(m[u], v[u], wt[u], er[u]);
+                double v[3], wt, er;
+                value(m[u], r[u], v, wt, er);
+                add(m[u], v, wt, er);
 #pragma unroll
-                for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[u][a];
+                for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
             }
         }
         for (; k < k1; k += 64) {
             const int m = G.pmap[k];
             double v[3], wt, er;
-            slot(m, v, wt, er);
+            value(m, load(m), v, wt, er);
             add(m, v, wt, er);
 #pragma unroll
             for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
