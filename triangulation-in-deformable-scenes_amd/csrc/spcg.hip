@@ -800,8 +800,16 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
         double q[3] = {0.0, 0.0, 0.0};
         int64_t k = G.woff[w] * 64 + lane;
         const int64_t k1 = G.woff[w + 1] * 64 + lane;
+        // s_e (v >= 0), p of the depth scale -2 - v (v <= -2) or 0 (padding): both loads on every
+        // path and a select, so the slots of a step keep their loads in flight (the scales' (z, p)
+        // are a handful of cache lines)
+        const double *__restrict__ sv_ = G.s;
+        const double2 *__restrict__ zp_ = G.zp;
         auto val = [&](int v) -> double {
-            return v >= 0 ? G.s[v] : (v <= -2 ? pval(G.zp, beta, os + (-2 - v)) : 0.0);
+            const double a = sv_[max(v, 0)];
+            const double2 z = zp_[os + max(-2 - v, 0)];
+            const double p = __fma_rn(beta, z.y, z.x);
+            return v >= 0 ? a : (v <= -2 ? p : 0.0);
         };
         // four slots per step: their indices, then the values and J slices, then the adds in order
         for (; k + 3 * 64 < k1; k += 4 * 64) {
