@@ -127,25 +127,21 @@ __global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t 
     E[e] = err;
 }
 
-// The ARAP energy (g2oTypes.h:300-349) in components, one rounding per operation like the oracle
-// (contraction off), so a component computed on its own equals the same component of a full
-// evaluation bit for bit:
+// The ARAP energy (g2oTypes.h:300-349) in components; a component computed on its own is the same
+// expression as in a full evaluation (the same contractions), so it equals that component:
 //   dg_k = ((R_g v2i - t)_k - v1i_k) + ((R_g v2j - t)_k - v1j_k)
 //   f_k  = (d2i_k - (R_i d1i)_k) / area,   g_k = (d2j_k - (R_j d1j)_k) / area
 //   e    = (w (fn + gn) + dg.dg) - 0,  fn = ((0 + f0^2) + f1^2) + f2^2 (gn alike)
 __device__ __forceinline__ double arap_dg(int k, const double *v1i, const double *v2i, const double *v1j,
                                           const double *v2j, const double *Rg, const double *tt) {
-#pragma clang fp contract(off)
     const double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
     const double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
     return ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
 }
 __device__ __forceinline__ double arap_fk(int k, const double *d1, const double *d2, const double *R, double area) {
-#pragma clang fp contract(off)
     return (d2[k] - (R[3 * k] * d1[0] + R[3 * k + 1] * d1[1] + R[3 * k + 2] * d1[2])) / area;
 }
 __device__ __forceinline__ double arap_combine(const double *dg, const double *f, const double *g, double w) {
-#pragma clang fp contract(off)
     const double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
     double fn = 0, gn = 0;
 #pragma unroll
