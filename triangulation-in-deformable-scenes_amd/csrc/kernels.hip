@@ -127,49 +127,32 @@ __global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t 
     E[e] = err;
 }
 
-// The ARAP energy (g2oTypes.h:300-349) in components; a component computed on its own is the same
-// expression as in a full evaluation (the same contractions), so it equals that component:
-//   dg_k = ((R_g v2i - t)_k - v1i_k) + ((R_g v2j - t)_k - v1j_k)
-//   f_k  = (d2i_k - (R_i d1i)_k) / area,   g_k = (d2j_k - (R_j d1j)_k) / area
-//   e    = (w (fn + gn) + dg.dg) - 0,  fn = ((0 + f0^2) + f1^2) + f2^2 (gn alike)
-__device__ __forceinline__ double arap_dg(int k, const double *v1i, const double *v2i, const double *v1j,
-                                          const double *v2j, const double *Rg, const double *tt) {
-    const double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
-    const double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
-    return ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
-}
-__device__ __forceinline__ double arap_fk(int k, const double *d1, const double *d2, const double *R, double area) {
-    return (d2[k] - (R[3 * k] * d1[0] + R[3 * k + 1] * d1[1] + R[3 * k + 2] * d1[2])) / area;
-}
-__device__ __forceinline__ double arap_combine(const double *dg, const double *f, const double *g, double w) {
-    const double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
-    double fn = 0, gn = 0;
+// the ARAP energy with the global transformation given as (rotation matrix, translation)
+__device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v2i, const double *v1j,
+                                              const double *v2j, const double *Rg, const double *tt,
+                                              const double *Ri, const double *Rj, double w, double area) {
+    double dg[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) { fn += f[k] * f[k]; gn += g[k] * g[k]; }
-    return (w * (fn + gn) + eg) - 0.0;
-}
-__device__ __forceinline__ void arap_diffs(const double *v1i, const double *v2i, const double *v1j, const double *v2j,
-                                           double *d1i, double *d2i, double *d1j, double *d2j) {
+    for (int k = 0; k < 3; k++) {
+        double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
+        double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
+        dg[k] = ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
+    }
+    double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
+    double d1i[3], d2i[3], d1j[3], d2j[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         d1i[k] = v1i[k] - v1j[k]; d2i[k] = v2i[k] - v2j[k];
         d1j[k] = v1j[k] - v1i[k]; d2j[k] = v2j[k] - v2i[k];
     }
-}
-
-// the ARAP energy with the global transformation given as (rotation matrix, translation)
-__device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v2i, const double *v1j,
-                                              const double *v2j, const double *Rg, const double *tt,
-                                              const double *Ri, const double *Rj, double w, double area) {
-    double dg[3], f[3], g[3], d1i[3], d2i[3], d1j[3], d2j[3];
-    arap_diffs(v1i, v2i, v1j, v2j, d1i, d2i, d1j, d2j);
+    double fn = 0, gn = 0;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        dg[k] = arap_dg(k, v1i, v2i, v1j, v2j, Rg, tt);
-        f[k] = arap_fk(k, d1i, d2i, Ri, area);
-        g[k] = arap_fk(k, d1j, d2j, Rj, area);
+        double f = (d2i[k] - (Ri[3 * k] * d1i[0] + Ri[3 * k + 1] * d1i[1] + Ri[3 * k + 2] * d1i[2])) / area;
+        double g = (d2j[k] - (Rj[3 * k] * d1j[0] + Rj[3 * k + 1] * d1j[1] + Rj[3 * k + 2] * d1j[2])) / area;
+        fn += f * f; gn += g * g;
     }
-    return arap_combine(dg, f, g, w);
+    return (w * (fn + gn) + eg) - 0.0;
 }
 
 __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
@@ -264,73 +247,36 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
     } else {                                       // g2o BaseMultiEdge numeric, delta 1e-9,
         const double delta = 1e-9, scalar = 1.0 / (2 * delta);   // the pair's transformations precomputed
         const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
-        double Rl[9], Rr[9];
+        double Rg[12];
 #pragma unroll
-        for (int k = 0; k < 9; k++) { Rl[k] = Ri[k]; Rr[k] = Rj[k]; }
-        // the unperturbed components; each perturbed evaluation recomputes only the components its
-        // coordinate enters (the others are the same operations on the same values):
-        //   v1i / v1j coordinate d: all of f and g, dg_d;  v2i / v2j coordinate d: all of dg, f_d, g_d;
-        //   T_g twist d: all of dg
-        double dg0[3], f0[3], g0[3], d1i[3], d2i[3], d1j[3], d2j[3];
-        arap_diffs(P[0], P[1], P[2], P[3], d1i, d2i, d1j, d2j);
+        for (int k = 0; k < 12; k++) Rg[k] = X[k];
+        // one coordinate at a time: x + delta (the others + 0.0, which leaves them unchanged), the
+        // coordinate loop kept rolled so a single evaluation's registers are live
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            dg0[k] = arap_dg(k, P[0], P[1], P[2], P[3], X, X + 9);
-            f0[k] = arap_fk(k, d1i, d2i, Rl, area);
-            g0[k] = arap_fk(k, d1j, d2j, Rr, area);
-        }
-#pragma unroll 1
         for (int vi = 0; vi < 4; vi++)
 #pragma unroll 1
             for (int dd = 0; dd < 3; dd++) {
-                double ev[2];
+                double Pp[4][3], Pm[4][3];
 #pragma unroll
-                for (int sgn = 0; sgn < 2; sgn++) {
-                    const double dl = sgn == 0 ? delta : -delta;
-                    // the perturbed vertex: + (+-delta) at dd, + 0.0 elsewhere (g2o's oplus of a copy)
-                    double V[4][3];
+                for (int a = 0; a < 4; a++)
 #pragma unroll
-                    for (int a2 = 0; a2 < 4; a2++)
-#pragma unroll
-                        for (int k = 0; k < 3; k++) V[a2][k] = (a2 == vi) ? P[a2][k] + (k == dd ? dl : 0.0) : P[a2][k];
-                    double dg[3], f[3], g[3];
-#pragma unroll
-                    for (int k = 0; k < 3; k++) { dg[k] = dg0[k]; f[k] = f0[k]; g[k] = g0[k]; }
-                    if (vi == 0 || vi == 2) {
-                        double e1i[3], e2i[3], e1j[3], e2j[3];
-                        arap_diffs(V[0], V[1], V[2], V[3], e1i, e2i, e1j, e2j);
-#pragma unroll
-                        for (int k = 0; k < 3; k++) {
-                            f[k] = arap_fk(k, e1i, e2i, Rl, area);
-                            g[k] = arap_fk(k, e1j, e2j, Rr, area);
-                        }
-                        dg[0] = arap_dg(0, V[0], V[1], V[2], V[3], X, X + 9);
-                        dg[1] = arap_dg(1, V[0], V[1], V[2], V[3], X, X + 9);
-                        dg[2] = arap_dg(2, V[0], V[1], V[2], V[3], X, X + 9);
-                    } else {
-                        double e1i[3], e2i[3], e1j[3], e2j[3];
-                        arap_diffs(V[0], V[1], V[2], V[3], e1i, e2i, e1j, e2j);
-#pragma unroll
-                        for (int k = 0; k < 3; k++) dg[k] = arap_dg(k, V[0], V[1], V[2], V[3], X, X + 9);
-                        f[dd] = arap_fk(dd, e1i, e2i, Rl, area);
-                        g[dd] = arap_fk(dd, e1j, e2j, Rr, area);
+                    for (int k = 0; k < 3; k++) {
+                        const double d = (a == vi && k == dd) ? delta : 0.0;
+                        Pp[a][k] = P[a][k] + d;
+                        Pm[a][k] = P[a][k] - d;
                     }
-                    ev[sgn] = arap_combine(dg, f, g, w);
-                }
-                const double jv = scalar * (ev[0] - ev[1]);
+                double ep = arap_err_rt(Pp[0], Pp[1], Pp[2], Pp[3], Rg, Rg + 9, Ri, Rj, w, area);
+                double em = arap_err_rt(Pm[0], Pm[1], Pm[2], Pm[3], Rg, Rg + 9, Ri, Rj, w, area);
+                const double jv = scalar * (ep - em);
                 if (dd == 0) Jv[3 * vi] = jv;
                 else if (dd == 1) Jv[3 * vi + 1] = jv;
                 else Jv[3 * vi + 2] = jv;
             }
         for (int dd = 0; dd < 6; dd++) {
             const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
-            double dgp[3], dgm[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                dgp[k] = arap_dg(k, P[0], P[1], P[2], P[3], Xp, Xp + 9);
-                dgm[k] = arap_dg(k, P[0], P[1], P[2], P[3], Xm, Xm + 9);
-            }
-            Jv[12 + dd] = scalar * (arap_combine(dgp, f0, g0, w) - arap_combine(dgm, f0, g0, w));
+            double ep = arap_err_rt(P[0], P[1], P[2], P[3], Xp, Xp + 9, Ri, Rj, w, area);
+            double em = arap_err_rt(P[0], P[1], P[2], P[3], Xm, Xm + 9, Ri, Rj, w, area);
+            Jv[12 + dd] = scalar * (ep - em);
         }
     }
     if (jld) {
