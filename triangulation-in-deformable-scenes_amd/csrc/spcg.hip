@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "spcg.h"
 
@@ -133,7 +134,8 @@ __device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; 
 // gathered once: added into H_v and stored).  Slots of a row: its incidences in the plan's order,
 // then its depth couplings, then padding.
 template <class JT>
-__global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3)))
+k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
     const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double mx = 0.0;
@@ -213,22 +215,26 @@ __global__ void __launch_bounds__(256) k_sp_glin_rows(const SpDev G, JT *__restr
             }
         };
         int64_t k = G.woff[w] * 64 + lane;
-        for (; k + 3 * 64 < k1; k += 4 * 64) {            // four slots: indices, loads, then in order
-            int m[4];
-            Raw r[4];
+        auto step = [&](auto U_) {                         // U slots: indices, loads, then in order
+            constexpr int U = decltype(U_)::value;
+            int m[U];
+            Raw r[U];
 #pragma unroll
-            for (int u = 0; u < 4; u++) m[u] = G.pmap[k + 64 * u];
+            for (int u = 0; u < U; u++) m[u] = G.pmap[k + 64 * u];
 #pragma unroll
-            for (int u = 0; u < 4; u++) r[u] = load(m[u]);
+            for (int u = 0; u < U; u++) r[u] = load(m[u]);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < U; u++) {
                 double v[3], wt, er;
                 value(m[u], r[u], v, wt, er);
                 add(m[u], v, wt, er);
 #pragma unroll
                 for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
             }
-        }
+            k += U * 64;
+        };
+        while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{});
+        if (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{});
         for (; k < k1; k += 64) {
             const int m = G.pmap[k];
             double v[3], wt, er;
@@ -766,8 +772,11 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
 
 // one wave per 64 rows of the wave layout: per slot (coalesced [k][64]) the entry's J slice times
 // s_e (ARAP) or p of the depth edge's scale; then the row's own terms
+// at most 4 waves per SIMD: the registers go to gathers in flight (a C2-size grid has ~3 waves per
+// SIMD to hide their latency with)
 template <class JT>
-__global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4)))
+k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     double beta;
     if (const int st = it_state(G, it, beta)) {
@@ -811,22 +820,26 @@ __global__ void __launch_bounds__(256) k_sp_phase2(int it, const SpDev G, double
             const double p = __fma_rn(beta, z.y, z.x);
             return v >= 0 ? a : (v <= -2 ? p : 0.0);
         };
-        // four slots per step: their indices, then the values and J slices, then the adds in order
-        for (; k + 3 * 64 < k1; k += 4 * 64) {
-            int v[4];
-            double sv[4], J[4][3];
+        // U slots per step: their indices, then the values and J slices, then the adds in order
+        auto step = [&](auto U_) {
+            constexpr int U = decltype(U_)::value;
+            int v[U];
+            double sv[U], J[U][3];
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = G.pidx[k + 64 * u];
+            for (int u = 0; u < U; u++) v[u] = G.pidx[k + 64 * u];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
+            for (int u = 0; u < U; u++) {
                 sv[u] = val(v[u]);
                 J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++)
+            for (int u = 0; u < U; u++)
 #pragma unroll
                 for (int a = 0; a < 3; a++) q[a] += J[u][a] * sv[u];
-        }
+            k += U * 64;
+        };
+        while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{});
+        if (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{});
         for (; k < k1; k += 64) {
             const double sv = val(G.pidx[k]);
             q[0] += (double)pjx[k] * sv;
