@@ -289,16 +289,30 @@ def cpu_baseline_sample(wl, window, n_sample, gpu_trials_per_iter):
     iteration x trial."""
     sys.path.insert(0, str(ROOT))
     from oracle import oracle
+    import threading
     prob, _ = build_workload(wl, n_sample, 1, window)
+    with capi.Context(-1) as hc:          # eliminate in the host analysis's order, as for C2
+        hc.analyse(prob)
+        oracle.set_vertex_order(hc.vertex_order())
     t = time.perf_counter()
-    r = oracle.solve_lm(prob, 1, analytic=False, max_trials=1)["report"]
+    done = threading.Event()
+
+    def heartbeat():
+        while not done.wait(30.0):
+            log(f"cpu baseline ({wl} sample): oracle running, {time.perf_counter() - t:.0f} s")
+    threading.Thread(target=heartbeat, daemon=True).start()
+    try:
+        r = oracle.solve_lm(prob, 1, analytic=False, max_trials=1)["report"]
+    finally:
+        done.set()
+        oracle.set_vertex_order(None)
     dt = time.perf_counter() - t
     lin = r["ms_linearize"] * 1e-3
     per_trial = (r["ms_factor"] + r["ms_solve"] + r["ms_update"]) * 1e-3 / max(r["trials_total"], 1)
     t_iter = lin + gpu_trials_per_iter * per_trial
     info = host_cpu_info()
     return {"value": 1.0 / t_iter, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"oracle LM (g2o numeric J, SimplicialLDLT) on the {wl} recipe at {n_sample} correspondences per "
+            "sample": f"oracle LM (g2o numeric J, SimplicialLDLT in the host analysis's elimination order) on the {wl} recipe at {n_sample} correspondences per "
                       f"keyframe ({prob.n_unknowns} unknowns, {len(prob.arap_pair)} ARAP edges), 1 thread: linearization "
                       f"{lin:.2f} s + one trial {per_trial:.2f} s, per iteration = linearization + "
                       f"{gpu_trials_per_iter:.2f} trials; {dt:.1f} s measured; host {info['cpu_model']}",
@@ -510,7 +524,7 @@ def main():
                     order = hc.vertex_order()
             cpu = cpu_baseline(prob, order, trials_per_it, args.cpu_full_iteration)
         else:
-            cpu = cpu_baseline_sample(wl, window, {"c3": 400, "c4": 400, "c5": 600}[wl], trials_per_it)
+            cpu = cpu_baseline_sample(wl, window, {"c3": 400, "c4": 400, "c5": 300}[wl], trials_per_it)
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     e2e = None
