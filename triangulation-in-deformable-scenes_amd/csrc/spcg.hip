@@ -108,6 +108,16 @@ __device__ __forceinline__ int it_state(const SpDev &G, int it, double &beta) {
     return 0;
 }
 
+// XCD-aware row blocks: workgroup b runs on XCD b % 8; the launch has 8 ceil(nrb / 8) row
+// workgroups and workgroup b takes logical row block (b % 8) seg + b / 8 (seg = ceil(nrb / 8)), so
+// each XCD walks one contiguous run of rows (its neighbours' s_e / p stay in that XCD's L2).
+// Logical blocks >= nrb are empty (they still take part in the launch's hand-off).
+__host__ __device__ __forceinline__ int row_grid(int nrb) { return 8 * ((max(nrb, 1) + 7) / 8); }
+__device__ __forceinline__ int row_block(int b, int nrb) {
+    const int seg = (max(nrb, 1) + 7) / 8;
+    return (b & 7) * seg + (b >> 3);
+}
+
 __device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q ? 6 * h : 6 * G.Q + (h - G.Q); }
 
 // Last-workgroup hand-off (G.fuse).  A workgroup's partials are published by thread 0 with
@@ -137,7 +147,8 @@ template <class JT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3)))
 k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lb = row_block(blockIdx.x, G.nrb);
+    const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double mx = 0.0;
     if (w < G.nwaves) {
         const int l = G.rowmap[64 * w + lane];
@@ -255,7 +266,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) G.mpart[blockIdx.x] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+    if (threadIdx.x == 0 && lb < max(G.nrb, 1)) G.mpart[lb] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
 }
 
 // heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1)
@@ -787,10 +798,11 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    if (G.fuse_heavy && (int)blockIdx.x >= max(G.nrb, 1)) {
+    const int rg = row_grid(G.nrb);
+    if (G.fuse_heavy && (int)blockIdx.x >= rg) {
         // the heavy vertices' sums (phase-1 partials only), concurrent with the rows
         __shared__ double lds[256];
-        heavy_sums_block(G, blockIdx.x - max(G.nrb, 1), red4, lds);
+        heavy_sums_block(G, blockIdx.x - rg, red4, lds);
         if (last_block(G, G.cnt)) {
             heavy_sums_block(G, G.Q + G.S, red4, lds);
             __syncthreads();
@@ -799,7 +811,8 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lb = row_block(blockIdx.x, G.nrb);
+    const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double pq = 0.0;
     if (w < G.nwaves) {
         const int l = G.rowmap[64 * w + lane];
@@ -868,9 +881,9 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
     }
     const double sm = block_sum(pq, red4);
-    if (threadIdx.x == 0) {
-        if (G.fuse_heavy) publish(G, G.rpart + blockIdx.x, sm);
-        else G.rpart[blockIdx.x] = sm;
+    if (threadIdx.x == 0 && lb < max(G.nrb, 1)) {
+        if (G.fuse_heavy) publish(G, G.rpart + lb, sm);
+        else G.rpart[lb] = sm;
     }
     if (G.fuse_heavy && last_block(G, G.cnt)) {
         // k_sp_heavy's finish of this iteration in the last workgroup (rows' p.q, heavy q, alpha)
@@ -1047,8 +1060,8 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
     } while (0)
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, std::max(G.nrb, 1), G, G.pj32);
-    else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, std::max(G.nrb, 1), G, G.pj);
+    if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, sp::row_grid(G.nrb), G, G.pj32);
+    else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, sp::row_grid(G.nrb), G, G.pj);
     if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
     if (G.nch > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.nch, G);
 }
@@ -1082,7 +1095,7 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         else SPL("sp_phase1", sp::k_sp_phase1<double>, G.nblk, it, G, G.Ja);
     }
     // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) after the row blocks
-    const int grid = std::max(G.nrb, 1) + (G.fuse_heavy ? G.Q + G.S : 0);
+    const int grid = sp::row_grid(G.nrb) + (G.fuse_heavy ? G.Q + G.S : 0);
     if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, grid, it, G, lambda, (const float *)G.pj32);
     else SPL("sp_phase2", sp::k_sp_phase2<double>, grid, it, G, lambda, (const double *)G.pj);
 }
