@@ -62,14 +62,25 @@ HBM_PEAK_GBS = 8000.0              # MI355X HBM3E spec (MI355X_MICROARCH.md; 6.2
 MFMA_F64_SUSTAINED_TFLOPS = 48.3   # v_mfma_f64_16x16x4 back-to-back on this box (tools/micro/mfma_f64_peak.hip)
 BASELINE_METRIC = "LM iterations/sec + ms/iter at 100k corr \u00d7 2 views; 1/2/4/8-GPU scaling"
 REP_W, ARAP_W, DEPTH_SIGMA = 1.0, 2e5, np.float32(3.0 / 1000.0)
+# the C2 scene under the three weight regimes of the reference's data sets (rep, arap, sigma_d, KB8):
+# Simulation.yaml; Drunkard.yaml:68,77 (DepthWeight 0.3 mm); Realcolon.yaml:15-23,101,110 (DepthWeight
+# 0.001 -> 1e-6 m, information 1e12, arap 0.1, distorted KB8)
+REGIME = "simulation"
+REGIMES = {
+    "simulation": (1.0, 2e5, np.float32(3.0 / 1000.0), None),
+    "drunkard": (1.0, 1e7, np.float32(0.3) / np.float32(1000.0), "DRUNKARD_KB8"),
+    "realcolon": (1.0, 0.1, np.float32(0.001) / np.float32(1000.0), "REALCOLON_KB8"),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_problem(n, seed):
-    return sim.two_view_problem(n, seed, REP_W, ARAP_W, DEPTH_SIGMA, return_map=True)
+def build_problem(n, seed, regime="simulation"):
+    rep, arap, sig, kb8 = REGIMES[regime]
+    return sim.two_view_problem(n, seed, rep, arap, sig, return_map=True,
+                                kb8=getattr(sim, kb8) if kb8 else None)
 
 
 def end_to_end(device, m, configure, n_it=25):
@@ -274,7 +285,7 @@ WORKLOADS = {
 def build_workload(wl, n, seed, window):
     spec = WORKLOADS[wl]
     if wl == "c2":
-        prob, m = build_problem(n, seed)
+        prob, m = build_problem(n, seed, REGIME)
         return prob, m
     kb8 = sim.DRUNKARD_KB8 if spec["kb8"] == "drunkard" else sim.REALCOLON_KB8
     rep, arap, sig = spec["w"]
@@ -391,6 +402,8 @@ def main():
                     help="a tiny torch kernel right before and after the timed region (kernel-trace windows)")
     ap.add_argument("--corr", type=int, default=0, help="correspondences per keyframe (default: the workload's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--regime", choices=list(REGIMES), default="simulation",
+                    help="c2: the weight regime (Simulation.yaml default; Drunkard / Realcolon weights and cameras)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "ba"], default="c2",
                     help="c2: the headline (BASELINE.json metric); c3-c5: the multi-keyframe configs; ba: bundle adjustment")
     ap.add_argument("--pair-window", type=int, default=-1,
@@ -414,6 +427,8 @@ def main():
     ap.add_argument("--cpu-full-iteration", action="store_true",
                     help="CPU baseline: time the oracle's whole first LM iteration (all trials)")
     args = ap.parse_args()
+    global REGIME
+    REGIME = args.regime
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -528,7 +543,7 @@ def main():
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     e2e = None
-    if world == 1 and not args.no_e2e and wl == "c2":
+    if world == 1 and not args.no_e2e and wl == "c2" and REGIME == "simulation":
         def configure(c):
             c.set_plan(args.plan)
             c.set_jacobian_storage(1 if args.jacobian_fp32 else 0)
@@ -538,10 +553,11 @@ def main():
         log(f"end-to-end arapOptimization: {e2e}")
 
     if rank == 0:
-        workload = ("C2" if n == 100000 else f"two-view-{n}") if wl == "c2" else \
+        workload = (("C2" if n == 100000 else f"two-view-{n}") + ("" if REGIME == "simulation" else f"-{REGIME}")) if wl == "c2" else \
             (wl.upper() if n == spec["n"] else f"{wl.upper()}-slice-{n}x{spec['k']}")
         out = {
-            "metric": BASELINE_METRIC if wl == "c2" else f"LM iterations/sec + ms/iter, {wl.upper()}: {spec['desc']}",
+            "metric": (BASELINE_METRIC if REGIME == "simulation" else f"LM iterations/sec + ms/iter at 100k corr x 2 views, {REGIME} weights")
+            if wl == "c2" else f"LM iterations/sec + ms/iter, {wl.upper()}: {spec['desc']}",
             "value": value, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak" if (world > 1 and not sharded) else "strong", "vs_baseline": None, "dtype": "f64",

@@ -14,7 +14,9 @@ Tolerances (the PCG stop test is 1e-12 on the recurrence residual):
     an all-pairs 8-keyframe scene: identical trials, chi2 rel 1e-8 analytic (1e-6 numeric), gathered
     state rel 1e-8 against the one-rank plan
   * fp32 Jacobian storage: identical trial counts on the golden-size all-pairs scene, RMSE within
-    1e-4 px of the fp64 run"""
+    1e-4 px of the fp64 run
+  * C5 shape (20 keyframes, Realcolon weights, 19 consecutive / all 190 pairs): identical trials,
+    chi2 rel 1e-6, points rel 1e-6 vs the oracle"""
 import os
 
 import numpy as np
@@ -113,6 +115,32 @@ def test_iterative_lm_all_pairs_matches_oracle(it_ctx, analytic, tol):
     pts, sc, tg = it_ctx.download()
     assert np.abs(pts - res["points"]).max() <= 1e-6 * max(np.abs(res["points"]).max(), 1.0)
     np.testing.assert_allclose(sc, res["scales"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("n,window,n_it", [(60, 1, 4), (24, 0, 3)])
+def test_iterative_lm_c5_shape_matches_oracle(it_ctx, n, window, n_it):
+    """BASELINE C5's shape at test size: 20 keyframes, Realcolon weights (Data/Realcolon.yaml:15-23,
+    101,110: KB8 with distortion, arap 0.1, DepthWeight 0.001 -> information 1e12), g2o numeric
+    Jacobians; the 19 consecutive pairs of the timed C5 (pair window 1) and the reference's all 190
+    pairs.  The oracle eliminates in the host analysis's order."""
+    p = sim.multi_view_problem(n, 20, seed=3, kb8=sim.REALCOLON_KB8, rep_weight=1.0, arap_weight=0.1,
+                               depth_sigma=np.float32(1e-6), pair_window=window)
+    assert p.n_pairs == (19 if window == 1 else 190) and p.n_scales == 2 * p.n_pairs
+    it_ctx.upload(p)
+    r = it_ctx.solve_lm(n_it, analytic=False)
+    with capi.Context(-1) as h:
+        h.analyse(p)
+        oracle.set_vertex_order(h.vertex_order())
+    try:
+        res = oracle.solve_lm(p, n_it, analytic=False)
+    finally:
+        oracle.set_vertex_order(None)
+    ref = res["report"]
+    assert r["iterations"] == ref["iterations"] and r["trials_total"] == ref["trials_total"]
+    np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=1e-6)
+    assert r["pcg_trials"] == r["trials_total"] and r["pcg_fallbacks"] == 0
+    pts, sc, tg = it_ctx.download()
+    assert np.abs(pts - res["points"]).max() <= 1e-6 * max(np.abs(res["points"]).max(), 1.0)
 
 
 def test_iterative_matches_multifrontal_two_view(gpu_ctx):

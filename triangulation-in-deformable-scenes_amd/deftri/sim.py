@@ -330,12 +330,14 @@ def multi_view_problem(n, k, seed=1, kb8=DRUNKARD_KB8, rep_weight=1.0, arap_weig
     return p
 
 
-def two_view_problem(n, seed=1, rep_weight=1.0, arap_weight=2e5, depth_sigma=np.float32(0.003), return_map=False):
+def two_view_problem(n, seed=1, rep_weight=1.0, arap_weight=2e5, depth_sigma=np.float32(0.003), return_map=False,
+                     kb8=None):
     """The benchmark scene (BASELINE C1/C2 shapes): simulate_two_view with the extents scaled to n
     correspondences and failed triangulations dropped, then the arapOptimization graph built by the
-    product's host builder (deftri_arap_build_graph)."""
+    product's host builder (deftri_arap_build_graph).  kb8: the camera (default Simulation.yaml's)."""
     from . import capi
-    m, _ = simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True)
+    kw = {} if kb8 is None else {"kb8": kb8}
+    m, _ = simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True, **kw)
     host = capi.Context(-1)
     p = host.build_graph(m, rep_weight, arap_weight, depth_sigma)
     host.close()
