@@ -80,7 +80,9 @@ struct Mesh {
     }
 };
 
-bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err) {
+void mesh_cot_weights(const std::vector<double> &pos, Mesh &M);
+
+bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err, bool host_weights = true) {
     if (n < 3) { err = "Not enough points to create a triangular mesh."; return false; }
     std::vector<double> xy(2 * (size_t)n);
     for (int i = 0; i < n; i++) { xy[2 * i] = pos[3 * i]; xy[2 * i + 1] = pos[3 * i + 1]; }
@@ -116,21 +118,23 @@ bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err
         M.off[i + 1] = M.off[i] + (int32_t)(e - b);
     }
     M.adj.resize(M.off[n]);
-    // cot weights: per undirected edge (lo, hi), the mean of a.b / |a x b| over its opposite
-    // vertices (at most 2 in a planar triangulation, so the sum is order-independent), a = p_lo - v,
-    // b = p_hi - v, clamped at 0; stored on both CSR entries
+    if (host_weights) mesh_cot_weights(pos, M);
+    return true;
+}
+
+// cot weights (ComputeEdgeWeightsCot, Geometry.cc:272-298): per undirected edge (lo, hi), the mean of
+// cot_term over its opposite vertices (at most 2 in a planar triangulation, so the sum does not
+// depend on their order), clamped at 0; stored on both CSR entries
+void mesh_cot_weights(const std::vector<double> &pos, Mesh &M) {
+    const int n = (int)M.off.size() - 1, ntri = (int)M.tris.size() / 3;
     std::vector<double> sum(M.adj.size(), 0.0);
     std::vector<int32_t> num(M.adj.size(), 0);
     for (int t = 0; t < ntri; t++) {
         const int v3[3] = {M.tris[3 * t], M.tris[3 * t + 1], M.tris[3 * t + 2]};
         for (int k = 0; k < 3; k++) {
             const int e0 = std::min(v3[k], v3[(k + 1) % 3]), e1 = std::max(v3[k], v3[(k + 1) % 3]), v2 = v3[(k + 2) % 3];
-            const double *A = &pos[3 * e0], *B = &pos[3 * e1], *V = &pos[3 * v2];
-            double a[3] = {A[0] - V[0], A[1] - V[1], A[2] - V[2]};
-            double b[3] = {B[0] - V[0], B[1] - V[1], B[2] - V[2]};
-            double cr[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
             const int64_t at = M.find(e0, e1);
-            sum[at] += (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+            sum[at] += cot_term(&pos[3 * e0], &pos[3 * e1], &pos[3 * v2]);
             num[at]++;
         }
     }
@@ -139,10 +143,8 @@ bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err
         for (int32_t k = M.off[i]; k < M.off[i + 1]; k++) {
             const int j = M.adj[k];
             if (j < i) continue;
-            const double wt = num[k] > 0 ? sum[k] / num[k] : 0;
-            M.w[k] = M.w[M.find(j, i)] = wt < 0.0 ? 0.0 : wt;
+            M.w[k] = M.w[M.find(j, i)] = cot_weight(sum[k], num[k]);
         }
-    return true;
 }
 
 // open-addressing MapPoint id -> graph point index (ids are >= 0)
@@ -343,7 +345,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             const int n1 = (int)pos1.size() / 3, n2 = (int)pos2.size() / 3;
             auto t0 = tnow();
             Mesh M;
-            if (!build_mesh(pos1, n1, M, err)) return false;
+            if (!build_mesh(pos1, n1, M, err, gdev == nullptr)) return false;   // device: weights in the device pass
             auto t1 = tnow();
             // T_global: map transformation for (kf1, kf2) or identity (:664-677)
             // getGlobalKeyFramesTransformation(k2->first, k1->first) = (kf1.id, kf2.id): the table
@@ -373,8 +375,9 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             g.rot.resize(rbase + 9 * (size_t)n1);
             double *Rs = g.rot.data() + rbase;
             if (gdev) {
-                if (!gdev->compute_r(n1, n2, M.off.data(), M.adj.data(), M.w.data(), (int64_t)M.adj.size(), posIdx.data(),
-                                     inv.data(), pos1.data(), pos2.data(), Rs, err))
+                M.w.resize(M.adj.size());
+                if (!gdev->mesh_pass(n1, n2, M.tris.data(), (int)M.tris.size() / 3, M.off.data(), M.adj.data(), (int64_t)M.adj.size(),
+                                     posIdx.data(), inv.data(), pos1.data(), pos2.data(), M.w.data(), Rs, err))
                     return false;
             } else {
                 parallel_for(n1, 2048, [&](int lo, int hi) {

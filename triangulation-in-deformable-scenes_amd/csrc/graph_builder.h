@@ -32,16 +32,18 @@ struct GraphResult {
     int64_t memo_hits = 0;                    // calls answered from the memo (kept across rebuilds)
 };
 
-// computeR on the device (graph_dev.hip): one thread per mesh vertex over the pair's CSR mesh,
-// the same arithmetic as the host loop (procrustes.h), so both give the same rotations bit for bit
+// The per-pair geometry on the device (graph_dev.hip): the cot weights of the pair's CSR mesh (one
+// thread per triangle corner, the edge's two corner terms added in the finishing pass) and computeR
+// (one thread per vertex); the same arithmetic as the host loops (procrustes.h), so both give the
+// same weights and rotations bit for bit
 class GraphDevice {
  public:
     GraphDevice(int device, hipStream_t st) : dev_(device), st_(st) {}
     ~GraphDevice();
-    bool compute_r(int n1, int n2, const int32_t *off, const int32_t *adj, const double *w, int64_t nadj,
-                   const int32_t *pos_idx, const int32_t *inv, const double *pos1, const double *pos2, double *R,
-                   std::string &err);
-    double ms_last = 0;          // device time of the last compute_r (kernel only)
+    bool mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const int32_t *off, const int32_t *adj, int64_t nadj,
+                   const int32_t *pos_idx, const int32_t *inv, const double *pos1, const double *pos2, double *w,
+                   double *R, std::string &err);
+    double ms_last = 0;          // device time of the last mesh_pass (kernels only)
 
  private:
     int dev_;

@@ -154,6 +154,20 @@ __host__ __device__ inline void mat_from_quat(const double q[4], double R[9]) {
 
 }  // namespace pr
 
+// ComputeEdgeWeightsCot's term for the edge (A, B) seen from its opposite vertex V (Geometry.cc:
+// 272-298): a.b / |a x b| with a = A - V, b = B - V (A the lower vertex index)
+__host__ __device__ inline double cot_term(const double *A, const double *B, const double *V) {
+    const double a[3] = {A[0] - V[0], A[1] - V[1], A[2] - V[2]};
+    const double b[3] = {B[0] - V[0], B[1] - V[1], B[2] - V[2]};
+    const double cr[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+    return (a[0] * b[0] + a[1] * b[1] + a[2] * b[2]) / sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+}
+// the edge's weight: the mean over its (at most two) opposite vertices, clamped at 0
+__host__ __device__ inline double cot_weight(double sum, int num) {
+    const double wt = num > 0 ? sum / num : 0;
+    return wt < 0.0 ? 0.0 : wt;
+}
+
 // R = the computeR rotation of the 3x3 cross-covariance S (row-major)
 __host__ __device__ inline void procrustes_rotation_hd(const double S[9], double R[9]) {
     double U[9], s[3], V[9];
