@@ -548,8 +548,11 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     constexpr int nw = 3 * kSpUpdRows / 64;
     double rz = 0.0, rr = 0.0;
-    if ((int)blockIdx.x < G.nrb) {
-        const int l0 = blockIdx.x * kSpUpdRows;
+    // workgroup 0: the heavy dofs (dispatched first: their serial work overlaps the rows); row block
+    // blockIdx - 1; partial slots as in k_sp_dots (rows 0..nrb-1, heavy nrb)
+    const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
+    if (rb >= 0) {
+        const int l0 = rb * kSpUpdRows;
         const int nrow = min(kSpUpdRows, G.nown - l0);
         const int64_t o0 = G.hd + 3 * (int64_t)(G.row0 + l0);
         const double *Hg = G.Hv + 6 * (int64_t)l0;
@@ -630,7 +633,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
         double s0 = 0.0, s1 = 0.0;
 #pragma unroll
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
-        double *out = G.upart + 2 * blockIdx.x;
+        double *out = G.upart + 2 * slot;
         if (G.fuse && !G.fence) {
             __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -798,11 +801,11 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    const int rg = row_grid(G.nrb);
-    if (G.fuse_heavy && (int)blockIdx.x >= rg) {
-        // the heavy vertices' sums (phase-1 partials only), concurrent with the rows
+    const int nhx = G.fuse_heavy ? G.Q + G.S : 0;
+    if ((int)blockIdx.x < nhx) {
+        // the heavy vertices' sums (phase-1 partials only): dispatched first, concurrent with the rows
         __shared__ double lds[256];
-        heavy_sums_block(G, blockIdx.x - rg, red4, lds);
+        heavy_sums_block(G, blockIdx.x, red4, lds);
         if (last_block(G, G.cnt)) {
             heavy_sums_block(G, G.Q + G.S, red4, lds);
             __syncthreads();
@@ -811,7 +814,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    const int lb = row_block(blockIdx.x, G.nrb);
+    const int lb = row_block(blockIdx.x - nhx, G.nrb);
     const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double pq = 0.0;
     if (w < G.nwaves) {
@@ -939,8 +942,11 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     constexpr int nw = 3 * kSpUpdRows / 64;
     double rz = 0.0, rr = 0.0;
-    if ((int)blockIdx.x < G.nrb) {
-        const int l0 = blockIdx.x * kSpUpdRows;
+    // workgroup 0: the heavy dofs (dispatched first: their serial work overlaps the rows); row block
+    // blockIdx - 1; partial slots as in k_sp_dots (rows 0..nrb-1, heavy nrb)
+    const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
+    if (rb >= 0) {
+        const int l0 = rb * kSpUpdRows;
         const int nrow = min(kSpUpdRows, G.nown - l0);
         const int64_t o0 = G.hd + 3 * (int64_t)(G.row0 + l0);
         const bool on = t < 3 * nrow;
@@ -1001,7 +1007,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
         double s0 = 0.0, s1 = 0.0;
 #pragma unroll
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
-        double *out = G.upart + 2 * blockIdx.x;
+        double *out = G.upart + 2 * slot;
         if (G.fuse && !G.fence) {
             __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
