@@ -149,6 +149,16 @@ struct SumJob { int64_t n = 0; const double *a = nullptr, *b = nullptr, *w = nul
 constexpr int kMaxSumJobs = 4;
 struct SumJobs { SumJob j[kMaxSumJobs]; int nj = 0; double *total = nullptr; };
 void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st);
+// the trial read-back (k_trial_readback) folded into launch_sum_multi_fused's last workgroup
+struct ReadBack {
+    const double *scal = nullptr; int ns = 0; const int *flag = nullptr; const double *rec = nullptr; int nrec = 0;
+    double *h_scal = nullptr; int *h_flag = nullptr; double *h_rec = nullptr;
+};
+// launch_sum_multi in one launch (same sums, same order; *cnt zero between launches), optionally
+// followed by the read-back
+void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st);
+// the errors and chi2 of all edges (launch_linearize without Jacobians) in one launch
+void launch_lin_chi(const DevProblem &P, hipStream_t st);
 void launch_pack_cb(const DevPlan &L, int64_t arena_off, int m, int s, double *buf, hipStream_t st);
 void launch_ea_packed(const DevPlan &L, int64_t ea_off, int nea, const double *buf, hipStream_t st);
 void launch_gather_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st);

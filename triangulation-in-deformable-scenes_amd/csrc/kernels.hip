@@ -40,13 +40,12 @@ __device__ __forceinline__ void huber_rho(double delta, double e2, double &rho0,
     else { double se = sqrt(e2); rho0 = 2 * se * delta - dsqr; rho1 = delta / se; }
 }
 
-__global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
+__device__ __forceinline__ void lin_rep_edge(int e, int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
                           const double *__restrict__ obs, const double *__restrict__ info, double hdelta,
                           const double *__restrict__ points, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, const float *__restrict__ kb8,
                           double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
                           double *__restrict__ chi, int want_jac) {
-    int e = TID;
     if (e >= R) return;
     int c = rc[e];
     const double *pp = points + 3 * (int64_t)rp[e];
@@ -85,13 +84,12 @@ __device__ __forceinline__ double depth_err(const SE3 &T, const double p[3], dou
     return error;
 }
 
-__global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
+__device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
                           const int32_t *__restrict__ dcam, const double *__restrict__ meas,
                           const double *__restrict__ info, const double *__restrict__ points,
                           const double *__restrict__ scales, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
-    int e = TID;
     if (e >= D) return;
     int c = dcam[e];
     const double *pp = points + 3 * (int64_t)dpt[e];
@@ -188,7 +186,7 @@ __global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restr
 // MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian (one kernel per
 // mode: each gets the registers of its own path)
 template <int MODE>
-__global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+__device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
                            const int32_t *__restrict__ arot, const double *__restrict__ aw,
                            const double *__restrict__ rot, const double *__restrict__ parea,
                            const double *__restrict__ pinfo, const double *__restrict__ points,
@@ -196,7 +194,6 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
                            double *__restrict__ J, double *__restrict__ W,
                            double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
                            int64_t jld) {
-    int e = TID;
     if (e >= E_) return;
     const int32_t *v = apts + 4 * (int64_t)e;
     double P[4][3];
@@ -287,6 +284,55 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
     }
     W[e] = om;
     E[e] = err;
+}
+
+__global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
+                          const double *__restrict__ obs, const double *__restrict__ info, double hdelta,
+                          const double *__restrict__ points, const double *__restrict__ cam_pose,
+                          const double *__restrict__ cam_R, const float *__restrict__ kb8,
+                          double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
+                          double *__restrict__ chi, int want_jac) {
+    lin_rep_edge(TID, R, rp, rc, obs, info, hdelta, points, cam_pose, cam_R, kb8, J, W, E, chi, want_jac);
+}
+
+__global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
+                          const int32_t *__restrict__ dcam, const double *__restrict__ meas,
+                          const double *__restrict__ info, const double *__restrict__ points,
+                          const double *__restrict__ scales, const double *__restrict__ cam_pose,
+                          const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
+                          double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+    lin_dep_edge(TID, D, dpt, dsc, dcam, meas, info, points, scales, cam_pose, cam_R, J, W, E, chi, want_jac, analytic);
+}
+
+// MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian (one kernel per
+// mode: each gets the registers of its own path)
+template <int MODE>
+__global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+                           const int32_t *__restrict__ arot, const double *__restrict__ aw,
+                           const double *__restrict__ rot, const double *__restrict__ parea,
+                           const double *__restrict__ pinfo, const double *__restrict__ points,
+                           const double *__restrict__ tg, const double *__restrict__ tg_pre,
+                           double *__restrict__ J, double *__restrict__ W,
+                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
+                           int64_t jld) {
+    lin_arap_edge<MODE>(TID, E_, apts, apair, arot, aw, rot, parea, pinfo, points, tg, tg_pre, J, W, E, chi, want_jac,
+                        analytic, jld);
+}
+
+// the errors and chi2 of every reprojection, depth and ARAP edge in one launch (the trial's
+// evaluation): the same per-edge code as k_lin_rep / k_lin_dep / k_lin_arap<0>, block ranges by type
+__global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, int nbd) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (b < nbr)
+        lin_rep_edge(b * 128 + t, P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose,
+                     P.cam_R, P.cam_kb8, P.Jrep, P.Wrep, P.Erep, P.chi_rep, 0);
+    else if (b < nbr + nbd)
+        lin_dep_edge((b - nbr) * 128 + t, P.D, P.dep_point, P.dep_scale, P.dep_cam, P.dep_meas, P.dep_info, P.points,
+                     P.scales, P.cam_pose, P.cam_R, P.Jdep, P.Wdep, P.Edep, P.chi_dep, 0, 0);
+    else
+        lin_arap_edge<0>((b - nbr - nbd) * 128 + t, P.E, P.arap_pts, P.arap_pair, P.arap_rot, P.arap_w, P.rot,
+                         P.pair_area, P.pair_info, P.points, P.tg, nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, 0, 0,
+                         P.jarap_ld);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1448,6 +1494,67 @@ __global__ void __launch_bounds__(256) k_sum_multi_partial(const SumJobs J, doub
 }
 
 // one wave per job: its parts strided over the lanes, then the butterfly (k_sum_final's order)
+// k_sum_multi_partial + k_sum_multi_final in one launch (the same sums in the same order): every
+// workgroup publishes its partial with an agent-scope atomic store and takes a ticket; the last one
+// forms the totals from the partials (agent-scope loads) and, when rb.h_scal is set, also does
+// k_trial_readback's copies into pinned host memory.  *cnt is 0 between launches.
+__global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt,
+                                                         const ReadBack rb) {
+    const SumJob &jb = J.j[blockIdx.y];
+    __shared__ double red[256];
+    __shared__ int last;
+    const int64_t n = jb.n;
+    int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+    int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
+    double acc = 0.0;
+    const int mode = jb.mode;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        double v = jb.a[i];
+        acc += (mode == 0) ? v : (mode == 1) ? v * (jb.lambda * v + jb.b[i]) : v * (jb.lambda * jb.w[i] * v + jb.b[i]);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+    }
+    const int nparts = gridDim.x, nblk = gridDim.x * gridDim.y;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(part + (int64_t)blockIdx.y * gridDim.x + blockIdx.x, red[0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __shared__ double s[kMaxSumJobs];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (w < J.nj) {
+        double a = 0.0;
+        for (int i = lane; i < nparts; i += 64)
+            a += __hip_atomic_load(part + (int64_t)w * nparts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+        if (lane == 0) {
+            const double v = J.j[w].n > 0 ? a : 0.0;
+            *J.j[w].out = v;
+            s[w] = v;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && J.total) *J.total = (s[0] + s[2]) + s[1];
+    __syncthreads();
+    if (rb.h_scal) {
+        const int t = threadIdx.x;
+        if (t < rb.ns) rb.h_scal[t] = rb.scal[t];
+        if (t == 0) *rb.h_flag = *rb.flag;
+        if (rb.rec && t < rb.nrec) rb.h_rec[t] = rb.rec[t];
+    }
+    if (threadIdx.x == 0) *cnt = 0;
+}
+
 __global__ void k_sum_multi_final(const SumJobs J, int nparts, const double *__restrict__ part) {
     __shared__ double s[kMaxSumJobs];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1900,6 +2007,17 @@ void launch_sum(int64_t n, const double *a, const double *b, double lambda, int 
     if (n <= 0) { hipMemsetAsync(out, 0, sizeof(double), st); return; }
     LAUNCH("sum_partial", dev::k_sum_partial, dim3(nparts), dim3(256), st, n, a, b, lambda, mode, w, part);
     LAUNCH("sum_final", dev::k_sum_final, dim3(1), dim3(64), st, nparts, part, out);
+}
+
+void launch_lin_chi(const DevProblem &P, hipStream_t st) {
+    const int nbr = P.R > 0 ? (int)nb(P.R, 128) : 0, nbd = P.D > 0 ? (int)nb(P.D, 128) : 0;
+    const int nba = P.E > 0 ? (int)nb(P.E, 128) : 0;
+    if (nbr + nbd + nba > 0) LAUNCH("lin_chi", dev::k_lin_chi, dim3(nbr + nbd + nba), dim3(128), st, P, nbr, nbd);
+}
+
+void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st) {
+    if (J.nj <= 0) return;
+    LAUNCH("sum_fused", dev::k_sum_multi_fused, dim3(nparts, J.nj), dim3(256), st, J, part, cnt, rb);
 }
 
 void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st) {

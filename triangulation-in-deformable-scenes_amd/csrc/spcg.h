@@ -234,6 +234,7 @@ class SpSolver {
     std::vector<double *> init_;      // initial state (points plan order, scales, tg)
     double *d_scal = nullptr, *d_part = nullptr, *d_dx0 = nullptr, *d_tmp = nullptr;
     int *d_flag = nullptr;
+    int *d_sumcnt = nullptr;           // launch_sum_multi_fused's ticket
     double *hpin = nullptr;
     int *ipin = nullptr;
     int32_t *d_send_rows = nullptr, *d_recv_rows = nullptr;
@@ -246,7 +247,7 @@ class SpSolver {
     int fail(int code, const std::string &m) { err = m; return code; }
     int budget() const;
     int lin_iteration(bool analytic, bool want_max, bool &ok);
-    int eval_chi2(bool analytic, int slot, const SumJob *extra);
+    int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr);
     void cg_setup(double lambda, const double *rhs);
     void cg_chain(double lambda, int from, int to);
     int cg_tail(int n);

@@ -289,8 +289,9 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
     SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
     SPOK(hipMemset(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (kSpMaxIt + 2))));
-    ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1);
+    ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1); ALLOC(d_sumcnt, 1);
     SPOK(hipMemset(d_flag, 0, sizeof(int)));
+    SPOK(hipMemset(d_sumcnt, 0, sizeof(int)));
     ALLOC(d_tmp, G.ndof); ALLOC(d_dx0, G.ndof);
     PUT(d_row_of_point, H.row_of_point);
     // halo lists: per peer, sends then receives, 6 doubles per row ((z, p) of 3 dofs)
@@ -337,8 +338,9 @@ int SpSolver::halo(int width, double *vec, bool zp) {
 
 // computeActiveErrors (+ linearizeOplus with jac) on the rank's edges, chi2 of its owned edges into
 // d_scal[slot]; `extra`: one more fixed-order sum in the same launches (the rho denominator)
-int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra) {
-    launch_linearize(P, st_, false, analytic);
+int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb) {
+    (void)analytic;                  // errors only: the Jacobian mode does not enter
+    launch_lin_chi(P, st_);          // k_lin_rep / k_lin_dep / k_lin_arap<0> in one launch
     SumJobs J;
     J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
     J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
@@ -346,7 +348,7 @@ int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra) {
     J.nj = 3;
     if (extra) J.j[J.nj++] = *extra;
     J.total = d_scal + slot;
-    launch_sum_multi(J, d_part, kSpRedParts, st_);
+    launch_sum_multi_fused(J, d_part, kSpRedParts, d_sumcnt, rb ? *rb : ReadBack{}, st_);
     return 0;
 }
 
@@ -361,7 +363,7 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
     J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
     J.nj = 3;
     J.total = d_scal;
-    launch_sum_multi(J, d_part, kSpRedParts, st_);
+    launch_sum_multi_fused(J, d_part, kSpRedParts, d_sumcnt, ReadBack{}, st_);
     int rc;
     if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_);
@@ -508,8 +510,15 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 SumJob den;
                 den.n = den_n; den.a = G.x + den_off; den.b = G.b + den_off; den.lambda = lambda; den.mode = 1;
                 den.out = d_scal + 1;
+                if (!dist) {         // the read-back rides the sums' last workgroup
+                    ReadBack rb;
+                    rb.scal = d_scal; rb.ns = 2; rb.flag = d_flag; rb.rec = G.rec; rb.nrec = kSpRecDoubles;
+                    rb.h_scal = sc; rb.h_flag = ipin; rb.h_rec = hpin + 16;
+                    eval_chi2(analytic, 0, &den, &rb);
+                    return 0;
+                }
                 eval_chi2(analytic, 0, &den);
-                if (dist && (r2 = tr_->allreduce(d_scal, 2, 0, st_))) return r2;
+                if ((r2 = tr_->allreduce(d_scal, 2, 0, st_))) return r2;
                 launch_trial_readback(d_scal, 2, d_flag, G.rec, kSpRecDoubles, sc, ipin, hpin + 16, st_);
                 return 0;
             };
