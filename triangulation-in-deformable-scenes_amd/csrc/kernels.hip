@@ -1533,7 +1533,16 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (w < J.nj) {
         double a = 0.0;
-        for (int i = lane; i < nparts; i += 64)
+        int i = lane;
+        for (; i + 7 * 64 < nparts; i += 8 * 64) {        // eight loads in flight, added in order
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                v[u] = __hip_atomic_load(part + (int64_t)w * nparts + i + 64 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int u = 0; u < 8; u++) a += v[u];
+        }
+        for (; i < nparts; i += 64)
             a += __hip_atomic_load(part + (int64_t)w * nparts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
