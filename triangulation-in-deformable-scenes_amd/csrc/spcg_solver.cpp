@@ -36,6 +36,12 @@ constexpr int kSpMaxIt = 4096;
 constexpr int kSpDefaultIt = 1000;
 constexpr int kSpRedParts = 512;
 constexpr int kSpRecDoubles = 8;
+// workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
+// chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
+int sum_parts() {
+    static const int v = std::getenv("DEFTRI_SP_SUM_PARTS") ? std::atoi(std::getenv("DEFTRI_SP_SUM_PARTS")) : 128;
+    return std::max(1, std::min(v, kSpRedParts));
+}
 
 void quat_norm(double *q) {      // SE3Quat::normalizeRotation
     if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
@@ -348,7 +354,7 @@ int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const Read
     J.nj = 3;
     if (extra) J.j[J.nj++] = *extra;
     J.total = d_scal + slot;
-    launch_sum_multi_fused(J, d_part, kSpRedParts, d_sumcnt, rb ? *rb : ReadBack{}, st_);
+    launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, rb ? *rb : ReadBack{}, st_);
     return 0;
 }
 
@@ -363,7 +369,7 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
     J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
     J.nj = 3;
     J.total = d_scal;
-    launch_sum_multi_fused(J, d_part, kSpRedParts, d_sumcnt, ReadBack{}, st_);
+    launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
     int rc;
     if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_);
