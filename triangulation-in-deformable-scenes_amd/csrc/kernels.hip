@@ -24,6 +24,7 @@
 #include "diag_panel.h"
 #include "kernels.h"
 #include "symbolic.h"
+#include "ticket.h"
 
 namespace deftri {
 namespace dev {
@@ -1498,7 +1499,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_partial(const SumJobs J, doub
 // workgroup publishes its partial with an agent-scope atomic store and takes a ticket; the last one
 // forms the totals from the partials (agent-scope loads) and, when rb.h_scal is set, also does
 // k_trial_readback's copies into pinned host memory.  *cnt is 0 between launches.
-__global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt,
+__global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt, int flat,
                                                          const ReadBack rb) {
     const SumJob &jb = J.j[blockIdx.y];
     __shared__ double red[256];
@@ -1525,7 +1526,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_s_waitcnt(0);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1;
+        last = ticket_last(cnt, nblk, (int)(blockIdx.y * gridDim.x + blockIdx.x), flat != 0);
     }
     __syncthreads();
     if (!last) return;
@@ -1561,7 +1562,6 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
         if (t == 0) *rb.h_flag = *rb.flag;
         if (rb.rec && t < rb.nrec) rb.h_rec[t] = rb.rec[t];
     }
-    if (threadIdx.x == 0) *cnt = 0;
 }
 
 __global__ void k_sum_multi_final(const SumJobs J, int nparts, const double *__restrict__ part) {
@@ -2026,7 +2026,8 @@ void launch_lin_chi(const DevProblem &P, hipStream_t st) {
 
 void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st) {
     if (J.nj <= 0) return;
-    LAUNCH("sum_fused", dev::k_sum_multi_fused, dim3(nparts, J.nj), dim3(256), st, J, part, cnt, rb);
+    LAUNCH("sum_fused", dev::k_sum_multi_fused, dim3(nparts, J.nj), dim3(256), st, J, part, cnt,
+           flat_ticket() ? 1 : 0, rb);
 }
 
 void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st) {

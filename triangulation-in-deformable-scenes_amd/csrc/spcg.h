@@ -148,7 +148,7 @@ struct SpDev {
     double *hbuf = nullptr;                               // [pq_rows, heavy sums (hd)]
     double *red = nullptr;                                // [max_it + 2][kSpRed]: rz, rr, -, alpha
     double *rec = nullptr;                                // [8]: status, its
-    int *cnt = nullptr;                                   // [4] last-workgroup counters (0 between launches)
+    int *cnt = nullptr;                                   // [48] last-workgroup tickets, 16 per site (0 between launches)
     // k_sp_glin_heavy chunks: chunk j sums hv_blk[ch_lo[j] .. ch_lo[j + 1]) of heavy ch_h[j]; heavy h
     // owns chunks hch_off[h] .. hch_off[h + 1] (at least one); chpart [nch][27]; hcnt per heavy
     int32_t nch = 0;
@@ -158,6 +158,7 @@ struct SpDev {
     int *hcnt = nullptr;
     int32_t fuse = 0;                                     // one rank: dots in the update's / setup's last workgroup
     int32_t fuse_heavy = 0;                               // ... and k_sp_heavy in k_sp_phase2's last workgroup
+    int32_t flat_ticket = 0;                              // single-counter last-workgroup ticket (A/B)
     int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
     double tol2 = 0;

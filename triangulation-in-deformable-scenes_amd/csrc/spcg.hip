@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "spcg.h"
+#include "ticket.h"
 
 namespace deftri {
 namespace sp {
@@ -515,7 +516,7 @@ __device__ __forceinline__ bool last_block(const SpDev &G, int *cnt) {
             __builtin_amdgcn_s_waitcnt(0);         // the published stores acknowledged
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
         }
-        last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+        last = ticket_last(cnt, (int)gridDim.x, (int)blockIdx.x, G.flat_ticket);
         if (last && G.fence) __threadfence();
     }
     __syncthreads();
@@ -642,12 +643,11 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
             out[1] = s1;
         }
     }
-    if (G.fuse && last_block(G, G.cnt + 2)) {
+    if (G.fuse && last_block(G, G.cnt + 32)) {
         // (a bad block recorded by any workgroup stops every later launch through rec[0], which the
         // next launch sees; the sums formed here are then never read)
         __syncthreads();
         if (t < 256) dots_block(G, 0, dred);
-        if (t == 0) G.cnt[2] = 0;
     }
 }
 
@@ -810,7 +810,6 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             heavy_sums_block(G, G.Q + G.S, red4, lds);
             __syncthreads();
             heavy_finish(G, it, lam, beta, red4);
-            if (threadIdx.x == 0) G.cnt[0] = 0;
         }
         return;
     }
@@ -894,7 +893,6 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         heavy_sums_block(G, G.Q + G.S, red4, lds);
         __syncthreads();
         heavy_finish(G, it, lam, beta, red4);
-        if (threadIdx.x == 0) G.cnt[0] = 0;
     }
 }
 
@@ -1016,11 +1014,10 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
             out[1] = s1;
         }
     }
-    if (G.fuse && last_block(G, G.cnt + 1)) {
+    if (G.fuse && last_block(G, G.cnt + 16)) {
         // k_sp_dots of iteration it + 1, in the last workgroup (its first 256 threads)
         __syncthreads();
         if (t < 256) dots_block(G, it + 1, dred);
-        if (t == 0) G.cnt[1] = 0;
     }
 }
 

@@ -26,6 +26,7 @@
 #include <limits>
 
 #include "spcg.h"
+#include "ticket.h"
 
 namespace deftri {
 
@@ -241,6 +242,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.fuse_heavy = (G.fuse && heavy_parts <= kSpFuseHeavyMax && Q + S <= 64) ? 1 : 0;
         static const bool fence = std::getenv("DEFTRI_SP_FENCE") != nullptr;
         G.fence = fence ? 1 : 0;
+        G.flat_ticket = flat_ticket() ? 1 : 0;
     }
     {
         int32_t *rm, *pm, *pi;
@@ -265,8 +267,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
-    ALLOC(G.cnt, 4);
-    SPOK(hipMemset(G.cnt, 0, 4 * sizeof(int)));
+    ALLOC(G.cnt, 48);                                      // three ticket sites, 16 counters each
+    SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
     {
         // heavy linearization chunks (k_sp_glin_heavy): kSpHeavyChunk block partials each, >= 1 per vertex
         std::vector<int32_t> chh, hcho(Q + S + 1, 0);
@@ -295,9 +297,9 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
     SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
     SPOK(hipMemset(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (kSpMaxIt + 2))));
-    ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1); ALLOC(d_sumcnt, 1);
+    ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1); ALLOC(d_sumcnt, 16);
     SPOK(hipMemset(d_flag, 0, sizeof(int)));
-    SPOK(hipMemset(d_sumcnt, 0, sizeof(int)));
+    SPOK(hipMemset(d_sumcnt, 0, 16 * sizeof(int)));
     ALLOC(d_tmp, G.ndof); ALLOC(d_dx0, G.ndof);
     PUT(d_row_of_point, H.row_of_point);
     // halo lists: per peer, sends then receives, 6 doubles per row ((z, p) of 3 dofs)
