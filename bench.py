@@ -339,7 +339,10 @@ def product_roofline(stats, rep, ctx, rank):
         by, ms = p1["bytes"] + p2["bytes"], p1["ms"] + p2["ms"]
         gbs = by / max(ms * 1e-3, 1e-12) / 1e9
         cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update") if k in stats)
-        out = {"bound": "hbm", "kernel": "k_sp_phase1+k_sp_phase2 (matrix-free product)", "achieved": round(gbs, 1),
+        merged = "sp_update" not in stats
+        kname = ("k_sp_phase1+k_sp_phase2 (merged CG iteration: matrix-free product + p.Ap row terms + update)"
+                 if merged else "k_sp_phase1+k_sp_phase2 (matrix-free product)")
+        out = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
                 "traffic_unit": "bytes per product", "bytes_per_launch": by / its, "launches": its,
                 "avg_active_launch_us": round(1e3 * ms / its, 3),

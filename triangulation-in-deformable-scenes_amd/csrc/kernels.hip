@@ -587,11 +587,10 @@ __global__ void __launch_bounds__(256) k_ea(int ntask, const int32_t *__restrict
 // hanging.
 constexpr int kSpinLimit = 1 << 22;
 __device__ __forceinline__ void st_coherent(double *p, double v) {
-    __hip_atomic_store((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    st_sc1((unsigned long long *)p, __builtin_bit_cast(unsigned long long, v));
 }
 __device__ __forceinline__ double ld_coherent(const double *p) {
-    return __builtin_bit_cast(double, __hip_atomic_load((unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return __builtin_bit_cast(double, ld_sc1((unsigned long long *)p));
 }
 // W[k][c] = Linv[c][k] / d_c from the factored block in LDS (X[c][k] at S[k][c], D at S[c][c]) —
 // the products k_trsm forms from the stored inverse and the front's diagonal
@@ -605,12 +604,12 @@ __device__ __forceinline__ void publish_panel(const double (*S)[DP], int kb, dou
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): this thread's W stores are complete
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(pf, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) st_sc1(pf, epoch);
 }
 __device__ __forceinline__ void wait_panel(const int *pf, int epoch, int *flag) {
     if (threadIdx.x == 0) {
         int it = 0;
-        while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        while (ld_sc1(pf) != epoch) {
             if (++it > kSpinLimit) { atomicOr(flag, kStatusWaitTimeout); break; }
             __builtin_amdgcn_s_sleep(2);
         }
@@ -1239,7 +1238,7 @@ __global__ void __launch_bounds__(256) k_bwd_step(int ntask, const int32_t *__re
 __device__ __forceinline__ void poll_flag(const int *pf, int epoch, int *flag) {
     if (threadIdx.x == 0) {
         int it = 0;
-        while (__hip_atomic_load(pf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        while (ld_sc1(pf) != epoch) {
             if (++it > kSpinLimit) { atomicOr(flag, kStatusWaitTimeout); break; }
             __builtin_amdgcn_s_sleep(1);
         }
@@ -1249,7 +1248,7 @@ __device__ __forceinline__ void poll_flag(const int *pf, int epoch, int *flag) {
 __device__ __forceinline__ void raise_flag(int *pf, int epoch) {
     __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0): this thread's coherent stores are complete
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(pf, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) st_sc1(pf, epoch);
 }
 
 // forward: task (front f, rows r0..r0+63).  Panels k0 < min(r0, s): wait for y_k0, v_rows -= L y;
@@ -1521,8 +1520,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
     }
     const int nparts = gridDim.x, nblk = gridDim.x * gridDim.y;
     if (threadIdx.x == 0) {
-        __hip_atomic_store(part + (int64_t)blockIdx.y * gridDim.x + blockIdx.x, red[0], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        st_sc1(part + (int64_t)blockIdx.y * gridDim.x + blockIdx.x, red[0]);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_s_waitcnt(0);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -1539,12 +1537,12 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
             double v[8];
 #pragma unroll
             for (int u = 0; u < 8; u++)
-                v[u] = __hip_atomic_load(part + (int64_t)w * nparts + i + 64 * u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[u] = ld_sc1(part + (int64_t)w * nparts + i + 64 * u);
 #pragma unroll
             for (int u = 0; u < 8; u++) a += v[u];
         }
         for (; i < nparts; i += 64)
-            a += __hip_atomic_load(part + (int64_t)w * nparts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a += ld_sc1(part + (int64_t)w * nparts + i);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
         if (lane == 0) {

@@ -46,6 +46,7 @@ constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per he
 constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one thread per dof)
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
+constexpr int64_t kSpMergeMinDof = 50000;  // one rank: the merged (two-launch) CG chain from this many unknowns
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0)
 enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4 };
@@ -158,6 +159,19 @@ struct SpDev {
     int *hcnt = nullptr;
     int32_t fuse = 0;                                     // one rank: dots in the update's / setup's last workgroup
     int32_t fuse_heavy = 0;                               // ... and k_sp_heavy in k_sp_phase2's last workgroup
+    // one rank, two launches per CG iteration (merged chain): phase 1 also forms p.Ap (alpha in its
+    // last workgroup), phase 2 also updates x, r, z and forms (r.z, r.r) of the next iteration
+    int32_t merged = 0;
+    int32_t m_nx = 0;                                     // phase 1's extra workgroups (heavy p + row terms), 8k
+    int32_t m_nh = 0;                                     // phase 2's heavy workgroups, 8k
+    double *ph = nullptr;                                 // p of the heavy dofs this iteration (phase 1 -> 2)
+    double *m1part = nullptr;                             // phase-1 p.Ap per workgroup [m1n = m_nx + nblk]
+    int32_t m1n = 0;
+    double *apub = nullptr;                               // alpha published by phase 2's workgroup 0
+    int *aflag = nullptr;                                 // ... and the iteration it belongs to (-1 after setup)
+    int32_t alpha_kernel = 0;                             // alpha by k_sp_alpha between the phases (no hand-off)
+    double *m2part = nullptr;                             // phase-2 (r.z, r.r) per workgroup [m_nh + row grid][2]
+    double *gsum = nullptr;                               // per XCD group sums [2 sites][8][2]
     int32_t flat_ticket = 0;                              // single-counter last-workgroup ticket (A/B)
     int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
@@ -173,6 +187,8 @@ void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st);
+int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
+int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
@@ -204,14 +220,21 @@ class SpSolver {
     int profile_trial(double lambda, KProf &prof, bool analytic);
     int vertex_owner(int32_t *owner, int64_t nv) const;
     int64_t ndof() const { return G.ndof; }
-    double product_bytes() const { return H.product_bytes; }
-    double product_bytes_phase(int k) const { return k == 1 ? H.phase1_bytes : H.phase2_bytes; }
+    // algorithmic bytes per CG iteration of phase 1 / 2; the merged chain adds its own work: phase 1
+    // the rows' p.(D + lambda)p terms ((z, p) and D in) and the heavy p (in, out), phase 2 the update
+    // (x, r in / out and M in per row, q no longer stored)
+    double product_bytes_phase(int k) const {
+        if (k == 1) return H.phase1_bytes + (G.merged ? (double)G.nown * (48 + 48) + (double)G.hd * (16 + 8) : 0.0);
+        return H.phase2_bytes + (G.merged ? (double)G.nown * (24 + 24 + 24 + 24 + 48 - 24) : 0.0);
+    }
+    double product_bytes() const { return product_bytes_phase(1) + product_bytes_phase(2); }
     int64_t halo_rows() const { return H.halo_rows; }
     int32_t own_rows() const { return H.hi - H.lo; }
     int32_t n_blocks() const { return G.nblk; }
     int32_t n_row_blocks() const { return G.nrb; }
     int32_t n_arap_local() const { return (int32_t)H.arap_ids.size(); }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
+        if (G.merged) return G.alpha_kernel ? 3 : 2;
         const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;
         return (G.fuse ? 0 : 1) + (G.nblk > 0 ? 1 : 0) + 1 + heavy + 1;
     }

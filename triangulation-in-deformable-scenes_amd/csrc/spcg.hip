@@ -10,9 +10,10 @@
 //   k_sp_glin_blocks  per phase-1 block: the heavy vertices' H / b partials (owned edges only)
 //   k_sp_glin_heavy   heavy H / b from the block partials (rank sums; all-reduced by the host)
 // Per CG iteration it (sharded: 6 launches, two all-reduces and the halo exchange of the boundary
-// rows' (z, p); one rank: 3 launches — k_sp_dots runs in the last workgroup of the update before it
-// (or of the setup), and k_sp_heavy in the last workgroup of k_sp_phase2 when the heavy vertices
-// have few block partials (G.fuse_heavy)):
+// rows' (z, p); one rank, merged chain (default): 2 launches — phase 1 also forms p.Ap and alpha,
+// phase 2 also the update and the next (r.z, r.r); one rank, DEFTRI_SP_NO_MERGE=1: 3 launches —
+// k_sp_dots runs in the last workgroup of the update before it (or of the setup), and k_sp_heavy in
+// the last workgroup of k_sp_phase2 when the heavy vertices have few block partials (G.fuse_heavy)):
 //   k_sp_dots    (r.z, r.r) from the previous update's row-block partials
 //   k_sp_phase1  per local ARAP edge s_e = W_e J_e p, per block J_T^T s (T_g) / depth-scale sums
 //   k_sp_phase2  per own row q_v (p formed from (z, p_prev) on the fly and stored), partial p.q
@@ -28,58 +29,13 @@
 
 #include "spcg.h"
 #include "ticket.h"
+#include "wave.h"
 
 namespace deftri {
 namespace sp {
 
-// xor butterflies over the 64 lanes without LDS: lane ^ 1 and ^ 2 by DPP quad_perm, ^ 4 and ^ 8 by
-// row_half_mirror / row_mirror (equivalent once the quads / half-rows are uniform), ^ 16 and ^ 32
-// by v_permlane16_swap / v_permlane32_swap.  Every lane ends with the same value (each step adds
-// the same two operands on both lanes of a pair).
-template <int CTRL>
-__device__ __forceinline__ double dpp(double v) {      // the 64-bit value as two 32-bit DPP moves
-    int2 p = __builtin_bit_cast(int2, v);
-    p.x = __builtin_amdgcn_update_dpp(0, p.x, CTRL, 0xf, 0xf, true);     // every lane has a source
-    p.y = __builtin_amdgcn_update_dpp(0, p.y, CTRL, 0xf, 0xf, true);
-    return __builtin_bit_cast(double, p);
-}
-__device__ __forceinline__ void swap16(double v, double &a, double &b) {   // a: rows (0,0,2,2), b: rows (1,1,3,3)
-    const int2 p = __builtin_bit_cast(int2, v);
-    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)p.x, (unsigned)p.x, false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)p.y, (unsigned)p.y, false, false);
-    a = __builtin_bit_cast(double, make_int2((int)lo[0], (int)hi[0]));
-    b = __builtin_bit_cast(double, make_int2((int)lo[1], (int)hi[1]));
-}
-__device__ __forceinline__ void swap32(double v, double &a, double &b) {   // a: rows (0,1,0,1), b: rows (2,3,2,3)
-    const int2 p = __builtin_bit_cast(int2, v);
-    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)p.x, (unsigned)p.x, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)p.y, (unsigned)p.y, false, false);
-    a = __builtin_bit_cast(double, make_int2((int)lo[0], (int)hi[0]));
-    b = __builtin_bit_cast(double, make_int2((int)lo[1], (int)hi[1]));
-}
-__device__ __forceinline__ double wave_sum(double v) {
-    v += dpp<0xB1>(v);      // quad_perm [1,0,3,2]
-    v += dpp<0x4E>(v);      // quad_perm [2,3,0,1]
-    v += dpp<0x141>(v);     // row_half_mirror
-    v += dpp<0x140>(v);     // row_mirror
-    double a, b;
-    swap16(v, a, b);
-    v = a + b;
-    swap32(v, a, b);
-    return a + b;
-}
-
-__device__ __forceinline__ double wave_max(double v) {
-    v = fmax(v, dpp<0xB1>(v));
-    v = fmax(v, dpp<0x4E>(v));
-    v = fmax(v, dpp<0x141>(v));
-    v = fmax(v, dpp<0x140>(v));
-    double a, b;
-    swap16(v, a, b);
-    v = fmax(a, b);
-    swap32(v, a, b);
-    return fmax(a, b);
-}
+using wv::wave_sum;
+using wv::wave_max;
 
 // fixed-order sum of a 256-thread workgroup: wave butterflies, then (w0 + w1) + (w2 + w3)
 __device__ __forceinline__ double block_sum(double v, double *red4) {
@@ -129,10 +85,10 @@ __device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q
 // __threadfence() instead (a whole-L2 write-back per workgroup on gfx950; kept for A/B).
 __device__ __forceinline__ void publish(const SpDev &G, double *p, double v) {
     if (G.fence) *p = v;
-    else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else st_sc1(p, v);
 }
 __device__ __forceinline__ double fetch(const double *p) {     // a partial published in this launch
-    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return ld_sc1(p);
 }
 
 // ---- per LM iteration -----------------------------------------------------------------------------
@@ -484,7 +440,9 @@ __device__ bool inv6(const double *Hl, double lam, double *Mo) {
     return true;
 }
 
-__device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out, const SpDev *pub = nullptr) {
+// pub: 0 plain stores; 1 partials for a last-workgroup hand-off (agent-scope stores; callers pass 0
+// under G.fence)
+__device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out, int pub = 0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     a0 = wave_sum(a0);
     a1 = wave_sum(a1);
@@ -493,12 +451,9 @@ __device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4]
     if (threadIdx.x == 0) {
         const double s0 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
         const double s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
-        if (pub) {             // partials for a last-workgroup hand-off (publish)
-            if (pub->fence) { out[0] = s0; out[1] = s1; }
-            else {
-                __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+        if (pub == 1) {        // partials for a last-workgroup hand-off (publish)
+            st_sc1(out, s0);
+            st_sc1(out + 1, s1);
         } else {
             out[0] = s0;
             out[1] = s1;
@@ -521,6 +476,66 @@ __device__ __forceinline__ bool last_block(const SpDev &G, int *cnt) {
     }
     __syncthreads();
     return last;
+}
+
+// Merged chain: a two-level fixed-order sum of NV doubles per workgroup (slot = blockIdx.x), the
+// hand-off split by XCD group.  Every thread calls it after thread 0 published its workgroup's values
+// at slots[NV * blockIdx.x].  The last workgroup of group x = blockIdx % 8 adds the group's slots
+// (thread t those at x + 8 (t + 256 k), in k order; the threads in the block_sum order), publishes
+// the group's sums into gs[NV * x] and takes a ticket on the top counter; the last of those adds the
+// group sums in group order.  True in that workgroup, with tot[0 .. NV) set in thread 0.
+template <int NV>
+__device__ bool group_sum(const SpDev &G, int *cnt, const double *slots, double *gs, double (*red)[4], double *tot) {
+    __shared__ int flag;
+    const int nb = (int)gridDim.x, x = (int)blockIdx.x & 7;
+    const int gsize = (nb - x + 7) >> 3, ngroups = nb < 8 ? nb : 8;
+    auto settle = [&] {                  // this thread's published stores acknowledged
+        if (G.fence) __threadfence();
+        else {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        }
+    };
+    if (threadIdx.x == 0) {
+        settle();
+        flag = __hip_atomic_fetch_add(cnt + 1 + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+        if (flag && G.fence) __threadfence();
+    }
+    __syncthreads();
+    if (!flag) return false;
+    double a[NV];
+#pragma unroll
+    for (int v = 0; v < NV; v++) a[v] = 0.0;
+    for (int j = x + 8 * (int)threadIdx.x; j < nb; j += 8 * 256)
+#pragma unroll
+        for (int v = 0; v < NV; v++) a[v] += fetch(slots + NV * j + v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < NV; v++) {
+        a[v] = wave_sum(a[v]);
+        if (lane == 0) red[v][w] = a[v];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; v++) publish(G, gs + NV * x + v, (red[v][0] + red[v][1]) + (red[v][2] + red[v][3]));
+        cnt[1 + x] = 0;                  // the group is done: nobody else touches its counter
+        settle();
+        flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        if (flag) {
+            if (G.fence) __threadfence();
+            cnt[0] = 0;
+#pragma unroll
+            for (int v = 0; v < NV; v++) {
+                double t = 0.0;
+                for (int g = 0; g < ngroups; g++) t += fetch(gs + NV * g + v);
+                tot[v] = t;
+            }
+        }
+    }
+    __syncthreads();
+    return flag;
 }
 
 // (r.z, r.r) of iteration it from the row-block partials of the update before it (or the setup), in
@@ -552,6 +567,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
     // workgroup 0: the heavy dofs (dispatched first: their serial work overlaps the rows); row block
     // blockIdx - 1; partial slots as in k_sp_dots (rows 0..nrb-1, heavy nrb)
     const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
+    if (rb < 0 && t == 0 && G.merged) *G.aflag = -1;      // no iteration's alpha published yet
     if (rb >= 0) {
         const int l0 = rb * kSpUpdRows;
         const int nrow = min(kSpUpdRows, G.nown - l0);
@@ -636,8 +652,8 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
         double *out = G.upart + 2 * slot;
         if (G.fuse && !G.fence) {
-            __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st_sc1(out, s0);
+            st_sc1(out + 1, s1);
         } else {
             out[0] = s0;
             out[1] = s1;
@@ -656,6 +672,33 @@ __global__ void __launch_bounds__(256) k_sp_dots(int it, const SpDev G) {
     __shared__ double red[2][4];
     if (G.rec[0] != 0.0) return;
     dots_block(G, it, red);
+}
+
+// the sum of heavy vertex h's phase-1 block partials, component threadIdx.x (< its dim): thread
+// (g, c) = (tid / 8, tid % 8) adds component c of every 32nd block partial (8 lanes read one 64-byte
+// partial), then the 32 groups are added in order through LDS
+__device__ __forceinline__ double heavy_part_sum(const SpDev &G, int h, double *lds) {
+    const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
+    const int dim = h < G.Q ? 6 : 1;
+    const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
+    double acc = 0.0;
+    if (c < dim) {
+        int64_t k = k0 + g;
+        for (; k + 7 * 32 < k1; k += 8 * 32) {        // eight partials in flight, added in order
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = G.part[(int64_t)kSpPart * G.hv_blk[k + 32 * u] + c];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; k < k1; k += 32) acc += G.part[(int64_t)kSpPart * G.hv_blk[k] + c];
+    }
+    lds[threadIdx.x] = acc;
+    __syncthreads();
+    double t = 0.0;
+    if ((int)threadIdx.x < dim)
+        for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
+    return t;
 }
 
 // heavy sums of one heavy vertex h into hbuf[1 + its dofs] (h == Q + S: p.q of the rank's rows into
@@ -678,28 +721,9 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
         if (threadIdx.x == 0) publish(G, G.hbuf, a);
         return;
     }
-    const int64_t k0 = G.hv_blk_off[h], k1 = G.hv_blk_off[h + 1];
-    const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
-    const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
-    double acc = 0.0;
-    if (c < dim) {
-        int64_t k = k0 + g;
-        for (; k + 7 * 32 < k1; k += 8 * 32) {        // eight partials in flight, added in order
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = G.part[(int64_t)kSpPart * G.hv_blk[k + 32 * u] + c];
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc += v[u];
-        }
-        for (; k < k1; k += 32) acc += G.part[(int64_t)kSpPart * G.hv_blk[k] + c];
-    }
-    lds[threadIdx.x] = acc;
-    __syncthreads();
-    if ((int)threadIdx.x < dim) {
-        double t = 0.0;
-        for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
-        publish(G, G.hbuf + 1 + o + threadIdx.x, t);
-    }
+    const int o = heavy_dof(G, h);
+    const double t = heavy_part_sum(G, h, lds);
+    if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) publish(G, G.hbuf + 1 + o + threadIdx.x, t);
     __syncthreads();
 }
 
@@ -723,16 +747,118 @@ __device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam,
     }
 }
 
-template <class JT>
-__global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const JT *__restrict__ Jarap) {
-    __shared__ double red[6][4];
+// merged chain, phase 2: alpha of iteration it.  Workgroup 0 (dispatched first, waits on nothing)
+// sums phase 1's p.Ap partials in a fixed order, records alpha (NaN on breakdown, with the status)
+// and publishes it: the value with an agent-scope store, acknowledged, then the flag = it.  The
+// other workgroups call m2_alpha_wait where they first need alpha (after their sums): thread 0
+// polls the flag (bounded; a timeout stops the solve like a breakdown), the value goes through LDS.
+__device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish) {
+    __shared__ double sa;
+    double a = 0.0;
+    int j = threadIdx.x;
+    const int n = G.m1n;
+    for (; j + 3 * 256 < n; j += 4 * 256) {        // four partials in flight, added in order
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = G.m1part[j + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a += v[u];
+    }
+    for (; j < n; j += 256) a += G.m1part[j];
+    a = block_sum(a, red4);
+    if (threadIdx.x == 0) {
+        double alpha = G.red[(int64_t)kSpRed * it] / a;
+        if (!(a > 0.0) || !isfinite(alpha)) {
+            G.rec[0] = kSpBreakdown;
+            G.rec[1] = it;
+            alpha = __builtin_nan("");
+        }
+        G.red[(int64_t)kSpRed * it + 3] = alpha;
+        if (publish) {
+            st_sc1(G.apub, alpha);
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            __builtin_amdgcn_s_waitcnt(0);            // the value acknowledged before the flag
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            st_sc1(G.aflag, it);
+        }
+        sa = alpha;
+    }
+    __syncthreads();
+    return sa;
+}
+__device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
+    __shared__ double sa;
+    if (threadIdx.x == 0) {
+        int n = 0;
+        while (ld_sc1(G.aflag) != it && n < (1 << 22)) {
+            __builtin_amdgcn_s_sleep(2);
+            n++;
+        }
+        if (n >= (1 << 22)) {                          // never expected: stop the solve, skip the update
+            G.rec[0] = kSpBreakdown;
+            G.rec[1] = it;
+            sa = __builtin_nan("");
+        } else {
+            sa = ld_sc1(G.apub);
+        }
+    }
+    __syncthreads();
+    return sa;
+}
+
+// merged chain, G.alpha_kernel: alpha of iteration it in a one-workgroup launch between the phases
+__global__ void __launch_bounds__(256) k_sp_alpha(int it, const SpDev G) {
+    __shared__ double red4[4];
     double beta;
     if (it_state(G, it, beta)) return;
-    const int4 d = G.blk[blockIdx.x];
-    const int kind = d.x & 0xff, owned = d.x >> 8;
+    m2_alpha_make(G, it, red4, false);
+}
+
+// MG (merged chain, one rank): also p.Ap = sum_e s_e (J_e p) + sum_dep p_s (2 c_e . p_v + W J_s^2 p_s)
+// + sum_v p_v . (D_v + lam) p_v + lam |p_h|^2 per workgroup — the first m_nx workgroups do the heavy
+// dofs (p_h stored for phase 2) and the row terms, 256 rows each — and alpha in the last workgroup
+template <class JT, bool MG>
+__global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
+    __shared__ double red[7][4];
+    double beta;
+    if (it_state(G, it, beta)) return;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if constexpr (MG) {
+        double pap = 0.0;
+        const int e = (int)blockIdx.x;
+        if (e < G.m_nx) {
+            if (e == 0) {
+                for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
+                    const double p = pval(G.zp, beta, dd);
+                    G.ph[dd] = p;
+                    pap += lam * (p * p);
+                }
+            } else if (e - 1 < G.nrb) {
+                const int l = (e - 1) * 256 + (int)threadIdx.x;
+                if (l < G.nown) {
+                    const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+                    double p[3], D[6];
+#pragma unroll
+                    for (int c = 0; c < 3; c++) p[c] = pval(G.zp, beta, o + c);
+#pragma unroll
+                    for (int k = 0; k < 6; k++) D[k] = G.Dv[6 * (int64_t)l + k];
+                    const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
+                    const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
+                    const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+                    pap = (p[0] * q0 + p[1] * q1) + p[2] * q2;
+                }
+            }
+            pap = block_sum(pap, red[0]);
+            if (threadIdx.x == 0) G.m1part[blockIdx.x] = pap;
+            return;
+        }
+    }
+    const int b = MG ? (int)blockIdx.x - G.m_nx : (int)blockIdx.x;
+    const int4 d = G.blk[b];
+    const int kind = d.x & 0xff, owned = d.x >> 8;
     const int i = d.z + threadIdx.x;
-    double *out = G.part + (int64_t)kSpPart * blockIdx.x;
+    double *out = G.part + (int64_t)kSpPart * b;
+    double pap = 0.0;
     if (kind == SP_ARAP) {
         double acc[6] = {0, 0, 0, 0, 0, 0};
         if (i < d.w) {
@@ -753,20 +879,27 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
             for (int c = 0; c < 6; c++) t += J[12 + c] * pval(G.zp, beta, oT + c);
             const double s = G.Wa[i] * t;
             G.s[i] = s;
+            if (MG) pap = s * t;
             if (owned)
 #pragma unroll
                 for (int c = 0; c < 6; c++) acc[c] = J[12 + c] * s;
         }
-        if (!owned) return;
+        if (!MG && !owned) return;           // (MG: one rank, every edge owned)
 #pragma unroll
         for (int c = 0; c < 6; c++) {
             const double v = wave_sum(acc[c]);
             if (lane == 0) red[c][w] = v;
         }
+        if (MG) {
+            pap = wave_sum(pap);
+            if (lane == 0) red[6][w] = pap;
+        }
         __syncthreads();
-        if (threadIdx.x < 6) {
+        if (threadIdx.x < (MG ? 7 : 6)) {
             const int c = threadIdx.x;
-            out[c] = (red[c][0] + red[c][1]) + (red[c][2] + red[c][3]);
+            const double v = (red[c][0] + red[c][1]) + (red[c][2] + red[c][3]);
+            if (c < 6) out[c] = v;
+            else G.m1part[blockIdx.x] = v;
         }
     } else {
         double t = 0.0;
@@ -774,13 +907,30 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
             const int le = G.dperm[i];
             const int64_t o = G.hd + 3 * (int64_t)G.drow[le];
             const double *c = G.cdep + 3 * (int64_t)le;
-            t = (c[0] * pval(G.zp, beta, o) + c[1] * pval(G.zp, beta, o + 1)) + c[2] * pval(G.zp, beta, o + 2);
-            t += G.wss[le] * pval(G.zp, beta, 6 * (int64_t)G.Q + d.y);
+            const double cp = (c[0] * pval(G.zp, beta, o) + c[1] * pval(G.zp, beta, o + 1)) + c[2] * pval(G.zp, beta, o + 2);
+            const double ps = pval(G.zp, beta, 6 * (int64_t)G.Q + d.y);
+            t = cp + G.wss[le] * ps;
+            if (MG) pap = ps * (cp + t);
         }
         t = wave_sum(t);
         if (lane == 0) red[0][w] = t;
+        if (MG) {
+            pap = wave_sum(pap);
+            if (lane == 0) red[6][w] = pap;
+        }
         __syncthreads();
         if (threadIdx.x == 0) out[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        if (MG && threadIdx.x == 6) G.m1part[blockIdx.x] = (red[6][0] + red[6][1]) + (red[6][2] + red[6][3]);
+    }
+}
+
+// merged chain, phase 2: after every workgroup published its (r.z, r.r) partial, the last one forms
+// those of iteration it + 1
+__device__ __forceinline__ void m2_dots(const SpDev &G, int it, double (*red)[4]) {
+    double tot[2];
+    if (group_sum<2>(G, G.cnt, G.m2part, G.gsum + 16, red, tot) && threadIdx.x == 0) {
+        G.red[(int64_t)kSpRed * (it + 1)] = tot[0];
+        G.red[(int64_t)kSpRed * (it + 1) + 1] = tot[1];
     }
 }
 
@@ -788,21 +938,41 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
 // s_e (ARAP) or p of the depth edge's scale; then the row's own terms
 // at most 4 waves per SIMD: the registers go to gathers in flight (a C2-size grid has ~3 waves per
 // SIMD to hide their latency with)
-template <class JT>
+// MG (merged chain, one rank): the update of iteration it follows in the same thread — x += alpha p,
+// r -= alpha q, z = M r, (z, p) stored (q never is) — and the (r.z, r.r) of iteration it + 1 are
+// formed by the last workgroup; the first m_nh workgroups do the heavy vertices (their sums, q, update)
+template <class JT, bool MG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4)))
 k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     double beta;
     if (const int st = it_state(G, it, beta)) {
         // with the heavy finish folded in here, k_sp_heavy's record of the first stopped iteration too
-        if (G.fuse_heavy && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
+        if ((MG || G.fuse_heavy) && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
             G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
             G.rec[1] = it;
         }
         return;
     }
-    const int nhx = G.fuse_heavy ? G.Q + G.S : 0;
-    if ((int)blockIdx.x < nhx) {
+    double alpha = 0.0;
+    double pq = 0.0, rr2 = 0.0;                             // (MG: r.z and r.r)
+    bool rows = true;
+    int hv = -1;                                            // MG: the heavy vertex of this workgroup
+    double th = 0.0;                                        // ... its component sum (thread < dim)
+    if constexpr (MG) {
+        if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];     // k_sp_alpha's
+        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true);
+        if ((int)blockIdx.x < G.m_nh) {
+            rows = false;
+            if ((int)blockIdx.x < G.Q + G.S) {
+                __shared__ double lds[256];
+                hv = blockIdx.x;
+                th = heavy_part_sum(G, hv, lds);
+            }
+        }
+    }
+    const int nhx = MG ? G.m_nh : G.fuse_heavy ? G.Q + G.S : 0;
+    if (!MG && (int)blockIdx.x < nhx) {
         // the heavy vertices' sums (phase-1 partials only): dispatched first, concurrent with the rows
         __shared__ double lds[256];
         heavy_sums_block(G, blockIdx.x, red4, lds);
@@ -813,10 +983,13 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    const int lb = row_block(blockIdx.x - nhx, G.nrb);
+    const int lb = rows ? row_block(blockIdx.x - nhx, G.nrb) : 0;
     const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    double pq = 0.0;
-    if (w < G.nwaves) {
+    // MG: the row's values for the update after alpha arrives (lrow >= 0: this lane has a row)
+    int lrow = -1;
+    int64_t orow = 0;
+    double pr[3] = {0, 0, 0}, qr[3] = {0, 0, 0}, xo[3] = {0, 0, 0}, ro[3] = {0, 0, 0}, M[6] = {0, 0, 0, 0, 0, 0};
+    if (rows && w < G.nwaves) {
         const int l = G.rowmap[64 * w + lane];
         const int64_t n = G.nslots * 64;
         const JT *pjx = pj, *pjy = pj + n, *pjz = pj + 2 * n;
@@ -829,10 +1002,15 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         // are a handful of cache lines)
         const double *__restrict__ sv_ = G.s;
         const double2 *__restrict__ zp_ = G.zp;
+        const double *__restrict__ ph_ = G.ph;
         auto val = [&](int v) -> double {
             const double a = sv_[max(v, 0)];
-            const double2 z = zp_[os + max(-2 - v, 0)];
-            const double p = __fma_rn(beta, z.y, z.x);
+            double p;
+            if constexpr (MG) p = ph_[os + max(-2 - v, 0)];     // (the heavy workgroups rewrite zp)
+            else {
+                const double2 z = zp_[os + max(-2 - v, 0)];
+                p = __fma_rn(beta, z.y, z.x);
+            }
             return v >= 0 ? a : (v <= -2 ? p : 0.0);
         };
         // U slots per step: their indices, then the values and J slices, then the adds in order
@@ -869,18 +1047,87 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             for (int c = 0; c < 3; c++) v[c] = G.zp[o + c];
 #pragma unroll
             for (int k = 0; k < 6; k++) D[k] = G.Dv[6 * (int64_t)l + k];
+            if constexpr (MG) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) { xo[c] = G.x[o + c]; ro[c] = G.r[o + c]; }
+#pragma unroll
+                for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
+            }
 #pragma unroll
             for (int c = 0; c < 3; c++) p[c] = __fma_rn(beta, v[c].y, v[c].x);
             q[0] += lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
             q[1] += lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
             q[2] += lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+            if constexpr (MG) {
+                lrow = l;
+                orow = o;
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                G.zp[o + c] = make_double2(v[c].x, p[c]);
-                G.q[o + c] = q[c];
-                pq += p[c] * q[c];
+                for (int c = 0; c < 3; c++) { pr[c] = p[c]; qr[c] = q[c]; }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    G.zp[o + c] = make_double2(v[c].x, p[c]);
+                    G.q[o + c] = q[c];
+                    pq += p[c] * q[c];
+                }
             }
         }
+    }
+    if constexpr (MG) {
+        if (!G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (hv >= 0) {
+            // thread a < dim: component a of the vertex (k_sp_update's heavy arithmetic; r through
+            // LDS, so no private arrays); its (r.z, r.r) terms added in component order
+            __shared__ double rs[6], tz[2][6];
+            const int h = hv, dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+            const int a = isnan(alpha) ? dim : (int)threadIdx.x;     // breakdown: no update
+            double p = 0.0, r = 0.0;
+            if (a < dim) {
+                p = G.ph[o + a];
+                const double q = th + lam * p;
+                G.x[o + a] += alpha * p;
+                r = G.r[o + a] - alpha * q;
+                G.r[o + a] = r;
+                rs[a] = r;
+            }
+            __syncthreads();
+            if (a < dim) {
+                const double *Mh = h < G.Q ? G.Mh + 36 * (int64_t)h + a * 6 : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+                double z = 0.0;
+                for (int c = 0; c < dim; c++) z += Mh[c] * rs[c];
+                G.zp[o + a] = make_double2(z, p);
+                tz[0][a] = r * z;
+                tz[1][a] = r * r;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0 && !isnan(alpha))
+                for (int c = 0; c < dim; c++) { pq += tz[0][c]; rr2 += tz[1][c]; }
+        } else if (rows) {
+            if (lrow >= 0 && !isnan(alpha)) {
+                // k_sp_update's arithmetic for the row
+                const int64_t o = orow;
+                double r[3], z[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    G.x[o + c] = xo[c] + alpha * pr[c];
+                    r[c] = ro[c] - alpha * qr[c];
+                }
+                z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
+                z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
+                z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    G.r[o + c] = r[c];
+                    G.zp[o + c] = make_double2(z[c], pr[c]);
+                    pq += r[c] * z[c];              // (r.z, r.r) of iteration it + 1
+                    rr2 += r[c] * r[c];
+                }
+            }
+        }
+        __shared__ double red[2][4];
+        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);   // (kernel args never by address)
+        m2_dots(G, it, red);
+        return;
     }
     const double sm = block_sum(pq, red4);
     if (threadIdx.x == 0 && lb < max(G.nrb, 1)) {
@@ -1007,8 +1254,8 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
         double *out = G.upart + 2 * slot;
         if (G.fuse && !G.fence) {
-            __hip_atomic_store(out, s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(out + 1, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st_sc1(out, s0);
+            st_sc1(out + 1, s1);
         } else {
             out[0] = s0;
             out[1] = s1;
@@ -1093,15 +1340,29 @@ void sp_launch_dots(const SpDev &G, int it, hipStream_t st) {
 }
 
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st) {
-    if (G.nblk > 0) {
-        if (fp32) SPL("sp_phase1", sp::k_sp_phase1<float>, G.nblk, it, G, G.Ja32);
-        else SPL("sp_phase1", sp::k_sp_phase1<double>, G.nblk, it, G, G.Ja);
+    if (G.merged) {
+        // [m_nx heavy-p / row-term workgroups][phase-1 blocks]; [m_nh heavy workgroups][row blocks]
+        // (both extra counts multiples of 8, so the blocks keep their XCD)
+        const int g1 = sp_merged_grid1(G), g2 = sp_merged_grid2(G);
+        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, true>), g1, it, G, G.Ja32, lambda);
+        else SPL("sp_phase1", (sp::k_sp_phase1<double, true>), g1, it, G, G.Ja, lambda);
+        if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
+        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, true>), g2, it, G, lambda, (const float *)G.pj32);
+        else SPL("sp_phase2", (sp::k_sp_phase2<double, true>), g2, it, G, lambda, (const double *)G.pj);
+        return;
     }
-    // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) after the row blocks
+    if (G.nblk > 0) {
+        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, false>), G.nblk, it, G, G.Ja32, lambda);
+        else SPL("sp_phase1", (sp::k_sp_phase1<double, false>), G.nblk, it, G, G.Ja, lambda);
+    }
+    // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) before the row blocks
     const int grid = sp::row_grid(G.nrb) + (G.fuse_heavy ? G.Q + G.S : 0);
-    if (fp32) SPL("sp_phase2", sp::k_sp_phase2<float>, grid, it, G, lambda, (const float *)G.pj32);
-    else SPL("sp_phase2", sp::k_sp_phase2<double>, grid, it, G, lambda, (const double *)G.pj);
+    if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, false>), grid, it, G, lambda, (const float *)G.pj32);
+    else SPL("sp_phase2", (sp::k_sp_phase2<double, false>), grid, it, G, lambda, (const double *)G.pj);
 }
+
+int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }
+int sp_merged_grid2(const SpDev &G) { return 8 * ((G.Q + G.S + 7) / 8) + sp::row_grid(G.nrb); }
 
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {
     // stage 1 over one workgroup per heavy vertex when the vertices have many blocks

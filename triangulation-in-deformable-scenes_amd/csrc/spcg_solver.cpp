@@ -243,6 +243,18 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         static const bool fence = std::getenv("DEFTRI_SP_FENCE") != nullptr;
         G.fence = fence ? 1 : 0;
         G.flat_ticket = flat_ticket() ? 1 : 0;
+        // one rank, from kSpMergeMinDof unknowns: two launches per CG iteration (merged chain; alpha
+        // from p.Ap).  Smaller problems keep the three-launch chain (alpha from p.q): they are the
+        // badly conditioned ones here (thousands of CG iterations per step), where the two alpha
+        // formulas' rounding differences can move a solve past its budget, and a CG iteration costs
+        // microseconds either way.  DEFTRI_SP_NO_MERGE=1 / DEFTRI_SP_MERGE=1 force either chain.
+        static const bool no_merge = std::getenv("DEFTRI_SP_NO_MERGE") != nullptr;
+        static const bool force_merge = std::getenv("DEFTRI_SP_MERGE") != nullptr;
+        G.merged = (G.fuse && !no_merge && Q + S <= 4096 && (force_merge || G.ndof >= kSpMergeMinDof)) ? 1 : 0;
+        G.m_nx = 8 * ((G.nrb + 1 + 7) / 8);
+        G.m_nh = 8 * ((Q + S + 7) / 8);
+        static const bool ak = std::getenv("DEFTRI_SP_ALPHA_KERNEL") != nullptr;
+        G.alpha_kernel = ak ? 1 : 0;
     }
     {
         int32_t *rm, *pm, *pi;
@@ -267,6 +279,11 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
+    ALLOC(G.ph, std::max<int64_t>(H.hd, 1));
+    G.m1n = sp_merged_grid1(G);
+    ALLOC(G.m1part, G.m1n); ALLOC(G.m2part, 2 * (int64_t)sp_merged_grid2(G)); ALLOC(G.gsum, 32);
+    ALLOC(G.apub, 1); ALLOC(G.aflag, 1);
+    SPOK(hipMemset(G.aflag, 0xff, sizeof(int)));
     ALLOC(G.cnt, 48);                                      // three ticket sites, 16 counters each
     SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
     {
@@ -396,6 +413,10 @@ void SpSolver::cg_setup(double lambda, const double *rhs) {
 void SpSolver::cg_chain(double lambda, int from, int to) {
     const bool dist = nranks_ > 1;
     for (int it = from; it < to; it++) {
+        if (G.merged) {                                // phase 1 (+ alpha), phase 2 (+ update, next dots)
+            sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
+            continue;
+        }
         if (!G.fuse) sp_launch_dots(G, it, st_);      // fused: the previous update's (setup's) last workgroup
         if (dist) tr_->allreduce(G.red + (int64_t)kSpRed * it, 2, 0, st_);
         sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
