@@ -1508,7 +1508,32 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
     int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
     double acc = 0.0;
     const int mode = jb.mode;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    // k_sum_multi_partial's strided order (blockDim 256), eight (mode 0) / four elements' loads in
+    // flight per step, added in order
+    int64_t i = lo + threadIdx.x;
+    if (mode == 0) {
+        for (; i + 7 * 256 < hi; i += 8 * 256) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = jb.a[i + 256 * u];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+    } else {
+        for (; i + 3 * 256 < hi; i += 4 * 256) {
+            double v[4], bb[4], ww[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                v[u] = jb.a[i + 256 * u];
+                bb[u] = jb.b[i + 256 * u];
+                ww[u] = mode == 1 ? 1.0 : jb.w[i + 256 * u];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                acc += (mode == 1) ? v[u] * (jb.lambda * v[u] + bb[u]) : v[u] * (jb.lambda * ww[u] * v[u] + bb[u]);
+        }
+    }
+    for (; i < hi; i += 256) {
         double v = jb.a[i];
         acc += (mode == 0) ? v : (mode == 1) ? v * (jb.lambda * v + jb.b[i]) : v * (jb.lambda * jb.w[i] * v + jb.b[i]);
     }
