@@ -260,7 +260,9 @@ def test_sharded_iterative_matches_one_rank(kind, world):
     for r in range(world):
         info = out[r][0]
         assert info["plan"] == "iterative" and info["nranks"] == world and info["halo_rows"] > 0
-    for analytic, tol in ((True, 1e-8), (False, 1e-6)):
+    # (a sharded solve splits every sum differently: rounding-level step differences, which the CG's
+    # 1e-12 residual bar lets through at ~kappa * 1e-12 and the LM iterations amplify)
+    for analytic, tol in ((True, 3e-8), (False, 1e-6)):
         rr, pts, sc, tg = ref[analytic]
         for r in range(world):
             rep, P, S, T = out[r][1][analytic]

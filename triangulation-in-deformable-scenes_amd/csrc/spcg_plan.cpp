@@ -5,6 +5,7 @@
 // passes are O(E + P) counting sorts and scans, so a 500k x 8-keyframe graph (84M ARAP edges,
 // SURVEY §8d C4) plans in seconds; nothing here depends on a fill-reducing ordering.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -128,6 +129,30 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             cum += (double)rw[r];
         }
         for (; next < nranks; next++) H.rank_row_begin[next] = P;
+    }
+    // 4b. inside every rank's range, rows sorted by their phase-2 slot count (ARAP incidences + depth
+    //     couplings; descending, stable) in windows of kSpSortWindow rows: the order the phase-2 wave
+    //     layout deals them to lanes (8b), so that layout is the identity and a wave's 64 rows are 64
+    //     consecutive rows (the per-row vectors then load coalesced).  Every rank permutes every range
+    //     the same way, so the global numbering agrees across ranks.  (DEFTRI_SP_NO_ROWSORT=1: A/B)
+    static const bool no_rowsort = std::getenv("DEFTRI_SP_NO_ROWSORT") != nullptr;
+    if (!no_rowsort) {
+        std::vector<int32_t> cnt(P, 0);
+        for (int64_t e = 0; e < 4 * E; e++) cnt[row[ap[e]]]++;
+        for (int64_t e = 0; e < D; e++) cnt[row[d.dep_point[e]]]++;
+        std::vector<int32_t> np(P);
+        for (int rk = 0; rk < nranks; rk++) {
+            const int32_t a = H.rank_row_begin[rk], b = H.rank_row_begin[rk + 1];
+            for (int32_t w0 = a; w0 < b; w0 += kSpSortWindow) {
+                const int32_t w1 = std::min(b, w0 + kSpSortWindow);
+                std::vector<int32_t> ord(w1 - w0);
+                std::iota(ord.begin(), ord.end(), w0);
+                std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
+                for (int32_t k = 0; k < w1 - w0; k++) np[w0 + k] = H.point_of_row[ord[k]];
+            }
+        }
+        H.point_of_row = np;
+        for (int32_t r = 0; r < P; r++) H.row_of_point[np[r]] = r;
     }
     H.lo = H.rank_row_begin[rank];
     H.hi = H.rank_row_begin[rank + 1];
