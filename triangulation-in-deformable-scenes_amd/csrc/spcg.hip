@@ -1005,13 +1005,17 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         const double *__restrict__ ph_ = G.ph;
         auto val = [&](int v) -> double {
             const double a = sv_[max(v, 0)];
-            double p;
-            if constexpr (MG) p = ph_[os + max(-2 - v, 0)];     // (the heavy workgroups rewrite zp)
-            else {
+            if constexpr (MG) {
+                // p from phase 1's copy (the heavy workgroups rewrite zp); blended arithmetically (both
+                // terms finite, one factor 1 and one 0: exact) — with a select the compiler sinks this
+                // load into a per-slot branch that waits on every load in flight
+                const double p = ph_[os + max(-2 - v, 0)];
+                return a * (v >= 0 ? 1.0 : 0.0) + p * (v <= -2 ? 1.0 : 0.0);
+            } else {
                 const double2 z = zp_[os + max(-2 - v, 0)];
-                p = __fma_rn(beta, z.y, z.x);
+                const double p = __fma_rn(beta, z.y, z.x);
+                return v >= 0 ? a : (v <= -2 ? p : 0.0);
             }
-            return v >= 0 ? a : (v <= -2 ? p : 0.0);
         };
         // U slots per step: their indices, then the values and J slices, then the adds in order
         auto step = [&](auto U_) {
@@ -1020,10 +1024,28 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             double sv[U], J[U][3];
 #pragma unroll
             for (int u = 0; u < U; u++) v[u] = G.pidx[k + 64 * u];
+            if constexpr (MG) {
+                // every load of the step first (s_e, the scale's p, the J slice), the arithmetic after:
+                // one round trip per step instead of one per slot
+                double a[U], pp[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                sv[u] = val(v[u]);
-                J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                for (int u = 0; u < U; u++) {
+                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    a[u] = sv_[max(v[u], 0)];
+                    pp[u] = ph_[os + max(-2 - v[u], 0)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    sv[u] = a[u] * (v[u] >= 0 ? 1.0 : 0.0) + pp[u] * (v[u] <= -2 ? 1.0 : 0.0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    sv[u] = val(v[u]);
+                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; u++)
