@@ -172,8 +172,9 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
             wt = arap ? r.w : 0.0;
             er = arap ? r.x : 0.0;
         };
-        auto add = [&](int m, const double *v, double wt, double er) {
-            if (m < 0) return;
+        // branch-free: depth couplings and padding come with wt = er = 0 from value() and add exact
+        // zeros (a per-slot branch here made the compiler serialize the slots' loads)
+        auto add = [&](const double *v, double wt, double er) {
 #pragma unroll
             for (int a = 0; a < 3; a++) {
                 const double ja = v[a] * wt;
@@ -195,7 +196,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
             for (int u = 0; u < U; u++) {
                 double v[3], wt, er;
                 value(m[u], r[u], v, wt, er);
-                add(m[u], v, wt, er);
+                add(v, wt, er);
 #pragma unroll
                 for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
             }
@@ -207,7 +208,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
             const int m = G.pmap[k];
             double v[3], wt, er;
             value(m, load(m), v, wt, er);
-            add(m, v, wt, er);
+            add(v, wt, er);
 #pragma unroll
             for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
         }
