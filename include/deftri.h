@@ -253,9 +253,10 @@ typedef struct deftri_plan_info {
     int32_t phase1_blocks, row_blocks;
     double  product_bytes;     /* algorithmic bytes of one matrix-free product on this rank */
     int32_t jacobian_fp32;
-    int32_t cg_launches;       /* iterative: kernel launches per CG iteration (3 on one rank: the dots
-                                  and the heavy-vertex finish run in the last workgroup of the update /
-                                  product launches; 5-6 otherwise) */
+    int32_t cg_launches;       /* iterative: kernel launches per CG iteration (one rank from 50,000
+                                  unknowns: 2, the merged chain — phase 1 forms p.Ap, phase 2 the
+                                  update; one rank below that: 3, the dots and the heavy-vertex finish
+                                  in last workgroups; sharded: 5-6) */
 } deftri_plan_info;
 int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info);
 /* TEST ONLY (no GPU): host emulation of one product q = (H + lambda I) p with the iterative plan's
