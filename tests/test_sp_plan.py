@@ -111,3 +111,41 @@ def test_sharded_product_matches_direct(kind, world):
     assert covered.max() == 1                       # no point row produced by two ranks
     total[:hd] = ref[:hd]
     np.testing.assert_allclose(total, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("kind", ["mv", "tv"])
+def test_merged_chain_pAp_decomposition(kind):
+    """The merged CG chain divides by p.Ap summed the way k_sp_phase1<MG> sums it:
+    per ARAP edge s_e (J_e p) = W_e (J_e p)^2, per depth edge p_s (2 c_e . p_v + W J_s^2 p_s) with
+    c_e = W J_p J_s, per row p_v . (D_v + lambda) p_v with D_v the row's folded reprojection and depth
+    point blocks, and lambda |p_h|^2 on the heavy dofs.  In exact arithmetic that is p . q for the
+    q = (H + lambda I) p the three-launch chain divides by; here with random Jacobians and weights it
+    must agree to rounding (1e-12 relative)."""
+    p = _problem(kind)
+    Ja, Wa, Jr, Wr, Jd, Wd, x = _random_lin(p)
+    lam = 0.37
+    q = _reference(p, Ja, Wa, Jr, Wr, Jd, Wd, lam, x)
+    Q, S = p.n_pairs, p.n_scales
+    hd = 6 * Q + S
+    pt = lambda idx: hd + 3 * np.asarray(idx)[:, None] + np.arange(3)[None, :]
+    cols = np.concatenate([pt(p.arap_pts[:, k]) for k in range(4)] + [6 * p.arap_pair[:, None] + np.arange(6)[None, :]], 1)
+    t = np.einsum("ej,ej->e", Ja, x[cols])
+    arap = np.sum((Wa * t) * t)
+    # rows: D_v = sum over the row's reprojection edges J2^T W J2 + its depth edges W J_p J_p^T
+    npt = p.n_points
+    D = np.zeros((npt, 3, 3))
+    J2 = Jr.reshape(-1, 2, 3)
+    np.add.at(D, p.rep_point, np.einsum("eri,erj,e->eij", J2, J2, Wr))
+    Jp, Js = Jd[:, :3], Jd[:, 3]
+    np.add.at(D, p.dep_point, np.einsum("ei,ej,e->eij", Jp, Jp, Wd))
+    pv = x[hd:].reshape(-1, 3)
+    rows = np.sum(pv * (np.einsum("vij,vj->vi", D, pv) + lam * pv))
+    # depth couplings: p_s (2 c_e . p_v + W J_s^2 p_s)
+    ps = x[6 * Q + p.dep_scale]
+    cp = np.einsum("ei,ei->e", (Wd * Js)[:, None] * Jp, pv[p.dep_point])
+    dep = np.sum(ps * (2.0 * cp + (Js * Wd) * Js * ps))
+    heavy = lam * np.sum(x[:hd] ** 2)
+    pap = arap + rows + dep + heavy
+    pq = float(np.dot(x, q))
+    assert abs(pap - pq) <= 1e-12 * abs(pq)
+    assert pap > 0
