@@ -40,7 +40,9 @@ constexpr int kSpRecDoubles = 8;
 // workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
 // chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
 int sum_parts() {
-    static const int v = std::getenv("DEFTRI_SP_SUM_PARTS") ? std::atoi(std::getenv("DEFTRI_SP_SUM_PARTS")) : 128;
+    // C2 under rocprofv3 (profiles/r03sp_sum_parts.json): 64 parts 11.1 us, 128 12.9, 256 18.5, 512 27.9 —
+    // every workgroup's ticket costs more than its share of the sum saves
+    static const int v = std::getenv("DEFTRI_SP_SUM_PARTS") ? std::atoi(std::getenv("DEFTRI_SP_SUM_PARTS")) : 64;
     return std::max(1, std::min(v, kSpRedParts));
 }
 
