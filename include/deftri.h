@@ -206,11 +206,17 @@ int deftri_set_factor_precision(deftri_ctx *ctx, int32_t fp32_updates);
 /* Linear solver of the LM step (H + lambda I) dx = b inside deftri_solve_lm /
    deftri_arap_optimization (the reference: g2o BlockSolver + LinearSolverEigen, an exact sparse
    LDL^T).  DEFTRI_SOLVER_PCG (default): conjugate gradients preconditioned by the vertex blocks of
-   H + lambda I (6x6 T_g, 1x1 scale, 3x3 point), stopped at ||b - A dx|| <= tol ||b|| (tol <= 0:
-   1e-12), with the multifrontal LDL^T as the fallback for a solve that has not converged after
-   max_iterations or breaks down.  max_iterations <= 0: a budget of about one factorization's cost,
-   from the plan's sizes (deterministic per problem structure; ~70 at 100k correspondences, ~25 for
-   a few hundred points).  Single-rank contexts only (point-sharded contexts always factor).  DEFTRI_SOLVER_DIRECT: the multifrontal LDL^T for every trial. */
+   H + lambda I (6x6 T_g, 1x1 scale, 3x3 point), stopped when the CG recurrence's residual r_k
+   (not a recomputed b - A dx) satisfies ||r_k|| <= tol ||b|| (tol <= 0: 1e-12); the true residual
+   differs from r_k by rounding drift, which tests/test_full_size_props.py measures through
+   deftri_eval_hessian_product (< 1e-11 relative at C2).  What a solve that misses its budget or
+   breaks down does depends on the plan: the multifrontal plan hands it to its LDL^T (max_iterations
+   <= 0: a budget of about one factorization's cost, from the plan's sizes: ~70 at 100k
+   correspondences, ~25 for a few hundred points); the iterative plan has no factorization, and the
+   trial counts as a failed linear solve — g2o's rejected trial (lambda *= ni) — with a budget of
+   1000 iterations when max_iterations <= 0 (DEFTRI_PLAN_ITERATIVE below).  Point-sharded contexts
+   take PCG steps on the iterative plan by default and LDL^T steps on the sharded multifrontal plan
+   with DEFTRI_SOLVER_DIRECT.  DEFTRI_SOLVER_DIRECT: the multifrontal LDL^T for every trial. */
 #define DEFTRI_SOLVER_DIRECT 0
 #define DEFTRI_SOLVER_PCG    1
 int deftri_set_linear_solver(deftri_ctx *ctx, int32_t solver, double tol, int32_t max_iterations);
@@ -228,7 +234,12 @@ int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_
    blocks); sharded: one halo exchange of the boundary rows' (z, p) and two all-reduces (the dot
    products, the global-vertex partials) per CG iteration.  A step whose PCG does not converge within
    the budget (deftri_set_linear_solver max_iterations; <= 0: 1000) counts as a failed linear solve
-   (g2o: the trial is rejected).  Any keyframe count (all-pairs graphs, BASELINE C3-C5).
+   (g2o: the trial is rejected; no LDL^T stands behind it).  One rank from 50,000 unknowns: two
+   launches per CG iteration (the merged chain), whose alpha is handed from phase 2's workgroup 0 to
+   the others through a published value and a flag; this relies on the dispatcher starting a
+   launch's workgroups in index order (workgroup 0 resident while the others poll), which HIP does not
+   promise: the poll is bounded, and a timeout fails the call with DEFTRI_E_HIP (never a rejected
+   trial) and switches the context to a separate alpha launch for later calls.  Any keyframe count (all-pairs graphs, BASELINE C3-C5).
    DEFTRI_PLAN_AUTO (default): ITERATIVE when the step solver is DEFTRI_SOLVER_PCG at upload and the
    context is point-sharded (nranks > 1) or the problem has >= 50,000 unknowns (measured faster from
    C2 up); MULTIFRONTAL otherwise.  Applies to the next deftri_problem_upload.  A
@@ -330,7 +341,10 @@ int deftri_eval_chi2(deftri_ctx *ctx, double *chi2);
 /* Linearize at the current state and return b (gradient side, g2o sign: b = -J^T W e)
    in the vertex order [T_g(6) per pair][scales][points(3)], and the diagonal of H. */
 int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n);
-/* y = H x for the current linearization (same vertex order). */
+/* y = H x for the current linearization (same vertex order).  On the iterative plan: the CG
+   chain's own matrix-free product kernels (H is never assembled; analytic-Jacobian linearization,
+   as deftri_eval_damped_solve), so a solve's true residual ||b - (H + lambda I) x|| can be measured
+   at any size; on the multifrontal plan: the assembled blocks. */
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n);
 /* Solve (H + lambda I) x = rhs (analytic-Jacobian linearization at the current state) with the
    configured step solver (deftri_set_linear_solver: PCG with LDL^T fallback, or the LDL^T). */

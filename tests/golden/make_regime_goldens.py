@@ -13,8 +13,12 @@ criterion can fail.  Stored per regime: chi2 and trials per iteration, final lam
 points' fixed subsample (every 53rd) and coordinate sums, the initial and final RMSE.  The scenes are
 regenerated from their seeds by the tests (deterministic host code).
 
-Usage: python tests/golden/make_regime_goldens.py   (about 5 minutes of one core)
+Usage: python tests/golden/make_regime_goldens.py [regime ...]   (about 5 minutes of one core)
+       python tests/golden/make_regime_goldens.py --n-corr 30000 --seed 7 --dir regimes_30k simulation realcolon
+       (the 30k set: 90k unknowns, above the merged CG chain's threshold, so the timed plan's
+       two-launch chain is pinned; about 10 minutes per regime)
 """
+import argparse
 import copy
 import json
 import pathlib
@@ -38,19 +42,25 @@ REGIMES = {
 }
 
 
-def scene(name):
+def scene(name, n_corr=None, seed=None):
     r = REGIMES[name]
-    m, _ = sim.simulate_two_view(n=N_CORR, seed=SEED, kb8=getattr(sim, r["kb8"]), scale_scene=True, compact=True)
+    m, _ = sim.simulate_two_view(n=n_corr or N_CORR, seed=seed or SEED, kb8=getattr(sim, r["kb8"]), scale_scene=True, compact=True)
     host = capi.Context(-1)
     p = host.build_graph(m, r["rep"], r["arap"], np.float32(r["sigma"]))
     return p, m, host
 
 
 def main():
-    d = HERE / "regimes"
+    ap = argparse.ArgumentParser()
+    ap.add_argument("regimes", nargs="*")
+    ap.add_argument("--n-corr", type=int, default=N_CORR)
+    ap.add_argument("--seed", type=int, default=SEED)
+    ap.add_argument("--dir", default="regimes")
+    a = ap.parse_args()
+    d = HERE / a.dir
     d.mkdir(exist_ok=True)
-    for name in (sys.argv[1:] or REGIMES):
-        p, m, host = scene(name)
+    for name in (a.regimes or REGIMES):
+        p, m, host = scene(name, a.n_corr, a.seed)
         host.analyse(p)
         oracle.set_vertex_order(host.vertex_order())
         t = time.time()
@@ -65,7 +75,7 @@ def main():
         pts = res["points"]
         np.savez_compressed(d / f"{name}.npz", points_sub=pts[::STRIDE], chi2_iter=np.array(R["chi2_iter"]),
                             trials_iter=np.array(R["trials_iter"]))
-        meta = {"regime": name, **REGIMES[name], "n_corr": N_CORR, "seed": SEED, "n_iterations": N_IT,
+        meta = {"regime": name, **REGIMES[name], "n_corr": a.n_corr, "seed": a.seed, "n_iterations": N_IT,
                 "stride": STRIDE, "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"],
                 "lambda_final": R["lambda_final"], "iterations": R["iterations"], "trials_total": R["trials_total"],
                 "point_sum": pts.sum(0).tolist(), "scales": res["scales"].tolist(), "tg": res["tg"].tolist(),

@@ -1,9 +1,14 @@
 """Headline workload parity (C2: 100k correspondences x 2 views, bench.py's scene) against the
 committed oracle run (tests/golden/c2, tests/golden/make_c2_golden.py: the reference LM restated in
-C with g2o numeric Jacobians — the reference's arithmetic — on the same full-size graph).  The
-device runs the same first iterations in the same numeric mode; identical trial counts, chi2 per
-iteration rel 1e-6, the solved points (fixed subsample and coordinate sums) and the reprojection
-RMSE of the solved map (calculatePixelsStandDev) within the north-star 1e-4 px."""
+C with g2o numeric Jacobians — the reference's arithmetic — on the same full-size graph, 6 LM
+iterations).  The device runs the same iterations in the same numeric mode on BOTH plans — the
+iterative plan with the merged two-launch CG chain is the one bench.py times (600,008 unknowns, far
+above the merged chain's 50,000) — : identical trial counts, chi2 per iteration rel 1e-6, the solved
+points (fixed subsample and coordinate sums) and the reprojection RMSE of the solved map
+(calculatePixelsStandDev) within the north-star 1e-4 px.  (This near-stalled headline LM moves the
+RMSE by ~1e-4 px; tests/test_regime_goldens.py pins the merged chain at 30k correspondences on runs
+whose RMSE moves by > 5e-3 px.)"""
+import copy
 import json
 
 import numpy as np
@@ -23,20 +28,38 @@ def golden():
     return json.loads((d / "expected_c2.json").read_text()), np.load(d / "expected_c2.npz")
 
 
-def test_c2_first_iterations_match_oracle(gpu_ctx, golden):
+@pytest.fixture(scope="module")
+def c2_scene(golden):
+    meta, _ = golden
+    return sim.two_view_problem(meta["n_corr"], meta["seed"], return_map=True)
+
+
+@pytest.mark.parametrize("plan", ["iterative", "multifrontal"])
+def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
     meta, z = golden
-    p, m = sim.two_view_problem(meta["n_corr"], meta["seed"], return_map=True)
+    p, m0 = c2_scene
+    m = copy.deepcopy(m0)
     assert p.summary() == meta["summary"]
-    gpu_ctx.set_lm_lanes(1)
-    gpu_ctx.upload(p)
-    r = gpu_ctx.solve_lm(meta["n_iterations"], analytic=False)
-    gpu_ctx.set_lm_lanes(0)
+    gpu_ctx.set_plan(plan)
+    try:
+        gpu_ctx.set_lm_lanes(1)
+        gpu_ctx.upload(p)
+        info = gpu_ctx.plan_info()
+        assert info["plan"] == plan
+        if plan == "iterative":
+            assert info["cg_launches"] == 2                      # the merged chain bench.py times
+        r = gpu_ctx.solve_lm(meta["n_iterations"], analytic=False)
+        pts, sc, tg = gpu_ctx.download()
+    finally:
+        gpu_ctx.set_plan("multifrontal")
+        gpu_ctx.set_lm_lanes(0)
+    if plan == "iterative":
+        assert r["pcg_trials"] == r["trials_total"] and r["pcg_fallbacks"] == 0
     assert r["chi2_initial"] == pytest.approx(meta["chi2_initial"], rel=1e-11)
     assert r["iterations"] == meta["iterations"]
     assert r["trials_iter"] == list(z["trials_iter"])
     np.testing.assert_allclose(r["chi2_iter"], z["chi2_iter"], rtol=1e-6)
     assert r["lambda_final"] == pytest.approx(meta["lambda_final"], rel=1e-9)
-    pts, sc, tg = gpu_ctx.download()
     ext = np.abs(pts).max()
     assert np.abs(pts[::meta["stride"]] - z["points_sub"]).max() <= 1e-7 * ext
     np.testing.assert_allclose(pts.sum(0), meta["point_sum"], rtol=1e-9)

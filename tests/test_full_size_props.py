@@ -1,0 +1,77 @@
+"""Full-size properties of the timed plan (the iterative plan, merged two-launch CG chain) at the
+BASELINE sizes, where the oracle takes minutes to hours per iteration: properties that hold for any
+correct g2o LM (g2oBundleAdjustment.cc:959-962) and need no reference run.
+
+  * accepted chi2 never increases (an LM iteration keeps only a trial with rho > 0)
+  * no PCG step fails (every trial solved by PCG within its budget)
+  * a repeated run from the same state is bit-identical (fixed-order sums, no atomics)
+  * a damped solve (H + lambda I) x = b at the LM's dampings has a true relative residual
+    ||b - (H + lambda I) x|| / ||b|| < 1e-11, measured with the plan's own matrix-free product
+    (deftri_eval_hessian_product on the iterative plan; the CG stops on its recurrence residual at
+    1e-12), and a normwise backward error ||r|| / (||(H + lambda I) x|| + ||b||) < 1e-12
+
+C2: bench.py's headline scene (100k correspondences x 2 views, 600,008 unknowns).  C3 shape: 50k
+correspondences x 8 keyframes, all 28 pairs (1.2M unknowns, 8.4M ARAP edges; Drunkard.yaml shapes
+and weights), bench.py --workload c3's scene."""
+import numpy as np
+import pytest
+
+from deftri import capi, sim
+
+pytestmark = pytest.mark.gpu
+
+
+def c2_problem():
+    return sim.two_view_problem(100000, 1)            # bench.py build_problem(100000, 1)
+
+
+def c3_problem():
+    return sim.multi_view_problem(50000, 8, seed=1, kb8=sim.DRUNKARD_KB8, rep_weight=1.0, arap_weight=1e7,
+                                  depth_sigma=np.float32(0.3), pair_window=0)
+
+
+def check_props(p, n_it, lambdas_rel):
+    with capi.Context(0) as ctx:
+        ctx.set_plan("auto")                      # the library's choice: iterative from 50k unknowns
+        ctx.upload(p)
+        info = ctx.plan_info()
+        assert info["plan"] == "iterative" and info["cg_launches"] == 2
+        r1 = ctx.solve_lm(n_it, analytic=False)
+        s1 = ctx.download()
+        assert r1["iterations"] == n_it
+        assert r1["pcg_fallbacks"] == 0 and r1["pcg_trials"] == r1["trials_total"]
+        chi = [r1["chi2_initial"]] + list(r1["chi2_iter"])
+        assert all(b <= a for a, b in zip(chi, chi[1:])), chi
+        assert r1["chi2_final"] < r1["chi2_initial"]
+        ctx.reset_state()
+        r2 = ctx.solve_lm(n_it, analytic=False)
+        s2 = ctx.download()
+        assert r2["chi2_iter"] == r1["chi2_iter"] and r2["trials_iter"] == r1["trials_iter"]
+        assert r2["pcg_iterations"] == r1["pcg_iterations"]
+        for a, b in zip(s1, s2):
+            assert np.array_equal(a, b)
+        # damped solves at the solved state: g2o's initial damping (tau max diag H) and the LM's last
+        b, d = ctx.gradient()
+        out = []
+        for lam in [rel * np.abs(d).max() for rel in lambdas_rel] + [r1["lambda_final"]]:
+            x = ctx.damped_solve(lam, b, solver="pcg", max_iterations=4096)
+            its, ok = ctx.last_step_info()
+            assert ok and its > 0
+            ax = ctx.hessian_product(x) + lam * x
+            res = np.linalg.norm(b - ax)
+            out.append((lam, its, res / np.linalg.norm(b)))
+            assert res / np.linalg.norm(b) < 1e-11, out
+            assert res / (np.linalg.norm(ax) + np.linalg.norm(b)) < 1e-12, out
+        return r1, out
+
+
+def test_c2_full_size_properties():
+    r, solves = check_props(c2_problem(), 6, (1e-5,))
+    print("C2", r["trials_iter"], solves)
+
+
+def test_c3_shape_full_size_properties():
+    p = c3_problem()
+    assert p.n_pairs == 28 and p.n_unknowns == 1200224
+    r, solves = check_props(p, 3, (1e-5,))
+    print("C3", r["trials_iter"], solves)

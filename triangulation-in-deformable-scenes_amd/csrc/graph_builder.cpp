@@ -374,12 +374,16 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             const size_t rbase = g.rot.size();
             g.rot.resize(rbase + 9 * (size_t)n1);
             double *Rs = g.rot.data() + rbase;
+            int dev_rc = 1;
             if (gdev) {
                 M.w.resize(M.adj.size());
-                if (!gdev->mesh_pass(n1, n2, M.tris.data(), (int)M.tris.size() / 3, M.off.data(), M.adj.data(), (int64_t)M.adj.size(),
-                                     posIdx.data(), inv.data(), pos1.data(), pos2.data(), M.w.data(), Rs, err))
-                    return false;
-            } else {
+                dev_rc = gdev->mesh_pass(n1, n2, M.tris.data(), (int)M.tris.size() / 3, M.off.data(), M.adj.data(),
+                                         (int64_t)M.adj.size(), posIdx.data(), inv.data(), pos1.data(), pos2.data(), M.w.data(),
+                                         Rs, err);
+                if (dev_rc < 0) return false;
+                if (dev_rc == 1) mesh_cot_weights(pos1, M);     // non-manifold edge: the host loops (all corners)
+            }
+            if (dev_rc != 0) {
                 parallel_for(n1, 2048, [&](int lo, int hi) {
                     for (int i = lo; i < hi; i++)
                         compute_r_vertex(i, n2, M.off.data(), M.adj.data(), M.w.data(), posIdx.data(), inv.data(), pos1.data(),

@@ -40,9 +40,11 @@ class GraphDevice {
  public:
     GraphDevice(int device, hipStream_t st) : dev_(device), st_(st) {}
     ~GraphDevice();
-    bool mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const int32_t *off, const int32_t *adj, int64_t nadj,
-                   const int32_t *pos_idx, const int32_t *inv, const double *pos1, const double *pos2, double *w,
-                   double *R, std::string &err);
+    // 0 done; 1 a non-manifold edge (more than two opposite corners): nothing usable, the caller
+    // runs the host loops for this pair; -1 a HIP error (err)
+    int mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const int32_t *off, const int32_t *adj, int64_t nadj,
+                  const int32_t *pos_idx, const int32_t *inv, const double *pos1, const double *pos2, double *w,
+                  double *R, std::string &err);
     double ms_last = 0;          // device time of the last mesh_pass (kernels only)
 
  private:

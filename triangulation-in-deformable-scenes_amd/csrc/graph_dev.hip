@@ -25,7 +25,9 @@ __device__ __forceinline__ int64_t csr_find(const int32_t *__restrict__ off, con
 
 // one thread per triangle corner: the cot term of the edge opposite the corner into one of the
 // edge's two slots (an integer ticket picks the slot; a planar triangulation has at most two
-// opposite corners per edge, more flags an error)
+// opposite corners per edge; more — duplicate or degenerate points — flags the pair, whose weights
+// and rotations the host loops then compute: they average over every opposite corner, as
+// Geometry.cc:283-290 does)
 __global__ __launch_bounds__(kRBlock) void k_cot_corners(int ntri, const int32_t *__restrict__ tris,
                                                          const int32_t *__restrict__ off, const int32_t *__restrict__ adj,
                                                          const double *__restrict__ pos, double *__restrict__ slot,
@@ -87,10 +89,10 @@ GraphDevice::~GraphDevice() {
     }
 }
 
-bool GraphDevice::mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const int32_t *off, const int32_t *adj,
-                            int64_t nadj, const int32_t *pos_idx, const int32_t *inv, const double *pos1,
-                            const double *pos2, double *w_out, double *R, std::string &err) {
-    if (n1 <= 0) return true;
+int GraphDevice::mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const int32_t *off, const int32_t *adj,
+                           int64_t nadj, const int32_t *pos_idx, const int32_t *inv, const double *pos1,
+                           const double *pos2, double *w_out, double *R, std::string &err) {
+    if (n1 <= 0) return 0;
     hipSetDevice(dev_);
     const size_t na = (size_t)std::max<int64_t>(nadj, 1);
     const size_t b_w = align_up(sizeof(double) * na), b_slot = align_up(2 * sizeof(double) * na);
@@ -107,7 +109,7 @@ bool GraphDevice::mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const
     };
     if (need > cap_) {
         if (buf_) { hipStreamSynchronize(st_); hipFree(buf_); buf_ = nullptr; cap_ = 0; }
-        if (!check(hipMalloc(&buf_, need), "hipMalloc")) return false;
+        if (!check(hipMalloc(&buf_, need), "hipMalloc")) return -1;
         cap_ = need;
     }
     char *b = static_cast<char *>(buf_);
@@ -131,7 +133,7 @@ bool GraphDevice::mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const
         !check(hipMemcpyAsync(dpi, pos_idx, sizeof(int32_t) * (size_t)n1, h2d, st_), "copy") ||
         !check(hipMemcpyAsync(dinv, inv, sizeof(int32_t) * (size_t)n1, h2d, st_), "copy") ||
         !check(hipMemsetAsync(dcnt, 0, sizeof(int) * (na + 1), st_), "memset"))
-        return false;
+        return -1;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
@@ -154,11 +156,8 @@ bool GraphDevice::mesh_pass(int n1, int n2, const int32_t *tris, int ntri, const
     ms_last = ms;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
-    if (ok && bad) {
-        err = "graph geometry on the device: an edge with more than two opposite vertices (non-planar mesh)";
-        return false;
-    }
-    return ok;
+    if (!ok) return -1;
+    return bad ? 1 : 0;      // 1: an edge with more than two opposite vertices — the host loops redo the pair
 }
 
 }  // namespace deftri

@@ -2121,9 +2121,11 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
 int deftri_eval_hessian_product(deftri_ctx *ctx, const double *x, double *y, int64_t n) {
     if (ctx && ctx->dist()) return fail(ctx, DEFTRI_E_ARG, "not available on a point-sharded context");
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
-    if (ctx->sp_on) {                        // the iterative plan never assembles H
-        const int rc0 = ensure_multifrontal(ctx);
-        if (rc0) return rc0;
+    if (ctx->sp_on) {                        // the iterative plan's own matrix-free product (H never assembled)
+        if (!x || !y) return fail(ctx, DEFTRI_E_ARG, "null array");
+        hipSetDevice(ctx->device);
+        int rc = ctx->sp->hessian_product(0.0, x, y, n);
+        return rc ? fail(ctx, rc, ctx->sp->err) : 0;
     }
     if (n != ctx->S.ndof || !x || !y) return fail(ctx, DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(ctx->device);

@@ -48,8 +48,10 @@ constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy 
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 constexpr int64_t kSpMergeMinDof = 50000;  // one rank: the merged (two-launch) CG chain from this many unknowns
 enum { SP_ARAP = 0, SP_DEP = 1 };
-// solve status (record word 0)
-enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4 };
+// solve status (record word 0).  kSpTimeout: the merged chain's alpha hand-off was not seen within
+// its poll bound (phase 2's workgroup 0 not resident while the others waited): an error, never a
+// rejected trial (SpSolver raises it and switches the context to the separate alpha launch)
+enum { kSpRunning = 0, kSpConverged = 1, kSpBreakdown = 2, kSpBadBlock = 3, kSpBudget = 4, kSpTimeout = 5 };
 
 // the transport of a sharded solve (solver.cpp: RCCL on the solver stream, or the caller's host
 // callback); every rank issues the same calls in the same order
@@ -147,7 +149,11 @@ struct SpDev {
     double *rpart = nullptr;                              // row-block partials: phase 2 p.q [nrb]; update (rz, rr) [nrb + 1][2]
     double *upart = nullptr;
     double *hbuf = nullptr;                               // [pq_rows, heavy sums (hd)]
-    double *red = nullptr;                                // [max_it + 2][kSpRed]: rz, rr, -, alpha
+    // [max_it + 2][kSpRed]: rz, rr, stop, alpha.  stop (word 2 of iteration it + 1): a breakdown /
+    // hand-off timeout found inside iteration it's phase 2 (merged chain).  It is read from the next
+    // launch on, so every workgroup of one launch sees the same state: a status written into rec[0]
+    // during phase 2 would send the workgroups dispatched after it home before their tickets
+    double *red = nullptr;
     double *rec = nullptr;                                // [8]: status, its
     int *cnt = nullptr;                                   // [48] last-workgroup tickets, 16 per site (0 between launches)
     // k_sp_glin_heavy chunks: chunk j sums hv_blk[ch_lo[j] .. ch_lo[j + 1]) of heavy ch_h[j]; heavy h
@@ -193,6 +199,7 @@ void sp_launch_update(const SpDev &G, int it, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
 void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
+void sp_launch_load_p(int64_t n, const double *v, double2 *zp, hipStream_t st);
 void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
                           hipStream_t st);
 void sp_launch_permute_out(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,
@@ -217,6 +224,7 @@ class SpSolver {
     int chi2(double *out);
     int gradient(double *b, double *hdiag, int64_t n);
     int damped_solve(double lambda, const double *rhs, double *x, int64_t n);
+    int hessian_product(double lambda, const double *x, double *y, int64_t n);   // y = (H + lambda I) x
     int profile_trial(double lambda, KProf &prof, bool analytic);
     int vertex_owner(int32_t *owner, int64_t nv) const;
     int64_t ndof() const { return G.ndof; }
@@ -269,6 +277,7 @@ class SpSolver {
     template <class T> int alloc(T **p, int64_t n);
     template <class T> int put(T **p, const std::vector<T> &v);
     int fail(int code, const std::string &m) { err = m; return code; }
+    int hand_off_timeout();
     int budget() const;
     int lin_iteration(bool analytic, bool want_max, bool &ok);
     int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr);

@@ -53,16 +53,28 @@ __device__ __forceinline__ double pval(const double2 *__restrict__ zp, double be
     return __fma_rn(beta, v.y, v.x);
 }
 
-// the state of CG iteration `it`: 0 run it (beta set), 1 converged before it, 2 stopped (budget, or a
-// status already recorded: breakdown, bad block, converged earlier)
+// the state of CG iteration `it`: 0 run it (beta set); otherwise the status that stops it — the one
+// already recorded (rec[0]: breakdown, bad block, converged earlier), a stop the merged chain's
+// phase 2 left for this iteration (red[it][2]: breakdown, hand-off timeout), kSpConverged or
+// kSpBudget.  Every input is fixed for the whole launch except rec[0], which a launch writes only
+// when every one of its workgroups stops, so all workgroups of a launch take the same branch
 __device__ __forceinline__ int it_state(const SpDev &G, int it, double &beta) {
     beta = 0.0;
-    if (G.rec[0] != 0.0) return 2;
+    if (G.rec[0] != 0.0) return (int)G.rec[0];
     const double *rk = G.red + (int64_t)kSpRed * it;
-    if (rk[1] <= G.tol2 * G.red[1]) return 1;
-    if (it >= G.max_it) return 2;
+    if (rk[2] != 0.0) return (int)rk[2];
+    if (rk[1] <= G.tol2 * G.red[1]) return kSpConverged;
+    if (it >= G.max_it) return kSpBudget;
     if (it > 0) beta = rk[0] / G.red[(int64_t)kSpRed * (it - 1)];
     return 0;
+}
+
+// record the status that stopped iteration it (one thread; the first stop wins)
+__device__ __forceinline__ void record_stop(const SpDev &G, int it, int st) {
+    if (G.rec[0] == 0.0) {
+        G.rec[0] = st;
+        G.rec[1] = it;
+    }
 }
 
 // XCD-aware row blocks: workgroup b runs on XCD b % 8; the launch has 8 ceil(nrb / 8) row
@@ -345,7 +357,7 @@ __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
             else G.b[6 * (int64_t)G.Q + (h - G.Q)] = t;
         }
     }
-    if (threadIdx.x == 0) G.hcnt[h] = 0;
+    if (threadIdx.x == 0) st_sc1(G.hcnt + h, 0);
 }
 
 // rank max of the rows' diagonal (stage 0), or that (all-reduced) combined with the heavy diagonal
@@ -521,12 +533,12 @@ __device__ bool group_sum(const SpDev &G, int *cnt, const double *slots, double 
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int v = 0; v < NV; v++) publish(G, gs + NV * x + v, (red[v][0] + red[v][1]) + (red[v][2] + red[v][3]));
-        cnt[1 + x] = 0;                  // the group is done: nobody else touches its counter
+        st_sc1(cnt + 1 + x, 0);          // the group is done: nobody else touches its counter
         settle();
         flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
         if (flag) {
             if (G.fence) __threadfence();
-            cnt[0] = 0;
+            st_sc1(cnt, 0);
 #pragma unroll
             for (int v = 0; v < NV; v++) {
                 double t = 0.0;
@@ -569,6 +581,9 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
     // blockIdx - 1; partial slots as in k_sp_dots (rows 0..nrb-1, heavy nrb)
     const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
     if (rb < 0 && t == 0 && G.merged) *G.aflag = -1;      // no iteration's alpha published yet
+    // the CG chain's ticket counters (sites 0 and 16; this launch counts at 32) start every solve at
+    // zero, whatever an earlier solve on this plan left
+    if (rb < 0 && t < 32) st_sc1(G.cnt + t, 0);
     if (rb >= 0) {
         const int l0 = rb * kSpUpdRows;
         const int nrow = min(kSpUpdRows, G.nown - l0);
@@ -749,10 +764,16 @@ __device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam,
 }
 
 // merged chain, phase 2: alpha of iteration it.  Workgroup 0 (dispatched first, waits on nothing)
-// sums phase 1's p.Ap partials in a fixed order, records alpha (NaN on breakdown, with the status)
-// and publishes it: the value with an agent-scope store, acknowledged, then the flag = it.  The
-// other workgroups call m2_alpha_wait where they first need alpha (after their sums): thread 0
-// polls the flag (bounded; a timeout stops the solve like a breakdown), the value goes through LDS.
+// sums phase 1's p.Ap partials in a fixed order, records alpha (NaN on breakdown, with the stop word
+// of iteration it + 1) and publishes it: the value with an agent-scope store, acknowledged, then the
+// flag = it.  The other workgroups call m2_alpha_wait where they first need alpha (after their
+// sums): thread 0 polls the flag, the value goes through LDS.
+// The wait rests on workgroup 0 being resident while the others poll: the dispatcher hands out a
+// launch's workgroups in index order, so workgroup 0 starts before any waiter; HIP does not promise
+// this.  The poll is bounded: a timeout skips the workgroup's update and leaves kSpTimeout for the
+// next iteration, which the host raises as an error (never a rejected trial) and answers by
+// switching the context to the separate alpha launch (k_sp_alpha).  Either way every workgroup still
+// draws its ticket in m2_dots, so the counters return to zero.
 __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish) {
     __shared__ double sa;
     double a = 0.0;
@@ -770,8 +791,7 @@ __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *
     if (threadIdx.x == 0) {
         double alpha = G.red[(int64_t)kSpRed * it] / a;
         if (!(a > 0.0) || !isfinite(alpha)) {
-            G.rec[0] = kSpBreakdown;
-            G.rec[1] = it;
+            G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpBreakdown;   // read from the next launch on
             alpha = __builtin_nan("");
         }
         G.red[(int64_t)kSpRed * it + 3] = alpha;
@@ -796,8 +816,7 @@ __device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
             n++;
         }
         if (n >= (1 << 22)) {                          // never expected: stop the solve, skip the update
-            G.rec[0] = kSpBreakdown;
-            G.rec[1] = it;
+            G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpTimeout;
             sa = __builtin_nan("");
         } else {
             sa = ld_sc1(G.apub);
@@ -949,10 +968,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     double beta;
     if (const int st = it_state(G, it, beta)) {
         // with the heavy finish folded in here, k_sp_heavy's record of the first stopped iteration too
-        if ((MG || G.fuse_heavy) && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
-            G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
-            G.rec[1] = it;
-        }
+        if ((MG || G.fuse_heavy) && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
     double alpha = 0.0;
@@ -1178,10 +1194,7 @@ __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double 
     double beta;
     const int st = it_state(G, it, beta);
     if (st || stage == 3) {
-        if (st && stage != 2 && blockIdx.x == 0 && threadIdx.x == 0 && G.rec[0] == 0.0) {
-            G.rec[0] = st == 1 ? kSpConverged : kSpBudget;
-            G.rec[1] = it;
-        }
+        if (st && stage != 2 && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
     __shared__ double lds[256];
@@ -1308,6 +1321,12 @@ __global__ void k_sp_unpack(int n, const int32_t *__restrict__ rows, int width, 
     dst[base + (int64_t)width * rows[i] + c] = buf[t];
 }
 
+// (z, p) = (v, 0): a vector the first CG iteration's product multiplies (p = z at it 0)
+__global__ void k_sp_load_p(int64_t n, const double *__restrict__ v, double2 *__restrict__ zp) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < n) zp[t] = make_double2(v[t], 0.0);
+}
+
 // problem order [heavy][points by id] <-> plan order [heavy][rows]
 __global__ void k_sp_permute(int32_t P, int64_t hd, const int32_t *__restrict__ row_of_point, const double *__restrict__ src,
                              double *__restrict__ dst, int to_plan) {
@@ -1408,6 +1427,10 @@ void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, co
 void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst,
                            hipStream_t st) {
     if (n > 0) SPL("sp_halo_unpack", sp::k_sp_unpack, nblk((int64_t)n * width, 256), n, rows, width, base, buf, dst);
+}
+
+void sp_launch_load_p(int64_t n, const double *v, double2 *zp, hipStream_t st) {
+    SPL("sp_load_p", sp::k_sp_load_p, nblk(n, 256), n, v, zp);
 }
 
 void sp_launch_permute_in(int32_t P, int64_t hd, const int32_t *row_of_point, const double *src, double *dst,

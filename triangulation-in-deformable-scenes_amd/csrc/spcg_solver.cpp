@@ -107,6 +107,19 @@ int SpSolver::put(T **p, const std::vector<T> &v) {
 
 int SpSolver::budget() const { return std::min(kSpMaxIt, max_it > 0 ? max_it : kSpDefaultIt); }
 
+// a merged-chain alpha hand-off that timed out (spcg.hip m2_alpha_wait): the trial's state is
+// restored, the context switches to the separate alpha launch and the call fails — a device
+// scheduling fault, not a numeric verdict, so it never becomes a rejected trial
+int SpSolver::hand_off_timeout() {
+    G.alpha_kernel = 1;
+    hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_);
+    hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_);
+    hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_);
+    hipStreamSynchronize(st_);
+    return fail(DEFTRI_E_HIP, "merged CG chain: the alpha hand-off timed out (phase 2's workgroup 0 not resident); "
+                              "the context now launches alpha separately — retry the call");
+}
+
 // the values of a problem in the plan's layout (points in row order, the rank's edges): everything
 // a structurally identical problem can change
 void SpSolver::gather_values(const deftri_problem_desc &d, SpValues &v) const {
@@ -470,6 +483,7 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
         SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
         SPOK(hipStreamSynchronize(st_));
         const int status = (int)hpin[16];
+        if (status == kSpTimeout) return hand_off_timeout();
         if (status == kSpConverged) { its = (int)hpin[17]; solved = true; break; }
         if (status != kSpRunning || j >= mx) { its = j; solved = false; break; }
         n = std::min(j + 4, mx);
@@ -563,6 +577,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; }
             int st = (int)hpin[16];
+            if (st == kSpTimeout) return hand_off_timeout();
             bool solved = st == kSpConverged, evaluated = solved;
             int its = solved ? (int)hpin[17] : j;
             if (!solved) {
@@ -579,6 +594,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                     SPOK(hipStreamSynchronize(st_));
                     st = (int)hpin[16];
                 }
+                if (st == kSpTimeout) return hand_off_timeout();
                 solved = st == kSpConverged;
                 its = solved ? (int)hpin[17] : j;
                 if (solved) {
@@ -726,6 +742,37 @@ int SpSolver::damped_solve(double lambda, const double *rhs, double *x, int64_t 
     SPOK(hipMemcpyAsync(x, d_dx0, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st_));
     SPOK(hipStreamSynchronize(st_));
     if (!solved) return fail(DEFTRI_E_NUMERIC, "PCG did not converge within its budget (" + std::to_string(its) + " iterations)");
+    return 0;
+}
+
+// y = (H + lambda I) x with the CG chain's own product kernels (the three-launch form: phase 1,
+// phase 2, the heavy finish), H linearized at the current state with the analytic Jacobians as
+// gradient() / damped_solve() do: the operator the solves invert, for their backward errors
+int SpSolver::hessian_product(double lambda, const double *x, double *y, int64_t n) {
+    if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
+    if (nranks_ > 1) return fail(DEFTRI_E_ARG, "not available on a point-sharded context");
+    if (n != G.ndof) return fail(DEFTRI_E_ARG, "size mismatch");
+    hipSetDevice(dev_);
+    bool ok;
+    int rc = lin_iteration(true, false, ok);
+    if (rc) return rc;
+    SPOK(hipMemcpyAsync(d_dx0, x, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, st_));
+    sp_launch_permute_in(G.P, G.hd, d_row_of_point, d_dx0, d_tmp, st_);
+    sp_launch_load_p(G.ndof, d_tmp, G.zp, st_);
+    // iteration 0 runs (r.r = 1 > 0), beta = 0 so p = z = x; every partial to plain stores
+    SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + 2 * kSpRed), st_));
+    const double one = 1.0;
+    SPOK(hipMemcpyAsync(G.red + 1, &one, sizeof(double), hipMemcpyHostToDevice, st_));
+    SpDev g = G;
+    g.merged = 0; g.fuse = 0; g.fuse_heavy = 0;
+    g.max_it = 1;
+    g.tol2 = 0.0;
+    sp_launch_product(g, 0, lambda, fp32_jac != 0, st_);
+    sp_launch_heavy(g, 0, lambda, 0, st_);
+    sp_launch_permute_out(G.P, G.hd, d_row_of_point, G.q, d_dx0, st_);
+    SPOK(hipMemcpyAsync(y, d_dx0, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + 2 * kSpRed), st_));
     return 0;
 }
 

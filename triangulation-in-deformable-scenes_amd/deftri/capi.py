@@ -148,6 +148,7 @@ class Context:
     """One solver context (one per host thread).  device < 0 = host-only (graph / analysis)."""
 
     def __init__(self, device=0):
+        self.h = None                    # close() / __del__ after a failed create
         self.lib = load()
         h = C.c_void_p()
         rc = self.lib.deftri_ctx_create(int(device), C.byref(h))
@@ -160,7 +161,7 @@ class Context:
         self._solver = ("pcg", 0.0, 0)
 
     def close(self):
-        if self.h:
+        if getattr(self, "h", None):
             self.lib.deftri_ctx_destroy(self.h)
             self.h = None
 
@@ -409,6 +410,7 @@ class BAContext:
     """Bundle-adjustment solver context on one GPU (deftri_ba_*).  `prob` is a ba.BAProblem."""
 
     def __init__(self, device=0):
+        self.h = None                    # close() / __del__ after a failed create
         self.lib = load()
         h = C.c_void_p()
         rc = self.lib.deftri_ba_create(int(device), C.byref(h))
@@ -421,7 +423,7 @@ class BAContext:
         self._cb = None
 
     def close(self):
-        if self.h:
+        if getattr(self, "h", None):
             self.lib.deftri_ba_destroy(self.h)
             self.h = None
 
