@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 4
+#define DEFTRI_ABI_VERSION 5
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -267,7 +267,14 @@ typedef struct deftri_plan_info {
     int32_t cg_launches;       /* iterative: kernel launches per CG iteration (one rank from 50,000
                                   unknowns: 2, the merged chain — phase 1 forms p.Ap, phase 2 the
                                   update; one rank below that: 3, the dots and the heavy-vertex finish
-                                  in last workgroups; sharded: 5-6) */
+                                  in last workgroups; sharded: 3, the single-reduction chain —
+                                  phase 1 and phase 2 form w = A z, k_sp_update_sd the update) */
+    int32_t cg_collectives;    /* iterative: all-reduces per CG iteration (one rank 0; sharded 1, plus
+                                  one grouped halo send / receive) */
+    int32_t sharded;           /* iterative: the sharded control flow (nranks > 1, or one rank with an
+                                  RCCL communicator: deftri_dist_init_rccl(ctx, 1, 0, id)) */
+    double  survey_bytes;      /* SURVEY.md §8(d)'s B_pcg of this rank's share: 176 E + 48 R + 40 D + 156 P
+                                  (owned ARAP edges, own rows' reprojection / depth edges, own rows) */
 } deftri_plan_info;
 int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info);
 /* TEST ONLY (no GPU): host emulation of one product q = (H + lambda I) p with the iterative plan's

@@ -9,9 +9,10 @@ solved map (calculatePixelsStandDev, Geometry.cc:370-498) within 1e-4 px of the 
 where the RMSE itself moves by more than 5e-3 px, so the check can fail.  The iterative plan (the
 default here: 60k unknowns) must solve every trial by PCG.
 
-The same three regimes at 30k correspondences (tests/golden/regimes_30k: 90k unknowns, seed 7) pin the
-merged two-launch CG chain — the chain bench.py times at C2 — on 25-iteration runs whose RMSE moves,
-the pinning the near-stalled C2 golden (tests/test_c2_golden.py) cannot give."""
+The same three regimes at 30k correspondences (tests/golden/regimes_30k: 90k unknowns, seed 7; oracle
+12-17 minutes each) pin the merged two-launch CG chain — the chain bench.py times at C2 — on
+25-iteration runs whose RMSE moves (5.7e-4 / 7.7e-4 / 3.0e-2 px), the pinning the near-stalled C2
+golden (tests/test_c2_golden.py) cannot give."""
 import copy
 import json
 
@@ -64,7 +65,10 @@ def test_regime_matches_oracle(gpu_ctx, name, sub, plan):
     assert r["chi2_initial"] == pytest.approx(meta["chi2_initial"], rel=1e-11)
     assert r["iterations"] == meta["iterations"]
     assert r["trials_iter"] == list(z["trials_iter"])
-    np.testing.assert_allclose(r["chi2_iter"], z["chi2_iter"], rtol=1e-5)
+    # the oracle's own spread between elimination orders: 1e-5 at 10k; at 30k the Realcolon run (Omega
+    # 1e12) moves one iteration's chi2 by 2.3e-5 on BOTH plans — the multifrontal plan's exact LDL^T
+    # steps included — so 5e-5 there
+    np.testing.assert_allclose(r["chi2_iter"], z["chi2_iter"], rtol=1e-5 if sub == "regimes" else 5e-5)
     if plan == "iterative":
         assert r["pcg_trials"] == r["trials_total"] and r["pcg_fallbacks"] == 0
     ext = np.abs(pts).max()
@@ -72,7 +76,9 @@ def test_regime_matches_oracle(gpu_ctx, name, sub, plan):
     m1 = copy.deepcopy(m)
     metrics.apply_solution(m1, list(p.point_ids), pts)
     rms = metrics.pixels_stand_dev(m1)
+    # the RMSE must move by several times the 1e-4 px tolerance, so a solver that did nothing fails:
+    # > 5e-3 px on every 10k run, > 5e-4 px at 30k (Realcolon 3e-2)
     moved = abs(meta["rms_final"]["desv"] - meta["rms_initial"]["desv"])
-    assert moved > 5e-3, moved
+    assert moved > (5e-3 if sub == "regimes" else 5e-4), moved
     for k in ("desv", "desvc1", "desvc2"):
         assert abs(rms[k] - meta["rms_final"][k]) < 1e-4, (k, rms[k], meta["rms_final"][k])

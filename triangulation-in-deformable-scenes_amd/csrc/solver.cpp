@@ -1199,6 +1199,9 @@ int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info) {
         info->product_bytes = s.product_bytes();
         info->jacobian_fp32 = s.fp32_jac;
         info->cg_launches = s.cg_launches();
+        info->cg_collectives = s.cg_collectives();
+        info->sharded = s.sharded() ? 1 : 0;
+        info->survey_bytes = s.survey_bytes();
         return 0;
     }
     if (!ctx->have) return DEFTRI_E_NOPROBLEM;
@@ -1486,7 +1489,7 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
         ctx->analysed = false;
         copy_host(ctx->hp, desc);
         if (!ctx->sp_tr) ctx->sp_tr = new CtxTransport(ctx);
-        ctx->sp.reset(new SpSolver(ctx->device, ctx->st, ctx->rank, ctx->nranks, ctx->sp_tr));
+        ctx->sp.reset(new SpSolver(ctx->device, ctx->st, ctx->rank, ctx->nranks, ctx->sp_tr, ctx->comm != nullptr));
         ctx->sp->tol = ctx->pcg_tol;
         ctx->sp->max_it = ctx->pcg_max_it;
         ctx->sp->fp32_jac = ctx->jac_fp32;

@@ -176,6 +176,16 @@ struct SpDev {
     double *apub = nullptr;                               // alpha published by phase 2's workgroup 0
     int *aflag = nullptr;                                 // ... and the iteration it belongs to (-1 after setup)
     int32_t alpha_kernel = 0;                             // alpha by k_sp_alpha between the phases (no hand-off)
+    // sharded single-reduction chain (sd, any rank count with a transport): per CG iteration phase 1
+    // and phase 2 form w = A z and this rank's part of xb, the host all-reduces xb, k_sp_update_sd
+    // updates and fills the send buffer; the boundary rows' (z, p) land in the receive region of zp
+    // (rows P .. P + halo: apts_p maps the local edges' halo rows there)
+    int32_t sd = 0;
+    double *sv = nullptr;                                 // s = A p by recurrence (ndof)
+    double *xb = nullptr;                                 // [3 + hd]: r.z, r.r, z.Az, heavy sums of A z
+    const int32_t *apts_p = nullptr;                      // local ARAP edges' rows, halo rows -> P + k
+    const int32_t *snd_off = nullptr, *snd_slot = nullptr;   // own row l: send slots (rows of sbuf)
+    double *sbuf = nullptr;                               // [send rows][6]: (z, p) of 3 dofs
     double *m2part = nullptr;                             // phase-2 (r.z, r.r) per workgroup [m_nh + row grid][2]
     double *gsum = nullptr;                               // per XCD group sums [2 sites][8][2]
     int32_t flat_ticket = 0;                              // single-counter last-workgroup ticket (A/B)
@@ -196,6 +206,7 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
 int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
 int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
+void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
 void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
@@ -214,7 +225,9 @@ struct SpValues {
 
 class SpSolver {
  public:
-    SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr);
+    // force_sharded: the sharded chain and the transport's collectives even on one rank (a context
+    // with an RCCL communicator of one rank: the production transport exercised on one GPU)
+    SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr, bool force_sharded = false);
     ~SpSolver();
     int upload(const deftri_problem_desc &d);
     int refresh(const deftri_problem_desc &d);     // same structure: values only, plan kept
@@ -236,12 +249,21 @@ class SpSolver {
         return H.phase2_bytes + (G.merged ? (double)G.nown * (24 + 24 + 24 + 24 + 48 - 24) : 0.0);
     }
     double product_bytes() const { return product_bytes_phase(1) + product_bytes_phase(2); }
+    // SURVEY.md §8(d) B_pcg = 176 E + 48 R + 40 D + 156 P on this rank's share (owned ARAP edges, own
+    // rows' edges, own rows): the minimal-traffic count the bench line's frac_survey is priced on
+    double survey_bytes() const {
+        return 176.0 * H.n_arap_owned + 48.0 * (double)H.rep_ids.size() + 40.0 * (double)H.dep_ids.size() +
+               156.0 * (double)(H.hi - H.lo);
+    }
     int64_t halo_rows() const { return H.halo_rows; }
+    bool sharded() const { return shard_; }
+    int32_t cg_collectives() const { return !shard_ ? 0 : G.sd ? 1 : 2; }   // all-reduces per CG iteration
     int32_t own_rows() const { return H.hi - H.lo; }
     int32_t n_blocks() const { return G.nblk; }
     int32_t n_row_blocks() const { return G.nrb; }
     int32_t n_arap_local() const { return (int32_t)H.arap_ids.size(); }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
+        if (G.sd) return 3;                      // + one all-reduce and one grouped send / receive
         if (G.merged) return G.alpha_kernel ? 3 : 2;
         const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;
         return (G.fuse ? 0 : 1) + (G.nblk > 0 ? 1 : 0) + 1 + heavy + 1;
@@ -259,6 +281,7 @@ class SpSolver {
     hipStream_t st_ = nullptr;
     int rank_ = 0, nranks_ = 1;
     SpTransport *tr_ = nullptr;
+    bool shard_ = false;                  // the sharded control flow (nranks > 1, or forced with a transport)
     SpPlanHost H;
     SpDev G;
     DevProblem P;
@@ -281,10 +304,11 @@ class SpSolver {
     int budget() const;
     int lin_iteration(bool analytic, bool want_max, bool &ok);
     int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr);
-    void cg_setup(double lambda, const double *rhs);
-    void cg_chain(double lambda, int from, int to);
-    int cg_tail(int n);
+    int cg_setup(double lambda, const double *rhs);
+    int cg_chain(double lambda, int from, int to);
+    int cg_tail(int n, double lambda);
     int halo(int width, double *vec, bool zp);
+    int halo_sd();
     int pcg_solve(double lambda, const double *rhs, bool &solved, int &its);
     void gather_values(const deftri_problem_desc &d, SpValues &v) const;
 };

@@ -567,6 +567,15 @@ __device__ __forceinline__ void dots_block(const SpDev &G, int it, double (*red)
     pair_tree(a0, a1, red, G.red + (int64_t)kSpRed * it);
 }
 
+// the sd chain: own row l's dof a, (z, p) into each of its send slots
+__device__ __forceinline__ void sd_send(const SpDev &G, int l, int a, double z, double p) {
+    for (int k = G.snd_off[l]; k < G.snd_off[l + 1]; k++) {
+        const int64_t o = 6 * (int64_t)G.snd_slot[k] + 2 * a;
+        G.sbuf[o] = z;
+        G.sbuf[o + 1] = p;
+    }
+}
+
 // setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
 // partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
 __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
@@ -619,6 +628,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
             G.r[o0 + t] = r;
             G.zp[o0 + t] = make_double2(z, 0.0);
             G.x[o0 + t] = 0.0;
+            if (G.sd) sd_send(G, l0 + row, a, z, 0.0);
             rz = r * z;
             rr = r * r;
         }
@@ -834,14 +844,21 @@ __global__ void __launch_bounds__(256) k_sp_alpha(int it, const SpDev G) {
     m2_alpha_make(G, it, red4, false);
 }
 
-// MG (merged chain, one rank): also p.Ap = sum_e s_e (J_e p) + sum_dep p_s (2 c_e . p_v + W J_s^2 p_s)
+// MG 1 (merged chain, one rank): also p.Ap = sum_e s_e (J_e p) + sum_dep p_s (2 c_e . p_v + W J_s^2 p_s)
 // + sum_v p_v . (D_v + lam) p_v + lam |p_h|^2 per workgroup — the first m_nx workgroups do the heavy
-// dofs (p_h stored for phase 2) and the row terms, 256 rows each — and alpha in the last workgroup
-template <class JT, bool MG>
+// dofs (p_h stored for phase 2) and the row terms, 256 rows each — and alpha in the last workgroup.
+// MG 2 (sharded single-reduction chain): the same sums with z in place of p (beta = 0: the product
+// is A z, the partials are z.Az over the rank's owned edges, own rows and — on the rank that counts
+// them — the heavy dofs); the rows' z are read through apts_p (halo rows in the receive region)
+template <class JT, int MG>
 __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     __shared__ double red[7][4];
-    double beta;
-    if (it_state(G, it, beta)) return;
+    double beta = 0.0;
+    if constexpr (MG == 2) {
+        if (G.rec[0] != 0.0) return;             // the state is decided by the update (k_sp_update_sd)
+    } else {
+        if (it_state(G, it, beta)) return;
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if constexpr (MG) {
         double pap = 0.0;
@@ -853,6 +870,7 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
                     G.ph[dd] = p;
                     pap += lam * (p * p);
                 }
+                if (!G.include_heavy) pap = 0.0;      // replicated dofs: counted on one rank
             } else if (e - 1 < G.nrb) {
                 const int l = (e - 1) * 256 + (int)threadIdx.x;
                 if (l < G.nown) {
@@ -882,7 +900,7 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
     if (kind == SP_ARAP) {
         double acc[6] = {0, 0, 0, 0, 0, 0};
         if (i < d.w) {
-            const int4 rw = reinterpret_cast<const int4 *>(G.apts)[i];
+            const int4 rw = reinterpret_cast<const int4 *>(MG == 2 ? G.apts_p : G.apts)[i];
             double J[18];
 #pragma unroll
             for (int k = 0; k < 18; k++) J[k] = (double)Jarap[k * G.jld + i];
@@ -899,12 +917,12 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
             for (int c = 0; c < 6; c++) t += J[12 + c] * pval(G.zp, beta, oT + c);
             const double s = G.Wa[i] * t;
             G.s[i] = s;
-            if (MG) pap = s * t;
+            if (MG && owned) pap = s * t;            // (one rank: every edge owned)
             if (owned)
 #pragma unroll
                 for (int c = 0; c < 6; c++) acc[c] = J[12 + c] * s;
         }
-        if (!MG && !owned) return;           // (MG: one rank, every edge owned)
+        if (!MG && !owned) return;
 #pragma unroll
         for (int c = 0; c < 6; c++) {
             const double v = wave_sum(acc[c]);
@@ -961,12 +979,39 @@ __device__ __forceinline__ void m2_dots(const SpDev &G, int it, double (*red)[4]
 // MG (merged chain, one rank): the update of iteration it follows in the same thread — x += alpha p,
 // r -= alpha q, z = M r, (z, p) stored (q never is) — and the (r.z, r.r) of iteration it + 1 are
 // formed by the last workgroup; the first m_nh workgroups do the heavy vertices (their sums, q, update)
-template <class JT, bool MG>
+// MG 2 (sharded single-reduction chain): the rows' w = A z stored into q; the first m_nh workgroups
+// write this rank's part of the reduction record xb = [r.z, r.r, z.Az, heavy sums of A z]: one per
+// heavy vertex its block partials' sums, then z.Az from phase 1's partials and (r.z, r.r) from the
+// last update's (or the setup's) — all from earlier launches, so no hand-off; the host all-reduces xb
+template <class JT, int MG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4)))
 k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
-    double beta;
-    if (const int st = it_state(G, it, beta)) {
+    double beta = 0.0;
+    if constexpr (MG == 2) {
+        if (G.rec[0] != 0.0) return;
+        if ((int)blockIdx.x < G.m_nh) {
+            const int nh = G.Q + G.S;
+            const int h = blockIdx.x;
+            if (h < nh) {
+                __shared__ double lds[256];
+                const double t = heavy_part_sum(G, h, lds);
+                if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) G.xb[3 + heavy_dof(G, h) + threadIdx.x] = t;
+            } else if (h == nh) {                     // z.Az: phase 1's workgroup partials, in order
+                double a = 0.0;
+                for (int j = threadIdx.x; j < G.m1n; j += 256) a += G.m1part[j];
+                a = block_sum(a, red4);
+                if (threadIdx.x == 0) G.xb[2] = a;
+            } else if (h == nh + 1) {                 // (r.z, r.r): the update's row-block partials
+                double a0 = 0.0, a1 = 0.0;
+                for (int j = threadIdx.x; j <= G.nrb; j += 256) { a0 += G.upart[2 * j]; a1 += G.upart[2 * j + 1]; }
+                a0 = block_sum(a0, red4);
+                a1 = block_sum(a1, red4);
+                if (threadIdx.x == 0) { G.xb[0] = a0; G.xb[1] = a1; }
+            }
+            return;
+        }
+    } else if (const int st = it_state(G, it, beta)) {
         // with the heavy finish folded in here, k_sp_heavy's record of the first stopped iteration too
         if ((MG || G.fuse_heavy) && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
@@ -976,7 +1021,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     bool rows = true;
     int hv = -1;                                            // MG: the heavy vertex of this workgroup
     double th = 0.0;                                        // ... its component sum (thread < dim)
-    if constexpr (MG) {
+    if constexpr (MG == 1) {
         if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];     // k_sp_alpha's
         else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true);
         if ((int)blockIdx.x < G.m_nh) {
@@ -989,6 +1034,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
     }
     const int nhx = MG ? G.m_nh : G.fuse_heavy ? G.Q + G.S : 0;
+    (void)alpha;
     if (!MG && (int)blockIdx.x < nhx) {
         // the heavy vertices' sums (phase-1 partials only): dispatched first, concurrent with the rows
         __shared__ double lds[256];
@@ -1086,18 +1132,21 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             for (int c = 0; c < 3; c++) v[c] = G.zp[o + c];
 #pragma unroll
             for (int k = 0; k < 6; k++) D[k] = G.Dv[6 * (int64_t)l + k];
-            if constexpr (MG) {
+            if constexpr (MG == 1) {
 #pragma unroll
                 for (int c = 0; c < 3; c++) { xo[c] = G.x[o + c]; ro[c] = G.r[o + c]; }
 #pragma unroll
                 for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
             }
 #pragma unroll
-            for (int c = 0; c < 3; c++) p[c] = __fma_rn(beta, v[c].y, v[c].x);
+            for (int c = 0; c < 3; c++) p[c] = MG == 2 ? v[c].x : __fma_rn(beta, v[c].y, v[c].x);
             q[0] += lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
             q[1] += lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
             q[2] += lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
-            if constexpr (MG) {
+            if constexpr (MG == 2) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];          // w = A z of the row
+            } else if constexpr (MG == 1) {
                 lrow = l;
                 orow = o;
 #pragma unroll
@@ -1112,7 +1161,9 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             }
         }
     }
-    if constexpr (MG) {
+    if constexpr (MG == 2) {
+        return;
+    } else if constexpr (MG == 1) {
         if (!G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
         if (hv >= 0) {
             // thread a < dim: component a of the vertex (k_sp_update's heavy arithmetic; r through
@@ -1304,6 +1355,120 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
     }
 }
 
+// Sharded single-reduction chain (Chronopoulos & Gear's CG): the update of iteration it from the
+// all-reduced record xb = [gamma = r.z, r.r, delta = z.Az, heavy sums of A z]:
+//   beta = gamma / gamma_prev, alpha = gamma / (delta - beta gamma / alpha_prev)   (it 0: beta 0, gamma / delta)
+//   p = z + beta p, s = w + beta s (w = A z: rows from phase 2, heavy from xb + lam z),
+//   x += alpha p, r -= alpha s, z = M r, partial (r.z, r.r); the boundary rows' (z, p) into the send
+//   buffer (slots snd_off[l] .. snd_off[l + 1] of own row l).
+// In exact arithmetic the iterates are CG's; the one reduction per iteration carries the next
+// iteration's dots with this one's product.  The stop test (r.r <= tol^2 r0.r0, the budget,
+// breakdown) is decided here from the reduced values, the same on every rank and in every workgroup;
+// tail = 1 only records the state of iteration it.
+__global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update_sd(int it, const SpDev G, double lam, int tail) {
+    __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
+    __shared__ double red[2][3 * kSpUpdRows / 64];
+    if (G.rec[0] != 0.0) return;
+    const double gamma = G.xb[0], rr = G.xb[1], delta = G.xb[2];
+    const double rr0 = it == 0 ? rr : G.red[1];
+    double beta = 0.0, alpha = 0.0;
+    int st = 0;
+    if (rr <= G.tol2 * rr0) st = kSpConverged;
+    else if (it >= G.max_it) st = kSpBudget;
+    else {
+        double den = delta;
+        if (it > 0) {
+            beta = gamma / G.red[(int64_t)kSpRed * (it - 1)];
+            den = delta - beta * gamma / G.red[(int64_t)kSpRed * (it - 1) + 3];
+        }
+        alpha = gamma / den;
+        if (!(den > 0.0) || !isfinite(alpha) || !isfinite(beta)) st = kSpBreakdown;
+    }
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (blockIdx.x == 0 && t == 0) {
+        double *rk = G.red + (int64_t)kSpRed * it;
+        rk[0] = gamma; rk[1] = rr; rk[3] = alpha; rk[4] = delta;
+        if (st) record_stop(G, it, st);
+    }
+    if (st || tail) return;
+    constexpr int nw = 3 * kSpUpdRows / 64;
+    double rz = 0.0, rr1 = 0.0;
+    const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
+    if (rb >= 0) {
+        const int l0 = rb * kSpUpdRows;
+        const int nrow = min(kSpUpdRows, G.nown - l0);
+        const int64_t o0 = G.hd + 3 * (int64_t)(G.row0 + l0);
+        const bool on = t < 3 * nrow;
+        double z = 0.0, pp = 0.0, w = 0.0, sp = 0.0, x = 0.0, r = 0.0;
+        if (on) {
+            const double2 v = G.zp[o0 + t];
+            z = v.x; pp = v.y;
+            w = G.q[o0 + t];
+            sp = G.sv[o0 + t];
+            x = G.x[o0 + t];
+            r = G.r[o0 + t];
+        }
+        const double *Mg = G.Mv + 6 * (int64_t)l0;
+        if (t < 6 * nrow) sM[t] = Mg[t];
+        if (t + 3 * kSpUpdRows < 6 * nrow) sM[t + 3 * kSpUpdRows] = Mg[t + 3 * kSpUpdRows];
+        const double p = it > 0 ? z + beta * pp : z;
+        const double s_ = it > 0 ? w + beta * sp : w;
+        x += alpha * p;
+        r -= alpha * s_;
+        sR[t] = r;
+        __syncthreads();
+        if (on) {
+            const int row = t / 3, a = t - 3 * row;
+            const double *M = sM + 6 * row, *rv = sR + 3 * row;
+            const int i0 = a == 0 ? 0 : a == 1 ? 1 : 3, i1 = a == 0 ? 1 : a == 1 ? 2 : 4, i2 = a == 0 ? 3 : a == 1 ? 4 : 5;
+            const double zn = M[i0] * rv[0] + M[i1] * rv[1] + M[i2] * rv[2];
+            G.x[o0 + t] = x;
+            G.r[o0 + t] = r;
+            G.sv[o0 + t] = s_;
+            G.zp[o0 + t] = make_double2(zn, p);
+            sd_send(G, l0 + row, a, zn, p);
+            rz = r * zn;
+            rr1 = r * r;
+        }
+    } else if (t < 256) {
+        for (int h = t; h < G.Q + G.S; h += 256) {
+            const int o = heavy_dof(G, h);
+            const int dim = h < G.Q ? 6 : 1;
+            double r[6], p[6];
+            for (int a = 0; a < dim; a++) {
+                const double2 v = G.zp[o + a];
+                const double w = G.xb[3 + o + a] + lam * v.x;
+                p[a] = it > 0 ? v.x + beta * v.y : v.x;
+                const double s_ = it > 0 ? w + beta * G.sv[o + a] : w;
+                G.sv[o + a] = s_;
+                G.x[o + a] += alpha * p[a];
+                r[a] = G.r[o + a] - alpha * s_;
+                G.r[o + a] = r[a];
+            }
+            const double *M = h < G.Q ? G.Mh + 36 * (int64_t)h : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+            for (int a = 0; a < dim; a++) {
+                double z = 0.0;
+                for (int c = 0; c < dim; c++) z += M[a * dim + c] * r[c];
+                G.zp[o + a] = make_double2(z, p[a]);
+                rz += r[a] * z;
+                rr1 += r[a] * r[a];
+            }
+        }
+        if (!G.include_heavy) rz = rr1 = 0.0;
+    }
+    rz = wave_sum(rz);
+    rr1 = wave_sum(rr1);
+    if (lane == 0) { red[0][wv] = rz; red[1][wv] = rr1; }
+    __syncthreads();
+    if (t == 0) {
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
+        G.upart[2 * slot] = s0;
+        G.upart[2 * slot + 1] = s1;
+    }
+}
+
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
 __global__ void k_sp_pack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ src,
                           double *__restrict__ buf) {
@@ -1382,25 +1547,35 @@ void sp_launch_dots(const SpDev &G, int it, hipStream_t st) {
 }
 
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st) {
+    if (G.sd) {
+        // sharded single-reduction chain: [m_nx heavy-z / row-term workgroups][phase-1 blocks];
+        // [m_nh heavy-sum / scalar workgroups][row blocks]
+        const int g1 = sp_merged_grid1(G), g2 = G.m_nh + sp::row_grid(G.nrb);
+        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 2>), g1, it, G, G.Ja32, lambda);
+        else SPL("sp_phase1", (sp::k_sp_phase1<double, 2>), g1, it, G, G.Ja, lambda);
+        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 2>), g2, it, G, lambda, (const float *)G.pj32);
+        else SPL("sp_phase2", (sp::k_sp_phase2<double, 2>), g2, it, G, lambda, (const double *)G.pj);
+        return;
+    }
     if (G.merged) {
         // [m_nx heavy-p / row-term workgroups][phase-1 blocks]; [m_nh heavy workgroups][row blocks]
         // (both extra counts multiples of 8, so the blocks keep their XCD)
         const int g1 = sp_merged_grid1(G), g2 = sp_merged_grid2(G);
-        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, true>), g1, it, G, G.Ja32, lambda);
-        else SPL("sp_phase1", (sp::k_sp_phase1<double, true>), g1, it, G, G.Ja, lambda);
+        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 1>), g1, it, G, G.Ja32, lambda);
+        else SPL("sp_phase1", (sp::k_sp_phase1<double, 1>), g1, it, G, G.Ja, lambda);
         if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
-        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, true>), g2, it, G, lambda, (const float *)G.pj32);
-        else SPL("sp_phase2", (sp::k_sp_phase2<double, true>), g2, it, G, lambda, (const double *)G.pj);
+        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 1>), g2, it, G, lambda, (const float *)G.pj32);
+        else SPL("sp_phase2", (sp::k_sp_phase2<double, 1>), g2, it, G, lambda, (const double *)G.pj);
         return;
     }
     if (G.nblk > 0) {
-        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, false>), G.nblk, it, G, G.Ja32, lambda);
-        else SPL("sp_phase1", (sp::k_sp_phase1<double, false>), G.nblk, it, G, G.Ja, lambda);
+        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 0>), G.nblk, it, G, G.Ja32, lambda);
+        else SPL("sp_phase1", (sp::k_sp_phase1<double, 0>), G.nblk, it, G, G.Ja, lambda);
     }
     // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) before the row blocks
     const int grid = sp::row_grid(G.nrb) + (G.fuse_heavy ? G.Q + G.S : 0);
-    if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, false>), grid, it, G, lambda, (const float *)G.pj32);
-    else SPL("sp_phase2", (sp::k_sp_phase2<double, false>), grid, it, G, lambda, (const double *)G.pj);
+    if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 0>), grid, it, G, lambda, (const float *)G.pj32);
+    else SPL("sp_phase2", (sp::k_sp_phase2<double, 0>), grid, it, G, lambda, (const double *)G.pj);
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }
@@ -1410,6 +1585,13 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
     // stage 1 over one workgroup per heavy vertex when the vertices have many blocks
     const int grid = (stage == 1 && G.heavy_split) ? G.Q + G.S + 1 : 1;
     SPL("sp_heavy", sp::k_sp_heavy, grid, it, G, lambda, stage);
+}
+
+void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st) {
+    const int grid = (G.nown + kSpUpdRows - 1) / kSpUpdRows + 1;
+    hipEvent_t e0_ = prof_begin(st);
+    hipLaunchKernelGGL(sp::k_sp_update_sd, dim3(grid), dim3(3 * kSpUpdRows), 0, st, it, G, lambda, tail);
+    prof_end("sp_update", e0_, (unsigned)grid, 0.0, st);
 }
 
 void sp_launch_update(const SpDev &G, int it, hipStream_t st) {

@@ -70,8 +70,8 @@ void quat_mat(const double *q, double *R) {
         if (e_ != hipSuccess) return fail(DEFTRI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
-SpSolver::SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr)
-    : dev_(device), st_(st), rank_(rank), nranks_(nranks), tr_(tr) {
+SpSolver::SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr, bool force_sharded)
+    : dev_(device), st_(st), rank_(rank), nranks_(nranks), tr_(tr), shard_(nranks > 1 || (force_sharded && tr)) {
     hipHostMalloc((void **)&hpin, 32 * sizeof(double), hipHostMallocDefault);
     hipHostMalloc((void **)&ipin, 16 * sizeof(int), hipHostMallocDefault);
     for (int i = 0; i < 32; i++) hpin[i] = 0.0;
@@ -253,7 +253,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     {
         static const bool no_fuse = std::getenv("DEFTRI_SP_NO_FUSE") != nullptr;
         const int64_t heavy_parts = H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back();
-        G.fuse = (nranks_ == 1 && !no_fuse) ? 1 : 0;
+        G.fuse = (!shard_ && !no_fuse) ? 1 : 0;
         G.fuse_heavy = (G.fuse && heavy_parts <= kSpFuseHeavyMax && Q + S <= 64) ? 1 : 0;
         static const bool fence = std::getenv("DEFTRI_SP_FENCE") != nullptr;
         G.fence = fence ? 1 : 0;
@@ -270,6 +270,11 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.m_nh = 8 * ((Q + S + 7) / 8);
         static const bool ak = std::getenv("DEFTRI_SP_ALPHA_KERNEL") != nullptr;
         G.alpha_kernel = ak ? 1 : 0;
+        // sharded: the single-reduction chain (3 launches + one all-reduce per CG iteration);
+        // DEFTRI_SP_TWO_REDUCTIONS=1 keeps the round-3 six-launch chain for A/Bs
+        static const bool two_red = std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
+        G.sd = (shard_ && !two_red) ? 1 : 0;
+        if (G.sd) G.m_nh = 8 * ((Q + S + 2 + 7) / 8);   // + the z.Az and (r.z, r.r) workgroups
     }
     {
         int32_t *rm, *pm, *pi;
@@ -288,8 +293,12 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.Mh, 36 * (int64_t)Q + S);
     ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(G.nrb, 1));
     ALLOC(G.r, G.ndof); ALLOC(G.q, G.ndof); ALLOC(G.x, G.ndof);
+    // zp: [heavy][rows][receive region: the halo rows, 3 dofs each, in the concatenated receive order]
+    int64_t nrecv = 0;
+    for (const auto &v : H.recv_rows) nrecv += (int64_t)v.size();
+    const int64_t zp_n = G.ndof + (G.sd ? 3 * nrecv : 0);
     double *zp;
-    ALLOC(zp, 2 * G.ndof);
+    ALLOC(zp, 2 * zp_n);
     G.zp = reinterpret_cast<double2 *>(zp);
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -327,7 +336,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     }
     G.red = G.rec + kSpRecDoubles;
     SPOK(hipMemset(G.x, 0, sizeof(double) * (size_t)G.ndof));     // rows no solve writes stay 0
-    SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)G.ndof));
+    SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)zp_n));
     SPOK(hipMemset(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (kSpMaxIt + 2))));
     ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1); ALLOC(d_sumcnt, 16);
     SPOK(hipMemset(d_flag, 0, sizeof(int)));
@@ -346,6 +355,41 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     }
     PUT(d_send_rows, srows); PUT(d_recv_rows, rrows);
     ALLOC(d_xbuf, 6 * (int64_t)(srows.size() + rrows.size()));
+    if (G.sd) {
+        ALLOC(G.sv, G.ndof);
+        SPOK(hipMemset(G.sv, 0, sizeof(double) * (size_t)G.ndof));
+        ALLOC(G.xb, 3 + H.hd);
+        G.sbuf = d_xbuf;                                   // the send half of the halo buffer
+        // phase 1's rows: a halo row (recv list position k, concatenated in peer order — the peers'
+        // row ranges ascend, so the concatenation is sorted) reads its (z, p) at row P + k
+        std::vector<int32_t> ap(4 * (size_t)nloc);
+        for (int64_t le = 0; le < nloc; le++)
+            for (int k = 0; k < 4; k++) {
+                const int32_t r = H.row_of_point[d.arap_pts[4 * H.arap_ids[le] + k]];
+                int32_t m = r;
+                if (r < H.lo || r >= H.hi) {
+                    const auto it = std::lower_bound(rrows.begin(), rrows.end(), r);
+                    if (it == rrows.end() || *it != r) return fail(DEFTRI_E_ARG, "iterative plan: a local edge's row is neither own nor halo");
+                    m = NP + (int32_t)(it - rrows.begin());
+                }
+                ap[4 * le + k] = m;
+            }
+        int32_t *d_ap;
+        PUT(d_ap, ap);
+        G.apts_p = d_ap;
+        // own row l -> its send slots (rows of sbuf), in the concatenated send order
+        std::vector<int32_t> so(nown + 1, 0), sl;
+        for (int32_t r : srows) so[r - H.lo + 1]++;
+        for (int32_t l = 0; l < nown; l++) so[l + 1] += so[l];
+        sl.resize(srows.size());
+        std::vector<int32_t> fill(so.begin(), so.end() - 1);
+        for (size_t k = 0; k < srows.size(); k++) sl[fill[srows[k] - H.lo]++] = (int32_t)k;
+        int32_t *d_so, *d_sl;
+        PUT(d_so, so); PUT(d_sl, sl);
+        G.snd_off = d_so; G.snd_slot = d_sl;
+    } else {
+        G.apts_p = G.apts;
+    }
 #undef PUT
 #undef ALLOC
     SPOK(hipDeviceSynchronize());
@@ -374,6 +418,25 @@ int SpSolver::halo(int width, double *vec, bool zp) {
     if (rc) return rc;
     sp_launch_halo_unpack((int)recv_off_[nranks_], d_recv_rows, width, base, rbuf, vec, st_);
     return 0;
+}
+
+// the sd chain's halo exchange: the boundary rows' (z, p) from the send buffer k_sp_update_sd (or
+// the setup) filled straight into the peers' receive regions of zp
+int SpSolver::halo_sd() {
+    if (!shard_ || nranks_ <= 1) return 0;
+    const int64_t nsend = send_off_[nranks_];
+    double *sbuf = G.sbuf, *rbuf = reinterpret_cast<double *>(G.zp + G.ndof);
+    std::vector<SpTransport::Op> ops;
+    for (int a = 0; a < nranks_; a++)
+        for (int b = 0; b < nranks_; b++) {
+            if (a == b) continue;
+            if (a == rank_ && send_off_[b + 1] > send_off_[b])
+                ops.push_back({b, true, sbuf + 6 * send_off_[b], 6 * (send_off_[b + 1] - send_off_[b])});
+            if (b == rank_ && recv_off_[a + 1] > recv_off_[a])
+                ops.push_back({a, false, rbuf + 6 * recv_off_[a], 6 * (recv_off_[a + 1] - recv_off_[a])});
+        }
+    (void)nsend;
+    return tr_->p2p(ops, st_);
 }
 
 // computeActiveErrors (+ linearizeOplus with jac) on the rank's edges, chi2 of its owned edges into
@@ -405,13 +468,13 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
     J.total = d_scal;
     launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
     int rc;
-    if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    if (shard_ && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_);
     sp_launch_glin(G, fp32_jac != 0, st_);
-    if (nranks_ > 1 && (rc = tr_->allreduce(G.hl, 21 * (int64_t)G.Q + G.S + G.hd, 0, st_))) return rc;
+    if (shard_ && (rc = tr_->allreduce(G.hl, 21 * (int64_t)G.Q + G.S + G.hd, 0, st_))) return rc;
     if (want_max) {
         sp_launch_maxdiag(G, d_scal + 2, st_);
-        if (nranks_ > 1 && (rc = tr_->allreduce(d_scal + 2, 1, 1, st_))) return rc;
+        if (shard_ && (rc = tr_->allreduce(d_scal + 2, 1, 1, st_))) return rc;
         sp_launch_maxdiag_heavy(G, d_scal + 2, st_);
     }
     return 0;
@@ -419,25 +482,36 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
 
 // the solve's setup (preconditioner at lambda, r = rhs, (z, p) = (M r, 0), x = 0); sharded: the
 // boundary rows' (z, p) to the ranks whose edges read them, as after every CG update
-void SpSolver::cg_setup(double lambda, const double *rhs) {
+int SpSolver::cg_setup(double lambda, const double *rhs) {
     sp_launch_setup(G, rhs, lambda, st_);
-    if (nranks_ > 1) halo(6, reinterpret_cast<double *>(G.zp), true);
+    if (G.sd) return halo_sd();
+    if (shard_) return halo(6, reinterpret_cast<double *>(G.zp), true);
+    return 0;
 }
 
-// CG iterations [from, to) at lambda
-void SpSolver::cg_chain(double lambda, int from, int to) {
-    const bool dist = nranks_ > 1;
+// CG iterations [from, to) at lambda; every transport call's status is checked (a failed collective
+// must not leave the ranks iterating on stale data)
+int SpSolver::cg_chain(double lambda, int from, int to) {
+    int rc;
     for (int it = from; it < to; it++) {
+        if (G.sd) {                                    // phase 1, phase 2 (A z), one all-reduce, update
+            sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
+            if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
+            sp_launch_update_sd(G, it, lambda, 0, st_);
+            if ((rc = halo_sd())) return rc;
+            continue;
+        }
         if (G.merged) {                                // phase 1 (+ alpha), phase 2 (+ update, next dots)
             sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
             continue;
         }
+        const bool dist = shard_;
         if (!G.fuse) sp_launch_dots(G, it, st_);      // fused: the previous update's (setup's) last workgroup
-        if (dist) tr_->allreduce(G.red + (int64_t)kSpRed * it, 2, 0, st_);
+        if (dist && (rc = tr_->allreduce(G.red + (int64_t)kSpRed * it, 2, 0, st_))) return rc;
         sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
         if (dist) {
             sp_launch_heavy(G, it, lambda, 1, st_);
-            tr_->allreduce(G.hbuf, 1 + G.hd, 0, st_);
+            if ((rc = tr_->allreduce(G.hbuf, 1 + G.hd, 0, st_))) return rc;
             sp_launch_heavy(G, it, lambda, 2, st_);
         } else if (G.fuse_heavy) {
             // in k_sp_phase2's last workgroup
@@ -448,17 +522,23 @@ void SpSolver::cg_chain(double lambda, int from, int to) {
             sp_launch_heavy(G, it, lambda, 0, st_);
         }
         sp_launch_update(G, it, st_);
-        if (dist) halo(6, reinterpret_cast<double *>(G.zp), true);
+        if (dist && (rc = halo(6, reinterpret_cast<double *>(G.zp), true))) return rc;
     }
+    return 0;
 }
 
-// the state of iteration n into the record (converged / budget), no other effect
-int SpSolver::cg_tail(int n) {
-    if (!G.fuse) sp_launch_dots(G, n, st_);
-    if (nranks_ > 1) {
-        int rc = tr_->allreduce(G.red + (int64_t)kSpRed * n, 2, 0, st_);
-        if (rc) return rc;
+// the state of iteration n into the record (converged / budget), no other effect (the sd chain
+// decides it after iteration n's product and reduction: they run, the update records only)
+int SpSolver::cg_tail(int n, double lambda) {
+    int rc;
+    if (G.sd) {
+        sp_launch_product(G, n, lambda, fp32_jac != 0, st_);
+        if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
+        sp_launch_update_sd(G, n, lambda, 1, st_);
+        return 0;
     }
+    if (!G.fuse) sp_launch_dots(G, n, st_);
+    if (shard_ && (rc = tr_->allreduce(G.red + (int64_t)kSpRed * n, 2, 0, st_))) return rc;
     // k_sp_heavy stage 1 records the state of a finished solve and returns; a running one would
     // compute its sums, so the tail records through stage 1 only when the state is final: launch
     // the status-only variant (stage 3)
@@ -472,14 +552,14 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
     G.max_it = mx;
     G.tol2 = tol * tol;
     SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (mx + 2)), st_));
-    cg_setup(lambda, rhs);
+    int rc = cg_setup(lambda, rhs);
+    if (rc) return rc;
     int j = 0;
     int n = std::min(std::max(2, last_its + 1), mx);
     for (;;) {
-        cg_chain(lambda, j, n);
+        if ((rc = cg_chain(lambda, j, n))) return rc;
         j = n;
-        int rc = cg_tail(j);
-        if (rc) return rc;
+        if ((rc = cg_tail(j, lambda))) return rc;
         SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
         SPOK(hipStreamSynchronize(st_));
         const int status = (int)hpin[16];
@@ -497,7 +577,7 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
 int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(dev_);
-    const bool dist = nranks_ > 1;
+    const bool dist = shard_;
     R.n_unknowns = G.ndof;
     R.rank = rank_;
     R.nranks = nranks_;
@@ -568,11 +648,11 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 return 0;
             };
             auto t0p = std::chrono::steady_clock::now();
-            cg_setup(lambda, G.b);
+            if ((rc = cg_setup(lambda, G.b))) return rc;
             const int n = std::min(std::max(2, last_its + 1), mx);
-            cg_chain(lambda, 0, n);
+            if ((rc = cg_chain(lambda, 0, n))) return rc;
             int j = n;
-            if ((rc = cg_tail(j))) return rc;
+            if ((rc = cg_tail(j, lambda))) return rc;
             if ((rc = evaluate())) return rc;
             SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; }
@@ -587,9 +667,9 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 SPOK(hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
                 while (st == kSpRunning && j < mx) {
                     const int n2 = std::min(j + 4, mx);
-                    cg_chain(lambda, j, n2);
+                    if ((rc = cg_chain(lambda, j, n2))) return rc;
                     j = n2;
-                    if ((rc = cg_tail(j))) return rc;
+                    if ((rc = cg_tail(j, lambda))) return rc;
                     SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
                     SPOK(hipStreamSynchronize(st_));
                     st = (int)hpin[16];
@@ -689,7 +769,7 @@ int SpSolver::chi2(double *out) {
     hipSetDevice(dev_);
     eval_chi2(true, 0, nullptr);
     int rc;
-    if (nranks_ > 1 && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
+    if (shard_ && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
     SPOK(hipStreamSynchronize(st_));
     *out = hpin[0];
@@ -792,9 +872,9 @@ int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
     if ((rc = pcg_solve(lambda, G.b, solved, its))) return rc;
     set_profiler(&prof);
     SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (G.max_it + 2)), st_));
-    cg_setup(lambda, G.b);
-    cg_chain(lambda, 0, its);
-    rc = cg_tail(its);
+    rc = cg_setup(lambda, G.b);
+    if (!rc) rc = cg_chain(lambda, 0, its);
+    if (!rc) rc = cg_tail(its, lambda);
     set_profiler(nullptr);
     if (rc) return rc;
     SPOK(hipStreamSynchronize(st_));
