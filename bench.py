@@ -12,23 +12,26 @@ solve (block-Jacobi PCG, or the multifrontal LDL^T) + update + chi2).  The scene
 reference's simulation recipe scaled to n points); the graph is built on the host once, then
 resident in HBM before the timed region starts.
 
-Multi-GPU (N > 1): N independent C2 problems, one per GPU (weak scaling, no data-path collective):
-with PCG steps a C2 LM iteration is ~3 ms and a CG iteration ~0.13 ms of latency-bound work, less than
-the latency of the halo exchange and two all-reduces a point-sharded CG iteration would need
-(DESIGN.md §7).  --sharded runs ONE C2 problem point-sharded over the N ranks with the multifrontal
-LDL^T (DistPlan, csrc/symbolic.cpp: a subtree of the nested-dissection tree per rank, separator
-fronts on the leading ranks; per LM trial RCCL send/recv of one packed contribution block, one
-forward vector and one boundary solution per rank, all-reduce of chi2 / rho denominator / pivot
-flags) — strong scaling.  The barrier and the max-over-ranks time use torch.distributed.
+Multi-GPU (N > 1, one process per GPU, RCCL): ONE problem point-sharded over the N ranks — the
+iterative plan (csrc/spcg.h): each rank owns a contiguous Morton range of point rows, per CG iteration
+three launches, one ncclAllReduce of [r.z, r.r, z.Az, the global vertices' sums] and one grouped
+send / receive of the boundary rows.  Default: weak scaling — the problem has
+N x 100k correspondences (each GPU holds a C2-sized share), value = LM iterations of that problem x N
+/ the slowest rank's time ("C2-equivalent LM iterations/s": the correspondence-iterations processed,
+in units of one C2 iteration).  --strong: the C2 problem itself split over the N ranks (value = its
+LM it/s).  --replicas: N independent C2 problems (no collective; per-problem rate).  --solver direct
+runs the sharded multifrontal LDL^T instead.  The barrier and the max-over-ranks time use
+torch.distributed.
 
-Printed roofline: the dominant kernel of the configured step solver.  PCG (default): the product,
-HBM-bound — k_mf_product (matrix-free, the default where the plan fits: per local edge its
-linearized J, W, vertex dofs and record, the incidence slots, own (z, p_prev) and (p, q); csrc/pcg.hip
-PcgMfHost::product_bytes) or k_pcg_product (assembled H: repacked slot records, heavy slots;
-PcgHost::product_bytes) — bytes per launch x active launches / their summed device time, against
-8 TB/s; `traffic` from the committed rocprofv3 PMC pass when it matches the plan.  The factorization's k_update roofline (algorithmic flops / device time, FP64 peak 78.6
-TFLOP/s, AMD's MI355X specification) is reported beside it as roofline_factorization.  Both from
-profiled trials right after the timed region, HIP events on the solver's own stream.
+Printed roofline (the iterative plan, the default): the CG iteration's kernels k_sp_phase1 +
+k_sp_phase2 (the matrix-free product with the update folded in), HBM-bound — from a profiled trial
+right after the timed region (HIP events on the solver's own stream, active launches only).  Two
+fractions of 8 TB/s: `frac` / `frac_survey` on SURVEY.md §8(d)'s minimal-traffic bytes per CG
+iteration (176 E + 48 R + 40 D + 156 P: fp32 Jacobians, one pass over the edges), and `frac_design`
+on the bytes this design actually moves (fp64 J stored column-major for phase 1 and again per slot
+for phase 2, the s_e round trip, the (z, p) pairs: the plan's own count).  `traffic` from the
+committed rocprofv3 PMC pass when it matches the plan, with the calibrated FETCH_SIZE factor
+(profiles/*_fetch_calibration.json) and `traffic_over_survey_bytes`.
 
 A "step" is one LM iteration; with PCG steps each trial is setup + CG iterations (product, heavy
 rows, update) instead of scatter + factorization + substitution.
@@ -217,6 +220,7 @@ def main_ba(args, world, rank, gpu, backend):
         f"chi2 {rep['chi2_initial']:.6e} -> {rep['chi2_final']:.6e}")
     iters = rep["iterations"]
     t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, "cuda" if backend == "nccl" else "cpu")
+    value = iters / t_max
     stats = ctx.profile_trial(rep["lambda_final"])
     # roofline: the edge linearization kernel (the dominant HBM stream): algorithmic bytes of one
     # trial's two ba_edges launches / their device time
@@ -262,11 +266,13 @@ def reduce_stats(dt, iters, trials, world, device):
     return float(v.item()), int(s[0].item()), int(s[1].item())
 
 
-def job_rate(t_max, iters):
+def job_rate(t_max, iters, units=1):
     """value and ms/step of the ARAP bench line: the LM iterations of ONE problem over the slowest
     rank's wall time — sharded, every rank ran the same iterations of the one problem; replicas, each
-    rank its own copy, so the rate is per problem (never a sum over ranks)."""
-    return iters / t_max, 1e3 * t_max / max(iters, 1)
+    rank its own copy, so the rate is per problem (never a sum over ranks).  units: the workload-sized
+    shares one iteration of the problem covers (weak scaling: N, each rank holding one share), so
+    value counts the correspondence-iterations of all ranks in units of the N = 1 iteration."""
+    return iters * units / t_max, 1e3 * t_max / max(iters, 1)
 
 
 # BASELINE workloads of the ARAP LM (SURVEY §8d): scene recipe, weights (rep, arap, depth sigma) and
@@ -330,6 +336,14 @@ def cpu_baseline_sample(wl, window, n_sample, gpu_trials_per_iter):
             "seconds_per_iteration": round(t_iter, 3), "sample_unknowns": prob.n_unknowns}
 
 
+def fetch_calibration():
+    """The committed FETCH_SIZE calibration of the access widths the CG kernels use
+    (tools/micro/fetch_calib.hip under rocprofv3, profiles/*_fetch_calibration.json), or None."""
+    for pm in sorted(ROOT.glob("profiles/*_fetch_calibration.json"), reverse=True):
+        return json.loads(pm.read_text()), pm.name
+    return None, None
+
+
 def product_roofline(stats, rep, ctx, rank):
     """Roofline of the step solver's dominant kernel from a profiled trial (HIP events on the solver
     stream): active launches only (the profiled replay launches exactly the solve's CG iterations)."""
@@ -338,12 +352,18 @@ def product_roofline(stats, rep, ctx, rank):
         its = max(p2["launches"], 1)
         by, ms = p1["bytes"] + p2["bytes"], p1["ms"] + p2["ms"]
         gbs = by / max(ms * 1e-3, 1e-12) / 1e9
+        survey = ctx.plan_info().get("survey_bytes") or 0.0
+        gbs_s = survey / max(ms / its * 1e-3, 1e-12) / 1e9
         cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update") if k in stats)
         merged = "sp_update" not in stats
         kname = ("k_sp_phase1+k_sp_phase2 (merged CG iteration: matrix-free product + p.Ap row terms + update)"
                  if merged else "k_sp_phase1+k_sp_phase2 (matrix-free product)")
-        out = {"bound": "hbm", "kernel": kname, "achieved": round(gbs, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+        out = {"bound": "hbm", "kernel": kname, "achieved": round(gbs_s, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs_s / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_basis": "SURVEY.md 8(d) B_pcg = 176E + 48R + 40D + 156P per CG iteration",
+                "survey_bytes_per_cg_iteration": survey,
+                "frac_survey": round(gbs_s / HBM_PEAK_GBS, 4),
+                "achieved_design": round(gbs, 1), "frac_design": round(gbs / HBM_PEAK_GBS, 4),
                 "traffic_unit": "bytes per product", "bytes_per_launch": by / its, "launches": its,
                 "avg_active_launch_us": round(1e3 * ms / its, 3),
                 "phase1": {"us": round(1e3 * p1["ms"] / its, 3), "bytes": p1["bytes"] / its,
@@ -352,11 +372,23 @@ def product_roofline(stats, rep, ctx, rank):
                            "gbs": round(p2["bytes"] / max(p2["ms"] * 1e-3, 1e-12) / 1e9, 1)},
                 "cg_iterations": its, "cg_iteration_us": round(1e3 * cg / its, 3), "lambda": rep["lambda_final"],
                 "rank": rank}
+        cal, cal_src = fetch_calibration()
         for pm in sorted(ROOT.glob("profiles/*_pmc_sp_product.json")):
             pj = json.loads(pm.read_text())
             if abs(pj.get("bytes_per_launch_algorithmic", -1) - out["bytes_per_launch"]) < 1e-6 * out["bytes_per_launch"]:
-                out["traffic"] = pj["traffic_bytes_per_launch"]
+                f = pj.get("fetch_bytes_per_launch_raw")
+                w = pj.get("write_bytes_per_launch")
+                if cal is not None and f is not None and w is not None:
+                    # the calibrated factors of 8-B-per-lane reads / writes (the kernels' dominant width)
+                    f = f / cal["factor_fetch_read8"]
+                    w = w / cal["factor_write8"]
+                    out["traffic"] = f + w
+                    out["traffic_calibration"] = cal_src
+                else:
+                    out["traffic"] = pj["traffic_bytes_per_launch"]
                 out["traffic_source"] = pm.name
+                if survey:
+                    out["traffic_over_survey_bytes"] = round(out["traffic"] / survey, 3)
         return out
     if "pcg_product" in stats:
         pp = stats["pcg_product"]
@@ -424,6 +456,8 @@ def main():
     ap.add_argument("--analytic", action="store_true",
                     help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
     ap.add_argument("--sharded", action="store_true", help="kept for scripts: N > 1 is point-sharded by default")
+    ap.add_argument("--strong", action="store_true",
+                    help="N > 1: the workload's own problem split over the N ranks (default: weak scaling, N x the correspondences)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: N independent problems, one per GPU; value = per-problem LM it/s")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end arapOptimization timing")
@@ -458,9 +492,11 @@ def main():
     n = args.corr or spec["n"]
     window = args.pair_window if args.pair_window >= 0 else spec.get("window", 0)
     sharded = world > 1 and not args.replicas
+    weak = sharded and not args.strong
+    n_build = n * world if weak else n        # weak: each rank's share is the workload's size
     plan = args.plan              # auto: the library's choice (iterative for PCG from 50k unknowns / sharded)
     t0 = time.perf_counter()
-    prob, prob_map = build_workload(wl, n, 1 if sharded else 1 + rank, window)
+    prob, prob_map = build_workload(wl, n_build, 1 if sharded else 1 + rank, window)
     log(f"[rank {rank}] {wl} graph built in {time.perf_counter() - t0:.1f}s: {prob.summary()}")
     ctx = capi.Context(gpu)
     if sharded:
@@ -508,7 +544,7 @@ def main():
     # one problem (sharded): every rank ran the same iterations, the job takes the slowest rank;
     # replicas: the slowest rank's time for its own problem (value = per-problem rate, never a sum)
     t_max, _, _ = reduce_stats(dt, iters, rep["trials_total"], world, red_dev)
-    value, ms_per_step = job_rate(t_max, iters)
+    value, ms_per_step = job_rate(t_max, iters, world if weak else 1)
 
     # profiled trial (HIP events on the solver stream) at the final lambda of the timed run (a
     # collective on a sharded context: each rank times its own part of the same trial)
@@ -546,7 +582,7 @@ def main():
         log(f"cpu baseline {time.perf_counter() - t0:.1f}s: {cpu}")
 
     e2e = None
-    if world == 1 and not args.no_e2e and wl == "c2" and REGIME == "simulation":
+    if world == 1 and not args.no_e2e and wl == "c2" and REGIME == "simulation" and n == 100000:
         def configure(c):
             c.set_plan(args.plan)
             c.set_jacobian_storage(1 if args.jacobian_fp32 else 0)
@@ -558,12 +594,14 @@ def main():
     if rank == 0:
         workload = (("C2" if n == 100000 else f"two-view-{n}") + ("" if REGIME == "simulation" else f"-{REGIME}")) if wl == "c2" else \
             (wl.upper() if n == spec["n"] else f"{wl.upper()}-slice-{n}x{spec['k']}")
+        if weak:
+            workload += f" x {world} (one problem of {n_build} correspondences per keyframe, point-sharded: {n} per GPU)"
         out = {
             "metric": (BASELINE_METRIC if REGIME == "simulation" else f"LM iterations/sec + ms/iter at 100k corr x 2 views, {REGIME} weights")
             if wl == "c2" else f"LM iterations/sec + ms/iter, {wl.upper()}: {spec['desc']}",
             "value": value, "unit": "LM iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak" if (world > 1 and not sharded) else "strong", "vs_baseline": None, "dtype": "f64",
+            "scaling": "weak" if (world > 1 and (weak or not sharded)) else "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": workload, "correspondences_per_keyframe": n, "keyframes": spec["k"],
                        "pairs": prob.n_pairs, "pair_window": window,
@@ -581,8 +619,12 @@ def main():
                        "lambda_final": rep["lambda_final"],
                        "own_rows_rank0": info.get("own_rows"), "halo_rows_rank0": info.get("halo_rows"),
                        "parallelism": (f"points{world}" if sharded else f"replicas{world}") if world > 1 else "single",
-                       "value_semantics": "one problem, all ranks" if (world == 1 or sharded)
-                       else "per-problem LM it/s of N independent problems (not summed)"},
+                       "value_semantics": "one problem, all ranks" if (world == 1 or (sharded and not weak))
+                       else ("LM iterations/s of the N x sized problem x N (C2-equivalent iterations/s)" if weak
+                             else "per-problem LM it/s of N independent problems (not summed)"),
+                       "cg_launches_per_iteration": info.get("cg_launches"),
+                       "cg_collectives_per_iteration": info.get("cg_collectives"),
+                       "lm_control": "host" if os.environ.get("DEFTRI_HOST_LM") or sharded else "device"},
             "roofline": roofline,
             "roofline_factorization": roofline_f if roofline is not roofline_f else None,
             "cpu_baseline": cpu,

@@ -15,8 +15,9 @@ def _worker(rank, world, port, q):
     # the sharded ARAP line: both ranks ran the same 5 iterations of one problem
     t1, _, _ = bench.reduce_stats(0.020 + 0.005 * rank, 5, 9, world, "cpu")
     value, ms = bench.job_rate(t1, 5)
+    weak, _ = bench.job_rate(t1, 5, world)          # weak scaling: world shares per iteration
     dist.barrier()
-    q.put((rank, t, it, tr, value, ms))
+    q.put((rank, t, it, tr, value, ms, weak))
     dist.destroy_process_group()
 
 
@@ -31,10 +32,12 @@ def test_reduce_stats_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, t, it, tr, value, ms in out:
+    for rank, t, it, tr, value, ms, weak in out:
         assert t == pytest.approx(1.5) and it == 10 and tr == 25
         # value = iterations of the one problem over the slowest rank's time (not a sum over ranks)
         assert value == pytest.approx(5 / 0.025) and ms == pytest.approx(5.0)
+        # weak scaling: the problem has 2 C2-sized shares, so one of its iterations counts twice
+        assert weak == pytest.approx(2 * 5 / 0.025)
 
 
 def test_reduce_stats_single():

@@ -265,6 +265,7 @@ def test_sharded_iterative_matches_oracle(kind, world):
     for r in range(world):
         info = out[r][0]
         assert info["plan"] == "iterative" and info["nranks"] == world and info["halo_rows"] > 0
+        assert info["sharded"] == 1 and info["cg_launches"] == 3 and info["cg_collectives"] == 1
     # the sharded chain (single-reduction CG, sums split over the ranks) against exact steps: the
     # step differences are ~kappa * 1e-12 and the LM iterations amplify them
     for analytic, tol in ((True, 1e-8), (False, 1e-6)):
@@ -391,3 +392,42 @@ def test_merged_chain_breakdown_then_solve():
     finally:
         a.close()
         b.close()
+
+
+def test_rccl_one_rank_sharded_chain():
+    """The production transport on the one-GPU box: an RCCL communicator of one rank puts the
+    iterative plan on the sharded control flow — the single-reduction CG chain (3 launches and one
+    ncclAllReduce per CG iteration), chi2 / H / trial scalars through ncclAllReduce on the solver
+    stream — against the oracle's LM."""
+    p = tv_problem(4000, seed=2)
+    c = capi.Context(0)
+    try:
+        c.dist_init_rccl(1, 0, capi.rccl_unique_id())
+        c.set_plan("iterative")
+        c.set_linear_solver("pcg", max_iterations=4096)
+        c.upload(p)
+        info = c.plan_info()
+        assert info["plan"] == "iterative" and info["sharded"] == 1
+        assert info["cg_launches"] == 3 and info["cg_collectives"] == 1
+        for analytic, tol in ((True, 1e-8), (False, 1e-6)):
+            c.reset_state()
+            r = c.solve_lm(4, analytic=analytic)
+            pts, sc, tg = c.download()
+            res = oracle_lm(p, 4, analytic)
+            ref = res["report"]
+            assert r["iterations"] == ref["iterations"] and r["trials_iter"] == ref["trials_iter"]
+            np.testing.assert_allclose(r["chi2_iter"], ref["chi2_iter"], rtol=tol)
+            assert r["pcg_fallbacks"] == 0
+            assert np.abs(pts - res["points"]).max() <= 10 * tol * np.abs(res["points"]).max()
+    finally:
+        c.close()
+
+
+def test_device_lm_matches_host_lm():
+    """The device-driven LM (k_lm_decide: rho, accept / reject, lambda / nu, g2o's Terminate test in
+    HBM; the host queues trial slots without reading each outcome) against the host loop
+    (DEFTRI_HOST_LM=1): the same decisions from the same sums — bit-identical LM runs."""
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{}, {"DEFTRI_HOST_LM": "1"}])
+    assert l0 == l1 == 2
+    assert c0 == c1 and t0 == t1 and i0 == i1
+    assert s0 == s1

@@ -33,6 +33,9 @@ struct DevProblem {
     int64_t jarap_ld = 0;       // 0: J per edge contiguous ([E][18], the multifrontal plan's kernels);
                                 // > 0: column-major [18][jarap_ld] (the iterative plan: coalesced loads)
     double *tg_pre = nullptr;   // per pair: T_g and its 12 numeric-Jacobian perturbations (k_arap_pre)
+    // device-driven LM (spcg_solver.cpp, one rank): kernels return at once when their gate word is 0 —
+    // gate_lin for the linearization's launches, gate_trial for a trial's; nullptr: always run
+    const int *gate_lin = nullptr, *gate_trial = nullptr;
 };
 
 struct FrontDev {
@@ -135,6 +138,33 @@ void launch_solve(const DevPlan &L, const double *rhs, double *x, hipStream_t st
 void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, const int *flag = nullptr);
 // a trial's prologue: state backup (restore: the state restored from the backup), zero-pivot flag and
 // nzero doubles at `zero` cleared, one launch
+// The device-driven LM (one rank, iterative plan; spcg_solver.cpp SpSolver::solve_lm_dev): the
+// variables of g2o's OptimizationAlgorithmLevenberg::solve (reference g2oBundleAdjustment.cc:959-962,
+// SURVEY Appendix A) in HBM, so the host queues trial slots without reading each trial's outcome.
+// A slot = [linearization (gate_lin)] [prologue] [setup + CG + evaluation (gate_trial)] [decide].
+struct LmState {
+    double lam, ni, cur, rho;            // _currentLambda, _ni, currentChi, the last trial's rho
+    int32_t gate_trial, gate_lin;        // the next slot's gates (read by every gated kernel)
+    int32_t it, q;                       // LM iteration, trials of it so far (g2o's qmax)
+    int32_t stop;                        // 0 running, 1 n_iterations done, 2 g2o Terminate, 3 PCG step unfinished
+    int32_t restore;                     // the last trial was rejected: the next prologue restores the state
+    int32_t need_lin;                    // the next slot starts a new iteration
+    int32_t slot;                        // the enqueue index of the last slot decided
+    int32_t trials_total, trials_rejected, pcg_trials, pcg_fail;
+    int32_t last_its, n_it, max_trials, stop_slot;   // stop_slot: the enqueue index that set stop
+    int64_t pcg_iterations;
+};
+// the device-driven LM's prologue: gate_trial 0 -> nothing; else the backup (or, restore != 0,
+// the restore) and the cleared records, as launch_trial_begin; thread 0 also folds the linearization
+// just run (gate_lin) into the LM state: current chi2 = scal[0], and at iteration 0 lambda = tau max diag
+void launch_trial_begin_dev(const DevProblem &P, int *flag, double *zero, int64_t nzero, LmState *lm, const double *scal,
+                            double tau, double user_lambda, hipStream_t st);
+// the device-driven LM's decision after a slot's evaluation (one thread): rho, accept / reject, the
+// lambda / nu update, g2o's loop and Terminate conditions, the per-iteration report, the next slot's
+// gates; a PCG step still running stops the slots for the host (stop 3).  A copy of the state goes
+// to pinned host memory (`snap`).  `slot`: the enqueue index (-1 for the host's continuation).
+void launch_lm_decide(LmState *lm, const double *scal, const double *rec, double *chi_it, int32_t *trials_it, int max_report,
+                      LmState *snap, int slot, hipStream_t st);
 void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st,
                         bool restore = false);
 // a trial's read-back: ns scalars, the flag and (rec != nullptr) nrec record values into pinned host memory
@@ -145,9 +175,11 @@ void launch_sum(int64_t n, const double *a, const double *b, double lambda, int 
 // several fixed-order sums in two launches (the per-array arithmetic of launch_sum: the same
 // partials and final butterfly), optionally total = (out0 + out2) + out1 — the order launch_sum's
 // three-value pass adds them in
-struct SumJob { int64_t n = 0; const double *a = nullptr, *b = nullptr, *w = nullptr; double lambda = 0; int mode = 0; double *out = nullptr; };
+// lambda_dev (when set) replaces lambda: the damping the device-driven LM keeps in HBM
+struct SumJob { int64_t n = 0; const double *a = nullptr, *b = nullptr, *w = nullptr; double lambda = 0; int mode = 0; double *out = nullptr;
+                const double *lambda_dev = nullptr; };
 constexpr int kMaxSumJobs = 4;
-struct SumJobs { SumJob j[kMaxSumJobs]; int nj = 0; double *total = nullptr; };
+struct SumJobs { SumJob j[kMaxSumJobs]; int nj = 0; double *total = nullptr; const int *gate = nullptr; };
 void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st);
 // the trial read-back (k_trial_readback) folded into launch_sum_multi_fused's last workgroup
 struct ReadBack {

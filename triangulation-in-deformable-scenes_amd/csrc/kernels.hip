@@ -167,7 +167,8 @@ __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i,
 // once per pair here: per pair kArapPre x (rotation matrix 9, translation 3), transformation 0 the
 // unperturbed one, 1 + 2d / 2 + 2d the +delta / -delta perturbations of twist coordinate d.
 constexpr int kArapPre = 13;
-__global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restrict__ pre) {
+__global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restrict__ pre, const int *gate) {
+    if (gate && !*gate) return;
     const int t = TID;
     if (t >= Q * kArapPre) return;
     const int q = t / kArapPre, k = t % kArapPre;
@@ -292,7 +293,8 @@ __global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *
                           const double *__restrict__ points, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, const float *__restrict__ kb8,
                           double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
-                          double *__restrict__ chi, int want_jac) {
+                          double *__restrict__ chi, int want_jac, const int *gate) {
+    if (gate && !*gate) return;
     lin_rep_edge(TID, R, rp, rc, obs, info, hdelta, points, cam_pose, cam_R, kb8, J, W, E, chi, want_jac);
 }
 
@@ -301,7 +303,8 @@ __global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t 
                           const double *__restrict__ info, const double *__restrict__ points,
                           const double *__restrict__ scales, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
-                          double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+                          double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic, const int *gate) {
+    if (gate && !*gate) return;
     lin_dep_edge(TID, D, dpt, dsc, dcam, meas, info, points, scales, cam_pose, cam_R, J, W, E, chi, want_jac, analytic);
 }
 
@@ -315,7 +318,8 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
                            const double *__restrict__ tg, const double *__restrict__ tg_pre,
                            double *__restrict__ J, double *__restrict__ W,
                            double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
-                           int64_t jld) {
+                           int64_t jld, const int *gate) {
+    if (gate && !*gate) return;
     lin_arap_edge<MODE>(TID, E_, apts, apair, arot, aw, rot, parea, pinfo, points, tg, tg_pre, J, W, E, chi, want_jac,
                         analytic, jld);
 }
@@ -323,6 +327,7 @@ __global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restr
 // the errors and chi2 of every reprojection, depth and ARAP edge in one launch (the trial's
 // evaluation): the same per-edge code as k_lin_rep / k_lin_dep / k_lin_arap<0>, block ranges by type
 __global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, int nbd) {
+    if (P.gate_trial && !*P.gate_trial) return;
     const int b = blockIdx.x, t = threadIdx.x;
     if (b < nbr)
         lin_rep_edge(b * 128 + t, P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose,
@@ -1398,9 +1403,11 @@ __global__ void __launch_bounds__(256) k_bwd_chain(int ntask, const int32_t *__r
 // ------------------------------------------------------------------------------------------
 // skipped when the factorization flagged a zero pivot (the trial is rejected and the state restored)
 __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
-                               double *__restrict__ scales, double *__restrict__ tg, const int *__restrict__ flag) {
+                               double *__restrict__ scales, double *__restrict__ tg, const int *__restrict__ flag,
+                               const int *gate) {
     int i = TID;
     if (flag && *flag) return;
+    if (gate && !*gate) return;
     int64_t pbase = 6 * (int64_t)Q + S;
     if (i < P) {
         points[3 * (int64_t)i] += dx[pbase + 3 * (int64_t)i];
@@ -1433,6 +1440,93 @@ __global__ void __launch_bounds__(256) k_trial_begin(int P, int S, int Q, const 
         if (i < nzero) zero[i] = 0.0;
         if (i == 0) *flag = 0;
     }
+}
+
+// the device-driven LM's prologue (kernels.h LmState): k_trial_begin's work in the direction the last
+// decision chose, gated; thread 0 folds the linearization that ran before it into the state
+__global__ void __launch_bounds__(256) k_trial_begin_dev(int P, int S, int Q, double *__restrict__ points,
+                                                         double *__restrict__ scales, double *__restrict__ tg,
+                                                         double *__restrict__ points_bak, double *__restrict__ scales_bak,
+                                                         double *__restrict__ tg_bak, int *__restrict__ flag,
+                                                         double *__restrict__ zero, int64_t nzero, int64_t n, LmState *lm,
+                                                         const double *__restrict__ scal, double tau, double user_lambda) {
+    if (!lm->gate_trial) return;
+    const bool restore = lm->restore != 0;
+    if (TID == 0 && lm->gate_lin) {
+        lm->cur = scal[0];                       // currentChi of the new linearization point
+        if (lm->it == 0) {                       // g2o: lambda = tau * max diag H at iteration 0
+            lm->lam = user_lambda > 0 ? user_lambda : tau * scal[2];
+            lm->ni = 2.0;
+        }
+    }
+    const double *sp = restore ? points_bak : points, *ss = restore ? scales_bak : scales, *stg = restore ? tg_bak : tg;
+    double *dp = restore ? points : points_bak, *ds = restore ? scales : scales_bak, *dtg = restore ? tg : tg_bak;
+    for (int64_t i = TID; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < 3 * (int64_t)P) dp[i] = sp[i];
+        if (i < S) ds[i] = ss[i];
+        if (i < 7 * (int64_t)Q) dtg[i] = stg[i];
+        if (i < nzero) zero[i] = 0.0;
+        if (i == 0) *flag = 0;
+    }
+}
+
+// the device-driven LM's decision (one thread; spcg_solver.cpp solve_lm_dev's host loop restated)
+__global__ void k_lm_decide(LmState *lm, const double *__restrict__ scal, const double *__restrict__ rec,
+                            double *__restrict__ chi_it, int32_t *__restrict__ trials_it, int max_report, LmState *snap,
+                            int slot) {
+    if (threadIdx.x != 0 || !lm->gate_trial) return;
+    LmState L = *lm;
+    const int st = (int)rec[0];
+    if (st == 0) {                               // the step needs more CG iterations than queued: the host's
+        L.stop = 3;
+        L.stop_slot = slot;
+        L.gate_trial = L.gate_lin = 0;
+        *lm = L;
+        *snap = L;
+        return;
+    }
+    const bool solved = st == 1;                 // kSpConverged (spcg.h)
+    L.pcg_iterations += (int64_t)rec[1];
+    if (solved) { L.pcg_trials++; L.last_its = (int)rec[1]; }
+    else L.pcg_fail++;
+    const double tempChi = solved ? scal[0] : 1.7976931348623157e308;
+    double rho = L.cur - tempChi;
+    const double scale = (solved ? scal[1] : 0.0) + 1e-3;
+    rho /= scale;
+    L.trials_total++;
+    bool broke = false;
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        const double scaleFactor = fmax(1. / 3., alpha);
+        L.lam *= scaleFactor;
+        L.ni = 2;
+        L.cur = tempChi;
+        L.restore = 0;
+    } else {
+        L.lam *= L.ni;
+        L.ni *= 2;
+        L.restore = 1;
+        L.trials_rejected++;
+        broke = !isfinite(L.lam);
+    }
+    L.q++;
+    L.rho = rho;
+    L.need_lin = 0;
+    if (broke || !(rho < 0 && L.q < L.max_trials)) {     // the iteration's trial loop ends
+        if (L.it < max_report) { chi_it[L.it] = L.cur; trials_it[L.it] = L.q; }
+        const bool term = L.q == L.max_trials || rho == 0 || !isfinite(L.lam);
+        L.it++;
+        L.q = 0;
+        L.need_lin = 1;
+        if (term) { L.stop = 2; L.stop_slot = slot; }
+        else if (L.it >= L.n_it) { L.stop = 1; L.stop_slot = slot; }
+    }
+    L.slot = slot;
+    L.gate_trial = L.stop == 0 ? 1 : 0;
+    L.gate_lin = (L.gate_trial && L.need_lin) ? 1 : 0;
+    *lm = L;
+    *snap = L;
 }
 
 // a trial's read-back in one launch (in place of two or three copies): the scalars, the zero-pivot
@@ -1500,6 +1594,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_partial(const SumJobs J, doub
 // k_trial_readback's copies into pinned host memory.  *cnt is 0 between launches.
 __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt, int flat,
                                                          const ReadBack rb) {
+    if (J.gate && !*J.gate) return;
     const SumJob &jb = J.j[blockIdx.y];
     __shared__ double red[256];
     __shared__ int last;
@@ -1508,6 +1603,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
     int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
     double acc = 0.0;
     const int mode = jb.mode;
+    const double lam = jb.lambda_dev ? *jb.lambda_dev : jb.lambda;
     // k_sum_multi_partial's strided order (blockDim 256), eight (mode 0) / four elements' loads in
     // flight per step, added in order
     int64_t i = lo + threadIdx.x;
@@ -1530,12 +1626,12 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
             }
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                acc += (mode == 1) ? v[u] * (jb.lambda * v[u] + bb[u]) : v[u] * (jb.lambda * ww[u] * v[u] + bb[u]);
+                acc += (mode == 1) ? v[u] * (lam * v[u] + bb[u]) : v[u] * (lam * ww[u] * v[u] + bb[u]);
         }
     }
     for (; i < hi; i += 256) {
         double v = jb.a[i];
-        acc += (mode == 0) ? v : (mode == 1) ? v * (jb.lambda * v + jb.b[i]) : v * (jb.lambda * jb.w[i] * v + jb.b[i]);
+        acc += (mode == 0) ? v : (mode == 1) ? v * (lam * v + jb.b[i]) : v * (lam * jb.w[i] * v + jb.b[i]);
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -1796,21 +1892,21 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
     if (P.R > 0)
         LAUNCH("lin_rep", dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), st, P.R, P.rep_point, P.rep_cam,
                            P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose, P.cam_R, P.cam_kb8, P.Jrep,
-                           P.Wrep, P.Erep, P.chi_rep, want_jac ? 1 : 0);
+                           P.Wrep, P.Erep, P.chi_rep, want_jac ? 1 : 0, P.gate_lin);
     if (P.D > 0)
         LAUNCH("lin_dep", dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), st, P.D, P.dep_point, P.dep_scale,
                            P.dep_cam, P.dep_meas, P.dep_info, P.points, P.scales, P.cam_pose, P.cam_R, P.Jdep,
-                           P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0);
+                           P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0, P.gate_lin);
     const bool pre = want_jac && !analytic && P.E > 0;   // the numeric Jacobians read the pair table
     if (pre)
         LAUNCH("arap_pre", dev::k_arap_pre, dim3(nb((int64_t)P.Q * dev::kArapPre, 64)), dim3(64), st, P.Q, P.tg,
-               P.tg_pre);
+               P.tg_pre, P.gate_lin);
     if (P.E > 0)
         LAUNCH("lin_arap", (!want_jac ? dev::k_lin_arap<0> : analytic ? dev::k_lin_arap<1> : dev::k_lin_arap<2>),
                            dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
                            P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg,
                            pre ? P.tg_pre : nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, want_jac ? 1 : 0,
-                           analytic ? 1 : 0, P.jarap_ld);
+                           analytic ? 1 : 0, P.jarap_ld, P.gate_lin);
 }
 
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
@@ -2013,7 +2109,7 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, 
     if (P.Q > n) n = P.Q;
     if (n > 0)
         LAUNCH("update_state", dev::k_update_state, dim3(nb(n, 128)), dim3(128), st, P.P, P.S, P.Q, dx, P.points,
-                           P.scales, P.tg, flag);
+                           P.scales, P.tg, flag, P.gate_trial);
 }
 
 void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st, bool restore) {
@@ -2026,6 +2122,20 @@ void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nz
     else
         LAUNCH("trial_begin", dev::k_trial_begin, dim3(grid), dim3(256), st, P.P, P.S, P.Q, P.points, P.scales, P.tg,
                P.points_bak, P.scales_bak, P.tg_bak, flag, zero, nzero, n);
+}
+
+void launch_trial_begin_dev(const DevProblem &P, int *flag, double *zero, int64_t nzero, LmState *lm, const double *scal,
+                            double tau, double user_lambda, hipStream_t st) {
+    int64_t n = std::max<int64_t>(std::max<int64_t>(3 * (int64_t)P.P, 7 * (int64_t)P.Q), std::max<int64_t>(P.S, nzero));
+    n = std::max<int64_t>(n, 1);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 4096);
+    LAUNCH("trial_begin", dev::k_trial_begin_dev, dim3(grid), dim3(256), st, P.P, P.S, P.Q, P.points, P.scales, P.tg,
+           P.points_bak, P.scales_bak, P.tg_bak, flag, zero, nzero, n, lm, scal, tau, user_lambda);
+}
+
+void launch_lm_decide(LmState *lm, const double *scal, const double *rec, double *chi_it, int32_t *trials_it, int max_report,
+                      LmState *snap, int slot, hipStream_t st) {
+    LAUNCH("lm_decide", dev::k_lm_decide, dim3(1), dim3(64), st, lm, scal, rec, chi_it, trials_it, max_report, snap, slot);
 }
 
 void launch_trial_readback(const double *scal, int ns, const int *flag, const double *rec, int nrec, double *h_scal,

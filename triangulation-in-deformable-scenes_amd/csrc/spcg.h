@@ -192,13 +192,17 @@ struct SpDev {
     int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
     double tol2 = 0;
+    // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the
+    // per-iteration ones when *lgate == 0; lambda from *lam_dev instead of the launch argument
+    const int *gate = nullptr, *lgate = nullptr;
+    const double *lam_dev = nullptr;
 };
 
 // launchers (spcg.hip); `heavy_stage` of k_sp_heavy: 0 both halves (one rank), 1 sums, 2 finish
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st);   // rows + blocks + heavy sums (rank partial)
 void sp_launch_maxdiag(const SpDev &G, double *out, hipStream_t st);   // rank max of the rows' diagonal
 void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);   // out = max(out, heavy diagonal)
-void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st);
+void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st, const int *gate = nullptr);
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st);
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
 void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
@@ -296,6 +300,9 @@ class SpSolver {
     double *d_xbuf = nullptr;
     std::vector<int64_t> send_off_, recv_off_;   // per peer, into the row lists (and x 6 per row)
     int32_t *d_row_of_point = nullptr;
+    LmState *d_lm = nullptr, *h_snap = nullptr;   // device-driven LM state; its pinned copy
+    double *d_chi_it = nullptr;
+    int32_t *d_trials_it = nullptr;
     bool have_ = false;
     template <class T> int alloc(T **p, int64_t n);
     template <class T> int put(T **p, const std::vector<T> &v);
@@ -310,6 +317,7 @@ class SpSolver {
     int halo(int width, double *vec, bool zp);
     int halo_sd();
     int pcg_solve(double lambda, const double *rhs, bool &solved, int &its);
+    int solve_lm_dev(const deftri_lm_params &prm, deftri_report &R);
     void gather_values(const deftri_problem_desc &d, SpValues &v) const;
 };
 

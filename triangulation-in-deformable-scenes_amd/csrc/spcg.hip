@@ -89,6 +89,10 @@ __device__ __forceinline__ int row_block(int b, int nrb) {
 
 __device__ __forceinline__ int heavy_dof(const SpDev &G, int h) { return h < G.Q ? 6 * h : 6 * G.Q + (h - G.Q); }
 
+// device-driven LM: the slot's gate words (spcg.h SpDev::gate / lgate) and its lambda
+__device__ __forceinline__ bool gated_off(const int *g) { return g && !*g; }
+__device__ __forceinline__ double lam_of(const SpDev &G, double lam) { return G.lam_dev ? *G.lam_dev : lam; }
+
 // Last-workgroup hand-off (G.fuse).  A workgroup's partials are published by thread 0 with
 // agent-scope relaxed atomic stores (coherent across the XCDs' L2s, no L2 write-back); after its
 // stores are acknowledged (s_waitcnt) it takes a ticket; the workgroup that draws the last ticket
@@ -116,6 +120,7 @@ template <class JT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3)))
 k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
+    if (gated_off(G.lgate)) return;
     const int lb = row_block(blockIdx.x, G.nrb);
     const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double mx = 0.0;
@@ -242,6 +247,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
 // heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1)
 __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
     __shared__ double red[kSpLin][4];
+    if (gated_off(G.lgate)) return;
     const int4 d = G.blk[blockIdx.x];
     const int kind = d.x & 0xff, owned = d.x >> 8;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -301,6 +307,7 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
 __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
     __shared__ double lds[8][32];
     __shared__ int last;
+    if (gated_off(G.lgate)) return;
     const int ch = blockIdx.x, h = G.ch_h[ch];
     const int dim = h < G.Q ? kSpLin : 2;
     const int c = threadIdx.x & 31, g = threadIdx.x >> 5;
@@ -363,6 +370,7 @@ __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
 // rank max of the rows' diagonal (stage 0), or that (all-reduced) combined with the heavy diagonal
 __global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, int stage) {
     __shared__ double red4[4];
+    if (gated_off(G.lgate)) return;
     double m = 0.0;
     if (stage == 0) {
         for (int i = threadIdx.x; i < G.nrb; i += 256) m = fmax(m, G.mpart[i]);
@@ -381,7 +389,8 @@ __global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, 
     }
 }
 
-__global__ void k_sp_cvt_j(const double *__restrict__ J, float *__restrict__ J32, int64_t n) {
+__global__ void k_sp_cvt_j(const double *__restrict__ J, float *__restrict__ J32, int64_t n, const int *gate) {
+    if (gated_off(gate)) return;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) J32[i] = (float)J[i];
 }
@@ -583,6 +592,8 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
     // block inverse (through LDS)
     __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
     __shared__ double red[2][3 * kSpUpdRows / 64], dred[2][4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     constexpr int nw = 3 * kSpUpdRows / 64;
     double rz = 0.0, rr = 0.0;
@@ -696,7 +707,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
 // (r.z, r.r) of iteration it from the previous update's (or the setup's) partials, in order
 __global__ void __launch_bounds__(256) k_sp_dots(int it, const SpDev G) {
     __shared__ double red[2][4];
-    if (G.rec[0] != 0.0) return;
+    if (gated_off(G.gate) || G.rec[0] != 0.0) return;
     dots_block(G, it, red);
 }
 
@@ -839,6 +850,7 @@ __device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
 // merged chain, G.alpha_kernel: alpha of iteration it in a one-workgroup launch between the phases
 __global__ void __launch_bounds__(256) k_sp_alpha(int it, const SpDev G) {
     __shared__ double red4[4];
+    if (gated_off(G.gate)) return;
     double beta;
     if (it_state(G, it, beta)) return;
     m2_alpha_make(G, it, red4, false);
@@ -853,6 +865,8 @@ __global__ void __launch_bounds__(256) k_sp_alpha(int it, const SpDev G) {
 template <class JT, int MG>
 __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     __shared__ double red[7][4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
     double beta = 0.0;
     if constexpr (MG == 2) {
         if (G.rec[0] != 0.0) return;             // the state is decided by the update (k_sp_update_sd)
@@ -987,6 +1001,8 @@ template <class JT, int MG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4)))
 k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
     double beta = 0.0;
     if constexpr (MG == 2) {
         if (G.rec[0] != 0.0) return;
@@ -1242,6 +1258,8 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
 // 1 and 2 instead.  Every path forms the same sums (heavy_sums_block, heavy_finish).
 __global__ void __launch_bounds__(256) k_sp_heavy(int it, const SpDev G, double lam, int stage) {
     __shared__ double red4[4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
     double beta;
     const int st = it_state(G, it, beta);
     if (st || stage == 3) {
@@ -1269,7 +1287,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
     static_assert(kSpUpdRows == kSpBlock, "update workgroups are the row blocks of the (r.z, r.r) partials");
     __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
     __shared__ double red[2][3 * kSpUpdRows / 64], dred[2][4];
-    if (G.rec[0] != 0.0) return;
+    if (gated_off(G.gate) || G.rec[0] != 0.0) return;
     const double alpha = G.red[(int64_t)kSpRed * it + 3];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     constexpr int nw = 3 * kSpUpdRows / 64;
@@ -1368,7 +1386,8 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
 __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update_sd(int it, const SpDev G, double lam, int tail) {
     __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
     __shared__ double red[2][3 * kSpUpdRows / 64];
-    if (G.rec[0] != 0.0) return;
+    if (gated_off(G.gate) || G.rec[0] != 0.0) return;
+    lam = lam_of(G, lam);
     const double gamma = G.xb[0], rr = G.xb[1], delta = G.xb[2];
     const double rr0 = it == 0 ? rr : G.red[1];
     double beta = 0.0, alpha = 0.0;
@@ -1531,8 +1550,8 @@ void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st) {
     SPL("sp_maxdiag", sp::k_sp_maxdiag, 1, G, out, 1);
 }
 
-void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st) {
-    if (n > 0) SPL("sp_cvt_j", sp::k_sp_cvt_j, nblk(n, 256), J, J32, n);
+void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st, const int *gate) {
+    if (n > 0) SPL("sp_cvt_j", sp::k_sp_cvt_j, nblk(n, 256), J, J32, n, gate);
 }
 
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st) {

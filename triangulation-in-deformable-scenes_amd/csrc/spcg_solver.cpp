@@ -83,6 +83,7 @@ SpSolver::~SpSolver() {
     for (void *p : allocs_) hipFree(p);
     if (hpin) hipHostFree(hpin);
     if (ipin) hipHostFree(ipin);
+    if (h_snap) hipHostFree(h_snap);
 }
 
 template <class T>
@@ -175,6 +176,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     hipStreamSynchronize(st_);
     for (void *p : allocs_) hipFree(p);
     allocs_.clear();
+    d_lm = nullptr; d_chi_it = nullptr; d_trials_it = nullptr;
     have_ = false;
     P = DevProblem();
     G = SpDev();
@@ -574,9 +576,216 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
     return 0;
 }
 
+// ---- device-driven LM (one rank) ------------------------------------------------------------------
+// The LM's decisions (rho, accept / reject, lambda and nu, g2o's loop and Terminate conditions) run on
+// the device (kernels.hip k_lm_decide), so the host queues "slots" — [linearization, gated on the
+// last trial's acceptance] [prologue: backup or restore] [setup, CG chain, tail, evaluation] [decide]
+// — without waiting for each trial's outcome.  It keeps two slots in flight and reads the decision of
+// the oldest one (an event per slot; the decide kernel copies the state to pinned memory); a slot
+// queued past the end of the solve returns at once in every kernel.  A step whose PCG needs more
+// iterations than its slot queued (the host's guess: the last converged count + 2) stops the slots
+// (stop 3): the host continues that solve in chunks of 4 exactly as solve_lm's host loop does, then
+// queues the evaluation and the decide.  Identical arithmetic and decisions as the host loop
+// (tests/test_gpu_sp.py::test_device_lm_matches_host_lm); DEFTRI_HOST_LM=1 selects the host loop.
+int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
+    hipSetDevice(dev_);
+    auto t_start = std::chrono::steady_clock::now();
+    const int max_trials = prm.max_trials > 0 ? prm.max_trials : 10;
+    const double tau = prm.tau > 0 ? prm.tau : 1e-5;
+    const bool analytic = prm.analytic_jacobians != 0;
+    const int mx = budget();
+    const int64_t nrec = kSpRecDoubles + (int64_t)kSpRed * (mx + 2);
+    int rc;
+    if (!d_lm) {
+        if ((rc = alloc(&d_lm, 1)) || (rc = alloc(&d_chi_it, DEFTRI_MAX_REPORT_ITERS)) ||
+            (rc = alloc(&d_trials_it, DEFTRI_MAX_REPORT_ITERS)))
+            return rc;
+        SPOK(hipHostMalloc((void **)&h_snap, sizeof(LmState), hipHostMallocDefault));
+    }
+    eval_chi2(analytic, 0, nullptr);
+    SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    R.chi2_initial = hpin[0];
+    LmState L{};
+    L.lam = 0.0; L.ni = 2.0; L.cur = R.chi2_initial;
+    L.gate_trial = prm.n_iterations > 0 ? 1 : 0;
+    L.gate_lin = L.gate_trial;
+    L.need_lin = 1;
+    L.stop = prm.n_iterations > 0 ? 0 : 1;
+    L.last_its = last_its;
+    L.n_it = prm.n_iterations;
+    L.max_trials = max_trials;
+    L.slot = L.stop_slot = -1;
+    *h_snap = L;
+    SPOK(hipMemcpyAsync(d_lm, &L, sizeof(LmState), hipMemcpyHostToDevice, st_));
+    SPOK(hipMemsetAsync(d_trials_it, 0, sizeof(int32_t) * DEFTRI_MAX_REPORT_ITERS, st_));
+    // gates and lambda from the state
+    P.gate_lin = &d_lm->gate_lin;
+    P.gate_trial = &d_lm->gate_trial;
+    G.gate = &d_lm->gate_trial;
+    G.lgate = &d_lm->gate_lin;
+    G.lam_dev = &d_lm->lam;
+    G.max_it = mx;
+    G.tol2 = tol * tol;
+    struct Clear {              // the gates off again whatever path leaves this function
+        SpSolver *s;
+        ~Clear() { s->P.gate_lin = s->P.gate_trial = nullptr; s->G.gate = s->G.lgate = nullptr; s->G.lam_dev = nullptr; }
+    } clear{this};
+    // the evaluation of a slot's step: state update, chi2 + the rho denominator (lambda from HBM)
+    auto evaluate = [&]() {
+        launch_update_state(P, G.x, st_, nullptr);
+        launch_lin_chi(P, st_);
+        SumJobs J;
+        J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+        J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+        J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+        J.j[3].n = G.hd + 3 * (int64_t)G.nown; J.j[3].a = G.x; J.j[3].b = G.b; J.j[3].lambda_dev = &d_lm->lam;
+        J.j[3].mode = 1; J.j[3].out = d_scal + 1;
+        J.nj = 4;
+        J.total = d_scal;
+        J.gate = &d_lm->gate_trial;
+        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+    };
+    struct Slot { int idx, n; hipEvent_t ev; };
+    std::vector<hipEvent_t> evpool;
+    std::vector<Slot> inflight;
+    int queued = 0, guess = std::max(2, last_its + 2);
+    auto enqueue = [&]() -> int {
+        const bool first = queued == 0;
+        // linearization (gate_lin): errors + Jacobians, chi2 sums, the rows' / heavy blocks, b
+        launch_linearize(P, st_, true, analytic);
+        SumJobs J;
+        J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+        J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+        J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+        J.nj = 3;
+        J.total = d_scal;
+        J.gate = &d_lm->gate_lin;
+        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+        if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_, &d_lm->gate_lin);
+        sp_launch_glin(G, fp32_jac != 0, st_);
+        if (first) {
+            sp_launch_maxdiag(G, d_scal + 2, st_);
+            sp_launch_maxdiag_heavy(G, d_scal + 2, st_);
+        }
+        // the trial (gate_trial)
+        launch_trial_begin_dev(P, d_flag, G.rec, nrec, d_lm, d_scal, tau, prm.user_lambda, st_);
+        int r2;
+        if ((r2 = cg_setup(0.0, G.b))) return r2;
+        const int n = std::min(guess, mx);
+        if ((r2 = cg_chain(0.0, 0, n))) return r2;
+        if ((r2 = cg_tail(n, 0.0))) return r2;
+        evaluate();
+        launch_lm_decide(d_lm, d_scal, G.rec, d_chi_it, d_trials_it, DEFTRI_MAX_REPORT_ITERS, h_snap, queued, st_);
+        if (evpool.empty()) { hipEvent_t e; SPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming)); evpool.push_back(e); }
+        hipEvent_t e = evpool.back();
+        evpool.pop_back();
+        SPOK(hipEventRecord(e, st_));
+        inflight.push_back({queued, n, e});
+        queued++;
+        return 0;
+    };
+    std::vector<int> slot_n;            // CG iterations queued per enqueue index
+    bool host_stop = false;
+    for (;;) {
+        while (!host_stop && inflight.size() < 2) {
+            if ((rc = enqueue())) return rc;
+            slot_n.push_back(inflight.back().n);
+        }
+        if (inflight.empty()) break;
+        const Slot sl = inflight.front();
+        inflight.erase(inflight.begin());
+        SPOK(hipEventSynchronize(sl.ev));
+        evpool.push_back(sl.ev);
+        const LmState S = *h_snap;
+        if (S.last_its > 0) guess = std::max(2, S.last_its + 2);
+        if (S.stop == 1 || S.stop == 2) { host_stop = true; continue; }
+        if (S.stop == 3) {
+            // the slot S.stop_slot queued too few CG iterations: every later slot returned at once
+            SPOK(hipStreamSynchronize(st_));
+            for (const Slot &o : inflight) evpool.push_back(o.ev);
+            inflight.clear();
+            int j = slot_n[S.stop_slot];
+            // the evaluation applied the unfinished x: restore, continue the solve in chunks of 4
+            SPOK(hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+            SPOK(hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+            SPOK(hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+            const int one = 1, zero = 0;
+            SPOK(hipMemcpyAsync(&d_lm->gate_trial, &one, sizeof(int), hipMemcpyHostToDevice, st_));
+            SPOK(hipMemcpyAsync(&d_lm->stop, &zero, sizeof(int), hipMemcpyHostToDevice, st_));
+            int st = kSpRunning;
+            while (st == kSpRunning && j < mx) {
+                const int n2 = std::min(j + 4, mx);
+                if ((rc = cg_chain(0.0, j, n2))) return rc;
+                j = n2;
+                if ((rc = cg_tail(j, 0.0))) return rc;
+                SPOK(hipMemcpyAsync(hpin + 16, G.rec, sizeof(double) * kSpRecDoubles, hipMemcpyDeviceToHost, st_));
+                SPOK(hipStreamSynchronize(st_));
+                st = (int)hpin[16];
+            }
+            if (st == kSpTimeout) return hand_off_timeout();
+            if (st == kSpRunning) {                        // budget: a failed solve, like the host loop's
+                const double rec_budget[2] = {(double)kSpBudget, (double)j};
+                SPOK(hipMemcpyAsync(G.rec, rec_budget, sizeof(rec_budget), hipMemcpyHostToDevice, st_));
+            }
+            if (j > 0) guess = std::max(guess, std::min(j + 2, mx));
+            evaluate();
+            launch_lm_decide(d_lm, d_scal, G.rec, d_chi_it, d_trials_it, DEFTRI_MAX_REPORT_ITERS, h_snap, -1, st_);
+            SPOK(hipStreamSynchronize(st_));
+            const LmState S2 = *h_snap;
+            if (S2.last_its > 0) guess = std::max(2, S2.last_its + 2);
+            if (S2.stop != 0) host_stop = true;
+            continue;
+        }
+    }
+    SPOK(hipStreamSynchronize(st_));
+    for (hipEvent_t e : evpool) hipEventDestroy(e);
+    LmState Lf;
+    SPOK(hipMemcpy(&Lf, d_lm, sizeof(LmState), hipMemcpyDeviceToHost));
+    const int nrep = std::min(Lf.it, (int)DEFTRI_MAX_REPORT_ITERS);
+    if (nrep > 0) {
+        SPOK(hipMemcpy(R.chi2_iter, d_chi_it, sizeof(double) * (size_t)nrep, hipMemcpyDeviceToHost));
+        SPOK(hipMemcpy(R.trials_iter, d_trials_it, sizeof(int32_t) * (size_t)nrep, hipMemcpyDeviceToHost));
+    }
+    if (Lf.restore) {                                      // the last trial rejected: pop
+        SPOK(hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+        SPOK(hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+        SPOK(hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+    }
+    last_its = Lf.last_its > 0 ? Lf.last_its : last_its;
+    R.trials_total += Lf.trials_total;
+    R.trials_executed += Lf.trials_total;
+    R.trials_rejected += Lf.trials_rejected;
+    R.pcg_trials += Lf.pcg_trials;
+    R.pcg_fallbacks += Lf.pcg_fail;
+    R.pcg_iterations += Lf.pcg_iterations;
+    R.status = Lf.stop == 2 ? DEFTRI_STATUS_TERMINATE : DEFTRI_STATUS_OK;
+    R.iterations = Lf.it;
+    R.lambda_final = Lf.lam;
+    P.gate_lin = P.gate_trial = nullptr;
+    G.gate = G.lgate = nullptr;
+    G.lam_dev = nullptr;
+    eval_chi2(analytic, 0, nullptr);
+    SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
+    SPOK(hipStreamSynchronize(st_));
+    R.chi2_final = hpin[0];
+    R.ms_linearize = -1.0;
+    R.ms_pcg = -1.0;
+    R.ms_factor = R.ms_solve = R.ms_update = -1.0;
+    R.plan = DEFTRI_PLAN_ITERATIVE;
+    R.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    return 0;
+}
+
 int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
     hipSetDevice(dev_);
+    R.n_unknowns = G.ndof;
+    R.rank = rank_;
+    R.nranks = nranks_;
+    R.lanes = 1;
+    static const bool host_lm = std::getenv("DEFTRI_HOST_LM") != nullptr;
+    if (!shard_ && !host_lm && !prm.verbose) return solve_lm_dev(prm, R);
     const bool dist = shard_;
     R.n_unknowns = G.ndof;
     R.rank = rank_;
