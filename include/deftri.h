@@ -492,6 +492,11 @@ int deftri_triangulate_nrslam(deftri_ctx *ctx, int32_t n, const float *uv1, cons
 /* MapPoint id of every point vertex of the last graph deftri_arap_build_graph built (n = its
    n_points): the write-back key of :974-990. */
 int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n);
+/* Graph builds of this context so far answered by the memo (the same map: NLopt's clones) and by
+   the structure memo (deformationOptimization's next round: positions, depth scales and T_g moved,
+   every pair's Delaunay triangulation still valid — the values refreshed in place, the descriptor
+   equal bit for bit to a full build's), and the host time of the last build in ms. */
+int deftri_graph_stats(const deftri_ctx *ctx, int64_t *memo_hits, int64_t *struct_hits, double *ms_last);
 /* Keyframe pairs of the graphs this context builds (deftri_arap_build_graph / _optimization): 0
    (default) every pair (a, b > a) in map order, as the reference's loop (g2oBundleAdjustment.cc:
    640-645); w > 0 only pairs with b - a <= w (a sliding window: the documented deviation used for

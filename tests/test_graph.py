@@ -166,3 +166,56 @@ def test_graph_memo_miss_on_moved_point():
         with capi.Context(-1) as f:
             _equal_problems(p1, f.build_graph(m, 1.0, 2e5, np.float32(0.003)))
         assert not np.array_equal(p0.points, p1.points)
+
+
+FIELDS_ALL = ("points", "tg", "scales", "cam_kb8", "cam_pose", "rep_point", "rep_cam", "rep_obs", "rep_info",
+              "dep_point", "dep_scale", "dep_cam", "dep_meas", "dep_info", "arap_pts", "arap_pair", "arap_rot",
+              "arap_w", "rot", "pair_area", "pair_info", "order_xy", "point_ids")
+
+
+def _same(pa, pb):
+    for f in FIELDS_ALL:
+        a, b = getattr(pa, f), getattr(pb, f)
+        assert a.shape == b.shape and np.array_equal(a, b), f
+
+
+@pytest.mark.parametrize("n,seed,k", [(3000, 5, 2), (800, 6, 4)])
+def test_next_round_fast_path_is_a_full_build(n, seed, k):
+    """deformationOptimization's next round (g2oBundleAdjustment.cc:482): the written-back map has
+    moved points, depth scales and T_g but the same structure.  When every pair's previous Delaunay
+    triangulation is still THE Delaunay triangulation of the moved points, the structure memo
+    refreshes the values in place — the descriptor must equal a fresh context's full build bit for
+    bit; when the motion flips an edge it must fall back to the full build (still equal)."""
+    import copy
+    from deftri import metrics
+    if k == 2:
+        m, _ = sim.simulate_two_view(n=n, seed=seed, scale_scene=True, compact=True)
+    else:
+        m = sim.multi_view_arrays(n=n, k=k, seed=seed)
+    rng = np.random.default_rng(seed)
+    with capi.Context(-1) as a:
+        p0 = a.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        ext = np.abs(p0.points).max()
+        for step, (scale, expect_fast) in enumerate([(1e-9, True), (3e-9, True), (3e-2, False)]):
+            m2 = copy.deepcopy(m)
+            pts = p0.points + rng.normal(0.0, scale * ext, p0.points.shape)
+            if k == 2:
+                metrics.apply_solution(m2, list(p0.point_ids), pts)
+                for kf in m2.keyframes.values():
+                    kf.estimated_depth_scale = 1.0 + 1e-6 * (step + 1)
+            else:                           # ArrayMap: MapPoint id = keyframe id * n + slot
+                for pid, x in zip(p0.point_ids, pts):
+                    kf = m2.kfs[int(pid) // n]
+                    kf["pos"][int(pid) % n] = np.asarray(x, np.float32)
+            before = a.graph_stats()[1]
+            pa = a.build_graph(m2, 1.5, 1e5, np.float32(0.004))
+            fast = a.graph_stats()[1] > before
+            with capi.Context(-1) as b:
+                pb = b.build_graph(m2, 1.5, 1e5, np.float32(0.004))
+            _same(pa, pb)
+            if expect_fast:
+                assert fast, (step, scale)
+            else:
+                assert not fast, (step, scale)
+            m = m2
+            p0 = pa

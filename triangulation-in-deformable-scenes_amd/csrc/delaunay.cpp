@@ -310,11 +310,100 @@ bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_s
     if (n < 3) return false;
     Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}};
     if (!s.run(skipped)) return false;
-    tris.assign(s.tri.begin(), s.tri.end());
+    // canonical order: each triangle rotated to start at its smallest vertex (orientation kept), the
+    // triangles sorted by (first, second, third) — the output then depends only on the triangle set,
+    // so the mesh area (a sum in this order) is the same whoever built the set (a full sweep or the
+    // graph builder's re-validated previous mesh, graph_builder.cpp)
+    const int nt = (int)s.tri.size() / 3;
+    std::vector<int32_t> rot3(s.tri.size());
+    std::vector<int32_t> cnt(n + 1, 0);
+    for (int t = 0; t < nt; t++) {
+        const int32_t a = s.tri[3 * t], b = s.tri[3 * t + 1], c = s.tri[3 * t + 2];
+        int32_t *o = &rot3[3 * (size_t)t];
+        if (a < b && a < c) { o[0] = a; o[1] = b; o[2] = c; }
+        else if (b < c) { o[0] = b; o[1] = c; o[2] = a; }
+        else { o[0] = c; o[1] = a; o[2] = b; }
+        cnt[o[0] + 1]++;
+    }
+    for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
+    std::vector<int32_t> order(nt);
+    {
+        std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
+        for (int t = 0; t < nt; t++) order[fill[rot3[3 * (size_t)t]]++] = t;
+    }
+    for (int i = 0; i < n; i++)           // a vertex starts ~2 triangles: a short sort per bucket
+        std::sort(order.begin() + cnt[i], order.begin() + cnt[i + 1], [&](int32_t x, int32_t y) {
+            const int32_t *a = &rot3[3 * (size_t)x], *b = &rot3[3 * (size_t)y];
+            return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
+        });
+    tris.resize(s.tri.size());
+    for (int k = 0; k < nt; k++)
+        for (int c = 0; c < 3; c++) tris[3 * (size_t)k + c] = rot3[3 * (size_t)order[k] + c];
     int h = 0, e = s.hstart;
     do { h++; e = s.hnext[e]; } while (e != s.hstart && h <= n);
     hull_size = h;
     return true;
+}
+
+bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &tris) {
+    const int nt = (int)tris.size() / 3;
+    if (n < 3 || nt == 0) return false;
+    auto P = [&](int i) { return xy + 2 * (size_t)i; };
+    // vertex -> incident triangles (CSR)
+    std::vector<int32_t> off(n + 1, 0), inc(3 * (size_t)nt);
+    for (int32_t v : tris) {
+        if (v < 0 || v >= n) return false;
+        off[v + 1]++;
+    }
+    for (int i = 0; i < n; i++) {
+        if (off[i + 1] == 0) return false;                // a vertex on no triangle (a skipped point)
+        off[i + 1] += off[i];
+    }
+    {
+        std::vector<int32_t> fill(off.begin(), off.end() - 1);
+        for (int t = 0; t < nt; t++)
+            for (int k = 0; k < 3; k++) inc[fill[tris[3 * (size_t)t + k]]++] = t;
+    }
+    std::vector<int32_t> bnext(n, -1);                   // boundary half-edge u -> v (counter-clockwise)
+    int nb = 0;
+    for (int t = 0; t < nt; t++) {
+        const int32_t *T = &tris[3 * (size_t)t];
+        if (orient2d(P(T[0]), P(T[1]), P(T[2])) <= 0) return false;
+        for (int k = 0; k < 3; k++) {
+            const int32_t u = T[k], v = T[(k + 1) % 3], w = T[(k + 2) % 3];
+            // the twin half-edge v -> u in a triangle around v
+            int32_t x = -1;
+            int twins = 0;
+            for (int32_t m = off[v]; m < off[v + 1]; m++) {
+                const int32_t t2 = inc[m];
+                if (t2 == t) continue;
+                const int32_t *S = &tris[3 * (size_t)t2];
+                for (int c = 0; c < 3; c++)
+                    if (S[c] == v && S[(c + 1) % 3] == u) { x = S[(c + 2) % 3]; twins++; }
+            }
+            if (twins > 1) return false;
+            if (twins == 0) {                            // boundary
+                if (bnext[u] >= 0) return false;         // not a simple boundary polygon
+                bnext[u] = v;
+                nb++;
+            } else if (u < v && incircle(P(u), P(v), P(w), P(x)) >= 0) {
+                return false;                            // not strictly locally Delaunay
+            }
+        }
+    }
+    // the boundary: one cycle, strictly convex
+    int start = -1;
+    for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
+    if (start < 0) return false;
+    int u = start, len = 0;
+    do {
+        const int v = bnext[u];
+        if (v < 0 || bnext[v] < 0) return false;
+        if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
+        u = v;
+        if (++len > nb) return false;
+    } while (u != start);
+    return len == nb;
 }
 
 int orient2d_sign(const double *a, const double *b, const double *c) { return orient2d(a, b, c); }

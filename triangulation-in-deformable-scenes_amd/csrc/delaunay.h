@@ -5,11 +5,20 @@
 
 namespace deftri {
 
-// xy: n points (x, y interleaved).  tris: 3 vertex indices per triangle, counter-clockwise.
-// hull_size: number of convex-hull vertices; skipped: duplicate points that were not inserted.
+// xy: n points (x, y interleaved).  tris: 3 vertex indices per triangle, counter-clockwise, in the
+// canonical order (each starting at its smallest vertex; sorted).  hull_size: number of convex-hull
+// vertices; skipped: duplicate points that were not inserted.
 bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_size, int &skipped);
 
 int orient2d_sign(const double *a, const double *b, const double *c);
 int incircle_sign(const double *a, const double *b, const double *c, const double *d);
+
+// Is the triangle list `tris` (canonical, counter-clockwise) still THE Delaunay triangulation of the
+// n points xy — the one delaunay2d would return, triangle for triangle?  True when every triangle is
+// strictly counter-clockwise, every interior edge strictly locally Delaunay (its opposite vertex
+// strictly outside the circumcircle: no cocircular ambiguity), every vertex is on a triangle and
+// the boundary is a strictly convex polygon (so it is the convex hull): then the triangulation is
+// the unique Delaunay triangulation.  Exact predicates; parallel over triangles / edges.
+bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &tris);
 
 }  // namespace deftri

@@ -71,7 +71,7 @@ struct Mesh {
     std::vector<int32_t> off, adj;    // CSR, rows sorted
     std::vector<double> w;            // per CSR entry
     double area = 0, ms_delaunay = 0;
-    int T = 0, hull = 0;
+    int T = 0, hull = 0, skipped = 0;
     int deg(int i) const { return off[i + 1] - off[i]; }
     int64_t find(int i, int j) const {
         const int32_t *b = adj.data() + off[i], *e = adj.data() + off[i + 1];
@@ -90,6 +90,7 @@ bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err
     auto td = std::chrono::steady_clock::now();
     if (!delaunay2d(xy.data(), n, M.tris, M.hull, skipped)) { err = "Delaunay triangulation failed (collinear input)"; return false; }
     M.ms_delaunay = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
+    M.skipped = skipped;
     const int ntri = (int)M.tris.size() / 3;
     M.T = ntri + std::max(0, M.hull - 2);       // qhull facets.count(): lower + upper Delaunay facets
     // adjacency: 2 candidate entries per triangle corner, then per-row sort + unique + compaction
@@ -233,7 +234,9 @@ void append(std::vector<unsigned char> &k, const void *p, size_t n) {
     k.insert(k.end(), c, c + n);
 }
 template <class T> void append_v(std::vector<unsigned char> &k, const T &v) { append(k, &v, sizeof(T)); }
-std::vector<unsigned char> graph_key(const deftri_map &map, int pair_window) {
+// values = false: the structure key — everything but the positions, the depth scales and the global
+// transformations' values (what deformationOptimization's write-back changes between rounds)
+std::vector<unsigned char> graph_key(const deftri_map &map, int pair_window, bool values = true) {
     std::vector<unsigned char> k;
     size_t sz = 64;
     for (int a = 0; a < map.n_keyframes; a++) {
@@ -242,20 +245,147 @@ std::vector<unsigned char> graph_key(const deftri_map &map, int pair_window) {
     }
     k.reserve(sz + (size_t)std::max(map.n_global, 0) * sizeof(deftri_global_entry));
     append_v(k, map.n_keyframes); append_v(k, pair_window); append_v(k, map.n_global);
-    append(k, map.global_t, sizeof(map.global_t));
-    if (map.n_global > 0) append(k, map.globals, sizeof(deftri_global_entry) * (size_t)map.n_global);
+    if (values) append(k, map.global_t, sizeof(map.global_t));
+    for (int e = 0; e < map.n_global; e++) {
+        append_v(k, map.globals[e].kf1); append_v(k, map.globals[e].kf2);
+        if (values) append(k, map.globals[e].t, sizeof(map.globals[e].t));
+    }
     for (int a = 0; a < map.n_keyframes; a++) {
         const deftri_keyframe &f = map.keyframes[a];
         append_v(k, f.id); append(k, f.pose, sizeof(f.pose)); append(k, f.kb8, sizeof(f.kb8));
-        append_v(k, f.n_scales); append_v(k, f.depth_scale); append_v(k, f.n_slots); append_v(k, f.n_obs);
+        append_v(k, f.n_scales); append_v(k, f.n_slots); append_v(k, f.n_obs);
+        if (values) append_v(k, f.depth_scale);
         if (f.n_scales > 0 && f.inv_sigma2) append(k, f.inv_sigma2, 4 * (size_t)f.n_scales);
         if (f.n_slots > 0) {
-            append(k, f.point_id, 8 * (size_t)f.n_slots); append(k, f.point_pos, 12 * (size_t)f.n_slots);
+            append(k, f.point_id, 8 * (size_t)f.n_slots);
+            if (values) append(k, f.point_pos, 12 * (size_t)f.n_slots);
             append(k, f.obs_index, 4 * (size_t)f.n_slots);
         }
         if (f.n_obs > 0) { append(k, f.kp_uv, 8 * (size_t)f.n_obs); append(k, f.kp_octave, 4 * (size_t)f.n_obs); append(k, f.depth, 4 * (size_t)f.n_obs); }
     }
     return k;
+}
+
+// T_global of pair (kf1 = b, kf2 = a): map transformation for (kf1, kf2) or identity (:664-677)
+// getGlobalKeyFramesTransformation(k2->first, k1->first) = (kf1.id, kf2.id): the table entry for
+// that ordered pair, a default (identity) SE3f when absent (Map.cc:332-343)
+void pair_tg(const deftri_map &map, int a, int b, double Tg[7]) {
+    const deftri_keyframe &kf1 = map.keyframes[b], &kf2 = map.keyframes[a];
+    const double I[7] = {0, 0, 0, 1, 0, 0, 0};
+    for (int i = 0; i < 7; i++) Tg[i] = I[i];
+    if (map.n_global > 0) {
+        for (int32_t e = 0; e < map.n_global; e++)
+            if (map.globals[e].kf1 == kf1.id && map.globals[e].kf2 == kf2.id) {
+                for (int i = 0; i < 7; i++) Tg[i] = map.globals[e].t[i];
+                break;
+            }
+    } else if (a == 0 && b == 1) {
+        for (int i = 0; i < 7; i++) Tg[i] = map.global_t[i];
+    }
+    float tn = std::sqrt((float)Tg[4] * (float)Tg[4] + (float)Tg[5] * (float)Tg[5] + (float)Tg[6] * (float)Tg[6]);
+    double qn = std::sqrt(Tg[0] * Tg[0] + Tg[1] * Tg[1] + Tg[2] * Tg[2] + Tg[3] * Tg[3]);
+    bool rot_id = qn > 0 && std::fabs(std::fabs(Tg[3] / qn) - 1.0) < 1e-10;
+    if (tn == 0.0f && rot_id) { Tg[0] = Tg[1] = Tg[2] = 0; Tg[3] = 1; Tg[4] = Tg[5] = Tg[6] = 0; }
+}
+
+// the mesh area in the triangles' (canonical) order, GetSurfaceArea's sum (build_mesh's arithmetic)
+double mesh_area(const std::vector<double> &pos, const std::vector<int32_t> &tris) {
+    double area = 0;
+    for (size_t t = 0; t + 2 < tris.size(); t += 3) {
+        const double *p0 = &pos[3 * tris[t]], *p1 = &pos[3 * tris[t + 1]], *p2 = &pos[3 * tris[t + 2]];
+        double x[3] = {p0[0] - p1[0], p0[1] - p1[1], p0[2] - p1[2]};
+        double y[3] = {p0[0] - p2[0], p0[1] - p2[1], p0[2] - p2[2]};
+        double cr[3] = {x[1] * y[2] - x[2] * y[1], x[2] * y[0] - x[0] * y[2], x[0] * y[1] - x[1] * y[0]};
+        area += 0.5 * std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+    }
+    return area;
+}
+
+// The structure memo's next-round path: the same descriptor a full build of `map` would give, when
+// every pair's previous mesh is still its Delaunay triangulation and its vector map the identity.
+// 0 refreshed; 1 not applicable (the caller builds in full; g untouched); -1 error.
+int refresh_graph(const deftri_map &map, double rep_weight, double arap_weight, double info_dep, GraphResult &g,
+                  GraphDevice *gdev, std::string &err) {
+    const size_t np = g.meshes.size();
+    std::vector<std::vector<double>> P1(np), P2(np);
+    for (size_t q = 0; q < np; q++) {
+        const GraphResult::PairMesh &pm = g.meshes[q];
+        if (!pm.identity_map) return 1;
+        const deftri_keyframe &kf1 = map.keyframes[pm.kf1], &kf2 = map.keyframes[pm.kf2];
+        std::vector<double> &pos1 = P1[q], &pos2 = P2[q];
+        pos1.reserve(3 * (size_t)pm.n1);
+        pos2.reserve(3 * (size_t)pm.n2);
+        for (int s = 0; s < kf1.n_slots; s++)
+            if (kf1.point_id[s] >= 0)
+                for (int k = 0; k < 3; k++) pos1.push_back((double)kf1.point_pos[3 * s + k]);
+        for (int s = 0; s < kf2.n_slots; s++)
+            if (kf2.point_id[s] >= 0)
+                for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
+        if ((int)pos1.size() != 3 * pm.n1 || (int)pos2.size() != 3 * pm.n2) return 1;
+        std::vector<double> xy(2 * (size_t)pm.n1);
+        for (int i = 0; i < pm.n1; i++) { xy[2 * i] = pos1[3 * i]; xy[2 * i + 1] = pos1[3 * i + 1]; }
+        if (!delaunay_still_valid(xy.data(), pm.n1, pm.tris)) return 1;
+        // createVectorMap stays the identity unless two points became approximately equal
+        // (isApprox 1e-6); such a pair's 2-D nearest neighbour is a Delaunay edge no longer than
+        // 1e-6 |p|: no such edge, no such pair
+        for (int i = 0; i < pm.n1; i++) {
+            const double *u = &pos1[3 * i];
+            const double nu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
+            for (int32_t k = pm.off[i]; k < pm.off[i + 1]; k++) {
+                const int j = pm.adj[k];
+                if (j < i) continue;
+                const double *v = &pos1[3 * j];
+                const double nv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+                const double dx = u[0] - v[0], dy = u[1] - v[1];
+                if (dx * dx + dy * dy <= 1e-12 * std::max(nu, nv)) return 1;
+            }
+        }
+    }
+    // every pair keeps its mesh: the values
+    size_t rbase = 0;
+    for (size_t q = 0; q < np; q++) {
+        const GraphResult::PairMesh &pm = g.meshes[q];
+        const deftri_keyframe &kf1 = map.keyframes[pm.kf1], &kf2 = map.keyframes[pm.kf2];
+        double Tg[7];
+        pair_tg(map, pm.kf2, pm.kf1, Tg);
+        for (int i = 0; i < 7; i++) g.tg[7 * q + i] = Tg[i];
+        g.scales[2 * q] = kf1.depth_scale;
+        g.scales[2 * q + 1] = kf2.depth_scale;
+        g.pair_area[q] = mesh_area(P1[q], pm.tris);
+        g.pair_info[q] = arap_weight * std::pow((double)pm.T, 2);
+        double *Rs = g.rot.data() + rbase;
+        double *w = g.wcat.data() + pm.w_off;
+        int dev_rc = 1;
+        if (gdev) {
+            dev_rc = gdev->mesh_pass(pm.n1, pm.n2, pm.tris.data(), (int)pm.tris.size() / 3, pm.off.data(), pm.adj.data(),
+                                     (int64_t)pm.adj.size(), pm.pos_idx.data(), pm.inv.data(), P1[q].data(), P2[q].data(), w,
+                                     Rs, err);
+            if (dev_rc < 0) return -1;
+        }
+        if (dev_rc != 0) {
+            Mesh M;
+            M.tris = pm.tris; M.off = pm.off; M.adj = pm.adj;
+            mesh_cot_weights(P1[q], M);
+            std::copy(M.w.begin(), M.w.end(), w);
+            parallel_for(pm.n1, 2048, [&](int lo, int hi) {
+                for (int i = lo; i < hi; i++)
+                    compute_r_vertex(i, pm.n2, pm.off.data(), pm.adj.data(), w, pm.pos_idx.data(), pm.inv.data(), P1[q].data(),
+                                     P2[q].data(), Rs + 9 * (size_t)i);
+            });
+        }
+        rbase += 9 * (size_t)pm.n1;
+    }
+    for (size_t i = 0; i < g.point_kf.size(); i++) {
+        const float *p = map.keyframes[g.point_kf[i]].point_pos + 3 * (size_t)g.point_slot[i];
+        for (int c = 0; c < 3; c++) { g.points[3 * i + c] = (double)p[c]; g.point_orig[3 * i + c] = p[c]; }
+        const float *o = map.keyframes[g.order_kf[i]].point_pos + 3 * (size_t)g.order_slot[i];
+        g.order_xy[2 * i] = (double)o[0];
+        g.order_xy[2 * i + 1] = (double)o[1];
+    }
+    for (size_t e = 0; e < g.arap_wk.size(); e++) g.arap_w[e] = g.wcat[g.arap_wk[e]];
+    for (size_t e = 0; e < g.rep_info.size(); e++) g.rep_info[e] = g.rep_base[e] * rep_weight;
+    std::fill(g.dep_info.begin(), g.dep_info.end(), info_dep);
+    return 0;
 }
 
 bool map_ok(const deftri_map &map, std::string &err) {
@@ -278,6 +408,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     if (!map_ok(map, err)) return false;
     const double info_dep = 1.0 / ((double)depth_error * (double)depth_error);
     static const bool no_memo = std::getenv("DEFTRI_NO_GRAPH_MEMO") != nullptr;
+    const auto t_build = std::chrono::steady_clock::now();
     std::vector<unsigned char> key = graph_key(map, pair_window);
     if (!no_memo && g.memo_valid && key == g.memo_key) {
         // the same map: only the weights can differ; recompute the information entries they scale
@@ -285,11 +416,27 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         for (size_t q = 0; q < g.pair_info.size(); q++) g.pair_info[q] = arap_weight * std::pow((double)g.pair_T[q], 2);
         std::fill(g.dep_info.begin(), g.dep_info.end(), info_dep);
         g.memo_hits++;
+        g.ms_last = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
         return true;
     }
-    const int64_t hits = g.memo_hits;
+    std::vector<unsigned char> skey = graph_key(map, pair_window, false);
+    static const bool no_struct = std::getenv("DEFTRI_NO_STRUCT_MEMO") != nullptr;
+    if (!no_memo && !no_struct && g.struct_valid && skey == g.struct_key) {
+        int rc = refresh_graph(map, rep_weight, arap_weight, info_dep, g, gdev, err);
+        if (rc < 0) return false;
+        if (rc == 0) {
+            g.memo_key = std::move(key);
+            g.memo_valid = true;
+            g.struct_hits++;
+            g.ms_last = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
+            return true;
+        }
+        // rc 1: a pair's triangulation or vector map changed — the full build below
+    }
+    const int64_t hits = g.memo_hits, shits = g.struct_hits;
     g = GraphResult();
     g.memo_hits = hits;
+    g.struct_hits = shits;
     const int K = map.n_keyframes;
     std::vector<int32_t> cam_of(K, -1);
     IdIndex pidx;
@@ -347,28 +494,13 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             Mesh M;
             if (!build_mesh(pos1, n1, M, err, gdev == nullptr)) return false;   // device: weights in the device pass
             auto t1 = tnow();
-            // T_global: map transformation for (kf1, kf2) or identity (:664-677)
-            // getGlobalKeyFramesTransformation(k2->first, k1->first) = (kf1.id, kf2.id): the table
-            // entry for that ordered pair, a default (identity) SE3f when absent (Map.cc:332-343)
-            double Tg[7] = {0, 0, 0, 1, 0, 0, 0};
-            if (map.n_global > 0) {
-                for (int32_t e = 0; e < map.n_global; e++)
-                    if (map.globals[e].kf1 == kf1.id && map.globals[e].kf2 == kf2.id) {
-                        for (int i = 0; i < 7; i++) Tg[i] = map.globals[e].t[i];
-                        break;
-                    }
-            } else if (a == 0 && b == 1) {
-                for (int i = 0; i < 7; i++) Tg[i] = map.global_t[i];
-            }
-            {
-                float tn = std::sqrt((float)Tg[4] * (float)Tg[4] + (float)Tg[5] * (float)Tg[5] + (float)Tg[6] * (float)Tg[6]);
-                double qn = std::sqrt(Tg[0] * Tg[0] + Tg[1] * Tg[1] + Tg[2] * Tg[2] + Tg[3] * Tg[3]);
-                bool rot_id = qn > 0 && std::fabs(std::fabs(Tg[3] / qn) - 1.0) < 1e-10;
-                if (tn == 0.0f && rot_id) { Tg[0] = Tg[1] = Tg[2] = 0; Tg[3] = 1; Tg[4] = Tg[5] = Tg[6] = 0; }
-            }
+            double Tg[7];
+            pair_tg(map, a, b, Tg);
             const std::vector<int32_t> posIdx = vector_map(pos1, n1);
             std::vector<int32_t> inv(n1, -1);           // invertedPosIndexes: the last vertex wins
             for (int v = 0; v < n1; v++) inv[posIdx[v]] = v;
+            bool identity = M.skipped == 0;
+            for (int v = 0; v < n1 && identity; v++) identity = posIdx[v] == v;
             auto t2 = tnow();
             // computeR: one Procrustes rotation per vertex, identity where no position maps to it
             const size_t rbase = g.rot.size();
@@ -391,6 +523,16 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 });
             }
             auto t3 = tnow();
+            {
+                GraphResult::PairMesh pm;
+                pm.tris = M.tris; pm.off = M.off; pm.adj = M.adj; pm.pos_idx = posIdx; pm.inv = inv;
+                pm.n1 = n1; pm.n2 = n2; pm.kf1 = b; pm.kf2 = a; pm.T = M.T;
+                pm.w_off = (int64_t)g.wcat.size();
+                pm.identity_map = identity;
+                g.wcat.insert(g.wcat.end(), M.w.begin(), M.w.end());
+                g.meshes.push_back(std::move(pm));
+            }
+            const int64_t w_off = g.meshes.back().w_off;
             for (int i = 0; i < 7; i++) g.tg.push_back(Tg[i]);
             const int32_t s1 = (int32_t)g.scales.size();
             g.scales.push_back(kf1.depth_scale); g.kf_scale[b] = s1;
@@ -401,15 +543,18 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             g.pair_info.push_back(arap_weight * std::pow((double)M.T, 2));
             g.pair_kf1.push_back(b); g.pair_kf2.push_back(a);
             g.pair_T.push_back(M.T); g.pair_hull.push_back(M.hull);
-            auto add_point = [&](int64_t id, const float *p, int ord_slot) {
+            auto add_point = [&](int64_t id, int kf, int slot, int ord_slot) {
                 int32_t *v = pidx.slot(id);
                 if (*v >= 0) return *v;
                 const int32_t k = (int32_t)g.point_mpid.size();
                 *v = k;
                 g.point_mpid.push_back(id);
+                const float *p = map.keyframes[kf].point_pos + 3 * (size_t)slot;
                 for (int c = 0; c < 3; c++) { g.points.push_back((double)p[c]); g.point_orig.push_back(p[c]); }
                 g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot]);
                 g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot + 1]);
+                g.point_kf.push_back(kf); g.point_slot.push_back(slot);
+                g.order_kf.push_back(b); g.order_slot.push_back(ord_slot);
                 return k;
             };
             // a slot's MapPoints are fixed within the pair: their graph indices are looked up once
@@ -419,8 +564,8 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             auto slot_points = [&](int slot, int32_t &a1, int32_t &a2) {
                 int32_t *c = &slot_pt[2 * (size_t)slot];
                 if (c[0] < 0) {
-                    c[0] = add_point(kf1.point_id[slot], kf1.point_pos + 3 * slot, slot);
-                    c[1] = add_point(kf2.point_id[slot], kf2.point_pos + 3 * slot, slot);
+                    c[0] = add_point(kf1.point_id[slot], b, slot, slot);
+                    c[1] = add_point(kf2.point_id[slot], a, slot, slot);
                 }
                 a1 = c[0];
                 a2 = c[1];
@@ -467,6 +612,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                     g.arap_pair.push_back(q);
                     g.arap_rot.push_back(rot_base + i); g.arap_rot.push_back(rot_base + j);
                     g.arap_w.push_back(M.w[k]);
+                    g.arap_wk.push_back(w_off + k);
                 }
             }
             rot_base += n1;
@@ -498,6 +644,9 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     d.order_xy = g.order_xy.data();
     g.memo_key = std::move(key);
     g.memo_valid = true;
+    g.struct_key = std::move(skey);
+    g.struct_valid = true;
+    g.ms_last = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
     return true;
 }
 

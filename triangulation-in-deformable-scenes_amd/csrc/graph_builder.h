@@ -30,6 +30,27 @@ struct GraphResult {
     std::vector<unsigned char> memo_key;
     bool memo_valid = false;
     int64_t memo_hits = 0;                    // calls answered from the memo (kept across rebuilds)
+    // structure memo (deformationOptimization's next round: the written-back map, positions / depth
+    // scales / T_g moved, everything else equal): the per-pair meshes and where every
+    // position-dependent value came from.  A later call with the same structure key whose every pair's
+    // previous triangulation is still THE Delaunay triangulation of the moved points (and whose vector
+    // map is still the identity) refreshes the values in place — the same descriptor, bit for bit, as a
+    // full build of that map (tests/test_graph.py::test_next_round_fast_path_is_a_full_build)
+    struct PairMesh {
+        std::vector<int32_t> tris, off, adj, pos_idx, inv;
+        int n1 = 0, n2 = 0, kf1 = 0, kf2 = 0, T = 0;
+        int64_t w_off = 0;
+        bool identity_map = false;
+    };
+    std::vector<unsigned char> struct_key;
+    bool struct_valid = false;
+    std::vector<PairMesh> meshes;
+    std::vector<double> wcat;                 // the pairs' CSR cot weights, concatenated
+    std::vector<int64_t> arap_wk;             // per ARAP edge: its weight's entry in wcat
+    std::vector<int32_t> point_kf, point_slot;   // per point: the keyframe (map order) and slot of its position
+    std::vector<int32_t> order_kf, order_slot;   // ... and of its ordering coordinates
+    int64_t struct_hits = 0;                  // calls answered by the structure memo
+    double ms_last = 0;                       // host time of the last build (either path)
 };
 
 // The per-pair geometry on the device (graph_dev.hip): the cot weights of the pair's CSR mesh (one

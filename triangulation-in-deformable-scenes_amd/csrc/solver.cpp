@@ -2216,6 +2216,14 @@ int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_w
     return 0;
 }
 
+int deftri_graph_stats(const deftri_ctx *ctx, int64_t *memo_hits, int64_t *struct_hits, double *ms_last) {
+    if (!ctx) return DEFTRI_E_ARG;
+    if (memo_hits) *memo_hits = ctx->graph.memo_hits;
+    if (struct_hits) *struct_hits = ctx->graph.struct_hits;
+    if (ms_last) *ms_last = ctx->graph.ms_last;
+    return 0;
+}
+
 int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n) {
     if (!ctx || !ids) return DEFTRI_E_ARG;
     if (n != (int64_t)ctx->graph.point_mpid.size()) return DEFTRI_E_ARG;

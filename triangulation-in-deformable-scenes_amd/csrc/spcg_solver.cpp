@@ -180,7 +180,19 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     have_ = false;
     P = DevProblem();
     G = SpDev();
+    static const bool timing = std::getenv("DEFTRI_UPLOAD_TIMING") != nullptr;
+    const auto tu0 = std::chrono::steady_clock::now();
     if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err)) return DEFTRI_E_ARG;
+    const auto tu1 = std::chrono::steady_clock::now();
+    struct Report {                 // DEFTRI_UPLOAD_TIMING=1: plan build vs the rest of the upload
+        bool on; std::chrono::steady_clock::time_point a, b;
+        ~Report() {
+            if (on)
+                std::fprintf(stderr, "[deftri upload] plan %.1f ms, values + allocations + copies %.1f ms\n",
+                             std::chrono::duration<double, std::milli>(b - a).count(),
+                             std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b).count());
+        }
+    } rep_{timing, tu0, tu1};
     const int32_t NP = d.n_points, Q = d.n_pairs, S = d.n_scales, C = d.n_cams;
     const int64_t nloc = (int64_t)H.arap_ids.size();
     const int32_t nown = H.hi - H.lo;
