@@ -110,7 +110,13 @@ def end_to_end(device, m, configure, n_it=25):
         out[key + "_lm_s"] = round(rep["ms_total"] * 1e-3, 4)
         out[key + "_iterations"] = rep["iterations"]
         out[key + "_plan_reuses"] = rep["plan_reuses"]
+        mh, sh, gms = c.graph_stats()
+        out[key + "_graph_ms"] = round(gms, 2)
+        out[key + "_graph_path"] = "memo" if mh > out.get("_mh", 0) else ("structure memo" if sh > out.get("_sh", 0) else "full")
+        out["_mh"], out["_sh"] = mh, sh
     fresh.close()
+    out.pop("_mh", None)
+    out.pop("_sh", None)
     return out
 
 

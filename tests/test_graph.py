@@ -173,8 +173,10 @@ FIELDS_ALL = ("points", "tg", "scales", "cam_kb8", "cam_pose", "rep_point", "rep
               "arap_w", "rot", "pair_area", "pair_info", "order_xy", "point_ids")
 
 
-def _same(pa, pb):
+def _same(pa, pb, skip=()):
     for f in FIELDS_ALL:
+        if f in skip:
+            continue
         a, b = getattr(pa, f), getattr(pb, f)
         assert a.shape == b.shape and np.array_equal(a, b), f
 
@@ -185,7 +187,8 @@ def test_next_round_fast_path_is_a_full_build(n, seed, k):
     moved points, depth scales and T_g but the same structure.  When every pair's previous Delaunay
     triangulation is still THE Delaunay triangulation of the moved points, the structure memo
     refreshes the values in place — the descriptor must equal a fresh context's full build bit for
-    bit; when the motion flips an edge it must fall back to the full build (still equal)."""
+    bit (except the ordering hint order_xy, kept from the structure's first build so the device plan
+    is reused); when the motion flips an edge it must fall back to the full build (then all equal)."""
     import copy
     from deftri import metrics
     if k == 2:
@@ -195,6 +198,7 @@ def test_next_round_fast_path_is_a_full_build(n, seed, k):
     rng = np.random.default_rng(seed)
     with capi.Context(-1) as a:
         p0 = a.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        order0 = p0.order_xy
         ext = np.abs(p0.points).max()
         for step, (scale, expect_fast) in enumerate([(1e-9, True), (3e-9, True), (3e-2, False)]):
             m2 = copy.deepcopy(m)
@@ -212,10 +216,14 @@ def test_next_round_fast_path_is_a_full_build(n, seed, k):
             fast = a.graph_stats()[1] > before
             with capi.Context(-1) as b:
                 pb = b.build_graph(m2, 1.5, 1e5, np.float32(0.004))
-            _same(pa, pb)
             if expect_fast:
+                # order_xy (the plan's ordering hint) stays that of the structure's first build
                 assert fast, (step, scale)
+                _same(pa, pb, skip=("order_xy",))
+                assert np.array_equal(pa.order_xy, order0)
             else:
                 assert not fast, (step, scale)
+                _same(pa, pb)
+                order0 = pa.order_xy
             m = m2
             p0 = pa

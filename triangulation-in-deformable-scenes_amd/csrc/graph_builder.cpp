@@ -375,12 +375,12 @@ int refresh_graph(const deftri_map &map, double rep_weight, double arap_weight, 
         }
         rbase += 9 * (size_t)pm.n1;
     }
+    // order_xy is kept: the ordering coordinates of the build that established this structure (the
+    // plan's row order is a locality choice, not arithmetic of the reference), so the device keeps
+    // its plan and only copies values (deftri_problem_upload's reuse test compares them)
     for (size_t i = 0; i < g.point_kf.size(); i++) {
         const float *p = map.keyframes[g.point_kf[i]].point_pos + 3 * (size_t)g.point_slot[i];
         for (int c = 0; c < 3; c++) { g.points[3 * i + c] = (double)p[c]; g.point_orig[3 * i + c] = p[c]; }
-        const float *o = map.keyframes[g.order_kf[i]].point_pos + 3 * (size_t)g.order_slot[i];
-        g.order_xy[2 * i] = (double)o[0];
-        g.order_xy[2 * i + 1] = (double)o[1];
     }
     for (size_t e = 0; e < g.arap_wk.size(); e++) g.arap_w[e] = g.wcat[g.arap_wk[e]];
     for (size_t e = 0; e < g.rep_info.size(); e++) g.rep_info[e] = g.rep_base[e] * rep_weight;

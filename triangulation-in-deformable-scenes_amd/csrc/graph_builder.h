@@ -35,7 +35,9 @@ struct GraphResult {
     // position-dependent value came from.  A later call with the same structure key whose every pair's
     // previous triangulation is still THE Delaunay triangulation of the moved points (and whose vector
     // map is still the identity) refreshes the values in place — the same descriptor, bit for bit, as a
-    // full build of that map (tests/test_graph.py::test_next_round_fast_path_is_a_full_build)
+    // full build of that map, except order_xy (the ordering hint): it keeps the coordinates of the
+    // build that established the structure, so the device plan is reused
+    // (tests/test_graph.py::test_next_round_fast_path_is_a_full_build)
     struct PairMesh {
         std::vector<int32_t> tris, off, adj, pos_idx, inv;
         int n1 = 0, n2 = 0, kf1 = 0, kf2 = 0, T = 0;
