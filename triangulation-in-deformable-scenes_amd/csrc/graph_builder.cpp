@@ -307,32 +307,33 @@ double mesh_area(const std::vector<double> &pos, const std::vector<int32_t> &tri
 int refresh_graph(const deftri_map &map, double rep_weight, double arap_weight, double info_dep, GraphResult &g,
                   GraphDevice *gdev, std::string &err) {
     const size_t np = g.meshes.size();
-    std::vector<std::vector<double>> P1(np), P2(np);
+    // validate every distinct mesh (pairs sharing keyframe 1 share one) on the moved positions
+    std::vector<const GraphResult::MeshData *> seen;
+    std::vector<std::vector<double>> P1;
+    std::vector<int> mesh_of(np, -1);
     for (size_t q = 0; q < np; q++) {
-        const GraphResult::PairMesh &pm = g.meshes[q];
-        if (!pm.identity_map) return 1;
-        const deftri_keyframe &kf1 = map.keyframes[pm.kf1], &kf2 = map.keyframes[pm.kf2];
-        std::vector<double> &pos1 = P1[q], &pos2 = P2[q];
-        pos1.reserve(3 * (size_t)pm.n1);
-        pos2.reserve(3 * (size_t)pm.n2);
+        const GraphResult::MeshData *md = g.meshes[q].mesh.get();
+        const auto it = std::find(seen.begin(), seen.end(), md);
+        if (it != seen.end()) { mesh_of[q] = (int)(it - seen.begin()); continue; }
+        if (!md->identity_map) return 1;
+        const deftri_keyframe &kf1 = map.keyframes[g.meshes[q].kf1];
+        std::vector<double> pos1;
+        pos1.reserve(3 * (size_t)md->n1);
         for (int s = 0; s < kf1.n_slots; s++)
             if (kf1.point_id[s] >= 0)
                 for (int k = 0; k < 3; k++) pos1.push_back((double)kf1.point_pos[3 * s + k]);
-        for (int s = 0; s < kf2.n_slots; s++)
-            if (kf2.point_id[s] >= 0)
-                for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
-        if ((int)pos1.size() != 3 * pm.n1 || (int)pos2.size() != 3 * pm.n2) return 1;
-        std::vector<double> xy(2 * (size_t)pm.n1);
-        for (int i = 0; i < pm.n1; i++) { xy[2 * i] = pos1[3 * i]; xy[2 * i + 1] = pos1[3 * i + 1]; }
-        if (!delaunay_still_valid(xy.data(), pm.n1, pm.tris)) return 1;
+        if ((int)pos1.size() != 3 * md->n1) return 1;
+        std::vector<double> xy(2 * (size_t)md->n1);
+        for (int i = 0; i < md->n1; i++) { xy[2 * i] = pos1[3 * i]; xy[2 * i + 1] = pos1[3 * i + 1]; }
+        if (!delaunay_still_valid(xy.data(), md->n1, md->tris)) return 1;
         // createVectorMap stays the identity unless two points became approximately equal
         // (isApprox 1e-6); such a pair's 2-D nearest neighbour is a Delaunay edge no longer than
         // 1e-6 |p|: no such edge, no such pair
-        for (int i = 0; i < pm.n1; i++) {
+        for (int i = 0; i < md->n1; i++) {
             const double *u = &pos1[3 * i];
             const double nu = u[0] * u[0] + u[1] * u[1] + u[2] * u[2];
-            for (int32_t k = pm.off[i]; k < pm.off[i + 1]; k++) {
-                const int j = pm.adj[k];
+            for (int32_t k = md->off[i]; k < md->off[i + 1]; k++) {
+                const int j = md->adj[k];
                 if (j < i) continue;
                 const double *v = &pos1[3 * j];
                 const double nv = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
@@ -340,40 +341,53 @@ int refresh_graph(const deftri_map &map, double rep_weight, double arap_weight, 
                 if (dx * dx + dy * dy <= 1e-12 * std::max(nu, nv)) return 1;
             }
         }
+        mesh_of[q] = (int)seen.size();
+        seen.push_back(md);
+        P1.push_back(std::move(pos1));
     }
-    // every pair keeps its mesh: the values
+    // every mesh still holds: the values
+    std::vector<double> areas(seen.size());
+    for (size_t m = 0; m < seen.size(); m++) areas[m] = mesh_area(P1[m], seen[m]->tris);
     size_t rbase = 0;
     for (size_t q = 0; q < np; q++) {
         const GraphResult::PairMesh &pm = g.meshes[q];
+        const GraphResult::MeshData &md = *pm.mesh;
+        const std::vector<double> &pos1 = P1[mesh_of[q]];
         const deftri_keyframe &kf1 = map.keyframes[pm.kf1], &kf2 = map.keyframes[pm.kf2];
+        std::vector<double> pos2;
+        pos2.reserve(3 * (size_t)pm.n2);
+        for (int s = 0; s < kf2.n_slots; s++)
+            if (kf2.point_id[s] >= 0)
+                for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
+        if ((int)pos2.size() != 3 * pm.n2) { err = "graph structure memo: keyframe 2 changed"; return -1; }
         double Tg[7];
         pair_tg(map, pm.kf2, pm.kf1, Tg);
         for (int i = 0; i < 7; i++) g.tg[7 * q + i] = Tg[i];
         g.scales[2 * q] = kf1.depth_scale;
         g.scales[2 * q + 1] = kf2.depth_scale;
-        g.pair_area[q] = mesh_area(P1[q], pm.tris);
-        g.pair_info[q] = arap_weight * std::pow((double)pm.T, 2);
+        g.pair_area[q] = areas[mesh_of[q]];
+        g.pair_info[q] = arap_weight * std::pow((double)md.T, 2);
         double *Rs = g.rot.data() + rbase;
         double *w = g.wcat.data() + pm.w_off;
         int dev_rc = 1;
         if (gdev) {
-            dev_rc = gdev->mesh_pass(pm.n1, pm.n2, pm.tris.data(), (int)pm.tris.size() / 3, pm.off.data(), pm.adj.data(),
-                                     (int64_t)pm.adj.size(), pm.pos_idx.data(), pm.inv.data(), P1[q].data(), P2[q].data(), w,
-                                     Rs, err);
+            dev_rc = gdev->mesh_pass(md.n1, pm.n2, md.tris.data(), (int)md.tris.size() / 3, md.off.data(), md.adj.data(),
+                                     (int64_t)md.adj.size(), md.pos_idx.data(), md.inv.data(), pos1.data(), pos2.data(), w, Rs,
+                                     err);
             if (dev_rc < 0) return -1;
         }
         if (dev_rc != 0) {
             Mesh M;
-            M.tris = pm.tris; M.off = pm.off; M.adj = pm.adj;
-            mesh_cot_weights(P1[q], M);
+            M.tris = md.tris; M.off = md.off; M.adj = md.adj;
+            mesh_cot_weights(pos1, M);
             std::copy(M.w.begin(), M.w.end(), w);
-            parallel_for(pm.n1, 2048, [&](int lo, int hi) {
+            parallel_for(md.n1, 2048, [&](int lo, int hi) {
                 for (int i = lo; i < hi; i++)
-                    compute_r_vertex(i, pm.n2, pm.off.data(), pm.adj.data(), w, pm.pos_idx.data(), pm.inv.data(), P1[q].data(),
-                                     P2[q].data(), Rs + 9 * (size_t)i);
+                    compute_r_vertex(i, pm.n2, md.off.data(), md.adj.data(), w, md.pos_idx.data(), md.inv.data(), pos1.data(),
+                                     pos2.data(), Rs + 9 * (size_t)i);
             });
         }
-        rbase += 9 * (size_t)pm.n1;
+        rbase += 9 * (size_t)md.n1;
     }
     // order_xy is kept: the ordering coordinates of the build that established this structure (the
     // plan's row order is a locality choice, not arithmetic of the reference), so the device keeps
@@ -473,6 +487,9 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     static const bool timing = std::getenv("DEFTRI_GRAPH_TIMING") != nullptr;
     auto tnow = [] { return std::chrono::steady_clock::now(); };
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    // the mesh of keyframe 1's positions (Delaunay, adjacency, area, cot weights, vector map), built
+    // once per keyframe: every pair with that keyframe 1 has the same v1Positions
+    std::vector<std::shared_ptr<GraphResult::MeshData>> kf1_mesh(K);
     for (int a = 0; a < K; a++) {
         for (int b = a + 1; b < K; b++) {
             if (pair_window > 0 && b - a > pair_window) continue;
@@ -480,27 +497,39 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             const deftri_keyframe &kf2 = map.keyframes[a];   // pKF2 = k1->second
             const int32_t q = (int32_t)g.pair_area.size();
             // extractPositions
-            std::vector<double> pos1, pos2;
-            pos1.reserve(3 * (size_t)kf1.n_slots);
+            std::vector<double> pos2;
             pos2.reserve(3 * (size_t)kf2.n_slots);
-            for (int s = 0; s < kf1.n_slots; s++)
-                if (kf1.point_id[s] >= 0)
-                    for (int k = 0; k < 3; k++) pos1.push_back((double)kf1.point_pos[3 * s + k]);
             for (int s = 0; s < kf2.n_slots; s++)
                 if (kf2.point_id[s] >= 0)
                     for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
-            const int n1 = (int)pos1.size() / 3, n2 = (int)pos2.size() / 3;
             auto t0 = tnow();
-            Mesh M;
-            if (!build_mesh(pos1, n1, M, err, gdev == nullptr)) return false;   // device: weights in the device pass
+            if (!kf1_mesh[b]) {
+                auto md = std::make_shared<GraphResult::MeshData>();
+                for (int s = 0; s < kf1.n_slots; s++)
+                    if (kf1.point_id[s] >= 0)
+                        for (int k = 0; k < 3; k++) md->pos1.push_back((double)kf1.point_pos[3 * s + k]);
+                md->n1 = (int)md->pos1.size() / 3;
+                Mesh M;
+                if (!build_mesh(md->pos1, md->n1, M, err, gdev == nullptr)) return false;   // device: weights in the device pass
+                md->tris = std::move(M.tris); md->off = std::move(M.off); md->adj = std::move(M.adj);
+                md->w = std::move(M.w);
+                md->T = M.T; md->hull = M.hull; md->area = M.area;
+                md->pos_idx = vector_map(md->pos1, md->n1);
+                md->inv.assign(md->n1, -1);          // invertedPosIndexes: the last vertex wins
+                for (int v = 0; v < md->n1; v++) md->inv[md->pos_idx[v]] = v;
+                md->identity_map = M.skipped == 0;
+                for (int v = 0; v < md->n1 && md->identity_map; v++) md->identity_map = md->pos_idx[v] == v;
+                kf1_mesh[b] = md;
+            }
+            const GraphResult::MeshData &MD = *kf1_mesh[b];
+            const std::vector<double> &pos1 = MD.pos1;
+            const std::vector<int32_t> &posIdx = MD.pos_idx, &inv = MD.inv;
+            const int n1 = MD.n1, n2 = (int)pos2.size() / 3;
+            Mesh M;                                         // this pair's weights over the shared structure
+            M.off = MD.off; M.adj = MD.adj; M.w = MD.w; M.T = MD.T; M.hull = MD.hull; M.area = MD.area;
             auto t1 = tnow();
             double Tg[7];
             pair_tg(map, a, b, Tg);
-            const std::vector<int32_t> posIdx = vector_map(pos1, n1);
-            std::vector<int32_t> inv(n1, -1);           // invertedPosIndexes: the last vertex wins
-            for (int v = 0; v < n1; v++) inv[posIdx[v]] = v;
-            bool identity = M.skipped == 0;
-            for (int v = 0; v < n1 && identity; v++) identity = posIdx[v] == v;
             auto t2 = tnow();
             // computeR: one Procrustes rotation per vertex, identity where no position maps to it
             const size_t rbase = g.rot.size();
@@ -509,11 +538,11 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             int dev_rc = 1;
             if (gdev) {
                 M.w.resize(M.adj.size());
-                dev_rc = gdev->mesh_pass(n1, n2, M.tris.data(), (int)M.tris.size() / 3, M.off.data(), M.adj.data(),
+                dev_rc = gdev->mesh_pass(n1, n2, MD.tris.data(), (int)MD.tris.size() / 3, M.off.data(), M.adj.data(),
                                          (int64_t)M.adj.size(), posIdx.data(), inv.data(), pos1.data(), pos2.data(), M.w.data(),
                                          Rs, err);
                 if (dev_rc < 0) return false;
-                if (dev_rc == 1) mesh_cot_weights(pos1, M);     // non-manifold edge: the host loops (all corners)
+                if (dev_rc == 1) { M.tris = MD.tris; mesh_cot_weights(pos1, M); }   // non-manifold edge: the host loops
             }
             if (dev_rc != 0) {
                 parallel_for(n1, 2048, [&](int lo, int hi) {
@@ -525,10 +554,9 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             auto t3 = tnow();
             {
                 GraphResult::PairMesh pm;
-                pm.tris = M.tris; pm.off = M.off; pm.adj = M.adj; pm.pos_idx = posIdx; pm.inv = inv;
-                pm.n1 = n1; pm.n2 = n2; pm.kf1 = b; pm.kf2 = a; pm.T = M.T;
+                pm.mesh = kf1_mesh[b];
+                pm.n2 = n2; pm.kf1 = b; pm.kf2 = a;
                 pm.w_off = (int64_t)g.wcat.size();
-                pm.identity_map = identity;
                 g.wcat.insert(g.wcat.end(), M.w.begin(), M.w.end());
                 g.meshes.push_back(std::move(pm));
             }

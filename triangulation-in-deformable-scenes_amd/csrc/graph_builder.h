@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -38,11 +39,19 @@ struct GraphResult {
     // full build of that map, except order_xy (the ordering hint): it keeps the coordinates of the
     // build that established the structure, so the device plan is reused
     // (tests/test_graph.py::test_next_round_fast_path_is_a_full_build)
-    struct PairMesh {
+    // a pair's mesh depends only on its keyframe 1's positions (v1Positions, :653-662): the pairs
+    // that share keyframe 1 (every all-pairs graph) share one mesh
+    struct MeshData {
         std::vector<int32_t> tris, off, adj, pos_idx, inv;
-        int n1 = 0, n2 = 0, kf1 = 0, kf2 = 0, T = 0;
-        int64_t w_off = 0;
+        std::vector<double> pos1, w;          // positions (x y z) and host cot weights (empty: device pass)
+        int n1 = 0, T = 0, hull = 0;
+        double area = 0;
         bool identity_map = false;
+    };
+    struct PairMesh {
+        std::shared_ptr<const MeshData> mesh;
+        int n2 = 0, kf1 = 0, kf2 = 0;
+        int64_t w_off = 0;
     };
     std::vector<unsigned char> struct_key;
     bool struct_valid = false;
