@@ -138,12 +138,6 @@ struct SpDev {
     const int4 *aslot = nullptr;
     const int32_t *dslot = nullptr;
     double *sval = nullptr;
-    // per LM iteration (fp64 storage): k_sp_scatter_slices writes each ARAP slot's J slice (pj), W
-    // (pw) and error (pe) from the edge side; k_sp_glin_rows streams them (DEFTRI_SP_NO_SCATTER=1: the
-    // gathering form)
-    int32_t scatter = 0;
-    int64_t nloc = 0;
-    double *pw = nullptr, *pe = nullptr;
     const int64_t *woff = nullptr;
     double *pj = nullptr;                              // packed J slices: [3][nslots * 64] (fp64)
     float *pj32 = nullptr;                             // the same in fp32 (fp32 Jacobian storage)

@@ -116,36 +116,7 @@ __device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; 
 // couplings c_e = W J_p J_s; and, slot by slot, the packed J slices phase 2 reads (an ARAP slice is
 // gathered once: added into H_v and stored).  Slots of a row: its incidences in the plan's order,
 // then its depth couplings, then padding.
-// k_sp_scatter_slices (fp64 storage, G.scatter): one thread per local ARAP edge reads its J (the 4
-// points' 3-column slices, coalesced column-major), W and e once and writes them into the slots of
-// its own-row roles (aslot) — pj, pw, pe — so k_sp_glin_rows<.., true> streams them instead of
-// gathering every slice through the slot's edge index (the same values: H_v and b_v bit-identical)
-__global__ void __launch_bounds__(256) k_sp_scatter_slices(const SpDev G) {
-    if (gated_off(G.lgate)) return;
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= G.nloc) return;
-    const int4 sl = G.aslot[e];
-    const int pos[4] = {sl.x, sl.y, sl.z, sl.w};
-    const int64_t n = G.nslots * 64, jld = G.jld;
-    double J[12];
-#pragma unroll
-    for (int c = 0; c < 12; c++) J[c] = G.Ja[c * jld + e];
-    const double w = G.Wa[e], er = G.Ea[e];
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-        const int k = pos[r];
-        if (k < 0) continue;
-#pragma unroll
-        for (int c = 0; c < 3; c++) G.pj[c * n + k] = J[3 * r + c];
-        G.pw[k] = w;
-        G.pe[k] = er;
-    }
-}
-
-// SC (G.scatter): the ARAP slots' slice, W and e come from the slot arrays k_sp_scatter_slices
-// filled (coalesced loads, no edge-index dependence); only depth couplings and padding are formed
-// and stored here
-template <class JT, bool SC>
+template <class JT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3)))
 k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
@@ -199,25 +170,16 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
         const double *__restrict__ Ja = G.Ja, *__restrict__ Wa = G.Wa, *__restrict__ Ea = G.Ea;
         const double *__restrict__ Jd = G.Jd, *__restrict__ Wd = G.Wd;
         const int64_t jld = G.jld;
-        auto load = [&](int m, int64_t kk) -> Raw {
+        auto load = [&](int m) -> Raw {
             const bool dep = m <= -2;
             const int mm = max(m, 0), jj = max(-2 - m, 0);
-            if constexpr (SC) {
-                // ARAP and padding from the slot arrays (padding holds zeros); a depth coupling from
-                // its edge (one per row: the only dependent load left)
-                const double *pd = Jd + 4 * (int64_t)jj;
-                const double s0 = G.pj[kk], s1 = G.pj[n + kk], s2 = G.pj[2 * n + kk], sw = G.pw[kk], se = G.pe[kk];
-                if (dep) return Raw{pd[0], pd[1], pd[2], Wd[jj], pd[3]};
-                return Raw{s0, s1, s2, sw, se};
-            } else {
-                const double *pa = Ja + (int64_t)(3 * (mm & 3)) * jld + (mm >> 2);   // ARAP (padding: edge 0)
-                const double *pd = Jd + 4 * (int64_t)jj;
-                const double *Jc = dep ? pd : pa;
-                const int64_t st = dep ? 1 : jld;
-                const double *W = dep ? Wd + jj : Wa + (mm >> 2);
-                const double *X = dep ? pd + 3 : Ea + (mm >> 2);
-                return Raw{Jc[0], Jc[st], Jc[2 * st], *W, *X};
-            }
+            const double *pa = Ja + (int64_t)(3 * (mm & 3)) * jld + (mm >> 2);   // ARAP (padding: edge 0)
+            const double *pd = Jd + 4 * (int64_t)jj;
+            const double *Jc = dep ? pd : pa;
+            const int64_t st = dep ? 1 : jld;
+            const double *W = dep ? Wd + jj : Wa + (mm >> 2);
+            const double *X = dep ? pd + 3 : Ea + (mm >> 2);
+            return Raw{Jc[0], Jc[st], Jc[2 * st], *W, *X};
         };
         auto value = [&](int m, const Raw &r, double *v, double &wt, double &er) {
             const bool arap = m >= 0, dep = m <= -2;
@@ -246,15 +208,14 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
 #pragma unroll
             for (int u = 0; u < U; u++) m[u] = G.pmap[k + 64 * u];
 #pragma unroll
-            for (int u = 0; u < U; u++) r[u] = load(m[u], k + 64 * u);
+            for (int u = 0; u < U; u++) r[u] = load(m[u]);
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 double v[3], wt, er;
                 value(m[u], r[u], v, wt, er);
                 add(v, wt, er);
-                if (!SC || m[u] < 0)
 #pragma unroll
-                    for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
+                for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
             }
             k += U * 64;
         };
@@ -263,11 +224,10 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
         for (; k < k1; k += 64) {
             const int m = G.pmap[k];
             double v[3], wt, er;
-            value(m, load(m, k), v, wt, er);
+            value(m, load(m), v, wt, er);
             add(v, wt, er);
-            if (!SC || m < 0)
 #pragma unroll
-                for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
+            for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
         }
         if (l >= 0) {
 #pragma unroll
@@ -1541,11 +1501,8 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
     } while (0)
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, false>), sp::row_grid(G.nrb), G, G.pj32);
-    else if (G.scatter) {
-        if (G.nloc > 0) SPL("sp_scatter", sp::k_sp_scatter_slices, nblk(G.nloc, 256), G);
-        SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, true>), sp::row_grid(G.nrb), G, G.pj);
-    } else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, false>), sp::row_grid(G.nrb), G, G.pj);
+    if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, sp::row_grid(G.nrb), G, G.pj32);
+    else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, sp::row_grid(G.nrb), G, G.pj);
     if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
     if (G.nch > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.nch, G);
 }

@@ -301,19 +301,10 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.dslot = ds;
         ALLOC(G.sval, 64 * G.nslots);
         SPOK(hipMemset(G.sval, 0, sizeof(double) * 64 * (size_t)G.nslots));
-        static const bool no_scatter = std::getenv("DEFTRI_SP_NO_SCATTER") != nullptr;
-        G.nloc = nloc;
-        G.scatter = (!fp32_jac && !no_scatter) ? 1 : 0;
-        if (G.scatter) {
-            ALLOC(G.pw, 64 * G.nslots); ALLOC(G.pe, 64 * G.nslots);
-            SPOK(hipMemset(G.pw, 0, sizeof(double) * 64 * (size_t)G.nslots));
-            SPOK(hipMemset(G.pe, 0, sizeof(double) * 64 * (size_t)G.nslots));
-        }
         H.aslot.clear(); H.aslot.shrink_to_fit();
         H.dslot.clear(); H.dslot.shrink_to_fit();
         if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
         else { ALLOC(G.pj, 3 * 64 * G.nslots); }
-        if (G.scatter) SPOK(hipMemset(G.pj, 0, sizeof(double) * 3 * 64 * (size_t)G.nslots));
         H.pmap.clear(); H.pmap.shrink_to_fit();
     }
     ALLOC(G.Hv, 6 * (int64_t)nown); ALLOC(G.Dv, 6 * (int64_t)nown); ALLOC(G.Mv, 6 * (int64_t)nown);
