@@ -88,13 +88,11 @@ struct SpPlanHost {
     // phase-2 wave layout: rows dealt to 64-lane waves (sorted by entry count inside windows of
     // kSpSortWindow rows so a wave pads little); wave w's entries are slots woff[w] .. woff[w + 1] - 1,
     // slot k of lane j at [k][64] + j.  pmap: ARAP incidence le << 2 | role, depth coupling -(2 + j)
-    // (local depth edge j), -1 padding (what k_sp_glin_rows packs the slot's J slice from)
+    // (local depth edge j), -1 padding; pidx (what phase 2 multiplies the slot's J by): s[le] for
+    // ARAP, -(2 + scale) for a depth coupling (p of the scale), -1 padding
     std::vector<int32_t> rowmap;                       // [nwaves * 64]: local row per lane (-1 padding)
     std::vector<int64_t> woff;                         // nwaves + 1, in slots
-    std::vector<int32_t> pmap;                         // [slots * 64]
-    // slot positions (k * 64 + lane in the wave layout) phase 1 writes its values into: per local ARAP
-    // edge and role (-1: a row of another rank), per local depth edge its coupling slot
-    std::vector<int32_t> aslot, dslot;
+    std::vector<int32_t> pmap, pidx;                   // [slots * 64]
     int32_t max_heavy_blocks = 0;                      // most phase-1 blocks of one heavy vertex
     // halo exchange: rows (global) sent to / received from each peer, ascending
     std::vector<std::vector<int32_t>> send_rows, recv_rows;
@@ -131,13 +129,7 @@ struct SpDev {
     int64_t jld = 0;                                   // column stride of Ja / Ja32 ([18][jld])
     int32_t nwaves = 0, heavy_split = 0;
     int64_t nslots = 0;                                // wave-layout slots (x 64 lanes)
-    const int32_t *rowmap = nullptr, *pmap = nullptr;
-    // phase 1 writes each product value straight into phase 2's slot layout: s_e into the slots of the
-    // edge's own-row roles (aslot), p of a depth edge's scale into its coupling slot (dslot); phase 2
-    // streams sval[k * 64 + lane] beside the J slices (padding slots stay 0)
-    const int4 *aslot = nullptr;
-    const int32_t *dslot = nullptr;
-    double *sval = nullptr;
+    const int32_t *rowmap = nullptr, *pmap = nullptr, *pidx = nullptr;
     const int64_t *woff = nullptr;
     double *pj = nullptr;                              // packed J slices: [3][nslots * 64] (fp64)
     float *pj32 = nullptr;                             // the same in fp32 (fp32 Jacobian storage)
@@ -152,6 +144,7 @@ struct SpDev {
     // CG
     double *r = nullptr, *q = nullptr, *x = nullptr;
     double2 *zp = nullptr;                                // (z, p) per dof
+    double *s = nullptr;                                  // phase-1 s_e per local ARAP edge
     double *part = nullptr;                               // phase-1 block partials [nblk][8]
     double *rpart = nullptr;                              // row-block partials: phase 2 p.q [nrb]; update (rz, rr) [nrb + 1][2]
     double *upart = nullptr;

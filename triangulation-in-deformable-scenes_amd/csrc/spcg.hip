@@ -930,11 +930,7 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
 #pragma unroll
             for (int c = 0; c < 6; c++) t += J[12 + c] * pval(G.zp, beta, oT + c);
             const double s = G.Wa[i] * t;
-            const int4 sl = G.aslot[i];              // the slots of the edge's own-row roles
-            if (sl.x >= 0) G.sval[sl.x] = s;
-            if (sl.y >= 0) G.sval[sl.y] = s;
-            if (sl.z >= 0) G.sval[sl.z] = s;
-            if (sl.w >= 0) G.sval[sl.w] = s;
+            G.s[i] = s;
             if (MG && owned) pap = s * t;            // (one rank: every edge owned)
             if (owned)
 #pragma unroll
@@ -965,7 +961,6 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
             const double *c = G.cdep + 3 * (int64_t)le;
             const double cp = (c[0] * pval(G.zp, beta, o) + c[1] * pval(G.zp, beta, o + 1)) + c[2] * pval(G.zp, beta, o + 2);
             const double ps = pval(G.zp, beta, 6 * (int64_t)G.Q + d.y);
-            G.sval[G.dslot[le]] = ps;                // p of the scale into the row's coupling slot
             t = cp + G.wss[le] * ps;
             if (MG) pap = ps * (cp + t);
         }
@@ -1077,19 +1072,59 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         const int l = G.rowmap[64 * w + lane];
         const int64_t n = G.nslots * 64;
         const JT *pjx = pj, *pjy = pj + n, *pjz = pj + 2 * n;
+        const int64_t os = 6 * (int64_t)G.Q;
         double q[3] = {0.0, 0.0, 0.0};
         int64_t k = G.woff[w] * 64 + lane;
         const int64_t k1 = G.woff[w + 1] * 64 + lane;
-        // the slot values phase 1 wrote (s_e of the incidence's edge, p of a depth coupling's scale, 0
-        // in padding) stream beside the J slices: every load of a step coalesced and independent
-        const double *__restrict__ sv_ = G.sval;
+        // s_e (v >= 0), p of the depth scale -2 - v (v <= -2) or 0 (padding): both loads on every
+        // path and a select, so the slots of a step keep their loads in flight (the scales' (z, p)
+        // are a handful of cache lines)
+        const double *__restrict__ sv_ = G.s;
+        const double2 *__restrict__ zp_ = G.zp;
+        const double *__restrict__ ph_ = G.ph;
+        auto val = [&](int v) -> double {
+            const double a = sv_[max(v, 0)];
+            if constexpr (MG) {
+                // p from phase 1's copy (the heavy workgroups rewrite zp); blended arithmetically (both
+                // terms finite, one factor 1 and one 0: exact) — with a select the compiler sinks this
+                // load into a per-slot branch that waits on every load in flight
+                const double p = ph_[os + max(-2 - v, 0)];
+                return a * (v >= 0 ? 1.0 : 0.0) + p * (v <= -2 ? 1.0 : 0.0);
+            } else {
+                const double2 z = zp_[os + max(-2 - v, 0)];
+                const double p = __fma_rn(beta, z.y, z.x);
+                return v >= 0 ? a : (v <= -2 ? p : 0.0);
+            }
+        };
+        // U slots per step: their indices, then the values and J slices, then the adds in order
         auto step = [&](auto U_) {
             constexpr int U = decltype(U_)::value;
+            int v[U];
             double sv[U], J[U][3];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
-                sv[u] = sv_[k + 64 * u];
+            for (int u = 0; u < U; u++) v[u] = G.pidx[k + 64 * u];
+            if constexpr (MG) {
+                // every load of the step first (s_e, the scale's p, the J slice), the arithmetic after:
+                // one round trip per step instead of one per slot
+                double a[U], pp[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    a[u] = sv_[max(v[u], 0)];
+                    pp[u] = ph_[os + max(-2 - v[u], 0)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    sv[u] = a[u] * (v[u] >= 0 ? 1.0 : 0.0) + pp[u] * (v[u] <= -2 ? 1.0 : 0.0);
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    sv[u] = val(v[u]);
+                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                }
             }
 #pragma unroll
             for (int u = 0; u < U; u++)
@@ -1100,7 +1135,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{});
         if (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{});
         for (; k < k1; k += 64) {
-            const double sv = sv_[k];
+            const double sv = val(G.pidx[k]);
             q[0] += (double)pjx[k] * sv;
             q[1] += (double)pjy[k] * sv;
             q[2] += (double)pjz[k] * sv;

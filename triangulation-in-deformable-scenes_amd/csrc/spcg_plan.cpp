@@ -315,8 +315,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         }
         const int64_t nsl = H.woff[nw];
         H.pmap.assign((size_t)nsl * 64, -1);
-        H.aslot.assign(4 * (size_t)nloc, -1);
-        H.dslot.assign(H.dep_ids.size(), -1);
+        H.pidx.assign((size_t)nsl * 64, -1);
         for (int32_t w = 0; w < nw; w++)
             for (int j = 0; j < 64; j++) {
                 const int32_t l = H.rowmap[64 * (size_t)w + j];
@@ -324,11 +323,11 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                 int64_t k = H.woff[w];
                 for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++, k++) {
                     H.pmap[64 * k + j] = H.inc[x];
-                    H.aslot[H.inc[x]] = (int32_t)(64 * k + j);        // incidence le << 2 | role
+                    H.pidx[64 * k + j] = H.inc[x] >> 2;
                 }
                 for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++, k++) {
                     H.pmap[64 * k + j] = -(2 + x);
-                    H.dslot[x] = (int32_t)(64 * k + j);
+                    H.pidx[64 * k + j] = -(2 + d.dep_scale[H.dep_ids[x]]);
                 }
             }
     }
@@ -370,12 +369,11 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     // 10. algorithmic bytes of one product (phase 1 + phase 2): compulsory loads and
     //     stores, the p gathers at an edge's other points not counted
     const double jb = fp32_jac ? 72.0 : 144.0;
-    H.phase1_bytes = (double)nloc * (jb + 8 + 16 + 16)                 // J, W, rows, slot positions
-                     + (double)H.inc.size() * 8                          // s_e into its slots (one per own-row role)
-                     + (double)ndl * (4 + 4 + 4 + 24 + 8 + 8);           // dperm, row, slot, c, W J_s^2, p_s out
+    H.phase1_bytes = (double)nloc * (jb + 8 + 16 + 8)                  // J, W, rows, s
+                     + (double)ndl * (4 + 4 + 24 + 8);                  // dperm, row, c, W J_s^2
     H.phase2_bytes = (double)nown * (48 + 48 + 48 + 24 + 4)            // (z,p) in / out, D, q, row map
-                     + (double)H.inc.size() * (8 + jb / 6)               // slot value, packed J slice
-                     + (double)ndl * (8 + jb / 6);                       // depth-coupling slots
+                     + (double)H.inc.size() * (4 + 8 + jb / 6)           // slot index, s, packed J slice
+                     + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
     return true;
 }

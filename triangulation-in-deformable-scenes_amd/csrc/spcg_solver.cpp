@@ -291,21 +291,14 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         if (G.sd) G.m_nh = 8 * ((Q + S + 2 + 7) / 8);   // + the z.Az and (r.z, r.r) workgroups
     }
     {
-        int32_t *rm, *pm;
+        int32_t *rm, *pm, *pi;
         int64_t *wo;
-        PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap);
-        G.rowmap = rm; G.woff = wo; G.pmap = pm;
-        int32_t *as, *ds;
-        PUT(as, H.aslot); PUT(ds, H.dslot);
-        G.aslot = reinterpret_cast<const int4 *>(as);
-        G.dslot = ds;
-        ALLOC(G.sval, 64 * G.nslots);
-        SPOK(hipMemset(G.sval, 0, sizeof(double) * 64 * (size_t)G.nslots));
-        H.aslot.clear(); H.aslot.shrink_to_fit();
-        H.dslot.clear(); H.dslot.shrink_to_fit();
+        PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx);
+        G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi;
         if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
         else { ALLOC(G.pj, 3 * 64 * G.nslots); }
         H.pmap.clear(); H.pmap.shrink_to_fit();
+        H.pidx.clear(); H.pidx.shrink_to_fit();
     }
     ALLOC(G.Hv, 6 * (int64_t)nown); ALLOC(G.Dv, 6 * (int64_t)nown); ALLOC(G.Mv, 6 * (int64_t)nown);
     ALLOC(G.cdep, 3 * (int64_t)nd); ALLOC(G.wss, nd);
@@ -321,7 +314,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     double *zp;
     ALLOC(zp, 2 * zp_n);
     G.zp = reinterpret_cast<double2 *>(zp);
-    ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
+    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
     ALLOC(G.ph, std::max<int64_t>(H.hd, 1));
