@@ -630,7 +630,7 @@ def main():
                              else "per-problem LM it/s of N independent problems (not summed)"),
                        "cg_launches_per_iteration": info.get("cg_launches"),
                        "cg_collectives_per_iteration": info.get("cg_collectives"),
-                       "lm_control": "host" if os.environ.get("DEFTRI_HOST_LM") or sharded else "device"},
+                       "lm_control": "device" if os.environ.get("DEFTRI_DEVICE_LM") and not os.environ.get("DEFTRI_HOST_LM") and not sharded else "host"},
             "roofline": roofline,
             "roofline_factorization": roofline_f if roofline is not roofline_f else None,
             "cpu_baseline": cpu,

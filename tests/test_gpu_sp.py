@@ -362,6 +362,30 @@ def test_merged_cg_chain_matches_three_launch_chain():
         assert np.max(np.abs(x - y)) <= 1e-7 * max(np.max(np.abs(y)), 1.0)
 
 
+def test_phase2_step_size_bit_identical():
+    """Phase 2's slot loop in steps of 4 (6 waves per SIMD) or 8 slots (DEFTRI_SP_P2_STEP): the same
+    adds in the same slot order (a clamped last step adds exact zeros) — bit-identical LM runs."""
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{"DEFTRI_SP_P2_STEP": "4"}, {"DEFTRI_SP_P2_STEP": "8"}])
+    assert l0 == l1 == 2
+    assert c0 == c1 and t0 == t1 and i0 == i1
+    assert s0 == s1
+
+
+@pytest.mark.parametrize("rs", ["1", "4"])
+def test_phase2_row_split_matches(rs):
+    """Phase 2 with each row's slot list split over rs waves (DEFTRI_SP_ROW_SPLIT; default 2): q_v is
+    summed as (part 0 + part 1 ...) instead of in one run, so the steps differ at rounding level.
+    Tolerances as for the merged vs three-launch chains: identical trials and CG iteration counts,
+    chi2 rel 1e-8, states within 1e-7 of their largest magnitude."""
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{}, {"DEFTRI_SP_ROW_SPLIT": rs}])
+    assert l0 == l1 == 2
+    assert t0 == t1 and i0 == i1
+    np.testing.assert_allclose(c0, c1, rtol=1e-8)
+    for a, b in zip(s0, s1):
+        x, y = np.frombuffer(a), np.frombuffer(b)
+        assert np.max(np.abs(x - y)) <= 1e-7 * max(np.max(np.abs(y)), 1.0)
+
+
 def test_merged_chain_breakdown_then_solve():
     """A solve that breaks down inside the merged chain (a NaN in the right-hand side: p.Ap is NaN, so
     phase 2's workgroup 0 finds the breakdown while the other workgroups are running) fails loudly and
@@ -426,8 +450,8 @@ def test_rccl_one_rank_sharded_chain():
 def test_device_lm_matches_host_lm():
     """The device-driven LM (k_lm_decide: rho, accept / reject, lambda / nu, g2o's Terminate test in
     HBM; the host queues trial slots without reading each outcome) against the host loop
-    (DEFTRI_HOST_LM=1): the same decisions from the same sums — bit-identical LM runs."""
-    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{}, {"DEFTRI_HOST_LM": "1"}])
+    (the default): the same decisions from the same sums — bit-identical LM runs."""
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{"DEFTRI_DEVICE_LM": "1"}, {}])
     assert l0 == l1 == 2
     assert c0 == c1 and t0 == t1 and i0 == i1
     assert s0 == s1

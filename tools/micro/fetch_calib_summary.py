@@ -20,9 +20,11 @@ SIZES = [96 << 20, 768 << 20]
 
 
 def per_dispatch(path, ctr):
+    """Per dispatch of the calibration kernels (the runtime's buffer fills in between are skipped)."""
     vals = collections.OrderedDict()
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != ctr:
+        if r["Counter_Name"] != ctr or not ("k_read" in r["Kernel_Name"] or "k_gather" in r["Kernel_Name"]
+                                            or "k_write" in r["Kernel_Name"]):
             continue
         k = int(r["Dispatch_Id"])
         vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"]) * 1024.0
@@ -62,7 +64,8 @@ def main():
         json.dump(out, fh, indent=1)
     print(json.dumps({k: v for k, v in out.items() if k.startswith("factor")}, indent=1))
     for c in out["cases"]:
-        print(c)
+        if c["rep"] == 2:
+            print(c)
 
 
 if __name__ == "__main__":

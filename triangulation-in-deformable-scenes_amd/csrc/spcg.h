@@ -42,6 +42,8 @@ constexpr int kSpRed = 16;             // doubles per iteration in the reduction
 constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
 constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
+constexpr int kSpRowSplit = 1;         // phase 2: waves per row-wave's slot list (DEFTRI_SP_ROW_SPLIT)
+constexpr int kSpP2Step = 8;           // phase 2: slots per step (DEFTRI_SP_P2_STEP = 4 or 8)
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
 constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one thread per dof)
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
@@ -128,6 +130,14 @@ struct SpDev {
     const int32_t *inc = nullptr, *rep_off = nullptr, *dep_off = nullptr;
     int64_t jld = 0;                                   // column stride of Ja / Ja32 ([18][jld])
     int32_t nwaves = 0, heavy_split = 0;
+    // phase 2: each row-wave's slot steps split over rs waves (1, 2, 4); its workgroups hold 4 / rs
+    // row-waves, nrb2 = ceil(nwaves rs / 4) of them (p.q partials rpart [nrb2])
+    int32_t rs = 1, nrb2 = 0;
+    int32_t p2u = 8;                                   // phase 2's slots per step (8 or 4)
+    // diagnostics (DEFTRI_SP_P2_TRACE=<file>): per phase-2 wave of CG iteration p2tr_it, wall-clock
+    // stamps [start, rows / heavy sums done, alpha known, end, hw id, steps]
+    long long *p2tr = nullptr;
+    int32_t p2tr_it = -1;
     int64_t nslots = 0;                                // wave-layout slots (x 64 lanes)
     const int32_t *rowmap = nullptr, *pmap = nullptr, *pidx = nullptr;
     const int64_t *woff = nullptr;
@@ -146,7 +156,7 @@ struct SpDev {
     double2 *zp = nullptr;                                // (z, p) per dof
     double *s = nullptr;                                  // phase-1 s_e per local ARAP edge
     double *part = nullptr;                               // phase-1 block partials [nblk][8]
-    double *rpart = nullptr;                              // row-block partials: phase 2 p.q [nrb]; update (rz, rr) [nrb + 1][2]
+    double *rpart = nullptr;                              // phase-2 row-block partials p.q [nrb2]
     double *upart = nullptr;
     double *hbuf = nullptr;                               // [pq_rows, heavy sums (hd)]
     // [max_it + 2][kSpRed]: rz, rr, stop, alpha.  stop (word 2 of iteration it + 1): a breakdown /

@@ -746,14 +746,14 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
     if (h == nh) {
         double a = 0.0;
         int i = threadIdx.x;
-        for (; i + 3 * 256 < G.nrb; i += 4 * 256) {
+        for (; i + 3 * 256 < G.nrb2; i += 4 * 256) {
             double v[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) v[u] = fetch(G.rpart + i + 256 * u);
 #pragma unroll
             for (int u = 0; u < 4; u++) a += v[u];
         }
-        for (; i < G.nrb; i += 256) a += fetch(G.rpart + i);
+        for (; i < G.nrb2; i += 256) a += fetch(G.rpart + i);
         a = block_sum(a, red4);
         if (threadIdx.x == 0) publish(G, G.hbuf, a);
         return;
@@ -997,13 +997,28 @@ __device__ __forceinline__ void m2_dots(const SpDev &G, int it, double (*red)[4]
 // write this rank's part of the reduction record xb = [r.z, r.r, z.Az, heavy sums of A z]: one per
 // heavy vertex its block partials' sums, then z.Az from phase 1's partials and (r.z, r.r) from the
 // last update's (or the setup's) — all from earlier launches, so no hand-off; the host all-reduces xb
-template <class JT, int MG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4)))
+// U (G.p2u): slots per step of the slot loop — 8 (up to 4 waves per SIMD) or 4 (registers for 8
+// waves per SIMD, for the row split's extra waves)
+template <class JT, int MG, int U8>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U8 == 4 ? 6 : 1, U8 == 4 ? 8 : 4)))
 k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
     double beta = 0.0;
+    long long *trw = nullptr;                               // diagnostics: this wave's stamps
+    if (G.p2tr && it == G.p2tr_it) {
+        trw = G.p2tr + 6 * ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+        if ((threadIdx.x & 63) == 0) {
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            trw[0] = wall_clock64();
+            trw[4] = hw;
+        }
+    }
+    auto stamp = [&](int i, long long v = -1) {
+        if (trw && (threadIdx.x & 63) == 0) trw[i] = v < 0 ? wall_clock64() : v;
+    };
     if constexpr (MG == 2) {
         if (G.rec[0] != 0.0) return;
         if ((int)blockIdx.x < G.m_nh) {
@@ -1062,20 +1077,34 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         }
         return;
     }
-    const int lb = rows ? row_block(blockIdx.x - nhx, G.nrb) : 0;
-    const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    // row split (G.rs = 1, 2 or 4): a workgroup's 4 waves are 4 / rs row-waves x rs parts; part j of a
+    // row-wave walks the j-th contiguous share of its slot steps, and part 0 adds the others' sums
+    // (through LDS, in part order) before the row's own terms — rs x the waves in flight for the
+    // slot gathers, whose latency bounds this loop at ~3 waves per SIMD (C2)
+    const int rpw = 4 >> (G.rs >> 1), wv = threadIdx.x >> 6;
+    const int lb = rows ? row_block(blockIdx.x - nhx, G.nrb2) : 0;
+    const int rw = wv & (rpw - 1), part = wv / rpw;
+    const int w = lb * rpw + rw, lane = threadIdx.x & 63;
+    __shared__ double qx[3][3][128];                        // parts 1..3: [part - 1][component][row lane]
     // MG: the row's values for the update after alpha arrives (lrow >= 0: this lane has a row)
     int lrow = -1;
     int64_t orow = 0;
     double pr[3] = {0, 0, 0}, qr[3] = {0, 0, 0}, xo[3] = {0, 0, 0}, ro[3] = {0, 0, 0}, M[6] = {0, 0, 0, 0, 0, 0};
+    double q[3] = {0.0, 0.0, 0.0};
+    int l = -1;
     if (rows && w < G.nwaves) {
-        const int l = G.rowmap[64 * w + lane];
+        l = G.rowmap[64 * w + lane];
         const int64_t n = G.nslots * 64;
         const JT *pjx = pj, *pjy = pj + n, *pjz = pj + 2 * n;
         const int64_t os = 6 * (int64_t)G.Q;
-        double q[3] = {0.0, 0.0, 0.0};
-        int64_t k = G.woff[w] * 64 + lane;
-        const int64_t k1 = G.woff[w + 1] * 64 + lane;
+        int64_t s0 = G.woff[w], s1 = G.woff[w + 1];
+        if (G.rs > 1) {
+            const int64_t per = (s1 - s0 + G.rs - 1) / G.rs;
+            s0 = min(s0 + part * per, s1);
+            s1 = min(s0 + per, s1);
+        }
+        int64_t k = s0 * 64 + lane;
+        const int64_t k1 = s1 * 64 + lane;
         // s_e (v >= 0), p of the depth scale -2 - v (v <= -2) or 0 (padding): both loads on every
         // path and a select, so the slots of a step keep their loads in flight (the scales' (z, p)
         // are a handful of cache lines)
@@ -1096,20 +1125,29 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
                 return v >= 0 ? a : (v <= -2 ? p : 0.0);
             }
         };
-        // U slots per step: their indices, then the values and J slices, then the adds in order
-        auto step = [&](auto U_) {
+        // U slots per step: their indices, then the values and J slices, then the adds in order.  A
+        // clamped step (the last, with fewer than U slots left: the count is uniform in the wave)
+        // reads the last slot again in place of the missing ones and adds them times zero
+        auto step = [&](auto U_, bool clamp) {
             constexpr int U = decltype(U_)::value;
             int v[U];
-            double sv[U], J[U][3];
+            int64_t kk[U];
+            double sv[U], J[U][3], mk[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = G.pidx[k + 64 * u];
+            for (int u = 0; u < U; u++) {
+                const bool in = k + 64 * u < k1;
+                kk[u] = clamp && !in ? k1 - 64 : k + 64 * u;
+                mk[u] = clamp && !in ? 0.0 : 1.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = G.pidx[kk[u]];
             if constexpr (MG) {
                 // every load of the step first (s_e, the scale's p, the J slice), the arithmetic after:
                 // one round trip per step instead of one per slot
                 double a[U], pp[U];
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                    J[u][0] = pjx[kk[u]]; J[u][1] = pjy[kk[u]]; J[u][2] = pjz[kk[u]];
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++) {
@@ -1118,12 +1156,12 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
                 }
 #pragma unroll
                 for (int u = 0; u < U; u++)
-                    sv[u] = a[u] * (v[u] >= 0 ? 1.0 : 0.0) + pp[u] * (v[u] <= -2 ? 1.0 : 0.0);
+                    sv[u] = (a[u] * (v[u] >= 0 ? 1.0 : 0.0) + pp[u] * (v[u] <= -2 ? 1.0 : 0.0)) * mk[u];
             } else {
 #pragma unroll
                 for (int u = 0; u < U; u++) {
-                    sv[u] = val(v[u]);
-                    J[u][0] = pjx[k + 64 * u]; J[u][1] = pjy[k + 64 * u]; J[u][2] = pjz[k + 64 * u];
+                    sv[u] = val(v[u]) * mk[u];
+                    J[u][0] = pjx[kk[u]]; J[u][1] = pjy[kk[u]]; J[u][2] = pjz[kk[u]];
                 }
             }
 #pragma unroll
@@ -1132,15 +1170,31 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
                 for (int a = 0; a < 3; a++) q[a] += J[u][a] * sv[u];
             k += U * 64;
         };
-        while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{});
-        if (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{});
-        for (; k < k1; k += 64) {
-            const double sv = val(G.pidx[k]);
-            q[0] += (double)pjx[k] * sv;
-            q[1] += (double)pjy[k] * sv;
-            q[2] += (double)pjz[k] * sv;
+        if constexpr (U8 == 8) {
+            while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{}, false);
+            if (k + 4 * 64 < k1) step(std::integral_constant<int, 8>{}, true);   // 5..7 slots left
+            else if (k < k1) step(std::integral_constant<int, 4>{}, true);      // 1..4
+        } else {
+            while (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{}, false);
+            if (k < k1) step(std::integral_constant<int, 4>{}, true);           // 1..3
         }
-        if (l >= 0) {
+        stamp(5, s1 - s0);
+    }
+    stamp(1);
+    if (G.rs > 1) {
+        // parts 1.. hand their sums to part 0 (uniform: every workgroup of the launch passes here)
+        if (part > 0) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) qx[part - 1][c][64 * rw + lane] = q[c];
+        }
+        __syncthreads();
+        if (part == 0)
+            for (int j = 1; j < G.rs; j++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) q[c] += qx[j - 1][c][64 * rw + lane];
+    }
+    if (part == 0 && l >= 0) {
+        {
             const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
             double2 v[3];
             double p[3], D[6];
@@ -1181,6 +1235,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         return;
     } else if constexpr (MG == 1) {
         if (!G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        stamp(2);
         if (hv >= 0) {
             // thread a < dim: component a of the vertex (k_sp_update's heavy arithmetic; r through
             // LDS, so no private arrays); its (r.z, r.r) terms added in component order
@@ -1233,10 +1288,11 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         __shared__ double red[2][4];
         pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);   // (kernel args never by address)
         m2_dots(G, it, red);
+        stamp(3);
         return;
     }
     const double sm = block_sum(pq, red4);
-    if (threadIdx.x == 0 && lb < max(G.nrb, 1)) {
+    if (threadIdx.x == 0 && lb < max(G.nrb2, 1)) {
         if (G.fuse_heavy) publish(G, G.rpart + lb, sm);
         else G.rpart[lb] = sm;
     }
@@ -1535,6 +1591,12 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
         prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                    \
     } while (0)
 
+template <class JT, int MG>
+static void launch_phase2(const SpDev &G, int grid, int it, double lambda, const JT *pj, hipStream_t st) {
+    if (G.p2u == 4) SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 4>), grid, it, G, lambda, pj);
+    else SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 8>), grid, it, G, lambda, pj);
+}
+
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
     if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, sp::row_grid(G.nrb), G, G.pj32);
     else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, sp::row_grid(G.nrb), G, G.pj);
@@ -1569,11 +1631,11 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     if (G.sd) {
         // sharded single-reduction chain: [m_nx heavy-z / row-term workgroups][phase-1 blocks];
         // [m_nh heavy-sum / scalar workgroups][row blocks]
-        const int g1 = sp_merged_grid1(G), g2 = G.m_nh + sp::row_grid(G.nrb);
+        const int g1 = sp_merged_grid1(G), g2 = G.m_nh + sp::row_grid(G.nrb2);
         if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 2>), g1, it, G, G.Ja32, lambda);
         else SPL("sp_phase1", (sp::k_sp_phase1<double, 2>), g1, it, G, G.Ja, lambda);
-        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 2>), g2, it, G, lambda, (const float *)G.pj32);
-        else SPL("sp_phase2", (sp::k_sp_phase2<double, 2>), g2, it, G, lambda, (const double *)G.pj);
+        if (fp32) launch_phase2<float, 2>(G, g2, it, lambda, G.pj32, st);
+        else launch_phase2<double, 2>(G, g2, it, lambda, G.pj, st);
         return;
     }
     if (G.merged) {
@@ -1583,8 +1645,8 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 1>), g1, it, G, G.Ja32, lambda);
         else SPL("sp_phase1", (sp::k_sp_phase1<double, 1>), g1, it, G, G.Ja, lambda);
         if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
-        if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 1>), g2, it, G, lambda, (const float *)G.pj32);
-        else SPL("sp_phase2", (sp::k_sp_phase2<double, 1>), g2, it, G, lambda, (const double *)G.pj);
+        if (fp32) launch_phase2<float, 1>(G, g2, it, lambda, G.pj32, st);
+        else launch_phase2<double, 1>(G, g2, it, lambda, G.pj, st);
         return;
     }
     if (G.nblk > 0) {
@@ -1592,13 +1654,13 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         else SPL("sp_phase1", (sp::k_sp_phase1<double, 0>), G.nblk, it, G, G.Ja, lambda);
     }
     // one rank, G.fuse_heavy: + one workgroup per heavy vertex (its sums) before the row blocks
-    const int grid = sp::row_grid(G.nrb) + (G.fuse_heavy ? G.Q + G.S : 0);
-    if (fp32) SPL("sp_phase2", (sp::k_sp_phase2<float, 0>), grid, it, G, lambda, (const float *)G.pj32);
-    else SPL("sp_phase2", (sp::k_sp_phase2<double, 0>), grid, it, G, lambda, (const double *)G.pj);
+    const int grid = sp::row_grid(G.nrb2) + (G.fuse_heavy ? G.Q + G.S : 0);
+    if (fp32) launch_phase2<float, 0>(G, grid, it, lambda, G.pj32, st);
+    else launch_phase2<double, 0>(G, grid, it, lambda, G.pj, st);
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }
-int sp_merged_grid2(const SpDev &G) { return 8 * ((G.Q + G.S + 7) / 8) + sp::row_grid(G.nrb); }
+int sp_merged_grid2(const SpDev &G) { return 8 * ((G.Q + G.S + 7) / 8) + sp::row_grid(G.nrb2); }
 
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {
     // stage 1 over one workgroup per heavy vertex when the vertices have many blocks

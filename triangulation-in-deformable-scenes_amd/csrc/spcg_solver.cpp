@@ -265,6 +265,23 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G.nslots = H.woff.back();
     G.heavy_split = H.max_heavy_blocks > kSpHeavySplit ? 1 : 0;
     {
+        // phase-2 row split (DEFTRI_SP_ROW_SPLIT = 1, 2 or 4)
+        static const int rs_env = [] {
+            const char *e = std::getenv("DEFTRI_SP_ROW_SPLIT");
+            const int v = e ? std::atoi(e) : kSpRowSplit;
+            return v == 1 || v == 2 || v == 4 ? v : kSpRowSplit;
+        }();
+        G.rs = rs_env;
+        static const int u_env = [] {
+            const char *e = std::getenv("DEFTRI_SP_P2_STEP");
+            const int v = e ? std::atoi(e) : kSpP2Step;
+            return v == 4 || v == 8 ? v : kSpP2Step;
+        }();
+        G.p2u = u_env;
+        const int rpw = 4 / G.rs;
+        G.nrb2 = (G.nwaves + rpw - 1) / rpw;
+    }
+    {
         static const bool no_fuse = std::getenv("DEFTRI_SP_NO_FUSE") != nullptr;
         const int64_t heavy_parts = H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back();
         G.fuse = (!shard_ && !no_fuse) ? 1 : 0;
@@ -314,13 +331,20 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     double *zp;
     ALLOC(zp, 2 * zp_n);
     G.zp = reinterpret_cast<double2 *>(zp);
-    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb, 1));
+    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
     ALLOC(G.ph, std::max<int64_t>(H.hd, 1));
     G.m1n = sp_merged_grid1(G);
     ALLOC(G.m1part, G.m1n); ALLOC(G.m2part, 2 * (int64_t)sp_merged_grid2(G)); ALLOC(G.gsum, 32);
     ALLOC(G.apub, 1); ALLOC(G.aflag, 1);
+    if (std::getenv("DEFTRI_SP_P2_TRACE")) {               // diagnostics: phase-2 wave stamps
+        const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
+        ALLOC(G.p2tr, 6 * nw);
+        SPOK(hipMemset(G.p2tr, 0, sizeof(long long) * 6 * (size_t)nw));
+        const char *e = std::getenv("DEFTRI_SP_P2_TRACE_IT");
+        G.p2tr_it = e ? std::atoi(e) : 2;
+    }
     SPOK(hipMemset(G.aflag, 0xff, sizeof(int)));
     ALLOC(G.cnt, 48);                                      // three ticket sites, 16 counters each
     SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
@@ -598,7 +622,7 @@ int SpSolver::pcg_solve(double lambda, const double *rhs, bool &solved, int &its
 // iterations than its slot queued (the host's guess: the last converged count + 2) stops the slots
 // (stop 3): the host continues that solve in chunks of 4 exactly as solve_lm's host loop does, then
 // queues the evaluation and the decide.  Identical arithmetic and decisions as the host loop
-// (tests/test_gpu_sp.py::test_device_lm_matches_host_lm); DEFTRI_HOST_LM=1 selects the host loop.
+// (tests/test_gpu_sp.py::test_device_lm_matches_host_lm).  Opt-in: DEFTRI_DEVICE_LM=1.
 int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
     hipSetDevice(dev_);
     auto t_start = std::chrono::steady_clock::now();
@@ -796,8 +820,11 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     R.rank = rank_;
     R.nranks = nranks_;
     R.lanes = 1;
-    static const bool host_lm = std::getenv("DEFTRI_HOST_LM") != nullptr;
-    if (!shard_ && !host_lm && !prm.verbose) return solve_lm_dev(prm, R);
+    // the device-driven LM is opt-in (DEFTRI_DEVICE_LM=1): measured ~5 % slower than this loop at C2
+    // (profiles/r04ab_lm_control.json) — a step that outruns its slot's guessed CG count costs the
+    // slot in flight behind it, more than the host round trip per trial it saves
+    static const bool dev_lm = std::getenv("DEFTRI_DEVICE_LM") != nullptr && std::getenv("DEFTRI_HOST_LM") == nullptr;
+    if (!shard_ && dev_lm && !prm.verbose) return solve_lm_dev(prm, R);
     const bool dist = shard_;
     R.n_unknowns = G.ndof;
     R.rank = rank_;
@@ -944,6 +971,18 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
         if (prm.verbose)
             std::fprintf(stderr, "[deftri/sp] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
         if (qmax == max_trials || rho == 0 || !std::isfinite(lambda)) { status = DEFTRI_STATUS_TERMINATE; it++; break; }
+    }
+    if (G.p2tr) {                                          // diagnostics: the last stamped launch
+        const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
+        std::vector<long long> h(6 * (size_t)nw);
+        SPOK(hipStreamSynchronize(st_));
+        SPOK(hipMemcpy(h.data(), G.p2tr, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(std::getenv("DEFTRI_SP_P2_TRACE"), "wb")) {
+            const long long hdr[4] = {nw, G.m_nh, G.rs, G.p2u};
+            std::fwrite(hdr, sizeof(hdr), 1, f);
+            std::fwrite(h.data(), sizeof(long long), h.size(), f);
+            std::fclose(f);
+        }
     }
     eval_chi2(analytic, 0, nullptr);
     if (dist && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
