@@ -363,12 +363,15 @@ def test_merged_cg_chain_matches_three_launch_chain():
 
 
 def test_phase2_step_size_bit_identical():
-    """Phase 2's slot loop in steps of 4 (6 waves per SIMD) or 8 slots (DEFTRI_SP_P2_STEP): the same
-    adds in the same slot order (a clamped last step adds exact zeros) — bit-identical LM runs."""
-    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1) = _fusion_runs([{"DEFTRI_SP_P2_STEP": "4"}, {"DEFTRI_SP_P2_STEP": "8"}])
-    assert l0 == l1 == 2
-    assert c0 == c1 and t0 == t1 and i0 == i1
-    assert s0 == s1
+    """Phase 2's slot loop in chunks of 4, 6 or 8 slots (DEFTRI_SP_P2_STEP): the same
+    adds in the same slot order (a clamped last step adds exact zeros) — bit-identical LM runs; the
+    same for k_sp_glin_rows' step (DEFTRI_SP_GLIN_STEP)."""
+    runs = _fusion_runs([{"DEFTRI_SP_P2_STEP": "4"}, {"DEFTRI_SP_P2_STEP": "6"}, {"DEFTRI_SP_P2_STEP": "8"},
+                         {"DEFTRI_SP_GLIN_STEP": "4"}, {"DEFTRI_SP_GLIN_STEP": "6"}, {"DEFTRI_SP_GLIN_STEP": "8"}])
+    for l, c, t, i, s in runs[1:]:
+        assert l == runs[0][0] == 2
+        assert c == runs[0][1] and t == runs[0][2] and i == runs[0][3]
+        assert s == runs[0][4]
 
 
 @pytest.mark.parametrize("rs", ["1", "4"])
@@ -384,6 +387,40 @@ def test_phase2_row_split_matches(rs):
     for a, b in zip(s0, s1):
         x, y = np.frombuffer(a), np.frombuffer(b)
         assert np.max(np.abs(x - y)) <= 1e-7 * max(np.max(np.abs(y)), 1.0)
+
+
+def _arap_j_worker(env, negz, q):
+    os.environ.update(env)
+    from deftri import capi as c
+    p = tv_problem(20000, seed=6)
+    if negz:                                        # -0.0 coordinates: the full-evaluation path
+        pts = p.points.copy()
+        for i in p.arap_pts[:50, 0]:
+            pts[i, 1] = -0.0
+        p.points = pts
+    with c.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.upload(p)
+        r = ctx.solve_lm(4, analytic=False)
+        q.put((r["chi2_iter"], r["trials_iter"], r["pcg_iterations"], [a.tobytes() for a in ctx.download()]))
+
+
+@pytest.mark.parametrize("negz", [False, True])
+def test_numeric_arap_jacobian_piece_reuse_bit_identical(negz):
+    """k_lin_arap<2> (g2o's numeric ARAP Jacobian with the pieces a perturbed evaluation shares with
+    the unperturbed one reused: no division for a T_g perturbation, 2 of 6 for a v2 one) against
+    k_lin_arap<3> (every one of the 36 evaluations in full, DEFTRI_ARAP_J_FULL=1): the same bits, so
+    bit-identical LM runs; with -0.0 coordinates (the edges that take the full path) too."""
+    cm = mp.get_context("spawn")
+    out = []
+    for env in ({}, {"DEFTRI_ARAP_J_FULL": "1"}):
+        qq = cm.Queue()
+        pr = cm.Process(target=_arap_j_worker, args=(env, negz, qq))
+        pr.start()
+        out.append(qq.get(timeout=300))
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert out[0] == out[1]
 
 
 def test_merged_chain_breakdown_then_solve():

@@ -126,32 +126,59 @@ __device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__rest
     E[e] = err;
 }
 
+// The ARAP energy's arithmetic, written out as explicit products, FMAs and sums (contraction off):
+// arap_err_rt and the numeric Jacobian's piece reuse (arap_base / arap_pert) form the same operations,
+// so an energy assembled from pieces of the unperturbed evaluation has the bits of a full one.
+__device__ __forceinline__ double arap_mrow(const double *R, const double *v) {
+#pragma clang fp contract(off)
+    return __fma_rn(R[2], v[2], __fma_rn(R[1], v[1], R[0] * v[0]));
+}
+// (w (fn + gn) + eg) - 0
+__device__ __forceinline__ double arap_sum(const double *dg, const double *f, const double *g, double w) {
+#pragma clang fp contract(off)
+    const double eg = __fma_rn(dg[2], dg[2], __fma_rn(dg[1], dg[1], dg[0] * dg[0]));
+    const double fn = __fma_rn(f[2], f[2], __fma_rn(f[1], f[1], f[0] * f[0]));
+    const double gn = __fma_rn(g[2], g[2], __fma_rn(g[1], g[1], g[0] * g[0]));
+    return __fma_rn(w, fn + gn, eg) - 0.0;
+}
+__device__ __forceinline__ double arap_fg(const double *f, const double *g) {
+#pragma clang fp contract(off)
+    const double fn = __fma_rn(f[2], f[2], __fma_rn(f[1], f[1], f[0] * f[0]));
+    const double gn = __fma_rn(g[2], g[2], __fma_rn(g[1], g[1], g[0] * g[0]));
+    return fn + gn;
+}
+__device__ __forceinline__ double arap_sum_fg(const double *dg, double fg, double w) {
+#pragma clang fp contract(off)
+    const double eg = __fma_rn(dg[2], dg[2], __fma_rn(dg[1], dg[1], dg[0] * dg[0]));
+    return __fma_rn(w, fg, eg) - 0.0;
+}
+
 // the ARAP energy with the global transformation given as (rotation matrix, translation)
 __device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v2i, const double *v1j,
                                               const double *v2j, const double *Rg, const double *tt,
                                               const double *Ri, const double *Rj, double w, double area) {
+    // every product and sum written out (no compiler contraction): the numeric Jacobian's reuse of
+    // pieces (arap_base / arap_pert) forms the same operations and so the same bits
+#pragma clang fp contract(off)
     double dg[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        double a = Rg[3 * k] * v2i[0] + Rg[3 * k + 1] * v2i[1] + Rg[3 * k + 2] * v2i[2];
-        double b = Rg[3 * k] * v2j[0] + Rg[3 * k + 1] * v2j[1] + Rg[3 * k + 2] * v2j[2];
+        const double a = arap_mrow(Rg + 3 * k, v2i), b = arap_mrow(Rg + 3 * k, v2j);
         dg[k] = ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
     }
-    double eg = dg[0] * dg[0] + dg[1] * dg[1] + dg[2] * dg[2];
     double d1i[3], d2i[3], d1j[3], d2j[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         d1i[k] = v1i[k] - v1j[k]; d2i[k] = v2i[k] - v2j[k];
         d1j[k] = v1j[k] - v1i[k]; d2j[k] = v2j[k] - v2i[k];
     }
-    double fn = 0, gn = 0;
+    double f[3], g[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        double f = (d2i[k] - (Ri[3 * k] * d1i[0] + Ri[3 * k + 1] * d1i[1] + Ri[3 * k + 2] * d1i[2])) / area;
-        double g = (d2j[k] - (Rj[3 * k] * d1j[0] + Rj[3 * k + 1] * d1j[1] + Rj[3 * k + 2] * d1j[2])) / area;
-        fn += f * f; gn += g * g;
+        f[k] = (d2i[k] - arap_mrow(Ri + 3 * k, d1i)) / area;
+        g[k] = (d2j[k] - arap_mrow(Rj + 3 * k, d1j)) / area;
     }
-    return (w * (fn + gn) + eg) - 0.0;
+    return arap_sum(dg, f, g, w);
 }
 
 __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
@@ -160,6 +187,87 @@ __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i,
     double Rg[9];
     quat_to_mat(T.r, Rg);
     return arap_err_rt(v1i, v2i, v1j, v2j, Rg, T.t, Ri, Rj, w, area);
+}
+
+struct ArapBase {                  // one point configuration's pieces
+    double A[3], B[3];             // (Rg v2i - t) - v1i, (Rg v2j - t) - v1j
+    double d1i[3], d1j[3];         // v1i - v1j, v1j - v1i
+    double rf[3], rg[3];           // rows of Ri d1i, Rj d1j
+    double f[3], g[3];
+};
+__device__ __forceinline__ void arap_base(const double *v1i, const double *v2i, const double *v1j, const double *v2j,
+                                          const double *Rg, const double *tt, const double *Ri, const double *Rj,
+                                          double area, ArapBase &o) {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const double a = arap_mrow(Rg + 3 * k, v2i), b = arap_mrow(Rg + 3 * k, v2j);
+        o.A[k] = (a - tt[k]) - v1i[k];
+        o.B[k] = (b - tt[k]) - v1j[k];
+        o.d1i[k] = v1i[k] - v1j[k];
+        o.d1j[k] = v1j[k] - v1i[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        o.rf[k] = arap_mrow(Ri + 3 * k, o.d1i);
+        o.rg[k] = arap_mrow(Rj + 3 * k, o.d1j);
+        o.f[k] = ((v2i[k] - v2j[k]) - o.rf[k]) / area;
+        o.g[k] = ((v2j[k] - v2i[k]) - o.rg[k]) / area;
+    }
+}
+// the energy with coordinate DD of point VI (0 v1i, 1 v2i, 2 v1j, 3 v2j) set to x; the others as in
+// the base `o` of the points Q (the perturbed evaluation's other coordinates)
+template <int VI, int DD>
+__device__ __forceinline__ double arap_pert(const ArapBase &o, const double (*Q)[3], double x, const double *Rg,
+                                            const double *tt, const double *Ri, const double *Rj, double w,
+                                            double area) {
+#pragma clang fp contract(off)
+    double dg[3], f[3], g[3];
+    if constexpr (VI == 0 || VI == 2) {
+        // v1i / v1j: d1i, d1j change in one coordinate -> every row of Ri d1i, Rj d1j
+        double v1i[3], v1j[3], d1i[3], d1j[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            v1i[k] = (VI == 0 && k == DD) ? x : Q[0][k];
+            v1j[k] = (VI == 2 && k == DD) ? x : Q[2][k];
+            d1i[k] = v1i[k] - v1j[k];
+            d1j[k] = v1j[k] - v1i[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            f[k] = ((Q[1][k] - Q[3][k]) - arap_mrow(Ri + 3 * k, d1i)) / area;
+            g[k] = ((Q[3][k] - Q[1][k]) - arap_mrow(Rj + 3 * k, d1j)) / area;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if (k != DD) dg[k] = o.A[k] + o.B[k];
+            else {
+                const double a = arap_mrow(Rg + 3 * k, Q[1]), b = arap_mrow(Rg + 3 * k, Q[3]);
+                dg[k] = ((a - tt[k]) - v1i[k]) + ((b - tt[k]) - v1j[k]);
+            }
+        }
+    } else {
+        // v2i / v2j: Rg v2 changes in every row; d2i, d2j in one coordinate -> f, g in one row
+        double v2i[3], v2j[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            v2i[k] = (VI == 1 && k == DD) ? x : Q[1][k];
+            v2j[k] = (VI == 3 && k == DD) ? x : Q[3][k];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            if constexpr (VI == 1) dg[k] = ((arap_mrow(Rg + 3 * k, v2i) - tt[k]) - Q[0][k]) + o.B[k];
+            else dg[k] = o.A[k] + ((arap_mrow(Rg + 3 * k, v2j) - tt[k]) - Q[2][k]);
+            if (k == DD) {
+                f[k] = ((v2i[k] - v2j[k]) - o.rf[k]) / area;
+                g[k] = ((v2j[k] - v2i[k]) - o.rg[k]) / area;
+            } else {
+                f[k] = o.f[k];
+                g[k] = o.g[k];
+            }
+        }
+    }
+    return arap_sum(dg, f, g, w);
 }
 
 // g2o's numeric Jacobian of an ARAP edge perturbs the pair's T_g by exp(+-delta e_d) * T_g; those
@@ -185,8 +293,39 @@ __global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restr
     o[9] = X.t[0]; o[10] = X.t[1]; o[11] = X.t[2];
 }
 
-// MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian (one kernel per
-// mode: each gets the registers of its own path)
+// the numeric ARAP Jacobian with every evaluation in full (MODE 3's loop), columns stored into J:
+// MODE 2's path for an edge with a -0.0 coordinate
+__device__ __noinline__ void arap_numeric_full(const double (*P)[3], const double *X, const double *Ri, const double *Rj,
+                                               double w, double area, double *J, int e, int64_t jld) {
+#pragma clang fp contract(off)
+    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    auto jst = [&](int k, double v) {
+        if (jld) J[k * jld + e] = v;
+        else J[18 * (int64_t)e + k] = v;
+    };
+    for (int vi = 0; vi < 4; vi++)
+        for (int dd = 0; dd < 3; dd++) {
+            double Pp[4][3], Pm[4][3];
+            for (int a = 0; a < 4; a++)
+                for (int k = 0; k < 3; k++) {
+                    const double d = (a == vi && k == dd) ? delta : 0.0;
+                    Pp[a][k] = P[a][k] + d;
+                    Pm[a][k] = P[a][k] - d;
+                }
+            const double ep = arap_err_rt(Pp[0], Pp[1], Pp[2], Pp[3], X, X + 9, Ri, Rj, w, area);
+            const double em = arap_err_rt(Pm[0], Pm[1], Pm[2], Pm[3], X, X + 9, Ri, Rj, w, area);
+            jst(3 * vi + dd, scalar * (ep - em));
+        }
+    for (int dd = 0; dd < 6; dd++) {
+        const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
+        const double ep = arap_err_rt(P[0], P[1], P[2], P[3], Xp, Xp + 9, Ri, Rj, w, area);
+        const double em = arap_err_rt(P[0], P[1], P[2], P[3], Xm, Xm + 9, Ri, Rj, w, area);
+        jst(12 + dd, scalar * (ep - em));
+    }
+}
+
+// MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian, pieces reused; 3: the
+// same, every evaluation in full (one kernel per mode: each gets the registers of its own path)
 template <int MODE>
 __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
                            const int32_t *__restrict__ arot, const double *__restrict__ aw,
@@ -243,8 +382,69 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
         Jv[13] = 2.0 * (u[2] * g[0] - u[0] * g[2]);
         Jv[14] = 2.0 * (u[0] * g[1] - u[1] * g[0]);
         Jv[15] = -4.0 * g[0]; Jv[16] = -4.0 * g[1]; Jv[17] = -4.0 * g[2];
-    } else {                                       // g2o BaseMultiEdge numeric, delta 1e-9,
-        const double delta = 1e-9, scalar = 1.0 / (2 * delta);   // the pair's transformations precomputed
+    } else if (MODE == 2) {
+#pragma clang fp contract(off)
+        // g2o BaseMultiEdge numeric, delta 1e-9, with the pieces an evaluation shares with the
+        // unperturbed one reused (the bits of MODE 3's full evaluations, tests/test_gpu_sp.py): a
+        // T_g perturbation leaves the rows' terms f, g unchanged (no division), a v2i / v2j one changes
+        // one row of each (2 of 6 divisions).  g2o's + evaluations see the other coordinates as
+        // x + 0.0, the - ones as x - 0.0 = x: the same bits unless a coordinate is -0.0, and an edge
+        // with one takes the full evaluations (arap_numeric_full).  Each column is stored when formed.
+        auto jst = [&](int k, double v) {
+            if (jld) J[k * jld + e] = v;
+            else J[18 * (int64_t)e + k] = v;
+        };
+        bool negz = false;
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) negz |= __double_as_longlong(P[a][k]) == (long long)0x8000000000000000ull;
+        if (negz) {
+            arap_numeric_full(P, tg_pre + 12 * kArapPre * (int64_t)q, Ri, Rj, w, area, J, e, jld);
+        } else {
+            const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+            const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
+            double Rg[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) Rg[k] = X[k];
+            ArapBase bm;
+            arap_base(P[0], P[1], P[2], P[3], Rg, Rg + 9, Ri, Rj, area, bm);
+            const double fgm = arap_fg(bm.f, bm.g);
+#pragma unroll 1
+            for (int dd = 0; dd < 6; dd++) {
+                const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
+                double dp[3], dm[3];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    dp[k] = ((arap_mrow(Xp + 3 * k, P[1]) - Xp[9 + k]) - P[0][k]) + ((arap_mrow(Xp + 3 * k, P[3]) - Xp[9 + k]) - P[2][k]);
+                    dm[k] = ((arap_mrow(Xm + 3 * k, P[1]) - Xm[9 + k]) - P[0][k]) + ((arap_mrow(Xm + 3 * k, P[3]) - Xm[9 + k]) - P[2][k]);
+                }
+                jst(12 + dd, scalar * (arap_sum_fg(dp, fgm, w) - arap_sum_fg(dm, fgm, w)));
+            }
+            auto point = [&](auto VI_, auto DD_) {
+                constexpr int VI = decltype(VI_)::value, DD = decltype(DD_)::value;
+                const double ep = arap_pert<VI, DD>(bm, P, P[VI][DD] + delta, Rg, Rg + 9, Ri, Rj, w, area);
+                const double em = arap_pert<VI, DD>(bm, P, P[VI][DD] - delta, Rg, Rg + 9, Ri, Rj, w, area);
+                jst(3 * VI + DD, scalar * (ep - em));
+                __builtin_amdgcn_sched_barrier(0);          // one evaluation pair's registers at a time
+            };
+            using std::integral_constant;
+            point(integral_constant<int, 0>{}, integral_constant<int, 0>{});
+            point(integral_constant<int, 0>{}, integral_constant<int, 1>{});
+            point(integral_constant<int, 0>{}, integral_constant<int, 2>{});
+            point(integral_constant<int, 1>{}, integral_constant<int, 0>{});
+            point(integral_constant<int, 1>{}, integral_constant<int, 1>{});
+            point(integral_constant<int, 1>{}, integral_constant<int, 2>{});
+            point(integral_constant<int, 2>{}, integral_constant<int, 0>{});
+            point(integral_constant<int, 2>{}, integral_constant<int, 1>{});
+            point(integral_constant<int, 2>{}, integral_constant<int, 2>{});
+            point(integral_constant<int, 3>{}, integral_constant<int, 0>{});
+            point(integral_constant<int, 3>{}, integral_constant<int, 1>{});
+            point(integral_constant<int, 3>{}, integral_constant<int, 2>{});
+        }
+    } else {                                       // MODE 3: g2o BaseMultiEdge numeric, delta 1e-9,
+#pragma clang fp contract(off)
+        const double delta = 1e-9, scalar = 1.0 / (2 * delta);   // every evaluation in full
         const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
         double Rg[12];
 #pragma unroll
@@ -278,11 +478,13 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
             Jv[12 + dd] = scalar * (ep - em);
         }
     }
-    if (jld) {
+    if (MODE != 2) {
+        if (jld) {
 #pragma unroll
-        for (int k = 0; k < 18; k++) J[k * jld + e] = Jv[k];
-    } else {
-        for (int k = 0; k < 18; k++) J[18 * (int64_t)e + k] = Jv[k];
+            for (int k = 0; k < 18; k++) J[k * jld + e] = Jv[k];
+        } else {
+            for (int k = 0; k < 18; k++) J[18 * (int64_t)e + k] = Jv[k];
+        }
     }
     W[e] = om;
     E[e] = err;
@@ -311,7 +513,7 @@ __global__ void k_lin_dep(int D, const int32_t *__restrict__ dpt, const int32_t 
 // MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian (one kernel per
 // mode: each gets the registers of its own path)
 template <int MODE>
-__global__ void __launch_bounds__(128) k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 2 : 1, 8))) k_lin_arap(int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
                            const int32_t *__restrict__ arot, const double *__restrict__ aw,
                            const double *__restrict__ rot, const double *__restrict__ parea,
                            const double *__restrict__ pinfo, const double *__restrict__ points,
@@ -1888,6 +2090,13 @@ void prof_end(const char *name, hipEvent_t e0, unsigned grid, double work, hipSt
         }                                                                            \
     } while (0)
 
+// DEFTRI_ARAP_J_FULL=1: the numeric ARAP Jacobian with every evaluation in full (k_lin_arap<3>,
+// the A/B and bit-identity reference of the piece-reusing k_lin_arap<2>)
+static bool arap_j_full() {
+    static const bool v = std::getenv("DEFTRI_ARAP_J_FULL") != nullptr;
+    return v;
+}
+
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic) {
     if (P.R > 0)
         LAUNCH("lin_rep", dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), st, P.R, P.rep_point, P.rep_cam,
@@ -1902,7 +2111,7 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
         LAUNCH("arap_pre", dev::k_arap_pre, dim3(nb((int64_t)P.Q * dev::kArapPre, 64)), dim3(64), st, P.Q, P.tg,
                P.tg_pre, P.gate_lin);
     if (P.E > 0)
-        LAUNCH("lin_arap", (!want_jac ? dev::k_lin_arap<0> : analytic ? dev::k_lin_arap<1> : dev::k_lin_arap<2>),
+        LAUNCH("lin_arap", (!want_jac ? dev::k_lin_arap<0> : analytic ? dev::k_lin_arap<1> : arap_j_full() ? dev::k_lin_arap<3> : dev::k_lin_arap<2>),
                            dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
                            P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg,
                            pre ? P.tg_pre : nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, want_jac ? 1 : 0,

@@ -42,8 +42,10 @@ constexpr int kSpRed = 16;             // doubles per iteration in the reduction
 constexpr int kSpPart = 8;             // doubles per phase-1 block partial
 constexpr int kSpLin = 27;             // doubles per block partial of the per-iteration heavy lin (21 H + 6 b)
 constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside windows of this many
+constexpr int kSpWaveSplit = 16;       // phase-2 waves with rows of more slots take 32 rows on lane pairs
 constexpr int kSpRowSplit = 1;         // phase 2: waves per row-wave's slot list (DEFTRI_SP_ROW_SPLIT)
 constexpr int kSpP2Step = 8;           // phase 2: slots per step (DEFTRI_SP_P2_STEP = 4 or 8)
+constexpr int kSpGlinStep = 8;         // k_sp_glin_rows: slots per step (DEFTRI_SP_GLIN_STEP = 4 or 8)
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
 constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one thread per dof)
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
@@ -94,6 +96,7 @@ struct SpPlanHost {
     // ARAP, -(2 + scale) for a depth coupling (p of the scale), -1 padding
     std::vector<int32_t> rowmap;                       // [nwaves * 64]: local row per lane (-1 padding)
     std::vector<int64_t> woff;                         // nwaves + 1, in slots
+    std::vector<uint8_t> wsplit;                       // per wave: 1 = 32 rows on lane pairs (j, j + 32)
     std::vector<int32_t> pmap, pidx;                   // [slots * 64]
     int32_t max_heavy_blocks = 0;                      // most phase-1 blocks of one heavy vertex
     // halo exchange: rows (global) sent to / received from each peer, ascending
@@ -134,6 +137,7 @@ struct SpDev {
     // row-waves, nrb2 = ceil(nwaves rs / 4) of them (p.q partials rpart [nrb2])
     int32_t rs = 1, nrb2 = 0;
     int32_t p2u = 8;                                   // phase 2's slots per step (8 or 4)
+    int32_t glu = 8;                                   // k_sp_glin_rows' slots per step (8 or 4)
     // diagnostics (DEFTRI_SP_P2_TRACE=<file>): per phase-2 wave of CG iteration p2tr_it, wall-clock
     // stamps [start, rows / heavy sums done, alpha known, end, hw id, steps]
     long long *p2tr = nullptr;
@@ -141,6 +145,7 @@ struct SpDev {
     int64_t nslots = 0;                                // wave-layout slots (x 64 lanes)
     const int32_t *rowmap = nullptr, *pmap = nullptr, *pidx = nullptr;
     const int64_t *woff = nullptr;
+    const uint8_t *wsplit = nullptr;                   // per wave: rows on lane pairs (spcg_plan.cpp 8b)
     double *pj = nullptr;                              // packed J slices: [3][nslots * 64] (fp64)
     float *pj32 = nullptr;                             // the same in fp32 (fp32 Jacobian storage)
     // per-LM-iteration
@@ -183,8 +188,6 @@ struct SpDev {
     double *ph = nullptr;                                 // p of the heavy dofs this iteration (phase 1 -> 2)
     double *m1part = nullptr;                             // phase-1 p.Ap per workgroup [m1n = m_nx + nblk]
     int32_t m1n = 0;
-    double *apub = nullptr;                               // alpha published by phase 2's workgroup 0
-    int *aflag = nullptr;                                 // ... and the iteration it belongs to (-1 after setup)
     int32_t alpha_kernel = 0;                             // alpha by k_sp_alpha between the phases (no hand-off)
     // sharded single-reduction chain (sd, any rank count with a transport): per CG iteration phase 1
     // and phase 2 form w = A z and this rank's part of xb, the host all-reduces xb, k_sp_update_sd
@@ -249,7 +252,7 @@ class SpSolver {
     int download(double *points, double *scales, double *tg);
     int reset_state();
     int chi2(double *out);
-    int gradient(double *b, double *hdiag, int64_t n);
+    int gradient(double *b, double *hdiag, int64_t n, bool analytic);   // J mode as the context's
     int damped_solve(double lambda, const double *rhs, double *x, int64_t n);
     int hessian_product(double lambda, const double *x, double *y, int64_t n);   // y = (H + lambda I) x
     int profile_trial(double lambda, KProf &prof, bool analytic);

@@ -116,12 +116,14 @@ __device__ __forceinline__ int tri6(int a, int b) { return a * (a + 1) / 2 + b; 
 // couplings c_e = W J_p J_s; and, slot by slot, the packed J slices phase 2 reads (an ARAP slice is
 // gathered once: added into H_v and stored).  Slots of a row: its incidences in the plan's order,
 // then its depth couplings, then padding.
-template <class JT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 3)))
+// GU (G.glu): slots per step — 8 (3 waves per SIMD) or 4 (5 waves per SIMD: a C2-size grid of
+// ~3100 waves then fits the chip in one round)
+template <class JT, int GU>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GU == 4 ? 5 : GU == 6 ? 4 : 1, GU == 4 ? 5 : GU == 6 ? 4 : 3)))
 k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     __shared__ double red4[4];
     if (gated_off(G.lgate)) return;
-    const int lb = row_block(blockIdx.x, G.nrb);
+    const int lb = row_block(blockIdx.x, G.nrb2);
     const int w = lb * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     double mx = 0.0;
     if (w < G.nwaves) {
@@ -161,7 +163,6 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
 #pragma unroll
         for (int k = 0; k < 6; k++) H[k] = D[k];
         const int64_t n = G.nslots * 64;
-        const int64_t k1 = G.woff[w + 1] * 64 + lane;
         // one slot: its J slice (ARAP incidence le << 2 | role, or the depth coupling of the row's
         // edge -2 - m), weight and error (ARAP) / J_s (depth).  load(): the same five loads on every
         // path (selected addresses; padding reads ARAP edge 0); value(): selects only — so the four
@@ -200,34 +201,53 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
                 bb[a] -= v[a] * (wt * er);
             }
         };
+        // U slots per step: indices, loads, then in order.  A clamped step (the last, fewer than U
+        // slots left; the count is uniform in the wave) repeats the last slot in place of the missing
+        // ones with wt = er = 0 (exact zeros added; its slice stored again, the same value)
         int64_t k = G.woff[w] * 64 + lane;
-        auto step = [&](auto U_) {                         // U slots: indices, loads, then in order
+        const int64_t k1 = G.woff[w + 1] * 64 + lane;
+        auto step = [&](auto U_, bool clamp) {
             constexpr int U = decltype(U_)::value;
             int m[U];
+            int64_t kk[U];
+            bool in[U];
             Raw r[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) m[u] = G.pmap[k + 64 * u];
+            for (int u = 0; u < U; u++) {
+                in[u] = !clamp || k + 64 * u < k1;
+                kk[u] = in[u] ? k + 64 * u : k1 - 64;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) m[u] = G.pmap[kk[u]];
 #pragma unroll
             for (int u = 0; u < U; u++) r[u] = load(m[u]);
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 double v[3], wt, er;
                 value(m[u], r[u], v, wt, er);
+                if (!in[u]) wt = er = 0.0;
                 add(v, wt, er);
 #pragma unroll
-                for (int a = 0; a < 3; a++) pj[a * n + k + 64 * u] = (JT)v[a];
+                for (int a = 0; a < 3; a++) pj[a * n + kk[u]] = (JT)v[a];
             }
             k += U * 64;
         };
-        while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{});
-        if (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{});
-        for (; k < k1; k += 64) {
-            const int m = G.pmap[k];
-            double v[3], wt, er;
-            value(m, load(m), v, wt, er);
-            add(v, wt, er);
+        using I4 = std::integral_constant<int, 4>;
+        if constexpr (GU == 4) {
+            while (k + 3 * 64 < k1) step(I4{}, false);
+        } else if constexpr (GU == 6) {
+            while (k + 5 * 64 < k1) step(std::integral_constant<int, 6>{}, false);
+            if (k + 4 * 64 < k1) step(std::integral_constant<int, 6>{}, true);   // 5 left
+        } else {
+            while (k + 7 * 64 < k1) step(std::integral_constant<int, 8>{}, false);
+            if (k + 4 * 64 < k1) step(std::integral_constant<int, 8>{}, true);   // 5..7 left
+        }
+        if (k < k1) step(I4{}, true);                                             // 1..4 left
+        if (G.wsplit[w]) {                             // lane pairs: lane j's sums + lane j + 32's
 #pragma unroll
-            for (int a = 0; a < 3; a++) pj[a * n + k] = (JT)v[a];
+            for (int k = 0; k < 6; k++) H[k] += __shfl_xor(H[k], 32);
+#pragma unroll
+            for (int a = 0; a < 3; a++) bb[a] += __shfl_xor(bb[a], 32);
         }
         if (l >= 0) {
 #pragma unroll
@@ -241,7 +261,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     mx = wave_max(mx);
     if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0 && lb < max(G.nrb, 1)) G.mpart[lb] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+    if (threadIdx.x == 0 && lb < max(G.nrb2, 1)) G.mpart[lb] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
 }
 
 // heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1)
@@ -373,7 +393,7 @@ __global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, 
     if (gated_off(G.lgate)) return;
     double m = 0.0;
     if (stage == 0) {
-        for (int i = threadIdx.x; i < G.nrb; i += 256) m = fmax(m, G.mpart[i]);
+        for (int i = threadIdx.x; i < G.nrb2; i += 256) m = fmax(m, G.mpart[i]);
     } else {
         for (int h = threadIdx.x; h < G.Q; h += 256)
 #pragma unroll
@@ -600,7 +620,6 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
     // workgroup 0: the heavy dofs (dispatched first: their serial work overlaps the rows); row block
     // blockIdx - 1; partial slots as in k_sp_dots (rows 0..nrb-1, heavy nrb)
     const int rb = (int)blockIdx.x - 1, slot = rb < 0 ? G.nrb : rb;
-    if (rb < 0 && t == 0 && G.merged) *G.aflag = -1;      // no iteration's alpha published yet
     // the CG chain's ticket counters (sites 0 and 16; this launch counts at 32) start every solve at
     // zero, whatever an earlier solve on this plan left
     if (rb < 0 && t < 32) st_sc1(G.cnt + t, 0);
@@ -797,32 +816,30 @@ __device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam,
 // draws its ticket in m2_dots, so the counters return to zero.
 __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish) {
     __shared__ double sa;
+    // thread t adds partials t, t + 256, ... in order; sixteen loads in flight (a C2-size launch,
+    // ~3,200 partials, in one round trip: alpha is on every row's path), the missing ones as zeros
     double a = 0.0;
-    int j = threadIdx.x;
     const int n = G.m1n;
-    for (; j + 3 * 256 < n; j += 4 * 256) {        // four partials in flight, added in order
-        double v[4];
+    const double gam = G.red[(int64_t)kSpRed * it];         // r.z, loaded with the partials
+    for (int j = threadIdx.x; j < n; j += 16 * 256) {
+        double v[16];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = G.m1part[j + 256 * u];
+        for (int u = 0; u < 16; u++) v[u] = j + 256 * u < n ? G.m1part[j + 256 * u] : 0.0;
 #pragma unroll
-        for (int u = 0; u < 4; u++) a += v[u];
+        for (int u = 0; u < 16; u++) a += v[u];
     }
-    for (; j < n; j += 256) a += G.m1part[j];
     a = block_sum(a, red4);
     if (threadIdx.x == 0) {
-        double alpha = G.red[(int64_t)kSpRed * it] / a;
-        if (!(a > 0.0) || !isfinite(alpha)) {
+        double alpha = gam / a;
+        if (!(a > 0.0) || !isfinite(alpha) || alpha == 0.0) {
             G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpBreakdown;   // read from the next launch on
             alpha = __builtin_nan("");
         }
-        G.red[(int64_t)kSpRed * it + 3] = alpha;
-        if (publish) {
-            st_sc1(G.apub, alpha);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);            // the value acknowledged before the flag
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            st_sc1(G.aflag, it);
-        }
+        // the value is its own flag: word 3 of iteration it's record is zero until this store (the
+        // record is cleared per solve; alpha == 0 counts as a breakdown above), so a waiter polls
+        // the one word — one round trip after the store instead of a flag and then the value
+        if (publish) st_sc1(G.red + (int64_t)kSpRed * it + 3, alpha);
+        else G.red[(int64_t)kSpRed * it + 3] = alpha;
         sa = alpha;
     }
     __syncthreads();
@@ -831,16 +848,19 @@ __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *
 __device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
     __shared__ double sa;
     if (threadIdx.x == 0) {
+        const double *w = G.red + (int64_t)kSpRed * it + 3;
         int n = 0;
-        while (ld_sc1(G.aflag) != it && n < (1 << 22)) {
+        double v = ld_sc1(w);
+        while (__double_as_longlong(v) == 0 && n < (1 << 22)) {
             __builtin_amdgcn_s_sleep(2);
+            v = ld_sc1(w);
             n++;
         }
         if (n >= (1 << 22)) {                          // never expected: stop the solve, skip the update
             G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpTimeout;
             sa = __builtin_nan("");
         } else {
-            sa = ld_sc1(G.apub);
+            sa = v;
         }
     }
     __syncthreads();
@@ -1000,7 +1020,7 @@ __device__ __forceinline__ void m2_dots(const SpDev &G, int it, double (*red)[4]
 // U (G.p2u): slots per step of the slot loop — 8 (up to 4 waves per SIMD) or 4 (registers for 8
 // waves per SIMD, for the row split's extra waves)
 template <class JT, int MG, int U8>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U8 == 4 ? 6 : 1, U8 == 4 ? 8 : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U8 == 4 ? 6 : 4, U8 == 4 ? 8 : 4)))
 k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     __shared__ double red4[4];
     if (gated_off(G.gate)) return;
@@ -1179,6 +1199,10 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             if (k < k1) step(std::integral_constant<int, 4>{}, true);           // 1..3
         }
         stamp(5, s1 - s0);
+    }
+    if (rows && w < G.nwaves && G.wsplit[w]) {          // lane pairs (wave-uniform): j's sums + j + 32's
+#pragma unroll
+        for (int c = 0; c < 3; c++) q[c] += __shfl_xor(q[c], 32);
     }
     stamp(1);
     if (G.rs > 1) {
@@ -1594,12 +1618,21 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
 template <class JT, int MG>
 static void launch_phase2(const SpDev &G, int grid, int it, double lambda, const JT *pj, hipStream_t st) {
     if (G.p2u == 4) SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 4>), grid, it, G, lambda, pj);
+    else if (G.p2u == 6) SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 6>), grid, it, G, lambda, pj);
     else SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 8>), grid, it, G, lambda, pj);
 }
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    if (fp32) SPL("sp_glin_rows", sp::k_sp_glin_rows<float>, sp::row_grid(G.nrb), G, G.pj32);
-    else SPL("sp_glin_rows", sp::k_sp_glin_rows<double>, sp::row_grid(G.nrb), G, G.pj);
+    if (G.glu == 4) {
+        if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 4>), sp::row_grid(G.nrb2), G, G.pj32);
+        else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 4>), sp::row_grid(G.nrb2), G, G.pj);
+    } else if (G.glu == 6) {
+        if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 6>), sp::row_grid(G.nrb2), G, G.pj32);
+        else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 6>), sp::row_grid(G.nrb2), G, G.pj);
+    } else {
+        if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 8>), sp::row_grid(G.nrb2), G, G.pj32);
+        else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 8>), sp::row_grid(G.nrb2), G, G.pj);
+    }
     if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
     if (G.nch > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.nch, G);
 }

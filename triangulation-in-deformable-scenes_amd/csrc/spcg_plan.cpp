@@ -291,8 +291,16 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     }
 
     // 8b. phase-2 wave layout: per own row its ARAP incidences then its depth couplings; rows sorted by
-    //     that count (descending, stable) inside windows of kSpSortWindow rows, 64 per wave
+    //     that count (descending, stable) inside windows of kSpSortWindow rows, 64 per wave.  A wave
+    //     whose rows hold more than kSpWaveSplit slots (DEFTRI_SP_WAVE_SPLIT; 0 = never) takes 32
+    //     rows instead, each on a lane pair: lane j the first ceil(c / 2) slots of its row, lane j + 32
+    //     the rest (rowmap -1: the pair's sums go to lane j) — the longest waves' step counts halve,
+    //     which is what bounds phase 2 and the rows' linearization (their span, not their bytes)
     {
+        static const int split_t = [] {
+            const char *e = std::getenv("DEFTRI_SP_WAVE_SPLIT");
+            return e ? std::atoi(e) : kSpWaveSplit;
+        }();
         std::vector<int32_t> cnt(nown);
         for (int32_t l = 0; l < nown; l++)
             cnt[l] = (int32_t)(H.inc_off[l + 1] - H.inc_off[l]) + (H.dep_off[l + 1] - H.dep_off[l]);
@@ -302,34 +310,54 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             const int32_t w1 = std::min(nown, w0 + kSpSortWindow);
             std::stable_sort(order.begin() + w0, order.begin() + w1, [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
         }
-        const int32_t nw = (nown + 63) / 64;
-        H.rowmap.assign((size_t)nw * 64, -1);
-        H.woff.assign(nw + 1, 0);
-        for (int32_t w = 0; w < nw; w++) {
+        H.rowmap.clear();
+        H.woff.assign(1, 0);
+        H.wsplit.clear();
+        std::vector<int32_t> first;                    // per wave: its first row in `order`
+        for (int32_t i = 0; i < nown;) {
             int32_t kmax = 0;
-            for (int j = 0; j < 64 && 64 * w + j < nown; j++) {
-                H.rowmap[64 * (size_t)w + j] = order[64 * w + j];
-                kmax = std::max(kmax, cnt[order[64 * w + j]]);
+            for (int j = 0; j < 64 && i + j < nown; j++) kmax = std::max(kmax, cnt[order[i + j]]);
+            const bool sp = split_t > 0 && kmax > split_t;
+            const int nr = sp ? 32 : 64;
+            int32_t steps = 0;
+            for (int j = 0; j < nr && i + j < nown; j++) {
+                const int32_t c = cnt[order[i + j]];
+                steps = std::max(steps, sp ? (c + 1) / 2 : c);
             }
-            H.woff[w + 1] = H.woff[w] + kmax;
+            first.push_back(i);
+            const size_t base = H.rowmap.size();
+            H.rowmap.resize(base + 64, -1);
+            for (int j = 0; j < nr && i + j < nown; j++) H.rowmap[base + j] = order[i + j];
+            H.woff.push_back(H.woff.back() + steps);
+            H.wsplit.push_back(sp ? 1 : 0);
+            i += nr;
         }
+        const int32_t nw = (int32_t)H.wsplit.size();
         const int64_t nsl = H.woff[nw];
         H.pmap.assign((size_t)nsl * 64, -1);
         H.pidx.assign((size_t)nsl * 64, -1);
-        for (int32_t w = 0; w < nw; w++)
-            for (int j = 0; j < 64; j++) {
+        std::vector<int32_t> pm, pi;                   // one row's slot list
+        for (int32_t w = 0; w < nw; w++) {
+            const bool sp = H.wsplit[w] != 0;
+            for (int j = 0; j < (sp ? 32 : 64); j++) {
                 const int32_t l = H.rowmap[64 * (size_t)w + j];
                 if (l < 0) continue;
-                int64_t k = H.woff[w];
-                for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++, k++) {
-                    H.pmap[64 * k + j] = H.inc[x];
-                    H.pidx[64 * k + j] = H.inc[x] >> 2;
+                pm.clear();
+                pi.clear();
+                for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++) { pm.push_back(H.inc[x]); pi.push_back(H.inc[x] >> 2); }
+                for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++) {
+                    pm.push_back(-(2 + x));
+                    pi.push_back(-(2 + d.dep_scale[H.dep_ids[x]]));
                 }
-                for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++, k++) {
-                    H.pmap[64 * k + j] = -(2 + x);
-                    H.pidx[64 * k + j] = -(2 + d.dep_scale[H.dep_ids[x]]);
+                const size_t h = sp ? (pm.size() + 1) / 2 : pm.size();
+                for (size_t t = 0; t < pm.size(); t++) {
+                    const int lane = t < h ? j : j + 32;
+                    const int64_t k = H.woff[w] + (int64_t)(t < h ? t : t - h);
+                    H.pmap[64 * k + lane] = pm[t];
+                    H.pidx[64 * k + lane] = pi[t];
                 }
             }
+        }
     }
     for (int32_t h = 0; h < Q + S; h++)
         H.max_heavy_blocks = std::max<int32_t>(H.max_heavy_blocks, (int32_t)(H.hv_blk_off[h + 1] - H.hv_blk_off[h]));

@@ -275,9 +275,15 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         static const int u_env = [] {
             const char *e = std::getenv("DEFTRI_SP_P2_STEP");
             const int v = e ? std::atoi(e) : kSpP2Step;
-            return v == 4 || v == 8 ? v : kSpP2Step;
+            return v == 4 || v == 6 || v == 8 ? v : kSpP2Step;
         }();
         G.p2u = u_env;
+        static const int g_env = [] {
+            const char *e = std::getenv("DEFTRI_SP_GLIN_STEP");
+            const int v = e ? std::atoi(e) : kSpGlinStep;
+            return v == 4 || v == 6 || v == 8 ? v : kSpGlinStep;
+        }();
+        G.glu = g_env;
         const int rpw = 4 / G.rs;
         G.nrb2 = (G.nwaves + rpw - 1) / rpw;
     }
@@ -310,8 +316,9 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     {
         int32_t *rm, *pm, *pi;
         int64_t *wo;
-        PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx);
-        G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi;
+        uint8_t *ws;
+        PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx); PUT(ws, H.wsplit);
+        G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi; G.wsplit = ws;
         if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
         else { ALLOC(G.pj, 3 * 64 * G.nslots); }
         H.pmap.clear(); H.pmap.shrink_to_fit();
@@ -322,7 +329,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.hl, 21 * (int64_t)Q + S + G.ndof);
     G.b = G.hl + 21 * (int64_t)Q + S;
     ALLOC(G.Mh, 36 * (int64_t)Q + S);
-    ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(G.nrb, 1));
+    ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(G.nrb2, 1));
     ALLOC(G.r, G.ndof); ALLOC(G.q, G.ndof); ALLOC(G.x, G.ndof);
     // zp: [heavy][rows][receive region: the halo rows, 3 dofs each, in the concatenated receive order]
     int64_t nrecv = 0;
@@ -337,7 +344,6 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.ph, std::max<int64_t>(H.hd, 1));
     G.m1n = sp_merged_grid1(G);
     ALLOC(G.m1part, G.m1n); ALLOC(G.m2part, 2 * (int64_t)sp_merged_grid2(G)); ALLOC(G.gsum, 32);
-    ALLOC(G.apub, 1); ALLOC(G.aflag, 1);
     if (std::getenv("DEFTRI_SP_P2_TRACE")) {               // diagnostics: phase-2 wave stamps
         const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
         ALLOC(G.p2tr, 6 * nw);
@@ -345,7 +351,6 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         const char *e = std::getenv("DEFTRI_SP_P2_TRACE_IT");
         G.p2tr_it = e ? std::atoi(e) : 2;
     }
-    SPOK(hipMemset(G.aflag, 0xff, sizeof(int)));
     ALLOC(G.cnt, 48);                                      // three ticket sites, 16 counters each
     SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
     {
@@ -1036,13 +1041,13 @@ int SpSolver::chi2(double *out) {
     return 0;
 }
 
-int SpSolver::gradient(double *b, double *hdiag, int64_t n) {
+int SpSolver::gradient(double *b, double *hdiag, int64_t n, bool analytic) {
     if (!have_) return fail(DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (nranks_ > 1) return fail(DEFTRI_E_ARG, "not available on a point-sharded context");
     if (n != G.ndof) return fail(DEFTRI_E_ARG, "size mismatch");
     hipSetDevice(dev_);
     bool ok;
-    int rc = lin_iteration(true, false, ok);
+    int rc = lin_iteration(analytic, false, ok);
     if (rc) return rc;
     if (b) {
         sp_launch_permute_out(G.P, G.hd, d_row_of_point, G.b, d_tmp, st_);
