@@ -490,6 +490,39 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     // the mesh of keyframe 1's positions (Delaunay, adjacency, area, cot weights, vector map), built
     // once per keyframe: every pair with that keyframe 1 has the same v1Positions
     std::vector<std::shared_ptr<GraphResult::MeshData>> kf1_mesh(K);
+    auto make_mesh = [&](int b, std::string &e) -> std::shared_ptr<GraphResult::MeshData> {
+        const deftri_keyframe &kf1 = map.keyframes[b];
+        auto md = std::make_shared<GraphResult::MeshData>();
+        for (int s = 0; s < kf1.n_slots; s++)
+            if (kf1.point_id[s] >= 0)
+                for (int k = 0; k < 3; k++) md->pos1.push_back((double)kf1.point_pos[3 * s + k]);
+        md->n1 = (int)md->pos1.size() / 3;
+        Mesh M;
+        if (!build_mesh(md->pos1, md->n1, M, e, gdev == nullptr)) return nullptr;   // device: weights in the device pass
+        md->tris = std::move(M.tris); md->off = std::move(M.off); md->adj = std::move(M.adj);
+        md->w = std::move(M.w);
+        md->T = M.T; md->hull = M.hull; md->area = M.area;
+        md->pos_idx = vector_map(md->pos1, md->n1);
+        md->inv.assign(md->n1, -1);          // invertedPosIndexes: the last vertex wins
+        for (int v = 0; v < md->n1; v++) md->inv[md->pos_idx[v]] = v;
+        md->identity_map = M.skipped == 0;
+        for (int v = 0; v < md->n1 && md->identity_map; v++) md->identity_map = md->pos_idx[v] == v;
+        return md;
+    };
+    {
+        // every keyframe 1's mesh up front, the keyframes on parallel host threads (each mesh is a
+        // function of its keyframe's positions alone)
+        std::vector<int> need;
+        for (int b = 1; b < K; b++)
+            for (int a = 0; a < b; a++)
+                if (!(pair_window > 0 && b - a > pair_window)) { need.push_back(b); break; }
+        std::vector<std::string> errs(need.size());
+        parallel_for((int)need.size(), 1, [&](int lo, int hi) {
+            for (int i = lo; i < hi; i++) kf1_mesh[need[i]] = make_mesh(need[i], errs[i]);
+        });
+        for (size_t i = 0; i < need.size(); i++)
+            if (!kf1_mesh[need[i]]) { err = errs[i]; return false; }
+    }
     for (int a = 0; a < K; a++) {
         for (int b = a + 1; b < K; b++) {
             if (pair_window > 0 && b - a > pair_window) continue;
@@ -503,24 +536,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 if (kf2.point_id[s] >= 0)
                     for (int k = 0; k < 3; k++) pos2.push_back((double)kf2.point_pos[3 * s + k]);
             auto t0 = tnow();
-            if (!kf1_mesh[b]) {
-                auto md = std::make_shared<GraphResult::MeshData>();
-                for (int s = 0; s < kf1.n_slots; s++)
-                    if (kf1.point_id[s] >= 0)
-                        for (int k = 0; k < 3; k++) md->pos1.push_back((double)kf1.point_pos[3 * s + k]);
-                md->n1 = (int)md->pos1.size() / 3;
-                Mesh M;
-                if (!build_mesh(md->pos1, md->n1, M, err, gdev == nullptr)) return false;   // device: weights in the device pass
-                md->tris = std::move(M.tris); md->off = std::move(M.off); md->adj = std::move(M.adj);
-                md->w = std::move(M.w);
-                md->T = M.T; md->hull = M.hull; md->area = M.area;
-                md->pos_idx = vector_map(md->pos1, md->n1);
-                md->inv.assign(md->n1, -1);          // invertedPosIndexes: the last vertex wins
-                for (int v = 0; v < md->n1; v++) md->inv[md->pos_idx[v]] = v;
-                md->identity_map = M.skipped == 0;
-                for (int v = 0; v < md->n1 && md->identity_map; v++) md->identity_map = md->pos_idx[v] == v;
-                kf1_mesh[b] = md;
-            }
+            if (!kf1_mesh[b] && !(kf1_mesh[b] = make_mesh(b, err))) return false;
             const GraphResult::MeshData &MD = *kf1_mesh[b];
             const std::vector<double> &pos1 = MD.pos1;
             const std::vector<int32_t> &posIdx = MD.pos_idx, &inv = MD.inv;

@@ -2098,7 +2098,7 @@ int deftri_eval_gradient(deftri_ctx *ctx, double *b, double *hdiag, int64_t n) {
     if (!ctx || !ctx->have) return fail(ctx, DEFTRI_E_NOPROBLEM, "no problem uploaded");
     if (ctx->sp_on) {
         hipSetDevice(ctx->device);
-        int rc = ctx->sp->gradient(b, hdiag, n, ctx->analytic_jac != 0);
+        int rc = ctx->sp->gradient(b, hdiag, n, true);   // analytic J, as the multifrontal plan
         return rc ? fail(ctx, rc, ctx->sp->err) : 0;
     }
     if (n != ctx->S.ndof) return fail(ctx, DEFTRI_E_ARG, "size mismatch");

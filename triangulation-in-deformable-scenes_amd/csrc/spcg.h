@@ -252,7 +252,7 @@ class SpSolver {
     int download(double *points, double *scales, double *tg);
     int reset_state();
     int chi2(double *out);
-    int gradient(double *b, double *hdiag, int64_t n, bool analytic);   // J mode as the context's
+    int gradient(double *b, double *hdiag, int64_t n, bool analytic);
     int damped_solve(double lambda, const double *rhs, double *x, int64_t n);
     int hessian_product(double lambda, const double *x, double *y, int64_t n);   // y = (H + lambda I) x
     int profile_trial(double lambda, KProf &prof, bool analytic);
