@@ -293,37 +293,6 @@ __global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restr
     o[9] = X.t[0]; o[10] = X.t[1]; o[11] = X.t[2];
 }
 
-// the numeric ARAP Jacobian with every evaluation in full (MODE 3's loop), columns stored into J:
-// MODE 2's path for an edge with a -0.0 coordinate
-__device__ __noinline__ void arap_numeric_full(const double (*P)[3], const double *X, const double *Ri, const double *Rj,
-                                               double w, double area, double *J, int e, int64_t jld) {
-#pragma clang fp contract(off)
-    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
-    auto jst = [&](int k, double v) {
-        if (jld) J[k * jld + e] = v;
-        else J[18 * (int64_t)e + k] = v;
-    };
-    for (int vi = 0; vi < 4; vi++)
-        for (int dd = 0; dd < 3; dd++) {
-            double Pp[4][3], Pm[4][3];
-            for (int a = 0; a < 4; a++)
-                for (int k = 0; k < 3; k++) {
-                    const double d = (a == vi && k == dd) ? delta : 0.0;
-                    Pp[a][k] = P[a][k] + d;
-                    Pm[a][k] = P[a][k] - d;
-                }
-            const double ep = arap_err_rt(Pp[0], Pp[1], Pp[2], Pp[3], X, X + 9, Ri, Rj, w, area);
-            const double em = arap_err_rt(Pm[0], Pm[1], Pm[2], Pm[3], X, X + 9, Ri, Rj, w, area);
-            jst(3 * vi + dd, scalar * (ep - em));
-        }
-    for (int dd = 0; dd < 6; dd++) {
-        const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
-        const double ep = arap_err_rt(P[0], P[1], P[2], P[3], Xp, Xp + 9, Ri, Rj, w, area);
-        const double em = arap_err_rt(P[0], P[1], P[2], P[3], Xm, Xm + 9, Ri, Rj, w, area);
-        jst(12 + dd, scalar * (ep - em));
-    }
-}
-
 // MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian, pieces reused; 3: the
 // same, every evaluation in full (one kernel per mode: each gets the registers of its own path)
 template <int MODE>
@@ -389,7 +358,7 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
         // T_g perturbation leaves the rows' terms f, g unchanged (no division), a v2i / v2j one changes
         // one row of each (2 of 6 divisions).  g2o's + evaluations see the other coordinates as
         // x + 0.0, the - ones as x - 0.0 = x: the same bits unless a coordinate is -0.0, and an edge
-        // with one takes the full evaluations (arap_numeric_full).  Each column is stored when formed.
+        // with one takes the full evaluations.  Each column is stored when formed.
         auto jst = [&](int k, double v) {
             if (jld) J[k * jld + e] = v;
             else J[18 * (int64_t)e + k] = v;
@@ -400,7 +369,33 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
 #pragma unroll
             for (int k = 0; k < 3; k++) negz |= __double_as_longlong(P[a][k]) == (long long)0x8000000000000000ull;
         if (negz) {
-            arap_numeric_full(P, tg_pre + 12 * kArapPre * (int64_t)q, Ri, Rj, w, area, J, e, jld);
+            // MODE 3's evaluations, inline (a call would give every wave a stack)
+            const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+            const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
+#pragma unroll
+            for (int vi = 0; vi < 4; vi++)
+#pragma unroll 1
+                for (int dd = 0; dd < 3; dd++) {
+                    double Pp[4][3], Pm[4][3];
+#pragma unroll
+                    for (int a = 0; a < 4; a++)
+#pragma unroll
+                        for (int k = 0; k < 3; k++) {
+                            const double d = (a == vi && k == dd) ? delta : 0.0;
+                            Pp[a][k] = P[a][k] + d;
+                            Pm[a][k] = P[a][k] - d;
+                        }
+                    const double ep = arap_err_rt(Pp[0], Pp[1], Pp[2], Pp[3], X, X + 9, Ri, Rj, w, area);
+                    const double em = arap_err_rt(Pm[0], Pm[1], Pm[2], Pm[3], X, X + 9, Ri, Rj, w, area);
+                    jst(3 * vi + dd, scalar * (ep - em));
+                }
+#pragma unroll 1
+            for (int dd = 0; dd < 6; dd++) {
+                const double *Xp = X + 12 * (1 + 2 * dd), *Xm = Xp + 12;
+                const double ep = arap_err_rt(P[0], P[1], P[2], P[3], Xp, Xp + 9, Ri, Rj, w, area);
+                const double em = arap_err_rt(P[0], P[1], P[2], P[3], Xm, Xm + 9, Ri, Rj, w, area);
+                jst(12 + dd, scalar * (ep - em));
+            }
         } else {
             const double delta = 1e-9, scalar = 1.0 / (2 * delta);
             const double *X = tg_pre + 12 * kArapPre * (int64_t)q;
@@ -426,7 +421,6 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
                 const double ep = arap_pert<VI, DD>(bm, P, P[VI][DD] + delta, Rg, Rg + 9, Ri, Rj, w, area);
                 const double em = arap_pert<VI, DD>(bm, P, P[VI][DD] - delta, Rg, Rg + 9, Ri, Rj, w, area);
                 jst(3 * VI + DD, scalar * (ep - em));
-                __builtin_amdgcn_sched_barrier(0);          // one evaluation pair's registers at a time
             };
             using std::integral_constant;
             point(integral_constant<int, 0>{}, integral_constant<int, 0>{});
