@@ -260,6 +260,69 @@ def main_ba(args, world, rank, gpu, backend):
         dist.destroy_process_group()
 
 
+def main_deformation(args, world, rank, gpu):
+    """deformationOptimization end to end (g2oBundleAdjustment.cc:446-606) at the Simulation.yaml
+    defaults (tests/golden/sim_default/settings.yaml is Data/Simulation.yaml byte for byte: 20 outer
+    rounds, twoOptimizations + nlopt with 30 Nelder-Mead evaluations per round — every evaluation an
+    arapOptimization of 25 LM iterations on a map clone (outerObjective, nloptOptimization.cc:4-37) —
+    then arapOptimization with the optimum; stop at sum |dp| < 1e-4 |MapPoints|; the documented
+    DepthWeight deviation 3.0) on the reference's simulation scene scaled to --corr
+    correspondences (C1: 1000).  Times the whole call on the device; the CPU leg runs the same loop
+    with the oracle's arapOptimization (tests/arap_oracle_fn.py: oracle/graph_ref.py graph build +
+    the oracle LM, 1 thread) for its first outer round (a bounded sample), compared round for round."""
+    import copy
+    from deftri import optimization
+    from deftri.settings import Settings
+    n = args.corr or 1000
+    st = Settings(path=str(ROOT / "tests" / "golden" / "sim_default" / "settings.yaml"))
+    st.depth_weight = 3.0
+    if args.rounds:
+        st.n_optimizations = args.rounds
+    m, _ = sim.simulate_two_view(n=n, seed=1, scale_scene=True, compact=True)
+    m0 = copy.deepcopy(m)
+    rounds = []
+    t0 = time.perf_counter()
+    t_last = [t0]
+
+    def log_round(info):
+        t = time.perf_counter()
+        rounds.append({"round": info["round"], "s": round(t - t_last[0], 3), "evaluations": len(info.get("evaluations", [])),
+                       "weights": info.get("weights"), "update": info["update"]})
+        t_last[0] = t
+    out_rounds = optimization.deformationOptimization(m, st, device=gpu, log=log_round)
+    dt = time.perf_counter() - t0
+    n_eval = sum(len(r.get("evaluations", [])) + 1 for r in out_rounds)
+    log(f"deformation: {len(out_rounds)} rounds, {n_eval} arapOptimization calls in {dt:.2f} s")
+    cpu = None
+    if not args.no_cpu_baseline:
+        # one arapOptimization of the loop (the first Nelder-Mead evaluation: the map's clone at the
+        # Simulation.yaml weights, 25 LM iterations) on the oracle — ~13 s of one core at 1k; the
+        # whole first round (8 calls) is ~100 s
+        sys.path.insert(0, str(ROOT))
+        sys.path.insert(0, str(ROOT / "tests"))
+        from arap_oracle_fn import oracle_arap
+        mc = copy.deepcopy(m0)
+        t1 = time.perf_counter()
+        upd = oracle_arap(mc, st.rep, st.global_, st.arap, st.alpha, st.beta, st.depth_sigma, st.n_iterations)
+        dc = time.perf_counter() - t1
+        info = host_cpu_info()
+        cpu = {"value": 1.0 / dc, "unit": "arapOptimization calls/s", "cores": 1, "kind": "port",
+               "sample": f"one arapOptimization of the loop (a clone of the {n}-correspondence map at the Simulation.yaml "
+                         f"weights, {st.n_iterations} LM iterations) with the oracle (Python graph build + C LM, 1 thread): "
+                         f"{dc:.2f} s, update {upd:.6g}; host {info['cpu_model']}",
+               "seconds_per_call": round(dc, 3)}
+        log(f"deformation cpu baseline: {cpu}")
+    out = {"metric": "arapOptimization calls/s inside deformationOptimization (Simulation.yaml defaults, NLopt weight search)",
+           "value": n_eval / dt, "unit": "arapOptimization calls/s", "n_gpus": 1, "steps": n_eval,
+           "warmup": 0, "ms_per_step": 1e3 * dt / max(n_eval, 1), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "config": {"workload": f"deformation-{n}", "correspondences": n, "rounds": len(out_rounds),
+                      "arap_calls": n_eval, "seconds_total": round(dt, 3), "outer_rounds_per_s": round(len(out_rounds) / dt, 4),
+                      "settings": "Data/Simulation.yaml (+ DepthWeight 3.0)"},
+           "rounds": rounds, "roofline": None, "cpu_baseline": cpu}
+    print(json.dumps(out), flush=True)
+
+
 def reduce_stats(dt, iters, trials, world, device):
     """Whole-job numbers from per-rank ones: max wall time over ranks, summed iterations/trials.
     The replicas share nothing else (no data-path collective)."""
@@ -445,7 +508,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--regime", choices=list(REGIMES), default="simulation",
                     help="c2: the weight regime (Simulation.yaml default; Drunkard / Realcolon weights and cameras)")
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "ba"], default="c2",
+    ap.add_argument("--rounds", type=int, default=0, help="--workload deformation: cap the outer rounds (0: Simulation.yaml's)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "ba", "deformation"], default="c2",
                     help="c2: the headline (BASELINE.json metric); c3-c5: the multi-keyframe configs; ba: bundle adjustment")
     ap.add_argument("--pair-window", type=int, default=-1,
                     help="keyframe pairs: 0 every pair (the reference), w > 0 pairs at most w apart (default: the workload's)")
@@ -492,6 +556,8 @@ def main():
     red_dev = "cuda" if backend == "nccl" else "cpu"
     if args.workload == "ba":
         return main_ba(args, world, rank, gpu, backend)
+    if args.workload == "deformation":
+        return main_deformation(args, world, rank, gpu)
 
     wl = args.workload
     spec = WORKLOADS[wl]
