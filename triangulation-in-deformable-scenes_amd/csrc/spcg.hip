@@ -814,14 +814,28 @@ __device__ __forceinline__ void heavy_finish(const SpDev &G, int it, double lam,
 // next iteration, which the host raises as an error (never a rejected trial) and answers by
 // switching the context to the separate alpha launch (k_sp_alpha).  Either way every workgroup still
 // draws its ticket in m2_dots, so the counters return to zero.
-__device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish) {
+// the first sixteen of thread t's partials (t, t + 256, ...; zeros past the end) and r.z: phase 2's
+// workgroup 0 issues these loads before its state test, so they overlap it
+struct AlphaPre {
+    double v[16];
+    double gam;
+};
+__device__ __forceinline__ void m2_alpha_loads(const SpDev &G, int it, AlphaPre &pf) {
+    const int n = G.m1n, j = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 16; u++) pf.v[u] = j + 256 * u < n ? G.m1part[j + 256 * u] : 0.0;
+    pf.gam = G.red[(int64_t)kSpRed * it];
+}
+__device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish, const AlphaPre &pf) {
     __shared__ double sa;
     // thread t adds partials t, t + 256, ... in order; sixteen loads in flight (a C2-size launch,
     // ~3,200 partials, in one round trip: alpha is on every row's path), the missing ones as zeros
     double a = 0.0;
     const int n = G.m1n;
-    const double gam = G.red[(int64_t)kSpRed * it];         // r.z, loaded with the partials
-    for (int j = threadIdx.x; j < n; j += 16 * 256) {
+    const double gam = pf.gam;
+#pragma unroll
+    for (int u = 0; u < 16; u++) a += pf.v[u];
+    for (int j = threadIdx.x + 16 * 256; j < n; j += 16 * 256) {
         double v[16];
 #pragma unroll
         for (int u = 0; u < 16; u++) v[u] = j + 256 * u < n ? G.m1part[j + 256 * u] : 0.0;
@@ -873,7 +887,9 @@ __global__ void __launch_bounds__(256) k_sp_alpha(int it, const SpDev G) {
     if (gated_off(G.gate)) return;
     double beta;
     if (it_state(G, it, beta)) return;
-    m2_alpha_make(G, it, red4, false);
+    AlphaPre pf;
+    m2_alpha_loads(G, it, pf);
+    m2_alpha_make(G, it, red4, false, pf);
 }
 
 // MG 1 (merged chain, one rank): also p.Ap = sum_e s_e (J_e p) + sum_dep p_s (2 c_e . p_v + W J_s^2 p_s)
@@ -1062,6 +1078,10 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             }
             return;
         }
+    }
+    AlphaPre pf;                                            // MG 1, workgroup 0: alpha's loads first
+    if (MG == 1 && !G.alpha_kernel && blockIdx.x == 0) m2_alpha_loads(G, it, pf);
+    if (MG == 2) {
     } else if (const int st = it_state(G, it, beta)) {
         // with the heavy finish folded in here, k_sp_heavy's record of the first stopped iteration too
         if ((MG || G.fuse_heavy) && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
@@ -1074,7 +1094,7 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     double th = 0.0;                                        // ... its component sum (thread < dim)
     if constexpr (MG == 1) {
         if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];     // k_sp_alpha's
-        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true);
+        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true, pf);
         if ((int)blockIdx.x < G.m_nh) {
             rows = false;
             if ((int)blockIdx.x < G.Q + G.S) {
