@@ -685,6 +685,7 @@ def main():
                        "ms_per_trial": round(ms_per_step / max(trials_per_it, 1e-9), 3),
                        "pcg_trials": rep["pcg_trials"], "pcg_failed_or_fallback": rep["pcg_fallbacks"],
                        "cg_iterations_per_pcg_trial": round(rep["pcg_iterations"] / max(rep["pcg_trials"], 1), 2),
+                       "pcg_continuations_per_trial": round(rep.get("pcg_continuations", 0) / max(rep["trials_total"], 1), 3),
                        "ms_per_cg_iteration_profiled": round(roofline["cg_iteration_us"] / 1e3, 4)
                        if roofline and "cg_iteration_us" in roofline else None,
                        "chi2_initial": rep["chi2_initial"], "chi2_final": rep["chi2_final"],

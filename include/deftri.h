@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 5
+#define DEFTRI_ABI_VERSION 6
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -164,6 +164,10 @@ typedef struct deftri_report {
     int32_t pcg_given_up;            /* multifrontal plan: 1 when two consecutive fallbacks sent the rest of
                                         the call's trials straight to the LDL^T */
     int32_t plan;                    /* DEFTRI_PLAN_MULTIFRONTAL / DEFTRI_PLAN_ITERATIVE */
+    /* round 4 (ABI 6) */
+    int32_t pcg_continuations;       /* iterative plan: trials whose PCG outran the CG iterations queued
+                                        before the evaluation (the last converged count + a margin):
+                                        evaluated, restored, continued in chunks of 4 */
 } deftri_report;
 
 /* ---- context ---------------------------------------------------------------------- */

@@ -46,6 +46,7 @@ constexpr int kSpWaveSplit = 16;       // phase-2 waves with rows of more slots 
 constexpr int kSpRowSplit = 1;         // phase 2: waves per row-wave's slot list (DEFTRI_SP_ROW_SPLIT)
 constexpr int kSpP2Step = 8;           // phase 2: slots per step (DEFTRI_SP_P2_STEP = 4 or 8)
 constexpr int kSpGlinStep = 8;         // k_sp_glin_rows: slots per step (DEFTRI_SP_GLIN_STEP = 4 or 8)
+constexpr int kSpGuessMargin = 1;      // CG iterations queued per trial: last converged count + this
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
 constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one thread per dof)
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup

@@ -607,7 +607,7 @@ __device__ __forceinline__ void sd_send(const SpDev &G, int l, int a, double z, 
 
 // setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
 // partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
-__global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
+__global__ void __launch_bounds__(3 * kSpUpdRows) __attribute__((amdgpu_waves_per_eu(6, 6))) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
     // the row blocks as in k_sp_update: one thread per dof for the vectors, one per row for the
     // block inverse (through LDS)
     __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
@@ -846,7 +846,7 @@ __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *
     if (threadIdx.x == 0) {
         double alpha = gam / a;
         if (!(a > 0.0) || !isfinite(alpha) || alpha == 0.0) {
-            G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpBreakdown;   // read from the next launch on
+            st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpBreakdown);   // read from the next launch on (and m2_dots)
             alpha = __builtin_nan("");
         }
         // the value is its own flag: word 3 of iteration it's record is zero until this store (the
@@ -871,7 +871,7 @@ __device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
             n++;
         }
         if (n >= (1 << 22)) {                          // never expected: stop the solve, skip the update
-            G.red[(int64_t)kSpRed * (it + 1) + 2] = kSpTimeout;
+            st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpTimeout);
             sa = __builtin_nan("");
         } else {
             sa = v;
@@ -1019,6 +1019,18 @@ __device__ __forceinline__ void m2_dots(const SpDev &G, int it, double (*red)[4]
     if (group_sum<2>(G, G.cnt, G.m2part, G.gsum + 16, red, tot) && threadIdx.x == 0) {
         G.red[(int64_t)kSpRed * (it + 1)] = tot[0];
         G.red[(int64_t)kSpRed * (it + 1) + 1] = tot[1];
+        // the state of iteration it + 1 as the next launch's it_state would find it — the stop word
+        // (stored agent-scope, settled before its workgroup's ticket), converged, budget — into the
+        // record: this is the launch's last workgroup, so every other one has tested its state
+        // already, and the chain needs no status-only tail launch
+        if (G.rec[0] == 0.0) {
+            const double sw = ld_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2);
+            int st = 0;
+            if (sw != 0.0) st = (int)sw;
+            else if (tot[1] <= G.tol2 * G.red[1]) st = kSpConverged;
+            else if (it + 1 >= G.max_it) st = kSpBudget;
+            if (st) { G.rec[0] = st; G.rec[1] = it + 1; }
+        }
     }
 }
 

@@ -574,6 +574,7 @@ int SpSolver::cg_chain(double lambda, int from, int to) {
 // decides it after iteration n's product and reduction: they run, the update records only)
 int SpSolver::cg_tail(int n, double lambda) {
     int rc;
+    if (G.merged) return 0;                            // phase 2's last workgroup records iteration n's state
     if (G.sd) {
         sp_launch_product(G, n, lambda, fp32_jac != 0, st_);
         if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
@@ -902,7 +903,13 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             };
             auto t0p = std::chrono::steady_clock::now();
             if ((rc = cg_setup(lambda, G.b))) return rc;
-            const int n = std::min(std::max(2, last_its + 1), mx);
+            // CG iterations queued before the trial's evaluation: the last converged count + a
+            // margin (DEFTRI_SP_GUESS_MARGIN).  A short guess costs the evaluation, a state restore
+            // and a host round trip; each extra queued iteration past convergence two early-out
+            // launches
+            static const int margin = std::getenv("DEFTRI_SP_GUESS_MARGIN") ? std::atoi(std::getenv("DEFTRI_SP_GUESS_MARGIN"))
+                                                                            : kSpGuessMargin;
+            const int n = std::min(std::max(2, last_its + margin), mx);
             if ((rc = cg_chain(lambda, 0, n))) return rc;
             int j = n;
             if ((rc = cg_tail(j, lambda))) return rc;
@@ -914,6 +921,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             bool solved = st == kSpConverged, evaluated = solved;
             int its = solved ? (int)hpin[17] : j;
             if (!solved) {
+                R.pcg_continuations++;
                 // restore the state the evaluation changed; continue the solve in chunks of 4
                 SPOK(hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
                 SPOK(hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));

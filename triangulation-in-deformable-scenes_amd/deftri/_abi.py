@@ -57,7 +57,7 @@ class Report(C.Structure):
         ("n_levels", i32), ("lanes", i32), ("trials_executed", i32),
         ("rank", i32), ("nranks", i32), ("factor_flops_total", f64), ("plan_reuses", i64),
         ("pcg_trials", i32), ("pcg_fallbacks", i32), ("pcg_iterations", i64), ("ms_pcg", f64),
-        ("pcg_given_up", i32), ("plan", i32),
+        ("pcg_given_up", i32), ("plan", i32), ("pcg_continuations", i32),
     ]
 
     def as_dict(self):
@@ -78,6 +78,7 @@ class Report(C.Structure):
             "pcg_trials": self.pcg_trials, "pcg_fallbacks": self.pcg_fallbacks,
             "pcg_iterations": self.pcg_iterations, "ms_pcg": self.ms_pcg,
             "pcg_given_up": self.pcg_given_up,
+            "pcg_continuations": self.pcg_continuations,
             "plan": {DEFTRI_PLAN_MULTIFRONTAL: "multifrontal", DEFTRI_PLAN_ITERATIVE: "iterative"}.get(self.plan, "none"),
         }
 
