@@ -12,7 +12,8 @@ correct g2o LM (g2oBundleAdjustment.cc:959-962) and need no r
 
 C2: bench.py's headline scene (100k correspondences x 2 views, 600,008 unknowns).  C3 shape: 50k
 correspondences x 8 keyframes, all 28 pairs (1.2M unknowns, 8.4M ARAP edges; Drunkard.yaml shapes
-and weights), bench.py --workload c3's scene."""
+and weights), bench.py --workload c3's scene.  C4: 500k x 8 keyframes, all 28 pairs (12M unknowns,
+84M ARAP edges), bench.py --workload c4's scene."""
 import numpy as np
 import pytest
 
@@ -23,6 +24,11 @@ pytestmark = pytest.mark.gpu
 
 def c2_problem():
     return sim.two_view_problem(100000, 1)            # bench.py build_problem(100000, 1)
+
+
+def c4_problem():
+    return sim.multi_view_problem(500000, 8, seed=1, kb8=sim.DRUNKARD_KB8, rep_weight=1.0, arap_weight=1e7,
+                                  depth_sigma=np.float32(0.3), pair_window=0)
 
 
 def c3_problem():
@@ -75,3 +81,13 @@ def test_c3_shape_full_size_properties():
     assert p.n_pairs == 28 and p.n_unknowns == 1200224
     r, solves = check_props(p, 3, (1e-5,))
     print("C3", r["trials_iter"], solves)
+
+
+def test_c4_full_size_properties():
+    """C4 (BASELINE configs[3]): 500k correspondences x 8 keyframes, all 28 pairs — 12,000,224
+    unknowns, 84M ARAP edges (bench.py --workload c4's scene), the same properties over 2 LM
+    iterations."""
+    p = c4_problem()
+    assert p.n_pairs == 28 and p.n_unknowns == 12000224
+    r, solves = check_props(p, 2, (1e-5,))
+    print("C4", r["trials_iter"], solves)

@@ -5,17 +5,38 @@
 // passes are O(E + P) counting sorts and scans, so a 500k x 8-keyframe graph (84M ARAP edges,
 // SURVEY §8d C4) plans in seconds; nothing here depends on a fill-reducing ordering.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <functional>
 #include <numeric>
+#include <thread>
 
 #include "spcg.h"
 
 namespace deftri {
 
 namespace {
+
+// [0, n) in contiguous chunks on up to 16 host threads (DEFTRI_HOST_THREADS); f(chunk, lo, hi).
+// The plan's parallel passes write disjoint ranges or per-chunk counters merged in chunk order, so
+// the plan does not depend on the split
+template <class F>
+int chunked(int64_t n, int64_t min_chunk, F f) {
+    static const int env_t = std::getenv("DEFTRI_HOST_THREADS") ? std::atoi(std::getenv("DEFTRI_HOST_THREADS")) : 0;
+    const int hw = env_t > 0 ? env_t : (int)std::max(1u, std::thread::hardware_concurrency());
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, 16, n / std::max<int64_t>(min_chunk, 1)}));
+    if (nt <= 1) { f(0, (int64_t)0, n); return 1; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; t++) {
+        const int64_t b = n * t / nt, e = n * (t + 1) / nt;
+        th.emplace_back([=, &f] { f(t, b, e); });
+    }
+    for (auto &x : th) x.join();
+    return nt;
+}
 
 // stable counting sort of `ids` by key(id) in [0, nkeys)
 template <class Key>
@@ -42,6 +63,14 @@ inline uint64_t spread21(uint64_t v) {       // bits 0..20 -> every third bit
 
 bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &H,
                    std::string &err) {
+    static const bool timing = std::getenv("DEFTRI_PLAN_TIMING") != nullptr;
+    auto t_prev = std::chrono::steady_clock::now();
+    auto stage = [&](const char *name) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[deftri plan] %-28s %8.2f ms\n", name, std::chrono::duration<double, std::milli>(t - t_prev).count());
+        t_prev = t;
+    };
     H = SpPlanHost();
     if (nranks < 1 || rank < 0 || rank >= nranks) { err = "bad rank"; return false; }
     H.rank = rank;
@@ -76,6 +105,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     }
     const int32_t ng = (int32_t)grep.size();
 
+    stage("1 groups (union-find)");
     // 2. groups in Morton order of the representative's mesh-plane position
     auto xy = [&](int32_t p, int c) { return d.order_xy ? d.order_xy[2 * (int64_t)p + c] : d.points[3 * (int64_t)p + c]; };
     double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
@@ -102,6 +132,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     std::vector<int32_t> gpos(ng);
     for (int32_t k = 0; k < ng; k++) gpos[gorder[k]] = k;
 
+    stage("2 Morton order");
     // 3. rows: groups in that order, points of a group by id
     std::vector<int32_t> pts(P);
     std::iota(pts.begin(), pts.end(), 0);
@@ -111,6 +142,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     for (int32_t r = 0; r < P; r++) H.row_of_point[pts[r]] = r;
     const std::vector<int32_t> &row = H.row_of_point;
 
+    stage("3 rows");
     // 4. work-balanced contiguous group ranges per rank: weight of a row = 2 + its ARAP incidences
     std::vector<int64_t> rw(P, 2);
     for (int64_t e = 0; e < 4 * E; e++) rw[row[ap[e]]]++;
@@ -130,6 +162,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         }
         for (; next < nranks; next++) H.rank_row_begin[next] = P;
     }
+    stage("4 rank ranges");
     // 4b. inside every rank's range, rows sorted by their phase-2 slot count (ARAP incidences + depth
     //     couplings; descending, stable) in windows of kSpSortWindow rows: the order the phase-2 wave
     //     layout deals them to lanes (8b), so that layout is the identity and a wave's 64 rows are 64
@@ -164,6 +197,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     auto own = [&](int32_t r) { return r >= lo_r && r < hi_r; };
     const int32_t nown = hi_r - lo_r;
 
+    stage("4b slot-count sort");
     // 5. local ARAP edges: owned (point 0 here) first, then halo-only; each by (pair, Morton row of point 0)
     std::vector<int32_t> owned_e, halo_e;
     for (int64_t e = 0; e < E; e++) {
@@ -194,6 +228,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             }
     }
 
+    stage("5 local ARAP edges");
     // 6. the own rows' reprojection / depth edges, by row
     for (int64_t e = 0; e < R; e++) if (own(row[d.rep_point[e]])) H.rep_ids.push_back((int32_t)e);
     for (int64_t e = 0; e < D; e++) if (own(row[d.dep_point[e]])) H.dep_ids.push_back((int32_t)e);
@@ -205,6 +240,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     for (int32_t e : H.dep_ids) H.dep_off[row[d.dep_point[e]] - lo_r + 1]++;
     for (int32_t l = 0; l < nown; l++) { H.rep_off[l + 1] += H.rep_off[l]; H.dep_off[l + 1] += H.dep_off[l]; }
 
+    stage("6 rep / depth by row");
     // 7. phase-1 blocks: ARAP (owned, then halo-only) per pair in runs of kSpBlock; depth edges by
     //    (scale, row) per scale
     const int32_t ndl = (int32_t)H.dep_ids.size();
@@ -271,25 +307,46 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         for (int64_t b = 0; b < nb; b++) { const int32_t h = blk_heavy(b); if (h >= 0) H.hv_blk[pos[h]++] = (int32_t)b; }
     }
 
+    stage("7 phase-1 blocks");
     // 8. own rows' ARAP incidences (local edge << 2 | role), each row's in local-edge order
+    //    (a counting sort over chunks of local edges: per-chunk row counts, chunk-ordered offsets,
+    //    every chunk scatters its edges in order — the sequential order)
     H.inc_off.assign(nown + 1, 0);
-    for (int64_t le = 0; le < nloc; le++) {
-        const int64_t e = H.arap_ids[le];
-        for (int k = 0; k < 4; k++) { const int32_t r = row[ap[4 * e + k]]; if (own(r)) H.inc_off[r - lo_r + 1]++; }
-    }
-    for (int32_t l = 0; l < nown; l++) H.inc_off[l + 1] += H.inc_off[l];
-    H.inc.resize((size_t)H.inc_off[nown]);
     {
-        std::vector<int64_t> pos(H.inc_off.begin(), H.inc_off.end() - 1);
-        for (int64_t le = 0; le < nloc; le++) {
-            const int64_t e = H.arap_ids[le];
-            for (int k = 0; k < 4; k++) {
-                const int32_t r = row[ap[4 * e + k]];
-                if (own(r)) H.inc[pos[r - lo_r]++] = (int32_t)(le << 2 | k);
+        constexpr int64_t kMin = 1 << 16;
+        const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, nloc / kMin));
+        std::vector<std::vector<int32_t>> ccnt((size_t)nch);
+        auto lo_of = [&](int64_t c) { return nloc * c / nch; };
+        chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+            for (int64_t c = c0; c < c1; c++) {
+                ccnt[c].assign(nown, 0);
+                for (int64_t le = lo_of(c); le < lo_of(c + 1); le++) {
+                    const int64_t e = H.arap_ids[le];
+                    for (int k = 0; k < 4; k++) { const int32_t r = row[ap[4 * e + k]]; if (own(r)) ccnt[c][r - lo_r]++; }
+                }
             }
+        });
+        // offsets: row-major, chunk order inside a row (ccnt becomes each chunk's write position)
+        int64_t acc = 0;
+        for (int32_t l = 0; l < nown; l++) {
+            H.inc_off[l] = acc;
+            for (int64_t c = 0; c < nch; c++) { const int32_t v = ccnt[c][l]; ccnt[c][l] = (int32_t)acc; acc += v; }
         }
+        H.inc_off[nown] = acc;
+        H.inc.resize((size_t)acc);
+        chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+            for (int64_t c = c0; c < c1; c++)
+                for (int64_t le = lo_of(c); le < lo_of(c + 1); le++) {
+                    const int64_t e = H.arap_ids[le];
+                    for (int k = 0; k < 4; k++) {
+                        const int32_t r = row[ap[4 * e + k]];
+                        if (own(r)) H.inc[ccnt[c][r - lo_r]++] = (int32_t)(le << 2 | k);
+                    }
+                }
+        });
     }
 
+    stage("8 incidences");
     // 8b. phase-2 wave layout: per own row its ARAP incidences then its depth couplings; rows sorted by
     //     that count (descending, stable) inside windows of kSpSortWindow rows, 64 per wave.  A wave
     //     whose rows hold more than kSpWaveSplit slots (DEFTRI_SP_WAVE_SPLIT; 0 = never) takes 32
@@ -306,10 +363,13 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             cnt[l] = (int32_t)(H.inc_off[l + 1] - H.inc_off[l]) + (H.dep_off[l + 1] - H.dep_off[l]);
         std::vector<int32_t> order(nown);
         std::iota(order.begin(), order.end(), 0);
-        for (int32_t w0 = 0; w0 < nown; w0 += kSpSortWindow) {
-            const int32_t w1 = std::min(nown, w0 + kSpSortWindow);
-            std::stable_sort(order.begin() + w0, order.begin() + w1, [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
-        }
+        const int64_t nwin = (nown + kSpSortWindow - 1) / kSpSortWindow;
+        chunked(nwin, 64, [&](int, int64_t a0, int64_t a1) {
+            for (int64_t a = a0; a < a1; a++) {
+                const int32_t w0 = (int32_t)(a * kSpSortWindow), w1 = std::min(nown, w0 + kSpSortWindow);
+                std::stable_sort(order.begin() + w0, order.begin() + w1, [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
+            }
+        });
         H.rowmap.clear();
         H.woff.assign(1, 0);
         H.wsplit.clear();
@@ -334,34 +394,39 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         }
         const int32_t nw = (int32_t)H.wsplit.size();
         const int64_t nsl = H.woff[nw];
-        H.pmap.assign((size_t)nsl * 64, -1);
-        H.pidx.assign((size_t)nsl * 64, -1);
-        std::vector<int32_t> pm, pi;                   // one row's slot list
-        for (int32_t w = 0; w < nw; w++) {
-            const bool sp = H.wsplit[w] != 0;
-            for (int j = 0; j < (sp ? 32 : 64); j++) {
-                const int32_t l = H.rowmap[64 * (size_t)w + j];
-                if (l < 0) continue;
-                pm.clear();
-                pi.clear();
-                for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++) { pm.push_back(H.inc[x]); pi.push_back(H.inc[x] >> 2); }
-                for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++) {
-                    pm.push_back(-(2 + x));
-                    pi.push_back(-(2 + d.dep_scale[H.dep_ids[x]]));
-                }
-                const size_t h = sp ? (pm.size() + 1) / 2 : pm.size();
-                for (size_t t = 0; t < pm.size(); t++) {
-                    const int lane = t < h ? j : j + 32;
-                    const int64_t k = H.woff[w] + (int64_t)(t < h ? t : t - h);
-                    H.pmap[64 * k + lane] = pm[t];
-                    H.pidx[64 * k + lane] = pi[t];
+        H.pmap.resize((size_t)nsl * 64);
+        H.pidx.resize((size_t)nsl * 64);
+        chunked(nw, 256, [&](int, int64_t w0, int64_t w1) {      // waves own disjoint slot ranges
+            std::vector<int32_t> pm, pi;               // one row's slot list
+            std::fill(H.pmap.begin() + 64 * H.woff[w0], H.pmap.begin() + 64 * H.woff[w1], -1);
+            std::fill(H.pidx.begin() + 64 * H.woff[w0], H.pidx.begin() + 64 * H.woff[w1], -1);
+            for (int64_t w = w0; w < w1; w++) {
+                const bool sp = H.wsplit[w] != 0;
+                for (int j = 0; j < (sp ? 32 : 64); j++) {
+                    const int32_t l = H.rowmap[64 * (size_t)w + j];
+                    if (l < 0) continue;
+                    pm.clear();
+                    pi.clear();
+                    for (int64_t x = H.inc_off[l]; x < H.inc_off[l + 1]; x++) { pm.push_back(H.inc[x]); pi.push_back(H.inc[x] >> 2); }
+                    for (int32_t x = H.dep_off[l]; x < H.dep_off[l + 1]; x++) {
+                        pm.push_back(-(2 + x));
+                        pi.push_back(-(2 + d.dep_scale[H.dep_ids[x]]));
+                    }
+                    const size_t h = sp ? (pm.size() + 1) / 2 : pm.size();
+                    for (size_t t = 0; t < pm.size(); t++) {
+                        const int lane = t < h ? j : j + 32;
+                        const int64_t k = H.woff[w] + (int64_t)(t < h ? t : t - h);
+                        H.pmap[64 * k + lane] = pm[t];
+                        H.pidx[64 * k + lane] = pi[t];
+                    }
                 }
             }
-        }
+        });
     }
     for (int32_t h = 0; h < Q + S; h++)
         H.max_heavy_blocks = std::max<int32_t>(H.max_heavy_blocks, (int32_t)(H.hv_blk_off[h + 1] - H.hv_blk_off[h]));
 
+    stage("8b wave layout");
     // 9. halo exchange lists
     H.send_rows.assign(nranks, {});
     H.recv_rows.assign(nranks, {});
@@ -394,6 +459,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         for (auto &v : H.recv_rows) H.halo_rows += (int64_t)v.size();
     }
 
+    stage("9 halo lists");
     // 10. algorithmic bytes of one product (phase 1 + phase 2): compulsory loads and
     //     stores, the p gathers at an edge's other points not counted
     const double jb = fp32_jac ? 72.0 : 144.0;
