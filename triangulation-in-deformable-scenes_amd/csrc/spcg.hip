@@ -607,7 +607,7 @@ __device__ __forceinline__ void sd_send(const SpDev &G, int l, int a, double z, 
 
 // setup at lambda: row / heavy preconditioner blocks, r = rhs, z = M r, (z, p) = (z, 0), x = 0,
 // partial (r.z, r.r) per row block (+ the heavy block's last, on the rank that counts the heavy dofs)
-__global__ void __launch_bounds__(3 * kSpUpdRows) __attribute__((amdgpu_waves_per_eu(6, 6))) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
+__global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, const double *__restrict__ rhs, double lam) {
     // the row blocks as in k_sp_update: one thread per dof for the vectors, one per row for the
     // block inverse (through LDS)
     __shared__ double sM[6 * kSpUpdRows], sR[3 * kSpUpdRows];
