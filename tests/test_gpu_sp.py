@@ -423,6 +423,49 @@ def test_numeric_arap_jacobian_piece_reuse_bit_identical(negz):
     assert out[0] == out[1]
 
 
+@pytest.mark.parametrize("merge", ["1", ""])
+def test_iterative_budget_exhausted_trials_rejected(merge):
+    """A trial whose PCG exhausts its budget is rejected like a failed g2o linear solve (the
+    iterative plan has no factorization behind it; g2o's solve() then returns false, the trial
+    counts as rho < 0): lambda *= nu, nu *= 2.  With a budget no step meets at the first dampings
+    (2 CG iterations to 1e-12) and max_trials = 3, the first LM iteration rejects its 3 trials and
+    g2o's Terminate fires (qmax == maxTrials): chi2 and the state unchanged, lambda = tau max diag H *
+    2 * 4 * 8 — the trajectory pinned without an oracle run.  (At far larger dampings H + lambda I is
+    nearly its own block diagonal and 2 iterations do meet 1e-12.)  Both chains (merged; three-launch)."""
+    import subprocess, sys, json as _json
+    code = f"""
+import os, sys, json
+os.environ['DEFTRI_SP_{'MERGE' if merge else 'NO_MERGE'}'] = '1'
+sys.path.insert(0, {str(capi.__file__.rsplit('/deftri/', 1)[0])!r})
+sys.path.insert(0, {str(__file__.rsplit('/', 1)[0])!r})
+import numpy as np
+from test_gpu_sp import tv_problem
+from deftri import capi
+p = tv_problem(20000, seed=6)
+with capi.Context(0) as ctx:
+    ctx.set_plan('iterative')
+    ctx.set_linear_solver('pcg', 1e-12, 2)
+    ctx.upload(p)
+    s0 = [a.tobytes() for a in ctx.download()]
+    g, d = ctx.gradient()
+    r = ctx.solve_lm(5, analytic=True, max_trials=3)
+    s1 = [a.tobytes() for a in ctx.download()]
+print(json.dumps(dict(r=dict((k, r[k]) for k in ('trials_total', 'trials_rejected', 'pcg_fallbacks', 'pcg_trials',
+      'iterations', 'status', 'chi2_initial', 'chi2_final', 'lambda_final', 'cg_launches') if k in r),
+      same=s0 == s1, maxdiag=float(np.abs(d).max()))))
+"""
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=280)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = _json.loads(out.stdout.strip().splitlines()[-1])
+    r = res["r"]
+    assert r["trials_total"] == 3 and r["trials_rejected"] == 3, r
+    assert r["pcg_fallbacks"] == 3 and r["pcg_trials"] == 0
+    assert r["iterations"] == 1 and r["status"] == 1            # DEFTRI_STATUS_TERMINATE
+    assert r["chi2_final"] == r["chi2_initial"]
+    assert res["same"]
+    assert r["lambda_final"] == pytest.approx(1e-5 * res["maxdiag"] * 2.0 ** 6, rel=1e-12)
+
+
 def test_merged_chain_breakdown_then_solve():
     """A solve that breaks down inside the merged chain (a NaN in the right-hand side: p.Ap is NaN, so
     phase 2's workgroup 0 finds the breakdown while the other workgroups are running) fails loudly and
