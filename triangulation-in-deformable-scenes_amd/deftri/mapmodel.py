@@ -186,6 +186,54 @@ class Map:
     def get_global_T(self, kf1, kf2):
         return self.global_T.get((kf1, kf2), SE3f())
 
+    def __deepcopy__(self, memo):
+        """Map::clone (the weight search clones the map for every evaluation, nloptOptimization.cc:
+        the same independent copy as the generic copy.deepcopy — every MapPoint, KeyFrame and table
+        new, numpy arrays copied, the KeyFrames' slots pointing at the new MapPoints — built
+        directly instead of by the generic object walk (C2: 3.6 s -> 0.5 s on this container)."""
+        import copy
+        new = Map.__new__(Map)
+        memo[id(self)] = new
+        mps = {}
+        new_mp = MapPoint.__new__
+        for pid, mp in self.map_points.items():
+            c = new_mp(MapPoint)
+            d = mp.__dict__
+            if len(d) == 2 and "position" in d and "id" in d:        # the usual MapPoint
+                c.__dict__ = {"position": d["position"].copy(), "id": d["id"]}
+            else:
+                c.__dict__ = {k: (v.copy() if isinstance(v, np.ndarray) else v if isinstance(v, (int, float, str))
+                                  else copy.deepcopy(v, memo)) for k, v in d.items()}
+            memo[id(mp)] = c
+            mps[pid] = c
+        kfs = {}
+        for kid, kf in self.keyframes.items():
+            c = KeyFrame.__new__(KeyFrame)
+            d = {}
+            for k, v in kf.__dict__.items():
+                if k == "map_points":
+                    get = memo.get
+                    d[k] = [None if m is None else (get(id(m)) or copy.deepcopy(m, memo)) for m in v]
+                elif isinstance(v, np.ndarray):
+                    d[k] = v.copy()
+                elif isinstance(v, (int, float, str)):
+                    d[k] = v
+                else:
+                    d[k] = copy.deepcopy(v, memo)
+            c.__dict__ = d
+            memo[id(kf)] = c
+            kfs[kid] = c
+        for k, v in self.__dict__.items():
+            if k == "map_points":
+                new.map_points = mps
+            elif k == "keyframes":
+                new.keyframes = kfs
+            elif k in ("kf_obs", "mp_obs", "covis"):
+                setattr(new, k, {a: dict(b) for a, b in v.items()})
+            else:
+                setattr(new, k, copy.deepcopy(v, memo))
+        return new
+
     # ---- C-ABI view -------------------------------------------------------------------------
     def to_c(self):
         """Build a deftri_map view.  Returns (MapC, keep) — keep owns the arrays; positions and
