@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -148,13 +149,29 @@ void mesh_cot_weights(const std::vector<double> &pos, Mesh &M) {
         }
 }
 
-// open-addressing MapPoint id -> graph point index (ids are >= 0)
+// MapPoint id -> graph point index (ids are >= 0): a direct table when the ids fall in a range
+// at most a few times the number of points (the usual case: ORB-SLAM hands out ids from a counter),
+// open addressing otherwise
 struct IdIndex {
     std::vector<int64_t> key;
     std::vector<int32_t> val;
     uint64_t mask = 0;
     int64_t size = 0;
+    int64_t lo = 0, span = -1;                 // span >= 0: direct table over ids [lo, lo + span)
+    // ids in [id_lo, id_hi] (id_hi < id_lo: none); expect = the number of distinct ids
+    void init_range(int64_t id_lo, int64_t id_hi, int64_t expect) {
+        const int64_t n = id_hi >= id_lo ? id_hi - id_lo + 1 : 0;
+        if (n <= std::max<int64_t>(4 * expect, 1 << 16) && n < ((int64_t)1 << 31)) {
+            lo = id_lo;
+            span = n;
+            val.assign((size_t)n, -1);
+            key.clear();
+            return;
+        }
+        init(expect);
+    }
     void init(int64_t expect) {
+        span = -1;
         uint64_t cap = 16;
         while (cap < (uint64_t)std::max<int64_t>(expect, 8) * 2) cap <<= 1;
         key.assign(cap, -1);
@@ -164,6 +181,7 @@ struct IdIndex {
     }
     static uint64_t mix(uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdULL; x ^= x >> 33; return x; }
     int32_t *slot(int64_t id) {
+        if (span >= 0) return &val[(size_t)(id - lo)];   // init_range saw every id
         if ((uint64_t)(size + 1) * 2 > mask + 1) grow();
         uint64_t h = mix((uint64_t)id) & mask;
         while (key[h] != -1 && key[h] != id) h = (h + 1) & mask;
@@ -171,6 +189,7 @@ struct IdIndex {
         return &val[h];
     }
     int32_t get(int64_t id) const {
+        if (span >= 0) return id >= lo && id - lo < span ? val[(size_t)(id - lo)] : -1;
         uint64_t h = mix((uint64_t)id) & mask;
         while (key[h] != -1) {
             if (key[h] == id) return val[h];
@@ -417,6 +436,57 @@ bool map_ok(const deftri_map &map, std::string &err) {
 }
 }  // namespace
 
+// one pair's edge layout, fixed by the sequential pass of build_arap_graph
+struct PairEmit {
+    int a = 0, b = 0, q = 0, ns12 = 0;
+    int32_t c1 = 0, c2 = 0, s1 = 0, s2 = 0, rot_base = 0;
+    int64_t w_off = 0, n_obs = 0, n_arap = 0, obs_off = 0, arap_off = 0;
+    std::vector<int32_t> slot_pt;          // per slot: the graph points of (keyframe 1, keyframe 2)
+};
+
+// the reprojection (:765-812), depth (:816-856) and ARAP (:871-953) edges of one pair, written
+// into the pair's ranges; the same filters as the counting pass, so the counts agree
+void emit_pair_edges(const deftri_map &map, const PairEmit &pe, const GraphResult::MeshData &MD, double rep_weight,
+                     double info_dep, GraphResult &g) {
+    const deftri_keyframe &kf1 = map.keyframes[pe.b], &kf2 = map.keyframes[pe.a];
+    const int32_t *sp = pe.slot_pt.data();
+    const double *w = g.wcat.data() + pe.w_off;
+    int64_t r = 2 * pe.obs_off, e = pe.arap_off;
+    for (int mp = 0; mp < pe.ns12; mp++) {
+        if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
+        const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
+        if (o1 < 0 || o2 < 0) continue;
+        const int32_t p1 = sp[2 * (size_t)mp], p2 = sp[2 * (size_t)mp + 1];
+        const double base1 = (double)kf1.inv_sigma2[kf1.kp_octave[o1]], base2 = (double)kf2.inv_sigma2[kf2.kp_octave[o2]];
+        g.rep_point[r] = p1; g.rep_cam[r] = pe.c1;
+        g.rep_obs[2 * r] = (double)kf1.kp_uv[2 * o1]; g.rep_obs[2 * r + 1] = (double)kf1.kp_uv[2 * o1 + 1];
+        g.rep_base[r] = base1; g.rep_info[r] = base1 * rep_weight;
+        g.rep_point[r + 1] = p2; g.rep_cam[r + 1] = pe.c2;
+        g.rep_obs[2 * r + 2] = (double)kf2.kp_uv[2 * o2]; g.rep_obs[2 * r + 3] = (double)kf2.kp_uv[2 * o2 + 1];
+        g.rep_base[r + 1] = base2; g.rep_info[r + 1] = base2 * rep_weight;
+        g.dep_point[r] = p1; g.dep_scale[r] = pe.s1; g.dep_cam[r] = pe.c1;
+        g.dep_meas[r] = (double)kf1.depth[o1]; g.dep_info[r] = info_dep;
+        g.dep_point[r + 1] = p2; g.dep_scale[r + 1] = pe.s2; g.dep_cam[r + 1] = pe.c2;
+        g.dep_meas[r + 1] = (double)kf2.depth[o2]; g.dep_info[r + 1] = info_dep;
+        r += 2;
+        if (mp >= MD.n1) continue;
+        const int i = MD.inv[mp];
+        if (i < 0) continue;
+        for (int32_t k = MD.off[i]; k < MD.off[i + 1]; k++) {
+            const int j = MD.adj[k];
+            const int slot = MD.pos_idx[j];
+            if (slot >= pe.ns12 || kf1.point_id[slot] < 0 || kf2.point_id[slot] < 0) continue;
+            g.arap_pts[4 * e] = p1; g.arap_pts[4 * e + 1] = p2;
+            g.arap_pts[4 * e + 2] = sp[2 * (size_t)slot]; g.arap_pts[4 * e + 3] = sp[2 * (size_t)slot + 1];
+            g.arap_pair[e] = pe.q;
+            g.arap_rot[2 * e] = pe.rot_base + i; g.arap_rot[2 * e + 1] = pe.rot_base + j;
+            g.arap_w[e] = w[k];
+            g.arap_wk[e] = pe.w_off + k;
+            e++;
+        }
+    }
+}
+
 bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weight, float depth_error,
                       GraphResult &g, std::string &err, int pair_window, GraphDevice *gdev) {
     if (!map_ok(map, err)) return false;
@@ -462,13 +532,19 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 slots += std::min(map.keyframes[a].n_slots, map.keyframes[b].n_slots);
                 npairs++;
             }
-        pidx.init(2 * slots);
-        g.rep_point.reserve(2 * slots); g.rep_cam.reserve(2 * slots); g.rep_obs.reserve(4 * slots);
-        g.rep_info.reserve(2 * slots); g.rep_base.reserve(2 * slots);
-        g.dep_point.reserve(2 * slots); g.dep_scale.reserve(2 * slots); g.dep_cam.reserve(2 * slots);
-        g.dep_meas.reserve(2 * slots); g.dep_info.reserve(2 * slots);
-        g.arap_pts.reserve(4 * 6 * slots); g.arap_pair.reserve(6 * slots); g.arap_rot.reserve(2 * 6 * slots);
-        g.arap_w.reserve(6 * slots); g.rot.reserve(9 * slots);
+        // the range of the MapPoint ids the pairs can meet, and how many distinct ones at most
+        int64_t id_lo = INT64_MAX, id_hi = -1, nid = 0;
+        for (int a = 0; a < K; a++) {
+            const deftri_keyframe &f = map.keyframes[a];
+            for (int s = 0; s < f.n_slots; s++)
+                if (f.point_id[s] >= 0) {
+                    id_lo = std::min(id_lo, f.point_id[s]);
+                    id_hi = std::max(id_hi, f.point_id[s]);
+                    nid++;
+                }
+        }
+        pidx.init_range(id_lo, id_hi, std::min<int64_t>(nid, 2 * slots));
+        g.rot.reserve(9 * slots);
         g.point_mpid.reserve(2 * slots); g.points.reserve(6 * slots); g.point_orig.reserve(6 * slots);
         g.order_xy.reserve(4 * slots);
         (void)npairs;
@@ -523,6 +599,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         for (size_t i = 0; i < need.size(); i++)
             if (!kf1_mesh[need[i]]) { err = errs[i]; return false; }
     }
+    std::vector<PairEmit> emits;
     for (int a = 0; a < K; a++) {
         for (int b = a + 1; b < K; b++) {
             if (pair_window > 0 && b - a > pair_window) continue;
@@ -602,61 +679,39 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 return k;
             };
             // a slot's MapPoints are fixed within the pair: their graph indices are looked up once
-            // (creation order unchanged: a point is still created at its first encounter)
+            // (creation order unchanged: a point is still created at its first encounter). This pass
+            // creates the points in the reference's order, checks the observations and counts the
+            // pair's edges; the edges themselves are written afterwards, the pairs in parallel.
             const int ns12 = std::min(kf1.n_slots, kf2.n_slots);
-            std::vector<int32_t> slot_pt(2 * (size_t)ns12, -1);
-            auto slot_points = [&](int slot, int32_t &a1, int32_t &a2) {
-                int32_t *c = &slot_pt[2 * (size_t)slot];
+            emits.emplace_back();
+            PairEmit &pe = emits.back();
+            pe.a = a; pe.b = b; pe.q = q; pe.c1 = c1; pe.c2 = c2; pe.s1 = s1; pe.s2 = s2;
+            pe.rot_base = rot_base; pe.w_off = w_off; pe.ns12 = ns12;
+            pe.slot_pt.assign(2 * (size_t)ns12, -1);
+            auto slot_points = [&](int slot) {
+                int32_t *c = &pe.slot_pt[2 * (size_t)slot];
                 if (c[0] < 0) {
                     c[0] = add_point(kf1.point_id[slot], b, slot, slot);
                     c[1] = add_point(kf2.point_id[slot], a, slot, slot);
                 }
-                a1 = c[0];
-                a2 = c[1];
             };
-            const int nslots = kf1.n_slots;
-            for (int mp = 0; mp < nslots; mp++) {
-                if (mp >= kf2.n_slots) break;
-                const int64_t id1 = kf1.point_id[mp], id2 = kf2.point_id[mp];
-                if (id1 < 0 || id2 < 0) continue;
-                int32_t p1, p2;
-                slot_points(mp, p1, p2);
+            for (int mp = 0; mp < ns12; mp++) {
+                if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
+                slot_points(mp);
                 const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
                 if (o1 < 0 || o2 < 0) continue;
                 if (o1 >= kf1.n_obs || o2 >= kf2.n_obs) { err = "observation index out of range"; return false; }
                 const int32_t oc1 = kf1.kp_octave[o1], oc2 = kf2.kp_octave[o2];
                 if (oc1 < 0 || oc1 >= kf1.n_scales || oc2 < 0 || oc2 >= kf2.n_scales) { err = "keypoint octave out of range"; return false; }
-                // reprojection edges (:765-812)
-                const double base1 = (double)kf1.inv_sigma2[oc1], base2 = (double)kf2.inv_sigma2[oc2];
-                g.rep_point.push_back(p1); g.rep_cam.push_back(c1);
-                g.rep_obs.push_back((double)kf1.kp_uv[2 * o1]); g.rep_obs.push_back((double)kf1.kp_uv[2 * o1 + 1]);
-                g.rep_base.push_back(base1); g.rep_info.push_back(base1 * rep_weight);
-                g.rep_point.push_back(p2); g.rep_cam.push_back(c2);
-                g.rep_obs.push_back((double)kf2.kp_uv[2 * o2]); g.rep_obs.push_back((double)kf2.kp_uv[2 * o2 + 1]);
-                g.rep_base.push_back(base2); g.rep_info.push_back(base2 * rep_weight);
-                // depth edges (:816-856), simulated per-index depth
-                g.dep_point.push_back(p1); g.dep_scale.push_back(s1); g.dep_cam.push_back(c1);
-                g.dep_meas.push_back((double)kf1.depth[o1]); g.dep_info.push_back(info_dep);
-                g.dep_point.push_back(p2); g.dep_scale.push_back(s2); g.dep_cam.push_back(c2);
-                g.dep_meas.push_back((double)kf2.depth[o2]); g.dep_info.push_back(info_dep);
-                // ARAP edges (:871-953)
+                pe.n_obs++;
                 if (mp >= n1) continue;
                 const int i = inv[mp];
                 if (i < 0) continue;
-                for (int32_t k = M.off[i]; k < M.off[i + 1]; k++) {
-                    const int j = M.adj[k];
-                    const int slot = posIdx[j];
-                    if (slot >= kf1.n_slots || slot >= kf2.n_slots) continue;
-                    const int64_t j1 = kf1.point_id[slot], j2 = kf2.point_id[slot];
-                    if (j1 < 0 || j2 < 0) continue;
-                    int32_t pj1, pj2;
-                    slot_points(slot, pj1, pj2);
-                    g.arap_pts.push_back(p1); g.arap_pts.push_back(p2);
-                    g.arap_pts.push_back(pj1); g.arap_pts.push_back(pj2);
-                    g.arap_pair.push_back(q);
-                    g.arap_rot.push_back(rot_base + i); g.arap_rot.push_back(rot_base + j);
-                    g.arap_w.push_back(M.w[k]);
-                    g.arap_wk.push_back(w_off + k);
+                for (int32_t k = MD.off[i]; k < MD.off[i + 1]; k++) {
+                    const int slot = posIdx[MD.adj[k]];
+                    if (slot >= ns12 || kf1.point_id[slot] < 0 || kf2.point_id[slot] < 0) continue;
+                    slot_points(slot);
+                    pe.n_arap++;
                 }
             }
             rot_base += n1;
@@ -665,6 +720,26 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                              ms(t0, t1), M.ms_delaunay, ms(t1, t2), ms(t2, t3), gdev ? " device" : " host", gdev ? gdev->ms_last : 0.0,
                              ms(t3, tnow()));
         }
+    }
+    {
+        // the edges, each pair into its own range (the reference's order: pairs, then slots)
+        auto t0 = tnow();
+        int64_t nobs = 0, narap = 0;
+        for (PairEmit &pe : emits) {
+            pe.obs_off = nobs; pe.arap_off = narap;
+            nobs += pe.n_obs; narap += pe.n_arap;
+        }
+        g.rep_point.resize(2 * nobs); g.rep_cam.resize(2 * nobs); g.rep_obs.resize(4 * nobs);
+        g.rep_info.resize(2 * nobs); g.rep_base.resize(2 * nobs);
+        g.dep_point.resize(2 * nobs); g.dep_scale.resize(2 * nobs); g.dep_cam.resize(2 * nobs);
+        g.dep_meas.resize(2 * nobs); g.dep_info.resize(2 * nobs);
+        g.arap_pts.resize(4 * narap); g.arap_pair.resize(narap); g.arap_rot.resize(2 * narap);
+        g.arap_w.resize(narap); g.arap_wk.resize(narap);
+        auto t1 = tnow();
+        parallel_for((int)emits.size(), 1, [&](int lo, int hi) {
+            for (int e = lo; e < hi; e++) emit_pair_edges(map, emits[e], *g.meshes[e].mesh, rep_weight, info_dep, g);
+        });
+        if (timing) std::fprintf(stderr, "[deftri graph] edges written: %.1f ms (arrays %.1f)\n", ms(t0, tnow()), ms(t0, t1));
     }
     deftri_problem_desc &d = g.desc;
     d = deftri_problem_desc{};
@@ -701,7 +776,11 @@ void writeback_arap(deftri_map &map, const GraphResult &g, const std::vector<dou
         if (g.kf_scale[k] >= 0) map.keyframes[k].depth_scale = scales[g.kf_scale[k]];
     // points: fp32 writeback + sum ||p_old - p_new|| (:974-990)
     IdIndex pidx;
-    pidx.init((int64_t)g.point_mpid.size());
+    {
+        int64_t id_lo = INT64_MAX, id_hi = -1;
+        for (int64_t id : g.point_mpid) { id_lo = std::min(id_lo, id); id_hi = std::max(id_hi, id); }
+        pidx.init_range(id_lo, id_hi, (int64_t)g.point_mpid.size());
+    }
     for (size_t i = 0; i < g.point_mpid.size(); i++) *pidx.slot(g.point_mpid[i]) = (int32_t)i;
     double upd = 0;
     for (size_t i = 0; i < g.point_mpid.size(); i++) {

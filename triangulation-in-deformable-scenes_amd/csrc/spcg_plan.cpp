@@ -14,29 +14,12 @@
 #include <numeric>
 #include <thread>
 
+#include "host_threads.h"
 #include "spcg.h"
 
 namespace deftri {
 
 namespace {
-
-// [0, n) in contiguous chunks on up to 16 host threads (DEFTRI_HOST_THREADS); f(chunk, lo, hi).
-// The plan's parallel passes write disjoint ranges or per-chunk counters merged in chunk order, so
-// the plan does not depend on the split
-template <class F>
-int chunked(int64_t n, int64_t min_chunk, F f) {
-    static const int env_t = std::getenv("DEFTRI_HOST_THREADS") ? std::atoi(std::getenv("DEFTRI_HOST_THREADS")) : 0;
-    const int hw = env_t > 0 ? env_t : (int)std::max(1u, std::thread::hardware_concurrency());
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, 16, n / std::max<int64_t>(min_chunk, 1)}));
-    if (nt <= 1) { f(0, (int64_t)0, n); return 1; }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; t++) {
-        const int64_t b = n * t / nt, e = n * (t + 1) / nt;
-        th.emplace_back([=, &f] { f(t, b, e); });
-    }
-    for (auto &x : th) x.join();
-    return nt;
-}
 
 // stable counting sort of `ids` by key(id) in [0, nkeys)
 template <class Key>
@@ -46,6 +29,37 @@ void counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
     for (int64_t k = 0; k < nkeys; k++) cnt[k + 1] += cnt[k];
     std::vector<int32_t> out(ids.size());
     for (int32_t i : ids) out[(size_t)cnt[(size_t)key(i)]++] = i;
+    ids.swap(out);
+}
+
+// the same stable counting sort over chunks of `ids` on host threads: per-chunk key counts,
+// offsets in (key, chunk) order, every chunk scatters its ids in order (a stable sort's output is
+// unique, so the result does not depend on the chunking)
+template <class Key>
+void par_counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
+    const int64_t n = (int64_t)ids.size();
+    const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, n / (1 << 18)));
+    if (nch <= 1) { counting_sort(ids, nkeys, key); return; }
+    std::vector<std::vector<int32_t>> cnt((size_t)nch);
+    auto lo_of = [&](int64_t c) { return n * c / nch; };
+    chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; c++) {
+            cnt[c].assign((size_t)nkeys, 0);
+            for (int64_t i = lo_of(c); i < lo_of(c + 1); i++) cnt[c][(size_t)key(ids[i])]++;
+        }
+    });
+    int64_t run = 0;
+    for (int64_t k = 0; k < nkeys; k++)
+        for (int64_t c = 0; c < nch; c++) {
+            const int32_t v = cnt[c][k];
+            cnt[c][k] = (int32_t)run;
+            run += v;
+        }
+    std::vector<int32_t> out((size_t)n);
+    chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+        for (int64_t c = c0; c < c1; c++)
+            for (int64_t i = lo_of(c); i < lo_of(c + 1); i++) out[(size_t)cnt[c][(size_t)key(ids[i])]++] = ids[i];
+    });
     ids.swap(out);
 }
 
@@ -144,14 +158,15 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
 
     stage("3 rows");
     // 4. work-balanced contiguous group ranges per rank: weight of a row = 2 + its ARAP incidences
-    std::vector<int64_t> rw(P, 2);
-    for (int64_t e = 0; e < 4 * E; e++) rw[row[ap[e]]]++;
-    for (int64_t e = 0; e < R; e++) rw[row[d.rep_point[e]]]++;
-    for (int64_t e = 0; e < D; e++) rw[row[d.dep_point[e]]]++;
-    const double total = std::accumulate(rw.begin(), rw.end(), 0.0);
+    //    (one rank: the whole range, no weights needed)
     H.rank_row_begin.assign(nranks + 1, P);
     H.rank_row_begin[0] = 0;
-    {
+    if (nranks > 1) {
+        std::vector<int64_t> rw(P, 2);
+        for (int64_t e = 0; e < 4 * E; e++) rw[row[ap[e]]]++;
+        for (int64_t e = 0; e < R; e++) rw[row[d.rep_point[e]]]++;
+        for (int64_t e = 0; e < D; e++) rw[row[d.dep_point[e]]]++;
+        const double total = std::accumulate(rw.begin(), rw.end(), 0.0);
         double cum = 0;
         int next = 1;
         for (int32_t r = 0; r < P && next < nranks; r++) {
@@ -200,14 +215,19 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     stage("4b slot-count sort");
     // 5. local ARAP edges: owned (point 0 here) first, then halo-only; each by (pair, Morton row of point 0)
     std::vector<int32_t> owned_e, halo_e;
-    for (int64_t e = 0; e < E; e++) {
-        const int32_t r0 = row[ap[4 * e]];
-        if (own(r0)) owned_e.push_back((int32_t)e);
-        else if (own(row[ap[4 * e + 1]]) || own(row[ap[4 * e + 2]]) || own(row[ap[4 * e + 3]])) halo_e.push_back((int32_t)e);
+    if (nranks == 1) {
+        owned_e.resize((size_t)E);
+        std::iota(owned_e.begin(), owned_e.end(), 0);
+    } else {
+        for (int64_t e = 0; e < E; e++) {
+            const int32_t r0 = row[ap[4 * e]];
+            if (own(r0)) owned_e.push_back((int32_t)e);
+            else if (own(row[ap[4 * e + 1]]) || own(row[ap[4 * e + 2]]) || own(row[ap[4 * e + 3]])) halo_e.push_back((int32_t)e);
+        }
     }
     for (auto *lst : {&owned_e, &halo_e}) {
-        counting_sort(*lst, P, [&](int32_t e) { return mrow[ap[4 * (int64_t)e]]; });
-        counting_sort(*lst, std::max(Q, 1), [&](int32_t e) { return d.arap_pair[e]; });
+        par_counting_sort(*lst, P, [&](int32_t e) { return mrow[ap[4 * (int64_t)e]]; });
+        par_counting_sort(*lst, std::max(Q, 1), [&](int32_t e) { return d.arap_pair[e]; });
     }
     H.n_arap_owned = (int32_t)owned_e.size();
     H.arap_ids = owned_e;
@@ -230,10 +250,17 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
 
     stage("5 local ARAP edges");
     // 6. the own rows' reprojection / depth edges, by row
-    for (int64_t e = 0; e < R; e++) if (own(row[d.rep_point[e]])) H.rep_ids.push_back((int32_t)e);
-    for (int64_t e = 0; e < D; e++) if (own(row[d.dep_point[e]])) H.dep_ids.push_back((int32_t)e);
-    counting_sort(H.rep_ids, P, [&](int32_t e) { return row[d.rep_point[e]]; });
-    counting_sort(H.dep_ids, P, [&](int32_t e) { return row[d.dep_point[e]]; });
+    if (nranks == 1) {
+        H.rep_ids.resize((size_t)R);
+        std::iota(H.rep_ids.begin(), H.rep_ids.end(), 0);
+        H.dep_ids.resize((size_t)D);
+        std::iota(H.dep_ids.begin(), H.dep_ids.end(), 0);
+    } else {
+        for (int64_t e = 0; e < R; e++) if (own(row[d.rep_point[e]])) H.rep_ids.push_back((int32_t)e);
+        for (int64_t e = 0; e < D; e++) if (own(row[d.dep_point[e]])) H.dep_ids.push_back((int32_t)e);
+    }
+    par_counting_sort(H.rep_ids, P, [&](int32_t e) { return row[d.rep_point[e]]; });
+    par_counting_sort(H.dep_ids, P, [&](int32_t e) { return row[d.dep_point[e]]; });
     H.rep_off.assign(nown + 1, 0);
     H.dep_off.assign(nown + 1, 0);
     for (int32_t e : H.rep_ids) H.rep_off[row[d.rep_point[e]] - lo_r + 1]++;
@@ -469,6 +496,25 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                      + (double)H.inc.size() * (4 + 8 + jb / 6)           // slot index, s, packed J slice
                      + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
+    static const bool digest = std::getenv("DEFTRI_PLAN_DIGEST") != nullptr;
+    if (digest) {
+        // FNV-1a over every plan array: a rewrite of the build is checked against the previous one
+        uint64_t h = 1469598103934665603ULL;
+        auto mix = [&](const void *v, size_t n) {
+            const unsigned char *c = (const unsigned char *)v;
+            for (size_t i = 0; i < n; i++) { h ^= c[i]; h *= 1099511628211ULL; }
+        };
+        auto vec = [&](const auto &x) { mix(x.data(), x.size() * sizeof(x[0])); };
+        vec(H.row_of_point); vec(H.point_of_row); vec(H.rank_row_begin); vec(H.arap_ids); vec(H.rep_ids);
+        vec(H.dep_ids); vec(H.rot_ids); vec(H.arap_rot_local); vec(H.blk); vec(H.hv_blk); vec(H.hv_blk_off);
+        vec(H.dperm); vec(H.inc_off); vec(H.inc); vec(H.rep_off); vec(H.dep_off); vec(H.rowmap); vec(H.woff);
+        vec(H.wsplit); vec(H.pmap); vec(H.pidx);
+        for (const auto &x : H.send_rows) vec(x);
+        for (const auto &x : H.recv_rows) vec(x);
+        const int64_t sc[4] = {H.lo, H.hi, H.n_arap_owned, H.halo_rows};
+        mix(sc, sizeof(sc));
+        std::fprintf(stderr, "[deftri plan] digest %016llx\n", (unsigned long long)h);
+    }
     return true;
 }
 

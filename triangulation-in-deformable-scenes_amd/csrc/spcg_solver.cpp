@@ -25,6 +25,7 @@
 #include <cstring>
 #include <limits>
 
+#include "host_threads.h"
 #include "spcg.h"
 #include "ticket.h"
 
@@ -125,9 +126,12 @@ int SpSolver::hand_off_timeout() {
 // a structurally identical problem can change
 void SpSolver::gather_values(const deftri_problem_desc &d, SpValues &v) const {
     const int32_t NP = d.n_points, Q = d.n_pairs, S = d.n_scales, C = d.n_cams;
+    // (the long gathers on host threads: disjoint output ranges)
     v.pts.resize(3 * (size_t)NP);
-    for (int32_t r = 0; r < NP; r++)
-        for (int c = 0; c < 3; c++) v.pts[3 * (size_t)r + c] = d.points[3 * (size_t)H.point_of_row[r] + c];
+    chunked(NP, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t r = lo; r < hi; r++)
+            for (int c = 0; c < 3; c++) v.pts[3 * (size_t)r + c] = d.points[3 * (size_t)H.point_of_row[r] + c];
+    });
     v.tg.assign(d.tg, d.tg + 7 * (size_t)Q);
     v.sc.assign(d.scales, d.scales + S);
     for (int32_t q = 0; q < Q; q++) quat_norm(&v.tg[7 * (size_t)q]);
@@ -137,15 +141,22 @@ void SpSolver::gather_values(const deftri_problem_desc &d, SpValues &v) const {
     v.kb8.assign(d.cam_kb8, d.cam_kb8 + 8 * (size_t)C);
     const size_t nr = H.rep_ids.size(), nd = H.dep_ids.size(), nloc = H.arap_ids.size();
     v.ro.resize(2 * nr); v.ri.resize(nr); v.dm.resize(nd); v.di.resize(nd); v.aw.resize(nloc);
-    for (size_t j = 0; j < nr; j++) {
-        const int32_t e = H.rep_ids[j];
-        v.ro[2 * j] = d.rep_obs[2 * (size_t)e]; v.ro[2 * j + 1] = d.rep_obs[2 * (size_t)e + 1]; v.ri[j] = d.rep_info[e];
-    }
-    for (size_t j = 0; j < nd; j++) { const int32_t e = H.dep_ids[j]; v.dm[j] = d.dep_meas[e]; v.di[j] = d.dep_info[e]; }
-    for (size_t le = 0; le < nloc; le++) v.aw[le] = d.arap_w[H.arap_ids[le]];
+    chunked((int64_t)nr, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t j = lo; j < hi; j++) {
+            const int32_t e = H.rep_ids[j];
+            v.ro[2 * j] = d.rep_obs[2 * (size_t)e]; v.ro[2 * j + 1] = d.rep_obs[2 * (size_t)e + 1]; v.ri[j] = d.rep_info[e];
+        }
+    });
+    chunked((int64_t)nd, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t j = lo; j < hi; j++) { const int32_t e = H.dep_ids[j]; v.dm[j] = d.dep_meas[e]; v.di[j] = d.dep_info[e]; }
+    });
+    chunked((int64_t)nloc, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t le = lo; le < hi; le++) v.aw[le] = d.arap_w[H.arap_ids[le]];
+    });
     v.rot.resize(9 * H.rot_ids.size());
-    for (size_t k = 0; k < H.rot_ids.size(); k++)
-        std::memcpy(&v.rot[9 * k], d.rot + 9 * (size_t)H.rot_ids[k], 9 * sizeof(double));
+    chunked((int64_t)H.rot_ids.size(), 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; k++) std::memcpy(&v.rot[9 * k], d.rot + 9 * (size_t)H.rot_ids[k], 9 * sizeof(double));
+    });
     v.parea.assign(d.pair_area, d.pair_area + Q);
     v.pinfo.assign(d.pair_info, d.pair_info + Q);
 }
@@ -203,17 +214,23 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     // the rank's edges: structure (rows, cameras, scales, pairs) in the plan's numbering
     const size_t nr = H.rep_ids.size(), nd = H.dep_ids.size();
     std::vector<int32_t> rp(nr), rc(nr), dp(nd), ds(nd), dc(nd);
-    for (size_t j = 0; j < nr; j++) { const int32_t e = H.rep_ids[j]; rp[j] = H.row_of_point[d.rep_point[e]]; rc[j] = d.rep_cam[e]; }
-    for (size_t j = 0; j < nd; j++) {
-        const int32_t e = H.dep_ids[j];
-        dp[j] = H.row_of_point[d.dep_point[e]]; ds[j] = d.dep_scale[e]; dc[j] = d.dep_cam[e];
-    }
+    chunked((int64_t)nr, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t j = lo; j < hi; j++) { const int32_t e = H.rep_ids[j]; rp[j] = H.row_of_point[d.rep_point[e]]; rc[j] = d.rep_cam[e]; }
+    });
+    chunked((int64_t)nd, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t j = lo; j < hi; j++) {
+            const int32_t e = H.dep_ids[j];
+            dp[j] = H.row_of_point[d.dep_point[e]]; ds[j] = d.dep_scale[e]; dc[j] = d.dep_cam[e];
+        }
+    });
     std::vector<int32_t> apts(4 * (size_t)nloc), apair(nloc);
-    for (int64_t le = 0; le < nloc; le++) {
-        const int64_t e = H.arap_ids[le];
-        for (int k = 0; k < 4; k++) apts[4 * le + k] = H.row_of_point[d.arap_pts[4 * e + k]];
-        apair[le] = d.arap_pair[e];
-    }
+    chunked(nloc, 1 << 16, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t le = lo; le < hi; le++) {
+            const int64_t e = H.arap_ids[le];
+            for (int k = 0; k < 4; k++) apts[4 * le + k] = H.row_of_point[d.arap_pts[4 * e + k]];
+            apair[le] = d.arap_pair[e];
+        }
+    });
     std::vector<double> &ro = v.ro, &ri = v.ri, &dm = v.dm, &di = v.di, &aw = v.aw, &rot = v.rot, &parea = v.parea,
                         &pinfo = v.pinfo;
     int rc_;
