@@ -442,17 +442,20 @@ struct PairEmit {
     int32_t c1 = 0, c2 = 0, s1 = 0, s2 = 0, rot_base = 0;
     int64_t w_off = 0, n_obs = 0, n_arap = 0, obs_off = 0, arap_off = 0;
     std::vector<int32_t> slot_pt;          // per slot: the graph points of (keyframe 1, keyframe 2)
+    std::vector<int64_t> chunk_obs, chunk_arap;   // the counts before each kEmitChunk-slot chunk
 };
+constexpr int kEmitChunk = 1 << 14;
 
 // the reprojection (:765-812), depth (:816-856) and ARAP (:871-953) edges of one pair, written
 // into the pair's ranges; the same filters as the counting pass, so the counts agree
-void emit_pair_edges(const deftri_map &map, const PairEmit &pe, const GraphResult::MeshData &MD, double rep_weight,
+void emit_pair_edges(const deftri_map &map, const PairEmit &pe, int chunk, const GraphResult::MeshData &MD, double rep_weight,
                      double info_dep, GraphResult &g) {
     const deftri_keyframe &kf1 = map.keyframes[pe.b], &kf2 = map.keyframes[pe.a];
     const int32_t *sp = pe.slot_pt.data();
     const double *w = g.wcat.data() + pe.w_off;
-    int64_t r = 2 * pe.obs_off, e = pe.arap_off;
-    for (int mp = 0; mp < pe.ns12; mp++) {
+    int64_t r = 2 * (pe.obs_off + pe.chunk_obs[chunk]), e = pe.arap_off + pe.chunk_arap[chunk];
+    const int mp1 = std::min(pe.ns12, (chunk + 1) * kEmitChunk);
+    for (int mp = chunk * kEmitChunk; mp < mp1; mp++) {
         if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
         const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
         if (o1 < 0 || o2 < 0) continue;
@@ -518,7 +521,21 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         // rc 1: a pair's triangulation or vector map changed — the full build below
     }
     const int64_t hits = g.memo_hits, shits = g.struct_hits;
+    // the edge arrays keep their storage across rebuilds (deformationOptimization's rounds): the
+    // pages are already mapped, so refilling them costs no page faults
+    auto keep = [](auto &dst, auto &src) { dst.swap(src); dst.clear(); };
+    GraphResult old;
+    keep(old.rep_point, g.rep_point); keep(old.rep_cam, g.rep_cam); keep(old.rep_obs, g.rep_obs);
+    keep(old.rep_info, g.rep_info); keep(old.rep_base, g.rep_base); keep(old.dep_point, g.dep_point);
+    keep(old.dep_scale, g.dep_scale); keep(old.dep_cam, g.dep_cam); keep(old.dep_meas, g.dep_meas);
+    keep(old.dep_info, g.dep_info); keep(old.arap_pts, g.arap_pts); keep(old.arap_pair, g.arap_pair);
+    keep(old.arap_rot, g.arap_rot); keep(old.arap_w, g.arap_w); keep(old.arap_wk, g.arap_wk);
     g = GraphResult();
+    keep(g.rep_point, old.rep_point); keep(g.rep_cam, old.rep_cam); keep(g.rep_obs, old.rep_obs);
+    keep(g.rep_info, old.rep_info); keep(g.rep_base, old.rep_base); keep(g.dep_point, old.dep_point);
+    keep(g.dep_scale, old.dep_scale); keep(g.dep_cam, old.dep_cam); keep(g.dep_meas, old.dep_meas);
+    keep(g.dep_info, old.dep_info); keep(g.arap_pts, old.arap_pts); keep(g.arap_pair, old.arap_pair);
+    keep(g.arap_rot, old.arap_rot); keep(g.arap_w, old.arap_w); keep(g.arap_wk, old.arap_wk);
     g.memo_hits = hits;
     g.struct_hits = shits;
     const int K = map.n_keyframes;
@@ -696,6 +713,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 }
             };
             for (int mp = 0; mp < ns12; mp++) {
+                if (mp % kEmitChunk == 0) { pe.chunk_obs.push_back(pe.n_obs); pe.chunk_arap.push_back(pe.n_arap); }
                 if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
                 slot_points(mp);
                 const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
@@ -736,8 +754,14 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         g.arap_pts.resize(4 * narap); g.arap_pair.resize(narap); g.arap_rot.resize(2 * narap);
         g.arap_w.resize(narap); g.arap_wk.resize(narap);
         auto t1 = tnow();
-        parallel_for((int)emits.size(), 1, [&](int lo, int hi) {
-            for (int e = lo; e < hi; e++) emit_pair_edges(map, emits[e], *g.meshes[e].mesh, rep_weight, info_dep, g);
+        std::vector<std::pair<int, int>> tasks;       // (pair, slot chunk)
+        for (size_t e = 0; e < emits.size(); e++)
+            for (int c = 0; c < (int)emits[e].chunk_obs.size(); c++) tasks.emplace_back((int)e, c);
+        parallel_for((int)tasks.size(), 1, [&](int lo, int hi) {
+            for (int t = lo; t < hi; t++) {
+                const int e = tasks[t].first;
+                emit_pair_edges(map, emits[e], tasks[t].second, *g.meshes[e].mesh, rep_weight, info_dep, g);
+            }
         });
         if (timing) std::fprintf(stderr, "[deftri graph] edges written: %.1f ms (arrays %.1f)\n", ms(t0, tnow()), ms(t0, t1));
     }

@@ -2236,11 +2236,20 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
                              int32_t n_iterations, double *optimization_update, deftri_report *report) {
     (void)global_weight; (void)alpha; (void)beta;   // stored but unused by the reference edges
     if (!ctx || !map) return DEFTRI_E_ARG;
+    static const bool timing = std::getenv("DEFTRI_CALL_TIMING") != nullptr;   // stage times of the call
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    };
     std::string err;
     if (!build_arap_graph(*map, rep_weight, arap_weight, depth_error, ctx->graph, err, ctx->pair_window, graph_device(ctx)))
         return fail(ctx, DEFTRI_E_GRAPH, err);
+    const double ms_graph = ms_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
     int rc = deftri_problem_upload(ctx, &ctx->graph.desc);
     if (rc) return rc;
+    const double ms_upload = ms_since(t1);
+    const auto t2 = std::chrono::steady_clock::now();
     deftri_lm_params prm{};
     prm.n_iterations = n_iterations;
     prm.max_trials = 10;
@@ -2248,11 +2257,16 @@ int deftri_arap_optimization(deftri_ctx *ctx, deftri_map *map, double rep_weight
     prm.analytic_jacobians = ctx->analytic_jac;   // 0 (default): g2o numeric ARAP/depth Jacobians, as the reference
     rc = deftri_solve_lm(ctx, &prm, report);
     if (rc) return rc;
+    const double ms_lm = ms_since(t2);
+    const auto t3 = std::chrono::steady_clock::now();
     const GraphResult &g = ctx->graph;
     std::vector<double> pts(3 * (size_t)g.desc.n_points), sc(g.desc.n_scales), tg(7 * (size_t)g.desc.n_pairs);
     rc = deftri_download(ctx, pts.data(), sc.data(), tg.data());
     if (rc) return rc;
     writeback_arap(*map, g, pts, sc, tg, optimization_update);
+    if (timing)
+        std::fprintf(stderr, "[deftri call] graph %.1f ms, upload %.1f, LM %.1f, download + write-back %.1f, total %.1f\n", ms_graph,
+                     ms_upload, ms_lm, ms_since(t3), ms_since(t0));
     return 0;
 }
 

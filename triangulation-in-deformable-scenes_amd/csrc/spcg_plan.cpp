@@ -37,6 +37,7 @@ void counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
 // unique, so the result does not depend on the chunking)
 template <class Key>
 void par_counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
+    if (nkeys <= 1) return;                   // one key: the stable order is the input order
     const int64_t n = (int64_t)ids.size();
     const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, n / (1 << 18)));
     if (nch <= 1) { counting_sort(ids, nkeys, key); return; }
