@@ -227,3 +227,27 @@ def test_next_round_fast_path_is_a_full_build(n, seed, k):
                 order0 = pa.order_xy
             m = m2
             p0 = pa
+
+
+@pytest.mark.parametrize("case", ["octave_first", "obs_only"])
+def test_graph_observation_errors_first_pair_wins(host, case):
+    """A bad observation index or keypoint octave fails the build (the reference would read out of
+    bounds): the pairs' slot scans run in parallel, and the error reported is the one the sequential
+    walk meets first — the earliest pair's first bad slot."""
+    m = sim.multi_view_arrays(n=200, k=4, seed=2)
+
+    class Corrupted:
+        def to_c(self):
+            mc, keep = m.to_c()
+            last = mc.keyframes[mc.n_keyframes - 1]     # only in pairs (a, K-1): after pair (0, 1)
+            last.obs_index[3] = last.n_obs + 3
+            if case == "octave_first":
+                first = mc.keyframes[0]                  # in pair (0, 1), the first pair
+                first.kp_octave[first.obs_index[7]] = 99
+            return mc, keep
+
+    with pytest.raises(capi.DeftriError) as e:
+        host.build_graph(Corrupted(), 1.0, 1e7, np.float32(0.3))
+    want = "keypoint octave out of range" if case == "octave_first" else "observation index out of range"
+    assert want in str(e.value)
+    host.build_graph(m, 1.0, 1e7, np.float32(0.3))      # the context builds a good map afterwards

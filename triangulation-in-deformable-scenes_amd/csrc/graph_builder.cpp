@@ -443,8 +443,41 @@ struct PairEmit {
     int64_t w_off = 0, n_obs = 0, n_arap = 0, obs_off = 0, arap_off = 0;
     std::vector<int32_t> slot_pt;          // per slot: the graph points of (keyframe 1, keyframe 2)
     std::vector<int64_t> chunk_obs, chunk_arap;   // the counts before each kEmitChunk-slot chunk
+    std::vector<int32_t> enc;              // the slots in the order the pair meets them
 };
 constexpr int kEmitChunk = 1 << 14;
+
+// one pair's slot walk (:765-953's loop): the observation checks, the edge counts per slot chunk and
+// the first-encounter order of the slots (a slot with both MapPoints, then its ARAP neighbours)
+void scan_pair(const deftri_map &map, PairEmit &pe, const GraphResult::MeshData &MD, std::string &err) {
+    const deftri_keyframe &kf1 = map.keyframes[pe.b], &kf2 = map.keyframes[pe.a];
+    const int ns12 = pe.ns12;
+    std::vector<uint8_t> seen((size_t)ns12, 0);
+    pe.enc.reserve((size_t)ns12);
+    auto meet = [&](int slot) {
+        if (!seen[slot]) { seen[slot] = 1; pe.enc.push_back(slot); }
+    };
+    for (int mp = 0; mp < ns12; mp++) {
+        if (mp % kEmitChunk == 0) { pe.chunk_obs.push_back(pe.n_obs); pe.chunk_arap.push_back(pe.n_arap); }
+        if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
+        meet(mp);
+        const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
+        if (o1 < 0 || o2 < 0) continue;
+        if (o1 >= kf1.n_obs || o2 >= kf2.n_obs) { err = "observation index out of range"; return; }
+        const int32_t oc1 = kf1.kp_octave[o1], oc2 = kf2.kp_octave[o2];
+        if (oc1 < 0 || oc1 >= kf1.n_scales || oc2 < 0 || oc2 >= kf2.n_scales) { err = "keypoint octave out of range"; return; }
+        pe.n_obs++;
+        if (mp >= MD.n1) continue;
+        const int i = MD.inv[mp];
+        if (i < 0) continue;
+        for (int32_t k = MD.off[i]; k < MD.off[i + 1]; k++) {
+            const int slot = MD.pos_idx[MD.adj[k]];
+            if (slot >= ns12 || kf1.point_id[slot] < 0 || kf2.point_id[slot] < 0) continue;
+            meet(slot);
+            pe.n_arap++;
+        }
+    }
+}
 
 // the reprojection (:765-812), depth (:816-856) and ARAP (:871-953) edges of one pair, written
 // into the pair's ranges; the same filters as the counting pass, so the counts agree
@@ -681,63 +714,57 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             g.pair_info.push_back(arap_weight * std::pow((double)M.T, 2));
             g.pair_kf1.push_back(b); g.pair_kf2.push_back(a);
             g.pair_T.push_back(M.T); g.pair_hull.push_back(M.hull);
-            auto add_point = [&](int64_t id, int kf, int slot, int ord_slot) {
-                int32_t *v = pidx.slot(id);
-                if (*v >= 0) return *v;
-                const int32_t k = (int32_t)g.point_mpid.size();
-                *v = k;
-                g.point_mpid.push_back(id);
-                const float *p = map.keyframes[kf].point_pos + 3 * (size_t)slot;
-                for (int c = 0; c < 3; c++) { g.points.push_back((double)p[c]); g.point_orig.push_back(p[c]); }
-                g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot]);
-                g.order_xy.push_back((double)kf1.point_pos[3 * ord_slot + 1]);
-                g.point_kf.push_back(kf); g.point_slot.push_back(slot);
-                g.order_kf.push_back(b); g.order_slot.push_back(ord_slot);
-                return k;
-            };
-            // a slot's MapPoints are fixed within the pair: their graph indices are looked up once
-            // (creation order unchanged: a point is still created at its first encounter). This pass
-            // creates the points in the reference's order, checks the observations and counts the
-            // pair's edges; the edges themselves are written afterwards, the pairs in parallel.
-            const int ns12 = std::min(kf1.n_slots, kf2.n_slots);
+            // the pair's slots are scanned after this loop, the pairs in parallel
             emits.emplace_back();
             PairEmit &pe = emits.back();
             pe.a = a; pe.b = b; pe.q = q; pe.c1 = c1; pe.c2 = c2; pe.s1 = s1; pe.s2 = s2;
-            pe.rot_base = rot_base; pe.w_off = w_off; pe.ns12 = ns12;
-            pe.slot_pt.assign(2 * (size_t)ns12, -1);
-            auto slot_points = [&](int slot) {
-                int32_t *c = &pe.slot_pt[2 * (size_t)slot];
-                if (c[0] < 0) {
-                    c[0] = add_point(kf1.point_id[slot], b, slot, slot);
-                    c[1] = add_point(kf2.point_id[slot], a, slot, slot);
-                }
-            };
-            for (int mp = 0; mp < ns12; mp++) {
-                if (mp % kEmitChunk == 0) { pe.chunk_obs.push_back(pe.n_obs); pe.chunk_arap.push_back(pe.n_arap); }
-                if (kf1.point_id[mp] < 0 || kf2.point_id[mp] < 0) continue;
-                slot_points(mp);
-                const int32_t o1 = kf1.obs_index[mp], o2 = kf2.obs_index[mp];
-                if (o1 < 0 || o2 < 0) continue;
-                if (o1 >= kf1.n_obs || o2 >= kf2.n_obs) { err = "observation index out of range"; return false; }
-                const int32_t oc1 = kf1.kp_octave[o1], oc2 = kf2.kp_octave[o2];
-                if (oc1 < 0 || oc1 >= kf1.n_scales || oc2 < 0 || oc2 >= kf2.n_scales) { err = "keypoint octave out of range"; return false; }
-                pe.n_obs++;
-                if (mp >= n1) continue;
-                const int i = inv[mp];
-                if (i < 0) continue;
-                for (int32_t k = MD.off[i]; k < MD.off[i + 1]; k++) {
-                    const int slot = posIdx[MD.adj[k]];
-                    if (slot >= ns12 || kf1.point_id[slot] < 0 || kf2.point_id[slot] < 0) continue;
-                    slot_points(slot);
-                    pe.n_arap++;
-                }
-            }
+            pe.rot_base = rot_base; pe.w_off = w_off; pe.ns12 = std::min(kf1.n_slots, kf2.n_slots);
             rot_base += n1;
             if (timing)
                 std::fprintf(stderr, "[deftri graph] pair %d: mesh %.1f ms (delaunay %.1f), vector map %.1f, computeR %.1f%s (kernel %.3f), edges %.1f\n", q,
                              ms(t0, t1), M.ms_delaunay, ms(t1, t2), ms(t2, t3), gdev ? " device" : " host", gdev ? gdev->ms_last : 0.0,
                              ms(t3, tnow()));
         }
+    }
+    {
+        // (i) every pair's slot scan on its own host thread: the observation checks, the pair's edge
+        //     counts per slot chunk and the order in which it meets its slots (its ARAP neighbours
+        //     included) — the order the reference creates their points in
+        auto ts = tnow();
+        std::vector<std::string> perr(emits.size());
+        parallel_for((int)emits.size(), 1, [&](int lo, int hi) {
+            for (int e = lo; e < hi; e++) scan_pair(map, emits[e], *g.meshes[e].mesh, perr[e]);
+        });
+        for (size_t e = 0; e < emits.size(); e++)
+            if (!perr[e].empty()) { err = perr[e]; return false; }   // the first pair's first error
+        // (ii) the points, created in the pairs' order, each at its first encounter; a slot's two
+        //      MapPoints are fixed within the pair, so their graph indices are looked up once
+        auto add_point = [&](int64_t id, int kf, int slot, int ord_kf, int ord_slot) {
+            int32_t *v = pidx.slot(id);
+            if (*v >= 0) return *v;
+            const int32_t k = (int32_t)g.point_mpid.size();
+            *v = k;
+            g.point_mpid.push_back(id);
+            const float *p = map.keyframes[kf].point_pos + 3 * (size_t)slot;
+            for (int c = 0; c < 3; c++) { g.points.push_back((double)p[c]); g.point_orig.push_back(p[c]); }
+            const float *o = map.keyframes[ord_kf].point_pos + 3 * (size_t)ord_slot;
+            g.order_xy.push_back((double)o[0]);
+            g.order_xy.push_back((double)o[1]);
+            g.point_kf.push_back(kf); g.point_slot.push_back(slot);
+            g.order_kf.push_back(ord_kf); g.order_slot.push_back(ord_slot);
+            return k;
+        };
+        for (PairEmit &pe : emits) {
+            const deftri_keyframe &kf1 = map.keyframes[pe.b], &kf2 = map.keyframes[pe.a];
+            pe.slot_pt.assign(2 * (size_t)pe.ns12, -1);
+            for (int32_t slot : pe.enc) {
+                pe.slot_pt[2 * (size_t)slot] = add_point(kf1.point_id[slot], pe.b, slot, pe.b, slot);
+                pe.slot_pt[2 * (size_t)slot + 1] = add_point(kf2.point_id[slot], pe.a, slot, pe.b, slot);
+            }
+            pe.enc.clear();
+            pe.enc.shrink_to_fit();
+        }
+        if (timing) std::fprintf(stderr, "[deftri graph] slot scan + points: %.1f ms\n", ms(ts, tnow()));
     }
     {
         // the edges, each pair into its own range (the reference's order: pairs, then slots)
