@@ -6,6 +6,7 @@
 // SURVEY §8d C4) plans in seconds; nothing here depends on a fill-reducing ordering.
 #include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -190,22 +191,45 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     static const bool no_rowsort = std::getenv("DEFTRI_SP_NO_ROWSORT") != nullptr;
     const std::vector<int32_t> mrow = H.row_of_point;     // Morton (pre-sort) row of each point
     if (!no_rowsort) {
+        // slot counts per row: per-chunk counts over the incidences on host threads, summed per row
+        const int64_t ninc = 4 * E + D;
+        const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, ninc / (1 << 20)));
+        std::vector<std::vector<int32_t>> ccnt((size_t)nch);
+        chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+            for (int64_t c = c0; c < c1; c++) {
+                std::vector<int32_t> &k = ccnt[c];
+                k.assign(P, 0);
+                for (int64_t x = ninc * c / nch; x < ninc * (c + 1) / nch; x++)
+                    k[row[x < 4 * E ? ap[x] : d.dep_point[x - 4 * E]]]++;
+            }
+        });
         std::vector<int32_t> cnt(P, 0);
-        for (int64_t e = 0; e < 4 * E; e++) cnt[row[ap[e]]]++;
-        for (int64_t e = 0; e < D; e++) cnt[row[d.dep_point[e]]]++;
+        chunked(P, 1 << 16, [&](int, int64_t r0, int64_t r1) {
+            for (int64_t c = 0; c < nch; c++)
+                for (int64_t r = r0; r < r1; r++) cnt[r] += ccnt[c][r];
+        });
+        ccnt.clear();
+        // the windows, each sorted on its own (every window writes its own rows)
         std::vector<int32_t> np(P);
-        for (int rk = 0; rk < nranks; rk++) {
-            const int32_t a = H.rank_row_begin[rk], b = H.rank_row_begin[rk + 1];
-            for (int32_t w0 = a; w0 < b; w0 += kSpSortWindow) {
-                const int32_t w1 = std::min(b, w0 + kSpSortWindow);
-                std::vector<int32_t> ord(w1 - w0);
+        std::vector<int32_t> wstart;
+        for (int rk = 0; rk < nranks; rk++)
+            for (int32_t w0 = H.rank_row_begin[rk]; w0 < H.rank_row_begin[rk + 1]; w0 += kSpSortWindow) wstart.push_back(w0);
+        chunked((int64_t)wstart.size(), 64, [&](int, int64_t i0, int64_t i1) {
+            std::vector<int32_t> ord;
+            for (int64_t i = i0; i < i1; i++) {
+                const int32_t w0 = wstart[i];
+                const int32_t rk_end = *std::upper_bound(H.rank_row_begin.begin(), H.rank_row_begin.end(), w0);
+                const int32_t w1 = std::min(rk_end, w0 + kSpSortWindow);
+                ord.resize(w1 - w0);
                 std::iota(ord.begin(), ord.end(), w0);
                 std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) { return cnt[x] > cnt[y]; });
                 for (int32_t k = 0; k < w1 - w0; k++) np[w0 + k] = H.point_of_row[ord[k]];
             }
-        }
+        });
         H.point_of_row = np;
-        for (int32_t r = 0; r < P; r++) H.row_of_point[np[r]] = r;
+        chunked(P, 1 << 16, [&](int, int64_t r0, int64_t r1) {
+            for (int64_t r = r0; r < r1; r++) H.row_of_point[np[r]] = (int32_t)r;
+        });
     }
     H.lo = H.rank_row_begin[rank];
     H.hi = H.rank_row_begin[rank + 1];
@@ -239,14 +263,40 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
 
     // rotation rows used by the local edges, compacted
     {
-        std::vector<int32_t> map(std::max(d.n_rot, 1), -1);
-        H.arap_rot_local.resize(2 * (size_t)nloc);
-        for (int64_t le = 0; le < nloc; le++)
-            for (int k = 0; k < 2; k++) {
-                const int32_t g = d.arap_rot[2 * (int64_t)H.arap_ids[le] + k];
-                if (map[g] < 0) { map[g] = (int32_t)H.rot_ids.size(); H.rot_ids.push_back(g); }
-                H.arap_rot_local[2 * le + k] = map[g];
+        // numbered in first-encounter order over the positions 2 le + k: each row's first position
+        // (an atomic minimum over host threads), the first positions flagged and prefix-summed
+        const int64_t npos = 2 * nloc;
+        auto rot_at = [&](int64_t x) { return d.arap_rot[2 * (int64_t)H.arap_ids[x >> 1] + (x & 1)]; };
+        std::vector<int64_t> first((size_t)std::max(d.n_rot, 1), INT64_MAX);
+        chunked(npos, 1 << 18, [&](int, int64_t x0, int64_t x1) {
+            for (int64_t x = x0; x < x1; x++) {
+                int64_t *f = &first[rot_at(x)];
+                int64_t cur = __atomic_load_n(f, __ATOMIC_RELAXED);
+                while (x < cur && !__atomic_compare_exchange_n(f, &cur, x, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
             }
+        });
+        const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, npos / (1 << 18)));
+        std::vector<int64_t> cbase((size_t)nch + 1, 0);
+        chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+            for (int64_t c = c0; c < c1; c++)
+                for (int64_t x = npos * c / nch; x < npos * (c + 1) / nch; x++) cbase[c + 1] += first[rot_at(x)] == x;
+        });
+        for (int64_t c = 0; c < nch; c++) cbase[c + 1] += cbase[c];
+        H.rot_ids.resize((size_t)cbase[nch]);
+        std::vector<int32_t> map(std::max(d.n_rot, 1), -1);
+        chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
+            for (int64_t c = c0; c < c1; c++) {
+                int64_t n = cbase[c];
+                for (int64_t x = npos * c / nch; x < npos * (c + 1) / nch; x++) {
+                    const int32_t g = rot_at(x);
+                    if (first[g] == x) { map[g] = (int32_t)n; H.rot_ids[n++] = g; }
+                }
+            }
+        });
+        H.arap_rot_local.resize((size_t)npos);
+        chunked(npos, 1 << 18, [&](int, int64_t x0, int64_t x1) {
+            for (int64_t x = x0; x < x1; x++) H.arap_rot_local[x] = map[rot_at(x)];
+        });
     }
 
     stage("5 local ARAP edges");
