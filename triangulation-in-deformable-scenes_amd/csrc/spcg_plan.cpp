@@ -33,6 +33,41 @@ void counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
     ids.swap(out);
 }
 
+// the offsets of a chunked counting sort, key-major with chunk order inside a key: cnt[c][k] becomes
+// chunk c's first write position for key k, key_start[k] (optional, nkeys + 1) key k's start. Key
+// ranges on host threads: their totals, a prefix over the ranges, then each range's offsets
+template <class T>
+int64_t chunk_offsets(std::vector<std::vector<T>> &cnt, int64_t nkeys, int64_t *key_start) {
+    const int64_t nch = (int64_t)cnt.size();
+    const int64_t nkr = std::max<int64_t>(1, std::min<int64_t>(16, nkeys / (1 << 16)));
+    auto k_of = [&](int64_t r) { return nkeys * r / nkr; };
+    std::vector<int64_t> rbase((size_t)nkr + 1, 0);
+    chunked(nkr, 1, [&](int, int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; r++) {
+            int64_t t = 0;
+            for (int64_t c = 0; c < nch; c++)
+                for (int64_t k = k_of(r); k < k_of(r + 1); k++) t += cnt[c][k];
+            rbase[r + 1] = t;
+        }
+    });
+    for (int64_t r = 0; r < nkr; r++) rbase[r + 1] += rbase[r];
+    chunked(nkr, 1, [&](int, int64_t r0, int64_t r1) {
+        for (int64_t r = r0; r < r1; r++) {
+            int64_t run = rbase[r];
+            for (int64_t k = k_of(r); k < k_of(r + 1); k++) {
+                if (key_start) key_start[k] = run;
+                for (int64_t c = 0; c < nch; c++) {
+                    const T v = cnt[c][k];
+                    cnt[c][k] = (T)run;
+                    run += v;
+                }
+            }
+        }
+    });
+    if (key_start) key_start[nkeys] = rbase[nkr];
+    return rbase[nkr];
+}
+
 // the same stable counting sort over chunks of `ids` on host threads: per-chunk key counts,
 // offsets in (key, chunk) order, every chunk scatters its ids in order (a stable sort's output is
 // unique, so the result does not depend on the chunking)
@@ -50,13 +85,7 @@ void par_counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
             for (int64_t i = lo_of(c); i < lo_of(c + 1); i++) cnt[c][(size_t)key(ids[i])]++;
         }
     });
-    int64_t run = 0;
-    for (int64_t k = 0; k < nkeys; k++)
-        for (int64_t c = 0; c < nch; c++) {
-            const int32_t v = cnt[c][k];
-            cnt[c][k] = (int32_t)run;
-            run += v;
-        }
+    chunk_offsets(cnt, nkeys, nullptr);
     std::vector<int32_t> out((size_t)n);
     chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
         for (int64_t c = c0; c < c1; c++)
@@ -405,12 +434,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             }
         });
         // offsets: row-major, chunk order inside a row (ccnt becomes each chunk's write position)
-        int64_t acc = 0;
-        for (int32_t l = 0; l < nown; l++) {
-            H.inc_off[l] = acc;
-            for (int64_t c = 0; c < nch; c++) { const int32_t v = ccnt[c][l]; ccnt[c][l] = (int32_t)acc; acc += v; }
-        }
-        H.inc_off[nown] = acc;
+        const int64_t acc = chunk_offsets(ccnt, nown, H.inc_off.data());
         H.inc.resize((size_t)acc);
         chunked(nch, 1, [&](int, int64_t c0, int64_t c1) {
             for (int64_t c = c0; c < c1; c++)
