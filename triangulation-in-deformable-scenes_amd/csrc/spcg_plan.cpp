@@ -353,7 +353,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     const int32_t ndl = (int32_t)H.dep_ids.size();
     H.dperm.resize(ndl);
     std::iota(H.dperm.begin(), H.dperm.end(), 0);
-    counting_sort(H.dperm, std::max(S, 1), [&](int32_t j) { return d.dep_scale[H.dep_ids[j]]; });
+    par_counting_sort(H.dperm, std::max(S, 1), [&](int32_t j) { return d.dep_scale[H.dep_ids[j]]; });
     auto add_blocks = [&](int kind, int owned, int64_t b0, int64_t b1, auto heavy_of) {
         int64_t i = b0;
         while (i < b1) {
