@@ -128,23 +128,42 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     const int32_t *ap = d.arap_pts;
 
     // 1. keyframe-copy groups: union-find over the ARAP edges' (p1_i, p2_i) and (p1_j, p2_j)
+    //    on host threads: a root is only ever linked under a smaller root (compare-and-swap), so every
+    //    tree's root is its smallest point id and the partition and roots do not depend on the order
     std::vector<int32_t> par(P);
     std::iota(par.begin(), par.end(), 0);
+    auto ld = [&](int32_t a) { return __atomic_load_n(&par[a], __ATOMIC_RELAXED); };
     auto find = [&](int32_t a) {
-        while (par[a] != a) { par[a] = par[par[a]]; a = par[a]; }
-        return a;
+        for (;;) {
+            const int32_t p = ld(a);
+            if (p == a) return a;
+            const int32_t gp = ld(p);
+            if (gp != p) { int32_t exp = p; __atomic_compare_exchange_n(&par[a], &exp, gp, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED); }
+            a = p;
+        }
     };
     auto unite = [&](int32_t a, int32_t b) {
-        a = find(a); b = find(b);
-        if (a != b) { if (a < b) par[b] = a; else par[a] = b; }   // root = smallest point id
+        for (;;) {
+            a = find(a); b = find(b);
+            if (a == b) return;
+            if (a > b) std::swap(a, b);
+            int32_t exp = b;                     // b still a root: link it under the smaller a
+            if (__atomic_compare_exchange_n(&par[b], &exp, a, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) return;
+        }
     };
-    for (int64_t e = 0; e < E; e++) {
-        unite(ap[4 * e], ap[4 * e + 1]);
-        unite(ap[4 * e + 2], ap[4 * e + 3]);
-    }
+    chunked(E, 1 << 18, [&](int, int64_t e0, int64_t e1) {
+        for (int64_t e = e0; e < e1; e++) {
+            unite(ap[4 * e], ap[4 * e + 1]);
+            unite(ap[4 * e + 2], ap[4 * e + 3]);
+        }
+    });
+    std::vector<int32_t> root(P);
+    chunked(P, 1 << 16, [&](int, int64_t p0, int64_t p1) {
+        for (int64_t p = p0; p < p1; p++) root[p] = find((int32_t)p);
+    });
     std::vector<int32_t> gid(P, -1), grep;   // group of each point; representative (smallest id) per group
     for (int32_t p = 0; p < P; p++) {
-        const int32_t r = find(p);
+        const int32_t r = root[p];
         if (gid[r] < 0) { gid[r] = (int32_t)grep.size(); grep.push_back(r); }
         gid[p] = gid[r];
     }
