@@ -235,8 +235,9 @@ int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_
    rows = points grouped by mesh vertex in Morton order, dealt to the ranks in contiguous
    work-balanced ranges; per CG iteration an edge-parallel pass s_e = W_e J_e p over the rank's local
    ARAP edges and a row-parallel gather q_v = sum J_{e,v}^T s_e (+ the folded reprojection / depth
-   blocks); sharded: one halo exchange of the boundary rows' (z, p) and two all-reduces (the dot
-   products, the global-vertex partials) per CG iteration.  A step whose PCG does not converge within
+   blocks); sharded: one halo exchange of the boundary rows' (z, p) and ONE all-reduce per CG
+   iteration (Chronopoulos-Gear single-reduction CG: r.z, r.r, z.Az and the global-vertex partials
+   of A z travel together; plan_info.cg_collectives = 1).  A step whose PCG does not converge within
    the budget (deftri_set_linear_solver max_iterations; <= 0: 1000) counts as a failed linear solve
    (g2o: the trial is rejected; no LDL^T stands behind it).  One rank from 50,000 unknowns: two
    launches per CG iteration (the merged chain), whose alpha is handed from phase 2's workgroup 0 to
@@ -248,8 +249,9 @@ int deftri_last_step_info(const deftri_ctx *ctx, int32_t *pcg_iterations, int32_
    context is point-sharded (nranks > 1) or the problem has >= 50,000 unknowns (measured faster from
    C2 up); MULTIFRONTAL otherwise.  Applies to the next deftri_problem_upload.  A
    context on the iterative plan that is asked for what only the factorization has (LDL^T steps or
-   solves after deftri_set_linear_solver(DIRECT), deftri_eval_hessian_product) analyses and uploads
-   the multifrontal plan at that point, continuing from its current state. */
+   solves after deftri_set_linear_solver(DIRECT)) analyses and uploads the multifrontal plan at that
+   point, continuing from its current state; deftri_eval_hessian_product stays on the iterative plan
+   (its own matrix-free product, H never assembled). */
 #define DEFTRI_PLAN_AUTO          0
 #define DEFTRI_PLAN_MULTIFRONTAL  1
 #define DEFTRI_PLAN_ITERATIVE     2

@@ -46,7 +46,8 @@ def main():
             "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"], "lambda_final": R["lambda_final"],
             "iterations": R["iterations"], "trials_total": R["trials_total"],
             "point_sum": pts.sum(0).tolist(), "scales": res["scales"].tolist(), "tg": res["tg"].tolist(),
-            "rms_initial": rms0, "rms_final": rms1, "summary": p.summary(), "oracle_seconds": round(dt, 1)}
+            "rms_initial": rms0, "rms_final": rms1, "summary": p.summary(), "problem_digest": p.digest(),
+            "oracle_seconds": round(dt, 1)}
     (d / "expected_c2.json").write_text(json.dumps(meta, indent=1))
     print(json.dumps(meta))
 

@@ -40,6 +40,8 @@ def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
     p, m0 = c2_scene
     m = copy.deepcopy(m0)
     assert p.summary() == meta["summary"]
+    if "problem_digest" in meta:                      # the graph the golden was computed on
+        assert p.digest() == meta["problem_digest"], "stale golden: the graph builder changed the graph"
     gpu_ctx.set_plan(plan)
     try:
         gpu_ctx.set_lm_lanes(1)

@@ -91,3 +91,60 @@ def test_c4_full_size_properties():
     assert p.n_pairs == 28 and p.n_unknowns == 12000224
     r, solves = check_props(p, 2, (1e-5,))
     print("C4", r["trials_iter"], solves)
+
+
+def c5_scene():
+    """bench.py --workload c5's scene: Realcolon.yaml (KB8 d0..d3, rep 1, arap 0.1, DepthWeight 0.001 ->
+    sigma_d 1e-6 m, Data/Realcolon.yaml:15-23,101,110), 20 keyframes x 200k, the 19 consecutive pairs"""
+    am = sim.multi_view_arrays(n=200000, k=20, seed=1, kb8=sim.REALCOLON_KB8)
+    host = capi.Context(-1)
+    host.set_pair_window(1)
+    p = host.build_graph(am, 1.0, 0.1, np.float32(1e-6))
+    host.close()
+    return p, am
+
+
+def _apply(am, ids, pts, n):
+    """the solved points (graph order, MapPoint id k * n + i) into the ArrayMap's keyframes"""
+    ids = np.asarray(ids)
+    k, i = ids // n, ids % n
+    for kk in range(len(am.kfs)):
+        sel = k == kk
+        am.kfs[kk]["pos"][i[sel]] = pts[sel].astype(np.float32)
+
+
+def test_c5_full_size_properties():
+    """C5 (BASELINE configs[4]): Realcolon 20 keyframes x 200k, 19 consecutive pairs — 12,000,152
+    unknowns (g2oBundleAdjustment.cc:640-962 over the sliding window).  The full-size properties over 3
+    LM iterations, then the configuration's fp32-vs-fp64 sweep AT this size: the same 3 iterations with
+    the ARAP Jacobians stored in fp32 for the product (deftri_set_jacobian_storage 1; b, the
+    preconditioner, the vectors and every reduction stay fp64) take the same trials, and the reprojection
+    RMSE of the solved map (calculatePixelsStandDev, Geometry.cc:370-498) is within the north-star
+    1e-4 px of the fp64 run's."""
+    p, am = c5_scene()
+    assert p.n_pairs == 19 and p.n_unknowns == 12000152
+    r64, solves = check_props(p, 3, (1e-5,))
+    print("C5", r64["trials_iter"], solves)
+    init = [kf["pos"].copy() for kf in am.kfs]
+    rms, runs = {}, {}
+    with capi.Context(0) as ctx:
+        for fp32 in (0, 1):
+            ctx.set_plan("auto")
+            ctx.set_jacobian_storage(fp32)
+            ctx.upload(p)
+            info = ctx.plan_info()
+            assert info["plan"] == "iterative" and bool(info["jacobian_fp32"]) == bool(fp32)
+            r = ctx.solve_lm(3, analytic=False)
+            pts, _, _ = ctx.download()
+            assert r["pcg_fallbacks"] == 0
+            for kk, kf in enumerate(am.kfs):
+                kf["pos"][:] = init[kk]
+            _apply(am, p.point_ids, pts, 200000)
+            rms[fp32] = ctx.pixels_stand_dev(am)
+            runs[fp32] = r
+    assert runs[0]["chi2_iter"] == r64["chi2_iter"]           # the fp64 run is the properties' run
+    assert runs[1]["trials_iter"] == runs[0]["trials_iter"]
+    np.testing.assert_allclose(runs[1]["chi2_iter"], runs[0]["chi2_iter"], rtol=1e-6)
+    for k in ("desv", "desvc1", "desvc2"):
+        assert abs(rms[1][k] - rms[0][k]) < 1e-4, (k, rms)
+    print("C5 fp32 vs fp64", {k: abs(rms[1][k] - rms[0][k]) for k in ("desv", "desvc1", "desvc2")})

@@ -535,3 +535,53 @@ def test_device_lm_matches_host_lm():
     assert l0 == l1 == 2
     assert c0 == c1 and t0 == t1 and i0 == i1
     assert s0 == s1
+
+
+def _timeout_worker(env, q):
+    os.environ.update(env)                          # read once, at the first upload of this process
+    from deftri import capi as c
+    p = tv_problem(20000, seed=6)                   # 60k unknowns: the merged chain
+    with c.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.upload(p)
+        code, state_after_error = None, None
+        if "DEFTRI_SP_INJECT_TIMEOUT_IT" in env:
+            try:
+                ctx.solve_lm(5)
+            except c.DeftriError as e:
+                code = e.code
+            state_after_error = [a.tobytes() for a in ctx.download()]
+        r = ctx.solve_lm(5)
+        q.put((code, state_after_error, ctx.plan_info()["cg_launches"], r["chi2_iter"], r["trials_iter"],
+               r["pcg_iterations"], [a.tobytes() for a in ctx.download()],
+               [np.ascontiguousarray(x).tobytes() for x in (p.points, p.scales)]))
+
+
+@pytest.mark.parametrize("lm", ["host", "device"])
+def test_alpha_hand_off_timeout_is_an_error(lm):
+    """A merged-chain alpha hand-off that times out (forced at CG iteration 1 by
+    DEFTRI_SP_INJECT_TIMEOUT_IT) fails the call with DEFTRI_E_HIP on BOTH LM paths — never a rejected
+    trial (the ADVICE r4 finding: the device-driven LM's k_lm_decide used to count it as a failed solve
+    and raise lambda).  The state the call started from is restored, the context switches to the
+    separate alpha launch, and the retried call equals a clean run bit for bit."""
+    extra = {"DEFTRI_DEVICE_LM": "1"} if lm == "device" else {}
+    faulted, clean = _fusion_runs_full([{"DEFTRI_SP_INJECT_TIMEOUT_IT": "1", **extra}, extra])
+    code, state, launches, chi, trials, its, final, init = faulted
+    assert code == -2                                # DEFTRI_E_HIP
+    assert state[0] == init[0] and state[1] == init[1]   # points, scales as uploaded
+    assert launches == 3                             # now the separate alpha launch
+    assert chi == clean[3] and trials == clean[4] and its == clean[5]
+    assert final == clean[6]
+
+
+def _fusion_runs_full(envs):
+    cm = mp.get_context("spawn")
+    out = []
+    for env in envs:
+        q = cm.Queue()
+        pr = cm.Process(target=_timeout_worker, args=(env, q))
+        pr.start()
+        out.append(q.get(timeout=300))
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    return out

@@ -49,6 +49,8 @@ def test_regime_matches_oracle(gpu_ctx, name, sub, plan):
     meta, z = golden(name, sub)
     p, m = scene(meta)
     assert p.summary() == meta["summary"]
+    if "problem_digest" in meta:                      # the graph the golden was computed on
+        assert p.digest() == meta["problem_digest"], "stale golden: the graph builder changed the graph"
     gpu_ctx.set_plan(plan)
     try:
         gpu_ctx.set_lm_lanes(1)

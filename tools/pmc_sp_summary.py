@@ -1,4 +1,4 @@
-"""Summarize a tools/r03_prof.sh run into profiles/<tag>_pmc_sp_product.json: HBM-side bytes of the
+"""Summarize a tools/archive/r03_prof.sh run into profiles/<tag>_pmc_sp_product.json: HBM-side bytes of the
 iterative plan's matrix-free product (k_sp_phase1 + k_sp_phase2, one CG iteration) per active launch
 pair, from rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs, KB * 1024), keyed by the plan's
 algorithmic bytes per product so bench.py attaches it only to the same plan.

@@ -391,19 +391,28 @@ bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &t
             }
         }
     }
-    // the boundary: one cycle, strictly convex
+    // the boundary: one cycle, strictly convex.  A strict left turn at every vertex still admits a
+    // cycle that winds several times (a pentagram), so the winding is counted too: with every turn in
+    // (0, pi), the edge direction passes angle 0 exactly when it moves from the lower half-plane
+    // [pi, 2 pi) to the upper [0, pi) — sign tests on coordinate comparisons, exact — and a simple
+    // convex polygon does that once
+    auto upper = [&](int a, int b) {           // direction a -> b in [0, pi)
+        const double *pa = P(a), *pb = P(b);
+        return pb[1] > pa[1] || (pb[1] == pa[1] && pb[0] > pa[0]);
+    };
     int start = -1;
     for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
     if (start < 0) return false;
-    int u = start, len = 0;
+    int u = start, len = 0, wraps = 0;
     do {
         const int v = bnext[u];
         if (v < 0 || bnext[v] < 0) return false;
         if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
+        if (!upper(u, v) && upper(v, bnext[v])) wraps++;
         u = v;
         if (++len > nb) return false;
     } while (u != start);
-    return len == nb;
+    return len == nb && wraps == 1;
 }
 
 int orient2d_sign(const double *a, const double *b, const double *c) { return orient2d(a, b, c); }

@@ -17,8 +17,9 @@ int incircle_sign(const double *a, const double *b, const double *c, const doubl
 // n points xy — the one delaunay2d would return, triangle for triangle?  True when every triangle is
 // strictly counter-clockwise, every interior edge strictly locally Delaunay (its opposite vertex
 // strictly outside the circumcircle: no cocircular ambiguity), every vertex is on a triangle and
-// the boundary is a strictly convex polygon (so it is the convex hull): then the triangulation is
-// the unique Delaunay triangulation.  Exact predicates; parallel over triangles / edges.
+// the boundary is a strictly convex polygon winding once (so it is the convex hull): then the
+// triangulation is the unique Delaunay triangulation.  Exact predicates; one sequential pass over the
+// triangles' half-edges, then the boundary cycle.
 bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &tris);
 
 }  // namespace deftri

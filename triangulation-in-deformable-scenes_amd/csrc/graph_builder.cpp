@@ -542,11 +542,15 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     std::vector<unsigned char> skey = graph_key(map, pair_window, false);
     static const bool no_struct = std::getenv("DEFTRI_NO_STRUCT_MEMO") != nullptr;
     if (!no_memo && !no_struct && g.struct_valid && skey == g.struct_key) {
+        // refresh_graph writes the values pair by pair: until it succeeds neither memo describes g
+        // (a failure half-way must not leave a memo hit on the previous map's mixed values)
+        g.memo_valid = g.struct_valid = false;
         int rc = refresh_graph(map, rep_weight, arap_weight, info_dep, g, gdev, err);
         if (rc < 0) return false;
         if (rc == 0) {
             g.memo_key = std::move(key);
             g.memo_valid = true;
+            g.struct_valid = true;
             g.struct_hits++;
             g.ms_last = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_build).count();
             return true;

@@ -146,7 +146,8 @@ struct LmState {
     double lam, ni, cur, rho;            // _currentLambda, _ni, currentChi, the last trial's rho
     int32_t gate_trial, gate_lin;        // the next slot's gates (read by every gated kernel)
     int32_t it, q;                       // LM iteration, trials of it so far (g2o's qmax)
-    int32_t stop;                        // 0 running, 1 n_iterations done, 2 g2o Terminate, 3 PCG step unfinished
+    int32_t stop;                        // 0 running, 1 n_iterations done, 2 g2o Terminate, 3 PCG step unfinished,
+                                         // 4 alpha hand-off timeout (an error, raised by the host)
     int32_t restore;                     // the last trial was rejected: the next prologue restores the state
     int32_t need_lin;                    // the next slot starts a new iteration
     int32_t slot;                        // the enqueue index of the last slot decided

@@ -1681,6 +1681,14 @@ __global__ void k_lm_decide(LmState *lm, const double *__restrict__ scal, const 
         *snap = L;
         return;
     }
+    if (st == 5) {                               // kSpTimeout (spcg.h): the merged chain's alpha hand-off timed
+        L.stop = 4;                              // out — a scheduling fault, never a rejected trial: no lambda
+        L.stop_slot = slot;                      // change, every later slot gated off; the host raises it
+        L.gate_trial = L.gate_lin = 0;
+        *lm = L;
+        *snap = L;
+        return;
+    }
     const bool solved = st == 1;                 // kSpConverged (spcg.h)
     L.pcg_iterations += (int64_t)rec[1];
     if (solved) { L.pcg_trials++; L.last_its = (int)rec[1]; }

@@ -190,6 +190,7 @@ struct SpDev {
     double *m1part = nullptr;                             // phase-1 p.Ap per workgroup [m1n = m_nx + nblk]
     int32_t m1n = 0;
     int32_t alpha_kernel = 0;                             // alpha by k_sp_alpha between the phases (no hand-off)
+    int32_t inj_timeout_it = -1;                          // tests: the hand-off of this CG iteration times out
     // sharded single-reduction chain (sd, any rank count with a transport): per CG iteration phase 1
     // and phase 2 form w = A z and this rank's part of xb, the host all-reduces xb, k_sp_update_sd
     // updates and fills the send buffer; the boundary rows' (z, p) land in the receive region of zp
@@ -305,6 +306,9 @@ class SpSolver {
     DevProblem P;
     std::vector<void *> allocs_;
     std::vector<double *> init_;      // initial state (points plan order, scales, tg)
+    double *d_entry[3] = {nullptr, nullptr, nullptr};   // the state at solve_lm's entry (restored on an error)
+    bool in_lm_ = false;                                // inside solve_lm (d_entry holds its entry state)
+    int save_entry();
     double *d_scal = nullptr, *d_part = nullptr, *d_dx0 = nullptr, *d_tmp = nullptr;
     int *d_flag = nullptr;
     int *d_sumcnt = nullptr;           // launch_sum_multi_fused's ticket

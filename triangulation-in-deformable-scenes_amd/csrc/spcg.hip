@@ -863,14 +863,16 @@ __device__ __forceinline__ double m2_alpha_wait(const SpDev &G, int it) {
     __shared__ double sa;
     if (threadIdx.x == 0) {
         const double *w = G.red + (int64_t)kSpRed * it + 3;
-        int n = 0;
+        // a waiter polls ~2^16 times (s_sleep 2 between polls: well above the ~3 us a publish takes,
+        // well below a second of stall); DEFTRI_SP_INJECT_TIMEOUT_IT forces the timeout (tests)
+        int n = it == G.inj_timeout_it ? (1 << 16) : 0;
         double v = ld_sc1(w);
-        while (__double_as_longlong(v) == 0 && n < (1 << 22)) {
+        while (__double_as_longlong(v) == 0 && n < (1 << 16)) {
             __builtin_amdgcn_s_sleep(2);
             v = ld_sc1(w);
             n++;
         }
-        if (n >= (1 << 22)) {                          // never expected: stop the solve, skip the update
+        if (n >= (1 << 16)) {                          // never expected: stop the solve, skip the update
             st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpTimeout);
             sa = __builtin_nan("");
         } else {

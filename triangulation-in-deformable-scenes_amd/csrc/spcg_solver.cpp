@@ -109,17 +109,30 @@ int SpSolver::put(T **p, const std::vector<T> &v) {
 
 int SpSolver::budget() const { return std::min(kSpMaxIt, max_it > 0 ? max_it : kSpDefaultIt); }
 
-// a merged-chain alpha hand-off that timed out (spcg.hip m2_alpha_wait): the trial's state is
-// restored, the context switches to the separate alpha launch and the call fails — a device
-// scheduling fault, not a numeric verdict, so it never becomes a rejected trial
+// the state at solve_lm's entry, which an error restores (hand_off_timeout)
+int SpSolver::save_entry() {
+    SPOK(hipMemcpyAsync(d_entry[0], P.points, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_));
+    SPOK(hipMemcpyAsync(d_entry[1], P.scales, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_));
+    SPOK(hipMemcpyAsync(d_entry[2], P.tg, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_));
+    return 0;
+}
+
+// a merged-chain alpha hand-off that timed out (spcg.hip m2_alpha_wait): the state the call started
+// from is restored (iterations it accepted before the fault are undone, so a retry is a clean run),
+// the context switches to the separate alpha launch and the call fails — a device scheduling fault,
+// not a numeric verdict, so it never becomes a rejected trial
 int SpSolver::hand_off_timeout() {
     G.alpha_kernel = 1;
-    hipMemcpyAsync(P.points, P.points_bak, sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_);
-    hipMemcpyAsync(P.scales, P.scales_bak, sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_);
-    hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_);
     hipStreamSynchronize(st_);
+    if (in_lm_) {                  // (a bare damped solve does not move the state)
+        hipMemcpyAsync(P.points, d_entry[0], sizeof(double) * 3 * (size_t)P.P, hipMemcpyDeviceToDevice, st_);
+        hipMemcpyAsync(P.scales, d_entry[1], sizeof(double) * (size_t)P.S, hipMemcpyDeviceToDevice, st_);
+        hipMemcpyAsync(P.tg, d_entry[2], sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, st_);
+        hipStreamSynchronize(st_);
+    }
     return fail(DEFTRI_E_HIP, "merged CG chain: the alpha hand-off timed out (phase 2's workgroup 0 not resident); "
-                              "the context now launches alpha separately — retry the call");
+                              "the state is restored to the call's start and the context now launches alpha "
+                              "separately — retry the call");
 }
 
 // the values of a problem in the plan's layout (points in row order, the rank's edges): everything
@@ -242,6 +255,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     P.jarap_ld = std::max<int64_t>(nloc, 1);        // column-major J: each of the 18 columns coalesced
     PUT(P.points, pts); PUT(P.scales, sc); PUT(P.tg, tg);
     ALLOC(P.points_bak, 3 * (int64_t)NP); ALLOC(P.scales_bak, S); ALLOC(P.tg_bak, 7 * (int64_t)Q);
+    ALLOC(d_entry[0], 3 * (int64_t)NP); ALLOC(d_entry[1], S); ALLOC(d_entry[2], 7 * (int64_t)Q);
     PUT(P.cam_kb8, kb8); PUT(P.cam_pose, cpose); PUT(P.cam_R, camR);
     PUT(P.rep_point, rp); PUT(P.rep_cam, rc); PUT(P.rep_obs, ro); PUT(P.rep_info, ri);
     PUT(P.dep_point, dp); PUT(P.dep_scale, ds); PUT(P.dep_cam, dc); PUT(P.dep_meas, dm); PUT(P.dep_info, di);
@@ -324,6 +338,9 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.m_nh = 8 * ((Q + S + 7) / 8);
         static const bool ak = std::getenv("DEFTRI_SP_ALPHA_KERNEL") != nullptr;
         G.alpha_kernel = ak ? 1 : 0;
+        // tests: every waiter of this CG iteration's alpha hand-off times out (the error path)
+        static const int inj = std::getenv("DEFTRI_SP_INJECT_TIMEOUT_IT") ? std::atoi(std::getenv("DEFTRI_SP_INJECT_TIMEOUT_IT")) : -1;
+        G.inj_timeout_it = inj;
         // sharded: the single-reduction chain (3 launches + one all-reduce per CG iteration);
         // DEFTRI_SP_TWO_REDUCTIONS=1 keeps the round-3 six-launch chain for A/Bs
         static const bool two_red = std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
@@ -661,6 +678,7 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
             return rc;
         SPOK(hipHostMalloc((void **)&h_snap, sizeof(LmState), hipHostMallocDefault));
     }
+    if ((rc = save_entry())) return rc;
     eval_chi2(analytic, 0, nullptr);
     SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));
     SPOK(hipStreamSynchronize(st_));
@@ -758,6 +776,12 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
         evpool.push_back(sl.ev);
         const LmState S = *h_snap;
         if (S.last_its > 0) guess = std::max(2, S.last_its + 2);
+        if (S.stop == 4) {                                 // alpha hand-off timeout: an error, not a trial
+            SPOK(hipStreamSynchronize(st_));
+            for (const Slot &o : inflight) evpool.push_back(o.ev);
+            for (hipEvent_t e : evpool) hipEventDestroy(e);
+            return hand_off_timeout();
+        }
         if (S.stop == 1 || S.stop == 2) { host_stop = true; continue; }
         if (S.stop == 3) {
             // the slot S.stop_slot queued too few CG iterations: every later slot returned at once
@@ -843,6 +867,11 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     R.rank = rank_;
     R.nranks = nranks_;
     R.lanes = 1;
+    struct InLm {
+        bool &f;
+        explicit InLm(bool &x) : f(x) { f = true; }
+        ~InLm() { f = false; }
+    } in_lm(in_lm_);
     // the device-driven LM is opt-in (DEFTRI_DEVICE_LM=1): measured ~5 % slower than this loop at C2
     // (profiles/r04ab_lm_control.json) — a step that outruns its slot's guessed CG count costs the
     // slot in flight behind it, more than the host round trip per trial it saves
@@ -858,6 +887,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     const bool analytic = prm.analytic_jacobians != 0;
     auto t_start = std::chrono::steady_clock::now();
     int rc;
+    if (!shard_ && (rc = save_entry())) return rc;     // (the sharded chain has no hand-off)
     eval_chi2(analytic, 0, nullptr);
     if (dist && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     SPOK(hipMemcpyAsync(hpin, d_scal, sizeof(double), hipMemcpyDeviceToHost, st_));

@@ -116,6 +116,22 @@ class Problem:
         self._keep = keep
         return d
 
+    def digest(self):
+        """sha256 (hex, 16 chars) over every array of the graph in field order: a golden records the
+        graph it was computed on, so a graph-builder change that moves any value shows as a stale
+        golden instead of a silently looser pin."""
+        import hashlib
+        h = hashlib.sha256()
+        for f in fields(self):
+            if f.name.startswith("_"):
+                continue
+            v = getattr(self, f.name)
+            if v is None:
+                continue
+            h.update(f.name.encode())
+            h.update(np.ascontiguousarray(v).tobytes() if isinstance(v, np.ndarray) else repr(v).encode())
+        return h.hexdigest()[:16]
+
     # persistence ----------------------------------------------------------------------------
     def save(self, path):
         arrs = {f.name: getattr(self, f.name) for f in fields(self)
