@@ -12,16 +12,21 @@ solve (block-Jacobi PCG, or the multifrontal LDL^T) + update + chi2).  The scene
 reference's simulation recipe scaled to n points); the graph is built on the host once, then
 resident in HBM before the timed region starts.
 
-Multi-GPU (N > 1, one process per GPU, RCCL): ONE problem point-sharded over the N ranks — the
-iterative plan (csrc/spcg.h): each rank owns a contiguous Morton range of point rows, per CG iteration
-three launches, one ncclAllReduce of [r.z, r.r, z.Az, the global vertices' sums] and one grouped
-send / receive of the boundary rows.  Default: weak scaling — the problem has
-N x 100k correspondences (each GPU holds a C2-sized share), value = LM iterations of that problem x N
-/ the slowest rank's time ("C2-equivalent LM iterations/s": the correspondence-iterations processed,
-in units of one C2 iteration).  --strong: the C2 problem itself split over the N ranks (value = its
-LM it/s).  --replicas: N independent C2 problems (no collective; per-problem rate).  --solver direct
-runs the sharded multifrontal LDL^T instead.  The barrier and the max-over-ranks time use
-torch.distributed.
+Multi-GPU (N > 1, one process per GPU, RCCL): the BASELINE metric's fixed problem (C2, 100k
+correspondences x 2 views) point-sharded over the N ranks — strong scaling, value = that problem's
+LM iterations/s.  The iterative plan (csrc/spcg.h): each rank owns a contiguous Morton range of point
+rows; per CG iteration one ncclAllReduce of [r.z, r.r, z.Az, the global vertices' sums] and one
+grouped send / receive of the boundary rows, overlapped with the interior edges' product
+(DESIGN.md §7).  The line also carries `north_star_500k`: the 500k x 2 problem (3M unknowns, the
+north star's size) split the same way.  --weak: one problem of N x 100k correspondences instead
+(value in C2-equivalent iterations/s).  --replicas: N independent C2 problems (no collective;
+per-problem rate).  --solver direct runs the sharded multifrontal LDL^T instead.  The barrier and the
+max-over-ranks time use torch.distributed.
+
+Legs of the default C2 line (--no-legs skips them): `north_star_500k` (above, any N) and, at N = 1,
+`regimes.realcolon`: the C2 scene under Realcolon.yaml's weights and camera (arap 0.1, sigma_d 1e-6 m,
+KB8 d0..d3; Data/Realcolon.yaml:15-23,101,110), a CG-heavy regime (the Simulation.yaml headline
+run is near-stalled: ~5 CG iterations per trial at lambda ~1e21).
 
 Printed roofline (the iterative plan, the default): the CG iteration's kernels k_sp_phase1 +
 k_sp_phase2 (the matrix-free product with the update folded in), HBM-bound — from a profiled trial
@@ -497,6 +502,55 @@ def factor_roofline(stats_f, rank):
             "flops_per_factorization": upd["flops"], "rank": rank}
 
 
+def timed_leg(prob, gpu, rank, world, backend, steps, warmup, label):
+    """One more timed LM run in the bench line: the same plan choice and transport as the headline,
+    `steps` LM iterations after `warmup`, max over ranks; CG iterations per trial and the product's
+    roofline from a profiled trial."""
+    ctx = capi.Context(gpu)
+    try:
+        if world > 1:
+            from deftri import dist as ddist
+            if backend == "nccl":
+                ddist.init_rccl(ctx, rank, world)
+            else:
+                ctx.dist_set_transport(world, rank, ddist.torch_transport())
+        t0 = time.perf_counter()
+        ctx.upload(prob)
+        info = ctx.plan_info()
+        log(f"[rank {rank}] {label}: upload {time.perf_counter() - t0:.1f}s, {prob.summary()}")
+        if warmup > 0:
+            ctx.solve_lm(warmup)
+        ctx.reset_state()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rep = ctx.solve_lm(steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        t_max, _, _ = reduce_stats(dt, rep["iterations"], rep["trials_total"], world,
+                                   "cuda" if backend == "nccl" else "cpu")
+        stats = ctx.profile_trial(rep["lambda_final"])
+        roof = product_roofline(stats, rep, ctx, rank)
+        its = max(rep["iterations"], 1)
+        out = {"value": its / t_max, "unit": "LM iterations/s", "ms_per_step": 1e3 * t_max / its, "steps": steps,
+               "iterations": rep["iterations"], "unknowns": rep["n_unknowns"], "points": prob.n_points,
+               "arap_edges": len(prob.arap_pair), "trials_per_iteration": round(rep["trials_total"] / its, 3),
+               "cg_iterations_per_trial": round(rep["pcg_iterations"] / max(rep["pcg_trials"], 1), 2),
+               "pcg_failed": rep["pcg_fallbacks"], "chi2_initial": rep["chi2_initial"], "chi2_final": rep["chi2_final"],
+               "lambda_final": rep["lambda_final"], "plan": info["plan"], "cg_launches_per_iteration": info.get("cg_launches"),
+               "parallelism": f"points{world}" if world > 1 else "single"}
+        if roof:
+            out.update({"cg_iteration_us": roof.get("cg_iteration_us"), "frac_survey": roof.get("frac_survey"),
+                        "frac_design": roof.get("frac_design")})
+        log(f"[rank {rank}] {label}: {out}")
+        return out
+    finally:
+        ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -526,8 +580,12 @@ def main():
     ap.add_argument("--analytic", action="store_true",
                     help="closed-form ARAP/depth Jacobians (default: g2o numeric, the reference's arithmetic)")
     ap.add_argument("--sharded", action="store_true", help="kept for scripts: N > 1 is point-sharded by default")
-    ap.add_argument("--strong", action="store_true",
-                    help="N > 1: the workload's own problem split over the N ranks (default: weak scaling, N x the correspondences)")
+    ap.add_argument("--strong", action="store_true", help="kept for scripts: N > 1 strong-scales by default")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: weak scaling instead (one problem of N x the correspondences; value in C2-equivalent "
+                         "iterations/s) — the default is the BASELINE metric's fixed problem split over the N ranks")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the extra legs of the C2 line (the 500k x 2 north-star size, the Realcolon regime)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: N independent problems, one per GPU; value = per-problem LM it/s")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end arapOptimization timing")
@@ -564,7 +622,7 @@ def main():
     n = args.corr or spec["n"]
     window = args.pair_window if args.pair_window >= 0 else spec.get("window", 0)
     sharded = world > 1 and not args.replicas
-    weak = sharded and not args.strong
+    weak = sharded and args.weak
     n_build = n * world if weak else n        # weak: each rank's share is the workload's size
     plan = args.plan              # auto: the library's choice (iterative for PCG from 50k unknowns / sharded)
     t0 = time.perf_counter()
@@ -663,6 +721,23 @@ def main():
         e2e = end_to_end(gpu, prob_map, configure)
         log(f"end-to-end arapOptimization: {e2e}")
 
+    legs_500k, regimes = None, None
+    headline = wl == "c2" and REGIME == "simulation" and n == 100000 and not args.replicas and not weak
+    if headline and not args.no_legs and args.solver == "pcg":
+        ctx.close()
+        ctx = None
+        p5 = build_problem(500000, 1)[0]
+        legs_500k = timed_leg(p5, gpu, rank, world, backend, args.steps, min(args.warmup, 2), "500k x 2")
+        legs_500k["correspondences_per_keyframe"] = 500000
+        legs_500k["scaling"] = "strong" if world > 1 else "single"
+        del p5
+        if world == 1:
+            pr, _ = build_problem(100000, 1, "realcolon")
+            regimes = {"realcolon": timed_leg(pr, gpu, rank, world, backend, args.steps, min(args.warmup, 2),
+                                              "C2 realcolon")}
+            regimes["realcolon"]["weights"] = "Realcolon.yaml: rep 1, arap 0.1, DepthWeight 0.001 (sigma_d 1e-6 m), KB8 d0..d3"
+            del pr
+
     if rank == 0:
         workload = (("C2" if n == 100000 else f"two-view-{n}") + ("" if REGIME == "simulation" else f"-{REGIME}")) if wl == "c2" else \
             (wl.upper() if n == spec["n"] else f"{wl.upper()}-slice-{n}x{spec['k']}")
@@ -706,9 +781,12 @@ def main():
             "factorization_trial_kernel_ms": ({k: round(v["ms"], 3) for k, v in sorted(stats_f.items(), key=lambda kv: -kv[1]["ms"])}
                                               if stats_f is not None and stats_f is not stats else None),
             "end_to_end_arap_optimization": e2e,
+            "north_star_500k": legs_500k,
+            "regimes": regimes,
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -149,3 +149,37 @@ def test_merged_chain_pAp_decomposition(kind):
     pq = float(np.dot(x, q))
     assert abs(pap - pq) <= 1e-12 * abs(pq)
     assert pap > 0
+
+
+@pytest.mark.parametrize("units,lds", [(None, None), ("16", None), ("128", "12000")])
+def test_tile_product_matches_direct(units, lds, monkeypatch):
+    """Tile mode (csrc/spcg_tile.cpp; one rank, one keyframe pair — the fused product of the timed
+    plan): the host emulation walks the tile layout exactly as k_sp_tile / k_sp_tupd do (le and cross
+    slots from the chunk bases and the valid / cut lanes before an entry, the own rows' sums, the LDS
+    remote slots, the cross slots added by the update launch) and checks the layout on the way (every
+    local edge visited once, every LDS and cross slot written and read exactly once, every entry's LDS
+    rows holding its points); its product equals the direct one to 1e-12.  Tile sizes: the default,
+    small tiles (many cut edges) and an LDS budget that forces small tiles."""
+    import subprocess, sys, json
+    env = dict(os.environ, DEFTRI_SP_EMULATE_TILE="1")
+    if units:
+        env["DEFTRI_SP_TILE_UNITS"] = units
+    if lds:
+        env["DEFTRI_SP_TILE_LDS"] = lds
+    code = """
+import sys, json, numpy as np
+sys.path.insert(0, 'tests'); sys.path.insert(0, 'triangulation-in-deformable-scenes_amd')
+from test_sp_plan import _problem, _random_lin, _reference
+from deftri import capi
+p = _problem('tv')
+lin = _random_lin(p)
+with capi.Context(-1) as ctx:
+    qv, st = ctx.debug_sp_product(p, *lin[:6], 0.37, lin[6])
+ref = _reference(p, *lin[:6], 0.37, lin[6])
+print(json.dumps([float(np.max(np.abs(qv - ref)) / np.max(np.abs(ref))), int(st[2])]))
+"""
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
+                         cwd=str(__import__("pathlib").Path(__file__).resolve().parent.parent))
+    assert out.returncode == 0, out.stderr[-2000:]
+    err, nloc = json.loads(out.stdout.strip().splitlines()[-1])
+    assert err < 1e-12, err

@@ -1,0 +1,62 @@
+"""A/B of the tile-mode fused product against the two-phase product (DEFTRI_SP_NO_TILE=1) on one GPU:
+the same LM run (trials, chi2 per iteration, CG iterations) and a profiled trial's CG kernels.
+
+usage: python tools/tile_ab.py N_CORR N_IT [ENV=VAL ...]   (one process per variant)"""
+import json
+import os
+import pathlib
+import subprocess
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def run_variant(n, n_it):
+    sys.path.insert(0, str(ROOT / "triangulation-in-deformable-scenes_amd"))
+    import torch  # noqa: F401  (the HIP runtime first, as bench.py)
+    from deftri import capi, sim
+    p = sim.two_view_problem(n, 1)
+    with capi.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.upload(p)
+        info = ctx.plan_info()
+        r = ctx.solve_lm(n_it, analytic=False)
+        pts = ctx.download()[0]
+        st = ctx.profile_trial(r["lambda_final"])
+        its = max(st.get("sp_tupd", st.get("sp_phase2", {"launches": 1}))["launches"], 1)
+        cg = {k: round(1e3 * v["ms"] / its, 3) for k, v in st.items() if k in ("sp_tile", "sp_tupd", "sp_phase1", "sp_phase2", "sp_alpha")}
+        ctx.reset_state()
+        import time
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        r2 = ctx.solve_lm(n_it, analytic=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+    return {"tiles": info["tiles"], "cg_launches": info["cg_launches"], "trials": r["trials_iter"], "chi2": r["chi2_iter"],
+            "pcg_its": r["pcg_iterations"], "cg_us": cg, "cg_iteration_us": round(sum(cg.values()), 3), "cg_its_profiled": its,
+            "lm_it_s": round(r2["iterations"] / dt, 1), "bytes": info["product_bytes"], "survey_bytes": info["survey_bytes"],
+            "pts_sum": float(pts.sum()), "repeat_same": r2["chi2_iter"] == r["chi2_iter"]}
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "--one":
+        print("RESULT " + json.dumps(run_variant(int(sys.argv[2]), int(sys.argv[3]))), flush=True)
+        sys.exit(0)
+    n, n_it = int(sys.argv[1]), int(sys.argv[2])
+    variants = [dict(kv.split("=", 1) for kv in v.split(",")) if v != "-" else {} for v in (sys.argv[3:] or ["-", "DEFTRI_SP_NO_TILE=1"])]
+    out = []
+    for env in variants:
+        res = subprocess.run([sys.executable, __file__, "--one", str(n), str(n_it)], env=dict(os.environ, **env),
+                             capture_output=True, text=True, timeout=600)
+        line = [l for l in res.stdout.splitlines() if l.startswith("RESULT ")]
+        if res.returncode or not line:
+            print(json.dumps({"env": env, "rc": res.returncode, "stderr": res.stderr[-3000:]}), flush=True)
+            sys.exit(1)
+        r = json.loads(line[0][7:])
+        r["env"] = env
+        out.append(r)
+        print(json.dumps(r), flush=True)
+    a, b = out[0], out[-1]
+    import numpy as np
+    print(json.dumps({"same_trials": a["trials"] == b["trials"], "same_pcg_its": a["pcg_its"] == b["pcg_its"],
+                      "chi2_max_rel": float(np.max(np.abs(np.array(a["chi2"]) - np.array(b["chi2"])) / np.abs(np.array(b["chi2"]))))}))

@@ -1149,15 +1149,23 @@ int deftri_debug_sp_product(deftri_ctx *ctx, const deftri_problem_desc *desc, co
     if (ctx->nranks > 1 && !ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "the emulation needs the callback transport");
     SpPlanHost H;
     std::string err;
-    if (!build_sp_plan(*desc, ctx->rank, ctx->nranks, false, H, err)) return fail(ctx, DEFTRI_E_ARG, err);
-    std::function<int(int, int, double *, int64_t)> xf = [ctx](int op, int peer, double *buf, int64_t cnt) {
-        return ctx->xfn(ctx->xuser, op, peer, buf, cnt);
-    };
-    rc = sp_emulate_product(*desc, H, jarap, warap, jrep, wrep, jdep, wdep, lambda, p, q, xf);
-    if (rc) return fail(ctx, DEFTRI_E_ARG, "transfer callback failed");
+    // DEFTRI_SP_EMULATE_TILE=1 (read per call): one rank, one pair — the tile layout's product instead
+    const bool tile = std::getenv("DEFTRI_SP_EMULATE_TILE") != nullptr;
+    if (!build_sp_plan(*desc, ctx->rank, ctx->nranks, false, H, err, tile)) return fail(ctx, DEFTRI_E_ARG, err);
+    if (tile) {
+        if (!H.tile) return fail(ctx, DEFTRI_E_ARG, "no tile layout: " + H.tile_why);
+        rc = sp_emulate_tile_product(*desc, H, jarap, warap, jrep, wrep, jdep, wdep, lambda, p, q, err);
+        if (rc) return fail(ctx, DEFTRI_E_ARG, "tile layout: " + err);
+    } else {
+        std::function<int(int, int, double *, int64_t)> xf = [ctx](int op, int peer, double *buf, int64_t cnt) {
+            return ctx->xfn(ctx->xuser, op, peer, buf, cnt);
+        };
+        rc = sp_emulate_product(*desc, H, jarap, warap, jrep, wrep, jdep, wdep, lambda, p, q, xf);
+        if (rc) return fail(ctx, DEFTRI_E_ARG, "transfer callback failed");
+    }
     if (stats) {
         stats[0] = H.hi - H.lo;
-        stats[1] = H.halo_rows;
+        stats[1] = tile ? 0 : H.halo_rows;
         stats[2] = (int64_t)H.arap_ids.size();
         stats[3] = H.n_arap_owned;
     }
@@ -1202,6 +1210,8 @@ int deftri_get_plan_info(const deftri_ctx *ctx, deftri_plan_info *info) {
         info->cg_collectives = s.cg_collectives();
         info->sharded = s.sharded() ? 1 : 0;
         info->survey_bytes = s.survey_bytes();
+        info->tiles = s.n_tiles();
+        info->halo_overlap = s.halo_overlap() ? 1 : 0;
         return 0;
     }
     if (!ctx->have) return DEFTRI_E_NOPROBLEM;
@@ -1367,8 +1377,10 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
             stats[k].ms += ms;
         }
         for (int32_t k = 0; k < n; k++) {
-            if (!std::strcmp(stats[k].name, "sp_phase1")) stats[k].bytes = ctx->sp->product_bytes_phase(1) * its;
-            if (!std::strcmp(stats[k].name, "sp_phase2")) stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
+            if (!std::strcmp(stats[k].name, "sp_phase1") || !std::strcmp(stats[k].name, "sp_tile"))
+                stats[k].bytes = ctx->sp->product_bytes_phase(1) * its;
+            if (!std::strcmp(stats[k].name, "sp_phase2") || !std::strcmp(stats[k].name, "sp_tupd"))
+                stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
         }
         for (hipEvent_t e : prof.pool) hipEventDestroy(e);
         *n_stats = n;

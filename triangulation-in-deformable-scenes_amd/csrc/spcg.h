@@ -52,6 +52,13 @@ constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 constexpr int64_t kSpMergeMinDof = 50000;  // one rank: the merged (two-launch) CG chain from this many unknowns
+// tile mode (spcg_tile.cpp): one rank, one keyframe pair — the fused product, every ARAP edge read once
+constexpr int kSpTileUnits = 128;          // mesh vertices (keyframe-copy groups) per tile at most
+constexpr int kSpTileLds = 52 * 1024;      // LDS bytes per tile at most (3 workgroups per CU)
+constexpr int kSpTileLdsFixed = 1024;      // the tile kernel's fixed LDS (heavy p, reductions)
+// tile entry meta word 0: LDS rows of p1_j (bits 0-11), p2_j (12-23), flags; word 1: LDS slots of
+// p1_j (0-11), p2_j (12-23), the unit's first tile row (24-31)
+constexpr uint32_t kTmHead = 1u << 24, kTmLast = 1u << 25, kTmSwap = 1u << 26, kTmValid = 1u << 27, kTmCut = 1u << 28;
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0).  kSpTimeout: the merged chain's alpha hand-off was not seen within
 // its poll bound (phase 2's workgroup 0 not resident while the others waited): an error, never a
@@ -105,10 +112,38 @@ struct SpPlanHost {
     int64_t halo_rows = 0;
     double product_bytes = 0;                          // algorithmic bytes of phase 1 + 2 (one CG iteration)
     double phase1_bytes = 0, phase2_bytes = 0;
+    // tile mode (spcg_tile.cpp; the local ARAP edges are then in tile-entry order)
+    bool tile = false;
+    std::string tile_why;                              // why a requested tile layout was not built
+    int32_t ntile = 0, tile_segmax = 1, tile_lds = 0;
+    int64_t tile_entries = 0, tile_cross = 0, tile_halo_rows = 0;
+    std::vector<int32_t> tile_tab;                     // 8 per tile: r0, nr, nh, e0, ne, h0, ns, 0
+    std::vector<uint32_t> tile_m0, tile_m1;            // per entry (padded to 64 per chunk)
+    std::vector<int32_t> tile_chunk;                   // 2 per chunk: first le, first cross slot
+    std::vector<int32_t> tile_rs;                      // per own row: LDS slot begin | count << 16
+    std::vector<int32_t> tile_halo;                    // the tiles' halo rows (local row ids)
+    std::vector<int32_t> tile_xoff, tile_xidx;         // per own row its cross slots (CSR)
+    double tile_bytes[2] = {0, 0};                     // algorithmic bytes per CG iteration: product, update
 };
+// the groups and rows build_tiles needs (spcg_plan.cpp step 5)
+struct TileInput {
+    int32_t P = 0, ng = 0;
+    int64_t E = 0;
+    const int32_t *ap = nullptr;                       // arap_pts [E][4]
+    const int32_t *gpos = nullptr;                     // per point: its group's Morton position
+    const int32_t *row_of_point = nullptr;
+};
+// tile layout of a one-rank, one-pair plan: false (why) when the graph does not fit tile mode; order:
+// the ARAP edges in tile-entry order (the plan's local edge order)
+bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why);
+// host emulation of one tile-mode product with its layout checks (tests; spcg_tile.cpp)
+int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
+                            const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
+                            const double *p, double *q, std::string &why);
 // rank's plan of a validated problem; false (err) when the problem cannot be planned
+// tile: try the tile layout (one rank, one pair; spcg_tile.cpp) — out.tile says whether it was built
 bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &out,
-                   std::string &err);
+                   std::string &err, bool tile = false);
 // host emulation of one sharded product on the plan (tests; spcg_plan.cpp)
 int sp_emulate_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
                        const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
@@ -207,6 +242,16 @@ struct SpDev {
     int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
     double tol2 = 0;
+    // tile mode (G.tile): k_sp_tile (the fused product + p.Ap) and k_sp_tupd (cross slots, alpha, update)
+    int32_t tile = 0, ntile = 0, tile_lds = 0, tile_segmax = 1;
+    const int32_t *ttab = nullptr;                        // [ntile][8]
+    const uint2 *tmeta = nullptr;                         // per entry (word 0, word 1)
+    const int2 *tchunk = nullptr;                         // per chunk (first le, first cross slot)
+    const int32_t *trs = nullptr, *thalo = nullptr, *txoff = nullptr, *txidx = nullptr;
+    double *xc = nullptr;                                 // cross slots [n][3]
+    const double *pinfo = nullptr;                        // per pair: Omega (= W of its ARAP edges)
+    int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
+    int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the
     // per-iteration ones when *lgate == 0; lambda from *lam_dev instead of the launch argument
     const int *gate = nullptr, *lgate = nullptr;
@@ -225,6 +270,7 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
 int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
 int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
+void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) p
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
@@ -264,6 +310,7 @@ class SpSolver {
     // the rows' p.(D + lambda)p terms ((z, p) and D in) and the heavy p (in, out), phase 2 the update
     // (x, r in / out and M in per row, q no longer stored)
     double product_bytes_phase(int k) const {
+        if (G.tile) return H.tile_bytes[k == 1 ? 0 : 1];
         if (k == 1) return H.phase1_bytes + (G.merged ? (double)G.nown * (48 + 48) + (double)G.hd * (16 + 8) : 0.0);
         return H.phase2_bytes + (G.merged ? (double)G.nown * (24 + 24 + 24 + 24 + 48 - 24) : 0.0);
     }
@@ -281,6 +328,8 @@ class SpSolver {
     int32_t n_blocks() const { return G.nblk; }
     int32_t n_row_blocks() const { return G.nrb; }
     int32_t n_arap_local() const { return (int32_t)H.arap_ids.size(); }
+    int32_t n_tiles() const { return G.tile ? G.ntile : 0; }
+    bool halo_overlap() const { return G.sd && G.ovl; }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
         if (G.sd) return 3;                      // + one all-reduce and one grouped send / receive
         if (G.merged) return G.alpha_kernel ? 3 : 2;

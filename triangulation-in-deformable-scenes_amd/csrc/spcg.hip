@@ -227,8 +227,9 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
                 value(m[u], r[u], v, wt, er);
                 if (!in[u]) wt = er = 0.0;
                 add(v, wt, er);
+                if (pj)                                    // (tile mode: no packed slices)
 #pragma unroll
-                for (int a = 0; a < 3; a++) pj[a * n + kk[u]] = (JT)v[a];
+                    for (int a = 0; a < 3; a++) pj[a * n + kk[u]] = (JT)v[a];
             }
             k += U * 64;
         };
@@ -1602,6 +1603,308 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update_sd(int it, const S
     }
 }
 
+// ---- tile mode (spcg_tile.cpp): one rank, one keyframe pair ----------------------------------------
+// k_sp_tile, one workgroup per tile (XCD-dealt like the row blocks) + one for the heavy dofs (last):
+//   P0  p = z + beta p_prev of the tile's rows and halo rows, and of the heavy dofs, into LDS
+//   P1  per entry (one out-edge of a tile vertex; 64-entry chunks, one per wave and round):
+//       t = J_e p, s = W t; the own rows' J^T s summed over the vertex's lanes (segmented scan, the
+//       last lane stores them in LDS); the j rows' J^T s into their LDS slots, or (cut edge) into two
+//       cross slots in HBM; p.Ap += s t; the pair's J_T^T s
+//   P2  per tile row q = own + its LDS slots + (D_v + lambda) p + sum_dep c_e p_s, stored; the row
+//       and depth terms of p.Ap, the depth scales' sums
+//   one fixed-order workgroup sum of [p.Ap, J_T^T s (6), scale sums (2)] into m1part / part
+// k_sp_tupd: the rows' cross slots added, alpha (workgroup 0, the merged chain's hand-off), the update
+// x += alpha p, r -= alpha q, z = M r and the next (r.z, r.r) — phase 2's tail without its slot loop.
+__device__ __forceinline__ double shfl_up_d(double v, int d) {
+    int2 p = __builtin_bit_cast(int2, v);
+    p.x = __shfl_up(p.x, (unsigned)d, 64);
+    p.y = __shfl_up(p.y, (unsigned)d, 64);
+    return __builtin_bit_cast(double, p);
+}
+
+template <class JT>
+__global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
+    extern __shared__ double lds[];
+    __shared__ double red[9][4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
+    double beta;
+    if (it_state(G, it, beta)) return;
+    const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (b == (int)gridDim.x - 1) {                 // the heavy dofs: p for the update, lambda |p_h|^2
+        double pap = 0.0;
+        for (int64_t dd = tid; dd < G.hd; dd += 256) {
+            const double p = pval(G.zp, beta, dd);
+            G.ph[dd] = p;
+            pap += lam * (p * p);
+        }
+        if (!G.include_heavy) pap = 0.0;
+        pap = block_sum(pap, red[0]);
+        if (tid == 0) G.m1part[b] = pap;
+        return;
+    }
+    const int seg = (G.ntile + 7) / 8;
+    const int t = (b & 7) * seg + (b >> 3);
+    double pap = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
+    if (t < G.ntile) {
+        const int32_t *T = G.ttab + 8 * (int64_t)t;
+        const int r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
+        double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
+        for (int i = tid; i < nr + nh; i += 256) {
+            const int row = i < nr ? r0 + i : G.thalo[h0 + i - nr];
+            const int64_t o = G.hd + 3 * (int64_t)row;
+#pragma unroll
+            for (int c = 0; c < 3; c++) pL[3 * i + c] = pval(G.zp, beta, o + c);
+        }
+        for (int i = tid; i < 3 * nr; i += 256) up[i] = 0.0;
+        if (tid < 8) hp[tid] = tid < G.hd ? pval(G.zp, beta, tid) : 0.0;     // T_g (6), scales (<= 2)
+        __syncthreads();
+        const double W = G.pinfo[0];               // W of every ARAP edge of the pair (k_lin_arap: W = Omega)
+        const int64_t jld = G.jld;
+        const uint64_t lt = (1ull << lane) - 1;
+        for (int base = 0; base < ne; base += 256) {
+            if (base + 64 * wv >= ne) break;       // (ne is a multiple of 64: whole waves in or out)
+            const int64_t k = (int64_t)e0 + base + tid;
+            const uint2 m = G.tmeta[k];
+            const int2 ch = G.tchunk[k >> 6];
+            const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
+            const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
+            const int le = ch.x + __popcll(vm & lt);
+            double J[18];
+#pragma unroll
+            for (int c = 0; c < 18; c++) J[c] = valid ? (double)Jarap[c * jld + le] : 0.0;
+            const int ub = (int)(m.y >> 24), sw = (int)((m.x >> 26) & 1u);
+            const int ra = valid ? ub + sw : 0, rb = valid ? ub + 1 - sw : 0;
+            const int rj0 = valid ? (int)(m.x & 0xfffu) : 0, rj1 = valid ? (int)((m.x >> 12) & 0xfffu) : 0;
+            const int rows[4] = {ra, rb, rj0, rj1};
+            double tt = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) tt += J[3 * kk + c] * pL[3 * rows[kk] + c];
+#pragma unroll
+            for (int c = 0; c < 6; c++) tt += J[12 + c] * hp[c];
+            const double s = W * tt;
+            pap += s * tt;
+#pragma unroll
+            for (int c = 0; c < 6; c++) jts[c] += J[12 + c] * s;
+            if (valid) {
+                if (cut) {
+                    const int64_t x = (int64_t)ch.y + 2 * __popcll(cm & lt);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) { G.xc[3 * x + c] = J[6 + c] * s; G.xc[3 * x + 3 + c] = J[9 + c] * s; }
+                } else {
+                    const int s0 = (int)(m.y & 0xfffu), s1 = (int)((m.y >> 12) & 0xfffu);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) { rs[3 * s0 + c] = J[6 + c] * s; rs[3 * s1 + c] = J[9 + c] * s; }
+                }
+            }
+            // the vertex's own rows: inclusive segmented scan over its lanes (segments start at head
+            // lanes; a vertex's lanes are consecutive and never cross the chunk), the last lane stores
+            double v[6];
+#pragma unroll
+            for (int c = 0; c < 6; c++) v[c] = J[c] * s;
+            const int sstart = 63 - __clzll(hm & (lt | (1ull << lane)));
+            for (int d = 1; d < G.tile_segmax; d <<= 1) {
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    const double y = shfl_up_d(v[c], d);
+                    if (lane - d >= sstart) v[c] += y;
+                }
+            }
+            if (valid && (m.x & kTmLast)) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) { up[3 * ra + c] = v[c]; up[3 * rb + c] = v[3 + c]; }
+            }
+        }
+        __syncthreads();
+        if (tid < nr) {
+            const int l = r0 + tid;
+            const int64_t o = G.hd + 3 * (int64_t)l;
+            double q[3], p[3], D[6];
+#pragma unroll
+            for (int c = 0; c < 3; c++) { q[c] = up[3 * tid + c]; p[c] = pL[3 * tid + c]; }
+#pragma unroll
+            for (int kk = 0; kk < 6; kk++) D[kk] = G.Dv[6 * (int64_t)l + kk];
+            const int rsi = G.trs[l], sb = rsi & 0xffff, sc = rsi >> 16;
+            for (int kk = sb; kk < sb + sc; kk++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) q[c] += rs[3 * kk + c];
+            const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
+            const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
+            const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+            pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
+            q[0] += q0; q[1] += q1; q[2] += q2;
+            for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {
+                const int sc_ = G.dsc[j];
+                const double *cd = G.cdep + 3 * (int64_t)j;
+                const double ps = hp[6 + sc_];
+                const double cp = (cd[0] * p[0] + cd[1] * p[1]) + cd[2] * p[2];
+                const double td = cp + G.wss[j] * ps;
+                pap += ps * (cp + td);
+                if (sc_ == 0) sacc[0] += td;
+                else sacc[1] += td;
+#pragma unroll
+                for (int c = 0; c < 3; c++) q[c] += cd[c] * ps;
+            }
+#pragma unroll
+            for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+        }
+    }
+    // [p.Ap, J_T^T s, scale sums]: wave butterflies, then the waves in order
+    double a[9] = {pap, jts[0], jts[1], jts[2], jts[3], jts[4], jts[5], sacc[0], sacc[1]};
+#pragma unroll
+    for (int kk = 0; kk < 9; kk++) {
+        const double v = wave_sum(a[kk]);
+        if (lane == 0) red[kk][wv] = v;
+    }
+    __syncthreads();
+    if (tid < 9) {
+        const double v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+        if (tid == 0) G.m1part[b] = v;
+        else G.part[(int64_t)kSpPart * b + tid - 1] = v;
+    }
+}
+
+// heavy vertex h's sum over the tile workgroups' partials (pair: components 0..5, scale s: 6 + s):
+// thread (g, c) = (tid / 8, tid % 8) adds component c of every 32nd partial, the 32 groups in order
+__device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *lds) {
+    const int nb = G.t_grid - 1;
+    const int dim = h < G.Q ? 6 : 1, off = h < G.Q ? 0 : 6 + (h - G.Q);
+    const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
+    double acc = 0.0;
+    if (c < dim) {
+        int k = g;
+        for (; k + 7 * 32 < nb; k += 8 * 32) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = G.part[(int64_t)kSpPart * (k + 32 * u) + off + c];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; k < nb; k += 32) acc += G.part[(int64_t)kSpPart * k + off + c];
+    }
+    lds[threadIdx.x] = acc;
+    __syncthreads();
+    double t = 0.0;
+    if ((int)threadIdx.x < dim)
+        for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
+    return t;
+}
+
+// FIN 0: the CG update of iteration it (merged-chain hand-off); FIN 1: the product only — q of every
+// row (its cross slots added) and of the heavy dofs stored (the iterative plan's Hessian product)
+template <int FIN>
+__global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double lam) {
+    __shared__ double red4[4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
+    double beta = 0.0;
+    AlphaPre pf;
+    if (!FIN && !G.alpha_kernel && blockIdx.x == 0) m2_alpha_loads(G, it, pf);
+    if (const int st = it_state(G, it, beta)) {
+        if (!FIN && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
+        return;
+    }
+    double alpha = 0.0, pq = 0.0, rr2 = 0.0;
+    if (!FIN) {
+        if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];
+        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true, pf);
+    }
+    if ((int)blockIdx.x < G.m_nh) {
+        __shared__ double lds[256];
+        __shared__ double rsh[6], tz[2][6];
+        const int h = blockIdx.x;
+        const bool has = h < G.Q + G.S;
+        const double th = has ? tile_heavy_sum(G, h, lds) : 0.0;
+        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (has) {
+            const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+            const int a = (!FIN && isnan(alpha)) ? dim : (int)threadIdx.x;
+            double p = 0.0, r = 0.0;
+            if (a < dim) {
+                p = G.ph[o + a];
+                const double q = th + lam * p;
+                if (FIN) {
+                    G.q[o + a] = q;
+                } else {
+                    G.x[o + a] += alpha * p;
+                    r = G.r[o + a] - alpha * q;
+                    G.r[o + a] = r;
+                    rsh[a] = r;
+                }
+            }
+            if (!FIN) {
+                __syncthreads();
+                if (a < dim) {
+                    const double *Mh = h < G.Q ? G.Mh + 36 * (int64_t)h + a * 6 : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+                    double z = 0.0;
+                    for (int c = 0; c < dim; c++) z += Mh[c] * rsh[c];
+                    G.zp[o + a] = make_double2(z, p);
+                    tz[0][a] = r * z;
+                    tz[1][a] = r * r;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0 && !isnan(alpha))
+                    for (int c = 0; c < dim; c++) { pq += tz[0][c]; rr2 += tz[1][c]; }
+            }
+        }
+    } else {
+        const int lb = row_block((int)blockIdx.x - G.m_nh, G.nrb);
+        const int l = lb * 256 + (int)threadIdx.x;
+        const bool on = l < G.nown;
+        double q[3] = {0, 0, 0}, pr[3] = {0, 0, 0}, xo[3] = {0, 0, 0}, ro[3] = {0, 0, 0}, M[6] = {0, 0, 0, 0, 0, 0};
+        int64_t o = 0;
+        if (on) {
+            o = G.hd + 3 * (int64_t)l;
+#pragma unroll
+            for (int c = 0; c < 3; c++) q[c] = G.q[o + c];
+            for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++) {
+                const int64_t x = G.txidx[k];
+#pragma unroll
+                for (int c = 0; c < 3; c++) q[c] += G.xc[3 * x + c];
+            }
+            if (FIN) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const double2 v = G.zp[o + c];
+                    pr[c] = __fma_rn(beta, v.y, v.x);
+                    xo[c] = G.x[o + c];
+                    ro[c] = G.r[o + c];
+                }
+#pragma unroll
+                for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
+            }
+        }
+        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (!FIN && on && !isnan(alpha)) {
+            double r[3], z[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.x[o + c] = xo[c] + alpha * pr[c];
+                r[c] = ro[c] - alpha * q[c];
+            }
+            z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
+            z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
+            z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.r[o + c] = r[c];
+                G.zp[o + c] = make_double2(z[c], pr[c]);
+                pq += r[c] * z[c];
+                rr2 += r[c] * r[c];
+            }
+        }
+    }
+    if (FIN) return;
+    __shared__ double red[2][4];
+    pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
+    m2_dots(G, it, red);
+}
+
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
 __global__ void k_sp_pack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ src,
                           double *__restrict__ buf) {
@@ -1705,6 +2008,16 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         else launch_phase2<double, 2>(G, g2, it, lambda, G.pj, st);
         return;
     }
+    if (G.tile) {
+        // [tiles, XCD-dealt][heavy dofs]; [m_nh heavy workgroups][row blocks]
+        hipEvent_t e0_ = prof_begin(st);
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda);
+        prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
+        if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
+        SPL("sp_tupd", (sp::k_sp_tupd<0>), G.m_nh + sp::row_grid(G.nrb), it, G, lambda);
+        return;
+    }
     if (G.merged) {
         // [m_nx heavy-p / row-term workgroups][phase-1 blocks]; [m_nh heavy workgroups][row blocks]
         // (both extra counts multiples of 8, so the blocks keep their XCD)
@@ -1724,6 +2037,14 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     const int grid = sp::row_grid(G.nrb2) + (G.fuse_heavy ? G.Q + G.S : 0);
     if (fp32) launch_phase2<float, 0>(G, grid, it, lambda, G.pj32, st);
     else launch_phase2<double, 0>(G, grid, it, lambda, G.pj, st);
+}
+
+void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {
+    hipEvent_t e0_ = prof_begin(st);
+    if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda);
+    else hipLaunchKernelGGL((sp::k_sp_tile<double>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda);
+    prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
+    SPL("sp_tupd", (sp::k_sp_tupd<1>), G.m_nh + sp::row_grid(G.nrb), 0, G, lambda);
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }

@@ -107,7 +107,7 @@ inline uint64_t spread21(uint64_t v) {       // bits 0..20 -> every third bit
 }  // namespace
 
 bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &H,
-                   std::string &err) {
+                   std::string &err, bool tile) {
     static const bool timing = std::getenv("DEFTRI_PLAN_TIMING") != nullptr;
     auto t_prev = std::chrono::steady_clock::now();
     auto stage = [&](const char *name) {
@@ -228,6 +228,27 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         for (; next < nranks; next++) H.rank_row_begin[next] = P;
     }
     stage("4 rank ranges");
+    // 4a. tile mode (one rank, one pair; spcg_tile.cpp): the groups cut into tiles in Morton order,
+    //     the ARAP edges in tile-entry order; the rows keep the Morton group order (no 4b sort: a
+    //     tile's rows are one contiguous range)
+    std::vector<int32_t> tile_order;
+    if (tile && nranks == 1 && Q == 1 && S <= 2 && E > 0) {
+        H.lo = H.rank_row_begin[rank];
+        H.hi = H.rank_row_begin[rank + 1];
+        std::vector<int32_t> gp(P);
+        for (int32_t p = 0; p < P; p++) gp[p] = gpos[gid[p]];
+        TileInput ti;
+        ti.P = P; ti.ng = ng; ti.E = E; ti.ap = ap; ti.gpos = gp.data(); ti.row_of_point = H.row_of_point.data();
+        std::string why;
+        H.tile = build_tiles(ti, H, tile_order, why);
+        if (!H.tile) {
+            H.tile_why = why;
+            tile_order.clear();
+        }
+    } else if (tile) {
+        H.tile_why = nranks != 1 ? "sharded" : Q != 1 ? "more than one keyframe pair" : "no ARAP edges";
+    }
+    stage("4a tiles");
     // 4b. inside every rank's range, rows sorted by their phase-2 slot count (ARAP incidences + depth
     //     couplings; descending, stable) in windows of kSpSortWindow rows: the order the phase-2 wave
     //     layout deals them to lanes (8b), so that layout is the identity and a wave's 64 rows are 64
@@ -238,7 +259,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     //     20.9 vs 23.6 with edges by the sorted rows).
     static const bool no_rowsort = std::getenv("DEFTRI_SP_NO_ROWSORT") != nullptr;
     const std::vector<int32_t> mrow = H.row_of_point;     // Morton (pre-sort) row of each point
-    if (!no_rowsort) {
+    if (!no_rowsort && !H.tile) {
         // slot counts per row: per-chunk counts over the incidences on host threads, summed per row
         const int64_t ninc = 4 * E + D;
         const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, ninc / (1 << 20)));
@@ -288,7 +309,9 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     stage("4b slot-count sort");
     // 5. local ARAP edges: owned (point 0 here) first, then halo-only; each by (pair, Morton row of point 0)
     std::vector<int32_t> owned_e, halo_e;
-    if (nranks == 1) {
+    if (H.tile) {
+        owned_e.swap(tile_order);                     // tile-entry order (spcg_tile.cpp)
+    } else if (nranks == 1) {
         owned_e.resize((size_t)E);
         std::iota(owned_e.begin(), owned_e.end(), 0);
     } else {
@@ -298,10 +321,11 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             else if (own(row[ap[4 * e + 1]]) || own(row[ap[4 * e + 2]]) || own(row[ap[4 * e + 3]])) halo_e.push_back((int32_t)e);
         }
     }
-    for (auto *lst : {&owned_e, &halo_e}) {
-        par_counting_sort(*lst, P, [&](int32_t e) { return mrow[ap[4 * (int64_t)e]]; });
-        par_counting_sort(*lst, std::max(Q, 1), [&](int32_t e) { return d.arap_pair[e]; });
-    }
+    if (!H.tile)
+        for (auto *lst : {&owned_e, &halo_e}) {
+            par_counting_sort(*lst, P, [&](int32_t e) { return mrow[ap[4 * (int64_t)e]]; });
+            par_counting_sort(*lst, std::max(Q, 1), [&](int32_t e) { return d.arap_pair[e]; });
+        }
     H.n_arap_owned = (int32_t)owned_e.size();
     H.arap_ids = owned_e;
     H.arap_ids.insert(H.arap_ids.end(), halo_e.begin(), halo_e.end());
@@ -590,6 +614,16 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                      + (double)H.inc.size() * (4 + 8 + jb / 6)           // slot index, s, packed J slice
                      + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
+    if (H.tile) {
+        // tile mode per CG iteration: k_sp_tile — per entry J + meta (padding: meta only), per tile
+        // row (z, p) + D + q out + slot range + its depth couplings (c, W J_s^2, scale, offset), per halo
+        // row (z, p), per cut entry two cross slots out; k_sp_tupd — per own row (z, p) in / out, x and r
+        // in / out, q in, M, cross range, per cross slot its index and value
+        const int64_t nvalid = (int64_t)H.arap_ids.size();
+        H.tile_bytes[0] = (double)nvalid * jb + (double)H.tile_entries * 8 + (double)nown * (48 + 48 + 24 + 4 + 4) +
+                          (double)ndl * (24 + 8 + 4) + (double)H.tile_halo_rows * 48 + (double)H.tile_cross * 24;
+        H.tile_bytes[1] = (double)nown * (96 + 48 + 48 + 24 + 48 + 4) + (double)H.tile_cross * (4 + 24);
+    }
     static const bool digest = std::getenv("DEFTRI_PLAN_DIGEST") != nullptr;
     if (digest) {
         // FNV-1a over every plan array: a rewrite of the build is checked against the previous one

@@ -206,7 +206,13 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G = SpDev();
     static const bool timing = std::getenv("DEFTRI_UPLOAD_TIMING") != nullptr;
     const auto tu0 = std::chrono::steady_clock::now();
-    if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err)) return DEFTRI_E_ARG;
+    // tile mode (spcg_tile.cpp: the fused product, every ARAP edge read once per CG iteration): one
+    // rank on the merged chain, one keyframe pair; DEFTRI_SP_NO_TILE=1 keeps the two-phase product
+    static const bool no_tile = std::getenv("DEFTRI_SP_NO_TILE") != nullptr;
+    const int64_t ndof_ = 6 * (int64_t)d.n_pairs + d.n_scales + 3 * (int64_t)d.n_points;
+    const bool want_tile = !shard_ && !no_tile && !std::getenv("DEFTRI_SP_NO_FUSE") && !std::getenv("DEFTRI_SP_NO_MERGE") &&
+                           d.n_pairs == 1 && (ndof_ >= kSpMergeMinDof || std::getenv("DEFTRI_SP_MERGE"));
+    if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err, want_tile)) return DEFTRI_E_ARG;
     const auto tu1 = std::chrono::steady_clock::now();
     struct Report {                 // DEFTRI_UPLOAD_TIMING=1: plan build vs the rest of the upload
         bool on; std::chrono::steady_clock::time_point a, b;
@@ -353,7 +359,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         uint8_t *ws;
         PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx); PUT(ws, H.wsplit);
         G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi; G.wsplit = ws;
-        if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
+        if (H.tile && G.merged) { G.pj = nullptr; G.pj32 = nullptr; }   // the fused product reads J once
+        else if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
         else { ALLOC(G.pj, 3 * 64 * G.nslots); }
         H.pmap.clear(); H.pmap.shrink_to_fit();
         H.pidx.clear(); H.pidx.shrink_to_fit();
@@ -372,12 +379,34 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     double *zp;
     ALLOC(zp, 2 * zp_n);
     G.zp = reinterpret_cast<double2 *>(zp);
-    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * G.nblk); ALLOC(G.rpart, std::max(G.nrb2, 1));
+    if (H.tile && G.merged) {
+        G.tile = 1;
+        G.ntile = H.ntile;
+        G.tile_lds = H.tile_lds;
+        G.tile_segmax = H.tile_segmax;
+        G.t_grid = 8 * ((H.ntile + 7) / 8) + 1;
+        int32_t *tt, *trs, *th, *txo, *txi, *tch;
+        uint32_t *tm;
+        PUT(tt, H.tile_tab); PUT(trs, H.tile_rs); PUT(th, H.tile_halo); PUT(txo, H.tile_xoff); PUT(txi, H.tile_xidx);
+        PUT(tch, H.tile_chunk);
+        {
+            std::vector<uint32_t> mm(2 * H.tile_m0.size());
+            for (size_t k = 0; k < H.tile_m0.size(); k++) { mm[2 * k] = H.tile_m0[k]; mm[2 * k + 1] = H.tile_m1[k]; }
+            PUT(tm, mm);
+        }
+        G.ttab = tt; G.trs = trs; G.thalo = th; G.txoff = txo; G.txidx = txi;
+        G.tchunk = reinterpret_cast<const int2 *>(tch);
+        G.tmeta = reinterpret_cast<const uint2 *>(tm);
+        ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));
+        G.pinfo = P.pair_info;
+    }
+    ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
     ALLOC(G.rec, kSpRecDoubles + (int64_t)kSpRed * (kSpMaxIt + 2));
     ALLOC(G.ph, std::max<int64_t>(H.hd, 1));
-    G.m1n = sp_merged_grid1(G);
-    ALLOC(G.m1part, G.m1n); ALLOC(G.m2part, 2 * (int64_t)sp_merged_grid2(G)); ALLOC(G.gsum, 32);
+    G.m1n = G.tile ? G.t_grid : sp_merged_grid1(G);
+    ALLOC(G.m1part, std::max(G.m1n, sp_merged_grid1(G)));
+    ALLOC(G.m2part, 2 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb + 7) / 8))); ALLOC(G.gsum, 32);
     if (std::getenv("DEFTRI_SP_P2_TRACE")) {               // diagnostics: phase-2 wave stamps
         const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
         ALLOC(G.p2tr, 6 * nw);
@@ -1167,8 +1196,12 @@ int SpSolver::hessian_product(double lambda, const double *x, double *y, int64_t
     g.merged = 0; g.fuse = 0; g.fuse_heavy = 0;
     g.max_it = 1;
     g.tol2 = 0.0;
-    sp_launch_product(g, 0, lambda, fp32_jac != 0, st_);
-    sp_launch_heavy(g, 0, lambda, 0, st_);
+    if (G.tile) {                                  // the fused product + its cross slots and heavy sums
+        sp_launch_tile_product(g, lambda, fp32_jac != 0, st_);
+    } else {
+        sp_launch_product(g, 0, lambda, fp32_jac != 0, st_);
+        sp_launch_heavy(g, 0, lambda, 0, st_);
+    }
     sp_launch_permute_out(G.P, G.hd, d_row_of_point, G.q, d_dx0, st_);
     SPOK(hipMemcpyAsync(y, d_dx0, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, st_));
     SPOK(hipStreamSynchronize(st_));

@@ -1,0 +1,388 @@
+// spcg_tile.cpp — the tile layout of the iterative plan's fused product (spcg.h "tile mode").
+//
+// One rank, one keyframe pair (the two-view graphs of BASELINE C2 and the 500k north-star size,
+// g2oBundleAdjustment.cc:640-953 with one pair): the product q = (H + lambda I) p is formed by ONE
+// edge pass in which every ARAP edge is read once.  The mesh vertices' keyframe-copy groups (2 rows
+// each: p1_i, p2_i) are cut, in Morton order, into tiles of consecutive groups; a tile is one
+// workgroup.  An edge (p1_i, p2_i, p1_j, p2_j, T_g) belongs to the tile of its vertex i ("out-edge");
+// its contribution J_{p1_i}^T s, J_{p2_i}^T s to the own rows is summed over the edges of the same
+// vertex (consecutive lanes, a segmented wave scan), its contribution to the rows of j goes to an LDS
+// slot of j's row when j is in the tile, else to a cross slot in HBM that the update launch adds
+// ("cut" edge).  So s_e never leaves the workgroup and J is read once — where the two-phase chain read
+// J in phase 1, stored s_e and read J again (packed per slot) in phase 2.
+//
+// Layout (per tile, 64-entry chunks = one wave per round):
+//   entries  the tile's out-edges grouped by vertex (unit), vertices in Morton order; a unit never
+//            straddles a chunk (the chunk is padded instead); local edge le = the order of the valid
+//            entries (so J, W, E, chi of the edges are in entry order: the loads of a chunk coalesce)
+//   meta     2 words per entry (spcg.h kTm*): word0 = the LDS rows of p1_j, p2_j (12 bits each) and
+//            the flags (segment head / last, swap: p1_i is the group's second row, valid, cut);
+//            word1 = the LDS remote slots of p1_j, p2_j (12 bits each) and the unit's first row (8)
+//   chunk    per 64 entries: the le of its first valid entry, its first cross slot
+//   rows     the tile's own rows (consecutive), then its halo rows (rows of cut edges' j vertices)
+//   slots    per own row its incoming LDS contributions, contiguous (row r: trs[r] = begin | count << 16)
+//   cross    per own row (all tiles) the cross slots aimed at it, in source order (xoff / xidx)
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "spcg.h"
+
+namespace deftri {
+
+bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why) {
+    const int32_t ng = in.ng;
+    const int64_t E = in.E;
+    const int32_t *ap = in.ap;
+    static const int umax = [] {
+        const char *e = std::getenv("DEFTRI_SP_TILE_UNITS");
+        const int v = e ? std::atoi(e) : kSpTileUnits;
+        return std::max(8, std::min(v, 128));
+    }();
+    static const int64_t lds_budget = [] {
+        const char *e = std::getenv("DEFTRI_SP_TILE_LDS");
+        return (int64_t)(e ? std::atoi(e) : kSpTileLds);
+    }();
+    // groups: size and first row (rows of a group are consecutive, groups in Morton order)
+    std::vector<int32_t> gsz(ng, 0), grow(ng, INT32_MAX);
+    for (int32_t p = 0; p < in.P; p++) {
+        const int32_t g = in.gpos[p];
+        gsz[g]++;
+        grow[g] = std::min(grow[g], in.row_of_point[p]);
+    }
+    for (int32_t g = 0; g < ng; g++)
+        if (gsz[g] > 2) { why = "a keyframe-copy group of more than 2 rows"; return false; }
+    // out-edges per group (edge order inside a group), in-edge sources per group
+    std::vector<int64_t> ooff(ng + 1, 0), ioff(ng + 1, 0);
+    for (int64_t e = 0; e < E; e++) {
+        const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
+        if (gi != in.gpos[ap[4 * e + 1]] || gj != in.gpos[ap[4 * e + 3]] || gi == gj) { why = "an edge's copies in two groups"; return false; }
+        ooff[gi + 1]++;
+        ioff[gj + 1]++;
+    }
+    for (int32_t g = 0; g < ng; g++) { ooff[g + 1] += ooff[g]; ioff[g + 1] += ioff[g]; }
+    std::vector<int32_t> oe(E), isrc(E);
+    {
+        std::vector<int64_t> fo(ooff.begin(), ooff.end() - 1), fi(ioff.begin(), ioff.end() - 1);
+        for (int64_t e = 0; e < E; e++) {
+            const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
+            oe[fo[gi]++] = (int32_t)e;
+            isrc[fi[gj]++] = gi;
+        }
+    }
+    for (int32_t g = 0; g < ng; g++)
+        if (ooff[g + 1] - ooff[g] > 64) { why = "a vertex with more than 64 ARAP edges"; return false; }
+    // (a group with edges holds p1_i and p2_i: 2 rows; a 1-row group has no ARAP edge)
+    // 1. greedy partition: consecutive groups while rows <= 2 umax and the LDS estimate fits
+    auto lds_of = [&](int64_t nr, int64_t nh, int64_t ns) { return 24 * (nr + nh) + 24 * nr + 24 * ns + kSpTileLdsFixed; };
+    std::vector<int32_t> tstart;
+    std::vector<int32_t> hcnt(ng, 0), stamp(ng, -1);
+    {
+        int32_t gs = 0, attempt = 0;
+        int64_t nr = 0, nh = 0, ns = 0, units = 0;
+        std::vector<int32_t> halo_members;
+        tstart.push_back(0);
+        for (int32_t g = 0; g < ng;) {
+            // tentative add of g (stamp: the halo groups this attempt already counted)
+            int64_t dnh = 0, dns = 0;
+            attempt++;
+            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
+                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                if (gj >= gs && gj < g) dns += 2;
+                else if (hcnt[gj] == 0 && stamp[gj] != attempt) { stamp[gj] = attempt; dnh += gsz[gj]; }
+            }
+            for (int64_t k = ioff[g]; k < ioff[g + 1]; k++)
+                if (isrc[k] >= gs && isrc[k] < g) dns += 2;
+            if (hcnt[g] > 0) dnh -= gsz[g];
+            const bool fits = units + 1 <= umax && lds_of(nr + gsz[g], nh + dnh, ns + dns) <= lds_budget &&
+                              nr + gsz[g] + nh + dnh < 4096 && ns + dns < 4096;
+            if (!fits && units > 0) {
+                // close the tile [gs, g): clear its halo counts
+                for (int32_t h : halo_members) hcnt[h] = 0;
+                halo_members.clear();
+                gs = g;
+                nr = nh = ns = units = 0;
+                tstart.push_back(g);
+                continue;
+            }
+            // commit
+            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
+                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                if (!(gj >= gs && gj < g)) {
+                    if (hcnt[gj]++ == 0) halo_members.push_back(gj);
+                }
+            }
+            hcnt[g] = 0;                           // g is a tile row now, no longer halo
+            nr += gsz[g];
+            nh += dnh;
+            ns += dns;
+            units++;
+            g++;
+        }
+        for (int32_t h : halo_members) hcnt[h] = 0;
+        tstart.push_back(ng);
+    }
+    const int32_t nt = (int32_t)tstart.size() - 1;
+    // 2. entries, le order, per tile rows / halo / slots
+    H.tile_tab.assign(8 * (size_t)nt, 0);
+    order.clear();
+    order.reserve(E);
+    std::vector<uint32_t> &m0 = H.tile_m0, &m1 = H.tile_m1;
+    m0.clear(); m1.clear();
+    H.tile_chunk.clear();
+    H.tile_halo.clear();
+    const int32_t nown = H.hi - H.lo;
+    H.tile_rs.assign(nown, 0);
+    // cross slots: (target row, slot) pairs, CSR by row at the end
+    std::vector<std::pair<int32_t, int32_t>> xt;
+    int64_t nx = 0;
+    int32_t segmax = 1, max_lds = 0;
+    std::vector<int32_t> lrow(ng, -1);            // group -> LDS row base inside the current tile
+    std::vector<int32_t> slotcnt, slotfill;       // per tile row
+    for (int32_t t = 0; t < nt; t++) {
+        const int32_t g0 = tstart[t], g1 = tstart[t + 1];
+        const int32_t r0 = grow[g0] - H.lo;
+        int32_t nr = 0;
+        for (int32_t g = g0; g < g1; g++) { lrow[g] = nr; nr += gsz[g]; }
+        // halo groups, ascending
+        std::vector<int32_t> hg;
+        for (int32_t g = g0; g < g1; g++)
+            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
+                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                if (gj < g0 || gj >= g1) hg.push_back(gj);
+            }
+        std::sort(hg.begin(), hg.end());
+        hg.erase(std::unique(hg.begin(), hg.end()), hg.end());
+        const int32_t h0 = (int32_t)H.tile_halo.size();
+        int32_t nh = 0;
+        for (int32_t gj : hg) {
+            lrow[gj] = nr + nh;
+            for (int32_t k = 0; k < gsz[gj]; k++) H.tile_halo.push_back(grow[gj] + k - H.lo);
+            nh += gsz[gj];
+        }
+        // remote slots: count per tile row, in entry order
+        slotcnt.assign(nr, 0);
+        for (int32_t g = g0; g < g1; g++)
+            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
+                const int64_t e = oe[k];
+                const int32_t gj = in.gpos[ap[4 * e + 2]];
+                if (gj >= g0 && gj < g1) {
+                    slotcnt[in.row_of_point[ap[4 * e + 2]] - H.lo - r0]++;
+                    slotcnt[in.row_of_point[ap[4 * e + 3]] - H.lo - r0]++;
+                }
+            }
+        slotfill.assign(nr, 0);
+        int32_t ns = 0;
+        for (int32_t r = 0; r < nr; r++) {
+            slotfill[r] = ns;
+            if (slotcnt[r] > 0xffff) { why = "too many slots on a row"; return false; }
+            H.tile_rs[r0 + r] = ns | slotcnt[r] << 16;
+            ns += slotcnt[r];
+        }
+        // entries
+        const int64_t e0 = (int64_t)m0.size();       // chunk aligned
+        int fill = 0;
+        auto pad_chunk = [&]() {
+            while (fill % 64) {
+                m0.push_back(kTmHead);              // padding: its own (empty) segment
+                m1.push_back(0);
+                fill++;
+            }
+        };
+        auto chunk_start = [&]() {
+            if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)order.size()), H.tile_chunk.push_back((int32_t)nx);
+        };
+        for (int32_t g = g0; g < g1; g++) {
+            const int64_t k0 = ooff[g], k1 = ooff[g + 1];
+            const int cnt = (int)(k1 - k0);
+            if (cnt == 0) continue;
+            segmax = std::max(segmax, cnt);
+            if (fill % 64 + cnt > 64) pad_chunk();
+            for (int64_t k = k0; k < k1; k++) {
+                chunk_start();
+                const int64_t e = oe[k];
+                const int32_t gj = in.gpos[ap[4 * e + 2]];
+                const bool cut = gj < g0 || gj >= g1;
+                const int32_t ra = in.row_of_point[ap[4 * e]] - H.lo - r0;       // tile rows of p1_i, p2_i
+                const int32_t ub = lrow[g];
+                const uint32_t swap = ra == ub + 1 ? 1u : 0u;
+                // LDS rows of p1_j, p2_j: tile rows, or the halo rows after them
+                auto ldsrow = [&](int32_t pt) {
+                    const int32_t row = in.row_of_point[pt] - H.lo;
+                    return cut ? lrow[gj] + (row - grow[gj] + H.lo) : row - r0;
+                };
+                const uint32_t rj0 = (uint32_t)ldsrow(ap[4 * e + 2]), rj1 = (uint32_t)ldsrow(ap[4 * e + 3]);
+                uint32_t w0 = rj0 | rj1 << 12 | kTmValid | swap * kTmSwap;
+                if (k == k0) w0 |= kTmHead;
+                if (k == k1 - 1) w0 |= kTmLast;
+                uint32_t w1 = (uint32_t)ub << 24;
+                if (cut) {
+                    w0 |= kTmCut;
+                    xt.push_back({in.row_of_point[ap[4 * e + 2]] - H.lo, (int32_t)nx});
+                    xt.push_back({in.row_of_point[ap[4 * e + 3]] - H.lo, (int32_t)nx + 1});
+                    nx += 2;
+                } else {
+                    const int32_t s0 = slotfill[rj0]++, s1 = slotfill[rj1]++;
+                    w1 |= (uint32_t)s0 | (uint32_t)s1 << 12;
+                }
+                m0.push_back(w0);
+                m1.push_back(w1);
+                order.push_back((int32_t)e);
+                fill++;
+            }
+        }
+        if (fill == 0) { chunk_start(); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
+        pad_chunk();
+        const int64_t ne = (int64_t)m0.size() - e0;
+        int32_t *T = &H.tile_tab[8 * (size_t)t];
+        T[0] = r0; T[1] = nr; T[2] = nh; T[3] = (int32_t)e0; T[4] = (int32_t)ne; T[5] = h0; T[6] = ns; T[7] = 0;
+        max_lds = std::max<int32_t>(max_lds, (int32_t)lds_of(nr, nh, ns));
+        for (int32_t g = g0; g < g1; g++) lrow[g] = -1;
+        for (int32_t gj : hg) lrow[gj] = -1;
+    }
+    if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
+    // cross slots by target row, source order inside a row
+    std::stable_sort(xt.begin(), xt.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    H.tile_xoff.assign(nown + 1, 0);
+    H.tile_xidx.resize(xt.size());
+    for (const auto &x : xt) H.tile_xoff[x.first + 1]++;
+    for (int32_t l = 0; l < nown; l++) H.tile_xoff[l + 1] += H.tile_xoff[l];
+    for (size_t k = 0; k < xt.size(); k++) H.tile_xidx[k] = xt[k].second;
+    H.ntile = nt;
+    H.tile_entries = (int64_t)m0.size();
+    H.tile_cross = nx;
+    H.tile_segmax = segmax;
+    H.tile_lds = max_lds;
+    H.tile_halo_rows = (int64_t)H.tile_halo.size();
+    return true;
+}
+
+}  // namespace deftri
+
+namespace deftri {
+
+// Host emulation of one tile-mode product q = (H + lambda I) p (tests, no GPU): k_sp_tile's entry
+// walk — le and cross slots from the chunk bases and the valid / cut lanes before an entry, the own
+// rows' sums, the LDS remote slots and the cross slots — then k_sp_tupd's cross sums, with the layout
+// checked on the way: every LDS slot and every cross slot written exactly once and read exactly once.
+// J / W in the problem's edge order; q in problem order.  Returns 0, or -1 (why) on a layout fault.
+int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
+                            const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
+                            const double *p, double *q, std::string &why) {
+    if (!H.tile) { why = "not a tile plan"; return -1; }
+    const int64_t hd = H.hd, ndof = hd + 3 * (int64_t)H.P;
+    const int32_t Q = H.Q, nown = H.hi - H.lo;
+    std::vector<double> pl(ndof, 0.0), qr(ndof, 0.0);
+    for (int64_t k = 0; k < hd; k++) pl[k] = p[k];
+    for (int32_t r = 0; r < H.P; r++)
+        for (int c = 0; c < 3; c++) pl[hd + 3 * (int64_t)r + c] = p[hd + 3 * (int64_t)H.point_of_row[r] + c];
+    std::vector<double> hsum(hd, 0.0), xc(3 * std::max<int64_t>(H.tile_cross, 1), 0.0);
+    std::vector<int> xw(std::max<int64_t>(H.tile_cross, 1), 0), xr(std::max<int64_t>(H.tile_cross, 1), 0);
+    std::vector<int> lew(H.arap_ids.size(), 0);
+    for (int32_t t = 0; t < H.ntile; t++) {
+        const int32_t *T = &H.tile_tab[8 * (size_t)t];
+        const int32_t r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
+        if (e0 % 64 || ne % 64) { why = "tile entries not chunk aligned"; return -1; }
+        std::vector<double> pL(3 * (size_t)(nr + nh)), up(3 * (size_t)nr, 0.0), rs(3 * (size_t)std::max(ns, 1), 0.0);
+        std::vector<int> rsw(std::max(ns, 1), 0), rsr(std::max(ns, 1), 0);
+        for (int32_t i = 0; i < nr + nh; i++) {
+            const int32_t row = i < nr ? r0 + i : H.tile_halo[h0 + i - nr];
+            for (int c = 0; c < 3; c++) pL[3 * (size_t)i + c] = pl[hd + 3 * (int64_t)row + c];
+        }
+        int nv = 0, nc = 0;
+        for (int32_t k = 0; k < ne; k++) {
+            const int64_t ke = (int64_t)e0 + k;
+            if ((ke & 63) == 0) nv = nc = 0;
+            const uint32_t m0 = H.tile_m0[ke], m1 = H.tile_m1[ke];
+            const int32_t *ch = &H.tile_chunk[2 * (size_t)(ke >> 6)];
+            if (!(m0 & kTmValid)) continue;
+            const int64_t le = ch[0] + nv++;
+            const bool cut = (m0 & kTmCut) != 0;
+            const int64_t x = ch[1] + 2 * (int64_t)(cut ? nc++ : nc);
+            if (le >= (int64_t)H.arap_ids.size()) { why = "le out of range"; return -1; }
+            lew[le]++;
+            const int64_t e = H.arap_ids[le];
+            const double *J = Ja + 18 * e;
+            const int ub = (int)(m1 >> 24), sw = (int)((m0 >> 26) & 1u);
+            const int rows[4] = {ub + sw, ub + 1 - sw, (int)(m0 & 0xfffu), (int)((m0 >> 12) & 0xfffu)};
+            for (int kk = 0; kk < 4; kk++) {
+                const int32_t lim = kk < 2 ? nr : nr + nh;
+                if (rows[kk] < 0 || rows[kk] >= lim) { why = "an entry's LDS row out of range"; return -1; }
+                // the LDS row must hold the edge's point
+                const int32_t prow = H.row_of_point[d.arap_pts[4 * e + kk]];
+                const int32_t lrow = rows[kk] < nr ? r0 + rows[kk] : H.tile_halo[h0 + rows[kk] - nr];
+                if (prow != lrow) { why = "an entry's LDS row is not its point's row"; return -1; }
+            }
+            double tt = 0.0;
+            for (int kk = 0; kk < 4; kk++)
+                for (int c = 0; c < 3; c++) tt += J[3 * kk + c] * pL[3 * (size_t)rows[kk] + c];
+            for (int c = 0; c < 6; c++) tt += J[12 + c] * pl[6 * (int64_t)d.arap_pair[e] + c];
+            const double s = Wa[e] * tt;
+            for (int c = 0; c < 6; c++) hsum[6 * (int64_t)d.arap_pair[e] + c] += J[12 + c] * s;
+            for (int c = 0; c < 3; c++) { up[3 * (size_t)rows[0] + c] += J[c] * s; up[3 * (size_t)rows[1] + c] += J[3 + c] * s; }
+            if (cut) {
+                if (x < 0 || x + 2 > H.tile_cross) { why = "cross slot out of range"; return -1; }
+                xw[x]++; xw[x + 1]++;
+                for (int c = 0; c < 3; c++) { xc[3 * x + c] = J[6 + c] * s; xc[3 * (x + 1) + c] = J[9 + c] * s; }
+            } else {
+                const int s0 = (int)(m1 & 0xfffu), s1 = (int)((m1 >> 12) & 0xfffu);
+                if (s0 >= ns || s1 >= ns) { why = "LDS slot out of range"; return -1; }
+                rsw[s0]++; rsw[s1]++;
+                for (int c = 0; c < 3; c++) { rs[3 * (size_t)s0 + c] = J[6 + c] * s; rs[3 * (size_t)s1 + c] = J[9 + c] * s; }
+            }
+        }
+        for (int32_t tr = 0; tr < nr; tr++) {
+            const int32_t l = r0 + tr;
+            const int rsi = H.tile_rs[l], sb = rsi & 0xffff, sc = rsi >> 16;
+            double acc[3];
+            for (int c = 0; c < 3; c++) acc[c] = up[3 * (size_t)tr + c] + lambda * pL[3 * (size_t)tr + c];
+            for (int k = sb; k < sb + sc; k++) {
+                if (k >= ns) { why = "row slot range out of range"; return -1; }
+                rsr[k]++;
+                for (int c = 0; c < 3; c++) acc[c] += rs[3 * (size_t)k + c];
+            }
+            const int64_t o = hd + 3 * (int64_t)l;
+            for (int32_t j = H.rep_off[l]; j < H.rep_off[l + 1]; j++) {
+                const int64_t e = H.rep_ids[j];
+                const double *J = Jr + 6 * e;
+                for (int rr = 0; rr < 2; rr++) {
+                    double tt = 0;
+                    for (int c = 0; c < 3; c++) tt += J[3 * rr + c] * pl[o + c];
+                    for (int c = 0; c < 3; c++) acc[c] += J[3 * rr + c] * Wr[e] * tt;
+                }
+            }
+            for (int32_t j = H.dep_off[l]; j < H.dep_off[l + 1]; j++) {
+                const int64_t e = H.dep_ids[j];
+                const double *J = Jd + 4 * e;
+                const int32_t sc_ = d.dep_scale[e];
+                double tt = J[3] * pl[6 * (int64_t)Q + sc_];
+                for (int c = 0; c < 3; c++) tt += J[c] * pl[o + c];
+                for (int c = 0; c < 3; c++) acc[c] += J[c] * Wd[e] * tt;
+                hsum[6 * (int64_t)Q + sc_] += J[3] * Wd[e] * tt;
+            }
+            for (int c = 0; c < 3; c++) qr[o + c] = acc[c];
+        }
+        for (int32_t k = 0; k < ns; k++)
+            if (rsw[k] != 1 || rsr[k] != 1) { why = "an LDS slot not written / read exactly once"; return -1; }
+    }
+    for (size_t le = 0; le < lew.size(); le++)
+        if (lew[le] != 1) { why = "a local edge not visited exactly once"; return -1; }
+    for (int32_t l = 0; l < nown; l++)
+        for (int32_t k = H.tile_xoff[l]; k < H.tile_xoff[l + 1]; k++) {
+            const int64_t x = H.tile_xidx[k];
+            xr[x]++;
+            for (int c = 0; c < 3; c++) qr[hd + 3 * (int64_t)l + c] += xc[3 * x + c];
+        }
+    for (int64_t x = 0; x < H.tile_cross; x++)
+        if (xw[x] != 1 || xr[x] != 1) { why = "a cross slot not written / read exactly once"; return -1; }
+    for (int64_t k = 0; k < ndof; k++) q[k] = 0.0;
+    for (int32_t r = 0; r < H.P; r++)
+        for (int c = 0; c < 3; c++) q[hd + 3 * (int64_t)H.point_of_row[r] + c] = qr[hd + 3 * (int64_t)r + c];
+    for (int64_t k = 0; k < hd; k++) q[k] = hsum[k] + lambda * pl[k];
+    return 0;
+}
+
+}  // namespace deftri

@@ -122,7 +122,7 @@ class PlanInfo(C.Structure):
     _fields_ = [("plan", i32), ("rank", i32), ("nranks", i32), ("own_rows", i32), ("halo_rows", i64),
                 ("local_arap_edges", i64), ("n_unknowns", i64), ("phase1_blocks", i32), ("row_blocks", i32),
                 ("product_bytes", f64), ("jacobian_fp32", i32), ("cg_launches", i32), ("cg_collectives", i32),
-                ("sharded", i32), ("survey_bytes", f64)]
+                ("sharded", i32), ("survey_bytes", f64), ("tiles", i32), ("halo_overlap", i32)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
