@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 6
+#define DEFTRI_ABI_VERSION 7
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -394,7 +394,9 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
                          int32_t max_stats, int32_t *n_stats);
 
 /* sizeof() of the ABI structs for binding checks: 0 deftri_problem_desc, 1 deftri_lm_params,
-   2 deftri_report, 3 deftri_keyframe, 4 deftri_map, 5 deftri_ba_desc, 6 deftri_pixels_error. */
+   2 deftri_report, 3 deftri_keyframe, 4 deftri_map, 5 deftri_ba_desc, 6 deftri_pixels_error,
+   7 deftri_plan_info, 8 deftri_deformation_params, 9 deftri_deformation_report,
+   10 deftri_deformation_eval. */
 int64_t deftri_sizeof(int32_t which);
 
 /* ---- map-level API (Modules/Optimization/g2oBundleAdjustment.h:56-60) ---------------- */
@@ -516,6 +518,69 @@ int deftri_set_pair_window(deftri_ctx *ctx, int32_t window);
 int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_weight,
                             double arap_weight, float depth_error,
                             const deftri_problem_desc **desc_out);
+
+/* ---- deformationOptimization (g2oBundleAdjustment.cc:446-606), round 5 --------------------
+   The outer loop in native code: rounds i = 1 .. n_optimizations while the last round's update
+   sum ||p_old - p_new|| >= 1e-4 n_map_points (:482).  A round of selection 0 ("g2oArap") is one
+   arapOptimization with the current weights; selection 1 ("twoOptimizations" + weightsSelection
+   "nlopt", the Simulation.yaml default) first runs NLopt's LN_NELDERMEAD over (rep, global, arap)
+   within [lb, ub] (xtol_rel, xtol_abs, maxeval; :486-530) — NLopt 2.x's nldrmd.c with its default
+   initial step, elimdim and relstop restated (deftri/nlopt_nm.py is the same algorithm) — whose
+   every evaluation is outerObjective (nloptOptimization.cc:4-37): arapOptimization on a clone of
+   the map as the round started (Map::clone, Map.cc:30-58: here a copy of the positions, depth
+   scales and global-transformation table, the rest shared read-only), then calculatePixelsStandDev
+   on the device, f = log(desvc1)^2 + log(desvc2)^2; then arapOptimization on the map itself with
+   the optimum, whose weights the next round starts from.  The map's positions and depth scales are
+   written back in place after every round and global_t holds the last T_g; the global table the
+   next round reads is updated as Map::insertGlobalKeyFramesTransformation(0, 1, T) does
+   (Map.cc:323-330: T and its fp32 inverse).  The Eigen-LM weight search (weightsSelection
+   "eigen", EigenOptimization.h) is not built (its functor reads 3 of 2 declared inputs). */
+typedef struct deftri_deformation_params {
+    int32_t selection;            /* 0 g2oArap (fixed weights), 1 twoOptimizations + nlopt */
+    double  rep, global, arap;    /* Optimization.* weights: the search's start */
+    double  alpha, beta;          /* stored on the ARAP edges, unused by their error (as the reference) */
+    float   depth_error;          /* sigma_d (m) */
+    int32_t n_iterations;         /* LM iterations per arapOptimization (Optimization.numberOfIterations) */
+    int32_t n_optimizations;      /* outer rounds at most (Optimization.numberOfOptimizations) */
+    double  lb[3], ub[3];         /* nlopt bounds of (rep, global, arap) */
+    double  xtol_rel, xtol_abs;   /* nlopt.relTolerance / absTolerance */
+    int32_t maxeval;              /* nlopt.numberOfIterations */
+    int32_t n_map_points;         /* |MapPoints| of the map (the stop test's scale) */
+} deftri_deformation_params;
+typedef struct deftri_deformation_eval {
+    int32_t round, eval;          /* 1-based round, 1-based evaluation inside the round's search */
+    double  x[3], f;              /* the weights evaluated and outerObjective's value */
+} deftri_deformation_eval;
+typedef struct deftri_deformation_report {
+    int32_t rounds;               /* outer rounds run */
+    int32_t arap_calls;           /* arapOptimization calls (evaluations + one per round) */
+    double  weights[3];           /* the last round's weights */
+    double  minf;                 /* the last search's best objective */
+    int32_t nlopt_result;         /* the last search's result code (1 success, 4 xtol, 5 maxeval, -1 failure) */
+    double  update;               /* the last round's update */
+    double  seconds;              /* wall time of the call */
+    deftri_deformation_eval *evals;   /* caller's buffer (may be NULL): every evaluation, in order */
+    int32_t max_evals, n_evals;   /* its capacity; evaluations recorded (all, up to the capacity) */
+    double  round_update[64];     /* per round (first 64): its update, */
+    double  round_weights[64][3]; /* its weights */
+} deftri_deformation_report;
+int deftri_deformation_optimization(deftri_ctx *ctx, deftri_map *map, const deftri_deformation_params *params,
+                                    deftri_deformation_report *report);
+/* Map::insertGlobalKeyFramesTransformation(0, 1, T) of the map-level call's T_g (global_t):
+   the (kf1, kf2) entry and its fp32 inverse for (kf2, kf1), each as the g2o::SE3Quat the next
+   arapOptimization reads back (getGlobalKeyFramesTransformation, :664) — Sophus SE3f from the
+   estimate cast to float (quaternion normalized in float), the inverse as the conjugate rotation and
+   -(R^T t) by Eigen's quaternion-vector product, in float.  The one implementation the native outer
+   loop and the host mirror's Map model both use.  No context, no GPU. */
+int deftri_global_insert(const double t7[7], double fwd7[7], double inv7[7]);
+/* TEST ONLY (no GPU): the restated NLopt LN_NELDERMEAD on a caller objective f(x, n, user) over n <= 8
+   dimensions — the search deftri_deformation_optimization runs.  x: in the start, out the best;
+   *result the NLopt result code (1 success, 4 xtol reached, 5 maxeval reached, -1 failure), *minf,
+   *nevals.  Returns 0, or DEFTRI_E_ARG (bad arguments, x0 outside the bounds). */
+typedef double (*deftri_objective_fn)(const double *x, int32_t n, void *user);
+int deftri_debug_nelder_mead(deftri_objective_fn f, void *user, int32_t n, double *x, const double *lb,
+                             const double *ub, double xtol_rel, double xtol_abs, int32_t maxeval, double *minf,
+                             int32_t *nevals, int32_t *result);
 
 /* ==== bundle adjustment ============================================
  * The BlockSolver_6_3 Schur LM of the reference's BA entry points:

@@ -24,5 +24,5 @@ def oracle_arap(m, rep, glob, arap, alpha, beta, depth_sigma, n_it):
     for s, kid in enumerate(info["scale_kf"]):
         m.keyframes[kid].estimated_depth_scale = float(ref["scales"][s])
     if prob.n_pairs:
-        m.insert_global_T(0, 1, SE3f.from7(ref["tg"][-1]))      # reference :1007 (KF ids 0, 1)
+        m.insert_global_from7(0, 1, list(ref["tg"][-1]))      # reference :1007 (KF ids 0, 1)
     return upd

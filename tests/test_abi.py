@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = capi.load()
-    assert lib.deftri_abi_version() == 6
+    assert lib.deftri_abi_version() == 7
     assert lib.deftri_sizeof(0) == C.sizeof(_abi.ProblemDesc)
     assert lib.deftri_sizeof(1) == C.sizeof(_abi.LMParams)
     assert lib.deftri_sizeof(2) == C.sizeof(_abi.Report)
@@ -37,6 +37,9 @@ def test_abi_version_and_struct_sizes():
     assert lib.deftri_sizeof(5) == C.sizeof(_abi.BADesc)
     assert lib.deftri_sizeof(6) == C.sizeof(_abi.PixelsError)
     assert lib.deftri_sizeof(7) == C.sizeof(_abi.PlanInfo)
+    assert lib.deftri_sizeof(8) == C.sizeof(_abi.DeformationParams)
+    assert lib.deftri_sizeof(9) == C.sizeof(_abi.DeformationReport)
+    assert lib.deftri_sizeof(10) == C.sizeof(_abi.DeformationEval)
 
 
 def test_ba_context_needs_a_device():

@@ -433,3 +433,36 @@ def test_plan_reuse_same_structure(golden_cases):
         r.arap_rot = r.arap_rot[:-1].copy(); r.arap_w = r.arap_w[:-1].copy()
         a.upload(r)                                        # other structure: analysed again
         assert a.solve_lm(1)["plan_reuses"] == 1
+
+
+def test_native_outer_loop_matches_host_loop():
+    """deformationOptimization behind the C-ABI (deftri_deformation_optimization: the Nelder-Mead
+    search restated in C++, map clones of positions / depth scales / the global table) against the
+    host loop over deftri/nlopt_nm.py (native=False), both with the device arapOptimization and
+    calculatePixelsStandDev: two outer rounds (the second starts from the first's global-table
+    update), the same evaluated weights and objective values bit for bit, the same weights and
+    updates per round and the same final map."""
+    import importlib, sys
+    from deftri import optimization
+    sys.path.insert(0, str(GOLDEN))
+    mg = importlib.import_module("make_golden")
+    out, maps = [], []
+    for native in (True, False):
+        m, st, _ = mg.scene("sim_default")
+        st.depth_weight = 3.0
+        st.n_optimizations, st.nlopt_iterations, st.n_iterations = 2, 6, 5
+        out.append(optimization.deformationOptimization(m, st, native=native))
+        maps.append(m)
+    a, b = out
+    assert len(a) == len(b) == 2
+    for ra, rb in zip(a, b):
+        assert [e["x"] for e in ra["evaluations"]] == [e["x"] for e in rb["evaluations"]]
+        assert [e["f"] for e in ra["evaluations"]] == [e["f"] for e in rb["evaluations"]]
+        assert list(ra["weights"]) == list(rb["weights"]) and ra["update"] == rb["update"]
+    assert a[-1]["minf"] == b[-1]["minf"] and a[-1]["nlopt_result"] == b[-1]["nlopt_result"]
+    ma, mb = maps
+    for pid in ma.map_points:
+        assert np.array_equal(ma.map_points[pid].position, mb.map_points[pid].position)
+    for kid in ma.keyframes:
+        assert ma.keyframes[kid].estimated_depth_scale == mb.keyframes[kid].estimated_depth_scale
+    assert np.array_equal(ma.global_T[(0, 1)].as7(), mb.global_T[(0, 1)].as7())

@@ -565,6 +565,7 @@ def test_alpha_hand_off_timeout_is_an_error(lm):
     and raise lambda).  The state the call started from is restored, the context switches to the
     separate alpha launch, and the retried call equals a clean run bit for bit."""
     extra = {"DEFTRI_DEVICE_LM": "1"} if lm == "device" else {}
+    extra["DEFTRI_SP_NO_TILE"] = "1"               # the merged two-phase chain (tile mode has no hand-off)
     faulted, clean = _fusion_runs_full([{"DEFTRI_SP_INJECT_TIMEOUT_IT": "1", **extra}, extra])
     code, state, launches, chi, trials, its, final, init = faulted
     assert code == -2                                # DEFTRI_E_HIP

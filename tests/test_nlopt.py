@@ -100,3 +100,42 @@ def test_speculative_prefetch_matches_sequential(case):
     assert np.array_equal(a[0], b[0]) and a[1:] == b[1:]
     assert seq_log == spec_log
     assert max(batches) > 1                                     # candidates really were batched
+
+
+@pytest.mark.parametrize("case", ["rosen2d", "quad3d_maxeval", "bounded1d", "sim_weights", "fixed_dims", "shrink"])
+def test_native_nelder_mead_matches_restatement(case):
+    """The native restatement behind deftri_deformation_optimization (csrc/deformation.cpp, via
+    deftri_debug_nelder_mead) and deftri/nlopt_nm.py are the same algorithm: the same evaluation
+    sequence point for point, the same best point, minimum, result code and evaluation count."""
+    from deftri import capi
+    f, x0, lb, ub, tr, ta, me = {
+        "rosen2d": (lambda x: (1 - x[0]) ** 2 + 100 * (x[1] - x[0] ** 2) ** 2, [-1.2, 1.0], [-5, -5], [5, 5], 1e-10, 1e-12, 400),
+        "quad3d_maxeval": (lambda x: (x[0] - 1) ** 2 + 2 * (x[1] + 2) ** 2 + 3 * x[2] ** 2, [0, 0, 1], [-4, -4, -4], [4, 4, 4], 0, 0, 57),
+        "bounded1d": (lambda x: (x[0] + 3.0) ** 2, [1.0], [0.0], [2.0], 1e-6, 1e-9, 200),
+        "sim_weights": (lambda x: math.log(x[2] / 3e5) ** 2 + 0.1 * math.sin(x[2] / 1e5), SIM_X0, SIM_LB, SIM_UB, 0.15, 0.15, 30),
+        "fixed_dims": (lambda x: (x[1] - 0.3) ** 2 + abs(x[2]), [1.0, 0.0, 2.0], [1.0, -1.0, -3.0], [1.0, 1.0, 3.0], 1e-7, 1e-9, 300),
+        "shrink": (lambda x: abs(x[0]) + abs(x[1]) + 0.01 * x[0] * x[1], [2.0, -1.5], [-4, -4], [4, 4], 1e-9, 1e-12, 500),
+    }[case]
+    seq = []
+    a = nlopt_nm.nelder_mead(f, x0, lb, ub, tr, ta, me, log=seq.append)
+    x, minf, res, nev, seen = capi.nelder_mead_native(f, x0, lb, ub, tr, ta, me)
+    assert [e["x"] for e in seq] == seen
+    assert list(a[0]) == x and a[1] == minf and a[2] == res and a[3] == nev
+
+
+def test_global_insert_is_the_map_models():
+    """Map::insertGlobalKeyFramesTransformation's two entries (deftri_global_insert): the Map model
+    stores exactly what the native loop stores, the inverse entry composes with the forward one to
+    the identity within fp32 rounding, and both are unit quaternions with w >= 0."""
+    from deftri import capi
+    from deftri.mapmodel import Map, SE3f, mat_from_quat
+    t7 = [0.01, -0.02, 0.03, 0.999, 0.004, -0.002, 0.001]
+    fwd, inv = capi.global_insert(t7)
+    m = Map()
+    m.insert_global_from7(0, 1, t7)
+    assert list(m.global_T[(0, 1)].as7()) == fwd and list(m.global_T[(1, 0)].as7()) == inv
+    for q in (fwd[:4], inv[:4]):
+        assert abs(np.linalg.norm(q) - 1) < 1e-15 and q[3] >= 0
+    Ra, Rb = mat_from_quat(fwd[:4]), mat_from_quat(inv[:4])
+    assert np.allclose(Ra @ Rb, np.eye(3), atol=1e-6)
+    assert np.allclose(Ra @ np.array(inv[4:]) + np.array(fwd[4:]), 0, atol=1e-6)

@@ -1377,10 +1377,10 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
             stats[k].ms += ms;
         }
         for (int32_t k = 0; k < n; k++) {
-            if (!std::strcmp(stats[k].name, "sp_phase1") || !std::strcmp(stats[k].name, "sp_tile"))
+            if (!std::strcmp(stats[k].name, "sp_phase1") || !std::strcmp(stats[k].name, "sp_tcg"))
                 stats[k].bytes = ctx->sp->product_bytes_phase(1) * its;
-            if (!std::strcmp(stats[k].name, "sp_phase2") || !std::strcmp(stats[k].name, "sp_tupd"))
-                stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
+            if (!std::strcmp(stats[k].name, "sp_phase2")) stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
+            if (!std::strcmp(stats[k].name, "sp_tcg0")) stats[k].bytes = ctx->sp->product_bytes_phase(1);
         }
         for (hipEvent_t e : prof.pool) hipEventDestroy(e);
         *n_stats = n;
@@ -1471,6 +1471,9 @@ int64_t deftri_sizeof(int32_t which) {
         case 5: return (int64_t)sizeof(deftri_ba_desc);
         case 6: return (int64_t)sizeof(deftri_pixels_error);
         case 7: return (int64_t)sizeof(deftri_plan_info);
+        case 8: return (int64_t)sizeof(deftri_deformation_params);
+        case 9: return (int64_t)sizeof(deftri_deformation_report);
+        case 10: return (int64_t)sizeof(deftri_deformation_eval);
         default: return -1;
     }
 }

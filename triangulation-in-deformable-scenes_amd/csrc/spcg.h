@@ -122,7 +122,8 @@ struct SpPlanHost {
     std::vector<int32_t> tile_chunk;                   // 2 per chunk: first le, first cross slot
     std::vector<int32_t> tile_rs;                      // per own row: LDS slot begin | count << 16
     std::vector<int32_t> tile_halo;                    // the tiles' halo rows (local row ids)
-    std::vector<int32_t> tile_xoff, tile_xidx;         // per own row its cross slots (CSR)
+    std::vector<int32_t> tile_xoff;                    // per own row its cross slots (destination order)
+    std::vector<int32_t> tile_xdst;                    // per cut entry (source order): its 2 cross slots
     double tile_bytes[2] = {0, 0};                     // algorithmic bytes per CG iteration: product, update
 };
 // the groups and rows build_tiles needs (spcg_plan.cpp step 5)
@@ -247,8 +248,14 @@ struct SpDev {
     const int32_t *ttab = nullptr;                        // [ntile][8]
     const uint2 *tmeta = nullptr;                         // per entry (word 0, word 1)
     const int2 *tchunk = nullptr;                         // per chunk (first le, first cross slot)
-    const int32_t *trs = nullptr, *thalo = nullptr, *txoff = nullptr, *txidx = nullptr;
-    double *xc = nullptr;                                 // cross slots [n][3]
+    const int32_t *trs = nullptr, *thalo = nullptr, *txoff = nullptr;
+    const int2 *txdst = nullptr;                          // per cut entry: its two cross slots (destination order)
+    // the single-reduction chain's state, double-buffered by iteration parity (k_sp_tcg)
+    double2 *tzp[2] = {nullptr, nullptr};                 // (z, p)
+    double *ts[2] = {nullptr, nullptr}, *tr[2] = {nullptr, nullptr}, *tw[2] = {nullptr, nullptr};
+    double *txc[2] = {nullptr, nullptr};                  // cross slots [n][3], by target row
+    double *hw = nullptr;                                 // heavy sums of A z of the last iteration
+    double *tpart = nullptr, *tgs = nullptr;              // per-workgroup sums [grid][11]; per-XCD group sums
     const double *pinfo = nullptr;                        // per pair: Omega (= W of its ARAP edges)
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
@@ -270,7 +277,8 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
 int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
 int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
-void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) p
+void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) z (zp .x)
+void sp_launch_tcg_setup(const SpDev &G, const double *rhs, double lambda, bool fp32, hipStream_t st);
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
@@ -331,6 +339,7 @@ class SpSolver {
     int32_t n_tiles() const { return G.tile ? G.ntile : 0; }
     bool halo_overlap() const { return G.sd && G.ovl; }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
+        if (G.tile) return 1;                    // tile mode: the update and the product in one launch
         if (G.sd) return 3;                      // + one all-reduce and one grouped send / receive
         if (G.merged) return G.alpha_kernel ? 3 : 2;
         const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;

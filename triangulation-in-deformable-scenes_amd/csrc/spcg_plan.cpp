@@ -615,14 +615,17 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                      + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
     if (H.tile) {
-        // tile mode per CG iteration: k_sp_tile — per entry J + meta (padding: meta only), per tile
-        // row (z, p) + D + q out + slot range + its depth couplings (c, W J_s^2, scale, offset), per halo
-        // row (z, p), per cut entry two cross slots out; k_sp_tupd — per own row (z, p) in / out, x and r
-        // in / out, q in, M, cross range, per cross slot its index and value
+        // tile mode, one k_sp_tcg launch per CG iteration (the update of it - 1 + the product of it):
+        // per own row (z, p), s, r, w, x in and (z, p), s, r, x, w out, M and D in, its cross range
+        // and slot range, its depth couplings (c, W J_s^2, scale, offset); per halo row (z, p), s, r,
+        // w, M and its cross range in (the redundant update); per entry J (valid) and meta; per cut
+        // entry its two cross slots out (+ their positions) and in again (own rows and halo rows)
         const int64_t nvalid = (int64_t)H.arap_ids.size();
-        H.tile_bytes[0] = (double)nvalid * jb + (double)H.tile_entries * 8 + (double)nown * (48 + 48 + 24 + 4 + 4) +
-                          (double)ndl * (24 + 8 + 4) + (double)H.tile_halo_rows * 48 + (double)H.tile_cross * 24;
-        H.tile_bytes[1] = (double)nown * (96 + 48 + 48 + 24 + 48 + 4) + (double)H.tile_cross * (4 + 24);
+        H.tile_bytes[0] = (double)nvalid * jb + (double)H.tile_entries * 8 +
+                          (double)nown * (48 + 24 + 24 + 24 + 24 + 48 + 48 + 8 + 4 + 48 + 24 + 24 + 24 + 24) +
+                          (double)ndl * (24 + 8 + 4 + 4) + (double)H.tile_halo_rows * (48 + 24 + 24 + 24 + 48 + 8) +
+                          (double)H.tile_cross * (24 + 4 + 24);
+        H.tile_bytes[1] = 0.0;
     }
     static const bool digest = std::getenv("DEFTRI_PLAN_DIGEST") != nullptr;
     if (digest) {
@@ -637,6 +640,8 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         vec(H.dep_ids); vec(H.rot_ids); vec(H.arap_rot_local); vec(H.blk); vec(H.hv_blk); vec(H.hv_blk_off);
         vec(H.dperm); vec(H.inc_off); vec(H.inc); vec(H.rep_off); vec(H.dep_off); vec(H.rowmap); vec(H.woff);
         vec(H.wsplit); vec(H.pmap); vec(H.pidx);
+        vec(H.tile_tab); vec(H.tile_m0); vec(H.tile_m1); vec(H.tile_chunk); vec(H.tile_rs); vec(H.tile_halo);
+        vec(H.tile_xoff); vec(H.tile_xdst);
         for (const auto &x : H.send_rows) vec(x);
         for (const auto &x : H.recv_rows) vec(x);
         const int64_t sc[4] = {H.lo, H.hi, H.n_arap_owned, H.halo_rows};

@@ -385,20 +385,31 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.tile_lds = H.tile_lds;
         G.tile_segmax = H.tile_segmax;
         G.t_grid = 8 * ((H.ntile + 7) / 8) + 1;
-        int32_t *tt, *trs, *th, *txo, *txi, *tch;
+        int32_t *tt, *trs, *th, *txo, *txd, *tch;
         uint32_t *tm;
-        PUT(tt, H.tile_tab); PUT(trs, H.tile_rs); PUT(th, H.tile_halo); PUT(txo, H.tile_xoff); PUT(txi, H.tile_xidx);
+        PUT(tt, H.tile_tab); PUT(trs, H.tile_rs); PUT(th, H.tile_halo); PUT(txo, H.tile_xoff); PUT(txd, H.tile_xdst);
         PUT(tch, H.tile_chunk);
         {
             std::vector<uint32_t> mm(2 * H.tile_m0.size());
             for (size_t k = 0; k < H.tile_m0.size(); k++) { mm[2 * k] = H.tile_m0[k]; mm[2 * k + 1] = H.tile_m1[k]; }
             PUT(tm, mm);
         }
-        G.ttab = tt; G.trs = trs; G.thalo = th; G.txoff = txo; G.txidx = txi;
+        G.ttab = tt; G.trs = trs; G.thalo = th; G.txoff = txo;
+        G.txdst = reinterpret_cast<const int2 *>(txd);
         G.tchunk = reinterpret_cast<const int2 *>(tch);
         G.tmeta = reinterpret_cast<const uint2 *>(tm);
-        ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));
         G.pinfo = P.pair_info;
+        for (int k = 0; k < 2; k++) {
+            double *z2;
+            ALLOC(z2, 2 * G.ndof);
+            G.tzp[k] = reinterpret_cast<double2 *>(z2);
+            ALLOC(G.ts[k], G.ndof); ALLOC(G.tr[k], G.ndof); ALLOC(G.tw[k], G.ndof);
+            ALLOC(G.txc[k], 3 * std::max<int64_t>(H.tile_cross, 1));
+        }
+        ALLOC(G.hw, std::max<int64_t>(H.hd, 1));
+        ALLOC(G.tpart, 11 * (int64_t)G.t_grid);
+        ALLOC(G.tgs, 11 * 8);
+        G.zp = G.tzp[0];                           // (load_p's target: the Hessian product reads buffer 0)
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -589,6 +600,10 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
 // the solve's setup (preconditioner at lambda, r = rhs, (z, p) = (M r, 0), x = 0); sharded: the
 // boundary rows' (z, p) to the ranks whose edges read them, as after every CG update
 int SpSolver::cg_setup(double lambda, const double *rhs) {
+    if (G.tile) {                                  // the setup and the first product in one launch
+        sp_launch_tcg_setup(G, rhs, lambda, fp32_jac != 0, st_);
+        return 0;
+    }
     sp_launch_setup(G, rhs, lambda, st_);
     if (G.sd) return halo_sd();
     if (shard_) return halo(6, reinterpret_cast<double *>(G.zp), true);
@@ -600,6 +615,10 @@ int SpSolver::cg_setup(double lambda, const double *rhs) {
 int SpSolver::cg_chain(double lambda, int from, int to) {
     int rc;
     for (int it = from; it < to; it++) {
+        if (G.tile) {                                  // the update of it and the product of it + 1
+            sp_launch_product(G, it + 1, lambda, fp32_jac != 0, st_);
+            continue;
+        }
         if (G.sd) {                                    // phase 1, phase 2 (A z), one all-reduce, update
             sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
             if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;

@@ -21,7 +21,8 @@
 //   chunk    per 64 entries: the le of its first valid entry, its first cross slot
 //   rows     the tile's own rows (consecutive), then its halo rows (rows of cut edges' j vertices)
 //   slots    per own row its incoming LDS contributions, contiguous (row r: trs[r] = begin | count << 16)
-//   cross    per own row (all tiles) the cross slots aimed at it, in source order (xoff / xidx)
+//   cross    per own row (all tiles) the cross slots aimed at it, contiguous in source order (xoff);
+//            per cut entry its two slots' positions (xdst)
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
@@ -246,11 +247,13 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
     // cross slots by target row, source order inside a row
     std::stable_sort(xt.begin(), xt.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    // (the writer scatters its two slots to their destination positions; a row's slots are then one
+    // contiguous range the reader sums without an index load)
     H.tile_xoff.assign(nown + 1, 0);
-    H.tile_xidx.resize(xt.size());
+    H.tile_xdst.assign(xt.size(), 0);
     for (const auto &x : xt) H.tile_xoff[x.first + 1]++;
     for (int32_t l = 0; l < nown; l++) H.tile_xoff[l + 1] += H.tile_xoff[l];
-    for (size_t k = 0; k < xt.size(); k++) H.tile_xidx[k] = xt[k].second;
+    for (size_t k = 0; k < xt.size(); k++) H.tile_xdst[xt[k].second] = (int32_t)k;
     H.ntile = nt;
     H.tile_entries = (int64_t)m0.size();
     H.tile_cross = nx;
@@ -325,8 +328,9 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
             for (int c = 0; c < 3; c++) { up[3 * (size_t)rows[0] + c] += J[c] * s; up[3 * (size_t)rows[1] + c] += J[3 + c] * s; }
             if (cut) {
                 if (x < 0 || x + 2 > H.tile_cross) { why = "cross slot out of range"; return -1; }
-                xw[x]++; xw[x + 1]++;
-                for (int c = 0; c < 3; c++) { xc[3 * x + c] = J[6 + c] * s; xc[3 * (x + 1) + c] = J[9 + c] * s; }
+                const int64_t d0 = H.tile_xdst[x], d1 = H.tile_xdst[x + 1];
+                xw[d0]++; xw[d1]++;
+                for (int c = 0; c < 3; c++) { xc[3 * d0 + c] = J[6 + c] * s; xc[3 * d1 + c] = J[9 + c] * s; }
             } else {
                 const int s0 = (int)(m1 & 0xfffu), s1 = (int)((m1 >> 12) & 0xfffu);
                 if (s0 >= ns || s1 >= ns) { why = "LDS slot out of range"; return -1; }
@@ -372,7 +376,7 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
         if (lew[le] != 1) { why = "a local edge not visited exactly once"; return -1; }
     for (int32_t l = 0; l < nown; l++)
         for (int32_t k = H.tile_xoff[l]; k < H.tile_xoff[l + 1]; k++) {
-            const int64_t x = H.tile_xidx[k];
+            const int64_t x = k;
             xr[x]++;
             for (int c = 0; c < 3; c++) qr[hd + 3 * (int64_t)l + c] += xc[3 * x + c];
         }

@@ -108,6 +108,25 @@ class MapC(C.Structure):
                 ("n_global", i32), ("globals", P(GlobalEntryC))]
 
 
+class DeformationParams(C.Structure):
+    _fields_ = [("selection", i32), ("rep", f64), ("global_", f64), ("arap", f64), ("alpha", f64), ("beta", f64),
+                ("depth_error", f32), ("n_iterations", i32), ("n_optimizations", i32), ("lb", f64 * 3),
+                ("ub", f64 * 3), ("xtol_rel", f64), ("xtol_abs", f64), ("maxeval", i32), ("n_map_points", i32)]
+
+
+class DeformationEval(C.Structure):
+    _fields_ = [("round", i32), ("eval", i32), ("x", f64 * 3), ("f", f64)]
+
+
+class DeformationReport(C.Structure):
+    _fields_ = [("rounds", i32), ("arap_calls", i32), ("weights", f64 * 3), ("minf", f64), ("nlopt_result", i32),
+                ("update", f64), ("seconds", f64), ("evals", P(DeformationEval)), ("max_evals", i32),
+                ("n_evals", i32), ("round_update", f64 * 64), ("round_weights", (f64 * 3) * 64)]
+
+
+OBJECTIVE_FN = C.CFUNCTYPE(C.c_double, P(C.c_double), C.c_int32, C.c_void_p)
+
+
 class AbsErrorsC(C.Structure):
     _fields_ = [("average_movement", f64), ("average_error_original", f64), ("average_error_moved", f64),
                 ("average_error", f64), ("rmse", f64), ("point_count", i64)]

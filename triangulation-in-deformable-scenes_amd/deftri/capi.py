@@ -76,6 +76,12 @@ def load():
         "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
                                                C.c_double, C.c_double, C.c_float, C.c_int32, P(C.c_double),
                                                P(_abi.Report)]),
+        "deftri_deformation_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.DeformationParams),
+                                                      P(_abi.DeformationReport)]),
+        "deftri_global_insert": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double)]),
+        "deftri_debug_nelder_mead": (C.c_int, [_abi.OBJECTIVE_FN, C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double),
+                                               P(C.c_double), C.c_double, C.c_double, C.c_int32, P(C.c_double),
+                                               P(C.c_int32), P(C.c_int32)]),
         # bundle adjustment
         "deftri_ba_create": (C.c_int, [C.c_int32, P(C.c_void_p)]),
         "deftri_ba_destroy": (C.c_int, [C.c_void_p]),
@@ -137,7 +143,8 @@ EXPORTED = [
     "deftri_dist_init_rccl", "deftri_dist_set_transport", "deftri_dist_vertex_owner", "deftri_plan_vertex_order", "deftri_sim_two_view", "deftri_sim_normal_stream",
     "deftri_measure_sim_absolute_map_errors", "deftri_measure_relative_map_errors", "deftri_dist_owned_edges",
     "deftri_debug_plan_solve_dist", "deftri_set_plan", "deftri_set_jacobian_storage", "deftri_get_plan_info",
-    "deftri_debug_sp_product", "deftri_set_pair_window",
+    "deftri_debug_sp_product", "deftri_set_pair_window", "deftri_deformation_optimization", "deftri_global_insert",
+    "deftri_debug_nelder_mead",
 ]
 
 
@@ -411,6 +418,81 @@ class Context:
         self._check(rc)
         m.from_c(mc, keep)
         return upd.value, rep.as_dict()
+
+
+    def deformation_optimization(self, m, settings, max_evals=4096):
+        """deformationOptimization (g2oBundleAdjustment.cc:446-606) in native code
+        (deftri_deformation_optimization): the outer rounds, the Nelder-Mead weight search on map
+        clones, arapOptimization and calculatePixelsStandDev on the device.  Writes the map back
+        (positions, depth scales, the global table) and returns the report as a dict with the
+        evaluation log."""
+        self._check(self.lib.deftri_set_jacobian_mode(self.h, 0))      # g2o numeric J (the reference's)
+        settings.validate_for_solver()
+        if settings.selection not in ("g2oArap", "twoOptimizations"):
+            raise NotImplementedError(f"selection {settings.selection!r} is out of scope")
+        if settings.selection == "twoOptimizations" and settings.weights_selection != "nlopt":
+            raise NotImplementedError("twoOptimizations with the Eigen LM weight search is not built")
+        prm = _abi.DeformationParams()
+        prm.selection = 1 if settings.selection == "twoOptimizations" else 0
+        prm.rep, prm.global_, prm.arap = float(settings.rep), float(settings.global_), float(settings.arap)
+        prm.alpha, prm.beta = float(settings.alpha), float(settings.beta)
+        prm.depth_error = float(settings.depth_sigma)
+        prm.n_iterations, prm.n_optimizations = int(settings.n_iterations), int(settings.n_optimizations)
+        prm.lb[:] = [settings.nlopt_rep_lb, settings.nlopt_global_lb, settings.nlopt_arap_lb]
+        prm.ub[:] = [settings.nlopt_rep_ub, settings.nlopt_global_ub, settings.nlopt_arap_ub]
+        prm.xtol_rel, prm.xtol_abs = float(settings.nlopt_rel_tol), float(settings.nlopt_abs_tol)
+        prm.maxeval = int(settings.nlopt_iterations)
+        prm.n_map_points = len(m.map_points)
+        evals = (_abi.DeformationEval * max_evals)()
+        rep = _abi.DeformationReport()
+        rep.evals = C.cast(evals, C.POINTER(_abi.DeformationEval))
+        rep.max_evals = max_evals
+        mc, keep = m.to_c()
+        t = time.perf_counter()
+        rc = self.lib.deftri_deformation_optimization(self.h, C.byref(mc), C.byref(prm), C.byref(rep))
+        self.last_call_s = time.perf_counter() - t
+        self._check(rc)
+        if rep.rounds > 0:
+            m.from_c(mc, keep)
+        ev = [{"round": evals[k].round, "eval": evals[k].eval, "x": list(evals[k].x), "f": evals[k].f}
+              for k in range(min(rep.n_evals, max_evals))]
+        return {"rounds": rep.rounds, "arap_calls": rep.arap_calls, "weights": list(rep.weights), "minf": rep.minf,
+                "nlopt_result": rep.nlopt_result, "update": rep.update, "seconds": rep.seconds, "evaluations": ev,
+                "round_update": list(rep.round_update[:min(rep.rounds, 64)]),
+                "round_weights": [list(rep.round_weights[k]) for k in range(min(rep.rounds, 64))]}
+
+
+def global_insert(t7):
+    """deftri_global_insert: the (0, 1) and (1, 0) entries Map::insertGlobalKeyFramesTransformation
+    stores for the solved T_g, as the 7-vectors the next arapOptimization reads (host, no GPU)."""
+    lib = load()
+    a = (C.c_double * 7)(*[float(v) for v in t7])
+    f, i = (C.c_double * 7)(), (C.c_double * 7)()
+    rc = lib.deftri_global_insert(a, f, i)
+    if rc:
+        raise DeftriError(rc, "deftri_global_insert")
+    return list(f), list(i)
+
+
+def nelder_mead_native(f, x0, lb, ub, xtol_rel=0.0, xtol_abs=0.0, maxeval=0):
+    """deftri_debug_nelder_mead: the native restated NLopt LN_NELDERMEAD on a Python objective (tests)."""
+    lib = load()
+    n = len(x0)
+    x = (C.c_double * n)(*map(float, x0))
+    lo, hi = (C.c_double * n)(*map(float, lb)), (C.c_double * n)(*map(float, ub))
+    seen = []
+
+    def cb(xp, nn, user):
+        xv = [xp[k] for k in range(nn)]
+        seen.append(xv)
+        return float(f(xv))
+    fn = _abi.OBJECTIVE_FN(cb)
+    minf, nev, res = C.c_double(), C.c_int32(), C.c_int32()
+    rc = lib.deftri_debug_nelder_mead(fn, None, n, x, lo, hi, float(xtol_rel), float(xtol_abs), int(maxeval),
+                                      C.byref(minf), C.byref(nev), C.byref(res))
+    if rc:
+        raise DeftriError(rc, "deftri_debug_nelder_mead")
+    return list(x), minf.value, res.value, nev.value, seen
 
 
 class BAContext:

@@ -78,6 +78,8 @@ class SE3f:
 
     def as7(self):
         """g2o::SE3Quat(unit_quaternion().cast<double>(), translation().cast<double>())."""
+        if getattr(self, "_as7", None) is not None:        # an entry deftri_global_insert formed
+            return np.array(self._as7, dtype=np.float64)
         q = (self.q if self.q is not None else self.unit_quaternion().astype(np.float32)).astype(np.float64)
         if q[3] < 0:
             q = -q
@@ -182,6 +184,16 @@ class Map:
     def insert_global_T(self, kf1, kf2, T):
         self.global_T[(kf1, kf2)] = T
         self.global_T[(kf2, kf1)] = T.inverse()
+
+    def insert_global_from7(self, kf1, kf2, t7):
+        """Map::insertGlobalKeyFramesTransformation(kf1, kf2, T) of a solved T_g (7-vector): the two
+        entries exactly as the native loop stores them (deftri_global_insert)."""
+        from .capi import global_insert
+        fwd, inv = global_insert(t7)
+        a, b = SE3f.from7(fwd), SE3f.from7(inv)
+        a._as7, b._as7 = fwd, inv
+        self.global_T[(kf1, kf2)] = a
+        self.global_T[(kf2, kf1)] = b
 
     def get_global_T(self, kf1, kf2):
         return self.global_T.get((kf1, kf2), SE3f())
@@ -294,4 +306,4 @@ class Map:
         if m.n_keyframes >= 2:
             # the reference hard-codes insertGlobalKeyFramesTransformation(0, 1, T) (:1007): KF ids 0
             # and 1, whatever the map's keyframe ids are
-            self.insert_global_T(0, 1, SE3f.from7(np.array(m.global_t[:])))
+            self.insert_global_from7(0, 1, list(m.global_t[:]))

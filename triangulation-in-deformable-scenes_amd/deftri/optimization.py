@@ -66,18 +66,36 @@ def outerObjective(x, pMap, settings, arap_fn=None, device=0):
 
 
 def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=None, device=0, log=None,
-                            arap_fn=None, workers=None):
+                            arap_fn=None, workers=None, native=True):
     """g2oBundleAdjustment.cc:446-606.  Outer rounds until sum ||dp|| < 1e-4 |MapPoints| or
     numberOfOptimizations; per round either the fixed weights ("g2oArap") or the weight search
     ("twoOptimizations" + "nlopt": Nelder-Mead over (rep, global, arap) within the nlopt bounds,
     each evaluation an arapOptimization on a map clone, then arapOptimization on the map with the
-    optimum, which becomes the next round's start).  `arap_fn` (tests only) replaces the device
-    arapOptimization with another implementation of the same signature.  `workers`
+    optimum, which becomes the next round's start).
+
+    native (default): the whole loop behind the C-ABI (deftri_deformation_optimization: the search
+    restated in C++, clones of the map's positions / scales / global table, every evaluation on the
+    device), one call.  native=False: this host loop over deftri/nlopt_nm.py — the same algorithm
+    (tests hold the two to the same search path).  `arap_fn` (tests only) replaces the device
+    arapOptimization with another implementation of the same signature; `workers`
     (deftri.workers.ObjectiveWorkers) evaluates each Nelder-Mead step's candidate points on several
-    GPUs at once; the search and its result are those of the sequential run."""
+    GPUs at once (the search and its result are those of the sequential run); both use the host loop."""
     import copy
     from .nlopt_nm import nelder_mead
     settings.validate_for_solver()
+    if native and arap_fn is None and workers is None:
+        r = _ctx(device).deformation_optimization(pMap, settings)
+        rounds = []
+        for k in range(r["rounds"]):
+            info = {"round": k + 1, "weights": r["round_weights"][k] if k < 64 else r["weights"],
+                    "update": r["round_update"][k] if k < 64 else r["update"],
+                    "evaluations": [e for e in r["evaluations"] if e["round"] == k + 1]}
+            if k == r["rounds"] - 1 and settings.selection == "twoOptimizations":
+                info.update({"minf": r["minf"], "nlopt_result": r["nlopt_result"]})
+            rounds.append(info)
+            if log:
+                log(info)
+        return rounds
     if settings.selection == "open3DArap":
         raise NotImplementedError("open3DArap is a different algorithm (Open3D DeformAsRigidAsPossible), out of scope")
     if settings.selection == "twoOptimizations" and settings.weights_selection != "nlopt":
