@@ -49,7 +49,7 @@ def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
         info = gpu_ctx.plan_info()
         assert info["plan"] == plan
         if plan == "iterative":
-            assert info["cg_launches"] == 2                      # the merged chain bench.py times
+            assert info["tiles"] > 0 and info["cg_launches"] in (1, 2)   # the tile chain bench.py times
         r = gpu_ctx.solve_lm(meta["n_iterations"], analytic=False)
         pts, sc, tg = gpu_ctx.download()
     finally:

@@ -41,7 +41,7 @@ def check_props(p, n_it, lambdas_rel):
         ctx.set_plan("auto")                      # the library's choice: iterative from 50k unknowns
         ctx.upload(p)
         info = ctx.plan_info()
-        assert info["plan"] == "iterative" and info["cg_launches"] == 2
+        assert info["plan"] == "iterative" and info["cg_launches"] in (1, 2)   # tile (C2) or merged chain
         r1 = ctx.solve_lm(n_it, analytic=False)
         s1 = ctx.download()
         assert r1["iterations"] == n_it

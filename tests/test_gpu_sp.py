@@ -311,6 +311,8 @@ def test_iterative_plan_reuse_matches_fresh_upload():
 
 
 def _fusion_worker(env, q):
+    # the two-phase chains unless the run asks for the tile chain (DEFTRI_SP_TILE)
+    env = dict(env) if "DEFTRI_SP_TILE" in env else {"DEFTRI_SP_NO_TILE": "1", **env}
     os.environ.update(env)                          # read once, at the first upload of this process
     from deftri import capi as c
     p = tv_problem(20000, seed=6)
@@ -477,7 +479,7 @@ def test_merged_chain_breakdown_then_solve():
         for c in (a, b):
             c.set_plan("iterative")
             c.upload(p)
-        assert a.plan_info()["cg_launches"] == 2
+        assert a.plan_info()["cg_launches"] in (1, 2)         # the tile chain (one rank, one pair)
         g, d = a.gradient()
         lam = 1e-3 * np.abs(d).max()
         bad = g.copy()
@@ -586,3 +588,21 @@ def _fusion_runs_full(envs):
         pr.join(timeout=60)
         assert pr.exitcode == 0
     return out
+
+
+def test_tile_chain_matches_two_phase_chain():
+    """Tile mode (csrc/spcg_tile.cpp; one rank, one pair — the timed C2 chain): the product and the
+    update as two launches (the default), the update fused into the product's cooperative launch
+    (DEFTRI_SP_TILE_FUSE: 1 launch per CG iteration), and the two-phase merged chain (2): the fused and
+    unfused tile chains take the same alpha from the same partials and update with the same
+    arithmetic, so they differ only in how the (r.z, r.r) partials are grouped — identical trials and
+    CG iteration counts, chi2 rel 1e-10; against the two-phase chain (q summed in another order)
+    chi2 rel 1e-9.  The device-driven LM on the tile chain takes the host loop's decisions: bit for bit."""
+    runs = _fusion_runs([{"DEFTRI_SP_TILE": "1"}, {"DEFTRI_SP_TILE": "1", "DEFTRI_SP_TILE_FUSE": "1"}, {},
+                         {"DEFTRI_SP_TILE": "1", "DEFTRI_DEVICE_LM": "1"}])
+    (l0, c0, t0, i0, s0), (l1, c1, t1, i1, s1), (l2, c2, t2, i2, s2), (l3, c3, t3, i3, s3) = runs
+    assert l0 == 2 and l1 == 1 and l2 == 2
+    assert t0 == t1 == t2 and i0 == i1 == i2
+    np.testing.assert_allclose(c0, c1, rtol=1e-10)
+    np.testing.assert_allclose(c0, c2, rtol=1e-9)
+    assert c3 == c0 and t3 == t0 and i3 == i0 and s3 == s0

@@ -58,7 +58,7 @@ def test_regime_matches_oracle(gpu_ctx, name, sub, plan):
         info = gpu_ctx.plan_info()
         assert info["plan"] == plan
         if plan == "iterative" and p.n_unknowns >= 50000:
-            assert info["cg_launches"] == 2                  # the merged chain (the timed one)
+            assert info["cg_launches"] in (1, 2)             # the tile / merged chain (the timed one)
         r = gpu_ctx.solve_lm(meta["n_iterations"], analytic=False)
         pts, sc, tg = gpu_ctx.download()
     finally:

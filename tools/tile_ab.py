@@ -23,8 +23,9 @@ def run_variant(n, n_it):
         r = ctx.solve_lm(n_it, analytic=False)
         pts = ctx.download()[0]
         st = ctx.profile_trial(r["lambda_final"])
-        its = max(st.get("sp_tupd", st.get("sp_phase2", {"launches": 1}))["launches"], 1)
+        its = max(st.get("sp_tupd", st.get("sp_phase2", st.get("sp_tile", {"launches": 1})))["launches"], 1)
         cg = {k: round(1e3 * v["ms"] / its, 3) for k, v in st.items() if k in ("sp_tile", "sp_tupd", "sp_phase1", "sp_phase2", "sp_alpha")}
+        cg0 = {k: round(1e3 * v["ms"], 3) for k, v in st.items() if k in ("sp_setup",)}
         ctx.reset_state()
         import time
         torch.cuda.synchronize()
@@ -33,7 +34,7 @@ def run_variant(n, n_it):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
     return {"tiles": info["tiles"], "cg_launches": info["cg_launches"], "trials": r["trials_iter"], "chi2": r["chi2_iter"],
-            "pcg_its": r["pcg_iterations"], "cg_us": cg, "cg_iteration_us": round(sum(cg.values()), 3), "cg_its_profiled": its,
+            "pcg_its": r["pcg_iterations"], "cg_us": cg, "cg_iteration_us": round(sum(cg.values()), 3), "cg_its_profiled": its, "setup_us": cg0,
             "lm_it_s": round(r2["iterations"] / dt, 1), "bytes": info["product_bytes"], "survey_bytes": info["survey_bytes"],
             "pts_sum": float(pts.sum()), "repeat_same": r2["chi2_iter"] == r["chi2_iter"]}
 

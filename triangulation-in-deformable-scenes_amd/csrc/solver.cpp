@@ -1377,10 +1377,10 @@ int deftri_profile_trial(deftri_ctx *ctx, double lambda, deftri_kernel_stat *sta
             stats[k].ms += ms;
         }
         for (int32_t k = 0; k < n; k++) {
-            if (!std::strcmp(stats[k].name, "sp_phase1") || !std::strcmp(stats[k].name, "sp_tcg"))
+            if (!std::strcmp(stats[k].name, "sp_phase1") || !std::strcmp(stats[k].name, "sp_tile"))
                 stats[k].bytes = ctx->sp->product_bytes_phase(1) * its;
-            if (!std::strcmp(stats[k].name, "sp_phase2")) stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
-            if (!std::strcmp(stats[k].name, "sp_tcg0")) stats[k].bytes = ctx->sp->product_bytes_phase(1);
+            if (!std::strcmp(stats[k].name, "sp_phase2") || !std::strcmp(stats[k].name, "sp_tupd"))
+                stats[k].bytes = ctx->sp->product_bytes_phase(2) * its;
         }
         for (hipEvent_t e : prof.pool) hipEventDestroy(e);
         *n_stats = n;

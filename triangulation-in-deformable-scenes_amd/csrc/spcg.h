@@ -54,8 +54,8 @@ constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one
 constexpr int64_t kSpMergeMinDof = 50000;  // one rank: the merged (two-launch) CG chain from this many unknowns
 // tile mode (spcg_tile.cpp): one rank, one keyframe pair — the fused product, every ARAP edge read once
 constexpr int kSpTileUnits = 128;          // mesh vertices (keyframe-copy groups) per tile at most
-constexpr int kSpTileLds = 52 * 1024;      // LDS bytes per tile at most (3 workgroups per CU)
-constexpr int kSpTileLdsFixed = 1024;      // the tile kernel's fixed LDS (heavy p, reductions)
+constexpr int kSpTileLds = 39 * 1024;      // dynamic LDS bytes per tile at most (with ~0.6 KB static: 4 workgroups per CU)
+constexpr int kSpTileLdsFixed = 2048;      // the tile kernel's fixed dynamic LDS (heavy p; the heavy workgroup's sums)
 // tile entry meta word 0: LDS rows of p1_j (bits 0-11), p2_j (12-23), flags; word 1: LDS slots of
 // p1_j (0-11), p2_j (12-23), the unit's first tile row (24-31)
 constexpr uint32_t kTmHead = 1u << 24, kTmLast = 1u << 25, kTmSwap = 1u << 26, kTmValid = 1u << 27, kTmCut = 1u << 28;
@@ -124,7 +124,7 @@ struct SpPlanHost {
     std::vector<int32_t> tile_halo;                    // the tiles' halo rows (local row ids)
     std::vector<int32_t> tile_xoff;                    // per own row its cross slots (destination order)
     std::vector<int32_t> tile_xdst;                    // per cut entry (source order): its 2 cross slots
-    double tile_bytes[2] = {0, 0};                     // algorithmic bytes per CG iteration: product, update
+    double tile_bytes[3] = {0, 0, 0};                  // algorithmic bytes per CG iteration: product, update; fused
 };
 // the groups and rows build_tiles needs (spcg_plan.cpp step 5)
 struct TileInput {
@@ -250,15 +250,11 @@ struct SpDev {
     const int2 *tchunk = nullptr;                         // per chunk (first le, first cross slot)
     const int32_t *trs = nullptr, *thalo = nullptr, *txoff = nullptr;
     const int2 *txdst = nullptr;                          // per cut entry: its two cross slots (destination order)
-    // the single-reduction chain's state, double-buffered by iteration parity (k_sp_tcg)
-    double2 *tzp[2] = {nullptr, nullptr};                 // (z, p)
-    double *ts[2] = {nullptr, nullptr}, *tr[2] = {nullptr, nullptr}, *tw[2] = {nullptr, nullptr};
-    double *txc[2] = {nullptr, nullptr};                  // cross slots [n][3], by target row
-    double *hw = nullptr;                                 // heavy sums of A z of the last iteration
-    double *tpart = nullptr, *tgs = nullptr;              // per-workgroup sums [grid][11]; per-XCD group sums
+    double *xc = nullptr;                                 // cross slots [n][3], by target row
     const double *pinfo = nullptr;                        // per pair: Omega (= W of its ARAP edges)
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
+    int32_t tile_fuse = 0;                                // tile mode: the update in the product's (cooperative) launch
     // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the
     // per-iteration ones when *lgate == 0; lambda from *lam_dev instead of the launch argument
     const int *gate = nullptr, *lgate = nullptr;
@@ -277,8 +273,8 @@ void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream
 int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
 int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
-void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) z (zp .x)
-void sp_launch_tcg_setup(const SpDev &G, const double *rhs, double lambda, bool fp32, hipStream_t st);
+void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) p
+int sp_tile_coop_capacity(int lds, int device);   // resident k_sp_tile<*, 1> workgroups (0: no cooperative launch)
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
@@ -318,7 +314,7 @@ class SpSolver {
     // the rows' p.(D + lambda)p terms ((z, p) and D in) and the heavy p (in, out), phase 2 the update
     // (x, r in / out and M in per row, q no longer stored)
     double product_bytes_phase(int k) const {
-        if (G.tile) return H.tile_bytes[k == 1 ? 0 : 1];
+        if (G.tile) return G.tile_fuse && !G.alpha_kernel ? (k == 1 ? H.tile_bytes[2] : 0.0) : H.tile_bytes[k == 1 ? 0 : 1];
         if (k == 1) return H.phase1_bytes + (G.merged ? (double)G.nown * (48 + 48) + (double)G.hd * (16 + 8) : 0.0);
         return H.phase2_bytes + (G.merged ? (double)G.nown * (24 + 24 + 24 + 24 + 48 - 24) : 0.0);
     }
@@ -339,7 +335,7 @@ class SpSolver {
     int32_t n_tiles() const { return G.tile ? G.ntile : 0; }
     bool halo_overlap() const { return G.sd && G.ovl; }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
-        if (G.tile) return 1;                    // tile mode: the update and the product in one launch
+        if (G.tile && G.tile_fuse && !G.alpha_kernel) return 1;   // tile mode: product + update, one launch
         if (G.sd) return 3;                      // + one all-reduce and one grouped send / receive
         if (G.merged) return G.alpha_kernel ? 3 : 2;
         const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;

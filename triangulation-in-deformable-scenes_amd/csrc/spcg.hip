@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <type_traits>
 
 #include "spcg.h"
@@ -1604,27 +1605,17 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update_sd(int it, const S
 }
 
 // ---- tile mode (spcg_tile.cpp): one rank, one keyframe pair ----------------------------------------
-// ONE launch per CG iteration: Chronopoulos & Gear's single-reduction CG (the sharded chain's
-// recurrences, k_sp_update_sd) with the tiles' fused product.  k_sp_tcg<MODE> at iteration it, one
-// workgroup per tile (XCD-dealt like the row blocks):
-//   state  from the record of iteration it - 1 (its reduction, summed by the last workgroup of the
-//          launch before): gamma = r.z, delta = z.Az; beta = gamma / gamma_prev, alpha = gamma /
-//          (delta - beta gamma / alpha_prev) — the same in every workgroup, so no hand-off
-//   update (MODE 1) of iteration it - 1 for the tile's rows AND its halo rows (the halo rows' new z
-//          recomputed here from their owners' previous state, bit for bit what the owner stores —
-//          so no workgroup waits on another): p = z + beta p, s = w + beta s (w = A z of it - 1: the
-//          owner tile's rows plus their cross slots), r -= alpha s, z = M r; own rows also x += alpha
-//          p and store; the heavy dofs the same (every workgroup; workgroup 0 stores)
-//          (MODE 0, the solve's first launch: the setup — M = (H_v + lambda)^-1, r = b, z = M r,
-//          p = s = x = 0 — for the same rows; MODE 2: z as loaded, the Hessian product)
-//   product w = A z over the tile's entries (k_sp_tile's edge pass: z from LDS, the own rows by a
-//          segmented wave scan, in-tile neighbours through LDS slots, cut edges into cross slots in
-//          HBM, destination-ordered), the rows' (D_v + lambda) z and depth couplings
-//   sums   [r.z, r.r, z.Az, the heavy vertices' sums of A z] per workgroup, in a fixed order; the
-//          launch's last workgroup (per-XCD groups, group_sum) writes iteration it's record and the
-//          state (converged, budget, a non-SPD block) the next launch tests
-// The state vectors (z, p), s, r, w and the cross slots are double-buffered by iteration parity: a
-// launch reads its halo rows' iteration it - 1 values while their owners write iteration it.
+// k_sp_tile, one workgroup per tile (XCD-dealt like the row blocks) + one for the heavy dofs (last):
+//   P0  p = z + beta p_prev of the tile's rows and halo rows, and of the heavy dofs, into LDS
+//   P1  per entry (one out-edge of a tile vertex; 64-entry chunks, one per wave and round):
+//       t = J_e p, s = W t; the own rows' J^T s summed over the vertex's lanes (segmented scan, the
+//       last lane stores them in LDS); the j rows' J^T s into their LDS slots, or (cut edge) into two
+//       cross slots in HBM; p.Ap += s t; the pair's J_T^T s
+//   P2  per tile row q = own + its LDS slots + (D_v + lambda) p + sum_dep c_e p_s, stored; the row
+//       and depth terms of p.Ap, the depth scales' sums
+//   one fixed-order workgroup sum of [p.Ap, J_T^T s (6), scale sums (2)] into m1part / part
+// k_sp_tupd: the rows' cross slots added, alpha (workgroup 0, the merged chain's hand-off), the update
+// x += alpha p, r -= alpha q, z = M r and the next (r.z, r.r) — phase 2's tail without its slot loop.
 __device__ __forceinline__ double shfl_up_d(double v, int d) {
     int2 p = __builtin_bit_cast(int2, v);
     p.x = __shfl_up(p.x, (unsigned)d, 64);
@@ -1632,197 +1623,92 @@ __device__ __forceinline__ double shfl_up_d(double v, int d) {
     return __builtin_bit_cast(double, p);
 }
 
-constexpr int kTcgNv = 11;                     // per-workgroup sums: r.z, r.r, z.Az, heavy (6 + 2)
+// heavy vertex h's sum over the tile workgroups' partials (pair: components 0..5, scale s: 6 + s):
+// thread (g, c) = (tid / 8, tid % 8) adds component c of every 32nd partial, the 32 groups in order
+__device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *lds, bool coherent = false) {
+    const int nb = G.t_grid - 1;
+    const int dim = h < G.Q ? 6 : 1, off = h < G.Q ? 0 : 6 + (h - G.Q);
+    const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
+    double acc = 0.0;
+    if (c < dim) {
+        int k = g;
+        for (; k + 7 * 32 < nb; k += 8 * 32) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const double *q = G.part + (int64_t)kSpPart * (k + 32 * u) + off + c;
+                v[u] = coherent ? fetch(q) : *q;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; k < nb; k += 32) {
+            const double *q = G.part + (int64_t)kSpPart * k + off + c;
+            acc += coherent ? fetch(q) : *q;
+        }
+    }
+    lds[threadIdx.x] = acc;
+    __syncthreads();
+    double t = 0.0;
+    if ((int)threadIdx.x < dim)
+        for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
+    return t;
+}
 
-template <class JT, int MODE>
-__global__ void __launch_bounds__(256) k_sp_tcg(int it, const SpDev G, const JT *__restrict__ Jarap, double lam,
-                                                const double *__restrict__ rhs) {
+// FU 1 (opt-in, DEFTRI_SP_TILE_FUSE=1, when the grid is co-resident: a cooperative launch): the update follows in the
+// same launch — every workgroup publishes its sums, the last to arrive forms alpha (phase 2's
+// workgroup-0 arithmetic: the same partials, the same order) and publishes it, the others wait for it;
+// then each tile updates its own rows from the q it holds (+ its cross slots, written agent-coherent)
+// and the heavy workgroup the heavy dofs, and the (r.z, r.r) of iteration it + 1 are summed as in
+// k_sp_tupd.  One launch per CG iteration; no q stored.
+template <class JT, int FU>
+__global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     extern __shared__ double lds[];
-    __shared__ double red[kTcgNv][4];
-    __shared__ double hz[8], hr[8];
+    __shared__ double red[9][4];
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
+    double beta;
+    if (const int st = it_state(G, it, beta)) {
+        if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
+        return;
+    }
     const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int cur = MODE == 2 ? 0 : it & 1, prv = cur ^ 1;
-    double alpha = 0.0, beta = 0.0;
-    if (MODE != 2 && G.rec[0] != 0.0) return;        // stopped (converged, budget, breakdown, bad block)
-    if (MODE == 1) {
-        const double *r1 = G.red + (int64_t)kSpRed * (it - 1);
-        const double g1 = r1[0], d1 = r1[4];
-        double den = d1;
-        if (it > 1) {
-            const double *r2 = G.red + (int64_t)kSpRed * (it - 2);
-            beta = g1 / r2[0];
-            den = d1 - beta * g1 / r2[3];
+    const bool heavy_wg = b == (int)gridDim.x - 1;
+    double pap = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
+    double qk[3] = {0, 0, 0}, pk[3] = {0, 0, 0}, phv = 0.0;     // FU: the row's q and p (tid < nr), heavy p
+    int lrow = -1;
+    if (heavy_wg) {                                // the heavy dofs: p for the update, lambda |p_h|^2
+        for (int64_t dd = tid; dd < G.hd; dd += 256) {
+            const double p = pval(G.zp, beta, dd);
+            G.ph[dd] = p;
+            phv = p;
+            pap += lam * (p * p);
         }
-        alpha = g1 / den;
-        if (!(den > 0.0) || !isfinite(alpha) || !isfinite(beta)) {
-            if (b == 0 && tid == 0) { G.rec[0] = kSpBreakdown; G.rec[1] = it - 1; }
-            return;                                   // (every workgroup takes this branch)
-        }
-        if (b == 0 && tid == 0) G.red[(int64_t)kSpRed * (it - 1) + 3] = alpha;
-    }
-    const int hd = (int)G.hd;
-    double gam = 0.0, rrs = 0.0, del = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
-    // heavy dofs (hd <= 8): every workgroup forms their new z (its edges need T_g z, the depth scales'
-    // z); workgroup 0 stores the state and counts them in the sums
-    if (MODE == 2) {
-        if (tid < hd) hz[tid] = G.tzp[0][tid].x;
-    } else if (MODE == 0) {
-        if (tid == 0) {
-            // M_h: T_g 6 x 6 (inverse of its block + lambda), scales 1 / (h + lambda); z = M r
-            double Mo[36];
-            bool ok = true;
-            for (int h = 0; h < G.Q + G.S; h++) {
-                const int o = heavy_dof(G, h);
-                if (h < G.Q) {
-                    if (!inv6(G.hl + 21 * (int64_t)h, lam, Mo)) { ok = false; for (int k = 0; k < 36; k++) Mo[k] = 0.0; }
-                    for (int a = 0; a < 6; a++) {
-                        double z = 0.0;
-                        for (int c = 0; c < 6; c++) z += Mo[a * 6 + c] * rhs[o + c];
-                        hz[o + a] = z;
-                        hr[o + a] = rhs[o + a];
-                    }
-                    if (b == 0) for (int k = 0; k < 36; k++) G.Mh[36 * (int64_t)h + k] = Mo[k];
-                } else {
-                    const double a = G.hl[21 * (int64_t)G.Q + (h - G.Q)] + lam;
-                    double m = 0.0;
-                    if (!(a > 0.0)) ok = false;
-                    else m = 1.0 / a;
-                    if (b == 0) G.Mh[36 * (int64_t)G.Q + (h - G.Q)] = m;
-                    hr[o] = rhs[o];
-                    hz[o] = m * rhs[o];
-                }
-            }
-            if (!ok && b == 0) st_sc1(G.rec + 4, 1.0);   // a non-SPD block: the solve stops (below)
-        }
-        __syncthreads();
-        if (b == 0 && tid < hd) {
-            G.tzp[0][tid] = make_double2(hz[tid], 0.0);
-            G.tr[0][tid] = hr[tid];
-            G.ts[0][tid] = 0.0;
-            G.x[tid] = 0.0;
-            if (G.include_heavy) { gam += hr[tid] * hz[tid]; rrs += hr[tid] * hr[tid]; }
-        }
-    } else {
-        __shared__ double hs[8], hpv[8];
-        if (tid < hd) {
-            const double2 v = G.tzp[prv][tid];
-            const double w = G.hw[tid] + lam * v.x;
-            const double p = v.x + beta * v.y;
-            const double s = w + beta * G.ts[prv][tid];
-            hr[tid] = G.tr[prv][tid] - alpha * s;
-            hs[tid] = s;
-            hpv[tid] = p;
-        }
-        __syncthreads();
-        if (tid < hd) {
-            double z;
-            if (tid < 6 * G.Q) {
-                const int h = tid / 6, a = tid - 6 * h;
-                const double *Mh = G.Mh + 36 * (int64_t)h + a * 6;
-                z = 0.0;
-                for (int c = 0; c < 6; c++) z += Mh[c] * hr[6 * h + c];
-            } else {
-                z = G.Mh[36 * (int64_t)G.Q + (tid - 6 * G.Q)] * hr[tid];
-            }
-            hz[tid] = z;
-            if (b == 0) {
-                G.x[tid] += alpha * hpv[tid];
-                G.tzp[cur][tid] = make_double2(z, hpv[tid]);
-                G.ts[cur][tid] = hs[tid];
-                G.tr[cur][tid] = hr[tid];
-                if (G.include_heavy) { gam += hr[tid] * z; rrs += hr[tid] * hr[tid]; }
-            }
+        if (!G.include_heavy) pap = 0.0;
+        if (!FU) {
+            pap = block_sum(pap, red[0]);
+            if (tid == 0) G.m1part[b] = pap;
+            return;
         }
     }
-    if (b == 0 && tid < hd && G.include_heavy) del += lam * (hz[tid] * hz[tid]);
     const int seg = (G.ntile + 7) / 8;
-    const int t = (b & 7) * seg + (b >> 3);
+    const int t = heavy_wg ? G.ntile : (b & 7) * seg + (b >> 3);
     if (t < G.ntile) {
         const int32_t *T = G.ttab + 8 * (int64_t)t;
-        const int r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5];
-        double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr;     // (rs: T[6] slots)
-        const double2 *__restrict__ zp0 = G.tzp[prv];
-        // the rows' z of this iteration: own rows then halo rows
+        const int r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
+        double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
         for (int i = tid; i < nr + nh; i += 256) {
-            const bool own = i < nr;
-            const int row = own ? r0 + i : G.thalo[h0 + i - nr];
+            const int row = i < nr ? r0 + i : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
-            double z[3];
-            if (MODE == 2) {
 #pragma unroll
-                for (int c = 0; c < 3; c++) z[c] = G.tzp[0][o + c].x;
-            } else if (MODE == 0) {
-                double Hl[6], M[6], r[3];
-#pragma unroll
-                for (int k = 0; k < 6; k++) Hl[k] = G.Hv[6 * (int64_t)row + k];
-#pragma unroll
-                for (int c = 0; c < 3; c++) r[c] = rhs[o + c];
-                if (!inv3(Hl, lam, M)) {
-                    if (own) st_sc1(G.rec + 4, 1.0);     // (coherent across the XCDs: the last workgroup reads it)
-#pragma unroll
-                    for (int k = 0; k < 6; k++) M[k] = 0.0;
-                }
-                mul3(M, r, z);
-                if (own) {
-#pragma unroll
-                    for (int k = 0; k < 6; k++) G.Mv[6 * (int64_t)row + k] = M[k];
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        G.tr[0][o + c] = r[c];
-                        G.tzp[0][o + c] = make_double2(z[c], 0.0);
-                        G.ts[0][o + c] = 0.0;
-                        G.x[o + c] = 0.0;
-                        gam += r[c] * z[c];
-                        rrs += r[c] * r[c];
-                    }
-                }
-            } else {
-                double2 v[3];
-                double s[3], r[3], w[3], M[6];
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    v[c] = zp0[o + c];
-                    s[c] = G.ts[prv][o + c];
-                    r[c] = G.tr[prv][o + c];
-                    w[c] = G.tw[prv][o + c];
-                }
-#pragma unroll
-                for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)row + k];
-                for (int k = G.txoff[row]; k < G.txoff[row + 1]; k++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) w[c] += G.txc[prv][3 * (int64_t)k + c];
-                double p[3];
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    p[c] = v[c].x + beta * v[c].y;
-                    s[c] = w[c] + beta * s[c];
-                    r[c] = r[c] - alpha * s[c];
-                }
-                mul3(M, r, z);
-                if (own) {
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        G.x[o + c] += alpha * p[c];
-                        G.tzp[cur][o + c] = make_double2(z[c], p[c]);
-                        G.ts[cur][o + c] = s[c];
-                        G.tr[cur][o + c] = r[c];
-                        gam += r[c] * z[c];
-                        rrs += r[c] * r[c];
-                    }
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 3; c++) pL[3 * i + c] = z[c];
+            for (int c = 0; c < 3; c++) pL[3 * i + c] = pval(G.zp, beta, o + c);
         }
         for (int i = tid; i < 3 * nr; i += 256) up[i] = 0.0;
+        if (tid < 8) hp[tid] = tid < G.hd ? pval(G.zp, beta, tid) : 0.0;     // T_g (6), scales (<= 2)
         __syncthreads();
-        // product: the tile's entries (64-entry chunks, one per wave and round)
         const double W = G.pinfo[0];               // W of every ARAP edge of the pair (k_lin_arap: W = Omega)
         const int64_t jld = G.jld;
         const uint64_t lt = (1ull << lane) - 1;
-        double *__restrict__ xcw = G.txc[cur];
         for (int base = 0; base < ne; base += 256) {
             if (base + 64 * wv >= ne) break;       // (ne is a multiple of 64: whole waves in or out)
             const int64_t k = (int64_t)e0 + base + tid;
@@ -1834,8 +1720,6 @@ __global__ void __launch_bounds__(256) k_sp_tcg(int it, const SpDev G, const JT 
             double J[18];
 #pragma unroll
             for (int c = 0; c < 18; c++) J[c] = valid ? (double)Jarap[c * jld + le] : 0.0;
-            int2 xd = make_int2(0, 0);
-            if (valid && cut) xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
             const int ub = (int)(m.y >> 24), sw = (int)((m.x >> 26) & 1u);
             const int ra = valid ? ub + sw : 0, rb = valid ? ub + 1 - sw : 0;
             const int rj0 = valid ? (int)(m.x & 0xfffu) : 0, rj1 = valid ? (int)((m.x >> 12) & 0xfffu) : 0;
@@ -1846,15 +1730,24 @@ __global__ void __launch_bounds__(256) k_sp_tcg(int it, const SpDev G, const JT 
 #pragma unroll
                 for (int c = 0; c < 3; c++) tt += J[3 * kk + c] * pL[3 * rows[kk] + c];
 #pragma unroll
-            for (int c = 0; c < 6; c++) tt += J[12 + c] * hz[c];
+            for (int c = 0; c < 6; c++) tt += J[12 + c] * hp[c];
             const double s = W * tt;
-            del += s * tt;
+            pap += s * tt;
 #pragma unroll
             for (int c = 0; c < 6; c++) jts[c] += J[12 + c] * s;
             if (valid) {
-                if (cut) {
+                if (cut) {                         // the two cross slots, at their rows' positions
+                    const int2 xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
 #pragma unroll
-                    for (int c = 0; c < 3; c++) { xcw[3 * (int64_t)xd.x + c] = J[6 + c] * s; xcw[3 * (int64_t)xd.y + c] = J[9 + c] * s; }
+                    for (int c = 0; c < 3; c++) {
+                        if (FU) {                  // read by other workgroups in this launch
+                            st_sc1(G.xc + 3 * (int64_t)xd.x + c, J[6 + c] * s);
+                            st_sc1(G.xc + 3 * (int64_t)xd.y + c, J[9 + c] * s);
+                        } else {
+                            G.xc[3 * (int64_t)xd.x + c] = J[6 + c] * s;
+                            G.xc[3 * (int64_t)xd.y + c] = J[9 + c] * s;
+                        }
+                    }
                 } else {
                     const int s0 = (int)(m.y & 0xfffu), s1 = (int)((m.y >> 12) & 0xfffu);
 #pragma unroll
@@ -1895,90 +1788,259 @@ __global__ void __launch_bounds__(256) k_sp_tcg(int it, const SpDev G, const JT 
             const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
             const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
             const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
-            del += (p[0] * q0 + p[1] * q1) + p[2] * q2;
+            pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
             q[0] += q0; q[1] += q1; q[2] += q2;
             for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {
                 const int sc_ = G.dsc[j];
                 const double *cd = G.cdep + 3 * (int64_t)j;
-                const double ps = hz[6 + sc_];
+                const double ps = hp[6 + sc_];
                 const double cp = (cd[0] * p[0] + cd[1] * p[1]) + cd[2] * p[2];
                 const double td = cp + G.wss[j] * ps;
-                del += ps * (cp + td);
+                pap += ps * (cp + td);
                 if (sc_ == 0) sacc[0] += td;
                 else sacc[1] += td;
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += cd[c] * ps;
             }
+            if (FU) {
+                lrow = l;
 #pragma unroll
-            for (int c = 0; c < 3; c++) G.tw[cur][o + c] = q[c];
+                for (int c = 0; c < 3; c++) { qk[c] = q[c]; pk[c] = p[c]; }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+            }
         }
     }
-    // [r.z, r.r, z.Az, J_T^T s (6), scale sums (2)]: wave butterflies, then the waves in order
-    double a[kTcgNv] = {gam, rrs, del, jts[0], jts[1], jts[2], jts[3], jts[4], jts[5], sacc[0], sacc[1]};
+    // [p.Ap, J_T^T s, scale sums]: wave butterflies, then the waves in order
+    double a[9] = {pap, jts[0], jts[1], jts[2], jts[3], jts[4], jts[5], sacc[0], sacc[1]};
 #pragma unroll
-    for (int kk = 0; kk < kTcgNv; kk++) {
+    for (int kk = 0; kk < 9; kk++) {
         const double v = wave_sum(a[kk]);
         if (lane == 0) red[kk][wv] = v;
     }
     __syncthreads();
-    if (MODE == 2) {                               // the Hessian product: the heavy partials only
-        if (tid >= 3 && tid < kTcgNv)
-            G.part[(int64_t)kSpPart * b + tid - 3] = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        return;
+    if (tid < 9) {
+        const double v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
+        if (FU) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
+        else if (tid == 0) G.m1part[b] = v;
+        else G.part[(int64_t)kSpPart * b + tid - 1] = v;
     }
-    if (tid == 0)
-        for (int kk = 0; kk < kTcgNv; kk++)
-            publish(G, G.tpart + (int64_t)kTcgNv * b + kk, (red[kk][0] + red[kk][1]) + (red[kk][2] + red[kk][3]));
-    double tot[kTcgNv];
-    if (group_sum<kTcgNv>(G, G.cnt, G.tpart, G.tgs, red, tot) && tid == 0) {
-        double *rk = G.red + (int64_t)kSpRed * it;
-        rk[0] = tot[0];
-        rk[1] = tot[1];
-        rk[4] = tot[2];
-        for (int h = 0; h < hd; h++) G.hw[h] = h < 6 ? tot[3 + h] : tot[9 + (h - 6)];
-        // the state of iteration it, which the next launch tests (this is the launch's last workgroup)
-        if (G.rec[0] == 0.0) {
-            const double rr0 = it == 0 ? tot[1] : G.red[1];
-            int st = 0;
-            if (ld_sc1(G.rec + 4) != 0.0) st = kSpBadBlock;
-            else if (tot[1] <= G.tol2 * rr0) st = kSpConverged;
-            else if (it >= G.max_it) st = kSpBudget;
-            if (st) { G.rec[0] = st; G.rec[1] = it; }
+    if constexpr (FU == 1) {
+        // the arrival: every thread's stores (cross slots, partials) acknowledged, then one ticket
+        __shared__ int s_last;
+        __shared__ double s_alpha;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __syncthreads();
+        if (tid == 0)
+            s_last = __hip_atomic_fetch_add(G.cnt + 44, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+        __syncthreads();
+        if (s_last) {
+            // alpha as m2_alpha_make forms it: thread t adds partials t, t + 256, ..., then the block
+            double acc = 0.0;
+            for (int j = tid; j < (int)gridDim.x; j += 256) acc += fetch(G.m1part + j);
+            acc = block_sum(acc, red[0]);
+            if (tid == 0) {
+                double alpha = G.red[(int64_t)kSpRed * it] / acc;
+                if (!(acc > 0.0) || !isfinite(alpha) || alpha == 0.0) {
+                    st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpBreakdown);
+                    alpha = __builtin_nan("");
+                }
+                st_sc1(G.cnt + 44, 0);
+                st_sc1(G.red + (int64_t)kSpRed * it + 3, alpha);
+                s_alpha = alpha;
+            }
+        } else if (tid == 0) {
+            const double *w = G.red + (int64_t)kSpRed * it + 3;
+            int n = it == G.inj_timeout_it ? (1 << 16) : 0;
+            double v = ld_sc1(w);
+            while (__double_as_longlong(v) == 0 && n < (1 << 16)) {
+                __builtin_amdgcn_s_sleep(2);
+                v = ld_sc1(w);
+                n++;
+            }
+            if (n >= (1 << 16)) {                  // never expected: stop the solve, skip the update
+                st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpTimeout);
+                v = __builtin_nan("");
+            }
+            s_alpha = v;
         }
+        __syncthreads();
+        const double alpha = s_alpha;
+        double pq = 0.0, rr2 = 0.0;
+        if (heavy_wg) {
+            // k_sp_tupd's heavy update, one heavy vertex after the other
+            __shared__ double rsh[6], tz[2][6];
+            for (int h = 0; h < G.Q + G.S; h++) {
+                const double th = tile_heavy_sum(G, h, lds, true);   // (the tile LDS is free here)
+                const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+                const int aa = isnan(alpha) ? dim : tid;
+                double p = 0.0, r = 0.0;
+                if (aa < dim) {
+                    p = G.ph[o + aa];
+                    const double q = th + lam * p;
+                    G.x[o + aa] += alpha * p;
+                    r = G.r[o + aa] - alpha * q;
+                    G.r[o + aa] = r;
+                    rsh[aa] = r;
+                }
+                __syncthreads();
+                if (aa < dim) {
+                    const double *Mh = h < G.Q ? G.Mh + 36 * (int64_t)h + aa * 6 : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+                    double z = 0.0;
+                    for (int c = 0; c < dim; c++) z += Mh[c] * rsh[c];
+                    G.zp[o + aa] = make_double2(z, p);
+                    tz[0][aa] = r * z;
+                    tz[1][aa] = r * r;
+                }
+                __syncthreads();
+                if (tid == 0 && !isnan(alpha))
+                    for (int c = 0; c < dim; c++) { pq += tz[0][c]; rr2 += tz[1][c]; }
+                __syncthreads();
+            }
+            (void)phv;
+        } else if (lrow >= 0 && !isnan(alpha)) {
+            const int l = lrow;
+            const int64_t o = G.hd + 3 * (int64_t)l;
+            for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) qk[c] += fetch(G.xc + 3 * (int64_t)k + c);
+            double M[6], r[3], z[3];
+#pragma unroll
+            for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.x[o + c] = G.x[o + c] + alpha * pk[c];
+                r[c] = G.r[o + c] - alpha * qk[c];
+            }
+            z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
+            z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
+            z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.r[o + c] = r[c];
+                G.zp[o + c] = make_double2(z[c], pk[c]);
+                pq += r[c] * z[c];
+                rr2 += r[c] * r[c];
+            }
+        }
+        __syncthreads();                           // (red is free again)
+        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
+        m2_dots(G, it, red);
     }
 }
 
-// the Hessian product's finish (after k_sp_tcg<*, 2>): q of every row = its w plus its cross slots,
-// q of the heavy dofs = the workgroups' partials + lambda z
-__global__ void __launch_bounds__(256) k_sp_tcg_fin(const SpDev G, double lam) {
-    __shared__ double lds[256];
-    if ((int)blockIdx.x < G.Q + G.S) {
-        const int h = blockIdx.x, dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h), off = h < G.Q ? 0 : 6 + (h - G.Q);
-        const int nb = G.t_grid;
-        const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
-        double acc = 0.0;
-        if (c < dim)
-            for (int k = g; k < nb; k += 32) acc += G.part[(int64_t)kSpPart * k + off + c];
-        lds[threadIdx.x] = acc;
-        __syncthreads();
-        if ((int)threadIdx.x < dim) {
-            double t = 0.0;
-            for (int gg = 0; gg < 32; gg++) t += lds[8 * gg + threadIdx.x];
-            G.q[o + threadIdx.x] = t + lam * G.tzp[0][o + threadIdx.x].x;
-        }
+// FIN 0: the CG update of iteration it (merged-chain hand-off); FIN 1: the product only — q of every
+// row (its cross slots added) and of the heavy dofs stored (the iterative plan's Hessian product)
+template <int FIN>
+__global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double lam) {
+    __shared__ double red4[4];
+    if (gated_off(G.gate)) return;
+    lam = lam_of(G, lam);
+    double beta = 0.0;
+    AlphaPre pf;
+    if (!FIN && !G.alpha_kernel && blockIdx.x == 0) m2_alpha_loads(G, it, pf);
+    if (const int st = it_state(G, it, beta)) {
+        if (!FIN && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
-    const int l = ((int)blockIdx.x - (G.Q + G.S)) * 256 + (int)threadIdx.x;
-    if (l >= G.nown) return;
-    const int64_t o = G.hd + 3 * (int64_t)l;
-    double q[3];
+    double alpha = 0.0, pq = 0.0, rr2 = 0.0;
+    if (!FIN) {
+        if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];
+        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true, pf);
+    }
+    if ((int)blockIdx.x < G.m_nh) {
+        __shared__ double lds[256];
+        __shared__ double rsh[6], tz[2][6];
+        const int h = blockIdx.x;
+        const bool has = h < G.Q + G.S;
+        const double th = has ? tile_heavy_sum(G, h, lds) : 0.0;
+        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (has) {
+            const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
+            const int a = (!FIN && isnan(alpha)) ? dim : (int)threadIdx.x;
+            double p = 0.0, r = 0.0;
+            if (a < dim) {
+                p = G.ph[o + a];
+                const double q = th + lam * p;
+                if (FIN) {
+                    G.q[o + a] = q;
+                } else {
+                    G.x[o + a] += alpha * p;
+                    r = G.r[o + a] - alpha * q;
+                    G.r[o + a] = r;
+                    rsh[a] = r;
+                }
+            }
+            if (!FIN) {
+                __syncthreads();
+                if (a < dim) {
+                    const double *Mh = h < G.Q ? G.Mh + 36 * (int64_t)h + a * 6 : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
+                    double z = 0.0;
+                    for (int c = 0; c < dim; c++) z += Mh[c] * rsh[c];
+                    G.zp[o + a] = make_double2(z, p);
+                    tz[0][a] = r * z;
+                    tz[1][a] = r * r;
+                }
+                __syncthreads();
+                if (threadIdx.x == 0 && !isnan(alpha))
+                    for (int c = 0; c < dim; c++) { pq += tz[0][c]; rr2 += tz[1][c]; }
+            }
+        }
+    } else {
+        const int lb = row_block((int)blockIdx.x - G.m_nh, G.nrb);
+        const int l = lb * 256 + (int)threadIdx.x;
+        const bool on = l < G.nown;
+        double q[3] = {0, 0, 0}, pr[3] = {0, 0, 0}, xo[3] = {0, 0, 0}, ro[3] = {0, 0, 0}, M[6] = {0, 0, 0, 0, 0, 0};
+        int64_t o = 0;
+        if (on) {
+            o = G.hd + 3 * (int64_t)l;
 #pragma unroll
-    for (int c = 0; c < 3; c++) q[c] = G.tw[0][o + c];
-    for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)
+            for (int c = 0; c < 3; c++) q[c] = G.q[o + c];
+            for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)          // the row's cross slots, contiguous
 #pragma unroll
-        for (int c = 0; c < 3; c++) q[c] += G.txc[0][3 * (int64_t)k + c];
+                for (int c = 0; c < 3; c++) q[c] += G.xc[3 * (int64_t)k + c];
+            if (FIN) {
 #pragma unroll
-    for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const double2 v = G.zp[o + c];
+                    pr[c] = __fma_rn(beta, v.y, v.x);
+                    xo[c] = G.x[o + c];
+                    ro[c] = G.r[o + c];
+                }
+#pragma unroll
+                for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
+            }
+        }
+        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (!FIN && on && !isnan(alpha)) {
+            double r[3], z[3];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.x[o + c] = xo[c] + alpha * pr[c];
+                r[c] = ro[c] - alpha * q[c];
+            }
+            z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
+            z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
+            z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                G.r[o + c] = r[c];
+                G.zp[o + c] = make_double2(z[c], pr[c]);
+                pq += r[c] * z[c];
+                rr2 += r[c] * r[c];
+            }
+        }
+    }
+    if (FIN) return;
+    __shared__ double red[2][4];
+    pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
+    m2_dots(G, it, red);
 }
 
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
@@ -2085,12 +2147,42 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         return;
     }
     if (G.tile) {
-        // one launch: the update of iteration it - 1 and the product of iteration it (it >= 1; the
-        // solve's first launch is sp_launch_tcg_setup's)
+        // [tiles, XCD-dealt][heavy dofs]; [m_nh heavy workgroups][row blocks]
         hipEvent_t e0_ = prof_begin(st);
-        if (fp32) hipLaunchKernelGGL((sp::k_sp_tcg<float, 1>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja32, lambda, nullptr);
-        else hipLaunchKernelGGL((sp::k_sp_tcg<double, 1>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda, nullptr);
-        prof_end("sp_tcg", e0_, (unsigned)G.t_grid, 0.0, st);
+        if (G.tile_fuse && !G.alpha_kernel) {
+            // one cooperative launch (every workgroup resident: the update waits on all of them)
+            int it_ = it;
+            SpDev g_ = G;
+            double lam_ = lambda;
+            hipError_t e;
+            if (fp32) {
+                const float *j_ = G.Ja32;
+                void *args[] = {&it_, &g_, &j_, &lam_};
+                e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&sp::k_sp_tile<float, 1>), dim3(G.t_grid), dim3(256),
+                                               args, (unsigned)G.tile_lds, st);
+            } else {
+                const double *j_ = G.Ja;
+                void *args[] = {&it_, &g_, &j_, &lam_};
+                e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&sp::k_sp_tile<double, 1>), dim3(G.t_grid), dim3(256),
+                                               args, (unsigned)G.tile_lds, st);
+            }
+            if (e == hipSuccess) {
+                prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
+                return;
+            }
+            // refused (the grid not resident at once): nothing ran — the separate update launch below
+            (void)hipGetLastError();
+            static bool warned = false;
+            if (!warned) {
+                std::fprintf(stderr, "[deftri] cooperative tile launch refused (%s): separate update launch\n", hipGetErrorString(e));
+                warned = true;
+            }
+        }
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda);
+        prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
+        if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
+        SPL("sp_tupd", (sp::k_sp_tupd<0>), G.m_nh + sp::row_grid(G.nrb), it, G, lambda);
         return;
     }
     if (G.merged) {
@@ -2114,19 +2206,24 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     else launch_phase2<double, 0>(G, grid, it, lambda, G.pj, st);
 }
 
-void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {
-    hipEvent_t e0_ = prof_begin(st);
-    if (fp32) hipLaunchKernelGGL((sp::k_sp_tcg<float, 2>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda, nullptr);
-    else hipLaunchKernelGGL((sp::k_sp_tcg<double, 2>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda, nullptr);
-    prof_end("sp_tcg_product", e0_, (unsigned)G.t_grid, 0.0, st);
-    SPL("sp_tcg_fin", sp::k_sp_tcg_fin, G.Q + G.S + (G.nown + 255) / 256, G, lambda);
+// workgroups of k_sp_tile<*, 1> the device keeps resident at once (a cooperative launch's limit)
+int sp_tile_coop_capacity(int lds, int device) {
+    int attr = 0;
+    if (hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !attr) return 0;
+    int nb = 0, nb32 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sp::k_sp_tile<double, 1>, 256, (size_t)lds) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb32, sp::k_sp_tile<float, 1>, 256, (size_t)lds) != hipSuccess) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    return std::min(nb, nb32) * prop.multiProcessorCount;
 }
 
-void sp_launch_tcg_setup(const SpDev &G, const double *rhs, double lambda, bool fp32, hipStream_t st) {
+void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {
     hipEvent_t e0_ = prof_begin(st);
-    if (fp32) hipLaunchKernelGGL((sp::k_sp_tcg<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda, rhs);
-    else hipLaunchKernelGGL((sp::k_sp_tcg<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda, rhs);
-    prof_end("sp_tcg0", e0_, (unsigned)G.t_grid, 0.0, st);
+    if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda);
+    else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda);
+    prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
+    SPL("sp_tupd", (sp::k_sp_tupd<1>), G.m_nh + sp::row_grid(G.nrb), 0, G, lambda);
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }

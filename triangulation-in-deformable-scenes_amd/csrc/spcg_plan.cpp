@@ -615,17 +615,16 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                      + (double)ndl * (4 + jb / 6);                       // depth-coupling slots (p_s in cache)
     H.product_bytes = H.phase1_bytes + H.phase2_bytes;
     if (H.tile) {
-        // tile mode, one k_sp_tcg launch per CG iteration (the update of it - 1 + the product of it):
-        // per own row (z, p), s, r, w, x in and (z, p), s, r, x, w out, M and D in, its cross range
-        // and slot range, its depth couplings (c, W J_s^2, scale, offset); per halo row (z, p), s, r,
-        // w, M and its cross range in (the redundant update); per entry J (valid) and meta; per cut
-        // entry its two cross slots out (+ their positions) and in again (own rows and halo rows)
+        // tile mode per CG iteration: k_sp_tile — per entry J (valid) + meta, per tile row (z, p) + D
+        // + q out + its slot range + its depth couplings (c, W J_s^2, scale, offset), per halo row
+        // (z, p), per cut entry two cross slots out and their positions; k_sp_tupd — per own row (z, p)
+        // in / out, x and r in / out, q in, M, its cross range, per cross slot its value
         const int64_t nvalid = (int64_t)H.arap_ids.size();
-        H.tile_bytes[0] = (double)nvalid * jb + (double)H.tile_entries * 8 +
-                          (double)nown * (48 + 24 + 24 + 24 + 24 + 48 + 48 + 8 + 4 + 48 + 24 + 24 + 24 + 24) +
-                          (double)ndl * (24 + 8 + 4 + 4) + (double)H.tile_halo_rows * (48 + 24 + 24 + 24 + 48 + 8) +
-                          (double)H.tile_cross * (24 + 4 + 24);
-        H.tile_bytes[1] = 0.0;
+        H.tile_bytes[0] = (double)nvalid * jb + (double)H.tile_entries * 8 + (double)nown * (48 + 48 + 24 + 4) +
+                          (double)ndl * (24 + 8 + 4 + 4) + (double)H.tile_halo_rows * 48 + (double)H.tile_cross * (24 + 4);
+        H.tile_bytes[1] = (double)nown * (96 + 48 + 48 + 24 + 48 + 8) + (double)H.tile_cross * 24;
+        // fused (one launch): q stays in registers, p in LDS — no q out / in, no (z, p) reload
+        H.tile_bytes[2] = H.tile_bytes[0] - (double)nown * 24 + H.tile_bytes[1] - (double)nown * (48 + 24);
     }
     static const bool digest = std::getenv("DEFTRI_PLAN_DIGEST") != nullptr;
     if (digest) {

@@ -399,17 +399,14 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.tchunk = reinterpret_cast<const int2 *>(tch);
         G.tmeta = reinterpret_cast<const uint2 *>(tm);
         G.pinfo = P.pair_info;
-        for (int k = 0; k < 2; k++) {
-            double *z2;
-            ALLOC(z2, 2 * G.ndof);
-            G.tzp[k] = reinterpret_cast<double2 *>(z2);
-            ALLOC(G.ts[k], G.ndof); ALLOC(G.tr[k], G.ndof); ALLOC(G.tw[k], G.ndof);
-            ALLOC(G.txc[k], 3 * std::max<int64_t>(H.tile_cross, 1));
-        }
-        ALLOC(G.hw, std::max<int64_t>(H.hd, 1));
-        ALLOC(G.tpart, 11 * (int64_t)G.t_grid);
-        ALLOC(G.tgs, 11 * 8);
-        G.zp = G.tzp[0];                           // (load_p's target: the Hessian product reads buffer 0)
+        ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));
+        // DEFTRI_SP_TILE_FUSE=1: the update in the product's launch when the whole grid is resident at
+        // once (a cooperative launch guarantees it or fails).  Not the default: measured at C2 on MI355X
+        // it is 85 us per CG iteration against 56 us for the two launches (the cooperative launch
+        // alone costs ~18 us; the fused kernel launched plainly still 68 us — the update's rows run
+        // at half a workgroup each behind a grid-wide wait).  DESIGN.md "Tile mode".
+        static const bool fuse_t = std::getenv("DEFTRI_SP_TILE_FUSE") != nullptr;
+        G.tile_fuse = (fuse_t && sp_tile_coop_capacity(G.tile_lds, dev_) >= G.t_grid) ? 1 : 0;
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -425,7 +422,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         const char *e = std::getenv("DEFTRI_SP_P2_TRACE_IT");
         G.p2tr_it = e ? std::atoi(e) : 2;
     }
-    ALLOC(G.cnt, 48);                                      // three ticket sites, 16 counters each
+    ALLOC(G.cnt, 48);                                      // three ticket sites (0, 16, 32: 9 counters each), the tile arrival (44)
     SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
     {
         // heavy linearization chunks (k_sp_glin_heavy): kSpHeavyChunk block partials each, >= 1 per vertex
@@ -600,10 +597,6 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
 // the solve's setup (preconditioner at lambda, r = rhs, (z, p) = (M r, 0), x = 0); sharded: the
 // boundary rows' (z, p) to the ranks whose edges read them, as after every CG update
 int SpSolver::cg_setup(double lambda, const double *rhs) {
-    if (G.tile) {                                  // the setup and the first product in one launch
-        sp_launch_tcg_setup(G, rhs, lambda, fp32_jac != 0, st_);
-        return 0;
-    }
     sp_launch_setup(G, rhs, lambda, st_);
     if (G.sd) return halo_sd();
     if (shard_) return halo(6, reinterpret_cast<double *>(G.zp), true);
@@ -615,10 +608,6 @@ int SpSolver::cg_setup(double lambda, const double *rhs) {
 int SpSolver::cg_chain(double lambda, int from, int to) {
     int rc;
     for (int it = from; it < to; it++) {
-        if (G.tile) {                                  // the update of it and the product of it + 1
-            sp_launch_product(G, it + 1, lambda, fp32_jac != 0, st_);
-            continue;
-        }
         if (G.sd) {                                    // phase 1, phase 2 (A z), one all-reduce, update
             sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
             if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
