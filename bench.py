@@ -28,8 +28,9 @@ Legs of the default C2 line (--no-legs skips them): `north_star_500k` (above, an
 KB8 d0..d3; Data/Realcolon.yaml:15-23,101,110), a CG-heavy regime (the Simulation.yaml headline
 run is near-stalled: ~5 CG iterations per trial at lambda ~1e21).
 
-Printed roofline (the iterative plan, the default): the CG iteration's kernels k_sp_phase1 +
-k_sp_phase2 (the matrix-free product with the update folded in), HBM-bound — from a profiled trial
+Printed roofline (the iterative plan, the default): the CG iteration's kernels — at C2 (one rank, one
+pair: tile mode) k_sp_tile (the matrix-free product, every ARAP edge read once) + k_sp_tupd (the
+update); otherwise k_sp_phase1 + k_sp_phase2 (the product with the update folded in) — HBM-bound, from a profiled trial
 right after the timed region (HIP events on the solver's own stream, active launches only).  Two
 fractions of 8 TB/s: `frac` / `frac_survey` on SURVEY.md §8(d)'s minimal-traffic bytes per CG
 iteration (176 E + 48 R + 40 D + 156 P: fp32 Jacobians, one pass over the edges), and `frac_design`
@@ -421,17 +422,27 @@ def fetch_calibration():
 def product_roofline(stats, rep, ctx, rank):
     """Roofline of the step solver's dominant kernel from a profiled trial (HIP events on the solver
     stream): active launches only (the profiled replay launches exactly the solve's CG iterations)."""
-    if "sp_phase1" in stats:
-        p1, p2 = stats["sp_phase1"], stats["sp_phase2"]
-        its = max(p2["launches"], 1)
+    tile = "sp_tile" in stats
+    if tile or "sp_phase1" in stats:
+        # tile mode (one rank, one pair): k_sp_tile (the product, every ARAP edge read once) +
+        # k_sp_tupd (the update), or k_sp_tile alone when the update is fused into its launch
+        n1, n2 = ("sp_tile", "sp_tupd") if tile else ("sp_phase1", "sp_phase2")
+        none = {"launches": 0, "ms": 0.0, "bytes": 0.0}
+        p1, p2 = stats[n1], stats.get(n2, none)
+        its = max(p2["launches"] or p1["launches"], 1)
         by, ms = p1["bytes"] + p2["bytes"], p1["ms"] + p2["ms"]
         gbs = by / max(ms * 1e-3, 1e-12) / 1e9
         survey = ctx.plan_info().get("survey_bytes") or 0.0
         gbs_s = survey / max(ms / its * 1e-3, 1e-12) / 1e9
-        cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update") if k in stats)
+        cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update", "sp_tile",
+                                          "sp_tupd", "sp_alpha") if k in stats)
         merged = "sp_update" not in stats
-        kname = ("k_sp_phase1+k_sp_phase2 (merged CG iteration: matrix-free product + p.Ap row terms + update)"
-                 if merged else "k_sp_phase1+k_sp_phase2 (matrix-free product)")
+        if tile:
+            kname = ("k_sp_tile+k_sp_tupd (tile mode: matrix-free product reading every ARAP edge once + update)"
+                     if n2 in stats else "k_sp_tile (tile mode, update fused: one cooperative launch per CG iteration)")
+        else:
+            kname = ("k_sp_phase1+k_sp_phase2 (merged CG iteration: matrix-free product + p.Ap row terms + update)"
+                     if merged else "k_sp_phase1+k_sp_phase2 (matrix-free product)")
         out = {"bound": "hbm", "kernel": kname, "achieved": round(gbs_s, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs_s / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_basis": "SURVEY.md 8(d) B_pcg = 176E + 48R + 40D + 156P per CG iteration",
@@ -440,10 +451,11 @@ def product_roofline(stats, rep, ctx, rank):
                 "achieved_design": round(gbs, 1), "frac_design": round(gbs / HBM_PEAK_GBS, 4),
                 "traffic_unit": "bytes per product", "bytes_per_launch": by / its, "launches": its,
                 "avg_active_launch_us": round(1e3 * ms / its, 3),
-                "phase1": {"us": round(1e3 * p1["ms"] / its, 3), "bytes": p1["bytes"] / its,
+                "phase1": {"kernel": "k_" + n1, "us": round(1e3 * p1["ms"] / its, 3), "bytes": p1["bytes"] / its,
                            "gbs": round(p1["bytes"] / max(p1["ms"] * 1e-3, 1e-12) / 1e9, 1)},
-                "phase2": {"us": round(1e3 * p2["ms"] / its, 3), "bytes": p2["bytes"] / its,
+                "phase2": {"kernel": "k_" + n2, "us": round(1e3 * p2["ms"] / its, 3), "bytes": p2["bytes"] / its,
                            "gbs": round(p2["bytes"] / max(p2["ms"] * 1e-3, 1e-12) / 1e9, 1)},
+                "tiles": ctx.plan_info().get("tiles", 0),
                 "cg_iterations": its, "cg_iteration_us": round(1e3 * cg / its, 3), "lambda": rep["lambda_final"],
                 "rank": rank}
         cal, cal_src = fetch_calibration()

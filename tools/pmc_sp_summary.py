@@ -1,6 +1,6 @@
 """Summarize a tools/archive/r03_prof.sh run into profiles/<tag>_pmc_sp_product.json: HBM-side bytes of the
-iterative plan's matrix-free product (k_sp_phase1 + k_sp_phase2, one CG iteration) per active launch
-pair, from rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs, KB * 1024), keyed by the plan's
+iterative plan's CG iteration (k_sp_tile + k_sp_tupd in tile mode, k_sp_phase1 + k_sp_phase2 otherwise)
+per active launch pair, from rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs, KB * 1024), keyed by the plan's
 algorithmic bytes per product so bench.py attaches it only to the same plan.
 
 Launches past convergence return after the state test: only launches longer than 30 % of the
@@ -38,9 +38,12 @@ def main():
     src, dst = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2])
     bench = json.loads((src / "pmc_fetch.json").read_text())
     alg = bench["roofline"]["bytes_per_launch"]
-    out = {"kernel": "k_sp_phase1+k_sp_phase2", "bytes_per_launch_algorithmic": alg, "per_kernel": {}}
+    names = [bench["roofline"]["phase1"].get("kernel", "k_sp_phase1"), bench["roofline"]["phase2"].get("kernel", "k_sp_phase2")]
+    fcsv = (src / "fetch" / "run_counter_collection.csv").read_text()
+    names = [k for k in names if k + "<" in fcsv or k + "(" in fcsv]        # (the fused tile chain: one kernel)
+    out = {"kernel": "+".join(names), "bytes_per_launch_algorithmic": alg, "per_kernel": {}}
     tf = tw = 0.0
-    for k in ("k_sp_phase1", "k_sp_phase2"):
+    for k in names:
         f, df, nf = active_mean(*per_dispatch(src / "fetch" / "run_counter_collection.csv", "FETCH_SIZE", k))
         w, dw, nw = active_mean(*per_dispatch(src / "write" / "run_counter_collection.csv", "WRITE_SIZE", k))
         out["per_kernel"][k] = {"fetch_bytes_raw": f, "write_bytes": w, "active_launches": nf, "mean_ns": df}

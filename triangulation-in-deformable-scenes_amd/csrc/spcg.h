@@ -255,6 +255,8 @@ struct SpDev {
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     int32_t tile_fuse = 0;                                // tile mode: the update in the product's (cooperative) launch
+    int32_t tparts = 0;                                   // tile mode: each k_sp_tile workgroup sums the update's
+                                                          // (r.z, r.r) partials itself (no ticket chain in k_sp_tupd)
     // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the
     // per-iteration ones when *lgate == 0; lambda from *lam_dev instead of the launch argument
     const int *gate = nullptr, *lgate = nullptr;
@@ -268,7 +270,9 @@ void sp_launch_maxdiag_heavy(const SpDev &G, double *out, hipStream_t st);   // 
 void sp_launch_cvt_j(const double *J, float *J32, int64_t n, hipStream_t st, const int *gate = nullptr);
 void sp_launch_setup(const SpDev &G, const double *rhs, double lambda, hipStream_t st);
 void sp_launch_dots(const SpDev &G, int it, hipStream_t st);
-void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
+// last: the chain's last queued iteration (tile mode with G.tparts: its update records the state of
+// iteration it + 1 — the only k_sp_tupd that takes the ticketed sum)
+void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, bool last = true);
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st);
 int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid sizes
 int sp_merged_grid2(const SpDev &G);

@@ -1623,6 +1623,57 @@ __device__ __forceinline__ double shfl_up_d(double v, int d) {
     return __builtin_bit_cast(double, p);
 }
 
+// G.tparts: the state of CG iteration it >= 1 from the (r.z, r.r) partials k_sp_tupd(it - 1) left, one
+// per workgroup of its grid — every k_sp_tile workgroup forms the two sums itself, in one fixed order
+// (thread t the partials t, t + 256, ...; then the block), so every workgroup takes the same branch
+// without the update's two-level ticket chain (~6 dependent round trips at its end).  Workgroup 0
+// writes them into iteration it's record words 0, 1 (k_sp_tupd's alpha, the next beta) and, when
+// the solve stops here, the record.  The checks and their order are it_state's.
+__device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, double (*red)[4]) {
+    beta = 0.0;
+    const double r0 = G.rec[0];
+    const double *rk = G.red + (int64_t)kSpRed * it;
+    const double sw = rk[2];
+    const int n2 = G.m_nh + row_grid(G.nrb);
+    double a0 = 0.0, a1 = 0.0;
+    int j = (int)threadIdx.x;
+    for (; j + 3 * 256 < n2; j += 4 * 256) {
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) v[u] = reinterpret_cast<const double2 *>(G.m2part)[j + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) { a0 += v[u].x; a1 += v[u].y; }
+    }
+    for (; j < n2; j += 256) {
+        const double2 v = reinterpret_cast<const double2 *>(G.m2part)[j];
+        a0 += v.x;
+        a1 += v.y;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    a0 = wave_sum(a0);
+    a1 = wave_sum(a1);
+    if (lane == 0) { red[0][w] = a0; red[1][w] = a1; }
+    __syncthreads();
+    const double s0 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    const double s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    __syncthreads();
+    int st = 0;
+    if (r0 != 0.0) st = (int)r0;
+    else if (sw != 0.0) st = (int)sw;
+    else if (s1 <= G.tol2 * G.red[1]) st = kSpConverged;
+    else if (it >= G.max_it) st = kSpBudget;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (!st) {
+            G.red[(int64_t)kSpRed * it] = s0;
+            G.red[(int64_t)kSpRed * it + 1] = s1;
+        } else {
+            record_stop(G, it, st);
+        }
+    }
+    if (!st) beta = s0 / G.red[(int64_t)kSpRed * (it - 1)];
+    return st;
+}
+
 // heavy vertex h's sum over the tile workgroups' partials (pair: components 0..5, scale s: 6 + s):
 // thread (g, c) = (tid / 8, tid % 8) adds component c of every 32nd partial, the 32 groups in order
 __device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *lds, bool coherent = false) {
@@ -1668,7 +1719,9 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
     double beta;
-    if (const int st = it_state(G, it, beta)) {
+    if (!FU && G.tparts && it > 0) {
+        if (tile_state(G, it, beta, reinterpret_cast<double(*)[4]>(&red[0][0]))) return;
+    } else if (const int st = it_state(G, it, beta)) {
         if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
@@ -1935,7 +1988,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
 // FIN 0: the CG update of iteration it (merged-chain hand-off); FIN 1: the product only — q of every
 // row (its cross slots added) and of the heavy dofs stored (the iterative plan's Hessian product)
 template <int FIN>
-__global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double lam) {
+__global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double lam, int last) {
     __shared__ double red4[4];
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
@@ -2039,6 +2092,10 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
     }
     if (FIN) return;
     __shared__ double red[2][4];
+    if (G.tparts && !last) {                       // the next k_sp_tile's workgroups sum them
+        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, 0);
+        return;
+    }
     pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
     m2_dots(G, it, red);
 }
@@ -2135,7 +2192,7 @@ void sp_launch_dots(const SpDev &G, int it, hipStream_t st) {
     SPL("sp_dots", sp::k_sp_dots, 1, it, G);
 }
 
-void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st) {
+void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, bool last) {
     if (G.sd) {
         // sharded single-reduction chain: [m_nx heavy-z / row-term workgroups][phase-1 blocks];
         // [m_nh heavy-sum / scalar workgroups][row blocks]
@@ -2182,7 +2239,7 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
         else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda);
         prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
         if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
-        SPL("sp_tupd", (sp::k_sp_tupd<0>), G.m_nh + sp::row_grid(G.nrb), it, G, lambda);
+        SPL("sp_tupd", (sp::k_sp_tupd<0>), G.m_nh + sp::row_grid(G.nrb), it, G, lambda, last ? 1 : 0);
         return;
     }
     if (G.merged) {
@@ -2223,7 +2280,7 @@ void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_
     if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda);
     else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda);
     prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
-    SPL("sp_tupd", (sp::k_sp_tupd<1>), G.m_nh + sp::row_grid(G.nrb), 0, G, lambda);
+    SPL("sp_tupd", (sp::k_sp_tupd<1>), G.m_nh + sp::row_grid(G.nrb), 0, G, lambda, 1);
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }

@@ -407,6 +407,11 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         // at half a workgroup each behind a grid-wide wait).  DESIGN.md "Tile mode".
         static const bool fuse_t = std::getenv("DEFTRI_SP_TILE_FUSE") != nullptr;
         G.tile_fuse = (fuse_t && sp_tile_coop_capacity(G.tile_lds, dev_) >= G.t_grid) ? 1 : 0;
+        // each product launch sums the last update's (r.z, r.r) partials itself; only the chain's
+        // last update takes the ticketed sum that records the state (DEFTRI_SP_TILE_TICKETS=1: every
+        // update does, round 4's merged-chain scheme)
+        static const bool tickets = std::getenv("DEFTRI_SP_TILE_TICKETS") != nullptr;
+        G.tparts = tickets ? 0 : 1;
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -616,7 +621,7 @@ int SpSolver::cg_chain(double lambda, int from, int to) {
             continue;
         }
         if (G.merged) {                                // phase 1 (+ alpha), phase 2 (+ update, next dots)
-            sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
+            sp_launch_product(G, it, lambda, fp32_jac != 0, st_, it == to - 1);
             continue;
         }
         const bool dist = shard_;
