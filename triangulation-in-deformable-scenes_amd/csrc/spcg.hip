@@ -828,7 +828,10 @@ __device__ __forceinline__ void m2_alpha_loads(const SpDev &G, int it, AlphaPre 
     for (int u = 0; u < 16; u++) pf.v[u] = j + 256 * u < n ? G.m1part[j + 256 * u] : 0.0;
     pf.gam = G.red[(int64_t)kSpRed * it];
 }
-__device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish, const AlphaPre &pf) {
+// writer = false (tile mode, G.tparts: every workgroup forms alpha itself, the same sum in the same
+// order): the value only, workgroup 0 records it
+__device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *red4, bool publish, const AlphaPre &pf,
+                                                bool writer = true) {
     __shared__ double sa;
     // thread t adds partials t, t + 256, ... in order; sixteen loads in flight (a C2-size launch,
     // ~3,200 partials, in one round trip: alpha is on every row's path), the missing ones as zeros
@@ -848,14 +851,18 @@ __device__ __forceinline__ double m2_alpha_make(const SpDev &G, int it, double *
     if (threadIdx.x == 0) {
         double alpha = gam / a;
         if (!(a > 0.0) || !isfinite(alpha) || alpha == 0.0) {
-            st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpBreakdown);   // read from the next launch on (and m2_dots)
+            if (writer) st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpBreakdown);   // read from the next launch on (and m2_dots)
             alpha = __builtin_nan("");
         }
         // the value is its own flag: word 3 of iteration it's record is zero until this store (the
         // record is cleared per solve; alpha == 0 counts as a breakdown above), so a waiter polls
         // the one word — one round trip after the store instead of a flag and then the value
-        if (publish) st_sc1(G.red + (int64_t)kSpRed * it + 3, alpha);
-        else G.red[(int64_t)kSpRed * it + 3] = alpha;
+        if (!writer) {
+        } else if (publish) {
+            st_sc1(G.red + (int64_t)kSpRed * it + 3, alpha);
+        } else {
+            G.red[(int64_t)kSpRed * it + 3] = alpha;
+        }
         sa = alpha;
     }
     __syncthreads();
@@ -1994,7 +2001,9 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
     lam = lam_of(G, lam);
     double beta = 0.0;
     AlphaPre pf;
-    if (!FIN && !G.alpha_kernel && blockIdx.x == 0) m2_alpha_loads(G, it, pf);
+    // G.tparts: every workgroup forms alpha from the product's partials (no hand-off wait)
+    const bool own_alpha = !FIN && !G.alpha_kernel && (G.tparts || blockIdx.x == 0);
+    if (own_alpha) m2_alpha_loads(G, it, pf);
     if (const int st = it_state(G, it, beta)) {
         if (!FIN && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
@@ -2002,7 +2011,7 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
     double alpha = 0.0, pq = 0.0, rr2 = 0.0;
     if (!FIN) {
         if (G.alpha_kernel) alpha = G.red[(int64_t)kSpRed * it + 3];
-        else if (blockIdx.x == 0) alpha = m2_alpha_make(G, it, red4, true, pf);
+        else if (own_alpha) alpha = m2_alpha_make(G, it, red4, !G.tparts, pf, blockIdx.x == 0);
     }
     if ((int)blockIdx.x < G.m_nh) {
         __shared__ double lds[256];
@@ -2010,7 +2019,7 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
         const int h = blockIdx.x;
         const bool has = h < G.Q + G.S;
         const double th = has ? tile_heavy_sum(G, h, lds) : 0.0;
-        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (!FIN && !own_alpha && !G.alpha_kernel) alpha = m2_alpha_wait(G, it);
         if (has) {
             const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
             const int a = (!FIN && isnan(alpha)) ? dim : (int)threadIdx.x;
@@ -2070,7 +2079,7 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
                 for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
             }
         }
-        if (!FIN && !G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
+        if (!FIN && !own_alpha && !G.alpha_kernel) alpha = m2_alpha_wait(G, it);
         if (!FIN && on && !isnan(alpha)) {
             double r[3], z[3];
 #pragma unroll
