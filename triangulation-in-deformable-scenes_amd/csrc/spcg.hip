@@ -717,7 +717,8 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
             out[1] = s1;
         }
     }
-    if (G.fuse && last_block(G, G.cnt + 32)) {
+    // tile mode (G.tparts, the update unfused): the first product's workgroups sum the partials
+    if (G.fuse && !(G.tparts && !G.tile_fuse) && last_block(G, G.cnt + 32)) {
         // (a bad block recorded by any workgroup stops every later launch through rec[0], which the
         // next launch sees; the sums formed here are then never read)
         __syncthreads();
@@ -1630,8 +1631,9 @@ __device__ __forceinline__ double shfl_up_d(double v, int d) {
     return __builtin_bit_cast(double, p);
 }
 
-// G.tparts: the state of CG iteration it >= 1 from the (r.z, r.r) partials k_sp_tupd(it - 1) left, one
-// per workgroup of its grid — every k_sp_tile workgroup forms the two sums itself, in one fixed order
+// G.tparts: the state of CG iteration it from the (r.z, r.r) partials k_sp_tupd(it - 1) left, one per
+// workgroup of its grid (it = 0: the setup's, one per row block + the heavy one) — every k_sp_tile
+// workgroup forms the two sums itself, in one fixed order
 // (thread t the partials t, t + 256, ...; then the block), so every workgroup takes the same branch
 // without the update's two-level ticket chain (~6 dependent round trips at its end).  Workgroup 0
 // writes them into iteration it's record words 0, 1 (k_sp_tupd's alpha, the next beta) and, when
@@ -1641,18 +1643,19 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
     const double r0 = G.rec[0];
     const double *rk = G.red + (int64_t)kSpRed * it;
     const double sw = rk[2];
-    const int n2 = G.m_nh + row_grid(G.nrb);
+    const int n2 = it == 0 ? G.nrb + 1 : G.m_nh + row_grid(G.nrb);
+    const double2 *parts = reinterpret_cast<const double2 *>(it == 0 ? G.upart : G.m2part);
     double a0 = 0.0, a1 = 0.0;
     int j = (int)threadIdx.x;
     for (; j + 3 * 256 < n2; j += 4 * 256) {
         double2 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = reinterpret_cast<const double2 *>(G.m2part)[j + 256 * u];
+        for (int u = 0; u < 4; u++) v[u] = parts[j + 256 * u];
 #pragma unroll
         for (int u = 0; u < 4; u++) { a0 += v[u].x; a1 += v[u].y; }
     }
     for (; j < n2; j += 256) {
-        const double2 v = reinterpret_cast<const double2 *>(G.m2part)[j];
+        const double2 v = parts[j];
         a0 += v.x;
         a1 += v.y;
     }
@@ -1667,17 +1670,14 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
     int st = 0;
     if (r0 != 0.0) st = (int)r0;
     else if (sw != 0.0) st = (int)sw;
-    else if (s1 <= G.tol2 * G.red[1]) st = kSpConverged;
+    else if (s1 <= G.tol2 * (it == 0 ? s1 : G.red[1])) st = kSpConverged;
     else if (it >= G.max_it) st = kSpBudget;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (!st) {
-            G.red[(int64_t)kSpRed * it] = s0;
-            G.red[(int64_t)kSpRed * it + 1] = s1;
-        } else {
-            record_stop(G, it, st);
-        }
+        G.red[(int64_t)kSpRed * it] = s0;
+        G.red[(int64_t)kSpRed * it + 1] = s1;
+        if (st) record_stop(G, it, st);
     }
-    if (!st) beta = s0 / G.red[(int64_t)kSpRed * (it - 1)];
+    if (!st && it > 0) beta = s0 / G.red[(int64_t)kSpRed * (it - 1)];
     return st;
 }
 
@@ -1726,7 +1726,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
     double beta;
-    if (!FU && G.tparts && it > 0) {
+    if (!FU && G.tparts && (it > 0 || !G.tile_fuse)) {
         if (tile_state(G, it, beta, reinterpret_cast<double(*)[4]>(&red[0][0]))) return;
     } else if (const int st = it_state(G, it, beta)) {
         if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);

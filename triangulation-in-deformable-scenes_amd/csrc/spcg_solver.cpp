@@ -1206,7 +1206,7 @@ int SpSolver::hessian_product(double lambda, const double *x, double *y, int64_t
     const double one = 1.0;
     SPOK(hipMemcpyAsync(G.red + 1, &one, sizeof(double), hipMemcpyHostToDevice, st_));
     SpDev g = G;
-    g.merged = 0; g.fuse = 0; g.fuse_heavy = 0;
+    g.merged = 0; g.fuse = 0; g.fuse_heavy = 0; g.tparts = 0;
     g.max_it = 1;
     g.tol2 = 0.0;
     if (G.tile) {                                  // the fused product + its cross slots and heavy sums
