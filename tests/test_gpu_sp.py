@@ -325,12 +325,24 @@ def _fusion_worker(env, q):
                [a.tobytes() for a in ctx.download()]))
 
 
-def _fusion_runs(envs):
+def _glin_worker(env, q):
+    os.environ.update(env)
+    from deftri import capi as c
+    p = tv_problem(20000, seed=6)
+    with c.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.upload(p)
+        g, d = ctx.gradient()
+        r = ctx.solve_lm(5)
+        q.put((ctx.plan_info()["tiles"], g.tobytes(), d.tobytes(), r["chi2_iter"], r["trials_iter"], r["pcg_iterations"]))
+
+
+def _fusion_runs(envs, worker=None):
     cm = mp.get_context("spawn")
     out = []
     for env in envs:
         q = cm.Queue()
-        pr = cm.Process(target=_fusion_worker, args=(env, q))
+        pr = cm.Process(target=worker or _fusion_worker, args=(env, q))
         pr.start()
         out.append(q.get(timeout=300))
         pr.join(timeout=60)
@@ -606,3 +618,20 @@ def test_tile_chain_matches_two_phase_chain():
     np.testing.assert_allclose(c0, c1, rtol=1e-10)
     np.testing.assert_allclose(c0, c2, rtol=1e-9)
     assert c3 == c0 and t3 == t0 and i3 == i0 and s3 == s0
+
+
+def test_tile_linearization_matches_row_gathers():
+    """Tile mode's linearization (k_sp_tglin: every ARAP edge read once, the rows' 3x3 blocks and b
+    summed by tiles, cut edges through cross slots; k_sp_tglin_rows: the single-point terms) against
+    k_sp_glin_rows' per-row slot gathers (the default; the tile form is opt-in, DEFTRI_SP_TILE_GLIN=1):
+    the same per-slot arithmetic summed in another order — b and diag(H) to rel 1e-12, then the same
+    LM run (identical trials and CG iteration counts, chi2 rel 1e-10)."""
+    runs = _fusion_runs([{"DEFTRI_SP_MERGE": "1", "DEFTRI_SP_TILE_GLIN": "1"}, {"DEFTRI_SP_MERGE": "1"}], _glin_worker)
+    (n0, g0, d0, c0, t0, i0), (n1, g1, d1, c1, t1, i1) = runs
+    assert n0 > 0 and n1 > 0
+    g0, g1 = np.frombuffer(g0), np.frombuffer(g1)
+    d0, d1 = np.frombuffer(d0), np.frombuffer(d1)
+    np.testing.assert_allclose(g0, g1, rtol=1e-12, atol=1e-12 * np.abs(g1).max())
+    np.testing.assert_allclose(d0, d1, rtol=1e-12)
+    assert t0 == t1 and i0 == i1
+    np.testing.assert_allclose(c0, c1, rtol=1e-10)

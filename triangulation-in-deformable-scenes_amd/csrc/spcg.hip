@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, 
     if (gated_off(G.lgate)) return;
     double m = 0.0;
     if (stage == 0) {
-        for (int i = threadIdx.x; i < G.nrb2; i += 256) m = fmax(m, G.mpart[i]);
+        for (int i = threadIdx.x; i < (G.tglin ? sp::row_grid(G.nrb) : G.nrb2); i += 256) m = fmax(m, G.mpart[i]);
     } else {
         for (int h = threadIdx.x; h < G.Q; h += 256)
 #pragma unroll
@@ -2109,6 +2109,174 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
     m2_dots(G, it, red);
 }
 
+// ---- tile mode, per LM iteration: the rows' ARAP blocks by tiles --------------------------------------
+// k_sp_tglin, one workgroup per tile (k_sp_tile's dealing, no heavy workgroup): every ARAP edge of the
+// tile is read once (J columns 0..11, e) — the own rows' W J_a J_a^T (lower 6) and -J_a W e (3) summed
+// over the vertex's lanes (segmented scan, as the product's), each in-tile j row's slice (J_j, e) into
+// its LDS slot, a cut edge's two into their cross slots; then per tile row: own + its slots' terms ->
+// ht [9][nown].  k_sp_tglin_rows: per row the reprojection / depth terms (D_v, c_e, W J_s^2 as
+// k_sp_glin_rows forms them), H_v = D_v + ht + the row's cross slots' terms, b_v, the max diagonal.
+// A slot's terms use k_sp_glin_rows' per-slot arithmetic (ja = J_a W; H += ja J_c; b -= J_a (W e)); the
+// sums' order differs from k_sp_glin_rows' (rounding-level differences in H_v, b_v).
+__device__ __forceinline__ void tg_terms(const double *v, double W, double e, double *o) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const double ja = v[a] * W;
+#pragma unroll
+        for (int c = 0; c <= a; c++) o[tri3(a, c)] = ja * v[c];
+        o[6 + a] = -(v[a] * (W * e));
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sp_tglin(const SpDev G) {
+    extern __shared__ double lds[];
+    if (gated_off(G.lgate)) return;
+    const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int seg = (G.ntile + 7) / 8;
+    const int t = (b & 7) * seg + (b >> 3);
+    if (t >= G.ntile) return;
+    const int32_t *T = G.ttab + 8 * (int64_t)t;
+    const int r0 = T[0], nr = T[1], e0 = T[3], ne = T[4];
+    double *up = lds, *rs = up + 9 * nr;                     // own rows [nr][9]; slots [ns][4] (J_j, e)
+    for (int i = tid; i < 9 * nr; i += 256) up[i] = 0.0;
+    __syncthreads();
+    const double W = G.pinfo[0];
+    const int64_t jld = G.jld;
+    const uint64_t lt = (1ull << lane) - 1;
+    for (int base = 0; base < ne; base += 256) {
+        if (base + 64 * wv >= ne) break;           // (ne is a multiple of 64: whole waves in or out)
+        const int64_t k = (int64_t)e0 + base + tid;
+        const uint2 m = G.tmeta[k];
+        const int2 ch = G.tchunk[k >> 6];
+        const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
+        const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
+        const int le = ch.x + __popcll(vm & lt);
+        double J[12];
+#pragma unroll
+        for (int c = 0; c < 12; c++) J[c] = valid ? G.Ja[c * jld + le] : 0.0;
+        const double e = valid ? G.Ea[le] : 0.0;
+        const int ub = (int)(m.y >> 24), sw = (int)((m.x >> 26) & 1u);
+        const int ra = valid ? ub + sw : 0, rb = valid ? ub + 1 - sw : 0;
+        if (valid) {
+            if (cut) {
+                const int2 xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    G.xc[4 * (int64_t)xd.x + c] = J[6 + c];
+                    G.xc[4 * (int64_t)xd.y + c] = J[9 + c];
+                }
+                G.xc[4 * (int64_t)xd.x + 3] = e;
+                G.xc[4 * (int64_t)xd.y + 3] = e;
+            } else {
+                const int s0 = (int)(m.y & 0xfffu), s1 = (int)((m.y >> 12) & 0xfffu);
+#pragma unroll
+                for (int c = 0; c < 3; c++) { rs[4 * s0 + c] = J[6 + c]; rs[4 * s1 + c] = J[9 + c]; }
+                rs[4 * s0 + 3] = e;
+                rs[4 * s1 + 3] = e;
+            }
+        }
+        // the own rows' terms: inclusive segmented scan over the vertex's lanes, the last lane stores
+        double v[18];
+        tg_terms(J, W, e, v);
+        tg_terms(J + 3, W, e, v + 9);
+        if (!valid)
+#pragma unroll
+            for (int c = 0; c < 18; c++) v[c] = 0.0;
+        const int sstart = 63 - __clzll(hm & (lt | (1ull << lane)));
+        for (int d = 1; d < G.tile_segmax; d <<= 1) {
+#pragma unroll
+            for (int c = 0; c < 18; c++) {
+                const double y = shfl_up_d(v[c], d);
+                if (lane - d >= sstart) v[c] += y;
+            }
+        }
+        if (valid && (m.x & kTmLast)) {
+#pragma unroll
+            for (int c = 0; c < 9; c++) { up[9 * ra + c] = v[c]; up[9 * rb + c] = v[9 + c]; }
+        }
+    }
+    __syncthreads();
+    if (tid < nr) {
+        const int l = r0 + tid;
+        double acc[9];
+#pragma unroll
+        for (int c = 0; c < 9; c++) acc[c] = up[9 * tid + c];
+        const int rsi = G.trs[l], sb = rsi & 0xffff, sc = rsi >> 16;
+        for (int kk = sb; kk < sb + sc; kk++) {
+            double o[9];
+            tg_terms(rs + 4 * kk, W, rs[4 * kk + 3], o);
+#pragma unroll
+            for (int c = 0; c < 9; c++) acc[c] += o[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 9; c++) G.ht[(int64_t)c * G.nown + l] = acc[c];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sp_tglin_rows(const SpDev G) {
+    __shared__ double red4[4];
+    if (gated_off(G.lgate)) return;
+    const int lb = row_block((int)blockIdx.x, G.nrb);
+    const int l = lb * 256 + (int)threadIdx.x;
+    double mx = 0.0;
+    if (l < G.nown) {
+        double D[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
+        for (int j = G.rep_off[l]; j < G.rep_off[l + 1]; j++) {     // reprojection: 2 x 3, W scalar
+            const double *J = G.Jr + 6 * (int64_t)j;
+            const double wt = G.Wr[j];
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const double er = G.Er[2 * (int64_t)j + r];
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const double ja = J[3 * r + a] * wt;
+#pragma unroll
+                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[3 * r + c];
+                    bb[a] -= J[3 * r + a] * (wt * er);
+                }
+            }
+        }
+        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
+            const double *J = G.Jd + 4 * (int64_t)j;
+            const double wt = G.Wd[j], er = G.Ed[j];
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                const double ja = J[a] * wt;
+#pragma unroll
+                for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
+                bb[a] -= J[a] * (wt * er);
+                G.cdep[3 * (int64_t)j + a] = ja * J[3];
+            }
+            G.wss[j] = (J[3] * wt) * J[3];
+        }
+        double H[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) H[k] = D[k] + G.ht[(int64_t)k * G.nown + l];
+#pragma unroll
+        for (int a = 0; a < 3; a++) bb[a] += G.ht[(int64_t)(6 + a) * G.nown + l];
+        const double W = G.pinfo[0];
+        for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++) {           // the row's cross slots
+            const double *x = G.xc + 4 * (int64_t)k;
+            double o[9];
+            tg_terms(x, W, x[3], o);
+#pragma unroll
+            for (int c = 0; c < 6; c++) H[c] += o[c];
+#pragma unroll
+            for (int a = 0; a < 3; a++) bb[a] += o[6 + a];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) { G.Hv[6 * (int64_t)l + k] = H[k]; G.Dv[6 * (int64_t)l + k] = D[k]; }
+        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
+#pragma unroll
+        for (int a = 0; a < 3; a++) G.b[o + a] = bb[a];
+        mx = fmax(fabs(H[0]), fmax(fabs(H[2]), fabs(H[5])));
+    }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) G.mpart[blockIdx.x] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+}
+
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
 __global__ void k_sp_pack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ src,
                           double *__restrict__ buf) {
@@ -2156,6 +2324,13 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
         prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                    \
     } while (0)
 
+#define SPLS(NAME, KER, GRID, LDS, ...)                                              \
+    do {                                                                             \
+        hipEvent_t e0_ = prof_begin(st);                                             \
+        hipLaunchKernelGGL(KER, dim3(GRID), dim3(256), (size_t)(LDS), st, __VA_ARGS__); \
+        prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                              \
+    } while (0)
+
 template <class JT, int MG>
 static void launch_phase2(const SpDev &G, int grid, int it, double lambda, const JT *pj, hipStream_t st) {
     if (G.p2u == 4) SPL("sp_phase2", (sp::k_sp_phase2<JT, MG, 4>), grid, it, G, lambda, pj);
@@ -2164,7 +2339,10 @@ static void launch_phase2(const SpDev &G, int grid, int it, double lambda, const
 }
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    if (G.glu == 4) {
+    if (G.tglin) {
+        SPLS("sp_tglin", sp::k_sp_tglin, 8 * ((G.ntile + 7) / 8), G.tglin_lds, G);
+        SPL("sp_tglin_rows", sp::k_sp_tglin_rows, sp::row_grid(G.nrb), G);
+    } else if (G.glu == 4) {
         if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 4>), sp::row_grid(G.nrb2), G, G.pj32);
         else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 4>), sp::row_grid(G.nrb2), G, G.pj);
     } else if (G.glu == 6) {

@@ -370,7 +370,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     ALLOC(G.hl, 21 * (int64_t)Q + S + G.ndof);
     G.b = G.hl + 21 * (int64_t)Q + S;
     ALLOC(G.Mh, 36 * (int64_t)Q + S);
-    ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(G.nrb2, 1));
+    ALLOC(G.lpart, (int64_t)kSpLin * G.nblk); ALLOC(G.mpart, std::max(std::max(G.nrb2, 8 * ((G.nrb + 7) / 8)), 1));
     ALLOC(G.r, G.ndof); ALLOC(G.q, G.ndof); ALLOC(G.x, G.ndof);
     // zp: [heavy][rows][receive region: the halo rows, 3 dofs each, in the concatenated receive order]
     int64_t nrecv = 0;
@@ -399,7 +399,16 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.tchunk = reinterpret_cast<const int2 *>(tch);
         G.tmeta = reinterpret_cast<const uint2 *>(tm);
         G.pinfo = P.pair_info;
-        ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));
+        ALLOC(G.xc, 4 * std::max<int64_t>(H.tile_cross, 1));    // (3 per slot in the product, 4 in k_sp_tglin)
+        // the linearization's ARAP row blocks by tiles: LDS 9 doubles per tile row + 4 per slot
+        int64_t tl = 0;
+        for (int32_t t = 0; t < H.ntile; t++) tl = std::max<int64_t>(tl, 8 * (9 * (int64_t)H.tile_tab[8 * t + 1] + 4 * (int64_t)H.tile_tab[8 * t + 6]));
+        // opt-in (DEFTRI_SP_TILE_GLIN=1): measured at C2 k_sp_tglin 46 + k_sp_tglin_rows 25 us against
+        // k_sp_glin_rows' 69 (DESIGN.md "Tile mode")
+        static const bool tglin = std::getenv("DEFTRI_SP_TILE_GLIN") != nullptr;
+        G.tglin = (tglin && tl <= 64 * 1024) ? 1 : 0;
+        G.tglin_lds = (int32_t)std::max<int64_t>(tl, 8);
+        if (G.tglin) ALLOC(G.ht, 9 * (int64_t)std::max(nown, 1));
         // DEFTRI_SP_TILE_FUSE=1: the update in the product's launch when the whole grid is resident at
         // once (a cooperative launch guarantees it or fails).  Not the default: measured at C2 on MI355X
         // it is 85 us per CG iteration against 56 us for the two launches (the cooperative launch
