@@ -386,6 +386,11 @@ def test_degenerate_maps():
     upd = [1.0]
     optimization.arapOptimization(m1, 1.0, 50.0, 2e5, 0.0, 0.0, np.float32(0.003), 5, upd)
     assert upd[0] == 0.0
+    # no launch of the empty problem was refused (a zero grid leaves an error pending for the
+    # thread's next hipGetLastError — the next call's own launch check would report it)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipGetLastError() == 0
     assert all(np.array_equal(before[k], mp.position) for k, mp in m1.map_points.items())
     ctx = capi.Context(0)
     pe = ctx.pixels_stand_dev(m1)

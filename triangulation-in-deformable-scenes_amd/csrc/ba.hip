@@ -656,6 +656,7 @@ static hipEvent_t ba_prof_event() {
 }
 #define BALAUNCH(NAME, KER, GRID, BLOCK, SHM, ST, ...)                              \
     do {                                                                             \
+        if (dim3(GRID).x == 0) break;                  /* (n = 0: not launched) */   \
         hipEvent_t e0_ = nullptr;                                                    \
         if (g_baprof) { e0_ = ba_prof_event(); hipEventRecord(e0_, ST); }            \
         hipLaunchKernelGGL(KER, GRID, BLOCK, SHM, ST, __VA_ARGS__);                  \

@@ -126,6 +126,23 @@ __device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__rest
     E[e] = err;
 }
 
+// x / area by the pair's reciprocal: q0 = x RN(1/area), the residual x - q0 area exact by FMA, one
+// correction q0 + res RN(1/area) — Markstein's sequence, the correctly rounded quotient (the bits of
+// x / area) for operands far from overflow / underflow, as the ARAP terms are (point differences
+// over a mesh area; tools/micro/div_markstein.c: 4e8 random operand pairs, no difference).  An exact
+// quotient (zero residual) returns q0 itself, so the sign of a zero quotient is kept.  One division
+// per edge instead of up to 108 (the numeric Jacobian's perturbed energies)
+struct AreaDiv {
+    double v, r;
+};
+__device__ __forceinline__ AreaDiv area_div(double area) { return AreaDiv{area, 1.0 / area}; }
+__device__ __forceinline__ double adiv(double x, const AreaDiv &a) {
+#pragma clang fp contract(off)
+    const double q0 = x * a.r;
+    const double res = __fma_rn(-q0, a.v, x);
+    return res == 0.0 ? q0 : __fma_rn(res, a.r, q0);
+}
+
 // The ARAP energy's arithmetic, written out as explicit products, FMAs and sums (contraction off):
 // arap_err_rt and the numeric Jacobian's piece reuse (arap_base / arap_pert) form the same operations,
 // so an energy assembled from pieces of the unperturbed evaluation has the bits of a full one.
@@ -156,7 +173,7 @@ __device__ __forceinline__ double arap_sum_fg(const double *dg, double fg, doubl
 // the ARAP energy with the global transformation given as (rotation matrix, translation)
 __device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v2i, const double *v1j,
                                               const double *v2j, const double *Rg, const double *tt,
-                                              const double *Ri, const double *Rj, double w, double area) {
+                                              const double *Ri, const double *Rj, double w, const AreaDiv &area) {
     // every product and sum written out (no compiler contraction): the numeric Jacobian's reuse of
     // pieces (arap_base / arap_pert) forms the same operations and so the same bits
 #pragma clang fp contract(off)
@@ -175,15 +192,15 @@ __device__ __forceinline__ double arap_err_rt(const double *v1i, const double *v
     double f[3], g[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        f[k] = (d2i[k] - arap_mrow(Ri + 3 * k, d1i)) / area;
-        g[k] = (d2j[k] - arap_mrow(Rj + 3 * k, d1j)) / area;
+        f[k] = adiv(d2i[k] - arap_mrow(Ri + 3 * k, d1i), area);
+        g[k] = adiv(d2j[k] - arap_mrow(Rj + 3 * k, d1j), area);
     }
     return arap_sum(dg, f, g, w);
 }
 
 __device__ __forceinline__ double arap_err(const double *v1i, const double *v2i, const double *v1j,
                                            const double *v2j, const SE3 &T, const double *Ri,
-                                           const double *Rj, double w, double area) {
+                                           const double *Rj, double w, const AreaDiv &area) {
     double Rg[9];
     quat_to_mat(T.r, Rg);
     return arap_err_rt(v1i, v2i, v1j, v2j, Rg, T.t, Ri, Rj, w, area);
@@ -197,7 +214,7 @@ struct ArapBase {                  // one point configuration's pieces
 };
 __device__ __forceinline__ void arap_base(const double *v1i, const double *v2i, const double *v1j, const double *v2j,
                                           const double *Rg, const double *tt, const double *Ri, const double *Rj,
-                                          double area, ArapBase &o) {
+                                          const AreaDiv &area, ArapBase &o) {
 #pragma clang fp contract(off)
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -211,8 +228,8 @@ __device__ __forceinline__ void arap_base(const double *v1i, const double *v2i, 
     for (int k = 0; k < 3; k++) {
         o.rf[k] = arap_mrow(Ri + 3 * k, o.d1i);
         o.rg[k] = arap_mrow(Rj + 3 * k, o.d1j);
-        o.f[k] = ((v2i[k] - v2j[k]) - o.rf[k]) / area;
-        o.g[k] = ((v2j[k] - v2i[k]) - o.rg[k]) / area;
+        o.f[k] = adiv((v2i[k] - v2j[k]) - o.rf[k], area);
+        o.g[k] = adiv((v2j[k] - v2i[k]) - o.rg[k], area);
     }
 }
 // the energy with coordinate DD of point VI (0 v1i, 1 v2i, 2 v1j, 3 v2j) set to x; the others as in
@@ -220,7 +237,7 @@ __device__ __forceinline__ void arap_base(const double *v1i, const double *v2i, 
 template <int VI, int DD>
 __device__ __forceinline__ double arap_pert(const ArapBase &o, const double (*Q)[3], double x, const double *Rg,
                                             const double *tt, const double *Ri, const double *Rj, double w,
-                                            double area) {
+                                            const AreaDiv &area) {
 #pragma clang fp contract(off)
     double dg[3], f[3], g[3];
     if constexpr (VI == 0 || VI == 2) {
@@ -235,8 +252,8 @@ __device__ __forceinline__ double arap_pert(const ArapBase &o, const double (*Q)
         }
 #pragma unroll
         for (int k = 0; k < 3; k++) {
-            f[k] = ((Q[1][k] - Q[3][k]) - arap_mrow(Ri + 3 * k, d1i)) / area;
-            g[k] = ((Q[3][k] - Q[1][k]) - arap_mrow(Rj + 3 * k, d1j)) / area;
+            f[k] = adiv((Q[1][k] - Q[3][k]) - arap_mrow(Ri + 3 * k, d1i), area);
+            g[k] = adiv((Q[3][k] - Q[1][k]) - arap_mrow(Rj + 3 * k, d1j), area);
         }
 #pragma unroll
         for (int k = 0; k < 3; k++) {
@@ -259,8 +276,8 @@ __device__ __forceinline__ double arap_pert(const ArapBase &o, const double (*Q)
             if constexpr (VI == 1) dg[k] = ((arap_mrow(Rg + 3 * k, v2i) - tt[k]) - Q[0][k]) + o.B[k];
             else dg[k] = o.A[k] + ((arap_mrow(Rg + 3 * k, v2j) - tt[k]) - Q[2][k]);
             if (k == DD) {
-                f[k] = ((v2i[k] - v2j[k]) - o.rf[k]) / area;
-                g[k] = ((v2j[k] - v2i[k]) - o.rg[k]) / area;
+                f[k] = adiv((v2i[k] - v2j[k]) - o.rf[k], area);
+                g[k] = adiv((v2j[k] - v2i[k]) - o.rg[k], area);
             } else {
                 f[k] = o.f[k];
                 g[k] = o.g[k];
@@ -316,7 +333,8 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
     SE3 T = se3_load(tg + 7 * q);
     const double *Ri = rot + 9 * (int64_t)arot[2 * (int64_t)e];
     const double *Rj = rot + 9 * (int64_t)arot[2 * (int64_t)e + 1];
-    double w = aw[e], area = parea[q], om = pinfo[q];
+    double w = aw[e], om = pinfo[q];
+    const AreaDiv area = area_div(parea[q]);
     double err = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
     chi[e] = err * (om * err);
     if (MODE == 0) return;
@@ -333,7 +351,7 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
             u[k] = rs - 2 * T.t[k];
             g[k] = u[k] - (P[0][k] + P[2][k]);
         }
-        double co = 2.0 * w / (area * area);
+        double co = 2.0 * w / (area.v * area.v);
         double qv[3], rv[3], rg[3];
         for (int k = 0; k < 3; k++) {
             qv[k] = co * (a[k] + c[k]);
@@ -2079,8 +2097,11 @@ void prof_end(const char *name, hipEvent_t e0, unsigned grid, double work, hipSt
     hipEventRecord(e1, st);
     g_prof->recs.push_back({name, e0, e1, grid, work, g_level});
 }
+// (an empty grid — nothing to do, n = 0 — is not launched: HIP would refuse it and leave the error
+// pending for the next hipGetLastError of the thread)
 #define LAUNCH(NAME, KER, GRID, BLOCK, ST, ...)                                     \
     do {                                                                             \
+        if (dim3(GRID).x == 0) break;                                                \
         hipEvent_t e0_ = nullptr;                                                    \
         if (g_prof) { e0_ = prof_event(); hipEventRecord(e0_, ST); }                 \
         hipLaunchKernelGGL(KER, GRID, BLOCK, 0, ST, __VA_ARGS__);                    \

@@ -1077,6 +1077,7 @@ void launch_mf_lin(const PcgDev &G, bool want_dvec, hipStream_t st) {
 void launch_pcg_setup(const PcgDev &G, const double *hval, const double *b, double lambda, double *x,
                       hipStream_t st, bool rec_cleared) {
     if (!rec_cleared) hipMemsetAsync(G.rec, 0, sizeof(double) * kPcgRec * (size_t)(G.max_it + 2), st);
+    if (G.nB <= 0) return;                             // (an empty problem: nothing to set up)
     hipEvent_t e0 = prof_begin(st);
     hipLaunchKernelGGL(dev::k_pcg_setup, dim3(G.nB), dim3(256), 0, st, G, hval, b, lambda, x);
     prof_end("pcg_setup", e0, G.nB, 0.0, st);
@@ -1105,6 +1106,7 @@ void launch_pcg_heavy(const PcgDev &G, int it, const double *hval, double lambda
 }
 
 void launch_pcg_update(const PcgDev &G, int it, double lambda, double *x, hipStream_t st) {
+    if (G.nB <= 0) return;
     hipEvent_t e0 = prof_begin(st);
     hipLaunchKernelGGL(dev::k_pcg_update, dim3(G.nB), dim3(256), 0, st, it, G, lambda, x);
     prof_end("pcg_update", e0, G.nB, 0.0, st);

@@ -2319,6 +2319,7 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
 
 #define SPL(NAME, KER, GRID, ...)                                          \
     do {                                                                   \
+        if ((GRID) <= 0) break;                        /* (n = 0) */       \
         hipEvent_t e0_ = prof_begin(st);                                   \
         hipLaunchKernelGGL(KER, dim3(GRID), dim3(256), 0, st, __VA_ARGS__); \
         prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                    \
@@ -2326,6 +2327,7 @@ static inline unsigned nblk(int64_t n, int bs) { return (unsigned)std::max<int64
 
 #define SPLS(NAME, KER, GRID, LDS, ...)                                              \
     do {                                                                             \
+        if ((GRID) <= 0) break;                                                      \
         hipEvent_t e0_ = prof_begin(st);                                             \
         hipLaunchKernelGGL(KER, dim3(GRID), dim3(256), (size_t)(LDS), st, __VA_ARGS__); \
         prof_end(NAME, e0_, (unsigned)(GRID), 0.0, st);                              \
