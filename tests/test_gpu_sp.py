@@ -635,3 +635,51 @@ def test_tile_linearization_matches_row_gathers():
     np.testing.assert_allclose(d0, d1, rtol=1e-12)
     assert t0 == t1 and i0 == i1
     np.testing.assert_allclose(c0, c1, rtol=1e-10)
+
+
+def _ovl_worker(rank, world, port, env, q):
+    os.environ.update(env)
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from deftri import capi as c
+    from deftri import dist as ddist
+    p = _problem("mv")
+    ctx = c.Context(0)
+    ctx.dist_set_transport(world, rank, ddist.torch_transport())
+    ctx.set_linear_solver("pcg", max_iterations=4096)
+    ctx.upload(p)
+    info = ctx.plan_info()
+    r = ctx.solve_lm(4, analytic=False)
+    pts, sc, tg = ctx.download()
+    q.put((rank, info, r["chi2_iter"], r["trials_iter"], r["pcg_iterations"], pts.tobytes(), sc.tobytes(), tg.tobytes()))
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def test_sharded_halo_overlap_matches_serialized():
+    """The sharded chain's halo exchange beside the interior product (phase-1 workgroups that read no
+    halo row run while the boundary rows' (z, p) travel on a second stream; the others wait for them;
+    SURVEY §8(e)) against the serialized order (DEFTRI_SP_NO_OVERLAP=1): the same workgroups compute
+    the same sums, only their launch order differs — bit-identical LM runs at 2 ranks on the
+    8-keyframe all-pairs scene, and plan_info reports the overlap."""
+    cm = mp.get_context("spawn")
+    runs = []
+    for k, env in enumerate(({}, {"DEFTRI_SP_NO_OVERLAP": "1"})):
+        q = cm.Queue()
+        port = 29420 + 17 * k + os.getpid() % 300
+        procs = [cm.Process(target=_ovl_worker, args=(r, 2, port, env, q)) for r in range(2)]
+        for pr in procs:
+            pr.start()
+        out = {}
+        for _ in procs:
+            res = q.get(timeout=300)
+            out[res[0]] = res[1:]
+        for pr in procs:
+            pr.join(timeout=60)
+            assert pr.exitcode == 0
+        runs.append(out)
+    for r in range(2):
+        assert runs[0][r][0]["halo_overlap"] == 1 and runs[1][r][0]["halo_overlap"] == 0
+        assert runs[0][r][1:] == runs[1][r][1:]

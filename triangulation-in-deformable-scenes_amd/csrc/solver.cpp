@@ -684,14 +684,17 @@ int dist_allreduce(deftri_ctx *ctx, double *buf, int64_t n, int op) {
 
 // point-to-point transfers of one step, in the DistPlan's global order (every rank walks the same
 // list, so the host transport's blocking send/recv cannot cross); RCCL groups them
+// (st: the stream the transfers are ordered on — the context's, or the iterative plan's exchange
+// stream when its halo exchange runs beside the interior product)
 struct P2P { int peer; bool send; double *buf; int64_t n; };
-int dist_p2p(deftri_ctx *ctx, const std::vector<P2P> &ops) {
+int dist_p2p(deftri_ctx *ctx, const std::vector<P2P> &ops, hipStream_t st = nullptr) {
     if (ops.empty()) return 0;
+    const hipStream_t s = st ? st : ctx->st;
     if (ctx->comm) {
         ncclGroupStart();
         for (const P2P &o : ops) {
-            ncclResult_t r = o.send ? ncclSend(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, ctx->st)
-                                    : ncclRecv(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, ctx->st);
+            ncclResult_t r = o.send ? ncclSend(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, s)
+                                    : ncclRecv(o.buf, (size_t)o.n, ncclDouble, o.peer, ctx->comm, s);
             if (r != ncclSuccess) { ncclGroupEnd(); return fail(ctx, DEFTRI_E_HIP, std::string("ncclSend/Recv: ") + ncclGetErrorString(r)); }
         }
         ncclResult_t r = ncclGroupEnd();
@@ -699,7 +702,7 @@ int dist_p2p(deftri_ctx *ctx, const std::vector<P2P> &ops) {
         return 0;
     }
     if (!ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "point-sharded context without a transport");
-    HIPOK(hipStreamSynchronize(ctx->st));
+    HIPOK(hipStreamSynchronize(s));
     for (const P2P &o : ops) {
         if ((int64_t)ctx->xstage.size() < o.n) ctx->xstage.resize((size_t)o.n);
         if (o.send) {
@@ -718,11 +721,11 @@ struct CtxTransport : SpTransport {
     deftri_ctx *ctx;
     explicit CtxTransport(deftri_ctx *c) : ctx(c) {}
     int allreduce(double *dev, int64_t n, int op, hipStream_t) override { return dist_allreduce(ctx, dev, n, op); }
-    int p2p(const std::vector<Op> &ops, hipStream_t) override {
+    int p2p(const std::vector<Op> &ops, hipStream_t st) override {
         std::vector<P2P> v;
         v.reserve(ops.size());
         for (const Op &o : ops) v.push_back({o.peer, o.send, o.buf, o.n});
-        return dist_p2p(ctx, v);
+        return dist_p2p(ctx, v, st);
     }
 };
 

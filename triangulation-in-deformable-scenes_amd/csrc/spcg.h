@@ -254,6 +254,7 @@ struct SpDev {
     const double *pinfo = nullptr;                        // per pair: Omega (= W of its ARAP edges)
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
+    const int32_t *p1list = nullptr;                      // sharded phase 1: the launch's workgroups -> logical ones
     int32_t tile_fuse = 0;                                // tile mode: the update in the product's (cooperative) launch
     int32_t tglin = 0, tglin_lds = 0;                    // tile mode: the rows' ARAP blocks by tiles (k_sp_tglin)
     double *ht = nullptr;                                 // k_sp_tglin's per-row sums [9][nown] (H lower 6, b 3)
@@ -282,6 +283,10 @@ void sp_launch_update(const SpDev &G, int it, hipStream_t st);
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) p
 int sp_tile_coop_capacity(int lds, int device);   // resident k_sp_tile<*, 1> workgroups (0: no cooperative launch)
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
+// sharded chain, phase 1 over `n` of its logical workgroups (list: their indices; nullptr: all, n =
+// sp_merged_grid1) and phase 2
+void sp_launch_sd_phase1(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n);
+void sp_launch_sd_phase2(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st);
 void sp_launch_halo_pack(int n, const int32_t *rows, int width, int64_t base, const double *src, double *buf,
                          hipStream_t st);
 void sp_launch_halo_unpack(int n, const int32_t *rows, int width, int64_t base, const double *buf, double *dst, hipStream_t st);
@@ -394,6 +399,15 @@ class SpSolver {
     int cg_tail(int n, double lambda);
     int halo(int width, double *vec, bool zp);
     int halo_sd();
+    // sharded chain with the halo exchange overlapped (G.ovl): phase 1's workgroups that read no halo
+    // row (d_p1int) run while the boundary rows' (z, p) travel on cs_; the rest (d_p1bnd) wait for
+    // ev_halo_.  int_pending_: the iteration whose interior phase 1 is already queued
+    hipStream_t cs_ = nullptr;
+    hipEvent_t ev_upd_ = nullptr, ev_halo_ = nullptr;
+    int32_t *d_p1int = nullptr, *d_p1bnd = nullptr;
+    int n_p1int = 0, n_p1bnd = 0, int_pending_ = -1;
+    int sd_product(int it, double lambda);
+    int sd_exchange(int next_it, double lambda);
     int pcg_solve(double lambda, const double *rhs, bool &solved, int &its);
     int solve_lm_dev(const deftri_lm_params &prm, deftri_report &R);
     void gather_values(const deftri_problem_desc &d, SpValues &v) const;

@@ -922,9 +922,10 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
         if (it_state(G, it, beta)) return;
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int bx = G.p1list ? G.p1list[blockIdx.x] : (int)blockIdx.x;    // (sharded overlap: a subset)
     if constexpr (MG) {
         double pap = 0.0;
-        const int e = (int)blockIdx.x;
+        const int e = bx;
         if (e < G.m_nx) {
             if (e == 0) {
                 for (int64_t dd = threadIdx.x; dd < G.hd; dd += 256) {
@@ -949,11 +950,11 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
                 }
             }
             pap = block_sum(pap, red[0]);
-            if (threadIdx.x == 0) G.m1part[blockIdx.x] = pap;
+            if (threadIdx.x == 0) G.m1part[bx] = pap;
             return;
         }
     }
-    const int b = MG ? (int)blockIdx.x - G.m_nx : (int)blockIdx.x;
+    const int b = MG ? bx - G.m_nx : bx;
     const int4 d = G.blk[b];
     const int kind = d.x & 0xff, owned = d.x >> 8;
     const int i = d.z + threadIdx.x;
@@ -999,7 +1000,7 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
             const int c = threadIdx.x;
             const double v = (red[c][0] + red[c][1]) + (red[c][2] + red[c][3]);
             if (c < 6) out[c] = v;
-            else G.m1part[blockIdx.x] = v;
+            else G.m1part[bx] = v;
         }
     } else {
         double t = 0.0;
@@ -1020,7 +1021,7 @@ __global__ void __launch_bounds__(256) k_sp_phase1(int it, const SpDev G, const 
         }
         __syncthreads();
         if (threadIdx.x == 0) out[0] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-        if (MG && threadIdx.x == 6) G.m1part[blockIdx.x] = (red[6][0] + red[6][1]) + (red[6][2] + red[6][3]);
+        if (MG && threadIdx.x == 6) G.m1part[bx] = (red[6][0] + red[6][1]) + (red[6][2] + red[6][3]);
     }
 }
 
@@ -2385,11 +2386,8 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     if (G.sd) {
         // sharded single-reduction chain: [m_nx heavy-z / row-term workgroups][phase-1 blocks];
         // [m_nh heavy-sum / scalar workgroups][row blocks]
-        const int g1 = sp_merged_grid1(G), g2 = G.m_nh + sp::row_grid(G.nrb2);
-        if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 2>), g1, it, G, G.Ja32, lambda);
-        else SPL("sp_phase1", (sp::k_sp_phase1<double, 2>), g1, it, G, G.Ja, lambda);
-        if (fp32) launch_phase2<float, 2>(G, g2, it, lambda, G.pj32, st);
-        else launch_phase2<double, 2>(G, g2, it, lambda, G.pj, st);
+        sp_launch_sd_phase1(G, it, lambda, fp32, st, nullptr, sp_merged_grid1(G));
+        sp_launch_sd_phase2(G, it, lambda, fp32, st);
         return;
     }
     if (G.tile) {
@@ -2473,6 +2471,19 @@ void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_
 }
 
 int sp_merged_grid1(const SpDev &G) { return 8 * ((G.nrb + 1 + 7) / 8) + G.nblk; }
+
+void sp_launch_sd_phase1(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n) {
+    SpDev g = G;
+    g.p1list = list;
+    if (fp32) SPL("sp_phase1", (sp::k_sp_phase1<float, 2>), n, it, g, G.Ja32, lambda);
+    else SPL("sp_phase1", (sp::k_sp_phase1<double, 2>), n, it, g, G.Ja, lambda);
+}
+
+void sp_launch_sd_phase2(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st) {
+    const int g2 = G.m_nh + sp::row_grid(G.nrb2);
+    if (fp32) launch_phase2<float, 2>(G, g2, it, lambda, G.pj32, st);
+    else launch_phase2<double, 2>(G, g2, it, lambda, G.pj, st);
+}
 int sp_merged_grid2(const SpDev &G) { return 8 * ((G.Q + G.S + 7) / 8) + sp::row_grid(G.nrb2); }
 
 void sp_launch_heavy(const SpDev &G, int it, double lambda, int stage, hipStream_t st) {

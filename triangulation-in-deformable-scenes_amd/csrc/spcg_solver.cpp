@@ -81,6 +81,12 @@ SpSolver::SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport
 SpSolver::~SpSolver() {
     hipSetDevice(dev_);
     hipStreamSynchronize(st_);
+    if (cs_) {
+        hipStreamSynchronize(cs_);
+        hipStreamDestroy(cs_);
+    }
+    if (ev_upd_) hipEventDestroy(ev_upd_);
+    if (ev_halo_) hipEventDestroy(ev_halo_);
     for (void *p : allocs_) hipFree(p);
     if (hpin) hipHostFree(hpin);
     if (ipin) hipHostFree(ipin);
@@ -515,6 +521,33 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         int32_t *d_so, *d_sl;
         PUT(d_so, so); PUT(d_sl, sl);
         G.snd_off = d_so; G.snd_slot = d_sl;
+        // the halo exchange beside phase 1's interior workgroups: phase-1 blocks whose
+        // ARAP edges read no halo row (and the heavy / row-term workgroups) run while the boundary
+        // rows' (z, p) travel; the blocks that read one wait for them.  DEFTRI_SP_NO_OVERLAP=1: one
+        // phase-1 launch after the exchange (round 4)
+        static const bool no_ovl = std::getenv("DEFTRI_SP_NO_OVERLAP") != nullptr;
+        G.ovl = (nranks_ > 1 && !no_ovl) ? 1 : 0;
+        if (G.ovl) {
+            std::vector<int32_t> li, lb;
+            for (int32_t e = 0; e < G.m_nx; e++) li.push_back(e);
+            for (int32_t b = 0; b < G.nblk; b++) {
+                const int32_t *d4 = &H.blk[4 * (size_t)b];
+                bool bnd = false;
+                if ((d4[0] & 0xff) == SP_ARAP)
+                    for (int32_t le = d4[2]; le < d4[3] && !bnd; le++)
+                        for (int k = 0; k < 4; k++) bnd |= ap[4 * (size_t)le + k] >= NP;
+                (bnd ? lb : li).push_back(G.m_nx + b);
+            }
+            n_p1int = (int)li.size();
+            n_p1bnd = (int)lb.size();
+            PUT(d_p1int, li);
+            if (lb.empty()) lb.push_back(0);
+            PUT(d_p1bnd, lb);
+            if (!cs_) SPOK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+            if (!ev_upd_) SPOK(hipEventCreateWithFlags(&ev_upd_, hipEventDisableTiming));
+            if (!ev_halo_) SPOK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        }
+        int_pending_ = -1;
     } else {
         G.apts_p = G.apts;
     }
@@ -552,6 +585,7 @@ int SpSolver::halo(int width, double *vec, bool zp) {
 // the setup) filled straight into the peers' receive regions of zp
 int SpSolver::halo_sd() {
     if (!shard_ || nranks_ <= 1) return 0;
+    if (G.ovl) SPOK(hipStreamWaitEvent(cs_, ev_upd_, 0));    // (the send buffer written on st_)
     const int64_t nsend = send_off_[nranks_];
     double *sbuf = G.sbuf, *rbuf = reinterpret_cast<double *>(G.zp + G.ndof);
     std::vector<SpTransport::Op> ops;
@@ -564,7 +598,38 @@ int SpSolver::halo_sd() {
                 ops.push_back({a, false, rbuf + 6 * recv_off_[a], 6 * (recv_off_[a + 1] - recv_off_[a])});
         }
     (void)nsend;
-    return tr_->p2p(ops, st_);
+    if (!G.ovl) return tr_->p2p(ops, st_);
+    const int rc = tr_->p2p(ops, cs_);
+    if (rc) return rc;
+    SPOK(hipEventRecord(ev_halo_, cs_));
+    return 0;
+}
+
+// the sharded chain's product of iteration it: phase 1 (G.ovl: the interior workgroups unless
+// already queued, the wait for the exchange, the boundary ones), phase 2
+int SpSolver::sd_product(int it, double lambda) {
+    const bool f32 = fp32_jac != 0;
+    if (!G.ovl) {
+        sp_launch_sd_phase1(G, it, lambda, f32, st_, nullptr, sp_merged_grid1(G));
+    } else {
+        if (int_pending_ != it) sp_launch_sd_phase1(G, it, lambda, f32, st_, d_p1int, n_p1int);
+        int_pending_ = -1;
+        SPOK(hipStreamWaitEvent(st_, ev_halo_, 0));
+        sp_launch_sd_phase1(G, it, lambda, f32, st_, d_p1bnd, n_p1bnd);
+    }
+    sp_launch_sd_phase2(G, it, lambda, f32, st_);
+    return 0;
+}
+
+// after the update (or the setup) wrote the boundary rows' (z, p): G.ovl — queue iteration next_it's
+// interior phase 1, then the exchange on cs_ beside it (a host transport blocks this thread while
+// the device runs it); otherwise the exchange on st_
+int SpSolver::sd_exchange(int next_it, double lambda) {
+    if (!G.ovl) return halo_sd();
+    SPOK(hipEventRecord(ev_upd_, st_));
+    sp_launch_sd_phase1(G, next_it, lambda, fp32_jac != 0, st_, d_p1int, n_p1int);
+    int_pending_ = next_it;
+    return halo_sd();
 }
 
 // computeActiveErrors (+ linearizeOplus with jac) on the rank's edges, chi2 of its owned edges into
@@ -611,8 +676,10 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
 // the solve's setup (preconditioner at lambda, r = rhs, (z, p) = (M r, 0), x = 0); sharded: the
 // boundary rows' (z, p) to the ranks whose edges read them, as after every CG update
 int SpSolver::cg_setup(double lambda, const double *rhs) {
+    if (G.ovl) SPOK(hipStreamWaitEvent(st_, ev_halo_, 0));   // (no exchange of an earlier solve in flight)
+    int_pending_ = -1;
     sp_launch_setup(G, rhs, lambda, st_);
-    if (G.sd) return halo_sd();
+    if (G.sd) return sd_exchange(0, lambda);
     if (shard_) return halo(6, reinterpret_cast<double *>(G.zp), true);
     return 0;
 }
@@ -623,10 +690,10 @@ int SpSolver::cg_chain(double lambda, int from, int to) {
     int rc;
     for (int it = from; it < to; it++) {
         if (G.sd) {                                    // phase 1, phase 2 (A z), one all-reduce, update
-            sp_launch_product(G, it, lambda, fp32_jac != 0, st_);
+            if ((rc = sd_product(it, lambda))) return rc;
             if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
             sp_launch_update_sd(G, it, lambda, 0, st_);
-            if ((rc = halo_sd())) return rc;
+            if ((rc = sd_exchange(it + 1, lambda))) return rc;
             continue;
         }
         if (G.merged) {                                // phase 1 (+ alpha), phase 2 (+ update, next dots)
@@ -661,7 +728,7 @@ int SpSolver::cg_tail(int n, double lambda) {
     int rc;
     if (G.merged) return 0;                            // phase 2's last workgroup records iteration n's state
     if (G.sd) {
-        sp_launch_product(G, n, lambda, fp32_jac != 0, st_);
+        if ((rc = sd_product(n, lambda))) return rc;
         if ((rc = tr_->allreduce(G.xb, 3 + G.hd, 0, st_))) return rc;
         sp_launch_update_sd(G, n, lambda, 1, st_);
         return 0;
