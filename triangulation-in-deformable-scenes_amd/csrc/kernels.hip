@@ -292,9 +292,7 @@ __device__ __forceinline__ double arap_pert(const ArapBase &o, const double (*Q)
 // once per pair here: per pair kArapPre x (rotation matrix 9, translation 3), transformation 0 the
 // unperturbed one, 1 + 2d / 2 + 2d the +delta / -delta perturbations of twist coordinate d.
 constexpr int kArapPre = 13;
-__global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restrict__ pre, const int *gate) {
-    if (gate && !*gate) return;
-    const int t = TID;
+__device__ __forceinline__ void arap_pre_one(int t, int Q, const double *__restrict__ tg, double *__restrict__ pre) {
     if (t >= Q * kArapPre) return;
     const int q = t / kArapPre, k = t % kArapPre;
     const SE3 T = se3_load(tg + 7 * q);
@@ -308,6 +306,10 @@ __global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restr
     double *o = pre + 12 * (int64_t)t;
     quat_to_mat(X.r, o);
     o[9] = X.t[0]; o[10] = X.t[1]; o[11] = X.t[2];
+}
+__global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restrict__ pre, const int *gate) {
+    if (gate && !*gate) return;
+    arap_pre_one(TID, Q, tg, pre);
 }
 
 // MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian, pieces reused; 3: the
@@ -540,6 +542,22 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MODE =
 
 // the errors and chi2 of every reprojection, depth and ARAP edge in one launch (the trial's
 // evaluation): the same per-edge code as k_lin_rep / k_lin_dep / k_lin_arap<0>, block ranges by type
+// the linearization's single-point edges and the pair table of the numeric ARAP Jacobian in one
+// launch (block ranges: reprojection, depth, then the pairs' perturbed T_g): k_lin_arap reads the
+// table, so it follows in its own launch
+__global__ void __launch_bounds__(128) k_lin_pts(const DevProblem P, int nbr, int nbd, int want_jac, int analytic) {
+    if (P.gate_lin && !*P.gate_lin) return;
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (b < nbr)
+        lin_rep_edge(b * 128 + t, P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose,
+                     P.cam_R, P.cam_kb8, P.Jrep, P.Wrep, P.Erep, P.chi_rep, want_jac);
+    else if (b < nbr + nbd)
+        lin_dep_edge((b - nbr) * 128 + t, P.D, P.dep_point, P.dep_scale, P.dep_cam, P.dep_meas, P.dep_info, P.points,
+                     P.scales, P.cam_pose, P.cam_R, P.Jdep, P.Wdep, P.Edep, P.chi_dep, want_jac, analytic);
+    else
+        arap_pre_one((b - nbr - nbd) * 128 + t, P.Q, P.tg, P.tg_pre);
+}
+
 __global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, int nbd) {
     if (P.gate_trial && !*P.gate_trial) return;
     const int b = blockIdx.x, t = threadIdx.x;
@@ -2121,18 +2139,11 @@ static bool arap_j_full() {
 }
 
 void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool analytic) {
-    if (P.R > 0)
-        LAUNCH("lin_rep", dev::k_lin_rep, dim3(nb(P.R, 128)), dim3(128), st, P.R, P.rep_point, P.rep_cam,
-                           P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose, P.cam_R, P.cam_kb8, P.Jrep,
-                           P.Wrep, P.Erep, P.chi_rep, want_jac ? 1 : 0, P.gate_lin);
-    if (P.D > 0)
-        LAUNCH("lin_dep", dev::k_lin_dep, dim3(nb(P.D, 128)), dim3(128), st, P.D, P.dep_point, P.dep_scale,
-                           P.dep_cam, P.dep_meas, P.dep_info, P.points, P.scales, P.cam_pose, P.cam_R, P.Jdep,
-                           P.Wdep, P.Edep, P.chi_dep, want_jac ? 1 : 0, analytic ? 1 : 0, P.gate_lin);
     const bool pre = want_jac && !analytic && P.E > 0;   // the numeric Jacobians read the pair table
-    if (pre)
-        LAUNCH("arap_pre", dev::k_arap_pre, dim3(nb((int64_t)P.Q * dev::kArapPre, 64)), dim3(64), st, P.Q, P.tg,
-               P.tg_pre, P.gate_lin);
+    const int nbr = P.R > 0 ? (int)nb(P.R, 128) : 0, nbd = P.D > 0 ? (int)nb(P.D, 128) : 0;
+    const int nbp = pre ? (int)nb((int64_t)P.Q * dev::kArapPre, 128) : 0;
+    LAUNCH("lin_pts", dev::k_lin_pts, dim3(nbr + nbd + nbp), dim3(128), st, P, nbr, nbd, want_jac ? 1 : 0,
+           analytic ? 1 : 0);
     if (P.E > 0)
         LAUNCH("lin_arap", (!want_jac ? dev::k_lin_arap<0> : analytic ? dev::k_lin_arap<1> : arap_j_full() ? dev::k_lin_arap<3> : dev::k_lin_arap<2>),
                            dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,

@@ -45,6 +45,7 @@ constexpr int kSpSortWindow = 512;     // rows sorted by entry count inside wind
 constexpr int kSpWaveSplit = 16;       // phase-2 waves with rows of more slots take 32 rows on lane pairs
 constexpr int kSpRowSplit = 1;         // phase 2: waves per row-wave's slot list (DEFTRI_SP_ROW_SPLIT)
 constexpr int kSpP2Step = 8;           // phase 2: slots per step (DEFTRI_SP_P2_STEP = 4 or 8)
+constexpr int kSpGlinGroup = 8;        // k_sp_glin_blocks: owned ARAP blocks per workgroup at most
 constexpr int kSpGlinStep = 8;         // k_sp_glin_rows: slots per step (DEFTRI_SP_GLIN_STEP = 4 or 8)
 constexpr int kSpGuessMargin = 1;      // CG iterations queued per trial: last converged count + this
 constexpr int kSpHeavySplit = 512;         // heavy sums by one workgroup per heavy vertex above this many blocks
@@ -158,6 +159,8 @@ struct SpDev {
     int32_t nblk = 0, nrb = 0;                         // phase-1 blocks, row blocks
     int32_t include_heavy = 1;                         // this rank counts the replicated heavy dofs in sums
     const int4 *blk = nullptr;
+    const int2 *glb = nullptr;                            // k_sp_glin_blocks' groups: (first block, count)
+    int32_t nglb = 0;
     const int32_t *hv_blk = nullptr;
     const int64_t *hv_blk_off = nullptr;
     const int32_t *apts = nullptr, *apair = nullptr;   // local ARAP edges: rows, pair

@@ -172,6 +172,9 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
         const double *__restrict__ Ja = G.Ja, *__restrict__ Wa = G.Wa, *__restrict__ Ea = G.Ea;
         const double *__restrict__ Jd = G.Jd, *__restrict__ Wd = G.Wd;
         const int64_t jld = G.jld;
+        // one pair: every ARAP edge's W is the pair's Omega (k_lin_arap stores W = pinfo[pair]), one
+        // uniform load instead of a gather per slot
+        const bool w1 = G.Q == 1 && G.pinfo != nullptr;
         auto load = [&](int m) -> Raw {
             const bool dep = m <= -2;
             const int mm = max(m, 0), jj = max(-2 - m, 0);
@@ -179,7 +182,7 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
             const double *pd = Jd + 4 * (int64_t)jj;
             const double *Jc = dep ? pd : pa;
             const int64_t st = dep ? 1 : jld;
-            const double *W = dep ? Wd + jj : Wa + (mm >> 2);
+            const double *W = dep ? Wd + jj : w1 ? G.pinfo : Wa + (mm >> 2);
             const double *X = dep ? pd + 3 : Ea + (mm >> 2);
             return Raw{Jc[0], Jc[st], Jc[2 * st], *W, *X};
         };
@@ -266,25 +269,29 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
     if (threadIdx.x == 0 && lb < max(G.nrb2, 1)) G.mpart[lb] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
 }
 
-// heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1)
+// heavy vertices' H / b partials per phase-1 block (owned ARAP edges: lower 6x6 + 6; depth: 1 + 1);
+// one workgroup per group of blocks (G.glb: consecutive owned ARAP blocks of one pair, their edges
+// contiguous) — the group's sums land in its first block's partial, its other blocks' are zero
 __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
     __shared__ double red[kSpLin][4];
     if (gated_off(G.lgate)) return;
-    const int4 d = G.blk[blockIdx.x];
+    const int2 gr = G.glb[blockIdx.x];
+    const int4 d = G.blk[gr.x];
     const int kind = d.x & 0xff, owned = d.x >> 8;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int i = d.z + threadIdx.x;
-    double *out = G.lpart + (int64_t)kSpLin * blockIdx.x;
+    double *out = G.lpart + (int64_t)kSpLin * gr.x;
     if (kind == SP_ARAP) {
         if (!owned) return;
         double a[kSpLin];
 #pragma unroll
         for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
-        if (i < d.w) {
+        const int iend = G.blk[gr.x + gr.y - 1].w;
+        for (int ii = i; ii < iend; ii += 256) {
             double J[6];
 #pragma unroll
-            for (int r = 0; r < 6; r++) J[r] = G.Ja[(12 + r) * G.jld + i];
-            const double wv = G.Wa[i], er = G.Ea[i];
+            for (int r = 0; r < 6; r++) J[r] = G.Ja[(12 + r) * G.jld + ii];
+            const double wv = G.Wa[ii], er = G.Ea[ii];
 #pragma unroll
             for (int r = 0; r < 6; r++) {
                 const double jr = J[r] * wv;
@@ -293,6 +300,7 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
                 a[21 + r] -= J[r] * (wv * er);
             }
         }
+        for (int k = threadIdx.x; k < kSpLin * (gr.y - 1); k += 256) out[kSpLin + k] = 0.0;
 #pragma unroll
         for (int k = 0; k < kSpLin; k++) {
             const double v = wave_sum(a[k]);
@@ -2355,7 +2363,7 @@ void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
         if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 8>), sp::row_grid(G.nrb2), G, G.pj32);
         else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 8>), sp::row_grid(G.nrb2), G, G.pj);
     }
-    if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nblk, G);
+    if (G.nblk > 0) SPL("sp_glin_blocks", sp::k_sp_glin_blocks, G.nglb, G);
     if (G.nch > 0) SPL("sp_glin_heavy", sp::k_sp_glin_heavy, G.nch, G);
 }
 

@@ -295,10 +295,37 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     PUT(blk, H.blk); PUT(hvb, H.hv_blk); PUT(hvbo, H.hv_blk_off); PUT(dperm, H.dperm);
     PUT(inc, H.inc); PUT(inco, H.inc_off); PUT(roff, H.rep_off); PUT(doff, H.dep_off);
     G.blk = reinterpret_cast<const int4 *>(blk);
+    {
+        // k_sp_glin_blocks' groups: up to kSpGlinGroup consecutive owned ARAP blocks of one pair with
+        // contiguous edges per workgroup (its 27 sums reduced once per group, not per 256 edges); any
+        // other block alone.  DEFTRI_SP_GLIN_GROUP=1: one block per workgroup (round 4)
+        static const char *ge = std::getenv("DEFTRI_SP_GLIN_GROUP");
+        const int gmax = ge ? std::max(1, std::atoi(ge)) : kSpGlinGroup;
+        std::vector<int32_t> gl;
+        const int32_t nb = (int32_t)(H.blk.size() / 4);
+        for (int32_t b = 0; b < nb;) {
+            const int32_t *d0 = &H.blk[4 * (size_t)b];
+            const bool arap_owned = (d0[0] & 0xff) == SP_ARAP && (d0[0] >> 8) != 0;
+            int32_t n = 1;
+            while (arap_owned && n < gmax && b + n < nb) {
+                const int32_t *dn = &H.blk[4 * (size_t)(b + n)], *dp = dn - 4;
+                if (dn[0] != d0[0] || dn[1] != d0[1] || dn[2] != dp[3]) break;
+                n++;
+            }
+            gl.push_back(b);
+            gl.push_back(n);
+            b += n;
+        }
+        int32_t *glb;
+        PUT(glb, gl);
+        G.glb = reinterpret_cast<const int2 *>(glb);
+        G.nglb = (int32_t)(gl.size() / 2);
+    }
     G.hv_blk = hvb; G.hv_blk_off = hvbo; G.dperm = dperm;
     G.inc = inc; G.inc_off = inco; G.rep_off = roff; G.dep_off = doff;
     G.apts = P.arap_pts; G.apair = P.arap_pair;
     G.Ja = P.Jarap; G.Wa = P.Warap; G.Ea = P.Earap;
+    G.pinfo = P.pair_info;
     G.Jr = P.Jrep; G.Wr = P.Wrep; G.Er = P.Erep;
     G.Jd = P.Jdep; G.Wd = P.Wdep; G.Ed = P.Edep;
     G.dsc = P.dep_scale; G.drow = P.dep_point;
