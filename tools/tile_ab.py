@@ -34,7 +34,7 @@ def run_variant(n, n_it):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
     return {"tiles": info["tiles"], "cg_launches": info["cg_launches"], "trials": r["trials_iter"], "chi2": r["chi2_iter"],
-            "pcg_its": r["pcg_iterations"], "cg_us": cg, "lin_us": {k: round(1e3 * v["ms"], 3) for k, v in st.items() if "glin" in k or k.startswith("lin_")}, "cg_iteration_us": round(sum(cg.values()), 3), "cg_its_profiled": its, "setup_us": cg0,
+            "pcg_its": r["pcg_iterations"], "cont": r2["pcg_continuations"], "cg_us": cg, "lin_us": {k: round(1e3 * v["ms"], 3) for k, v in st.items() if "glin" in k or k.startswith("lin_")}, "cg_iteration_us": round(sum(cg.values()), 3), "cg_its_profiled": its, "setup_us": cg0,
             "lm_it_s": round(r2["iterations"] / dt, 1), "bytes": info["product_bytes"], "survey_bytes": info["survey_bytes"],
             "pts_sum": float(pts.sum()), "repeat_same": r2["chi2_iter"] == r["chi2_iter"]}
 
