@@ -24,12 +24,15 @@
 //   cross    per own row (all tiles) the cross slots aimed at it, contiguous in source order (xoff);
 //            per cut entry its two slots' positions (xdst)
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdint>
 #include <cstdlib>
 #include <numeric>
 #include <string>
 #include <vector>
 
+#include "host_threads.h"
 #include "spcg.h"
 
 namespace deftri {
@@ -47,6 +50,15 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         const char *e = std::getenv("DEFTRI_SP_TILE_LDS");
         return (int64_t)(e ? std::atoi(e) : kSpTileLds);
     }();
+    // DEFTRI_PLAN_TIMING: the stages of this build too
+    static const bool timing = std::getenv("DEFTRI_PLAN_TIMING") != nullptr;
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *w) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[deftri plan]   4a %-26s %8.2f ms\n", w, std::chrono::duration<double, std::milli>(t - T0).count());
+        T0 = t;
+    };
     // groups: size and first row (rows of a group are consecutive, groups in Morton order)
     std::vector<int32_t> gsz(ng, 0), grow(ng, INT32_MAX);
     for (int32_t p = 0; p < in.P; p++) {
@@ -56,26 +68,65 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     }
     for (int32_t g = 0; g < ng; g++)
         if (gsz[g] > 2) { why = "a keyframe-copy group of more than 2 rows"; return false; }
-    // out-edges per group (edge order inside a group), in-edge sources per group
+    // out-edges per group (edge order inside a group), in-edge sources per group: counting sorts by
+    // group over contiguous edge chunks on host threads (per-chunk counts, each chunk's edges placed
+    // after the earlier chunks' — the sequential order)
+    std::vector<int32_t> egi(E), egj(E), erow(4 * (size_t)E);
     std::vector<int64_t> ooff(ng + 1, 0), ioff(ng + 1, 0);
-    for (int64_t e = 0; e < E; e++) {
-        const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
-        if (gi != in.gpos[ap[4 * e + 1]] || gj != in.gpos[ap[4 * e + 3]] || gi == gj) { why = "an edge's copies in two groups"; return false; }
-        ooff[gi + 1]++;
-        ioff[gj + 1]++;
-    }
-    for (int32_t g = 0; g < ng; g++) { ooff[g + 1] += ooff[g]; ioff[g + 1] += ioff[g]; }
     std::vector<int32_t> oe(E), isrc(E);
     {
-        std::vector<int64_t> fo(ooff.begin(), ooff.end() - 1), fi(ioff.begin(), ioff.end() - 1);
-        for (int64_t e = 0; e < E; e++) {
-            const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
-            oe[fo[gi]++] = (int32_t)e;
-            isrc[fi[gj]++] = gi;
+        constexpr int kMaxChunks = 16;
+        std::vector<std::vector<int32_t>> co(kMaxChunks), ci(kMaxChunks);
+        int bad[kMaxChunks] = {0};
+        const int nch = chunked(E, 1 << 15, [&](int c, int64_t lo, int64_t hi) {
+            co[c].assign(ng, 0);
+            ci[c].assign(ng, 0);
+            for (int64_t e = lo; e < hi; e++) {
+                const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
+                if (gi != in.gpos[ap[4 * e + 1]] || gj != in.gpos[ap[4 * e + 3]] || gi == gj) bad[c] = 1;
+                egi[e] = gi;
+                egj[e] = gj;
+                for (int k = 0; k < 4; k++) erow[4 * e + k] = in.row_of_point[ap[4 * e + k]] - H.lo;
+                co[c][gi]++;
+                ci[c][gj]++;
+            }
+        });
+        for (int c = 0; c < nch; c++)
+            if (bad[c]) { why = "an edge's copies in two groups"; return false; }
+        // per group: its total, then each chunk's first position (chunk order)
+        for (int32_t g = 0; g < ng; g++) {
+            int64_t so = 0, si = 0;
+            for (int c = 0; c < nch; c++) { so += co[c][g]; si += ci[c][g]; }
+            ooff[g + 1] = ooff[g] + so;
+            ioff[g + 1] = ioff[g] + si;
         }
+        chunked(ng, 1 << 12, [&](int, int64_t lo, int64_t hi) {
+            for (int64_t g = lo; g < hi; g++) {
+                int64_t fo = ooff[g], fi = ioff[g];
+                for (int c = 0; c < nch; c++) {
+                    const int32_t a = co[c][g], b = ci[c][g];
+                    co[c][g] = (int32_t)fo;
+                    ci[c][g] = (int32_t)fi;
+                    fo += a;
+                    fi += b;
+                }
+            }
+        });
+        chunked(E, 1 << 15, [&](int c, int64_t lo, int64_t hi) {
+            for (int64_t e = lo; e < hi; e++) {
+                oe[co[c][egi[e]]++] = (int32_t)e;
+                isrc[ci[c][egj[e]]++] = egi[e];
+            }
+        });
     }
+    // the j group of every out-edge, in out-edge order
+    std::vector<int32_t> okj(E);
+    chunked(E, 1 << 15, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; k++) okj[k] = egj[oe[k]];
+    });
     for (int32_t g = 0; g < ng; g++)
         if (ooff[g + 1] - ooff[g] > 64) { why = "a vertex with more than 64 ARAP edges"; return false; }
+    lap("groups, edges by group");
     // (a group with edges holds p1_i and p2_i: 2 rows; a 1-row group has no ARAP edge)
     // 1. greedy partition: consecutive groups while rows <= 2 umax and the LDS estimate fits
     auto lds_of = [&](int64_t nr, int64_t nh, int64_t ns) { return 24 * (nr + nh) + 24 * nr + 24 * ns + kSpTileLdsFixed; };
@@ -91,7 +142,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             int64_t dnh = 0, dns = 0;
             attempt++;
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
-                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                const int32_t gj = okj[k];
                 if (gj >= gs && gj < g) dns += 2;
                 else if (hcnt[gj] == 0 && stamp[gj] != attempt) { stamp[gj] = attempt; dnh += gsz[gj]; }
             }
@@ -111,7 +162,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             }
             // commit
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
-                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                const int32_t gj = okj[k];
                 if (!(gj >= gs && gj < g)) {
                     if (hcnt[gj]++ == 0) halo_members.push_back(gj);
                 }
@@ -126,6 +177,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         for (int32_t h : halo_members) hcnt[h] = 0;
         tstart.push_back(ng);
     }
+    lap("partition");
     const int32_t nt = (int32_t)tstart.size() - 1;
     // 2. entries, le order, per tile rows / halo / slots
     H.tile_tab.assign(8 * (size_t)nt, 0);
@@ -152,7 +204,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         std::vector<int32_t> hg;
         for (int32_t g = g0; g < g1; g++)
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
-                const int32_t gj = in.gpos[ap[4 * (int64_t)oe[k] + 2]];
+                const int32_t gj = okj[k];
                 if (gj < g0 || gj >= g1) hg.push_back(gj);
             }
         std::sort(hg.begin(), hg.end());
@@ -169,10 +221,10 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         for (int32_t g = g0; g < g1; g++)
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
                 const int64_t e = oe[k];
-                const int32_t gj = in.gpos[ap[4 * e + 2]];
+                const int32_t gj = okj[k];
                 if (gj >= g0 && gj < g1) {
-                    slotcnt[in.row_of_point[ap[4 * e + 2]] - H.lo - r0]++;
-                    slotcnt[in.row_of_point[ap[4 * e + 3]] - H.lo - r0]++;
+                    slotcnt[erow[4 * e + 2] - r0]++;
+                    slotcnt[erow[4 * e + 3] - r0]++;
                 }
             }
         slotfill.assign(nr, 0);
@@ -205,25 +257,24 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             for (int64_t k = k0; k < k1; k++) {
                 chunk_start();
                 const int64_t e = oe[k];
-                const int32_t gj = in.gpos[ap[4 * e + 2]];
+                const int32_t gj = okj[k];
                 const bool cut = gj < g0 || gj >= g1;
-                const int32_t ra = in.row_of_point[ap[4 * e]] - H.lo - r0;       // tile rows of p1_i, p2_i
+                const int32_t ra = erow[4 * e] - r0;                              // tile rows of p1_i, p2_i
                 const int32_t ub = lrow[g];
                 const uint32_t swap = ra == ub + 1 ? 1u : 0u;
                 // LDS rows of p1_j, p2_j: tile rows, or the halo rows after them
-                auto ldsrow = [&](int32_t pt) {
-                    const int32_t row = in.row_of_point[pt] - H.lo;
+                auto ldsrow = [&](int32_t row) {
                     return cut ? lrow[gj] + (row - grow[gj] + H.lo) : row - r0;
                 };
-                const uint32_t rj0 = (uint32_t)ldsrow(ap[4 * e + 2]), rj1 = (uint32_t)ldsrow(ap[4 * e + 3]);
+                const uint32_t rj0 = (uint32_t)ldsrow(erow[4 * e + 2]), rj1 = (uint32_t)ldsrow(erow[4 * e + 3]);
                 uint32_t w0 = rj0 | rj1 << 12 | kTmValid | swap * kTmSwap;
                 if (k == k0) w0 |= kTmHead;
                 if (k == k1 - 1) w0 |= kTmLast;
                 uint32_t w1 = (uint32_t)ub << 24;
                 if (cut) {
                     w0 |= kTmCut;
-                    xt.push_back({in.row_of_point[ap[4 * e + 2]] - H.lo, (int32_t)nx});
-                    xt.push_back({in.row_of_point[ap[4 * e + 3]] - H.lo, (int32_t)nx + 1});
+                    xt.push_back({erow[4 * e + 2], (int32_t)nx});
+                    xt.push_back({erow[4 * e + 3], (int32_t)nx + 1});
                     nx += 2;
                 } else {
                     const int32_t s0 = slotfill[rj0]++, s1 = slotfill[rj1]++;
@@ -244,16 +295,20 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         for (int32_t g = g0; g < g1; g++) lrow[g] = -1;
         for (int32_t gj : hg) lrow[gj] = -1;
     }
+    lap("entries, slots");
     if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
-    // cross slots by target row, source order inside a row
-    std::stable_sort(xt.begin(), xt.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-    // (the writer scatters its two slots to their destination positions; a row's slots are then one
-    // contiguous range the reader sums without an index load)
+    // cross slots by target row, source order inside a row (a counting sort; xt is in source order):
+    // the writer scatters its two slots to their destination positions, so a row's slots are one
+    // contiguous range the reader sums without an index load
     H.tile_xoff.assign(nown + 1, 0);
     H.tile_xdst.assign(xt.size(), 0);
     for (const auto &x : xt) H.tile_xoff[x.first + 1]++;
     for (int32_t l = 0; l < nown; l++) H.tile_xoff[l + 1] += H.tile_xoff[l];
-    for (size_t k = 0; k < xt.size(); k++) H.tile_xdst[xt[k].second] = (int32_t)k;
+    {
+        std::vector<int32_t> fill(H.tile_xoff.begin(), H.tile_xoff.end() - 1);
+        for (const auto &x : xt) H.tile_xdst[x.second] = fill[x.first]++;
+    }
+    lap("cross slots");
     H.ntile = nt;
     H.tile_entries = (int64_t)m0.size();
     H.tile_cross = nx;
