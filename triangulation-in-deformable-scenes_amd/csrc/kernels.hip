@@ -129,7 +129,8 @@ __device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__rest
 // x / area by the pair's reciprocal: q0 = x RN(1/area), the residual x - q0 area exact by FMA, one
 // correction q0 + res RN(1/area) — Markstein's sequence, the correctly rounded quotient (the bits of
 // x / area) for operands far from overflow / underflow, as the ARAP terms are (point differences
-// over a mesh area; tools/micro/div_markstein.c: 4e8 random operand pairs, no difference).  An exact
+// over a mesh area; tools/micro/div_markstein.c: 4e8 random operand pairs, no difference;
+// tests/test_markstein.py runs it on every CPU suite).  An exact
 // quotient (zero residual) returns q0 itself, so the sign of a zero quotient is kept.  One division
 // per edge instead of up to 108 (the numeric Jacobian's perturbed energies)
 struct AreaDiv {
