@@ -56,9 +56,11 @@ def _reference(p, Ja, Wa, Jr, Wr, Jd, Wd, lam, x):
     return q
 
 
-def _worker(rank, world, port, kind, q):
+def _worker(rank, world, port, kind, q, tile=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if tile:
+        os.environ["DEFTRI_SP_EMULATE_TILE"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from deftri import capi
     from deftri import dist as ddist
@@ -72,13 +74,18 @@ def _worker(rank, world, port, kind, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["mv", "tv"])
+@pytest.mark.parametrize("kind", ["mv", "tv", "tv-tile"])
 @pytest.mark.parametrize("world", [1, 2, 3])
 def test_sharded_product_matches_direct(kind, world):
+    """tv-tile: the sharded tile layout (spcg_tile.cpp) through its host emulation — owned edges
+    whose j vertex is another rank's keep only their own rows' share, the halo-only edges add theirs
+    to this rank's j rows through LDS slots, the heavy sums over owned edges all-reduced."""
+    tile = kind == "tv-tile"
+    kind = "tv" if tile else kind
     cm = mp.get_context("spawn")
     q = cm.Queue()
-    port = 29600 + 17 * world + (1 if kind == "mv" else 0) + os.getpid() % 400
-    procs = [cm.Process(target=_worker, args=(r, world, port, kind, q)) for r in range(world)]
+    port = 29600 + 17 * world + (1 if kind == "mv" else 0) + (5 if tile else 0) + os.getpid() % 400
+    procs = [cm.Process(target=_worker, args=(r, world, port, kind, q, tile)) for r in range(world)]
     for pr in procs:
         pr.start()
     out = {}
@@ -103,7 +110,9 @@ def test_sharded_product_matches_direct(kind, world):
         total[hd:] += qv[hd:]
         owned += st[3]
         assert st[0] > 0 and st[2] >= st[3]
-        if world > 1:
+        if tile:
+            assert world > 1 or st[2] == st[3] == len(p.arap_pair)
+        elif world > 1:
             assert st[1] > 0                        # a halo exists between mesh-adjacent shards
         else:
             assert st[1] == 0 and st[2] == st[3] == len(p.arap_pair)

@@ -1152,13 +1152,18 @@ int deftri_debug_sp_product(deftri_ctx *ctx, const deftri_problem_desc *desc, co
     if (ctx->nranks > 1 && !ctx->xfn) return fail(ctx, DEFTRI_E_ARG, "the emulation needs the callback transport");
     SpPlanHost H;
     std::string err;
-    // DEFTRI_SP_EMULATE_TILE=1 (read per call): one rank, one pair — the tile layout's product instead
+    // DEFTRI_SP_EMULATE_TILE=1 (read per call): one pair — the tile layout's product instead (sharded:
+    // this rank's rows and its share of the heavy sums, all-reduced through the transport)
     const bool tile = std::getenv("DEFTRI_SP_EMULATE_TILE") != nullptr;
     if (!build_sp_plan(*desc, ctx->rank, ctx->nranks, false, H, err, tile)) return fail(ctx, DEFTRI_E_ARG, err);
     if (tile) {
         if (!H.tile) return fail(ctx, DEFTRI_E_ARG, "no tile layout: " + H.tile_why);
         rc = sp_emulate_tile_product(*desc, H, jarap, warap, jrep, wrep, jdep, wdep, lambda, p, q, err);
         if (rc) return fail(ctx, DEFTRI_E_ARG, "tile layout: " + err);
+        if (ctx->nranks > 1) {
+            if (ctx->xfn(ctx->xuser, 0, -1, q, H.hd) != 0) return fail(ctx, DEFTRI_E_ARG, "all-reduce callback failed");
+            for (int64_t k = 0; k < H.hd; k++) q[k] += lambda * p[k];
+        }
     } else {
         std::function<int(int, int, double *, int64_t)> xf = [ctx](int op, int peer, double *buf, int64_t cnt) {
             return ctx->xfn(ctx->xuser, op, peer, buf, cnt);

@@ -60,6 +60,10 @@ constexpr int kSpTileLdsFixed = 2048;      // the tile kernel's fixed dynamic LD
 // tile entry meta word 0: LDS rows of p1_j (bits 0-11), p2_j (12-23), flags; word 1: LDS slots of
 // p1_j (0-11), p2_j (12-23), the unit's first tile row (24-31)
 constexpr uint32_t kTmHead = 1u << 24, kTmLast = 1u << 25, kTmSwap = 1u << 26, kTmValid = 1u << 27, kTmCut = 1u << 28;
+// sharded tile plans: kTmDrop — an owned edge whose j vertex is another rank's (its j rows' share is
+// that rank's); kTmForeign — a halo-only edge (another rank's i vertex, this tile's j vertex): its i
+// rows in the j fields, its j rows at ub / swap, only the j rows' slots written, no owned sums
+constexpr uint32_t kTmDrop = 1u << 29, kTmForeign = 1u << 30;
 enum { SP_ARAP = 0, SP_DEP = 1 };
 // solve status (record word 0).  kSpTimeout: the merged chain's alpha hand-off was not seen within
 // its poll bound (phase 2's workgroup 0 not resident while the others waited): an error, never a
@@ -122,7 +126,7 @@ struct SpPlanHost {
     std::vector<uint32_t> tile_m0, tile_m1;            // per entry (padded to 64 per chunk)
     std::vector<int32_t> tile_chunk;                   // 2 per chunk: first le, first cross slot
     std::vector<int32_t> tile_rs;                      // per own row: LDS slot begin | count << 16
-    std::vector<int32_t> tile_halo;                    // the tiles' halo rows (local row ids)
+    std::vector<int32_t> tile_halo;                    // the tiles' halo rows (global row ids)
     std::vector<int32_t> tile_xoff;                    // per own row its cross slots (destination order)
     std::vector<int32_t> tile_xdst;                    // per cut entry (source order): its 2 cross slots
     double tile_bytes[3] = {0, 0, 0};                  // algorithmic bytes per CG iteration: product, update; fused
@@ -137,7 +141,10 @@ struct TileInput {
 };
 // tile layout of a one-rank, one-pair plan: false (why) when the graph does not fit tile mode; order:
 // the ARAP edges in tile-entry order (the plan's local edge order)
-bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why);
+// order: the owned ARAP edges in tile-entry order (the plan's first local edges), order_foreign: the
+// halo-only ones (sharded plans; after them); H.lo / H.hi the rank's rows
+bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::vector<int32_t> &order_foreign,
+                 std::string &why);
 // host emulation of one tile-mode product with its layout checks (tests; spcg_tile.cpp)
 int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
                             const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,

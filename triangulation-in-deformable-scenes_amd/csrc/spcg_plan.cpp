@@ -231,8 +231,8 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     // 4a. tile mode (one rank, one pair; spcg_tile.cpp): the groups cut into tiles in Morton order,
     //     the ARAP edges in tile-entry order; the rows keep the Morton group order (no 4b sort: a
     //     tile's rows are one contiguous range)
-    std::vector<int32_t> tile_order;
-    if (tile && nranks == 1 && Q == 1 && S <= 2 && E > 0) {
+    std::vector<int32_t> tile_order, tile_foreign;
+    if (tile && Q == 1 && S <= 2 && E > 0) {
         H.lo = H.rank_row_begin[rank];
         H.hi = H.rank_row_begin[rank + 1];
         std::vector<int32_t> gp(P);
@@ -240,13 +240,14 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         TileInput ti;
         ti.P = P; ti.ng = ng; ti.E = E; ti.ap = ap; ti.gpos = gp.data(); ti.row_of_point = H.row_of_point.data();
         std::string why;
-        H.tile = build_tiles(ti, H, tile_order, why);
+        H.tile = build_tiles(ti, H, tile_order, tile_foreign, why);
         if (!H.tile) {
             H.tile_why = why;
             tile_order.clear();
+            tile_foreign.clear();
         }
     } else if (tile) {
-        H.tile_why = nranks != 1 ? "sharded" : Q != 1 ? "more than one keyframe pair" : "no ARAP edges";
+        H.tile_why = Q != 1 ? "more than one keyframe pair" : S > 2 ? "more than two depth scales" : "no ARAP edges";
     }
     stage("4a tiles");
     // 4b. inside every rank's range, rows sorted by their phase-2 slot count (ARAP incidences + depth
@@ -311,6 +312,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     std::vector<int32_t> owned_e, halo_e;
     if (H.tile) {
         owned_e.swap(tile_order);                     // tile-entry order (spcg_tile.cpp)
+        halo_e.swap(tile_foreign);
     } else if (nranks == 1) {
         owned_e.resize((size_t)E);
         std::iota(owned_e.begin(), owned_e.end(), 0);

@@ -37,10 +37,12 @@
 
 namespace deftri {
 
-bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why) {
+bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::vector<int32_t> &order_foreign,
+                 std::string &why) {
     const int32_t ng = in.ng;
     const int64_t E = in.E;
     const int32_t *ap = in.ap;
+    const int32_t lo = H.lo, hi = H.hi;
     static const int umax = [] {
         const char *e = std::getenv("DEFTRI_SP_TILE_UNITS");
         const int v = e ? std::atoi(e) : kSpTileUnits;
@@ -59,72 +61,98 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         std::fprintf(stderr, "[deftri plan]   4a %-26s %8.2f ms\n", w, std::chrono::duration<double, std::milli>(t - T0).count());
         T0 = t;
     };
-    // groups: size and first row (rows of a group are consecutive, groups in Morton order)
+    // groups: size and first row (rows of a group are consecutive, groups in Morton order); this
+    // rank's groups are one range [G0, G1) of that order (ranks are cut at group starts)
     std::vector<int32_t> gsz(ng, 0), grow(ng, INT32_MAX);
     for (int32_t p = 0; p < in.P; p++) {
         const int32_t g = in.gpos[p];
         gsz[g]++;
         grow[g] = std::min(grow[g], in.row_of_point[p]);
     }
-    for (int32_t g = 0; g < ng; g++)
+    int32_t G0 = ng, G1 = 0;
+    for (int32_t g = 0; g < ng; g++) {
         if (gsz[g] > 2) { why = "a keyframe-copy group of more than 2 rows"; return false; }
-    // out-edges per group (edge order inside a group), in-edge sources per group: counting sorts by
-    // group over contiguous edge chunks on host threads (per-chunk counts, each chunk's edges placed
-    // after the earlier chunks' — the sequential order)
+        if (gsz[g] > 0 && grow[g] >= lo && grow[g] < hi) { G0 = std::min(G0, g); G1 = std::max(G1, g + 1); }
+    }
+    if (G0 >= G1) { G0 = G1 = 0; }
+    for (int32_t g = G0; g < G1; g++)
+        if (gsz[g] > 0 && (grow[g] < lo || grow[g] >= hi)) { why = "the rank's groups are not one range"; return false; }
+    auto own = [&](int32_t g) { return g >= G0 && g < G1; };
+    // the local ARAP edges by group: out-edges of the rank's groups (the owned edges), in-edges of its
+    // groups from its groups, and in-edges from other ranks' groups (the halo-only edges: their j
+    // vertex is this rank's).  Counting sorts by group over contiguous edge chunks on host threads
+    // (per-chunk counts, each chunk's edges after the earlier chunks' — the sequential order)
     std::vector<int32_t> egi(E), egj(E), erow(4 * (size_t)E);
-    std::vector<int64_t> ooff(ng + 1, 0), ioff(ng + 1, 0);
-    std::vector<int32_t> oe(E), isrc(E);
+    std::vector<int64_t> ooff(ng + 1, 0), ioff(ng + 1, 0), foff(ng + 1, 0);
+    std::vector<int32_t> oe, isrc, fe;
     {
         constexpr int kMaxChunks = 16;
-        std::vector<std::vector<int32_t>> co(kMaxChunks), ci(kMaxChunks);
+        std::vector<std::vector<int32_t>> co(kMaxChunks), ci(kMaxChunks), cf(kMaxChunks);
         int bad[kMaxChunks] = {0};
-        const int nch = chunked(E, 1 << 15, [&](int c, int64_t lo, int64_t hi) {
+        const int nch = chunked(E, 1 << 15, [&](int c, int64_t elo, int64_t ehi) {
             co[c].assign(ng, 0);
             ci[c].assign(ng, 0);
-            for (int64_t e = lo; e < hi; e++) {
+            cf[c].assign(ng, 0);
+            for (int64_t e = elo; e < ehi; e++) {
                 const int32_t gi = in.gpos[ap[4 * e]], gj = in.gpos[ap[4 * e + 2]];
-                if (gi != in.gpos[ap[4 * e + 1]] || gj != in.gpos[ap[4 * e + 3]] || gi == gj) bad[c] = 1;
                 egi[e] = gi;
                 egj[e] = gj;
-                for (int k = 0; k < 4; k++) erow[4 * e + k] = in.row_of_point[ap[4 * e + k]] - H.lo;
-                co[c][gi]++;
-                ci[c][gj]++;
+                for (int k = 0; k < 4; k++) erow[4 * e + k] = in.row_of_point[ap[4 * e + k]] - lo;
+                if (!own(gi) && !own(gj)) continue;
+                if (gi != in.gpos[ap[4 * e + 1]] || gj != in.gpos[ap[4 * e + 3]] || gi == gj) bad[c] = 1;
+                if (own(gi)) {
+                    co[c][gi]++;
+                    if (own(gj)) ci[c][gj]++;
+                } else {
+                    cf[c][gj]++;
+                }
             }
         });
         for (int c = 0; c < nch; c++)
             if (bad[c]) { why = "an edge's copies in two groups"; return false; }
-        // per group: its total, then each chunk's first position (chunk order)
         for (int32_t g = 0; g < ng; g++) {
-            int64_t so = 0, si = 0;
-            for (int c = 0; c < nch; c++) { so += co[c][g]; si += ci[c][g]; }
+            int64_t so = 0, si = 0, sf = 0;
+            for (int c = 0; c < nch; c++) { so += co[c][g]; si += ci[c][g]; sf += cf[c][g]; }
             ooff[g + 1] = ooff[g] + so;
             ioff[g + 1] = ioff[g] + si;
+            foff[g + 1] = foff[g] + sf;
         }
-        chunked(ng, 1 << 12, [&](int, int64_t lo, int64_t hi) {
-            for (int64_t g = lo; g < hi; g++) {
-                int64_t fo = ooff[g], fi = ioff[g];
+        oe.resize(ooff[ng]);
+        isrc.resize(ioff[ng]);
+        fe.resize(foff[ng]);
+        chunked(ng, 1 << 12, [&](int, int64_t glo, int64_t ghi) {
+            for (int64_t g = glo; g < ghi; g++) {
+                int64_t fo = ooff[g], fi = ioff[g], ff = foff[g];
                 for (int c = 0; c < nch; c++) {
-                    const int32_t a = co[c][g], b = ci[c][g];
+                    const int32_t a = co[c][g], b = ci[c][g], f = cf[c][g];
                     co[c][g] = (int32_t)fo;
                     ci[c][g] = (int32_t)fi;
+                    cf[c][g] = (int32_t)ff;
                     fo += a;
                     fi += b;
+                    ff += f;
                 }
             }
         });
-        chunked(E, 1 << 15, [&](int c, int64_t lo, int64_t hi) {
-            for (int64_t e = lo; e < hi; e++) {
-                oe[co[c][egi[e]]++] = (int32_t)e;
-                isrc[ci[c][egj[e]]++] = egi[e];
+        chunked(E, 1 << 15, [&](int c, int64_t elo, int64_t ehi) {
+            for (int64_t e = elo; e < ehi; e++) {
+                const int32_t gi = egi[e], gj = egj[e];
+                if (own(gi)) {
+                    oe[co[c][gi]++] = (int32_t)e;
+                    if (own(gj)) isrc[ci[c][gj]++] = gi;
+                } else if (own(gj)) {
+                    fe[cf[c][gj]++] = (int32_t)e;
+                }
             }
         });
     }
-    // the j group of every out-edge, in out-edge order
-    std::vector<int32_t> okj(E);
-    chunked(E, 1 << 15, [&](int, int64_t lo, int64_t hi) {
-        for (int64_t k = lo; k < hi; k++) okj[k] = egj[oe[k]];
+    // the j group of every out-edge (out-edge order), the i group of every halo-only in-edge
+    std::vector<int32_t> okj(oe.size()), fki(fe.size());
+    chunked((int64_t)oe.size(), 1 << 15, [&](int, int64_t klo, int64_t khi) {
+        for (int64_t k = klo; k < khi; k++) okj[k] = egj[oe[k]];
     });
-    for (int32_t g = 0; g < ng; g++)
+    for (size_t k = 0; k < fe.size(); k++) fki[k] = egi[fe[k]];
+    for (int32_t g = G0; g < G1; g++)
         if (ooff[g + 1] - ooff[g] > 64) { why = "a vertex with more than 64 ARAP edges"; return false; }
     lap("groups, edges by group");
     // (a group with edges holds p1_i and p2_i: 2 rows; a 1-row group has no ARAP edge)
@@ -133,11 +161,11 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     std::vector<int32_t> tstart;
     std::vector<int32_t> hcnt(ng, 0), stamp(ng, -1);
     {
-        int32_t gs = 0, attempt = 0;
+        int32_t gs = G0, attempt = 0;
         int64_t nr = 0, nh = 0, ns = 0, units = 0;
         std::vector<int32_t> halo_members;
-        tstart.push_back(0);
-        for (int32_t g = 0; g < ng;) {
+        tstart.push_back(G0);
+        for (int32_t g = G0; g < G1;) {
             // tentative add of g (stamp: the halo groups this attempt already counted)
             int64_t dnh = 0, dns = 0;
             attempt++;
@@ -148,6 +176,11 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             }
             for (int64_t k = ioff[g]; k < ioff[g + 1]; k++)
                 if (isrc[k] >= gs && isrc[k] < g) dns += 2;
+            for (int64_t k = foff[g]; k < foff[g + 1]; k++) {       // halo-only in-edges: 2 slots on g
+                const int32_t gi = fki[k];
+                dns += 2;
+                if (hcnt[gi] == 0 && stamp[gi] != attempt) { stamp[gi] = attempt; dnh += gsz[gi]; }
+            }
             if (hcnt[g] > 0) dnh -= gsz[g];
             const bool fits = units + 1 <= umax && lds_of(nr + gsz[g], nh + dnh, ns + dns) <= lds_budget &&
                               nr + gsz[g] + nh + dnh < 4096 && ns + dns < 4096;
@@ -167,6 +200,8 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
                     if (hcnt[gj]++ == 0) halo_members.push_back(gj);
                 }
             }
+            for (int64_t k = foff[g]; k < foff[g + 1]; k++)
+                if (hcnt[fki[k]]++ == 0) halo_members.push_back(fki[k]);
             hcnt[g] = 0;                           // g is a tile row now, no longer halo
             nr += gsz[g];
             nh += dnh;
@@ -175,19 +210,25 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             g++;
         }
         for (int32_t h : halo_members) hcnt[h] = 0;
-        tstart.push_back(ng);
+        tstart.push_back(G1);
     }
+    const int32_t nt = G1 > G0 ? (int32_t)tstart.size() - 1 : 0;
     lap("partition");
-    const int32_t nt = (int32_t)tstart.size() - 1;
-    // 2. entries, le order, per tile rows / halo / slots
+    // 2. entries, le order, per tile rows / halo / slots; a tile's owned entries (its vertices'
+    //    out-edges) first, then — in chunks of their own — its halo-only entries (other ranks'
+    //    vertices' edges into its rows), whose le follow every owned edge's (the plan keeps the owned
+    //    edges first)
     H.tile_tab.assign(8 * (size_t)nt, 0);
     order.clear();
-    order.reserve(E);
+    order.reserve(oe.size());
+    order_foreign.clear();
+    order_foreign.reserve(fe.size());
+    const int64_t n_owned = (int64_t)oe.size();
     std::vector<uint32_t> &m0 = H.tile_m0, &m1 = H.tile_m1;
     m0.clear(); m1.clear();
     H.tile_chunk.clear();
     H.tile_halo.clear();
-    const int32_t nown = H.hi - H.lo;
+    const int32_t nown = hi - lo;
     H.tile_rs.assign(nown, 0);
     // cross slots: (target row, slot) pairs, CSR by row at the end
     std::vector<std::pair<int32_t, int32_t>> xt;
@@ -197,36 +238,41 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     std::vector<int32_t> slotcnt, slotfill;       // per tile row
     for (int32_t t = 0; t < nt; t++) {
         const int32_t g0 = tstart[t], g1 = tstart[t + 1];
-        const int32_t r0 = grow[g0] - H.lo;
+        const int32_t r0 = grow[g0] - lo;
         int32_t nr = 0;
         for (int32_t g = g0; g < g1; g++) { lrow[g] = nr; nr += gsz[g]; }
-        // halo groups, ascending
+        // halo groups, ascending: out-edges' j groups outside the tile, halo-only edges' i groups
         std::vector<int32_t> hg;
-        for (int32_t g = g0; g < g1; g++)
-            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
-                const int32_t gj = okj[k];
-                if (gj < g0 || gj >= g1) hg.push_back(gj);
-            }
+        for (int32_t g = g0; g < g1; g++) {
+            for (int64_t k = ooff[g]; k < ooff[g + 1]; k++)
+                if (okj[k] < g0 || okj[k] >= g1) hg.push_back(okj[k]);
+            for (int64_t k = foff[g]; k < foff[g + 1]; k++) hg.push_back(fki[k]);
+        }
         std::sort(hg.begin(), hg.end());
         hg.erase(std::unique(hg.begin(), hg.end()), hg.end());
         const int32_t h0 = (int32_t)H.tile_halo.size();
         int32_t nh = 0;
         for (int32_t gj : hg) {
             lrow[gj] = nr + nh;
-            for (int32_t k = 0; k < gsz[gj]; k++) H.tile_halo.push_back(grow[gj] + k - H.lo);
+            for (int32_t k = 0; k < gsz[gj]; k++) H.tile_halo.push_back(grow[gj] + k);   // (global rows)
             nh += gsz[gj];
         }
         // remote slots: count per tile row, in entry order
         slotcnt.assign(nr, 0);
-        for (int32_t g = g0; g < g1; g++)
+        for (int32_t g = g0; g < g1; g++) {
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++) {
                 const int64_t e = oe[k];
-                const int32_t gj = okj[k];
-                if (gj >= g0 && gj < g1) {
+                if (okj[k] >= g0 && okj[k] < g1) {
                     slotcnt[erow[4 * e + 2] - r0]++;
                     slotcnt[erow[4 * e + 3] - r0]++;
                 }
             }
+            for (int64_t k = foff[g]; k < foff[g + 1]; k++) {
+                const int64_t e = fe[k];
+                slotcnt[erow[4 * e + 2] - r0]++;
+                slotcnt[erow[4 * e + 3] - r0]++;
+            }
+        }
         slotfill.assign(nr, 0);
         int32_t ns = 0;
         for (int32_t r = 0; r < nr; r++) {
@@ -245,8 +291,8 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
                 fill++;
             }
         };
-        auto chunk_start = [&]() {
-            if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)order.size()), H.tile_chunk.push_back((int32_t)nx);
+        auto chunk_start = [&](int64_t le) {
+            if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)le), H.tile_chunk.push_back((int32_t)nx);
         };
         for (int32_t g = g0; g < g1; g++) {
             const int64_t k0 = ooff[g], k1 = ooff[g + 1];
@@ -255,23 +301,26 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             segmax = std::max(segmax, cnt);
             if (fill % 64 + cnt > 64) pad_chunk();
             for (int64_t k = k0; k < k1; k++) {
-                chunk_start();
+                chunk_start((int64_t)order.size());
                 const int64_t e = oe[k];
                 const int32_t gj = okj[k];
-                const bool cut = gj < g0 || gj >= g1;
-                const int32_t ra = erow[4 * e] - r0;                              // tile rows of p1_i, p2_i
+                const bool remote = !own(gj);                   // j on another rank: its rows' share there
+                const bool cut = !remote && (gj < g0 || gj >= g1);
+                const int32_t ra = erow[4 * e] - r0;             // tile rows of p1_i, p2_i
                 const int32_t ub = lrow[g];
                 const uint32_t swap = ra == ub + 1 ? 1u : 0u;
                 // LDS rows of p1_j, p2_j: tile rows, or the halo rows after them
                 auto ldsrow = [&](int32_t row) {
-                    return cut ? lrow[gj] + (row - grow[gj] + H.lo) : row - r0;
+                    return (cut || remote) ? lrow[gj] + (row + lo - grow[gj]) : row - r0;
                 };
                 const uint32_t rj0 = (uint32_t)ldsrow(erow[4 * e + 2]), rj1 = (uint32_t)ldsrow(erow[4 * e + 3]);
                 uint32_t w0 = rj0 | rj1 << 12 | kTmValid | swap * kTmSwap;
                 if (k == k0) w0 |= kTmHead;
                 if (k == k1 - 1) w0 |= kTmLast;
                 uint32_t w1 = (uint32_t)ub << 24;
-                if (cut) {
+                if (remote) {
+                    w0 |= kTmDrop;
+                } else if (cut) {
                     w0 |= kTmCut;
                     xt.push_back({erow[4 * e + 2], (int32_t)nx});
                     xt.push_back({erow[4 * e + 3], (int32_t)nx + 1});
@@ -286,7 +335,30 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
                 fill++;
             }
         }
-        if (fill == 0) { chunk_start(); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
+        // halo-only entries, in chunks of their own: each its own segment (no own-row sums); the
+        // kernel reads their i rows (halo) through the j fields and their j rows (this tile's)
+        // through ub / swap, and writes only the j rows' slots
+        bool any_f = false;
+        for (int32_t g = g0; g < g1 && !any_f; g++) any_f = foff[g + 1] > foff[g];
+        if (any_f) pad_chunk();
+        for (int32_t g = g0; g < g1; g++)
+            for (int64_t k = foff[g]; k < foff[g + 1]; k++) {
+                chunk_start(n_owned + (int64_t)order_foreign.size());
+                const int64_t e = fe[k];
+                const int32_t gi = fki[k];
+                const int32_t ub = lrow[g];
+                const int32_t rj = erow[4 * e + 2] - r0;        // p1_j's tile row
+                const uint32_t swap = rj == ub + 1 ? 1u : 0u;
+                const uint32_t ri0 = (uint32_t)(lrow[gi] + (erow[4 * e] + lo - grow[gi]));
+                const uint32_t ri1 = (uint32_t)(lrow[gi] + (erow[4 * e + 1] + lo - grow[gi]));
+                const uint32_t w0 = ri0 | ri1 << 12 | kTmValid | kTmHead | kTmForeign | swap * kTmSwap;
+                const int32_t s0 = slotfill[erow[4 * e + 2] - r0]++, s1 = slotfill[erow[4 * e + 3] - r0]++;
+                m0.push_back(w0);
+                m1.push_back((uint32_t)s0 | (uint32_t)s1 << 12 | (uint32_t)ub << 24);
+                order_foreign.push_back((int32_t)e);
+                fill++;
+            }
+        if (fill == 0) { chunk_start((int64_t)order.size()); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
         pad_chunk();
         const int64_t ne = (int64_t)m0.size() - e0;
         int32_t *T = &H.tile_tab[8 * (size_t)t];
@@ -296,7 +368,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         for (int32_t gj : hg) lrow[gj] = -1;
     }
     lap("entries, slots");
-    if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
+    if ((int64_t)order.size() != n_owned || order_foreign.size() != fe.size()) { why = "tile order lost edges"; return false; }
     // cross slots by target row, source order inside a row (a counting sort; xt is in source order):
     // the writer scatters its two slots to their destination positions, so a row's slots are one
     // contiguous range the reader sums without an index load
@@ -324,15 +396,18 @@ namespace deftri {
 
 // Host emulation of one tile-mode product q = (H + lambda I) p (tests, no GPU): k_sp_tile's entry
 // walk — le and cross slots from the chunk bases and the valid / cut lanes before an entry, the own
-// rows' sums, the LDS remote slots and the cross slots — then k_sp_tupd's cross sums, with the layout
-// checked on the way: every LDS slot and every cross slot written exactly once and read exactly once.
-// J / W in the problem's edge order; q in problem order.  Returns 0, or -1 (why) on a layout fault.
+// rows' sums, the LDS remote slots and the cross slots — then the update's cross sums, with the
+// layout checked on the way: every LDS slot and every cross slot written exactly once and read exactly
+// once, every local edge visited once (owned ones in the owned range, halo-only ones after it).
+// J / W in the problem's edge order; q in problem order: this rank's rows, and the heavy rows' sums
+// over its owned edges and own depth edges (+ lambda p on one rank; a sharded caller all-reduces them
+// and adds it).  Returns 0, or -1 (why) on a layout fault.
 int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
                             const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
                             const double *p, double *q, std::string &why) {
     if (!H.tile) { why = "not a tile plan"; return -1; }
     const int64_t hd = H.hd, ndof = hd + 3 * (int64_t)H.P;
-    const int32_t Q = H.Q, nown = H.hi - H.lo;
+    const int32_t Q = H.Q, nown = H.hi - H.lo, lo = H.lo;
     std::vector<double> pl(ndof, 0.0), qr(ndof, 0.0);
     for (int64_t k = 0; k < hd; k++) pl[k] = p[k];
     for (int32_t r = 0; r < H.P; r++)
@@ -346,10 +421,9 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
         if (e0 % 64 || ne % 64) { why = "tile entries not chunk aligned"; return -1; }
         std::vector<double> pL(3 * (size_t)(nr + nh)), up(3 * (size_t)nr, 0.0), rs(3 * (size_t)std::max(ns, 1), 0.0);
         std::vector<int> rsw(std::max(ns, 1), 0), rsr(std::max(ns, 1), 0);
-        for (int32_t i = 0; i < nr + nh; i++) {
-            const int32_t row = i < nr ? r0 + i : H.tile_halo[h0 + i - nr];
-            for (int c = 0; c < 3; c++) pL[3 * (size_t)i + c] = pl[hd + 3 * (int64_t)row + c];
-        }
+        auto grow_of = [&](int32_t i) { return i < nr ? lo + r0 + i : H.tile_halo[h0 + i - nr]; };
+        for (int32_t i = 0; i < nr + nh; i++)
+            for (int c = 0; c < 3; c++) pL[3 * (size_t)i + c] = pl[hd + 3 * (int64_t)grow_of(i) + c];
         int nv = 0, nc = 0;
         for (int32_t k = 0; k < ne; k++) {
             const int64_t ke = (int64_t)e0 + k;
@@ -358,29 +432,33 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
             const int32_t *ch = &H.tile_chunk[2 * (size_t)(ke >> 6)];
             if (!(m0 & kTmValid)) continue;
             const int64_t le = ch[0] + nv++;
-            const bool cut = (m0 & kTmCut) != 0;
+            const bool cut = (m0 & kTmCut) != 0, foreign = (m0 & kTmForeign) != 0, drop = (m0 & kTmDrop) != 0;
             const int64_t x = ch[1] + 2 * (int64_t)(cut ? nc++ : nc);
             if (le >= (int64_t)H.arap_ids.size()) { why = "le out of range"; return -1; }
+            if (foreign != (le >= H.n_arap_owned)) { why = "an entry's le outside its class's range"; return -1; }
             lew[le]++;
             const int64_t e = H.arap_ids[le];
             const double *J = Ja + 18 * e;
             const int ub = (int)(m1 >> 24), sw = (int)((m0 >> 26) & 1u);
-            const int rows[4] = {ub + sw, ub + 1 - sw, (int)(m0 & 0xfffu), (int)((m0 >> 12) & 0xfffu)};
+            const int ro0 = ub + sw, ro1 = ub + 1 - sw, rf0 = (int)(m0 & 0xfffu), rf1 = (int)((m0 >> 12) & 0xfffu);
+            const int rows[4] = {foreign ? rf0 : ro0, foreign ? rf1 : ro1, foreign ? ro0 : rf0, foreign ? ro1 : rf1};
             for (int kk = 0; kk < 4; kk++) {
-                const int32_t lim = kk < 2 ? nr : nr + nh;
+                const bool tile_row = foreign ? kk >= 2 : kk < 2;
+                const int32_t lim = tile_row ? nr : nr + nh;
                 if (rows[kk] < 0 || rows[kk] >= lim) { why = "an entry's LDS row out of range"; return -1; }
                 // the LDS row must hold the edge's point
-                const int32_t prow = H.row_of_point[d.arap_pts[4 * e + kk]];
-                const int32_t lrow = rows[kk] < nr ? r0 + rows[kk] : H.tile_halo[h0 + rows[kk] - nr];
-                if (prow != lrow) { why = "an entry's LDS row is not its point's row"; return -1; }
+                if (H.row_of_point[d.arap_pts[4 * e + kk]] != grow_of(rows[kk])) { why = "an entry's LDS row is not its point's row"; return -1; }
             }
             double tt = 0.0;
             for (int kk = 0; kk < 4; kk++)
                 for (int c = 0; c < 3; c++) tt += J[3 * kk + c] * pL[3 * (size_t)rows[kk] + c];
             for (int c = 0; c < 6; c++) tt += J[12 + c] * pl[6 * (int64_t)d.arap_pair[e] + c];
             const double s = Wa[e] * tt;
-            for (int c = 0; c < 6; c++) hsum[6 * (int64_t)d.arap_pair[e] + c] += J[12 + c] * s;
-            for (int c = 0; c < 3; c++) { up[3 * (size_t)rows[0] + c] += J[c] * s; up[3 * (size_t)rows[1] + c] += J[3 + c] * s; }
+            if (!foreign) {
+                for (int c = 0; c < 6; c++) hsum[6 * (int64_t)d.arap_pair[e] + c] += J[12 + c] * s;
+                for (int c = 0; c < 3; c++) { up[3 * (size_t)rows[0] + c] += J[c] * s; up[3 * (size_t)rows[1] + c] += J[3 + c] * s; }
+            }
+            if (drop) continue;
             if (cut) {
                 if (x < 0 || x + 2 > H.tile_cross) { why = "cross slot out of range"; return -1; }
                 const int64_t d0 = H.tile_xdst[x], d1 = H.tile_xdst[x + 1];
@@ -403,7 +481,7 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
                 rsr[k]++;
                 for (int c = 0; c < 3; c++) acc[c] += rs[3 * (size_t)k + c];
             }
-            const int64_t o = hd + 3 * (int64_t)l;
+            const int64_t o = hd + 3 * (int64_t)(lo + l);
             for (int32_t j = H.rep_off[l]; j < H.rep_off[l + 1]; j++) {
                 const int64_t e = H.rep_ids[j];
                 const double *J = Jr + 6 * e;
@@ -433,14 +511,15 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
         for (int32_t k = H.tile_xoff[l]; k < H.tile_xoff[l + 1]; k++) {
             const int64_t x = k;
             xr[x]++;
-            for (int c = 0; c < 3; c++) qr[hd + 3 * (int64_t)l + c] += xc[3 * x + c];
+            for (int c = 0; c < 3; c++) qr[hd + 3 * (int64_t)(lo + l) + c] += xc[3 * x + c];
         }
     for (int64_t x = 0; x < H.tile_cross; x++)
         if (xw[x] != 1 || xr[x] != 1) { why = "a cross slot not written / read exactly once"; return -1; }
     for (int64_t k = 0; k < ndof; k++) q[k] = 0.0;
-    for (int32_t r = 0; r < H.P; r++)
-        for (int c = 0; c < 3; c++) q[hd + 3 * (int64_t)H.point_of_row[r] + c] = qr[hd + 3 * (int64_t)r + c];
-    for (int64_t k = 0; k < hd; k++) q[k] = hsum[k] + lambda * pl[k];
+    for (int32_t l = 0; l < nown; l++)
+        for (int c = 0; c < 3; c++) q[hd + 3 * (int64_t)H.point_of_row[lo + l] + c] = qr[hd + 3 * (int64_t)(lo + l) + c];
+    const bool one = H.nranks <= 1;
+    for (int64_t k = 0; k < hd; k++) q[k] = hsum[k] + (one ? lambda * pl[k] : 0.0);
     return 0;
 }
 
