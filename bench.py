@@ -426,7 +426,8 @@ def product_roofline(stats, rep, ctx, rank):
     if tile or "sp_phase1" in stats:
         # tile mode (one rank, one pair): k_sp_tile (the product, every ARAP edge read once) +
         # k_sp_tupd (the update), or k_sp_tile alone when the update is fused into its launch
-        n1, n2 = ("sp_tile", "sp_tupd") if tile else ("sp_phase1", "sp_phase2")
+        # (the sharded tile chain: k_sp_tile (interior + boundary launches) + k_sp_update_sd)
+        n1, n2 = ("sp_tile", "sp_tupd" if "sp_tupd" in stats else "sp_update") if tile else ("sp_phase1", "sp_phase2")
         none = {"launches": 0, "ms": 0.0, "bytes": 0.0}
         p1, p2 = stats[n1], stats.get(n2, none)
         its = max(p2["launches"] or p1["launches"], 1)
@@ -435,9 +436,11 @@ def product_roofline(stats, rep, ctx, rank):
         survey = ctx.plan_info().get("survey_bytes") or 0.0
         gbs_s = survey / max(ms / its * 1e-3, 1e-12) / 1e9
         cg = sum(stats[k]["ms"] for k in ("sp_dots", "sp_phase1", "sp_phase2", "sp_heavy", "sp_update", "sp_tile",
-                                          "sp_tupd", "sp_alpha") if k in stats)
+                                          "sp_tupd", "sp_alpha", "sp_txb") if k in stats)
         merged = "sp_update" not in stats
-        if tile:
+        if tile and n2 == "sp_update":
+            kname = "k_sp_tile+k_sp_update_sd (sharded tile chain: A z by tiles, every ARAP edge read once + update)"
+        elif tile:
             kname = ("k_sp_tile+k_sp_tupd (tile mode: matrix-free product reading every ARAP edge once + update)"
                      if n2 in stats else "k_sp_tile (tile mode, update fused: one cooperative launch per CG iteration)")
         else:

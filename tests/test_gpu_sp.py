@@ -266,6 +266,7 @@ def test_sharded_iterative_matches_oracle(kind, world):
         info = out[r][0]
         assert info["plan"] == "iterative" and info["nranks"] == world and info["halo_rows"] > 0
         assert info["sharded"] == 1 and info["cg_launches"] == 3 and info["cg_collectives"] == 1
+        assert (info["tiles"] > 0) == (kind == "tv")   # one pair: the sharded tile chain (spcg_tile.cpp)
     # the sharded chain (single-reduction CG, sums split over the ranks) against exact steps: the
     # step differences are ~kappa * 1e-12 and the LM iterations amplify them
     for analytic, tol in ((True, 1e-8), (False, 1e-6)):

@@ -291,6 +291,10 @@ int sp_merged_grid1(const SpDev &G);    // merged chain: phase-1 / phase-2 grid 
 int sp_merged_grid2(const SpDev &G);
 void sp_launch_update(const SpDev &G, int it, hipStream_t st);
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st);   // q = (H + lambda I) p
+// sharded tile chain: w = A z by tiles (k_sp_tile, beta 0) and the rank's record xb (k_sp_txb)
+// (list: the launch's logical workgroups, n of them — nullptr / t_grid: all; txb: then k_sp_txb)
+void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n,
+                       bool txb);
 int sp_tile_coop_capacity(int lds, int device);   // resident k_sp_tile<*, 1> workgroups (0: no cooperative launch)
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 // sharded chain, phase 1 over `n` of its logical workgroups (list: their indices; nullptr: all, n =

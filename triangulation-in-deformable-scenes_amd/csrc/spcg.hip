@@ -1556,6 +1556,10 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update_sd(int it, const S
             const double2 v = G.zp[o0 + t];
             z = v.x; pp = v.y;
             w = G.q[o0 + t];
+            if (G.tile) {                              // the row's cross slots (other tiles' edges)
+                const int l = l0 + t / 3, a = t - 3 * (t / 3);
+                for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++) w += G.xc[3 * (int64_t)k + a];
+            }
             sp = G.sv[o0 + t];
             x = G.x[o0 + t];
             r = G.r[o0 + t];
@@ -1735,14 +1739,19 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
     double beta;
-    if (!FU && G.tparts && (it > 0 || !G.tile_fuse)) {
+    if (G.sd) {
+        // sharded single-reduction chain: the product is A z (beta 0); the state is the update's
+        beta = 0.0;
+        if (G.rec[0] != 0.0) return;
+    } else if (!FU && G.tparts && (it > 0 || !G.tile_fuse)) {
         if (tile_state(G, it, beta, reinterpret_cast<double(*)[4]>(&red[0][0]))) return;
     } else if (const int st = it_state(G, it, beta)) {
         if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
-    const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool heavy_wg = b == (int)gridDim.x - 1;
+    // (sharded overlap: the launch runs a subset of the logical workgroups, G.p1list)
+    const int b = G.p1list ? G.p1list[blockIdx.x] : (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool heavy_wg = b == G.t_grid - 1;
     double pap = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
     double qk[3] = {0, 0, 0}, pk[3] = {0, 0, 0}, phv = 0.0;     // FU: the row's q and p (tid < nr), heavy p
     int lrow = -1;
@@ -1767,7 +1776,9 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         const int r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
         double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
         for (int i = tid; i < nr + nh; i += 256) {
-            const int row = i < nr ? r0 + i : G.thalo[h0 + i - nr];
+            // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another
+            // rank's in the receive region)
+            const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) pL[3 * i + c] = pval(G.zp, beta, o + c);
@@ -1784,6 +1795,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             const uint2 m = G.tmeta[k];
             const int2 ch = G.tchunk[k >> 6];
             const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
+            const bool foreign = (m.x & kTmForeign) != 0, drop = (m.x & kTmDrop) != 0;   // (sharded plans)
             const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
             const int le = ch.x + __popcll(vm & lt);
             double J[18];
@@ -1792,7 +1804,8 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             const int ub = (int)(m.y >> 24), sw = (int)((m.x >> 26) & 1u);
             const int ra = valid ? ub + sw : 0, rb = valid ? ub + 1 - sw : 0;
             const int rj0 = valid ? (int)(m.x & 0xfffu) : 0, rj1 = valid ? (int)((m.x >> 12) & 0xfffu) : 0;
-            const int rows[4] = {ra, rb, rj0, rj1};
+            // a halo-only entry: its i rows in the j fields, its j rows at ub / swap
+            const int rows[4] = {foreign ? rj0 : ra, foreign ? rj1 : rb, foreign ? ra : rj0, foreign ? rb : rj1};
             double tt = 0.0;
 #pragma unroll
             for (int kk = 0; kk < 4; kk++)
@@ -1801,10 +1814,12 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
 #pragma unroll
             for (int c = 0; c < 6; c++) tt += J[12 + c] * hp[c];
             const double s = W * tt;
-            pap += s * tt;
+            if (!foreign) {                        // (an owned edge's terms count on its owner only)
+                pap += s * tt;
 #pragma unroll
-            for (int c = 0; c < 6; c++) jts[c] += J[12 + c] * s;
-            if (valid) {
+                for (int c = 0; c < 6; c++) jts[c] += J[12 + c] * s;
+            }
+            if (valid && !drop) {
                 if (cut) {                         // the two cross slots, at their rows' positions
                     const int2 xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
 #pragma unroll
@@ -1844,7 +1859,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         __syncthreads();
         if (tid < nr) {
             const int l = r0 + tid;
-            const int64_t o = G.hd + 3 * (int64_t)l;
+            const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
             double q[3], p[3], D[6];
 #pragma unroll
             for (int c = 0; c < 3; c++) { q[c] = up[3 * tid + c]; p[c] = pL[3 * tid + c]; }
@@ -2116,6 +2131,33 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
     }
     pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
     m2_dots(G, it, red);
+}
+
+// sharded tile chain (G.sd && G.tile): the rank's share of the single-reduction record xb from the
+// tile product's partials — per heavy vertex its sums of A z over the tiles (one workgroup each), z.Az
+// from every tile workgroup's partial, (r.z, r.r) from the update's (or the setup's) row-block
+// partials — as k_sp_phase2<MG 2>'s first workgroups form it from phase 1's; the host all-reduces xb
+__global__ void __launch_bounds__(256) k_sp_txb(int it, const SpDev G) {
+    __shared__ double red4[4];
+    __shared__ double lds[256];
+    (void)it;
+    if (gated_off(G.gate) || G.rec[0] != 0.0) return;
+    const int nh = G.Q + G.S, h = (int)blockIdx.x;
+    if (h < nh) {
+        const double t = tile_heavy_sum(G, h, lds);
+        if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) G.xb[3 + heavy_dof(G, h) + threadIdx.x] = t;
+    } else if (h == nh) {
+        double a = 0.0;
+        for (int j = threadIdx.x; j < G.t_grid; j += 256) a += G.m1part[j];
+        a = block_sum(a, red4);
+        if (threadIdx.x == 0) G.xb[2] = a;
+    } else {
+        double a0 = 0.0, a1 = 0.0;
+        for (int j = threadIdx.x; j <= G.nrb; j += 256) { a0 += G.upart[2 * j]; a1 += G.upart[2 * j + 1]; }
+        a0 = block_sum(a0, red4);
+        a1 = block_sum(a1, red4);
+        if (threadIdx.x == 0) { G.xb[0] = a0; G.xb[1] = a1; }
+    }
 }
 
 // ---- tile mode, per LM iteration: the rows' ARAP blocks by tiles --------------------------------------
@@ -2468,6 +2510,19 @@ int sp_tile_coop_capacity(int lds, int device) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
     return std::min(nb, nb32) * prop.multiProcessorCount;
+}
+
+void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n,
+                       bool txb) {
+    if (n > 0) {
+        SpDev g = G;
+        g.p1list = list;
+        hipEvent_t e0_ = prof_begin(st);
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
+        prof_end("sp_tile", e0_, (unsigned)n, 0.0, st);
+    }
+    if (txb) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
 }
 
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {

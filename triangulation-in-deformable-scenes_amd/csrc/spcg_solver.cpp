@@ -212,12 +212,17 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G = SpDev();
     static const bool timing = std::getenv("DEFTRI_UPLOAD_TIMING") != nullptr;
     const auto tu0 = std::chrono::steady_clock::now();
-    // tile mode (spcg_tile.cpp: the fused product, every ARAP edge read once per CG iteration): one
-    // rank on the merged chain, one keyframe pair; DEFTRI_SP_NO_TILE=1 keeps the two-phase product
+    // tile mode (spcg_tile.cpp: the fused product, every ARAP edge read once per CG iteration), one
+    // keyframe pair: one rank on the merged chain from kSpMergeMinDof unknowns, and every sharded
+    // context on the single-reduction chain (the product on z there); DEFTRI_SP_NO_TILE=1 keeps the
+    // two-phase product everywhere, DEFTRI_SP_SD_NO_TILE=1 on sharded contexts
     static const bool no_tile = std::getenv("DEFTRI_SP_NO_TILE") != nullptr;
+    static const bool sd_no_tile = std::getenv("DEFTRI_SP_SD_NO_TILE") != nullptr || std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
     const int64_t ndof_ = 6 * (int64_t)d.n_pairs + d.n_scales + 3 * (int64_t)d.n_points;
-    const bool want_tile = !shard_ && !no_tile && !std::getenv("DEFTRI_SP_NO_FUSE") && !std::getenv("DEFTRI_SP_NO_MERGE") &&
-                           d.n_pairs == 1 && (ndof_ >= kSpMergeMinDof || std::getenv("DEFTRI_SP_MERGE"));
+    const bool want_tile = !no_tile && d.n_pairs == 1 &&
+                           (shard_ ? !sd_no_tile
+                                   : !std::getenv("DEFTRI_SP_NO_FUSE") && !std::getenv("DEFTRI_SP_NO_MERGE") &&
+                                         (ndof_ >= kSpMergeMinDof || std::getenv("DEFTRI_SP_MERGE")));
     if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err, want_tile)) return DEFTRI_E_ARG;
     const auto tu1 = std::chrono::steady_clock::now();
     struct Report {                 // DEFTRI_UPLOAD_TIMING=1: plan build vs the rest of the upload
@@ -392,7 +397,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         uint8_t *ws;
         PUT(rm, H.rowmap); PUT(wo, H.woff); PUT(pm, H.pmap); PUT(pi, H.pidx); PUT(ws, H.wsplit);
         G.rowmap = rm; G.woff = wo; G.pmap = pm; G.pidx = pi; G.wsplit = ws;
-        if (H.tile && G.merged) { G.pj = nullptr; G.pj32 = nullptr; }   // the fused product reads J once
+        if (H.tile && (G.merged || G.sd)) { G.pj = nullptr; G.pj32 = nullptr; }   // the fused product reads J once
         else if (fp32_jac) { ALLOC(G.pj32, 3 * 64 * G.nslots); }
         else { ALLOC(G.pj, 3 * 64 * G.nslots); }
         H.pmap.clear(); H.pmap.shrink_to_fit();
@@ -412,7 +417,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     double *zp;
     ALLOC(zp, 2 * zp_n);
     G.zp = reinterpret_cast<double2 *>(zp);
-    if (H.tile && G.merged) {
+    if (H.tile && (G.merged || G.sd)) {
         G.tile = 1;
         G.ntile = H.ntile;
         G.tile_lds = H.tile_lds;
@@ -420,7 +425,20 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.t_grid = 8 * ((H.ntile + 7) / 8) + 1;
         int32_t *tt, *trs, *th, *txo, *txd, *tch;
         uint32_t *tm;
-        PUT(tt, H.tile_tab); PUT(trs, H.tile_rs); PUT(th, H.tile_halo); PUT(txo, H.tile_xoff); PUT(txd, H.tile_xdst);
+        // halo rows as zp rows: this rank's (global row = row0 + local) as they are, another rank's
+        // at NP + its position in the concatenated receive lists (ascending: the peers' ranges ascend)
+        std::vector<int32_t> hz(H.tile_halo);
+        if (nranks_ > 1) {
+            std::vector<int32_t> rr;
+            for (const auto &v : H.recv_rows) rr.insert(rr.end(), v.begin(), v.end());
+            for (auto &r : hz)
+                if (r < H.lo || r >= H.hi) {
+                    const auto itr = std::lower_bound(rr.begin(), rr.end(), r);
+                    if (itr == rr.end() || *itr != r) return fail(DEFTRI_E_ARG, "tile plan: a halo row is neither own nor received");
+                    r = NP + (int32_t)(itr - rr.begin());
+                }
+        }
+        PUT(tt, H.tile_tab); PUT(trs, H.tile_rs); PUT(th, hz); PUT(txo, H.tile_xoff); PUT(txd, H.tile_xdst);
         PUT(tch, H.tile_chunk);
         {
             std::vector<uint32_t> mm(2 * H.tile_m0.size());
@@ -453,7 +471,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         // last update takes the ticketed sum that records the state (DEFTRI_SP_TILE_TICKETS=1: every
         // update does, round 4's merged-chain scheme)
         static const bool tickets = std::getenv("DEFTRI_SP_TILE_TICKETS") != nullptr;
-        G.tparts = tickets ? 0 : 1;
+        G.tparts = (tickets || G.sd) ? 0 : 1;
+        if (G.sd) G.tile_fuse = 0;
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -554,7 +573,29 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         // phase-1 launch after the exchange (round 4)
         static const bool no_ovl = std::getenv("DEFTRI_SP_NO_OVERLAP") != nullptr;
         G.ovl = (nranks_ > 1 && !no_ovl) ? 1 : 0;
-        if (G.ovl) {
+        if (G.ovl && G.tile) {
+            // the tile chain: the workgroups of tiles that read no other rank's row (and the heavy
+            // one, and the empty slots) beside the exchange, the others after it
+            std::vector<int32_t> li, lb;
+            const int32_t seg = (H.ntile + 7) / 8;
+            for (int32_t b = 0; b < G.t_grid; b++) {
+                const int32_t t = b == G.t_grid - 1 ? H.ntile : (b & 7) * seg + (b >> 3);
+                bool bnd = false;
+                if (t < H.ntile) {
+                    const int32_t *T = &H.tile_tab[8 * (size_t)t];
+                    for (int32_t k = T[5]; k < T[5] + T[2] && !bnd; k++) bnd = H.tile_halo[k] < H.lo || H.tile_halo[k] >= H.hi;
+                }
+                (bnd ? lb : li).push_back(b);
+            }
+            n_p1int = (int)li.size();
+            n_p1bnd = (int)lb.size();
+            PUT(d_p1int, li);
+            if (lb.empty()) lb.push_back(0);
+            PUT(d_p1bnd, lb);
+            if (!cs_) SPOK(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+            if (!ev_upd_) SPOK(hipEventCreateWithFlags(&ev_upd_, hipEventDisableTiming));
+            if (!ev_halo_) SPOK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
+        } else if (G.ovl) {
             std::vector<int32_t> li, lb;
             for (int32_t e = 0; e < G.m_nx; e++) li.push_back(e);
             for (int32_t b = 0; b < G.nblk; b++) {
@@ -636,6 +677,17 @@ int SpSolver::halo_sd() {
 // already queued, the wait for the exchange, the boundary ones), phase 2
 int SpSolver::sd_product(int it, double lambda) {
     const bool f32 = fp32_jac != 0;
+    if (G.tile) {                                  // w = A z by tiles, the rank's record xb
+        if (!G.ovl) {
+            sp_launch_tile_sd(G, it, lambda, f32, st_, nullptr, G.t_grid, true);
+            return 0;
+        }
+        if (int_pending_ != it) sp_launch_tile_sd(G, it, lambda, f32, st_, d_p1int, n_p1int, false);
+        int_pending_ = -1;
+        SPOK(hipStreamWaitEvent(st_, ev_halo_, 0));
+        sp_launch_tile_sd(G, it, lambda, f32, st_, d_p1bnd, n_p1bnd, true);
+        return 0;
+    }
     if (!G.ovl) {
         sp_launch_sd_phase1(G, it, lambda, f32, st_, nullptr, sp_merged_grid1(G));
     } else {
@@ -654,7 +706,8 @@ int SpSolver::sd_product(int it, double lambda) {
 int SpSolver::sd_exchange(int next_it, double lambda) {
     if (!G.ovl) return halo_sd();
     SPOK(hipEventRecord(ev_upd_, st_));
-    sp_launch_sd_phase1(G, next_it, lambda, fp32_jac != 0, st_, d_p1int, n_p1int);
+    if (G.tile) sp_launch_tile_sd(G, next_it, lambda, fp32_jac != 0, st_, d_p1int, n_p1int, false);
+    else sp_launch_sd_phase1(G, next_it, lambda, fp32_jac != 0, st_, d_p1int, n_p1int);
     int_pending_ = next_it;
     return halo_sd();
 }
