@@ -268,6 +268,7 @@ struct SpDev {
     int32_t tile_fuse = 0;                                // tile mode: the update in the product's (cooperative) launch
     int32_t tglin = 0, tglin_lds = 0;                    // tile mode: the rows' ARAP blocks by tiles (k_sp_tglin)
     double *ht = nullptr;                                 // k_sp_tglin's per-row sums [9][nown] (H lower 6, b 3)
+    int32_t txb_fold = 0;                                 // sharded tiles: xb by k_sp_tile's last workgroup
     int32_t tparts = 0;                                   // tile mode: each k_sp_tile workgroup sums the update's
                                                           // (r.z, r.r) partials itself (no ticket chain in k_sp_tupd)
     // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the

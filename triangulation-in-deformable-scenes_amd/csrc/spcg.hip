@@ -1726,13 +1726,47 @@ __device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *
     return t;
 }
 
+// sharded tiles with G.txb_fold: every logical workgroup (over the interior and boundary launches of
+// one product) publishes its partials and draws a ticket; the last forms the rank's record xb as
+// k_sp_txb does (its own launch otherwise) and resets the counter
+__device__ __forceinline__ void tile_sd_tail(const SpDev &G, double *lds, double *red4) {
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);             // the published partials acknowledged
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        s_last = __hip_atomic_fetch_add(G.cnt + 48, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G.t_grid - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    for (int h = 0; h < G.Q + G.S; h++) {
+        const double t = tile_heavy_sum(G, h, lds, true);
+        if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) G.xb[3 + heavy_dof(G, h) + threadIdx.x] = t;
+        __syncthreads();
+    }
+    double a = 0.0;
+    for (int j = threadIdx.x; j < G.t_grid; j += 256) a += fetch(G.m1part + j);
+    a = block_sum(a, red4);
+    double a0 = 0.0, a1 = 0.0;
+    for (int j = threadIdx.x; j <= G.nrb; j += 256) { a0 += G.upart[2 * j]; a1 += G.upart[2 * j + 1]; }
+    a0 = block_sum(a0, red4);
+    a1 = block_sum(a1, red4);
+    if (threadIdx.x == 0) {
+        G.xb[0] = a0;
+        G.xb[1] = a1;
+        G.xb[2] = a;
+        st_sc1(G.cnt + 48, 0);
+    }
+}
+
 // FU 1 (opt-in, DEFTRI_SP_TILE_FUSE=1, when the grid is co-resident: a cooperative launch): the update follows in the
 // same launch — every workgroup publishes its sums, the last to arrive forms alpha (phase 2's
 // workgroup-0 arithmetic: the same partials, the same order) and publishes it, the others wait for it;
 // then each tile updates its own rows from the q it holds (+ its cross slots, written agent-coherent)
 // and the heavy workgroup the heavy dofs, and the (r.z, r.r) of iteration it + 1 are summed as in
 // k_sp_tupd.  One launch per CG iteration; no q stored.
-template <class JT, int FU>
+template <class JT, int FU, int SD = 0>
 __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     extern __shared__ double lds[];
     __shared__ double red[9][4];
@@ -1765,7 +1799,11 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         if (!G.include_heavy) pap = 0.0;
         if (!FU) {
             pap = block_sum(pap, red[0]);
-            if (tid == 0) G.m1part[b] = pap;
+            if (tid == 0) {
+                if (SD && G.txb_fold) publish(G, G.m1part + b, pap);
+                else G.m1part[b] = pap;
+            }
+            if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
             return;
         }
     }
@@ -1906,10 +1944,11 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     __syncthreads();
     if (tid < 9) {
         const double v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        if (FU) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
+        if (FU || (SD && G.txb_fold)) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
         else if (tid == 0) G.m1part[b] = v;
         else G.part[(int64_t)kSpPart * b + tid - 1] = v;
     }
+    if (!FU && SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
     if constexpr (FU == 1) {
         // the arrival: every thread's stores (cross slots, partials) acknowledged, then one ticket
         __shared__ int s_last;
@@ -2518,11 +2557,11 @@ void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStre
         SpDev g = G;
         g.p1list = list;
         hipEvent_t e0_ = prof_begin(st);
-        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja32, lambda);
-        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
         prof_end("sp_tile", e0_, (unsigned)n, 0.0, st);
     }
-    if (txb) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
+    if (txb && !G.txb_fold) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
 }
 
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {

@@ -473,6 +473,11 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         static const bool tickets = std::getenv("DEFTRI_SP_TILE_TICKETS") != nullptr;
         G.tparts = (tickets || G.sd) ? 0 : 1;
         if (G.sd) G.tile_fuse = 0;
+        // sharded: the rank's record xb in its own small launch (k_sp_txb); DEFTRI_SP_TXB_FOLD=1 forms
+        // it in the product's last workgroup instead (a ticket over both product launches) — the
+        // same on the 2-rank gloo rehearsal (165.8 vs 171.8 LM it/s), so the simpler order stays
+        static const bool txb_fold = std::getenv("DEFTRI_SP_TXB_FOLD") != nullptr;
+        G.txb_fold = (G.sd && txb_fold) ? 1 : 0;
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -488,8 +493,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         const char *e = std::getenv("DEFTRI_SP_P2_TRACE_IT");
         G.p2tr_it = e ? std::atoi(e) : 2;
     }
-    ALLOC(G.cnt, 48);                                      // three ticket sites (0, 16, 32: 9 counters each), the tile arrival (44)
-    SPOK(hipMemset(G.cnt, 0, 48 * sizeof(int)));
+    ALLOC(G.cnt, 64);      // three ticket sites (0, 16, 32: 9 counters each), the tile arrival (44), the sharded tiles' (48)
+    SPOK(hipMemset(G.cnt, 0, 64 * sizeof(int)));
     {
         // heavy linearization chunks (k_sp_glin_heavy): kSpHeavyChunk block partials each, >= 1 per vertex
         std::vector<int32_t> chh, hcho(Q + S + 1, 0);
