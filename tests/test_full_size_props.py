@@ -76,6 +76,20 @@ def test_c2_full_size_properties():
     print("C2", r["trials_iter"], solves)
 
 
+def test_north_star_500k_properties():
+    """The north-star size (500k correspondences x 2 views, 3,000,008 unknowns: bench.py's
+    north_star_500k leg) on the tile chain — the largest tile plan: monotone accepted chi2, a
+    bit-identical repeat, damped solves to a backward error < 1e-12."""
+    p = sim.two_view_problem(500000, 1)
+    assert p.n_unknowns == 3000008
+    with capi.Context(0) as ctx:
+        ctx.set_plan("auto")
+        ctx.upload(p)
+        assert ctx.plan_info()["tiles"] > 0
+    r, solves = check_props(p, 3, (1e-5,))
+    print("500k", r["trials_iter"], solves)
+
+
 def test_c3_shape_full_size_properties():
     p = c3_problem()
     assert p.n_pairs == 28 and p.n_unknowns == 1200224
