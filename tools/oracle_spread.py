@@ -1,0 +1,32 @@
+"""The oracle's own spread on a regime golden: the same LM run with other elimination orders of the
+exact LDL^T step (the oracle's own nested dissection), chi2 per iteration against the committed golden
+(which eliminates in the host analysis' nested-dissection order).  Test infrastructure only.
+
+usage: python tools/oracle_spread.py NAME [SUB]"""
+import json
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tests" / "golden"))
+sys.path.insert(0, str(ROOT / "triangulation-in-deformable-scenes_amd"))
+sys.path.insert(0, str(ROOT))
+from make_regime_goldens import scene, N_IT   # noqa: E402
+from oracle import oracle                      # noqa: E402
+
+name, sub = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "regimes")
+d = ROOT / "tests" / "golden" / sub
+meta = json.loads((d / f"{name}.json").read_text())
+z = np.load(d / f"{name}.npz")
+p, m, host = scene(name, meta["n_corr"], meta["seed"])
+host.analyse(p)
+for label, order in (("oracle_nd", None),):
+    oracle.set_vertex_order(order)
+    r = oracle.solve_lm(p, N_IT, analytic=False)["report"]
+    oracle.set_vertex_order(None)
+    a, b = np.array(r["chi2_iter"]), np.array(z["chi2_iter"])
+    rel = np.abs(a - b) / np.abs(b)
+    print(json.dumps({"order": label, "max_rel": float(rel.max()), "at": int(rel.argmax()),
+                      "trials_same": list(r["trials_iter"]) == list(z["trials_iter"])}), flush=True)

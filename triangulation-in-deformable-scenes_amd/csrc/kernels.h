@@ -192,6 +192,45 @@ struct ReadBack {
 void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st);
 // the errors and chi2 of all edges (launch_linearize without Jacobians) in one launch
 void launch_lin_chi(const DevProblem &P, hipStream_t st);
+// a trial's evaluation in one launch (launch_lin_chi + launch_sum_multi_fused without the per-edge
+// chi2 arrays): each workgroup sums the chi2 of a run of reprojection / depth / owned ARAP edges,
+// or a run of dx.(lambda dx + b), into its partial; the last workgroup (ticket) adds each kind's
+// partials in order into out[0..2] (rep, dep, arap), den_out and total = (rep + arap) + dep, then
+// the read-back.  The sums' order is this launch's own: every caller of the trial's evaluation
+// uses it.  *cnt zero between launches.
+struct EvalJob {
+    int64_t n_arap = 0;                          // the edges whose chi2 is summed (the owned ones)
+    const double *dx = nullptr, *b = nullptr;    // n_den > 0: den_out = sum dx (lambda dx + b)
+    int64_t n_den = 0;
+    double lambda = 0;
+    const double *lambda_dev = nullptr;          // replaces lambda (the device-driven LM)
+    double *out = nullptr, *den_out = nullptr, *total = nullptr;
+    const int *gate = nullptr;
+    // set: each workgroup stores its partial into this pinned host array and workgroup 0 does the
+    // read-back's record / flag copies; no ticket, no device sums — the host finishes the sums after
+    // its stream synchronization (trial_eval_host_sums, the last workgroup's order)
+    double *h_part = nullptr;
+    // with h_part: after its read-back copies, workgroup 0 clears the solve records (nclear doubles) and
+    // the flag — k_trial_begin's clears, for the next trial — when the record's status word is final
+    // (a running solve is continued by the host and keeps its records)
+    double *rec_clear = nullptr;
+    int64_t nclear = 0;
+    int *flag_clear = nullptr;
+};
+// the trial's state update with k_trial_begin's backup folded in: base = the backup (restore: after a
+// rejected trial, or a second evaluation of the same trial) or the current state; backup = base (not
+// restore); state = base + dx (k_update_state's arithmetic)
+void launch_update_state_bak(const DevProblem &P, const double *dx, bool restore, hipStream_t st);
+// the workgroup counts of the four kinds (rep, dep, arap, den) of a trial evaluation
+void trial_eval_blocks(const DevProblem &P, const EvalJob &J, int nb[4]);
+// the four sums from the host partials, in the device's final order (per kind: lane l adds partials
+// l, l + 64, ... in order, then the xor butterfly 32 .. 1; lane 0's value)
+void trial_eval_host_sums(const double *h_part, const int nb[4], double out[4]);
+// edges per thread of a trial evaluation's workgroup (DEFTRI_EVAL_EPT, 1..8; default 2)
+int eval_edges_per_thread();
+// the partial slots launch_trial_eval needs (part's length)
+int64_t trial_eval_parts(const DevProblem &P, const EvalJob &J);
+void launch_trial_eval(const DevProblem &P, const EvalJob &J, double *part, int *cnt, const ReadBack &rb, hipStream_t st);
 void launch_pack_cb(const DevPlan &L, int64_t arena_off, int m, int s, double *buf, hipStream_t st);
 void launch_ea_packed(const DevPlan &L, int64_t ea_off, int nea, const double *buf, hipStream_t st);
 void launch_gather_idx(int n, const int32_t *idx, const double *src, double *dst, hipStream_t st);

@@ -41,13 +41,13 @@ __device__ __forceinline__ void huber_rho(double delta, double e2, double &rho0,
     else { double se = sqrt(e2); rho0 = 2 * se * delta - dsqr; rho1 = delta / se; }
 }
 
-__device__ __forceinline__ void lin_rep_edge(int e, int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
+__device__ __forceinline__ double lin_rep_edge(int e, int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
                           const double *__restrict__ obs, const double *__restrict__ info, double hdelta,
                           const double *__restrict__ points, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, const float *__restrict__ kb8,
                           double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
                           double *__restrict__ chi, int want_jac) {
-    if (e >= R) return;
+    if (e >= R) return 0.0;
     int c = rc[e];
     const double *pp = points + 3 * (int64_t)rp[e];
     double p[3] = {pp[0], pp[1], pp[2]}, pc[3];
@@ -60,8 +60,8 @@ __device__ __forceinline__ void lin_rep_edge(int e, int R, const int32_t *__rest
     double c2 = e0 * (om * e0) + e1 * (om * e1);
     double rho0, rho1;
     huber_rho(hdelta, c2, rho0, rho1);
-    chi[e] = rho0;
-    if (!want_jac) return;
+    if (chi) chi[e] = rho0;
+    if (!want_jac) return rho0;
     float jf[6];
     kb8_project_jac(kb8 + 8 * c, pf, jf);
     const double *Rm = cam_R + 9 * c;
@@ -74,6 +74,7 @@ __device__ __forceinline__ void lin_rep_edge(int e, int R, const int32_t *__rest
     W[e] = rho1 * om;
     E[2 * (int64_t)e] = e0;
     E[2 * (int64_t)e + 1] = e1;
+    return rho0;
 }
 
 __device__ __forceinline__ double depth_err(const SE3 &T, const double p[3], double meas, double s) {
@@ -85,13 +86,13 @@ __device__ __forceinline__ double depth_err(const SE3 &T, const double p[3], dou
     return error;
 }
 
-__device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
+__device__ __forceinline__ double lin_dep_edge(int e, int D, const int32_t *__restrict__ dpt, const int32_t *__restrict__ dsc,
                           const int32_t *__restrict__ dcam, const double *__restrict__ meas,
                           const double *__restrict__ info, const double *__restrict__ points,
                           const double *__restrict__ scales, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
-    if (e >= D) return;
+    if (e >= D) return 0.0;
     int c = dcam[e];
     const double *pp = points + 3 * (int64_t)dpt[e];
     double p[3] = {pp[0], pp[1], pp[2]};
@@ -99,8 +100,9 @@ __device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__rest
     SE3 T = se3_load(cam_pose + 7 * c);
     double err = depth_err(T, p, mv, s);
     double om = info[e];
-    chi[e] = err * (om * err);
-    if (!want_jac) return;
+    const double c2 = err * (om * err);
+    if (chi) chi[e] = c2;
+    if (!want_jac) return c2;
     double Jv[4];
     if (analytic) {
         double pc[3];
@@ -124,6 +126,7 @@ __device__ __forceinline__ void lin_dep_edge(int e, int D, const int32_t *__rest
     for (int k = 0; k < 4; k++) J[4 * (int64_t)e + k] = Jv[k];
     W[e] = om;
     E[e] = err;
+    return c2;
 }
 
 // x / area by the pair's reciprocal: q0 = x RN(1/area), the residual x - q0 area exact by FMA, one
@@ -316,7 +319,7 @@ __global__ void k_arap_pre(int Q, const double *__restrict__ tg, double *__restr
 // MODE 0: error and chi2 only; 1: + analytic Jacobian; 2: + g2o numeric Jacobian, pieces reused; 3: the
 // same, every evaluation in full (one kernel per mode: each gets the registers of its own path)
 template <int MODE>
-__device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
+__device__ __forceinline__ double lin_arap_edge(int e, int E_, const int32_t *__restrict__ apts, const int32_t *__restrict__ apair,
                            const int32_t *__restrict__ arot, const double *__restrict__ aw,
                            const double *__restrict__ rot, const double *__restrict__ parea,
                            const double *__restrict__ pinfo, const double *__restrict__ points,
@@ -324,7 +327,7 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
                            double *__restrict__ J, double *__restrict__ W,
                            double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
                            int64_t jld) {
-    if (e >= E_) return;
+    if (e >= E_) return 0.0;
     const int32_t *v = apts + 4 * (int64_t)e;
     double P[4][3];
 #pragma unroll
@@ -339,8 +342,9 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
     double w = aw[e], om = pinfo[q];
     const AreaDiv area = area_div(parea[q]);
     double err = arap_err(P[0], P[1], P[2], P[3], T, Ri, Rj, w, area);
-    chi[e] = err * (om * err);
-    if (MODE == 0) return;
+    const double c2 = err * (om * err);
+    if (chi) chi[e] = c2;
+    if (MODE == 0) return c2;
     double Jv[18];
     if (MODE == 1) {
         double Rg[9];
@@ -503,6 +507,7 @@ __device__ __forceinline__ void lin_arap_edge(int e, int E_, const int32_t *__re
     }
     W[e] = om;
     E[e] = err;
+    return c2;
 }
 
 __global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
@@ -572,6 +577,104 @@ __global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, in
         lin_arap_edge<0>((b - nbr - nbd) * 128 + t, P.E, P.arap_pts, P.arap_pair, P.arap_rot, P.arap_w, P.rot,
                          P.pair_area, P.pair_info, P.points, P.tg, nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, 0, 0,
                          P.jarap_ld);
+}
+
+// a trial's evaluation (kernels.h EvalJob): workgroups [0, nbr) reprojection edges, then nbd depth,
+// nba owned ARAP edges, then runs of dx.(lambda dx + b); each a run of 256 ept, thread t taking
+// entries t, t + 256, ... of it in order.  The per-edge arithmetic is k_lin_chi's; no per-edge chi2
+// is stored.
+__global__ void __launch_bounds__(256) k_trial_eval(const DevProblem P, const EvalJob J, int ept, int nbr, int nbd, int nba,
+                                                   double *__restrict__ part, int *cnt, int flat, const ReadBack rb) {
+    if (J.gate && !*J.gate) return;
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int64_t run = 256 * (int64_t)ept;
+    double acc = 0.0;
+    if (b < nbr) {
+        const int64_t e0 = b * run + t;
+        for (int u = 0; u < ept; u++)
+            acc += lin_rep_edge((int)(e0 + 256 * u), P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points,
+                                P.cam_pose, P.cam_R, P.cam_kb8, nullptr, nullptr, nullptr, nullptr, 0);
+    } else if (b < nbr + nbd) {
+        const int64_t e0 = (b - nbr) * run + t;
+        for (int u = 0; u < ept; u++)
+            acc += lin_dep_edge((int)(e0 + 256 * u), P.D, P.dep_point, P.dep_scale, P.dep_cam, P.dep_meas, P.dep_info, P.points,
+                                P.scales, P.cam_pose, P.cam_R, nullptr, nullptr, nullptr, nullptr, 0, 0);
+    } else if (b < nbr + nbd + nba) {
+        const int64_t e0 = (b - nbr - nbd) * run + t;
+        for (int u = 0; u < ept; u++)
+            acc += lin_arap_edge<0>((int)(e0 + 256 * u), (int)J.n_arap, P.arap_pts, P.arap_pair, P.arap_rot, P.arap_w, P.rot,
+                                    P.pair_area, P.pair_info, P.points, P.tg, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
+                                    P.jarap_ld);
+    } else {
+        const double lam = J.lambda_dev ? *J.lambda_dev : J.lambda;
+        const int64_t i0 = (b - nbr - nbd - nba) * run + t;
+        for (int u = 0; u < ept; u++) {
+            const int64_t i = i0 + 256 * u;
+            if (i < J.n_den) {
+                const double v = J.dx[i];
+                acc += v * (lam * v + J.b[i]);
+            }
+        }
+    }
+    // the workgroup's partial: a butterfly per wave, then the four waves
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    __shared__ double red[4], s[4];
+    __shared__ int last;
+    const int w = t >> 6, lane = t & 63;
+    if (lane == 0) red[w] = acc;
+    __syncthreads();
+    if (J.h_part) {                                // the host finishes the sums: no ticket
+        if (t == 0) J.h_part[b] = (red[0] + red[1]) + (red[2] + red[3]);
+        if (b == 0 && rb.h_rec) {
+            const bool final_st = J.rec_clear && rb.rec[0] != 0.0;
+            if (t < rb.nrec) rb.h_rec[t] = rb.rec[t];
+            if (t == 0) *rb.h_flag = *rb.flag;
+            __syncthreads();                       // (every read of the record done)
+            if (final_st) {
+                for (int64_t i = t; i < J.nclear; i += 256) J.rec_clear[i] = 0.0;
+                if (t == 0) *J.flag_clear = 0;
+            }
+        }
+        return;
+    }
+    if (t == 0) {
+        st_sc1(part + b, (red[0] + red[1]) + (red[2] + red[3]));
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        last = ticket_last(cnt, (int)gridDim.x, b, flat != 0);
+    }
+    __syncthreads();
+    if (!last) return;
+    // wave w adds kind w's partials: lane-strided, eight loads in flight, added in order; a butterfly
+    const int lo = w == 0 ? 0 : w == 1 ? nbr : w == 2 ? nbr + nbd : nbr + nbd + nba;
+    const int hi = w == 0 ? nbr : w == 1 ? nbr + nbd : w == 2 ? nbr + nbd + nba : (int)gridDim.x;
+    double a = 0.0;
+    int i = lo + lane;
+    for (; i + 7 * 64 < hi; i += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = ld_sc1(part + i + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 8; u++) a += v[u];
+    }
+    for (; i < hi; i += 64) a += ld_sc1(part + i);
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+    if (lane == 0) s[w] = a;
+    __syncthreads();
+    if (t == 0) {
+        J.out[0] = s[0];
+        J.out[1] = s[1];
+        J.out[2] = s[2];
+        if (J.den_out) *J.den_out = s[3];
+        if (J.total) *J.total = (s[0] + s[2]) + s[1];
+    }
+    __syncthreads();
+    if (rb.h_scal) {
+        if (t < rb.ns) rb.h_scal[t] = rb.scal[t];
+        if (t == 0) *rb.h_flag = *rb.flag;
+        if (rb.rec && t < rb.nrec) rb.h_rec[t] = rb.rec[t];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1658,6 +1761,38 @@ __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ d
     }
 }
 
+__global__ void k_update_state_bak(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
+                                   double *__restrict__ scales, double *__restrict__ tg, double *__restrict__ pb,
+                                   double *__restrict__ sb, double *__restrict__ tb, int restore) {
+    const int i = TID;
+    const int64_t pbase = 6 * (int64_t)Q + S;
+    if (i < P) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const int64_t k = 3 * (int64_t)i + c;
+            const double base = restore ? pb[k] : points[k];
+            if (!restore) pb[k] = base;
+            points[k] = base + dx[pbase + k];
+        }
+    }
+    if (i < S) {
+        const double base = restore ? sb[i] : scales[i];
+        if (!restore) sb[i] = base;
+        scales[i] = base + dx[6 * (int64_t)Q + i];
+    }
+    if (i < Q) {
+        double u[6];
+        for (int k = 0; k < 6; k++) u[k] = dx[6 * (int64_t)i + k];
+        double *src = restore ? tb + 7 * i : tg + 7 * i;
+        SE3 T = se3_load(src);
+        if (!restore)
+            for (int k = 0; k < 7; k++) tb[7 * i + k] = tg[7 * i + k];
+        SE3 Ex = se3_exp(u);
+        SE3 Tn = se3_mul(Ex, T);
+        se3_store(Tn, tg + 7 * i);
+    }
+}
+
 // a trial's prologue in one launch: the state backup (push_state's three copies) — or, after a
 // rejected trial, its restore from the backup (pop_state's) — the zero-pivot flag and the PCG records
 // cleared (two fills); grid-stride over the longest of them
@@ -2356,6 +2491,14 @@ void launch_update_state(const DevProblem &P, const double *dx, hipStream_t st, 
                            P.scales, P.tg, flag, P.gate_trial);
 }
 
+void launch_update_state_bak(const DevProblem &P, const double *dx, bool restore, hipStream_t st) {
+    int n = P.P > P.S ? P.P : P.S;
+    if (P.Q > n) n = P.Q;
+    if (n > 0)
+        LAUNCH("update_state", dev::k_update_state_bak, dim3(nb(n, 128)), dim3(128), st, P.P, P.S, P.Q, dx, P.points,
+               P.scales, P.tg, P.points_bak, P.scales_bak, P.tg_bak, restore ? 1 : 0);
+}
+
 void launch_trial_begin(const DevProblem &P, int *flag, double *zero, int64_t nzero, hipStream_t st, bool restore) {
     int64_t n = std::max<int64_t>(std::max<int64_t>(3 * (int64_t)P.P, 7 * (int64_t)P.Q), std::max<int64_t>(P.S, nzero));
     n = std::max<int64_t>(n, 1);
@@ -2399,6 +2542,56 @@ void launch_lin_chi(const DevProblem &P, hipStream_t st) {
     const int nbr = P.R > 0 ? (int)nb(P.R, 128) : 0, nbd = P.D > 0 ? (int)nb(P.D, 128) : 0;
     const int nba = P.E > 0 ? (int)nb(P.E, 128) : 0;
     if (nbr + nbd + nba > 0) LAUNCH("lin_chi", dev::k_lin_chi, dim3(nbr + nbd + nba), dim3(128), st, P, nbr, nbd);
+}
+
+int eval_edges_per_thread() {
+    static const int v = std::getenv("DEFTRI_EVAL_EPT") ? std::max(1, std::min(8, std::atoi(std::getenv("DEFTRI_EVAL_EPT")))) : 2;
+    return v;
+}
+
+static void eval_blocks(const DevProblem &P, const EvalJob &J, int &nbr, int &nbd, int &nba, int &nbx) {
+    const int64_t run = 256 * (int64_t)eval_edges_per_thread();
+    nbr = P.R > 0 ? (int)((P.R + run - 1) / run) : 0;
+    nbd = P.D > 0 ? (int)((P.D + run - 1) / run) : 0;
+    nba = J.n_arap > 0 ? (int)((J.n_arap + run - 1) / run) : 0;
+    nbx = J.n_den > 0 ? (int)((J.n_den + run - 1) / run) : 0;
+}
+
+void trial_eval_blocks(const DevProblem &P, const EvalJob &J, int nb[4]) { eval_blocks(P, J, nb[0], nb[1], nb[2], nb[3]); }
+
+void trial_eval_host_sums(const double *h_part, const int nb[4], double out[4]) {
+    int lo = 0;
+    for (int k = 0; k < 4; k++) {
+        const int hi = lo + nb[k];
+        double v[64];
+        for (int l = 0; l < 64; l++) {
+            double a = 0.0;
+            for (int i = lo + l; i < hi; i += 64) a += h_part[i];
+            v[l] = a;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            double u[64];
+            for (int l = 0; l < 64; l++) u[l] = v[l] + v[l ^ off];
+            for (int l = 0; l < 64; l++) v[l] = u[l];
+        }
+        out[k] = v[0];
+        lo = hi;
+    }
+}
+
+int64_t trial_eval_parts(const DevProblem &P, const EvalJob &J) {
+    int nbr, nbd, nba, nbx;
+    eval_blocks(P, J, nbr, nbd, nba, nbx);
+    return std::max<int64_t>(1, (int64_t)nbr + nbd + nba + nbx);
+}
+
+void launch_trial_eval(const DevProblem &P, const EvalJob &J, double *part, int *cnt, const ReadBack &rb, hipStream_t st) {
+    int nbr, nbd, nba, nbx;
+    eval_blocks(P, J, nbr, nbd, nba, nbx);
+    // an empty problem still runs one workgroup: the sums are written (0) and the read-back done
+    const int grid = std::max(1, nbr + nbd + nba + nbx);
+    LAUNCH("trial_eval", dev::k_trial_eval, dim3(grid), dim3(256), st, P, J, eval_edges_per_thread(), nbr, nbd, nba, part,
+           cnt, flat_ticket() ? 1 : 0, rb);
 }
 
 void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st) {

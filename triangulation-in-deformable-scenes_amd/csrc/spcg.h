@@ -391,7 +391,11 @@ class SpSolver {
     int save_entry();
     double *d_scal = nullptr, *d_part = nullptr, *d_dx0 = nullptr, *d_tmp = nullptr;
     int *d_flag = nullptr;
-    int *d_sumcnt = nullptr;           // launch_sum_multi_fused's ticket
+    int *d_sumcnt = nullptr;           // launch_sum_multi_fused's / launch_trial_eval's ticket
+    double *d_epart = nullptr;         // launch_trial_eval's partials
+    int64_t n_epart_ = 0;
+    double *h_epart_ = nullptr;        // pinned: the partials of a host-finished trial evaluation
+    int eval_nb_[4] = {0, 0, 0, 0};    // its workgroups per kind (trial_eval_blocks)
     double *hpin = nullptr;
     int *ipin = nullptr;
     int32_t *d_send_rows = nullptr, *d_recv_rows = nullptr;
@@ -408,7 +412,8 @@ class SpSolver {
     int hand_off_timeout();
     int budget() const;
     int lin_iteration(bool analytic, bool want_max, bool &ok);
-    int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr);
+    int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr, double *h_part = nullptr,
+                  double *rec_clear = nullptr, int64_t nclear = 0);
     int cg_setup(double lambda, const double *rhs);
     int cg_chain(double lambda, int from, int to);
     int cg_tail(int n, double lambda);

@@ -38,6 +38,13 @@ constexpr int kSpMaxIt = 4096;
 constexpr int kSpDefaultIt = 1000;
 constexpr int kSpRedParts = 512;
 constexpr int kSpRecDoubles = 8;
+// the host LM's trial evaluation finishes its sums on the host (DEFTRI_EVAL_DEVICE_SUMS=1: the
+// evaluation's last workgroup; DEFTRI_EVAL_SPLIT=1: round 5's two launches)
+bool eval_host_sums() {
+    static const bool v = std::getenv("DEFTRI_EVAL_DEVICE_SUMS") == nullptr && std::getenv("DEFTRI_EVAL_SPLIT") == nullptr;
+    return v;
+}
+
 // workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
 // chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
 int sum_parts() {
@@ -89,6 +96,7 @@ SpSolver::~SpSolver() {
     if (ev_halo_) hipEventDestroy(ev_halo_);
     for (void *p : allocs_) hipFree(p);
     if (hpin) hipHostFree(hpin);
+    if (h_epart_) hipHostFree(h_epart_);
     if (ipin) hipHostFree(ipin);
     if (h_snap) hipHostFree(h_snap);
 }
@@ -524,6 +532,16 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     SPOK(hipMemset(G.zp, 0, sizeof(double) * 2 * (size_t)zp_n));
     SPOK(hipMemset(G.rec, 0, sizeof(double) * (size_t)(kSpRecDoubles + kSpRed * (kSpMaxIt + 2))));
     ALLOC(d_scal, 8); ALLOC(d_part, kMaxSumJobs * kSpRedParts); ALLOC(d_flag, 1); ALLOC(d_sumcnt, 16);
+    {                                  // the trial evaluation's partials: every edge kind and the whole dx
+        EvalJob ej;
+        ej.n_arap = H.n_arap_owned;
+        ej.n_den = G.ndof;
+        n_epart_ = trial_eval_parts(P, ej);
+        ALLOC(d_epart, n_epart_);
+        if (h_epart_) hipHostFree(h_epart_);
+        h_epart_ = nullptr;
+        SPOK(hipHostMalloc((void **)&h_epart_, sizeof(double) * (size_t)n_epart_, hipHostMallocDefault));
+    }
     SPOK(hipMemset(d_flag, 0, sizeof(int)));
     SPOK(hipMemset(d_sumcnt, 0, 16 * sizeof(int)));
     ALLOC(d_tmp, G.ndof); ALLOC(d_dx0, G.ndof);
@@ -719,17 +737,39 @@ int SpSolver::sd_exchange(int next_it, double lambda) {
 
 // computeActiveErrors (+ linearizeOplus with jac) on the rank's edges, chi2 of its owned edges into
 // d_scal[slot]; `extra`: one more fixed-order sum in the same launches (the rho denominator)
-int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb) {
+int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb, double *h_part,
+                        double *rec_clear, int64_t nclear) {
     (void)analytic;                  // errors only: the Jacobian mode does not enter
-    launch_lin_chi(P, st_);          // k_lin_rep / k_lin_dep / k_lin_arap<0> in one launch
-    SumJobs J;
-    J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
-    J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
-    J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
-    J.nj = 3;
-    if (extra) J.j[J.nj++] = *extra;
+    static const bool split = std::getenv("DEFTRI_EVAL_SPLIT") != nullptr;
+    if (split) {                     // A/B: round 5's two launches (k_lin_chi, then the fixed-order sums)
+        launch_lin_chi(P, st_);
+        SumJobs S;
+        S.j[0].n = P.R; S.j[0].a = P.chi_rep; S.j[0].out = d_scal + 4;
+        S.j[1].n = P.D; S.j[1].a = P.chi_dep; S.j[1].out = d_scal + 5;
+        S.j[2].n = H.n_arap_owned; S.j[2].a = P.chi_arap; S.j[2].out = d_scal + 6;
+        S.nj = 3;
+        if (extra) S.j[S.nj++] = *extra;
+        S.total = d_scal + slot;
+        S.gate = P.gate_trial;
+        launch_sum_multi_fused(S, d_part, sum_parts(), d_sumcnt, rb ? *rb : ReadBack{}, st_);
+        return 0;
+    }
+    // the edges' errors and every sum in one launch (k_trial_eval)
+    EvalJob J;
+    J.n_arap = H.n_arap_owned;
+    J.out = d_scal + 4;
+    if (extra) {
+        if (extra->mode != 1) return fail(DEFTRI_E_ARG, "trial evaluation: the extra sum must be dx.(lambda dx + b)");
+        J.dx = extra->a; J.b = extra->b; J.n_den = extra->n;
+        J.lambda = extra->lambda; J.lambda_dev = extra->lambda_dev; J.den_out = extra->out;
+    }
     J.total = d_scal + slot;
-    launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, rb ? *rb : ReadBack{}, st_);
+    J.gate = P.gate_trial;
+    J.h_part = h_part;
+    if (h_part && rec_clear) { J.rec_clear = rec_clear; J.nclear = nclear; J.flag_clear = d_flag; }
+    trial_eval_blocks(P, J, eval_nb_);
+    if (trial_eval_parts(P, J) > n_epart_) return fail(DEFTRI_E_ARG, "trial evaluation: partial buffer too small");
+    launch_trial_eval(P, J, d_epart, d_sumcnt, rb ? *rb : ReadBack{}, st_);
     return 0;
 }
 
@@ -914,17 +954,10 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
     // the evaluation of a slot's step: state update, chi2 + the rho denominator (lambda from HBM)
     auto evaluate = [&]() {
         launch_update_state(P, G.x, st_, nullptr);
-        launch_lin_chi(P, st_);
-        SumJobs J;
-        J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
-        J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
-        J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
-        J.j[3].n = G.hd + 3 * (int64_t)G.nown; J.j[3].a = G.x; J.j[3].b = G.b; J.j[3].lambda_dev = &d_lm->lam;
-        J.j[3].mode = 1; J.j[3].out = d_scal + 1;
-        J.nj = 4;
-        J.total = d_scal;
-        J.gate = &d_lm->gate_trial;
-        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+        SumJob den;
+        den.n = G.hd + 3 * (int64_t)G.nown; den.a = G.x; den.b = G.b; den.lambda_dev = &d_lm->lam;
+        den.mode = 1; den.out = d_scal + 1;
+        return eval_chi2(analytic, 0, &den);     // gated by P.gate_trial (= the LM state's gate_trial)
     };
     struct Slot { int idx, n; hipEvent_t ev; };
     std::vector<hipEvent_t> evpool;
@@ -955,7 +988,7 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
         const int n = std::min(guess, mx);
         if ((r2 = cg_chain(0.0, 0, n))) return r2;
         if ((r2 = cg_tail(n, 0.0))) return r2;
-        evaluate();
+        if ((r2 = evaluate())) return r2;
         launch_lm_decide(d_lm, d_scal, G.rec, d_chi_it, d_trials_it, DEFTRI_MAX_REPORT_ITERS, h_snap, queued, st_);
         if (evpool.empty()) { hipEvent_t e; SPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming)); evpool.push_back(e); }
         hipEvent_t e = evpool.back();
@@ -1015,7 +1048,7 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
                 SPOK(hipMemcpyAsync(G.rec, rec_budget, sizeof(rec_budget), hipMemcpyHostToDevice, st_));
             }
             if (j > 0) guess = std::max(guess, std::min(j + 2, mx));
-            evaluate();
+            if ((rc = evaluate())) return rc;
             launch_lm_decide(d_lm, d_scal, G.rec, d_chi_it, d_trials_it, DEFTRI_MAX_REPORT_ITERS, h_snap, -1, st_);
             SPOK(hipStreamSynchronize(st_));
             const LmState S2 = *h_snap;
@@ -1106,6 +1139,17 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     const int64_t den_off = rank_ == 0 ? 0 : G.hd + 3 * (int64_t)G.row0;
     const int64_t den_n = rank_ == 0 ? G.hd + 3 * (int64_t)G.nown : 3 * (int64_t)G.nown;
     double t_lin = 0;
+    // the trial's sums finished on the host (DEFTRI_EVAL_DEVICE_SUMS=1: by the evaluation's last workgroup)
+    const bool host_sums = eval_host_sums();
+    bool sums_pending = false;
+    // one rank, host sums: k_trial_begin folded away — the backup into the trial's state update, the
+    // records' clear into the evaluation (DEFTRI_TRIAL_BEGIN=1: the prologue launch)
+    static const bool fold_env = std::getenv("DEFTRI_TRIAL_BEGIN") == nullptr;
+    const bool fold = fold_env && host_sums && !dist;
+    if (fold) {                                   // the first trial's records start clear
+        SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)nrec, st_));
+        SPOK(hipMemsetAsync(d_flag, 0, sizeof(int), st_));
+    }
     for (it = 0; it < prm.n_iterations; it++) {
         auto t0 = std::chrono::steady_clock::now();
         bool ok;
@@ -1127,7 +1171,8 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
         do {
             G.max_it = mx;
             G.tol2 = tol * tol;
-            launch_trial_begin(P, d_flag, G.rec, nrec, st_, restore_pending);
+            if (!fold) launch_trial_begin(P, d_flag, G.rec, nrec, st_, restore_pending);
+            bool base_in_bak = restore_pending;   // (fold: the state update reads the backup)
             restore_pending = false;
             double *sc = hpin + 4;
             // update (x, halo rows from their owners), chi2 of the owned edges, the rank's share of
@@ -1135,10 +1180,22 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             auto evaluate = [&]() -> int {
                 int r2;
                 if (dist && (r2 = halo(3, G.x, false))) return r2;
-                launch_update_state(P, G.x, st_, nullptr);
+                if (fold) {
+                    launch_update_state_bak(P, G.x, base_in_bak, st_);
+                    base_in_bak = true;                // a second evaluation starts from the backup
+                } else {
+                    launch_update_state(P, G.x, st_, nullptr);
+                }
                 SumJob den;
                 den.n = den_n; den.a = G.x + den_off; den.b = G.b + den_off; den.lambda = lambda; den.mode = 1;
                 den.out = d_scal + 1;
+                if (!dist && host_sums) {   // workgroup partials to the host, which finishes the sums
+                    ReadBack rb;
+                    rb.flag = d_flag; rb.rec = G.rec; rb.nrec = kSpRecDoubles; rb.h_flag = ipin; rb.h_rec = hpin + 16;
+                    eval_chi2(analytic, 0, &den, &rb, h_epart_, fold ? G.rec : nullptr, nrec);
+                    sums_pending = true;
+                    return 0;
+                }
                 if (!dist) {         // the read-back rides the sums' last workgroup
                     ReadBack rb;
                     rb.scal = d_scal; rb.ns = 2; rb.flag = d_flag; rb.rec = G.rec; rb.nrec = kSpRecDoubles;
@@ -1150,6 +1207,15 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 if ((r2 = tr_->allreduce(d_scal, 2, 0, st_))) return r2;
                 launch_trial_readback(d_scal, 2, d_flag, G.rec, kSpRecDoubles, sc, ipin, hpin + 16, st_);
                 return 0;
+            };
+            // after the stream synchronization that follows an evaluation: its sums, if the host finishes them
+            auto finish_sums = [&]() {
+                if (!sums_pending) return;
+                double s4[4];
+                trial_eval_host_sums(h_epart_, eval_nb_, s4);
+                sc[0] = (s4[0] + s4[2]) + s4[1];
+                sc[1] = s4[3];
+                sums_pending = false;
             };
             auto t0p = std::chrono::steady_clock::now();
             if ((rc = cg_setup(lambda, G.b))) return rc;
@@ -1165,6 +1231,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             if ((rc = cg_tail(j, lambda))) return rc;
             if ((rc = evaluate())) return rc;
             SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
+            finish_sums();
             if (chi_pending) { currentChi = chis[0]; chi_pending = false; }
             int st = (int)hpin[16];
             if (st == kSpTimeout) return hand_off_timeout();
@@ -1188,9 +1255,14 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 if (st == kSpTimeout) return hand_off_timeout();
                 solved = st == kSpConverged;
                 its = solved ? (int)hpin[17] : j;
+                if (fold && !solved) {                 // no evaluation clears this solve's records
+                    SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)nrec, st_));
+                    SPOK(hipMemsetAsync(d_flag, 0, sizeof(int), st_));
+                }
                 if (solved) {
                     if ((rc = evaluate())) return rc;
                     SPOK(hipStreamSynchronize(st_));
+                    finish_sums();
                     evaluated = true;
                 }
             }
@@ -1402,6 +1474,12 @@ int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
     rc = cg_setup(lambda, G.b);
     if (!rc) rc = cg_chain(lambda, 0, its);
     if (!rc) rc = cg_tail(its, lambda);
+    if (!rc && !shard_) {               // the trial's evaluation (of the current state: no update)
+        SumJob den;
+        den.n = G.hd + 3 * (int64_t)G.nown; den.a = G.x; den.b = G.b; den.lambda = lambda; den.mode = 1;
+        den.out = d_scal + 1;
+        rc = eval_chi2(analytic, 0, &den, nullptr, eval_host_sums() ? h_epart_ : nullptr);
+    }
     set_profiler(nullptr);
     if (rc) return rc;
     SPOK(hipStreamSynchronize(st_));
