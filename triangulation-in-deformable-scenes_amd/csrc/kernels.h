@@ -36,6 +36,12 @@ struct DevProblem {
     // device-driven LM (spcg_solver.cpp, one rank): kernels return at once when their gate word is 0 —
     // gate_lin for the linearization's launches, gate_trial for a trial's; nullptr: always run
     const int *gate_lin = nullptr, *gate_trial = nullptr;
+    // the linearization's chi2 as per-workgroup partials (the iterative plan, one rank): set, k_lin_pts'
+    // reprojection / depth workgroups and k_lin_arap's workgroups over the first n_arap_sum edges store
+    // their sums at lin_part[b] (lin_chi_blocks' layout) instead of per-edge chi2 — pinned host memory
+    // (the host adds them after its synchronization) or HBM (launch_part_sums adds them)
+    double *lin_part = nullptr;
+    int64_t n_arap_sum = 0;
 };
 
 struct FrontDev {
@@ -226,6 +232,12 @@ void trial_eval_blocks(const DevProblem &P, const EvalJob &J, int nb[4]);
 // the four sums from the host partials, in the device's final order (per kind: lane l adds partials
 // l, l + 64, ... in order, then the xor butterfly 32 .. 1; lane 0's value)
 void trial_eval_host_sums(const double *h_part, const int nb[4], double out[4]);
+// the linearization's chi2 partial layout (DevProblem::lin_part): rep, dep, arap workgroup counts
+void lin_chi_blocks(const DevProblem &P, int nb[4]);
+// one workgroup: the four sums of a partial layout in trial_eval_host_sums' order into out[0..2],
+// den_out (nb[3] > 0), total = (out0 + out2) + out1; gated like the linearization (gate)
+void launch_part_sums(const double *part, const int nb[4], double *out, double *den_out, double *total, const int *gate,
+                      hipStream_t st);
 // edges per thread of a trial evaluation's workgroup (DEFTRI_EVAL_EPT, 1..8; default 2)
 int eval_edges_per_thread();
 // the partial slots launch_trial_eval needs (part's length)

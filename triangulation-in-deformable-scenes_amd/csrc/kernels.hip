@@ -510,6 +510,16 @@ __device__ __forceinline__ double lin_arap_edge(int e, int E_, const int32_t *__
     return c2;
 }
 
+// a 128-thread workgroup's sum (the linearization's chi2 partials): a butterfly per wave, then the two
+// waves; the value in thread 0
+__device__ __forceinline__ double block128_sum(double v) {
+    __shared__ double r2[2];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63) == 0) r2[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return r2[0] + r2[1];
+}
+
 __global__ void k_lin_rep(int R, const int32_t *__restrict__ rp, const int32_t *__restrict__ rc,
                           const double *__restrict__ obs, const double *__restrict__ info, double hdelta,
                           const double *__restrict__ points, const double *__restrict__ cam_pose,
@@ -540,10 +550,14 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MODE =
                            const double *__restrict__ tg, const double *__restrict__ tg_pre,
                            double *__restrict__ J, double *__restrict__ W,
                            double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic,
-                           int64_t jld, const int *gate) {
+                           int64_t jld, const int *gate, double *__restrict__ lpart, int64_t nsum) {
     if (gate && !*gate) return;
-    lin_arap_edge<MODE>(TID, E_, apts, apair, arot, aw, rot, parea, pinfo, points, tg, tg_pre, J, W, E, chi, want_jac,
-                        analytic, jld);
+    const double c = lin_arap_edge<MODE>(TID, E_, apts, apair, arot, aw, rot, parea, pinfo, points, tg, tg_pre, J, W, E,
+                                         lpart ? nullptr : chi, want_jac, analytic, jld);
+    if (lpart && (int64_t)blockIdx.x * 128 < nsum) {
+        const double v = block128_sum(TID < nsum ? c : 0.0);
+        if (threadIdx.x == 0) lpart[blockIdx.x] = v;
+    }
 }
 
 // the errors and chi2 of every reprojection, depth and ARAP edge in one launch (the trial's
@@ -554,14 +568,21 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(MODE =
 __global__ void __launch_bounds__(128) k_lin_pts(const DevProblem P, int nbr, int nbd, int want_jac, int analytic) {
     if (P.gate_lin && !*P.gate_lin) return;
     const int b = blockIdx.x, t = threadIdx.x;
+    double c = 0.0;
     if (b < nbr)
-        lin_rep_edge(b * 128 + t, P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points, P.cam_pose,
-                     P.cam_R, P.cam_kb8, P.Jrep, P.Wrep, P.Erep, P.chi_rep, want_jac);
+        c = lin_rep_edge(b * 128 + t, P.R, P.rep_point, P.rep_cam, P.rep_obs, P.rep_info, P.huber_delta, P.points,
+                         P.cam_pose, P.cam_R, P.cam_kb8, P.Jrep, P.Wrep, P.Erep, P.lin_part ? nullptr : P.chi_rep,
+                         want_jac);
     else if (b < nbr + nbd)
-        lin_dep_edge((b - nbr) * 128 + t, P.D, P.dep_point, P.dep_scale, P.dep_cam, P.dep_meas, P.dep_info, P.points,
-                     P.scales, P.cam_pose, P.cam_R, P.Jdep, P.Wdep, P.Edep, P.chi_dep, want_jac, analytic);
+        c = lin_dep_edge((b - nbr) * 128 + t, P.D, P.dep_point, P.dep_scale, P.dep_cam, P.dep_meas, P.dep_info, P.points,
+                         P.scales, P.cam_pose, P.cam_R, P.Jdep, P.Wdep, P.Edep, P.lin_part ? nullptr : P.chi_dep,
+                         want_jac, analytic);
     else
         arap_pre_one((b - nbr - nbd) * 128 + t, P.Q, P.tg, P.tg_pre);
+    if (P.lin_part && b < nbr + nbd) {             // (a workgroup-uniform branch)
+        const double v = block128_sum(c);
+        if (t == 0) P.lin_part[b] = v;
+    }
 }
 
 __global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, int nbd) {
@@ -577,6 +598,42 @@ __global__ void __launch_bounds__(128) k_lin_chi(const DevProblem P, int nbr, in
         lin_arap_edge<0>((b - nbr - nbd) * 128 + t, P.E, P.arap_pts, P.arap_pair, P.arap_rot, P.arap_w, P.rot,
                          P.pair_area, P.pair_info, P.points, P.tg, nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, 0, 0,
                          P.jarap_ld);
+}
+
+// the four sums of a partial layout (nb0 rep, nb1 dep, nb2 arap, nb3 den workgroups) by one 256-thread
+// workgroup: wave w adds kind w's partials (lane-strided, eight loads in flight, added in order), then
+// a butterfly; s[w] set for every thread on return (trial_eval_host_sums is the same order on the host)
+__device__ __forceinline__ void part_sums_block(const double *part, int nb0, int nb1, int nb2, int nb3, double *s) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lo = w == 0 ? 0 : w == 1 ? nb0 : w == 2 ? nb0 + nb1 : nb0 + nb1 + nb2;
+    const int hi = w == 0 ? nb0 : w == 1 ? nb0 + nb1 : w == 2 ? nb0 + nb1 + nb2 : nb0 + nb1 + nb2 + nb3;
+    double a = 0.0;
+    int i = lo + lane;
+    for (; i + 7 * 64 < hi; i += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = ld_sc1(part + i + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 8; u++) a += v[u];
+    }
+    for (; i < hi; i += 64) a += ld_sc1(part + i);
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+    if (lane == 0) s[w] = a;
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_part_sums(const double *__restrict__ part, int nb0, int nb1, int nb2, int nb3,
+                                                  double *out, double *den_out, double *total, const int *gate) {
+    if (gate && !*gate) return;
+    __shared__ double s[4];
+    part_sums_block(part, nb0, nb1, nb2, nb3, s);
+    if (threadIdx.x == 0) {
+        out[0] = s[0];
+        out[1] = s[1];
+        out[2] = s[2];
+        if (den_out) *den_out = s[3];
+        if (total) *total = (s[0] + s[2]) + s[1];
+    }
 }
 
 // a trial's evaluation (kernels.h EvalJob): workgroups [0, nbr) reprojection edges, then nbd depth,
@@ -646,22 +703,7 @@ __global__ void __launch_bounds__(256) k_trial_eval(const DevProblem P, const Ev
     }
     __syncthreads();
     if (!last) return;
-    // wave w adds kind w's partials: lane-strided, eight loads in flight, added in order; a butterfly
-    const int lo = w == 0 ? 0 : w == 1 ? nbr : w == 2 ? nbr + nbd : nbr + nbd + nba;
-    const int hi = w == 0 ? nbr : w == 1 ? nbr + nbd : w == 2 ? nbr + nbd + nba : (int)gridDim.x;
-    double a = 0.0;
-    int i = lo + lane;
-    for (; i + 7 * 64 < hi; i += 8 * 64) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = ld_sc1(part + i + 64 * u);
-#pragma unroll
-        for (int u = 0; u < 8; u++) a += v[u];
-    }
-    for (; i < hi; i += 64) a += ld_sc1(part + i);
-    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
-    if (lane == 0) s[w] = a;
-    __syncthreads();
+    part_sums_block(part, nbr, nbd, nba, (int)gridDim.x - nbr - nbd - nba, s);
     if (t == 0) {
         J.out[0] = s[0];
         J.out[1] = s[1];
@@ -2285,7 +2327,8 @@ void launch_linearize(const DevProblem &P, hipStream_t st, bool want_jac, bool a
                            dim3(nb(P.E, 128)), dim3(128), st, P.E, P.arap_pts, P.arap_pair,
                            P.arap_rot, P.arap_w, P.rot, P.pair_area, P.pair_info, P.points, P.tg,
                            pre ? P.tg_pre : nullptr, P.Jarap, P.Warap, P.Earap, P.chi_arap, want_jac ? 1 : 0,
-                           analytic ? 1 : 0, P.jarap_ld, P.gate_lin);
+                           analytic ? 1 : 0, P.jarap_ld, P.gate_lin, P.lin_part ? P.lin_part + nbr + nbd : nullptr,
+                           P.n_arap_sum);
 }
 
 void launch_assemble(const DevProblem &P, const DevPlan &L, hipStream_t st) {
@@ -2542,6 +2585,19 @@ void launch_lin_chi(const DevProblem &P, hipStream_t st) {
     const int nbr = P.R > 0 ? (int)nb(P.R, 128) : 0, nbd = P.D > 0 ? (int)nb(P.D, 128) : 0;
     const int nba = P.E > 0 ? (int)nb(P.E, 128) : 0;
     if (nbr + nbd + nba > 0) LAUNCH("lin_chi", dev::k_lin_chi, dim3(nbr + nbd + nba), dim3(128), st, P, nbr, nbd);
+}
+
+void lin_chi_blocks(const DevProblem &P, int nbk[4]) {
+    nbk[0] = P.R > 0 ? (int)nb(P.R, 128) : 0;
+    nbk[1] = P.D > 0 ? (int)nb(P.D, 128) : 0;
+    nbk[2] = P.n_arap_sum > 0 ? (int)nb(P.n_arap_sum, 128) : 0;
+    nbk[3] = 0;
+}
+
+void launch_part_sums(const double *part, const int nbk[4], double *out, double *den_out, double *total, const int *gate,
+                      hipStream_t st) {
+    LAUNCH("part_sums", dev::k_part_sums, dim3(1), dim3(256), st, part, nbk[0], nbk[1], nbk[2], nbk[3], out, den_out, total,
+           gate);
 }
 
 int eval_edges_per_thread() {

@@ -396,6 +396,12 @@ class SpSolver {
     int64_t n_epart_ = 0;
     double *h_epart_ = nullptr;        // pinned: the partials of a host-finished trial evaluation
     int eval_nb_[4] = {0, 0, 0, 0};    // its workgroups per kind (trial_eval_blocks)
+    // the linearization's chi2 partials (one rank: DevProblem::lin_part): in HBM for launch_part_sums,
+    // pinned for the host loop, which adds them after its synchronization (lin_host_pending_)
+    double *d_lpart_ = nullptr, *h_lpart_ = nullptr;
+    int lin_nb_[4] = {0, 0, 0, 0};
+    bool lin_host_pending_ = false;
+    double lin_chi_host() const;       // the pending partials' total ((rep + arap) + dep)
     double *hpin = nullptr;
     int *ipin = nullptr;
     int32_t *d_send_rows = nullptr, *d_recv_rows = nullptr;
@@ -411,7 +417,7 @@ class SpSolver {
     int fail(int code, const std::string &m) { err = m; return code; }
     int hand_off_timeout();
     int budget() const;
-    int lin_iteration(bool analytic, bool want_max, bool &ok);
+    int lin_iteration(bool analytic, bool want_max, bool &ok, bool host_chi = false);
     int eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb = nullptr, double *h_part = nullptr,
                   double *rec_clear = nullptr, int64_t nclear = 0);
     int cg_setup(double lambda, const double *rhs);

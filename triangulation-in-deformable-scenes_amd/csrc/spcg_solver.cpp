@@ -45,6 +45,13 @@ bool eval_host_sums() {
     return v;
 }
 
+// one rank: the linearization's chi2 summed from its workgroups' partials (DEFTRI_LIN_CHI_ARRAYS=1:
+// per-edge chi2 and the fixed-order sums of round 5)
+bool lin_part_sums() {
+    static const bool v = std::getenv("DEFTRI_LIN_CHI_ARRAYS") == nullptr;
+    return v;
+}
+
 // workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
 // chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
 int sum_parts() {
@@ -97,6 +104,7 @@ SpSolver::~SpSolver() {
     for (void *p : allocs_) hipFree(p);
     if (hpin) hipHostFree(hpin);
     if (h_epart_) hipHostFree(h_epart_);
+    if (h_lpart_) hipHostFree(h_lpart_);
     if (ipin) hipHostFree(ipin);
     if (h_snap) hipHostFree(h_snap);
 }
@@ -541,6 +549,14 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         if (h_epart_) hipHostFree(h_epart_);
         h_epart_ = nullptr;
         SPOK(hipHostMalloc((void **)&h_epart_, sizeof(double) * (size_t)n_epart_, hipHostMallocDefault));
+        // the linearization's chi2 partials (one rank; sharded contexts keep the per-edge chi2 sums)
+        P.n_arap_sum = H.n_arap_owned;
+        lin_chi_blocks(P, lin_nb_);
+        const int64_t nl = std::max<int64_t>(1, (int64_t)lin_nb_[0] + lin_nb_[1] + lin_nb_[2]);
+        ALLOC(d_lpart_, nl);
+        if (h_lpart_) hipHostFree(h_lpart_);
+        h_lpart_ = nullptr;
+        SPOK(hipHostMalloc((void **)&h_lpart_, sizeof(double) * (size_t)nl, hipHostMallocDefault));
     }
     SPOK(hipMemset(d_flag, 0, sizeof(int)));
     SPOK(hipMemset(d_sumcnt, 0, 16 * sizeof(int)));
@@ -775,16 +791,35 @@ int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const Read
 
 // per LM iteration: linearize, chi2 (reduced), the rows' / heavy blocks and b (heavy reduced), and at
 // iteration 0 max diag H into d_scal[2]
-int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok) {
+double SpSolver::lin_chi_host() const {
+    double s4[4];
+    trial_eval_host_sums(h_lpart_, lin_nb_, s4);
+    return (s4[0] + s4[2]) + s4[1];
+}
+
+// host_chi (one rank, the host loop): the chi2 partials go to pinned memory and the caller adds them
+// (lin_chi_host) after its next synchronization; d_scal[0] is then not written
+int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok, bool host_chi) {
     ok = true;
-    launch_linearize(P, st_, true, analytic);
-    SumJobs J;
-    J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
-    J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
-    J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
-    J.nj = 3;
-    J.total = d_scal;
-    launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+    lin_host_pending_ = false;
+    if (!shard_ && lin_part_sums()) {
+        // per-workgroup chi2 partials from the linearization's own launches (no per-edge chi2, no
+        // separate sum launch on the host loop)
+        P.lin_part = host_chi ? h_lpart_ : d_lpart_;
+        launch_linearize(P, st_, true, analytic);
+        P.lin_part = nullptr;
+        if (host_chi) lin_host_pending_ = true;
+        else launch_part_sums(d_lpart_, lin_nb_, d_scal + 4, nullptr, d_scal, P.gate_lin, st_);
+    } else {
+        launch_linearize(P, st_, true, analytic);
+        SumJobs J;
+        J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+        J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+        J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+        J.nj = 3;
+        J.total = d_scal;
+        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+    }
     int rc;
     if (shard_ && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
     if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_);
@@ -966,15 +1001,22 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
     auto enqueue = [&]() -> int {
         const bool first = queued == 0;
         // linearization (gate_lin): errors + Jacobians, chi2 sums, the rows' / heavy blocks, b
-        launch_linearize(P, st_, true, analytic);
-        SumJobs J;
-        J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
-        J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
-        J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
-        J.nj = 3;
-        J.total = d_scal;
-        J.gate = &d_lm->gate_lin;
-        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+        if (lin_part_sums()) {              // the host loop's partials and order (bit-identical chi2)
+            P.lin_part = d_lpart_;
+            launch_linearize(P, st_, true, analytic);
+            P.lin_part = nullptr;
+            launch_part_sums(d_lpart_, lin_nb_, d_scal + 4, nullptr, d_scal, &d_lm->gate_lin, st_);
+        } else {
+            launch_linearize(P, st_, true, analytic);
+            SumJobs J;
+            J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
+            J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
+            J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
+            J.nj = 3;
+            J.total = d_scal;
+            J.gate = &d_lm->gate_lin;
+            launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+        }
         if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_, &d_lm->gate_lin);
         sp_launch_glin(G, fp32_jac != 0, st_);
         if (first) {
@@ -1153,13 +1195,15 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     for (it = 0; it < prm.n_iterations; it++) {
         auto t0 = std::chrono::steady_clock::now();
         bool ok;
-        if ((rc = lin_iteration(analytic, it == 0, ok))) return rc;
+        if ((rc = lin_iteration(analytic, it == 0, ok, !dist))) return rc;
         double *chis = hpin;
         SPOK(hipMemcpyAsync(chis, d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, st_));
         bool chi_pending = true;
+        // (after a synchronization) the linearization's chi2: the host-added partials or d_scal[0]
+        auto lin_chi = [&]() { return lin_host_pending_ ? lin_chi_host() : chis[0]; };
         if (it == 0) {
             SPOK(hipStreamSynchronize(st_));
-            currentChi = chis[0];
+            currentChi = lin_chi();
             chi_pending = false;
             lambda = prm.user_lambda > 0 ? prm.user_lambda : tau * chis[2];
             ni = 2;
@@ -1232,7 +1276,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             if ((rc = evaluate())) return rc;
             SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
             finish_sums();
-            if (chi_pending) { currentChi = chis[0]; chi_pending = false; }
+            if (chi_pending) { currentChi = lin_chi(); chi_pending = false; }
             int st = (int)hpin[16];
             if (st == kSpTimeout) return hand_off_timeout();
             bool solved = st == kSpConverged, evaluated = solved;
