@@ -117,12 +117,15 @@ def end_to_end(device, m, configure, n_it=25):
         out[key + "_iterations"] = rep["iterations"]
         out[key + "_plan_reuses"] = rep["plan_reuses"]
         mh, sh, gms = c.graph_stats()
+        nrep, nfl = c.graph_repairs()
         out[key + "_graph_ms"] = round(gms, 2)
         out[key + "_graph_path"] = "memo" if mh > out.get("_mh", 0) else ("structure memo" if sh > out.get("_sh", 0) else "full")
-        out["_mh"], out["_sh"] = mh, sh
+        if out[key + "_graph_path"] == "full" and nrep > out.get("_rep", 0):
+            out[key + "_graph_path"] = f"full (mesh flip-repaired: {nfl - out.get('_fl', 0)} flips)"
+        out["_mh"], out["_sh"], out["_rep"], out["_fl"] = mh, sh, nrep, nfl
     fresh.close()
-    out.pop("_mh", None)
-    out.pop("_sh", None)
+    for k in ("_mh", "_sh", "_rep", "_fl"):
+        out.pop(k, None)
     return out
 
 

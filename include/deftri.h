@@ -510,6 +510,11 @@ int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n);
    every pair's Delaunay triangulation still valid — the values refreshed in place, the descriptor
    equal bit for bit to a full build's), and the host time of the last build in ms. */
 int deftri_graph_stats(const deftri_ctx *ctx, int64_t *memo_hits, int64_t *struct_hits, double *ms_last);
+/* Full graph builds' keyframe meshes that were repaired from the previous build's triangulation of
+   the same vertices (Lawson flips with exact predicates, then the same strict uniqueness check as the
+   structure memo — so the mesh equals a new Delaunay triangulation triangle for triangle) instead of
+   triangulated anew, and the flips they took, over this context's life. */
+int deftri_graph_repairs(const deftri_ctx *ctx, int64_t *meshes, int64_t *flips);
 /* Keyframe pairs of the graphs this context builds (deftri_arap_build_graph / _optimization): 0
    (default) every pair (a, b > a) in map order, as the reference's loop (g2oBundleAdjustment.cc:
    640-645); w > 0 only pairs with b - a <= w (a sliding window: the documented deviation used for

@@ -251,3 +251,28 @@ def test_graph_observation_errors_first_pair_wins(host, case):
     want = "keypoint octave out of range" if case == "octave_first" else "observation index out of range"
     assert want in str(e.value)
     host.build_graph(m, 1.0, 1e7, np.float32(0.3))      # the context builds a good map afterwards
+
+
+@pytest.mark.parametrize("rel", [1e-6, 1e-5])
+def test_next_round_mesh_repair_equals_new_triangulation(rel, monkeypatch):
+    """A full build after the points moved (the structure memo's triangulations no longer Delaunay):
+    the keyframe's previous triangulation is repaired by Lawson flips (delaunay.cpp delaunay_repair,
+    exact predicates, accepted only when the strict uniqueness check passes) — the descriptor must equal
+    a fresh context's build (a new triangulation) field for field."""
+    import copy
+    from deftri import metrics
+    monkeypatch.setenv("DEFTRI_DELAUNAY_REPAIR", "1")          # (opt-in: graph_builder.cpp build_mesh)
+    m, _ = sim.simulate_two_view(n=3000, seed=5, scale_scene=True, compact=True)
+    rng = np.random.default_rng(11)
+    with capi.Context(-1) as a:
+        p0 = a.build_graph(m, 1.0, 2e5, np.float32(0.003))
+        ext = np.abs(p0.points).max()
+        m2 = copy.deepcopy(m)
+        metrics.apply_solution(m2, list(p0.point_ids), p0.points + rng.normal(0.0, rel * ext, p0.points.shape))
+        r0 = a.graph_repairs()
+        pa = a.build_graph(m2, 1.5, 1e5, np.float32(0.004))
+        r1 = a.graph_repairs()
+        assert r1[0] == r0[0] + 1 and r1[1] > r0[1], (r0, r1)      # repaired, with flips
+        monkeypatch.delenv("DEFTRI_DELAUNAY_REPAIR")              # the fresh build: a new triangulation
+        with capi.Context(-1) as b:
+            _same(pa, b.build_graph(m2, 1.5, 1e5, np.float32(0.004)))

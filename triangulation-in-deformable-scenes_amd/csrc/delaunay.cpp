@@ -303,22 +303,16 @@ struct Sweep {
 
 }  // namespace
 
-bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_size, int &skipped) {
-    tris.clear();
-    hull_size = 0;
-    skipped = 0;
-    if (n < 3) return false;
-    Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}};
-    if (!s.run(skipped)) return false;
-    // canonical order: each triangle rotated to start at its smallest vertex (orientation kept), the
-    // triangles sorted by (first, second, third) — the output then depends only on the triangle set,
-    // so the mesh area (a sum in this order) is the same whoever built the set (a full sweep or the
-    // graph builder's re-validated previous mesh, graph_builder.cpp)
-    const int nt = (int)s.tri.size() / 3;
-    std::vector<int32_t> rot3(s.tri.size());
+// canonical order: each triangle rotated to start at its smallest vertex (orientation kept), the
+// triangles sorted by (first, second, third) — the output then depends only on the triangle set,
+// so the mesh area (a sum in this order) is the same whoever built the set (a full sweep, the graph
+// builder's re-validated previous mesh or a flip-repaired one, graph_builder.cpp)
+static void canonical_tris(const std::vector<int32_t> &in, int n, std::vector<int32_t> &tris) {
+    const int nt = (int)in.size() / 3;
+    std::vector<int32_t> rot3(in.size());
     std::vector<int32_t> cnt(n + 1, 0);
     for (int t = 0; t < nt; t++) {
-        const int32_t a = s.tri[3 * t], b = s.tri[3 * t + 1], c = s.tri[3 * t + 2];
+        const int32_t a = in[3 * t], b = in[3 * t + 1], c = in[3 * t + 2];
         int32_t *o = &rot3[3 * (size_t)t];
         if (a < b && a < c) { o[0] = a; o[1] = b; o[2] = c; }
         else if (b < c) { o[0] = b; o[1] = c; o[2] = a; }
@@ -336,9 +330,19 @@ bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_s
             const int32_t *a = &rot3[3 * (size_t)x], *b = &rot3[3 * (size_t)y];
             return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
         });
-    tris.resize(s.tri.size());
+    tris.resize(in.size());
     for (int k = 0; k < nt; k++)
         for (int c = 0; c < 3; c++) tris[3 * (size_t)k + c] = rot3[3 * (size_t)order[k] + c];
+}
+
+bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_size, int &skipped) {
+    tris.clear();
+    hull_size = 0;
+    skipped = 0;
+    if (n < 3) return false;
+    Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}};
+    if (!s.run(skipped)) return false;
+    canonical_tris(s.tri, n, tris);
     int h = 0, e = s.hstart;
     do { h++; e = s.hnext[e]; } while (e != s.hstart && h <= n);
     hull_size = h;
@@ -413,6 +417,149 @@ bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &t
         if (++len > nb) return false;
     } while (u != start);
     return len == nb && wraps == 1;
+}
+
+// the boundary cycle bnext (nb half-edges u -> bnext[u]) is one strictly convex polygon winding once:
+// with every turn in (0, pi), the edge direction passes angle 0 exactly when it moves from the lower
+// half-plane [pi, 2 pi) to the upper [0, pi) — sign tests on coordinate comparisons, exact — and a
+// simple convex polygon does that once (a strict left turn everywhere still admits a pentagram)
+static bool boundary_convex_once(const double *xy, int n, const std::vector<int32_t> &bnext, int nb) {
+    auto P = [&](int i) { return xy + 2 * (size_t)i; };
+    auto upper = [&](int a, int b) {           // direction a -> b in [0, pi)
+        const double *pa = P(a), *pb = P(b);
+        return pb[1] > pa[1] || (pb[1] == pa[1] && pb[0] > pa[0]);
+    };
+    int start = -1;
+    for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
+    if (start < 0) return false;
+    int u = start, len = 0, wraps = 0;
+    do {
+        const int v = bnext[u];
+        if (v < 0 || bnext[v] < 0) return false;
+        if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
+        if (!upper(u, v) && upper(v, bnext[v])) wraps++;
+        u = v;
+        if (++len > nb) return false;
+    } while (u != start);
+    return len == nb && wraps == 1;
+}
+
+bool delaunay_repair(const double *xy, int n, const std::vector<int32_t> &prev, std::vector<int32_t> &tris, int &hull_size,
+                     int &flips) {
+    flips = 0;
+    hull_size = 0;
+    const int nt = (int)prev.size() / 3;
+    if (n < 3 || nt == 0 || n >= (1 << 30)) return false;
+    auto P = [&](int i) { return xy + 2 * (size_t)i; };
+    std::vector<int32_t> T(prev);
+    std::vector<uint8_t> seen(n, 0);
+    for (int32_t v : T) {
+        if (v < 0 || v >= n) return false;
+        seen[v] = 1;
+    }
+    for (int i = 0; i < n; i++)
+        if (!seen[i]) return false;                      // a vertex on no triangle (a skipped point)
+    // a triangle the motion folded (a sliver's vertex crossed its opposite edge): the flips cannot
+    // untangle it — fail before any other work
+    for (int t = 0; t < nt; t++)
+        if (orient2d(P(T[3 * t]), P(T[3 * t + 1]), P(T[3 * t + 2])) <= 0) return false;
+    // half-edge h = 3 t + k runs T[h] -> T[3 t + (k + 1) % 3]; twin[h] its opposite (-1: boundary),
+    // paired by an LSD radix sort of the undirected keys (min << 32 | max; sequential passes)
+    auto nx = [](int h) { return h - h % 3 + (h % 3 + 1) % 3; };
+    const int nh = 3 * nt;
+    std::vector<uint64_t> key(nh), key2(nh);
+    std::vector<int32_t> idx(nh), idx2(nh);
+    for (int h = 0; h < nh; h++) {
+        const uint64_t u = (uint64_t)T[h], v = (uint64_t)T[nx(h)];
+        key[h] = u < v ? (u << 32 | v) : (v << 32 | u);
+        idx[h] = h;
+    }
+    {
+        int bits = 1;
+        while ((1 << bits) < n) bits++;
+        std::vector<int> shifts;                         // 11-bit digits of the low, then the high word
+        for (int sh = 0; sh < bits; sh += 11) shifts.push_back(sh);
+        for (int sh = 0; sh < bits; sh += 11) shifts.push_back(32 + sh);
+        for (int shift : shifts) {
+            std::vector<int32_t> cnt(2049, 0);
+            for (int h = 0; h < nh; h++) cnt[((key[h] >> shift) & 2047) + 1]++;
+            for (int d = 0; d < 2048; d++) cnt[d + 1] += cnt[d];
+            for (int h = 0; h < nh; h++) {
+                const int d = (int)((key[h] >> shift) & 2047);
+                key2[cnt[d]] = key[h];
+                idx2[cnt[d]++] = idx[h];
+            }
+            key.swap(key2);
+            idx.swap(idx2);
+        }
+    }
+    std::vector<int32_t> twin(nh, -1);
+    for (int i = 0; i < nh;) {
+        int j = i + 1;
+        while (j < nh && key[j] == key[i]) j++;
+        if (j - i > 2) return false;                      // a non-manifold edge
+        if (j - i == 2) {
+            const int a = idx[i], b = idx[i + 1];
+            if (T[a] == T[b]) return false;              // the same direction twice: not oriented
+            twin[a] = b;
+            twin[b] = a;
+        }
+        i = j;
+    }
+    // Lawson's flips: an interior edge whose opposite vertex lies strictly inside the circumcircle is
+    // replaced by the other diagonal of its quadrilateral; the four outer edges are checked again.
+    // Each flip lowers the lifted surface, so the flips end; a cap guards the loop
+    std::vector<int32_t> stack;
+    stack.reserve(nh);
+    for (int h = 0; h < nh; h++)
+        if (twin[h] > h) stack.push_back(h);
+    const int64_t cap = 16 * (int64_t)nt + 64;
+    while (!stack.empty()) {
+        const int h = stack.back();
+        stack.pop_back();
+        const int g = twin[h];
+        if (g < 0) continue;
+        const int h1 = nx(h), h2 = nx(h1), g1 = nx(g), g2 = nx(g1);
+        const int32_t u = T[h], v = T[h1], w = T[h2], x = T[g2];      // t = (u, v, w), t2 = (v, u, x)
+        if (incircle(P(u), P(v), P(w), P(x)) <= 0) continue;
+        if (++flips > cap) return false;
+        // the new triangles (u, x, w) and (x, v, w): strictly counter-clockwise (a convex quadrilateral)
+        if (orient2d(P(u), P(x), P(w)) <= 0 || orient2d(P(x), P(v), P(w)) <= 0) return false;
+        const int t = h / 3, t2 = g / 3;
+        // outer half-edges before the flip: v -> w (h1), w -> u (h2), u -> x (g1), x -> v (g2)
+        const int o_vw = twin[h1], o_wu = twin[h2], o_ux = twin[g1], o_xv = twin[g2];
+        T[3 * t] = u; T[3 * t + 1] = x; T[3 * t + 2] = w;
+        T[3 * t2] = x; T[3 * t2 + 1] = v; T[3 * t2 + 2] = w;
+        auto link = [&](int a, int b) { twin[a] = b; if (b >= 0) twin[b] = a; };
+        link(3 * t, o_ux);             // u -> x
+        link(3 * t + 1, 3 * t2 + 2);   // x -> w  |  w -> x
+        link(3 * t + 2, o_wu);         // w -> u
+        link(3 * t2, o_xv);            // x -> v
+        link(3 * t2 + 1, o_vw);        // v -> w
+        for (int e : {3 * t, 3 * t + 2, 3 * t2, 3 * t2 + 1})
+            if (twin[e] >= 0) stack.push_back(e);
+    }
+    // THE Delaunay triangulation — delaunay_still_valid's conditions on this structure: every vertex on
+    // a triangle (above), every triangle strictly counter-clockwise (above and at every flip), every
+    // interior edge strictly locally Delaunay (no cocircular ambiguity), the boundary one strictly
+    // convex polygon winding once (the convex hull).  Then tris is triangle for triangle delaunay2d's
+    std::vector<int32_t> bnext(n, -1);
+    int nb = 0;
+    for (int h = 0; h < nh; h++) {
+        const int g = twin[h];
+        if (g < 0) {
+            const int32_t u = T[h], v = T[nx(h)];
+            if (bnext[u] >= 0) return false;             // not a simple boundary polygon
+            bnext[u] = v;
+            nb++;
+        } else if (g > h && incircle(P(T[h]), P(T[nx(h)]), P(T[nx(nx(h))]), P(T[nx(nx(g))])) >= 0) {
+            return false;
+        }
+    }
+    if (!boundary_convex_once(xy, n, bnext, nb)) return false;
+    hull_size = nb;
+    canonical_tris(T, n, tris);
+    return true;
 }
 
 int orient2d_sign(const double *a, const double *b, const double *c) { return orient2d(a, b, c); }

@@ -22,4 +22,12 @@ int incircle_sign(const double *a, const double *b, const double *c, const doubl
 // triangles' half-edges, then the boundary cycle.
 bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &tris);
 
+// The Delaunay triangulation of the moved points from a previous triangulation `prev` of the same
+// vertices (canonical, counter-clockwise): Lawson's edge flips with exact predicates, then the canonical
+// order and delaunay_still_valid — true only when the result is THE Delaunay triangulation, so `tris`
+// is then triangle for triangle delaunay2d's.  False (tris unspecified) when a triangle folded, the
+// hull changed, a cocircular tie remains or the flips ran past their cap: the caller triangulates anew.
+bool delaunay_repair(const double *xy, int n, const std::vector<int32_t> &prev, std::vector<int32_t> &tris, int &hull_size,
+                     int &flips);
+
 }  // namespace deftri

@@ -73,6 +73,7 @@ struct Mesh {
     std::vector<double> w;            // per CSR entry
     double area = 0, ms_delaunay = 0;
     int T = 0, hull = 0, skipped = 0;
+    int flips = -1;                   // >= 0: repaired from the previous round's mesh by that many flips
     int deg(int i) const { return off[i + 1] - off[i]; }
     int64_t find(int i, int j) const {
         const int32_t *b = adj.data() + off[i], *e = adj.data() + off[i + 1];
@@ -83,13 +84,26 @@ struct Mesh {
 
 void mesh_cot_weights(const std::vector<double> &pos, Mesh &M);
 
-bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err, bool host_weights = true) {
+// prev (optional): the previous round's triangulation of the same vertices — repaired by flips when
+// that gives THE Delaunay triangulation (delaunay_repair: then identical to a new one), else unused
+bool build_mesh(const std::vector<double> &pos, int n, Mesh &M, std::string &err, bool host_weights = true,
+                const std::vector<int32_t> *prev = nullptr) {
     if (n < 3) { err = "Not enough points to create a triangular mesh."; return false; }
     std::vector<double> xy(2 * (size_t)n);
     for (int i = 0; i < n; i++) { xy[2 * i] = pos[3 * i]; xy[2 * i + 1] = pos[3 * i + 1]; }
     int skipped = 0;
     auto td = std::chrono::steady_clock::now();
-    if (!delaunay2d(xy.data(), n, M.tris, M.hull, skipped)) { err = "Delaunay triangulation failed (collinear input)"; return false; }
+    // opt-in (DEFTRI_DELAUNAY_REPAIR=1, read per build): measured at 100k points the repair is no
+    // faster than a new triangulation — ~100 ns per exact in-circle test on the points' scattered
+    // vertex order — and a smooth motion already folds a few slivers, which it cannot untangle
+    const char *rep_env = std::getenv("DEFTRI_DELAUNAY_REPAIR");
+    int flips = 0;
+    if (prev && rep_env && std::atoi(rep_env) != 0 && delaunay_repair(xy.data(), n, *prev, M.tris, M.hull, flips)) {
+        M.flips = flips;
+    } else if (!delaunay2d(xy.data(), n, M.tris, M.hull, skipped)) {
+        err = "Delaunay triangulation failed (collinear input)";
+        return false;
+    }
     M.ms_delaunay = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
     M.skipped = skipped;
     const int ntri = (int)M.tris.size() / 3;
@@ -557,7 +571,12 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         }
         // rc 1: a pair's triangulation or vector map changed — the full build below
     }
-    const int64_t hits = g.memo_hits, shits = g.struct_hits;
+    const int64_t hits = g.memo_hits, shits = g.struct_hits, reps = g.mesh_repairs, nflips = g.mesh_flips;
+    // the previous round's meshes by keyframe 1 (deformationOptimization's next round: the same
+    // vertices moved), the hint for a flip repair of each keyframe's triangulation
+    std::vector<std::shared_ptr<const GraphResult::MeshData>> prev_mesh(map.n_keyframes);
+    for (const GraphResult::PairMesh &pm : g.meshes)
+        if (pm.kf1 >= 0 && pm.kf1 < map.n_keyframes && pm.mesh && pm.mesh->skipped == 0) prev_mesh[pm.kf1] = pm.mesh;
     // the edge arrays keep their storage across rebuilds (deformationOptimization's rounds): the
     // pages are already mapped, so refilling them costs no page faults
     auto keep = [](auto &dst, auto &src) { dst.swap(src); dst.clear(); };
@@ -575,6 +594,8 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
     keep(g.arap_rot, old.arap_rot); keep(g.arap_w, old.arap_w); keep(g.arap_wk, old.arap_wk);
     g.memo_hits = hits;
     g.struct_hits = shits;
+    g.mesh_repairs = reps;
+    g.mesh_flips = nflips;
     const int K = map.n_keyframes;
     std::vector<int32_t> cam_of(K, -1);
     IdIndex pidx;
@@ -628,10 +649,13 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
                 for (int k = 0; k < 3; k++) md->pos1.push_back((double)kf1.point_pos[3 * s + k]);
         md->n1 = (int)md->pos1.size() / 3;
         Mesh M;
-        if (!build_mesh(md->pos1, md->n1, M, e, gdev == nullptr)) return nullptr;   // device: weights in the device pass
+        const std::vector<int32_t> *hint =
+            prev_mesh[b] && prev_mesh[b]->n1 == md->n1 ? &prev_mesh[b]->tris : nullptr;
+        if (!build_mesh(md->pos1, md->n1, M, e, gdev == nullptr, hint)) return nullptr;   // device: weights in the device pass
         md->tris = std::move(M.tris); md->off = std::move(M.off); md->adj = std::move(M.adj);
         md->w = std::move(M.w);
         md->T = M.T; md->hull = M.hull; md->area = M.area;
+        md->skipped = M.skipped; md->flips = M.flips;
         md->pos_idx = vector_map(md->pos1, md->n1);
         md->inv.assign(md->n1, -1);          // invertedPosIndexes: the last vertex wins
         for (int v = 0; v < md->n1; v++) md->inv[md->pos_idx[v]] = v;
@@ -652,6 +676,8 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         });
         for (size_t i = 0; i < need.size(); i++)
             if (!kf1_mesh[need[i]]) { err = errs[i]; return false; }
+        for (int b : need)
+            if (kf1_mesh[b]->flips >= 0) { g.mesh_repairs++; g.mesh_flips += kf1_mesh[b]->flips; }
     }
     std::vector<PairEmit> emits;
     for (int a = 0; a < K; a++) {

@@ -45,6 +45,8 @@ struct GraphResult {
         std::vector<int32_t> tris, off, adj, pos_idx, inv;
         std::vector<double> pos1, w;          // positions (x y z) and host cot weights (empty: device pass)
         int n1 = 0, T = 0, hull = 0;
+        int skipped = 0;                      // duplicate points the triangulation left out
+        int flips = -1;                       // >= 0: repaired from the previous round's mesh (flips)
         double area = 0;
         bool identity_map = false;
     };
@@ -61,6 +63,7 @@ struct GraphResult {
     std::vector<int32_t> point_kf, point_slot;   // per point: the keyframe (map order) and slot of its position
     std::vector<int32_t> order_kf, order_slot;   // ... and of its ordering coordinates
     int64_t struct_hits = 0;                  // calls answered by the structure memo
+    int64_t mesh_repairs = 0, mesh_flips = 0; // full builds' meshes flip-repaired from the previous round (kept)
     double ms_last = 0;                       // host time of the last build (either path)
 };
 

@@ -2247,6 +2247,13 @@ int deftri_graph_stats(const deftri_ctx *ctx, int64_t *memo_hits, int64_t *struc
     return 0;
 }
 
+int deftri_graph_repairs(const deftri_ctx *ctx, int64_t *meshes, int64_t *flips) {
+    if (!ctx) return DEFTRI_E_ARG;
+    if (meshes) *meshes = ctx->graph.mesh_repairs;
+    if (flips) *flips = ctx->graph.mesh_flips;
+    return 0;
+}
+
 int deftri_arap_graph_point_ids(const deftri_ctx *ctx, int64_t *ids, int64_t n) {
     if (!ctx || !ids) return DEFTRI_E_ARG;
     if (n != (int64_t)ctx->graph.point_mpid.size()) return DEFTRI_E_ARG;

@@ -1653,7 +1653,14 @@ __device__ __forceinline__ double shfl_up_d(double v, int d) {
 // the solve stops here, the record.  The checks and their order are it_state's.
 __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, double (*red)[4]) {
     beta = 0.0;
-    const double r0 = G.rec[0];
+    // a stop recorded by an earlier launch (a queued iteration past convergence): no sums needed.  One
+    // read per workgroup, so its waves take the same branch (workgroup 0 of this launch may write
+    // the record while another workgroup's waves start)
+    __shared__ double s_r0;
+    if (threadIdx.x == 0) s_r0 = G.rec[0];
+    __syncthreads();
+    const double r0 = s_r0;
+    if (r0 != 0.0) return (int)r0;
     const double *rk = G.red + (int64_t)kSpRed * it;
     const double sw = rk[2];
     const int n2 = it == 0 ? G.nrb + 1 : G.m_nh + row_grid(G.nrb);
@@ -1681,8 +1688,7 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
     const double s1 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
     __syncthreads();
     int st = 0;
-    if (r0 != 0.0) st = (int)r0;
-    else if (sw != 0.0) st = (int)sw;
+    if (sw != 0.0) st = (int)sw;
     else if (s1 <= G.tol2 * (it == 0 ? s1 : G.red[1])) st = kSpConverged;
     else if (it >= G.max_it) st = kSpBudget;
     if (blockIdx.x == 0 && threadIdx.x == 0) {

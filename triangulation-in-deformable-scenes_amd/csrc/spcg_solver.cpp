@@ -52,6 +52,17 @@ bool lin_part_sums() {
     return v;
 }
 
+// the host loop's per-trial wait: poll the stream (no interrupt wake-up; the thread waits anyway) —
+// DEFTRI_SYNC_BLOCK=1: hipStreamSynchronize
+hipError_t stream_wait(hipStream_t st) {
+    static const bool block = std::getenv("DEFTRI_SYNC_BLOCK") != nullptr;
+    if (block) return hipStreamSynchronize(st);
+    hipError_t e;
+    while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+    }
+    return e;
+}
+
 // workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
 // chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
 int sum_parts() {
@@ -1197,12 +1208,13 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
         bool ok;
         if ((rc = lin_iteration(analytic, it == 0, ok, !dist))) return rc;
         double *chis = hpin;
-        SPOK(hipMemcpyAsync(chis, d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, st_));
+        // (the host-added chi2 needs nothing from d_scal after iteration 0's max diag)
+        if (it == 0 || !lin_host_pending_) SPOK(hipMemcpyAsync(chis, d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, st_));
         bool chi_pending = true;
         // (after a synchronization) the linearization's chi2: the host-added partials or d_scal[0]
         auto lin_chi = [&]() { return lin_host_pending_ ? lin_chi_host() : chis[0]; };
         if (it == 0) {
-            SPOK(hipStreamSynchronize(st_));
+            SPOK(stream_wait(st_));
             currentChi = lin_chi();
             chi_pending = false;
             lambda = prm.user_lambda > 0 ? prm.user_lambda : tau * chis[2];
@@ -1274,7 +1286,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             int j = n;
             if ((rc = cg_tail(j, lambda))) return rc;
             if ((rc = evaluate())) return rc;
-            SPOK(hipStreamSynchronize(st_));        // the one host round trip of a trial (prediction held)
+            SPOK(stream_wait(st_));                 // the one host round trip of a trial (prediction held)
             finish_sums();
             if (chi_pending) { currentChi = lin_chi(); chi_pending = false; }
             int st = (int)hpin[16];
@@ -1305,7 +1317,7 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 }
                 if (solved) {
                     if ((rc = evaluate())) return rc;
-                    SPOK(hipStreamSynchronize(st_));
+                    SPOK(stream_wait(st_));
                     finish_sums();
                     evaluated = true;
                 }
@@ -1507,7 +1519,7 @@ int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
     SPOK(hipStreamSynchronize(st_));
     set_profiler(&prof);
     bool ok;
-    int rc = lin_iteration(analytic, false, ok);
+    int rc = lin_iteration(analytic, false, ok, !shard_);   // (the host loop's launches)
     set_profiler(nullptr);
     if (rc) return rc;
     bool solved = false;

@@ -71,6 +71,7 @@ def load():
         "deftri_profile_trial": (C.c_int, [C.c_void_p, C.c_double, P(_abi.KernelStat), C.c_int32, P(C.c_int32)]),
         "deftri_arap_graph_point_ids": (C.c_int, [C.c_void_p, P(C.c_int64), C.c_int64]),
         "deftri_graph_stats": (C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_double)]),
+        "deftri_graph_repairs": (C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64)]),
         "deftri_arap_build_graph": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_float,
                                               P(P(_abi.ProblemDesc))]),
         "deftri_arap_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), C.c_double, C.c_double, C.c_double,
@@ -134,7 +135,7 @@ EXPORTED = [
     "deftri_problem_upload", "deftri_problem_analyse", "deftri_plan_stats", "deftri_debug_plan_solve",
     "deftri_solve_lm", "deftri_set_lm_lanes", "deftri_set_jacobian_mode", "deftri_set_factor_precision", "deftri_set_linear_solver", "deftri_last_step_info", "deftri_pixels_stand_dev", "deftri_triangulate_nrslam", "deftri_download", "deftri_reset_state", "deftri_eval_chi2",
     "deftri_eval_gradient", "deftri_eval_hessian_product", "deftri_eval_damped_solve",
-    "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_graph_point_ids", "deftri_graph_stats", "deftri_arap_optimization",
+    "deftri_num_unknowns", "deftri_sizeof", "deftri_arap_build_graph", "deftri_arap_graph_point_ids", "deftri_graph_stats", "deftri_graph_repairs", "deftri_arap_optimization",
     "deftri_profile_trial",
     "deftri_ba_create", "deftri_ba_destroy", "deftri_ba_last_error", "deftri_ba_upload", "deftri_ba_set_state",
     "deftri_ba_set_edge_flags", "deftri_ba_solve_lm", "deftri_ba_compute_errors", "deftri_ba_edge_chi2",
@@ -373,6 +374,13 @@ class Context:
         self._check(self.lib.deftri_arap_graph_point_ids(self.h, ids.ctypes.data_as(C.POINTER(C.c_int64)), p.n_points))
         p.point_ids = ids
         return p
+
+    def graph_repairs(self):
+        """(keyframe meshes of full graph builds repaired from the previous build's triangulation, their
+        flips) over this context's life."""
+        a, b = C.c_int64(), C.c_int64()
+        self._check(self.lib.deftri_graph_repairs(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def graph_stats(self):
         """(memo hits, structure-memo hits, host ms of the last graph build)."""
