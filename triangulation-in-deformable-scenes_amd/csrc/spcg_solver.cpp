@@ -1195,6 +1195,22 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     // the trial's sums finished on the host (DEFTRI_EVAL_DEVICE_SUMS=1: by the evaluation's last workgroup)
     const bool host_sums = eval_host_sums();
     bool sums_pending = false;
+    // DEFTRI_HOST_TIMING=1: the host's time from a trial's wait to the next launch call (a further
+    // trial's setup or the next linearization) and the linearization's launch calls, per solve
+    struct HostTiming {
+        bool on = std::getenv("DEFTRI_HOST_TIMING") != nullptr, mark = false;
+        std::chrono::steady_clock::time_point t_wait;
+        double to_trial = 0, to_lin = 0, lin_issue = 0, trial_issue = 0;
+        int n_trial = 0, n_lin = 0, n_issue = 0;
+        double since() const { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_wait).count(); }
+        ~HostTiming() {
+            if (on)
+                std::fprintf(stderr, "[deftri host] wait -> further trial %.1f us (%d), wait -> linearization %.1f us (%d), "
+                             "linearization launch calls %.1f us per iteration, a trial's launch calls %.1f us\n",
+                             n_trial ? to_trial / n_trial : 0.0, n_trial, n_lin ? to_lin / n_lin : 0.0, n_lin,
+                             n_lin ? lin_issue / (n_lin + 1) : 0.0, n_issue ? trial_issue / n_issue : 0.0);
+        }
+    } ht;
     // one rank, host sums: k_trial_begin folded away — the backup into the trial's state update, the
     // records' clear into the evaluation (DEFTRI_TRIAL_BEGIN=1: the prologue launch)
     static const bool fold_env = std::getenv("DEFTRI_TRIAL_BEGIN") == nullptr;
@@ -1206,7 +1222,10 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     for (it = 0; it < prm.n_iterations; it++) {
         auto t0 = std::chrono::steady_clock::now();
         bool ok;
+        if (ht.on && ht.mark) { ht.to_lin += ht.since(); ht.n_lin++; ht.mark = false; }
+        const auto tl0 = std::chrono::steady_clock::now();
         if ((rc = lin_iteration(analytic, it == 0, ok, !dist))) return rc;
+        if (ht.on) ht.lin_issue += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tl0).count();
         double *chis = hpin;
         // (the host-added chi2 needs nothing from d_scal after iteration 0's max diag)
         if (it == 0 || !lin_host_pending_) SPOK(hipMemcpyAsync(chis, d_scal, sizeof(double) * 3, hipMemcpyDeviceToHost, st_));
@@ -1274,6 +1293,8 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 sums_pending = false;
             };
             auto t0p = std::chrono::steady_clock::now();
+            if (ht.on && ht.mark) { ht.to_trial += ht.since(); ht.n_trial++; ht.mark = false; }
+            const auto tt0 = std::chrono::steady_clock::now();
             if ((rc = cg_setup(lambda, G.b))) return rc;
             // CG iterations queued before the trial's evaluation: the last converged count + a
             // margin (DEFTRI_SP_GUESS_MARGIN).  A short guess costs the evaluation, a state restore
@@ -1286,7 +1307,9 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             int j = n;
             if ((rc = cg_tail(j, lambda))) return rc;
             if ((rc = evaluate())) return rc;
+            if (ht.on) { ht.trial_issue += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tt0).count(); ht.n_issue++; }
             SPOK(stream_wait(st_));                 // the one host round trip of a trial (prediction held)
+            if (ht.on) { ht.t_wait = std::chrono::steady_clock::now(); ht.mark = true; }
             finish_sums();
             if (chi_pending) { currentChi = lin_chi(); chi_pending = false; }
             int st = (int)hpin[16];
