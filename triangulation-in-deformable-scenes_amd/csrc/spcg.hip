@@ -287,9 +287,11 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
 #pragma unroll
         for (int k = 0; k < kSpLin; k++) a[k] = 0.0;
         const int iend = G.blk[gr.x + gr.y - 1].w;
-        // the edges ii, ii + 256, ... added in order; their loads issued four edges at a time (a
-        // group's up to 8 edges per thread would otherwise be 8 dependent memory round trips)
-        auto add = [&](const double *J, double wv, double er) {
+        for (int ii = i; ii < iend; ii += 256) {
+            double J[6];
+#pragma unroll
+            for (int r = 0; r < 6; r++) J[r] = G.Ja[(12 + r) * G.jld + ii];
+            const double wv = G.Wa[ii], er = G.Ea[ii];
 #pragma unroll
             for (int r = 0; r < 6; r++) {
                 const double jr = J[r] * wv;
@@ -297,25 +299,6 @@ __global__ void __launch_bounds__(256) k_sp_glin_blocks(const SpDev G) {
                 for (int c = 0; c <= r; c++) a[tri6(r, c)] += jr * J[c];
                 a[21 + r] -= J[r] * (wv * er);
             }
-        };
-        int ii = i;
-        for (; ii + 3 * 256 < iend; ii += 4 * 256) {
-            double J[4][6], wv[4], er[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-#pragma unroll
-                for (int r = 0; r < 6; r++) J[u][r] = G.Ja[(12 + r) * G.jld + ii + 256 * u];
-                wv[u] = G.Wa[ii + 256 * u];
-                er[u] = G.Ea[ii + 256 * u];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) add(J[u], wv[u], er[u]);
-        }
-        for (; ii < iend; ii += 256) {
-            double J[6];
-#pragma unroll
-            for (int r = 0; r < 6; r++) J[r] = G.Ja[(12 + r) * G.jld + ii];
-            add(J, G.Wa[ii], G.Ea[ii]);
         }
         for (int k = threadIdx.x; k < kSpLin * (gr.y - 1); k += 256) out[kSpLin + k] = 0.0;
 #pragma unroll
