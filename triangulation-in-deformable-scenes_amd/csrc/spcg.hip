@@ -1778,6 +1778,33 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     __shared__ double red[9][4];
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
+    // what does not depend on the state — the tile's table row, its rows' (z, p) for i = tid, its
+    // first entries' meta — is loaded before the state test's sums, so those round trips overlap
+    // (sharded overlap: the launch runs a subset of the logical workgroups, G.p1list)
+    const int b = G.p1list ? G.p1list[blockIdx.x] : (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool heavy_wg = b == G.t_grid - 1;
+    const int seg = (G.ntile + 7) / 8;
+    const int t = heavy_wg ? G.ntile : (b & 7) * seg + (b >> 3);
+    int r0 = 0, nr = 0, nh = 0, e0 = 0, ne = 0, h0 = 0, ns = 0;
+    double2 zpre[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+    uint2 m0 = make_uint2(0u, 0u);
+    int2 ch0 = make_int2(0, 0);
+    if (t < G.ntile) {
+        const int32_t *T = G.ttab + 8 * (int64_t)t;
+        r0 = T[0]; nr = T[1]; nh = T[2]; e0 = T[3]; ne = T[4]; h0 = T[5]; ns = T[6];
+        if (tid < nr + nh) {
+            // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another
+            // rank's in the receive region)
+            const int row = tid < nr ? G.row0 + r0 + tid : G.thalo[h0 + tid - nr];
+            const int64_t o = G.hd + 3 * (int64_t)row;
+#pragma unroll
+            for (int c = 0; c < 3; c++) zpre[c] = G.zp[o + c];
+        }
+        if (tid < ne) {
+            m0 = G.tmeta[(int64_t)e0 + tid];
+            ch0 = G.tchunk[((int64_t)e0 + tid) >> 6];
+        }
+    }
     double beta;
     if (G.sd) {
         // sharded single-reduction chain: the product is A z (beta 0); the state is the update's
@@ -1789,9 +1816,6 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
         return;
     }
-    // (sharded overlap: the launch runs a subset of the logical workgroups, G.p1list)
-    const int b = G.p1list ? G.p1list[blockIdx.x] : (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool heavy_wg = b == G.t_grid - 1;
     double pap = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
     double qk[3] = {0, 0, 0}, pk[3] = {0, 0, 0}, phv = 0.0;     // FU: the row's q and p (tid < nr), heavy p
     int lrow = -1;
@@ -1813,15 +1837,12 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             return;
         }
     }
-    const int seg = (G.ntile + 7) / 8;
-    const int t = heavy_wg ? G.ntile : (b & 7) * seg + (b >> 3);
     if (t < G.ntile) {
-        const int32_t *T = G.ttab + 8 * (int64_t)t;
-        const int r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
         double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
-        for (int i = tid; i < nr + nh; i += 256) {
-            // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another
-            // rank's in the receive region)
+        if (tid < nr + nh)
+#pragma unroll
+            for (int c = 0; c < 3; c++) pL[3 * tid + c] = __fma_rn(beta, zpre[c].y, zpre[c].x);   // pval
+        for (int i = tid + 256; i < nr + nh; i += 256) {
             const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
@@ -1836,8 +1857,8 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         for (int base = 0; base < ne; base += 256) {
             if (base + 64 * wv >= ne) break;       // (ne is a multiple of 64: whole waves in or out)
             const int64_t k = (int64_t)e0 + base + tid;
-            const uint2 m = G.tmeta[k];
-            const int2 ch = G.tchunk[k >> 6];
+            const uint2 m = base == 0 ? m0 : G.tmeta[k];
+            const int2 ch = base == 0 ? ch0 : G.tchunk[k >> 6];
             const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
             const bool foreign = (m.x & kTmForeign) != 0, drop = (m.x & kTmDrop) != 0;   // (sharded plans)
             const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
