@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define DEFTRI_ABI_VERSION 7
+#define DEFTRI_ABI_VERSION 8
 
 /* error codes */
 #define DEFTRI_OK             0
@@ -46,6 +46,8 @@ extern "C" {
 #define DEFTRI_E_NUMERIC     -4   /* non-finite state */
 #define DEFTRI_E_NODEVICE    -5   /* no usable gfx950 device */
 #define DEFTRI_E_GRAPH       -6   /* graph construction failed (e.g. < 3 mesh points) */
+#define DEFTRI_E_SEARCH      -7   /* the weight search ended on a failure code (nlopt::opt::optimize
+                                     throws there, g2oBundleAdjustment.cc:515): the round is not run */
 
 /* solver status written into deftri_report.status (g2o SparseOptimizer::optimize semantics) */
 #define DEFTRI_STATUS_OK         0  /* ran all requested iterations */
@@ -532,10 +534,19 @@ int deftri_arap_build_graph(deftri_ctx *ctx, const deftri_map *map, double rep_w
    within [lb, ub] (xtol_rel, xtol_abs, maxeval; :486-530) — NLopt 2.x's nldrmd.c with its default
    initial step, elimdim and relstop restated (deftri/nlopt_nm.py is the same algorithm) — whose
    every evaluation is outerObjective (nloptOptimization.cc:4-37): arapOptimization on a clone of
-   the map as the round started (Map::clone, Map.cc:30-58: here a copy of the positions, depth
-   scales and global-transformation table, the rest shared read-only), then calculatePixelsStandDev
+   a clone of the map as the round started (:499, nloptOptimization.cc:13; Map::clone, Map.cc:30-58:
+   here a copy of the positions and depth scales, the rest shared read-only — with the reference's
+   two observable properties: the clone's global table is EMPTY, Map::clone does not copy
+   mGTransformation_, so its pairs start T_g at the identity; and the clone iterates its keyframes
+   in the order deftri_keyframe_order gives), then calculatePixelsStandDev
    on the device, f = log(desvc1)^2 + log(desvc2)^2; then arapOptimization on the map itself with
-   the optimum, whose weights the next round starts from.  The map's positions and depth scales are
+   the optimum, whose weights the next round starts from.  A search that ends on a failure code
+   (nldrmd's degenerate initial simplex) returns DEFTRI_E_SEARCH before that round's
+   arapOptimization (the reference's nlopt::opt::optimize throws there); weightsSelection "eigen"
+   is selection 0: the reference's Eigen::LevenbergMarquardt::minimize returns
+   ImproperInputParameters before evaluating anything (its functor declares 2 values for 3 inputs,
+   m < n, EigenOptimization.h:31, g2oBundleAdjustment.cc:532-550) and the round runs
+   arapOptimization with the unchanged weights.  The map's positions and depth scales are
    written back in place after every round and global_t holds the last T_g; the global table the
    next round reads is updated as Map::insertGlobalKeyFramesTransformation(0, 1, T) does
    (Map.cc:323-330: T and its fp32 inverse).  The Eigen-LM weight search (weightsSelection
@@ -578,6 +589,12 @@ int deftri_deformation_optimization(deftri_ctx *ctx, deftri_map *map, const deft
    -(R^T t) by Eigen's quaternion-vector product, in float.  The one implementation the native outer
    loop and the host mirror's Map model both use.  No context, no GPU. */
 int deftri_global_insert(const double t7[7], double fwd7[7], double inv7[7]);
+/* The KeyFrame iteration order of Map::mKeyFrames_ (std::unordered_map<ID, KeyFrame_>, Map.h:185),
+   which every reference loop over keyframes follows (:640-645, Geometry.cc:387): `insert_ids` in the
+   order Map::insertKeyFrame was called; `clones` applications of Map::clone (Map.cc:30-58, which
+   re-inserts the keyframes in the source's iteration order) after that.  Evaluated with the same
+   standard-library container (libstdc++), not restated.  out[n]: ids in iteration order.  No GPU. */
+int deftri_keyframe_order(const int64_t *insert_ids, int32_t n, int32_t clones, int64_t *out);
 /* TEST ONLY (no GPU): the restated NLopt LN_NELDERMEAD on a caller objective f(x, n, user) over n <= 8
    dimensions — the search deftri_deformation_optimization runs.  x: in the start, out the best;
    *result the NLopt result code (1 success, 4 xtol reached, 5 maxeval reached, -1 failure), *minf,

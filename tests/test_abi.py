@@ -28,7 +28,7 @@ def test_every_declared_symbol_is_exported():
 
 def test_abi_version_and_struct_sizes():
     lib = capi.load()
-    assert lib.deftri_abi_version() == 7
+    assert lib.deftri_abi_version() == 8
     assert lib.deftri_sizeof(0) == C.sizeof(_abi.ProblemDesc)
     assert lib.deftri_sizeof(1) == C.sizeof(_abi.LMParams)
     assert lib.deftri_sizeof(2) == C.sizeof(_abi.Report)

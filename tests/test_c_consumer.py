@@ -29,7 +29,7 @@ def _run(exe, *args):
 
 def test_c_consumer_host(exe):
     out = _run(exe)
-    assert out["abi"] == ["7"] and "ok" in out
+    assert out["abi"] == ["8"] and "ok" in out
     P, Q, S, R, D, E = map(int, out["graph"])
     assert (P, Q, S, R, D) == (800, 1, 2, 800, 800) and E > 2000
     n_unk, nnz, mflop, nf, nl = out["plan"]

@@ -5,10 +5,16 @@
 // clones, and Map::insertGlobalKeyFramesTransformation's table update (Map.cc:323-330).
 //
 // A Map clone (Map.cc:30-58) here is what arapOptimization can change: every keyframe's slot
-// positions and depth scale and the global-transformation table; the keypoints, poses, calibration
-// and observation tables are shared read-only.  Every evaluation starts from the round's base map,
-// so the context's graph memo answers its graph build and the iterative plan is reused (the
-// evaluations differ only in the weights).
+// positions and depth scale; the keypoints, poses, calibration and observation tables are shared
+// read-only.  Two properties of the reference's clone reach the solver and are kept:
+//   - it does NOT copy mGTransformation_: a clone's global-transformation table is empty, so every
+//     pair of a clone's graph starts T_g at the identity (:664-677);
+//   - it inserts the KeyFrames in the source's unordered_map iteration order, so a clone iterates
+//     them in the order libstdc++'s std::unordered_map gives that insertion sequence (reversed for
+//     up to 13 keyframes).  The evaluation maps are clones of the round's clone (:499, then
+//     nloptOptimization.cc:13), i.e. two such re-insertions.
+// Every evaluation starts from the round's base map, so the context's graph memo answers its graph
+// build and the iterative plan is reused (the evaluations differ only in the weights).
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -16,6 +22,8 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/deftri.h"
@@ -185,6 +193,16 @@ int nelder_mead(const std::function<double(const double *)> &f, int n0, double *
     return code;
 }
 
+// Iteration order of std::unordered_map<ID, KeyFrame_> (Map::mKeyFrames_, ID = long unsigned int)
+// after inserting `ids` in the given order — the container the reference iterates, evaluated by the
+// same standard library rather than restated.
+void unordered_order(const int64_t *ids, int n, std::vector<int64_t> &out) {
+    std::unordered_map<unsigned long, int> m;
+    for (int k = 0; k < n; k++) m[(unsigned long)ids[k]] = k;
+    out.clear();
+    for (const auto &kv : m) out.push_back((int64_t)kv.first);
+}
+
 // ---- Map::insertGlobalKeyFramesTransformation (Map.cc:323-330): T and T.inverse() as Sophus
 // SE3f, read back by getGlobalKeyFramesTransformation as g2o::SE3Quat (double) ----------------------
 void se3f_as7(const float q[4], const float t[3], double out[7]) {
@@ -198,6 +216,17 @@ void se3f_as7(const float q[4], const float t[3], double out[7]) {
 }
 
 }  // namespace
+
+extern "C" int deftri_keyframe_order(const int64_t *insert_ids, int32_t n, int32_t clones, int64_t *out) {
+    if (n < 0 || clones < 0 || (n > 0 && (!insert_ids || !out))) return DEFTRI_E_ARG;
+    std::vector<int64_t> cur(insert_ids, insert_ids + n), next;
+    for (int c = 0; c <= clones; c++) {
+        unordered_order(cur.data(), n, next);
+        cur.swap(next);
+    }
+    std::copy(cur.begin(), cur.end(), out);
+    return 0;
+}
 
 extern "C" int deftri_global_insert(const double t7[7], double fwd7[7], double inv7[7]) {
     if (!t7 || !fwd7 || !inv7) return DEFTRI_E_ARG;
@@ -237,25 +266,33 @@ extern "C" int deftri_debug_nelder_mead(deftri_objective_fn f, void *user, int32
 
 namespace {
 
-// the mutable part of a Map (its clone): every keyframe's slot positions and depth scale, the
-// global-transformation table; `view` is a deftri_map over them plus the source's read-only arrays
+// the mutable part of a Map clone: every keyframe's slot positions and depth scale, in the clone's
+// keyframe order; `view` is a deftri_map over them plus the source's read-only arrays, with an empty
+// global table (Map::clone does not copy mGTransformation_) and T_g's start at the identity
 struct MapClone {
     std::vector<deftri_keyframe> kfs;
     std::vector<std::vector<float>> pos;
-    std::vector<deftri_global_entry> globals;
     deftri_map view{};
-    void from(const deftri_map &m, const std::vector<deftri_global_entry> &g) {
-        kfs.assign(m.keyframes, m.keyframes + m.n_keyframes);
+    // Map::clone of `m`: keyframes re-inserted in m's iteration order
+    void from(const deftri_map &m) {
+        std::vector<int64_t> ids(m.n_keyframes), order;
+        for (int k = 0; k < m.n_keyframes; k++) ids[k] = m.keyframes[k].id;
+        unordered_order(ids.data(), m.n_keyframes, order);
+        kfs.resize(m.n_keyframes);
         pos.resize(m.n_keyframes);
         for (int k = 0; k < m.n_keyframes; k++) {
-            pos[k].assign(m.keyframes[k].point_pos, m.keyframes[k].point_pos + 3 * (size_t)m.keyframes[k].n_slots);
+            int src = 0;
+            while (m.keyframes[src].id != order[k]) src++;
+            kfs[k] = m.keyframes[src];
+            pos[k].assign(m.keyframes[src].point_pos, m.keyframes[src].point_pos + 3 * (size_t)m.keyframes[src].n_slots);
             kfs[k].point_pos = pos[k].data();
         }
-        globals = g;
         view = m;
         view.keyframes = kfs.data();
-        view.n_global = (int32_t)globals.size();
-        view.globals = globals.data();
+        view.n_global = 0;
+        view.globals = nullptr;
+        const double identity[7] = {0, 0, 0, 1, 0, 0, 0};
+        std::memcpy(view.global_t, identity, sizeof(identity));
     }
 };
 
@@ -295,12 +332,12 @@ extern "C" int deftri_deformation_optimization(deftri_ctx *ctx, deftri_map *map,
     int i = 1;
     for (; i <= prm->n_optimizations && update >= 0.0001 * prm->n_map_points; i++) {
         if (prm->selection == 1) {
-            base.from(*map, table);                            // optData.pMap = pMap->clone()
+            base.from(*map);                                   // optData.pMap = pMap->clone()
             int nev = 0, ev_round = 0;
             double minf = INFINITY;
             auto objective = [&](const double *x) -> double {  // outerObjective
                 if (rc) return INFINITY;
-                eval.from(base.view, base.globals);            // pData->pMap->clone()
+                eval.from(base.view);                          // pData->pMap->clone()
                 double upd = 0.0;
                 int r = deftri_arap_optimization(ctx, &eval.view, x[0], x[1], x[2], prm->alpha, prm->beta, prm->depth_error,
                                                  prm->n_iterations, &upd, nullptr);
@@ -308,8 +345,8 @@ extern "C" int deftri_deformation_optimization(deftri_ctx *ctx, deftri_map *map,
                 if (!r) r = deftri_pixels_stand_dev(ctx, &eval.view, &pe);
                 if (r) { rc = r; return INFINITY; }
                 rep->arap_calls++;
-                auto lg2 = [](double v) { return v > 0 ? std::log(v) * std::log(v) : INFINITY; };
-                const double fv = lg2(pe.desvc1) + lg2(pe.desvc2);
+                // nloptOptimization.cc:31-33: pow(log(desvc), 2) — +inf at 0, NaN for a NaN deviation
+                const double fv = std::pow(std::log(pe.desvc1), 2) + std::pow(std::log(pe.desvc2), 2);
                 ev_round++;
                 if (evals && rep->n_evals < max_evals) {
                     deftri_deformation_eval &e = evals[rep->n_evals];
@@ -325,6 +362,11 @@ extern "C" int deftri_deformation_optimization(deftri_ctx *ctx, deftri_map *map,
                                             minf, nev);
             if (rc) break;
             rep->minf = minf;
+            // nlopt::opt::optimize throws on a failure code (the reference stops there, before :525)
+            if (rep->nlopt_result < 0) {
+                rc = DEFTRI_E_SEARCH;
+                break;
+            }
         }
         // arapOptimization on the map itself; positions and depth scales written back in place
         map->n_global = (int32_t)table.size();

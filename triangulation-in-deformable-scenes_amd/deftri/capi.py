@@ -80,6 +80,7 @@ def load():
         "deftri_deformation_optimization": (C.c_int, [C.c_void_p, P(_abi.MapC), P(_abi.DeformationParams),
                                                       P(_abi.DeformationReport)]),
         "deftri_global_insert": (C.c_int, [P(C.c_double), P(C.c_double), P(C.c_double)]),
+        "deftri_keyframe_order": (C.c_int, [P(C.c_int64), C.c_int32, C.c_int32, P(C.c_int64)]),
         "deftri_debug_nelder_mead": (C.c_int, [_abi.OBJECTIVE_FN, C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double),
                                                P(C.c_double), C.c_double, C.c_double, C.c_int32, P(C.c_double),
                                                P(C.c_int32), P(C.c_int32)]),
@@ -145,7 +146,7 @@ EXPORTED = [
     "deftri_measure_sim_absolute_map_errors", "deftri_measure_relative_map_errors", "deftri_dist_owned_edges",
     "deftri_debug_plan_solve_dist", "deftri_set_plan", "deftri_set_jacobian_storage", "deftri_get_plan_info",
     "deftri_debug_sp_product", "deftri_set_pair_window", "deftri_deformation_optimization", "deftri_global_insert",
-    "deftri_debug_nelder_mead",
+    "deftri_debug_nelder_mead", "deftri_keyframe_order",
 ]
 
 
@@ -436,12 +437,12 @@ class Context:
         evaluation log."""
         self._check(self.lib.deftri_set_jacobian_mode(self.h, 0))      # g2o numeric J (the reference's)
         settings.validate_for_solver()
-        if settings.selection not in ("g2oArap", "twoOptimizations"):
-            raise NotImplementedError(f"selection {settings.selection!r} is out of scope")
-        if settings.selection == "twoOptimizations" and settings.weights_selection != "nlopt":
-            raise NotImplementedError("twoOptimizations with the Eigen LM weight search is not built")
+        if settings.selection == "open3DArap":
+            raise NotImplementedError("open3DArap (Open3D DeformAsRigidAsPossible) is out of scope")
         prm = _abi.DeformationParams()
-        prm.selection = 1 if settings.selection == "twoOptimizations" else 0
+        # any other selection is the fixed-weight round (:565-568); "twoOptimizations" with a
+        # weightsSelection other than "nlopt" too (the Eigen LM returns before evaluating, deftri.h)
+        prm.selection = 1 if (settings.selection == "twoOptimizations" and settings.weights_selection == "nlopt") else 0
         prm.rep, prm.global_, prm.arap = float(settings.rep), float(settings.global_), float(settings.arap)
         prm.alpha, prm.beta = float(settings.alpha), float(settings.beta)
         prm.depth_error = float(settings.depth_sigma)
@@ -468,6 +469,19 @@ class Context:
                 "nlopt_result": rep.nlopt_result, "update": rep.update, "seconds": rep.seconds, "evaluations": ev,
                 "round_update": list(rep.round_update[:min(rep.rounds, 64)]),
                 "round_weights": [list(rep.round_weights[k]) for k in range(min(rep.rounds, 64))]}
+
+
+def keyframe_order(insert_ids, clones=0):
+    """deftri_keyframe_order: the iteration order of Map::mKeyFrames_ (std::unordered_map<ID,
+    KeyFrame_>) after inserting `insert_ids` in order, then `clones` Map::clone re-insertions."""
+    lib = load()
+    n = len(insert_ids)
+    a = (C.c_int64 * max(n, 1))(*[int(v) for v in insert_ids])
+    out = (C.c_int64 * max(n, 1))()
+    rc = lib.deftri_keyframe_order(a, n, int(clones), out)
+    if rc:
+        raise DeftriError(rc, "deftri_keyframe_order")
+    return [int(out[k]) for k in range(n)]
 
 
 def global_insert(t7):

@@ -9,9 +9,15 @@ solver reads and writes (SURVEY §8b "Ownership"):
               global KF-pair transformations (Map.cc:323-330)
 
 Iteration order of the reference's `std::unordered_map<ID, KeyFrame_>` (libstdc++, integer
-hash): nodes whose buckets are distinct are iterated in reverse insertion order, which is what
-makes pKF1 = KF 0 and pKF2 = KF 1 for the two-view case.  `Map.kf_order()`
-returns that order and is what the C-ABI receives.
+hash): `Map.kf_order()` asks the native library for it (deftri_keyframe_order: the same container
+filled in this map's insertion order, not a restatement).  Up to 13 keyframes it is the reverse
+insertion order, which is what makes pKF1 = KF 0 and pKF2 = KF 1 for the two-view case (SURVEY
+Appendix B.1); from 14 on the rehash to 29 buckets interleaves it.  It is what the C-ABI receives.
+
+`Map.clone()` is Map::clone (Map.cc:30-58) as the weight search sees it: new MapPoints and
+KeyFrames, the keyframes re-inserted in this map's iteration order (so the clone iterates them in
+the order that insertion sequence gives), and NO global-transformation table (the reference does not
+copy mGTransformation_).  `copy.deepcopy` stays a plain deep copy (tests use it for isolation).
 """
 import ctypes as C
 import numpy as np
@@ -178,8 +184,18 @@ class Map:
         return self.kf_obs.get(kf_id, {}).get(mp_id, -1)
 
     def kf_order(self):
-        """libstdc++ unordered_map<ID,KF> iteration order (reverse insertion, see module doc)."""
-        return list(reversed(list(self.keyframes.keys())))
+        """libstdc++ unordered_map<ID,KF> iteration order of this map's insertion sequence."""
+        from .capi import keyframe_order
+        return keyframe_order(list(self.keyframes.keys()))
+
+    def clone(self):
+        """Map::clone (Map.cc:30-58): an independent copy whose keyframes were inserted in this map's
+        iteration order and whose global-transformation table is empty."""
+        import copy
+        new = copy.deepcopy(self)
+        new.keyframes = {kid: new.keyframes[kid] for kid in self.kf_order()}
+        new.global_T = {}
+        return new
 
     def insert_global_T(self, kf1, kf2, T):
         self.global_T[(kf1, kf2)] = T

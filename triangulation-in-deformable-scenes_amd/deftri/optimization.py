@@ -49,10 +49,8 @@ def arapOptimization(pMap, repBalanceWeight, globalBalanceWeight, arapBalanceWei
 def outerObjective(x, pMap, settings, arap_fn=None, device=0):
     """nloptOptimization.cc:5-38: arapOptimization on a clone of the map with weights x = (rep,
     global, arap), then (log desvc1)^2 + (log desvc2)^2 of calculatePixelsStandDev."""
-    import copy
-    import math
     from . import metrics
-    clone = copy.deepcopy(pMap)                 # pData->pMap->clone()
+    clone = pMap.clone()                        # pData->pMap->clone()
     fn = arap_fn or (lambda m, *a: arapOptimization(m, *a, device=device))
     fn(clone, float(x[0]), float(x[1]), float(x[2]), settings.alpha, settings.beta, settings.depth_sigma,
        settings.n_iterations)
@@ -60,9 +58,15 @@ def outerObjective(x, pMap, settings, arap_fn=None, device=0):
     # when a test substitutes the solver (arap_fn)
     pe = metrics.pixels_stand_dev(clone) if arap_fn is not None else _ctx(device).pixels_stand_dev(clone)
 
-    def lg2(v):
-        return math.log(v) ** 2 if v > 0 else math.inf
-    return lg2(pe["desvc1"]) + lg2(pe["desvc2"])
+    return _log2(pe["desvc1"]) + _log2(pe["desvc2"])
+
+
+def _log2(v):
+    """std::pow(std::log(v), 2) (nloptOptimization.cc:31-32): +inf at 0, NaN below 0 or for NaN."""
+    import math
+    if v != v or v < 0:
+        return math.nan
+    return math.inf if v == 0 else math.log(v) ** 2
 
 
 def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=None, device=0, log=None,
@@ -80,7 +84,6 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
     arapOptimization with another implementation of the same signature; `workers`
     (deftri.workers.ObjectiveWorkers) evaluates each Nelder-Mead step's candidate points on several
     GPUs at once (the search and its result are those of the sequential run); both use the host loop."""
-    import copy
     from .nlopt_nm import nelder_mead
     settings.validate_for_solver()
     if native and arap_fn is None and workers is None:
@@ -90,7 +93,7 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
             info = {"round": k + 1, "weights": r["round_weights"][k] if k < 64 else r["weights"],
                     "update": r["round_update"][k] if k < 64 else r["update"],
                     "evaluations": [e for e in r["evaluations"] if e["round"] == k + 1]}
-            if k == r["rounds"] - 1 and settings.selection == "twoOptimizations":
+            if k == r["rounds"] - 1 and settings.selection == "twoOptimizations" and settings.weights_selection == "nlopt":
                 info.update({"minf": r["minf"], "nlopt_result": r["nlopt_result"]})
             rounds.append(info)
             if log:
@@ -98,9 +101,10 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
         return rounds
     if settings.selection == "open3DArap":
         raise NotImplementedError("open3DArap is a different algorithm (Open3D DeformAsRigidAsPossible), out of scope")
-    if settings.selection == "twoOptimizations" and settings.weights_selection != "nlopt":
-        raise NotImplementedError("twoOptimizations with the Eigen LM weight search (EigenOptimization.h) is not "
-                                  "built: its functor declares 2 inputs but reads 3 (SURVEY §2 row 3); use nlopt")
+    # weightsSelection other than "nlopt" (the Eigen LM, :531-564): Eigen::LevenbergMarquardt::minimize
+    # returns ImproperInputParameters before any evaluation (the functor declares 2 values for the 3
+    # weights, m < n, EigenOptimization.h:31), so the round is arapOptimization at the unchanged weights
+    search = settings.selection == "twoOptimizations" and settings.weights_selection == "nlopt"
 
     def run_arap(m, rep, glob, arap):
         if arap_fn is not None:
@@ -116,8 +120,8 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
     i = 1
     while i <= settings.n_optimizations and update >= 0.0001 * n_mp:
         info = {"round": i}
-        if settings.selection == "twoOptimizations":
-            base = copy.deepcopy(pMap)            # optData.pMap = pMap->clone()
+        if search:
+            base = pMap.clone()                   # optData.pMap = pMap->clone()
             evals = []
             prefetch = None
             if workers is not None and arap_fn is None:
@@ -129,6 +133,8 @@ def deformationOptimization(pMap, settings, originalPoints=None, movedPoints=Non
                 [settings.nlopt_rep_ub, settings.nlopt_global_ub, settings.nlopt_arap_ub],
                 xtol_rel=settings.nlopt_rel_tol, xtol_abs=settings.nlopt_abs_tol,
                 maxeval=int(settings.nlopt_iterations), log=evals.append, prefetch=prefetch)
+            if res < 0:        # nlopt::opt::optimize throws on a failure code (before :525)
+                raise RuntimeError(f"nlopt failure (result {res}) in round {i}")
             rep_w, glob_w, arap_w = (float(v) for v in x)
             info.update({"weights": [rep_w, glob_w, arap_w], "minf": minf, "nlopt_result": res,
                          "evaluations": evals})
