@@ -54,8 +54,10 @@ private:
     deftri_map m_{};
 };
 
-// the solver report of this thread's last arapOptimization (zeroed before each call)
+// the solver report of this thread's last arapOptimization, or of the last optimize() of its last
+// bundle-adjustment call (zeroed before each call); report_slot() is where the adapter writes it
 const deftri_report &last_report();
+deftri_report &report_slot();
 // the report of this thread's last deformationOptimization round
 const deftri_deformation_report &last_deformation_report();
 

@@ -124,7 +124,8 @@ void bundleAdjustment(Map *pMap) {
     }
     const deftri_ba_desc d = g.desc();
     deftri_lm_params p = lm_params(20);                                    // optimizer.optimize(20)
-    deftri_report r{};
+    deftri_report &r = deftri_adapter::report_slot();
+    r = deftri_report{};
     std::vector<double> poses(g.poses.size()), pts(g.points.size());
     if (!report(ba, deftri_ba_upload(ba, &d), "bundleAdjustment") ||
         !report(ba, deftri_ba_solve_lm(ba, &p, 0, &r), "bundleAdjustment") ||
@@ -160,7 +161,8 @@ void localBundleAdjustment(Map *pMap, ID currKeyFrameId) {
     const size_t nLocal = sLocalKeyFrames.size();
     const deftri_ba_desc d = g.desc();
     const size_t E = g.edge_point.size();
-    deftri_report r{};
+    deftri_report &r = deftri_adapter::report_slot();
+    r = deftri_report{};
     deftri_lm_params p5 = lm_params(5), p10 = lm_params(10);
     std::vector<double> chi(E);
     std::vector<uint8_t> dpos(E), level(E), robust(E, 0);
@@ -214,7 +216,8 @@ int poseOnlyOptimization(Frame &currFrame) {
     }
     std::vector<double> chi(E);
     deftri_lm_params p10 = lm_params(10);
-    deftri_report r{};
+    deftri_report &r = deftri_adapter::report_slot();
+    r = deftri_report{};
     // 4 rounds: reset the pose, initializeOptimization(0), optimize(10), reclassify (:189-228).  The
     // guard before computeError() reads vInlier[round] instead of vInlier[j] (:196-197): edges j <=
     // round are checked against vInlier[round] as it was before edge `round` is reclassified, later

@@ -64,6 +64,7 @@ deftri_ba_ctx *ba_context() {
 }
 
 const deftri_report &last_report() { return t_report; }
+deftri_report &report_slot() { return t_report; }
 const deftri_deformation_report &last_deformation_report() { return t_def_report; }
 
 void se3quat7(const Sophus::SE3f &T, double out[7]) {
@@ -191,7 +192,7 @@ void arapOptimization(Map *pMap, double repBalanceWeight, double globalBalanceWe
     if (!ctx) return;                                                      // map unchanged
     MapView view(pMap);
     double update = 0.0;
-    deftri_report &rep = const_cast<deftri_report &>(deftri_adapter::last_report());
+    deftri_report &rep = deftri_adapter::report_slot();
     rep = deftri_report{};
     const int rc = deftri_arap_optimization(ctx, view.map(), repBalanceWeight, globalBalanceWeight, arapBalanceWeight,
                                             alphaWeight, betaWeight, DepthError, nOptIterations, &update, &rep);

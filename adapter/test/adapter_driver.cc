@@ -103,9 +103,13 @@ int main(int argc, char **argv) {
         extra = {pe.avgc1, pe.avgc2, pe.avg, pe.desvc1, pe.desvc2, pe.desv};
     } else if (mode == "ba") {
         bundleAdjustment(d.map.get());
+        const deftri_report &r = deftri_adapter::last_report();
+        extra = {r.chi2_initial, r.chi2_final, (double)r.iterations, (double)r.trials_total};
     } else if (mode == "localba") {
         if (argc < 5) return 2;
         localBundleAdjustment(d.map.get(), (ID)std::atol(argv[4]));
+        const deftri_report &r = deftri_adapter::last_report();
+        extra = {r.chi2_initial, r.chi2_final, (double)r.iterations, (double)r.trials_total};
     } else if (mode == "poseonly") {
         if (argc < 5) return 2;
         Frame &f = *d.frames.at((ID)std::atol(argv[4]));

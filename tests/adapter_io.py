@@ -8,7 +8,10 @@ from deftri import mapmodel
 
 
 def _pose_q(T):
-    """The fp32 quaternion (x, y, z, w) the Python model's pose carries (as7's source)."""
+    """The fp32 quaternion (x, y, z, w) the Python model's pose carries (as7's source), or the one a
+    test chose to dump for it (q_dump: the C++ model normalizes it into T.q)."""
+    if getattr(T, "q_dump", None) is not None:
+        return np.asarray(T.q_dump, np.float32)
     if T.q is not None:
         return np.asarray(T.q, np.float32)
     return mapmodel.quat_from_mat(T.R.astype(np.float64)).astype(np.float32)

@@ -7,6 +7,10 @@ subsample of the solved points (every 97th), sums of all coordinates, and the re
 (deterministic host code), so only these numbers are committed.
 
 Usage: python tests/golden/make_c2_golden.py   (about 45 minutes of one core)
+       python tests/golden/make_c2_golden.py realcolon 20
+           the same scene under Data/Realcolon.yaml's weights and distorted KB8 camera (bench.py's
+           regimes.realcolon: rep 1, arap 0.1, DepthWeight 0.001 -> sigma_d 1e-6 m), 20 iterations,
+           into c2_realcolon/ — a headline-size pin whose RMSE moves by whole pixels
 """
 import json
 import pathlib
@@ -23,26 +27,32 @@ from deftri import capi, metrics, sim               # noqa: E402
 from oracle import oracle                             # noqa: E402
 
 N_CORR, SEED, N_IT, STRIDE = 100000, 1, 6, 97
+# bench.py REGIMES: (rep, arap, sigma_d, camera)
+REGIMES = {"simulation": (1.0, 2e5, np.float32(3.0 / 1000.0), None),
+           "realcolon": (1.0, 0.1, np.float32(0.001) / np.float32(1000.0), "REALCOLON_KB8")}
 
 
-def main():
-    p, m = sim.two_view_problem(N_CORR, SEED, return_map=True)
+def main(regime="simulation", n_it=N_IT):
+    rep, arap, sig, kb8 = REGIMES[regime]
+    p, m = sim.two_view_problem(N_CORR, SEED, rep, arap, sig, return_map=True,
+                                kb8=getattr(sim, kb8) if kb8 else None)
     host = capi.Context(-1)
     host.analyse(p)
     oracle.set_vertex_order(host.vertex_order())
     t = time.time()
-    res = oracle.solve_lm(p, N_IT, analytic=False)
+    res = oracle.solve_lm(p, n_it, analytic=False)
     dt = time.time() - t
     R = res["report"]
     rms0 = metrics.pixels_stand_dev(m)
     metrics.apply_solution(m, list(p.point_ids), res["points"])
     rms1 = metrics.pixels_stand_dev(m)
-    d = HERE / "c2"
+    d = HERE / ("c2" if regime == "simulation" else "c2_" + regime)
     d.mkdir(exist_ok=True)
     pts = res["points"]
     np.savez_compressed(d / "expected_c2.npz", points_sub=pts[::STRIDE], chi2_iter=np.array(R["chi2_iter"]),
                         trials_iter=np.array(R["trials_iter"]))
-    meta = {"n_corr": N_CORR, "seed": SEED, "n_iterations": N_IT, "stride": STRIDE,
+    meta = {"n_corr": N_CORR, "seed": SEED, "n_iterations": n_it, "stride": STRIDE, "regime": regime,
+            "weights": {"rep": rep, "arap": arap, "depth_sigma": float(sig), "camera": kb8 or "SIM_KB8"},
             "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"], "lambda_final": R["lambda_final"],
             "iterations": R["iterations"], "trials_total": R["trials_total"],
             "point_sum": pts.sum(0).tolist(), "scales": res["scales"].tolist(), "tg": res["tg"].tolist(),
@@ -53,4 +63,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "simulation", int(sys.argv[2]) if len(sys.argv) > 2 else N_IT)

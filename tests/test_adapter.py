@@ -170,10 +170,29 @@ def test_arap_optimization_and_pixels_match_host_mirror(bindir, tmp_path):
     assert got == [pe[k] for k in ("avgc1", "avgc2", "avg", "desvc1", "desvc2", "desv")]
 
 
+def _exact_float_poses(m):
+    """Make the Python model's pose the one the C++ model will hold: the dump carries an fp32
+    quaternion q0, which Sophus (the model's SO3) normalizes on construction in fp32 (q0 times
+    1 / sqrt(((x² + y²) + z²) + w²)); the Python pose takes that normalized q1, so both sides read the
+    same pose bit for bit.  Monocular BA with one fixed keyframe keeps a free scale, and an ulp of
+    difference in the start moves the points along it."""
+    from deftri import mapmodel
+    f = np.float32
+    for kf in m.keyframes.values():
+        q0 = mapmodel.quat_from_mat(kf.pose.R.astype(np.float64)).astype(f)
+        n2 = f(f(f(q0[0] * q0[0] + q0[1] * q0[1]) + q0[2] * q0[2]) + q0[3] * q0[3])
+        inv = f(f(1.0) / np.sqrt(n2))
+        q1 = (q0 * inv).astype(f)
+        kf.pose.q_dump = q0
+        kf.pose.q = q1
+        kf.pose.R = mapmodel.mat_from_quat(q1.astype(np.float64)).astype(f)
+
+
 @pytest.mark.gpu
 def test_ba_entry_points_match_host_mirror(bindir, tmp_path):
     from deftri import ba
     m, _ = ba.simulate_ba_map(n=300, k=4, seed=5, outliers=0.05, visibility=0.9)
+    _exact_float_poses(m)
     for mode, args in (("ba", []), ("localba", [1])):
         mm = copy.deepcopy(m)
         write_map(tmp_path / f"{mode}.bin", mm)

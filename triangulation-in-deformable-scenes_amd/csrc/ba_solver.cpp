@@ -30,6 +30,7 @@
 
 #include "../../include/deftri.h"
 #include "ba.h"
+#include "exit_guard.h"
 
 using namespace deftri;
 
@@ -249,6 +250,8 @@ float ev_ms(deftri_ba_ctx *ctx, int a, int b) {
 
 }  // namespace
 
+using LiveBa = deftri::LiveContexts<deftri_ba_ctx, deftri_ba_destroy>;
+
 extern "C" {
 
 int deftri_ba_create(int32_t device, deftri_ba_ctx **out) {
@@ -268,12 +271,14 @@ int deftri_ba_create(int32_t device, deftri_ba_ctx **out) {
         delete ctx;
         return DEFTRI_E_HIP;
     }
+    LiveBa::add(ctx);
     *out = ctx;
     return 0;
 }
 
 int deftri_ba_destroy(deftri_ba_ctx *ctx) {
     if (!ctx) return 0;
+    LiveBa::remove(ctx);
     hipSetDevice(ctx->device);
     if (ctx->st) hipStreamSynchronize(ctx->st);
     free_device(ctx);

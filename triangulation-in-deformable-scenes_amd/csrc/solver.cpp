@@ -30,6 +30,7 @@
 #include "kernels.h"
 #include "pcg.h"
 #include "spcg.h"
+#include "exit_guard.h"
 #include "symbolic.h"
 
 using namespace deftri;
@@ -1034,6 +1035,8 @@ float ev_ms(deftri_ctx *ctx, int a, int b) {
 // ==========================================================================================
 // C-ABI
 // ==========================================================================================
+using LiveCtx = deftri::LiveContexts<deftri_ctx, deftri_ctx_destroy>;
+
 extern "C" {
 
 int deftri_abi_version(void) { return DEFTRI_ABI_VERSION; }
@@ -1075,6 +1078,7 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
         deftri_ctx_destroy(ctx);
         return DEFTRI_E_HIP;
     }
+    LiveCtx::add(ctx);
     *out = ctx;
     return 0;
 }
@@ -1082,6 +1086,7 @@ int deftri_ctx_create(int32_t device, deftri_ctx **out) {
 int deftri_ctx_destroy(deftri_ctx *ctx) {
     if (!ctx) return 0;
     if (ctx->device < 0) { delete ctx; return 0; }
+    LiveCtx::remove(ctx);
     hipSetDevice(ctx->device);
     free_device(ctx);
     ctx->gdev.reset();

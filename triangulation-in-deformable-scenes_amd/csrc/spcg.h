@@ -129,7 +129,7 @@ struct SpPlanHost {
     std::vector<int32_t> tile_halo;                    // the tiles' halo rows (global row ids)
     std::vector<int32_t> tile_xoff;                    // per own row its cross slots (destination order)
     std::vector<int32_t> tile_xdst;                    // per cut entry (source order): its 2 cross slots
-    double tile_bytes[3] = {0, 0, 0};                  // algorithmic bytes per CG iteration: product, update; fused
+    double tile_bytes[2] = {0, 0};                     // algorithmic bytes per CG iteration: product, update
 };
 // the groups and rows build_tiles needs (spcg_plan.cpp step 5)
 struct TileInput {
@@ -265,9 +265,6 @@ struct SpDev {
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     const int32_t *p1list = nullptr;                      // sharded phase 1: the launch's workgroups -> logical ones
-    int32_t tile_fuse = 0;                                // tile mode: the update in the product's (cooperative) launch
-    int32_t tglin = 0, tglin_lds = 0;                    // tile mode: the rows' ARAP blocks by tiles (k_sp_tglin)
-    double *ht = nullptr;                                 // k_sp_tglin's per-row sums [9][nown] (H lower 6, b 3)
     int32_t txb_fold = 0;                                 // sharded tiles: xb by k_sp_tile's last workgroup
     int32_t tparts = 0;                                   // tile mode: each k_sp_tile workgroup sums the update's
                                                           // (r.z, r.r) partials itself (no ticket chain in k_sp_tupd)
@@ -296,7 +293,6 @@ void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_
 // (list: the launch's logical workgroups, n of them — nullptr / t_grid: all; txb: then k_sp_txb)
 void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n,
                        bool txb);
-int sp_tile_coop_capacity(int lds, int device);   // resident k_sp_tile<*, 1> workgroups (0: no cooperative launch)
 void sp_launch_update_sd(const SpDev &G, int it, double lambda, int tail, hipStream_t st);
 // sharded chain, phase 1 over `n` of its logical workgroups (list: their indices; nullptr: all, n =
 // sp_merged_grid1) and phase 2
@@ -340,7 +336,7 @@ class SpSolver {
     // the rows' p.(D + lambda)p terms ((z, p) and D in) and the heavy p (in, out), phase 2 the update
     // (x, r in / out and M in per row, q no longer stored)
     double product_bytes_phase(int k) const {
-        if (G.tile) return G.tile_fuse && !G.alpha_kernel ? (k == 1 ? H.tile_bytes[2] : 0.0) : H.tile_bytes[k == 1 ? 0 : 1];
+        if (G.tile) return H.tile_bytes[k == 1 ? 0 : 1];
         if (k == 1) return H.phase1_bytes + (G.merged ? (double)G.nown * (48 + 48) + (double)G.hd * (16 + 8) : 0.0);
         return H.phase2_bytes + (G.merged ? (double)G.nown * (24 + 24 + 24 + 24 + 48 - 24) : 0.0);
     }
@@ -361,7 +357,6 @@ class SpSolver {
     int32_t n_tiles() const { return G.tile ? G.ntile : 0; }
     bool halo_overlap() const { return G.sd && G.ovl; }
     int32_t cg_launches() const {     // per CG iteration: [dots], phase 1, phase 2, [heavy x 1-2], update
-        if (G.tile && G.tile_fuse && !G.alpha_kernel) return 1;   // tile mode: product + update, one launch
         if (G.sd) return 3;                      // + one all-reduce and one grouped send / receive
         if (G.merged) return G.alpha_kernel ? 3 : 2;
         const int heavy = G.fuse_heavy ? 0 : (nranks_ > 1 || G.heavy_split) ? 2 : 1;

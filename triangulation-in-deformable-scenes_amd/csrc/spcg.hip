@@ -403,7 +403,7 @@ __global__ void __launch_bounds__(256) k_sp_maxdiag(const SpDev G, double *out, 
     if (gated_off(G.lgate)) return;
     double m = 0.0;
     if (stage == 0) {
-        for (int i = threadIdx.x; i < (G.tglin ? sp::row_grid(G.nrb) : G.nrb2); i += 256) m = fmax(m, G.mpart[i]);
+        for (int i = threadIdx.x; i < G.nrb2; i += 256) m = fmax(m, G.mpart[i]);
     } else {
         for (int h = threadIdx.x; h < G.Q; h += 256)
 #pragma unroll
@@ -726,7 +726,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
         }
     }
     // tile mode (G.tparts, the update unfused): the first product's workgroups sum the partials
-    if (G.fuse && !(G.tparts && !G.tile_fuse) && last_block(G, G.cnt + 32)) {
+    if (G.fuse && !G.tparts && last_block(G, G.cnt + 32)) {
         // (a bad block recorded by any workgroup stops every later launch through rec[0], which the
         // next launch sees; the sums formed here are then never read)
         __syncthreads();
@@ -1766,13 +1766,7 @@ __device__ __forceinline__ void tile_sd_tail(const SpDev &G, double *lds, double
     }
 }
 
-// FU 1 (opt-in, DEFTRI_SP_TILE_FUSE=1, when the grid is co-resident: a cooperative launch): the update follows in the
-// same launch — every workgroup publishes its sums, the last to arrive forms alpha (phase 2's
-// workgroup-0 arithmetic: the same partials, the same order) and publishes it, the others wait for it;
-// then each tile updates its own rows from the q it holds (+ its cross slots, written agent-coherent)
-// and the heavy workgroup the heavy dofs, and the (r.z, r.r) of iteration it + 1 are summed as in
-// k_sp_tupd.  One launch per CG iteration; no q stored.
-template <class JT, int FU, int SD = 0>
+template <class JT, int SD = 0>
 __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     extern __shared__ double lds[];
     __shared__ double red[9][4];
@@ -1810,32 +1804,26 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         // sharded single-reduction chain: the product is A z (beta 0); the state is the update's
         beta = 0.0;
         if (G.rec[0] != 0.0) return;
-    } else if (!FU && G.tparts && (it > 0 || !G.tile_fuse)) {
+    } else if (G.tparts) {
         if (tile_state(G, it, beta, reinterpret_cast<double(*)[4]>(&red[0][0]))) return;
-    } else if (const int st = it_state(G, it, beta)) {
-        if (FU && blockIdx.x == 0 && threadIdx.x == 0) record_stop(G, it, st);
+    } else if (it_state(G, it, beta)) {
         return;
     }
     double pap = 0.0, jts[6] = {0, 0, 0, 0, 0, 0}, sacc[2] = {0, 0};
-    double qk[3] = {0, 0, 0}, pk[3] = {0, 0, 0}, phv = 0.0;     // FU: the row's q and p (tid < nr), heavy p
-    int lrow = -1;
     if (heavy_wg) {                                // the heavy dofs: p for the update, lambda |p_h|^2
         for (int64_t dd = tid; dd < G.hd; dd += 256) {
             const double p = pval(G.zp, beta, dd);
             G.ph[dd] = p;
-            phv = p;
             pap += lam * (p * p);
         }
         if (!G.include_heavy) pap = 0.0;
-        if (!FU) {
-            pap = block_sum(pap, red[0]);
-            if (tid == 0) {
-                if (SD && G.txb_fold) publish(G, G.m1part + b, pap);
-                else G.m1part[b] = pap;
-            }
-            if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
-            return;
+        pap = block_sum(pap, red[0]);
+        if (tid == 0) {
+            if (SD && G.txb_fold) publish(G, G.m1part + b, pap);
+            else G.m1part[b] = pap;
         }
+        if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
+        return;
     }
     if (t < G.ntile) {
         double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
@@ -1889,13 +1877,8 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
                     const int2 xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
-                        if (FU) {                  // read by other workgroups in this launch
-                            st_sc1(G.xc + 3 * (int64_t)xd.x + c, J[6 + c] * s);
-                            st_sc1(G.xc + 3 * (int64_t)xd.y + c, J[9 + c] * s);
-                        } else {
-                            G.xc[3 * (int64_t)xd.x + c] = J[6 + c] * s;
-                            G.xc[3 * (int64_t)xd.y + c] = J[9 + c] * s;
-                        }
+                        G.xc[3 * (int64_t)xd.x + c] = J[6 + c] * s;
+                        G.xc[3 * (int64_t)xd.y + c] = J[9 + c] * s;
                     }
                 } else {
                     const int s0 = (int)(m.y & 0xfffu), s1 = (int)((m.y >> 12) & 0xfffu);
@@ -1951,14 +1934,8 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += cd[c] * ps;
             }
-            if (FU) {
-                lrow = l;
 #pragma unroll
-                for (int c = 0; c < 3; c++) { qk[c] = q[c]; pk[c] = p[c]; }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
-            }
+            for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
         }
     }
     // [p.Ap, J_T^T s, scale sums]: wave butterflies, then the waves in order
@@ -1971,115 +1948,11 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     __syncthreads();
     if (tid < 9) {
         const double v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        if (FU || (SD && G.txb_fold)) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
+        if (SD && G.txb_fold) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
         else if (tid == 0) G.m1part[b] = v;
         else G.part[(int64_t)kSpPart * b + tid - 1] = v;
     }
-    if (!FU && SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
-    if constexpr (FU == 1) {
-        // the arrival: every thread's stores (cross slots, partials) acknowledged, then one ticket
-        __shared__ int s_last;
-        __shared__ double s_alpha;
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_waitcnt(0);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __syncthreads();
-        if (tid == 0)
-            s_last = __hip_atomic_fetch_add(G.cnt + 44, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-        __syncthreads();
-        if (s_last) {
-            // alpha as m2_alpha_make forms it: thread t adds partials t, t + 256, ..., then the block
-            double acc = 0.0;
-            for (int j = tid; j < (int)gridDim.x; j += 256) acc += fetch(G.m1part + j);
-            acc = block_sum(acc, red[0]);
-            if (tid == 0) {
-                double alpha = G.red[(int64_t)kSpRed * it] / acc;
-                if (!(acc > 0.0) || !isfinite(alpha) || alpha == 0.0) {
-                    st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpBreakdown);
-                    alpha = __builtin_nan("");
-                }
-                st_sc1(G.cnt + 44, 0);
-                st_sc1(G.red + (int64_t)kSpRed * it + 3, alpha);
-                s_alpha = alpha;
-            }
-        } else if (tid == 0) {
-            const double *w = G.red + (int64_t)kSpRed * it + 3;
-            int n = it == G.inj_timeout_it ? (1 << 16) : 0;
-            double v = ld_sc1(w);
-            while (__double_as_longlong(v) == 0 && n < (1 << 16)) {
-                __builtin_amdgcn_s_sleep(2);
-                v = ld_sc1(w);
-                n++;
-            }
-            if (n >= (1 << 16)) {                  // never expected: stop the solve, skip the update
-                st_sc1(G.red + (int64_t)kSpRed * (it + 1) + 2, (double)kSpTimeout);
-                v = __builtin_nan("");
-            }
-            s_alpha = v;
-        }
-        __syncthreads();
-        const double alpha = s_alpha;
-        double pq = 0.0, rr2 = 0.0;
-        if (heavy_wg) {
-            // k_sp_tupd's heavy update, one heavy vertex after the other
-            __shared__ double rsh[6], tz[2][6];
-            for (int h = 0; h < G.Q + G.S; h++) {
-                const double th = tile_heavy_sum(G, h, lds, true);   // (the tile LDS is free here)
-                const int dim = h < G.Q ? 6 : 1, o = heavy_dof(G, h);
-                const int aa = isnan(alpha) ? dim : tid;
-                double p = 0.0, r = 0.0;
-                if (aa < dim) {
-                    p = G.ph[o + aa];
-                    const double q = th + lam * p;
-                    G.x[o + aa] += alpha * p;
-                    r = G.r[o + aa] - alpha * q;
-                    G.r[o + aa] = r;
-                    rsh[aa] = r;
-                }
-                __syncthreads();
-                if (aa < dim) {
-                    const double *Mh = h < G.Q ? G.Mh + 36 * (int64_t)h + aa * 6 : G.Mh + 36 * (int64_t)G.Q + (h - G.Q);
-                    double z = 0.0;
-                    for (int c = 0; c < dim; c++) z += Mh[c] * rsh[c];
-                    G.zp[o + aa] = make_double2(z, p);
-                    tz[0][aa] = r * z;
-                    tz[1][aa] = r * r;
-                }
-                __syncthreads();
-                if (tid == 0 && !isnan(alpha))
-                    for (int c = 0; c < dim; c++) { pq += tz[0][c]; rr2 += tz[1][c]; }
-                __syncthreads();
-            }
-            (void)phv;
-        } else if (lrow >= 0 && !isnan(alpha)) {
-            const int l = lrow;
-            const int64_t o = G.hd + 3 * (int64_t)l;
-            for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) qk[c] += fetch(G.xc + 3 * (int64_t)k + c);
-            double M[6], r[3], z[3];
-#pragma unroll
-            for (int k = 0; k < 6; k++) M[k] = G.Mv[6 * (int64_t)l + k];
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                G.x[o + c] = G.x[o + c] + alpha * pk[c];
-                r[c] = G.r[o + c] - alpha * qk[c];
-            }
-            z[0] = M[0] * r[0] + M[1] * r[1] + M[3] * r[2];
-            z[1] = M[1] * r[0] + M[2] * r[1] + M[4] * r[2];
-            z[2] = M[3] * r[0] + M[4] * r[1] + M[5] * r[2];
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                G.r[o + c] = r[c];
-                G.zp[o + c] = make_double2(z[c], pk[c]);
-                pq += r[c] * z[c];
-                rr2 += r[c] * r[c];
-            }
-        }
-        __syncthreads();                           // (red is free again)
-        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
-        m2_dots(G, it, red);
-    }
+    if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
 }
 
 // FIN 0: the CG update of iteration it (merged-chain hand-off); FIN 1: the product only — q of every
@@ -2226,173 +2099,6 @@ __global__ void __launch_bounds__(256) k_sp_txb(int it, const SpDev G) {
     }
 }
 
-// ---- tile mode, per LM iteration: the rows' ARAP blocks by tiles --------------------------------------
-// k_sp_tglin, one workgroup per tile (k_sp_tile's dealing, no heavy workgroup): every ARAP edge of the
-// tile is read once (J columns 0..11, e) — the own rows' W J_a J_a^T (lower 6) and -J_a W e (3) summed
-// over the vertex's lanes (segmented scan, as the product's), each in-tile j row's slice (J_j, e) into
-// its LDS slot, a cut edge's two into their cross slots; then per tile row: own + its slots' terms ->
-// ht [9][nown].  k_sp_tglin_rows: per row the reprojection / depth terms (D_v, c_e, W J_s^2 as
-// k_sp_glin_rows forms them), H_v = D_v + ht + the row's cross slots' terms, b_v, the max diagonal.
-// A slot's terms use k_sp_glin_rows' per-slot arithmetic (ja = J_a W; H += ja J_c; b -= J_a (W e)); the
-// sums' order differs from k_sp_glin_rows' (rounding-level differences in H_v, b_v).
-__device__ __forceinline__ void tg_terms(const double *v, double W, double e, double *o) {
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const double ja = v[a] * W;
-#pragma unroll
-        for (int c = 0; c <= a; c++) o[tri3(a, c)] = ja * v[c];
-        o[6 + a] = -(v[a] * (W * e));
-    }
-}
-
-__global__ void __launch_bounds__(256) k_sp_tglin(const SpDev G) {
-    extern __shared__ double lds[];
-    if (gated_off(G.lgate)) return;
-    const int b = (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int seg = (G.ntile + 7) / 8;
-    const int t = (b & 7) * seg + (b >> 3);
-    if (t >= G.ntile) return;
-    const int32_t *T = G.ttab + 8 * (int64_t)t;
-    const int r0 = T[0], nr = T[1], e0 = T[3], ne = T[4];
-    double *up = lds, *rs = up + 9 * nr;                     // own rows [nr][9]; slots [ns][4] (J_j, e)
-    for (int i = tid; i < 9 * nr; i += 256) up[i] = 0.0;
-    __syncthreads();
-    const double W = G.pinfo[0];
-    const int64_t jld = G.jld;
-    const uint64_t lt = (1ull << lane) - 1;
-    for (int base = 0; base < ne; base += 256) {
-        if (base + 64 * wv >= ne) break;           // (ne is a multiple of 64: whole waves in or out)
-        const int64_t k = (int64_t)e0 + base + tid;
-        const uint2 m = G.tmeta[k];
-        const int2 ch = G.tchunk[k >> 6];
-        const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
-        const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
-        const int le = ch.x + __popcll(vm & lt);
-        double J[12];
-#pragma unroll
-        for (int c = 0; c < 12; c++) J[c] = valid ? G.Ja[c * jld + le] : 0.0;
-        const double e = valid ? G.Ea[le] : 0.0;
-        const int ub = (int)(m.y >> 24), sw = (int)((m.x >> 26) & 1u);
-        const int ra = valid ? ub + sw : 0, rb = valid ? ub + 1 - sw : 0;
-        if (valid) {
-            if (cut) {
-                const int2 xd = G.txdst[(int64_t)ch.y / 2 + __popcll(cm & lt)];
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    G.xc[4 * (int64_t)xd.x + c] = J[6 + c];
-                    G.xc[4 * (int64_t)xd.y + c] = J[9 + c];
-                }
-                G.xc[4 * (int64_t)xd.x + 3] = e;
-                G.xc[4 * (int64_t)xd.y + 3] = e;
-            } else {
-                const int s0 = (int)(m.y & 0xfffu), s1 = (int)((m.y >> 12) & 0xfffu);
-#pragma unroll
-                for (int c = 0; c < 3; c++) { rs[4 * s0 + c] = J[6 + c]; rs[4 * s1 + c] = J[9 + c]; }
-                rs[4 * s0 + 3] = e;
-                rs[4 * s1 + 3] = e;
-            }
-        }
-        // the own rows' terms: inclusive segmented scan over the vertex's lanes, the last lane stores
-        double v[18];
-        tg_terms(J, W, e, v);
-        tg_terms(J + 3, W, e, v + 9);
-        if (!valid)
-#pragma unroll
-            for (int c = 0; c < 18; c++) v[c] = 0.0;
-        const int sstart = 63 - __clzll(hm & (lt | (1ull << lane)));
-        for (int d = 1; d < G.tile_segmax; d <<= 1) {
-#pragma unroll
-            for (int c = 0; c < 18; c++) {
-                const double y = shfl_up_d(v[c], d);
-                if (lane - d >= sstart) v[c] += y;
-            }
-        }
-        if (valid && (m.x & kTmLast)) {
-#pragma unroll
-            for (int c = 0; c < 9; c++) { up[9 * ra + c] = v[c]; up[9 * rb + c] = v[9 + c]; }
-        }
-    }
-    __syncthreads();
-    if (tid < nr) {
-        const int l = r0 + tid;
-        double acc[9];
-#pragma unroll
-        for (int c = 0; c < 9; c++) acc[c] = up[9 * tid + c];
-        const int rsi = G.trs[l], sb = rsi & 0xffff, sc = rsi >> 16;
-        for (int kk = sb; kk < sb + sc; kk++) {
-            double o[9];
-            tg_terms(rs + 4 * kk, W, rs[4 * kk + 3], o);
-#pragma unroll
-            for (int c = 0; c < 9; c++) acc[c] += o[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 9; c++) G.ht[(int64_t)c * G.nown + l] = acc[c];
-    }
-}
-
-__global__ void __launch_bounds__(256) k_sp_tglin_rows(const SpDev G) {
-    __shared__ double red4[4];
-    if (gated_off(G.lgate)) return;
-    const int lb = row_block((int)blockIdx.x, G.nrb);
-    const int l = lb * 256 + (int)threadIdx.x;
-    double mx = 0.0;
-    if (l < G.nown) {
-        double D[6] = {0, 0, 0, 0, 0, 0}, bb[3] = {0, 0, 0};
-        for (int j = G.rep_off[l]; j < G.rep_off[l + 1]; j++) {     // reprojection: 2 x 3, W scalar
-            const double *J = G.Jr + 6 * (int64_t)j;
-            const double wt = G.Wr[j];
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const double er = G.Er[2 * (int64_t)j + r];
-#pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    const double ja = J[3 * r + a] * wt;
-#pragma unroll
-                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[3 * r + c];
-                    bb[a] -= J[3 * r + a] * (wt * er);
-                }
-            }
-        }
-        for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
-            const double *J = G.Jd + 4 * (int64_t)j;
-            const double wt = G.Wd[j], er = G.Ed[j];
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                const double ja = J[a] * wt;
-#pragma unroll
-                for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
-                bb[a] -= J[a] * (wt * er);
-                G.cdep[3 * (int64_t)j + a] = ja * J[3];
-            }
-            G.wss[j] = (J[3] * wt) * J[3];
-        }
-        double H[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) H[k] = D[k] + G.ht[(int64_t)k * G.nown + l];
-#pragma unroll
-        for (int a = 0; a < 3; a++) bb[a] += G.ht[(int64_t)(6 + a) * G.nown + l];
-        const double W = G.pinfo[0];
-        for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++) {           // the row's cross slots
-            const double *x = G.xc + 4 * (int64_t)k;
-            double o[9];
-            tg_terms(x, W, x[3], o);
-#pragma unroll
-            for (int c = 0; c < 6; c++) H[c] += o[c];
-#pragma unroll
-            for (int a = 0; a < 3; a++) bb[a] += o[6 + a];
-        }
-#pragma unroll
-        for (int k = 0; k < 6; k++) { G.Hv[6 * (int64_t)l + k] = H[k]; G.Dv[6 * (int64_t)l + k] = D[k]; }
-        const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-#pragma unroll
-        for (int a = 0; a < 3; a++) G.b[o + a] = bb[a];
-        mx = fmax(fabs(H[0]), fmax(fabs(H[2]), fabs(H[5])));
-    }
-    mx = wave_max(mx);
-    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) G.mpart[blockIdx.x] = fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
-}
 
 // halo exchange: rows' values (width doubles per row at base + width * row) into / out of a buffer
 __global__ void k_sp_pack(int n, const int32_t *__restrict__ rows, int width, int64_t base, const double *__restrict__ src,
@@ -2458,10 +2164,7 @@ static void launch_phase2(const SpDev &G, int grid, int it, double lambda, const
 }
 
 void sp_launch_glin(const SpDev &G, bool fp32, hipStream_t st) {
-    if (G.tglin) {
-        SPLS("sp_tglin", sp::k_sp_tglin, 8 * ((G.ntile + 7) / 8), G.tglin_lds, G);
-        SPL("sp_tglin_rows", sp::k_sp_tglin_rows, sp::row_grid(G.nrb), G);
-    } else if (G.glu == 4) {
+    if (G.glu == 4) {
         if (fp32) SPL("sp_glin_rows", (sp::k_sp_glin_rows<float, 4>), sp::row_grid(G.nrb2), G, G.pj32);
         else SPL("sp_glin_rows", (sp::k_sp_glin_rows<double, 4>), sp::row_grid(G.nrb2), G, G.pj);
     } else if (G.glu == 6) {
@@ -2509,37 +2212,8 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     if (G.tile) {
         // [tiles, XCD-dealt][heavy dofs]; [m_nh heavy workgroups][row blocks]
         hipEvent_t e0_ = prof_begin(st);
-        if (G.tile_fuse && !G.alpha_kernel) {
-            // one cooperative launch (every workgroup resident: the update waits on all of them)
-            int it_ = it;
-            SpDev g_ = G;
-            double lam_ = lambda;
-            hipError_t e;
-            if (fp32) {
-                const float *j_ = G.Ja32;
-                void *args[] = {&it_, &g_, &j_, &lam_};
-                e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&sp::k_sp_tile<float, 1>), dim3(G.t_grid), dim3(256),
-                                               args, (unsigned)G.tile_lds, st);
-            } else {
-                const double *j_ = G.Ja;
-                void *args[] = {&it_, &g_, &j_, &lam_};
-                e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&sp::k_sp_tile<double, 1>), dim3(G.t_grid), dim3(256),
-                                               args, (unsigned)G.tile_lds, st);
-            }
-            if (e == hipSuccess) {
-                prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
-                return;
-            }
-            // refused (the grid not resident at once): nothing ran — the separate update launch below
-            (void)hipGetLastError();
-            static bool warned = false;
-            if (!warned) {
-                std::fprintf(stderr, "[deftri] cooperative tile launch refused (%s): separate update launch\n", hipGetErrorString(e));
-                warned = true;
-            }
-        }
-        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja32, lambda);
-        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda);
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, it, G, G.Ja, lambda);
         prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
         if (G.alpha_kernel) SPL("sp_alpha", sp::k_sp_alpha, 1, it, G);
         SPL("sp_tupd", (sp::k_sp_tupd<0>), G.m_nh + sp::row_grid(G.nrb), it, G, lambda, last ? 1 : 0);
@@ -2566,26 +2240,14 @@ void sp_launch_product(const SpDev &G, int it, double lambda, bool fp32, hipStre
     else launch_phase2<double, 0>(G, grid, it, lambda, G.pj, st);
 }
 
-// workgroups of k_sp_tile<*, 1> the device keeps resident at once (a cooperative launch's limit)
-int sp_tile_coop_capacity(int lds, int device) {
-    int attr = 0;
-    if (hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess || !attr) return 0;
-    int nb = 0, nb32 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sp::k_sp_tile<double, 1>, 256, (size_t)lds) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb32, sp::k_sp_tile<float, 1>, 256, (size_t)lds) != hipSuccess) return 0;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
-    return std::min(nb, nb32) * prop.multiProcessorCount;
-}
-
 void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStream_t st, const int32_t *list, int n,
                        bool txb) {
     if (n > 0) {
         SpDev g = G;
         g.p1list = list;
         hipEvent_t e0_ = prof_begin(st);
-        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja32, lambda);
-        else hipLaunchKernelGGL((sp::k_sp_tile<double, 0, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
+        if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja32, lambda);
+        else hipLaunchKernelGGL((sp::k_sp_tile<double, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
         prof_end("sp_tile", e0_, (unsigned)n, 0.0, st);
     }
     if (txb && !G.txb_fold) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
@@ -2593,8 +2255,8 @@ void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStre
 
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {
     hipEvent_t e0_ = prof_begin(st);
-    if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda);
-    else hipLaunchKernelGGL((sp::k_sp_tile<double, 0>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda);
+    if (fp32) hipLaunchKernelGGL((sp::k_sp_tile<float>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja32, lambda);
+    else hipLaunchKernelGGL((sp::k_sp_tile<double>), dim3(G.t_grid), dim3(256), (size_t)G.tile_lds, st, 0, G, G.Ja, lambda);
     prof_end("sp_tile", e0_, (unsigned)G.t_grid, 0.0, st);
     SPL("sp_tupd", (sp::k_sp_tupd<1>), G.m_nh + sp::row_grid(G.nrb), 0, G, lambda, 1);
 }

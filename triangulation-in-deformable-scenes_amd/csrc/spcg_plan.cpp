@@ -626,7 +626,6 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                           (double)ndl * (24 + 8 + 4 + 4) + (double)H.tile_halo_rows * 48 + (double)H.tile_cross * (24 + 4);
         H.tile_bytes[1] = (double)nown * (96 + 48 + 48 + 24 + 48 + 8) + (double)H.tile_cross * 24;
         // fused (one launch): q stays in registers, p in LDS — no q out / in, no (z, p) reload
-        H.tile_bytes[2] = H.tile_bytes[0] - (double)nown * 24 + H.tile_bytes[1] - (double)nown * (48 + 24);
     }
     static const bool digest = std::getenv("DEFTRI_PLAN_DIGEST") != nullptr;
     if (digest) {

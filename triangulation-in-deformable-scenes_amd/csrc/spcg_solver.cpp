@@ -477,29 +477,11 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.tchunk = reinterpret_cast<const int2 *>(tch);
         G.tmeta = reinterpret_cast<const uint2 *>(tm);
         G.pinfo = P.pair_info;
-        ALLOC(G.xc, 4 * std::max<int64_t>(H.tile_cross, 1));    // (3 per slot in the product, 4 in k_sp_tglin)
-        // the linearization's ARAP row blocks by tiles: LDS 9 doubles per tile row + 4 per slot
-        int64_t tl = 0;
-        for (int32_t t = 0; t < H.ntile; t++) tl = std::max<int64_t>(tl, 8 * (9 * (int64_t)H.tile_tab[8 * t + 1] + 4 * (int64_t)H.tile_tab[8 * t + 6]));
-        // opt-in (DEFTRI_SP_TILE_GLIN=1): measured at C2 k_sp_tglin 46 + k_sp_tglin_rows 25 us against
-        // k_sp_glin_rows' 69 (DESIGN.md "Tile mode")
-        static const bool tglin = std::getenv("DEFTRI_SP_TILE_GLIN") != nullptr;
-        G.tglin = (tglin && tl <= 64 * 1024) ? 1 : 0;
-        G.tglin_lds = (int32_t)std::max<int64_t>(tl, 8);
-        if (G.tglin) ALLOC(G.ht, 9 * (int64_t)std::max(nown, 1));
-        // DEFTRI_SP_TILE_FUSE=1: the update in the product's launch when the whole grid is resident at
-        // once (a cooperative launch guarantees it or fails).  Not the default: measured at C2 on MI355X
-        // it is 85 us per CG iteration against 56 us for the two launches (the cooperative launch
-        // alone costs ~18 us; the fused kernel launched plainly still 68 us — the update's rows run
-        // at half a workgroup each behind a grid-wide wait).  DESIGN.md "Tile mode".
-        static const bool fuse_t = std::getenv("DEFTRI_SP_TILE_FUSE") != nullptr;
-        G.tile_fuse = (fuse_t && sp_tile_coop_capacity(G.tile_lds, dev_) >= G.t_grid) ? 1 : 0;
+        ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));    // 3 per cross slot
         // each product launch sums the last update's (r.z, r.r) partials itself; only the chain's
-        // last update takes the ticketed sum that records the state (DEFTRI_SP_TILE_TICKETS=1: every
-        // update does, round 4's merged-chain scheme)
-        static const bool tickets = std::getenv("DEFTRI_SP_TILE_TICKETS") != nullptr;
-        G.tparts = (tickets || G.sd) ? 0 : 1;
-        if (G.sd) G.tile_fuse = 0;
+        // last update takes the ticketed sum that records the state (the sharded chain's record is
+        // all-reduced instead)
+        G.tparts = G.sd ? 0 : 1;
         // sharded: the rank's record xb in its own small launch (k_sp_txb); DEFTRI_SP_TXB_FOLD=1 forms
         // it in the product's last workgroup instead (a ticket over both product launches) — the
         // same on the 2-rank gloo rehearsal (165.8 vs 171.8 LM it/s), so the simpler order stays

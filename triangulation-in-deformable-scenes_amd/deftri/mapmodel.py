@@ -89,7 +89,9 @@ class SE3f:
         q = (self.q if self.q is not None else self.unit_quaternion().astype(np.float32)).astype(np.float64)
         if q[3] < 0:
             q = -q
-        q = q / np.linalg.norm(q)
+        # SE3Quat::normalizeRotation in one fixed order of additions (the native se3f_as7 / the C++
+        # adapter's se3quat7 use the same)
+        q = q / np.sqrt(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3])
         return np.concatenate([q, self.t.astype(np.float64)])
 
     @staticmethod
