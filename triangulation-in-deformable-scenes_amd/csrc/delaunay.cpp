@@ -349,6 +349,31 @@ bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_s
     return true;
 }
 
+// the boundary cycle bnext (nb half-edges u -> bnext[u]) is one strictly convex polygon winding once:
+// with every turn in (0, pi), the edge direction passes angle 0 exactly when it moves from the lower
+// half-plane [pi, 2 pi) to the upper [0, pi) — sign tests on coordinate comparisons, exact — and a
+// simple convex polygon does that once (a strict left turn everywhere still admits a pentagram)
+static bool boundary_convex_once(const double *xy, int n, const std::vector<int32_t> &bnext, int nb) {
+    auto P = [&](int i) { return xy + 2 * (size_t)i; };
+    auto upper = [&](int a, int b) {           // direction a -> b in [0, pi)
+        const double *pa = P(a), *pb = P(b);
+        return pb[1] > pa[1] || (pb[1] == pa[1] && pb[0] > pa[0]);
+    };
+    int start = -1;
+    for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
+    if (start < 0) return false;
+    int u = start, len = 0, wraps = 0;
+    do {
+        const int v = bnext[u];
+        if (v < 0 || bnext[v] < 0) return false;
+        if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
+        if (!upper(u, v) && upper(v, bnext[v])) wraps++;
+        u = v;
+        if (++len > nb) return false;
+    } while (u != start);
+    return len == nb && wraps == 1;
+}
+
 bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &tris) {
     const int nt = (int)tris.size() / 3;
     if (n < 3 || nt == 0) return false;
@@ -395,53 +420,8 @@ bool delaunay_still_valid(const double *xy, int n, const std::vector<int32_t> &t
             }
         }
     }
-    // the boundary: one cycle, strictly convex.  A strict left turn at every vertex still admits a
-    // cycle that winds several times (a pentagram), so the winding is counted too: with every turn in
-    // (0, pi), the edge direction passes angle 0 exactly when it moves from the lower half-plane
-    // [pi, 2 pi) to the upper [0, pi) — sign tests on coordinate comparisons, exact — and a simple
-    // convex polygon does that once
-    auto upper = [&](int a, int b) {           // direction a -> b in [0, pi)
-        const double *pa = P(a), *pb = P(b);
-        return pb[1] > pa[1] || (pb[1] == pa[1] && pb[0] > pa[0]);
-    };
-    int start = -1;
-    for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
-    if (start < 0) return false;
-    int u = start, len = 0, wraps = 0;
-    do {
-        const int v = bnext[u];
-        if (v < 0 || bnext[v] < 0) return false;
-        if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
-        if (!upper(u, v) && upper(v, bnext[v])) wraps++;
-        u = v;
-        if (++len > nb) return false;
-    } while (u != start);
-    return len == nb && wraps == 1;
-}
-
-// the boundary cycle bnext (nb half-edges u -> bnext[u]) is one strictly convex polygon winding once:
-// with every turn in (0, pi), the edge direction passes angle 0 exactly when it moves from the lower
-// half-plane [pi, 2 pi) to the upper [0, pi) — sign tests on coordinate comparisons, exact — and a
-// simple convex polygon does that once (a strict left turn everywhere still admits a pentagram)
-static bool boundary_convex_once(const double *xy, int n, const std::vector<int32_t> &bnext, int nb) {
-    auto P = [&](int i) { return xy + 2 * (size_t)i; };
-    auto upper = [&](int a, int b) {           // direction a -> b in [0, pi)
-        const double *pa = P(a), *pb = P(b);
-        return pb[1] > pa[1] || (pb[1] == pa[1] && pb[0] > pa[0]);
-    };
-    int start = -1;
-    for (int i = 0; i < n && start < 0; i++) if (bnext[i] >= 0) start = i;
-    if (start < 0) return false;
-    int u = start, len = 0, wraps = 0;
-    do {
-        const int v = bnext[u];
-        if (v < 0 || bnext[v] < 0) return false;
-        if (orient2d(P(u), P(v), P(bnext[v])) <= 0) return false;
-        if (!upper(u, v) && upper(v, bnext[v])) wraps++;
-        u = v;
-        if (++len > nb) return false;
-    } while (u != start);
-    return len == nb && wraps == 1;
+    // the boundary: one cycle, strictly convex, winding once (the convex hull)
+    return boundary_convex_once(xy, n, bnext, nb);
 }
 
 bool delaunay_repair(const double *xy, int n, const std::vector<int32_t> &prev, std::vector<int32_t> &tris, int &hull_size,

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -57,8 +58,15 @@ bool lin_part_sums() {
 hipError_t stream_wait(hipStream_t st) {
     static const bool block = std::getenv("DEFTRI_SYNC_BLOCK") != nullptr;
     if (block) return hipStreamSynchronize(st);
+    // spin for the first ~100 us (a C2 trial is ~0.4 ms, so the wake-up stays immediate), then yield
+    // the core between queries, so a rank sharing a node with its transport's threads (gloo, RCCL's
+    // proxy) does not hold a core for the whole CG chain
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
+    int n = 0;
     while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+        if ((++n & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100))
+            std::this_thread::yield();
     }
     return e;
 }

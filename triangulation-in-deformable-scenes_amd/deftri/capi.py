@@ -169,6 +169,12 @@ class Context:
         self._desc = None
         self._prob = None
         self._solver = ("pcg", 0.0, 0)
+        self.jacobian_mode = False       # deftri_set_jacobian_mode's default: g2o numeric Jacobians
+
+    def set_jacobian_mode(self, analytic):
+        """The Jacobians of deftri_arap_optimization / _deformation_optimization on this context."""
+        self._check(self.lib.deftri_set_jacobian_mode(self.h, 1 if analytic else 0))
+        self.jacobian_mode = bool(analytic)
 
     def close(self):
         if getattr(self, "h", None):
@@ -414,15 +420,19 @@ class Context:
     def arap_optimization(self, m, rep_weight, global_weight, arap_weight, alpha, beta, depth_error,
                           n_iterations, want_update=True, analytic=False):
         """analytic=False (default): g2o numeric ARAP/depth Jacobians, the reference's arithmetic."""
-        self._check(self.lib.deftri_set_jacobian_mode(self.h, 1 if analytic else 0))
+        prev = self.jacobian_mode
+        self.set_jacobian_mode(analytic)
         mc, keep = m.to_c()
         upd = C.c_double(0.0)
         rep = _abi.Report()
         t = time.perf_counter()
-        rc = self.lib.deftri_arap_optimization(
-            self.h, C.byref(mc), float(rep_weight), float(global_weight), float(arap_weight), float(alpha),
-            float(beta), C.c_float(depth_error), int(n_iterations), C.byref(upd) if want_update else None,
-            C.byref(rep))
+        try:
+            rc = self.lib.deftri_arap_optimization(
+                self.h, C.byref(mc), float(rep_weight), float(global_weight), float(arap_weight), float(alpha),
+                float(beta), C.c_float(depth_error), int(n_iterations), C.byref(upd) if want_update else None,
+                C.byref(rep))
+        finally:
+            self.set_jacobian_mode(prev)               # the caller's mode again
         self.last_call_s = time.perf_counter() - t     # the C-ABI call alone (no Python marshalling)
         self._check(rc)
         m.from_c(mc, keep)
@@ -435,7 +445,6 @@ class Context:
         clones, arapOptimization and calculatePixelsStandDev on the device.  Writes the map back
         (positions, depth scales, the global table) and returns the report as a dict with the
         evaluation log."""
-        self._check(self.lib.deftri_set_jacobian_mode(self.h, 0))      # g2o numeric J (the reference's)
         settings.validate_for_solver()
         if settings.selection == "open3DArap":
             raise NotImplementedError("open3DArap (Open3D DeformAsRigidAsPossible) is out of scope")
@@ -457,8 +466,13 @@ class Context:
         rep.evals = C.cast(evals, C.POINTER(_abi.DeformationEval))
         rep.max_evals = max_evals
         mc, keep = m.to_c()
+        prev = self.jacobian_mode
+        self.set_jacobian_mode(False)                  # g2o numeric J (the reference's)
         t = time.perf_counter()
-        rc = self.lib.deftri_deformation_optimization(self.h, C.byref(mc), C.byref(prm), C.byref(rep))
+        try:
+            rc = self.lib.deftri_deformation_optimization(self.h, C.byref(mc), C.byref(prm), C.byref(rep))
+        finally:
+            self.set_jacobian_mode(prev)               # the caller's mode again
         self.last_call_s = time.perf_counter() - t
         self._check(rc)
         if rep.rounds > 0:
