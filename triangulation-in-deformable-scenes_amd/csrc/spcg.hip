@@ -1657,12 +1657,13 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
     // read per workgroup, so its waves take the same branch (workgroup 0 of this launch may write
     // the record while another workgroup's waves start)
     __shared__ double s_r0;
+    const double *rk = G.red + (int64_t)kSpRed * it;
+    // the record words the test reads after the sums, loaded with the stop word (one round trip)
+    const double sw = rk[2], rr0 = G.red[1], gprev = it > 0 ? G.red[(int64_t)kSpRed * (it - 1)] : 1.0;
     if (threadIdx.x == 0) s_r0 = G.rec[0];
     __syncthreads();
     const double r0 = s_r0;
     if (r0 != 0.0) return (int)r0;
-    const double *rk = G.red + (int64_t)kSpRed * it;
-    const double sw = rk[2];
     const int n2 = it == 0 ? G.nrb + 1 : G.m_nh + row_grid(G.nrb);
     const double2 *parts = reinterpret_cast<const double2 *>(it == 0 ? G.upart : G.m2part);
     double a0 = 0.0, a1 = 0.0;
@@ -1689,14 +1690,14 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
     __syncthreads();
     int st = 0;
     if (sw != 0.0) st = (int)sw;
-    else if (s1 <= G.tol2 * (it == 0 ? s1 : G.red[1])) st = kSpConverged;
+    else if (s1 <= G.tol2 * (it == 0 ? s1 : rr0)) st = kSpConverged;
     else if (it >= G.max_it) st = kSpBudget;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         G.red[(int64_t)kSpRed * it] = s0;
         G.red[(int64_t)kSpRed * it + 1] = s1;
         if (st) record_stop(G, it, st);
     }
-    if (!st && it > 0) beta = s0 / G.red[(int64_t)kSpRed * (it - 1)];
+    if (!st && it > 0) beta = s0 / gprev;
     return st;
 }
 
@@ -1772,8 +1773,11 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     __shared__ double red[9][4];
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
-    // what does not depend on the state — the tile's table row, its rows' (z, p) for i = tid, its
-    // first entries' meta — is loaded before the state test's sums, so those round trips overlap
+    // everything that does not depend on the CG state is loaded before the state test's sums, so
+    // those round trips overlap: the tile's table row; its rows' and halo rows' (z, p) (two per
+    // thread); the heavy dofs' (z, p); the meta and chunk words of its first two entry passes; its
+    // own row's slot range and depth-coupling range.  In the entry loop the meta of the pass after
+    // the next is requested before the current pass is processed.
     // (sharded overlap: the launch runs a subset of the logical workgroups, G.p1list)
     const int b = G.p1list ? G.p1list[blockIdx.x] : (int)blockIdx.x, tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const bool heavy_wg = b == G.t_grid - 1;
@@ -1781,22 +1785,38 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     const int t = heavy_wg ? G.ntile : (b & 7) * seg + (b >> 3);
     int r0 = 0, nr = 0, nh = 0, e0 = 0, ne = 0, h0 = 0, ns = 0;
     double2 zpre[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
-    uint2 m0 = make_uint2(0u, 0u);
-    int2 ch0 = make_int2(0, 0);
+    double2 zpre2[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+    double2 hz = make_double2(0.0, 0.0);
+    uint2 mA = make_uint2(0u, 0u), mB = mA;     // the meta of passes 0, 1
+    int2 cA = make_int2(0, 0), cB = cA;
+    int rsi = 0, dj0 = 0, dj1 = 0;
     if (t < G.ntile) {
         const int32_t *T = G.ttab + 8 * (int64_t)t;
         r0 = T[0]; nr = T[1]; nh = T[2]; e0 = T[3]; ne = T[4]; h0 = T[5]; ns = T[6];
+        // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another rank's in
+        // the receive region)
         if (tid < nr + nh) {
-            // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another
-            // rank's in the receive region)
             const int row = tid < nr ? G.row0 + r0 + tid : G.thalo[h0 + tid - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) zpre[c] = G.zp[o + c];
         }
-        if (tid < ne) {
-            m0 = G.tmeta[(int64_t)e0 + tid];
-            ch0 = G.tchunk[((int64_t)e0 + tid) >> 6];
+        if (tid + 256 < nr + nh) {
+            const int i = tid + 256;
+            const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
+            const int64_t o = G.hd + 3 * (int64_t)row;
+#pragma unroll
+            for (int c = 0; c < 3; c++) zpre2[c] = G.zp[o + c];
+        }
+        if (tid < 8 && tid < G.hd) hz = G.zp[tid];
+        const int64_t k0 = (int64_t)e0 + tid;
+        if (tid < ne) { mA = G.tmeta[k0]; cA = G.tchunk[k0 >> 6]; }
+        if (tid + 256 < ne) { mB = G.tmeta[k0 + 256]; cB = G.tchunk[(k0 + 256) >> 6]; }
+        if (tid < nr) {
+            const int l = r0 + tid;
+            rsi = G.trs[l];
+            dj0 = G.dep_off[l];
+            dj1 = G.dep_off[l + 1];
         }
     }
     double beta;
@@ -1827,26 +1847,33 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     }
     if (t < G.ntile) {
         double *pL = lds, *up = pL + 3 * (nr + nh), *rs = up + 3 * nr, *hp = rs + 3 * ns;
+        const int64_t jld = G.jld;
+        const uint64_t lt = (1ull << lane) - 1;
         if (tid < nr + nh)
 #pragma unroll
             for (int c = 0; c < 3; c++) pL[3 * tid + c] = __fma_rn(beta, zpre[c].y, zpre[c].x);   // pval
-        for (int i = tid + 256; i < nr + nh; i += 256) {
+        if (tid + 256 < nr + nh)
+#pragma unroll
+            for (int c = 0; c < 3; c++) pL[3 * (tid + 256) + c] = __fma_rn(beta, zpre2[c].y, zpre2[c].x);
+        for (int i = tid + 512; i < nr + nh; i += 256) {
             const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) pL[3 * i + c] = pval(G.zp, beta, o + c);
         }
         for (int i = tid; i < 3 * nr; i += 256) up[i] = 0.0;
-        if (tid < 8) hp[tid] = tid < G.hd ? pval(G.zp, beta, tid) : 0.0;     // T_g (6), scales (<= 2)
+        if (tid < 8) hp[tid] = tid < G.hd ? __fma_rn(beta, hz.y, hz.x) : 0.0;     // T_g (6), scales (<= 2)
         __syncthreads();
         const double W = G.pinfo[0];               // W of every ARAP edge of the pair (k_lin_arap: W = Omega)
-        const int64_t jld = G.jld;
-        const uint64_t lt = (1ull << lane) - 1;
         for (int base = 0; base < ne; base += 256) {
             if (base + 64 * wv >= ne) break;       // (ne is a multiple of 64: whole waves in or out)
-            const int64_t k = (int64_t)e0 + base + tid;
-            const uint2 m = base == 0 ? m0 : G.tmeta[k];
-            const int2 ch = base == 0 ? ch0 : G.tchunk[k >> 6];
+            const uint2 m = mA;
+            const int2 ch = cA;
+            // the next pass's meta moves up; the meta of the pass after it is requested now
+            mA = mB; cA = cB;
+            const int64_t k2 = (int64_t)e0 + base + 512 + tid;
+            if (base + 512 + tid < ne) { mB = G.tmeta[k2]; cB = G.tchunk[k2 >> 6]; }
+            else { mB = make_uint2(0u, 0u); cB = make_int2(0, 0); }
             const bool valid = (m.x & kTmValid) != 0, cut = (m.x & kTmCut) != 0;
             const bool foreign = (m.x & kTmForeign) != 0, drop = (m.x & kTmDrop) != 0;   // (sharded plans)
             const uint64_t vm = __ballot(valid), cm = __ballot(valid && cut), hm = __ballot((m.x & kTmHead) != 0);
@@ -1913,7 +1940,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             for (int c = 0; c < 3; c++) { q[c] = up[3 * tid + c]; p[c] = pL[3 * tid + c]; }
 #pragma unroll
             for (int kk = 0; kk < 6; kk++) D[kk] = G.Dv[6 * (int64_t)l + kk];
-            const int rsi = G.trs[l], sb = rsi & 0xffff, sc = rsi >> 16;
+            const int sb = rsi & 0xffff, sc = rsi >> 16;
             for (int kk = sb; kk < sb + sc; kk++)
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += rs[3 * kk + c];
@@ -1922,7 +1949,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
             pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
             q[0] += q0; q[1] += q1; q[2] += q2;
-            for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {
+            for (int j = dj0; j < dj1; j++) {
                 const int sc_ = G.dsc[j];
                 const double *cd = G.cdep + 3 * (int64_t)j;
                 const double ps = hp[6 + sc_];
