@@ -23,7 +23,9 @@ north star's size) split the same way.  --weak: one problem of N x 100k correspo
 per-problem rate).  --solver direct runs the sharded multifrontal LDL^T instead.  The barrier and the
 max-over-ranks time use torch.distributed.
 
-Legs of the default C2 line (--no-legs skips them): `north_star_500k` (above, any N) and, at N = 1,
+Legs of the default C2 line (--no-legs skips them): `north_star_500k` (above, any N); at N > 1 `c4`:
+BASELINE C4 (8 keyframes x 500k, all 28 pairs, 12M unknowns) point-sharded over the same ranks, 1 +
+min(steps, 3) LM iterations (strong scaling; the multi-pair graph's sharded chain); and, at N = 1,
 `regimes.realcolon`: the C2 scene under Realcolon.yaml's weights and camera (arap 0.1, sigma_d 1e-6 m,
 KB8 d0..d3; Data/Realcolon.yaml:15-23,101,110), a CG-heavy regime (the Simulation.yaml headline
 run is near-stalled: ~5 CG iterations per trial at lambda ~1e21).
@@ -427,9 +429,9 @@ def product_roofline(stats, rep, ctx, rank):
     stream): active launches only (the profiled replay launches exactly the solve's CG iterations)."""
     tile = "sp_tile" in stats
     if tile or "sp_phase1" in stats:
-        # tile mode (one rank, one pair): k_sp_tile (the product, every ARAP edge read once) +
-        # k_sp_tupd (the update), or k_sp_tile alone when the update is fused into its launch
-        # (the sharded tile chain: k_sp_tile (interior + boundary launches) + k_sp_update_sd)
+        # tile mode (one rank: one pair or several): k_sp_tile (the product, every ARAP edge read once)
+        # + k_sp_tupd (the update) (the sharded tile chain: k_sp_tile (interior + boundary launches) +
+        # k_sp_update_sd)
         n1, n2 = ("sp_tile", "sp_tupd" if "sp_tupd" in stats else "sp_update") if tile else ("sp_phase1", "sp_phase2")
         none = {"launches": 0, "ms": 0.0, "bytes": 0.0}
         p1, p2 = stats[n1], stats.get(n2, none)
@@ -444,8 +446,7 @@ def product_roofline(stats, rep, ctx, rank):
         if tile and n2 == "sp_update":
             kname = "k_sp_tile+k_sp_update_sd (sharded tile chain: A z by tiles, every ARAP edge read once + update)"
         elif tile:
-            kname = ("k_sp_tile+k_sp_tupd (tile mode: matrix-free product reading every ARAP edge once + update)"
-                     if n2 in stats else "k_sp_tile (tile mode, update fused: one cooperative launch per CG iteration)")
+            kname = "k_sp_tile+k_sp_tupd (tile mode: matrix-free product reading every ARAP edge once + update)"
         else:
             kname = ("k_sp_phase1+k_sp_phase2 (merged CG iteration: matrix-free product + p.Ap row terms + update)"
                      if merged else "k_sp_phase1+k_sp_phase2 (matrix-free product)")
@@ -604,6 +605,8 @@ def main():
                          "iterations/s) — the default is the BASELINE metric's fixed problem split over the N ranks")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the extra legs of the C2 line (the 500k x 2 north-star size, the Realcolon regime)")
+    ap.add_argument("--c4-corr", type=int, default=WORKLOADS["c4"]["n"],
+                    help="N > 1: correspondences per keyframe of the c4 leg (rehearsals on one GPU)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: N independent problems, one per GPU; value = per-problem LM it/s")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end arapOptimization timing")
@@ -739,7 +742,7 @@ def main():
         e2e = end_to_end(gpu, prob_map, configure)
         log(f"end-to-end arapOptimization: {e2e}")
 
-    legs_500k, regimes = None, None
+    legs_500k, regimes, legs_c4 = None, None, None
     headline = wl == "c2" and REGIME == "simulation" and n == 100000 and not args.replicas and not weak
     if headline and not args.no_legs and args.solver == "pcg":
         ctx.close()
@@ -749,6 +752,15 @@ def main():
         legs_500k["correspondences_per_keyframe"] = 500000
         legs_500k["scaling"] = "strong" if world > 1 else "single"
         del p5
+        if world > 1:
+            # C4 (8 keyframes x 500k, all 28 pairs) point-sharded over the same ranks: the multi-pair
+            # graph's sharded chain, a few LM iterations
+            pc4, _ = build_workload("c4", args.c4_corr, 1, 0)
+            legs_c4 = timed_leg(pc4, gpu, rank, world, backend, min(args.steps, 3), 1, "C4")
+            legs_c4["workload"] = ("C4: " if args.c4_corr == WORKLOADS["c4"]["n"] else f"C4-slice-{args.c4_corr}x8: ") + \
+                WORKLOADS["c4"]["desc"]
+            legs_c4["scaling"] = "strong"
+            del pc4
         if world == 1:
             pr, _ = build_problem(100000, 1, "realcolon")
             regimes = {"realcolon": timed_leg(pr, gpu, rank, world, backend, args.steps, min(args.warmup, 2),
@@ -800,6 +812,7 @@ def main():
                                               if stats_f is not None and stats_f is not stats else None),
             "end_to_end_arap_optimization": e2e,
             "north_star_500k": legs_500k,
+            "c4": legs_c4,
             "regimes": regimes,
         }
         print(json.dumps(out), flush=True)

@@ -10,7 +10,8 @@ Usage: python tests/golden/make_c2_golden.py   (about 45 minutes of one core)
        python tests/golden/make_c2_golden.py realcolon 20
            the same scene under Data/Realcolon.yaml's weights and distorted KB8 camera (bench.py's
            regimes.realcolon: rep 1, arap 0.1, DepthWeight 0.001 -> sigma_d 1e-6 m), 20 iterations,
-           into c2_realcolon/ — a headline-size pin whose RMSE moves by whole pixels
+           into c2_realcolon/ — a headline-size pin whose chi2 falls 9 orders and RMSE moves 7e-4 px
+           (about an hour of one core)
 """
 import json
 import pathlib

@@ -698,3 +698,60 @@ def test_process_exit_with_live_contexts_is_clean():
     code = _EXIT_CHILD.format(pkg=str(capi.__file__.rsplit("/deftri/", 1)[0]), tests=str(__file__.rsplit("/", 1)[0]))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "done" in r.stdout, (r.returncode, r.stderr[-3000:])
+
+
+def _multi_tile_worker(env, q):
+    # the tile chain below kSpMergeMinDof unknowns: DEFTRI_SP_MERGE=1 (read once per process)
+    os.environ.update(env)
+    from deftri import capi as c
+    kind, n_it, analytic = env["_KIND"], int(env["_NIT"]), env["_ANALYTIC"] == "1"
+    if kind == "mv":
+        p = mv_problem()
+    else:
+        n, w = (60, 1) if kind == "c5w" else (24, 0)
+        p = sim.multi_view_problem(n, 20, seed=3, kb8=sim.REALCOLON_KB8, rep_weight=1.0, arap_weight=0.1,
+                                   depth_sigma=np.float32(1e-6), pair_window=w)
+    with c.Context(0) as ctx:
+        ctx.set_plan("iterative")
+        ctx.set_linear_solver("pcg", max_iterations=4096)
+        ctx.upload(p)
+        info = ctx.plan_info()
+        r = ctx.solve_lm(n_it, analytic=analytic)
+        pts, sc, tg = ctx.download()
+        q.put((info["tiles"], info["cg_launches"], r["iterations"], r["trials_iter"], r["chi2_iter"],
+               r["pcg_trials"], r["trials_total"], r["pcg_fallbacks"], pts.tobytes(), sc.tobytes()))
+
+
+@pytest.mark.parametrize("kind,n_it,analytic,tol", [("mv", 6, True, 1e-8), ("mv", 4, False, 1e-6),
+                                                     ("c5w", 4, False, 1e-6), ("c5all", 3, False, 1e-6)])
+def test_multi_pair_tile_chain_matches_oracle(kind, n_it, analytic, tol):
+    """Tile mode over several keyframe pairs (csrc/spcg_tile.cpp build_tiles_multi; the chain C3-C5
+    time): 8 keyframes with all 28 pairs (the reference's pair loop, g2oBundleAdjustment.cc:640-645),
+    and BASELINE C5's shape — 20 keyframes under the Realcolon weights with the 19 consecutive pairs
+    and with all 190 — against the oracle's LM: the same iterations and trials, chi2 per iteration and
+    the solved points to the all-pairs test's tolerances; every trial solved by PCG on the tile chain
+    (tiles > 0, two launches per CG iteration)."""
+    env = {"DEFTRI_SP_MERGE": "1", "_KIND": kind, "_NIT": str(n_it), "_ANALYTIC": "1" if analytic else "0"}
+    (tiles, launches, its, trials, chi2, pcg_trials, trials_total, fallbacks, pts, sc), = _fusion_runs([env], _multi_tile_worker)
+    assert tiles > 0 and launches == 2
+    if kind == "mv":
+        p = mv_problem()
+        res = oracle.solve_lm(p, n_it, analytic=analytic)
+    else:
+        n, w = (60, 1) if kind == "c5w" else (24, 0)
+        p = sim.multi_view_problem(n, 20, seed=3, kb8=sim.REALCOLON_KB8, rep_weight=1.0, arap_weight=0.1,
+                                   depth_sigma=np.float32(1e-6), pair_window=w)
+        with capi.Context(-1) as h:
+            h.analyse(p)
+            oracle.set_vertex_order(h.vertex_order())
+        try:
+            res = oracle.solve_lm(p, n_it, analytic=analytic)
+        finally:
+            oracle.set_vertex_order(None)
+    ref = res["report"]
+    assert its == ref["iterations"] and trials_total == ref["trials_total"]
+    np.testing.assert_allclose(chi2, ref["chi2_iter"], rtol=tol)
+    assert pcg_trials == trials_total and fallbacks == 0
+    pts = np.frombuffer(pts).reshape(-1, 3)
+    assert np.abs(pts - res["points"]).max() <= 1e-6 * max(np.abs(res["points"]).max(), 1.0)
+    np.testing.assert_allclose(np.frombuffer(sc), res["scales"], rtol=1e-6)

@@ -2,8 +2,9 @@
 reference's arithmetic) against the committed oracle runs (tests/golden/regimes,
 tests/golden/make_regime_goldens.py; Data/Simulation.yaml, Drunkard.yaml:68,77, Realcolon.yaml:101,110).
 
-On both plans: identical iteration and per-iteration trial counts, chi2 per iteration rel 1e-5 (the
-oracle's own spread between elimination orders at this size and depth), the solved points (fixed
+On both plans: identical iteration and per-iteration trial counts, chi2 per iteration within
+max(4 x the oracle's own spread between elimination orders, 1e-6) — the spread recorded in each
+golden's oracle_order_spread —, the solved points (fixed
 subsample) rel 1e-6 of the scene extent, and the north-star criterion: the reprojection RMSE of the
 solved map (calculatePixelsStandDev, Geometry.cc:370-498) within 1e-4 px of the oracle's — on runs
 where the RMSE itself moves by more than 5e-3 px, so the check can fail.  The iterative plan (the
@@ -67,13 +68,19 @@ def test_regime_matches_oracle(gpu_ctx, name, sub, plan):
     assert r["chi2_initial"] == pytest.approx(meta["chi2_initial"], rel=1e-11)
     assert r["iterations"] == meta["iterations"]
     assert r["trials_iter"] == list(z["trials_iter"])
-    # the oracle's own spread between elimination orders (tools/oracle_spread.py: its nested dissection
-    # against the host analysis' order the goldens use) — at 10k: Realcolon 7.95e-6 (iteration 14),
-    # Simulation 8.5e-9, Drunkard 1.7e-9; a reordered fixed-order sum on the GPU moves Realcolon's
-    # iteration 14 by 7.7e-7 .. 1.07e-5 (tools/regime_dev.py) — so 1e-5; at 30k the Realcolon run
-    # (Omega 1e12) moves one iteration's chi2 by 2.3e-5 on BOTH plans — the multifrontal plan's exact
-    # LDL^T steps included — so 5e-5 there
-    np.testing.assert_allclose(r["chi2_iter"], z["chi2_iter"], rtol=1e-5 if sub == "regimes" else 5e-5)
+    # chi2 per iteration within a band derived from the oracle's own spread: the same LM rerun with
+    # another legal elimination order (tools/oracle_spread.py, recorded in the golden's
+    # oracle_order_spread with its log) moves Realcolon's conditioning-bound iteration by 7.95e-6 (10k)
+    # and 8.4e-6 (30k), Simulation / Drunkard by <= 8.5e-9.  Legal GPU summation orders land inside
+    # 4x that (Realcolon 10k: 7.7e-7 .. 1.07e-5 over tools/regime_dev.py's variants; 30k: 2.3e-5 on
+    # both plans, the multifrontal plan's exact LDL^T included), so the test pins correctness, not
+    # one summation order; the floor 1e-6 covers the well-conditioned regimes' spreads of ~1e-9.
+    spread = meta["oracle_order_spread"]["max_rel_chi2"]
+    tol = max(4.0 * spread, 1e-6)
+    dev = np.abs(np.asarray(r["chi2_iter"]) - z["chi2_iter"]) / np.abs(z["chi2_iter"])
+    print(f"{name}/{sub}/{plan}: chi2 max rel dev {dev.max():.3e} at {int(dev.argmax())}, "
+          f"oracle order spread {spread:.3e}, tolerance {tol:.3e}")
+    assert dev.max() <= tol, (dev.max(), int(dev.argmax()), tol)
     if plan == "iterative":
         assert r["pcg_trials"] == r["trials_total"] and r["pcg_fallbacks"] == 0
     ext = np.abs(pts).max()

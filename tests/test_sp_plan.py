@@ -160,15 +160,19 @@ def test_merged_chain_pAp_decomposition(kind):
     assert pap > 0
 
 
-@pytest.mark.parametrize("units,lds", [(None, None), ("16", None), ("128", "12000")])
-def test_tile_product_matches_direct(units, lds, monkeypatch):
+@pytest.mark.parametrize("kind,units,lds", [("tv", None, None), ("tv", "16", None), ("tv", "128", "12000"),
+                                            ("mv", None, None), ("mv", "16", None)])
+def test_tile_product_matches_direct(kind, units, lds, monkeypatch):
     """Tile mode (csrc/spcg_tile.cpp; one rank, one keyframe pair — the fused product of the timed
     plan): the host emulation walks the tile layout exactly as k_sp_tile / k_sp_tupd do (le and cross
     slots from the chunk bases and the valid / cut lanes before an entry, the own rows' sums, the LDS
     remote slots, the cross slots added by the update launch) and checks the layout on the way (every
     local edge visited once, every LDS and cross slot written and read exactly once, every entry's LDS
     rows holding its points); its product equals the direct one to 1e-12.  Tile sizes: the default,
-    small tiles (many cut edges) and an LDS budget that forces small tiles."""
+    small tiles (many cut edges) and an LDS budget that forces small tiles.  "mv": 8 keyframes, every
+    pair (Q = 28, g2oBundleAdjustment.cc:640-645) — tiles per pair over (pair, group) units, each row's
+    home tile adding its diagonal terms and the other pairs' tiles their shares through cross slots,
+    every depth edge summed once by its pair's tile."""
     import subprocess, sys, json
     env = dict(os.environ, DEFTRI_SP_EMULATE_TILE="1")
     if units:
@@ -180,13 +184,14 @@ import sys, json, numpy as np
 sys.path.insert(0, 'tests'); sys.path.insert(0, 'triangulation-in-deformable-scenes_amd')
 from test_sp_plan import _problem, _random_lin, _reference
 from deftri import capi
-p = _problem('tv')
+p = _problem(%r)
+assert (p.n_pairs > 1) == (%r == 'mv')
 lin = _random_lin(p)
 with capi.Context(-1) as ctx:
     qv, st = ctx.debug_sp_product(p, *lin[:6], 0.37, lin[6])
 ref = _reference(p, *lin[:6], 0.37, lin[6])
 print(json.dumps([float(np.max(np.abs(qv - ref)) / np.max(np.abs(ref))), int(st[2])]))
-"""
+""" % (kind, kind)
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300,
                          cwd=str(__import__("pathlib").Path(__file__).resolve().parent.parent))
     assert out.returncode == 0, out.stderr[-2000:]

@@ -53,9 +53,11 @@ constexpr int kSpUpdRows = 256;           // rows per k_sp_update workgroup (one
 constexpr int kSpHeavyChunk = 128;        // block partials per k_sp_glin_heavy workgroup
 constexpr int kSpFuseHeavyMax = 8192;      // one rank: heavy block partials one workgroup reduces after phase 2
 constexpr int64_t kSpMergeMinDof = 50000;  // one rank: the merged (two-launch) CG chain from this many unknowns
-// tile mode (spcg_tile.cpp): one rank, one keyframe pair — the fused product, every ARAP edge read once
+// tile mode (spcg_tile.cpp): the fused product, every ARAP edge read once — one pair (one rank or
+// sharded), or on one rank several pairs (tiles per pair, tile_multi)
 constexpr int kSpTileUnits = 128;          // mesh vertices (keyframe-copy groups) per tile at most
 constexpr int kSpTileLds = 39 * 1024;      // dynamic LDS bytes per tile at most (with ~0.6 KB static: 4 workgroups per CU)
+constexpr int kSpTilePartsMax = 2048;      // tile grids above this: ticketed CG sums (spcg_solver.cpp)
 constexpr int kSpTileLdsFixed = 2048;      // the tile kernel's fixed dynamic LDS (heavy p; the heavy workgroup's sums)
 // tile entry meta word 0: LDS rows of p1_j (bits 0-11), p2_j (12-23), flags; word 1: LDS slots of
 // p1_j (0-11), p2_j (12-23), the unit's first tile row (24-31)
@@ -122,10 +124,17 @@ struct SpPlanHost {
     std::string tile_why;                              // why a requested tile layout was not built
     int32_t ntile = 0, tile_segmax = 1, tile_lds = 0;
     int64_t tile_entries = 0, tile_cross = 0, tile_halo_rows = 0;
-    std::vector<int32_t> tile_tab;                     // 8 per tile: r0, nr, nh, e0, ne, h0, ns, 0
+    std::vector<int32_t> tile_tab;                     // 8 per tile: r0, nr, nh, e0, ne, h0, ns, pair
+    // several pairs (tile_multi): a tile's own rows are listed (tile_trow from r0: row | home << 31,
+    // home = the first tile holding the row, which adds its diagonal terms and stores q; the others
+    // store their share in share plane tile_tdst - 1); tiles of pair q are tile_poff[q] .. [q + 1] - 1
+    bool tile_multi = false;
+    std::vector<int32_t> tile_trow, tile_tdst, tile_poff;   // tile_tdst: the entry's share (0 = home)
+    std::vector<int32_t> tile_nshare;                  // per row: its shares (tiles); planes = max - 1
+    int32_t tile_planes = 0;
     std::vector<uint32_t> tile_m0, tile_m1;            // per entry (padded to 64 per chunk)
     std::vector<int32_t> tile_chunk;                   // 2 per chunk: first le, first cross slot
-    std::vector<int32_t> tile_rs;                      // per own row: LDS slot begin | count << 16
+    std::vector<int32_t> tile_rs;                      // per own row (entry): LDS slot begin | count << 16
     std::vector<int32_t> tile_halo;                    // the tiles' halo rows (global row ids)
     std::vector<int32_t> tile_xoff;                    // per own row its cross slots (destination order)
     std::vector<int32_t> tile_xdst;                    // per cut entry (source order): its 2 cross slots
@@ -138,6 +147,11 @@ struct TileInput {
     const int32_t *ap = nullptr;                       // arap_pts [E][4]
     const int32_t *gpos = nullptr;                     // per point: its group's Morton position
     const int32_t *row_of_point = nullptr;
+    // several pairs (build_tiles_multi)
+    int32_t Q = 1, S = 0;
+    const int32_t *pair = nullptr;                     // arap_pair [E]
+    int64_t D = 0;
+    const int32_t *dep_point = nullptr, *dep_scale = nullptr;
 };
 // tile layout of a one-rank, one-pair plan: false (why) when the graph does not fit tile mode; order:
 // the ARAP edges in tile-entry order (the plan's local edge order)
@@ -145,6 +159,9 @@ struct TileInput {
 // halo-only ones (sharded plans; after them); H.lo / H.hi the rank's rows
 bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::vector<int32_t> &order_foreign,
                  std::string &why);
+// the same on one rank for a graph of several keyframe pairs (the all-pairs graph of
+// g2oBundleAdjustment.cc:640-645 or its window): tiles per pair over (pair, group) units
+bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why);
 // host emulation of one tile-mode product with its layout checks (tests; spcg_tile.cpp)
 int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, const double *Ja, const double *Wa,
                             const double *Jr, const double *Wr, const double *Jd, const double *Wd, double lambda,
@@ -263,6 +280,9 @@ struct SpDev {
     double *xc = nullptr;                                 // cross slots [n][3], by target row
     const double *pinfo = nullptr;                        // per pair: Omega (= W of its ARAP edges)
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
+    int32_t tmulti = 0;                                   // several pairs (SpPlanHost::tile_multi)
+    const int32_t *trow = nullptr, *tdst = nullptr, *tpoff = nullptr, *tnshare = nullptr;
+    double *qs = nullptr;                                 // share planes [planes][nown][3]
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     const int32_t *p1list = nullptr;                      // sharded phase 1: the launch's workgroups -> logical ones
     int32_t txb_fold = 0;                                 // sharded tiles: xb by k_sp_tile's last workgroup

@@ -1705,10 +1705,21 @@ __device__ __forceinline__ int tile_state(const SpDev &G, int it, double &beta, 
 // thread (g, c) = (tid / 8, tid % 8) adds component c of every 32nd partial, the 32 groups in order
 __device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *lds, bool coherent = false) {
     const int nb = G.t_grid - 1;
-    const int dim = h < G.Q ? 6 : 1, off = h < G.Q ? 0 : 6 + (h - G.Q);
+    const int dim = h < G.Q ? 6 : 1;
     const int c = threadIdx.x & 7, g = threadIdx.x >> 3;
     double acc = 0.0;
-    if (c < dim) {
+    if (G.tmulti) {
+        // several pairs: pair q's tiles t = tpoff[q] .. tpoff[q + 1] - 1 (workgroup b = 8 (t % seg) +
+        // t / seg, the inverse of the tiles' XCD dealing); a scale s is component 6 + (s & 1) of pair s / 2
+        const int q = h < G.Q ? h : (h - G.Q) >> 1, off = h < G.Q ? 0 : 6 + ((h - G.Q) & 1);
+        const int seg = (G.ntile + 7) / 8, t1 = G.tpoff[q + 1];
+        if (c < dim)
+            for (int t = G.tpoff[q] + g; t < t1; t += 32) {
+                const double *p = G.part + (int64_t)kSpPart * (8 * (t % seg) + t / seg) + off + c;
+                acc += coherent ? fetch(p) : *p;
+            }
+    } else if (c < dim) {
+        const int off = h < G.Q ? 0 : 6 + (h - G.Q);
         int k = g;
         for (; k + 7 * 32 < nb; k += 8 * 32) {
             double v[8];
@@ -1783,7 +1794,9 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     const bool heavy_wg = b == G.t_grid - 1;
     const int seg = (G.ntile + 7) / 8;
     const int t = heavy_wg ? G.ntile : (b & 7) * seg + (b >> 3);
-    int r0 = 0, nr = 0, nh = 0, e0 = 0, ne = 0, h0 = 0, ns = 0;
+    int r0 = 0, nr = 0, nh = 0, e0 = 0, ne = 0, h0 = 0, ns = 0, tq = 0;
+    // own row i of the tile (local row index): consecutive from r0, or (several pairs) listed
+    auto own_row = [&](int i) { return G.tmulti ? (G.trow[r0 + i] & 0x7fffffff) : G.row0 + r0 + i; };
     double2 zpre[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
     double2 zpre2[3] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
     double2 hz = make_double2(0.0, 0.0);
@@ -1792,29 +1805,31 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     int rsi = 0, dj0 = 0, dj1 = 0;
     if (t < G.ntile) {
         const int32_t *T = G.ttab + 8 * (int64_t)t;
-        r0 = T[0]; nr = T[1]; nh = T[2]; e0 = T[3]; ne = T[4]; h0 = T[5]; ns = T[6];
+        r0 = T[0]; nr = T[1]; nh = T[2]; e0 = T[3]; ne = T[4]; h0 = T[5]; ns = T[6]; tq = T[7];
         // (zp rows: own rows at row0 + local, halo rows as the upload mapped them — another rank's in
         // the receive region)
         if (tid < nr + nh) {
-            const int row = tid < nr ? G.row0 + r0 + tid : G.thalo[h0 + tid - nr];
+            const int row = tid < nr ? own_row(tid) : G.thalo[h0 + tid - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) zpre[c] = G.zp[o + c];
         }
         if (tid + 256 < nr + nh) {
             const int i = tid + 256;
-            const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
+            const int row = i < nr ? own_row(i) : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) zpre2[c] = G.zp[o + c];
         }
-        if (tid < 8 && tid < G.hd) hz = G.zp[tid];
+        // the pair's T_g (6) and its two scales: dofs 6 q .. 6 q + 5, 6 Q + 2 q, 6 Q + 2 q + 1
+        const int hdof = tid < 6 ? 6 * tq + tid : 6 * G.Q + 2 * tq + tid - 6;
+        if (tid < 8 && hdof < G.hd) hz = G.zp[hdof];
         const int64_t k0 = (int64_t)e0 + tid;
         if (tid < ne) { mA = G.tmeta[k0]; cA = G.tchunk[k0 >> 6]; }
         if (tid + 256 < ne) { mB = G.tmeta[k0 + 256]; cB = G.tchunk[(k0 + 256) >> 6]; }
         if (tid < nr) {
-            const int l = r0 + tid;
-            rsi = G.trs[l];
+            const int l = G.tmulti ? own_row(tid) : r0 + tid;
+            rsi = G.trs[r0 + tid];
             dj0 = G.dep_off[l];
             dj1 = G.dep_off[l + 1];
         }
@@ -1856,15 +1871,15 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
 #pragma unroll
             for (int c = 0; c < 3; c++) pL[3 * (tid + 256) + c] = __fma_rn(beta, zpre2[c].y, zpre2[c].x);
         for (int i = tid + 512; i < nr + nh; i += 256) {
-            const int row = i < nr ? G.row0 + r0 + i : G.thalo[h0 + i - nr];
+            const int row = i < nr ? own_row(i) : G.thalo[h0 + i - nr];
             const int64_t o = G.hd + 3 * (int64_t)row;
 #pragma unroll
             for (int c = 0; c < 3; c++) pL[3 * i + c] = pval(G.zp, beta, o + c);
         }
         for (int i = tid; i < 3 * nr; i += 256) up[i] = 0.0;
-        if (tid < 8) hp[tid] = tid < G.hd ? __fma_rn(beta, hz.y, hz.x) : 0.0;     // T_g (6), scales (<= 2)
+        if (tid < 8) hp[tid] = __fma_rn(beta, hz.y, hz.x);     // T_g (6), scales (<= 2); 0 past hd
         __syncthreads();
-        const double W = G.pinfo[0];               // W of every ARAP edge of the pair (k_lin_arap: W = Omega)
+        const double W = G.pinfo[tq];              // W of every ARAP edge of the pair (k_lin_arap: W = Omega)
         for (int base = 0; base < ne; base += 256) {
             if (base + 64 * wv >= ne) break;       // (ne is a multiple of 64: whole waves in or out)
             const uint2 m = mA;
@@ -1933,24 +1948,34 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         }
         __syncthreads();
         if (tid < nr) {
-            const int l = r0 + tid;
+            // several pairs: the row's home tile adds its diagonal terms and stores q, every other
+            // tile of the row stores its share (its pair's sums) in the row's cross slot
+            const int l = G.tmulti ? own_row(tid) : r0 + tid;
+            const bool home = !G.tmulti || G.trow[r0 + tid] < 0;
             const int64_t o = G.hd + 3 * (int64_t)(G.row0 + l);
-            double q[3], p[3], D[6];
+            double q[3], p[3];
 #pragma unroll
             for (int c = 0; c < 3; c++) { q[c] = up[3 * tid + c]; p[c] = pL[3 * tid + c]; }
-#pragma unroll
-            for (int kk = 0; kk < 6; kk++) D[kk] = G.Dv[6 * (int64_t)l + kk];
             const int sb = rsi & 0xffff, sc = rsi >> 16;
             for (int kk = sb; kk < sb + sc; kk++)
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += rs[3 * kk + c];
-            const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
-            const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
-            const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
-            pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
-            q[0] += q0; q[1] += q1; q[2] += q2;
+            if (home) {
+                double D[6];
+#pragma unroll
+                for (int kk = 0; kk < 6; kk++) D[kk] = G.Dv[6 * (int64_t)l + kk];
+                const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
+                const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
+                const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
+                pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
+                q[0] += q0; q[1] += q1; q[2] += q2;
+            }
             for (int j = dj0; j < dj1; j++) {
-                const int sc_ = G.dsc[j];
+                int sc_ = G.dsc[j];
+                if (G.tmulti) {                    // the pair's two scales only (2 tq, 2 tq + 1)
+                    if ((sc_ >> 1) != tq) continue;
+                    sc_ &= 1;
+                }
                 const double *cd = G.cdep + 3 * (int64_t)j;
                 const double ps = hp[6 + sc_];
                 const double cp = (cd[0] * p[0] + cd[1] * p[1]) + cd[2] * p[2];
@@ -1961,8 +1986,14 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += cd[c] * ps;
             }
+            if (home) {
 #pragma unroll
-            for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+                for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
+            } else {                               // share j > 0: plane j - 1
+                const int64_t x = 3 * ((int64_t)(G.tdst[r0 + tid] - 1) * G.nown + l);
+#pragma unroll
+                for (int c = 0; c < 3; c++) G.qs[x + c] = q[c];
+            }
         }
     }
     // [p.Ap, J_T^T s, scale sums]: wave butterflies, then the waves in order
@@ -2051,6 +2082,10 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
             o = G.hd + 3 * (int64_t)l;
 #pragma unroll
             for (int c = 0; c < 3; c++) q[c] = G.q[o + c];
+            if (G.tmulti)                                              // several pairs: the row's shares
+                for (int j = 1; j < G.tnshare[l]; j++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) q[c] += G.qs[3 * ((int64_t)(j - 1) * G.nown + l) + c];
             for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)          // the row's cross slots, contiguous
 #pragma unroll
                 for (int c = 0; c < 3; c++) q[c] += G.xc[3 * (int64_t)k + c];

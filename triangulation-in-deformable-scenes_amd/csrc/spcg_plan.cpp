@@ -197,10 +197,26 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     for (int32_t k = 0; k < ng; k++) gpos[gorder[k]] = k;
 
     stage("2 Morton order");
-    // 3. rows: groups in that order, points of a group by id
+    // 3. rows: groups in that order, points of a group by id.  A tile plan of several pairs (one rank)
+    //    numbers them keyframe-major instead — by the camera of the point's reprojection edges, then
+    //    its group's Morton position — so a tile of pair (a, b), consecutive groups of that pair, owns
+    //    two contiguous row ranges (keyframe a's and keyframe b's) and its loads and stores coalesce
     std::vector<int32_t> pts(P);
     std::iota(pts.begin(), pts.end(), 0);
     counting_sort(pts, ng, [&](int32_t p) { return gpos[gid[p]]; });
+    if (tile && Q > 1 && nranks == 1) {
+        std::vector<int32_t> pcam(P, -1);
+        bool one_cam = true;
+        for (int64_t e = 0; e < R; e++) {
+            int32_t &c = pcam[d.rep_point[e]];
+            if (c < 0) c = d.rep_cam[e];
+            else if (c != d.rep_cam[e]) one_cam = false;
+        }
+        if (one_cam) {
+            const int32_t C = std::max(d.n_cams, 1);
+            counting_sort(pts, (int64_t)C + 1, [&](int32_t p) { return pcam[p] < 0 ? C : pcam[p]; });
+        }
+    }
     H.point_of_row = pts;
     H.row_of_point.assign(P, 0);
     for (int32_t r = 0; r < P; r++) H.row_of_point[pts[r]] = r;
@@ -246,8 +262,23 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             tile_order.clear();
             tile_foreign.clear();
         }
+    } else if (tile && Q > 1 && nranks == 1 && E > 0) {
+        // several pairs on one rank: tiles per pair over (pair, group) units (spcg_tile.cpp)
+        H.lo = H.rank_row_begin[rank];
+        H.hi = H.rank_row_begin[rank + 1];
+        std::vector<int32_t> gp(P);
+        for (int32_t p = 0; p < P; p++) gp[p] = gpos[gid[p]];
+        TileInput ti;
+        ti.P = P; ti.ng = ng; ti.E = E; ti.ap = ap; ti.gpos = gp.data(); ti.row_of_point = H.row_of_point.data();
+        ti.Q = Q; ti.S = S; ti.pair = d.arap_pair; ti.D = D; ti.dep_point = d.dep_point; ti.dep_scale = d.dep_scale;
+        std::string why;
+        H.tile = build_tiles_multi(ti, H, tile_order, why);
+        if (!H.tile) {
+            H.tile_why = why;
+            tile_order.clear();
+        }
     } else if (tile) {
-        H.tile_why = Q != 1 ? "more than one keyframe pair" : S > 2 ? "more than two depth scales" : "no ARAP edges";
+        H.tile_why = Q != 1 ? "more than one keyframe pair on a sharded plan" : S > 2 ? "more than two depth scales" : "no ARAP edges";
     }
     stage("4a tiles");
     // 4b. inside every rank's range, rows sorted by their phase-2 slot count (ARAP incidences + depth

@@ -254,7 +254,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     static const bool no_tile = std::getenv("DEFTRI_SP_NO_TILE") != nullptr;
     static const bool sd_no_tile = std::getenv("DEFTRI_SP_SD_NO_TILE") != nullptr || std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
     const int64_t ndof_ = 6 * (int64_t)d.n_pairs + d.n_scales + 3 * (int64_t)d.n_points;
-    const bool want_tile = !no_tile && d.n_pairs == 1 &&
+    const bool want_tile = !no_tile && (d.n_pairs == 1 || !shard_) &&
                            (shard_ ? !sd_no_tile
                                    : !std::getenv("DEFTRI_SP_NO_FUSE") && !std::getenv("DEFTRI_SP_NO_MERGE") &&
                                          (ndof_ >= kSpMergeMinDof || std::getenv("DEFTRI_SP_MERGE")));
@@ -481,15 +481,24 @@ int SpSolver::upload(const deftri_problem_desc &d) {
             PUT(tm, mm);
         }
         G.ttab = tt; G.trs = trs; G.thalo = th; G.txoff = txo;
+        if (H.tile_multi) {                        // several pairs: own-row lists, shares, pair ranges
+            int32_t *tr, *tdd, *tpo, *tns;
+            PUT(tr, H.tile_trow); PUT(tdd, H.tile_tdst); PUT(tpo, H.tile_poff); PUT(tns, H.tile_nshare);
+            G.tmulti = 1;
+            G.trow = tr; G.tdst = tdd; G.tpoff = tpo; G.tnshare = tns;
+            ALLOC(G.qs, 3 * std::max<int64_t>((int64_t)H.tile_planes * nown, 1));
+        }
         G.txdst = reinterpret_cast<const int2 *>(txd);
         G.tchunk = reinterpret_cast<const int2 *>(tch);
         G.tmeta = reinterpret_cast<const uint2 *>(tm);
         G.pinfo = P.pair_info;
         ALLOC(G.xc, 3 * std::max<int64_t>(H.tile_cross, 1));    // 3 per cross slot
-        // each product launch sums the last update's (r.z, r.r) partials itself; only the chain's
-        // last update takes the ticketed sum that records the state (the sharded chain's record is
-        // all-reduced instead)
-        G.tparts = G.sd ? 0 : 1;
+        // each product launch sums the last update's (r.z, r.r) partials itself, and each update
+        // workgroup alpha from the product's; only the chain's last update takes the ticketed sum that
+        // records the state.  Every workgroup reading every partial costs O(workgroups^2) reads, so
+        // from kSpTilePartsMax tiles (the multi-keyframe graphs: C3 has 12k) the ticketed sums and the
+        // alpha hand-off take over, as on the sharded chain (whose record is all-reduced)
+        G.tparts = (G.sd || G.t_grid > kSpTilePartsMax) ? 0 : 1;
         // sharded: the rank's record xb in its own small launch (k_sp_txb); DEFTRI_SP_TXB_FOLD=1 forms
         // it in the product's last workgroup instead (a ticket over both product launches) — the
         // same on the 2-rank gloo rehearsal (165.8 vs 171.8 LM it/s), so the simpler order stays

@@ -390,6 +390,281 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     return true;
 }
 
+// Several keyframe pairs on one rank (the all-pairs graph of g2oBundleAdjustment.cc:640-645, or its
+// window).  A point belongs to the pairs of its keyframe, so a keyframe-copy group holds K rows and
+// an ARAP edge of pair q touches the two rows of pair q's keyframes in its i and j groups.  The unit
+// is (pair, group): its two rows are the pair's p1_i, p2_i.  Units are ordered by pair, then Morton
+// group; tiles are cut per pair exactly as build_tiles cuts one pair's groups (the same LDS budget,
+// slots and cross slots), so a tile reads one T_g, one pair's two scales and one W.  A row is an own
+// row of one tile per pair containing it: the first of them (its home, share 0) adds the row's
+// diagonal terms (D_v + lambda) and stores q; share j > 0 stores its pair's ARAP sums and depth
+// couplings in plane j - 1 of a share array, which the update adds to q with the cut edges' slots.
+// The plan numbers the rows keyframe-major (spcg_plan.cpp step 3), so a tile's rows are two runs.
+bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::string &why) {
+    const int32_t P = in.P, ng = in.ng, Q = in.Q;
+    const int64_t E = in.E;
+    const int32_t *ap = in.ap, *row = in.row_of_point;
+    static const int umax = [] {
+        const char *e = std::getenv("DEFTRI_SP_TILE_UNITS");
+        const int v = e ? std::atoi(e) : kSpTileUnits;
+        return std::max(8, std::min(v, 128));
+    }();
+    static const int64_t lds_budget = [] {
+        const char *e = std::getenv("DEFTRI_SP_TILE_LDS");
+        return (int64_t)(e ? std::atoi(e) : kSpTileLds);
+    }();
+    if (H.nranks != 1) { why = "several pairs on a sharded plan"; return false; }
+    if (in.S != 2 * Q) { why = "not two depth scales per pair"; return false; }
+    if ((int64_t)Q * ng >= (1LL << 31)) { why = "too many (pair, group) units"; return false; }
+    // 1. units (pair, group) with edges, in (pair, Morton group) order; their two rows
+    std::vector<int32_t> uid((size_t)Q * ng, -1);
+    for (int64_t e = 0; e < E; e++) {
+        const int32_t q = in.pair[e];
+        if (q < 0 || q >= Q) { why = "an edge's pair out of range"; return false; }
+        uid[(size_t)q * ng + in.gpos[ap[4 * e]]] = 0;
+        uid[(size_t)q * ng + in.gpos[ap[4 * e + 2]]] = 0;
+    }
+    int32_t nu = 0;
+    for (size_t k = 0; k < uid.size(); k++)
+        if (uid[k] == 0) uid[k] = nu++;
+    std::vector<int32_t> urow(2 * (size_t)nu, -1), upair(nu);
+    for (int32_t q = 0; q < Q; q++)
+        for (int32_t g = 0; g < ng; g++)
+            if (uid[(size_t)q * ng + g] >= 0) upair[uid[(size_t)q * ng + g]] = q;
+    std::vector<int32_t> egi(E), egj(E);
+    std::vector<int32_t> ocnt(nu + 1, 0), icnt(nu + 1, 0);
+    for (int64_t e = 0; e < E; e++) {
+        const size_t qb = (size_t)in.pair[e] * ng;
+        const int32_t ui = uid[qb + in.gpos[ap[4 * e]]], uj = uid[qb + in.gpos[ap[4 * e + 2]]];
+        if (ui == uj) { why = "an edge inside one group"; return false; }
+        if (in.gpos[ap[4 * e]] != in.gpos[ap[4 * e + 1]] || in.gpos[ap[4 * e + 2]] != in.gpos[ap[4 * e + 3]]) {
+            why = "an edge's copies in two groups";
+            return false;
+        }
+        for (int s = 0; s < 2; s++) {
+            const int32_t u = s ? uj : ui;
+            const int32_t r0 = row[ap[4 * e + 2 * s]], r1 = row[ap[4 * e + 2 * s + 1]];
+            if (urow[2 * (size_t)u] < 0) { urow[2 * (size_t)u] = r0; urow[2 * (size_t)u + 1] = r1; }
+            else if (urow[2 * (size_t)u] != r0 || urow[2 * (size_t)u + 1] != r1) { why = "a unit's rows differ between its edges"; return false; }
+        }
+        egi[e] = ui;
+        egj[e] = uj;
+        ocnt[ui + 1]++;
+        icnt[uj + 1]++;
+    }
+    for (int32_t u = 0; u < nu; u++) { ocnt[u + 1] += ocnt[u]; icnt[u + 1] += icnt[u]; }
+    std::vector<int32_t> oe(E), isrc(E);
+    {
+        std::vector<int32_t> fo(ocnt.begin(), ocnt.end() - 1), fi(icnt.begin(), icnt.end() - 1);
+        for (int64_t e = 0; e < E; e++) {
+            oe[fo[egi[e]]++] = (int32_t)e;
+            isrc[fi[egj[e]]++] = egi[e];
+        }
+    }
+    for (int32_t u = 0; u < nu; u++)
+        if (ocnt[u + 1] - ocnt[u] > 64) { why = "a vertex with more than 64 ARAP edges in a pair"; return false; }
+    // every depth edge's (row, pair of its scale) is a unit's row: it is summed by that unit's tile
+    {
+        std::vector<int64_t> key;
+        key.reserve(2 * (size_t)nu);
+        for (int32_t u = 0; u < nu; u++)
+            for (int k = 0; k < 2; k++) key.push_back((int64_t)urow[2 * (size_t)u + k] * Q + upair[u]);
+        std::sort(key.begin(), key.end());
+        if (std::adjacent_find(key.begin(), key.end()) != key.end()) { why = "a row in two units of one pair"; return false; }
+        for (int64_t d = 0; d < in.D; d++) {
+            const int64_t k = (int64_t)row[in.dep_point[d]] * Q + (in.dep_scale[d] >> 1);
+            if (!std::binary_search(key.begin(), key.end(), k)) { why = "a depth edge outside its pair's mesh"; return false; }
+        }
+        std::vector<uint8_t> seen(P, 0);
+        for (int32_t k : urow) seen[k] = 1;
+        for (int32_t r = 0; r < P; r++)
+            if (!seen[r]) { why = "a row in no pair's mesh"; return false; }
+    }
+    // 2. greedy partition per pair: consecutive units while units <= umax and the LDS estimate fits
+    auto lds_of = [&](int64_t nr, int64_t nh, int64_t ns) { return 24 * (nr + nh) + 24 * nr + 24 * ns + kSpTileLdsFixed; };
+    std::vector<int32_t> tstart;
+    std::vector<int32_t> hcnt(nu, 0), stamp(nu, -1);
+    {
+        int32_t us = 0, attempt = 0;
+        int64_t nr = 0, nh = 0, ns = 0, units = 0;
+        std::vector<int32_t> halo_members;
+        tstart.push_back(0);
+        for (int32_t u = 0; u < nu;) {
+            int64_t dnh = 0, dns = 0;
+            attempt++;
+            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
+                const int32_t uj = egj[oe[k]];
+                if (uj >= us && uj < u) dns += 2;
+                else if (hcnt[uj] == 0 && stamp[uj] != attempt) { stamp[uj] = attempt; dnh += 2; }
+            }
+            for (int32_t k = icnt[u]; k < icnt[u + 1]; k++)
+                if (isrc[k] >= us && isrc[k] < u) dns += 2;
+            if (hcnt[u] > 0) dnh -= 2;
+            const bool same_pair = units == 0 || upair[u] == upair[us];
+            const bool fits = same_pair && units + 1 <= umax && lds_of(nr + 2, nh + dnh, ns + dns) <= lds_budget &&
+                              nr + 2 + nh + dnh < 4096 && ns + dns < 4096;
+            if (!fits && units > 0) {
+                for (int32_t h : halo_members) hcnt[h] = 0;
+                halo_members.clear();
+                us = u;
+                nr = nh = ns = units = 0;
+                tstart.push_back(u);
+                continue;
+            }
+            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
+                const int32_t uj = egj[oe[k]];
+                if (!(uj >= us && uj < u))
+                    if (hcnt[uj]++ == 0) halo_members.push_back(uj);
+            }
+            hcnt[u] = 0;
+            nr += 2;
+            nh += dnh;
+            ns += dns;
+            units++;
+            u++;
+        }
+        for (int32_t h : halo_members) hcnt[h] = 0;
+        tstart.push_back(nu);
+    }
+    const int32_t nt = nu > 0 ? (int32_t)tstart.size() - 1 : 0;
+    // 3. entries, own-row lists, slots, cross slots (the cut edges' first: chunk bases count them)
+    H.tile_tab.assign(8 * (size_t)nt, 0);
+    H.tile_poff.assign(Q + 1, nt);
+    order.clear();
+    order.reserve(E);
+    std::vector<uint32_t> &m0 = H.tile_m0, &m1 = H.tile_m1;
+    m0.clear(); m1.clear();
+    H.tile_chunk.clear();
+    H.tile_halo.clear();
+    H.tile_trow.clear();
+    H.tile_rs.clear();
+    std::vector<std::pair<int32_t, int32_t>> xt;         // (target row, slot id)
+    int64_t nx = 0;
+    int32_t segmax = 1, max_lds = 0;
+    std::vector<int32_t> lrow(nu, -1);                  // unit -> LDS row base inside the current tile
+    std::vector<int32_t> slotcnt, slotfill;
+    for (int32_t t = 0; t < nt; t++) {
+        const int32_t u0 = tstart[t], u1 = tstart[t + 1], q = upair[u0];
+        if (H.tile_poff[q] == nt) H.tile_poff[q] = t;
+        const int32_t nr = 2 * (u1 - u0), r0 = (int32_t)H.tile_trow.size();
+        for (int32_t u = u0; u < u1; u++) {
+            lrow[u] = 2 * (u - u0);
+            H.tile_trow.push_back(urow[2 * (size_t)u]);
+            H.tile_trow.push_back(urow[2 * (size_t)u + 1]);
+        }
+        std::vector<int32_t> hu;
+        for (int32_t u = u0; u < u1; u++)
+            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++)
+                if (egj[oe[k]] < u0 || egj[oe[k]] >= u1) hu.push_back(egj[oe[k]]);
+        std::sort(hu.begin(), hu.end());
+        hu.erase(std::unique(hu.begin(), hu.end()), hu.end());
+        const int32_t h0 = (int32_t)H.tile_halo.size();
+        const int32_t nh = 2 * (int32_t)hu.size();
+        for (size_t k = 0; k < hu.size(); k++) {
+            lrow[hu[k]] = nr + 2 * (int32_t)k;
+            H.tile_halo.push_back(urow[2 * (size_t)hu[k]]);
+            H.tile_halo.push_back(urow[2 * (size_t)hu[k] + 1]);
+        }
+        slotcnt.assign(nr, 0);
+        for (int32_t u = u0; u < u1; u++)
+            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
+                const int32_t uj = egj[oe[k]];
+                if (uj >= u0 && uj < u1) { slotcnt[lrow[uj]]++; slotcnt[lrow[uj] + 1]++; }
+            }
+        slotfill.assign(nr, 0);
+        int32_t ns = 0;
+        for (int32_t r = 0; r < nr; r++) {
+            slotfill[r] = ns;
+            if (slotcnt[r] > 0xffff) { why = "too many slots on a row"; return false; }
+            H.tile_rs.push_back(ns | slotcnt[r] << 16);
+            ns += slotcnt[r];
+        }
+        const int64_t e0 = (int64_t)m0.size();
+        int fill = 0;
+        auto pad_chunk = [&]() {
+            while (fill % 64) {
+                m0.push_back(kTmHead);
+                m1.push_back(0);
+                fill++;
+            }
+        };
+        for (int32_t u = u0; u < u1; u++) {
+            const int32_t k0 = ocnt[u], k1 = ocnt[u + 1];
+            const int cnt = k1 - k0;
+            if (cnt == 0) continue;
+            segmax = std::max(segmax, cnt);
+            if (fill % 64 + cnt > 64) pad_chunk();
+            for (int32_t k = k0; k < k1; k++) {
+                if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)order.size()), H.tile_chunk.push_back((int32_t)nx);
+                const int64_t e = oe[k];
+                const int32_t uj = egj[e];
+                const bool cut = uj < u0 || uj >= u1;
+                const uint32_t ub = (uint32_t)lrow[u];
+                const uint32_t rj0 = (uint32_t)lrow[uj], rj1 = (uint32_t)lrow[uj] + 1;
+                uint32_t w0 = rj0 | rj1 << 12 | kTmValid;
+                if (k == k0) w0 |= kTmHead;
+                if (k == k1 - 1) w0 |= kTmLast;
+                uint32_t w1 = ub << 24;
+                if (cut) {
+                    w0 |= kTmCut;
+                    xt.push_back({row[ap[4 * e + 2]], (int32_t)nx});
+                    xt.push_back({row[ap[4 * e + 3]], (int32_t)nx + 1});
+                    nx += 2;
+                } else {
+                    const int32_t s0 = slotfill[rj0]++, s1 = slotfill[rj1]++;
+                    w1 |= (uint32_t)s0 | (uint32_t)s1 << 12;
+                }
+                m0.push_back(w0);
+                m1.push_back(w1);
+                order.push_back((int32_t)e);
+                fill++;
+            }
+        }
+        if (fill == 0) { H.tile_chunk.push_back((int32_t)order.size()); H.tile_chunk.push_back((int32_t)nx); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
+        pad_chunk();
+        const int64_t ne = (int64_t)m0.size() - e0;
+        if (nr > 256) { why = "a tile of more than 128 units"; return false; }   // (ub: 8 bits)
+        int32_t *T = &H.tile_tab[8 * (size_t)t];
+        T[0] = r0; T[1] = nr; T[2] = nh; T[3] = (int32_t)e0; T[4] = (int32_t)ne; T[5] = h0; T[6] = ns; T[7] = q;
+        max_lds = std::max<int32_t>(max_lds, (int32_t)lds_of(nr, nh, ns));
+        for (int32_t u = u0; u < u1; u++) lrow[u] = -1;
+        for (int32_t u : hu) lrow[u] = -1;
+    }
+    for (int32_t q = Q - 1; q >= 0; q--)
+        if (H.tile_poff[q] == nt) H.tile_poff[q] = H.tile_poff[q + 1];
+    if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
+    // 4. shares: a row's tiles in tile (= pair) order are its shares 0, 1, ...; share 0 (the home)
+    //    adds the row's diagonal terms and stores q, share j > 0 its pair's sums in plane j - 1 of the
+    //    share array (row-major per plane, so a tile's stores and the update's loads coalesce)
+    H.tile_tdst.assign(H.tile_trow.size(), 0);
+    H.tile_nshare.assign(P, 0);
+    for (size_t k = 0; k < H.tile_trow.size(); k++) {
+        const int32_t r = H.tile_trow[k];
+        const int32_t j = H.tile_nshare[r]++;
+        H.tile_tdst[k] = j;
+        if (j == 0) H.tile_trow[k] = r | (int32_t)(1u << 31);
+    }
+    H.tile_planes = 0;
+    for (int32_t c : H.tile_nshare) H.tile_planes = std::max(H.tile_planes, c - 1);
+    // cross slots by target row, source order inside a row
+    H.tile_xoff.assign(P + 1, 0);
+    H.tile_xdst.assign(xt.size(), 0);
+    for (const auto &x : xt) H.tile_xoff[x.first + 1]++;
+    for (int32_t l = 0; l < P; l++) H.tile_xoff[l + 1] += H.tile_xoff[l];
+    {
+        std::vector<int32_t> fill(H.tile_xoff.begin(), H.tile_xoff.end() - 1);
+        for (const auto &x : xt) H.tile_xdst[x.second] = fill[x.first]++;
+    }
+    H.tile_multi = true;
+    H.ntile = nt;
+    H.tile_entries = (int64_t)m0.size();
+    H.tile_cross = nx;
+    H.tile_segmax = segmax;
+    H.tile_lds = max_lds;
+    H.tile_halo_rows = (int64_t)H.tile_halo.size();
+    return true;
+}
+
 }  // namespace deftri
 
 namespace deftri {
@@ -415,13 +690,20 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
     std::vector<double> hsum(hd, 0.0), xc(3 * std::max<int64_t>(H.tile_cross, 1), 0.0);
     std::vector<int> xw(std::max<int64_t>(H.tile_cross, 1), 0), xr(std::max<int64_t>(H.tile_cross, 1), 0);
     std::vector<int> lew(H.arap_ids.size(), 0);
+    std::vector<int> dw(d.n_depth, 0);                   // every depth edge summed exactly once
+    const bool multi = H.tile_multi;
+    std::vector<double> qs(3 * (size_t)std::max(H.tile_planes, 0) * nown, 0.0);   // share planes
+    std::vector<int> sw_((size_t)std::max(H.tile_planes, 0) * nown, 0);
     for (int32_t t = 0; t < H.ntile; t++) {
         const int32_t *T = &H.tile_tab[8 * (size_t)t];
-        const int32_t r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6];
+        const int32_t r0 = T[0], nr = T[1], nh = T[2], e0 = T[3], ne = T[4], h0 = T[5], ns = T[6], tq = T[7];
         if (e0 % 64 || ne % 64) { why = "tile entries not chunk aligned"; return -1; }
+        if (multi && (t < H.tile_poff[tq] || t >= H.tile_poff[tq + 1])) { why = "a tile outside its pair's range"; return -1; }
         std::vector<double> pL(3 * (size_t)(nr + nh)), up(3 * (size_t)nr, 0.0), rs(3 * (size_t)std::max(ns, 1), 0.0);
         std::vector<int> rsw(std::max(ns, 1), 0), rsr(std::max(ns, 1), 0);
-        auto grow_of = [&](int32_t i) { return i < nr ? lo + r0 + i : H.tile_halo[h0 + i - nr]; };
+        auto grow_of = [&](int32_t i) {
+            return i < nr ? (multi ? (H.tile_trow[r0 + i] & 0x7fffffff) : lo + r0 + i) : H.tile_halo[h0 + i - nr];
+        };
         for (int32_t i = 0; i < nr + nh; i++)
             for (int c = 0; c < 3; c++) pL[3 * (size_t)i + c] = pl[hd + 3 * (int64_t)grow_of(i) + c];
         int nv = 0, nc = 0;
@@ -439,6 +721,7 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
             lew[le]++;
             const int64_t e = H.arap_ids[le];
             const double *J = Ja + 18 * e;
+            if (multi && d.arap_pair[e] != tq) { why = "an entry of another pair"; return -1; }
             const int ub = (int)(m1 >> 24), sw = (int)((m0 >> 26) & 1u);
             const int ro0 = ub + sw, ro1 = ub + 1 - sw, rf0 = (int)(m0 & 0xfffu), rf1 = (int)((m0 >> 12) & 0xfffu);
             const int rows[4] = {foreign ? rf0 : ro0, foreign ? rf1 : ro1, foreign ? ro0 : rf0, foreign ? ro1 : rf1};
@@ -472,17 +755,18 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
             }
         }
         for (int32_t tr = 0; tr < nr; tr++) {
-            const int32_t l = r0 + tr;
-            const int rsi = H.tile_rs[l], sb = rsi & 0xffff, sc = rsi >> 16;
+            const int32_t l = multi ? (H.tile_trow[r0 + tr] & 0x7fffffff) - lo : r0 + tr;
+            const bool home = !multi || H.tile_trow[r0 + tr] < 0;
+            const int rsi = H.tile_rs[r0 + tr], sb = rsi & 0xffff, sc = rsi >> 16;
             double acc[3];
-            for (int c = 0; c < 3; c++) acc[c] = up[3 * (size_t)tr + c] + lambda * pL[3 * (size_t)tr + c];
+            for (int c = 0; c < 3; c++) acc[c] = up[3 * (size_t)tr + c] + (home ? lambda * pL[3 * (size_t)tr + c] : 0.0);
             for (int k = sb; k < sb + sc; k++) {
                 if (k >= ns) { why = "row slot range out of range"; return -1; }
                 rsr[k]++;
                 for (int c = 0; c < 3; c++) acc[c] += rs[3 * (size_t)k + c];
             }
             const int64_t o = hd + 3 * (int64_t)(lo + l);
-            for (int32_t j = H.rep_off[l]; j < H.rep_off[l + 1]; j++) {
+            for (int32_t j = home ? H.rep_off[l] : 0; home && j < H.rep_off[l + 1]; j++) {
                 const int64_t e = H.rep_ids[j];
                 const double *J = Jr + 6 * e;
                 for (int rr = 0; rr < 2; rr++) {
@@ -495,18 +779,37 @@ int sp_emulate_tile_product(const deftri_problem_desc &d, const SpPlanHost &H, c
                 const int64_t e = H.dep_ids[j];
                 const double *J = Jd + 4 * e;
                 const int32_t sc_ = d.dep_scale[e];
+                if (multi && (sc_ >> 1) != tq) continue;  // another pair's tile sums it
+                dw[e]++;
                 double tt = J[3] * pl[6 * (int64_t)Q + sc_];
                 for (int c = 0; c < 3; c++) tt += J[c] * pl[o + c];
                 for (int c = 0; c < 3; c++) acc[c] += J[c] * Wd[e] * tt;
                 hsum[6 * (int64_t)Q + sc_] += J[3] * Wd[e] * tt;
             }
-            for (int c = 0; c < 3; c++) qr[o + c] = acc[c];
+            if (home) {
+                for (int c = 0; c < 3; c++) qr[o + c] = acc[c];
+            } else {
+                const int64_t j = H.tile_tdst[r0 + tr];
+                if (j < 1 || j > H.tile_planes) { why = "a share's plane out of range"; return -1; }
+                const int64_t x = (j - 1) * nown + l;
+                if (sw_[x]++) { why = "a share written twice"; return -1; }
+                for (int c = 0; c < 3; c++) qs[3 * x + c] = acc[c];
+            }
         }
         for (int32_t k = 0; k < ns; k++)
             if (rsw[k] != 1 || rsr[k] != 1) { why = "an LDS slot not written / read exactly once"; return -1; }
     }
     for (size_t le = 0; le < lew.size(); le++)
         if (lew[le] != 1) { why = "a local edge not visited exactly once"; return -1; }
+    if (H.nranks <= 1)
+        for (int64_t e = 0; e < d.n_depth; e++)
+            if (dw[e] != 1) { why = "a depth edge not summed exactly once"; return -1; }
+    for (int32_t l = 0; l < nown && multi; l++)                 // the update: q + the row's shares
+        for (int32_t j = 1; j < H.tile_nshare[lo + l]; j++) {
+            const int64_t x = (int64_t)(j - 1) * nown + l;
+            if (sw_[x] != 1) { why = "a share not written exactly once"; return -1; }
+            for (int c = 0; c < 3; c++) qr[hd + 3 * (int64_t)(lo + l) + c] += qs[3 * x + c];
+        }
     for (int32_t l = 0; l < nown; l++)
         for (int32_t k = H.tile_xoff[l]; k < H.tile_xoff[l + 1]; k++) {
             const int64_t x = k;
