@@ -69,7 +69,17 @@ def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
     assert r["chi2_initial"] == pytest.approx(meta["chi2_initial"], rel=1e-11)
     assert r["iterations"] == meta["iterations"]
     assert r["trials_iter"] == list(z["trials_iter"])
-    np.testing.assert_allclose(r["chi2_iter"], z["chi2_iter"], rtol=1e-6)
+    # chi2 per iteration within max(4 x the oracle's own spread between elimination orders, 1e-6), the
+    # rule of tests/test_regime_goldens.py: the spread recorded in the golden's oracle_order_spread
+    # (tools/oracle_spread.py; the Simulation C2 run is well conditioned and has none: 1e-6).  Under
+    # Realcolon's weights (Omega_depth 1e12) iteration 9 is conditioning-bound: the device's exact
+    # multifrontal LDL^T lands 1.8e-6 from the oracle and the tile chain 2.3e-6.
+    spread = meta.get("oracle_order_spread", {}).get("max_rel_chi2", 0.0)
+    tol = max(4.0 * spread, 1e-6)
+    dev = np.abs(np.asarray(r["chi2_iter"]) - z["chi2_iter"]) / np.abs(z["chi2_iter"])
+    print(f"{meta.get('regime', 'simulation')}/{plan}: chi2 max rel dev {dev.max():.3e} at {int(dev.argmax())}, "
+          f"oracle order spread {spread:.3e}, tolerance {tol:.3e}")
+    assert dev.max() <= tol, (dev.max(), int(dev.argmax()), tol)
     assert r["lambda_final"] == pytest.approx(meta["lambda_final"], rel=1e-9)
     if meta.get("regime") == "realcolon":             # the pin is meaningful: the solve moves the RMSE
         assert abs(meta["rms_final"]["desv"] - meta["rms_initial"]["desv"]) > 5e-4

@@ -2,7 +2,9 @@
 exact LDL^T step (the oracle's own nested dissection), chi2 per iteration against the committed golden
 (which eliminates in the host analysis' nested-dissection order).  Test infrastructure only.
 
-usage: python tools/oracle_spread.py NAME [SUB]"""
+usage: python tools/oracle_spread.py NAME [SUB]
+       python tools/oracle_spread.py c2_realcolon     (the C2 Realcolon golden, tests/golden/c2_realcolon:
+                                                       about an hour of one core)"""
 import json
 import pathlib
 import sys
@@ -17,11 +19,21 @@ from make_regime_goldens import scene, N_IT   # noqa: E402
 from oracle import oracle                      # noqa: E402
 
 name, sub = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "regimes")
-d = ROOT / "tests" / "golden" / sub
-meta = json.loads((d / f"{name}.json").read_text())
-z = np.load(d / f"{name}.npz")
-p, m, host = scene(name, meta["n_corr"], meta["seed"])
-host.analyse(p)
+if name == "c2_realcolon":
+    from make_c2_golden import REGIMES as C2R, N_CORR, SEED
+    from deftri import capi, sim
+    d = ROOT / "tests" / "golden" / name
+    meta = json.loads((d / "expected_c2.json").read_text())
+    z = np.load(d / "expected_c2.npz")
+    rep, arap, sig, kb8 = C2R["realcolon"]
+    p = sim.two_view_problem(N_CORR, SEED, rep, arap, sig, kb8=getattr(sim, kb8))
+    N_IT = meta["n_iterations"]
+else:
+    d = ROOT / "tests" / "golden" / sub
+    meta = json.loads((d / f"{name}.json").read_text())
+    z = np.load(d / f"{name}.npz")
+    p, m, host = scene(name, meta["n_corr"], meta["seed"])
+    host.analyse(p)
 for label, order in (("oracle_nd", None),):
     oracle.set_vertex_order(order)
     r = oracle.solve_lm(p, N_IT, analytic=False)["report"]

@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(256) k_part_sums(const double *__restrict__ pa
 // entries t, t + 256, ... of it in order.  The per-edge arithmetic is k_lin_chi's; no per-edge chi2
 // is stored.
 __global__ void __launch_bounds__(256) k_trial_eval(const DevProblem P, const EvalJob J, int ept, int nbr, int nbd, int nba,
-                                                   double *__restrict__ part, int *cnt, int flat, const ReadBack rb) {
+                                                   double *__restrict__ part, int *cnt, const ReadBack rb) {
     if (J.gate && !*J.gate) return;
     const int b = blockIdx.x, t = threadIdx.x;
     const int64_t run = 256 * (int64_t)ept;
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(256) k_trial_eval(const DevProblem P, const Ev
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_s_waitcnt(0);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        last = ticket_last(cnt, (int)gridDim.x, b, flat != 0);
+        last = ticket_last(cnt, (int)gridDim.x, b);
     }
     __syncthreads();
     if (!last) return;
@@ -2010,7 +2010,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_partial(const SumJobs J, doub
 // workgroup publishes its partial with an agent-scope atomic store and takes a ticket; the last one
 // forms the totals from the partials (agent-scope loads) and, when rb.h_scal is set, also does
 // k_trial_readback's copies into pinned host memory.  *cnt is 0 between launches.
-__global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt, int flat,
+__global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double *__restrict__ part, int *cnt,
                                                          const ReadBack rb) {
     if (J.gate && !*J.gate) return;
     const SumJob &jb = J.j[blockIdx.y];
@@ -2063,7 +2063,7 @@ __global__ void __launch_bounds__(256) k_sum_multi_fused(const SumJobs J, double
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         __builtin_amdgcn_s_waitcnt(0);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        last = ticket_last(cnt, nblk, (int)(blockIdx.y * gridDim.x + blockIdx.x), flat != 0);
+        last = ticket_last(cnt, nblk, (int)(blockIdx.y * gridDim.x + blockIdx.x));
     }
     __syncthreads();
     if (!last) return;
@@ -2405,8 +2405,7 @@ void launch_factor(const DevPlan &L, hipStream_t st, hipStream_t side, hipEvent_
             if (stp.ntrsm > 0)
                 LAUNCH("trsm", dev::k_trsm, dim3(stp.ntrsm, L.nlanes), dim3(256), st, stp.ntrsm,
                                    L.tasks + 3 * stp.trsm_off, L.fd, L.arena, L.inv, L.lo);
-            static const bool no_side = std::getenv("DEFTRI_NO_SIDE_STREAM") != nullptr;   // A/B experiments
-            if (stp.stream == 1 && !no_side) {
+            if (stp.stream == 1) {
                 // "rest" update of an outer block: after the block's panel chain on the main stream,
                 // concurrent with the next block's lookahead + panel chain there
                 prev_side = cur_side;
@@ -2600,10 +2599,9 @@ void launch_part_sums(const double *part, const int nbk[4], double *out, double 
            gate);
 }
 
-int eval_edges_per_thread() {
-    static const int v = std::getenv("DEFTRI_EVAL_EPT") ? std::max(1, std::min(8, std::atoi(std::getenv("DEFTRI_EVAL_EPT")))) : 2;
-    return v;
-}
+// edges per thread of the trial evaluation: C2 on HIP events (profiles/r05ex_trial_eval_ab.log) 1: 26.0
+// us, 2: 23.2, 4: 23.2, 8: 26.8
+int eval_edges_per_thread() { return 2; }
 
 static void eval_blocks(const DevProblem &P, const EvalJob &J, int &nbr, int &nbd, int &nba, int &nbx) {
     const int64_t run = 256 * (int64_t)eval_edges_per_thread();
@@ -2647,13 +2645,13 @@ void launch_trial_eval(const DevProblem &P, const EvalJob &J, double *part, int 
     // an empty problem still runs one workgroup: the sums are written (0) and the read-back done
     const int grid = std::max(1, nbr + nbd + nba + nbx);
     LAUNCH("trial_eval", dev::k_trial_eval, dim3(grid), dim3(256), st, P, J, eval_edges_per_thread(), nbr, nbd, nba, part,
-           cnt, flat_ticket() ? 1 : 0, rb);
+           cnt, rb);
 }
 
 void launch_sum_multi_fused(const SumJobs &J, double *part, int nparts, int *cnt, const ReadBack &rb, hipStream_t st) {
     if (J.nj <= 0) return;
     LAUNCH("sum_fused", dev::k_sum_multi_fused, dim3(nparts, J.nj), dim3(256), st, J, part, cnt,
-           flat_ticket() ? 1 : 0, rb);
+           rb);
 }
 
 void launch_sum_multi(const SumJobs &J, double *part, int nparts, hipStream_t st) {

@@ -1154,9 +1154,7 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     H.v_heavy.assign(nv, -1);
     H.h_first.push_back(0);
     H.h_dofbase.push_back(0);
-    // A/B knobs (measurements in DESIGN.md): heavy-row chunk size, rows sliced or all generic
-    static const int64_t chunk = [] { const char *e = std::getenv("DEFTRI_PCG_CHUNK"); return e ? std::max(64, std::atoi(e)) : kPcgChunk; }();
-    static const bool no_slice = std::getenv("DEFTRI_PCG_NO_SLICE") != nullptr;
+    const int64_t chunk = kPcgChunk;
     std::vector<int32_t> sliced;
     for (int64_t v = 0; v < nv; v++) {
         const int64_t n = H.ent_begin[v + 1] - H.ent_begin[v];
@@ -1164,7 +1162,7 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
             H.v_heavy[v] = (int32_t)H.heavy_v.size();
             H.heavy_v.push_back((int32_t)v);
             H.h_dofbase.push_back(H.h_dofbase.back() + vdim[v]);
-        } else if (vdim[v] == 3 && !no_slice) {
+        } else if (vdim[v] == 3) {
             sliced.push_back((int32_t)v);
         } else {
             H.light_v.push_back((int32_t)v);
@@ -1219,8 +1217,7 @@ bool build_pcg_host(int64_t nv, const std::vector<int64_t> &voff, const std::vec
     // the whole vector.
     std::vector<int32_t> rows(nsl * 64, -1);
     {
-        static const bool no_xcd = std::getenv("DEFTRI_PCG_NO_XCD") != nullptr;
-        const int nx = (!no_xcd && nsl >= 16) ? 8 : 1;
+        const int nx = nsl >= 16 ? 8 : 1;
         std::vector<int64_t> start(nx + 1, 0);
         for (int x = 0; x < nx; x++) start[x + 1] = start[x] + (nsl - x + nx - 1) / nx;
         for (int64_t b = 0; b < nsl; b++) {
@@ -1383,8 +1380,7 @@ bool build_pcg_mf(int64_t nv, const std::vector<int64_t> &voff, const std::vecto
     const int64_t nsl = ((int64_t)sliced.size() + 63) / 64;
     H.sl_v.assign(nsl * 64, -1);
     {
-        static const bool no_xcd = std::getenv("DEFTRI_PCG_NO_XCD") != nullptr;
-        const int nx = (!no_xcd && nsl >= 16) ? 8 : 1;
+        const int nx = nsl >= 16 ? 8 : 1;
         std::vector<int64_t> start(nx + 1, 0);
         for (int x = 0; x < nx; x++) start[x + 1] = start[x] + (nsl - x + nx - 1) / nx;
         for (int64_t b = 0; b < nsl; b++) {

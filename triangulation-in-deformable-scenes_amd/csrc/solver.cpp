@@ -892,12 +892,6 @@ void pop_state(deftri_ctx *ctx) {
     hipMemcpyAsync(P.tg, P.tg_bak, sizeof(double) * 7 * (size_t)P.Q, hipMemcpyDeviceToDevice, ctx->st);
 }
 
-// DEFTRI_TRIAL_FUSE=0: the trial prologue / read-back as separate copies and fills (A/B)
-bool trial_fuse_on() {
-    static const bool on = [] { const char *e = std::getenv("DEFTRI_TRIAL_FUSE"); return !e || std::atoi(e) != 0; }();
-    return on;
-}
-
 // DEFTRI_TRIAL_EVENTS=1: per-trial timing events on the sequential trial path, for the factor /
 // solve / update split of the report (off by default: each event record is a barrier packet, ~6 us
 // of stream time per event, 4 per trial; measured 0.874 -> 0.849 ms per C2 PCG trial without them)
@@ -1647,10 +1641,9 @@ int pcg_step(deftri_ctx *ctx, double lambda, const double *rhs, bool &solved, in
 }
 
 // the sequential trial (scatter + factorization + solve) as one graph launch: single stream, no
-// cross-rank hooks, no per-launch profiling, no fused-TRSM epochs (DEFTRI_GRAPH=0 disables)
+// cross-rank hooks, no per-launch profiling, no fused-TRSM epochs
 bool trial_graph_usable(const deftri_ctx *ctx) {
-    static const bool off = [] { const char *e = std::getenv("DEFTRI_GRAPH"); return e && std::atoi(e) == 0; }();
-    if (off || ctx->trial_graph_failed || ctx->dist() || ctx->S.trsm_fused || profiling()) return false;
+    if (ctx->trial_graph_failed || ctx->dist() || ctx->S.trsm_fused || profiling()) return false;
     for (const auto &lv : ctx->L.levels)
         for (const auto &stp : lv.steps)
             if (stp.stream != 0) return false;
@@ -1824,7 +1817,7 @@ int deftri_solve_lm(deftri_ctx *ctx, const deftri_lm_params *prm, deftri_report 
         } else do {
             // PCG trials on one rank: the prologue (state backup, flag and PCG records cleared) and
             // the read-back (scalars, flag, the solve's record) are one launch each
-            const bool fused = pcg && !dist && trial_fuse_on();
+            const bool fused = pcg && !dist;
             if (fused) {
                 // after a rejected trial the prologue restores the state from the backup instead
                 pcg_limits(ctx);
@@ -2223,10 +2216,9 @@ int deftri_eval_damped_solve(deftri_ctx *ctx, double lambda, const double *rhs, 
 // ---------------------------------------------------------------------------------------------
 }  // extern "C"
 namespace {
-// a context with a device runs computeR there (DEFTRI_HOST_COMPUTE_R=1: on the host, for A/B timing)
+// a context with a device runs computeR there
 GraphDevice *graph_device(deftri_ctx *ctx) {
-    static const bool host_only = std::getenv("DEFTRI_HOST_COMPUTE_R") != nullptr;
-    if (ctx->device < 0 || host_only) return nullptr;
+    if (ctx->device < 0) return nullptr;
     hipSetDevice(ctx->device);
     if (!ctx->gdev) ctx->gdev.reset(new GraphDevice(ctx->device, ctx->st));
     return ctx->gdev.get();

@@ -202,10 +202,6 @@ struct SpDev {
     int32_t rs = 1, nrb2 = 0;
     int32_t p2u = 8;                                   // phase 2's slots per step (8 or 4)
     int32_t glu = 8;                                   // k_sp_glin_rows' slots per step (8 or 4)
-    // diagnostics (DEFTRI_SP_P2_TRACE=<file>): per phase-2 wave of CG iteration p2tr_it, wall-clock
-    // stamps [start, rows / heavy sums done, alpha known, end, hw id, steps]
-    long long *p2tr = nullptr;
-    int32_t p2tr_it = -1;
     int64_t nslots = 0;                                // wave-layout slots (x 64 lanes)
     const int32_t *rowmap = nullptr, *pmap = nullptr, *pidx = nullptr;
     const int64_t *woff = nullptr;
@@ -266,8 +262,6 @@ struct SpDev {
     double *sbuf = nullptr;                               // [send rows][6]: (z, p) of 3 dofs
     double *m2part = nullptr;                             // phase-2 (r.z, r.r) per workgroup [m_nh + row grid][2]
     double *gsum = nullptr;                               // per XCD group sums [2 sites][8][2]
-    int32_t flat_ticket = 0;                              // single-counter last-workgroup ticket (A/B)
-    int32_t fence = 0;                                    // hand-off by __threadfence instead of coherent stores (A/B)
     int32_t max_it = 0;
     double tol2 = 0;
     // tile mode (G.tile): k_sp_tile (the fused product + p.Ap) and k_sp_tupd (cross slots, alpha, update)
@@ -285,7 +279,6 @@ struct SpDev {
     double *qs = nullptr;                                 // share planes [planes][nown][3]
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     const int32_t *p1list = nullptr;                      // sharded phase 1: the launch's workgroups -> logical ones
-    int32_t txb_fold = 0;                                 // sharded tiles: xb by k_sp_tile's last workgroup
     int32_t tparts = 0;                                   // tile mode: each k_sp_tile workgroup sums the update's
                                                           // (r.z, r.r) partials itself (no ticket chain in k_sp_tupd)
     // device-driven LM (SpSolver::solve_lm_dev): a trial's kernels return at once when *gate == 0, the

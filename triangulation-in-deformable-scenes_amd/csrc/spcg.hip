@@ -98,12 +98,9 @@ __device__ __forceinline__ double lam_of(const SpDev &G, double lam) { return G.
 // agent-scope relaxed atomic stores (coherent across the XCDs' L2s, no L2 write-back); after its
 // stores are acknowledged (s_waitcnt) it takes a ticket; the workgroup that draws the last ticket
 // reads every partial with agent-scope atomic loads and forms the sums in a fixed order, so the
-// result does not depend on the arrival order.  G.fence = 1: plain stores and loads around
-// __threadfence() instead (a whole-L2 write-back per workgroup on gfx950; kept for A/B).
-__device__ __forceinline__ void publish(const SpDev &G, double *p, double v) {
-    if (G.fence) *p = v;
-    else st_sc1(p, v);
-}
+// result does not depend on the arrival order.  (Plain stores and loads around __threadfence()
+// instead: a whole-L2 write-back per workgroup on gfx950, measured slower in round 3.)
+__device__ __forceinline__ void publish(double *p, double v) { st_sc1(p, v); }
 __device__ __forceinline__ double fetch(const double *p) {     // a partial published in this launch
     return ld_sc1(p);
 }
@@ -360,18 +357,14 @@ __global__ void __launch_bounds__(256) k_sp_glin_heavy(const SpDev G) {
         double t = 0.0;
 #pragma unroll
         for (int gg = 0; gg < 8; gg++) t += lds[gg][threadIdx.x];
-        publish(G, G.chpart + (int64_t)kSpLin * ch + threadIdx.x, t);
+        publish(G.chpart + (int64_t)kSpLin * ch + threadIdx.x, t);
     }
     const int c0 = G.hch_off[h], c1 = G.hch_off[h + 1];
     if (threadIdx.x == 0) {
-        if (G.fence) __threadfence();
-        else {
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         last = __hip_atomic_fetch_add(G.hcnt + h, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == c1 - c0 - 1;
-        if (last && G.fence) __threadfence();
     }
     __syncthreads();
     if (!last) return;
@@ -492,8 +485,7 @@ __device__ bool inv6(const double *Hl, double lam, double *Mo) {
     return true;
 }
 
-// pub: 0 plain stores; 1 partials for a last-workgroup hand-off (agent-scope stores; callers pass 0
-// under G.fence)
+// pub: 0 plain stores; 1 partials for a last-workgroup hand-off (agent-scope stores)
 __device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4], double *out, int pub = 0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     a0 = wave_sum(a0);
@@ -517,14 +509,10 @@ __device__ __forceinline__ void pair_tree(double a0, double a1, double (*red)[4]
 __device__ __forceinline__ bool last_block(const SpDev &G, int *cnt) {
     __shared__ int last;
     if (threadIdx.x == 0) {
-        if (G.fence) __threadfence();
-        else {
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);         // the published stores acknowledged
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        }
-        last = ticket_last(cnt, (int)gridDim.x, (int)blockIdx.x, G.flat_ticket);
-        if (last && G.fence) __threadfence();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);             // the published stores acknowledged
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        last = ticket_last(cnt, (int)gridDim.x, (int)blockIdx.x);
     }
     __syncthreads();
     return last;
@@ -542,17 +530,13 @@ __device__ __forceinline__ bool group_sum(const SpDev &G, int *cnt, const double
     const int nb = (int)gridDim.x, x = (int)blockIdx.x & 7;
     const int gsize = (nb - x + 7) >> 3, ngroups = nb < 8 ? nb : 8;
     auto settle = [&] {                  // this thread's published stores acknowledged
-        if (G.fence) __threadfence();
-        else {
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            __builtin_amdgcn_s_waitcnt(0);
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_s_waitcnt(0);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
     };
     if (threadIdx.x == 0) {
         settle();
         flag = __hip_atomic_fetch_add(cnt + 1 + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
-        if (flag && G.fence) __threadfence();
     }
     __syncthreads();
     if (!flag) return false;
@@ -571,12 +555,11 @@ __device__ __forceinline__ bool group_sum(const SpDev &G, int *cnt, const double
     __syncthreads();
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int v = 0; v < NV; v++) publish(G, gs + NV * x + v, (red[v][0] + red[v][1]) + (red[v][2] + red[v][3]));
+        for (int v = 0; v < NV; v++) publish(gs + NV * x + v, (red[v][0] + red[v][1]) + (red[v][2] + red[v][3]));
         st_sc1(cnt + 1 + x, 0);          // the group is done: nobody else touches its counter
         settle();
         flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
         if (flag) {
-            if (G.fence) __threadfence();
             st_sc1(cnt, 0);
 #pragma unroll
             for (int v = 0; v < NV; v++) {
@@ -717,7 +700,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_setup(const SpDev G, cons
 #pragma unroll
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
         double *out = G.upart + 2 * slot;
-        if (G.fuse && !G.fence) {
+        if (G.fuse) {
             st_sc1(out, s0);
             st_sc1(out + 1, s1);
         } else {
@@ -785,12 +768,12 @@ __device__ __forceinline__ void heavy_sums_block(const SpDev &G, int h, double *
         }
         for (; i < G.nrb2; i += 256) a += fetch(G.rpart + i);
         a = block_sum(a, red4);
-        if (threadIdx.x == 0) publish(G, G.hbuf, a);
+        if (threadIdx.x == 0) publish(G.hbuf, a);
         return;
     }
     const int o = heavy_dof(G, h);
     const double t = heavy_part_sum(G, h, lds);
-    if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) publish(G, G.hbuf + 1 + o + threadIdx.x, t);
+    if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) publish(G.hbuf + 1 + o + threadIdx.x, t);
     __syncthreads();
 }
 
@@ -1075,19 +1058,6 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
     if (gated_off(G.gate)) return;
     lam = lam_of(G, lam);
     double beta = 0.0;
-    long long *trw = nullptr;                               // diagnostics: this wave's stamps
-    if (G.p2tr && it == G.p2tr_it) {
-        trw = G.p2tr + 6 * ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6));
-        if ((threadIdx.x & 63) == 0) {
-            unsigned hw;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            trw[0] = wall_clock64();
-            trw[4] = hw;
-        }
-    }
-    auto stamp = [&](int i, long long v = -1) {
-        if (trw && (threadIdx.x & 63) == 0) trw[i] = v < 0 ? wall_clock64() : v;
-    };
     if constexpr (MG == 2) {
         if (G.rec[0] != 0.0) return;
         if ((int)blockIdx.x < G.m_nh) {
@@ -1251,13 +1221,11 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             while (k + 3 * 64 < k1) step(std::integral_constant<int, 4>{}, false);
             if (k < k1) step(std::integral_constant<int, 4>{}, true);           // 1..3
         }
-        stamp(5, s1 - s0);
     }
     if (rows && w < G.nwaves && G.wsplit[w]) {          // lane pairs (wave-uniform): j's sums + j + 32's
 #pragma unroll
         for (int c = 0; c < 3; c++) q[c] += __shfl_xor(q[c], 32);
     }
-    stamp(1);
     if (G.rs > 1) {
         // parts 1.. hand their sums to part 0 (uniform: every workgroup of the launch passes here)
         if (part > 0) {
@@ -1312,7 +1280,6 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
         return;
     } else if constexpr (MG == 1) {
         if (!G.alpha_kernel && blockIdx.x != 0) alpha = m2_alpha_wait(G, it);
-        stamp(2);
         if (hv >= 0) {
             // thread a < dim: component a of the vertex (k_sp_update's heavy arithmetic; r through
             // LDS, so no private arrays); its (r.z, r.r) terms added in component order
@@ -1363,14 +1330,13 @@ k_sp_phase2(int it, const SpDev G, double lam, const JT *__restrict__ pj) {
             }
         }
         __shared__ double red[2][4];
-        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);   // (kernel args never by address)
+        pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, 1);   // (kernel args never by address)
         m2_dots(G, it, red);
-        stamp(3);
         return;
     }
     const double sm = block_sum(pq, red4);
     if (threadIdx.x == 0 && lb < max(G.nrb2, 1)) {
-        if (G.fuse_heavy) publish(G, G.rpart + lb, sm);
+        if (G.fuse_heavy) publish(G.rpart + lb, sm);
         else G.rpart[lb] = sm;
     }
     if (G.fuse_heavy && last_block(G, G.cnt)) {
@@ -1491,7 +1457,7 @@ __global__ void __launch_bounds__(3 * kSpUpdRows) k_sp_update(int it, const SpDe
 #pragma unroll
         for (int k = 0; k < nw; k++) { s0 += red[0][k]; s1 += red[1][k]; }
         double *out = G.upart + 2 * slot;
-        if (G.fuse && !G.fence) {
+        if (G.fuse) {
             st_sc1(out, s0);
             st_sc1(out + 1, s1);
         } else {
@@ -1744,40 +1710,6 @@ __device__ __forceinline__ double tile_heavy_sum(const SpDev &G, int h, double *
     return t;
 }
 
-// sharded tiles with G.txb_fold: every logical workgroup (over the interior and boundary launches of
-// one product) publishes its partials and draws a ticket; the last forms the rank's record xb as
-// k_sp_txb does (its own launch otherwise) and resets the counter
-__device__ __forceinline__ void tile_sd_tail(const SpDev &G, double *lds, double *red4) {
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_s_waitcnt(0);             // the published partials acknowledged
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        s_last = __hip_atomic_fetch_add(G.cnt + 48, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G.t_grid - 1;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    for (int h = 0; h < G.Q + G.S; h++) {
-        const double t = tile_heavy_sum(G, h, lds, true);
-        if ((int)threadIdx.x < (h < G.Q ? 6 : 1)) G.xb[3 + heavy_dof(G, h) + threadIdx.x] = t;
-        __syncthreads();
-    }
-    double a = 0.0;
-    for (int j = threadIdx.x; j < G.t_grid; j += 256) a += fetch(G.m1part + j);
-    a = block_sum(a, red4);
-    double a0 = 0.0, a1 = 0.0;
-    for (int j = threadIdx.x; j <= G.nrb; j += 256) { a0 += G.upart[2 * j]; a1 += G.upart[2 * j + 1]; }
-    a0 = block_sum(a0, red4);
-    a1 = block_sum(a1, red4);
-    if (threadIdx.x == 0) {
-        G.xb[0] = a0;
-        G.xb[1] = a1;
-        G.xb[2] = a;
-        st_sc1(G.cnt + 48, 0);
-    }
-}
-
 template <class JT, int SD = 0>
 __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT *__restrict__ Jarap, double lam) {
     extern __shared__ double lds[];
@@ -1853,11 +1785,7 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         }
         if (!G.include_heavy) pap = 0.0;
         pap = block_sum(pap, red[0]);
-        if (tid == 0) {
-            if (SD && G.txb_fold) publish(G, G.m1part + b, pap);
-            else G.m1part[b] = pap;
-        }
-        if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
+        if (tid == 0) G.m1part[b] = pap;
         return;
     }
     if (t < G.ntile) {
@@ -2006,11 +1934,9 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     __syncthreads();
     if (tid < 9) {
         const double v = (red[tid][0] + red[tid][1]) + (red[tid][2] + red[tid][3]);
-        if (SD && G.txb_fold) publish(G, tid == 0 ? G.m1part + b : G.part + (int64_t)kSpPart * b + tid - 1, v);
-        else if (tid == 0) G.m1part[b] = v;
+        if (tid == 0) G.m1part[b] = v;
         else G.part[(int64_t)kSpPart * b + tid - 1] = v;
     }
-    if (SD && G.txb_fold) tile_sd_tail(G, lds, red[0]);
 }
 
 // FIN 0: the CG update of iteration it (merged-chain hand-off); FIN 1: the product only — q of every
@@ -2130,7 +2056,7 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
         pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, 0);
         return;
     }
-    pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, G.fence ? 0 : 1);
+    pair_tree(pq, rr2, red, G.m2part + 2 * blockIdx.x, 1);
     m2_dots(G, it, red);
 }
 
@@ -2312,7 +2238,7 @@ void sp_launch_tile_sd(const SpDev &G, int it, double lambda, bool fp32, hipStre
         else hipLaunchKernelGGL((sp::k_sp_tile<double, 1>), dim3(n), dim3(256), (size_t)G.tile_lds, st, it, g, G.Ja, lambda);
         prof_end("sp_tile", e0_, (unsigned)n, 0.0, st);
     }
-    if (txb && !G.txb_fold) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
+    if (txb) SPL("sp_txb", sp::k_sp_txb, G.Q + G.S + 2, it, G);
 }
 
 void sp_launch_tile_product(const SpDev &G, double lambda, bool fp32, hipStream_t st) {

@@ -285,13 +285,12 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     //     couplings; descending, stable) in windows of kSpSortWindow rows: the order the phase-2 wave
     //     layout deals them to lanes (8b), so that layout is the identity and a wave's 64 rows are 64
     //     consecutive rows (the per-row vectors then load coalesced).  Every rank permutes every range
-    //     the same way, so the global numbering agrees across ranks.  (DEFTRI_SP_NO_ROWSORT=1: A/B)
+    //     the same way, so the global numbering agrees across ranks.
     //     The edges keep the Morton order (mrow, below): an edge run then walks its points, their
     //     rotations and (z, p) in spatial order (C2 under rocprofv3: k_lin_chi 19.3 vs 24.9 us, phase 1
     //     20.9 vs 23.6 with edges by the sorted rows).
-    static const bool no_rowsort = std::getenv("DEFTRI_SP_NO_ROWSORT") != nullptr;
     const std::vector<int32_t> mrow = H.row_of_point;     // Morton (pre-sort) row of each point
-    if (!no_rowsort && !H.tile) {
+    if (!H.tile) {
         // slot counts per row: per-chunk counts over the incidences on host threads, summed per row
         const int64_t ninc = 4 * E + D;
         const int64_t nch = std::max<int64_t>(1, std::min<int64_t>(16, ninc / (1 << 20)));
@@ -527,15 +526,12 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     stage("8 incidences");
     // 8b. phase-2 wave layout: per own row its ARAP incidences then its depth couplings; rows sorted by
     //     that count (descending, stable) inside windows of kSpSortWindow rows, 64 per wave.  A wave
-    //     whose rows hold more than kSpWaveSplit slots (DEFTRI_SP_WAVE_SPLIT; 0 = never) takes 32
+    //     whose rows hold more than kSpWaveSplit slots takes 32
     //     rows instead, each on a lane pair: lane j the first ceil(c / 2) slots of its row, lane j + 32
     //     the rest (rowmap -1: the pair's sums go to lane j) — the longest waves' step counts halve,
     //     which is what bounds phase 2 and the rows' linearization (their span, not their bytes)
     {
-        static const int split_t = [] {
-            const char *e = std::getenv("DEFTRI_SP_WAVE_SPLIT");
-            return e ? std::atoi(e) : kSpWaveSplit;
-        }();
+        const int split_t = kSpWaveSplit;
         std::vector<int32_t> cnt(nown);
         for (int32_t l = 0; l < nown; l++)
             cnt[l] = (int32_t)(H.inc_off[l + 1] - H.inc_off[l]) + (H.dep_off[l + 1] - H.dep_off[l]);

@@ -39,20 +39,6 @@ constexpr int kSpMaxIt = 4096;
 constexpr int kSpDefaultIt = 1000;
 constexpr int kSpRedParts = 512;
 constexpr int kSpRecDoubles = 8;
-// the host LM's trial evaluation finishes its sums on the host (DEFTRI_EVAL_DEVICE_SUMS=1: the
-// evaluation's last workgroup; DEFTRI_EVAL_SPLIT=1: round 5's two launches)
-bool eval_host_sums() {
-    static const bool v = std::getenv("DEFTRI_EVAL_DEVICE_SUMS") == nullptr && std::getenv("DEFTRI_EVAL_SPLIT") == nullptr;
-    return v;
-}
-
-// one rank: the linearization's chi2 summed from its workgroups' partials (DEFTRI_LIN_CHI_ARRAYS=1:
-// per-edge chi2 and the fixed-order sums of round 5)
-bool lin_part_sums() {
-    static const bool v = std::getenv("DEFTRI_LIN_CHI_ARRAYS") == nullptr;
-    return v;
-}
-
 // the host loop's per-trial wait: poll the stream (no interrupt wake-up; the thread waits anyway) —
 // DEFTRI_SYNC_BLOCK=1: hipStreamSynchronize
 hipError_t stream_wait(hipStream_t st) {
@@ -72,13 +58,10 @@ hipError_t stream_wait(hipStream_t st) {
 }
 
 // workgroups per job of the fused chi2 sums: every one takes a ticket on one counter, so fewer, larger
-// chunks (DEFTRI_SP_SUM_PARTS overrides, up to kSpRedParts)
-int sum_parts() {
-    // C2 under rocprofv3 (profiles/r03sp_sum_parts.json): 64 parts 11.1 us, 128 12.9, 256 18.5, 512 27.9 —
-    // every workgroup's ticket costs more than its share of the sum saves
-    static const int v = std::getenv("DEFTRI_SP_SUM_PARTS") ? std::atoi(std::getenv("DEFTRI_SP_SUM_PARTS")) : 64;
-    return std::max(1, std::min(v, kSpRedParts));
-}
+// chunks.  C2 under rocprofv3 (profiles/r03sp_sum_parts.json): 64 parts 11.1 us, 128 12.9, 256 18.5,
+// 512 27.9 — every workgroup's ticket costs more than its share of the sum saves
+constexpr int kSumParts = 64;
+static_assert(kSumParts <= kSpRedParts, "sum parts");
 
 void quat_norm(double *q) {      // SE3Quat::normalizeRotation
     if (q[3] < 0) { q[0] = -q[0]; q[1] = -q[1]; q[2] = -q[2]; q[3] = -q[3]; }
@@ -252,7 +235,7 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     // context on the single-reduction chain (the product on z there); DEFTRI_SP_NO_TILE=1 keeps the
     // two-phase product everywhere, DEFTRI_SP_SD_NO_TILE=1 on sharded contexts
     static const bool no_tile = std::getenv("DEFTRI_SP_NO_TILE") != nullptr;
-    static const bool sd_no_tile = std::getenv("DEFTRI_SP_SD_NO_TILE") != nullptr || std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
+    static const bool sd_no_tile = std::getenv("DEFTRI_SP_SD_NO_TILE") != nullptr;
     const int64_t ndof_ = 6 * (int64_t)d.n_pairs + d.n_scales + 3 * (int64_t)d.n_points;
     const bool want_tile = !no_tile && (d.n_pairs == 1 || !shard_) &&
                            (shard_ ? !sd_no_tile
@@ -338,9 +321,8 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     {
         // k_sp_glin_blocks' groups: up to kSpGlinGroup consecutive owned ARAP blocks of one pair with
         // contiguous edges per workgroup (its 27 sums reduced once per group, not per 256 edges); any
-        // other block alone.  DEFTRI_SP_GLIN_GROUP=1: one block per workgroup (round 4)
-        static const char *ge = std::getenv("DEFTRI_SP_GLIN_GROUP");
-        const int gmax = ge ? std::max(1, std::atoi(ge)) : kSpGlinGroup;
+        // other block alone
+        const int gmax = kSpGlinGroup;
         std::vector<int32_t> gl;
         const int32_t nb = (int32_t)(H.blk.size() / 4);
         for (int32_t b = 0; b < nb;) {
@@ -402,9 +384,6 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         const int64_t heavy_parts = H.hv_blk_off.empty() ? 0 : H.hv_blk_off.back();
         G.fuse = (!shard_ && !no_fuse) ? 1 : 0;
         G.fuse_heavy = (G.fuse && heavy_parts <= kSpFuseHeavyMax && Q + S <= 64) ? 1 : 0;
-        static const bool fence = std::getenv("DEFTRI_SP_FENCE") != nullptr;
-        G.fence = fence ? 1 : 0;
-        G.flat_ticket = flat_ticket() ? 1 : 0;
         // one rank, from kSpMergeMinDof unknowns: two launches per CG iteration (merged chain; alpha
         // from p.Ap).  Smaller problems keep the three-launch chain (alpha from p.q): they are the
         // badly conditioned ones here (thousands of CG iterations per step), where the two alpha
@@ -415,15 +394,12 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         G.merged = (G.fuse && !no_merge && Q + S <= 4096 && (force_merge || G.ndof >= kSpMergeMinDof)) ? 1 : 0;
         G.m_nx = 8 * ((G.nrb + 1 + 7) / 8);
         G.m_nh = 8 * ((Q + S + 7) / 8);
-        static const bool ak = std::getenv("DEFTRI_SP_ALPHA_KERNEL") != nullptr;
-        G.alpha_kernel = ak ? 1 : 0;
+        G.alpha_kernel = 0;                        // (1 after a hand-off timeout: hand_off_timeout)
         // tests: every waiter of this CG iteration's alpha hand-off times out (the error path)
         static const int inj = std::getenv("DEFTRI_SP_INJECT_TIMEOUT_IT") ? std::atoi(std::getenv("DEFTRI_SP_INJECT_TIMEOUT_IT")) : -1;
         G.inj_timeout_it = inj;
-        // sharded: the single-reduction chain (3 launches + one all-reduce per CG iteration);
-        // DEFTRI_SP_TWO_REDUCTIONS=1 keeps the round-3 six-launch chain for A/Bs
-        static const bool two_red = std::getenv("DEFTRI_SP_TWO_REDUCTIONS") != nullptr;
-        G.sd = (shard_ && !two_red) ? 1 : 0;
+        // sharded: the single-reduction chain (3 launches + one all-reduce per CG iteration)
+        G.sd = shard_ ? 1 : 0;
         if (G.sd) G.m_nh = 8 * ((Q + S + 2 + 7) / 8);   // + the z.Az and (r.z, r.r) workgroups
     }
     {
@@ -499,11 +475,9 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         // from kSpTilePartsMax tiles (the multi-keyframe graphs: C3 has 12k) the ticketed sums and the
         // alpha hand-off take over, as on the sharded chain (whose record is all-reduced)
         G.tparts = (G.sd || G.t_grid > kSpTilePartsMax) ? 0 : 1;
-        // sharded: the rank's record xb in its own small launch (k_sp_txb); DEFTRI_SP_TXB_FOLD=1 forms
-        // it in the product's last workgroup instead (a ticket over both product launches) — the
-        // same on the 2-rank gloo rehearsal (165.8 vs 171.8 LM it/s), so the simpler order stays
-        static const bool txb_fold = std::getenv("DEFTRI_SP_TXB_FOLD") != nullptr;
-        G.txb_fold = (G.sd && txb_fold) ? 1 : 0;
+        // sharded: the rank's record xb in its own small launch (k_sp_txb) — forming it in the
+        // product's last workgroup instead (a ticket over both product launches) measured the same on
+        // the 2-rank gloo rehearsal (165.8 vs 171.8 LM it/s), so the simpler order stays
     }
     ALLOC(G.s, nloc); ALLOC(G.part, (int64_t)kSpPart * std::max(G.nblk, G.t_grid)); ALLOC(G.rpart, std::max(G.nrb2, 1));
     ALLOC(G.upart, 2 * (int64_t)(G.nrb + 1)); ALLOC(G.hbuf, 1 + H.hd);
@@ -512,13 +486,6 @@ int SpSolver::upload(const deftri_problem_desc &d) {
     G.m1n = G.tile ? G.t_grid : sp_merged_grid1(G);
     ALLOC(G.m1part, std::max(G.m1n, sp_merged_grid1(G)));
     ALLOC(G.m2part, 2 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb + 7) / 8))); ALLOC(G.gsum, 32);
-    if (std::getenv("DEFTRI_SP_P2_TRACE")) {               // diagnostics: phase-2 wave stamps
-        const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
-        ALLOC(G.p2tr, 6 * nw);
-        SPOK(hipMemset(G.p2tr, 0, sizeof(long long) * 6 * (size_t)nw));
-        const char *e = std::getenv("DEFTRI_SP_P2_TRACE_IT");
-        G.p2tr_it = e ? std::atoi(e) : 2;
-    }
     ALLOC(G.cnt, 64);      // three ticket sites (0, 16, 32: 9 counters each), the tile arrival (44), the sharded tiles' (48)
     SPOK(hipMemset(G.cnt, 0, 64 * sizeof(int)));
     {
@@ -766,20 +733,6 @@ int SpSolver::sd_exchange(int next_it, double lambda) {
 int SpSolver::eval_chi2(bool analytic, int slot, const SumJob *extra, const ReadBack *rb, double *h_part,
                         double *rec_clear, int64_t nclear) {
     (void)analytic;                  // errors only: the Jacobian mode does not enter
-    static const bool split = std::getenv("DEFTRI_EVAL_SPLIT") != nullptr;
-    if (split) {                     // A/B: round 5's two launches (k_lin_chi, then the fixed-order sums)
-        launch_lin_chi(P, st_);
-        SumJobs S;
-        S.j[0].n = P.R; S.j[0].a = P.chi_rep; S.j[0].out = d_scal + 4;
-        S.j[1].n = P.D; S.j[1].a = P.chi_dep; S.j[1].out = d_scal + 5;
-        S.j[2].n = H.n_arap_owned; S.j[2].a = P.chi_arap; S.j[2].out = d_scal + 6;
-        S.nj = 3;
-        if (extra) S.j[S.nj++] = *extra;
-        S.total = d_scal + slot;
-        S.gate = P.gate_trial;
-        launch_sum_multi_fused(S, d_part, sum_parts(), d_sumcnt, rb ? *rb : ReadBack{}, st_);
-        return 0;
-    }
     // the edges' errors and every sum in one launch (k_trial_eval)
     EvalJob J;
     J.n_arap = H.n_arap_owned;
@@ -812,7 +765,7 @@ double SpSolver::lin_chi_host() const {
 int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok, bool host_chi) {
     ok = true;
     lin_host_pending_ = false;
-    if (!shard_ && lin_part_sums()) {
+    if (!shard_) {
         // per-workgroup chi2 partials from the linearization's own launches (no per-edge chi2, no
         // separate sum launch on the host loop)
         P.lin_part = host_chi ? h_lpart_ : d_lpart_;
@@ -828,7 +781,7 @@ int SpSolver::lin_iteration(bool analytic, bool want_max, bool &ok, bool host_ch
         J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
         J.nj = 3;
         J.total = d_scal;
-        launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
+        launch_sum_multi_fused(J, d_part, kSumParts, d_sumcnt, ReadBack{}, st_);
     }
     int rc;
     if (shard_ && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
@@ -1011,22 +964,11 @@ int SpSolver::solve_lm_dev(const deftri_lm_params &prm, deftri_report &R) {
     auto enqueue = [&]() -> int {
         const bool first = queued == 0;
         // linearization (gate_lin): errors + Jacobians, chi2 sums, the rows' / heavy blocks, b
-        if (lin_part_sums()) {              // the host loop's partials and order (bit-identical chi2)
-            P.lin_part = d_lpart_;
-            launch_linearize(P, st_, true, analytic);
-            P.lin_part = nullptr;
-            launch_part_sums(d_lpart_, lin_nb_, d_scal + 4, nullptr, d_scal, &d_lm->gate_lin, st_);
-        } else {
-            launch_linearize(P, st_, true, analytic);
-            SumJobs J;
-            J.j[0].n = P.R; J.j[0].a = P.chi_rep; J.j[0].out = d_scal + 4;
-            J.j[1].n = P.D; J.j[1].a = P.chi_dep; J.j[1].out = d_scal + 5;
-            J.j[2].n = H.n_arap_owned; J.j[2].a = P.chi_arap; J.j[2].out = d_scal + 6;
-            J.nj = 3;
-            J.total = d_scal;
-            J.gate = &d_lm->gate_lin;
-            launch_sum_multi_fused(J, d_part, sum_parts(), d_sumcnt, ReadBack{}, st_);
-        }
+        // (the host loop's partials and order: bit-identical chi2)
+        P.lin_part = d_lpart_;
+        launch_linearize(P, st_, true, analytic);
+        P.lin_part = nullptr;
+        launch_part_sums(d_lpart_, lin_nb_, d_scal + 4, nullptr, d_scal, &d_lm->gate_lin, st_);
         if (fp32_jac) sp_launch_cvt_j(P.Jarap, const_cast<float *>(G.Ja32), 18 * G.jld, st_, &d_lm->gate_lin);
         sp_launch_glin(G, fp32_jac != 0, st_);
         if (first) {
@@ -1191,8 +1133,8 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
     const int64_t den_off = rank_ == 0 ? 0 : G.hd + 3 * (int64_t)G.row0;
     const int64_t den_n = rank_ == 0 ? G.hd + 3 * (int64_t)G.nown : 3 * (int64_t)G.nown;
     double t_lin = 0;
-    // the trial's sums finished on the host (DEFTRI_EVAL_DEVICE_SUMS=1: by the evaluation's last workgroup)
-    const bool host_sums = eval_host_sums();
+    // (one rank) the trial's sums are finished on the host; sharded, by the evaluation's last workgroup
+    // before the all-reduce
     bool sums_pending = false;
     // DEFTRI_HOST_TIMING=1: the host's time from a trial's wait to the next launch call (a further
     // trial's setup or the next linearization) and the linearization's launch calls, per solve
@@ -1210,10 +1152,9 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                              n_lin ? lin_issue / (n_lin + 1) : 0.0, n_issue ? trial_issue / n_issue : 0.0);
         }
     } ht;
-    // one rank, host sums: k_trial_begin folded away — the backup into the trial's state update, the
-    // records' clear into the evaluation (DEFTRI_TRIAL_BEGIN=1: the prologue launch)
-    static const bool fold_env = std::getenv("DEFTRI_TRIAL_BEGIN") == nullptr;
-    const bool fold = fold_env && host_sums && !dist;
+    // one rank: k_trial_begin folded away — the backup into the trial's state update, the records'
+    // clear into the evaluation (sharded: the prologue launch)
+    const bool fold = !dist;
     if (fold) {                                   // the first trial's records start clear
         SPOK(hipMemsetAsync(G.rec, 0, sizeof(double) * (size_t)nrec, st_));
         SPOK(hipMemsetAsync(d_flag, 0, sizeof(int), st_));
@@ -1263,18 +1204,11 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
                 SumJob den;
                 den.n = den_n; den.a = G.x + den_off; den.b = G.b + den_off; den.lambda = lambda; den.mode = 1;
                 den.out = d_scal + 1;
-                if (!dist && host_sums) {   // workgroup partials to the host, which finishes the sums
+                if (!dist) {         // workgroup partials to the host, which finishes the sums
                     ReadBack rb;
                     rb.flag = d_flag; rb.rec = G.rec; rb.nrec = kSpRecDoubles; rb.h_flag = ipin; rb.h_rec = hpin + 16;
-                    eval_chi2(analytic, 0, &den, &rb, h_epart_, fold ? G.rec : nullptr, nrec);
+                    eval_chi2(analytic, 0, &den, &rb, h_epart_, G.rec, nrec);
                     sums_pending = true;
-                    return 0;
-                }
-                if (!dist) {         // the read-back rides the sums' last workgroup
-                    ReadBack rb;
-                    rb.scal = d_scal; rb.ns = 2; rb.flag = d_flag; rb.rec = G.rec; rb.nrec = kSpRecDoubles;
-                    rb.h_scal = sc; rb.h_flag = ipin; rb.h_rec = hpin + 16;
-                    eval_chi2(analytic, 0, &den, &rb);
                     return 0;
                 }
                 eval_chi2(analytic, 0, &den);
@@ -1296,12 +1230,9 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
             const auto tt0 = std::chrono::steady_clock::now();
             if ((rc = cg_setup(lambda, G.b))) return rc;
             // CG iterations queued before the trial's evaluation: the last converged count + a
-            // margin (DEFTRI_SP_GUESS_MARGIN).  A short guess costs the evaluation, a state restore
-            // and a host round trip; each extra queued iteration past convergence two early-out
-            // launches
-            static const int margin = std::getenv("DEFTRI_SP_GUESS_MARGIN") ? std::atoi(std::getenv("DEFTRI_SP_GUESS_MARGIN"))
-                                                                            : kSpGuessMargin;
-            const int n = std::min(std::max(2, last_its + margin), mx);
+            // margin.  A short guess costs the evaluation, a state restore and a host round trip;
+            // each extra queued iteration past convergence two early-out launches
+            const int n = std::min(std::max(2, last_its + kSpGuessMargin), mx);
             if ((rc = cg_chain(lambda, 0, n))) return rc;
             int j = n;
             if ((rc = cg_tail(j, lambda))) return rc;
@@ -1384,18 +1315,6 @@ int SpSolver::solve_lm(const deftri_lm_params &prm, deftri_report &R) {
         if (prm.verbose)
             std::fprintf(stderr, "[deftri/sp] it %d chi2 %.9e lambda %.6e trials %d\n", it, currentChi, lambda, qmax);
         if (qmax == max_trials || rho == 0 || !std::isfinite(lambda)) { status = DEFTRI_STATUS_TERMINATE; it++; break; }
-    }
-    if (G.p2tr) {                                          // diagnostics: the last stamped launch
-        const int64_t nw = 4 * (int64_t)std::max(sp_merged_grid2(G), G.m_nh + 8 * ((G.nrb2 + 7) / 8) + G.Q + G.S);
-        std::vector<long long> h(6 * (size_t)nw);
-        SPOK(hipStreamSynchronize(st_));
-        SPOK(hipMemcpy(h.data(), G.p2tr, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
-        if (FILE *f = std::fopen(std::getenv("DEFTRI_SP_P2_TRACE"), "wb")) {
-            const long long hdr[4] = {nw, G.m_nh, G.rs, G.p2u};
-            std::fwrite(hdr, sizeof(hdr), 1, f);
-            std::fwrite(h.data(), sizeof(long long), h.size(), f);
-            std::fclose(f);
-        }
     }
     eval_chi2(analytic, 0, nullptr);
     if (dist && (rc = tr_->allreduce(d_scal, 1, 0, st_))) return rc;
@@ -1556,7 +1475,7 @@ int SpSolver::profile_trial(double lambda, KProf &prof, bool analytic) {
         SumJob den;
         den.n = G.hd + 3 * (int64_t)G.nown; den.a = G.x; den.b = G.b; den.lambda = lambda; den.mode = 1;
         den.out = d_scal + 1;
-        rc = eval_chi2(analytic, 0, &den, nullptr, eval_host_sums() ? h_epart_ : nullptr);
+        rc = eval_chi2(analytic, 0, &den, nullptr, h_epart_);
     }
     set_profiler(nullptr);
     if (rc) return rc;

@@ -381,6 +381,19 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         for (const auto &x : xt) H.tile_xdst[x.second] = fill[x.first]++;
     }
     lap("cross slots");
+    if (timing && nt > 0) {                        // the tiles' shapes: entries, rows, halo rows, slots
+        for (int f = 1; f <= 6; f++) {
+            if (f == 3 || f == 5) continue;
+            std::vector<int32_t> v(nt);
+            for (int32_t t = 0; t < nt; t++) v[t] = H.tile_tab[8 * (size_t)t + f];
+            std::sort(v.begin(), v.end());
+            double s = 0;
+            for (int32_t x : v) s += x;
+            std::fprintf(stderr, "[deftri plan]   4a tiles %d, %-6s min %d mean %.1f p50 %d p90 %d max %d\n", nt,
+                         f == 1 ? "rows" : f == 2 ? "halo" : f == 4 ? "ne" : "slots", v[0], s / nt, v[nt / 2],
+                         v[(size_t)(0.9 * nt)], v[nt - 1]);
+        }
+    }
     H.ntile = nt;
     H.tile_entries = (int64_t)m0.size();
     H.tile_cross = nx;

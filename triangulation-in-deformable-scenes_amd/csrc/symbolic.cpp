@@ -352,11 +352,6 @@ struct Builder {
             else { xy[2 * p] = d.points[3 * (int64_t)p]; xy[2 * p + 1] = d.points[3 * (int64_t)p + 1]; }
         }
 
-        if (const char *e = std::getenv("DEFTRI_ND_TRY")) nd_try = std::atoi(e);
-        if (const char *e = std::getenv("DEFTRI_ND_PASSES")) nd_passes = std::atoi(e);
-        if (const char *e = std::getenv("DEFTRI_ND_BAL")) nd_bal = std::atof(e);
-        if (const char *e = std::getenv("DEFTRI_ND_DIRS")) nd_dirs = std::min(16, std::max(1, std::atoi(e)));
-        if (const char *e = std::getenv("DEFTRI_ND_THREADS")) par_depth = std::max(0, std::atoi(e));
         std::vector<int32_t> rootch;
         if (P > 0) {
             std::vector<int64_t> nodes(P);
@@ -873,20 +868,12 @@ struct Builder {
                     so.stream = stream; so.wait_side = wait_side;
                     LT.steps.push_back(so);
                 };
-                // DEFTRI_CB_SIDE: 0 = off, 1 = only when some front of the level continues past this block
-                // (there is a panel chain to overlap), 2 = always
-                static const int cb_side = [] {
-                    const char *e = std::getenv("DEFTRI_CB_SIDE");
-                    return e ? std::atoi(e) : 0;   // measured at C2: 1 and 2 slower (side-stream contention)
-                }();
+                // (the contribution-block update first on the side stream, the OWN update concurrently
+                // on the main stream: measured at C2 slower — side-stream contention)
+                (void)cont_any;
                 if (cont) {
                     outer_step(UP_REST, 1, 0);
                     outer_step(UP_LOOK, 0, 1);
-                } else if (cb_side == 2 || (cb_side == 1 && cont_any)) {
-                    // CB first: its launch on the side stream waits only for this block's panel chain;
-                    // the OWN update then runs on the main stream concurrently with it
-                    outer_step(UP_CB, 1, 0);
-                    outer_step(UP_OWN, 0, 0);
                 } else {
                     // touches the trailing columns an earlier REST (side stream) may still be updating
                     outer_step(UP_FULL, 0, 2);
@@ -954,7 +941,6 @@ struct Builder {
 bool analyse(const deftri_problem_desc &d, Symbolic &S, int leaf_points, int rank, int nranks) {
     S = Symbolic();
     if (nranks < 1 || rank < 0 || rank >= nranks) { S.error = "bad rank / nranks"; return false; }
-    if (const char *e = std::getenv("DEFTRI_ND_LEAF")) leaf_points = std::max(2, std::atoi(e));   // tuning
     Builder b(d, S, leaf_points, rank, nranks);
     const bool ok = b.run();
     if (const char *path = std::getenv("DEFTRI_DUMP_FRONTS"); ok && path) {   // plan inspection (tools/)

@@ -4,7 +4,6 @@
 // one thread after its workgroup's partials are published and acknowledged; cnt[0..8] are zero
 // between launches (the counters are reset, by agent-scope stores like the atomics that count in
 // them, by the workgroups that finish them).
-// DEFTRI_FLAT_TICKET=1 selects the single-counter ticket for A/Bs.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -27,12 +26,7 @@ __device__ __forceinline__ void st_sc1(T *p, T v) {
     __hip_atomic_store((GP)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ bool ticket_last(int *cnt, int nblk, int bid, bool flat = false) {
-    if (flat) {                                            // one counter for every workgroup (A/B)
-        if (__hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != nblk - 1) return false;
-        st_sc1(cnt, 0);
-        return true;
-    }
+__device__ __forceinline__ bool ticket_last(int *cnt, int nblk, int bid) {
     const int x = bid & 7;
     const int gsize = (nblk - x + 7) >> 3;                 // workgroups b < nblk with b % 8 == x
     if (__hip_atomic_fetch_add(cnt + 1 + x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gsize - 1) return false;
@@ -41,12 +35,6 @@ __device__ __forceinline__ bool ticket_last(int *cnt, int nblk, int bid, bool fl
     if (__hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ngroups - 1) return false;
     st_sc1(cnt, 0);
     return true;
-}
-
-// the DEFTRI_FLAT_TICKET switch, read once on the host
-inline bool flat_ticket() {
-    static const bool v = std::getenv("DEFTRI_FLAT_TICKET") != nullptr;
-    return v;
 }
 
 }  // namespace deftri
