@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r06multi}
-STEPS=${2:-10}
+STEPS=${2:-25}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
