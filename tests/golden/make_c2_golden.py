@@ -12,6 +12,9 @@ Usage: python tests/golden/make_c2_golden.py   (about 45 minutes of one core)
            regimes.realcolon: rep 1, arap 0.1, DepthWeight 0.001 -> sigma_d 1e-6 m), 20 iterations,
            into c2_realcolon/ — a headline-size pin whose chi2 falls 9 orders and RMSE moves 7e-4 px
            (about an hour of one core)
+       python tests/golden/make_c2_golden.py realcolon 4 500000
+           the north-star size (500k correspondences x 2 views, 3M unknowns) under the same weights, 4
+           iterations, into ns500k_realcolon/
 """
 import json
 import pathlib
@@ -33,9 +36,9 @@ REGIMES = {"simulation": (1.0, 2e5, np.float32(3.0 / 1000.0), None),
            "realcolon": (1.0, 0.1, np.float32(0.001) / np.float32(1000.0), "REALCOLON_KB8")}
 
 
-def main(regime="simulation", n_it=N_IT):
+def main(regime="simulation", n_it=N_IT, n_corr=N_CORR):
     rep, arap, sig, kb8 = REGIMES[regime]
-    p, m = sim.two_view_problem(N_CORR, SEED, rep, arap, sig, return_map=True,
+    p, m = sim.two_view_problem(n_corr, SEED, rep, arap, sig, return_map=True,
                                 kb8=getattr(sim, kb8) if kb8 else None)
     host = capi.Context(-1)
     host.analyse(p)
@@ -47,12 +50,13 @@ def main(regime="simulation", n_it=N_IT):
     rms0 = metrics.pixels_stand_dev(m)
     metrics.apply_solution(m, list(p.point_ids), res["points"])
     rms1 = metrics.pixels_stand_dev(m)
-    d = HERE / ("c2" if regime == "simulation" else "c2_" + regime)
+    d = HERE / (("c2" if regime == "simulation" else "c2_" + regime) if n_corr == N_CORR
+                else f"ns{n_corr // 1000}k_{regime}")
     d.mkdir(exist_ok=True)
     pts = res["points"]
     np.savez_compressed(d / "expected_c2.npz", points_sub=pts[::STRIDE], chi2_iter=np.array(R["chi2_iter"]),
                         trials_iter=np.array(R["trials_iter"]))
-    meta = {"n_corr": N_CORR, "seed": SEED, "n_iterations": n_it, "stride": STRIDE, "regime": regime,
+    meta = {"n_corr": n_corr, "seed": SEED, "n_iterations": n_it, "stride": STRIDE, "regime": regime,
             "weights": {"rep": rep, "arap": arap, "depth_sigma": float(sig), "camera": kb8 or "SIM_KB8"},
             "chi2_initial": R["chi2_initial"], "chi2_final": R["chi2_final"], "lambda_final": R["lambda_final"],
             "iterations": R["iterations"], "trials_total": R["trials_total"],
@@ -64,4 +68,5 @@ def main(regime="simulation", n_it=N_IT):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "simulation", int(sys.argv[2]) if len(sys.argv) > 2 else N_IT)
+    main(sys.argv[1] if len(sys.argv) > 1 else "simulation", int(sys.argv[2]) if len(sys.argv) > 2 else N_IT,
+         int(sys.argv[3]) if len(sys.argv) > 3 else N_CORR)

@@ -2,8 +2,8 @@
 committed oracle run (tests/golden/c2, tests/golden/make_c2_golden.py: the reference LM restated in
 C with g2o numeric Jacobians — the reference's arithmetic — on the same full-size graph, 6 LM
 iterations).  The device runs the same iterations in the same numeric mode on BOTH plans — the
-iterative plan with the merged two-launch CG chain is the one bench.py times (600,008 unknowns, far
-above the merged chain's 50,000) — : identical trial counts, chi2 per iteration rel 1e-6, the solved
+iterative plan's tile chain is the one bench.py times (600,008 unknowns) — : identical trial counts,
+chi2 per iteration within the band derived from the oracle's own order spread (below), the solved
 points (fixed subsample and coordinate sums) and the reprojection RMSE of the solved map
 (calculatePixelsStandDev) within the north-star 1e-4 px.  (This near-stalled headline LM moves the
 RMSE by ~1e-4 px; tests/test_regime_goldens.py pins the merged chain at 30k correspondences on runs
@@ -12,7 +12,11 @@ whose RMSE moves by > 5e-3 px.)
 c2_realcolon: the same 100k scene under Data/Realcolon.yaml's weights and distorted KB8 camera
 (rep 1, arap 0.1, sigma_d 1e-6 m), 20 oracle iterations: chi2 falls by 9 orders of magnitude (the
 depth edges dominate), the RMSE moves by 7e-4 px — 7x the 1e-4 px tolerance — and the tile chain
-(the plan bench.py times) must land on the oracle's solution."""
+(the plan bench.py times) must land on the oracle's solution.
+
+ns500k_realcolon: the north-star size (500k correspondences x 2 views, 3,000,008 unknowns) under the
+same weights, 4 oracle iterations (tests/golden/make_c2_golden.py realcolon 4 500000), on the tile
+chain only."""
 import copy
 import json
 
@@ -25,7 +29,7 @@ from deftri import capi, metrics, sim
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["c2", "c2_realcolon"])
+@pytest.fixture(scope="module", params=["c2", "c2_realcolon", "ns500k_realcolon"])
 def golden(request):
     d = GOLDEN / request.param
     if not (d / "expected_c2.json").exists():
@@ -46,6 +50,8 @@ def c2_scene(golden):
 @pytest.mark.parametrize("plan", ["iterative", "multifrontal"])
 def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
     meta, z = golden
+    if plan == "multifrontal" and meta["n_corr"] > 100000:
+        pytest.skip("the north-star golden pins the timed (iterative) plan")
     p, m0 = c2_scene
     m = copy.deepcopy(m0)
     assert p.summary() == meta["summary"]
