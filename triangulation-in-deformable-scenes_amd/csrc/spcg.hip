@@ -2008,13 +2008,43 @@ __global__ void __launch_bounds__(256) k_sp_tupd(int it, const SpDev G, double l
             o = G.hd + 3 * (int64_t)l;
 #pragma unroll
             for (int c = 0; c < 3; c++) q[c] = G.q[o + c];
-            if (G.tmulti)                                              // several pairs: the row's shares
-                for (int j = 1; j < G.tnshare[l]; j++)
+            // several pairs: the row's shares, then its cross slots (contiguous) — four at a time, their
+            // loads issued before the first is added (the additions in the same order)
+            if (G.tmulti) {
+                const int ns = G.tnshare[l];
+                for (int j0 = 1; j0 < ns; j0 += 4) {
+                    double v[4][3];
 #pragma unroll
-                    for (int c = 0; c < 3; c++) q[c] += G.qs[3 * ((int64_t)(j - 1) * G.nown + l) + c];
-            for (int k = G.txoff[l]; k < G.txoff[l + 1]; k++)          // the row's cross slots, contiguous
+                    for (int u = 0; u < 4; u++) {
+                        const int j = j0 + u < ns ? j0 + u : j0;
+                        const double *s = G.qs + 3 * ((int64_t)(j - 1) * G.nown + l);
 #pragma unroll
-                for (int c = 0; c < 3; c++) q[c] += G.xc[3 * (int64_t)k + c];
+                        for (int c = 0; c < 3; c++) v[u][c] = s[c];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (j0 + u < ns)
+#pragma unroll
+                            for (int c = 0; c < 3; c++) q[c] += v[u][c];
+                }
+            }
+            {
+                const int k0 = G.txoff[l], k1 = G.txoff[l + 1];
+                for (int kb = k0; kb < k1; kb += 4) {
+                    double v[4][3];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int64_t k = kb + u < k1 ? kb + u : kb;
+#pragma unroll
+                        for (int c = 0; c < 3; c++) v[u][c] = G.xc[3 * k + c];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (kb + u < k1)
+#pragma unroll
+                            for (int c = 0; c < 3; c++) q[c] += v[u][c];
+                }
+            }
             if (FIN) {
 #pragma unroll
                 for (int c = 0; c < 3; c++) G.q[o + c] = q[c];
