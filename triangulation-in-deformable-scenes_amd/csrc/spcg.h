@@ -276,6 +276,7 @@ struct SpDev {
     int32_t t_grid = 0;                                   // k_sp_tile's workgroups (tiles XCD-dealt + heavy)
     int32_t tmulti = 0;                                   // several pairs (SpPlanHost::tile_multi)
     const int32_t *trow = nullptr, *tdst = nullptr, *tpoff = nullptr, *tnshare = nullptr;
+    const int32_t *tdep = nullptr;             // per tile row: 2 j + (scale & 1) of its depth edge j in the tile's pair, or -1
     double *qs = nullptr;                                 // share planes [planes][nown][3]
     int32_t ovl = 0;                                      // sharded: halo exchange beside the interior product
     const int32_t *p1list = nullptr;                      // sharded phase 1: the launch's workgroups -> logical ones

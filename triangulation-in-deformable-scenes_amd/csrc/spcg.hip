@@ -1735,6 +1735,11 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
     uint2 mA = make_uint2(0u, 0u), mB = mA;     // the meta of passes 0, 1
     int2 cA = make_int2(0, 0), cB = cA;
     int rsi = 0, dj0 = 0, dj1 = 0;
+    // several pairs: the own row's depth coupling in the tile's pair (G.tdep) and its diagonal block
+    // loaded here too, so P2 waits on no load of its own (C3 / C5 products -2 to -3 %; one pair: the
+    // same loads in P2 measured 0.5 us faster at C2)
+    int dsc0 = -1;
+    double cd0[3] = {0.0, 0.0, 0.0}, ws0 = 0.0, Dp[6] = {0, 0, 0, 0, 0, 0};
     if (t < G.ntile) {
         const int32_t *T = G.ttab + 8 * (int64_t)t;
         r0 = T[0]; nr = T[1]; nh = T[2]; e0 = T[3]; ne = T[4]; h0 = T[5]; ns = T[6]; tq = T[7];
@@ -1762,8 +1767,22 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
         if (tid < nr) {
             const int l = G.tmulti ? own_row(tid) : r0 + tid;
             rsi = G.trs[r0 + tid];
-            dj0 = G.dep_off[l];
-            dj1 = G.dep_off[l + 1];
+            if (G.tmulti) {
+                const int tdv = G.tdep[r0 + tid];
+                if (tdv >= 0) {
+                    const int jd = tdv >> 1;
+                    dsc0 = tdv & 1;
+#pragma unroll
+                    for (int c = 0; c < 3; c++) cd0[c] = G.cdep[3 * (int64_t)jd + c];
+                    ws0 = G.wss[jd];
+                }
+                if (G.trow[r0 + tid] < 0)
+#pragma unroll
+                    for (int kk = 0; kk < 6; kk++) Dp[kk] = G.Dv[6 * (int64_t)l + kk];
+            } else {
+                dj0 = G.dep_off[l];
+                dj1 = G.dep_off[l + 1];
+            }
         }
     }
     double beta;
@@ -1891,23 +1910,27 @@ __global__ void __launch_bounds__(256) k_sp_tile(int it, const SpDev G, const JT
             if (home) {
                 double D[6];
 #pragma unroll
-                for (int kk = 0; kk < 6; kk++) D[kk] = G.Dv[6 * (int64_t)l + kk];
+                for (int kk = 0; kk < 6; kk++) D[kk] = G.tmulti ? Dp[kk] : G.Dv[6 * (int64_t)l + kk];
                 const double q0 = lam * p[0] + ((D[0] * p[0] + D[1] * p[1]) + D[3] * p[2]);
                 const double q1 = lam * p[1] + ((D[1] * p[0] + D[2] * p[1]) + D[4] * p[2]);
                 const double q2 = lam * p[2] + ((D[3] * p[0] + D[4] * p[1]) + D[5] * p[2]);
                 pap += (p[0] * q0 + p[1] * q1) + p[2] * q2;
                 q[0] += q0; q[1] += q1; q[2] += q2;
             }
-            for (int j = dj0; j < dj1; j++) {
-                int sc_ = G.dsc[j];
-                if (G.tmulti) {                    // the pair's two scales only (2 tq, 2 tq + 1)
-                    if ((sc_ >> 1) != tq) continue;
-                    sc_ &= 1;
-                }
-                const double *cd = G.cdep + 3 * (int64_t)j;
+            // the depth couplings: several pairs, the row's one in the tile's pair (G.tdep, loaded
+            // above with its scale 2 tq or 2 tq + 1); one pair, the row's in order
+            const int jend = G.tmulti ? (dsc0 >= 0 ? 1 : 0) : dj1 - dj0;
+            for (int jj = 0; jj < jend; jj++) {
+                const int j = dj0 + jj;
+                const bool pre = G.tmulti != 0;
+                const int sc_ = pre ? dsc0 : G.dsc[j];
+                double cd[3];
+#pragma unroll
+                for (int c = 0; c < 3; c++) cd[c] = pre ? cd0[c] : G.cdep[3 * (int64_t)j + c];
+                const double wsj = pre ? ws0 : G.wss[j];
                 const double ps = hp[6 + sc_];
                 const double cp = (cd[0] * p[0] + cd[1] * p[1]) + cd[2] * p[2];
-                const double td = cp + G.wss[j] * ps;
+                const double td = cp + wsj * ps;
                 pap += ps * (cp + td);
                 if (sc_ == 0) sacc[0] += td;
                 else sacc[1] += td;

@@ -458,10 +458,26 @@ int SpSolver::upload(const deftri_problem_desc &d) {
         }
         G.ttab = tt; G.trs = trs; G.thalo = th; G.txoff = txo;
         if (H.tile_multi) {                        // several pairs: own-row lists, shares, pair ranges
-            int32_t *tr, *tdd, *tpo, *tns;
+            int32_t *tr, *tdd, *tpo, *tns, *tdp;
             PUT(tr, H.tile_trow); PUT(tdd, H.tile_tdst); PUT(tpo, H.tile_poff); PUT(tns, H.tile_nshare);
+            // each tile row's depth edge in the tile's pair (the reference gives a point one depth edge
+            // per pair, on the scale of its keyframe in that pair): 2 j + (scale & 1), or -1
+            std::vector<int32_t> tdep(H.tile_trow.size(), -1);
+            for (int32_t t = 0; t < H.ntile; t++) {
+                const int32_t *T = &H.tile_tab[8 * (size_t)t];
+                for (int32_t i = 0; i < T[1]; i++) {
+                    const int32_t l = H.tile_trow[T[0] + i] & 0x7fffffff;
+                    for (int32_t j = H.dep_off[l]; j < H.dep_off[l + 1]; j++) {
+                        if ((ds[j] >> 1) != T[7]) continue;
+                        if (tdep[T[0] + i] >= 0 || j >= (1 << 30))
+                            return fail(DEFTRI_E_ARG, "tile plan: a row with two depth edges in one pair");
+                        tdep[T[0] + i] = 2 * j + (ds[j] & 1);
+                    }
+                }
+            }
+            PUT(tdp, tdep);
             G.tmulti = 1;
-            G.trow = tr; G.tdst = tdd; G.tpoff = tpo; G.tnshare = tns;
+            G.trow = tr; G.tdst = tdd; G.tpoff = tpo; G.tnshare = tns; G.tdep = tdp;
             ALLOC(G.qs, 3 * std::max<int64_t>((int64_t)H.tile_planes * nown, 1));
         }
         G.txdst = reinterpret_cast<const int2 *>(txd);
