@@ -143,18 +143,35 @@ k_sp_glin_rows(const SpDev G, JT *__restrict__ pj) {
                     }
                 }
             }
-            for (int j = G.dep_off[l]; j < G.dep_off[l + 1]; j++) {     // depth: J_p (3), J_s
-                const double *J = G.Jd + 4 * (int64_t)j;
-                const double wt = G.Wd[j], er = G.Ed[j];
+            // depth: J_p (3), J_s — four edges' loads issued before the first is used (several pairs:
+            // a row has one per pair), the sums in edge order
+            const int d0 = G.dep_off[l], d1 = G.dep_off[l + 1];
+            for (int jb = d0; jb < d1; jb += 4) {
+                double Jb[4][4], wb[4], eb[4];
 #pragma unroll
-                for (int a = 0; a < 3; a++) {
-                    const double ja = J[a] * wt;
+                for (int u = 0; u < 4; u++) {
+                    const int64_t j = jb + u < d1 ? jb + u : jb;
 #pragma unroll
-                    for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
-                    bb[a] -= J[a] * (wt * er);
-                    G.cdep[3 * (int64_t)j + a] = ja * J[3];
+                    for (int c = 0; c < 4; c++) Jb[u][c] = G.Jd[4 * j + c];
+                    wb[u] = G.Wd[j];
+                    eb[u] = G.Ed[j];
                 }
-                G.wss[j] = (J[3] * wt) * J[3];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (jb + u >= d1) break;
+                    const int64_t j = jb + u;
+                    const double *J = Jb[u];
+                    const double wt = wb[u], er = eb[u];
+#pragma unroll
+                    for (int a = 0; a < 3; a++) {
+                        const double ja = J[a] * wt;
+#pragma unroll
+                        for (int c = 0; c <= a; c++) D[tri3(a, c)] += ja * J[c];
+                        bb[a] -= J[a] * (wt * er);
+                        G.cdep[3 * j + a] = ja * J[3];
+                    }
+                    G.wss[j] = (J[3] * wt) * J[3];
+                }
             }
         }
         double H[6];
