@@ -152,6 +152,7 @@ struct TileInput {
     const int32_t *pair = nullptr;                     // arap_pair [E]
     int64_t D = 0;
     const int32_t *dep_point = nullptr, *dep_scale = nullptr;
+    const double *points = nullptr;                    // [P][3]: a pair's units ordered by their mesh positions
 };
 // tile layout of a one-rank, one-pair plan: false (why) when the graph does not fit tile mode; order:
 // the ARAP edges in tile-entry order (the plan's local edge order)

@@ -199,8 +199,8 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     stage("2 Morton order");
     // 3. rows: groups in that order, points of a group by id.  A tile plan of several pairs (one rank)
     //    numbers them keyframe-major instead — by the camera of the point's reprojection edges, then
-    //    its group's Morton position — so a tile of pair (a, b), consecutive groups of that pair, owns
-    //    two contiguous row ranges (keyframe a's and keyframe b's) and its loads and stores coalesce
+    //    the Morton order of the point's own position — so a tile of pair (a, b), consecutive units of
+    //    that pair in the Morton order of keyframe b's positions, owns runs of keyframe b's rows
     std::vector<int32_t> pts(P);
     std::iota(pts.begin(), pts.end(), 0);
     counting_sort(pts, ng, [&](int32_t p) { return gpos[gid[p]]; });
@@ -214,7 +214,38 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         }
         if (one_cam) {
             const int32_t C = std::max(d.n_cams, 1);
-            counting_sort(pts, (int64_t)C + 1, [&](int32_t p) { return pcam[p] < 0 ? C : pcam[p]; });
+            {
+                // inside a keyframe, its points in the Morton order of their own positions: the order in
+                // which the pairs whose mesh is that keyframe's (it is their keyframe 1) cut their tiles
+                // (spcg_tile.cpp), so those tiles' keyframe-1 rows are runs (C5's CG iteration -3 %)
+                std::vector<double> blo(2 * (size_t)(C + 1), 1e300), bhi(2 * (size_t)(C + 1), -1e300);
+                auto cam = [&](int32_t p) { return pcam[p] < 0 ? C : pcam[p]; };
+                for (int32_t p = 0; p < P; p++)
+                    for (int c = 0; c < 2; c++) {
+                        const double v = d.points[3 * (int64_t)p + c];
+                        if (std::isfinite(v)) {
+                            blo[2 * cam(p) + c] = std::min(blo[2 * cam(p) + c], v);
+                            bhi[2 * cam(p) + c] = std::max(bhi[2 * cam(p) + c], v);
+                        }
+                    }
+                std::vector<uint64_t> pk(P);
+                for (int32_t p = 0; p < P; p++) {
+                    uint64_t k[2];
+                    for (int c = 0; c < 2; c++) {
+                        const double l = blo[2 * cam(p) + c], h = bhi[2 * cam(p) + c];
+                        const double span = h > l ? h - l : 1.0;
+                        const double v = d.points[3 * (int64_t)p + c];
+                        double t = std::isfinite(v) ? (v - l) / span : 0.0;
+                        t = std::min(1.0, std::max(0.0, t));
+                        k[c] = (uint64_t)(t * 2097151.0);
+                    }
+                    pk[p] = spread21(k[0]) | (spread21(k[1]) << 1);
+                }
+                std::sort(pts.begin(), pts.end(), [&](int32_t a, int32_t b) {
+                    const int32_t ca = cam(a), cb = cam(b);
+                    return ca != cb ? ca < cb : pk[a] != pk[b] ? pk[a] < pk[b] : a < b;
+                });
+            }
         }
     }
     H.point_of_row = pts;
@@ -271,6 +302,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         TileInput ti;
         ti.P = P; ti.ng = ng; ti.E = E; ti.ap = ap; ti.gpos = gp.data(); ti.row_of_point = H.row_of_point.data();
         ti.Q = Q; ti.S = S; ti.pair = d.arap_pair; ti.D = D; ti.dep_point = d.dep_point; ti.dep_scale = d.dep_scale;
+        ti.points = d.points;
         std::string why;
         H.tile = build_tiles_multi(ti, H, tile_order, why);
         if (!H.tile) {
