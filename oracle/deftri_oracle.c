@@ -313,11 +313,19 @@ static void huber(double delta, double e2, double rho[3]) {
     }
 }
 
+/* Edge order of the sums (tools/oracle_spread.py: the oracle's own spread over legal summation
+   orders): 0 the descriptor's order (g2o's insertion order), 1 every edge type walked backwards —
+   the chi2 sums and H / b accumulate in the opposite order. */
+static int g_edge_rev = 0;
+void oracle_set_edge_order(int reversed) { g_edge_rev = reversed ? 1 : 0; }
+#define EDGE_IDX(i, n) (g_edge_rev ? (n) - 1 - (i) : (i))
+
 /* SparseOptimizer::activeRobustChi2 (computeActiveErrors + chi2 + robustify) */
 static double active_robust_chi2(const problem *pb, const state *s) {
     const deftri_problem_desc *d = pb->d;
     double chi = 0.0, rho[3];
-    for (int e = 0; e < d->n_rep; e++) {
+    for (int i = 0; i < d->n_rep; i++) {
+        const int e = EDGE_IDX(i, d->n_rep);
         double err[2];
         rep_error(pb, s, e, err);
         double om = d->rep_info[e];
@@ -325,11 +333,13 @@ static double active_robust_chi2(const problem *pb, const state *s) {
         if (d->huber_delta > 0) { huber(d->huber_delta, c2, rho); chi += rho[0]; }
         else chi += c2;
     }
-    for (int e = 0; e < d->n_depth; e++) {
+    for (int i = 0; i < d->n_depth; i++) {
+        const int e = EDGE_IDX(i, d->n_depth);
         double err = depth_error_v(pb, e, s->points + 3 * (size_t)d->dep_point[e], s->scales[d->dep_scale[e]]);
         chi += err * (d->dep_info[e] * err);
     }
-    for (int e = 0; e < d->n_arap; e++) {
+    for (int i = 0; i < d->n_arap; i++) {
+        const int e = EDGE_IDX(i, d->n_arap);
         double err = arap_error(pb, s, e);
         chi += err * (d->pair_info[d->arap_pair[e]] * err);
     }
@@ -558,7 +568,8 @@ static void build_system(const problem *pb, const state *s, bsr *H, int analytic
     const deftri_problem_desc *d = pb->d;
     memset(H->val, 0, sizeof(double) * (size_t)H->nval);
     memset(H->b, 0, sizeof(double) * (size_t)pb->ndof);
-    for (int e = 0; e < d->n_rep; e++) {
+    for (int i = 0; i < d->n_rep; i++) {
+        const int e = EDGE_IDX(i, d->n_rep);
         double err[2];
         rep_error(pb, s, e, err);
         const double *p = s->points + 3 * (size_t)d->rep_point[e];
@@ -582,7 +593,8 @@ static void build_system(const problem *pb, const state *s, bsr *H, int analytic
         add_block(H, pb, a, a, J, 3, J, 3, 2, W);
         add_b(H, pb, a, J, 3, 2, wr);
     }
-    for (int e = 0; e < d->n_depth; e++) {
+    for (int i = 0; i < d->n_depth; i++) {
+        const int e = EDGE_IDX(i, d->n_depth);
         double J[4];
         if (analytic) depth_jac_analytic(pb, s, e, J); else depth_jac_numeric(pb, s, e, J);
         double err = depth_error_v(pb, e, s->points + 3 * (size_t)d->dep_point[e], s->scales[d->dep_scale[e]]);
@@ -595,7 +607,8 @@ static void build_system(const problem *pb, const state *s, bsr *H, int analytic
         add_b(H, pb, a, J, 3, 1, wr);
         add_b(H, pb, b, J + 3, 1, 1, wr);
     }
-    for (int e = 0; e < d->n_arap; e++) {
+    for (int i = 0; i < d->n_arap; i++) {
+        const int e = EDGE_IDX(i, d->n_arap);
         double J[18];
         if (analytic) arap_jac_analytic(pb, s, e, J); else arap_jac_numeric(pb, s, e, J);
         double err = arap_error(pb, s, e);

@@ -102,6 +102,12 @@ def set_vertex_order(order):
     lib().oracle_set_vertex_order(_p(o, C.c_int64), C.c_int64(len(o)))
 
 
+def set_edge_order(reversed_):
+    """The order of the chi2 sums and of the H / b accumulation: the descriptor's (False, g2o's
+    insertion order) or every edge type walked backwards (True; tools/oracle_spread.py)."""
+    lib().oracle_set_edge_order(C.c_int(1 if reversed_ else 0))
+
+
 def solve_lm(prob, n_iterations=10, analytic=False, tau=1e-5, max_trials=10, verbose=False):
     A = _abi()
     d = prob.to_desc()

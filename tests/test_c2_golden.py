@@ -87,8 +87,10 @@ def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
           f"oracle order spread {spread:.3e}, tolerance {tol:.3e}")
     assert dev.max() <= tol, (dev.max(), int(dev.argmax()), tol)
     assert r["lambda_final"] == pytest.approx(meta["lambda_final"], rel=1e-9)
-    if meta.get("regime") == "realcolon":             # the pin is meaningful: the solve moves the RMSE
-        assert abs(meta["rms_final"]["desv"] - meta["rms_initial"]["desv"]) > 5e-4
+    if meta.get("regime") == "realcolon" and meta["n_corr"] == 100000:   # the pin is meaningful: the
+        assert abs(meta["rms_final"]["desv"] - meta["rms_initial"]["desv"]) > 5e-4   # solve moves the RMSE
+    if meta["n_corr"] > 100000:                       # north-star size, 4 iterations: chi2 falls 1500x
+        assert meta["chi2_final"] < 1e-3 * meta["chi2_initial"]
     ext = np.abs(pts).max()
     assert np.abs(pts[::meta["stride"]] - z["points_sub"]).max() <= 1e-7 * ext
     np.testing.assert_allclose(pts.sum(0), meta["point_sum"], rtol=1e-9)

@@ -2,7 +2,7 @@
 exact LDL^T step (the oracle's own nested dissection), chi2 per iteration against the committed golden
 (which eliminates in the host analysis' nested-dissection order).  Test infrastructure only.
 
-usage: python tools/oracle_spread.py NAME [SUB]
+usage: python tools/oracle_spread.py NAME [SUB [MODES]]   (MODES: oracle_nd,edge_rev)
        python tools/oracle_spread.py c2_realcolon     (the C2 Realcolon golden, tests/golden/c2_realcolon:
                                                        about an hour of one core)"""
 import json
@@ -34,10 +34,21 @@ else:
     z = np.load(d / f"{name}.npz")
     p, m, host = scene(name, meta["n_corr"], meta["seed"])
     host.analyse(p)
-for label, order in (("oracle_nd", None),):
-    oracle.set_vertex_order(order)
+# the modes: "oracle_nd" the oracle's own nested dissection instead of the golden's elimination order;
+# "edge_rev" the golden's order, every edge type's chi2 sums and H / b accumulation walked backwards
+modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["oracle_nd"]
+golden_order = None
+if "edge_rev" in modes:
+    from deftri import capi as _capi
+    with _capi.Context(-1) as hc:
+        hc.analyse(p)
+        golden_order = hc.vertex_order()
+for label in modes:
+    oracle.set_vertex_order(None if label == "oracle_nd" else golden_order)
+    oracle.set_edge_order(label == "edge_rev")
     r = oracle.solve_lm(p, N_IT, analytic=False)["report"]
     oracle.set_vertex_order(None)
+    oracle.set_edge_order(False)
     a, b = np.array(r["chi2_iter"]), np.array(z["chi2_iter"])
     rel = np.abs(a - b) / np.abs(b)
     print(json.dumps({"order": label, "max_rel": float(rel.max()), "at": int(rel.argmax()),
