@@ -27,6 +27,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <functional>
 #include <string>
@@ -141,6 +142,22 @@ struct SpPlanHost {
     double tile_bytes[2] = {0, 0};                     // algorithmic bytes per CG iteration: product, update
 };
 // the groups and rows build_tiles needs (spcg_plan.cpp step 5)
+// the Z-order (Morton) key of a point from its (x, y) in a bounding box, 21 bits per coordinate — the
+// plans' point orders (a Hilbert curve measured no better: C2 and C5 slower, 500k and C3 1-3 % faster)
+inline uint64_t curve_key(double x, double y, const double lo[2], const double hi[2]) {
+    uint32_t k[2];
+    const double v[2] = {x, y};
+    for (int c = 0; c < 2; c++) {
+        const double span = hi[c] > lo[c] ? hi[c] - lo[c] : 1.0;
+        double t = std::isfinite(v[c]) ? (v[c] - lo[c]) / span : 0.0;
+        t = t < 0.0 ? 0.0 : t > 1.0 ? 1.0 : t;
+        k[c] = (uint32_t)(t * 2097151.0);
+    }
+    uint64_t m = 0;
+    for (int b = 0; b < 21; b++) m |= (uint64_t)((k[0] >> b) & 1u) << (2 * b) | (uint64_t)((k[1] >> b) & 1u) << (2 * b + 1);
+    return m;
+}
+
 struct TileInput {
     int32_t P = 0, ng = 0;
     int64_t E = 0;

@@ -94,16 +94,6 @@ void par_counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
     ids.swap(out);
 }
 
-inline uint64_t spread21(uint64_t v) {       // bits 0..20 -> every third bit
-    v &= 0x1fffff;
-    v = (v | v << 32) & 0x1f00000000ffffULL;
-    v = (v | v << 16) & 0x1f0000ff0000ffULL;
-    v = (v | v << 8) & 0x100f00f00f00f00fULL;
-    v = (v | v << 4) & 0x10c30c30c30c30c3ULL;
-    v = (v | v << 2) & 0x1249249249249249ULL;
-    return v;
-}
-
 }  // namespace
 
 bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &H,
@@ -179,17 +169,7 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
             if (std::isfinite(v)) { lo[c] = std::min(lo[c], v); hi[c] = std::max(hi[c], v); }
         }
     std::vector<uint64_t> key(ng);
-    for (int32_t g = 0; g < ng; g++) {
-        uint64_t k[2];
-        for (int c = 0; c < 2; c++) {
-            const double span = hi[c] > lo[c] ? hi[c] - lo[c] : 1.0;
-            double v = xy(grep[g], c);
-            double t = std::isfinite(v) ? (v - lo[c]) / span : 0.0;
-            t = std::min(1.0, std::max(0.0, t));
-            k[c] = (uint64_t)(t * 2097151.0);
-        }
-        key[g] = spread21(k[0]) | (spread21(k[1]) << 1);
-    }
+    for (int32_t g = 0; g < ng; g++) key[g] = curve_key(xy(grep[g], 0), xy(grep[g], 1), lo, hi);
     std::vector<int32_t> gorder(ng);
     std::iota(gorder.begin(), gorder.end(), 0);
     std::sort(gorder.begin(), gorder.end(), [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : grep[a] < grep[b]; });
@@ -229,18 +209,9 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                         }
                     }
                 std::vector<uint64_t> pk(P);
-                for (int32_t p = 0; p < P; p++) {
-                    uint64_t k[2];
-                    for (int c = 0; c < 2; c++) {
-                        const double l = blo[2 * cam(p) + c], h = bhi[2 * cam(p) + c];
-                        const double span = h > l ? h - l : 1.0;
-                        const double v = d.points[3 * (int64_t)p + c];
-                        double t = std::isfinite(v) ? (v - l) / span : 0.0;
-                        t = std::min(1.0, std::max(0.0, t));
-                        k[c] = (uint64_t)(t * 2097151.0);
-                    }
-                    pk[p] = spread21(k[0]) | (spread21(k[1]) << 1);
-                }
+                            for (int32_t p = 0; p < P; p++)
+                    pk[p] = curve_key(d.points[3 * (int64_t)p], d.points[3 * (int64_t)p + 1], &blo[2 * cam(p)],
+                                      &bhi[2 * cam(p)]);
                 std::sort(pts.begin(), pts.end(), [&](int32_t a, int32_t b) {
                     const int32_t ca = cam(a), cb = cam(b);
                     return ca != cb ? ca < cb : pk[a] != pk[b] ? pk[a] < pk[b] : a < b;

@@ -462,18 +462,11 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
                     lo[c] = std::min(lo[c], v); hi[c] = std::max(hi[c], v);
                 }
             }
-            for (int32_t g = 0; g < ng; g++) {
+                    for (int32_t g = 0; g < ng; g++) {
                 const size_t k = (size_t)q * ng + g;
                 if (uid[k] != 0) continue;
-                uint64_t m[2];
-                for (int c = 0; c < 2; c++) {
-                    const double span = hi[c] > lo[c] ? hi[c] - lo[c] : 1.0;
-                    const double t = std::min(1.0, std::max(0.0, (in.points[3 * (int64_t)upt[k] + c] - lo[c]) / span));
-                    m[c] = (uint64_t)(t * 2097151.0);
-                }
-                uint64_t key = 0;
-                for (int bit = 0; bit < 21; bit++) key |= ((m[0] >> bit) & 1ull) << (2 * bit) | ((m[1] >> bit) & 1ull) << (2 * bit + 1);
-                ks.push_back({key, g});
+                const double *pp = in.points + 3 * (int64_t)upt[k];
+                ks.push_back({curve_key(pp[0], pp[1], lo, hi), g});
             }
             std::sort(ks.begin(), ks.end());
             for (const auto &kg : ks) uid[(size_t)q * ng + kg.second] = nu++;
