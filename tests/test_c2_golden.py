@@ -78,15 +78,20 @@ def test_c2_iterations_match_oracle(gpu_ctx, golden, c2_scene, plan):
     # chi2 per iteration within max(4 x the oracle's own spread between elimination orders, 1e-6), the
     # rule of tests/test_regime_goldens.py: the spread recorded in the golden's oracle_order_spread
     # (tools/oracle_spread.py; the Simulation C2 run is well conditioned and has none: 1e-6).  Under
-    # Realcolon's weights (Omega_depth 1e12) iteration 9 is conditioning-bound: the device's exact
-    # multifrontal LDL^T lands 1.8e-6 from the oracle and the tile chain 2.3e-6.
+    # Realcolon's weights (Omega_depth 1e12) iteration 9 is conditioning-bound: with the SE3 / depth
+    # arithmetic uncontracted as in the reference (device_math.h) both device plans land 9.3-9.4e-7 from
+    # the oracle (2.3e-6 with FMA contraction).
     spread = meta.get("oracle_order_spread", {}).get("max_rel_chi2", 0.0)
     tol = max(4.0 * spread, 1e-6)
     dev = np.abs(np.asarray(r["chi2_iter"]) - z["chi2_iter"]) / np.abs(z["chi2_iter"])
     print(f"{meta.get('regime', 'simulation')}/{plan}: chi2 max rel dev {dev.max():.3e} at {int(dev.argmax())}, "
           f"oracle order spread {spread:.3e}, tolerance {tol:.3e}")
     assert dev.max() <= tol, (dev.max(), int(dev.argmax()), tol)
-    assert r["lambda_final"] == pytest.approx(meta["lambda_final"], rel=1e-9)
+    # the final damping inherits the chi2 deviations through g2o's rho rule (a ratio of chi2
+    # differences): the same rule, 4 x the oracle's own spread of lambda_final (recorded with the chi2
+    # spread), 1e-9 where none is recorded
+    lam_tol = max(4.0 * meta.get("oracle_order_spread", {}).get("max_rel_lambda", 0.0), 1e-9)
+    assert r["lambda_final"] == pytest.approx(meta["lambda_final"], rel=lam_tol)
     if meta.get("regime") == "realcolon" and meta["n_corr"] == 100000:   # the pin is meaningful: the
         assert abs(meta["rms_final"]["desv"] - meta["rms_initial"]["desv"]) > 5e-4   # solve moves the RMSE
     if meta["n_corr"] > 100000:                       # north-star size, 4 iterations: chi2 falls 1500x

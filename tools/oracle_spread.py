@@ -51,5 +51,7 @@ for label in modes:
     oracle.set_edge_order(False)
     a, b = np.array(r["chi2_iter"]), np.array(z["chi2_iter"])
     rel = np.abs(a - b) / np.abs(b)
-    print(json.dumps({"order": label, "max_rel": float(rel.max()), "at": int(rel.argmax()),
+    lam_ref = meta.get("lambda_final")
+    lam_rel = abs(r["lambda_final"] - lam_ref) / abs(lam_ref) if lam_ref else None
+    print(json.dumps({"order": label, "max_rel": float(rel.max()), "at": int(rel.argmax()), "lambda_final_rel": lam_rel,
                       "trials_same": list(r["trials_iter"]) == list(z["trials_iter"])}), flush=True)

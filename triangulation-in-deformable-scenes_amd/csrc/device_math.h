@@ -11,15 +11,22 @@
 namespace deftri {
 namespace dev {
 
+// The SE3 / quaternion helpers restate the reference's double arithmetic operation for operation:
+// no FMA contraction (the reference's x86-64 build has no FMA), so a depth or reprojection error and
+// the numeric Jacobians built from it (a difference of two evaluations 2e-9 apart, which amplifies an
+// ulp into ~1e-7 of the derivative) carry the reference's bits.
+
 struct Quat { double x, y, z, w; };
 
 __device__ __forceinline__ void quat_normalize_rot(Quat &q) {
+#pragma clang fp contract(off)
     if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
     double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
     q.x /= n; q.y /= n; q.z /= n; q.w /= n;
 }
 
 __device__ __forceinline__ void quat_to_mat(const Quat &q, double R[9]) {
+#pragma clang fp contract(off)
     double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
     double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
     double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
@@ -30,6 +37,7 @@ __device__ __forceinline__ void quat_to_mat(const Quat &q, double R[9]) {
 }
 
 __device__ __forceinline__ Quat quat_from_mat(const double m[9]) {
+#pragma clang fp contract(off)
     Quat q;
     double t = m[0] + m[4] + m[8];
     if (t > 0) {
@@ -57,6 +65,7 @@ __device__ __forceinline__ Quat quat_from_mat(const double m[9]) {
 }
 
 __device__ __forceinline__ void quat_rotate(const Quat &q, const double v[3], double o[3]) {
+#pragma clang fp contract(off)
     double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
     uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
     double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
@@ -66,6 +75,7 @@ __device__ __forceinline__ void quat_rotate(const Quat &q, const double v[3], do
 }
 
 __device__ __forceinline__ Quat quat_mul(const Quat &a, const Quat &b) {
+#pragma clang fp contract(off)
     Quat r;
     r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
     r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
@@ -88,12 +98,14 @@ __device__ __forceinline__ void se3_store(const SE3 &T, double *a) {
 }
 
 __device__ __forceinline__ void se3_map(const SE3 &T, const double p[3], double o[3]) {
+#pragma clang fp contract(off)
     quat_rotate(T.r, p, o);
     o[0] += T.t[0]; o[1] += T.t[1]; o[2] += T.t[2];
 }
 
 // g2o SE3Quat::exp(omega, upsilon)
 __device__ __forceinline__ SE3 se3_exp(const double u[6]) {
+#pragma clang fp contract(off)
     const double *w = u, *ups = u + 3;
     double theta = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     double O[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};
@@ -128,6 +140,7 @@ __device__ __forceinline__ SE3 se3_exp(const double u[6]) {
 
 // A * B (SE3Quat::operator*)
 __device__ __forceinline__ SE3 se3_mul(const SE3 &A, const SE3 &B) {
+#pragma clang fp contract(off)
     SE3 r = A;
     double tb[3];
     quat_rotate(A.r, B.t, tb);

@@ -35,6 +35,7 @@ namespace dev {
 // edge errors / Jacobians
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void huber_rho(double delta, double e2, double &rho0, double &rho1) {
+#pragma clang fp contract(off)
     if (delta <= 0) { rho0 = e2; rho1 = 1.0; return; }
     double dsqr = delta * delta;
     if (e2 <= dsqr) { rho0 = e2; rho1 = 1.0; }
@@ -47,6 +48,7 @@ __device__ __forceinline__ double lin_rep_edge(int e, int R, const int32_t *__re
                           const double *__restrict__ cam_R, const float *__restrict__ kb8,
                           double *__restrict__ J, double *__restrict__ W, double *__restrict__ E,
                           double *__restrict__ chi, int want_jac) {
+#pragma clang fp contract(off)
     if (e >= R) return 0.0;
     int c = rc[e];
     const double *pp = points + 3 * (int64_t)rp[e];
@@ -78,6 +80,7 @@ __device__ __forceinline__ double lin_rep_edge(int e, int R, const int32_t *__re
 }
 
 __device__ __forceinline__ double depth_err(const SE3 &T, const double p[3], double meas, double s) {
+#pragma clang fp contract(off)
     double pc[3];
     se3_map(T, p, pc);
     double x = meas / s - pc[2];
@@ -92,6 +95,7 @@ __device__ __forceinline__ double lin_dep_edge(int e, int D, const int32_t *__re
                           const double *__restrict__ scales, const double *__restrict__ cam_pose,
                           const double *__restrict__ cam_R, double *__restrict__ J, double *__restrict__ W,
                           double *__restrict__ E, double *__restrict__ chi, int want_jac, int analytic) {
+#pragma clang fp contract(off)
     if (e >= D) return 0.0;
     int c = dcam[e];
     const double *pp = points + 3 * (int64_t)dpt[e];
@@ -1783,6 +1787,7 @@ __global__ void __launch_bounds__(256) k_bwd_chain(int ntask, const int32_t *__r
 __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
                                double *__restrict__ scales, double *__restrict__ tg, const int *__restrict__ flag,
                                const int *gate) {
+#pragma clang fp contract(off)
     int i = TID;
     if (flag && *flag) return;
     if (gate && !*gate) return;
@@ -1806,6 +1811,7 @@ __global__ void k_update_state(int P, int S, int Q, const double *__restrict__ d
 __global__ void k_update_state_bak(int P, int S, int Q, const double *__restrict__ dx, double *__restrict__ points,
                                    double *__restrict__ scales, double *__restrict__ tg, double *__restrict__ pb,
                                    double *__restrict__ sb, double *__restrict__ tb, int restore) {
+#pragma clang fp contract(off)
     const int i = TID;
     const int64_t pbase = 6 * (int64_t)Q + S;
     if (i < P) {
