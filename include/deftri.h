@@ -283,9 +283,9 @@ typedef struct deftri_plan_info {
                                   RCCL communicator: deftri_dist_init_rccl(ctx, 1, 0, id)) */
     double  survey_bytes;      /* SURVEY.md §8(d)'s B_pcg of this rank's share: 176 E + 48 R + 40 D + 156 P
                                   (owned ARAP edges, own rows' reprojection / depth edges, own rows) */
-    int32_t tiles;             /* iterative, one rank, one keyframe pair (round 5): the fused product's
-                                  tiles (every ARAP edge read once per CG iteration); 0: the two-phase
-                                  product */
+    int32_t tiles;             /* iterative: the fused product's tiles (every ARAP edge read once per CG
+                                  iteration) — one rank (one keyframe pair since round 5, several since
+                                  round 6) or a sharded one-pair plan; 0: the two-phase product */
     int32_t halo_overlap;      /* iterative, sharded (round 5): 1 when the boundary rows' exchange runs
                                   on its own stream beside the interior edges' product */
 } deftri_plan_info;
