@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 #include <cmath>
@@ -463,18 +464,21 @@ int SpSolver::upload(const deftri_problem_desc &d) {
             // each tile row's depth edge in the tile's pair (the reference gives a point one depth edge
             // per pair, on the scale of its keyframe in that pair): 2 j + (scale & 1), or -1
             std::vector<int32_t> tdep(H.tile_trow.size(), -1);
-            for (int32_t t = 0; t < H.ntile; t++) {
-                const int32_t *T = &H.tile_tab[8 * (size_t)t];
-                for (int32_t i = 0; i < T[1]; i++) {
-                    const int32_t l = H.tile_trow[T[0] + i] & 0x7fffffff;
-                    for (int32_t j = H.dep_off[l]; j < H.dep_off[l + 1]; j++) {
-                        if ((ds[j] >> 1) != T[7]) continue;
-                        if (tdep[T[0] + i] >= 0 || j >= (1 << 30))
-                            return fail(DEFTRI_E_ARG, "tile plan: a row with two depth edges in one pair");
-                        tdep[T[0] + i] = 2 * j + (ds[j] & 1);
+            std::atomic<int> twice{0};
+            chunked(H.ntile, 256, [&](int, int64_t t0, int64_t t1) {
+                for (int64_t t = t0; t < t1; t++) {
+                    const int32_t *T = &H.tile_tab[8 * (size_t)t];
+                    for (int32_t i = 0; i < T[1]; i++) {
+                        const int32_t l = H.tile_trow[T[0] + i] & 0x7fffffff;
+                        for (int32_t j = H.dep_off[l]; j < H.dep_off[l + 1]; j++) {
+                            if ((ds[j] >> 1) != T[7]) continue;
+                            if (tdep[T[0] + i] >= 0 || j >= (1 << 30)) twice = 1;
+                            tdep[T[0] + i] = 2 * j + (ds[j] & 1);
+                        }
                     }
                 }
-            }
+            });
+            if (twice) return fail(DEFTRI_E_ARG, "tile plan: a row with two depth edges in one pair");
             PUT(tdp, tdep);
             G.tmulti = 1;
             G.trow = tr; G.tdst = tdd; G.tpoff = tpo; G.tnshare = tns; G.tdep = tdp;

@@ -431,6 +431,14 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         const char *e = std::getenv("DEFTRI_SP_TILE_LDS");
         return (int64_t)(e ? std::atoi(e) : kSpTileLds);
     }();
+    static const bool timing = std::getenv("DEFTRI_PLAN_TIMING") != nullptr;
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *w) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[deftri plan]   4a %-26s %8.2f ms\n", w, std::chrono::duration<double, std::milli>(t - T0).count());
+        T0 = t;
+    };
     if (H.nranks != 1) { why = "several pairs on a sharded plan"; return false; }
     if (in.S != 2 * Q) { why = "not two depth scales per pair"; return false; }
     if ((int64_t)Q * ng >= (1LL << 31)) { why = "too many (pair, group) units"; return false; }
@@ -475,6 +483,7 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         for (size_t k = 0; k < uid.size(); k++)
             if (uid[k] == 0) uid[k] = nu++;
     }
+    lap("units");
     std::vector<int32_t> urow(2 * (size_t)nu, -1), upair(nu);
     for (int32_t q = 0; q < Q; q++)
         for (int32_t g = 0; g < ng; g++)
@@ -509,25 +518,37 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
             isrc[fi[egj[e]]++] = egi[e];
         }
     }
+    lap("edges by unit");
     for (int32_t u = 0; u < nu; u++)
         if (ocnt[u + 1] - ocnt[u] > 64) { why = "a vertex with more than 64 ARAP edges in a pair"; return false; }
-    // every depth edge's (row, pair of its scale) is a unit's row: it is summed by that unit's tile
+    // every depth edge's (row, pair of its scale) is a unit's row: it is summed by that unit's tile.
+    // A row's unit in pair q is (q, its group); the checks are direct lookups (a sort of every
+    // (row, pair) key and a binary search per depth edge took 1.4 s at C3)
     {
-        std::vector<int64_t> key;
-        key.reserve(2 * (size_t)nu);
+        std::vector<int32_t> point_of(P);
+        for (int32_t p = 0; p < P; p++) point_of[row[p]] = p;
+        // a row in two units of one pair: the unit (q, group of its point) holds it, or it is another
+        // group's row — then the row's own (q, group) unit must not list it as well
         for (int32_t u = 0; u < nu; u++)
-            for (int k = 0; k < 2; k++) key.push_back((int64_t)urow[2 * (size_t)u + k] * Q + upair[u]);
-        std::sort(key.begin(), key.end());
-        if (std::adjacent_find(key.begin(), key.end()) != key.end()) { why = "a row in two units of one pair"; return false; }
+            for (int k = 0; k < 2; k++) {
+                const int32_t r = urow[2 * (size_t)u + k];
+                const int32_t uo = uid[(size_t)upair[u] * ng + in.gpos[point_of[r]]];
+                if (uo != u) { why = "a row in two units of one pair"; return false; }
+            }
         for (int64_t d = 0; d < in.D; d++) {
-            const int64_t k = (int64_t)row[in.dep_point[d]] * Q + (in.dep_scale[d] >> 1);
-            if (!std::binary_search(key.begin(), key.end(), k)) { why = "a depth edge outside its pair's mesh"; return false; }
+            const int32_t p = in.dep_point[d], q = in.dep_scale[d] >> 1;
+            const int32_t u = (q >= 0 && q < Q) ? uid[(size_t)q * ng + in.gpos[p]] : -1;
+            if (u < 0 || (urow[2 * (size_t)u] != row[p] && urow[2 * (size_t)u + 1] != row[p])) {
+                why = "a depth edge outside its pair's mesh";
+                return false;
+            }
         }
         std::vector<uint8_t> seen(P, 0);
         for (int32_t k : urow) seen[k] = 1;
         for (int32_t r = 0; r < P; r++)
             if (!seen[r]) { why = "a row in no pair's mesh"; return false; }
     }
+    lap("depth check");
     // 2. greedy partition per pair: consecutive units while units <= umax and the LDS estimate fits
     auto lds_of = [&](int64_t nr, int64_t nh, int64_t ns) { return 24 * (nr + nh) + 24 * nr + 24 * ns + kSpTileLdsFixed; };
     std::vector<int32_t> tstart;
@@ -574,6 +595,7 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         for (int32_t h : halo_members) hcnt[h] = 0;
         tstart.push_back(nu);
     }
+    lap("partition");
     const int32_t nt = nu > 0 ? (int32_t)tstart.size() - 1 : 0;
     // 3. entries, own-row lists, slots, cross slots (the cut edges' first: chunk bases count them)
     H.tile_tab.assign(8 * (size_t)nt, 0);
@@ -678,6 +700,7 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         for (int32_t u = u0; u < u1; u++) lrow[u] = -1;
         for (int32_t u : hu) lrow[u] = -1;
     }
+    lap("entries, slots");
     for (int32_t q = Q - 1; q >= 0; q--)
         if (H.tile_poff[q] == nt) H.tile_poff[q] = H.tile_poff[q + 1];
     if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
@@ -692,6 +715,7 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         H.tile_tdst[k] = j;
         if (j == 0) H.tile_trow[k] = r | (int32_t)(1u << 31);
     }
+    lap("shares");
     H.tile_planes = 0;
     for (int32_t c : H.tile_nshare) H.tile_planes = std::max(H.tile_planes, c - 1);
     // cross slots by target row, source order inside a row
@@ -703,7 +727,7 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         std::vector<int32_t> fill(H.tile_xoff.begin(), H.tile_xoff.end() - 1);
         for (const auto &x : xt) H.tile_xdst[x.second] = fill[x.first]++;
     }
-    static const bool timing = std::getenv("DEFTRI_PLAN_TIMING") != nullptr;
+    lap("cross slots");
     if (timing) tile_shape_stats(H.tile_tab, nt, nx);
     H.tile_multi = true;
     H.ntile = nt;
