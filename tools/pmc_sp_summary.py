@@ -8,7 +8,7 @@ kernel's longest are counted as active.  FETCH_SIZE is reported raw: the guide c
 for 16-byte-per-lane coalesced reads; these kernels read 8-byte lanes (column-major J, packed slots)
 and 16-byte (z, p) gathers, an uncalibrated mix — `fetch_bytes_x2` gives the upper bound.
 
-usage: python tools/pmc_sp_summary.py gpurun_out/<tag> profiles/<tag>_pmc_sp_product.json
+usage: python tools/pmc_sp_summary.py gpurun_out/<tag> profiles/<tag>_pmc_sp_product.json [WORKLOAD]
 """
 import collections
 import csv
@@ -36,6 +36,7 @@ def active_mean(vals, dur):
 
 def main():
     src, dst = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2])
+    wl = sys.argv[3] if len(sys.argv) > 3 else "C2"
     bench = json.loads((src / "pmc_fetch.json").read_text())
     alg = bench["roofline"]["bytes_per_launch"]
     names = [bench["roofline"]["phase1"].get("kernel", "k_sp_phase1"), bench["roofline"]["phase2"].get("kernel", "k_sp_phase2")]
@@ -53,7 +54,7 @@ def main():
                 "traffic_bytes_per_launch": tf + tw,
                 "traffic_over_algorithmic": (tf + tw) / alg,
                 "note": "rocprofv3 FETCH_SIZE / WRITE_SIZE in separate passes over `bench.py --steps 3 --warmup 1 "
-                        "--no-cpu-baseline --no-e2e` (C2, iterative plan); active launches only; FETCH_SIZE raw "
+                        f"--no-cpu-baseline --no-e2e` ({wl}, iterative plan); active launches only; FETCH_SIZE raw "
                         "(8-B lane reads: uncalibrated; x2 = the 16-B-lane calibration, an upper bound)"})
     dst.write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
