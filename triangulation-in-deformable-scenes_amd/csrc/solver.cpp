@@ -1489,8 +1489,18 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
     if (!ctx) return DEFTRI_E_ARG;
     if (ctx->device < 0) return fail(ctx, DEFTRI_E_NODEVICE, "host-only context");
     hipSetDevice(ctx->device);
+    // DEFTRI_UPLOAD_TIMING=1: the call's host stages before the plan build
+    static const bool utiming = std::getenv("DEFTRI_UPLOAD_TIMING") != nullptr;
+    auto ut = std::chrono::steady_clock::now();
+    auto ulap = [&](const char *w) {
+        if (!utiming) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[deftri upload] %-22s %7.2f ms\n", w, std::chrono::duration<double, std::milli>(t - ut).count());
+        ut = t;
+    };
     int rc = validate(ctx, desc);
     if (rc) return rc;
+    ulap("validate");
     if (want_iterative(ctx, desc)) {
         static const bool no_cache = std::getenv("DEFTRI_NO_PLAN_CACHE") != nullptr;
         if (!no_cache && ctx->sp_on && ctx->sp && ctx->sp->fp32_jac == ctx->jac_fp32 && same_structure(ctx->hp.d, *desc) &&
@@ -1506,12 +1516,16 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
             return 0;
         }
         // the point-sharded iterative plan: no ordering, no symbolic analysis, no factor
+        ulap("structure check");
         free_device(ctx);
+        ulap("free device");
         ctx->plan_hash = 0;
         ctx->analysed = false;
         copy_host(ctx->hp, desc);
+        ulap("copy host");
         if (!ctx->sp_tr) ctx->sp_tr = new CtxTransport(ctx);
         ctx->sp.reset(new SpSolver(ctx->device, ctx->st, ctx->rank, ctx->nranks, ctx->sp_tr, ctx->comm != nullptr));
+        ulap("solver object");
         ctx->sp->tol = ctx->pcg_tol;
         ctx->sp->max_it = ctx->pcg_max_it;
         ctx->sp->fp32_jac = ctx->jac_fp32;
