@@ -54,6 +54,79 @@ static void tile_shape_stats(const std::vector<int32_t> &tab, int32_t nt, int64_
     std::fprintf(stderr, "[deftri plan]   4a cross slots %lld\n", (long long)nx);
 }
 
+// The entries stage on host threads: each thread builds a contiguous range of tiles into buffers of
+// its own, its counters starting from zero; the buffers are then concatenated in tile order and the
+// earlier ranges' sizes added to the tile table's entry and halo bases, the chunk bases and the cross
+// slot ids — the arrays one sequential pass over the tiles writes (plan digests unchanged)
+namespace {
+
+constexpr int32_t kLeForeign = 1 << 30;                 // a chunk base counted among the halo-only edges
+
+struct TileBuf {
+    int64_t t0 = 0, t1 = 0;
+    std::vector<uint32_t> m0, m1;
+    std::vector<int32_t> halo, order, foreign, chunk;   // chunk: (le, first cross slot) per 64 entries
+    std::vector<std::pair<int32_t, int32_t>> xt;        // (target row, cross slot)
+    int64_t nx = 0;
+    int32_t segmax = 1, max_lds = 0;
+    const char *err = nullptr;
+};
+
+bool merge_tile_bufs(std::vector<TileBuf> &B, int nb, SpPlanHost &H, std::vector<int32_t> &order,
+                     std::vector<int32_t> *order_foreign, int64_t n_owned, std::vector<std::pair<int32_t, int32_t>> &xt,
+                     int64_t &nx, int32_t &segmax, int32_t &max_lds, std::string &why) {
+    for (int b = 0; b < nb; b++)
+        if (B[b].err) { why = B[b].err; return false; }
+    std::vector<int64_t> bm(nb + 1, 0), bh(nb + 1, 0), bo(nb + 1, 0), bf(nb + 1, 0), bc(nb + 1, 0), bx(nb + 1, 0),
+        bt(nb + 1, 0);
+    for (int b = 0; b < nb; b++) {
+        bm[b + 1] = bm[b] + (int64_t)B[b].m0.size();
+        bh[b + 1] = bh[b] + (int64_t)B[b].halo.size();
+        bo[b + 1] = bo[b] + (int64_t)B[b].order.size();
+        bf[b + 1] = bf[b] + (int64_t)B[b].foreign.size();
+        bc[b + 1] = bc[b] + (int64_t)B[b].chunk.size();
+        bx[b + 1] = bx[b] + B[b].nx;
+        bt[b + 1] = bt[b] + (int64_t)B[b].xt.size();
+        segmax = std::max(segmax, B[b].segmax);
+        max_lds = std::max(max_lds, B[b].max_lds);
+    }
+    if (bm[nb] >= (1LL << 31) || bx[nb] >= (1LL << 31)) { why = "more than 2^31 tile entries or cross slots"; return false; }
+    H.tile_m0.resize(bm[nb]);
+    H.tile_m1.resize(bm[nb]);
+    H.tile_halo.resize(bh[nb]);
+    H.tile_chunk.resize(bc[nb]);
+    order.resize(bo[nb]);
+    if (order_foreign) order_foreign->resize(bf[nb]);
+    xt.resize(bt[nb]);
+    auto cp = [&](int, int64_t b0, int64_t b1) {
+        for (int64_t b = b0; b < b1; b++) {
+            TileBuf &X = B[b];
+            std::copy(X.m0.begin(), X.m0.end(), H.tile_m0.begin() + bm[b]);
+            std::copy(X.m1.begin(), X.m1.end(), H.tile_m1.begin() + bm[b]);
+            std::copy(X.halo.begin(), X.halo.end(), H.tile_halo.begin() + bh[b]);
+            std::copy(X.order.begin(), X.order.end(), order.begin() + bo[b]);
+            if (order_foreign) std::copy(X.foreign.begin(), X.foreign.end(), order_foreign->begin() + bf[b]);
+            for (size_t k = 0; k < X.chunk.size(); k += 2) {
+                const int32_t le = X.chunk[k];
+                H.tile_chunk[bc[b] + k] = (le & kLeForeign) ? (int32_t)(n_owned + bf[b] + (le & ~kLeForeign)) : (int32_t)(bo[b] + le);
+                H.tile_chunk[bc[b] + k + 1] = (int32_t)(bx[b] + X.chunk[k + 1]);
+            }
+            for (size_t k = 0; k < X.xt.size(); k++) xt[bt[b] + k] = {X.xt[k].first, (int32_t)(bx[b] + X.xt[k].second)};
+            for (int64_t t = X.t0; t < X.t1; t++) {
+                int32_t *T = &H.tile_tab[8 * (size_t)t];
+                T[3] += (int32_t)bm[b];
+                T[5] += (int32_t)bh[b];
+            }
+            X = TileBuf();
+        }
+    };
+    chunked(nb, 1, cp);
+    nx = bx[nb];
+    return true;
+}
+
+}  // namespace
+
 bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order, std::vector<int32_t> &order_foreign,
                  std::string &why) {
     const int32_t ng = in.ng;
@@ -237,9 +310,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     //    edges first)
     H.tile_tab.assign(8 * (size_t)nt, 0);
     order.clear();
-    order.reserve(oe.size());
     order_foreign.clear();
-    order_foreign.reserve(fe.size());
     const int64_t n_owned = (int64_t)oe.size();
     std::vector<uint32_t> &m0 = H.tile_m0, &m1 = H.tile_m1;
     m0.clear(); m1.clear();
@@ -251,15 +322,26 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
     std::vector<std::pair<int32_t, int32_t>> xt;
     int64_t nx = 0;
     int32_t segmax = 1, max_lds = 0;
-    std::vector<int32_t> lrow(ng, -1);            // group -> LDS row base inside the current tile
-    std::vector<int32_t> slotcnt, slotfill;       // per tile row
-    for (int32_t t = 0; t < nt; t++) {
+    std::vector<TileBuf> bufs(16);
+    const int nbuf = chunked(nt, 16, [&](int c, int64_t t_lo, int64_t t_hi) {
+      TileBuf &B = bufs[c];
+      B.t0 = t_lo;
+      B.t1 = t_hi;
+      std::vector<uint32_t> &m0 = B.m0, &m1 = B.m1;
+      std::vector<int32_t> &order = B.order, &order_foreign = B.foreign;
+      std::vector<std::pair<int32_t, int32_t>> &xt = B.xt;
+      int64_t &nx = B.nx;
+      int32_t &segmax = B.segmax, &max_lds = B.max_lds;
+      std::vector<int32_t> lrow(ng, -1);          // group -> LDS row base inside the current tile
+      std::vector<int32_t> slotcnt, slotfill;     // per tile row
+      std::vector<int32_t> hg;
+      for (int64_t t = t_lo; t < t_hi; t++) {
         const int32_t g0 = tstart[t], g1 = tstart[t + 1];
         const int32_t r0 = grow[g0] - lo;
         int32_t nr = 0;
         for (int32_t g = g0; g < g1; g++) { lrow[g] = nr; nr += gsz[g]; }
         // halo groups, ascending: out-edges' j groups outside the tile, halo-only edges' i groups
-        std::vector<int32_t> hg;
+        hg.clear();
         for (int32_t g = g0; g < g1; g++) {
             for (int64_t k = ooff[g]; k < ooff[g + 1]; k++)
                 if (okj[k] < g0 || okj[k] >= g1) hg.push_back(okj[k]);
@@ -267,11 +349,11 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         }
         std::sort(hg.begin(), hg.end());
         hg.erase(std::unique(hg.begin(), hg.end()), hg.end());
-        const int32_t h0 = (int32_t)H.tile_halo.size();
+        const int32_t h0 = (int32_t)B.halo.size();
         int32_t nh = 0;
         for (int32_t gj : hg) {
             lrow[gj] = nr + nh;
-            for (int32_t k = 0; k < gsz[gj]; k++) H.tile_halo.push_back(grow[gj] + k);   // (global rows)
+            for (int32_t k = 0; k < gsz[gj]; k++) B.halo.push_back(grow[gj] + k);   // (global rows)
             nh += gsz[gj];
         }
         // remote slots: count per tile row, in entry order
@@ -294,7 +376,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         int32_t ns = 0;
         for (int32_t r = 0; r < nr; r++) {
             slotfill[r] = ns;
-            if (slotcnt[r] > 0xffff) { why = "too many slots on a row"; return false; }
+            if (slotcnt[r] > 0xffff) { B.err = "too many slots on a row"; return; }
             H.tile_rs[r0 + r] = ns | slotcnt[r] << 16;
             ns += slotcnt[r];
         }
@@ -309,7 +391,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
             }
         };
         auto chunk_start = [&](int64_t le) {
-            if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)le), H.tile_chunk.push_back((int32_t)nx);
+            if (fill % 64 == 0) B.chunk.push_back((int32_t)le), B.chunk.push_back((int32_t)nx);
         };
         for (int32_t g = g0; g < g1; g++) {
             const int64_t k0 = ooff[g], k1 = ooff[g + 1];
@@ -360,7 +442,7 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         if (any_f) pad_chunk();
         for (int32_t g = g0; g < g1; g++)
             for (int64_t k = foff[g]; k < foff[g + 1]; k++) {
-                chunk_start(n_owned + (int64_t)order_foreign.size());
+                chunk_start(kLeForeign | (int64_t)order_foreign.size());
                 const int64_t e = fe[k];
                 const int32_t gi = fki[k];
                 const int32_t ub = lrow[g];
@@ -383,8 +465,11 @@ bool build_tiles(const TileInput &in, SpPlanHost &H, std::vector<int32_t> &order
         max_lds = std::max<int32_t>(max_lds, (int32_t)lds_of(nr, nh, ns));
         for (int32_t g = g0; g < g1; g++) lrow[g] = -1;
         for (int32_t gj : hg) lrow[gj] = -1;
-    }
+      }
+    });
     lap("entries, slots");
+    if (!merge_tile_bufs(bufs, nbuf, H, order, &order_foreign, n_owned, xt, nx, segmax, max_lds, why)) return false;
+    lap("entries merged");
     if ((int64_t)order.size() != n_owned || order_foreign.size() != fe.size()) { why = "tile order lost edges"; return false; }
     // cross slots by target row, source order inside a row (a counting sort; xt is in source order):
     // the writer scatters its two slots to their destination positions, so a row's slots are one
@@ -443,14 +528,24 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
     if (in.S != 2 * Q) { why = "not two depth scales per pair"; return false; }
     if ((int64_t)Q * ng >= (1LL << 31)) { why = "too many (pair, group) units"; return false; }
     // 1. units (pair, group) with edges, in (pair, Morton group) order; their two rows
+    //    (on host threads: a unit's flag and point are the same from every edge of a valid graph; an
+    //    invalid one, a unit with two points, fails the row check below whichever edge wrote last)
     std::vector<int32_t> uid((size_t)Q * ng, -1), upt((size_t)Q * ng, -1);
-    for (int64_t e = 0; e < E; e++) {
-        const int32_t q = in.pair[e];
-        if (q < 0 || q >= Q) { why = "an edge's pair out of range"; return false; }
-        uid[(size_t)q * ng + in.gpos[ap[4 * e]]] = 0;
-        uid[(size_t)q * ng + in.gpos[ap[4 * e + 2]]] = 0;
-        upt[(size_t)q * ng + in.gpos[ap[4 * e]]] = ap[4 * e];
-        upt[(size_t)q * ng + in.gpos[ap[4 * e + 2]]] = ap[4 * e + 2];
+    {
+        int bad[16] = {0};
+        const int nch = chunked(E, 1 << 16, [&](int c, int64_t e0, int64_t e1) {
+            for (int64_t e = e0; e < e1; e++) {
+                const int32_t q = in.pair[e];
+                if (q < 0 || q >= Q) { bad[c] = 1; return; }
+                for (int s = 0; s < 2; s++) {
+                    const size_t k = (size_t)q * ng + in.gpos[ap[4 * e + 2 * s]];
+                    __atomic_store_n(&uid[k], 0, __ATOMIC_RELAXED);
+                    __atomic_store_n(&upt[k], ap[4 * e + 2 * s], __ATOMIC_RELAXED);
+                }
+            }
+        });
+        for (int c = 0; c < nch; c++)
+            if (bad[c]) { why = "an edge's pair out of range"; return false; }
     }
     int32_t nu = 0;
     if (in.points) {
@@ -458,8 +553,17 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
         // (its keyframe 1's positions).  The groups' global Morton order follows one keyframe's
         // positions; cut by it, the other pairs' tiles had twice the halo rows and cut edges (C3: 240
         // halo rows per tile, 36 % of the edges cut, against 124 and 18 % in the pair's own order)
-        std::vector<std::pair<uint64_t, int32_t>> ks;
-        for (int32_t q = 0; q < Q; q++) {
+        // pairs on host threads: each pair's units counted, then numbered from the pair's base
+        std::vector<int32_t> qb(Q + 1, 0);
+        chunked(Q, 1, [&](int, int64_t q0, int64_t q1) {
+            for (int64_t q = q0; q < q1; q++)
+                for (int32_t g = 0; g < ng; g++) qb[q + 1] += uid[(size_t)q * ng + g] == 0;
+        });
+        for (int32_t q = 0; q < Q; q++) qb[q + 1] += qb[q];
+        nu = qb[Q];
+        chunked(Q, 1, [&](int, int64_t q0, int64_t q1) {
+          std::vector<std::pair<uint64_t, int32_t>> ks;
+          for (int64_t q = q0; q < q1; q++) {
             ks.clear();
             double lo[2] = {1e300, 1e300}, hi[2] = {-1e300, -1e300};
             for (int32_t g = 0; g < ng; g++) {
@@ -470,15 +574,17 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
                     lo[c] = std::min(lo[c], v); hi[c] = std::max(hi[c], v);
                 }
             }
-                    for (int32_t g = 0; g < ng; g++) {
+            for (int32_t g = 0; g < ng; g++) {
                 const size_t k = (size_t)q * ng + g;
                 if (uid[k] != 0) continue;
                 const double *pp = in.points + 3 * (int64_t)upt[k];
                 ks.push_back({curve_key(pp[0], pp[1], lo, hi), g});
             }
             std::sort(ks.begin(), ks.end());
-            for (const auto &kg : ks) uid[(size_t)q * ng + kg.second] = nu++;
-        }
+            int32_t n = qb[q];
+            for (const auto &kg : ks) uid[(size_t)q * ng + kg.second] = n++;
+          }
+        });
     } else {
         for (size_t k = 0; k < uid.size(); k++)
             if (uid[k] == 0) uid[k] = nu++;
@@ -488,35 +594,62 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
     for (int32_t q = 0; q < Q; q++)
         for (int32_t g = 0; g < ng; g++)
             if (uid[(size_t)q * ng + g] >= 0) upair[uid[(size_t)q * ng + g]] = q;
+    // the edges by unit: one pass that sets and checks every unit's rows and counts its out- / in-edges,
+    // then a counting sort.  When the edges are pair-major (the graph builder writes them pair by pair)
+    // a pair's edges touch only that pair's units, so the pairs run on host threads, each exactly the
+    // sequential loop over its own edge range (the first failing pair's first error is the sequential
+    // one); otherwise one thread
     std::vector<int32_t> egi(E), egj(E);
     std::vector<int32_t> ocnt(nu + 1, 0), icnt(nu + 1, 0);
-    for (int64_t e = 0; e < E; e++) {
-        const size_t qb = (size_t)in.pair[e] * ng;
-        const int32_t ui = uid[qb + in.gpos[ap[4 * e]]], uj = uid[qb + in.gpos[ap[4 * e + 2]]];
-        if (ui == uj) { why = "an edge inside one group"; return false; }
-        if (in.gpos[ap[4 * e]] != in.gpos[ap[4 * e + 1]] || in.gpos[ap[4 * e + 2]] != in.gpos[ap[4 * e + 3]]) {
-            why = "an edge's copies in two groups";
-            return false;
-        }
-        for (int s = 0; s < 2; s++) {
-            const int32_t u = s ? uj : ui;
-            const int32_t r0 = row[ap[4 * e + 2 * s]], r1 = row[ap[4 * e + 2 * s + 1]];
-            if (urow[2 * (size_t)u] < 0) { urow[2 * (size_t)u] = r0; urow[2 * (size_t)u + 1] = r1; }
-            else if (urow[2 * (size_t)u] != r0 || urow[2 * (size_t)u + 1] != r1) { why = "a unit's rows differ between its edges"; return false; }
-        }
-        egi[e] = ui;
-        egj[e] = uj;
-        ocnt[ui + 1]++;
-        icnt[uj + 1]++;
+    std::vector<int64_t> eb(Q + 1, E);
+    bool pair_major = true;
+    for (int64_t e = 1; e < E && pair_major; e++) pair_major = in.pair[e] >= in.pair[e - 1];
+    if (pair_major) {
+        for (int64_t e = E - 1; e >= 0; e--) eb[in.pair[e]] = e;
+        for (int32_t q = Q - 1; q >= 0; q--) eb[q] = std::min(eb[q], eb[q + 1]);
+    } else {
+        std::fill(eb.begin(), eb.end(), E);
+        eb[0] = 0;
     }
+    const int32_t npart = pair_major ? Q : 1;
+    std::vector<const char *> qbad(npart, nullptr);
+    chunked(npart, 1, [&](int, int64_t q0, int64_t q1) {
+        for (int64_t q = q0; q < q1; q++)
+            for (int64_t e = eb[q]; e < eb[q + 1]; e++) {
+                const size_t qb = (size_t)in.pair[e] * ng;
+                const int32_t ui = uid[qb + in.gpos[ap[4 * e]]], uj = uid[qb + in.gpos[ap[4 * e + 2]]];
+                if (ui == uj) { qbad[q] = "an edge inside one group"; break; }
+                if (in.gpos[ap[4 * e]] != in.gpos[ap[4 * e + 1]] || in.gpos[ap[4 * e + 2]] != in.gpos[ap[4 * e + 3]]) {
+                    qbad[q] = "an edge's copies in two groups";
+                    break;
+                }
+                bool differ = false;
+                for (int s = 0; s < 2; s++) {
+                    const int32_t u = s ? uj : ui;
+                    const int32_t r0 = row[ap[4 * e + 2 * s]], r1 = row[ap[4 * e + 2 * s + 1]];
+                    if (urow[2 * (size_t)u] < 0) { urow[2 * (size_t)u] = r0; urow[2 * (size_t)u + 1] = r1; }
+                    else if (urow[2 * (size_t)u] != r0 || urow[2 * (size_t)u + 1] != r1) differ = true;
+                }
+                if (differ) { qbad[q] = "a unit's rows differ between its edges"; break; }
+                egi[e] = ui;
+                egj[e] = uj;
+                ocnt[ui + 1]++;
+                icnt[uj + 1]++;
+            }
+    });
+    for (int32_t q = 0; q < npart; q++)
+        if (qbad[q]) { why = qbad[q]; return false; }
     for (int32_t u = 0; u < nu; u++) { ocnt[u + 1] += ocnt[u]; icnt[u + 1] += icnt[u]; }
     std::vector<int32_t> oe(E), isrc(E);
     {
         std::vector<int32_t> fo(ocnt.begin(), ocnt.end() - 1), fi(icnt.begin(), icnt.end() - 1);
-        for (int64_t e = 0; e < E; e++) {
-            oe[fo[egi[e]]++] = (int32_t)e;
-            isrc[fi[egj[e]]++] = egi[e];
-        }
+        chunked(npart, 1, [&](int, int64_t q0, int64_t q1) {
+            for (int64_t q = q0; q < q1; q++)
+                for (int64_t e = eb[q]; e < eb[q + 1]; e++) {
+                    oe[fo[egi[e]]++] = (int32_t)e;
+                    isrc[fi[egj[e]]++] = egi[e];
+                }
+        });
     }
     lap("edges by unit");
     for (int32_t u = 0; u < nu; u++)
@@ -551,48 +684,65 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
     lap("depth check");
     // 2. greedy partition per pair: consecutive units while units <= umax and the LDS estimate fits
     auto lds_of = [&](int64_t nr, int64_t nh, int64_t ns) { return 24 * (nr + nh) + 24 * nr + 24 * ns + kSpTileLdsFixed; };
+    //    A pair's units are one range [pb[q], pb[q + 1]) and its edges stay inside it, so the pairs are
+    //    cut independently, on host threads; the tile starts are concatenated in pair order
     std::vector<int32_t> tstart;
-    std::vector<int32_t> hcnt(nu, 0), stamp(nu, -1);
     {
-        int32_t us = 0, attempt = 0;
-        int64_t nr = 0, nh = 0, ns = 0, units = 0;
-        std::vector<int32_t> halo_members;
-        tstart.push_back(0);
-        for (int32_t u = 0; u < nu;) {
-            int64_t dnh = 0, dns = 0;
-            attempt++;
-            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
-                const int32_t uj = egj[oe[k]];
-                if (uj >= us && uj < u) dns += 2;
-                else if (hcnt[uj] == 0 && stamp[uj] != attempt) { stamp[uj] = attempt; dnh += 2; }
-            }
-            for (int32_t k = icnt[u]; k < icnt[u + 1]; k++)
-                if (isrc[k] >= us && isrc[k] < u) dns += 2;
-            if (hcnt[u] > 0) dnh -= 2;
-            const bool same_pair = units == 0 || upair[u] == upair[us];
-            const bool fits = same_pair && units + 1 <= umax && lds_of(nr + 2, nh + dnh, ns + dns) <= lds_budget &&
-                              nr + 2 + nh + dnh < 4096 && ns + dns < 4096;
-            if (!fits && units > 0) {
-                for (int32_t h : halo_members) hcnt[h] = 0;
+        std::vector<int32_t> pb(Q + 1, nu);
+        for (int32_t u = nu - 1; u >= 0; u--) pb[upair[u]] = u;
+        for (int32_t q = Q - 1; q >= 0; q--) pb[q] = std::min(pb[q], pb[q + 1]);
+        int32_t pmax = 0;
+        for (int32_t q = 0; q < Q; q++) pmax = std::max(pmax, pb[q + 1] - pb[q]);
+        std::vector<std::vector<int32_t>> ts(16);
+        const int nts = chunked(Q, 1, [&](int c, int64_t q_lo, int64_t q_hi) {
+            std::vector<int32_t> &out = ts[c];
+            std::vector<int32_t> hcnt(pmax, 0), stamp(pmax, -1), halo_members;   // by unit - pb[q]
+            int32_t attempt = 0;
+            for (int64_t q = q_lo; q < q_hi; q++) {
+                const int32_t ub = pb[q], ue = pb[q + 1];
+                if (ub >= ue) continue;
+                int32_t us = ub;
+                int64_t nr = 0, nh = 0, ns = 0, units = 0;
+                out.push_back(ub);
+                for (int32_t u = ub; u < ue;) {
+                    int64_t dnh = 0, dns = 0;
+                    attempt++;
+                    for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
+                        const int32_t uj = egj[oe[k]];
+                        if (uj >= us && uj < u) dns += 2;
+                        else if (hcnt[uj - ub] == 0 && stamp[uj - ub] != attempt) { stamp[uj - ub] = attempt; dnh += 2; }
+                    }
+                    for (int32_t k = icnt[u]; k < icnt[u + 1]; k++)
+                        if (isrc[k] >= us && isrc[k] < u) dns += 2;
+                    if (hcnt[u - ub] > 0) dnh -= 2;
+                    const bool fits = units + 1 <= umax && lds_of(nr + 2, nh + dnh, ns + dns) <= lds_budget &&
+                                      nr + 2 + nh + dnh < 4096 && ns + dns < 4096;
+                    if (!fits && units > 0) {
+                        for (int32_t h : halo_members) hcnt[h - ub] = 0;
+                        halo_members.clear();
+                        us = u;
+                        nr = nh = ns = units = 0;
+                        out.push_back(u);
+                        continue;
+                    }
+                    for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
+                        const int32_t uj = egj[oe[k]];
+                        if (!(uj >= us && uj < u))
+                            if (hcnt[uj - ub]++ == 0) halo_members.push_back(uj);
+                    }
+                    hcnt[u - ub] = 0;
+                    nr += 2;
+                    nh += dnh;
+                    ns += dns;
+                    units++;
+                    u++;
+                }
+                for (int32_t h : halo_members) hcnt[h - ub] = 0;
                 halo_members.clear();
-                us = u;
-                nr = nh = ns = units = 0;
-                tstart.push_back(u);
-                continue;
             }
-            for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
-                const int32_t uj = egj[oe[k]];
-                if (!(uj >= us && uj < u))
-                    if (hcnt[uj]++ == 0) halo_members.push_back(uj);
-            }
-            hcnt[u] = 0;
-            nr += 2;
-            nh += dnh;
-            ns += dns;
-            units++;
-            u++;
-        }
-        for (int32_t h : halo_members) hcnt[h] = 0;
+        });
+        for (int c = 0; c < nts; c++) tstart.insert(tstart.end(), ts[c].begin(), ts[c].end());
+        if (tstart.empty()) tstart.push_back(0);
         tstart.push_back(nu);
     }
     lap("partition");
@@ -601,7 +751,6 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
     H.tile_tab.assign(8 * (size_t)nt, 0);
     H.tile_poff.assign(Q + 1, nt);
     order.clear();
-    order.reserve(E);
     std::vector<uint32_t> &m0 = H.tile_m0, &m1 = H.tile_m1;
     m0.clear(); m1.clear();
     H.tile_chunk.clear();
@@ -611,42 +760,56 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
     std::vector<std::pair<int32_t, int32_t>> xt;         // (target row, slot id)
     int64_t nx = 0;
     int32_t segmax = 1, max_lds = 0;
-    std::vector<int32_t> lrow(nu, -1);                  // unit -> LDS row base inside the current tile
-    std::vector<int32_t> slotcnt, slotfill;
-    for (int32_t t = 0; t < nt; t++) {
+    // a tile's rows are units [u0, u1)'s: rows 2 u0 .. 2 u1 of the tile row list (tiles cover the units
+    // in order), so each thread writes its tiles' trow / rs ranges in place
+    H.tile_trow.assign(2 * (size_t)nu, 0);
+    H.tile_rs.assign(2 * (size_t)nu, 0);
+    std::vector<TileBuf> bufs(16);
+    const int nbuf = chunked(nt, 16, [&](int c, int64_t t_lo, int64_t t_hi) {
+      TileBuf &B = bufs[c];
+      B.t0 = t_lo;
+      B.t1 = t_hi;
+      std::vector<uint32_t> &m0 = B.m0, &m1 = B.m1;
+      std::vector<int32_t> &order = B.order;
+      std::vector<std::pair<int32_t, int32_t>> &xt = B.xt;
+      int64_t &nx = B.nx;
+      int32_t &segmax = B.segmax, &max_lds = B.max_lds;
+      std::vector<int32_t> slotcnt, slotfill, hu;
+      for (int64_t t = t_lo; t < t_hi; t++) {
         const int32_t u0 = tstart[t], u1 = tstart[t + 1], q = upair[u0];
-        if (H.tile_poff[q] == nt) H.tile_poff[q] = t;
-        const int32_t nr = 2 * (u1 - u0), r0 = (int32_t)H.tile_trow.size();
+        const int32_t nr = 2 * (u1 - u0), r0 = 2 * u0;
         for (int32_t u = u0; u < u1; u++) {
-            lrow[u] = 2 * (u - u0);
-            H.tile_trow.push_back(urow[2 * (size_t)u]);
-            H.tile_trow.push_back(urow[2 * (size_t)u + 1]);
+            H.tile_trow[2 * (size_t)u] = urow[2 * (size_t)u];
+            H.tile_trow[2 * (size_t)u + 1] = urow[2 * (size_t)u + 1];
         }
-        std::vector<int32_t> hu;
+        hu.clear();
         for (int32_t u = u0; u < u1; u++)
             for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++)
                 if (egj[oe[k]] < u0 || egj[oe[k]] >= u1) hu.push_back(egj[oe[k]]);
         std::sort(hu.begin(), hu.end());
         hu.erase(std::unique(hu.begin(), hu.end()), hu.end());
-        const int32_t h0 = (int32_t)H.tile_halo.size();
+        // unit -> LDS row base: the tile's units, then the halo units in ascending order
+        auto lrow = [&](int32_t u) {
+            return u >= u0 && u < u1 ? 2 * (u - u0) : nr + 2 * (int32_t)(std::lower_bound(hu.begin(), hu.end(), u) - hu.begin());
+        };
+        const int32_t h0 = (int32_t)B.halo.size();
         const int32_t nh = 2 * (int32_t)hu.size();
         for (size_t k = 0; k < hu.size(); k++) {
-            lrow[hu[k]] = nr + 2 * (int32_t)k;
-            H.tile_halo.push_back(urow[2 * (size_t)hu[k]]);
-            H.tile_halo.push_back(urow[2 * (size_t)hu[k] + 1]);
+            B.halo.push_back(urow[2 * (size_t)hu[k]]);
+            B.halo.push_back(urow[2 * (size_t)hu[k] + 1]);
         }
         slotcnt.assign(nr, 0);
         for (int32_t u = u0; u < u1; u++)
             for (int32_t k = ocnt[u]; k < ocnt[u + 1]; k++) {
                 const int32_t uj = egj[oe[k]];
-                if (uj >= u0 && uj < u1) { slotcnt[lrow[uj]]++; slotcnt[lrow[uj] + 1]++; }
+                if (uj >= u0 && uj < u1) { slotcnt[2 * (uj - u0)]++; slotcnt[2 * (uj - u0) + 1]++; }
             }
         slotfill.assign(nr, 0);
         int32_t ns = 0;
         for (int32_t r = 0; r < nr; r++) {
             slotfill[r] = ns;
-            if (slotcnt[r] > 0xffff) { why = "too many slots on a row"; return false; }
-            H.tile_rs.push_back(ns | slotcnt[r] << 16);
+            if (slotcnt[r] > 0xffff) { B.err = "too many slots on a row"; return; }
+            H.tile_rs[r0 + r] = ns | slotcnt[r] << 16;
             ns += slotcnt[r];
         }
         const int64_t e0 = (int64_t)m0.size();
@@ -665,12 +828,12 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
             segmax = std::max(segmax, cnt);
             if (fill % 64 + cnt > 64) pad_chunk();
             for (int32_t k = k0; k < k1; k++) {
-                if (fill % 64 == 0) H.tile_chunk.push_back((int32_t)order.size()), H.tile_chunk.push_back((int32_t)nx);
+                if (fill % 64 == 0) B.chunk.push_back((int32_t)order.size()), B.chunk.push_back((int32_t)nx);
                 const int64_t e = oe[k];
                 const int32_t uj = egj[e];
                 const bool cut = uj < u0 || uj >= u1;
-                const uint32_t ub = (uint32_t)lrow[u];
-                const uint32_t rj0 = (uint32_t)lrow[uj], rj1 = (uint32_t)lrow[uj] + 1;
+                const uint32_t ub = (uint32_t)(2 * (u - u0));
+                const uint32_t rj0 = (uint32_t)lrow(uj), rj1 = rj0 + 1;
                 uint32_t w0 = rj0 | rj1 << 12 | kTmValid;
                 if (k == k0) w0 |= kTmHead;
                 if (k == k1 - 1) w0 |= kTmLast;
@@ -690,17 +853,20 @@ bool build_tiles_multi(const TileInput &in, SpPlanHost &H, std::vector<int32_t> 
                 fill++;
             }
         }
-        if (fill == 0) { H.tile_chunk.push_back((int32_t)order.size()); H.tile_chunk.push_back((int32_t)nx); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
+        if (fill == 0) { B.chunk.push_back((int32_t)order.size()); B.chunk.push_back((int32_t)nx); m0.push_back(kTmHead); m1.push_back(0); fill = 1; }
         pad_chunk();
         const int64_t ne = (int64_t)m0.size() - e0;
-        if (nr > 256) { why = "a tile of more than 128 units"; return false; }   // (ub: 8 bits)
+        if (nr > 256) { B.err = "a tile of more than 128 units"; return; }   // (ub: 8 bits)
         int32_t *T = &H.tile_tab[8 * (size_t)t];
         T[0] = r0; T[1] = nr; T[2] = nh; T[3] = (int32_t)e0; T[4] = (int32_t)ne; T[5] = h0; T[6] = ns; T[7] = q;
         max_lds = std::max<int32_t>(max_lds, (int32_t)lds_of(nr, nh, ns));
-        for (int32_t u = u0; u < u1; u++) lrow[u] = -1;
-        for (int32_t u : hu) lrow[u] = -1;
-    }
+      }
+    });
     lap("entries, slots");
+    if (!merge_tile_bufs(bufs, nbuf, H, order, nullptr, 0, xt, nx, segmax, max_lds, why)) return false;
+    for (int32_t t = 0; t < nt; t++)
+        if (H.tile_poff[H.tile_tab[8 * (size_t)t + 7]] == nt) H.tile_poff[H.tile_tab[8 * (size_t)t + 7]] = t;
+    lap("entries merged");
     for (int32_t q = Q - 1; q >= 0; q--)
         if (H.tile_poff[q] == nt) H.tile_poff[q] = H.tile_poff[q + 1];
     if ((int64_t)order.size() != E) { why = "tile order lost edges"; return false; }
