@@ -131,6 +131,8 @@ struct Sweep {
     int hsize = 0, hstart = 0;
     double cx = 0, cy = 0;
     std::vector<int> stack;
+    std::vector<int> ids;                                // sweep position -> point id
+    std::vector<double> sorted_xy;
 
     const double *P(int i) const { return xy + 2 * (size_t)i; }
 
@@ -235,11 +237,24 @@ struct Sweep {
         if (i2 < 0) return false;                        // all collinear
         if (orient2d(P(i0), P(i1), P(i2)) < 0) std::swap(i1, i2);
         circumr2(i0, i1, i2, cx, cy);
-        std::vector<double> dist(n);
-        for (int i = 0; i < n; i++) dist[i] = d2(i, cx, cy);
-        std::vector<int> ids(n);
-        std::iota(ids.begin(), ids.end(), 0);
-        std::sort(ids.begin(), ids.end(), [&](int a, int b) { return dist[a] < dist[b] || (dist[a] == dist[b] && a < b); });
+        // the sweep order (distance from the seed circumcentre, then index); the points are copied into
+        // that order and the sweep runs on positions, so its hull walks and in-circle tests read
+        // neighbouring memory (the triangles are mapped back to point ids at the end)
+        std::vector<std::pair<double, int>> di(n);
+        for (int i = 0; i < n; i++) di[i] = {d2(i, cx, cy), i};
+        std::sort(di.begin(), di.end());
+        ids.resize(n);
+        std::vector<int> pos(n);
+        sorted_xy.resize(2 * (size_t)n);
+        for (int k = 0; k < n; k++) {
+            ids[k] = di[k].second;
+            pos[ids[k]] = k;
+            sorted_xy[2 * (size_t)k] = P(ids[k])[0];
+            sorted_xy[2 * (size_t)k + 1] = P(ids[k])[1];
+        }
+        std::vector<std::pair<double, int>>().swap(di);
+        xy = sorted_xy.data();
+        i0 = pos[i0]; i1 = pos[i1]; i2 = pos[i2];
         hsize = std::max(1, (int)std::ceil(std::sqrt((double)n)));
         hprev.assign(n, -1); hnext.assign(n, -1); htri.assign(n, -1); hhash.assign(hsize, -1);
         hstart = i0;
@@ -254,7 +269,7 @@ struct Sweep {
         add_tri(i0, i1, i2, -1, -1, -1);
         double px = 0, py = 0;
         for (int k = 0; k < n; k++) {
-            int i = ids[k];
+            int i = k;
             double x = P(i)[0], y = P(i)[1];
             if (k > 0 && x == px && y == py) { skipped++; continue; }      // exact duplicate
             px = x; py = y;
@@ -296,7 +311,7 @@ struct Sweep {
             hhash[key(x, y)] = i;
             hhash[key(P(e)[0], P(e)[1])] = e;
         }
-        // hull size
+        for (int &v : tri) v = ids[v];                  // positions -> point ids
         return true;
     }
 };
@@ -308,31 +323,42 @@ struct Sweep {
 // so the mesh area (a sum in this order) is the same whoever built the set (a full sweep, the graph
 // builder's re-validated previous mesh or a flip-repaired one, graph_builder.cpp)
 static void canonical_tris(const std::vector<int32_t> &in, int n, std::vector<int32_t> &tris) {
+    // bucketed by first vertex (a counting sort), each bucket's (second, third) packed in one 64-bit
+    // key and insertion-sorted in place (a vertex starts ~2 triangles)
     const int nt = (int)in.size() / 3;
-    std::vector<int32_t> rot3(in.size());
+    auto rot = [&](int t, int32_t &a, int32_t &b, int32_t &c) {
+        const int32_t x = in[3 * (size_t)t], y = in[3 * (size_t)t + 1], z = in[3 * (size_t)t + 2];
+        if (x < y && x < z) { a = x; b = y; c = z; }
+        else if (y < z) { a = y; b = z; c = x; }
+        else { a = z; b = x; c = y; }
+    };
     std::vector<int32_t> cnt(n + 1, 0);
     for (int t = 0; t < nt; t++) {
-        const int32_t a = in[3 * t], b = in[3 * t + 1], c = in[3 * t + 2];
-        int32_t *o = &rot3[3 * (size_t)t];
-        if (a < b && a < c) { o[0] = a; o[1] = b; o[2] = c; }
-        else if (b < c) { o[0] = b; o[1] = c; o[2] = a; }
-        else { o[0] = c; o[1] = a; o[2] = b; }
-        cnt[o[0] + 1]++;
+        int32_t a, b, c;
+        rot(t, a, b, c);
+        cnt[a + 1]++;
     }
     for (int i = 0; i < n; i++) cnt[i + 1] += cnt[i];
-    std::vector<int32_t> order(nt);
+    std::vector<uint64_t> key(nt);
     {
         std::vector<int32_t> fill(cnt.begin(), cnt.end() - 1);
-        for (int t = 0; t < nt; t++) order[fill[rot3[3 * (size_t)t]]++] = t;
+        for (int t = 0; t < nt; t++) {
+            int32_t a, b, c;
+            rot(t, a, b, c);
+            key[fill[a]++] = (uint64_t)(uint32_t)b << 32 | (uint32_t)c;
+        }
     }
-    for (int i = 0; i < n; i++)           // a vertex starts ~2 triangles: a short sort per bucket
-        std::sort(order.begin() + cnt[i], order.begin() + cnt[i + 1], [&](int32_t x, int32_t y) {
-            const int32_t *a = &rot3[3 * (size_t)x], *b = &rot3[3 * (size_t)y];
-            return a[1] != b[1] ? a[1] < b[1] : a[2] < b[2];
-        });
     tris.resize(in.size());
-    for (int k = 0; k < nt; k++)
-        for (int c = 0; c < 3; c++) tris[3 * (size_t)k + c] = rot3[3 * (size_t)order[k] + c];
+    for (int i = 0; i < n; i++) {
+        uint64_t *k0 = key.data() + cnt[i], *k1 = key.data() + cnt[i + 1];
+        for (uint64_t *p = k0 + 1; p < k1; p++)
+            for (uint64_t *q = p; q > k0 && q[-1] > q[0]; q--) std::swap(q[-1], q[0]);
+        for (int32_t k = cnt[i]; k < cnt[i + 1]; k++) {
+            tris[3 * (size_t)k] = i;
+            tris[3 * (size_t)k + 1] = (int32_t)(key[k] >> 32);
+            tris[3 * (size_t)k + 2] = (int32_t)(key[k] & 0xffffffffu);
+        }
+    }
 }
 
 bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_size, int &skipped) {
@@ -340,7 +366,7 @@ bool delaunay2d(const double *xy, int n, std::vector<int32_t> &tris, int &hull_s
     hull_size = 0;
     skipped = 0;
     if (n < 3) return false;
-    Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}};
+    Sweep s{xy, n, {}, {}, {}, {}, {}, {}, 0, 0, 0, 0, {}, {}, {}};
     if (!s.run(skipped)) return false;
     canonical_tris(s.tri, n, tris);
     int h = 0, e = s.hstart;
