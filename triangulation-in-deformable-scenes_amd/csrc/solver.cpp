@@ -21,6 +21,7 @@
 #include <functional>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <memory>
@@ -172,6 +173,7 @@ struct deftri_ctx {
     int plan_mode = DEFTRI_PLAN_AUTO;
     int jac_fp32 = 0;                       // deftri_set_jacobian_storage
     std::unique_ptr<SpSolver> sp;
+    std::thread sp_reaper;                  // a re-upload's previous solver, destroyed off the caller's thread
     bool sp_on = false;
     SpTransport *sp_tr = nullptr;           // RCCL / callback transport of `sp` (owned)
     int small_direct = 0;                   // PCG skipped for this problem (too small to win, see upload)
@@ -221,7 +223,24 @@ void drop_trial_graph(deftri_ctx *ctx) {
     ctx->trial_graph_failed = false;
 }
 
-void free_device(deftri_ctx *ctx) {
+void join_reaper(deftri_ctx *ctx) {
+    if (ctx->sp_reaper.joinable()) ctx->sp_reaper.join();
+}
+
+// reap_async (an iterative re-upload): the previous solver's streams, events, pinned and device
+// buffers are released on a thread of their own while the caller builds the next plan on the host
+// (~10 ms of hipFree / hipHostFree at C2); the new solver joins it before its first allocation, and
+// every other free_device (context destroy included) joins it first
+void free_device(deftri_ctx *ctx, bool reap_async = false) {
+    join_reaper(ctx);
+    if (reap_async && ctx->sp) {
+        SpSolver *old = ctx->sp.release();
+        const int dev = ctx->device;
+        ctx->sp_reaper = std::thread([old, dev] {
+            hipSetDevice(dev);
+            delete old;
+        });
+    }
     ctx->sp.reset();
     ctx->sp_on = false;
     drop_trial_graph(ctx);
@@ -1517,7 +1536,7 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
         }
         // the point-sharded iterative plan: no ordering, no symbolic analysis, no factor
         ulap("structure check");
-        free_device(ctx);
+        free_device(ctx, true);
         ulap("free device");
         ctx->plan_hash = 0;
         ctx->analysed = false;
@@ -1529,6 +1548,7 @@ int deftri_problem_upload(deftri_ctx *ctx, const deftri_problem_desc *desc) {
         ctx->sp->tol = ctx->pcg_tol;
         ctx->sp->max_it = ctx->pcg_max_it;
         ctx->sp->fp32_jac = ctx->jac_fp32;
+        ctx->sp->before_alloc = [ctx] { join_reaper(ctx); };
         rc = ctx->sp->upload(*desc);
         if (rc) { ctx->err = ctx->sp->err; ctx->sp.reset(); return rc; }
         ctx->sp_on = true;

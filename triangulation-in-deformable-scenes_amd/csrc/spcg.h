@@ -353,6 +353,7 @@ class SpSolver {
     SpSolver(int device, hipStream_t st, int rank, int nranks, SpTransport *tr, bool force_sharded = false);
     ~SpSolver();
     int upload(const deftri_problem_desc &d);
+    std::function<void()> before_alloc;            // upload: called once after the host plan build
     int refresh(const deftri_problem_desc &d);     // same structure: values only, plan kept
     int solve_lm(const deftri_lm_params &prm, deftri_report &R);
     int download(double *points, double *scales, double *tg);

@@ -242,7 +242,12 @@ int SpSolver::upload(const deftri_problem_desc &d) {
                            (shard_ ? !sd_no_tile
                                    : !std::getenv("DEFTRI_SP_NO_FUSE") && !std::getenv("DEFTRI_SP_NO_MERGE") &&
                                          (ndof_ >= kSpMergeMinDof || std::getenv("DEFTRI_SP_MERGE")));
-    if (!build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err, want_tile)) return DEFTRI_E_ARG;
+    const bool planned = build_sp_plan(d, rank_, nranks_, fp32_jac != 0, H, err, want_tile);
+    if (before_alloc) {
+        before_alloc();
+        before_alloc = nullptr;
+    }
+    if (!planned) return DEFTRI_E_ARG;
     const auto tu1 = std::chrono::steady_clock::now();
     struct Report {                 // DEFTRI_UPLOAD_TIMING=1: plan build vs the rest of the upload
         bool on; std::chrono::steady_clock::time_point a, b;
