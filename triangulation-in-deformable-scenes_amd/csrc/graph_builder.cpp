@@ -767,6 +767,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
         });
         for (size_t e = 0; e < emits.size(); e++)
             if (!perr[e].empty()) { err = perr[e]; return false; }   // the first pair's first error
+        const auto ts_scan = tnow();
         // (ii) the points, created in the pairs' order, each at its first encounter; a slot's two
         //      MapPoints are fixed within the pair, so their graph indices are looked up once
         auto add_point = [&](int64_t id, int kf, int slot, int ord_kf, int ord_slot) {
@@ -784,7 +785,82 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             g.order_kf.push_back(ord_kf); g.order_slot.push_back(ord_slot);
             return k;
         };
+        // With the direct id table (every id in one dense range) and no point yet, on host threads: the
+        //  occurrences j = 2 (the pair's encounter index) + side, pairs concatenated, each id's first
+        //  occurrence by an atomic minimum, the first occurrences flagged and prefix-summed into the
+        //  point numbers — the numbering of the sequential loop below
+        std::vector<int64_t> pbase(emits.size() + 1, 0);
+        for (size_t e = 0; e < emits.size(); e++) pbase[e + 1] = pbase[e] + 2 * (int64_t)emits[e].enc.size();
+        const int64_t nocc = pbase[emits.size()];
+        const bool par_points = pidx.span >= 0 && g.point_mpid.empty() && nocc >= (1 << 16) && nocc < (1LL << 31);
+        if (par_points) {
+            auto occ = [&](int64_t j, int64_t &id, int &kf, int &slot, int &okf) {
+                const size_t e = (size_t)(std::upper_bound(pbase.begin(), pbase.end(), j) - pbase.begin()) - 1;
+                const PairEmit &pe = emits[e];
+                const int64_t x = j - pbase[e];
+                slot = pe.enc[(size_t)(x >> 1)];
+                kf = (x & 1) ? pe.a : pe.b;
+                okf = pe.b;
+                id = map.keyframes[kf].point_id[slot];
+            };
+            std::vector<int32_t> first((size_t)pidx.span, INT32_MAX);
+            parallel_for((int)nocc, 1 << 15, [&](int j0, int j1) {
+                for (int j = j0; j < j1; j++) {
+                    int64_t id; int kf, slot, okf;
+                    occ(j, id, kf, slot, okf);
+                    int32_t *f = &first[(size_t)(id - pidx.lo)];
+                    int32_t cur = __atomic_load_n(f, __ATOMIC_RELAXED);
+                    while (j < cur && !__atomic_compare_exchange_n(f, &cur, j, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+                }
+            });
+            const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(64, nocc >> 15));
+            std::vector<int64_t> cb(nch + 1, 0);
+            auto lo_of = [&](int c) { return (int)(nocc * c / nch); };
+            parallel_for(nch, 1, [&](int c0, int c1) {
+                for (int c = c0; c < c1; c++)
+                    for (int j = lo_of(c); j < lo_of(c + 1); j++) {
+                        int64_t id; int kf, slot, okf;
+                        occ(j, id, kf, slot, okf);
+                        cb[c + 1] += first[(size_t)(id - pidx.lo)] == j;
+                    }
+            });
+            for (int c = 0; c < nch; c++) cb[c + 1] += cb[c];
+            const size_t np = (size_t)cb[nch];
+            g.point_mpid.resize(np); g.points.resize(3 * np); g.point_orig.resize(3 * np); g.order_xy.resize(2 * np);
+            g.point_kf.resize(np); g.point_slot.resize(np); g.order_kf.resize(np); g.order_slot.resize(np);
+            parallel_for(nch, 1, [&](int c0, int c1) {
+                for (int c = c0; c < c1; c++) {
+                    int64_t k = cb[c];
+                    for (int j = lo_of(c); j < lo_of(c + 1); j++) {
+                        int64_t id; int kf, slot, okf;
+                        occ(j, id, kf, slot, okf);
+                        if (first[(size_t)(id - pidx.lo)] != j) continue;
+                        pidx.val[(size_t)(id - pidx.lo)] = (int32_t)k;
+                        g.point_mpid[k] = id;
+                        const float *p = map.keyframes[kf].point_pos + 3 * (size_t)slot;
+                        for (int cc = 0; cc < 3; cc++) { g.points[3 * k + cc] = (double)p[cc]; g.point_orig[3 * k + cc] = p[cc]; }
+                        const float *o = map.keyframes[okf].point_pos + 3 * (size_t)slot;
+                        g.order_xy[2 * k] = (double)o[0];
+                        g.order_xy[2 * k + 1] = (double)o[1];
+                        g.point_kf[k] = kf; g.point_slot[k] = slot;
+                        g.order_kf[k] = okf; g.order_slot[k] = slot;
+                        k++;
+                    }
+                }
+            });
+            for (PairEmit &pe : emits) pe.slot_pt.assign(2 * (size_t)pe.ns12, -1);
+            parallel_for((int)nocc, 1 << 15, [&](int j0, int j1) {
+                for (int j = j0; j < j1; j++) {
+                    int64_t id; int kf, slot, okf;
+                    occ(j, id, kf, slot, okf);
+                    const size_t e = (size_t)(std::upper_bound(pbase.begin(), pbase.end(), (int64_t)j) - pbase.begin()) - 1;
+                    emits[e].slot_pt[2 * (size_t)slot + ((j - pbase[e]) & 1)] = pidx.val[(size_t)(id - pidx.lo)];
+                }
+            });
+            for (PairEmit &pe : emits) { pe.enc.clear(); pe.enc.shrink_to_fit(); }
+        }
         for (PairEmit &pe : emits) {
+            if (par_points) break;
             const deftri_keyframe &kf1 = map.keyframes[pe.b], &kf2 = map.keyframes[pe.a];
             pe.slot_pt.assign(2 * (size_t)pe.ns12, -1);
             for (int32_t slot : pe.enc) {
@@ -794,7 +870,7 @@ bool build_arap_graph(const deftri_map &map, double rep_weight, double arap_weig
             pe.enc.clear();
             pe.enc.shrink_to_fit();
         }
-        if (timing) std::fprintf(stderr, "[deftri graph] slot scan + points: %.1f ms\n", ms(ts, tnow()));
+        if (timing) std::fprintf(stderr, "[deftri graph] slot scan %.1f + points %.1f ms (%s)\n", ms(ts, ts_scan), ms(ts_scan, tnow()), par_points ? "threads" : "one thread");
     }
     {
         // the edges, each pair into its own range (the reference's order: pairs, then slots)
