@@ -94,6 +94,22 @@ void par_counting_sort(std::vector<int32_t> &ids, int64_t nkeys, Key key) {
     ids.swap(out);
 }
 
+// a stable LSD radix sort of ids by their 42-bit curve keys (three 14-bit digits): ids with equal keys
+// keep their order, so from ascending ids it is std::sort by (key, id)
+void radix_sort_by_key(std::vector<int32_t> &ids, const std::vector<uint64_t> &key) {
+    std::vector<int32_t> tmp(ids.size());
+    std::vector<uint32_t> cnt(1 << 14);
+    for (int pass = 0; pass < 3; pass++) {
+        const int sh = 14 * pass;
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (int32_t i : ids) cnt[(key[i] >> sh) & 0x3fff]++;
+        uint32_t sum = 0;
+        for (uint32_t &c : cnt) { const uint32_t t = c; c = sum; sum += t; }
+        for (int32_t i : ids) tmp[cnt[(key[i] >> sh) & 0x3fff]++] = i;
+        ids.swap(tmp);
+    }
+}
+
 }  // namespace
 
 bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32_jac, SpPlanHost &H,
@@ -172,7 +188,9 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
     for (int32_t g = 0; g < ng; g++) key[g] = curve_key(xy(grep[g], 0), xy(grep[g], 1), lo, hi);
     std::vector<int32_t> gorder(ng);
     std::iota(gorder.begin(), gorder.end(), 0);
-    std::sort(gorder.begin(), gorder.end(), [&](int32_t a, int32_t b) { return key[a] != key[b] ? key[a] < key[b] : grep[a] < grep[b]; });
+    // by (key, representative): the representatives ascend with the group number (each group is met
+    // first at its smallest point), so a stable sort by key from the identity is that order
+    radix_sort_by_key(gorder, key);
     std::vector<int32_t> gpos(ng);
     for (int32_t k = 0; k < ng; k++) gpos[gorder[k]] = k;
 
@@ -212,10 +230,10 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
                             for (int32_t p = 0; p < P; p++)
                     pk[p] = curve_key(d.points[3 * (int64_t)p], d.points[3 * (int64_t)p + 1], &blo[2 * cam(p)],
                                       &bhi[2 * cam(p)]);
-                std::sort(pts.begin(), pts.end(), [&](int32_t a, int32_t b) {
-                    const int32_t ca = cam(a), cb = cam(b);
-                    return ca != cb ? ca < cb : pk[a] != pk[b] ? pk[a] < pk[b] : a < b;
-                });
+                // by (camera, key, point): stable by key from ascending points, then stable by camera
+                std::iota(pts.begin(), pts.end(), 0);
+                radix_sort_by_key(pts, pk);
+                counting_sort(pts, C + 1, [&](int32_t p) { return cam(p); });
             }
         }
     }
