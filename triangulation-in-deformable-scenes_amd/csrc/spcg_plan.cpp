@@ -391,7 +391,16 @@ bool build_sp_plan(const deftri_problem_desc &d, int rank, int nranks, bool fp32
         // numbered in first-encounter order over the positions 2 le + k: each row's first position
         // (an atomic minimum over host threads), the first positions flagged and prefix-summed
         const int64_t npos = 2 * nloc;
-        auto rot_at = [&](int64_t x) { return d.arap_rot[2 * (int64_t)H.arap_ids[x >> 1] + (x & 1)]; };
+        // the rotation rows gathered once in position order (the passes below then read them in order)
+        std::vector<int32_t> rv((size_t)npos);
+        chunked(nloc, 1 << 17, [&](int, int64_t l0, int64_t l1) {
+            for (int64_t l = l0; l < l1; l++) {
+                const int64_t e = H.arap_ids[l];
+                rv[2 * l] = d.arap_rot[2 * e];
+                rv[2 * l + 1] = d.arap_rot[2 * e + 1];
+            }
+        });
+        auto rot_at = [&](int64_t x) { return rv[x]; };
         std::vector<int64_t> first((size_t)std::max(d.n_rot, 1), INT64_MAX);
         chunked(npos, 1 << 18, [&](int, int64_t x0, int64_t x1) {
             for (int64_t x = x0; x < x1; x++) {
